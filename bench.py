@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 training images/sec on N MI355X GPUs.
+
+Metric and config come from BASELINE.json ("images/sec ResNet-50 TfJob at
+1/2/4/8 MI355X"): ResNet-50 v1.5, synthetic ImageNet (224x224x3, 1000
+classes, random-init weights -- no datasets or checkpoints are reachable),
+bf16 compute with fp32 master weights/BN statistics, SGD+momentum (fused HIP
+kernel), data parallel with bucketed RCCL all-reduce overlapped with
+backward. Per-GPU batch is fixed as N grows (weak scaling).
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line; ``value`` is the whole-job images/sec computed
+from the MAX per-rank wall time over exactly K timed steps bracketed by a
+barrier + device synchronize on both sides.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from k8s_amd.models.resnet import resnet50  # noqa: E402
+from k8s_amd.ops import nn as K  # noqa: E402
+from k8s_amd.ops.optim import FusedSGD  # noqa: E402
+from k8s_amd.parallel import dist as kdist  # noqa: E402
+from k8s_amd.parallel.ddp import GradReducer  # noqa: E402
+from k8s_amd.parallel.flat import ParamStore  # noqa: E402
+
+BASELINE_VALUE = None  # BASELINE.json "published": {} -- the reference publishes no number
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--profile-steps", type=int, default=0, help="(internal) roctx-free short run")
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    a = parse(argv)
+    info = kdist.init_process_group()
+    n = info.world_size
+    if n != a.gpus and info.rank == 0:
+        print("warning: --gpus %d but world size %d" % (a.gpus, n), file=sys.stderr)
+    dev = torch.device("cuda", info.local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    torch.manual_seed(1234 + info.rank)
+
+    store = ParamStore()
+    model = resnet50(store).finalize(dev)
+    model.train()
+    # DP replicas start from identical weights (same seed in finalize); broadcast for safety
+    if n > 1:
+        torch.distributed.broadcast(store.master, 0)
+        store.refresh_lowp()
+    reducer = GradReducer(store, bucket_mb=a.bucket_mb)
+    opt = FusedSGD(store, lr=a.lr, momentum=0.9, weight_decay=5e-5, nesterov=False)
+
+    dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
+    images = torch.randn(a.batch, a.image, a.image, 3, device=dev, dtype=dtype)
+    x = model.prepare_input(images).contiguous()
+    labels = torch.randint(0, 1000, (a.batch,), device=dev)
+
+    def step():
+        reducer.begin_step()
+        logits = model(x)
+        loss = K.cross_entropy(logits, labels)
+        loss.backward()
+        reducer.finish()
+        opt.step(grad_scale=reducer.grad_scale)
+        return loss
+
+    for _ in range(a.warmup):
+        loss = step()
+    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+    sync()
+    kdist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    sync()
+    kdist.barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    dt_max = kdist.all_reduce_max(dt, dev)
+    final_loss = float(loss.detach().float().item())
+    ips = n * a.batch * a.steps / dt_max
+    if info.rank == 0:
+        out = {
+            "metric": "images/sec ResNet-50 TfJob (train, synthetic ImageNet)",
+            "value": round(ips, 2),
+            "unit": "images/s",
+            "n_gpus": n,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000.0 * dt_max / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (ips / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": "bf16",
+            "data": "synthetic (random 224x224x3 images, random labels, random-init weights)",
+            "config": {
+                "model": "resnet50-v1.5",
+                "global_batch": n * a.batch,
+                "per_gpu_batch": a.batch,
+                "seq_len": None,
+                "image_size": a.image,
+                "parallelism": "dp%d" % n,
+                "optimizer": "fused SGD momentum 0.9 (HIP)",
+                "bucket_mb": a.bucket_mb,
+            },
+            "final_loss": round(final_loss, 4),
+        }
+        print(json.dumps(out), flush=True)
+    kdist.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,346 @@
+// K3: NHWC BatchNorm (training statistics) fused with residual add + ReLU.
+//
+// Activations are [M = N*H*W, C] bf16 rows (channels_last). Every kernel
+// reads/writes 16-B bf16x8 vectors; a thread owns 8 consecutive channels.
+//
+//  fwd:  stats  : per-block Welford/Chan partials (count-weighted mean, M2)
+//        final  : combine partials -> mean, invstd; update running stats
+//        apply  : y = relu(x*scale + shift [+ res])    (scale/shift per channel)
+//  bwd:  reduce : sum(dy_eff), sum(dy_eff * xhat)  with dy_eff = dy * (y > 0)
+//        final  : dgamma, dbeta (fp32, written straight into the flat grad bucket)
+//        apply  : dx = gamma*invstd*(dy_eff - sum_dy/M - xhat*sum_dyxh/M), dres = dy_eff
+#include "common.h"
+#include "launchers.h"
+
+namespace k8s_amd {
+
+constexpr int BN_THREADS = 256;
+
+struct BnGeom {
+  int cgroups;        // C / 8
+  int tpr;            // threads per row (channel groups handled per block column)
+  int rows_per_iter;  // rows processed per block iteration
+  int grid_y;         // channel slices
+};
+
+static inline BnGeom bn_geom(int C) {
+  BnGeom g;
+  g.cgroups = C / 8;
+  g.tpr = g.cgroups < BN_THREADS ? g.cgroups : BN_THREADS;
+  g.rows_per_iter = BN_THREADS / g.tpr;
+  g.grid_y = (g.cgroups + g.tpr - 1) / g.tpr;
+  return g;
+}
+
+// Partial stats per block: part[(bx * C + c) * 2 + {0,1}] = (mean, M2) over the
+// block's rows; count per block is derivable from rows_per_block.
+__global__ void __launch_bounds__(BN_THREADS) bn_stats_kernel(const uint16_t* __restrict__ x, long M, int C,
+                                                              int tpr, int rows_per_iter, long rows_per_block,
+                                                              float* __restrict__ part) {
+  __shared__ float sh[2][BN_THREADS][9];  // +1 pad
+  const int t = threadIdx.x;
+  const int r = t / tpr, cg_local = t % tpr;
+  const int cg = blockIdx.y * tpr + cg_local;
+  const bool active = (r < rows_per_iter) && (cg * 8 < C);
+  const long r0 = blockIdx.x * rows_per_block;
+  long r1 = r0 + rows_per_block;
+  if (r1 > M) r1 = M;
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+  float shift[8];
+  // shift by the first row of the block to avoid catastrophic cancellation
+  if (active && r0 < M) {
+    load8(x + r0 * C + cg * 8, shift);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) shift[j] = 0.f;
+  }
+  int n = 0;
+  if (active) {
+    for (long row = r0 + r; row < r1; row += rows_per_iter) {
+      float v[8];
+      load8(x + row * C + cg * 8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float d = v[j] - shift[j];
+        s[j] += d;
+        q[j] += d * d;
+      }
+      ++n;
+    }
+  }
+  // per-thread (mean, M2) in shifted coordinates
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float mean = n ? s[j] / n : 0.f;
+    sh[0][t][j] = mean;
+    sh[1][t][j] = n ? (q[j] - s[j] * mean) : 0.f;
+  }
+  sh[0][t][8] = (float)n;
+  __syncthreads();
+  // combine rows (threads with the same cg_local) -- row 0 threads do it
+  if (r == 0 && cg * 8 < C) {
+    float cnt = sh[0][t][8];
+    float mean[8], m2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { mean[j] = sh[0][t][j]; m2[j] = sh[1][t][j]; }
+    for (int rr = 1; rr < rows_per_iter; ++rr) {
+      const int o = rr * tpr + cg_local;
+      const float nb = sh[0][o][8];
+      if (nb == 0.f) continue;
+      const float tot = cnt + nb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = sh[0][o][j] - mean[j];
+        mean[j] += d * nb / tot;
+        m2[j] += sh[1][o][j] + d * d * cnt * nb / tot;
+      }
+      cnt = tot;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const long idx = ((long)blockIdx.x * C + cg * 8 + j) * 2;
+      part[idx] = mean[j] + shift[j];
+      part[idx + 1] = m2[j];
+    }
+  }
+}
+
+// One thread per channel: Chan-combine the per-block partials.
+__global__ void bn_stats_final_kernel(const float* __restrict__ part, int nblocks, long M, long rows_per_block,
+                                      int C, float eps, float momentum, float* __restrict__ mean_out,
+                                      float* __restrict__ invstd_out, float* __restrict__ run_mean,
+                                      float* __restrict__ run_var) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float cnt = 0.f, mean = 0.f, m2 = 0.f;
+  for (int b = 0; b < nblocks; ++b) {
+    long rows = M - (long)b * rows_per_block;
+    if (rows > rows_per_block) rows = rows_per_block;
+    if (rows <= 0) break;
+    const float nb = (float)rows;
+    const float bm = part[((long)b * C + c) * 2];
+    const float bq = part[((long)b * C + c) * 2 + 1];
+    const float tot = cnt + nb;
+    const float d = bm - mean;
+    mean += d * nb / tot;
+    m2 += bq + d * d * cnt * nb / tot;
+    cnt = tot;
+  }
+  const float var = m2 / cnt;
+  mean_out[c] = mean;
+  invstd_out[c] = rsqrtf(var + eps);
+  if (run_mean) {
+    const float unbiased = cnt > 1.f ? m2 / (cnt - 1.f) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unbiased;
+  }
+}
+
+// y = act(x*scale + shift + res); scale = gamma*invstd, shift = beta - mean*scale
+__global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(const uint16_t* __restrict__ x,
+                                                              const uint16_t* __restrict__ res,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta,
+                                                              uint16_t* __restrict__ y, long nvec, int cgroups,
+                                                              int relu) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nvec; e += (long)gridDim.x * blockDim.x) {
+    const int cg = (int)(e % cgroups);
+    float v[8];
+    load8(x + e * 8, v);
+    float rv[8];
+    if (res) load8(res + e * 8, rv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = cg * 8 + j;
+      const float sc = gamma[c] * invstd[c];
+      float o = (v[j] - mean[c]) * sc + beta[c];
+      if (res) o += rv[j];
+      if (relu) o = fmaxf(o, 0.f);
+      v[j] = o;
+    }
+    store8(y + e * 8, v);
+  }
+}
+
+// Eval-mode: same apply with running stats (mean/invstd precomputed on host side kernel below).
+__global__ void bn_eval_prep_kernel(const float* __restrict__ run_mean, const float* __restrict__ run_var, int C,
+                                    float eps, float* __restrict__ mean, float* __restrict__ invstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  mean[c] = run_mean[c];
+  invstd[c] = rsqrtf(run_var[c] + eps);
+}
+
+// Backward reduce: part[(bx*C + c)*2] = sum dy_eff, [+1] = sum dy_eff * xhat
+__global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy,
+                                                                   const uint16_t* __restrict__ x,
+                                                                   const uint16_t* __restrict__ y,
+                                                                   const float* __restrict__ mean,
+                                                                   const float* __restrict__ invstd, long M,
+                                                                   int C, int tpr, int rows_per_iter,
+                                                                   long rows_per_block, float* __restrict__ part) {
+  __shared__ float sh[2][BN_THREADS][9];
+  const int t = threadIdx.x;
+  const int r = t / tpr, cg_local = t % tpr;
+  const int cg = blockIdx.y * tpr + cg_local;
+  const bool active = (r < rows_per_iter) && (cg * 8 < C);
+  const long r0 = blockIdx.x * rows_per_block;
+  long r1 = r0 + rows_per_block;
+  if (r1 > M) r1 = M;
+  float sd[8], sx[8], mu[8], is[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sd[j] = sx[j] = 0.f;
+    mu[j] = active ? mean[cg * 8 + j] : 0.f;
+    is[j] = active ? invstd[cg * 8 + j] : 0.f;
+  }
+  if (active) {
+    for (long row = r0 + r; row < r1; row += rows_per_iter) {
+      const long off = row * C + cg * 8;
+      float g[8], xv[8];
+      load8(dy + off, g);
+      load8(x + off, xv);
+      if (y) {
+        bf16x8_t yv = *reinterpret_cast<const bf16x8_t*>(y + off);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (bf2f((uint16_t)yv[j]) <= 0.f) g[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sd[j] += g[j];
+        sx[j] += g[j] * (xv[j] - mu[j]) * is[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sh[0][t][j] = sd[j];
+    sh[1][t][j] = sx[j];
+  }
+  __syncthreads();
+  if (r == 0 && cg * 8 < C) {
+    for (int rr = 1; rr < rows_per_iter; ++rr) {
+      const int o = rr * tpr + cg_local;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sd[j] += sh[0][o][j];
+        sx[j] += sh[1][o][j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const long idx = ((long)blockIdx.x * C + cg * 8 + j) * 2;
+      part[idx] = sd[j];
+      part[idx + 1] = sx[j];
+    }
+  }
+}
+
+__global__ void bn_bwd_final_kernel(const float* __restrict__ part, int nblocks, int C,
+                                    float* __restrict__ sums, float* __restrict__ dgamma,
+                                    float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f, b = 0.f;
+  for (int i = 0; i < nblocks; ++i) {
+    a += part[((long)i * C + c) * 2];
+    b += part[((long)i * C + c) * 2 + 1];
+  }
+  sums[c] = a;
+  sums[C + c] = b;
+  if (dbeta) dbeta[c] = a;
+  if (dgamma) dgamma[c] = b;
+}
+
+__global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t* __restrict__ dy,
+                                                                  const uint16_t* __restrict__ x,
+                                                                  const uint16_t* __restrict__ y,
+                                                                  const float* __restrict__ mean,
+                                                                  const float* __restrict__ invstd,
+                                                                  const float* __restrict__ gamma,
+                                                                  const float* __restrict__ sums,
+                                                                  uint16_t* __restrict__ dx,
+                                                                  uint16_t* __restrict__ dres, long nvec,
+                                                                  int cgroups, int C, float inv_m) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nvec; e += (long)gridDim.x * blockDim.x) {
+    const int cg = (int)(e % cgroups);
+    float g[8], xv[8];
+    load8(dy + e * 8, g);
+    load8(x + e * 8, xv);
+    if (y) {
+      bf16x8_t yv = *reinterpret_cast<const bf16x8_t*>(y + e * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (bf2f((uint16_t)yv[j]) <= 0.f) g[j] = 0.f;
+    }
+    if (dres) store8(dres + e * 8, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = cg * 8 + j;
+      const float is = invstd[c];
+      const float xh = (xv[j] - mean[c]) * is;
+      xv[j] = gamma[c] * is * (g[j] - sums[c] * inv_m - xh * sums[C + c] * inv_m);
+    }
+    store8(dx + e * 8, xv);
+  }
+}
+
+// ---------------------------------------------------------------- launchers
+static long bn_rows_per_block(long M, const BnGeom& g) {
+  // aim for ~1024 blocks in total; at least rows_per_iter*4 rows per block
+  long blocks_x = 1024 / g.grid_y;
+  if (blocks_x < 1) blocks_x = 1;
+  long rpb = (M + blocks_x - 1) / blocks_x;
+  long minr = (long)g.rows_per_iter * 4;
+  if (rpb < minr) rpb = minr;
+  rpb = (rpb + g.rows_per_iter - 1) / g.rows_per_iter * g.rows_per_iter;
+  return rpb;
+}
+
+int bn_workspace_floats(long M, int C) {
+  BnGeom g = bn_geom(C);
+  long rpb = bn_rows_per_block(M, g);
+  long nb = (M + rpb - 1) / rpb;
+  return (int)(nb * C * 2);
+}
+
+void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta, uint16_t* y,
+                   float* save_mean, float* save_invstd, float* run_mean, float* run_var, float* work, long M, int C,
+                   float eps, float momentum, bool training, bool relu, hipStream_t st) {
+  if (training) {
+    BnGeom g = bn_geom(C);
+    long rpb = bn_rows_per_block(M, g);
+    int nb = (int)((M + rpb - 1) / rpb);
+    hipLaunchKernelGGL(bn_stats_kernel, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, x, M, C, g.tpr,
+                       g.rows_per_iter, rpb, work);
+    hipLaunchKernelGGL(bn_stats_final_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, work, nb, M, rpb, C, eps,
+                       momentum, save_mean, save_invstd, run_mean, run_var);
+  } else {
+    hipLaunchKernelGGL(bn_eval_prep_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, run_mean, run_var, C, eps,
+                       save_mean, save_invstd);
+  }
+  const long nvec = M * C / 8;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(stream_grid(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, x, res,
+                     save_mean, save_invstd, gamma, beta, y, nvec, C / 8, (int)relu);
+}
+
+void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
+                   const float* gamma, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, float* work,
+                   float* sums, long M, int C, hipStream_t st) {
+  BnGeom g = bn_geom(C);
+  long rpb = bn_rows_per_block(M, g);
+  int nb = (int)((M + rpb - 1) / rpb);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, dy, x, y, mean, invstd, M,
+                     C, g.tpr, g.rows_per_iter, rpb, work);
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, work, nb, C, sums, dgamma, dbeta);
+  const long nvec = M * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, dy, x, y,
+                     mean, invstd, gamma, sums, dx, dres, nvec, C / 8, C, 1.f / (float)M);
+}
+
+}  // namespace k8s_amd

@@ -1,0 +1,91 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of k8s_amd.
+//
+// Everything here is written for a 64-lane wavefront: reductions use
+// __shfl_xor over 64 lanes, vector types are sized for 16-byte global
+// accesses (bf16x8 / float4), and bf16 conversion is round-to-nearest-even.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace k8s_amd {
+
+constexpr int kWave = 64;
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8_t;   // 8 bf16 = 16 B
+typedef __attribute__((ext_vector_type(4))) short bf16x4_t;   // 4 bf16 = 8 B
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+typedef uint16_t bf16_raw;
+
+__device__ __forceinline__ float bf2f(uint16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+
+// round-to-nearest-even, NaN preserved as quiet NaN
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum; `red` must hold blockDim.x/64 floats. Result broadcast to all threads.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+__device__ __forceinline__ float block_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = -INFINITY;
+  for (int i = 0; i < nw; ++i) t = fmaxf(t, red[i]);
+  return t;
+}
+
+// Load 8 bf16 as floats.
+__device__ __forceinline__ void load8(const uint16_t* p, float (&o)[8]) {
+  bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = bf2f((uint16_t)v[j]);
+}
+
+__device__ __forceinline__ void store8(uint16_t* p, const float (&o)[8]) {
+  bf16x8_t v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(o[j]);
+  *reinterpret_cast<bf16x8_t*>(p) = v;
+}
+
+inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// Memory-bound launch sizing: cap at 256 CUs x 8 blocks and grid-stride.
+inline int stream_grid(long work_items, int block) {
+  long g = (work_items + block - 1) / block;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace k8s_amd

@@ -1,0 +1,45 @@
+// Host-side launcher declarations for every gfx950 kernel translation unit.
+// The kernels themselves are compiled without any PyTorch headers (fast,
+// parallel builds); only ops_binding.cpp sees torch.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace k8s_amd {
+
+// optim.hip
+void launch_sgd(float* p, float* mom, const void* g, bool g_bf16, uint16_t* pbf, long n, const uint8_t* decay_mask, float lr,
+                float mu, float wd, float scale, const float* scale_ptr, bool nesterov, bool first_step,
+                hipStream_t st);
+void launch_adam(float* p, float* m1, float* m2, const void* g, bool g_bf16, uint16_t* pbf, long n, const uint8_t* decay_mask,
+                 float lr, float b1, float b2, float eps, float wd, float scale, const float* scale_ptr, float bc1,
+                 float bc2, bool decoupled, hipStream_t st);
+void launch_sumsq(const void* g, bool g_bf16, long n, float* out, hipStream_t st);
+void launch_clip_factor(const float* stats, float max_norm, float* factor, hipStream_t st);
+
+// batchnorm.hip
+int bn_workspace_floats(long M, int C);
+void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta, uint16_t* y,
+                   float* save_mean, float* save_invstd, float* run_mean, float* run_var, float* work, long M, int C,
+                   float eps, float momentum, bool training, bool relu, hipStream_t st);
+void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
+                   const float* gamma, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, float* work,
+                   float* sums, long M, int C, hipStream_t st);
+
+// norm.hip
+void launch_norm_fwd(bool rms, const uint16_t* x, const uint16_t* res, uint16_t* xsum, const float* gamma,
+                     const float* beta, uint16_t* y, float* mean, float* rstd, long R, int D, float eps,
+                     hipStream_t st);
+int norm_workspace_floats(long R, int D);
+void launch_norm_bwd(bool rms, const uint16_t* dy, const uint16_t* x, const float* gamma, const float* mean,
+                     const float* rstd, const uint16_t* dres, uint16_t* dx, float* dgamma, float* dbeta, float* work,
+                     long R, int D, hipStream_t st);
+
+// xent.hip
+void launch_xent_fwd(const void* logits, bool bf16, const int64_t* labels, long R, long V, long ld, float* loss,
+                     float* lse, long ignore_index, float smoothing, hipStream_t st);
+void launch_xent_bwd(const void* logits, bool bf16, const int64_t* labels, const float* lse, const float* dscale,
+                     bool per_row, long R, long V, long ld, void* dlogits, long ignore_index, float smoothing,
+                     hipStream_t st);
+
+}  // namespace k8s_amd

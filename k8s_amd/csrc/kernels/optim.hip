@@ -1,0 +1,186 @@
+// Fused multi-tensor optimizers (K7 fused SGD+momentum, K8 fused Adam/AdamW)
+// and gradient-norm utilities.
+//
+// "Multi-tensor" on this framework means FLAT: every parameter of a model
+// lives in one contiguous fp32 master buffer (64-element aligned slots, see
+// k8s_amd/parallel/flat.py), its optimizer state in same-shaped buffers and
+// its gradients in one contiguous buffer that is also the all-reduce bucket
+// storage. One launch therefore updates the whole model: no per-tensor
+// launches, no pointer tables, and every access is a 16-B vector access.
+//
+// Weight decay is selected per 64-element chunk by `decay_mask` (one byte per
+// chunk; parameter slots are 64-aligned, so a chunk never straddles two
+// parameters). A null mask means "decay everything".
+//
+// An optional device-side scale pointer (gradient clip factor / loss-scale
+// inverse) keeps the step free of host synchronisation so the whole step can
+// be captured in a hipGraph.
+#include "common.h"
+#include "launchers.h"
+
+namespace k8s_amd {
+
+template <typename GT>
+__device__ __forceinline__ void load_grad4(const GT* g, long i, float (&o)[4]);
+
+template <>
+__device__ __forceinline__ void load_grad4<float>(const float* g, long i, float (&o)[4]) {
+  float4 v = *reinterpret_cast<const float4*>(g + i);
+  o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+}
+template <>
+__device__ __forceinline__ void load_grad4<uint16_t>(const uint16_t* g, long i, float (&o)[4]) {
+  bf16x4_t v = *reinterpret_cast<const bf16x4_t*>(g + i);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = bf2f((uint16_t)v[j]);
+}
+
+__device__ __forceinline__ void store_bf4(uint16_t* p, long i, const float4& v) {
+  bf16x4_t o;
+  o[0] = (short)f2bf(v.x); o[1] = (short)f2bf(v.y); o[2] = (short)f2bf(v.z); o[3] = (short)f2bf(v.w);
+  *reinterpret_cast<bf16x4_t*>(p + i) = o;
+}
+
+template <typename GT>
+__global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* __restrict__ mom,
+                                                  const GT* __restrict__ g, uint16_t* __restrict__ pbf,
+                                                  long n4, const uint8_t* __restrict__ decay_mask, float lr, float mu, float wd,
+                                                  float scale, const float* __restrict__ scale_ptr,
+                                                  int nesterov, int first_step) {
+  const float s = scale * (scale_ptr ? *scale_ptr : 1.f);
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n4; q += (long)gridDim.x * blockDim.x) {
+    const long i = q * 4;
+    float gv[4];
+    load_grad4<GT>(g, i, gv);
+    float4 pv = *reinterpret_cast<float4*>(p + i);
+    float4 mv = *reinterpret_cast<float4*>(mom + i);
+    float* pp = &pv.x;
+    float* mp = &mv.x;
+    const float w = (!decay_mask || decay_mask[i >> 6]) ? wd : 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float d = gv[j] * s + w * pp[j];
+      float m = first_step ? d : mu * mp[j] + d;
+      mp[j] = m;
+      pp[j] -= lr * (nesterov ? d + mu * m : m);
+    }
+    *reinterpret_cast<float4*>(p + i) = pv;
+    *reinterpret_cast<float4*>(mom + i) = mv;
+    if (pbf) store_bf4(pbf, i, pv);
+  }
+}
+
+template <typename GT>
+__global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float* __restrict__ m1,
+                                                   float* __restrict__ m2, const GT* __restrict__ g,
+                                                   uint16_t* __restrict__ pbf, long n4, const uint8_t* __restrict__ decay_mask,
+                                                   float lr, float b1, float b2, float eps, float wd,
+                                                   float scale, const float* __restrict__ scale_ptr,
+                                                   float bc1, float bc2, int decoupled) {
+  const float s = scale * (scale_ptr ? *scale_ptr : 1.f);
+  const float step1 = lr / bc1;
+  const float rbc2 = 1.f / sqrtf(bc2);
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n4; q += (long)gridDim.x * blockDim.x) {
+    const long i = q * 4;
+    float gv[4];
+    load_grad4<GT>(g, i, gv);
+    float4 pv = *reinterpret_cast<float4*>(p + i);
+    float4 av = *reinterpret_cast<float4*>(m1 + i);
+    float4 bv = *reinterpret_cast<float4*>(m2 + i);
+    float* pp = &pv.x;
+    float* ap = &av.x;
+    float* bp = &bv.x;
+    const float w = (!decay_mask || decay_mask[i >> 6]) ? wd : 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gr = gv[j] * s;
+      if (!decoupled) gr += w * pp[j];
+      float a = b1 * ap[j] + (1.f - b1) * gr;
+      float b = b2 * bp[j] + (1.f - b2) * gr * gr;
+      ap[j] = a;
+      bp[j] = b;
+      float upd = step1 * a / (sqrtf(b) * rbc2 + eps);
+      if (decoupled) pp[j] -= lr * w * pp[j];
+      pp[j] -= upd;
+    }
+    *reinterpret_cast<float4*>(p + i) = pv;
+    *reinterpret_cast<float4*>(m1 + i) = av;
+    *reinterpret_cast<float4*>(m2 + i) = bv;
+    if (pbf) store_bf4(pbf, i, pv);
+  }
+}
+
+// Sum of squares of a flat buffer into out[0] (fp32, atomics once per block);
+// also counts non-finite values into out[1]. out must be zeroed beforehand.
+template <typename GT>
+__global__ void __launch_bounds__(256) sumsq_kernel(const GT* __restrict__ g, long n4, float* __restrict__ out) {
+  __shared__ float red[8];
+  float acc = 0.f, bad = 0.f;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n4; q += (long)gridDim.x * blockDim.x) {
+    float gv[4];
+    load_grad4<GT>(g, q * 4, gv);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc += gv[j] * gv[j];
+      bad += isfinite(gv[j]) ? 0.f : 1.f;
+    }
+  }
+  acc = block_sum(acc, red);
+  bad = block_sum(bad, red);
+  if (threadIdx.x == 0) {
+    atomicAdd(out, acc);
+    atomicAdd(out + 1, bad);
+  }
+}
+
+// clip factor = min(1, max_norm / (sqrt(sumsq) + 1e-6)); 0 if non-finite grads (skip step semantics
+// are the caller's: a zero factor makes the update a pure decay step).
+__global__ void clip_factor_kernel(const float* __restrict__ stats, float max_norm, float* __restrict__ factor) {
+  float norm = sqrtf(stats[0]);
+  float f = max_norm / (norm + 1e-6f);
+  f = f < 1.f ? f : 1.f;
+  if (stats[1] > 0.f || !isfinite(norm)) f = 0.f;
+  factor[0] = f;
+}
+
+// ---------------------------------------------------------------- launchers
+void launch_sgd(float* p, float* mom, const void* g, bool g_bf16, uint16_t* pbf, long n, const uint8_t* decay_mask,
+                float lr, float mu, float wd, float scale, const float* scale_ptr, bool nesterov,
+                bool first_step, hipStream_t st) {
+  const long n4 = n / 4;
+  const int grid = stream_grid(n4, 256);
+  if (g_bf16)
+    hipLaunchKernelGGL(sgd_kernel<uint16_t>, dim3(grid), dim3(256), 0, st, p, mom, (const uint16_t*)g, pbf, n4,
+                       decay_mask, lr, mu, wd, scale, scale_ptr, (int)nesterov, (int)first_step);
+  else
+    hipLaunchKernelGGL(sgd_kernel<float>, dim3(grid), dim3(256), 0, st, p, mom, (const float*)g, pbf, n4, decay_mask,
+                       lr, mu, wd, scale, scale_ptr, (int)nesterov, (int)first_step);
+}
+
+void launch_adam(float* p, float* m1, float* m2, const void* g, bool g_bf16, uint16_t* pbf, long n, const uint8_t* decay_mask,
+                 float lr, float b1, float b2, float eps, float wd, float scale, const float* scale_ptr, float bc1,
+                 float bc2, bool decoupled, hipStream_t st) {
+  const long n4 = n / 4;
+  const int grid = stream_grid(n4, 256);
+  if (g_bf16)
+    hipLaunchKernelGGL(adam_kernel<uint16_t>, dim3(grid), dim3(256), 0, st, p, m1, m2, (const uint16_t*)g, pbf, n4,
+                       decay_mask, lr, b1, b2, eps, wd, scale, scale_ptr, bc1, bc2, (int)decoupled);
+  else
+    hipLaunchKernelGGL(adam_kernel<float>, dim3(grid), dim3(256), 0, st, p, m1, m2, (const float*)g, pbf, n4,
+                       decay_mask, lr, b1, b2, eps, wd, scale, scale_ptr, bc1, bc2, (int)decoupled);
+}
+
+void launch_sumsq(const void* g, bool g_bf16, long n, float* out, hipStream_t st) {
+  const long n4 = n / 4;
+  const int grid = stream_grid(n4, 256) > 512 ? 512 : stream_grid(n4, 256);
+  if (g_bf16)
+    hipLaunchKernelGGL(sumsq_kernel<uint16_t>, dim3(grid), dim3(256), 0, st, (const uint16_t*)g, n4, out);
+  else
+    hipLaunchKernelGGL(sumsq_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)g, n4, out);
+}
+
+void launch_clip_factor(const float* stats, float max_norm, float* factor, hipStream_t st) {
+  hipLaunchKernelGGL(clip_factor_kernel, dim3(1), dim3(1), 0, st, stats, max_norm, factor);
+}
+
+}  // namespace k8s_amd

@@ -1,0 +1,208 @@
+// Python bindings of the k8s_amd gfx950 kernels (module k8s_amd._C).
+//
+// Every entry point validates device, dtype, contiguity and shape on the host
+// before launching, so a mis-shaped call raises a Python exception instead of
+// faulting the GPU. Kernels are launched on PyTorch's current HIP stream so
+// they compose with torch ops, streams and hipGraph capture.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+
+#include "kernels/launchers.h"
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void check_dtype(const Tensor& t, at::ScalarType d, const char* name) {
+  TORCH_CHECK(t.scalar_type() == d, name, " has dtype ", t.scalar_type(), ", expected ", d);
+}
+void check_aligned(const Tensor& t, const char* name) {
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, name, " must be 16-byte aligned");
+}
+uint16_t* bf(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+const uint16_t* cbf(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+float* f32(const Tensor& t) { return t.data_ptr<float>(); }
+const float* optf(const c10::optional<Tensor>& t) { return t.has_value() ? t->data_ptr<float>() : nullptr; }
+
+// ------------------------------------------------------------------ optimizers
+const uint8_t* mask_ptr(const c10::optional<Tensor>& m, long n) {
+  if (!m) return nullptr;
+  TORCH_CHECK(m->is_cuda() && m->scalar_type() == at::kByte && m->is_contiguous(), "decay_mask must be uint8 GPU");
+  TORCH_CHECK(m->numel() * 64 >= n, "decay_mask must have one byte per 64 elements");
+  return m->data_ptr<uint8_t>();
+}
+
+void fused_sgd(Tensor p, Tensor mom, Tensor g, c10::optional<Tensor> pbf, c10::optional<Tensor> decay_mask, double lr, double mu,
+               double wd, double scale, c10::optional<Tensor> scale_t, bool nesterov, bool first_step) {
+  check_cuda(p, "param"); check_cuda(mom, "momentum"); check_cuda(g, "grad");
+  check_dtype(p, at::kFloat, "param"); check_dtype(mom, at::kFloat, "momentum");
+  const long n = p.numel();
+  TORCH_CHECK(n % 4 == 0, "flat buffer length must be a multiple of 4");
+  TORCH_CHECK(mom.numel() == n && g.numel() == n, "size mismatch");
+  TORCH_CHECK(g.scalar_type() == at::kFloat || g.scalar_type() == at::kBFloat16, "grad must be fp32 or bf16");
+  if (pbf) { check_cuda(*pbf, "param_bf16"); check_dtype(*pbf, at::kBFloat16, "param_bf16"); TORCH_CHECK(pbf->numel() == n); }
+  const uint8_t* dm = mask_ptr(decay_mask, n);
+  k8s_amd::launch_sgd(f32(p), f32(mom), g.data_ptr(), g.scalar_type() == at::kBFloat16, pbf ? bf(*pbf) : nullptr, n,
+                      dm, (float)lr, (float)mu, (float)wd, (float)scale, optf(scale_t), nesterov, first_step,
+                      cur_stream());
+}
+
+void fused_adam(Tensor p, Tensor m1, Tensor m2, Tensor g, c10::optional<Tensor> pbf, c10::optional<Tensor> decay_mask, double lr,
+                double b1, double b2, double eps, double wd, double scale, c10::optional<Tensor> scale_t, int64_t step,
+                bool decoupled) {
+  check_cuda(p, "param"); check_cuda(m1, "exp_avg"); check_cuda(m2, "exp_avg_sq"); check_cuda(g, "grad");
+  const long n = p.numel();
+  TORCH_CHECK(n % 4 == 0, "flat buffer length must be a multiple of 4");
+  TORCH_CHECK(m1.numel() == n && m2.numel() == n && g.numel() == n, "size mismatch");
+  TORCH_CHECK(g.scalar_type() == at::kFloat || g.scalar_type() == at::kBFloat16, "grad must be fp32 or bf16");
+  if (pbf) { check_cuda(*pbf, "param_bf16"); check_dtype(*pbf, at::kBFloat16, "param_bf16"); TORCH_CHECK(pbf->numel() == n); }
+  const float bc1 = 1.f - std::pow((float)b1, (float)step);
+  const float bc2 = 1.f - std::pow((float)b2, (float)step);
+  k8s_amd::launch_adam(f32(p), f32(m1), f32(m2), g.data_ptr(), g.scalar_type() == at::kBFloat16,
+                       pbf ? bf(*pbf) : nullptr, n, mask_ptr(decay_mask, n), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd,
+                       (float)scale, optf(scale_t), bc1, bc2, decoupled, cur_stream());
+}
+
+Tensor grad_sumsq(Tensor g) {
+  check_cuda(g, "grad");
+  TORCH_CHECK(g.numel() % 4 == 0);
+  auto out = torch::zeros({2}, g.options().dtype(at::kFloat));
+  k8s_amd::launch_sumsq(g.data_ptr(), g.scalar_type() == at::kBFloat16, g.numel(), f32(out), cur_stream());
+  return out;
+}
+
+Tensor clip_factor(Tensor stats, double max_norm) {
+  auto f = torch::empty({1}, stats.options());
+  k8s_amd::launch_clip_factor(f32(stats), (float)max_norm, f32(f), cur_stream());
+  return f;
+}
+
+// ------------------------------------------------------------------ batchnorm (NHWC)
+std::vector<Tensor> bn_fwd(Tensor x, c10::optional<Tensor> res, Tensor gamma, Tensor beta, Tensor run_mean,
+                           Tensor run_var, bool training, double momentum, double eps, bool relu) {
+  check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x"); check_aligned(x, "x");
+  const int C = (int)x.size(-1);
+  TORCH_CHECK(C % 8 == 0, "channels must be a multiple of 8");
+  const long M = x.numel() / C;
+  TORCH_CHECK(gamma.numel() == C && beta.numel() == C && run_mean.numel() == C && run_var.numel() == C);
+  check_dtype(gamma, at::kFloat, "gamma");
+  if (res) { check_cuda(*res, "res"); TORCH_CHECK(res->sizes() == x.sizes(), "residual shape mismatch"); }
+  auto y = torch::empty_like(x);
+  auto mean = torch::empty({C}, gamma.options());
+  auto invstd = torch::empty({C}, gamma.options());
+  Tensor work = training ? torch::empty({k8s_amd::bn_workspace_floats(M, C)}, gamma.options()) : mean;
+  k8s_amd::launch_bn_fwd(cbf(x), res ? cbf(*res) : nullptr, f32(gamma), f32(beta), bf(y), f32(mean), f32(invstd),
+                         f32(run_mean), f32(run_var), f32(work), M, C, (float)eps, (float)momentum, training, relu,
+                         cur_stream());
+  return {y, mean, invstd};
+}
+
+// returns dx, dres (or empty), writes dgamma/dbeta into the given (flat-bucket view) tensors
+std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor mean, Tensor invstd, Tensor gamma,
+                           Tensor dgamma, Tensor dbeta, bool want_dres) {
+  check_cuda(dy, "dy"); check_cuda(x, "x");
+  check_dtype(dy, at::kBFloat16, "dy"); check_dtype(x, at::kBFloat16, "x");
+  TORCH_CHECK(dy.sizes() == x.sizes());
+  const int C = (int)x.size(-1);
+  const long M = x.numel() / C;
+  TORCH_CHECK(dgamma.numel() == C && dbeta.numel() == C && dgamma.is_contiguous() && dbeta.is_contiguous());
+  check_dtype(dgamma, at::kFloat, "dgamma");
+  if (y) { check_cuda(*y, "y"); TORCH_CHECK(y->sizes() == x.sizes()); }
+  auto dx = torch::empty_like(x);
+  Tensor dres = want_dres ? torch::empty_like(x) : Tensor();
+  auto work = torch::empty({k8s_amd::bn_workspace_floats(M, C)}, gamma.options());
+  auto sums = torch::empty({2 * C}, gamma.options());
+  k8s_amd::launch_bn_bwd(cbf(dy), cbf(x), y ? cbf(*y) : nullptr, f32(mean), f32(invstd), f32(gamma), bf(dx),
+                         want_dres ? bf(dres) : nullptr, f32(dgamma), f32(dbeta), f32(work), f32(sums), M, C,
+                         cur_stream());
+  return {dx, dres};
+}
+
+// ------------------------------------------------------------------ layernorm / rmsnorm
+std::vector<Tensor> norm_fwd(Tensor x, c10::optional<Tensor> res, Tensor gamma, c10::optional<Tensor> beta, double eps,
+                             bool rms) {
+  check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x"); check_aligned(x, "x");
+  const int D = (int)x.size(-1);
+  TORCH_CHECK(D % 8 == 0 && D <= 8192, "norm row length must be a multiple of 8 and <= 8192");
+  const long R = x.numel() / D;
+  TORCH_CHECK(gamma.numel() == D); check_dtype(gamma, at::kFloat, "gamma");
+  if (!rms) TORCH_CHECK(beta.has_value() && beta->numel() == D, "layernorm needs beta");
+  if (res) { check_cuda(*res, "res"); TORCH_CHECK(res->sizes() == x.sizes()); }
+  auto y = torch::empty_like(x);
+  Tensor xsum = res ? torch::empty_like(x) : Tensor();
+  auto mean = torch::empty({rms ? 1 : R}, gamma.options());
+  auto rstd = torch::empty({R}, gamma.options());
+  k8s_amd::launch_norm_fwd(rms, cbf(x), res ? cbf(*res) : nullptr, res ? bf(xsum) : nullptr, f32(gamma),
+                           beta ? beta->data_ptr<float>() : nullptr, bf(y), f32(mean), f32(rstd), R, D, (float)eps,
+                           cur_stream());
+  return {y, mean, rstd, xsum};
+}
+
+Tensor norm_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tensor rstd, c10::optional<Tensor> dres,
+                Tensor dgamma, c10::optional<Tensor> dbeta, bool rms) {
+  check_cuda(dy, "dy"); check_cuda(x, "x");
+  check_dtype(dy, at::kBFloat16, "dy");
+  TORCH_CHECK(dy.sizes() == x.sizes());
+  const int D = (int)x.size(-1);
+  const long R = x.numel() / D;
+  TORCH_CHECK(dgamma.numel() == D && dgamma.is_contiguous());
+  if (!rms) TORCH_CHECK(dbeta.has_value() && dbeta->numel() == D);
+  if (dres) TORCH_CHECK(dres->sizes() == x.sizes() && dres->is_contiguous());
+  auto dx = torch::empty_like(x);
+  auto work = torch::empty({k8s_amd::norm_workspace_floats(R, D)}, gamma.options());
+  k8s_amd::launch_norm_bwd(rms, cbf(dy), cbf(x), f32(gamma), f32(mean), f32(rstd), dres ? cbf(*dres) : nullptr,
+                           bf(dx), f32(dgamma), dbeta ? dbeta->data_ptr<float>() : nullptr, f32(work), R, D,
+                           cur_stream());
+  return dx;
+}
+
+// ------------------------------------------------------------------ cross entropy
+std::vector<Tensor> xent_fwd(Tensor logits, Tensor labels, int64_t ignore_index, double smoothing) {
+  TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "logits must be [R, V] row-major");
+  TORCH_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat);
+  check_cuda(labels, "labels"); check_dtype(labels, at::kLong, "labels");
+  const long R = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(labels.numel() == R);
+  auto opt = logits.options().dtype(at::kFloat);
+  auto loss = torch::empty({R}, opt);
+  auto lse = torch::empty({R}, opt);
+  k8s_amd::launch_xent_fwd(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, labels.data_ptr<int64_t>(), R, V,
+                           logits.stride(0), f32(loss), f32(lse), ignore_index, (float)smoothing, cur_stream());
+  return {loss, lse};
+}
+
+Tensor xent_bwd(Tensor logits, Tensor labels, Tensor lse, Tensor dscale, int64_t ignore_index, double smoothing) {
+  const long R = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(dscale.numel() == 1 || dscale.numel() == R);
+  auto d = dscale.to(at::kFloat).contiguous();
+  auto dl = torch::empty({R, V}, logits.options());
+  TORCH_CHECK(logits.stride(0) == V, "xent_bwd expects dense logits");
+  k8s_amd::launch_xent_bwd(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, labels.data_ptr<int64_t>(),
+                           f32(lse), f32(d), d.numel() == R, R, V, V, dl.data_ptr(), ignore_index, (float)smoothing,
+                           cur_stream());
+  return dl;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "k8s_amd gfx950 (MI355X) HIP kernels";
+  m.def("fused_sgd", &fused_sgd);
+  m.def("fused_adam", &fused_adam);
+  m.def("grad_sumsq", &grad_sumsq);
+  m.def("clip_factor", &clip_factor);
+  m.def("bn_fwd", &bn_fwd);
+  m.def("bn_bwd", &bn_bwd);
+  m.def("norm_fwd", &norm_fwd);
+  m.def("norm_bwd", &norm_bwd);
+  m.def("xent_fwd", &xent_fwd);
+  m.def("xent_bwd", &xent_bwd);
+  m.attr("arch") = "gfx950";
+}

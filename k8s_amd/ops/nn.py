@@ -1,0 +1,263 @@
+"""Autograd ops of k8s_amd: HIP kernels on GPU, fp32 references on CPU.
+
+Every op that owns parameters takes :class:`~k8s_amd.parallel.flat.Param`
+handles plus the store's ``anchor`` and deposits parameter gradients straight
+into the flat gradient buffer (see ``parallel/flat.py``); it returns ``None``
+for them to autograd.
+
+Layouts: convolution activations are NHWC ``[N, H, W, C]`` bf16 (channels
+last, what the MFMA implicit-GEMM and the NHWC BatchNorm kernels want);
+conv weights are KRSC ``[K, R, S, C]``; linear weights ``[out, in]``.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from k8s_amd.ops import reference as ref
+from k8s_amd.ops._ext import load as _load_ext
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def _C():
+    return _load_ext()
+
+
+# =========================================================================== convolution
+def _conv_impl():
+    from k8s_amd.ops import conv as _conv  # lazy: conv module selects HIP implicit-GEMM vs MIOpen oracle
+
+    return _conv
+
+
+class _Conv2dNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, p, stride, padding):
+        impl = _conv_impl()
+        w = p.weight if x.dtype == p.weight.dtype else p.master.to(x.dtype)
+        y = impl.conv_fwd(x, w, stride, padding)
+        ctx.save_for_backward(x)
+        ctx.p, ctx.stride, ctx.padding = p, stride, padding
+        ctx.x_requires_grad = x.requires_grad
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        p = ctx.p
+        impl = _conv_impl()
+        w = p.weight if x.dtype == p.weight.dtype else p.master.to(x.dtype)
+        gy = gy.contiguous()
+        dx, dw = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, ctx.x_requires_grad)
+        p.store.deposit(p, dw)
+        return dx, None, None, None, None
+
+
+def conv2d_nhwc(x: torch.Tensor, p, stride: int = 1, padding: int = 0) -> torch.Tensor:
+    """NHWC convolution with KRSC weight ``p`` (no bias)."""
+    return _Conv2dNHWC.apply(x, p.store.anchor, p, stride, padding)
+
+
+# =========================================================================== batchnorm + act
+class _BnAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, res, anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu):
+        x = x.contiguous()
+        if res is not None:
+            res = res.contiguous()
+        if _gpu(x):
+            y, mean, invstd = _C().bn_fwd(x, res, pg.master, pb.master, run_mean, run_var, training, momentum, eps,
+                                          relu)
+        else:
+            y, mean, invstd = ref.bn_fwd(x, res, pg.master, pb.master, run_mean, run_var, training, momentum, eps,
+                                         relu)
+        ctx.save_for_backward(x, y if relu else None, mean, invstd)
+        ctx.pg, ctx.pb, ctx.has_res = pg, pb, res is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, invstd = ctx.saved_tensors
+        pg, pb = ctx.pg, ctx.pb
+        store = pg.store
+        dy = dy.contiguous()
+        if _gpu(x):
+            sg, sb = store.slot_for_write(pg), store.slot_for_write(pb)
+            dg = sg if sg is not None else torch.empty(pg.shape, device=x.device, dtype=torch.float32)
+            db = sb if sb is not None else torch.empty(pb.shape, device=x.device, dtype=torch.float32)
+            dx, dres = _C().bn_bwd(dy, x, y, mean, invstd, pg.master, dg, db, ctx.has_res)
+            if sg is not None:
+                store.mark_written(pg)
+            else:
+                store.deposit(pg, dg)
+            if sb is not None:
+                store.mark_written(pb)
+            else:
+                store.deposit(pb, db)
+        else:
+            dx, dres, dg, db = ref.bn_bwd(dy, x, y, mean, invstd, pg.master)
+            store.deposit(pg, dg)
+            store.deposit(pb, db)
+        return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None
+
+
+def batch_norm_act(x, pg, pb, run_mean, run_var, residual=None, relu=True, training=True, momentum=0.1,
+                   eps=1e-5):
+    """y = act(BN(x) + residual) over the last (channel) dim of an NHWC tensor."""
+    return _BnAct.apply(x, residual, pg.store.anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu)
+
+
+# =========================================================================== layernorm / rmsnorm
+class _Norm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, res, anchor, pg, pb, eps, rms):
+        x = x.contiguous()
+        if res is not None:
+            res = res.contiguous()
+        beta = pb.master if pb is not None else None
+        if _gpu(x):
+            y, mean, rstd, xsum = _C().norm_fwd(x, res, pg.master, beta, eps, rms)
+        else:
+            y, mean, rstd, xsum = ref.norm_fwd(x, res, pg.master, beta, eps, rms)
+        xin = xsum if res is not None else x
+        ctx.save_for_backward(xin, mean, rstd)
+        ctx.pg, ctx.pb, ctx.rms, ctx.has_res = pg, pb, rms, res is not None
+        if res is not None:
+            return y, xsum
+        return y, None
+
+    @staticmethod
+    def backward(ctx, dy, dxsum):
+        xin, mean, rstd = ctx.saved_tensors
+        pg, pb = ctx.pg, ctx.pb
+        store = pg.store
+        dy = dy.contiguous()
+        dres = dxsum.contiguous() if (dxsum is not None and ctx.has_res) else None
+        if _gpu(xin):
+            dg = torch.empty(pg.shape, device=xin.device, dtype=torch.float32)
+            db = torch.empty(pb.shape, device=xin.device, dtype=torch.float32) if pb is not None else None
+            dx = _C().norm_bwd(dy, xin, pg.master, mean, rstd, dres, dg, db, ctx.rms)
+        else:
+            dx, dg, db = ref.norm_bwd(dy, xin, pg.master, mean, rstd, dres, ctx.rms)
+        store.deposit(pg, dg)
+        if pb is not None:
+            store.deposit(pb, db)
+        return dx, (dx if ctx.has_res else None), None, None, None, None, None
+
+
+def layer_norm(x, pg, pb, eps=1e-12, residual=None):
+    """LayerNorm over the last dim; with ``residual`` returns (norm(x+res), x+res)."""
+    y, xsum = _Norm.apply(x, residual, pg.store.anchor, pg, pb, eps, False)
+    return (y, xsum) if residual is not None else y
+
+
+def rms_norm(x, pg, eps=1e-5, residual=None):
+    y, xsum = _Norm.apply(x, residual, pg.store.anchor, pg, None, eps, True)
+    return (y, xsum) if residual is not None else y
+
+
+# =========================================================================== linear
+def _gemm():
+    from k8s_amd.ops import gemm as _g
+
+    return _g
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, pw, pb, act):
+        g = _gemm()
+        w = pw.weight if x.dtype == pw.weight.dtype else pw.master.to(x.dtype)
+        x2 = x.reshape(-1, x.shape[-1])
+        b = pb.master if pb is not None else None
+        y, pre = g.linear_fwd(x2, w, b, act)
+        ctx.save_for_backward(x2, pre)
+        ctx.pw, ctx.pb, ctx.act, ctx.xshape = pw, pb, act, x.shape
+        return y.reshape(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, pre = ctx.saved_tensors
+        pw, pb = ctx.pw, ctx.pb
+        g = _gemm()
+        w = pw.weight if x2.dtype == pw.weight.dtype else pw.master.to(x2.dtype)
+        gy2 = gy.reshape(-1, gy.shape[-1]).contiguous()
+        dx, dw, db = g.linear_bwd(gy2, x2, w, pre, ctx.act, pb is not None)
+        pw.store.deposit(pw, dw)
+        if pb is not None:
+            pb.store.deposit(pb, db)
+        return dx.reshape(ctx.xshape), None, None, None, None
+
+
+def linear(x, pw, pb=None, act: Optional[str] = None):
+    """y = act(x @ W^T + b); W [out, in] bf16 from the flat store."""
+    return _Linear.apply(x, pw.store.anchor, pw, pb, act)
+
+
+# =========================================================================== embedding
+class _Embedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, anchor, pw, dtype):
+        w = pw.weight if pw.weight.dtype == dtype else pw.master.to(dtype)
+        ctx.save_for_backward(ids)
+        ctx.pw = pw
+        return F.embedding(ids, w)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (ids,) = ctx.saved_tensors
+        pw = ctx.pw
+        V, D = pw.shape
+        dw = torch.zeros((V, D), device=gy.device, dtype=torch.float32)
+        dw.index_add_(0, ids.reshape(-1), gy.reshape(-1, D).float())
+        pw.store.deposit(pw, dw)
+        return None, None, None, None
+
+
+def embedding(ids, pw, dtype=torch.bfloat16):
+    return _Embedding.apply(ids, pw.store.anchor, pw, dtype)
+
+
+# =========================================================================== loss
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index, smoothing):
+        logits = logits.contiguous()
+        if _gpu(logits):
+            loss, lse = _C().xent_fwd(logits, labels, ignore_index, smoothing)
+        else:
+            loss, lse = ref.xent_fwd(logits, labels, ignore_index, smoothing)
+        valid = (labels != ignore_index).sum().clamp_min(1).float()
+        ctx.save_for_backward(logits, labels, lse, valid)
+        ctx.ignore_index, ctx.smoothing = ignore_index, smoothing
+        return loss.sum() / valid
+
+    @staticmethod
+    def backward(ctx, gl):
+        logits, labels, lse, valid = ctx.saved_tensors
+        dscale = (gl.float() / valid).reshape(1)
+        if _gpu(logits):
+            d = _C().xent_bwd(logits, labels, lse, dscale, ctx.ignore_index, ctx.smoothing)
+        else:
+            d = ref.xent_bwd(logits, labels, lse, dscale, ctx.ignore_index, ctx.smoothing)
+        return d, None, None, None
+
+
+def cross_entropy(logits, labels, ignore_index: int = -100, smoothing: float = 0.0):
+    """Mean softmax cross-entropy over valid rows of [R, V] logits."""
+    return _CrossEntropy.apply(logits.reshape(-1, logits.shape[-1]), labels.reshape(-1), ignore_index, smoothing)
+
+
+# =========================================================================== pooling (NHWC)
+def max_pool_nhwc(x, k=3, s=2, p=1):
+    y = F.max_pool2d(x.permute(0, 3, 1, 2), k, s, p)
+    return y.permute(0, 2, 3, 1).contiguous()
+
+
+def global_avg_pool_nhwc(x):
+    return x.mean(dim=(1, 2))

@@ -1,0 +1,141 @@
+"""Numerics of the gfx950 HIP kernels vs the plain-PyTorch fp32 references."""
+import pytest
+import torch
+
+from k8s_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _C():
+    from k8s_amd.ops._ext import load
+
+    return load()
+
+
+def _close(a, b, tol):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-6
+    assert err <= tol * max(1.0, scale), "max err %g (scale %g)" % (err, scale)
+
+
+@pytest.mark.parametrize("C,M", [(64, 4096), (256, 1000), (2048, 98), (24, 333)])
+@pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
+def test_bn_fwd_bwd(cuda, C, M, relu, res):
+    torch.manual_seed(0)
+    x = (torch.randn(M, C, device=cuda) * 3 + 1).bfloat16()
+    r = torch.randn(M, C, device=cuda).bfloat16() if res else None
+    g = torch.rand(C, device=cuda) + 0.5
+    b = torch.randn(C, device=cuda)
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    rm2, rv2 = rm.clone(), rv.clone()
+    y, mean, invstd = _C().bn_fwd(x, r, g, b, rm, rv, True, 0.1, 1e-5, relu)
+    yr, meanr, invr = ref.bn_fwd(x, r, g, b, rm2, rv2, True, 0.1, 1e-5, relu)
+    _close(mean, meanr, 1e-4)
+    _close(invstd, invr, 1e-3)
+    _close(y, yr, 2e-2)
+    _close(rm, rm2, 1e-4)
+    _close(rv, rv2, 1e-3)
+    dy = torch.randn(M, C, device=cuda).bfloat16()
+    dg, db = torch.empty(C, device=cuda), torch.empty(C, device=cuda)
+    dx, dres = _C().bn_bwd(dy, x, y if relu else None, mean, invstd, g, dg, db, res)
+    dxr, dresr, dgr, dbr = ref.bn_bwd(dy, x, yr if relu else None, meanr, invr, g)
+    _close(dg, dgr, 2e-2)
+    _close(db, dbr, 2e-2)
+    _close(dx, dxr, 3e-2)
+    if res:
+        _close(dres, dresr, 1e-2)
+
+
+@pytest.mark.parametrize("D", [768, 4096, 1024, 136])
+@pytest.mark.parametrize("rms", [False, True])
+@pytest.mark.parametrize("res", [False, True])
+def test_norm_fwd_bwd(cuda, D, rms, res):
+    torch.manual_seed(1)
+    R = 257
+    x = torch.randn(R, D, device=cuda).bfloat16()
+    r = torch.randn(R, D, device=cuda).bfloat16() if res else None
+    g = torch.rand(D, device=cuda) + 0.5
+    b = None if rms else torch.randn(D, device=cuda)
+    y, mean, rstd, xs = _C().norm_fwd(x, r, g, b, 1e-5, rms)
+    yr, meanr, rstdr, xsr = ref.norm_fwd(x, r, g, b, 1e-5, rms)
+    _close(y, yr, 2e-2)
+    _close(rstd, rstdr, 1e-3)
+    xin = xs if res else x
+    dy = torch.randn(R, D, device=cuda).bfloat16()
+    dres = torch.randn(R, D, device=cuda).bfloat16() if res else None
+    dg = torch.empty(D, device=cuda)
+    db = None if rms else torch.empty(D, device=cuda)
+    dx = _C().norm_bwd(dy, xin, g, mean, rstd, dres, dg, db, rms)
+    dxr, dgr, dbr = ref.norm_bwd(dy, xin, g, meanr, rstdr, dres, rms)
+    _close(dx, dxr, 3e-2)
+    _close(dg, dgr, 2e-2)
+    if not rms:
+        _close(db, dbr, 2e-2)
+
+
+@pytest.mark.parametrize("R,V,dt", [(64, 1000, torch.bfloat16), (8, 30522, torch.bfloat16), (16, 1003, torch.float32),
+                                    (4, 128256, torch.bfloat16)])
+@pytest.mark.parametrize("smooth", [0.0, 0.1])
+def test_xent(cuda, R, V, dt, smooth):
+    torch.manual_seed(2)
+    x = (torch.randn(R, V, device=cuda) * 4).to(dt)
+    lab = torch.randint(0, V, (R,), device=cuda)
+    lab[1] = -100
+    loss, lse = _C().xent_fwd(x, lab, -100, smooth)
+    lr, lser = ref.xent_fwd(x, lab, -100, smooth)
+    _close(lse, lser, 1e-4)
+    _close(loss, lr, 1e-3)
+    ds = torch.tensor([0.37], device=cuda)
+    d = _C().xent_bwd(x, lab, lse, ds, -100, smooth)
+    dr = ref.xent_bwd(x, lab, lser, ds, -100, smooth)
+    _close(d, dr, 2e-2 if dt == torch.bfloat16 else 1e-5)
+
+
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("nesterov", [False, True])
+def test_fused_sgd(cuda, gdt, nesterov):
+    torch.manual_seed(3)
+    n = 64 * 1000
+    p = torch.randn(n, device=cuda)
+    mom = torch.randn(n, device=cuda)
+    g = torch.randn(n, device=cuda).to(gdt)
+    mask = (torch.rand(n // 64, device=cuda) > 0.5).to(torch.uint8)
+    pbf = torch.empty(n, device=cuda, dtype=torch.bfloat16)
+    p2, m2, pbf2 = p.clone(), mom.clone(), pbf.clone()
+    st = torch.tensor([0.5], device=cuda)
+    _C().fused_sgd(p, mom, g, pbf, mask, 0.1, 0.9, 1e-2, 0.25, st, nesterov, False)
+    ref.sgd(p2, m2, g, pbf2, mask, 0.1, 0.9, 1e-2, 0.25, st, nesterov, False)
+    _close(p, p2, 1e-6)
+    _close(mom, m2, 1e-6)
+    _close(pbf, pbf2, 1e-2)
+
+
+@pytest.mark.parametrize("decoupled", [True, False])
+def test_fused_adam(cuda, decoupled):
+    torch.manual_seed(4)
+    n = 64 * 777
+    p = torch.randn(n, device=cuda)
+    m1 = torch.randn(n, device=cuda) * 0.1
+    m2 = torch.rand(n, device=cuda) * 0.1
+    g = torch.randn(n, device=cuda).bfloat16()
+    mask = (torch.rand(n // 64, device=cuda) > 0.3).to(torch.uint8)
+    P, A, B = p.clone(), m1.clone(), m2.clone()
+    _C().fused_adam(p, m1, m2, g, None, mask, 1e-3, 0.9, 0.999, 1e-8, 0.01, 0.5, None, 7, decoupled)
+    ref.adam(P, A, B, g, None, mask, 1e-3, 0.9, 0.999, 1e-8, 0.01, 0.5, None, 7, decoupled)
+    _close(p, P, 1e-5)
+    _close(m1, A, 1e-6)
+    _close(m2, B, 1e-6)
+
+
+def test_grad_clip(cuda):
+    g = torch.randn(64 * 100, device=cuda)
+    st = _C().grad_sumsq(g)
+    _close(st, ref.grad_sumsq(g), 1e-4)
+    f = _C().clip_factor(st, 1.0)
+    norm = g.norm().item()
+    assert abs(f.item() - min(1.0, 1.0 / (norm + 1e-6))) < 1e-5
+    g[5] = float("nan")
+    st = _C().grad_sumsq(g)
+    assert _C().clip_factor(st, 1.0).item() == 0.0
