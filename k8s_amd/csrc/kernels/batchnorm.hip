@@ -107,34 +107,53 @@ __global__ void __launch_bounds__(BN_THREADS) bn_stats_kernel(const uint16_t* __
   }
 }
 
-// One thread per channel: Chan-combine the per-block partials.
-__global__ void bn_stats_final_kernel(const float* __restrict__ part, int nblocks, long M, long rows_per_block,
-                                      int C, float eps, float momentum, float* __restrict__ mean_out,
-                                      float* __restrict__ invstd_out, float* __restrict__ run_mean,
-                                      float* __restrict__ run_var) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// Parallel finalize: a 256-thread block owns 32 channels; its 8 row groups
+// Chan-combine strided subsets of the per-block partials (coalesced: 32
+// consecutive channels = 256 contiguous bytes), then one LDS combine.
+constexpr int FIN_CH = 32, FIN_RG = 8;
+
+__device__ __forceinline__ void chan_merge(float& cnt, float& mean, float& m2, float nb, float bm, float bq) {
+  if (nb == 0.f) return;
+  const float tot = cnt + nb;
+  const float d = bm - mean;
+  mean += d * nb / tot;
+  m2 += bq + d * d * cnt * nb / tot;
+  cnt = tot;
+}
+
+__global__ void __launch_bounds__(256) bn_stats_final_kernel(const float* __restrict__ part, int nblocks, long M,
+                                                             long rows_per_block, int C, float eps, float momentum,
+                                                             float* __restrict__ mean_out,
+                                                             float* __restrict__ invstd_out,
+                                                             float* __restrict__ run_mean,
+                                                             float* __restrict__ run_var) {
+  __shared__ float sh[3][FIN_RG][FIN_CH];
+  const int cl = threadIdx.x % FIN_CH, rg = threadIdx.x / FIN_CH;
+  const int c = blockIdx.x * FIN_CH + cl;
   float cnt = 0.f, mean = 0.f, m2 = 0.f;
-  for (int b = 0; b < nblocks; ++b) {
-    long rows = M - (long)b * rows_per_block;
-    if (rows > rows_per_block) rows = rows_per_block;
-    if (rows <= 0) break;
-    const float nb = (float)rows;
-    const float bm = part[((long)b * C + c) * 2];
-    const float bq = part[((long)b * C + c) * 2 + 1];
-    const float tot = cnt + nb;
-    const float d = bm - mean;
-    mean += d * nb / tot;
-    m2 += bq + d * d * cnt * nb / tot;
-    cnt = tot;
+  if (c < C) {
+#pragma unroll 4
+    for (int b = rg; b < nblocks; b += FIN_RG) {
+      long rows = M - (long)b * rows_per_block;
+      rows = rows > rows_per_block ? rows_per_block : rows;
+      const float2 v = *reinterpret_cast<const float2*>(part + ((long)b * C + c) * 2);
+      chan_merge(cnt, mean, m2, rows > 0 ? (float)rows : 0.f, v.x, v.y);
+    }
   }
-  const float var = m2 / cnt;
-  mean_out[c] = mean;
-  invstd_out[c] = rsqrtf(var + eps);
-  if (run_mean) {
-    const float unbiased = cnt > 1.f ? m2 / (cnt - 1.f) : var;
-    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
-    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unbiased;
+  sh[0][rg][cl] = cnt;
+  sh[1][rg][cl] = mean;
+  sh[2][rg][cl] = m2;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    for (int r = 1; r < FIN_RG; ++r) chan_merge(cnt, mean, m2, sh[0][r][cl], sh[1][r][cl], sh[2][r][cl]);
+    const float var = m2 / cnt;
+    mean_out[c] = mean;
+    invstd_out[c] = rsqrtf(var + eps);
+    if (run_mean) {
+      const float unbiased = cnt > 1.f ? m2 / (cnt - 1.f) : var;
+      run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+      run_var[c] = (1.f - momentum) * run_var[c] + momentum * unbiased;
+    }
   }
 }
 
@@ -241,20 +260,34 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
   }
 }
 
-__global__ void bn_bwd_final_kernel(const float* __restrict__ part, int nblocks, int C,
-                                    float* __restrict__ sums, float* __restrict__ dgamma,
-                                    float* __restrict__ dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float a = 0.f, b = 0.f;
-  for (int i = 0; i < nblocks; ++i) {
-    a += part[((long)i * C + c) * 2];
-    b += part[((long)i * C + c) * 2 + 1];
+__global__ void __launch_bounds__(256) bn_bwd_final_kernel(const float* __restrict__ part, int nblocks, int C,
+                                                           float* __restrict__ sums, float* __restrict__ dgamma,
+                                                           float* __restrict__ dbeta) {
+  __shared__ float sh[2][FIN_RG][FIN_CH];
+  const int cl = threadIdx.x % FIN_CH, rg = threadIdx.x / FIN_CH;
+  const int c = blockIdx.x * FIN_CH + cl;
+  float a = 0.f, b2 = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int i = rg; i < nblocks; i += FIN_RG) {
+      const float2 v = *reinterpret_cast<const float2*>(part + ((long)i * C + c) * 2);
+      a += v.x;
+      b2 += v.y;
+    }
   }
-  sums[c] = a;
-  sums[C + c] = b;
-  if (dbeta) dbeta[c] = a;
-  if (dgamma) dgamma[c] = b;
+  sh[0][rg][cl] = a;
+  sh[1][rg][cl] = b2;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    for (int r = 1; r < FIN_RG; ++r) {
+      a += sh[0][r][cl];
+      b2 += sh[1][r][cl];
+    }
+    sums[c] = a;
+    sums[C + c] = b2;
+    if (dbeta) dbeta[c] = a;
+    if (dgamma) dgamma[c] = b2;
+  }
 }
 
 __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t* __restrict__ dy,
@@ -293,7 +326,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t
 // ---------------------------------------------------------------- launchers
 static long bn_rows_per_block(long M, const BnGeom& g) {
   // aim for ~1024 blocks in total; at least rows_per_iter*4 rows per block
-  long blocks_x = 1024 / g.grid_y;
+  long blocks_x = 512 / g.grid_y;
   if (blocks_x < 1) blocks_x = 1;
   long rpb = (M + blocks_x - 1) / blocks_x;
   long minr = (long)g.rows_per_iter * 4;
@@ -318,7 +351,7 @@ void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, c
     int nb = (int)((M + rpb - 1) / rpb);
     hipLaunchKernelGGL(bn_stats_kernel, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, x, M, C, g.tpr,
                        g.rows_per_iter, rpb, work);
-    hipLaunchKernelGGL(bn_stats_final_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, work, nb, M, rpb, C, eps,
+    hipLaunchKernelGGL(bn_stats_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, nb, M, rpb, C, eps,
                        momentum, save_mean, save_invstd, run_mean, run_var);
   } else {
     hipLaunchKernelGGL(bn_eval_prep_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, run_mean, run_var, C, eps,
@@ -337,7 +370,7 @@ void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, con
   int nb = (int)((M + rpb - 1) / rpb);
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, dy, x, y, mean, invstd, M,
                      C, g.tpr, g.rows_per_iter, rpb, work);
-  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, work, nb, C, sums, dgamma, dbeta);
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, nb, C, sums, dgamma, dbeta);
   const long nvec = M * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, dy, x, y,
                      mean, invstd, gamma, sums, dx, dres, nvec, C / 8, C, 1.f / (float)M);
