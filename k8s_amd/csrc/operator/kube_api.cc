@@ -1,0 +1,523 @@
+#include "kube_api.h"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <openssl/err.h>
+#include <openssl/ssl.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <sstream>
+
+#include "spec.h"
+#include "yaml_lite.h"
+
+namespace tfop {
+
+std::string ApiResult::message() const {
+  if (!error.empty()) return error;
+  if (body.is_object()) {
+    std::string m = get_str(body, "message");
+    if (!m.empty()) return m;
+  }
+  return "HTTP " + std::to_string(code);
+}
+
+std::string url_escape(const std::string& s) {
+  static const char* hex = "0123456789ABCDEF";
+  std::string o;
+  for (unsigned char c : s) {
+    if (isalnum(c) || c == '-' || c == '_' || c == '.' || c == '~' || c == '/') {
+      o += (char)c;
+    } else {
+      o += '%';
+      o += hex[c >> 4];
+      o += hex[c & 15];
+    }
+  }
+  return o;
+}
+
+std::string core_path(const std::string& ns, const std::string& resource, const std::string& name) {
+  std::string p = "/api/v1";
+  if (!ns.empty()) p += "/namespaces/" + ns;
+  p += "/" + resource;
+  if (!name.empty()) p += "/" + name;
+  return p;
+}
+
+std::string group_path(const std::string& gv, const std::string& ns, const std::string& resource,
+                       const std::string& name) {
+  std::string p = "/apis/" + gv;
+  if (!ns.empty()) p += "/namespaces/" + ns;
+  p += "/" + resource;
+  if (!name.empty()) p += "/" + name;
+  return p;
+}
+
+std::string tfjobs_path(const std::string& ns, const std::string& name) {
+  return group_path(std::string(kCRDGroup) + "/" + kCRDVersion, ns, kCRDKindPlural, name);
+}
+
+std::string crd_path(const std::string& name) {
+  return "/apis/apiextensions.k8s.io/v1/customresourcedefinitions" + (name.empty() ? "" : "/" + name);
+}
+
+// ------------------------------------------------------------------ config
+ClusterConfig parse_master_url(const std::string& url) {
+  ClusterConfig c;
+  std::string u = url;
+  if (u.rfind("http://", 0) == 0) {
+    c.tls = false;
+    c.port = 80;
+    u = u.substr(7);
+  } else if (u.rfind("https://", 0) == 0) {
+    c.tls = true;
+    c.port = 443;
+    u = u.substr(8);
+  }
+  size_t slash = u.find('/');
+  if (slash != std::string::npos) u = u.substr(0, slash);
+  size_t colon = u.rfind(':');
+  if (colon != std::string::npos && u.find(']') == std::string::npos) {
+    c.port = atoi(u.substr(colon + 1).c_str());
+    u = u.substr(0, colon);
+  }
+  c.host = u;
+  return c;
+}
+
+static std::string env(const char* k) {
+  const char* v = getenv(k);
+  return v ? v : "";
+}
+
+ClusterConfig cluster_config_from_env(const std::string& master_url) {
+  if (!master_url.empty()) return parse_master_url(master_url);
+  if (!env("K8S_AMD_APISERVER").empty()) return parse_master_url(env("K8S_AMD_APISERVER"));
+  const std::string kc = env("KUBECONFIG");
+  if (!kc.empty()) {
+    Json cfg = yaml_parse(read_file(kc));
+    std::string cur = get_str(cfg, "current-context");
+    std::string cluster_name, user_name;
+    if (const Json* ctxs = cfg.find("contexts"); ctxs && ctxs->is_array())
+      for (auto& c : ctxs->as_array())
+        if (get_str(c, "name") == cur || cur.empty()) {
+          if (const Json* cc = c.find("context")) {
+            cluster_name = get_str(*cc, "cluster");
+            user_name = get_str(*cc, "user");
+          }
+          break;
+        }
+    ClusterConfig out;
+    if (const Json* cl = cfg.find("clusters"); cl && cl->is_array())
+      for (auto& c : cl->as_array())
+        if (get_str(c, "name") == cluster_name || cluster_name.empty()) {
+          if (const Json* cc = c.find("cluster")) {
+            out = parse_master_url(get_str(*cc, "server"));
+            out.ca_file = get_str(*cc, "certificate-authority");
+            if (const Json* v = cc->find("insecure-skip-tls-verify"); v && v->is_bool()) out.insecure = v->as_bool();
+          }
+          break;
+        }
+    if (const Json* us = cfg.find("users"); us && us->is_array())
+      for (auto& u : us->as_array())
+        if (get_str(u, "name") == user_name || user_name.empty()) {
+          if (const Json* uu = u.find("user")) out.token = get_str(*uu, "token");
+          break;
+        }
+    return out;
+  }
+  // in-cluster (pkg/util/k8sutil/k8sutil.go:54-63: default port 443)
+  ClusterConfig c;
+  c.host = env("KUBERNETES_SERVICE_HOST");
+  if (c.host.empty()) c.host = "kubernetes.default.svc";
+  const std::string port = env("KUBERNETES_SERVICE_PORT");
+  c.port = port.empty() ? 443 : atoi(port.c_str());
+  c.tls = true;
+  const std::string sa = "/var/run/secrets/kubernetes.io/serviceaccount/";
+  try {
+    c.token = read_file(sa + "token");
+    while (!c.token.empty() && isspace((unsigned char)c.token.back())) c.token.pop_back();
+  } catch (...) {
+  }
+  c.ca_file = sa + "ca.crt";
+  return c;
+}
+
+// ------------------------------------------------------------------ transport
+namespace {
+
+std::once_flag ssl_once;
+
+class Conn {
+ public:
+  Conn(const ClusterConfig& cfg) : cfg_(cfg) {}
+  ~Conn() { close(); }
+
+  bool open(std::string& err) {
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_UNSPEC;
+    hints.ai_socktype = SOCK_STREAM;
+    int rc = getaddrinfo(cfg_.host.c_str(), std::to_string(cfg_.port).c_str(), &hints, &res);
+    if (rc != 0) {
+      err = std::string("resolve ") + cfg_.host + ": " + gai_strerror(rc);
+      return false;
+    }
+    for (addrinfo* a = res; a; a = a->ai_next) {
+      fd_ = socket(a->ai_family, a->ai_socktype, a->ai_protocol);
+      if (fd_ < 0) continue;
+      if (connect(fd_, a->ai_addr, a->ai_addrlen) == 0) break;
+      ::close(fd_);
+      fd_ = -1;
+    }
+    freeaddrinfo(res);
+    if (fd_ < 0) {
+      err = "connect " + cfg_.host + ":" + std::to_string(cfg_.port) + ": " + strerror(errno);
+      return false;
+    }
+    int one = 1;
+    setsockopt(fd_, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    if (cfg_.tls) {
+      std::call_once(ssl_once, [] {
+        SSL_library_init();
+        SSL_load_error_strings();
+      });
+      ctx_ = SSL_CTX_new(TLS_client_method());
+      if (!cfg_.insecure) {
+        if (!cfg_.ca_file.empty()) SSL_CTX_load_verify_locations(ctx_, cfg_.ca_file.c_str(), nullptr);
+        else SSL_CTX_set_default_verify_paths(ctx_);
+        SSL_CTX_set_verify(ctx_, SSL_VERIFY_PEER, nullptr);
+      }
+      ssl_ = SSL_new(ctx_);
+      SSL_set_fd(ssl_, fd_);
+      SSL_set_tlsext_host_name(ssl_, cfg_.host.c_str());
+      if (SSL_connect(ssl_) != 1) {
+        char buf[256];
+        ERR_error_string_n(ERR_get_error(), buf, sizeof buf);
+        err = std::string("TLS handshake: ") + buf;
+        return false;
+      }
+    }
+    return true;
+  }
+
+  void close() {
+    if (ssl_) {
+      SSL_shutdown(ssl_);
+      SSL_free(ssl_);
+      ssl_ = nullptr;
+    }
+    if (ctx_) {
+      SSL_CTX_free(ctx_);
+      ctx_ = nullptr;
+    }
+    if (fd_ >= 0) {
+      ::close(fd_);
+      fd_ = -1;
+    }
+  }
+
+  bool write_all(const std::string& s) {
+    size_t off = 0;
+    while (off < s.size()) {
+      long n = ssl_ ? SSL_write(ssl_, s.data() + off, (int)(s.size() - off))
+                    : ::send(fd_, s.data() + off, s.size() - off, MSG_NOSIGNAL);
+      if (n <= 0) return false;
+      off += (size_t)n;
+    }
+    return true;
+  }
+
+  // -1 error/EOF, 0 timeout, >0 bytes
+  long read_some(char* buf, size_t n, int timeout_ms) {
+    if (!(ssl_ && SSL_pending(ssl_) > 0) && timeout_ms >= 0) {
+      pollfd p{fd_, POLLIN, 0};
+      int r = poll(&p, 1, timeout_ms);
+      if (r == 0) return 0;
+      if (r < 0) return -1;
+    }
+    long k = ssl_ ? SSL_read(ssl_, buf, (int)n) : ::recv(fd_, buf, n, 0);
+    return k <= 0 ? -1 : k;
+  }
+
+ private:
+  ClusterConfig cfg_;
+  int fd_ = -1;
+  SSL_CTX* ctx_ = nullptr;
+  SSL* ssl_ = nullptr;
+};
+
+// Buffered HTTP/1.1 response reader (Content-Length, chunked, or read-to-close bodies).
+class Reader {
+ public:
+  explicit Reader(Conn& c) : c_(c) {}
+
+  // returns -1 err, 0 timeout, 1 ok
+  int fill(int timeout_ms) {
+    char buf[16384];
+    long n = c_.read_some(buf, sizeof buf, timeout_ms);
+    if (n == 0) return 0;
+    if (n < 0) return -1;
+    buf_.append(buf, (size_t)n);
+    return 1;
+  }
+
+  bool line(std::string& out, int timeout_ms = -1) {
+    while (true) {
+      size_t p = buf_.find("\r\n");
+      if (p != std::string::npos) {
+        out = buf_.substr(0, p);
+        buf_.erase(0, p + 2);
+        return true;
+      }
+      if (fill(timeout_ms) <= 0) return false;
+    }
+  }
+
+  bool exact(size_t n, std::string& out) {
+    while (buf_.size() < n)
+      if (fill(-1) <= 0) return false;
+    out = buf_.substr(0, n);
+    buf_.erase(0, n);
+    return true;
+  }
+
+  std::string rest_until_close() {
+    while (fill(-1) > 0) {
+    }
+    std::string o;
+    o.swap(buf_);
+    return o;
+  }
+
+  std::string& buffer() { return buf_; }
+
+ private:
+  Conn& c_;
+  std::string buf_;
+};
+
+struct Head {
+  int code = 0;
+  bool chunked = false;
+  long content_length = -1;
+};
+
+bool read_head(Reader& r, Head& h, std::string& err) {
+  std::string l;
+  if (!r.line(l)) {
+    err = "connection closed before response";
+    return false;
+  }
+  // HTTP/1.1 200 OK
+  size_t sp = l.find(' ');
+  h.code = sp == std::string::npos ? 0 : atoi(l.c_str() + sp + 1);
+  while (r.line(l)) {
+    if (l.empty()) return true;
+    size_t c = l.find(':');
+    if (c == std::string::npos) continue;
+    std::string k = l.substr(0, c), v = l.substr(c + 1);
+    while (!v.empty() && v[0] == ' ') v.erase(0, 1);
+    for (auto& ch : k) ch = (char)tolower((unsigned char)ch);
+    if (k == "transfer-encoding" && v.find("chunked") != std::string::npos) h.chunked = true;
+    if (k == "content-length") h.content_length = atol(v.c_str());
+  }
+  err = "truncated headers";
+  return false;
+}
+
+std::string build_request(const ClusterConfig& cfg, const std::string& method, const std::string& path,
+                          const std::string& body, const std::string& ctype, bool keep) {
+  std::ostringstream o;
+  o << method << " " << path << " HTTP/1.1\r\n";
+  o << "Host: " << cfg.host << ":" << cfg.port << "\r\n";
+  o << "User-Agent: tf_operator-amd/0.3.0\r\n";
+  o << "Accept: application/json\r\n";
+  if (!cfg.token.empty()) o << "Authorization: Bearer " << cfg.token << "\r\n";
+  if (!body.empty() || method == "POST" || method == "PUT" || method == "PATCH") {
+    o << "Content-Type: " << ctype << "\r\n";
+    o << "Content-Length: " << body.size() << "\r\n";
+  }
+  o << "Connection: " << (keep ? "keep-alive" : "close") << "\r\n\r\n";
+  o << body;
+  return o.str();
+}
+
+class HttpWatch : public WatchStream {
+ public:
+  HttpWatch(std::unique_ptr<Conn> c, bool chunked, std::string prefix)
+      : conn_(std::move(c)), rd_(*conn_), chunked_(chunked) {
+    rd_.buffer() = std::move(prefix);  // body bytes already read together with the headers
+  }
+  bool next(Json& ev, int timeout_ms, std::string& err) override {
+    ev = Json();
+    while (true) {
+      size_t p = lines_.find('\n');
+      if (p != std::string::npos) {
+        std::string l = lines_.substr(0, p);
+        lines_.erase(0, p + 1);
+        if (l.find_first_not_of(" \r\t") == std::string::npos) continue;
+        try {
+          ev = Json::parse(l);
+        } catch (const std::exception& e) {
+          err = e.what();
+          return false;
+        }
+        return true;
+      }
+      if (!pull(timeout_ms, err)) return false;
+      if (timed_out_) {
+        timed_out_ = false;
+        return true;
+      }
+    }
+  }
+  void close() override { conn_->close(); }
+
+ private:
+  // move decoded body bytes into lines_
+  bool pull(int timeout_ms, std::string& err) {
+    if (!chunked_) {
+      int r = rd_.fill(timeout_ms);
+      if (r == 0) {
+        timed_out_ = true;
+        return true;
+      }
+      if (r < 0) {
+        err = "watch stream closed";
+        return false;
+      }
+      lines_ += rd_.buffer();
+      rd_.buffer().clear();
+      return true;
+    }
+    while (true) {
+      std::string& b = rd_.buffer();
+      if (chunk_left_ > 0) {
+        if (b.empty()) {
+          int r = rd_.fill(timeout_ms);
+          if (r == 0) {
+            timed_out_ = true;
+            return true;
+          }
+          if (r < 0) {
+            err = "watch stream closed";
+            return false;
+          }
+          continue;
+        }
+        size_t n = std::min<size_t>(chunk_left_, b.size());
+        lines_.append(b, 0, n);
+        b.erase(0, n);
+        chunk_left_ -= n;
+        if (chunk_left_ == 0) need_crlf_ = true;
+        return true;
+      }
+      std::string l;
+      if (need_crlf_) {
+        if (!rd_.line(l, timeout_ms)) {
+          err = "watch stream closed";
+          return false;
+        }
+        need_crlf_ = false;
+      }
+      if (!rd_.line(l, timeout_ms)) {
+        err = "watch stream closed";
+        return false;
+      }
+      long n = strtol(l.c_str(), nullptr, 16);
+      if (n == 0) {
+        err = "watch stream ended";
+        return false;
+      }
+      chunk_left_ = (size_t)n;
+    }
+  }
+
+  std::unique_ptr<Conn> conn_;
+  Reader rd_;
+  bool chunked_;
+  std::string lines_;
+  size_t chunk_left_ = 0;
+  bool need_crlf_ = false;
+  bool timed_out_ = false;
+};
+
+class HttpKubeApi : public KubeApi {
+ public:
+  explicit HttpKubeApi(ClusterConfig cfg) : cfg_(std::move(cfg)) {}
+
+  ApiResult request(const std::string& method, const std::string& path, const Json* body,
+                    const std::string& ctype) override {
+    ApiResult res;
+    Conn c(cfg_);
+    if (!c.open(res.error)) return res;
+    std::string b = body ? body->dump() : "";
+    if (!c.write_all(build_request(cfg_, method, path, b, ctype, false))) {
+      res.error = "write failed";
+      return res;
+    }
+    Reader r(c);
+    Head h;
+    if (!read_head(r, h, res.error)) return res;
+    std::string payload;
+    if (h.chunked) {
+      std::string l, chunk;
+      while (r.line(l)) {
+        long n = strtol(l.c_str(), nullptr, 16);
+        if (n <= 0) break;
+        if (!r.exact((size_t)n, chunk)) break;
+        payload += chunk;
+        r.line(l);
+      }
+    } else if (h.content_length >= 0) {
+      r.exact((size_t)h.content_length, payload);
+    } else {
+      payload = r.rest_until_close();
+    }
+    res.code = h.code;
+    if (!payload.empty()) {
+      try {
+        res.body = Json::parse(payload);
+      } catch (...) {
+        res.body = Json(payload);
+      }
+    }
+    return res;
+  }
+
+  std::unique_ptr<WatchStream> watch(const std::string& path, std::string& err) override {
+    auto c = std::make_unique<Conn>(cfg_);
+    if (!c->open(err)) return nullptr;
+    if (!c->write_all(build_request(cfg_, "GET", path, "", "", true))) {
+      err = "write failed";
+      return nullptr;
+    }
+    Reader r(*c);
+    Head h;
+    if (!read_head(r, h, err)) return nullptr;
+    if (h.code != 200) {
+      err = "watch HTTP " + std::to_string(h.code);
+      return nullptr;
+    }
+    std::string leftover = r.buffer();
+    return std::make_unique<HttpWatch>(std::move(c), h.chunked, std::move(leftover));
+  }
+
+ private:
+  ClusterConfig cfg_;
+};
+
+}  // namespace
+
+std::unique_ptr<KubeApi> make_http_api(const ClusterConfig& cfg) { return std::make_unique<HttpKubeApi>(cfg); }
+
+}  // namespace tfop
