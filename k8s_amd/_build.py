@@ -140,7 +140,7 @@ def build_operator(force=False) -> list:
             fut.result()
     outs = []
     core_objs = [objs[s] for s in core]
-    libflags = ["-lpthread"] + extra
+    libflags = ["-lssl", "-lcrypto", "-lpthread"] + extra
     for s in srcs:
         b = os.path.basename(s)
         if b.startswith("py_"):

@@ -1,0 +1,214 @@
+#include "controller.h"
+
+#include <cstdlib>
+#include <thread>
+
+#include "log.h"
+
+namespace tfop {
+
+Json crd_manifest() {
+  const char* text = R"JSON({
+  "apiVersion": "apiextensions.k8s.io/v1",
+  "kind": "CustomResourceDefinition",
+  "metadata": {"name": "tfjobs.tensorflow.org"},
+  "spec": {
+    "group": "tensorflow.org",
+    "scope": "Namespaced",
+    "names": {"plural": "tfjobs", "singular": "tfjob", "kind": "TfJob", "shortNames": ["tfj"]},
+    "versions": [{
+      "name": "v1alpha1", "served": true, "storage": true,
+      "schema": {"openAPIV3Schema": {"type": "object", "x-kubernetes-preserve-unknown-fields": true}},
+      "additionalPrinterColumns": [
+        {"name": "Phase", "type": "string", "jsonPath": ".status.phase"},
+        {"name": "State", "type": "string", "jsonPath": ".status.state"},
+        {"name": "RuntimeId", "type": "string", "jsonPath": ".spec.RuntimeId"},
+        {"name": "Age", "type": "date", "jsonPath": ".metadata.creationTimestamp"}
+      ]
+    }]
+  }
+})JSON";
+  return Json::parse(text);
+}
+
+Controller::Controller(KubeApi& api, ControllerConfig cfg, ControllerOptions opts)
+    : api_(api), cfg_(std::move(cfg)), opts_(std::move(opts)) {}
+
+Controller::~Controller() {
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto& kv : jobs_) kv.second->stop();
+  jobs_.clear();
+}
+
+static bool crd_established(const Json& crd) {
+  const Json* st = crd.find("status");
+  if (!st) return false;
+  const Json* conds = st->find("conditions");
+  if (!conds || !conds->is_array()) return false;
+  for (auto& c : conds->as_array())
+    if (get_str(c, "type") == "Established" && get_str(c, "status") == "True") return true;
+  return false;
+}
+
+std::string Controller::init_resource() {
+  if (opts_.create_crd) {
+    Json crd = crd_manifest();
+    ApiResult r = api_.post(crd_path(), crd);
+    if (!r.ok() && !r.already_exists()) return "create CRD: " + r.message();
+    const auto deadline = std::chrono::steady_clock::now() + opts_.crd_timeout;
+    while (true) {
+      ApiResult g = api_.get(crd_path(crd_name()));
+      if (g.ok() && crd_established(g.body)) break;
+      if (std::chrono::steady_clock::now() > deadline) {
+        if (r.ok()) api_.del(crd_path(crd_name()));  // we created it; do not leave a half-initialised CRD
+        return "CRD " + crd_name() + " did not become Established";
+      }
+      std::this_thread::sleep_for(opts_.crd_poll);
+    }
+  }
+  return "";
+}
+
+std::string Controller::find_all_jobs(std::string& rv) {
+  ApiResult r = api_.get(list_path());
+  if (!r.ok()) return "list tfjobs: " + r.message();
+  if (const Json* m = r.body.find("metadata")) rv = get_str(*m, "resourceVersion");
+  if (const Json* items = r.body.find("items"); items && items->is_array()) {
+    for (auto& it : items->as_array()) handle_event("ADDED", it);
+  }
+  return "";
+}
+
+void Controller::handle_event(const std::string& type, const Json& obj) {
+  TfJob job;
+  try {
+    job = tfjob_from_json(obj);
+  } catch (const std::exception& e) {
+    log_error("bad TfJob object in %s event: %s", type.c_str(), e.what());
+    return;
+  }
+  const std::string key = job.ns() + "/" + job.name();
+  std::lock_guard<std::mutex> g(mu_);
+  job_rvs_[key] = job.resource_version();
+  if (type == "DELETED") {
+    auto it = jobs_.find(key);
+    if (it != jobs_.end()) it->second->request_delete();
+    job_rvs_.erase(key);
+    return;
+  }
+  // Failed jobs are ignored until deleted (controller.go:126-133)
+  if (job.status.state == "Failed" && !jobs_.count(key)) return;
+  auto it = jobs_.find(key);
+  if (it != jobs_.end() && !it->second->finished()) {
+    if (type == "MODIFIED") it->second->update(job);
+    return;
+  }
+  if (type == "ADDED" || type == "MODIFIED") {
+    log_info("Starting TfJob %s (phase=%s)", key.c_str(), job.status.phase.c_str());
+    auto tj = std::make_unique<TrainingJob>(api_, job, cfg_, opts_.reconcile);
+    jobs_[key] = std::make_unique<JobWorker>(std::move(tj), opts_.reconcile.interval);
+  }
+}
+
+void Controller::reap_finished() {
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto it = jobs_.begin(); it != jobs_.end();) {
+    if (it->second->finished() && !job_rvs_.count(it->first)) it = jobs_.erase(it);
+    else ++it;
+  }
+}
+
+size_t Controller::num_jobs() {
+  std::lock_guard<std::mutex> g(mu_);
+  return jobs_.size();
+}
+
+std::map<std::string, TfJobStatus> Controller::statuses() {
+  std::lock_guard<std::mutex> g(mu_);
+  std::map<std::string, TfJobStatus> out;
+  for (auto& kv : jobs_) out[kv.first] = kv.second->job().status();
+  return out;
+}
+
+std::string Controller::run() {
+  // initResource with retry (controller.go:86-96)
+  while (!stop_) {
+    std::string err = init_resource();
+    if (err.empty()) break;
+    log_error("initResource failed: %s; retrying in %lld ms", err.c_str(), (long long)opts_.init_retry.count());
+    for (int i = 0; i < opts_.init_retry.count() / 100 && !stop_; ++i)
+      std::this_thread::sleep_for(std::chrono::milliseconds(100));
+  }
+  std::string rv;
+  while (!stop_) {
+    std::string err = find_all_jobs(rv);
+    if (err.empty()) break;
+    log_error("%s; retrying", err.c_str());
+    std::this_thread::sleep_for(std::chrono::seconds(1));
+  }
+  while (!stop_) {
+    std::string err;
+    auto w = api_.watch(list_path() + "?watch=true&resourceVersion=" + rv, err);
+    if (!w) {
+      log_warn("watch failed: %s; retrying", err.c_str());
+      std::this_thread::sleep_for(std::chrono::seconds(1));
+      continue;
+    }
+    while (!stop_) {
+      Json ev;
+      if (!w->next(ev, 1000, err)) {
+        log_v(1, "watch stream ended: %s; re-watching from %s", err.c_str(), rv.c_str());
+        break;
+      }
+      reap_finished();
+      if (ev.is_null()) continue;  // timeout tick
+      const std::string type = get_str(ev, "type");
+      const Json* obj = ev.find("object");
+      if (type == "ERROR") {
+        const int code = obj ? (int)(obj->find("code") ? obj->at("code").as_int() : 0) : 0;
+        if (code == 410) {
+          // resourceVersion too old: relist and diff (removed jobs are deleted, new ones started)
+          log_warn("watch 410 Gone at rv=%s: relisting", rv.c_str());
+          std::map<std::string, std::string> before;
+          {
+            std::lock_guard<std::mutex> g(mu_);
+            before = job_rvs_;
+          }
+          ApiResult l = api_.get(list_path());
+          if (!l.ok()) break;
+          std::map<std::string, bool> seen;
+          if (const Json* items = l.body.find("items"); items && items->is_array())
+            for (auto& it : items->as_array()) {
+              TfJob j = tfjob_from_json(it);
+              seen[j.ns() + "/" + j.name()] = true;
+              handle_event("ADDED", it);
+            }
+          for (auto& kv : before)
+            if (!seen.count(kv.first)) {
+              std::lock_guard<std::mutex> g(mu_);
+              auto jt = jobs_.find(kv.first);
+              if (jt != jobs_.end()) jt->second->request_delete();
+              job_rvs_.erase(kv.first);
+            }
+          if (const Json* m = l.body.find("metadata")) rv = get_str(*m, "resourceVersion");
+          break;
+        }
+        log_error("watch ERROR event: %s", obj ? obj->dump().c_str() : "");
+        break;
+      }
+      if (!obj) continue;
+      if (const Json* m = obj->find("metadata")) rv = get_str(*m, "resourceVersion");
+      // panicTimer equivalent: a single event handler must not wedge the controller
+      auto t0 = std::chrono::steady_clock::now();
+      handle_event(type, *obj);
+      if (std::chrono::steady_clock::now() - t0 > opts_.event_watchdog) {
+        log_error("handling a TfJob event took longer than the watchdog; aborting");
+        std::abort();
+      }
+    }
+    w->close();
+  }
+  return "";
+}
+
+}  // namespace tfop

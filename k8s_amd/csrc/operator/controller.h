@@ -1,0 +1,69 @@
+// TfJob controller: CRD registration, list + re-adopt, watch, dispatch.
+//
+// Parity: /root/reference/pkg/controller/controller.go (Run :80-121,
+// handleTfJobEvent :123-170, findAllTfJobs :172-201, initResource/createCRD
+// :213-286, watch + 410 relist :292-376) and pkg/controller/util.go
+// (pollEvent, panicTimer watchdog).
+//
+// Differences by design: CRD is apiextensions.k8s.io/v1 (v1beta1 is gone
+// since K8s 1.22); jobs are keyed by namespace/name everywhere (Q4/Q5 fix);
+// a 410 Gone relists and diffs instead of tearing the controller down.
+#pragma once
+
+#include <atomic>
+#include <chrono>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+
+#include "kube_api.h"
+#include "reconciler.h"
+#include "spec.h"
+
+namespace tfop {
+
+struct ControllerOptions {
+  std::string ns;               // namespace to manage ("" = all namespaces)
+  ReconcileOptions reconcile;   // per-job options (interval, PS server)
+  std::chrono::milliseconds init_retry{30000};
+  std::chrono::milliseconds crd_poll{500};
+  std::chrono::milliseconds crd_timeout{60000};
+  std::chrono::milliseconds event_watchdog{60000};  // panicTimer: abort if one event takes longer
+  bool create_crd = true;
+};
+
+Json crd_manifest();  // the CustomResourceDefinition the operator installs
+
+class Controller {
+ public:
+  Controller(KubeApi& api, ControllerConfig cfg, ControllerOptions opts);
+  ~Controller();
+
+  // Blocks until stop() is called (or a fatal error). Returns an error message ("" on clean stop).
+  std::string run();
+  void stop() { stop_ = true; }
+
+  // introspection for tests
+  size_t num_jobs();
+  std::map<std::string, TfJobStatus> statuses();
+
+  // one-shot pieces, public for tests
+  std::string init_resource();
+  std::string find_all_jobs(std::string& resource_version);
+  void handle_event(const std::string& type, const Json& obj);
+
+ private:
+  std::string list_path() const { return tfjobs_path(opts_.ns); }
+  void reap_finished();
+
+  KubeApi& api_;
+  ControllerConfig cfg_;
+  ControllerOptions opts_;
+  std::atomic<bool> stop_{false};
+  std::mutex mu_;
+  std::map<std::string, std::unique_ptr<JobWorker>> jobs_;  // ns/name -> worker
+  std::map<std::string, std::string> job_rvs_;               // ns/name -> resourceVersion
+};
+
+}  // namespace tfop

@@ -1,0 +1,58 @@
+// Leader election for operator HA.
+//
+// Parity: /root/reference/pkg/util/k8sutil/election/election.go (acquire /
+// renew / tryAcquireOrRenew :141-265, lease > renew > 1.2 x retry check
+// :73-86) and resourcelock/endpointslock.go + interface.go (record stored as
+// JSON in the Endpoints annotation control-plane.alpha.kubernetes.io/leader).
+// The record format is unchanged so mixed deployments interoperate.
+#pragma once
+
+#include <atomic>
+#include <chrono>
+#include <functional>
+#include <string>
+
+#include "kube_api.h"
+
+namespace tfop {
+
+constexpr const char* kLeaderAnnotation = "control-plane.alpha.kubernetes.io/leader";
+
+struct LeaderElectionRecord {
+  std::string holder_identity;
+  int lease_duration_seconds = 0;
+  std::string acquire_time, renew_time;  // RFC3339
+  int leader_transitions = 0;
+  Json to_json() const;
+  static LeaderElectionRecord from_json(const Json& j);
+};
+
+struct ElectionConfig {
+  std::string ns, name, identity;
+  std::chrono::milliseconds lease{15000}, renew_deadline{5000}, retry{3000};
+};
+
+class LeaderElector {
+ public:
+  LeaderElector(KubeApi& api, ElectionConfig cfg);
+  // error text if the durations are inconsistent (lease > renew > 1.2*retry)
+  std::string check() const;
+  // one acquire/renew attempt; true if we hold the lock afterwards
+  bool try_acquire_or_renew();
+  // Blocks: acquire, run on_started (in this thread's caller's stead: a separate thread), renew until lost.
+  // Returns when leadership is lost or stop is set.
+  void run(const std::function<void()>& on_started, const std::function<void()>& on_stopped,
+           const std::atomic<bool>& stop);
+  bool is_leader() const { return leader_; }
+
+ private:
+  KubeApi& api_;
+  ElectionConfig cfg_;
+  LeaderElectionRecord observed_;
+  std::chrono::steady_clock::time_point observed_time_;
+  bool leader_ = false;
+};
+
+std::string now_rfc3339();
+
+}  // namespace tfop

@@ -7,6 +7,7 @@
 #pragma once
 
 #include <cstdint>
+#include <deque>
 #include <map>
 #include <memory>
 #include <stdexcept>
@@ -18,7 +19,7 @@ namespace tfop {
 
 class Json;
 using JsonArray = std::vector<Json>;
-using JsonObject = std::vector<std::pair<std::string, Json>>;
+using JsonObject = std::deque<std::pair<std::string, Json>>;  // deque: references stay valid on insert
 
 struct JsonError : std::runtime_error {
   using std::runtime_error::runtime_error;

@@ -1,0 +1,156 @@
+// tf_operator: the TfJob operator binary.
+//
+// Parity: /root/reference/cmd/tf_operator/main.go (flags :48-54, config
+// file :68-85, MY_POD_NAMESPACE / MY_POD_NAME :89-96, signal exit :98-103,
+// version :105-116, Endpoints leader election 15s/5s/3s :42-44,125-148,
+// controller run loop :153-169). The chaos monkey the reference left
+// commented out (:171-207) is implemented: -chaos-level N deletes a random
+// TfJob pod every 30/N seconds (fault injection for the exit-code/restart
+// state machine).
+#include <signal.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <thread>
+
+#include "controller.h"
+#include "election.h"
+#include "flags.h"
+#include "log.h"
+#include "yaml_lite.h"
+
+using namespace tfop;
+
+static std::atomic<bool> g_stop{false};
+
+static long parse_duration_ms(const std::string& s, long def) {
+  if (s.empty()) return def;
+  size_t i = 0;
+  double v = std::stod(s, &i);
+  std::string unit = s.substr(i);
+  if (unit == "ms") return (long)v;
+  if (unit == "s" || unit.empty()) return (long)(v * 1000);
+  if (unit == "m") return (long)(v * 60000);
+  if (unit == "h") return (long)(v * 3600000);
+  return def;
+}
+
+static void chaos_loop(KubeApi* api, std::string ns, int level) {
+  std::mt19937 rng{std::random_device{}()};
+  while (!g_stop) {
+    for (int i = 0; i < 300 / level && !g_stop; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    ApiResult l = api->get(core_path(ns, "pods") + "?labelSelector=tensorflow.org%3D");
+    if (!l.ok()) continue;
+    const Json* items = l.body.find("items");
+    if (!items || !items->is_array() || items->size() == 0) continue;
+    const Json& p = (*items)[rng() % items->size()];
+    const std::string name = get_str(p.at("metadata"), "name");
+    log_warn("chaos: deleting pod %s/%s", ns.c_str(), name.c_str());
+    api->del(core_path(ns, "pods", name));
+  }
+}
+
+int main(int argc, char** argv) {
+  Flags fl;
+  fl.def("controller_config_file", "", "Path to file containing the controller config.");
+  fl.def("version", "false", "Show version and quit", true);
+  fl.def("chaos-level", "-1", "DO NOT USE IN PRODUCTION - level of chaos injected into the TfJob created by the operator.");
+  fl.def("gc-interval", "10m", "GC interval");
+  fl.def("master", "", "API server URL (default: $K8S_AMD_APISERVER, $KUBECONFIG, then in-cluster)");
+  fl.def("namespace", "", "Namespace to manage (default $MY_POD_NAMESPACE)");
+  fl.def("all-namespaces", "false", "Manage TfJobs in every namespace", true);
+  fl.def("reconcile-interval", "8s", "Resync period of every TfJob (reference: 8s)");
+  fl.def("leader-elect", "true", "Run leader election on Endpoints tf-operator", true);
+  fl.def("create-crd", "true", "Register the tfjobs.tensorflow.org CRD at startup", true);
+  std::string err = fl.parse(argc, argv);
+  if (!err.empty()) {
+    fprintf(stderr, "%s\nUsage of tf_operator:\n%s", err.c_str(), fl.usage().c_str());
+    return 2;
+  }
+  g_verbosity = fl.num("v");
+  if (fl.on("version")) {
+    printf("tf_operator Version: %s\nGit SHA: %s\nGo Version: n/a (C++17)\nGo OS/Arch: linux/amd64\n", kVersion,
+           kGitSHA);
+    return 0;
+  }
+  ControllerConfig cfg;
+  if (!fl.str("controller_config_file").empty()) {
+    try {
+      cfg = controller_config_from_json(yaml_parse(read_file(fl.str("controller_config_file"))));
+    } catch (const std::exception& e) {
+      log_error("could not read controller config file %s: %s", fl.str("controller_config_file").c_str(), e.what());
+      return 1;
+    }
+  } else {
+    log_info("No controller_config_file provided; using empty config.");
+  }
+  std::string ns = fl.str("namespace");
+  if (ns.empty() && getenv("MY_POD_NAMESPACE")) ns = getenv("MY_POD_NAMESPACE");
+  if (ns.empty()) {
+    log_error("must set env MY_POD_NAMESPACE");
+    return 1;
+  }
+  std::string pod = getenv("MY_POD_NAME") ? getenv("MY_POD_NAME") : "";
+  if (pod.empty()) {
+    log_error("must set env MY_POD_NAME");
+    return 1;
+  }
+  for (int s : {SIGINT, SIGTERM}) signal(s, [](int sig) {
+      log_info("received signal: %d, exiting", sig);
+      _exit(1);
+    });
+  log_info("tf_operator Version: %s", kVersion);
+
+  ClusterConfig cc;
+  try {
+    cc = cluster_config_from_env(fl.str("master"));
+  } catch (const std::exception& e) {
+    log_error("cluster config: %s", e.what());
+    return 1;
+  }
+  auto api = make_http_api(cc);
+
+  ControllerOptions opts;
+  opts.ns = fl.on("all-namespaces") ? "" : ns;
+  opts.create_crd = fl.on("create-crd");
+  opts.reconcile.interval = std::chrono::milliseconds(parse_duration_ms(fl.str("reconcile-interval"), 8000));
+  if (!cfg.grpc_server_file_path.empty()) {
+    try {
+      opts.reconcile.ps_server_source = read_file(cfg.grpc_server_file_path);
+    } catch (const std::exception& e) {
+      log_error("cannot read grpcServerFilePath %s: %s", cfg.grpc_server_file_path.c_str(), e.what());
+    }
+  }
+  const int chaos = fl.num("chaos-level");
+  if (chaos > 0) std::thread(chaos_loop, api.get(), ns, chaos).detach();
+
+  auto run_controller = [&] {
+    Controller c(*api, cfg, opts);
+    std::string e = c.run();
+    if (!e.empty()) {
+      log_error("controller Run() ended with failure: %s", e.c_str());
+      _exit(1);
+    }
+  };
+  if (!fl.on("leader-elect")) {
+    run_controller();
+    return 0;
+  }
+  ElectionConfig ec;
+  ec.ns = ns;
+  ec.name = "tf-operator";
+  ec.identity = pod;
+  LeaderElector el(*api, ec);
+  if (std::string e = el.check(); !e.empty()) {
+    log_error("leader election config: %s", e.c_str());
+    return 1;
+  }
+  el.run(run_controller, [] {
+    log_error("leader election lost");
+    _exit(1);
+  }, g_stop);
+  return 0;
+}

@@ -1,0 +1,110 @@
+// Per-TfJob reconciler (the TrainingJob of the reference).
+//
+// Parity: /root/reference/pkg/trainer/training.go (setup :245-301,
+// createResources :131-145, GetStatus :163-199, updateTPRStatus :331-347,
+// reconcile :350-409, run :412-456, delete :303-320),
+// pkg/trainer/replicas.go (Create :124-271, Delete :299-356, GetStatus
+// :415-492) and pkg/trainer/tensorboard.go (Create/Delete :40-138).
+//
+// Deliberate fixes of the reference quirks:
+//  Q1  re-adopted jobs rebuild their replica sets from the persisted spec;
+//  Q2  default-PS ConfigMap AlreadyExists is tolerated;
+//  Q3  status writes go through a re-GET-on-conflict retry loop on a copy;
+//  Q6  API errors while reading pods/jobs are Unknown, never Failed;
+//  Q7  the job decision follows TerminationPolicy.chief (default MASTER);
+//  Q9  the PS ConfigMap carries an owner reference;
+//  Q16 existing objects are not re-POSTed every tick;
+//  and the phase moves Creating -> Running once every resource exists.
+#pragma once
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <thread>
+
+#include "kube_api.h"
+#include "replicas.h"
+#include "spec.h"
+
+namespace tfop {
+
+struct ReconcileOptions {
+  std::chrono::milliseconds interval{8000};
+  std::string ps_script_path = std::string(kPSServerMount) + "/" + kPSServerFile;
+  std::string ps_server_source;  // contents of ControllerConfig.grpcServerFilePath (read once)
+};
+
+std::string rand_string(int n);  // [0-9a-z], DNS-1035 friendly (pkg/util/util.go:25-54)
+
+class TrainingJob {
+ public:
+  TrainingJob(KubeApi& api, TfJob job, ControllerConfig cfg, ReconcileOptions opts);
+
+  // One reconcile pass (safe to call repeatedly).
+  void reconcile();
+  // Tear down every child resource (Jobs, Pods, Services, ConfigMap, TensorBoard).
+  void delete_resources();
+
+  void update_object(const TfJob& j);  // newer resourceVersion from a watch event (spec changes are ignored)
+
+  const TfJob& job() const { return job_; }
+  const TfJobStatus& status() const { return status_; }
+  std::string key() const { return job_.ns() + "/" + job_.name(); }
+  int api_calls() const { return api_calls_; }
+
+  // Build replica bookkeeping from the (defaulted) spec; returns error text.
+  std::string build_replica_sets();
+  void setup();
+  std::string chief_type() const;
+
+ private:
+  ApiResult call(const std::string& method, const std::string& path, const Json* body = nullptr);
+  bool create_if_absent(const std::string& collection, const std::string& name, const Json& obj, bool* created);
+  void create_resources();
+  void get_status(std::string& state, std::vector<TfReplicaStatus>& out);
+  bool update_status();
+
+  KubeApi& api_;
+  TfJob job_;
+  ControllerConfig cfg_;
+  ReconcileOptions opts_;
+  TfJobStatus status_;
+  std::vector<TfReplicaSpec> replicas_;
+  bool tensorboard_ = false;
+  bool setup_ok_ = false;
+  std::set<std::string> existing_;  // objects known to exist (kind/name)
+  int api_calls_ = 0;
+};
+
+// Runs a TrainingJob on its own thread: reconcile immediately, then every
+// `interval` or when poked; Delete -> cleanup and exit.
+class JobWorker {
+ public:
+  JobWorker(std::unique_ptr<TrainingJob> job, std::chrono::milliseconds interval);
+  ~JobWorker();
+  void poke();
+  void request_delete();
+  void update(const TfJob& j);
+  void stop();
+  bool finished() const { return finished_; }
+  TrainingJob& job() { return *job_; }
+
+ private:
+  void run();
+  std::unique_ptr<TrainingJob> job_;
+  std::chrono::milliseconds interval_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool poked_ = false, deleted_ = false, stop_ = false;
+  std::atomic<bool> finished_{false};
+  std::unique_ptr<TfJob> pending_update_;
+  std::thread th_;
+};
+
+}  // namespace tfop

@@ -163,6 +163,8 @@ Json make_replica_job(const TfJob& job, const TfReplicaSpec& r, int index, const
   Labels l = task_labels(job, r.type, index);
   // deep copy of the template: the spec's template is never mutated by resource creation
   Json tmpl = r.tmpl ? r.tmpl->clone() : Json::object();
+  // insert every top-level key BEFORE taking references into the object (vector storage may move)
+  if (!tmpl.find("metadata") || !tmpl["metadata"].is_object()) tmpl["metadata"] = Json::object();
   if (!tmpl.find("spec")) tmpl["spec"] = Json::object();
   Json& pspec = tmpl["spec"];
   if (r.is_default_ps) {
@@ -180,7 +182,6 @@ Json make_replica_job(const TfJob& job, const TfReplicaSpec& r, int index, const
       cmd.push_back(s);
     cs0["command"] = cmd;
   }
-  if (!tmpl.find("metadata") || !tmpl["metadata"].is_object()) tmpl["metadata"] = Json::object();
   Json& tl = tmpl["metadata"]["labels"];
   if (!tl.is_object()) tl = Json::object();
   for (auto& kv : l) tl[kv.first] = kv.second;
