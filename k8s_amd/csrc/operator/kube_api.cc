@@ -383,10 +383,10 @@ class HttpWatch : public WatchStream {
   void close() override { conn_->close(); }
 
  private:
-  // move decoded body bytes into lines_
+  // move decoded body bytes into lines_; a timeout with nothing buffered sets timed_out_
   bool pull(int timeout_ms, std::string& err) {
-    if (!chunked_) {
-      int r = rd_.fill(timeout_ms);
+    if (rd_.buffer().empty()) {
+      const int r = rd_.fill(timeout_ms);
       if (r == 0) {
         timed_out_ = true;
         return true;
@@ -395,41 +395,37 @@ class HttpWatch : public WatchStream {
         err = "watch stream closed";
         return false;
       }
+    }
+    if (!chunked_) {
       lines_ += rd_.buffer();
       rd_.buffer().clear();
       return true;
     }
+    // chunked framing: data is arriving, block until the current piece is complete
     while (true) {
       std::string& b = rd_.buffer();
       if (chunk_left_ > 0) {
-        if (b.empty()) {
-          int r = rd_.fill(timeout_ms);
-          if (r == 0) {
-            timed_out_ = true;
-            return true;
-          }
-          if (r < 0) {
-            err = "watch stream closed";
-            return false;
-          }
-          continue;
+        if (b.empty() && rd_.fill(-1) <= 0) {
+          err = "watch stream closed";
+          return false;
         }
-        size_t n = std::min<size_t>(chunk_left_, b.size());
-        lines_.append(b, 0, n);
-        b.erase(0, n);
+        size_t n = std::min<size_t>(chunk_left_, rd_.buffer().size());
+        lines_.append(rd_.buffer(), 0, n);
+        rd_.buffer().erase(0, n);
         chunk_left_ -= n;
         if (chunk_left_ == 0) need_crlf_ = true;
         return true;
       }
       std::string l;
       if (need_crlf_) {
-        if (!rd_.line(l, timeout_ms)) {
+        if (!rd_.line(l, -1)) {
           err = "watch stream closed";
           return false;
         }
         need_crlf_ = false;
+        if (rd_.buffer().empty()) return true;  // next chunk not here yet: go back to the timed wait
       }
-      if (!rd_.line(l, timeout_ms)) {
+      if (!rd_.line(l, -1)) {
         err = "watch stream closed";
         return false;
       }

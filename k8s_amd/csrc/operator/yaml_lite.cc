@@ -320,6 +320,19 @@ std::vector<std::vector<std::string>> split_docs(const std::string& text) {
 }
 
 Json parse_doc(const std::vector<std::string>& raw) {
+  // a document that is one flow collection (JSON is a YAML subset)
+  std::string all;
+  for (auto& r : raw) all += strip_comment(r) + "\n";
+  std::string t = strip(all);
+  if (!t.empty() && (t[0] == '{' || t[0] == '[')) {
+    try {
+      return Json::parse(t);
+    } catch (const JsonError&) {
+      std::string flat;
+      for (char c : t) flat += (c == '\n' ? ' ' : c);
+      return flow_parse(flat);
+    }
+  }
   std::vector<Line> lines;
   for (size_t i = 0; i < raw.size(); ++i) {
     std::string s = strip_comment(raw[i]);

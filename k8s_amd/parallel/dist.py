@@ -38,31 +38,54 @@ class RankInfo:
     compute_world: int = 1  # ranks that run the model (everything but ps)
 
 
+def resolve(addr: str) -> str:
+    """Map a TF_CONFIG "service:port" through $K8S_AMD_SERVICE_MAP (local kubelet's cluster-DNS stand-in)."""
+    m = os.environ.get("K8S_AMD_SERVICE_MAP")
+    if not m:
+        return addr
+    table = json.loads(m)
+    if addr in table:
+        return table[addr]
+    host = addr.rsplit(":", 1)[0]
+    return table.get(host, addr)
+
+
 def rank_from_tf_config(tf_config: str, port_offset: int = 1) -> RankInfo:
-    """Deterministic rank assignment from a TF_CONFIG JSON string."""
+    """Deterministic rank assignment from a TF_CONFIG JSON string.
+
+    Compute ranks (the collective group) are master/chief first, then workers;
+    PS tasks do not join the RCCL group (rank -1): in this framework the
+    parameter service is sharded over the compute ranks (parallel/ps.py) and
+    the PS replicas run the parameter/rendezvous server (ps_server/).
+    """
     cfg = json.loads(tf_config)
     cluster: Dict[str, List[str]] = cfg.get("cluster", {})
     task = cfg.get("task", {})
     ttype, tidx = task.get("type", "master").lower(), int(task.get("index", 0))
     order = []
     for role in ROLE_ORDER:
+        if role == "ps":
+            continue
         for i, addr in enumerate(cluster.get(role, [])):
             order.append((role, i, addr))
     for role in sorted(cluster):  # unknown roles last, deterministic
         if role not in ROLE_ORDER:
             for i, addr in enumerate(cluster[role]):
                 order.append((role, i, addr))
-    if not order:
+    if not order and not cluster.get("ps"):
         raise ValueError("TF_CONFIG has an empty cluster")
-    try:
-        rank = [(r, i) for r, i, _ in order].index((ttype, tidx))
-    except ValueError:
-        raise ValueError("task %s:%d not in cluster %s" % (ttype, tidx, sorted(cluster))) from None
-    host, _, port = order[0][2].rpartition(":")
-    compute = sum(1 for r, _, _ in order if r != "ps")
+    keys = [(r, i) for r, i, _ in order]
+    if ttype == "ps":
+        rank = -1
+    elif (ttype, tidx) in keys:
+        rank = keys.index((ttype, tidx))
+    else:
+        raise ValueError("task %s:%d not in cluster %s" % (ttype, tidx, sorted(cluster)))
+    first = order[0][2] if order else cluster["ps"][0]
+    host, _, port = resolve(first).rpartition(":")
     return RankInfo(rank=rank, world_size=len(order), local_rank=int(os.environ.get("LOCAL_RANK", 0)),
-                    master_addr=host or order[0][2], master_port=int(port or 2222) + port_offset, role=ttype,
-                    role_index=tidx, compute_world=compute)
+                    master_addr=host or first, master_port=int(port or 2222) + port_offset, role=ttype,
+                    role_index=tidx, compute_world=len(order))
 
 
 def rank_from_env() -> Optional[RankInfo]:
