@@ -1,0 +1,429 @@
+// K1 + K2: MFMA GEMM and NHWC implicit-GEMM convolution for gfx950.
+//
+//   C[M,N] (+)= A[M,K] . B[K,N]   bf16 in, fp32 accumulate, bf16/fp32 out
+//
+// One kernel template, four operand "sources":
+//   KMajor   : operand stored row-major with K contiguous   (activations x[m][k], weights w[n][k])
+//   MNMajor  : operand stored with M (or N) contiguous      (dY^T in wgrad, w[k][n] in dgrad)
+//   ConvA    : implicit im2col of an NHWC input, K = (r, s, c), K contiguous per (r, s)
+//   ConvWgB  : implicit im2col used as the N-major B operand of the weight-gradient GEMM
+//
+// Design (MI355X_MICROARCH / cdna_hip_programming guide):
+//  * 128x128 block tile, BK = 64, 256 threads = 4 waves (2x2), each wave 64x64 = 4x4
+//    v_mfma_f32_16x16x32_bf16 tiles (64 accumulator VGPRs).
+//  * global -> LDS with 16-byte global_load_lds (no VGPR round trip); the LDS image is
+//    lane-linear, so bank-conflict swizzles are applied to the per-lane SOURCE address and
+//    the same XOR on the read (rule 21):
+//      K-major   [128 rows][64 k]  : 16-B chunk c of row r stored at c ^ ((r >> 1) & 7)
+//                                    -> conflict-free ds_read_b128 fragment reads
+//      MN-major  [64 k][128 mn]    : 16-B unit u of k-row r stored at u ^ h(r),
+//                                    h(r) = 2 * ((r & 3) | ((r >> 3 & 1) << 2))
+//                                    -> conflict-free ds_read_b64_tr_b16 transposed reads
+//  * double-buffered LDS (2 x 32 KB), next tile's loads issued before the current tile's MFMAs.
+//  * operands swapped in the MFMA (B tile as the "A" operand) so each lane ends with 4
+//    CONSECUTIVE output columns: 8-byte bf16 / 16-byte fp32 stores in the epilogue.
+//  * XCD-aware, bijective block remap + grouped tile order so blocks sharing an A or B panel
+//    run on the same XCD (private L2).
+//  * epilogue: bias, ReLU / GELU(tanh), pre-activation side output, fp32 accumulate, split-K
+//    fp32 atomics (for the tall-K weight gradients).
+#include "common.h"
+#include "launchers.h"
+
+namespace k8s_amd {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 mfma_bf16x8;
+typedef __attribute__((ext_vector_type(4))) short short4_t;
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) short4_t lds_short4;
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int GEMM_THREADS = 256;
+constexpr int TILE_BYTES = BM * BK * 2;  // 16 KB per operand tile
+
+// 16-byte zero line for out-of-image implicit-GEMM loads
+__device__ __attribute__((aligned(64))) uint16_t g_zero_page[64];
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(src, (lds_void*)lds_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ int mn_swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+
+// ----------------------------------------------------------------------------- operand sources
+// stage(): called for round 0..3, writes slot s = round*256 + tid of a 16 KB tile.
+struct KMajor {
+  const uint16_t* p;
+  long ld;    // elements between rows
+  int rows;   // valid rows (M or N)
+  // row-major [rows][K]; tile rows start at r0, k at k0
+  __device__ __forceinline__ const void* src(int s, int r0, int k0) const {
+    const int row = s >> 3, cp = s & 7;
+    const int c = cp ^ ((row >> 1) & 7);
+    int gr = r0 + row;
+    gr = gr < rows ? gr : rows - 1;
+    return p + (long)gr * ld + k0 + c * 8;
+  }
+  static constexpr bool kmajor = true;
+};
+
+struct MNMajor {
+  const uint16_t* p;
+  long ld;   // elements between k rows
+  int cols;  // valid M (or N) extent; must be a multiple of 8
+  __device__ __forceinline__ const void* src(int s, int c0, int k0) const {
+    const int krow = s >> 4, up = s & 15;
+    const int u = up ^ mn_swz(krow);
+    int col = c0 + u * 8;
+    col = col < cols ? col : cols - 8;
+    return p + (long)(k0 + krow) * ld + col;
+  }
+  static constexpr bool kmajor = false;
+};
+
+// Implicit im2col of NHWC input x[N][H][W][C] for a KRSC weight: row m = (n, ho, wo), k = (r, s, c).
+// Requires C % 64 == 0 so one 64-wide k tile lies inside a single (r, s).
+struct ConvA {
+  const uint16_t* x;
+  int N, H, W, C, Ho, Wo, S, stride, pad, dil;
+  int rows;  // N*Ho*Wo
+  __device__ __forceinline__ const void* src(int s, int r0, int k0) const {
+    const int row = s >> 3, cp = s & 7;
+    const int c = cp ^ ((row >> 1) & 7);
+    int m = r0 + row;
+    m = m < rows ? m : rows - 1;
+    const int rs = k0 / C, c0 = k0 - rs * C;
+    const int r = rs / S, sx = rs - r * S;
+    const int hw = Ho * Wo;
+    const int n = m / hw, rem = m - n * hw;
+    const int ho = rem / Wo, wo = rem - ho * Wo;
+    const int hi = ho * stride - pad + r * dil, wi = wo * stride - pad + sx * dil;
+    if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) return g_zero_page;
+    return x + (((long)n * H + hi) * W + wi) * C + c0 + c * 8;
+  }
+  static constexpr bool kmajor = true;
+};
+
+// B operand of the weight gradient: B[k' = m][n' = (r, s, c)] = x[n][ho*st-pad+r][wo*st-pad+s][c]
+// (N-major: 8 consecutive c per 16-B unit). Requires C % 8 == 0.
+struct ConvWgB {
+  const uint16_t* x;
+  int N, H, W, C, Ho, Wo, S, stride, pad, dil;
+  int cols;  // R*S*C
+  int mtot;  // N*Ho*Wo
+  __device__ __forceinline__ const void* src(int s, int c0, int k0) const {
+    const int krow = s >> 4, up = s & 15;
+    const int u = up ^ mn_swz(krow);
+    int col = c0 + u * 8;
+    if (col >= cols) return g_zero_page;
+    const int m = k0 + krow;
+    if (m >= mtot) return g_zero_page;
+    const int rs = col / C, c = col - rs * C;
+    const int r = rs / S, sx = rs - r * S;
+    const int hw = Ho * Wo;
+    const int n = m / hw, rem = m - n * hw;
+    const int ho = rem / Wo, wo = rem - ho * Wo;
+    const int hi = ho * stride - pad + r * dil, wi = wo * stride - pad + sx * dil;
+    if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) return g_zero_page;
+    return x + (((long)n * H + hi) * W + wi) * C + c;
+  }
+  static constexpr bool kmajor = false;
+};
+
+// MN-major operand whose K rows may run past the end (split-K tails): zero rows beyond mtot.
+struct MNMajorK {
+  const uint16_t* p;
+  long ld;
+  int cols, ktot;
+  __device__ __forceinline__ const void* src(int s, int c0, int k0) const {
+    const int krow = s >> 4, up = s & 15;
+    const int u = up ^ mn_swz(krow);
+    int col = c0 + u * 8;
+    if (col >= cols || k0 + krow >= ktot) return g_zero_page;
+    return p + (long)(k0 + krow) * ld + col;
+  }
+  static constexpr bool kmajor = false;
+};
+
+// ----------------------------------------------------------------------------- fragment reads
+__device__ __forceinline__ mfma_bf16x8 frag_kmajor(const char* tile, int rb, int kk, int lane) {
+  const int row = rb + (lane & 15);
+  const int c = kk * 4 + (lane >> 4);
+  const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(tile + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+  return __builtin_bit_cast(mfma_bf16x8, v);
+}
+
+__device__ __forceinline__ mfma_bf16x8 frag_mnmajor(const char* tile, int cb, int kk, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int u = (cb >> 3) + (p >> 1);
+  const int r0 = kk * 32 + 8 * g + q;
+  const int r1 = r0 + 4;
+  const char* a0 = tile + r0 * 256 + ((u ^ mn_swz(r0)) << 4) + (p & 1) * 8;
+  const char* a1 = tile + r1 * 256 + ((u ^ mn_swz(r1)) << 4) + (p & 1) * 8;
+  short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(a0));
+  short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(a1));
+  bf16x8_t v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return __builtin_bit_cast(mfma_bf16x8, v);
+}
+
+template <class Src>
+__device__ __forceinline__ mfma_bf16x8 frag(const char* tile, int b, int kk, int lane) {
+  if constexpr (Src::kmajor) return frag_kmajor(tile, b, kk, lane);
+  else return frag_mnmajor(tile, b, kk, lane);
+}
+
+// ----------------------------------------------------------------------------- epilogue
+struct Epi {
+  void* c;           // output (bf16 or fp32)
+  long ldc;
+  const float* bias;  // [N] or null
+  uint16_t* pre;      // bf16 pre-activation copy or null
+  int out_f32;        // 1: fp32 output
+  int act;            // 0 none, 1 relu, 2 gelu(tanh)
+  int mode;           // 0 store, 1 accumulate (fp32 C += acc), 2 atomic add (fp32)
+  float alpha;
+};
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+// ----------------------------------------------------------------------------- the kernel
+template <class ASrc, class BSrc>
+__global__ void __launch_bounds__(GEMM_THREADS, 2)
+gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
+  __shared__ __attribute__((aligned(1024))) char smem[4 * TILE_BYTES];  // [buf][A|B]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  // ---- XCD-aware bijective remap, then grouped (GROUP_M = 8) tile order
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  int wg;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int group = 8 * tiles_n;
+  const int first_m = (wg / group) * 8;
+  const int gm = min(tiles_m - first_m, 8);
+  const int tm = first_m + (wg % group) % gm;
+  const int tn = (wg % group) / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int kbeg = blockIdx.z * k_per_split;
+  const int kend = min(K, kbeg + k_per_split);
+  const int nt = (kend - kbeg + BK - 1) / BK;
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);  // provably wave-uniform for the M0 (LDS base) operand
+  auto stage = [&](int buf, int k0) {
+    char* ta = smem + buf * 2 * TILE_BYTES;
+    char* tb = ta + TILE_BYTES;
+#pragma unroll
+    for (int rd = 0; rd < 4; ++rd) {
+      const int s = rd * GEMM_THREADS + tid;
+      char* wave_base_a = ta + (rd * GEMM_THREADS + wid_u * 64) * 16;
+      char* wave_base_b = tb + (rd * GEMM_THREADS + wid_u * 64) * 16;
+      glds16(A.src(s, m0, k0), wave_base_a);
+      glds16(B.src(s, n0, k0), wave_base_b);
+    }
+  };
+
+  if (nt > 0) {
+    stage(0, kbeg);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) stage(cur ^ 1, kbeg + (t + 1) * BK);
+    const char* ta = smem + cur * 2 * TILE_BYTES;
+    const char* tb = ta + TILE_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      mfma_bf16x8 af[4], bfv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag<ASrc>(ta, wm * 64 + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfv[j] = frag<BSrc>(tb, wn * 64 + j * 16, kk, lane);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfv[j], af[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds C[m][n..n+3]
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
+      if (n >= N) continue;
+      float v[4] = {acc[i][j][0] * E.alpha, acc[i][j][1] * E.alpha, acc[i][j][2] * E.alpha, acc[i][j][3] * E.alpha};
+      const bool full = (n + 3 < N);
+      if (E.bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n + r < N) v[r] += E.bias[n + r];
+      }
+      if (E.pre) {
+        uint16_t* pp = E.pre + (long)m * E.ldc + n;
+        if (full) {
+          bf16x4_t o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r]);
+          *reinterpret_cast<bf16x4_t*>(pp) = o;
+        } else {
+          for (int r = 0; r < 4 && n + r < N; ++r) pp[r] = f2bf(v[r]);
+        }
+      }
+      if (E.act == 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      } else if (E.act == 2) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+      }
+      if (E.out_f32) {
+        float* cp = reinterpret_cast<float*>(E.c) + (long)m * E.ldc + n;
+        if (E.mode == 2) {
+          for (int r = 0; r < 4 && n + r < N; ++r) atomicAdd(cp + r, v[r]);
+        } else if (full) {
+          float4 o = make_float4(v[0], v[1], v[2], v[3]);
+          if (E.mode == 1) {
+            const float4 old = *reinterpret_cast<const float4*>(cp);
+            o.x += old.x; o.y += old.y; o.z += old.z; o.w += old.w;
+          }
+          *reinterpret_cast<float4*>(cp) = o;
+        } else {
+          for (int r = 0; r < 4 && n + r < N; ++r) cp[r] = (E.mode == 1 ? cp[r] : 0.f) + v[r];
+        }
+      } else {
+        uint16_t* cp = reinterpret_cast<uint16_t*>(E.c) + (long)m * E.ldc + n;
+        if (full) {
+          bf16x4_t o;
+          if (E.mode == 1) {
+            const bf16x4_t old = *reinterpret_cast<const bf16x4_t*>(cp);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += bf2f((uint16_t)old[r]);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r]);
+          *reinterpret_cast<bf16x4_t*>(cp) = o;
+        } else {
+          for (int r = 0; r < 4 && n + r < N; ++r) cp[r] = f2bf(v[r] + (E.mode == 1 ? bf2f(cp[r]) : 0.f));
+        }
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- host side
+template <class ASrc, class BSrc>
+static void launch(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int splits, hipStream_t st) {
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const int kps = ((K + splits - 1) / splits + BK - 1) / BK * BK;
+  splits = (K + kps - 1) / kps;
+  hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc>), dim3(tiles, 1, splits), dim3(GEMM_THREADS), 0, st, a, b, e, M,
+                     N, K, kps);
+}
+
+static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act, uint16_t* pre, int mode,
+                    float alpha) {
+  Epi e;
+  e.c = c;
+  e.ldc = ldc;
+  e.bias = bias;
+  e.pre = pre;
+  e.out_f32 = out_f32;
+  e.act = act;
+  e.mode = mode;
+  e.alpha = alpha;
+  return e;
+}
+
+// Choose split-K so that small-MN / tall-K products (weight gradients) still fill 256 CUs.
+int gemm_choose_splits(int M, int N, int K) {
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const int ktiles = (K + BK - 1) / BK;
+  int s = 1;
+  while (tiles * s < 512 && ktiles / (s * 2) >= 4 && s < 256) s *= 2;
+  return s;
+}
+
+// C[M,N] = act(alpha * op(A) op(B) + bias)
+//  a_kmajor: A stored [M][K] (lda) else [K][M];  b_kmajor: B stored [N][K] (ldb) else [K][N]
+void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
+                 long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
+                 float alpha, int splits, hipStream_t st) {
+  if (splits <= 0) splits = (mode == 2) ? gemm_choose_splits(M, N, K) : 1;
+  Epi e = make_epi(C, ldc, c_f32, bias, act, pre, mode, alpha);
+  if (a_kmajor && b_kmajor)
+    launch(KMajor{A, lda, M}, KMajor{B, ldb, N}, e, M, N, K, splits, st);
+  else if (a_kmajor && !b_kmajor)
+    launch(KMajor{A, lda, M}, MNMajorK{B, ldb, N, K}, e, M, N, K, splits, st);
+  else if (!a_kmajor && b_kmajor)
+    launch(MNMajorK{A, lda, M, K}, KMajor{B, ldb, N}, e, M, N, K, splits, st);
+  else
+    launch(MNMajorK{A, lda, M, K}, MNMajorK{B, ldb, N, K}, e, M, N, K, splits, st);
+}
+
+// NHWC conv forward: y[N,Ho,Wo,K] = conv(x[N,H,W,C], w[K,R,S,C]); requires C % 64 == 0.
+void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int K,
+                     int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
+                     int mode, hipStream_t st) {
+  const int M = N * Ho * Wo;
+  ConvA a{x, N, H, W, C, Ho, Wo, S, stride, pad, dil, M};
+  KMajor b{w, (long)R * S * C, K};
+  Epi e = make_epi(y, K, y_f32, bias, act, nullptr, mode, 1.f);
+  launch(a, b, e, M, K, R * S * C, 1, st);
+}
+
+// Weight gradient: dw[K][R*S*C] (fp32, accumulated with atomics unless splits == 1 and mode 0)
+void launch_conv_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int C, int K, int R,
+                       int S, int stride, int pad, int dil, int Ho, int Wo, int splits, hipStream_t st) {
+  const int M = N * Ho * Wo;  // reduction dim
+  MNMajorK a{dy, (long)K, K, M};
+  ConvWgB b{x, N, H, W, C, Ho, Wo, S, stride, pad, dil, R * S * C, M};
+  if (splits <= 0) splits = gemm_choose_splits(K, R * S * C, M);
+  Epi e = make_epi(dw, (long)R * S * C, true, nullptr, 0, nullptr, splits > 1 ? 2 : 0, 1.f);
+  launch(a, b, e, K, R * S * C, M, splits, st);
+}
+
+// dgrad weight transform: w2[c][r][s][k] = w[k][R-1-r][S-1-s][c]
+__global__ void conv_dgrad_wtrans_kernel(const uint16_t* __restrict__ w, uint16_t* __restrict__ w2, int K, int R,
+                                         int S, int C) {
+  const long total = (long)K * R * S * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int k = (int)(i % K);
+    long t = i / K;
+    const int s = (int)(t % S);
+    t /= S;
+    const int r = (int)(t % R);
+    const int c = (int)(t / R);
+    w2[i] = w[(((long)k * R + (R - 1 - r)) * S + (S - 1 - s)) * C + c];
+  }
+}
+
+void launch_conv_dgrad_wtrans(const uint16_t* w, uint16_t* w2, int K, int R, int S, int C, hipStream_t st) {
+  const long total = (long)K * R * S * C;
+  hipLaunchKernelGGL(conv_dgrad_wtrans_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, st, w, w2, K, R, S, C);
+}
+
+}  // namespace k8s_amd

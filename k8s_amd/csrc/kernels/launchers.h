@@ -42,4 +42,16 @@ void launch_xent_bwd(const void* logits, bool bf16, const int64_t* labels, const
                      bool per_row, long R, long V, long ld, void* dlogits, long ignore_index, float smoothing,
                      hipStream_t st);
 
+// gemm.hip
+int gemm_choose_splits(int M, int N, int K);
+void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
+                 long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
+                 float alpha, int splits, hipStream_t st);
+void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int K,
+                     int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
+                     int mode, hipStream_t st);
+void launch_conv_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int C, int K, int R,
+                       int S, int stride, int pad, int dil, int Ho, int Wo, int splits, hipStream_t st);
+void launch_conv_dgrad_wtrans(const uint16_t* w, uint16_t* w2, int K, int R, int S, int C, hipStream_t st);
+
 }  // namespace k8s_amd

@@ -190,6 +190,98 @@ Tensor xent_bwd(Tensor logits, Tensor labels, Tensor lse, Tensor dscale, int64_t
   return dl;
 }
 
+// ------------------------------------------------------------------ GEMM / conv (MFMA)
+void check_bf16_operand(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1, name, " must be a 2-D row-major GPU tensor");
+  check_dtype(t, at::kBFloat16, name);
+  check_aligned(t, name);
+  TORCH_CHECK(t.stride(0) % 8 == 0, name, " leading dimension must be a multiple of 8 elements");
+}
+
+// a: [M,K] if a_kmajor else [K,M];  b: [N,K] if b_kmajor else [K,N];  returns / writes C[M,N]
+Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tensor> out, bool out_f32,
+            c10::optional<Tensor> bias, int64_t act, c10::optional<Tensor> pre, bool accumulate, double alpha,
+            int64_t splits) {
+  check_bf16_operand(a, "A");
+  check_bf16_operand(b, "B");
+  const long M = a_kmajor ? a.size(0) : a.size(1), K = a_kmajor ? a.size(1) : a.size(0);
+  const long N = b_kmajor ? b.size(0) : b.size(1), Kb = b_kmajor ? b.size(1) : b.size(0);
+  TORCH_CHECK(K == Kb, "inner dimensions differ: ", K, " vs ", Kb);
+  if (a_kmajor || b_kmajor) TORCH_CHECK(K % 64 == 0, "K-major operands need K % 64 == 0 (got ", K, ")");
+  if (!a_kmajor) TORCH_CHECK(M % 8 == 0, "M-major A needs M % 8 == 0");
+  if (!b_kmajor) TORCH_CHECK(N % 8 == 0, "N-major B needs N % 8 == 0");
+  TORCH_CHECK(N % 4 == 0, "N must be a multiple of 4");
+  Tensor c;
+  if (out) {
+    c = *out;
+    TORCH_CHECK(c.is_cuda() && c.is_contiguous() && c.numel() == M * N, "out must be a contiguous [M,N] tensor");
+    TORCH_CHECK(c.scalar_type() == (out_f32 ? at::kFloat : at::kBFloat16), "out dtype mismatch");
+  } else {
+    c = torch::empty({M, N}, a.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  }
+  if (bias) TORCH_CHECK(bias->numel() == N && bias->scalar_type() == at::kFloat && bias->is_contiguous());
+  if (pre) TORCH_CHECK(pre->numel() == M * N && pre->scalar_type() == at::kBFloat16 && pre->is_contiguous());
+  int mode = accumulate ? 1 : 0;
+  int sp = (int)splits;
+  if (sp != 1 && out_f32 && !bias && act == 0 && !pre) {
+    if (sp <= 0) sp = k8s_amd::gemm_choose_splits((int)M, (int)N, (int)K);
+    if (sp > 1) {
+      if (!accumulate) c.zero_();
+      mode = 2;
+    }
+  } else {
+    sp = 1;
+  }
+  k8s_amd::launch_gemm(cbf(a), a.stride(0), a_kmajor, cbf(b), b.stride(0), b_kmajor, c.data_ptr(), N, out_f32,
+                       (int)M, (int)N, (int)K, bias ? bias->data_ptr<float>() : nullptr, (int)act,
+                       pre ? bf(*pre) : nullptr, mode, (float)alpha, sp, cur_stream());
+  return c;
+}
+
+static inline int conv_out(int in, int k, int st, int pad, int dil) { return (in + 2 * pad - dil * (k - 1) - 1) / st + 1; }
+
+Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, bool out_f32, c10::optional<Tensor> bias,
+                int64_t act) {
+  check_cuda(x, "x"); check_cuda(w, "w");
+  check_dtype(x, at::kBFloat16, "x"); check_dtype(w, at::kBFloat16, "w");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "x [N,H,W,C], w [K,R,S,C]");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int K = w.size(0), R = w.size(1), S = w.size(2);
+  TORCH_CHECK(w.size(3) == C, "channel mismatch");
+  TORCH_CHECK(C % 64 == 0, "implicit-GEMM conv needs C % 64 == 0");
+  TORCH_CHECK(K % 8 == 0, "output channels must be a multiple of 8");
+  const int Ho = conv_out(H, R, stride, pad, dil), Wo = conv_out(W, S, stride, pad, dil);
+  auto y = torch::empty({N, Ho, Wo, K}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  k8s_amd::launch_conv_fwd(cbf(x), cbf(w), y.data_ptr(), out_f32, N, H, W, C, K, R, S, (int)stride, (int)pad,
+                           (int)dil, Ho, Wo, bias ? bias->data_ptr<float>() : nullptr, (int)act, 0, cur_stream());
+  return y;
+}
+
+// dw[K,R,S,C] fp32 (+)= dy^T . im2col(x)
+void conv_wgrad(Tensor x, Tensor dy, Tensor dw, int64_t stride, int64_t pad, int64_t dil, int64_t splits,
+                bool accumulate) {
+  check_cuda(x, "x"); check_cuda(dy, "dy"); check_cuda(dw, "dw");
+  check_dtype(x, at::kBFloat16, "x"); check_dtype(dy, at::kBFloat16, "dy"); check_dtype(dw, at::kFloat, "dw");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int K = dw.size(0), R = dw.size(1), S = dw.size(2);
+  TORCH_CHECK(dw.size(3) == C && C % 8 == 0 && K % 8 == 0);
+  const int Ho = conv_out(H, R, stride, pad, dil), Wo = conv_out(W, S, stride, pad, dil);
+  TORCH_CHECK(dy.size(0) == N && dy.size(1) == Ho && dy.size(2) == Wo && dy.size(3) == K, "dy shape mismatch");
+  int sp = splits <= 0 ? k8s_amd::gemm_choose_splits(K, R * S * C, N * Ho * Wo) : (int)splits;
+  if (sp > 1 && !accumulate) dw.zero_();
+  TORCH_CHECK(sp > 1 || !accumulate, "accumulate needs split-K atomics");
+  k8s_amd::launch_conv_wgrad(cbf(x), cbf(dy), f32(dw), N, H, W, C, K, R, S, (int)stride, (int)pad, (int)dil, Ho, Wo,
+                             sp, cur_stream());
+}
+
+Tensor conv_dgrad_wtrans(Tensor w) {
+  check_cuda(w, "w"); check_dtype(w, at::kBFloat16, "w");
+  const int K = w.size(0), R = w.size(1), S = w.size(2), C = w.size(3);
+  auto w2 = torch::empty({C, R, S, K}, w.options());
+  k8s_amd::launch_conv_dgrad_wtrans(cbf(w), bf(w2), K, R, S, C, cur_stream());
+  return w2;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -204,5 +296,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("norm_bwd", &norm_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
+  m.def("gemm", &gemm);
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_dgrad_wtrans", &conv_dgrad_wtrans);
   m.attr("arch") = "gfx950";
 }

@@ -1,15 +1,26 @@
-"""NHWC convolution entry points (K2).
+"""NHWC convolution (K2) on the gfx950 implicit-GEMM MFMA kernel.
 
-``conv_fwd`` / ``conv_bwd`` take NHWC bf16 activations and KRSC weights and
-return NHWC / KRSC results. The gfx950 implicit-GEMM kernels
-(``csrc/kernels/conv_igemm.hip``) serve every shape they support; the
-remaining shapes (and CPU tensors) go through ATen's convolution on a
-channels-last view, which on ROCm is MIOpen.
+Activations NHWC bf16, weights KRSC bf16. Per product:
+
+    fwd    y  = conv(x, w)                  ConvA implicit im2col (C % 64 == 0)
+    wgrad  dw = dy^T . im2col(x)            fp32, split-K atomics, written straight into the
+                                            parameter's flat gradient slot
+    dgrad  1x1, stride 1: dx = dy . w       plain GEMM, w read N-major (no transpose)
+           RxS, stride 1: dx = conv(dy, w') w' = spatially flipped, in/out-swapped w
+                                            (tiny per-step transform), pad' = R-1-pad
+
+Shapes outside those rules (the 8-channel stem, stride-2 dgrad) and CPU
+tensors run through ATen's convolution on a channels-last view (MIOpen on
+ROCm) -- see ``coverage()`` for which path each layer takes.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn.functional as F
+
+from k8s_amd.ops._ext import load as _load
+
+STATS = {"hip_fwd": 0, "aten_fwd": 0, "hip_wgrad": 0, "aten_wgrad": 0, "hip_dgrad": 0, "aten_dgrad": 0}
 
 
 def _nchw(x):
@@ -20,13 +31,64 @@ def _nhwc(y):
     return y.permute(0, 2, 3, 1).contiguous()
 
 
+def _hip(*ts):
+    return all(t.is_cuda and t.dtype == torch.bfloat16 for t in ts)
+
+
+def fwd_ok(x, w):
+    return _hip(x, w) and x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0
+
+
 def conv_fwd(x, w, stride, padding):
-    y = F.conv2d(_nchw(x), _nchw(w), None, stride, padding)
-    return _nhwc(y)
+    if fwd_ok(x, w):
+        STATS["hip_fwd"] += 1
+        return _load().conv_fwd(x, w, stride, padding, 1, False, None, 0)
+    STATS["aten_fwd"] += 1
+    return _nhwc(F.conv2d(_nchw(x), _nchw(w), None, stride, padding))
 
 
-def conv_bwd(gy, x, w, stride, padding, need_dx=True):
+def _aten_bwd(gy, x, w, stride, padding, need_dx, need_dw):
     dx, dw, _ = torch.ops.aten.convolution_backward(
         _nchw(gy), _nchw(x), _nchw(w), None, [stride, stride], [padding, padding], [1, 1], False, [0, 0], 1,
-        [bool(need_dx), True, False])
-    return (_nhwc(dx) if dx is not None else None), dw.permute(0, 2, 3, 1)
+        [bool(need_dx), bool(need_dw), False])
+    return (_nhwc(dx) if dx is not None else None), (dw.permute(0, 2, 3, 1) if dw is not None else None)
+
+
+def conv_bwd(gy, x, w, stride, padding, need_dx, p=None):
+    """Returns dx (or None); deposits dw into ``p``'s flat gradient slot."""
+    K, R, S, C = w.shape
+    C_ = _load() if gy.is_cuda else None
+    hip = _hip(gy, x, w)
+    # ---- weight gradient
+    if hip and C % 8 == 0 and K % 8 == 0 and p is not None and p.grad.dtype == torch.float32:
+        STATS["hip_wgrad"] += 1
+        acc = p.written
+        C_.conv_wgrad(x, gy, p.grad, stride, padding, 1, 0, acc)
+        if acc:
+            p.store._notify(p)
+        else:
+            p.store.mark_written(p)
+        dw_done = True
+    else:
+        dw_done = False
+    # ---- data gradient
+    dx = None
+    if need_dx:
+        if hip and stride == 1 and K % 64 == 0 and C % 8 == 0:
+            STATS["hip_dgrad"] += 1
+            if R == 1 and S == 1 and padding == 0:
+                N, H, W_, _ = gy.shape
+                dx = C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, None, False, None, 0, None, False,
+                             1.0, 1).reshape(N, H, W_, C)
+            else:
+                w2 = C_.conv_dgrad_wtrans(w)
+                dx = C_.conv_fwd(gy, w2, 1, R - 1 - padding, 1, False, None, 0)
+        else:
+            STATS["aten_dgrad"] += 1
+            dx, _ = _aten_bwd(gy, x, w, stride, padding, True, False)
+    if not dw_done and p is not None:
+        STATS["aten_wgrad"] += 1
+        _, dw = _aten_bwd(gy, x, w, stride, padding, False, True)
+        if p is not None:
+            p.store.deposit(p, dw)
+    return dx

@@ -1,14 +1,40 @@
-"""GEMM entry points (K1) used by linear layers.
+"""GEMM entry points (K1) for linear layers, on the gfx950 MFMA kernel.
 
-``linear_fwd(x, w, b, act)`` computes ``act(x @ w^T + b)`` and
-``linear_bwd`` the three backward products (dgrad NN, wgrad TN, bias
-reduction). The gfx950 MFMA kernels (``csrc/kernels/gemm.hip``) serve GPU
-tensors; CPU tensors use the fp32 reference.
+``mm(a, b, a_kmajor, b_kmajor, ...)`` is the raw kernel (bf16 in, fp32 acc,
+bf16/fp32 out, bias / ReLU / GELU epilogue, fp32 accumulate, split-K
+atomics). ``linear_fwd`` / ``linear_bwd`` express a Linear layer's three
+products with it WITHOUT materialising any transpose:
+
+    fwd    y  = x . W^T          A = x   [M,K] K-major,  B = W [N,K] K-major
+    dgrad  dx = g . W            A = g   [M,N] K-major,  B = W [N,K] read N-major
+    wgrad  dW = g^T . x          A = g   read M-major,   B = x read N-major  (split-K, fp32 out
+                                                             straight into the flat gradient slot)
+
+CPU tensors (and shapes the kernel does not take) use plain PyTorch.
 """
 from __future__ import annotations
 
+from typing import Optional
+
 import torch
 import torch.nn.functional as F
+
+from k8s_amd.ops._ext import load as _load
+
+ACT = {None: 0, "relu": 1, "gelu": 2}
+
+
+def hip_ok(*ts) -> bool:
+    return all(t.is_cuda and t.dtype == torch.bfloat16 for t in ts)
+
+
+def mm(a, b, a_kmajor=True, b_kmajor=True, out=None, out_f32=False, bias=None, act=None, pre=None,
+       accumulate=False, alpha=1.0, splits=1):
+    return _load().gemm(a, a_kmajor, b, b_kmajor, out, out_f32, bias, ACT[act], pre, accumulate, alpha, splits)
+
+
+def _shape_ok(M, N, K) -> bool:
+    return K % 64 == 0 and N % 8 == 0 and M % 8 == 0
 
 
 def _act_fwd(y, act):
@@ -21,30 +47,55 @@ def _act_fwd(y, act):
     raise ValueError(act)
 
 
-def _act_bwd(gy, pre, act):
+def _act_bwd(gy, pre_or_out, act):
     if act is None:
         return gy
     if act == "relu":
-        return gy * (pre > 0)
+        return gy * (pre_or_out > 0)
     if act == "gelu":
-        with torch.enable_grad():
-            p = pre.detach().float().requires_grad_(True)
-            (g,) = torch.autograd.grad(F.gelu(p, approximate="tanh"), p, gy.float())
-        return g.to(gy.dtype)
+        x = pre_or_out.float()
+        k0, k1 = 0.7978845608028654, 0.044715
+        t = torch.tanh(k0 * (x + k1 * x ** 3))
+        d = 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k0 * (1 + 3 * k1 * x * x)
+        return (gy.float() * d).to(gy.dtype)
     raise ValueError(act)
 
 
 def linear_fwd(x, w, b, act=None):
-    pre = torch.matmul(x, w.t())
+    """Returns (y, saved) where saved is what linear_bwd needs for the activation derivative."""
+    M, K = x.shape
+    N = w.shape[0]
+    if hip_ok(x, w) and _shape_ok(M, N, K) and x.stride(1) == 1:
+        pre = torch.empty((M, N), device=x.device, dtype=torch.bfloat16) if act == "gelu" else None
+        y = mm(x, w, True, True, bias=b, act=act, pre=pre)
+        return y, (pre if act == "gelu" else (y if act == "relu" else None))
+    y = torch.matmul(x, w.t())
     if b is not None:
-        pre = pre + b.to(pre.dtype)
-    y = _act_fwd(pre, act)
-    return y, (pre if act is not None else None)
+        y = y + b.to(y.dtype)
+    pre = y
+    y = _act_fwd(y, act)
+    return y, (pre if act == "gelu" else (y if act == "relu" else None))
 
 
-def linear_bwd(gy, x, w, pre, act, has_bias):
-    g = _act_bwd(gy, pre, act)
+def linear_bwd(gy, x, w, saved, act, pw=None, store=None):
+    """dx and the parameter gradient. With (pw, store) on GPU the weight gradient is written
+    (or accumulated) straight into the flat fp32 gradient slot; returns (dx, dw_or_None, db)."""
+    g = _act_bwd(gy, saved, act)
+    M, K = x.shape
+    N = w.shape[0]
+    db = g.float().sum(0) if True else None
+    if hip_ok(g, x, w) and _shape_ok(M, N, K) and N % 64 == 0:
+        dx = mm(g, w, True, False)
+        if pw is not None and store is not None and pw.grad.dtype == torch.float32:
+            acc = pw.written
+            mm(g, x, False, False, out=pw.grad, out_f32=True, accumulate=acc, splits=0)
+            if acc:
+                store._notify(pw)
+            else:
+                store.mark_written(pw)
+            return dx, None, db
+        dw = mm(g, x, False, False, out_f32=True, splits=0)
+        return dx, dw, db
     dx = torch.matmul(g, w)
     dw = torch.matmul(g.t(), x)
-    db = g.float().sum(0) if has_bias else None
     return dx, dw, db

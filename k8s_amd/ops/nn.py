@@ -53,8 +53,7 @@ class _Conv2dNHWC(torch.autograd.Function):
         impl = _conv_impl()
         w = p.weight if x.dtype == p.weight.dtype else p.master.to(x.dtype)
         gy = gy.contiguous()
-        dx, dw = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, ctx.x_requires_grad)
-        p.store.deposit(p, dw)
+        dx = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, ctx.x_requires_grad, p)
         return dx, None, None, None, None
 
 
@@ -187,8 +186,9 @@ class _Linear(torch.autograd.Function):
         g = _gemm()
         w = pw.weight if x2.dtype == pw.weight.dtype else pw.master.to(x2.dtype)
         gy2 = gy.reshape(-1, gy.shape[-1]).contiguous()
-        dx, dw, db = g.linear_bwd(gy2, x2, w, pre, ctx.act, pb is not None)
-        pw.store.deposit(pw, dw)
+        dx, dw, db = g.linear_bwd(gy2, x2, w, pre, ctx.act, pw=pw, store=pw.store)
+        if dw is not None:
+            pw.store.deposit(pw, dw)
         if pb is not None:
             pb.store.deposit(pb, db)
         return dx.reshape(ctx.xshape), None, None, None, None

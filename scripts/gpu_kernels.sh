@@ -1,0 +1,13 @@
+#!/bin/bash
+# GPU session: kernel numerics first (stop on failure), then kernel microbench, then the model bench + profile.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+echo "pytest exit $rc" >> gpurun_out/pytest_gpu.log; tail -5 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+timeout -k 10 600 python scripts/bench_kernels.py > gpurun_out/bench_kernels.log 2>&1; rc=$?; tail -20 gpurun_out/bench_kernels.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 && tail -1 gpurun_out/bench.log &&
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 5 --warmup 3 > gpurun_out/prof.log 2>&1 && echo prof ok

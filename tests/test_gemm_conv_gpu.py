@@ -1,0 +1,126 @@
+"""MFMA GEMM / implicit-GEMM conv kernels vs plain PyTorch fp32 references."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _C():
+    from k8s_amd.ops._ext import load
+
+    return load()
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-6)).item()
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 520, 192), (4096, 4096, 1024), (129, 136, 128),
+                                   (8, 1000, 2048)])
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+def test_gemm_layouts(cuda, M, N, K, ak, bk):
+    if (not ak and M % 8) or (not bk and N % 8):
+        pytest.skip("MN-major operands need a multiple of 8")
+    torch.manual_seed(0)
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    b = torch.randn(N, K, device=cuda).bfloat16()
+    ref = a.float() @ b.float().t()
+    A = a if ak else a.t().contiguous()
+    B = b if bk else b.t().contiguous()
+    c = _C().gemm(A, ak, B, bk, None, False, None, 0, None, False, 1.0, 1)
+    assert c.shape == (M, N)
+    assert _rel(c, ref) < 1e-2
+    cf = _C().gemm(A, ak, B, bk, None, True, None, 0, None, False, 1.0, 1)
+    assert _rel(cf, ref) < 1e-3
+
+
+def test_gemm_identity_asymmetric(cuda):
+    """A = I with an asymmetric B catches a transposed C write (guide §3)."""
+    n = 128
+    eye = torch.eye(n, device=cuda).bfloat16()
+    b = (torch.arange(n * n, device=cuda).reshape(n, n) % 251).float().bfloat16()  # asymmetric, exact in bf16
+    c = _C().gemm(eye, True, b, True, None, True, None, 0, None, False, 1.0, 1)
+    assert torch.equal(c, b.float().t())
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_gemm_epilogue(cuda, act):
+    torch.manual_seed(1)
+    M, N, K = 512, 768, 768
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    w = torch.randn(N, K, device=cuda).bfloat16() * 0.05
+    bias = torch.randn(N, device=cuda)
+    pre = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    y = _C().gemm(a, True, w, True, None, False, bias, act, pre, False, 1.0, 1)
+    p_ref = a.float() @ w.float().t() + bias
+    y_ref = [p_ref, torch.relu(p_ref), F.gelu(p_ref, approximate="tanh")][act]
+    assert _rel(pre, p_ref) < 1e-2
+    assert _rel(y, y_ref) < 1e-2
+
+
+def test_gemm_splitk_accumulate(cuda):
+    torch.manual_seed(2)
+    M, N, K = 64, 128, 50000  # tall-K weight-gradient shape
+    a = torch.randn(K, M, device=cuda).bfloat16()
+    b = torch.randn(K, N, device=cuda).bfloat16()
+    ref = a.float().t() @ b.float()
+    out = torch.full((M, N), 3.0, device=cuda)
+    _C().gemm(a, False, b, False, out, True, None, 0, None, True, 1.0, 0)  # accumulate onto 3.0
+    assert _rel(out - 3.0, ref) < 2e-3
+    out2 = _C().gemm(a, False, b, False, None, True, None, 0, None, False, 1.0, 0)
+    assert _rel(out2, ref) < 2e-3
+
+
+CONV_CASES = [
+    # N, H, W, C, K, R, stride, pad
+    (4, 14, 14, 64, 64, 3, 1, 1),
+    (2, 28, 28, 128, 128, 3, 2, 1),
+    (3, 7, 7, 512, 2048, 1, 1, 0),
+    (2, 16, 16, 256, 128, 1, 2, 0),
+    (2, 9, 11, 64, 72, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd(cuda, case):
+    N, H, W, C, K, R, st, pad = case
+    torch.manual_seed(3)
+    x = torch.randn(N, H, W, C, device=cuda).bfloat16()
+    w = (torch.randn(K, R, R, C, device=cuda) * 0.05).bfloat16()
+    y = _C().conv_fwd(x, w, st, pad, 1, False, None, 0)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, st, pad).permute(0, 2, 3, 1)
+    assert y.shape == ref.shape
+    assert _rel(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("case", CONV_CASES + [(2, 32, 32, 8, 64, 7, 2, 3)])
+def test_conv_wgrad(cuda, case):
+    N, H, W, C, K, R, st, pad = case
+    torch.manual_seed(4)
+    x = torch.randn(N, H, W, C, device=cuda).bfloat16()
+    Ho = (H + 2 * pad - R) // st + 1
+    Wo = (W + 2 * pad - R) // st + 1
+    dy = torch.randn(N, Ho, Wo, K, device=cuda).bfloat16()
+    dw = torch.empty(K, R, R, C, device=cuda)
+    _C().conv_wgrad(x, dy, dw, st, pad, 1, 0, False)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(False)
+    wr = torch.zeros(K, C, R, R, device=cuda, requires_grad=True)
+    F.conv2d(xr, wr, None, st, pad).backward(dy.float().permute(0, 3, 1, 2))
+    assert _rel(dw, wr.grad.permute(0, 2, 3, 1)) < 5e-3
+
+
+@pytest.mark.parametrize("case", [c for c in CONV_CASES if c[6] == 1])
+def test_conv_dgrad_stride1(cuda, case):
+    from k8s_amd.ops import conv as kc
+
+    N, H, W, C, K, R, st, pad = case
+    torch.manual_seed(5)
+    x = torch.randn(N, H, W, C, device=cuda).bfloat16()
+    w = (torch.randn(K, R, R, C, device=cuda) * 0.05).bfloat16()
+    dy = torch.randn(N, H, W, K, device=cuda).bfloat16()
+    dx = kc.conv_bwd(dy, x, w, st, pad, True, None)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    F.conv2d(xr, w.float().permute(0, 3, 1, 2), None, st, pad).backward(dy.float().permute(0, 3, 1, 2))
+    assert _rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
