@@ -157,6 +157,24 @@ __global__ void __launch_bounds__(256) bn_stats_final_kernel(const float* __rest
   }
 }
 
+// Statistics arrive as fp32 (sum, sum of squares) per channel, accumulated by the producing conv's
+// epilogue (gemm.hip, Epi::stats): no extra pass over the activation.
+__global__ void bn_finalize_sums_kernel(const float* __restrict__ sums, int C, float count, float eps, float momentum,
+                                        float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                                        float* __restrict__ run_mean, float* __restrict__ run_var) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float mean = sums[c] / count;
+  const float var = fmaxf(sums[C + c] / count - mean * mean, 0.f);
+  mean_out[c] = mean;
+  invstd_out[c] = rsqrtf(var + eps);
+  if (run_mean) {
+    const float unbiased = count > 1.f ? var * count / (count - 1.f) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unbiased;
+  }
+}
+
 // y = act(x*scale + shift + res); scale = gamma*invstd, shift = beta - mean*scale
 __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ res,
@@ -199,7 +217,9 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
                                                                    const uint16_t* __restrict__ x,
                                                                    const uint16_t* __restrict__ y,
                                                                    const float* __restrict__ mean,
-                                                                   const float* __restrict__ invstd, long M,
+                                                                   const float* __restrict__ invstd,
+                                                                   const float* __restrict__ gamma,
+                                                                   const float* __restrict__ beta, int relu_x, long M,
                                                                    int C, int tpr, int rows_per_iter,
                                                                    long rows_per_block, float* __restrict__ part) {
   __shared__ float sh[2][BN_THREADS][9];
@@ -228,6 +248,12 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (bf2f((uint16_t)yv[j]) <= 0.f) g[j] = 0.f;
+      } else if (relu_x) {  // ReLU mask recomputed from x: no read of y (non-residual BN)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int c = cg * 8 + j;
+          if (bf2f(f2bf((xv[j] - mu[j]) * (gamma[c] * is[j]) + beta[c])) <= 0.f) g[j] = 0.f;
+        }
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -295,6 +321,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t
                                                                   const uint16_t* __restrict__ y,
                                                                   const float* __restrict__ mean,
                                                                   const float* __restrict__ invstd,
+                                                                  const float* __restrict__ beta, int relu_x,
                                                                   const float* __restrict__ gamma,
                                                                   const float* __restrict__ sums,
                                                                   uint16_t* __restrict__ dx,
@@ -310,6 +337,12 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (bf2f((uint16_t)yv[j]) <= 0.f) g[j] = 0.f;
+    } else if (relu_x) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = cg * 8 + j;
+        if (bf2f(f2bf((xv[j] - mean[c]) * (gamma[c] * invstd[c]) + beta[c])) <= 0.f) g[j] = 0.f;
+      }
     }
     if (dres) store8(dres + e * 8, g);
 #pragma unroll
@@ -362,18 +395,28 @@ void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, c
                      save_mean, save_invstd, gamma, beta, y, nvec, C / 8, (int)relu);
 }
 
+void launch_bn_fwd_from_sums(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
+                             uint16_t* y, const float* sums, float* save_mean, float* save_invstd, float* run_mean,
+                             float* run_var, long M, int C, float eps, float momentum, bool relu, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, C, (float)M, eps, momentum,
+                     save_mean, save_invstd, run_mean, run_var);
+  const long nvec = M * C / 8;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(stream_grid(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, x, res,
+                     save_mean, save_invstd, gamma, beta, y, nvec, C / 8, (int)relu);
+}
+
 void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
-                   const float* gamma, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, float* work,
-                   float* sums, long M, int C, hipStream_t st) {
+                   const float* gamma, const float* beta, bool relu_x, uint16_t* dx, uint16_t* dres, float* dgamma,
+                   float* dbeta, float* work, float* sums, long M, int C, hipStream_t st) {
   BnGeom g = bn_geom(C);
   long rpb = bn_rows_per_block(M, g);
   int nb = (int)((M + rpb - 1) / rpb);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, dy, x, y, mean, invstd, M,
-                     C, g.tpr, g.rows_per_iter, rpb, work);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, dy, x, y, mean, invstd,
+                     gamma, beta, (int)relu_x, M, C, g.tpr, g.rows_per_iter, rpb, work);
   hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, nb, C, sums, dgamma, dbeta);
   const long nvec = M * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, dy, x, y,
-                     mean, invstd, gamma, sums, dx, dres, nvec, C / 8, C, 1.f / (float)M);
+                     mean, invstd, beta, (int)relu_x, gamma, sums, dx, dres, nvec, C / 8, C, 1.f / (float)M);
 }
 
 }  // namespace k8s_amd

@@ -47,6 +47,20 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
   __builtin_amdgcn_global_load_lds(src, (lds_void*)lds_base, 16, 0, 0);
 }
 
+// Division by a runtime-invariant divisor as multiply-high + shift (valid for 0 <= n < 2^31).
+struct FastDiv {
+  uint32_t d, m, s;
+  __device__ __forceinline__ int div(int n) const { return (int)((__umulhi((uint32_t)n, m) + (uint32_t)n) >> s); }
+};
+static inline FastDiv make_fastdiv(int d) {
+  FastDiv f;
+  f.d = (uint32_t)d;
+  f.s = 0;
+  while ((1u << f.s) < f.d) ++f.s;
+  f.m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << f.s) - f.d)) / f.d + 1);
+  return f;
+}
+
 __device__ __forceinline__ int mn_swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
 
 // ----------------------------------------------------------------------------- operand sources
@@ -86,16 +100,16 @@ struct ConvA {
   const uint16_t* x;
   int N, H, W, C, Ho, Wo, S, stride, pad, dil;
   int rows;  // N*Ho*Wo
+  FastDiv fC, fS, fHW, fWo;
   __device__ __forceinline__ const void* src(int s, int r0, int k0) const {
     const int row = s >> 3, cp = s & 7;
     const int c = cp ^ ((row >> 1) & 7);
     int m = r0 + row;
     m = m < rows ? m : rows - 1;
-    const int rs = k0 / C, c0 = k0 - rs * C;
-    const int r = rs / S, sx = rs - r * S;
-    const int hw = Ho * Wo;
-    const int n = m / hw, rem = m - n * hw;
-    const int ho = rem / Wo, wo = rem - ho * Wo;
+    const int rs = fC.div(k0), c0 = k0 - rs * C;
+    const int r = fS.div(rs), sx = rs - r * S;
+    const int n = fHW.div(m), rem = m - n * (Ho * Wo);
+    const int ho = fWo.div(rem), wo = rem - ho * Wo;
     const int hi = ho * stride - pad + r * dil, wi = wo * stride - pad + sx * dil;
     if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) return g_zero_page;
     return x + (((long)n * H + hi) * W + wi) * C + c0 + c * 8;
@@ -110,6 +124,7 @@ struct ConvWgB {
   int N, H, W, C, Ho, Wo, S, stride, pad, dil;
   int cols;  // R*S*C
   int mtot;  // N*Ho*Wo
+  FastDiv fC, fS, fHW, fWo;
   __device__ __forceinline__ const void* src(int s, int c0, int k0) const {
     const int krow = s >> 4, up = s & 15;
     const int u = up ^ mn_swz(krow);
@@ -117,11 +132,10 @@ struct ConvWgB {
     if (col >= cols) return g_zero_page;
     const int m = k0 + krow;
     if (m >= mtot) return g_zero_page;
-    const int rs = col / C, c = col - rs * C;
-    const int r = rs / S, sx = rs - r * S;
-    const int hw = Ho * Wo;
-    const int n = m / hw, rem = m - n * hw;
-    const int ho = rem / Wo, wo = rem - ho * Wo;
+    const int rs = fC.div(col), c = col - rs * C;
+    const int r = fS.div(rs), sx = rs - r * S;
+    const int n = fHW.div(m), rem = m - n * (Ho * Wo);
+    const int ho = fWo.div(rem), wo = rem - ho * Wo;
     const int hi = ho * stride - pad + r * dil, wi = wo * stride - pad + sx * dil;
     if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) return g_zero_page;
     return x + (((long)n * H + hi) * W + wi) * C + c;
@@ -183,6 +197,7 @@ struct Epi {
   int act;            // 0 none, 1 relu, 2 gelu(tanh)
   int mode;           // 0 store, 1 accumulate (fp32 C += acc), 2 atomic add (fp32)
   float alpha;
+  float* stats;       // [2][N] fp32 per-column sum / sum of squares of the stored outputs (BN fusion) or null
 };
 
 __device__ __forceinline__ float gelu_tanh(float x) {
@@ -267,6 +282,11 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
   }
 
   // ---- epilogue: lane holds C[m][n..n+3]
+  float st_s[4][4], st_q[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) st_s[j][r] = st_q[j][r] = 0.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + wm * 64 + i * 16 + (lane & 15);
@@ -300,6 +320,15 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
       }
+      if (E.stats) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float vr = E.out_f32 ? v[r] : bf2f(f2bf(v[r]));  // statistics of what is stored
+          const bool ok = n + r < N;
+          st_s[j][r] += ok ? vr : 0.f;
+          st_q[j][r] += ok ? vr * vr : 0.f;
+        }
+      }
       if (E.out_f32) {
         float* cp = reinterpret_cast<float*>(E.c) + (long)m * E.ldc + n;
         if (E.mode == 2) {
@@ -332,6 +361,26 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
       }
     }
   }
+  if (E.stats) {
+    // lanes with equal (lane >> 4) hold the same 4 columns: reduce over the 16 row lanes, one atomic per column
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float a = st_s[j][r], b = st_q[j][r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          a += __shfl_xor(a, o, 64);
+          b += __shfl_xor(b, o, 64);
+        }
+        if ((lane & 15) == 0 && n + r < N) {
+          atomicAdd(E.stats + n + r, a);
+          atomicAdd(E.stats + N + n + r, b);
+        }
+      }
+    }
+  }
 }
 
 // ----------------------------------------------------------------------------- host side
@@ -355,6 +404,7 @@ static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act,
   e.act = act;
   e.mode = mode;
   e.alpha = alpha;
+  e.stats = nullptr;
   return e;
 }
 
@@ -387,11 +437,13 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
 // NHWC conv forward: y[N,Ho,Wo,K] = conv(x[N,H,W,C], w[K,R,S,C]); requires C % 64 == 0.
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int K,
                      int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
-                     int mode, hipStream_t st) {
+                     int mode, float* stats, hipStream_t st) {
   const int M = N * Ho * Wo;
-  ConvA a{x, N, H, W, C, Ho, Wo, S, stride, pad, dil, M};
+  ConvA a{x, N, H, W, C, Ho, Wo, S, stride, pad, dil, M,
+          make_fastdiv(C), make_fastdiv(S), make_fastdiv(Ho * Wo), make_fastdiv(Wo)};
   KMajor b{w, (long)R * S * C, K};
   Epi e = make_epi(y, K, y_f32, bias, act, nullptr, mode, 1.f);
+  e.stats = stats;
   launch(a, b, e, M, K, R * S * C, 1, st);
 }
 
@@ -400,7 +452,8 @@ void launch_conv_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int N, 
                        int S, int stride, int pad, int dil, int Ho, int Wo, int splits, hipStream_t st) {
   const int M = N * Ho * Wo;  // reduction dim
   MNMajorK a{dy, (long)K, K, M};
-  ConvWgB b{x, N, H, W, C, Ho, Wo, S, stride, pad, dil, R * S * C, M};
+  ConvWgB b{x, N, H, W, C, Ho, Wo, S, stride, pad, dil, R * S * C, M,
+            make_fastdiv(C), make_fastdiv(S), make_fastdiv(Ho * Wo), make_fastdiv(Wo)};
   if (splits <= 0) splits = gemm_choose_splits(K, R * S * C, M);
   Epi e = make_epi(dw, (long)R * S * C, true, nullptr, 0, nullptr, splits > 1 ? 2 : 0, 1.f);
   launch(a, b, e, K, R * S * C, M, splits, st);

@@ -22,9 +22,12 @@ int bn_workspace_floats(long M, int C);
 void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta, uint16_t* y,
                    float* save_mean, float* save_invstd, float* run_mean, float* run_var, float* work, long M, int C,
                    float eps, float momentum, bool training, bool relu, hipStream_t st);
+void launch_bn_fwd_from_sums(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
+                             uint16_t* y, const float* sums, float* save_mean, float* save_invstd, float* run_mean,
+                             float* run_var, long M, int C, float eps, float momentum, bool relu, hipStream_t st);
 void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
-                   const float* gamma, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, float* work,
-                   float* sums, long M, int C, hipStream_t st);
+                   const float* gamma, const float* beta, bool relu_x, uint16_t* dx, uint16_t* dres, float* dgamma,
+                   float* dbeta, float* work, float* sums, long M, int C, hipStream_t st);
 
 // norm.hip
 void launch_norm_fwd(bool rms, const uint16_t* x, const uint16_t* res, uint16_t* xsum, const float* gamma,
@@ -49,7 +52,7 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
                  float alpha, int splits, hipStream_t st);
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int K,
                      int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
-                     int mode, hipStream_t st);
+                     int mode, float* stats, hipStream_t st);
 void launch_conv_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int C, int K, int R,
                        int S, int stride, int pad, int dil, int Ho, int Wo, int splits, hipStream_t st);
 void launch_conv_dgrad_wtrans(const uint16_t* w, uint16_t* w2, int K, int R, int S, int C, hipStream_t st);

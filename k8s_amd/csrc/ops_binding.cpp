@@ -105,8 +105,25 @@ std::vector<Tensor> bn_fwd(Tensor x, c10::optional<Tensor> res, Tensor gamma, Te
 }
 
 // returns dx, dres (or empty), writes dgamma/dbeta into the given (flat-bucket view) tensors
+std::vector<Tensor> bn_fwd_from_sums(Tensor x, c10::optional<Tensor> res, Tensor gamma, Tensor beta, Tensor sums,
+                                     Tensor run_mean, Tensor run_var, double momentum, double eps, bool relu) {
+  check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x"); check_aligned(x, "x");
+  const int C = (int)x.size(-1);
+  TORCH_CHECK(C % 8 == 0, "channels must be a multiple of 8");
+  const long M = x.numel() / C;
+  TORCH_CHECK(sums.numel() == 2 * C && sums.scalar_type() == at::kFloat, "sums must be fp32 [2, C]");
+  if (res) { check_cuda(*res, "res"); TORCH_CHECK(res->sizes() == x.sizes(), "residual shape mismatch"); }
+  auto y = torch::empty_like(x);
+  auto mean = torch::empty({C}, gamma.options());
+  auto invstd = torch::empty({C}, gamma.options());
+  k8s_amd::launch_bn_fwd_from_sums(cbf(x), res ? cbf(*res) : nullptr, f32(gamma), f32(beta), bf(y), f32(sums),
+                                   f32(mean), f32(invstd), f32(run_mean), f32(run_var), M, C, (float)eps,
+                                   (float)momentum, relu, cur_stream());
+  return {y, mean, invstd};
+}
+
 std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor mean, Tensor invstd, Tensor gamma,
-                           Tensor dgamma, Tensor dbeta, bool want_dres) {
+                           Tensor beta, bool relu_x, Tensor dgamma, Tensor dbeta, bool want_dres) {
   check_cuda(dy, "dy"); check_cuda(x, "x");
   check_dtype(dy, at::kBFloat16, "dy"); check_dtype(x, at::kBFloat16, "x");
   TORCH_CHECK(dy.sizes() == x.sizes());
@@ -119,8 +136,9 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor 
   Tensor dres = want_dres ? torch::empty_like(x) : Tensor();
   auto work = torch::empty({k8s_amd::bn_workspace_floats(M, C)}, gamma.options());
   auto sums = torch::empty({2 * C}, gamma.options());
-  k8s_amd::launch_bn_bwd(cbf(dy), cbf(x), y ? cbf(*y) : nullptr, f32(mean), f32(invstd), f32(gamma), bf(dx),
-                         want_dres ? bf(dres) : nullptr, f32(dgamma), f32(dbeta), f32(work), f32(sums), M, C,
+  TORCH_CHECK(!(relu_x && y), "relu mask from x and y are exclusive");
+  k8s_amd::launch_bn_bwd(cbf(dy), cbf(x), y ? cbf(*y) : nullptr, f32(mean), f32(invstd), f32(gamma), f32(beta),
+                         relu_x, bf(dx), want_dres ? bf(dres) : nullptr, f32(dgamma), f32(dbeta), f32(work), f32(sums), M, C,
                          cur_stream());
   return {dx, dres};
 }
@@ -241,7 +259,7 @@ Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tens
 static inline int conv_out(int in, int k, int st, int pad, int dil) { return (in + 2 * pad - dil * (k - 1) - 1) / st + 1; }
 
 Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, bool out_f32, c10::optional<Tensor> bias,
-                int64_t act) {
+                int64_t act, c10::optional<Tensor> stats) {
   check_cuda(x, "x"); check_cuda(w, "w");
   check_dtype(x, at::kBFloat16, "x"); check_dtype(w, at::kBFloat16, "w");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "x [N,H,W,C], w [K,R,S,C]");
@@ -252,8 +270,11 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, bo
   TORCH_CHECK(K % 8 == 0, "output channels must be a multiple of 8");
   const int Ho = conv_out(H, R, stride, pad, dil), Wo = conv_out(W, S, stride, pad, dil);
   auto y = torch::empty({N, Ho, Wo, K}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  if (stats) TORCH_CHECK(stats->numel() == 2 * K && stats->scalar_type() == at::kFloat && stats->is_contiguous(),
+                         "stats must be fp32 [2, K] (zeroed)");
   k8s_amd::launch_conv_fwd(cbf(x), cbf(w), y.data_ptr(), out_f32, N, H, W, C, K, R, S, (int)stride, (int)pad,
-                           (int)dil, Ho, Wo, bias ? bias->data_ptr<float>() : nullptr, (int)act, 0, cur_stream());
+                           (int)dil, Ho, Wo, bias ? bias->data_ptr<float>() : nullptr, (int)act, 0,
+                           stats ? f32(*stats) : nullptr, cur_stream());
   return y;
 }
 
@@ -292,6 +313,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("clip_factor", &clip_factor);
   m.def("bn_fwd", &bn_fwd);
   m.def("bn_bwd", &bn_bwd);
+  m.def("bn_fwd_from_sums", &bn_fwd_from_sums);
   m.def("norm_fwd", &norm_fwd);
   m.def("norm_bwd", &norm_bwd);
   m.def("xent_fwd", &xent_fwd);

@@ -32,8 +32,11 @@ class BN(nn.Module):
         self.momentum, self.eps = 0.1, 1e-5
 
     def forward(self, x, residual=None, relu=True):
+        sums = None
+        if isinstance(x, tuple):  # (conv output, fused statistics)
+            x, sums = x
         return K.batch_norm_act(x, self.gamma, self.beta, self.running_mean, self.running_var, residual, relu,
-                                self.training, self.momentum, self.eps)
+                                self.training, self.momentum, self.eps, sums=sums)
 
 
 class Conv(nn.Module):
@@ -43,7 +46,8 @@ class Conv(nn.Module):
         self.stride, self.pad = stride, k // 2
 
     def forward(self, x):
-        return K.conv2d_nhwc(x, self.w, self.stride, self.pad)
+        # BN statistics are accumulated in the conv epilogue (returned alongside y)
+        return K.conv2d_nhwc(x, self.w, self.stride, self.pad, with_stats=True)
 
 
 class Bottleneck(nn.Module):

@@ -39,10 +39,12 @@ def fwd_ok(x, w):
     return _hip(x, w) and x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0
 
 
-def conv_fwd(x, w, stride, padding):
+def conv_fwd(x, w, stride, padding, stats=None):
+    """y = conv(x, w); with ``stats`` (zeroed fp32 [2, K]) the epilogue also accumulates the per-channel
+    sum / sum-of-squares of y for the following BatchNorm (HIP path only; returns whether it did)."""
     if fwd_ok(x, w):
         STATS["hip_fwd"] += 1
-        return _load().conv_fwd(x, w, stride, padding, 1, False, None, 0)
+        return _load().conv_fwd(x, w, stride, padding, 1, False, None, 0, stats)
     STATS["aten_fwd"] += 1
     return _nhwc(F.conv2d(_nchw(x), _nchw(w), None, stride, padding))
 
@@ -63,7 +65,12 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None):
     if hip and C % 8 == 0 and K % 8 == 0 and p is not None and p.grad.dtype == torch.float32:
         STATS["hip_wgrad"] += 1
         acc = p.written
-        C_.conv_wgrad(x, gy, p.grad, stride, padding, 1, 0, acc)
+        if R == 1 and S == 1 and stride == 1 and padding == 0:
+            # 1x1 / stride 1: dW = dY^T . X as a plain tall-K GEMM (both operands read M-major, no im2col)
+            C_.gemm(gy.reshape(-1, K), False, x.reshape(-1, C), False, p.grad.view(K, C), True, None, 0, None, acc,
+                    1.0, 0)
+        else:
+            C_.conv_wgrad(x, gy, p.grad, stride, padding, 1, 0, acc)
         if acc:
             p.store._notify(p)
         else:
@@ -82,7 +89,7 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None):
                              1.0, 1).reshape(N, H, W_, C)
             else:
                 w2 = C_.conv_dgrad_wtrans(w)
-                dx = C_.conv_fwd(gy, w2, 1, R - 1 - padding, 1, False, None, 0)
+                dx = C_.conv_fwd(gy, w2, 1, R - 1 - padding, 1, False, None, 0, None)
         else:
             STATS["aten_dgrad"] += 1
             dx, _ = _aten_bwd(gy, x, w, stride, padding, True, False)

@@ -37,46 +37,62 @@ def _conv_impl():
 
 class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, anchor, p, stride, padding):
+    def forward(ctx, x, anchor, p, stride, padding, with_stats):
         impl = _conv_impl()
         w = p.weight if x.dtype == p.weight.dtype else p.master.to(x.dtype)
-        y = impl.conv_fwd(x, w, stride, padding)
+        sums = None
+        if with_stats and impl.fwd_ok(x, w):
+            sums = torch.zeros(2, w.shape[0], device=x.device, dtype=torch.float32)
+        y = impl.conv_fwd(x, w, stride, padding, sums)
         ctx.save_for_backward(x)
         ctx.p, ctx.stride, ctx.padding = p, stride, padding
         ctx.x_requires_grad = x.requires_grad
-        return y
+        if sums is not None:
+            ctx.mark_non_differentiable(sums)
+        return y, sums
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, gy, _gsums=None):
         (x,) = ctx.saved_tensors
         p = ctx.p
         impl = _conv_impl()
         w = p.weight if x.dtype == p.weight.dtype else p.master.to(x.dtype)
         gy = gy.contiguous()
         dx = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, ctx.x_requires_grad, p)
-        return dx, None, None, None, None
+        return dx, None, None, None, None, None
 
 
-def conv2d_nhwc(x: torch.Tensor, p, stride: int = 1, padding: int = 0) -> torch.Tensor:
-    """NHWC convolution with KRSC weight ``p`` (no bias)."""
-    return _Conv2dNHWC.apply(x, p.store.anchor, p, stride, padding)
+def conv2d_nhwc(x: torch.Tensor, p, stride: int = 1, padding: int = 0, with_stats: bool = False):
+    """NHWC convolution with KRSC weight ``p`` (no bias).
+
+    With ``with_stats`` returns ``(y, sums)``: ``sums`` = fp32 [2, K] per-channel sum / sum of squares of y
+    accumulated in the conv epilogue (None when the layer runs on the fallback path) -- the following
+    ``batch_norm_act(..., sums=sums)`` then needs no statistics pass."""
+    y, sums = _Conv2dNHWC.apply(x, p.store.anchor, p, stride, padding, with_stats)
+    return (y, sums) if with_stats else y
 
 
 # =========================================================================== batchnorm + act
 class _BnAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu):
+    def forward(ctx, x, res, anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu, sums=None):
         x = x.contiguous()
         if res is not None:
             res = res.contiguous()
-        if _gpu(x):
+        if _gpu(x) and sums is not None and training:
+            y, mean, invstd = _C().bn_fwd_from_sums(x, res, pg.master, pb.master, sums, run_mean, run_var, momentum,
+                                                    eps, relu)
+        elif _gpu(x):
             y, mean, invstd = _C().bn_fwd(x, res, pg.master, pb.master, run_mean, run_var, training, momentum, eps,
                                           relu)
         else:
             y, mean, invstd = ref.bn_fwd(x, res, pg.master, pb.master, run_mean, run_var, training, momentum, eps,
                                          relu)
-        ctx.save_for_backward(x, y if relu else None, mean, invstd)
+        # without a residual the ReLU mask is recomputed from x in the backward kernels (no need to keep y)
+        keep_y = relu and (res is not None or not _gpu(x))
+        ctx.save_for_backward(x, y if keep_y else None, mean, invstd)
         ctx.pg, ctx.pb, ctx.has_res = pg, pb, res is not None
+        ctx.relu_x = relu and not keep_y
         return y
 
     @staticmethod
@@ -89,7 +105,7 @@ class _BnAct(torch.autograd.Function):
             sg, sb = store.slot_for_write(pg), store.slot_for_write(pb)
             dg = sg if sg is not None else torch.empty(pg.shape, device=x.device, dtype=torch.float32)
             db = sb if sb is not None else torch.empty(pb.shape, device=x.device, dtype=torch.float32)
-            dx, dres = _C().bn_bwd(dy, x, y, mean, invstd, pg.master, dg, db, ctx.has_res)
+            dx, dres = _C().bn_bwd(dy, x, y, mean, invstd, pg.master, pb.master, ctx.relu_x, dg, db, ctx.has_res)
             if sg is not None:
                 store.mark_written(pg)
             else:
@@ -102,13 +118,16 @@ class _BnAct(torch.autograd.Function):
             dx, dres, dg, db = ref.bn_bwd(dy, x, y, mean, invstd, pg.master)
             store.deposit(pg, dg)
             store.deposit(pb, db)
-        return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None
+        return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm_act(x, pg, pb, run_mean, run_var, residual=None, relu=True, training=True, momentum=0.1,
-                   eps=1e-5):
-    """y = act(BN(x) + residual) over the last (channel) dim of an NHWC tensor."""
-    return _BnAct.apply(x, residual, pg.store.anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu)
+                   eps=1e-5, sums=None):
+    """y = act(BN(x) + residual) over the last (channel) dim of an NHWC tensor.
+
+    ``sums`` (fp32 [2, C] from ``conv2d_nhwc(..., with_stats=True)``) skips the statistics pass."""
+    return _BnAct.apply(x, residual, pg.store.anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu,
+                        sums)
 
 
 # =========================================================================== layernorm / rmsnorm

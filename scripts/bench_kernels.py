@@ -74,7 +74,7 @@ def main():
         w = (torch.randn(K, 3, 3, Cc, device=dev) * 0.05).bfloat16()
         Ho = (H + 2 - 3) // st + 1
         flops = 2.0 * N * Ho * Ho * K * 9 * Cc
-        t_ours = timeit(lambda: C.conv_fwd(x, w, st, 1, 1, False, None, 0))
+        t_ours = timeit(lambda: C.conv_fwd(x, w, st, 1, 1, False, None, 0, None))
         xc, wc = x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2)
         t_ref = timeit(lambda: F.conv2d(xc, wc, None, st, 1))
         dy = torch.randn(N, Ho, Ho, K, device=dev).bfloat16()

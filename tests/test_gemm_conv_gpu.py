@@ -89,7 +89,7 @@ def test_conv_fwd(cuda, case):
     torch.manual_seed(3)
     x = torch.randn(N, H, W, C, device=cuda).bfloat16()
     w = (torch.randn(K, R, R, C, device=cuda) * 0.05).bfloat16()
-    y = _C().conv_fwd(x, w, st, pad, 1, False, None, 0)
+    y = _C().conv_fwd(x, w, st, pad, 1, False, None, 0, None)
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, st, pad).permute(0, 2, 3, 1)
     assert y.shape == ref.shape
     assert _rel(y, ref) < 1e-2
