@@ -159,13 +159,18 @@ __global__ void __launch_bounds__(256) bn_stats_final_kernel(const float* __rest
 
 // Statistics arrive as fp32 (sum, sum of squares) per channel, accumulated by the producing conv's
 // epilogue (gemm.hip, Epi::stats): no extra pass over the activation.
-__global__ void bn_finalize_sums_kernel(const float* __restrict__ sums, int C, float count, float eps, float momentum,
-                                        float* __restrict__ mean_out, float* __restrict__ invstd_out,
+__global__ void bn_finalize_sums_kernel(const float* __restrict__ sums, int nrep, int C, float count, float eps,
+                                        float momentum, float* __restrict__ mean_out, float* __restrict__ invstd_out,
                                         float* __restrict__ run_mean, float* __restrict__ run_var) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  const float mean = sums[c] / count;
-  const float var = fmaxf(sums[C + c] / count - mean * mean, 0.f);
+  float s = 0.f, q = 0.f;
+  for (int r = 0; r < nrep; ++r) {  // replicas written by the conv epilogue
+    s += sums[(long)r * 2 * C + c];
+    q += sums[(long)r * 2 * C + C + c];
+  }
+  const float mean = s / count;
+  const float var = fmaxf(q / count - mean * mean, 0.f);
   mean_out[c] = mean;
   invstd_out[c] = rsqrtf(var + eps);
   if (run_mean) {
@@ -175,7 +180,9 @@ __global__ void bn_finalize_sums_kernel(const float* __restrict__ sums, int C, f
   }
 }
 
-// y = act(x*scale + shift + res); scale = gamma*invstd, shift = beta - mean*scale
+// y = act((x - mean) * (gamma * invstd) + beta [+ res]).
+// The grid is sized so (gridDim.x * blockDim.x) % cgroups == 0: every thread then keeps ONE channel group
+// for the whole grid-stride loop and holds its 8 channels' parameters in registers.
 __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ res,
                                                               const float* __restrict__ mean,
@@ -184,17 +191,24 @@ __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(const uint16_t* __
                                                               const float* __restrict__ beta,
                                                               uint16_t* __restrict__ y, long nvec, int cgroups,
                                                               int relu) {
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nvec; e += (long)gridDim.x * blockDim.x) {
-    const int cg = (int)(e % cgroups);
+  const long e0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int cg = (int)(e0 % cgroups);
+  float mu[8], sc[8], bt[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = cg * 8 + j;
+    mu[j] = mean[c];
+    sc[j] = gamma[c] * invstd[c];
+    bt[j] = beta[c];
+  }
+  for (long e = e0; e < nvec; e += (long)gridDim.x * blockDim.x) {
     float v[8];
     load8(x + e * 8, v);
     float rv[8];
     if (res) load8(res + e * 8, rv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = cg * 8 + j;
-      const float sc = gamma[c] * invstd[c];
-      float o = (v[j] - mean[c]) * sc + beta[c];
+      float o = (v[j] - mu[j]) * sc[j] + bt[j];
       if (res) o += rv[j];
       if (relu) o = fmaxf(o, 0.f);
       v[j] = o;
@@ -230,12 +244,14 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
   const long r0 = blockIdx.x * rows_per_block;
   long r1 = r0 + rows_per_block;
   if (r1 > M) r1 = M;
-  float sd[8], sx[8], mu[8], is[8];
+  float sd[8], sx[8], mu[8], is[8], sc[8], bt[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     sd[j] = sx[j] = 0.f;
     mu[j] = active ? mean[cg * 8 + j] : 0.f;
     is[j] = active ? invstd[cg * 8 + j] : 0.f;
+    sc[j] = (active && relu_x) ? gamma[cg * 8 + j] * is[j] : 0.f;
+    bt[j] = (active && relu_x) ? beta[cg * 8 + j] : 0.f;
   }
   if (active) {
     for (long row = r0 + r; row < r1; row += rows_per_iter) {
@@ -250,10 +266,8 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
           if (bf2f((uint16_t)yv[j]) <= 0.f) g[j] = 0.f;
       } else if (relu_x) {  // ReLU mask recomputed from x: no read of y (non-residual BN)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int c = cg * 8 + j;
-          if (bf2f(f2bf((xv[j] - mu[j]) * (gamma[c] * is[j]) + beta[c])) <= 0.f) g[j] = 0.f;
-        }
+        for (int j = 0; j < 8; ++j)
+          if (bf2f(f2bf((xv[j] - mu[j]) * sc[j] + bt[j])) <= 0.f) g[j] = 0.f;
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -327,8 +341,20 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t
                                                                   uint16_t* __restrict__ dx,
                                                                   uint16_t* __restrict__ dres, long nvec,
                                                                   int cgroups, int C, float inv_m) {
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nvec; e += (long)gridDim.x * blockDim.x) {
-    const int cg = (int)(e % cgroups);
+  const long e0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int cg = (int)(e0 % cgroups);  // fixed per thread: grid sized so (grid*block) % cgroups == 0
+  float mu[8], is[8], sc[8], bt[8], k1[8], k2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = cg * 8 + j;
+    mu[j] = mean[c];
+    is[j] = invstd[c];
+    sc[j] = gamma[c] * is[j];
+    bt[j] = beta ? beta[c] : 0.f;
+    k1[j] = sums[c] * inv_m;      // mean(dy_eff)
+    k2[j] = sums[C + c] * inv_m;  // mean(dy_eff * xhat)
+  }
+  for (long e = e0; e < nvec; e += (long)gridDim.x * blockDim.x) {
     float g[8], xv[8];
     load8(dy + e * 8, g);
     load8(x + e * 8, xv);
@@ -339,18 +365,14 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t
         if (bf2f((uint16_t)yv[j]) <= 0.f) g[j] = 0.f;
     } else if (relu_x) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = cg * 8 + j;
-        if (bf2f(f2bf((xv[j] - mean[c]) * (gamma[c] * invstd[c]) + beta[c])) <= 0.f) g[j] = 0.f;
-      }
+      for (int j = 0; j < 8; ++j)
+        if (bf2f(f2bf((xv[j] - mu[j]) * sc[j] + bt[j])) <= 0.f) g[j] = 0.f;
     }
     if (dres) store8(dres + e * 8, g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = cg * 8 + j;
-      const float is = invstd[c];
-      const float xh = (xv[j] - mean[c]) * is;
-      xv[j] = gamma[c] * is * (g[j] - sums[c] * inv_m - xh * sums[C + c] * inv_m);
+      const float xh = (xv[j] - mu[j]) * is[j];
+      xv[j] = sc[j] * (g[j] - k1[j] - xh * k2[j]);
     }
     store8(dx + e * 8, xv);
   }
@@ -366,6 +388,19 @@ static long bn_rows_per_block(long M, const BnGeom& g) {
   if (rpb < minr) rpb = minr;
   rpb = (rpb + g.rows_per_iter - 1) / g.rows_per_iter * g.rows_per_iter;
   return rpb;
+}
+
+// grid for the per-element kernels: (grid * BN_THREADS) % cgroups == 0 keeps each thread on one channel group
+static int bn_elem_grid(long nvec, int cgroups) {
+  int g = stream_grid(nvec, BN_THREADS);
+  if ((BN_THREADS % cgroups) != 0) {
+    // cgroups does not divide the block: round the grid up to a multiple of cgroups / gcd(cgroups, BN_THREADS)
+    int a = cgroups, b = BN_THREADS;
+    while (b) { int t = a % b; a = b; b = t; }
+    const int step = cgroups / a;
+    g = (g + step - 1) / step * step;
+  }
+  return g;
 }
 
 int bn_workspace_floats(long M, int C) {
@@ -391,17 +426,18 @@ void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, c
                        save_mean, save_invstd);
   }
   const long nvec = M * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(stream_grid(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, x, res,
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(bn_elem_grid(nvec, C / 8)), dim3(BN_THREADS), 0, st, x, res,
                      save_mean, save_invstd, gamma, beta, y, nvec, C / 8, (int)relu);
 }
 
 void launch_bn_fwd_from_sums(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
-                             uint16_t* y, const float* sums, float* save_mean, float* save_invstd, float* run_mean,
-                             float* run_var, long M, int C, float eps, float momentum, bool relu, hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, C, (float)M, eps, momentum,
-                     save_mean, save_invstd, run_mean, run_var);
+                             uint16_t* y, const float* sums, int nrep, float* save_mean, float* save_invstd,
+                             float* run_mean, float* run_var, long M, int C, float eps, float momentum, bool relu,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, nrep, C, (float)M, eps,
+                     momentum, save_mean, save_invstd, run_mean, run_var);
   const long nvec = M * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(stream_grid(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, x, res,
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(bn_elem_grid(nvec, C / 8)), dim3(BN_THREADS), 0, st, x, res,
                      save_mean, save_invstd, gamma, beta, y, nvec, C / 8, (int)relu);
 }
 
@@ -415,7 +451,7 @@ void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, con
                      gamma, beta, (int)relu_x, M, C, g.tpr, g.rows_per_iter, rpb, work);
   hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, nb, C, sums, dgamma, dbeta);
   const long nvec = M * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, dy, x, y,
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(bn_elem_grid(nvec, C / 8)), dim3(BN_THREADS), 0, st, dy, x, y,
                      mean, invstd, beta, (int)relu_x, gamma, sums, dx, dres, nvec, C / 8, C, 1.f / (float)M);
 }
 

@@ -1,0 +1,187 @@
+// K9: transformer elementwise fusions, bf16 16-byte vectors, fp32 math.
+//
+//  * SwiGLU   y = silu(g) * u over a fused [T, 2F] gate|up GEMM output, and its backward
+//  * RoPE     rotary embedding on [T, H, D] q/k in place of the usual 4 elementwise passes
+//             (cos/sin from a precomputed fp32 table, host-built once -- no device trig)
+//  * GELU(tanh) backward from the saved pre-activation
+//  * column sums (bias gradients) without atomics: block partials + fold
+#include "common.h"
+#include "launchers.h"
+
+namespace k8s_amd {
+
+__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+
+// gu: [T, 2F] (gate in [:, :F], up in [:, F:]) -> y: [T, F]
+__global__ void __launch_bounds__(256) swiglu_fwd_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ y,
+                                                         long T, int F) {
+  const int fv = F / 8;
+  const long total = T * fv;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long t = e / fv;
+    const int c = (int)(e - t * fv) * 8;
+    float g[8], u[8], o[8];
+    load8(gu + t * 2 * F + c, g);
+    load8(gu + t * 2 * F + F + c, u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = silu(g[j]) * u[j];
+    store8(y + t * F + c, o);
+  }
+}
+
+// dgu[:, :F] = dy * u * silu'(g),  dgu[:, F:] = dy * silu(g)
+__global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restrict__ gu,
+                                                         const uint16_t* __restrict__ dy, uint16_t* __restrict__ dgu,
+                                                         long T, int F) {
+  const int fv = F / 8;
+  const long total = T * fv;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long t = e / fv;
+    const int c = (int)(e - t * fv) * 8;
+    float g[8], u[8], d[8], dg[8], du[8];
+    load8(gu + t * 2 * F + c, g);
+    load8(gu + t * 2 * F + F + c, u);
+    load8(dy + t * F + c, d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float s = 1.f / (1.f + __expf(-g[j]));
+      const float sl = g[j] * s;
+      du[j] = d[j] * sl;
+      dg[j] = d[j] * u[j] * (s * (1.f + g[j] * (1.f - s)));
+    }
+    store8(dgu + t * 2 * F + c, dg);
+    store8(dgu + t * 2 * F + F + c, du);
+  }
+}
+
+// x: [T, H, D] bf16 (row stride ld elements between tokens), pos: [T] int32, table: [maxpos, D/2] (cos, sin)
+// rotate-half convention (x1 = x[:D/2], x2 = x[D/2:]): out1 = x1 c - x2 s, out2 = x2 c + x1 s.
+// sign = -1 applies the inverse rotation (backward).
+__global__ void __launch_bounds__(256) rope_kernel(uint16_t* __restrict__ x, long ld, const int* __restrict__ pos,
+                                                   const float2* __restrict__ table, long T, int H, int D, float sign) {
+  const int half = D / 2, hv = half / 8;
+  const long total = T * H * hv;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long th = e / hv;
+    const int c = (int)(e - th * hv) * 8;
+    const long t = th / H;
+    const int h = (int)(th - t * H);
+    uint16_t* row = x + t * ld + (long)h * D;
+    const float2* tb = table + (long)pos[t] * half + c;
+    float a[8], b[8];
+    load8(row + c, a);
+    load8(row + half + c, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float cs = tb[j].x, sn = sign * tb[j].y;
+      const float x1 = a[j], x2 = b[j];
+      a[j] = x1 * cs - x2 * sn;
+      b[j] = x2 * cs + x1 * sn;
+    }
+    store8(row + c, a);
+    store8(row + half + c, b);
+  }
+}
+
+__global__ void __launch_bounds__(256) gelu_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ pre,
+                                                       uint16_t* __restrict__ dx, long nvec) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nvec; e += (long)gridDim.x * blockDim.x) {
+    float d[8], x[8];
+    load8(dy + e * 8, d);
+    load8(pre + e * 8, x);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float u = k0 * (x[j] + k1 * x[j] * x[j] * x[j]);
+      const float t = tanhf(u);
+      const float g = 0.5f * (1.f + t) + 0.5f * x[j] * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x[j] * x[j]);
+      d[j] *= g;
+    }
+    store8(dx + e * 8, d);
+  }
+}
+
+// relu backward with the mask taken from the (post-ReLU) output y
+__global__ void __launch_bounds__(256) relu_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+                                                       uint16_t* __restrict__ dx, long nvec) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nvec; e += (long)gridDim.x * blockDim.x) {
+    float d[8], v[8];
+    load8(dy + e * 8, d);
+    load8(y + e * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = v[j] > 0.f ? d[j] : 0.f;
+    store8(dx + e * 8, d);
+  }
+}
+
+// column sums of a [R, C] bf16 matrix -> fp32 [C] (written, or added when accumulate)
+__global__ void __launch_bounds__(256) colsum_partial_kernel(const uint16_t* __restrict__ x, long R, int C, long rpb,
+                                                             float* __restrict__ part) {
+  const int cv = C / 8;
+  const int cg = blockIdx.y * 32 + (threadIdx.x & 31);
+  const int rg = threadIdx.x >> 5;  // 8 row groups
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (cg < cv) {
+    const long r0 = blockIdx.x * rpb;
+    const long r1 = r0 + rpb < R ? r0 + rpb : R;
+    for (long r = r0 + rg; r < r1; r += 8) {
+      float v[8];
+      load8(x + r * C + cg * 8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += v[j];
+    }
+  }
+  __shared__ float sh[8][32][9];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sh[rg][threadIdx.x & 31][j] = s[j];
+  __syncthreads();
+  if (rg == 0 && cg < cv) {
+    for (int g = 1; g < 8; ++g)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += sh[g][threadIdx.x][j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part[(long)blockIdx.x * C + cg * 8 + j] = s[j];
+  }
+}
+
+__global__ void colsum_fold_kernel(const float* __restrict__ part, int P, int C, float* __restrict__ out, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += part[(long)p * C + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+// ----------------------------------------------------------------------------- launchers
+void launch_swiglu_fwd(const uint16_t* gu, uint16_t* y, long T, int F, hipStream_t st) {
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(stream_grid(T * F / 8, 256)), dim3(256), 0, st, gu, y, T, F);
+}
+void launch_swiglu_bwd(const uint16_t* gu, const uint16_t* dy, uint16_t* dgu, long T, int F, hipStream_t st) {
+  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(stream_grid(T * F / 8, 256)), dim3(256), 0, st, gu, dy, dgu, T, F);
+}
+void launch_rope(uint16_t* x, long ld, const int* pos, const float* table, long T, int H, int D, bool inverse,
+                 hipStream_t st) {
+  hipLaunchKernelGGL(rope_kernel, dim3(stream_grid(T * H * (D / 16), 256)), dim3(256), 0, st, x, ld, pos,
+                     (const float2*)table, T, H, D, inverse ? -1.f : 1.f);
+}
+void launch_gelu_bwd(const uint16_t* dy, const uint16_t* pre, uint16_t* dx, long n, hipStream_t st) {
+  hipLaunchKernelGGL(gelu_bwd_kernel, dim3(stream_grid(n / 8, 256)), dim3(256), 0, st, dy, pre, dx, n / 8);
+}
+void launch_relu_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n, hipStream_t st) {
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3(stream_grid(n / 8, 256)), dim3(256), 0, st, dy, y, dx, n / 8);
+}
+int colsum_workspace_floats(long R, int C) {
+  long nb = (R + 255) / 256;
+  if (nb > 256) nb = 256;
+  return (int)(nb * C);
+}
+void launch_colsum(const uint16_t* x, long R, int C, float* work, float* out, bool accumulate, hipStream_t st) {
+  long nb = (R + 255) / 256;
+  if (nb > 256) nb = 256;
+  const long rpb = (R + nb - 1) / nb;
+  dim3 g((unsigned)nb, (unsigned)((C / 8 + 31) / 32));
+  hipLaunchKernelGGL(colsum_partial_kernel, g, dim3(256), 0, st, x, R, C, rpb, work);
+  hipLaunchKernelGGL(colsum_fold_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, work, (int)nb, C, out, (int)accumulate);
+}
+
+}  // namespace k8s_amd

@@ -197,8 +197,11 @@ struct Epi {
   int act;            // 0 none, 1 relu, 2 gelu(tanh)
   int mode;           // 0 store, 1 accumulate (fp32 C += acc), 2 atomic add (fp32)
   float alpha;
-  float* stats;       // [2][N] fp32 per-column sum / sum of squares of the stored outputs (BN fusion) or null
+  float* stats;       // [STAT_REPL][2][N] fp32 per-column sum / sum of squares of the stored outputs
+                      // (BN fusion) or null; tile row tm adds into replica tm % STAT_REPL so the atomics
+                      // spread over STAT_REPL x 2N addresses instead of contending on 2N
 };
+constexpr int STAT_REPL = 32;
 
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
@@ -375,8 +378,9 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
           b += __shfl_xor(b, o, 64);
         }
         if ((lane & 15) == 0 && n + r < N) {
-          atomicAdd(E.stats + n + r, a);
-          atomicAdd(E.stats + N + n + r, b);
+          float* rep = E.stats + (long)(tm % STAT_REPL) * 2 * N;
+          atomicAdd(rep + n + r, a);
+          atomicAdd(rep + N + n + r, b);
         }
       }
     }

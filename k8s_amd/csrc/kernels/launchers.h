@@ -23,8 +23,10 @@ void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, c
                    float* save_mean, float* save_invstd, float* run_mean, float* run_var, float* work, long M, int C,
                    float eps, float momentum, bool training, bool relu, hipStream_t st);
 void launch_bn_fwd_from_sums(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
-                             uint16_t* y, const float* sums, float* save_mean, float* save_invstd, float* run_mean,
-                             float* run_var, long M, int C, float eps, float momentum, bool relu, hipStream_t st);
+                             uint16_t* y, const float* sums, int nrep, float* save_mean, float* save_invstd,
+                             float* run_mean, float* run_var, long M, int C, float eps, float momentum, bool relu,
+                             hipStream_t st);
+constexpr int kConvStatReplicas = 32;  // must match STAT_REPL in gemm.hip
 void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
                    const float* gamma, const float* beta, bool relu_x, uint16_t* dx, uint16_t* dres, float* dgamma,
                    float* dbeta, float* work, float* sums, long M, int C, hipStream_t st);
@@ -56,5 +58,15 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, 
 void launch_conv_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int C, int K, int R,
                        int S, int stride, int pad, int dil, int Ho, int Wo, int splits, hipStream_t st);
 void launch_conv_dgrad_wtrans(const uint16_t* w, uint16_t* w2, int K, int R, int S, int C, hipStream_t st);
+
+// elementwise.hip
+void launch_swiglu_fwd(const uint16_t* gu, uint16_t* y, long T, int F, hipStream_t st);
+void launch_swiglu_bwd(const uint16_t* gu, const uint16_t* dy, uint16_t* dgu, long T, int F, hipStream_t st);
+void launch_rope(uint16_t* x, long ld, const int* pos, const float* table, long T, int H, int D, bool inverse,
+                 hipStream_t st);
+void launch_gelu_bwd(const uint16_t* dy, const uint16_t* pre, uint16_t* dx, long n, hipStream_t st);
+void launch_relu_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n, hipStream_t st);
+int colsum_workspace_floats(long R, int C);
+void launch_colsum(const uint16_t* x, long R, int C, float* work, float* out, bool accumulate, hipStream_t st);
 
 }  // namespace k8s_amd

@@ -111,13 +111,14 @@ std::vector<Tensor> bn_fwd_from_sums(Tensor x, c10::optional<Tensor> res, Tensor
   const int C = (int)x.size(-1);
   TORCH_CHECK(C % 8 == 0, "channels must be a multiple of 8");
   const long M = x.numel() / C;
-  TORCH_CHECK(sums.numel() == 2 * C && sums.scalar_type() == at::kFloat, "sums must be fp32 [2, C]");
+  TORCH_CHECK(sums.numel() % (2 * C) == 0 && sums.scalar_type() == at::kFloat, "sums must be fp32 [R, 2, C]");
+  const int nrep = (int)(sums.numel() / (2 * C));
   if (res) { check_cuda(*res, "res"); TORCH_CHECK(res->sizes() == x.sizes(), "residual shape mismatch"); }
   auto y = torch::empty_like(x);
   auto mean = torch::empty({C}, gamma.options());
   auto invstd = torch::empty({C}, gamma.options());
   k8s_amd::launch_bn_fwd_from_sums(cbf(x), res ? cbf(*res) : nullptr, f32(gamma), f32(beta), bf(y), f32(sums),
-                                   f32(mean), f32(invstd), f32(run_mean), f32(run_var), M, C, (float)eps,
+                                   nrep, f32(mean), f32(invstd), f32(run_mean), f32(run_var), M, C, (float)eps,
                                    (float)momentum, relu, cur_stream());
   return {y, mean, invstd};
 }
@@ -270,8 +271,9 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, bo
   TORCH_CHECK(K % 8 == 0, "output channels must be a multiple of 8");
   const int Ho = conv_out(H, R, stride, pad, dil), Wo = conv_out(W, S, stride, pad, dil);
   auto y = torch::empty({N, Ho, Wo, K}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
-  if (stats) TORCH_CHECK(stats->numel() == 2 * K && stats->scalar_type() == at::kFloat && stats->is_contiguous(),
-                         "stats must be fp32 [2, K] (zeroed)");
+  if (stats) TORCH_CHECK(stats->numel() == (long)k8s_amd::kConvStatReplicas * 2 * K &&
+                             stats->scalar_type() == at::kFloat && stats->is_contiguous(),
+                         "stats must be zeroed fp32 [conv_stat_replicas, 2, K]");
   k8s_amd::launch_conv_fwd(cbf(x), cbf(w), y.data_ptr(), out_f32, N, H, W, C, K, R, S, (int)stride, (int)pad,
                            (int)dil, Ho, Wo, bias ? bias->data_ptr<float>() : nullptr, (int)act, 0,
                            stats ? f32(*stats) : nullptr, cur_stream());
@@ -303,6 +305,62 @@ Tensor conv_dgrad_wtrans(Tensor w) {
   return w2;
 }
 
+// ------------------------------------------------------------------ elementwise (K9)
+Tensor swiglu_fwd(Tensor gu) {
+  check_cuda(gu, "gu"); check_dtype(gu, at::kBFloat16, "gu");
+  const long F2 = gu.size(-1);
+  TORCH_CHECK(F2 % 16 == 0, "2F must be a multiple of 16");
+  const long T = gu.numel() / F2;
+  auto sizes = gu.sizes().vec();
+  sizes.back() = F2 / 2;
+  auto y = torch::empty(sizes, gu.options());
+  k8s_amd::launch_swiglu_fwd(cbf(gu), bf(y), T, (int)(F2 / 2), cur_stream());
+  return y;
+}
+Tensor swiglu_bwd(Tensor gu, Tensor dy) {
+  check_cuda(gu, "gu"); check_cuda(dy, "dy");
+  const long F2 = gu.size(-1);
+  TORCH_CHECK(dy.numel() * 2 == gu.numel());
+  auto dgu = torch::empty_like(gu);
+  k8s_amd::launch_swiglu_bwd(cbf(gu), cbf(dy), bf(dgu), gu.numel() / F2, (int)(F2 / 2), cur_stream());
+  return dgu;
+}
+void rope_(Tensor x, Tensor pos, Tensor table, bool inverse) {
+  check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x");
+  check_cuda(pos, "pos"); check_dtype(pos, at::kInt, "pos");
+  check_cuda(table, "table"); check_dtype(table, at::kFloat, "table");
+  const int D = (int)table.size(1) * 2;
+  TORCH_CHECK(D % 16 == 0, "head dim must be a multiple of 16");
+  const long T = pos.numel();
+  TORCH_CHECK(x.numel() % (T * D) == 0, "x must be [T, H*D]");
+  const int H = (int)(x.numel() / (T * D));
+  k8s_amd::launch_rope(bf(x), (long)H * D, pos.data_ptr<int>(), f32(table), T, H, D, inverse, cur_stream());
+}
+Tensor gelu_bwd(Tensor dy, Tensor pre) {
+  check_cuda(dy, "dy"); check_cuda(pre, "pre");
+  TORCH_CHECK(dy.numel() == pre.numel() && dy.numel() % 8 == 0);
+  auto dx = torch::empty_like(dy);
+  k8s_amd::launch_gelu_bwd(cbf(dy), cbf(pre), bf(dx), dy.numel(), cur_stream());
+  return dx;
+}
+Tensor relu_bwd(Tensor dy, Tensor y) {
+  check_cuda(dy, "dy"); check_cuda(y, "y");
+  TORCH_CHECK(dy.numel() == y.numel() && dy.numel() % 8 == 0);
+  auto dx = torch::empty_like(dy);
+  k8s_amd::launch_relu_bwd(cbf(dy), cbf(y), bf(dx), dy.numel(), cur_stream());
+  return dx;
+}
+Tensor colsum(Tensor x) {
+  check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x");
+  const int C = (int)x.size(-1);
+  TORCH_CHECK(C % 8 == 0);
+  const long R = x.numel() / C;
+  auto out = torch::empty({C}, x.options().dtype(at::kFloat));
+  auto work = torch::empty({k8s_amd::colsum_workspace_floats(R, C)}, out.options());
+  k8s_amd::launch_colsum(cbf(x), R, C, f32(work), f32(out), false, cur_stream());
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -319,8 +377,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
   m.def("gemm", &gemm);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("rope_", &rope_);
+  m.def("gelu_bwd", &gelu_bwd);
+  m.def("relu_bwd", &relu_bwd);
+  m.def("colsum", &colsum);
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_dgrad_wtrans", &conv_dgrad_wtrans);
+  m.attr("conv_stat_replicas") = k8s_amd::kConvStatReplicas;
   m.attr("arch") = "gfx950";
 }

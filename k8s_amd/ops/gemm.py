@@ -50,6 +50,10 @@ def _act_fwd(y, act):
 def _act_bwd(gy, pre_or_out, act):
     if act is None:
         return gy
+    if gy.is_cuda and gy.dtype == torch.bfloat16 and gy.numel() % 8 == 0 and act in ("relu", "gelu"):
+        C = _load()
+        g = gy.contiguous()
+        return C.relu_bwd(g, pre_or_out.contiguous()) if act == "relu" else C.gelu_bwd(g, pre_or_out.contiguous())
     if act == "relu":
         return gy * (pre_or_out > 0)
     if act == "gelu":
@@ -83,7 +87,11 @@ def linear_bwd(gy, x, w, saved, act, pw=None, store=None):
     g = _act_bwd(gy, saved, act)
     M, K = x.shape
     N = w.shape[0]
-    db = g.float().sum(0) if True else None
+    db = None
+    if g.is_cuda and g.dtype == torch.bfloat16 and N % 8 == 0:
+        db = _load().colsum(g.contiguous())
+    else:
+        db = g.float().sum(0)
     if hip_ok(g, x, w) and _shape_ok(M, N, K) and N % 64 == 0:
         dx = mm(g, w, True, False)
         if pw is not None and store is not None and pw.grad.dtype == torch.float32:

@@ -42,7 +42,7 @@ class _Conv2dNHWC(torch.autograd.Function):
         w = p.weight if x.dtype == p.weight.dtype else p.master.to(x.dtype)
         sums = None
         if with_stats and impl.fwd_ok(x, w):
-            sums = torch.zeros(2, w.shape[0], device=x.device, dtype=torch.float32)
+            sums = torch.zeros(_C().conv_stat_replicas, 2, w.shape[0], device=x.device, dtype=torch.float32)
         y = impl.conv_fwd(x, w, stride, padding, sums)
         ctx.save_for_backward(x)
         ctx.p, ctx.stride, ctx.padding = p, stride, padding
@@ -280,3 +280,80 @@ def max_pool_nhwc(x, k=3, s=2, p=1):
 
 def global_avg_pool_nhwc(x):
     return x.mean(dim=(1, 2))
+
+
+# =========================================================================== transformer elementwise (K9)
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        gu = gu.contiguous()
+        F2 = gu.shape[-1] // 2
+        if _gpu(gu) and gu.dtype == torch.bfloat16 and F2 % 8 == 0:
+            y = _C().swiglu_fwd(gu)
+        else:
+            g, u = gu.float().split(F2, -1)
+            y = (torch.nn.functional.silu(g) * u).to(gu.dtype)
+        ctx.save_for_backward(gu)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (gu,) = ctx.saved_tensors
+        F2 = gu.shape[-1] // 2
+        dy = dy.contiguous()
+        if _gpu(gu) and gu.dtype == torch.bfloat16 and F2 % 8 == 0:
+            return _C().swiglu_bwd(gu, dy)
+        g, u = gu.float().split(F2, -1)
+        s = torch.sigmoid(g)
+        d = dy.float()
+        return torch.cat([d * u * s * (1 + g * (1 - s)), d * g * s], -1).to(gu.dtype)
+
+
+def swiglu(gu):
+    """silu(gate) * up over a fused [.., 2F] gate|up projection."""
+    return _SwiGLU.apply(gu)
+
+
+def rope_table(max_pos: int, dim: int, theta: float = 10000.0, device=None) -> torch.Tensor:
+    """[max_pos, dim/2, 2] fp32 (cos, sin), built once on the host side of the step."""
+    inv = 1.0 / (theta ** (torch.arange(0, dim, 2, dtype=torch.float64) / dim))
+    ang = torch.arange(max_pos, dtype=torch.float64)[:, None] * inv[None, :]
+    return torch.stack([ang.cos(), ang.sin()], -1).float().to(device)
+
+
+def _rope_ref(x, pos, table, inverse=False):
+    T = x.shape[0]
+    D = table.shape[1] * 2
+    xs = x.float().reshape(T, -1, D)
+    cs = table[pos.long()]  # [T, D/2, 2]
+    c, s = cs[..., 0][:, None, :], cs[..., 1][:, None, :]
+    if inverse:
+        s = -s
+    x1, x2 = xs[..., : D // 2], xs[..., D // 2:]
+    out = torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], -1)
+    return out.reshape(x.shape).to(x.dtype)
+
+
+class _Rope(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, pos, table):
+        ctx.save_for_backward(pos, table)
+        if _gpu(x) and x.dtype == torch.bfloat16:
+            y = x.contiguous().clone()
+            _C().rope_(y, pos, table, False)
+            return y
+        return _rope_ref(x, pos, table)
+
+    @staticmethod
+    def backward(ctx, dy):
+        pos, table = ctx.saved_tensors
+        if _gpu(dy) and dy.dtype == torch.bfloat16:
+            d = dy.contiguous().clone()
+            _C().rope_(d, pos, table, True)
+            return d, None, None
+        return _rope_ref(dy, pos, table, inverse=True), None, None
+
+
+def rope(x, pos, table):
+    """Rotary embedding of x [T, H*D] (token-major, rotate-half), pos [T] int32, table from ``rope_table``."""
+    return _Rope.apply(x, pos, table)

@@ -124,3 +124,51 @@ def test_conv_dgrad_stride1(cuda, case):
     xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
     F.conv2d(xr, w.float().permute(0, 3, 1, 2), None, st, pad).backward(dy.float().permute(0, 3, 1, 2))
     assert _rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_bn_stats_epilogue(cuda, case):
+    N, H, W, C, K, R, st, pad = case
+    torch.manual_seed(6)
+    x = torch.randn(N, H, W, C, device=cuda).bfloat16()
+    w = (torch.randn(K, R, R, C, device=cuda) * 0.05).bfloat16()
+    stats = torch.zeros(_C().conv_stat_replicas, 2, K, device=cuda)
+    y = _C().conv_fwd(x, w, st, pad, 1, False, None, 0, stats)
+    yf = y.float().reshape(-1, K)
+    tot = stats.sum(0)
+    assert _rel(tot[0], yf.sum(0)) < 1e-3
+    assert _rel(tot[1], (yf * yf).sum(0)) < 1e-3
+
+
+def test_elementwise_kernels(cuda):
+    from k8s_amd.ops import nn as K
+
+    torch.manual_seed(8)
+    T, F2 = 96, 2 * 256
+    gu = torch.randn(T, F2, device=cuda).bfloat16()
+    y = _C().swiglu_fwd(gu)
+    g, u = gu.float().split(F2 // 2, -1)
+    assert _rel(y, F.silu(g) * u) < 1e-2
+    dy = torch.randn(T, F2 // 2, device=cuda).bfloat16()
+    gg = gu.float().requires_grad_(True)
+    a, b = gg.split(F2 // 2, -1)
+    (F.silu(a) * b).backward(dy.float())
+    assert _rel(_C().swiglu_bwd(gu, dy), gg.grad) < 1e-2
+    # rope forward then inverse = identity; matches the reference
+    H, D = 4, 128
+    x = torch.randn(T, H * D, device=cuda).bfloat16()
+    pos = torch.arange(T, device=cuda, dtype=torch.int32)
+    table = K.rope_table(512, D, 500000.0, cuda)
+    xr = x.clone()
+    _C().rope_(xr, pos, table, False)
+    assert _rel(xr, K._rope_ref(x, pos, table)) < 1e-2
+    _C().rope_(xr, pos, table, True)
+    assert _rel(xr, x) < 2e-2
+    # gelu / relu backward and column sums
+    pre = torch.randn(T, 512, device=cuda).bfloat16()
+    d = torch.randn(T, 512, device=cuda).bfloat16()
+    pp = pre.float().requires_grad_(True)
+    F.gelu(pp, approximate="tanh").backward(d.float())
+    assert _rel(_C().gelu_bwd(d, pre), pp.grad) < 1e-2
+    assert _rel(_C().relu_bwd(d, torch.relu(pre)), d.float() * (pre.float() > 0)) < 1e-3
+    assert _rel(_C().colsum(d), d.float().sum(0)) < 1e-3

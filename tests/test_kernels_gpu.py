@@ -39,13 +39,44 @@ def test_bn_fwd_bwd(cuda, C, M, relu, res):
     _close(rv, rv2, 1e-3)
     dy = torch.randn(M, C, device=cuda).bfloat16()
     dg, db = torch.empty(C, device=cuda), torch.empty(C, device=cuda)
-    dx, dres = _C().bn_bwd(dy, x, y if relu else None, mean, invstd, g, dg, db, res)
+    dx, dres = _C().bn_bwd(dy, x, y if relu else None, mean, invstd, g, b, False, dg, db, res)
     dxr, dresr, dgr, dbr = ref.bn_bwd(dy, x, yr if relu else None, meanr, invr, g)
     _close(dg, dgr, 2e-2)
     _close(db, dbr, 2e-2)
     _close(dx, dxr, 3e-2)
     if res:
         _close(dres, dresr, 1e-2)
+
+
+@pytest.mark.parametrize("C,M", [(64, 4096), (256, 1000), (2048, 98)])
+def test_bn_from_conv_sums_and_relu_from_x(cuda, C, M):
+    """BN fed by conv-epilogue statistics (replicated partial sums) and backward with the ReLU mask
+    recomputed from x must match the two-pass kernels."""
+    torch.manual_seed(7)
+    x = (torch.randn(M, C, device=cuda) * 2 + 0.5).bfloat16()
+    g = torch.rand(C, device=cuda) + 0.5
+    b = torch.randn(C, device=cuda)
+    R = _C().conv_stat_replicas
+    sums = torch.zeros(R, 2, C, device=cuda)
+    xf = x.float()
+    for r in range(R):  # spread the row sums over the replicas like the conv epilogue does
+        part = xf[r::R]
+        sums[r, 0] = part.sum(0)
+        sums[r, 1] = (part * part).sum(0)
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    y, mean, invstd = _C().bn_fwd_from_sums(x, None, g, b, sums, rm, rv, 0.1, 1e-5, True)
+    yr, meanr, invr = ref.bn_fwd(x, None, g, b, torch.zeros(C, device=cuda), torch.ones(C, device=cuda), True, 0.1,
+                                 1e-5, True)
+    _close(mean, meanr, 1e-4)
+    _close(invstd, invr, 1e-3)
+    _close(y, yr, 2e-2)
+    dy = torch.randn(M, C, device=cuda).bfloat16()
+    dg, db = torch.empty(C, device=cuda), torch.empty(C, device=cuda)
+    dx, _ = _C().bn_bwd(dy, x, None, mean, invstd, g, b, True, dg, db, False)
+    dxr, _, dgr, dbr = ref.bn_bwd(dy, x, y, mean, invstd, g)
+    _close(dx, dxr, 3e-2)
+    _close(dg, dgr, 2e-2)
+    _close(db, dbr, 2e-2)
 
 
 @pytest.mark.parametrize("D", [768, 4096, 1024, 136])
