@@ -197,15 +197,18 @@ std::vector<Tensor> xent_fwd(Tensor logits, Tensor labels, int64_t ignore_index,
   return {loss, lse};
 }
 
-Tensor xent_bwd(Tensor logits, Tensor labels, Tensor lse, Tensor dscale, int64_t ignore_index, double smoothing) {
-  const long R = logits.size(0), V = logits.size(1);
+// logits [R, Vpad] dense; classes are the first V columns; returns dlogits [R, Vpad] (pad columns zero)
+Tensor xent_bwd(Tensor logits, Tensor labels, Tensor lse, Tensor dscale, int64_t ignore_index, double smoothing,
+                int64_t V) {
+  const long R = logits.size(0), Vpad = logits.size(1);
+  TORCH_CHECK(logits.is_contiguous(), "xent_bwd expects dense logits");
+  TORCH_CHECK(V > 0 && V <= Vpad);
   TORCH_CHECK(dscale.numel() == 1 || dscale.numel() == R);
   auto d = dscale.to(at::kFloat).contiguous();
-  auto dl = torch::empty({R, V}, logits.options());
-  TORCH_CHECK(logits.stride(0) == V, "xent_bwd expects dense logits");
+  auto dl = V == Vpad ? torch::empty({R, Vpad}, logits.options()) : torch::zeros({R, Vpad}, logits.options());
   k8s_amd::launch_xent_bwd(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, labels.data_ptr<int64_t>(),
-                           f32(lse), f32(d), d.numel() == R, R, V, V, dl.data_ptr(), ignore_index, (float)smoothing,
-                           cur_stream());
+                           f32(lse), f32(d), d.numel() == R, R, V, Vpad, dl.data_ptr(), ignore_index,
+                           (float)smoothing, cur_stream());
   return dl;
 }
 

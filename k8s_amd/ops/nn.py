@@ -245,31 +245,39 @@ def embedding(ids, pw, dtype=torch.bfloat16):
 # =========================================================================== loss
 class _CrossEntropy(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, logits, labels, ignore_index, smoothing):
-        logits = logits.contiguous()
+    def forward(ctx, logits, labels, ignore_index, smoothing, valid):
+        # logits [R, Vpad]: only the first `valid` columns are classes (MFMA-friendly padded vocabularies)
+        logits = logits if logits.stride(-1) == 1 else logits.contiguous()
+        ctx.valid = valid
+        full = logits
+        if valid is not None and valid != logits.shape[1]:
+            logits = logits[:, :valid]
         if _gpu(logits):
             loss, lse = _C().xent_fwd(logits, labels, ignore_index, smoothing)
         else:
             loss, lse = ref.xent_fwd(logits, labels, ignore_index, smoothing)
-        valid = (labels != ignore_index).sum().clamp_min(1).float()
-        ctx.save_for_backward(logits, labels, lse, valid)
+        nvalid = (labels != ignore_index).sum().clamp_min(1).float()
+        ctx.save_for_backward(full, labels, lse, nvalid)
         ctx.ignore_index, ctx.smoothing = ignore_index, smoothing
-        return loss.sum() / valid
+        return loss.sum() / nvalid
 
     @staticmethod
     def backward(ctx, gl):
-        logits, labels, lse, valid = ctx.saved_tensors
-        dscale = (gl.float() / valid).reshape(1)
-        if _gpu(logits):
-            d = _C().xent_bwd(logits, labels, lse, dscale, ctx.ignore_index, ctx.smoothing)
+        full, labels, lse, nvalid = ctx.saved_tensors
+        dscale = (gl.float() / nvalid).reshape(1)
+        V = ctx.valid if ctx.valid is not None else full.shape[1]
+        if _gpu(full):
+            d = _C().xent_bwd(full, labels, lse, dscale, ctx.ignore_index, ctx.smoothing, V)
         else:
-            d = ref.xent_bwd(logits, labels, lse, dscale, ctx.ignore_index, ctx.smoothing)
-        return d, None, None, None
+            d = torch.zeros_like(full)
+            d[:, :V] = ref.xent_bwd(full[:, :V], labels, lse, dscale, ctx.ignore_index, ctx.smoothing)
+        return d, None, None, None, None
 
 
-def cross_entropy(logits, labels, ignore_index: int = -100, smoothing: float = 0.0):
-    """Mean softmax cross-entropy over valid rows of [R, V] logits."""
-    return _CrossEntropy.apply(logits.reshape(-1, logits.shape[-1]), labels.reshape(-1), ignore_index, smoothing)
+def cross_entropy(logits, labels, ignore_index: int = -100, smoothing: float = 0.0, valid: int = None):
+    """Mean softmax cross-entropy over valid rows of [R, V] logits (classes = first ``valid`` columns)."""
+    return _CrossEntropy.apply(logits.reshape(-1, logits.shape[-1]), labels.reshape(-1), ignore_index, smoothing,
+                               valid)
 
 
 # =========================================================================== pooling (NHWC)

@@ -119,7 +119,7 @@ def test_xent(cuda, R, V, dt, smooth):
     _close(lse, lser, 1e-4)
     _close(loss, lr, 1e-3)
     ds = torch.tensor([0.37], device=cuda)
-    d = _C().xent_bwd(x, lab, lse, ds, -100, smooth)
+    d = _C().xent_bwd(x, lab, lse, ds, -100, smooth, V)
     dr = ref.xent_bwd(x, lab, lser, ds, -100, smooth)
     _close(d, dr, 2e-2 if dt == torch.bfloat16 else 1e-5)
 
