@@ -126,6 +126,11 @@ def main(argv=None):
             "final_loss": round(final_loss, 4),
         }
         print(json.dumps(out), flush=True)
+        if dev.type == "cuda":
+            from k8s_amd.ops import autotune, conv
+
+            print("conv paths: %s" % json.dumps(conv.STATS), file=sys.stderr)
+            print("autotune: %s" % json.dumps(autotune.choices(), sort_keys=True), file=sys.stderr)
     kdist.destroy()
 
 

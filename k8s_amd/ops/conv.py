@@ -11,13 +11,17 @@ Activations NHWC bf16, weights KRSC bf16. Per product:
 
 Shapes outside those rules (the 8-channel stem, stride-2 dgrad) and CPU
 tensors run through ATen's convolution on a channels-last view (MIOpen on
-ROCm) -- see ``coverage()`` for which path each layer takes.
+ROCm). Where both paths can run a shape, ``ops.autotune`` times them once on
+the real tensors (the vendor forward is charged for the extra BatchNorm
+statistics pass it implies) and the faster one is used from then on;
+``STATS`` / ``autotune.choices()`` show which path each layer takes.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn.functional as F
 
+from k8s_amd.ops import autotune
 from k8s_amd.ops._ext import load as _load
 
 STATS = {"hip_fwd": 0, "aten_fwd": 0, "hip_wgrad": 0, "aten_wgrad": 0, "hip_dgrad": 0, "aten_dgrad": 0}
@@ -39,10 +43,31 @@ def fwd_ok(x, w):
     return _hip(x, w) and x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0
 
 
+def _key(op, x, w, stride, padding):
+    return "%s|%s|%s|%d|%d" % (op, "x".join(map(str, x.shape)), "x".join(map(str, w.shape)), stride, padding)
+
+
+def fwd_uses_hip(x, w, stride, padding) -> bool:
+    """Whether the forward of this shape runs on our kernel (tuned against the vendor conv)."""
+    if not fwd_ok(x, w):
+        return False
+    C_ = _load()
+    K = w.shape[0]
+
+    def hip():
+        st = torch.zeros(C_.conv_stat_replicas, 2, K, device=x.device)
+        C_.conv_fwd(x, w, stride, padding, 1, False, None, 0, st)
+
+    def aten():  # + one read of y: the statistics pass BatchNorm then has to run itself
+        _nhwc(F.conv2d(_nchw(x), _nchw(w), None, stride, padding)).view(-1, K).sum(0)
+
+    return autotune.choose(_key("conv_fwd", x, w, stride, padding), [("hip", hip), ("aten", aten)]) == "hip"
+
+
 def conv_fwd(x, w, stride, padding, stats=None):
-    """y = conv(x, w); with ``stats`` (zeroed fp32 [2, K]) the epilogue also accumulates the per-channel
-    sum / sum-of-squares of y for the following BatchNorm (HIP path only; returns whether it did)."""
-    if fwd_ok(x, w):
+    """y = conv(x, w); with ``stats`` (zeroed fp32 [R, 2, K]) the epilogue also accumulates the per-channel
+    sum / sum-of-squares of y for the following BatchNorm (HIP path only)."""
+    if fwd_uses_hip(x, w, stride, padding):
         STATS["hip_fwd"] += 1
         return _load().conv_fwd(x, w, stride, padding, 1, False, None, 0, stats)
     STATS["aten_fwd"] += 1
@@ -56,46 +81,62 @@ def _aten_bwd(gy, x, w, stride, padding, need_dx, need_dw):
     return (_nhwc(dx) if dx is not None else None), (dw.permute(0, 2, 3, 1) if dw is not None else None)
 
 
+def _wgrad_hip(C_, gy, x, out, stride, padding, acc):
+    K, C = out.shape[0], out.shape[-1]
+    R, S = out.shape[1], out.shape[2]
+    if R == 1 and S == 1 and stride == 1 and padding == 0:
+        # 1x1 / stride 1: dW = dY^T . X as a plain tall-K GEMM (both operands read M-major, no im2col)
+        C_.gemm(gy.reshape(-1, K), False, x.reshape(-1, C), False, out.view(K, C), True, None, 0, None, acc, 1.0, 0)
+    else:
+        C_.conv_wgrad(x, gy, out, stride, padding, 1, 0, acc)
+
+
+def _dgrad_hip(C_, gy, w, padding):
+    K, R, S, C = w.shape
+    if R == 1 and S == 1 and padding == 0:
+        N, H, W_, _ = gy.shape
+        return C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, None, False, None, 0, None, False, 1.0,
+                       1).reshape(N, H, W_, C)
+    return C_.conv_fwd(gy, C_.conv_dgrad_wtrans(w), 1, R - 1 - padding, 1, False, None, 0, None)
+
+
 def conv_bwd(gy, x, w, stride, padding, need_dx, p=None):
     """Returns dx (or None); deposits dw into ``p``'s flat gradient slot."""
     K, R, S, C = w.shape
     C_ = _load() if gy.is_cuda else None
     hip = _hip(gy, x, w)
     # ---- weight gradient
+    dw_done = False
     if hip and C % 8 == 0 and K % 8 == 0 and p is not None and p.grad.dtype == torch.float32:
-        STATS["hip_wgrad"] += 1
-        acc = p.written
-        if R == 1 and S == 1 and stride == 1 and padding == 0:
-            # 1x1 / stride 1: dW = dY^T . X as a plain tall-K GEMM (both operands read M-major, no im2col)
-            C_.gemm(gy.reshape(-1, K), False, x.reshape(-1, C), False, p.grad.view(K, C), True, None, 0, None, acc,
-                    1.0, 0)
-        else:
-            C_.conv_wgrad(x, gy, p.grad, stride, padding, 1, 0, acc)
-        if acc:
-            p.store._notify(p)
-        else:
-            p.store.mark_written(p)
-        dw_done = True
-    else:
-        dw_done = False
+        choice = autotune.choose(_key("conv_wgrad", x, w, stride, padding), [
+            ("hip", lambda: _wgrad_hip(C_, gy, x, torch.empty(w.shape, device=w.device, dtype=torch.float32),
+                                       stride, padding, False)),
+            ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, False, True))])
+        if choice == "hip":
+            STATS["hip_wgrad"] += 1
+            acc = p.written
+            _wgrad_hip(C_, gy, x, p.grad.view(w.shape), stride, padding, acc)
+            if acc:
+                p.store._notify(p)
+            else:
+                p.store.mark_written(p)
+            dw_done = True
     # ---- data gradient
     dx = None
     if need_dx:
+        use_hip = False
         if hip and stride == 1 and K % 64 == 0 and C % 8 == 0:
+            use_hip = autotune.choose(_key("conv_dgrad", x, w, stride, padding), [
+                ("hip", lambda: _dgrad_hip(C_, gy, w, padding)),
+                ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, True, False))]) == "hip"
+        if use_hip:
             STATS["hip_dgrad"] += 1
-            if R == 1 and S == 1 and padding == 0:
-                N, H, W_, _ = gy.shape
-                dx = C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, None, False, None, 0, None, False,
-                             1.0, 1).reshape(N, H, W_, C)
-            else:
-                w2 = C_.conv_dgrad_wtrans(w)
-                dx = C_.conv_fwd(gy, w2, 1, R - 1 - padding, 1, False, None, 0, None)
+            dx = _dgrad_hip(C_, gy, w, padding)
         else:
             STATS["aten_dgrad"] += 1
             dx, _ = _aten_bwd(gy, x, w, stride, padding, True, False)
     if not dw_done and p is not None:
         STATS["aten_wgrad"] += 1
         _, dw = _aten_bwd(gy, x, w, stride, padding, False, True)
-        if p is not None:
-            p.store.deposit(p, dw)
+        p.store.deposit(p, dw)
     return dx

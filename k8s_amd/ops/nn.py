@@ -41,7 +41,7 @@ class _Conv2dNHWC(torch.autograd.Function):
         impl = _conv_impl()
         w = p.weight if x.dtype == p.weight.dtype else p.master.to(x.dtype)
         sums = None
-        if with_stats and impl.fwd_ok(x, w):
+        if with_stats and impl.fwd_uses_hip(x, w, stride, padding):
             sums = torch.zeros(_C().conv_stat_replicas, 2, w.shape[0], device=x.device, dtype=torch.float32)
         y = impl.conv_fwd(x, w, stride, padding, sums)
         ctx.save_for_backward(x)

@@ -8,7 +8,7 @@ parallelism and gradient clipping are folded into the kernel's scale
 """
 from __future__ import annotations
 
-from typing import Optional
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -25,17 +25,34 @@ class _FlatOptimizer:
         self.max_grad_norm = max_grad_norm
         self.step_count = 0
 
-    def _clip(self, scale: float) -> Optional[torch.Tensor]:
+    def _ranges(self, ranges: Optional[Sequence[Tuple[int, int]]]) -> List[Tuple[int, int]]:
+        return [(0, self.store.total)] if ranges is None else list(ranges)
+
+    def _views(self, lo: int, hi: int):
+        s = self.store
+        return (s.master[lo:hi], s.grad[lo:hi], None if s.half is None else s.half[lo:hi],
+                s.decay_mask[lo // 64: hi // 64])
+
+    def _clip(self, scale: float, ranges, stats_reduce: Optional[Callable] = None) -> Optional[torch.Tensor]:
+        """Device-side clip factor from the gradient norm over ``ranges``; ``stats_reduce`` (e.g. an
+        all-reduce) combines the [sum of squares, non-finite count] partials of a sharded update."""
         if not self.max_grad_norm:
             return None
         g = self.store.grad
         if g.is_cuda:
             C = _load_ext()
-            stats = C.grad_sumsq(g)
+            stats = None
+            for lo, hi in ranges:
+                st = C.grad_sumsq(g[lo:hi])
+                stats = st if stats is None else stats + st
+            if stats_reduce is not None:
+                stats_reduce(stats)
             # the clip test sees the *scaled* (averaged) gradient norm
             stats[0:1].mul_(scale * scale)
             return C.clip_factor(stats, float(self.max_grad_norm))
-        stats = ref.grad_sumsq(g)
+        stats = sum(ref.grad_sumsq(g[lo:hi]) for lo, hi in ranges)
+        if stats_reduce is not None:
+            stats_reduce(stats)
         norm = float(stats[0].sqrt()) * scale
         f = min(1.0, self.max_grad_norm / (norm + 1e-6)) if bool(stats[1] == 0) else 0.0
         return torch.tensor([f])
@@ -55,17 +72,21 @@ class FusedSGD(_FlatOptimizer):
         self.nesterov = nesterov
         self.mom = torch.zeros_like(store.master)
 
-    def step(self, grad_scale: float = 1.0, lr: Optional[float] = None):
-        s = self.store
+    def step(self, grad_scale: float = 1.0, lr: Optional[float] = None, ranges=None, stats_reduce=None):
+        """Update the flat buffers (or only ``ranges`` of them: the shards this rank owns)."""
         lr = self.lr if lr is None else lr
-        clip = self._clip(grad_scale)
+        ranges = self._ranges(ranges)
+        clip = self._clip(grad_scale, ranges, stats_reduce)
         first = self.step_count == 0
-        if s.master.is_cuda:
-            _load_ext().fused_sgd(s.master, self.mom, s.grad, s.half, s.decay_mask, lr, self.momentum,
-                                  self.weight_decay, grad_scale, clip, self.nesterov, first)
-        else:
-            ref.sgd(s.master, self.mom, s.grad, s.half, s.decay_mask, lr, self.momentum, self.weight_decay,
-                    grad_scale, clip, self.nesterov, first)
+        for lo, hi in ranges:
+            p, g, h, mask = self._views(lo, hi)
+            m = self.mom[lo:hi]
+            if p.is_cuda:
+                _load_ext().fused_sgd(p, m, g, h, mask, lr, self.momentum, self.weight_decay, grad_scale, clip,
+                                      self.nesterov, first)
+            else:
+                ref.sgd(p, m, g, h, mask, lr, self.momentum, self.weight_decay, grad_scale, clip, self.nesterov,
+                        first)
         self.step_count += 1
 
     def state_dict(self):
@@ -86,17 +107,20 @@ class FusedAdam(_FlatOptimizer):
         self.m1 = torch.zeros_like(store.master)
         self.m2 = torch.zeros_like(store.master)
 
-    def step(self, grad_scale: float = 1.0, lr: Optional[float] = None):
-        s = self.store
+    def step(self, grad_scale: float = 1.0, lr: Optional[float] = None, ranges=None, stats_reduce=None):
         lr = self.lr if lr is None else lr
-        clip = self._clip(grad_scale)
+        ranges = self._ranges(ranges)
+        clip = self._clip(grad_scale, ranges, stats_reduce)
         self.step_count += 1
-        if s.master.is_cuda:
-            _load_ext().fused_adam(s.master, self.m1, self.m2, s.grad, s.half, s.decay_mask, lr, self.b1, self.b2,
-                                   self.eps, self.weight_decay, grad_scale, clip, self.step_count, self.adamw)
-        else:
-            ref.adam(s.master, self.m1, self.m2, s.grad, s.half, s.decay_mask, lr, self.b1, self.b2, self.eps,
-                     self.weight_decay, grad_scale, clip, self.step_count, self.adamw)
+        for lo, hi in ranges:
+            p, g, h, mask = self._views(lo, hi)
+            a, b = self.m1[lo:hi], self.m2[lo:hi]
+            if p.is_cuda:
+                _load_ext().fused_adam(p, a, b, g, h, mask, lr, self.b1, self.b2, self.eps, self.weight_decay,
+                                       grad_scale, clip, self.step_count, self.adamw)
+            else:
+                ref.adam(p, a, b, g, h, mask, lr, self.b1, self.b2, self.eps, self.weight_decay, grad_scale, clip,
+                         self.step_count, self.adamw)
 
     def state_dict(self):
         return {"exp_avg": self.m1, "exp_avg_sq": self.m2, "step": self.step_count}
