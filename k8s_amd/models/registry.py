@@ -34,14 +34,15 @@ MODELS = ("resnet50", "resnet_tiny", "bert_base", "bert_tiny", "llama3_8b", "lla
 
 
 def build(name: str, device, batch: int, seq: Optional[int] = None, image: Optional[int] = None,
-          seed: int = 0, grad_dtype=torch.float32, fixed_batch: bool = True) -> Workload:
+          seed: int = 0, grad_dtype=torch.float32, fixed_batch: bool = True, pad_to: int = 64,
+          data_seed: Optional[int] = None) -> Workload:
     """Construct ``name`` on ``device`` with per-rank ``batch``. ``fixed_batch`` reuses one synthetic batch
     (what a throughput benchmark wants); otherwise every step draws a new one."""
     device = torch.device(device)
     dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
     store = ParamStore()
     gen = torch.Generator(device=device)
-    gen.manual_seed(1000 + seed)
+    gen.manual_seed(1000 + (seed if data_seed is None else data_seed))
 
     def cached(make):
         box = {}
@@ -61,7 +62,7 @@ def build(name: str, device, batch: int, seq: Optional[int] = None, image: Optio
         ncls = 1000 if name == "resnet50" else 10
         image = image or (224 if name == "resnet50" else 32)
         model = (resnet50(store, ncls) if name == "resnet50" else resnet_tiny(store, ncls))
-        model = model.finalize(device, grad_dtype=grad_dtype, seed=seed)
+        model = model.finalize(device, grad_dtype=grad_dtype, seed=seed, pad_to=pad_to)
 
         def make():
             x = torch.randn(batch, image, image, 3, device=device, generator=gen).to(dtype)
@@ -76,7 +77,7 @@ def build(name: str, device, batch: int, seq: Optional[int] = None, image: Optio
 
         cfg = M.BERT_BASE if name == "bert_base" else M.BERT_TINY
         seq = seq or (128 if name == "bert_base" else 32)
-        model = M.BertForPreTraining(store, cfg).finalize(device, grad_dtype=grad_dtype, seed=seed)
+        model = M.BertForPreTraining(store, cfg).finalize(device, grad_dtype=grad_dtype, seed=seed, pad_to=pad_to)
 
         def make():
             return M.synthetic_batch(cfg, batch, seq, device, generator=gen)
@@ -89,7 +90,7 @@ def build(name: str, device, batch: int, seq: Optional[int] = None, image: Optio
 
         cfg = {"llama3_8b": M.LLAMA3_8B, "llama_1b": M.LLAMA_1B, "llama_tiny": M.LLAMA_TINY}[name]
         seq = seq or (4096 if name != "llama_tiny" else 64)
-        model = M.LlamaForCausalLM(store, cfg).finalize(device, grad_dtype=grad_dtype, seed=seed)
+        model = M.LlamaForCausalLM(store, cfg).finalize(device, grad_dtype=grad_dtype, seed=seed, pad_to=pad_to)
 
         def make():
             return M.synthetic_batch(cfg, batch, seq, device, generator=gen)

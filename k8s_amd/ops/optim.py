@@ -89,6 +89,9 @@ class FusedSGD(_FlatOptimizer):
                         first)
         self.step_count += 1
 
+    def state_tensors(self):
+        return [self.mom]
+
     def state_dict(self):
         return {"momentum_buffer": self.mom, "step": self.step_count}
 
@@ -121,6 +124,9 @@ class FusedAdam(_FlatOptimizer):
             else:
                 ref.adam(p, a, b, g, h, mask, lr, self.b1, self.b2, self.eps, self.weight_decay, grad_scale, clip,
                          self.step_count, self.adamw)
+
+    def state_tensors(self):
+        return [self.m1, self.m2]
 
     def state_dict(self):
         return {"exp_avg": self.m1, "exp_avg_sq": self.m2, "step": self.step_count}

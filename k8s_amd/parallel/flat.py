@@ -122,13 +122,16 @@ class ParamStore:
         self.by_name[name] = p
         return p
 
-    def finalize(self, device, grad_dtype=torch.float32, seed: int = 0, lowp_dtype=torch.bfloat16):
+    def finalize(self, device, grad_dtype=torch.float32, seed: int = 0, lowp_dtype=torch.bfloat16,
+                 pad_to: int = ALIGN):
+        """Lay the parameters out in the flat buffers. ``pad_to`` rounds the total up (the sharded
+        parameter service needs a multiple of world_size * ALIGN)."""
         device = torch.device(device)
         off = 0
         for p in self.params:
             p.offset = off
             off += _round_up(p.numel)
-        self.total = max(off, ALIGN)
+        self.total = _round_up(max(off, ALIGN), max(pad_to, ALIGN))
         self.master = torch.zeros(self.total, dtype=torch.float32, device=device)
         any_lowp = any(p.lowp for p in self.params)
         self.half = torch.zeros(self.total, dtype=lowp_dtype, device=device) if any_lowp else None

@@ -1,0 +1,125 @@
+"""The TfJob trainer on CPU: TF_CONFIG roles, gloo DP (all-reduce and sharded PS), checkpoint/resume,
+exit-code contract (reference: pkg/trainer/training.go:45-73 retry rules)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from k8s_amd.fakeapi.server import free_port
+from k8s_amd.utils import checkpoint as ckpt
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env(tf_config=None):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = REPO + os.pathsep + env.get("PYTHONPATH", "")
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    env["HIP_VISIBLE_DEVICES"] = ""
+    env["OMP_NUM_THREADS"] = "2"
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "TF_CONFIG"):
+        env.pop(k, None)
+    if tf_config is not None:
+        env["TF_CONFIG"] = json.dumps(tf_config)
+    return env
+
+
+def _trainer(args, tf_config=None):
+    return subprocess.Popen([sys.executable, "-m", "k8s_amd.trainer", "--device", "cpu"] + args,
+                            env=_env(tf_config), stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+
+
+def _events(out):
+    recs = []
+    for line in out.splitlines():
+        if line.startswith("{"):
+            try:
+                recs.append(json.loads(line))
+            except ValueError:
+                pass
+    return recs
+
+
+def test_single_rank_checkpoint_resume(tmp_path):
+    ck, lg = str(tmp_path / "ckpt"), str(tmp_path / "log")
+    p = _trainer(["--model", "resnet_tiny", "--steps", "4", "--ckpt-dir", ck, "--logdir", lg, "--ckpt-every", "2",
+                  "--log-every", "1"])
+    out, _ = p.communicate(timeout=240)
+    assert p.returncode == 0, out
+    ev = _events(out)
+    assert [e["event"] for e in ev][:2] == ["start", "step0"]
+    assert ev[-1]["event"] == "done"
+    latest, allp = ckpt.read_state(ck)
+    assert latest == "model.ckpt-3" and allp == ["model.ckpt-1", "model.ckpt-3"]
+    assert any(f.startswith("events.out.tfevents.") for f in os.listdir(lg))
+    # resume: continues at step 4
+    p = _trainer(["--model", "resnet_tiny", "--steps", "6", "--ckpt-dir", ck, "--log-every", "1"])
+    out, _ = p.communicate(timeout=240)
+    assert p.returncode == 0, out
+    ev = _events(out)
+    restored = [e for e in ev if e["event"] == "restored"]
+    assert restored and restored[0]["step"] == 3
+    assert [e for e in ev if e["event"] == "step0"][0]["step"] == 4
+    step, tensors, meta = ckpt.load(ckpt.latest_checkpoint(ck))
+    assert step == 5 and meta["optim_step"] == 6
+    assert any(k.startswith("buffers/") and k.endswith("running_mean") for k in tensors)
+
+
+def test_retryable_exit_then_resume(tmp_path):
+    ck = str(tmp_path / "ckpt")
+    args = ["--model", "resnet_tiny", "--steps", "4", "--ckpt-dir", ck, "--ckpt-every", "1", "--fail-at-step", "2"]
+    p = _trainer(args)
+    out, _ = p.communicate(timeout=240)
+    assert p.returncode >= 128, out  # retryable per the operator's exit-code contract
+    assert ckpt.read_state(ck)[0] == "model.ckpt-1"
+    p = _trainer(args)  # the restarted replica resumes and finishes
+    out, _ = p.communicate(timeout=240)
+    assert p.returncode == 0, out
+    assert ckpt.read_state(ck)[0] == "model.ckpt-3"
+
+
+def test_bad_model_is_permanent_failure():
+    p = subprocess.run([sys.executable, "-m", "k8s_amd.trainer", "--model", "nope"], env=_env(),
+                       capture_output=True, text=True, timeout=120)
+    assert 0 < p.returncode < 128
+
+
+def _run_job(tmp_path, strategy, with_ps):
+    pm, pw, pp = free_port(), free_port(), free_port()
+    cluster = {"master": ["127.0.0.1:%d" % pm], "worker": ["127.0.0.1:%d" % pw]}
+    if with_ps:
+        cluster["ps"] = ["127.0.0.1:%d" % pp]
+    ck = str(tmp_path / strategy)
+    common = ["--model", "resnet_tiny", "--steps", "3", "--strategy", strategy, "--ckpt-dir", ck, "--log-every", "1",
+              "--optimizer", "adam", "--lr", "0.01"]
+    procs = []
+    if with_ps:
+        procs.append(_trainer(common, {"cluster": cluster, "task": {"type": "ps", "index": 0},
+                                       "environment": "cloud"}))
+    procs.append(_trainer(common, {"cluster": cluster, "task": {"type": "master", "index": 0},
+                                   "environment": "cloud"}))
+    procs.append(_trainer(common, {"cluster": cluster, "task": {"type": "worker", "index": 0},
+                                   "environment": "cloud"}))
+    outs = []
+    for p in procs:
+        out, _ = p.communicate(timeout=300)
+        outs.append(out)
+        assert p.returncode == 0, out
+    _, tensors, meta = ckpt.load(ckpt.latest_checkpoint(ck))
+    assert meta["world"] == 2
+    return tensors, outs
+
+
+def test_two_rank_allreduce_and_sharded_ps_agree(tmp_path):
+    """1 MASTER + 1 WORKER (+ 1 PS task running the parameter server, shut down by the master): the
+    sharded parameter service (reduce-scatter / owner update / all-gather) must produce the same weights
+    and optimizer state as the all-reduce strategy."""
+    a, _ = _run_job(tmp_path, "allreduce", with_ps=False)
+    b, outs = _run_job(tmp_path, "ps", with_ps=True)
+    assert "Started server /job:ps/task:0" in outs[0]
+    for k in a:
+        if k.startswith("params/") or k.startswith("optim/"):
+            torch.testing.assert_close(a[k], b[k], rtol=1e-4, atol=1e-5, msg=k)
