@@ -46,6 +46,21 @@ std::string strip_comment(const std::string& s) {
   return s;
 }
 
+// unclosed '[' / '{' outside quotes (> 0: the flow collection continues on the next line)
+int flow_depth(const std::string& s) {
+  bool sq = false, dq = false;
+  int d = 0;
+  for (size_t i = 0; i < s.size(); ++i) {
+    const char c = s[i];
+    if (dq && c == '\\') { ++i; continue; }
+    if (c == '\'' && !dq) sq = !sq;
+    else if (c == '"' && !sq) dq = !dq;
+    else if (!sq && !dq && (c == '[' || c == '{')) ++d;
+    else if (!sq && !dq && (c == ']' || c == '}')) --d;
+  }
+  return d;
+}
+
 Json scalar(const std::string& raw) {
   std::string s = strip(raw);
   if (s.empty() || s == "~" || s == "null" || s == "Null" || s == "NULL") return Json();
@@ -337,11 +352,14 @@ Json parse_doc(const std::vector<std::string>& raw) {
   for (size_t i = 0; i < raw.size(); ++i) {
     std::string s = strip_comment(raw[i]);
     if (strip(s).empty()) continue;
+    // a flow collection continued over several lines: join until the brackets balance
+    const size_t first = i;
+    while (flow_depth(s) > 0 && i + 1 < raw.size()) s = rstrip(s) + " " + strip(strip_comment(raw[++i]));
     if (s.find('\t') != std::string::npos && s.find_first_not_of(" \t") > s.find('\t'))
       throw std::runtime_error("yaml: tabs are not allowed for indentation");
     int ind = 0;
     while (ind < (int)s.size() && s[ind] == ' ') ++ind;
-    lines.push_back({ind, rstrip(s.substr(ind)), (int)i});
+    lines.push_back({ind, rstrip(s.substr(ind)), (int)first});
   }
   // block scalars need raw (comment-preserving) text; Parser reads raw_ for them
   Parser p(std::move(lines), raw);

@@ -49,6 +49,9 @@ DEFAULT_ENTRYPOINTS = [
 ]
 
 
+LOG_ANNOTATION = "k8s-amd.io/log-path"
+
+
 class _Container:
     def __init__(self, pod_name, proc, log_path):
         self.pod = pod_name
@@ -314,6 +317,9 @@ class LocalKubelet:
         code, pod = self.api.request("GET", self._path(ns, "pods", pod_name))
         if code != 200:
             return
+        c = self.running.get(pod_name)
+        if c is not None:  # where `tfjob logs` finds the container output (the local stand-in for /log)
+            pod["metadata"].setdefault("annotations", {})[LOG_ANNOTATION] = c.log_path
         st = pod.setdefault("status", {})
         st["phase"] = phase
         st.setdefault("startTime", now_rfc3339())

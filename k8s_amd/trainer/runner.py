@@ -117,10 +117,33 @@ def _shutdown_ps(tf_config: Optional[str]):
 
     cluster = json.loads(tf_config).get("cluster", {})
     for addr in cluster.get("ps", []):
-        try:
-            call(resolve(addr), {"op": "shutdown"}, timeout=5)
-        except OSError:
-            pass
+        for _ in range(20):
+            try:
+                call(resolve(addr), {"op": "shutdown"}, timeout=5)
+                break
+            except OSError:
+                time.sleep(0.5)
+
+
+def _wait_for_ps(tf_config: Optional[str], timeout: float = 120.0):
+    """Liveness rendezvous with the PS tasks (the reference's workers block until the PS gRPC servers
+    answer); raises RetryableError when they never come up."""
+    if not tf_config:
+        return
+    from k8s_amd.parallel.dist import resolve
+    from k8s_amd.ps_server.grpc_tensorflow_server import call
+
+    end = time.time() + timeout
+    for addr in json.loads(tf_config).get("cluster", {}).get("ps", []):
+        while True:
+            try:
+                if call(resolve(addr), {"op": "ping"}, timeout=5).get("ok"):
+                    break
+            except OSError:
+                pass
+            if time.time() > end:
+                raise RetryableError("PS task %s unreachable" % addr)
+            time.sleep(0.2)
 
 
 def _run_ps(info, tf_config: str) -> int:
@@ -155,6 +178,8 @@ def train(a) -> int:
     chief = rank == 0
     dev = torch.device("cuda", info.local_rank) if use_cuda else torch.device("cpu")
     torch.manual_seed(a.seed + rank)
+    if chief:
+        _wait_for_ps(tf_config)
     metrics = _Metrics(a.logdir, chief)
     metrics.event(event="start", rank=rank, world=world, role=info.role, model=a.model, strategy=a.strategy,
                   device=str(dev), start_time=t_start)
