@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""BASELINE.json's second metric: TfJob create -> step 0 latency.
+
+Brings up the one-box cluster (fake API server + local kubelet + the C++
+``tf_operator``), submits a single-MASTER ResNet-50 TfJob asking for
+``amd.com/gpu: 1`` (CPU fallback: ``resnet_tiny`` without a GPU), and
+measures from just before the create POST to the trainer's ``step0`` record
+(first optimizer step finished, loss synced to host). Also reports the split:
+create -> trainer process start (operator reconcile + kubelet) and process
+start -> step 0 (imports, model build on the GPU, first step incl. conv
+autotuning), and the job's total time to ``Succeeded``.
+
+    python benchmarks/job_latency.py [--runs 3] [--steps 5]
+
+Prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import tempfile
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from k8s_amd.fakeapi.cluster import LocalCluster  # noqa: E402
+
+
+def _manifest(name, model, steps, logdir, gpu):
+    c = {"image": "k8s-amd/trainer:rocm7-gfx950", "name": "tensorflow",
+         "args": ["--model", model, "--steps", str(steps), "--log-every", "1", "--logdir", logdir]}
+    if gpu:
+        c["resources"] = {"limits": {"amd.com/gpu": 1}}
+    else:
+        c["args"] += ["--device", "cpu"]
+    return {"apiVersion": "tensorflow.org/v1alpha1", "kind": "TfJob", "metadata": {"name": name},
+            "spec": {"replicaSpecs": [{"tfReplicaType": "MASTER", "replicas": 1,
+                                       "template": {"spec": {"containers": [c], "restartPolicy": "OnFailure"}}}]}}
+
+
+def _events(path):
+    out = {}
+    if os.path.exists(path):
+        for line in open(path):
+            try:
+                r = json.loads(line)
+            except ValueError:
+                continue
+            out.setdefault(r.get("event"), r)
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--runs", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--model", default=None)
+    ap.add_argument("--timeout", type=float, default=600)
+    a = ap.parse_args(argv)
+    try:
+        import torch
+
+        gpu = torch.cuda.device_count() > 0  # does not initialise HIP in this process
+    except ImportError:
+        gpu = False
+    model = a.model or ("resnet50" if gpu else "resnet_tiny")
+    work = tempfile.mkdtemp(prefix="k8s_amd_latency_")
+    results = []
+    with LocalCluster(gpus=[0] if gpu else []) as c:
+        for i in range(a.runs):
+            name = "latency-%d" % i
+            logdir = os.path.join(work, name)
+            t0 = time.time()
+            c.create(_manifest(name, model, a.steps, logdir, gpu))
+            job = c.wait(name, timeout=a.timeout)
+            t_done = time.time()
+            ev = _events(os.path.join(logdir, "metrics.jsonl"))
+            state = job.get("status", {}).get("state")
+            if state != "Succeeded" or "step0" not in ev:
+                print(json.dumps({"error": "job %s ended %s" % (name, state), "events": list(ev)}), flush=True)
+                return 1
+            start = ev["start"]["start_time"]
+            results.append({"create_to_step0_s": ev["step0"]["time"] - t0, "create_to_trainer_start_s": start - t0,
+                            "trainer_start_to_step0_s": ev["step0"]["time"] - start,
+                            "create_to_succeeded_s": t_done - t0})
+            c.delete(name)
+            print(json.dumps({"run": i, **{k: round(v, 3) for k, v in results[-1].items()}}), file=sys.stderr,
+                  flush=True)
+    med = {k: round(statistics.median(r[k] for r in results), 3) for k in results[0]}
+    print(json.dumps({"metric": "TfJob create -> step0 latency", "value": med["create_to_step0_s"], "unit": "s",
+                      "higher_is_better": False, "runs": a.runs, "model": model, "gpu": gpu, "median": med,
+                      "all": results}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

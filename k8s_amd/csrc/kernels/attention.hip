@@ -1,0 +1,491 @@
+// K5: flash attention forward / backward for gfx950 (bf16 in, fp32 softmax/accumulate).
+//
+// Layout: token-major q [B, Sq, Hq, D], k/v [B, Sk, Hkv, D] with arbitrary batch / token / head
+// strides (q, k, v are usually column slices of one fused QKV GEMM output -- no copies), D in
+// {64, 128}, GQA (Hq % Hkv == 0), causal (bottom-right aligned) and per-batch key lengths.
+//
+// Forward (one block = 4 waves = 128 queries, KV tiles of 64 keys, double-buffered in LDS via
+// global_load_lds):
+//   S^T = K . Q^T    MFMA(first = K fragment, second = Q fragment held in VGPRs): each lane ends
+//                    with ONE query (lane & 15) and 4 keys per 16-key subtile.
+//   online softmax   per query column: row max = in-lane max + 2 xor-shuffles; the running sum
+//                    stays lane-partial until the end (exp2 domain, scale * log2(e) folded in).
+//   O^T += V^T . P^T P^T is consumed straight from the S^T accumulators: the MFMA's k order is
+//                    permuted (keys 4g..4g+3 | 16+4g..16+4g+3 for lane group g) and V^T is read
+//                    with the SAME permutation through ds_read_b64_tr_b16 -- no register shuffle,
+//                    no LDS round trip for P.
+//   writes O (bf16) and lse2 = m + log2(l) (fp32, [B, Hq, Sq]) for the backward.
+//
+// Backward (FA2 order, one block = 64 keys of one KV head, looping over every query tile of
+// every query head of its GQA group, so dK/dV accumulate in VGPRs without atomics):
+//   S = Q K^T, dP = dO V^T       (K, V fragments of the wave's 16 keys stay in VGPRs)
+//   P = exp2(S*c - lse2), dS = P (dP - delta)
+//   dV^T += dO^T P, dK^T += Q^T dS  (P / dS consumed in place through the permuted-k trick,
+//                                   dO^T / Q^T read transposed from LDS)
+//   dQ += dS K                    (dS through LDS, fp32 atomics into a [B,Sq,Hq,D] accumulator)
+//   delta = rowsum(dO * O) is a separate tiny kernel; dQ is converted to bf16 at the end.
+#include <algorithm>
+
+#include "common.h"
+#include "launchers.h"
+#include "mfma.h"
+
+namespace k8s_amd {
+
+constexpr int FA_BM = 128, FA_BN = 64, FA_THREADS = 256;
+constexpr int FB_BN = 64, FB_BM = 64;
+
+template <int D>
+__device__ __forceinline__ int v_swz(int r) {
+  return D == 128 ? mn_swz(r) : (mn_swz(r) & 7);
+}
+
+// XCD-aware bijective remap of a linear block id (blocks sharing K/V land on the same XCD / L2)
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// K-major-halves tile: [rows][D] stored as D/64 halves of [rows][64] with 128-B swizzled rows.
+// Byte address of (row, column d .. d+3) for the transposed reads.
+__device__ __forceinline__ const char* kh_addr(const char* tile, int rows, int row, int d) {
+  const int half = d >> 6, c = (d & 63) >> 3;
+  return tile + half * rows * 128 + row * 128 + ((c ^ ((row >> 1) & 7)) << 4) + (d & 7) * 2;
+}
+
+// global source of unit s (16 B) of a K-major-halves tile with `rows` rows starting at row0
+__device__ __forceinline__ const uint16_t* kh_src(const uint16_t* base, long rstride, int rows, int row0, int nrows,
+                                                  int s) {
+  const int per_half = rows * 8;
+  const int half = s / per_half, rem = s - half * per_half;
+  const int row = rem >> 3, cp = rem & 7;
+  const int c = cp ^ ((row >> 1) & 7);
+  int gr = row0 + row;
+  gr = gr < nrows ? gr : nrows - 1;
+  return base + (long)gr * rstride + half * 64 + c * 8;
+}
+
+// =============================================================================== forward
+template <int D>
+__global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a) {
+  constexpr int KT = FA_BN * D * 2;  // bytes of one K (or V) tile
+  constexpr int UPR = D / 8;         // 16-B units per V row
+  constexpr int ND = D / 16, NK = D / 32;
+  __shared__ __attribute__((aligned(1024))) char smem[4 * KT];  // [buf][K | V]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+
+  const int nqb = (a.Sq + FA_BM - 1) / FA_BM;
+  const int nwg = nqb * a.Hq * a.B;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int qb = nqb - 1 - (wg % nqb);  // heavier (causal) query blocks first
+  const int h = (wg / nqb) % a.Hq;
+  const int b = wg / (nqb * a.Hq);
+  const int hk = h / (a.Hq / a.Hkv);
+  const int q0 = qb * FA_BM, q0w = q0 + wid * 32;
+  const int off = a.Sk - a.Sq;
+  int kv_end = a.Sk;
+  if (a.kv_lens) kv_end = min(kv_end, a.kv_lens[b]);
+  int kv_stop = kv_end;
+  if (a.causal) kv_stop = min(kv_stop, q0 + FA_BM + off);
+  const int ntiles = kv_stop > 0 ? (kv_stop + FA_BN - 1) / FA_BN : 0;
+
+  const uint16_t* qp = a.q + (long)b * a.sqb + (long)h * a.sqh;
+  const uint16_t* kp = a.k + (long)b * a.skb + (long)hk * a.skh;
+  const uint16_t* vp = a.v + (long)b * a.svb + (long)hk * a.svh;
+
+  // Q fragments (operand "B" of S^T = K Q^T): query q0w + 16*qs + li, d = 32*kk + 8*g
+  mfma_bf16x8 qf[2][NK];
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    const int qi = q0w + qs * 16 + li;
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      bf16x8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (qi < a.Sq) v = *reinterpret_cast<const bf16x8_t*>(qp + (long)qi * a.sqs + kk * 32 + g * 8);
+      qf[qs][kk] = __builtin_bit_cast(mfma_bf16x8, v);
+    }
+  }
+
+  f32x4_t oacc[ND][2];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) oacc[i][0] = oacc[i][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-1e30f, -1e30f}, l[2] = {0.f, 0.f};
+
+  auto stage = [&](int buf, int key0) {
+    char* tk = smem + buf * 2 * KT;
+    char* tv = tk + KT;
+#pragma unroll
+    for (int rd = 0; rd < KT / (16 * FA_THREADS); ++rd) {
+      const int s = rd * FA_THREADS + tid;
+      const size_t wb = (size_t)(rd * FA_THREADS + wid_u * 64) * 16;  // this wave's 1 KB of the round
+      glds16(kh_src(kp, a.sks, FA_BN, key0, a.Sk, s), tk + wb);
+      const int krow = s / UPR, up = s - krow * UPR;
+      const int u = up ^ v_swz<D>(krow);
+      int gr = key0 + krow;
+      gr = gr < a.Sk ? gr : a.Sk - 1;
+      glds16(vp + (long)gr * a.svs + u * 8, tv + wb);
+    }
+  };
+
+  if (ntiles > 0) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1, key0 = t * FA_BN;
+    if (t + 1 < ntiles) stage(cur ^ 1, key0 + FA_BN);
+    const char* tk = smem + cur * 2 * KT;
+    const char* tv = tk + KT;
+    const bool skip = a.causal && key0 > q0w + 31 + off;  // whole tile masked for this wave
+    if (!skip) {
+      // ---- S^T = K Q^T
+      f32x4_t s[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s[i][0] = s[i][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const mfma_bf16x8 kf = frag_kmajor(tk + (kk >> 1) * (FA_BN * 128), i * 16, kk & 1, lane);
+          s[i][0] = mfma16(kf, qf[0][kk], s[i][0]);
+          s[i][1] = mfma16(kf, qf[1][kk], s[i][1]);
+        }
+      }
+      // ---- online softmax (per query column = lane & 15)
+      const bool need_mask = (key0 + FA_BN > kv_end) || (a.causal && key0 + FA_BN - 1 > q0w + off);
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        const int qi = q0w + qs * 16 + li;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float x = s[i][qs][r] * a.scale_log2;
+            if (need_mask) {
+              const int key = key0 + i * 16 + g * 4 + r;
+              if (key >= kv_end || (a.causal && key > qi + off)) x = -INFINITY;
+            }
+            s[i][qs][r] = x;
+            mx = fmaxf(mx, x);
+          }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mn = fmaxf(m[qs], mx);
+        const float alpha = exp2f(m[qs] - mn);
+        float rs = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float p = exp2f(s[i][qs][r] - mn);
+            s[i][qs][r] = p;
+            rs += p;
+          }
+        l[qs] = l[qs] * alpha + rs;
+        m[qs] = mn;
+#pragma unroll
+        for (int d = 0; d < ND; ++d)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) oacc[d][qs][r] *= alpha;
+      }
+      // ---- O^T += V^T P^T (k = keys in the permuted order of the S^T accumulators)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        mfma_bf16x8 pf[2];
+#pragma unroll
+        for (int qs = 0; qs < 2; ++qs) {
+          const float lo[4] = {s[2 * s2][qs][0], s[2 * s2][qs][1], s[2 * s2][qs][2], s[2 * s2][qs][3]};
+          const float hi[4] = {s[2 * s2 + 1][qs][0], s[2 * s2 + 1][qs][1], s[2 * s2 + 1][qs][2], s[2 * s2 + 1][qs][3]};
+          pf[qs] = pack8(lo, hi);
+        }
+        const int q_ = li >> 2, p = li & 3;
+        const int r0 = 32 * s2 + 4 * g + q_, r1 = r0 + 16;
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+          const int u = 2 * d + (p >> 1);
+          const char* a0 = tv + r0 * (2 * D) + ((u ^ v_swz<D>(r0)) << 4) + (p & 1) * 8;
+          const char* a1 = tv + r1 * (2 * D) + ((u ^ v_swz<D>(r1)) << 4) + (p & 1) * 8;
+          const mfma_bf16x8 vf = join8(tr16(a0), tr16(a1));
+          oacc[d][0] = mfma16(vf, pf[0], oacc[d][0]);
+          oacc[d][1] = mfma16(vf, pf[1], oacc[d][1]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: O = O^T / l, lse2 = m + log2(l)
+  uint16_t* op = a.o + (long)b * a.sob + (long)h * a.soh;
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    float lt = l[qs];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const int qi = q0w + qs * 16 + li;
+    if (qi >= a.Sq) continue;
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      bf16x4_t o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(oacc[d][qs][r] * inv);
+      *reinterpret_cast<bf16x4_t*>(op + (long)qi * a.sos + d * 16 + g * 4) = o;
+    }
+    if (g == 0) a.lse[((long)b * a.Hq + h) * a.Sq + qi] = lt > 0.f ? m[qs] + log2f(lt) : INFINITY;
+  }
+}
+
+// =============================================================================== backward
+// delta[b, h, q] = sum_d dO * O  (16 lanes per row, 8 elements per lane for D = 128)
+template <int D>
+__global__ void __launch_bounds__(256) flash_delta_kernel(const uint16_t* o, long sob, long sos, long soh,
+                                                         const uint16_t* dO, long sdb, long sds, long sdh,
+                                                         float* delta, int B, int Sq, int Hq) {
+  constexpr int LPR = D / 8;  // lanes per row
+  const long row = ((long)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+  const int part = threadIdx.x % LPR;
+  const long R = (long)B * Sq * Hq;
+  float acc = 0.f;
+  int b = 0, q = 0, h = 0;
+  if (row < R) {
+    b = (int)(row / ((long)Sq * Hq));
+    const int rem = (int)(row - (long)b * Sq * Hq);
+    q = rem / Hq;
+    h = rem - q * Hq;
+    float x[8], y[8];
+    load8(o + b * sob + q * sos + h * soh + part * 8, x);
+    load8(dO + b * sdb + q * sds + h * sdh + part * 8, y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
+  }
+#pragma unroll
+  for (int w = LPR / 2; w > 0; w >>= 1) acc += __shfl_xor(acc, w, 64);
+  if (row < R && part == 0) delta[((long)b * Hq + h) * Sq + q] = acc;
+}
+
+template <int D>
+__global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_kernel(AttnBwdArgs a) {
+  constexpr int ND = D / 16, NK = D / 32;
+  constexpr int TQ = FB_BM * D * 2;  // Q / dO tile bytes
+  constexpr int TK = FB_BN * D * 2;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * TQ + TK + FB_BM * FB_BN * 2];
+  char* tq = smem;
+  char* tdo = smem + TQ;
+  char* tk = smem + 2 * TQ;
+  char* tds = tk + TK;  // dS [64 q][64 keys] bf16, K-major swizzled (128-B rows)
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+
+  const int nkb = (a.Sk + FB_BN - 1) / FB_BN;
+  const int nwg = nkb * a.Hkv * a.B;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int kb = wg % nkb;
+  const int hk = (wg / nkb) % a.Hkv;
+  const int b = wg / (nkb * a.Hkv);
+  const int rep = a.Hq / a.Hkv;
+  const int k0 = kb * FB_BN, kw = k0 + wid * 16;  // this wave's 16 keys
+  const int off = a.Sk - a.Sq;
+  int kv_end = a.Sk;
+  if (a.kv_lens) kv_end = min(kv_end, a.kv_lens[b]);
+
+  const uint16_t* kp = a.k + (long)b * a.skb + (long)hk * a.skh;
+  const uint16_t* vp = a.v + (long)b * a.svb + (long)hk * a.svh;
+
+  f32x4_t dka[ND], dva[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) dka[i] = dva[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (k0 < kv_end) {
+    // K / V fragments of the wave's keys (second operand of S = Q K^T and dP = dO V^T)
+    mfma_bf16x8 kf[NK], vf[NK];
+    {
+      const int key = kw + li;
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        bf16x8_t x = {0, 0, 0, 0, 0, 0, 0, 0}, y = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (key < a.Sk) {
+          x = *reinterpret_cast<const bf16x8_t*>(kp + (long)key * a.sks + kk * 32 + g * 8);
+          y = *reinterpret_cast<const bf16x8_t*>(vp + (long)key * a.svs + kk * 32 + g * 8);
+        }
+        kf[kk] = __builtin_bit_cast(mfma_bf16x8, x);
+        vf[kk] = __builtin_bit_cast(mfma_bf16x8, y);
+      }
+    }
+    // K tile in LDS for dQ = dS K
+#pragma unroll
+    for (int rd = 0; rd < TK / (16 * FA_THREADS); ++rd) {
+      const int s = rd * FA_THREADS + tid;
+      glds16(kh_src(kp, a.sks, FB_BN, k0, a.Sk, s), tk + (size_t)(rd * FA_THREADS + wid_u * 64) * 16);
+    }
+    const int qt0 = a.causal ? max(0, k0 - off) / FB_BM : 0;
+    const int nqt = (a.Sq + FB_BM - 1) / FB_BM;
+    for (int hr = 0; hr < rep; ++hr) {
+      const int h = hk * rep + hr;
+      const uint16_t* qp = a.q + (long)b * a.sqb + (long)h * a.sqh;
+      const uint16_t* dop = a.dO + (long)b * a.sdb + (long)h * a.sdh;
+      const float* lse = a.lse + ((long)b * a.Hq + h) * a.Sq;
+      const float* dlt = a.delta + ((long)b * a.Hq + h) * a.Sq;
+      float* dq = a.dq + (long)b * a.Sq * a.Hq * D + (long)h * D;
+      for (int qt = qt0; qt < nqt; ++qt) {
+        const int q0 = qt * FB_BM;
+#pragma unroll
+        for (int rd = 0; rd < TQ / (16 * FA_THREADS); ++rd) {
+          const int s = rd * FA_THREADS + tid;
+          const size_t wb = (size_t)(rd * FA_THREADS + wid_u * 64) * 16;
+          glds16(kh_src(qp, a.sqs, FB_BM, q0, a.Sq, s), tq + wb);
+          glds16(kh_src(dop, a.sds, FB_BM, q0, a.Sq, s), tdo + wb);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        // ---- S = Q K^T, dP = dO V^T  (lane: key = kw + li, q = q0 + 16*qs + 4*g + r)
+        f32x4_t sv[4], dp[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sv[i] = dp[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+#pragma unroll
+          for (int qs = 0; qs < 4; ++qs) {
+            const mfma_bf16x8 qa = frag_kmajor(tq + (kk >> 1) * (FB_BM * 128), qs * 16, kk & 1, lane);
+            const mfma_bf16x8 da = frag_kmajor(tdo + (kk >> 1) * (FB_BM * 128), qs * 16, kk & 1, lane);
+            sv[qs] = mfma16(qa, kf[kk], sv[qs]);
+            dp[qs] = mfma16(da, vf[kk], dp[qs]);
+          }
+        }
+        // ---- P, dS
+        const int key = kw + li;
+#pragma unroll
+        for (int qs = 0; qs < 4; ++qs)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int qi = q0 + qs * 16 + g * 4 + r;
+            float p = 0.f, ds = 0.f;
+            if (qi < a.Sq && key < kv_end && !(a.causal && key > qi + off)) {
+              p = exp2f(sv[qs][r] * a.scale_log2 - lse[qi]);
+              ds = p * (dp[qs][r] - dlt[qi]);
+            }
+            sv[qs][r] = p;
+            dp[qs][r] = ds;
+          }
+        // ---- dV^T += dO^T P, dK^T += Q^T dS   (k = queries, permuted order)
+        {
+          const int q_ = li >> 2, pp = li & 3;
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const float p0[4] = {sv[2 * s2][0], sv[2 * s2][1], sv[2 * s2][2], sv[2 * s2][3]};
+            const float p1[4] = {sv[2 * s2 + 1][0], sv[2 * s2 + 1][1], sv[2 * s2 + 1][2], sv[2 * s2 + 1][3]};
+            const float d0[4] = {dp[2 * s2][0], dp[2 * s2][1], dp[2 * s2][2], dp[2 * s2][3]};
+            const float d1[4] = {dp[2 * s2 + 1][0], dp[2 * s2 + 1][1], dp[2 * s2 + 1][2], dp[2 * s2 + 1][3]};
+            const mfma_bf16x8 pf = pack8(p0, p1), dsf = pack8(d0, d1);
+            const int r0 = 32 * s2 + 4 * g + q_, r1 = r0 + 16;
+#pragma unroll
+            for (int d = 0; d < ND; ++d) {
+              const int dc = d * 16 + pp * 4;
+              const mfma_bf16x8 dot = join8(tr16(kh_addr(tdo, FB_BM, r0, dc)), tr16(kh_addr(tdo, FB_BM, r1, dc)));
+              const mfma_bf16x8 qtf = join8(tr16(kh_addr(tq, FB_BM, r0, dc)), tr16(kh_addr(tq, FB_BM, r1, dc)));
+              dva[d] = mfma16(dot, pf, dva[d]);
+              dka[d] = mfma16(qtf, dsf, dka[d]);
+            }
+          }
+        }
+        // ---- dS -> LDS as [q][key] (K-major, 128-B swizzled rows)
+#pragma unroll
+        for (int qs = 0; qs < 4; ++qs)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = qs * 16 + g * 4 + r, col = wid * 16 + li;
+            const int c = col >> 3;
+            *reinterpret_cast<uint16_t*>(tds + row * 128 + ((c ^ ((row >> 1) & 7)) << 4) + (col & 7) * 2) =
+                f2bf(dp[qs][r]);
+          }
+        __syncthreads();
+        // ---- dQ^T[d][q] += K^T dS^T  (wave `wid` takes query subtile wid)
+        {
+          const int q_ = li >> 2, pp = li & 3;
+          f32x4_t acc[ND];
+#pragma unroll
+          for (int d = 0; d < ND; ++d) acc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const mfma_bf16x8 dsq = frag_kmajor(tds, wid * 16, s2, lane);
+            const int r0 = 32 * s2 + 8 * g + q_, r1 = r0 + 4;
+#pragma unroll
+            for (int d = 0; d < ND; ++d) {
+              const int dc = d * 16 + pp * 4;
+              const mfma_bf16x8 kt = join8(tr16(kh_addr(tk, FB_BN, r0, dc)), tr16(kh_addr(tk, FB_BN, r1, dc)));
+              acc[d] = mfma16(kt, dsq, acc[d]);
+            }
+          }
+          const int qi = q0 + wid * 16 + li;
+          if (qi < a.Sq) {
+            float* dqr = dq + (long)qi * a.Hq * D;
+#pragma unroll
+            for (int d = 0; d < ND; ++d)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) atomicAdd(dqr + d * 16 + g * 4 + r, acc[d][r] * a.scale);
+          }
+        }
+        __syncthreads();  // tq / tdo / tds are rewritten by the next tile
+      }
+    }
+  }
+  // ---- dK = scale * dK^T^T, dV (bf16, [B, Sk, Hkv, D])
+  const int key = kw + li;
+  if (key < a.Sk) {
+    uint16_t* dkp = a.dk + (((long)b * a.Sk + key) * a.Hkv + hk) * D;
+    uint16_t* dvp = a.dv + (((long)b * a.Sk + key) * a.Hkv + hk) * D;
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      bf16x4_t x, y;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        x[r] = (short)f2bf(dka[d][r] * a.scale);
+        y[r] = (short)f2bf(dva[d][r]);
+      }
+      *reinterpret_cast<bf16x4_t*>(dkp + d * 16 + g * 4) = x;
+      *reinterpret_cast<bf16x4_t*>(dvp + d * 16 + g * 4) = y;
+    }
+  }
+}
+
+__global__ void f32_to_bf16_kernel(const float* x, uint16_t* y, long n8) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const float4 u = reinterpret_cast<const float4*>(x)[2 * i];
+    const float4 v = reinterpret_cast<const float4*>(x)[2 * i + 1];
+    const float o[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+    store8(y + i * 8, o);
+  }
+}
+
+// =============================================================================== launchers
+void launch_flash_fwd(const AttnFwdArgs& a, int D, hipStream_t st) {
+  const int nqb = (a.Sq + FA_BM - 1) / FA_BM;
+  const dim3 grid(nqb * a.Hq * a.B);
+  if (D == 128) hipLaunchKernelGGL(flash_fwd_kernel<128>, grid, dim3(FA_THREADS), 0, st, a);
+  else hipLaunchKernelGGL(flash_fwd_kernel<64>, grid, dim3(FA_THREADS), 0, st, a);
+}
+
+void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, long sos, long soh, uint16_t* dq_out,
+                      hipStream_t st) {
+  const long R = (long)a.B * a.Sq * a.Hq;
+  const int lpr = D / 8;
+  const dim3 dgrid((unsigned)((R * lpr + 255) / 256));
+  if (D == 128)
+    hipLaunchKernelGGL(flash_delta_kernel<128>, dgrid, dim3(256), 0, st, o, sob, sos, soh, a.dO, a.sdb, a.sds, a.sdh,
+                       a.delta, a.B, a.Sq, a.Hq);
+  else
+    hipLaunchKernelGGL(flash_delta_kernel<64>, dgrid, dim3(256), 0, st, o, sob, sos, soh, a.dO, a.sdb, a.sds, a.sdh,
+                       a.delta, a.B, a.Sq, a.Hq);
+  const int nkb = (a.Sk + FB_BN - 1) / FB_BN;
+  const dim3 grid(nkb * a.Hkv * a.B);
+  if (D == 128) hipLaunchKernelGGL(flash_bwd_kernel<128>, grid, dim3(FA_THREADS), 0, st, a);
+  else hipLaunchKernelGGL(flash_bwd_kernel<64>, grid, dim3(FA_THREADS), 0, st, a);
+  const long n8 = R * D / 8;
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)std::min<long>((n8 + 255) / 256, 4096L)), dim3(256), 0, st, a.dq,
+                     dq_out, n8);
+}
+
+}  // namespace k8s_amd

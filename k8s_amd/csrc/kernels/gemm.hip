@@ -28,13 +28,9 @@
 //    fp32 atomics (for the tall-K weight gradients).
 #include "common.h"
 #include "launchers.h"
+#include "mfma.h"
 
 namespace k8s_amd {
-
-typedef __attribute__((ext_vector_type(8))) __bf16 mfma_bf16x8;
-typedef __attribute__((ext_vector_type(4))) short short4_t;
-typedef __attribute__((address_space(3))) void lds_void;
-typedef __attribute__((address_space(3))) short4_t lds_short4;
 
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int GEMM_THREADS = 256;
@@ -42,10 +38,6 @@ constexpr int TILE_BYTES = BM * BK * 2;  // 16 KB per operand tile
 
 // 16-byte zero line for out-of-image implicit-GEMM loads
 __device__ __attribute__((aligned(64))) uint16_t g_zero_page[64];
-
-__device__ __forceinline__ void glds16(const void* src, void* lds_base) {
-  __builtin_amdgcn_global_load_lds(src, (lds_void*)lds_base, 16, 0, 0);
-}
 
 // Division by a runtime-invariant divisor as multiply-high + shift (valid for 0 <= n < 2^31).
 struct FastDiv {
@@ -60,8 +52,6 @@ static inline FastDiv make_fastdiv(int d) {
   f.m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << f.s) - f.d)) / f.d + 1);
   return f;
 }
-
-__device__ __forceinline__ int mn_swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
 
 // ----------------------------------------------------------------------------- operand sources
 // stage(): called for round 0..3, writes slot s = round*256 + tid of a 16 KB tile.
@@ -159,13 +149,6 @@ struct MNMajorK {
 };
 
 // ----------------------------------------------------------------------------- fragment reads
-__device__ __forceinline__ mfma_bf16x8 frag_kmajor(const char* tile, int rb, int kk, int lane) {
-  const int row = rb + (lane & 15);
-  const int c = kk * 4 + (lane >> 4);
-  const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(tile + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
-  return __builtin_bit_cast(mfma_bf16x8, v);
-}
-
 __device__ __forceinline__ mfma_bf16x8 frag_mnmajor(const char* tile, int cb, int kk, int lane) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
   const int u = (cb >> 3) + (p >> 1);

@@ -69,4 +69,29 @@ void launch_relu_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n
 int colsum_workspace_floats(long R, int C);
 void launch_colsum(const uint16_t* x, long R, int C, float* work, float* out, bool accumulate, hipStream_t st);
 
+// ---- K5 flash attention (attention.hip). q [B,Sq,Hq,D], k/v [B,Sk,Hkv,D] (strided, last dim contiguous)
+struct AttnFwdArgs {
+  const uint16_t *q, *k, *v;
+  uint16_t* o;
+  float* lse;          // [B, Hq, Sq]: m + log2(l) in the exp2 domain (scores scaled by scale*log2(e))
+  const int* kv_lens;  // [B] or null
+  long sqb, sqs, sqh, skb, sks, skh, svb, svs, svh, sob, sos, soh;
+  int B, Sq, Sk, Hq, Hkv, causal;
+  float scale_log2;
+};
+struct AttnBwdArgs {
+  const uint16_t *q, *k, *v, *dO;
+  const float* lse;
+  float* delta;  // [B, Hq, Sq] scratch
+  float* dq;     // [B, Sq, Hq, D] fp32 accumulator (zeroed)
+  uint16_t *dk, *dv;  // [B, Sk, Hkv, D]
+  const int* kv_lens;
+  long sqb, sqs, sqh, skb, sks, skh, svb, svs, svh, sdb, sds, sdh;
+  int B, Sq, Sk, Hq, Hkv, causal;
+  float scale_log2, scale;
+};
+void launch_flash_fwd(const AttnFwdArgs& a, int D, hipStream_t st);
+void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, long sos, long soh, uint16_t* dq_out,
+                      hipStream_t st);
+
 }  // namespace k8s_amd

@@ -364,6 +364,76 @@ Tensor colsum(Tensor x) {
   return out;
 }
 
+// ------------------------------------------------------------------ flash attention (K5)
+void check_attn_operand(const Tensor& t, const char* name, long D) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  check_dtype(t, at::kBFloat16, name);
+  TORCH_CHECK(t.dim() == 4, name, " must be [B, S, H, D]");
+  TORCH_CHECK(t.size(3) == D && t.stride(3) == 1, name, " must have a contiguous head dim of ", D);
+  for (int i = 0; i < 3; ++i) TORCH_CHECK(t.stride(i) % 8 == 0, name, " strides must be multiples of 8 elements");
+  check_aligned(t, name);
+}
+
+const int* kv_lens_ptr(const c10::optional<Tensor>& kv_lens, long B) {
+  if (!kv_lens) return nullptr;
+  TORCH_CHECK(kv_lens->is_cuda() && kv_lens->scalar_type() == at::kInt && kv_lens->is_contiguous() &&
+                  kv_lens->numel() == B, "kv_lens must be an int32 GPU tensor of length B");
+  return kv_lens->data_ptr<int>();
+}
+
+std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, bool causal, c10::optional<Tensor> kv_lens,
+                              double scale) {
+  const long D = q.size(-1);
+  TORCH_CHECK(D == 64 || D == 128, "head dim must be 64 or 128");
+  check_attn_operand(q, "q", D); check_attn_operand(k, "k", D); check_attn_operand(v, "v", D);
+  const long B = q.size(0), Sq = q.size(1), Hq = q.size(2), Sk = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(k.size(0) == B && v.size(0) == B && v.size(1) == Sk && v.size(2) == Hkv, "k/v shape mismatch");
+  TORCH_CHECK(Hkv > 0 && Hq % Hkv == 0, "Hq must be a multiple of Hkv");
+  TORCH_CHECK(Sq > 0 && Sk > 0, "empty sequence");
+  auto o = torch::empty({B, Sq, Hq, D}, q.options());
+  auto lse = torch::empty({B, Hq, Sq}, q.options().dtype(at::kFloat));
+  k8s_amd::AttnFwdArgs a;
+  a.q = cbf(q); a.k = cbf(k); a.v = cbf(v); a.o = bf(o); a.lse = f32(lse); a.kv_lens = kv_lens_ptr(kv_lens, B);
+  a.sqb = q.stride(0); a.sqs = q.stride(1); a.sqh = q.stride(2);
+  a.skb = k.stride(0); a.sks = k.stride(1); a.skh = k.stride(2);
+  a.svb = v.stride(0); a.svs = v.stride(1); a.svh = v.stride(2);
+  a.sob = o.stride(0); a.sos = o.stride(1); a.soh = o.stride(2);
+  a.B = B; a.Sq = Sq; a.Sk = Sk; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal;
+  a.scale_log2 = (float)(scale * 1.4426950408889634);
+  k8s_amd::launch_flash_fwd(a, (int)D, cur_stream());
+  return {o, lse};
+}
+
+std::vector<Tensor> flash_bwd(Tensor dO, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal,
+                              c10::optional<Tensor> kv_lens, double scale) {
+  const long D = q.size(-1);
+  TORCH_CHECK(D == 64 || D == 128, "head dim must be 64 or 128");
+  check_attn_operand(q, "q", D); check_attn_operand(k, "k", D); check_attn_operand(v, "v", D);
+  check_attn_operand(o, "o", D); check_attn_operand(dO, "dO", D);
+  const long B = q.size(0), Sq = q.size(1), Hq = q.size(2), Sk = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(dO.sizes() == q.sizes() && o.sizes() == q.sizes(), "dO / o must match q");
+  TORCH_CHECK(Hq % Hkv == 0, "Hq must be a multiple of Hkv");
+  check_cuda(lse, "lse"); check_dtype(lse, at::kFloat, "lse");
+  TORCH_CHECK(lse.numel() == B * Hq * Sq, "lse must be [B, Hq, Sq]");
+  auto dq_acc = torch::zeros({B, Sq, Hq, D}, q.options().dtype(at::kFloat));
+  auto delta = torch::empty({B, Hq, Sq}, q.options().dtype(at::kFloat));
+  auto dq = torch::empty({B, Sq, Hq, D}, q.options());
+  auto dk = torch::empty({B, Sk, Hkv, D}, q.options());
+  auto dv = torch::empty({B, Sk, Hkv, D}, q.options());
+  k8s_amd::AttnBwdArgs a;
+  a.q = cbf(q); a.k = cbf(k); a.v = cbf(v); a.dO = cbf(dO); a.lse = f32(lse); a.delta = f32(delta);
+  a.dq = f32(dq_acc); a.dk = bf(dk); a.dv = bf(dv); a.kv_lens = kv_lens_ptr(kv_lens, B);
+  a.sqb = q.stride(0); a.sqs = q.stride(1); a.sqh = q.stride(2);
+  a.skb = k.stride(0); a.sks = k.stride(1); a.skh = k.stride(2);
+  a.svb = v.stride(0); a.svs = v.stride(1); a.svh = v.stride(2);
+  a.sdb = dO.stride(0); a.sds = dO.stride(1); a.sdh = dO.stride(2);
+  a.B = B; a.Sq = Sq; a.Sk = Sk; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal;
+  a.scale_log2 = (float)(scale * 1.4426950408889634);
+  a.scale = (float)scale;
+  k8s_amd::launch_flash_bwd(a, (int)D, cbf(o), o.stride(0), o.stride(1), o.stride(2), bf(dq), cur_stream());
+  return {dq, dk, dv};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -389,6 +459,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_dgrad_wtrans", &conv_dgrad_wtrans);
+  m.def("flash_fwd", &flash_fwd);
+  m.def("flash_bwd", &flash_bwd);
   m.attr("conv_stat_replicas") = k8s_amd::kConvStatReplicas;
   m.attr("arch") = "gfx950";
 }

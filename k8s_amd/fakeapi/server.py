@@ -40,11 +40,14 @@ class _Handler(BaseHTTPRequestHandler):
 
     def _send(self, code: int, body):
         data = json.dumps(body).encode() if body is not None else b""
-        self.send_response(code)
-        self.send_header("Content-Type", "application/json")
-        self.send_header("Content-Length", str(len(data)))
-        self.end_headers()
-        self.wfile.write(data)
+        try:
+            self.send_response(code)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(data)))
+            self.end_headers()
+            self.wfile.write(data)
+        except (BrokenPipeError, ConnectionResetError):
+            pass  # the client went away (e.g. an operator shutting down mid-request)
 
     def _dispatch(self, method):
         u = urlparse(self.path)

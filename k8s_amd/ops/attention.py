@@ -4,9 +4,11 @@
 q [B, S, Hq, D], k/v [B, S, Hkv, D] (GQA: Hq % Hkv == 0), bf16.
 
 GPU: the gfx950 flash-attention kernels (``csrc/kernels/attention.hip``:
-online-softmax forward writing the log-sum-exp, recompute backward) when the
-extension provides them; otherwise -- and on CPU -- an explicit
-matmul/softmax reference (no SDPA dispatch, so no Triton-built kernels run).
+online-softmax forward writing the log-sum-exp, recompute backward with
+dK/dV in registers and atomically accumulated dQ). q/k/v may be strided
+views (e.g. column slices of the fused QKV projection) -- no copies. Head
+dims other than 64/128 and CPU tensors use an explicit matmul/softmax
+reference (no SDPA dispatch, so no Triton-built kernels run).
 """
 from __future__ import annotations
 
@@ -18,11 +20,12 @@ import torch
 from k8s_amd.ops._ext import load as _load
 
 
-def _has_flash() -> bool:
-    try:
-        return hasattr(_load(), "flash_fwd")
-    except ImportError:
+def _flash_ok(q, k, v) -> bool:
+    if not (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in (64, 128)):
         return False
+    ok = all(t.stride(-1) == 1 and all(s % 8 == 0 for s in t.stride()[:3]) and t.data_ptr() % 16 == 0
+             for t in (q, k, v))
+    return ok and hasattr(_load(), "flash_fwd")  # _load() raises if the extension is missing on a GPU box
 
 
 def attention_reference(q, k, v, causal: bool, kv_lens: Optional[torch.Tensor] = None, scale: Optional[float] = None):
@@ -50,6 +53,8 @@ class _Flash(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, causal, kv_lens, scale):
         C = _load()
+        if kv_lens is not None:
+            kv_lens = kv_lens.to(device=q.device, dtype=torch.int32).contiguous()
         o, lse = C.flash_fwd(q, k, v, causal, kv_lens, scale)
         ctx.save_for_backward(q, k, v, o, lse, kv_lens if kv_lens is not None else torch.empty(0))
         ctx.causal, ctx.scale, ctx.has_lens = causal, scale, kv_lens is not None
@@ -84,6 +89,6 @@ class _Reference(torch.autograd.Function):
 
 def attention(q, k, v, causal: bool = False, kv_lens: Optional[torch.Tensor] = None, scale: Optional[float] = None):
     scale = scale or 1.0 / math.sqrt(q.shape[-1])
-    if q.is_cuda and q.dtype == torch.bfloat16 and _has_flash() and q.shape[-1] in (64, 128):
+    if _flash_ok(q, k, v):
         return _Flash.apply(q, k, v, causal, kv_lens, scale)
     return _Reference.apply(q, k, v, causal, kv_lens, scale)

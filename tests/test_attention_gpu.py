@@ -1,0 +1,68 @@
+"""Flash attention (K5) fwd/bwd vs the fp32 matmul/softmax reference: strided QKV views, GQA, causal,
+key-padding lengths, sequence tails."""
+import math
+
+import pytest
+import torch
+
+from k8s_amd.ops.attention import _Flash, attention_reference
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, tol, what):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-6
+    assert err <= tol * max(1.0, scale), "%s: max err %g (scale %g)" % (what, err, scale)
+
+
+CASES = [
+    # B, S, Hq, Hkv, D, causal, lens
+    (2, 128, 12, 12, 64, False, None),
+    (2, 200, 4, 4, 64, False, [200, 77]),
+    (1, 256, 8, 2, 128, True, None),
+    (2, 333, 4, 1, 128, True, None),
+    (2, 192, 4, 4, 128, False, [1, 150]),
+    (1, 64, 2, 2, 64, True, None),
+]
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,D,causal,lens", CASES)
+def test_flash_fwd_bwd(cuda, B, S, Hq, Hkv, D, causal, lens):
+    torch.manual_seed(0)
+    # q, k, v as column slices of one fused projection output (the models' layout)
+    qkv = torch.randn(B, S, (Hq + 2 * Hkv) * D, device=cuda).bfloat16()
+    q = qkv[..., :Hq * D].view(B, S, Hq, D)
+    k = qkv[..., Hq * D:(Hq + Hkv) * D].view(B, S, Hkv, D)
+    v = qkv[..., (Hq + Hkv) * D:].view(B, S, Hkv, D)
+    kv_lens = torch.tensor(lens, device=cuda, dtype=torch.int32) if lens else None
+    scale = 1.0 / math.sqrt(D)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ref = attention_reference(qr, kr, vr, causal, kv_lens, scale)
+    qq, kk, vv = (t.detach().clone().requires_grad_(True) for t in (q, k, v))
+    out = _Flash.apply(qq, kk, vv, causal, kv_lens, scale)
+    valid = torch.ones(B, S, 1, 1, device=cuda)
+    if lens:  # rows whose keys are all masked: the reference gives NaN, the kernel 0
+        for bi, n in enumerate(lens):
+            if n == 0:
+                valid[bi] = 0
+    _close(out * valid, torch.nan_to_num(ref) * valid, 2e-2, "O")
+    do = torch.randn_like(out)
+    ref.backward(do.float())
+    out.backward(do)
+    _close(qq.grad, torch.nan_to_num(qr.grad), 3e-2, "dQ")
+    _close(kk.grad, torch.nan_to_num(kr.grad), 3e-2, "dK")
+    _close(vv.grad, torch.nan_to_num(vr.grad), 3e-2, "dV")
+
+
+def test_flash_lse(cuda):
+    from k8s_amd.ops._ext import load
+
+    torch.manual_seed(1)
+    B, S, H, D = 1, 130, 2, 128
+    q, k, v = (torch.randn(B, S, H, D, device=cuda).bfloat16() for _ in range(3))
+    o, lse = load().flash_fwd(q, k, v, False, None, 0.1)
+    s = torch.einsum("bqhd,bkhd->bhqk", q.float(), k.float()) * 0.1
+    ref = torch.logsumexp(s, -1) / math.log(2.0)  # the kernel stores log2-domain lse
+    _close(lse, ref, 1e-3, "lse")
