@@ -3,9 +3,11 @@
 For ops with more than one implementation (our MFMA implicit-GEMM vs the
 vendor path for the same conv shape, tile variants, ...) the first call of a
 shape times every candidate on the real tensors (cuda events, median of a few
-runs) and caches the winner for the process (and in
-``$K8S_AMD_AUTOTUNE_CACHE`` if set, so later runs and other ranks reuse it).
-Candidates must be side-effect free or write to scratch while tuning.
+runs) and caches the winner for the process and in a JSON file
+(``$K8S_AMD_AUTOTUNE_CACHE``, default ``~/.cache/k8s_amd/autotune-v1.json``;
+``none`` disables the file) so restarted replicas and later jobs on the node
+skip tuning -- part of the job-create -> step 0 latency. Candidates must be
+side-effect free or write to scratch while tuning.
 
 ``K8S_AMD_AUTOTUNE=0`` disables tuning (always the first candidate = ours).
 """
@@ -28,12 +30,23 @@ def enabled() -> bool:
     return os.environ.get("K8S_AMD_AUTOTUNE", "1") != "0"
 
 
+CACHE_VERSION = "v1"  # bump when kernels / candidates change
+
+
+def cache_path():
+    p = os.environ.get("K8S_AMD_AUTOTUNE_CACHE")
+    if p is None:
+        base = os.environ.get("XDG_CACHE_HOME") or os.path.join(os.path.expanduser("~"), ".cache")
+        p = os.path.join(base, "k8s_amd", "autotune-%s.json" % CACHE_VERSION)
+    return None if p in ("", "none") else p
+
+
 def _load_cache():
     global _loaded
     if _loaded:
         return
     _loaded = True
-    p = os.environ.get("K8S_AMD_AUTOTUNE_CACHE")
+    p = cache_path()
     if p and os.path.exists(p):
         try:
             _cache.update(json.load(open(p)))
@@ -42,12 +55,17 @@ def _load_cache():
 
 
 def _save_cache():
-    p = os.environ.get("K8S_AMD_AUTOTUNE_CACHE")
-    if p:
+    p = cache_path()
+    if not p:
+        return
+    try:
+        os.makedirs(os.path.dirname(p), exist_ok=True)
         tmp = p + ".tmp.%d" % os.getpid()
         with open(tmp, "w") as f:
             json.dump(_cache, f, indent=1, sort_keys=True)
         os.replace(tmp, p)
+    except OSError:
+        pass  # read-only home: keep the in-process cache
 
 
 def _time(fn, reps=3) -> float:
