@@ -16,14 +16,15 @@
 //                    no LDS round trip for P.
 //   writes O (bf16) and lse2 = m + log2(l) (fp32, [B, Hq, Sq]) for the backward.
 //
-// Backward (FA2 order, one block = 64 keys of one KV head, looping over every query tile of
-// every query head of its GQA group, so dK/dV accumulate in VGPRs without atomics):
+// Backward (FA2 order, dK/dV kernel: one block = 64 keys of one KV head, looping over every query tile
+// of every query head of its GQA group, so dK/dV accumulate in VGPRs without atomics):
 //   S = Q K^T, dP = dO V^T       (K, V fragments of the wave's 16 keys stay in VGPRs)
 //   P = exp2(S*c - lse2), dS = P (dP - delta)
 //   dV^T += dO^T P, dK^T += Q^T dS  (P / dS consumed in place through the permuted-k trick,
 //                                   dO^T / Q^T read transposed from LDS)
-//   dQ += dS K                    (dS through LDS, fp32 atomics into a [B,Sq,Hq,D] accumulator)
-//   delta = rowsum(dO * O) is a separate tiny kernel; dQ is converted to bf16 at the end.
+//   dQ in a second kernel shaped like the forward (per query block: S^T, dP^T recomputed, dQ^T += K^T dS^T),
+//   so no fp32 atomics; delta = rowsum(dO * O) is a tiny kernel ahead of both. lse / delta rows are padded
+//   to a multiple of 64 so a query tile's 256 B of each can be staged by one global_load_lds.
 #include <algorithm>
 
 #include "common.h"
@@ -235,16 +236,16 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
       for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(oacc[d][qs][r] * inv);
       *reinterpret_cast<bf16x4_t*>(op + (long)qi * a.sos + d * 16 + g * 4) = o;
     }
-    if (g == 0) a.lse[((long)b * a.Hq + h) * a.Sq + qi] = lt > 0.f ? m[qs] + log2f(lt) : INFINITY;
+    if (g == 0) a.lse[((long)b * a.Hq + h) * a.lse_ld + qi] = lt > 0.f ? m[qs] + log2f(lt) : INFINITY;
   }
 }
 
 // =============================================================================== backward
-// delta[b, h, q] = sum_d dO * O  (16 lanes per row, 8 elements per lane for D = 128)
+// delta[b, h, q] = sum_d dO * O  (D/8 lanes per row, 8 elements per lane); rows of stride lse_ld
 template <int D>
 __global__ void __launch_bounds__(256) flash_delta_kernel(const uint16_t* o, long sob, long sos, long soh,
                                                          const uint16_t* dO, long sdb, long sds, long sdh,
-                                                         float* delta, int B, int Sq, int Hq) {
+                                                         float* delta, int B, int Sq, int Hq, long ld) {
   constexpr int LPR = D / 8;  // lanes per row
   const long row = ((long)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
   const int part = threadIdx.x % LPR;
@@ -264,19 +265,18 @@ __global__ void __launch_bounds__(256) flash_delta_kernel(const uint16_t* o, lon
   }
 #pragma unroll
   for (int w = LPR / 2; w > 0; w >>= 1) acc += __shfl_xor(acc, w, 64);
-  if (row < R && part == 0) delta[((long)b * Hq + h) * Sq + q] = acc;
+  if (row < R && part == 0) delta[((long)b * Hq + h) * ld + q] = acc;
 }
 
+// ---- dK, dV: one block = 64 keys of one KV head (wave w: keys k0 + 16w .. +15, K/V fragments in VGPRs),
+// looping over every (query head of the GQA group, 64-query tile); Q / dO / lse / delta tiles double-buffered
+// in LDS through global_load_lds. Lane layout of S, dP, P, dS: key = li, query = 16*qs + 4*g + r.
 template <int D>
-__global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_kernel(AttnBwdArgs a) {
+__global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArgs a) {
   constexpr int ND = D / 16, NK = D / 32;
-  constexpr int TQ = FB_BM * D * 2;  // Q / dO tile bytes
-  constexpr int TK = FB_BN * D * 2;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * TQ + TK + FB_BM * FB_BN * 2];
-  char* tq = smem;
-  char* tdo = smem + TQ;
-  char* tk = smem + 2 * TQ;
-  char* tds = tk + TK;  // dS [64 q][64 keys] bf16, K-major swizzled (128-B rows)
+  constexpr int TQ = FB_BM * D * 2;        // Q / dO tile bytes
+  constexpr int STAGE = 2 * TQ + 1024;     // Q | dO | lse (256 B) delta (256 B) pad
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
 
@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_kernel(AttnBwdArgs a)
   const int hk = (wg / nkb) % a.Hkv;
   const int b = wg / (nkb * a.Hkv);
   const int rep = a.Hq / a.Hkv;
-  const int k0 = kb * FB_BN, kw = k0 + wid * 16;  // this wave's 16 keys
+  const int k0 = kb * FB_BN, kw = k0 + wid * 16;
   const int off = a.Sk - a.Sq;
   int kv_end = a.Sk;
   if (a.kv_lens) kv_end = min(kv_end, a.kv_lens[b]);
@@ -299,8 +299,11 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_kernel(AttnBwdArgs a)
 #pragma unroll
   for (int i = 0; i < ND; ++i) dka[i] = dva[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  if (k0 < kv_end) {
-    // K / V fragments of the wave's keys (second operand of S = Q K^T and dP = dO V^T)
+  const int qt0 = a.causal ? max(0, k0 - off) / FB_BM : 0;
+  const int nqt = (a.Sq + FB_BM - 1) / FB_BM;
+  const int per_head = nqt - qt0;
+  const int total = (k0 < kv_end && per_head > 0) ? rep * per_head : 0;
+  if (total > 0) {
     mfma_bf16x8 kf[NK], vf[NK];
     {
       const int key = kw + li;
@@ -315,124 +318,87 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_kernel(AttnBwdArgs a)
         vf[kk] = __builtin_bit_cast(mfma_bf16x8, y);
       }
     }
-    // K tile in LDS for dQ = dS K
-#pragma unroll
-    for (int rd = 0; rd < TK / (16 * FA_THREADS); ++rd) {
-      const int s = rd * FA_THREADS + tid;
-      glds16(kh_src(kp, a.sks, FB_BN, k0, a.Sk, s), tk + (size_t)(rd * FA_THREADS + wid_u * 64) * 16);
-    }
-    const int qt0 = a.causal ? max(0, k0 - off) / FB_BM : 0;
-    const int nqt = (a.Sq + FB_BM - 1) / FB_BM;
-    for (int hr = 0; hr < rep; ++hr) {
-      const int h = hk * rep + hr;
+    auto stage = [&](int buf, int it) {
+      const int h = hk * rep + it / per_head, q0 = (qt0 + it % per_head) * FB_BM;
       const uint16_t* qp = a.q + (long)b * a.sqb + (long)h * a.sqh;
       const uint16_t* dop = a.dO + (long)b * a.sdb + (long)h * a.sdh;
-      const float* lse = a.lse + ((long)b * a.Hq + h) * a.Sq;
-      const float* dlt = a.delta + ((long)b * a.Hq + h) * a.Sq;
-      float* dq = a.dq + (long)b * a.Sq * a.Hq * D + (long)h * D;
-      for (int qt = qt0; qt < nqt; ++qt) {
-        const int q0 = qt * FB_BM;
+      char* base = smem + buf * STAGE;
 #pragma unroll
-        for (int rd = 0; rd < TQ / (16 * FA_THREADS); ++rd) {
-          const int s = rd * FA_THREADS + tid;
-          const size_t wb = (size_t)(rd * FA_THREADS + wid_u * 64) * 16;
-          glds16(kh_src(qp, a.sqs, FB_BM, q0, a.Sq, s), tq + wb);
-          glds16(kh_src(dop, a.sds, FB_BM, q0, a.Sq, s), tdo + wb);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        // ---- S = Q K^T, dP = dO V^T  (lane: key = kw + li, q = q0 + 16*qs + 4*g + r)
-        f32x4_t sv[4], dp[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sv[i] = dp[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < NK; ++kk) {
-#pragma unroll
-          for (int qs = 0; qs < 4; ++qs) {
-            const mfma_bf16x8 qa = frag_kmajor(tq + (kk >> 1) * (FB_BM * 128), qs * 16, kk & 1, lane);
-            const mfma_bf16x8 da = frag_kmajor(tdo + (kk >> 1) * (FB_BM * 128), qs * 16, kk & 1, lane);
-            sv[qs] = mfma16(qa, kf[kk], sv[qs]);
-            dp[qs] = mfma16(da, vf[kk], dp[qs]);
-          }
-        }
-        // ---- P, dS
-        const int key = kw + li;
-#pragma unroll
-        for (int qs = 0; qs < 4; ++qs)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int qi = q0 + qs * 16 + g * 4 + r;
-            float p = 0.f, ds = 0.f;
-            if (qi < a.Sq && key < kv_end && !(a.causal && key > qi + off)) {
-              p = exp2f(sv[qs][r] * a.scale_log2 - lse[qi]);
-              ds = p * (dp[qs][r] - dlt[qi]);
-            }
-            sv[qs][r] = p;
-            dp[qs][r] = ds;
-          }
-        // ---- dV^T += dO^T P, dK^T += Q^T dS   (k = queries, permuted order)
-        {
-          const int q_ = li >> 2, pp = li & 3;
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const float p0[4] = {sv[2 * s2][0], sv[2 * s2][1], sv[2 * s2][2], sv[2 * s2][3]};
-            const float p1[4] = {sv[2 * s2 + 1][0], sv[2 * s2 + 1][1], sv[2 * s2 + 1][2], sv[2 * s2 + 1][3]};
-            const float d0[4] = {dp[2 * s2][0], dp[2 * s2][1], dp[2 * s2][2], dp[2 * s2][3]};
-            const float d1[4] = {dp[2 * s2 + 1][0], dp[2 * s2 + 1][1], dp[2 * s2 + 1][2], dp[2 * s2 + 1][3]};
-            const mfma_bf16x8 pf = pack8(p0, p1), dsf = pack8(d0, d1);
-            const int r0 = 32 * s2 + 4 * g + q_, r1 = r0 + 16;
-#pragma unroll
-            for (int d = 0; d < ND; ++d) {
-              const int dc = d * 16 + pp * 4;
-              const mfma_bf16x8 dot = join8(tr16(kh_addr(tdo, FB_BM, r0, dc)), tr16(kh_addr(tdo, FB_BM, r1, dc)));
-              const mfma_bf16x8 qtf = join8(tr16(kh_addr(tq, FB_BM, r0, dc)), tr16(kh_addr(tq, FB_BM, r1, dc)));
-              dva[d] = mfma16(dot, pf, dva[d]);
-              dka[d] = mfma16(qtf, dsf, dka[d]);
-            }
-          }
-        }
-        // ---- dS -> LDS as [q][key] (K-major, 128-B swizzled rows)
-#pragma unroll
-        for (int qs = 0; qs < 4; ++qs)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = qs * 16 + g * 4 + r, col = wid * 16 + li;
-            const int c = col >> 3;
-            *reinterpret_cast<uint16_t*>(tds + row * 128 + ((c ^ ((row >> 1) & 7)) << 4) + (col & 7) * 2) =
-                f2bf(dp[qs][r]);
-          }
-        __syncthreads();
-        // ---- dQ^T[d][q] += K^T dS^T  (wave `wid` takes query subtile wid)
-        {
-          const int q_ = li >> 2, pp = li & 3;
-          f32x4_t acc[ND];
-#pragma unroll
-          for (int d = 0; d < ND; ++d) acc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const mfma_bf16x8 dsq = frag_kmajor(tds, wid * 16, s2, lane);
-            const int r0 = 32 * s2 + 8 * g + q_, r1 = r0 + 4;
-#pragma unroll
-            for (int d = 0; d < ND; ++d) {
-              const int dc = d * 16 + pp * 4;
-              const mfma_bf16x8 kt = join8(tr16(kh_addr(tk, FB_BN, r0, dc)), tr16(kh_addr(tk, FB_BN, r1, dc)));
-              acc[d] = mfma16(kt, dsq, acc[d]);
-            }
-          }
-          const int qi = q0 + wid * 16 + li;
-          if (qi < a.Sq) {
-            float* dqr = dq + (long)qi * a.Hq * D;
-#pragma unroll
-            for (int d = 0; d < ND; ++d)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) atomicAdd(dqr + d * 16 + g * 4 + r, acc[d][r] * a.scale);
-          }
-        }
-        __syncthreads();  // tq / tdo / tds are rewritten by the next tile
+      for (int rd = 0; rd < TQ / (16 * FA_THREADS); ++rd) {
+        const int s = rd * FA_THREADS + tid;
+        const size_t wb = (size_t)(rd * FA_THREADS + wid_u * 64) * 16;
+        glds16(kh_src(qp, a.sqs, FB_BM, q0, a.Sq, s), base + wb);
+        glds16(kh_src(dop, a.sds, FB_BM, q0, a.Sq, s), base + TQ + wb);
       }
+      if (wid_u == 0) {  // lse | delta of the 64 queries (rows padded to lse_ld, so never out of bounds)
+        const long row = ((long)b * a.Hq + h) * a.lse_ld + q0;
+        const float* src = lane < 16 ? a.lse + row + lane * 4 : (lane < 32 ? a.delta + row + (lane - 16) * 4
+                                                                          : a.lse + row);
+        glds16(src, base + 2 * TQ);
+      }
+    };
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int key = kw + li;
+    for (int it = 0; it < total; ++it) {
+      const int cur = it & 1;
+      if (it + 1 < total) stage(cur ^ 1, it + 1);
+      const char* tq = smem + cur * STAGE;
+      const char* tdo = tq + TQ;
+      const float* tl = reinterpret_cast<const float*>(tq + 2 * TQ);
+      const int q0 = (qt0 + it % per_head) * FB_BM;
+      // ---- S = Q K^T, dP = dO V^T
+      f32x4_t sv[4], dp[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sv[i] = dp[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+#pragma unroll
+        for (int qs = 0; qs < 4; ++qs) {
+          const mfma_bf16x8 qa = frag_kmajor(tq + (kk >> 1) * (FB_BM * 128), qs * 16, kk & 1, lane);
+          const mfma_bf16x8 da = frag_kmajor(tdo + (kk >> 1) * (FB_BM * 128), qs * 16, kk & 1, lane);
+          sv[qs] = mfma16(qa, kf[kk], sv[qs]);
+          dp[qs] = mfma16(da, vf[kk], dp[qs]);
+        }
+      }
+      // ---- P = exp2(S c - lse2), dS = P (dP - delta)
+#pragma unroll
+      for (int qs = 0; qs < 4; ++qs) {
+        const f32x4_t l4 = *reinterpret_cast<const f32x4_t*>(tl + qs * 16 + g * 4);
+        const f32x4_t d4 = *reinterpret_cast<const f32x4_t*>(tl + 64 + qs * 16 + g * 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qi = q0 + qs * 16 + g * 4 + r;
+          const bool ok = qi < a.Sq && key < kv_end && !(a.causal && key > qi + off);
+          const float p = ok ? exp2f(sv[qs][r] * a.scale_log2 - l4[r]) : 0.f;
+          sv[qs][r] = p;
+          dp[qs][r] = ok ? p * (dp[qs][r] - d4[r]) : 0.f;  // padded rows of lse / delta are uninitialised
+        }
+      }
+      // ---- dV^T += dO^T P, dK^T += Q^T dS   (k = queries in the permuted order of the accumulators)
+      const int q_ = li >> 2, pp = li & 3;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const float p0[4] = {sv[2 * s2][0], sv[2 * s2][1], sv[2 * s2][2], sv[2 * s2][3]};
+        const float p1[4] = {sv[2 * s2 + 1][0], sv[2 * s2 + 1][1], sv[2 * s2 + 1][2], sv[2 * s2 + 1][3]};
+        const float d0[4] = {dp[2 * s2][0], dp[2 * s2][1], dp[2 * s2][2], dp[2 * s2][3]};
+        const float d1[4] = {dp[2 * s2 + 1][0], dp[2 * s2 + 1][1], dp[2 * s2 + 1][2], dp[2 * s2 + 1][3]};
+        const mfma_bf16x8 pf = pack8(p0, p1), dsf = pack8(d0, d1);
+        const int r0 = 32 * s2 + 4 * g + q_, r1 = r0 + 16;
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+          const int dc = d * 16 + pp * 4;
+          const mfma_bf16x8 dot = join8(tr16(kh_addr(tdo, FB_BM, r0, dc)), tr16(kh_addr(tdo, FB_BM, r1, dc)));
+          const mfma_bf16x8 qtf = join8(tr16(kh_addr(tq, FB_BM, r0, dc)), tr16(kh_addr(tq, FB_BM, r1, dc)));
+          dva[d] = mfma16(dot, pf, dva[d]);
+          dka[d] = mfma16(qtf, dsf, dka[d]);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
     }
   }
-  // ---- dK = scale * dK^T^T, dV (bf16, [B, Sk, Hkv, D])
   const int key = kw + li;
   if (key < a.Sk) {
     uint16_t* dkp = a.dk + (((long)b * a.Sk + key) * a.Hkv + hk) * D;
@@ -451,12 +417,130 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_kernel(AttnBwdArgs a)
   }
 }
 
-__global__ void f32_to_bf16_kernel(const float* x, uint16_t* y, long n8) {
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
-    const float4 u = reinterpret_cast<const float4*>(x)[2 * i];
-    const float4 v = reinterpret_cast<const float4*>(x)[2 * i + 1];
-    const float o[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-    store8(y + i * 8, o);
+// ---- dQ: one block = 4 waves x 16 queries of one head (the forward's structure): K/V tiles of 64 keys
+// double-buffered in LDS, S^T = K Q^T and dP^T = V dO^T recomputed (lane: query = li, keys 4g+r), and
+// dQ^T += K^T dS^T with dS^T consumed in place (permuted k) and K^T read transposed from the K tile.
+// No atomics: each block owns its queries.
+template <int D>
+__global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dq_kernel(AttnBwdArgs a) {
+  constexpr int ND = D / 16, NK = D / 32;
+  constexpr int KT = FB_BN * D * 2;
+  constexpr int BMQ = 64;
+  __shared__ __attribute__((aligned(1024))) char smem[4 * KT];  // [buf][K | V], both K-major halves
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+
+  const int nqb = (a.Sq + BMQ - 1) / BMQ;
+  const int nwg = nqb * a.Hq * a.B;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int qb = nqb - 1 - (wg % nqb);
+  const int h = (wg / nqb) % a.Hq;
+  const int b = wg / (nqb * a.Hq);
+  const int hk = h / (a.Hq / a.Hkv);
+  const int q0 = qb * BMQ, q0w = q0 + wid * 16, qi = q0w + li;
+  const int off = a.Sk - a.Sq;
+  int kv_end = a.Sk;
+  if (a.kv_lens) kv_end = min(kv_end, a.kv_lens[b]);
+  int kv_stop = kv_end;
+  if (a.causal) kv_stop = min(kv_stop, q0 + BMQ + off);
+  const int ntiles = kv_stop > 0 ? (kv_stop + FB_BN - 1) / FB_BN : 0;
+
+  const uint16_t* qp = a.q + (long)b * a.sqb + (long)h * a.sqh;
+  const uint16_t* dop = a.dO + (long)b * a.sdb + (long)h * a.sdh;
+  const uint16_t* kp = a.k + (long)b * a.skb + (long)hk * a.skh;
+  const uint16_t* vp = a.v + (long)b * a.svb + (long)hk * a.svh;
+
+  mfma_bf16x8 qf[NK], df[NK];
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) {
+    bf16x8_t x = {0, 0, 0, 0, 0, 0, 0, 0}, y = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (qi < a.Sq) {
+      x = *reinterpret_cast<const bf16x8_t*>(qp + (long)qi * a.sqs + kk * 32 + g * 8);
+      y = *reinterpret_cast<const bf16x8_t*>(dop + (long)qi * a.sds + kk * 32 + g * 8);
+    }
+    qf[kk] = __builtin_bit_cast(mfma_bf16x8, x);
+    df[kk] = __builtin_bit_cast(mfma_bf16x8, y);
+  }
+  const long lrow = ((long)b * a.Hq + h) * a.lse_ld;
+  const float lq = qi < a.Sq ? a.lse[lrow + qi] : INFINITY;
+  const float dq_ = qi < a.Sq ? a.delta[lrow + qi] : 0.f;
+
+  f32x4_t acc[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int buf, int key0) {
+    char* tk = smem + buf * 2 * KT;
+#pragma unroll
+    for (int rd = 0; rd < KT / (16 * FA_THREADS); ++rd) {
+      const int s = rd * FA_THREADS + tid;
+      const size_t wb = (size_t)(rd * FA_THREADS + wid_u * 64) * 16;
+      glds16(kh_src(kp, a.sks, FB_BN, key0, a.Sk, s), tk + wb);
+      glds16(kh_src(vp, a.svs, FB_BN, key0, a.Sk, s), tk + KT + wb);
+    }
+  };
+  if (ntiles > 0) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const int q_ = li >> 2, pp = li & 3;
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1, key0 = t * FB_BN;
+    if (t + 1 < ntiles) stage(cur ^ 1, key0 + FB_BN);
+    const char* tk = smem + cur * 2 * KT;
+    const char* tv = tk + KT;
+    if (!(a.causal && key0 > q0w + 15 + off)) {
+      f32x4_t s[4], dp[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s[i] = dp[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          s[i] = mfma16(frag_kmajor(tk + (kk >> 1) * (FB_BN * 128), i * 16, kk & 1, lane), qf[kk], s[i]);
+          dp[i] = mfma16(frag_kmajor(tv + (kk >> 1) * (FB_BN * 128), i * 16, kk & 1, lane), df[kk], dp[i]);
+        }
+      }
+      const bool need_mask = (key0 + FB_BN > kv_end) || (a.causal && key0 + FB_BN - 1 > q0w + off);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          bool ok = true;
+          if (need_mask) {
+            const int key = key0 + i * 16 + g * 4 + r;
+            ok = key < kv_end && !(a.causal && key > qi + off);
+          }
+          const float p = ok ? exp2f(s[i][r] * a.scale_log2 - lq) : 0.f;
+          dp[i][r] = p * (dp[i][r] - dq_);
+        }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const float d0[4] = {dp[2 * s2][0], dp[2 * s2][1], dp[2 * s2][2], dp[2 * s2][3]};
+        const float d1[4] = {dp[2 * s2 + 1][0], dp[2 * s2 + 1][1], dp[2 * s2 + 1][2], dp[2 * s2 + 1][3]};
+        const mfma_bf16x8 dsf = pack8(d0, d1);
+        const int r0 = 32 * s2 + 4 * g + q_, r1 = r0 + 16;
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+          const int dc = d * 16 + pp * 4;
+          const mfma_bf16x8 kt = join8(tr16(kh_addr(tk, FB_BN, r0, dc)), tr16(kh_addr(tk, FB_BN, r1, dc)));
+          acc[d] = mfma16(kt, dsf, acc[d]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (qi < a.Sq) {
+    uint16_t* dqp = a.dq + (((long)b * a.Sq + qi) * a.Hq + h) * D;
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      bf16x4_t x;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) x[r] = (short)f2bf(acc[d][r] * a.scale);
+      *reinterpret_cast<bf16x4_t*>(dqp + d * 16 + g * 4) = x;
+    }
   }
 }
 
@@ -468,24 +552,26 @@ void launch_flash_fwd(const AttnFwdArgs& a, int D, hipStream_t st) {
   else hipLaunchKernelGGL(flash_fwd_kernel<64>, grid, dim3(FA_THREADS), 0, st, a);
 }
 
-void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, long sos, long soh, uint16_t* dq_out,
+void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, long sos, long soh,
                       hipStream_t st) {
   const long R = (long)a.B * a.Sq * a.Hq;
   const int lpr = D / 8;
   const dim3 dgrid((unsigned)((R * lpr + 255) / 256));
   if (D == 128)
     hipLaunchKernelGGL(flash_delta_kernel<128>, dgrid, dim3(256), 0, st, o, sob, sos, soh, a.dO, a.sdb, a.sds, a.sdh,
-                       a.delta, a.B, a.Sq, a.Hq);
+                       a.delta, a.B, a.Sq, a.Hq, a.lse_ld);
   else
     hipLaunchKernelGGL(flash_delta_kernel<64>, dgrid, dim3(256), 0, st, o, sob, sos, soh, a.dO, a.sdb, a.sds, a.sdh,
-                       a.delta, a.B, a.Sq, a.Hq);
-  const int nkb = (a.Sk + FB_BN - 1) / FB_BN;
-  const dim3 grid(nkb * a.Hkv * a.B);
-  if (D == 128) hipLaunchKernelGGL(flash_bwd_kernel<128>, grid, dim3(FA_THREADS), 0, st, a);
-  else hipLaunchKernelGGL(flash_bwd_kernel<64>, grid, dim3(FA_THREADS), 0, st, a);
-  const long n8 = R * D / 8;
-  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)std::min<long>((n8 + 255) / 256, 4096L)), dim3(256), 0, st, a.dq,
-                     dq_out, n8);
+                       a.delta, a.B, a.Sq, a.Hq, a.lse_ld);
+  const dim3 gkv(((a.Sk + FB_BN - 1) / FB_BN) * a.Hkv * a.B);
+  const dim3 gq(((a.Sq + 63) / 64) * a.Hq * a.B);
+  if (D == 128) {
+    hipLaunchKernelGGL(flash_bwd_dkv_kernel<128>, gkv, dim3(FA_THREADS), 0, st, a);
+    hipLaunchKernelGGL(flash_bwd_dq_kernel<128>, gq, dim3(FA_THREADS), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(flash_bwd_dkv_kernel<64>, gkv, dim3(FA_THREADS), 0, st, a);
+    hipLaunchKernelGGL(flash_bwd_dq_kernel<64>, gq, dim3(FA_THREADS), 0, st, a);
+  }
 }
 
 }  // namespace k8s_amd

@@ -58,7 +58,22 @@ __global__ void __launch_bounds__(BN_THREADS) bn_stats_kernel(const uint16_t* __
   }
   int n = 0;
   if (active) {
-    for (long row = r0 + r; row < r1; row += rows_per_iter) {
+    long row = r0 + r;
+    for (; row + 3 * rows_per_iter < r1; row += 4 * rows_per_iter) {
+      float v4[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) load8(x + (row + u * rows_per_iter) * C + cg * 8, v4[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = v4[u][j] - shift[j];
+          s[j] += d;
+          q[j] += d * d;
+        }
+      n += 4;
+    }
+    for (; row < r1; row += rows_per_iter) {
       float v[8];
       load8(x + row * C + cg * 8, v);
 #pragma unroll
@@ -254,7 +269,38 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
     bt[j] = (active && relu_x) ? beta[cg * 8 + j] : 0.f;
   }
   if (active) {
-    for (long row = r0 + r; row < r1; row += rows_per_iter) {
+    // 4 rows per trip: 8-12 independent 16-B loads in flight per thread before any is used
+    long row = r0 + r;
+    for (; row + 3 * rows_per_iter < r1; row += 4 * rows_per_iter) {
+      float g4[4][8], x4[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long off = (row + u * rows_per_iter) * C + cg * 8;
+        load8(dy + off, g4[u]);
+        load8(x + off, x4[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float* g = g4[u];
+        const float* xv = x4[u];
+        if (y) {
+          bf16x8_t yv = *reinterpret_cast<const bf16x8_t*>(y + (row + u * rows_per_iter) * C + cg * 8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (bf2f((uint16_t)yv[j]) <= 0.f) g[j] = 0.f;
+        } else if (relu_x) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (bf2f(f2bf((xv[j] - mu[j]) * sc[j] + bt[j])) <= 0.f) g[j] = 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sd[j] += g[j];
+          sx[j] += g[j] * (xv[j] - mu[j]) * is[j];
+        }
+      }
+    }
+    for (; row < r1; row += rows_per_iter) {
       const long off = row * C + cg * 8;
       float g[8], xv[8];
       load8(dy + off, g);
@@ -380,8 +426,8 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t
 
 // ---------------------------------------------------------------- launchers
 static long bn_rows_per_block(long M, const BnGeom& g) {
-  // aim for ~1024 blocks in total; at least rows_per_iter*4 rows per block
-  long blocks_x = 512 / g.grid_y;
+  // ~1024 blocks in total (4 per CU: enough loads in flight to cover HBM latency); >= 4 row trips per block
+  long blocks_x = 1024 / g.grid_y;
   if (blocks_x < 1) blocks_x = 1;
   long rpb = (M + blocks_x - 1) / blocks_x;
   long minr = (long)g.rows_per_iter * 4;

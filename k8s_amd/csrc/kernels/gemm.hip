@@ -59,12 +59,14 @@ struct KMajor {
   const uint16_t* p;
   long ld;    // elements between rows
   int rows;   // valid rows (M or N)
+  int ktot = 1 << 30;  // valid K (a K % 64 tail reads zeros instead of the next row / past the end)
   // row-major [rows][K]; tile rows start at r0, k at k0
   __device__ __forceinline__ const void* src(int s, int r0, int k0) const {
     const int row = s >> 3, cp = s & 7;
     const int c = cp ^ ((row >> 1) & 7);
     int gr = r0 + row;
     gr = gr < rows ? gr : rows - 1;
+    if (k0 + c * 8 >= ktot) return g_zero_page;
     return p + (long)gr * ld + k0 + c * 8;
   }
   static constexpr bool kmajor = true;
@@ -103,6 +105,32 @@ struct ConvA {
     const int hi = ho * stride - pad + r * dil, wi = wo * stride - pad + sx * dil;
     if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) return g_zero_page;
     return x + (((long)n * H + hi) * W + wi) * C + c0 + c * 8;
+  }
+  static constexpr bool kmajor = true;
+};
+
+// Implicit im2col for any C % 8 == 0 (the 8-channel ResNet stem): every 16-B unit decodes its own
+// (r, s, c) and the K = R*S*C tail (K % 64 != 0) reads zeros.
+struct ConvAG {
+  const uint16_t* x;
+  int N, H, W, C, Ho, Wo, S, stride, pad, dil;
+  int rows;  // N*Ho*Wo
+  int ktot;  // R*S*C
+  FastDiv fC, fS, fHW, fWo;
+  __device__ __forceinline__ const void* src(int s, int r0, int k0) const {
+    const int row = s >> 3, cp = s & 7;
+    const int c = cp ^ ((row >> 1) & 7);
+    int m = r0 + row;
+    m = m < rows ? m : rows - 1;
+    const int k = k0 + c * 8;
+    if (k >= ktot) return g_zero_page;
+    const int rs = fC.div(k), c0 = k - rs * C;
+    const int r = fS.div(rs), sx = rs - r * S;
+    const int n = fHW.div(m), rem = m - n * (Ho * Wo);
+    const int ho = fWo.div(rem), wo = rem - ho * Wo;
+    const int hi = ho * stride - pad + r * dil, wi = wo * stride - pad + sx * dil;
+    if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) return g_zero_page;
+    return x + (((long)n * H + hi) * W + wi) * C + c0;
   }
   static constexpr bool kmajor = true;
 };
@@ -178,7 +206,9 @@ struct Epi {
   uint16_t* pre;      // bf16 pre-activation copy or null
   int out_f32;        // 1: fp32 output
   int act;            // 0 none, 1 relu, 2 gelu(tanh)
-  int mode;           // 0 store, 1 accumulate (fp32 C += acc), 2 atomic add (fp32)
+  int mode;           // 0 store, 1 accumulate (fp32 C += acc), 2 atomic add (fp32),
+                      // 3 split-K slab: split z stores plain fp32 at c + z * slab (reduced by splitk_reduce)
+  long slab;
   float alpha;
   float* stats;       // [STAT_REPL][2][N] fp32 per-column sum / sum of squares of the stored outputs
                       // (BN fusion) or null; tile row tm adds into replica tm % STAT_REPL so the atomics
@@ -192,10 +222,14 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 }
 
 // ----------------------------------------------------------------------------- the kernel
-template <class ASrc, class BSrc>
-__global__ void __launch_bounds__(GEMM_THREADS, 2)
+// NBUF = 2: double-buffered K loop (the next tile's loads in flight during this tile's MFMAs), 64 KB LDS,
+// 2 blocks/CU. NBUF = 1: single buffer, 32 KB LDS, 3 blocks/CU -- for short K ranges (K <= 128: the
+// memory-bound 1x1 convolutions of the early ResNet stages), where there is no next tile to prefetch and
+// block-level overlap is what hides HBM latency.
+template <class ASrc, class BSrc, int NBUF>
+__global__ void __launch_bounds__(GEMM_THREADS, NBUF == 1 ? 3 : 2)
 gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
-  __shared__ __attribute__((aligned(1024))) char smem[4 * TILE_BYTES];  // [buf][A|B]
+  __shared__ __attribute__((aligned(1024))) char smem[NBUF * 2 * TILE_BYTES];  // [buf][A|B]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
 
@@ -245,8 +279,16 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
     __syncthreads();
   }
   for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nt) stage(cur ^ 1, kbeg + (t + 1) * BK);
+    const int cur = NBUF == 1 ? 0 : (t & 1);
+    if (NBUF == 1) {
+      if (t > 0) {  // the previous tile's reads are done (barrier at the end of the last iteration)
+        stage(0, kbeg + t * BK);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    } else if (t + 1 < nt) {
+      stage(cur ^ 1, kbeg + (t + 1) * BK);
+    }
     const char* ta = smem + cur * 2 * TILE_BYTES;
     const char* tb = ta + TILE_BYTES;
 #pragma unroll
@@ -268,6 +310,10 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
   }
 
   // ---- epilogue: lane holds C[m][n..n+3]
+  if (E.mode == 3) {  // this split's private fp32 slab, plain stores
+    E.c = reinterpret_cast<float*>(E.c) + (long)blockIdx.z * E.slab;
+    E.mode = 0;
+  }
   float st_s[4][4], st_q[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -348,10 +394,12 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
     }
   }
   if (E.stats) {
-    // lanes with equal (lane >> 4) hold the same 4 columns: reduce over the 16 row lanes, one atomic per column
+    // lanes with equal (lane >> 4) hold the same 4 columns: reduce over the 16 row lanes, then over the two
+    // row-waves through LDS, so the block issues 4 full-wave atomic instructions (256 columns x {sum, sumsq})
+    // instead of 128 quarter-empty ones -- float atomics cost ~50 ns per wave-instruction per CU.
+    float* red = reinterpret_cast<float*>(smem);  // [wm][2][128]; the K loop's last barrier freed the tiles
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float a = st_s[j][r], b = st_q[j][r];
@@ -360,24 +408,42 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
           a += __shfl_xor(a, o, 64);
           b += __shfl_xor(b, o, 64);
         }
-        if ((lane & 15) == 0 && n + r < N) {
-          float* rep = E.stats + (long)(tm % STAT_REPL) * 2 * N;
-          atomicAdd(rep + n + r, a);
-          atomicAdd(rep + N + n + r, b);
+        if ((lane & 15) == 0) {
+          const int col = wn * 64 + j * 16 + (lane >> 4) * 4 + r;
+          red[(wm * 2 + 0) * 128 + col] = a;
+          red[(wm * 2 + 1) * 128 + col] = b;
         }
       }
+    }
+    __syncthreads();
+    const int col = tid & 127, which = tid >> 7;
+    const int n = n0 + col;
+    if (n < N) {
+      const float v = red[which * 128 + col] + red[(2 + which) * 128 + col];
+      atomicAdd(E.stats + (long)(tm % STAT_REPL) * 2 * N + (long)which * N + n, v);
     }
   }
 }
 
 // ----------------------------------------------------------------------------- host side
+// splits actually launched for a requested count (each split a whole number of BK tiles)
+static int effective_splits(int K, int splits) {
+  if (splits <= 1) return 1;
+  const int kps = ((K + splits - 1) / splits + BK - 1) / BK * BK;
+  return (K + kps - 1) / kps;
+}
+
 template <class ASrc, class BSrc>
 static void launch(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int splits, hipStream_t st) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const int kps = ((K + splits - 1) / splits + BK - 1) / BK * BK;
   splits = (K + kps - 1) / kps;
-  hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc>), dim3(tiles, 1, splits), dim3(GEMM_THREADS), 0, st, a, b, e, M,
-                     N, K, kps);
+  if (kps <= 2 * BK)
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1>), dim3(tiles, 1, splits), dim3(GEMM_THREADS), 0, st, a, b, e,
+                       M, N, K, kps);
+  else
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2>), dim3(tiles, 1, splits), dim3(GEMM_THREADS), 0, st, a, b, e,
+                       M, N, K, kps);
 }
 
 static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act, uint16_t* pre, int mode,
@@ -392,6 +458,7 @@ static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act,
   e.mode = mode;
   e.alpha = alpha;
   e.stats = nullptr;
+  e.slab = 0;
   return e;
 }
 
@@ -404,13 +471,38 @@ int gemm_choose_splits(int M, int N, int K) {
   return s;
 }
 
+// out[i] (+)= sum_z ws[z][i]  -- the split-K combine (float4 over MN, MN % 4 == 0)
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, long mn4, float* __restrict__ out,
+                                     int accumulate) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < mn4; i += (long)gridDim.x * blockDim.x) {
+    float4 acc = accumulate ? reinterpret_cast<const float4*>(out)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int z = 0; z < splits; ++z) {
+      const float4 v = reinterpret_cast<const float4*>(ws)[(long)z * mn4 + i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(out)[i] = acc;
+  }
+}
+
+static void splitk_reduce(const float* ws, int splits, long mn, float* out, bool accumulate, hipStream_t st) {
+  const long mn4 = mn / 4;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(stream_grid(mn4, 256)), dim3(256), 0, st, ws, splits, mn4, out,
+                     accumulate ? 1 : 0);
+}
+
+long gemm_splitk_workspace(int M, int N, int splits) { return splits > 1 ? (long)splits * M * N : 0; }
+
 // C[M,N] = act(alpha * op(A) op(B) + bias)
 //  a_kmajor: A stored [M][K] (lda) else [K][M];  b_kmajor: B stored [N][K] (ldb) else [K][N]
+//  mode 0 store / 1 accumulate; with splits > 1 (fp32 C, plain epilogue) the K range is split over
+//  blockIdx.z, each split writes an fp32 slab of `ws` and a reduce kernel combines them into C.
 void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                  long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
-                 float alpha, int splits, hipStream_t st) {
-  if (splits <= 0) splits = (mode == 2) ? gemm_choose_splits(M, N, K) : 1;
-  Epi e = make_epi(C, ldc, c_f32, bias, act, pre, mode, alpha);
+                 float alpha, int splits, float* ws, hipStream_t st) {
+  splits = effective_splits(K, splits);
+  const bool slab = splits > 1;
+  Epi e = make_epi(slab ? (void*)ws : C, slab ? (long)N : ldc, c_f32, bias, act, pre, slab ? 3 : mode, alpha);
+  e.slab = (long)M * N;
   if (a_kmajor && b_kmajor)
     launch(KMajor{A, lda, M}, KMajor{B, ldb, N}, e, M, N, K, splits, st);
   else if (a_kmajor && !b_kmajor)
@@ -419,31 +511,45 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
     launch(MNMajorK{A, lda, M, K}, KMajor{B, ldb, N}, e, M, N, K, splits, st);
   else
     launch(MNMajorK{A, lda, M, K}, MNMajorK{B, ldb, N, K}, e, M, N, K, splits, st);
+  if (slab) splitk_reduce(ws, splits, (long)M * N, reinterpret_cast<float*>(C), mode == 1, st);
 }
 
-// NHWC conv forward: y[N,Ho,Wo,K] = conv(x[N,H,W,C], w[K,R,S,C]); requires C % 64 == 0.
+// NHWC conv forward: y[N,Ho,Wo,K] = conv(x[N,H,W,C], w[K,R,S,C]); C % 64 == 0 takes the per-tile (r, s)
+// decode, any other C % 8 == 0 the per-unit one.
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int K,
                      int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
                      int mode, float* stats, hipStream_t st) {
-  const int M = N * Ho * Wo;
-  ConvA a{x, N, H, W, C, Ho, Wo, S, stride, pad, dil, M,
-          make_fastdiv(C), make_fastdiv(S), make_fastdiv(Ho * Wo), make_fastdiv(Wo)};
-  KMajor b{w, (long)R * S * C, K};
+  const int M = N * Ho * Wo, RSC = R * S * C;
+  KMajor b{w, (long)RSC, K, RSC};
   Epi e = make_epi(y, K, y_f32, bias, act, nullptr, mode, 1.f);
   e.stats = stats;
-  launch(a, b, e, M, K, R * S * C, 1, st);
+  if (C % 64 == 0) {
+    ConvA a{x, N, H, W, C, Ho, Wo, S, stride, pad, dil, M,
+            make_fastdiv(C), make_fastdiv(S), make_fastdiv(Ho * Wo), make_fastdiv(Wo)};
+    launch(a, b, e, M, K, RSC, 1, st);
+  } else {
+    ConvAG a{x, N, H, W, C, Ho, Wo, S, stride, pad, dil, M, RSC,
+             make_fastdiv(C), make_fastdiv(S), make_fastdiv(Ho * Wo), make_fastdiv(Wo)};
+    launch(a, b, e, M, K, RSC, 1, st);
+  }
 }
 
-// Weight gradient: dw[K][R*S*C] (fp32, accumulated with atomics unless splits == 1 and mode 0)
+// Weight gradient: dw[K][R*S*C] fp32 (+)= dY^T . im2col(x); split-K through fp32 slabs in `ws`
 void launch_conv_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int C, int K, int R,
-                       int S, int stride, int pad, int dil, int Ho, int Wo, int splits, hipStream_t st) {
+                       int S, int stride, int pad, int dil, int Ho, int Wo, int splits, bool accumulate, float* ws,
+                       hipStream_t st) {
   const int M = N * Ho * Wo;  // reduction dim
   MNMajorK a{dy, (long)K, K, M};
   ConvWgB b{x, N, H, W, C, Ho, Wo, S, stride, pad, dil, R * S * C, M,
             make_fastdiv(C), make_fastdiv(S), make_fastdiv(Ho * Wo), make_fastdiv(Wo)};
-  if (splits <= 0) splits = gemm_choose_splits(K, R * S * C, M);
-  Epi e = make_epi(dw, (long)R * S * C, true, nullptr, 0, nullptr, splits > 1 ? 2 : 0, 1.f);
-  launch(a, b, e, K, R * S * C, M, splits, st);
+  splits = effective_splits(M, splits);
+  const int RSC = R * S * C;
+  const bool slab = splits > 1;
+  Epi e = make_epi(slab ? (void*)ws : (void*)dw, (long)RSC, true, nullptr, 0, nullptr, slab ? 3 : (accumulate ? 1 : 0),
+                   1.f);
+  e.slab = (long)K * RSC;
+  launch(a, b, e, K, RSC, M, splits, st);
+  if (slab) splitk_reduce(ws, splits, (long)K * RSC, dw, accumulate, st);
 }
 
 // dgrad weight transform: w2[c][r][s][k] = w[k][R-1-r][S-1-s][c]

@@ -51,12 +51,14 @@ void launch_xent_bwd(const void* logits, bool bf16, const int64_t* labels, const
 int gemm_choose_splits(int M, int N, int K);
 void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                  long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
-                 float alpha, int splits, hipStream_t st);
+                 float alpha, int splits, float* ws, hipStream_t st);
+long gemm_splitk_workspace(int M, int N, int splits);  // fp32 elements of the split-K slab workspace
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int K,
                      int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
                      int mode, float* stats, hipStream_t st);
 void launch_conv_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int C, int K, int R,
-                       int S, int stride, int pad, int dil, int Ho, int Wo, int splits, hipStream_t st);
+                       int S, int stride, int pad, int dil, int Ho, int Wo, int splits, bool accumulate, float* ws,
+                       hipStream_t st);
 void launch_conv_dgrad_wtrans(const uint16_t* w, uint16_t* w2, int K, int R, int S, int C, hipStream_t st);
 
 // elementwise.hip
@@ -73,25 +75,26 @@ void launch_colsum(const uint16_t* x, long R, int C, float* work, float* out, bo
 struct AttnFwdArgs {
   const uint16_t *q, *k, *v;
   uint16_t* o;
-  float* lse;          // [B, Hq, Sq]: m + log2(l) in the exp2 domain (scores scaled by scale*log2(e))
+  float* lse;          // [B, Hq, lse_ld]: m + log2(l) in the exp2 domain (scores scaled by scale*log2(e))
   const int* kv_lens;  // [B] or null
   long sqb, sqs, sqh, skb, sks, skh, svb, svs, svh, sob, sos, soh;
+  long lse_ld;         // row stride of lse (Sq rounded up to 64)
   int B, Sq, Sk, Hq, Hkv, causal;
   float scale_log2;
 };
 struct AttnBwdArgs {
   const uint16_t *q, *k, *v, *dO;
   const float* lse;
-  float* delta;  // [B, Hq, Sq] scratch
-  float* dq;     // [B, Sq, Hq, D] fp32 accumulator (zeroed)
+  float* delta;       // [B, Hq, lse_ld] scratch
+  uint16_t* dq;       // [B, Sq, Hq, D]
   uint16_t *dk, *dv;  // [B, Sk, Hkv, D]
   const int* kv_lens;
   long sqb, sqs, sqh, skb, sks, skh, svb, svs, svh, sdb, sds, sdh;
+  long lse_ld;
   int B, Sq, Sk, Hq, Hkv, causal;
   float scale_log2, scale;
 };
 void launch_flash_fwd(const AttnFwdArgs& a, int D, hipStream_t st);
-void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, long sos, long soh, uint16_t* dq_out,
-                      hipStream_t st);
+void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, long sos, long soh, hipStream_t st);
 
 }  // namespace k8s_amd

@@ -243,20 +243,18 @@ Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tens
   }
   if (bias) TORCH_CHECK(bias->numel() == N && bias->scalar_type() == at::kFloat && bias->is_contiguous());
   if (pre) TORCH_CHECK(pre->numel() == M * N && pre->scalar_type() == at::kBFloat16 && pre->is_contiguous());
-  int mode = accumulate ? 1 : 0;
+  const int mode = accumulate ? 1 : 0;
   int sp = (int)splits;
-  if (sp != 1 && out_f32 && !bias && act == 0 && !pre) {
+  if (sp != 1 && out_f32 && !bias && act == 0 && !pre && N % 4 == 0) {
     if (sp <= 0) sp = k8s_amd::gemm_choose_splits((int)M, (int)N, (int)K);
-    if (sp > 1) {
-      if (!accumulate) c.zero_();
-      mode = 2;
-    }
   } else {
     sp = 1;
   }
+  Tensor ws;
+  if (sp > 1) ws = torch::empty({k8s_amd::gemm_splitk_workspace((int)M, (int)N, sp)}, a.options().dtype(at::kFloat));
   k8s_amd::launch_gemm(cbf(a), a.stride(0), a_kmajor, cbf(b), b.stride(0), b_kmajor, c.data_ptr(), N, out_f32,
                        (int)M, (int)N, (int)K, bias ? bias->data_ptr<float>() : nullptr, (int)act,
-                       pre ? bf(*pre) : nullptr, mode, (float)alpha, sp, cur_stream());
+                       pre ? bf(*pre) : nullptr, mode, (float)alpha, sp, sp > 1 ? f32(ws) : nullptr, cur_stream());
   return c;
 }
 
@@ -270,7 +268,7 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, bo
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int K = w.size(0), R = w.size(1), S = w.size(2);
   TORCH_CHECK(w.size(3) == C, "channel mismatch");
-  TORCH_CHECK(C % 64 == 0, "implicit-GEMM conv needs C % 64 == 0");
+  TORCH_CHECK(C % 8 == 0, "implicit-GEMM conv needs C % 8 == 0");
   TORCH_CHECK(K % 8 == 0, "output channels must be a multiple of 8");
   const int Ho = conv_out(H, R, stride, pad, dil), Wo = conv_out(W, S, stride, pad, dil);
   auto y = torch::empty({N, Ho, Wo, K}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
@@ -294,10 +292,10 @@ void conv_wgrad(Tensor x, Tensor dy, Tensor dw, int64_t stride, int64_t pad, int
   const int Ho = conv_out(H, R, stride, pad, dil), Wo = conv_out(W, S, stride, pad, dil);
   TORCH_CHECK(dy.size(0) == N && dy.size(1) == Ho && dy.size(2) == Wo && dy.size(3) == K, "dy shape mismatch");
   int sp = splits <= 0 ? k8s_amd::gemm_choose_splits(K, R * S * C, N * Ho * Wo) : (int)splits;
-  if (sp > 1 && !accumulate) dw.zero_();
-  TORCH_CHECK(sp > 1 || !accumulate, "accumulate needs split-K atomics");
+  Tensor ws;
+  if (sp > 1) ws = torch::empty({k8s_amd::gemm_splitk_workspace(K, R * S * C, sp)}, dw.options());
   k8s_amd::launch_conv_wgrad(cbf(x), cbf(dy), f32(dw), N, H, W, C, K, R, S, (int)stride, (int)pad, (int)dil, Ho, Wo,
-                             sp, cur_stream());
+                             sp, accumulate, sp > 1 ? f32(ws) : nullptr, cur_stream());
 }
 
 Tensor conv_dgrad_wtrans(Tensor w) {
@@ -391,13 +389,15 @@ std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, bool causal, c10::op
   TORCH_CHECK(Hkv > 0 && Hq % Hkv == 0, "Hq must be a multiple of Hkv");
   TORCH_CHECK(Sq > 0 && Sk > 0, "empty sequence");
   auto o = torch::empty({B, Sq, Hq, D}, q.options());
-  auto lse = torch::empty({B, Hq, Sq}, q.options().dtype(at::kFloat));
+  const long ld = (Sq + 63) / 64 * 64;  // padded rows: the backward stages 64-query slices with 16-B copies
+  auto lse = torch::empty({B, Hq, ld}, q.options().dtype(at::kFloat));
   k8s_amd::AttnFwdArgs a;
   a.q = cbf(q); a.k = cbf(k); a.v = cbf(v); a.o = bf(o); a.lse = f32(lse); a.kv_lens = kv_lens_ptr(kv_lens, B);
   a.sqb = q.stride(0); a.sqs = q.stride(1); a.sqh = q.stride(2);
   a.skb = k.stride(0); a.sks = k.stride(1); a.skh = k.stride(2);
   a.svb = v.stride(0); a.svs = v.stride(1); a.svh = v.stride(2);
   a.sob = o.stride(0); a.sos = o.stride(1); a.soh = o.stride(2);
+  a.lse_ld = ld;
   a.B = B; a.Sq = Sq; a.Sk = Sk; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal;
   a.scale_log2 = (float)(scale * 1.4426950408889634);
   k8s_amd::launch_flash_fwd(a, (int)D, cur_stream());
@@ -414,15 +414,17 @@ std::vector<Tensor> flash_bwd(Tensor dO, Tensor q, Tensor k, Tensor v, Tensor o,
   TORCH_CHECK(dO.sizes() == q.sizes() && o.sizes() == q.sizes(), "dO / o must match q");
   TORCH_CHECK(Hq % Hkv == 0, "Hq must be a multiple of Hkv");
   check_cuda(lse, "lse"); check_dtype(lse, at::kFloat, "lse");
-  TORCH_CHECK(lse.numel() == B * Hq * Sq, "lse must be [B, Hq, Sq]");
-  auto dq_acc = torch::zeros({B, Sq, Hq, D}, q.options().dtype(at::kFloat));
-  auto delta = torch::empty({B, Hq, Sq}, q.options().dtype(at::kFloat));
+  const long ld = (Sq + 63) / 64 * 64;
+  TORCH_CHECK(lse.dim() == 3 && lse.size(0) == B && lse.size(1) == Hq && lse.size(2) == ld,
+              "lse must be the [B, Hq, round_up(Sq, 64)] tensor flash_fwd returned");
+  auto delta = torch::empty({B, Hq, ld}, q.options().dtype(at::kFloat));
   auto dq = torch::empty({B, Sq, Hq, D}, q.options());
   auto dk = torch::empty({B, Sk, Hkv, D}, q.options());
   auto dv = torch::empty({B, Sk, Hkv, D}, q.options());
   k8s_amd::AttnBwdArgs a;
   a.q = cbf(q); a.k = cbf(k); a.v = cbf(v); a.dO = cbf(dO); a.lse = f32(lse); a.delta = f32(delta);
-  a.dq = f32(dq_acc); a.dk = bf(dk); a.dv = bf(dv); a.kv_lens = kv_lens_ptr(kv_lens, B);
+  a.dq = bf(dq); a.dk = bf(dk); a.dv = bf(dv); a.kv_lens = kv_lens_ptr(kv_lens, B);
+  a.lse_ld = ld;
   a.sqb = q.stride(0); a.sqs = q.stride(1); a.sqh = q.stride(2);
   a.skb = k.stride(0); a.sks = k.stride(1); a.skh = k.stride(2);
   a.svb = v.stride(0); a.svs = v.stride(1); a.svh = v.stride(2);
@@ -430,7 +432,7 @@ std::vector<Tensor> flash_bwd(Tensor dO, Tensor q, Tensor k, Tensor v, Tensor o,
   a.B = B; a.Sq = Sq; a.Sk = Sk; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal;
   a.scale_log2 = (float)(scale * 1.4426950408889634);
   a.scale = (float)scale;
-  k8s_amd::launch_flash_bwd(a, (int)D, cbf(o), o.stride(0), o.stride(1), o.stride(2), bf(dq), cur_stream());
+  k8s_amd::launch_flash_bwd(a, (int)D, cbf(o), o.stride(0), o.stride(1), o.stride(2), cur_stream());
   return {dq, dk, dv};
 }
 

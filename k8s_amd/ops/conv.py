@@ -2,14 +2,15 @@
 
 Activations NHWC bf16, weights KRSC bf16. Per product:
 
-    fwd    y  = conv(x, w)                  ConvA implicit im2col (C % 64 == 0)
+    fwd    y  = conv(x, w)                  ConvA implicit im2col (C % 64 == 0; per-16-B-unit decode for
+                                            other C % 8 == 0, e.g. the 8-channel stem)
     wgrad  dw = dy^T . im2col(x)            fp32, split-K atomics, written straight into the
                                             parameter's flat gradient slot
     dgrad  1x1, stride 1: dx = dy . w       plain GEMM, w read N-major (no transpose)
            RxS, stride 1: dx = conv(dy, w') w' = spatially flipped, in/out-swapped w
                                             (tiny per-step transform), pad' = R-1-pad
 
-Shapes outside those rules (the 8-channel stem, stride-2 dgrad) and CPU
+Shapes outside those rules (stride-2 dgrad) and CPU
 tensors run through ATen's convolution on a channels-last view (MIOpen on
 ROCm). Where both paths can run a shape, ``ops.autotune`` times them once on
 the real tensors (the vendor forward is charged for the extra BatchNorm
@@ -40,7 +41,7 @@ def _hip(*ts):
 
 
 def fwd_ok(x, w):
-    return _hip(x, w) and x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0
+    return _hip(x, w) and x.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0
 
 
 def _key(op, x, w, stride, padding):

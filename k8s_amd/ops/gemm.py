@@ -10,7 +10,13 @@ products with it WITHOUT materialising any transpose:
     wgrad  dW = g^T . x          A = g   read M-major,   B = x read N-major  (split-K, fp32 out
                                                              straight into the flat gradient slot)
 
-CPU tensors (and shapes the kernel does not take) use plain PyTorch.
+Where the vendor library (hipBLASLt behind torch.matmul / addmm) can run the
+same plain product, ``ops.autotune`` times both once per shape and keeps the
+faster; fused epilogues the library lacks (GELU with the pre-activation side
+output, fp32 split-K accumulation straight into the flat gradient slot) are
+charged the extra elementwise / cast passes the library path needs, so the
+comparison is end to end. CPU tensors (and shapes the kernel does not take)
+use plain PyTorch.
 """
 from __future__ import annotations
 
@@ -19,6 +25,7 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
+from k8s_amd.ops import autotune
 from k8s_amd.ops._ext import load as _load
 
 ACT = {None: 0, "relu": 1, "gelu": 2}
@@ -65,14 +72,30 @@ def _act_bwd(gy, pre_or_out, act):
     raise ValueError(act)
 
 
+def _blas_fwd(x, w, b, act):
+    y = torch.addmm(b.to(x.dtype), x, w.t()) if b is not None else torch.mm(x, w.t())
+    pre = y
+    y = _act_fwd(y, act)
+    return y, (pre if act == "gelu" else (y if act == "relu" else None))
+
+
+def _hip_fwd(x, w, b, act):
+    M, N = x.shape[0], w.shape[0]
+    pre = torch.empty((M, N), device=x.device, dtype=torch.bfloat16) if act == "gelu" else None
+    y = mm(x, w, True, True, bias=b, act=act, pre=pre)
+    return y, (pre if act == "gelu" else (y if act == "relu" else None))
+
+
 def linear_fwd(x, w, b, act=None):
     """Returns (y, saved) where saved is what linear_bwd needs for the activation derivative."""
     M, K = x.shape
     N = w.shape[0]
     if hip_ok(x, w) and _shape_ok(M, N, K) and x.stride(1) == 1:
-        pre = torch.empty((M, N), device=x.device, dtype=torch.bfloat16) if act == "gelu" else None
-        y = mm(x, w, True, True, bias=b, act=act, pre=pre)
-        return y, (pre if act == "gelu" else (y if act == "relu" else None))
+        key = "linear_fwd|%dx%dx%d|%s|%d" % (M, N, K, act, b is not None)
+        if autotune.choose(key, [("hip", lambda: _hip_fwd(x, w, b, act)),
+                                 ("blas", lambda: _blas_fwd(x, w, b, act))]) == "hip":
+            return _hip_fwd(x, w, b, act)
+        return _blas_fwd(x, w, b, act)
     y = torch.matmul(x, w.t())
     if b is not None:
         y = y + b.to(y.dtype)
@@ -93,10 +116,29 @@ def linear_bwd(gy, x, w, saved, act, pw=None, store=None):
     else:
         db = g.float().sum(0)
     if hip_ok(g, x, w) and _shape_ok(M, N, K) and N % 64 == 0:
-        dx = mm(g, w, True, False)
+        g = g.contiguous()
+        dims = "%dx%dx%d" % (M, N, K)
+        if autotune.choose("linear_dgrad|" + dims, [("hip", lambda: mm(g, w, True, False)),
+                                                    ("blas", lambda: torch.mm(g, w))]) == "hip":
+            dx = mm(g, w, True, False)
+        else:
+            dx = torch.mm(g, w)
         if pw is not None and store is not None and pw.grad.dtype == torch.float32:
             acc = pw.written
-            mm(g, x, False, False, out=pw.grad, out_f32=True, accumulate=acc, splits=0)
+
+            def hip_w(out, accumulate):
+                mm(g, x, False, False, out=out, out_f32=True, accumulate=accumulate, splits=0)
+
+            def blas_w(out, accumulate):
+                d = torch.mm(g.t(), x)
+                out.add_(d) if accumulate else out.copy_(d)
+
+            if autotune.choose("linear_wgrad|" + dims, [
+                    ("hip", lambda: hip_w(torch.empty_like(pw.grad), False)),
+                    ("blas", lambda: blas_w(torch.empty_like(pw.grad), False))]) == "hip":
+                hip_w(pw.grad, acc)
+            else:
+                blas_w(pw.grad, acc)
             if acc:
                 store._notify(pw)
             else:

@@ -35,6 +35,15 @@ def _conv_impl():
     return _conv
 
 
+def _zero_scratch(store, device, n):
+    from k8s_amd.parallel.flat import ZeroArena
+
+    arena = store.__dict__.get("zero_arena")
+    if arena is None or arena.device != torch.device(device):
+        arena = store.zero_arena = ZeroArena(device)
+    return arena.take(n)
+
+
 class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, p, stride, padding, with_stats):
@@ -42,7 +51,8 @@ class _Conv2dNHWC(torch.autograd.Function):
         w = p.weight if x.dtype == p.weight.dtype else p.master.to(x.dtype)
         sums = None
         if with_stats and impl.fwd_uses_hip(x, w, stride, padding):
-            sums = torch.zeros(_C().conv_stat_replicas, 2, w.shape[0], device=x.device, dtype=torch.float32)
+            sums = _zero_scratch(p.store, x.device, _C().conv_stat_replicas * 2 * w.shape[0]).view(
+                _C().conv_stat_replicas, 2, w.shape[0])
         y = impl.conv_fwd(x, w, stride, padding, sums)
         ctx.save_for_backward(x)
         ctx.p, ctx.stride, ctx.padding = p, stride, padding

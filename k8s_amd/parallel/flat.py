@@ -96,6 +96,34 @@ def init_const(v: float) -> Callable:
     return f
 
 
+class ZeroArena:
+    """Per-step bump allocator of ZEROED fp32 scratch (e.g. the conv epilogue's BatchNorm statistics
+    accumulators): one fill kernel per step at ``reset()`` instead of a tiny ``torch.zeros`` launch per layer.
+    Slices handed out in a step stay valid until the next ``reset()`` (stream-ordered)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.buf: Optional[torch.Tensor] = None
+        self.off = 0
+        self.dirty = 0
+
+    def take(self, n: int) -> torch.Tensor:
+        n = _round_up(n)
+        if self.buf is None or self.off + n > self.buf.numel():
+            cap = max(1 << 16, 2 * (self.off + n))
+            self.buf = torch.zeros(cap, dtype=torch.float32, device=self.device)  # old slices keep the old buffer
+            self.off = self.dirty = 0
+        t = self.buf[self.off:self.off + n]
+        self.off += n
+        self.dirty = max(self.dirty, self.off)
+        return t
+
+    def reset(self):
+        if self.buf is not None and self.dirty:
+            self.buf[:self.dirty].zero_()
+        self.off = self.dirty = 0
+
+
 class ParamStore:
     """Owns the flat master / low-precision / gradient buffers of one model."""
 
@@ -164,6 +192,9 @@ class ParamStore:
     def begin_step(self):
         for p in self.params:
             p.written = False
+        arena = self.__dict__.get("zero_arena")
+        if arena is not None:
+            arena.reset()
 
     def deposit(self, p: Param, g: torch.Tensor):
         """Write (first use in this step) or accumulate a parameter gradient into its slot."""

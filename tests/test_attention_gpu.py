@@ -65,4 +65,4 @@ def test_flash_lse(cuda):
     o, lse = load().flash_fwd(q, k, v, False, None, 0.1)
     s = torch.einsum("bqhd,bkhd->bhqk", q.float(), k.float()) * 0.1
     ref = torch.logsumexp(s, -1) / math.log(2.0)  # the kernel stores log2-domain lse
-    _close(lse, ref, 1e-3, "lse")
+    _close(lse[..., :S], ref, 1e-3, "lse")

@@ -83,7 +83,10 @@ CONV_CASES = [
 ]
 
 
-@pytest.mark.parametrize("case", CONV_CASES)
+SMALL_C_CASES = [(2, 32, 32, 8, 64, 7, 2, 3), (2, 15, 13, 24, 40, 3, 1, 1), (1, 9, 9, 8, 16, 1, 1, 0)]
+
+
+@pytest.mark.parametrize("case", CONV_CASES + SMALL_C_CASES)
 def test_conv_fwd(cuda, case):
     N, H, W, C, K, R, st, pad = case
     torch.manual_seed(3)
@@ -126,7 +129,7 @@ def test_conv_dgrad_stride1(cuda, case):
     assert _rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
 
 
-@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("case", CONV_CASES + SMALL_C_CASES[:1])
 def test_conv_fwd_bn_stats_epilogue(cuda, case):
     N, H, W, C, K, R, st, pad = case
     torch.manual_seed(6)
