@@ -97,4 +97,10 @@ struct AttnBwdArgs {
 void launch_flash_fwd(const AttnFwdArgs& a, int D, hipStream_t st);
 void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, long sos, long soh, hipStream_t st);
 
+// ---- NHWC max pooling (pool.hip): idx = winning window position per output element (uint8)
+void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
+                        int k, int s, int p, hipStream_t st);
+void launch_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W, int C, int Ho,
+                        int Wo, int k, int s, int p, hipStream_t st);
+
 }  // namespace k8s_amd

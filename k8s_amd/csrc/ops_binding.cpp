@@ -436,6 +436,32 @@ std::vector<Tensor> flash_bwd(Tensor dO, Tensor q, Tensor k, Tensor v, Tensor o,
   return {dq, dk, dv};
 }
 
+// ------------------------------------------------------------------ max pooling (NHWC)
+std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t p) {
+  check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "x must be NHWC with C % 8 == 0");
+  TORCH_CHECK(k <= 15 && p < k, "window too large");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
+  auto y = torch::empty({N, Ho, Wo, C}, x.options());
+  auto idx = torch::empty({N, Ho, Wo, C}, x.options().dtype(at::kByte));
+  k8s_amd::launch_maxpool_fwd(cbf(x), bf(y), idx.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, (int)k, (int)s, (int)p,
+                              cur_stream());
+  return {y, idx};
+}
+
+Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, int64_t s, int64_t p) {
+  check_cuda(dy, "dy"); check_dtype(dy, at::kBFloat16, "dy");
+  check_cuda(idx, "idx"); check_dtype(idx, at::kByte, "idx");
+  TORCH_CHECK(dy.sizes() == idx.sizes() && dy.dim() == 4 && dy.size(3) % 8 == 0, "dy / idx mismatch");
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), C = dy.size(3);
+  TORCH_CHECK(Ho == (H + 2 * p - k) / s + 1 && Wo == (W + 2 * p - k) / s + 1, "input size mismatch");
+  auto dx = torch::empty({N, H, W, C}, dy.options());
+  k8s_amd::launch_maxpool_bwd(cbf(dy), idx.data_ptr<uint8_t>(), bf(dx), N, (int)H, (int)W, C, Ho, Wo, (int)k,
+                              (int)s, (int)p, cur_stream());
+  return dx;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -462,6 +488,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_dgrad_wtrans", &conv_dgrad_wtrans);
   m.def("flash_fwd", &flash_fwd);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
   m.def("flash_bwd", &flash_bwd);
   m.attr("conv_stat_replicas") = k8s_amd::kConvStatReplicas;
   m.attr("arch") = "gfx950";

@@ -291,7 +291,25 @@ def cross_entropy(logits, labels, ignore_index: int = -100, smoothing: float = 0
 
 
 # =========================================================================== pooling (NHWC)
+class _MaxPoolNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        y, idx = _C().maxpool_fwd(x.contiguous(), k, s, p)
+        ctx.save_for_backward(idx)
+        ctx.hw, ctx.ksp = x.shape[1:3], (k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        H, W = ctx.hw
+        return _C().maxpool_bwd(dy.contiguous(), idx, H, W, *ctx.ksp), None, None, None
+
+
 def max_pool_nhwc(x, k=3, s=2, p=1):
+    """NHWC max pooling; GPU: gfx950 kernel saving the winning window position as uint8 (gather backward)."""
+    if _gpu(x) and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0:
+        return _MaxPoolNHWC.apply(x, k, s, p)
     y = F.max_pool2d(x.permute(0, 3, 1, 2), k, s, p)
     return y.permute(0, 2, 3, 1).contiguous()
 

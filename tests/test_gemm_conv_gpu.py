@@ -175,3 +175,21 @@ def test_elementwise_kernels(cuda):
     assert _rel(_C().gelu_bwd(d, pre), pp.grad) < 1e-2
     assert _rel(_C().relu_bwd(d, torch.relu(pre)), d.float() * (pre.float() > 0)) < 1e-3
     assert _rel(_C().colsum(d), d.float().sum(0)) < 1e-3
+
+
+@pytest.mark.parametrize("shape,ksp", [((2, 112, 112, 64), (3, 2, 1)), ((3, 9, 7, 16), (3, 2, 1)),
+                                       ((2, 8, 8, 8), (2, 2, 0))])
+def test_maxpool_nhwc(cuda, shape, ksp):
+    from k8s_amd.ops import nn as K
+
+    torch.manual_seed(9)
+    k, s, p = ksp
+    x = torch.randn(*shape, device=cuda).bfloat16().requires_grad_(True)
+    y = K.max_pool_nhwc(x, k, s, p)
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.max_pool2d(xr, k, s, p)
+    assert torch.equal(y.float(), yr.permute(0, 2, 3, 1))
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    assert _rel(x.grad, xr.grad.permute(0, 2, 3, 1)) < 1e-2
