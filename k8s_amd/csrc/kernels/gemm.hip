@@ -32,9 +32,8 @@
 
 namespace k8s_amd {
 
-constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int BM = 128, BN = 128, BK = 64;  // the general tile (split-K sizing); see gemm_bf16_kernel
 constexpr int GEMM_THREADS = 256;
-constexpr int TILE_BYTES = BM * BK * 2;  // 16 KB per operand tile
 
 // 16-byte zero line for out-of-image implicit-GEMM loads
 __device__ __attribute__((aligned(64))) uint16_t g_zero_page[64];
@@ -226,12 +225,20 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 // 2 blocks/CU. NBUF = 1: single buffer, 32 KB LDS, 3 blocks/CU -- for short K ranges (K <= 128: the
 // memory-bound 1x1 convolutions of the early ResNet stages), where there is no next tile to prefetch and
 // block-level overlap is what hides HBM latency.
-template <class ASrc, class BSrc, int NBUF>
+//
+// WM x WN waves (WM * WN = 4), each owning a 64 x 64 piece: 128 x 128 tiles (2 x 2) in general, 256 x 64
+// (4 x 1) when N = 64 (the early ResNet convolutions and the stem) so no MFMA work is spent on padding.
+// Only K-major sources may sit on a 64-wide side (the MN-major swizzle assumes 256-B rows).
+template <class ASrc, class BSrc, int NBUF, int WM = 2, int WN = 2>
 __global__ void __launch_bounds__(GEMM_THREADS, NBUF == 1 ? 3 : 2)
 gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
-  __shared__ __attribute__((aligned(1024))) char smem[NBUF * 2 * TILE_BYTES];  // [buf][A|B]
+  constexpr int BM = 64 * WM, BN = 64 * WN;
+  constexpr int TA = BM * BK * 2, TB = BN * BK * 2;  // operand tile bytes
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert((WM == 2 || ASrc::kmajor) && (WN == 2 || BSrc::kmajor), "MN-major operands need a 128 side");
+  __shared__ __attribute__((aligned(1024))) char smem[NBUF * (TA + TB)];  // [buf][A|B]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
 
   // ---- XCD-aware bijective remap, then grouped (GROUP_M = 8) tile order
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
@@ -261,15 +268,17 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
 
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);  // provably wave-uniform for the M0 (LDS base) operand
   auto stage = [&](int buf, int k0) {
-    char* ta = smem + buf * 2 * TILE_BYTES;
-    char* tb = ta + TILE_BYTES;
+    char* ta = smem + buf * (TA + TB);
+    char* tb = ta + TA;
 #pragma unroll
-    for (int rd = 0; rd < 4; ++rd) {
+    for (int rd = 0; rd < TA / (16 * GEMM_THREADS); ++rd) {
       const int s = rd * GEMM_THREADS + tid;
-      char* wave_base_a = ta + (rd * GEMM_THREADS + wid_u * 64) * 16;
-      char* wave_base_b = tb + (rd * GEMM_THREADS + wid_u * 64) * 16;
-      glds16(A.src(s, m0, k0), wave_base_a);
-      glds16(B.src(s, n0, k0), wave_base_b);
+      glds16(A.src(s, m0, k0), ta + (rd * GEMM_THREADS + wid_u * 64) * 16);
+    }
+#pragma unroll
+    for (int rd = 0; rd < TB / (16 * GEMM_THREADS); ++rd) {
+      const int s = rd * GEMM_THREADS + tid;
+      glds16(B.src(s, n0, k0), tb + (rd * GEMM_THREADS + wid_u * 64) * 16);
     }
   };
 
@@ -289,8 +298,8 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
     } else if (t + 1 < nt) {
       stage(cur ^ 1, kbeg + (t + 1) * BK);
     }
-    const char* ta = smem + cur * 2 * TILE_BYTES;
-    const char* tb = ta + TILE_BYTES;
+    const char* ta = smem + cur * (TA + TB);
+    const char* tb = ta + TA;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       mfma_bf16x8 af[4], bfv[4];
@@ -397,7 +406,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
     // lanes with equal (lane >> 4) hold the same 4 columns: reduce over the 16 row lanes, then over the two
     // row-waves through LDS, so the block issues 4 full-wave atomic instructions (256 columns x {sum, sumsq})
     // instead of 128 quarter-empty ones -- float atomics cost ~50 ns per wave-instruction per CU.
-    float* red = reinterpret_cast<float*>(smem);  // [wm][2][128]; the K loop's last barrier freed the tiles
+    float* red = reinterpret_cast<float*>(smem);  // [wm][2][BN]; the K loop's last barrier freed the tiles
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
 #pragma unroll
@@ -410,17 +419,21 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
         }
         if ((lane & 15) == 0) {
           const int col = wn * 64 + j * 16 + (lane >> 4) * 4 + r;
-          red[(wm * 2 + 0) * 128 + col] = a;
-          red[(wm * 2 + 1) * 128 + col] = b;
+          red[(wm * 2 + 0) * BN + col] = a;
+          red[(wm * 2 + 1) * BN + col] = b;
         }
       }
     }
     __syncthreads();
-    const int col = tid & 127, which = tid >> 7;
-    const int n = n0 + col;
-    if (n < N) {
-      const float v = red[which * 128 + col] + red[(2 + which) * 128 + col];
-      atomicAdd(E.stats + (long)(tm % STAT_REPL) * 2 * N + (long)which * N + n, v);
+    if (tid < 2 * BN) {
+      const int col = tid % BN, which = tid / BN;
+      const int n = n0 + col;
+      if (n < N) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) v += red[(w * 2 + which) * BN + col];
+        atomicAdd(E.stats + (long)(tm % STAT_REPL) * 2 * N + (long)which * N + n, v);
+      }
     }
   }
 }
@@ -433,17 +446,29 @@ static int effective_splits(int K, int splits) {
   return (K + kps - 1) / kps;
 }
 
+template <class ASrc, class BSrc, int WM, int WN>
+static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
+                         hipStream_t st) {
+  const int tiles = ((M + 64 * WM - 1) / (64 * WM)) * ((N + 64 * WN - 1) / (64 * WN));
+  if (kps <= 2 * BK)
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN>), dim3(tiles, 1, splits), dim3(GEMM_THREADS), 0, st,
+                       a, b, e, M, N, K, kps);
+  else
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2, WM, WN>), dim3(tiles, 1, splits), dim3(GEMM_THREADS), 0, st,
+                       a, b, e, M, N, K, kps);
+}
+
 template <class ASrc, class BSrc>
 static void launch(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int splits, hipStream_t st) {
-  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const int kps = ((K + splits - 1) / splits + BK - 1) / BK * BK;
   splits = (K + kps - 1) / kps;
-  if (kps <= 2 * BK)
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1>), dim3(tiles, 1, splits), dim3(GEMM_THREADS), 0, st, a, b, e,
-                       M, N, K, kps);
-  else
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2>), dim3(tiles, 1, splits), dim3(GEMM_THREADS), 0, st, a, b, e,
-                       M, N, K, kps);
+  if constexpr (ASrc::kmajor && BSrc::kmajor) {
+    if (N <= 64) {  // 256 x 64 tiles: no half-empty 128-wide column tile
+      launch_tiles<ASrc, BSrc, 4, 1>(a, b, e, M, N, K, kps, splits, st);
+      return;
+    }
+  }
+  launch_tiles<ASrc, BSrc, 2, 2>(a, b, e, M, N, K, kps, splits, st);
 }
 
 static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act, uint16_t* pre, int mode,
