@@ -31,12 +31,12 @@ class BN(nn.Module):
         self.register_buffer("running_var", torch.ones(c))
         self.momentum, self.eps = 0.1, 1e-5
 
-    def forward(self, x, residual=None, relu=True):
+    def forward(self, x, residual=None, relu=True, res_link=None):
         sums = None
         if isinstance(x, tuple):  # (conv output, fused statistics)
             x, sums = x
         return K.batch_norm_act(x, self.gamma, self.beta, self.running_mean, self.running_var, residual, relu,
-                                self.training, self.momentum, self.eps, sums=sums)
+                                self.training, self.momentum, self.eps, sums=sums, res_link=res_link)
 
 
 class Conv(nn.Module):
@@ -45,9 +45,9 @@ class Conv(nn.Module):
         self.w = store.new(name + ".weight", (cout, k, k, cin), init_kaiming_normal(cin * k * k))
         self.stride, self.pad = stride, k // 2
 
-    def forward(self, x):
+    def forward(self, x, grad_link=None):
         # BN statistics are accumulated in the conv epilogue (returned alongside y)
-        return K.conv2d_nhwc(x, self.w, self.stride, self.pad, with_stats=True)
+        return K.conv2d_nhwc(x, self.w, self.stride, self.pad, with_stats=True, grad_link=grad_link)
 
 
 class Bottleneck(nn.Module):
@@ -69,11 +69,14 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         idn = x
-        y = self.bn1(self.conv1(x))
+        # identity block: x's two gradient contributions (residual via bn3, main path via conv1) are summed
+        # inside conv1's dgrad epilogue instead of by a separate elementwise add
+        link = K.GradLink() if (self.down is None and x.requires_grad) else None
+        y = self.bn1(self.conv1(x, grad_link=link))
         y = self.bn2(self.conv2(y))
         if self.down is not None:
             idn = self.down_bn(self.down(x), relu=False)
-        return self.bn3(self.conv3(y), residual=idn, relu=True)
+        return self.bn3(self.conv3(y), residual=idn, relu=True, res_link=link)
 
 
 class ResNet(nn.Module):

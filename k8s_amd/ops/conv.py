@@ -92,17 +92,25 @@ def _wgrad_hip(C_, gy, x, out, stride, padding, acc):
         C_.conv_wgrad(x, gy, out, stride, padding, 1, 0, acc)
 
 
-def _dgrad_hip(C_, gy, w, padding):
+def _dgrad_hip(C_, gy, w, padding, addend=None):
+    """dx on our kernels; with ``addend`` (bf16, shape of dx) a 1x1 dgrad accumulates onto it in the GEMM
+    epilogue and returns it (the fused residual-gradient add)."""
     K, R, S, C = w.shape
     if R == 1 and S == 1 and padding == 0:
         N, H, W_, _ = gy.shape
+        if addend is not None:
+            C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, addend.view(-1, C), False, None, 0, None, True,
+                    1.0, 1)
+            return addend
         return C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, None, False, None, 0, None, False, 1.0,
                        1).reshape(N, H, W_, C)
-    return C_.conv_fwd(gy, C_.conv_dgrad_wtrans(w), 1, R - 1 - padding, 1, False, None, 0, None)
+    dx = C_.conv_fwd(gy, C_.conv_dgrad_wtrans(w), 1, R - 1 - padding, 1, False, None, 0, None)
+    return dx if addend is None else dx.add_(addend)
 
 
-def conv_bwd(gy, x, w, stride, padding, need_dx, p=None):
-    """Returns dx (or None); deposits dw into ``p``'s flat gradient slot."""
+def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None):
+    """Returns dx (+ ``addend``, e.g. the residual branch's gradient of the same tensor, fused into the
+    dgrad epilogue where our kernel runs) or None; deposits dw into ``p``'s flat gradient slot."""
     K, R, S, C = w.shape
     C_ = _load() if gy.is_cuda else None
     hip = _hip(gy, x, w)
@@ -127,15 +135,22 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None):
     if need_dx:
         use_hip = False
         if hip and stride == 1 and K % 64 == 0 and C % 8 == 0:
-            use_hip = autotune.choose(_key("conv_dgrad", x, w, stride, padding), [
-                ("hip", lambda: _dgrad_hip(C_, gy, w, padding)),
-                ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, True, False))]) == "hip"
+            if addend is None:
+                use_hip = autotune.choose(_key("conv_dgrad", x, w, stride, padding), [
+                    ("hip", lambda: _dgrad_hip(C_, gy, w, padding)),
+                    ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, True, False))]) == "hip"
+            else:  # compare the fused accumulate against the vendor dgrad + a separate add
+                use_hip = autotune.choose(_key("conv_dgrad_acc", x, w, stride, padding), [
+                    ("hip", lambda: _dgrad_hip(C_, gy, w, padding, torch.empty_like(addend))),
+                    ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, True, False)[0].add_(addend))]) == "hip"
         if use_hip:
             STATS["hip_dgrad"] += 1
-            dx = _dgrad_hip(C_, gy, w, padding)
+            dx = _dgrad_hip(C_, gy, w, padding, addend)
         else:
             STATS["aten_dgrad"] += 1
             dx, _ = _aten_bwd(gy, x, w, stride, padding, True, False)
+            if addend is not None:
+                dx = dx + addend
     if not dw_done and p is not None:
         STATS["aten_wgrad"] += 1
         _, dw = _aten_bwd(gy, x, w, stride, padding, False, True)

@@ -44,9 +44,19 @@ def _zero_scratch(store, device, n):
     return arena.take(n)
 
 
+class GradLink:
+    """Carries one tensor's gradient from one autograd node to another that runs later in the backward
+    pass, so the sum of the two contributions is formed inside a kernel (e.g. a ResNet identity block:
+    the residual branch's dres is accumulated in conv1's dgrad epilogue instead of by a separate add)."""
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+
 class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, anchor, p, stride, padding, with_stats):
+    def forward(ctx, x, anchor, p, stride, padding, with_stats, link=None):
         impl = _conv_impl()
         w = p.weight if x.dtype == p.weight.dtype else p.master.to(x.dtype)
         sums = None
@@ -55,7 +65,7 @@ class _Conv2dNHWC(torch.autograd.Function):
                 _C().conv_stat_replicas, 2, w.shape[0])
         y = impl.conv_fwd(x, w, stride, padding, sums)
         ctx.save_for_backward(x)
-        ctx.p, ctx.stride, ctx.padding = p, stride, padding
+        ctx.p, ctx.stride, ctx.padding, ctx.link = p, stride, padding, link
         ctx.x_requires_grad = x.requires_grad
         if sums is not None:
             ctx.mark_non_differentiable(sums)
@@ -68,24 +78,30 @@ class _Conv2dNHWC(torch.autograd.Function):
         impl = _conv_impl()
         w = p.weight if x.dtype == p.weight.dtype else p.master.to(x.dtype)
         gy = gy.contiguous()
-        dx = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, ctx.x_requires_grad, p)
-        return dx, None, None, None, None, None
+        addend = None
+        if ctx.link is not None:
+            addend, ctx.link.grad = ctx.link.grad, None
+        dx = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, ctx.x_requires_grad, p, addend=addend)
+        return dx, None, None, None, None, None, None
 
 
-def conv2d_nhwc(x: torch.Tensor, p, stride: int = 1, padding: int = 0, with_stats: bool = False):
+def conv2d_nhwc(x: torch.Tensor, p, stride: int = 1, padding: int = 0, with_stats: bool = False,
+                grad_link: "GradLink" = None):
     """NHWC convolution with KRSC weight ``p`` (no bias).
 
     With ``with_stats`` returns ``(y, sums)``: ``sums`` = fp32 [2, K] per-channel sum / sum of squares of y
     accumulated in the conv epilogue (None when the layer runs on the fallback path) -- the following
-    ``batch_norm_act(..., sums=sums)`` then needs no statistics pass."""
-    y, sums = _Conv2dNHWC.apply(x, p.store.anchor, p, stride, padding, with_stats)
+    ``batch_norm_act(..., sums=sums)`` then needs no statistics pass. ``grad_link``: a gradient for x
+    deposited there by a later-backward node (``batch_norm_act(res_link=...)``) is added to dx in the dgrad."""
+    y, sums = _Conv2dNHWC.apply(x, p.store.anchor, p, stride, padding, with_stats, grad_link)
     return (y, sums) if with_stats else y
 
 
 # =========================================================================== batchnorm + act
 class _BnAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu, sums=None):
+    def forward(ctx, x, res, anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu, sums=None,
+                res_link=None):
         x = x.contiguous()
         if res is not None:
             res = res.contiguous()
@@ -101,7 +117,7 @@ class _BnAct(torch.autograd.Function):
         # without a residual the ReLU mask is recomputed from x in the backward kernels (no need to keep y)
         keep_y = relu and (res is not None or not _gpu(x))
         ctx.save_for_backward(x, y if keep_y else None, mean, invstd)
-        ctx.pg, ctx.pb, ctx.has_res = pg, pb, res is not None
+        ctx.pg, ctx.pb, ctx.has_res, ctx.res_link = pg, pb, res is not None, res_link
         ctx.relu_x = relu and not keep_y
         return y
 
@@ -128,16 +144,20 @@ class _BnAct(torch.autograd.Function):
             dx, dres, dg, db = ref.bn_bwd(dy, x, y, mean, invstd, pg.master)
             store.deposit(pg, dg)
             store.deposit(pb, db)
-        return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None
+        if ctx.has_res and ctx.res_link is not None:  # hand dres to the node that adds it in a kernel
+            ctx.res_link.grad, dres = dres, None
+        return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm_act(x, pg, pb, run_mean, run_var, residual=None, relu=True, training=True, momentum=0.1,
-                   eps=1e-5, sums=None):
+                   eps=1e-5, sums=None, res_link=None):
     """y = act(BN(x) + residual) over the last (channel) dim of an NHWC tensor.
 
-    ``sums`` (fp32 [2, C] from ``conv2d_nhwc(..., with_stats=True)``) skips the statistics pass."""
+    ``sums`` (fp32 [2, C] from ``conv2d_nhwc(..., with_stats=True)``) skips the statistics pass.
+    ``res_link``: the residual's gradient is handed to that GradLink (and NOT returned to autograd); the
+    node consuming the link must add it (``conv2d_nhwc(..., grad_link=link)`` on the same tensor)."""
     return _BnAct.apply(x, residual, pg.store.anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu,
-                        sums)
+                        sums, res_link)
 
 
 # =========================================================================== layernorm / rmsnorm
