@@ -33,8 +33,11 @@
 
 namespace k8s_amd {
 
-constexpr int FA_BM = 128, FA_BN = 64, FA_THREADS = 256;
-constexpr int FB_BN = 64, FB_BM = 64;
+constexpr int FA_BM = 128, FA_THREADS = 256;
+constexpr int FB_BN = 64;
+// Per-iteration tiles scale with 1/D so every K/V (forward, dQ) or Q/dO (dK/dV) step carries the same MFMA work
+// per barrier: 64 keys / queries at D = 128, 128 at D = 64.
+// (host side picks TILE = 128 for D = 64 only when the sequence is long enough to keep the grid full)
 
 template <int D>
 __device__ __forceinline__ int v_swz(int r) {
@@ -67,9 +70,11 @@ __device__ __forceinline__ const uint16_t* kh_src(const uint16_t* base, long rst
 }
 
 // =============================================================================== forward
-template <int D>
+template <int D, int TILE>
 __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a) {
-  constexpr int KT = FA_BN * D * 2;  // bytes of one K (or V) tile
+  constexpr int FA_BN = TILE;  // keys per iteration
+  constexpr int NI = FA_BN / 16;       // 16-key subtiles
+  constexpr int KT = FA_BN * D * 2;    // bytes of one K (or V) tile
   constexpr int UPR = D / 8;         // 16-B units per V row
   constexpr int ND = D / 16, NK = D / 32;
   __shared__ __attribute__((aligned(1024))) char smem[4 * KT];  // [buf][K | V]
@@ -142,13 +147,13 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
     const bool skip = a.causal && key0 > q0w + 31 + off;  // whole tile masked for this wave
     if (!skip) {
       // ---- S^T = K Q^T
-      f32x4_t s[4][2];
+      f32x4_t s[NI][2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) s[i][0] = s[i][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < NI; ++i) s[i][0] = s[i][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < NI; ++i) {
           const mfma_bf16x8 kf = frag_kmajor(tk + (kk >> 1) * (FA_BN * 128), i * 16, kk & 1, lane);
           s[i][0] = mfma16(kf, qf[0][kk], s[i][0]);
           s[i][1] = mfma16(kf, qf[1][kk], s[i][1]);
@@ -161,7 +166,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
         const int qi = q0w + qs * 16 + li;
         float mx = -INFINITY;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < NI; ++i)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float x = s[i][qs][r] * a.scale_log2;
@@ -178,7 +183,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
         const float alpha = exp2f(m[qs] - mn);
         float rs = 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < NI; ++i)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float p = exp2f(s[i][qs][r] - mn);
@@ -194,7 +199,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
       }
       // ---- O^T += V^T P^T (k = keys in the permuted order of the S^T accumulators)
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
+      for (int s2 = 0; s2 < NI / 2; ++s2) {
         mfma_bf16x8 pf[2];
 #pragma unroll
         for (int qs = 0; qs < 2; ++qs) {
@@ -271,9 +276,11 @@ __global__ void __launch_bounds__(256) flash_delta_kernel(const uint16_t* o, lon
 // ---- dK, dV: one block = 64 keys of one KV head (wave w: keys k0 + 16w .. +15, K/V fragments in VGPRs),
 // looping over every (query head of the GQA group, 64-query tile); Q / dO / lse / delta tiles double-buffered
 // in LDS through global_load_lds. Lane layout of S, dP, P, dS: key = li, query = 16*qs + 4*g + r.
-template <int D>
+template <int D, int TILE>
 __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArgs a) {
   constexpr int ND = D / 16, NK = D / 32;
+  constexpr int FB_BM = TILE;              // queries per iteration
+  constexpr int NQ = FB_BM / 16;           // 16-query subtiles
   constexpr int TQ = FB_BM * D * 2;        // Q / dO tile bytes
   constexpr int STAGE = 2 * TQ + 1024;     // Q | dO | lse (256 B) delta (256 B) pad
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
@@ -330,10 +337,11 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
         glds16(kh_src(qp, a.sqs, FB_BM, q0, a.Sq, s), base + wb);
         glds16(kh_src(dop, a.sds, FB_BM, q0, a.Sq, s), base + TQ + wb);
       }
-      if (wid_u == 0) {  // lse | delta of the 64 queries (rows padded to lse_ld, so never out of bounds)
+      if (wid_u == 0) {  // lse | delta of the tile's queries (rows padded to lse_ld, so never out of bounds)
+        constexpr int L4 = FB_BM / 4;  // lanes per 4-float row piece
         const long row = ((long)b * a.Hq + h) * a.lse_ld + q0;
-        const float* src = lane < 16 ? a.lse + row + lane * 4 : (lane < 32 ? a.delta + row + (lane - 16) * 4
-                                                                          : a.lse + row);
+        const float* src = lane < L4 ? a.lse + row + lane * 4
+                                     : (lane < 2 * L4 ? a.delta + row + (lane - L4) * 4 : a.lse + row);
         glds16(src, base + 2 * TQ);
       }
     };
@@ -349,13 +357,13 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
       const float* tl = reinterpret_cast<const float*>(tq + 2 * TQ);
       const int q0 = (qt0 + it % per_head) * FB_BM;
       // ---- S = Q K^T, dP = dO V^T
-      f32x4_t sv[4], dp[4];
+      f32x4_t sv[NQ], dp[NQ];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sv[i] = dp[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < NQ; ++i) sv[i] = dp[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk) {
 #pragma unroll
-        for (int qs = 0; qs < 4; ++qs) {
+        for (int qs = 0; qs < NQ; ++qs) {
           const mfma_bf16x8 qa = frag_kmajor(tq + (kk >> 1) * (FB_BM * 128), qs * 16, kk & 1, lane);
           const mfma_bf16x8 da = frag_kmajor(tdo + (kk >> 1) * (FB_BM * 128), qs * 16, kk & 1, lane);
           sv[qs] = mfma16(qa, kf[kk], sv[qs]);
@@ -364,9 +372,9 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
       }
       // ---- P = exp2(S c - lse2), dS = P (dP - delta)
 #pragma unroll
-      for (int qs = 0; qs < 4; ++qs) {
+      for (int qs = 0; qs < NQ; ++qs) {
         const f32x4_t l4 = *reinterpret_cast<const f32x4_t*>(tl + qs * 16 + g * 4);
-        const f32x4_t d4 = *reinterpret_cast<const f32x4_t*>(tl + 64 + qs * 16 + g * 4);
+        const f32x4_t d4 = *reinterpret_cast<const f32x4_t*>(tl + FB_BM + qs * 16 + g * 4);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int qi = q0 + qs * 16 + g * 4 + r;
@@ -379,7 +387,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
       // ---- dV^T += dO^T P, dK^T += Q^T dS   (k = queries in the permuted order of the accumulators)
       const int q_ = li >> 2, pp = li & 3;
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
+      for (int s2 = 0; s2 < NQ / 2; ++s2) {
         const float p0[4] = {sv[2 * s2][0], sv[2 * s2][1], sv[2 * s2][2], sv[2 * s2][3]};
         const float p1[4] = {sv[2 * s2 + 1][0], sv[2 * s2 + 1][1], sv[2 * s2 + 1][2], sv[2 * s2 + 1][3]};
         const float d0[4] = {dp[2 * s2][0], dp[2 * s2][1], dp[2 * s2][2], dp[2 * s2][3]};
@@ -421,9 +429,11 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
 // double-buffered in LDS, S^T = K Q^T and dP^T = V dO^T recomputed (lane: query = li, keys 4g+r), and
 // dQ^T += K^T dS^T with dS^T consumed in place (permuted k) and K^T read transposed from the K tile.
 // No atomics: each block owns its queries.
-template <int D>
+template <int D, int TILE>
 __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dq_kernel(AttnBwdArgs a) {
   constexpr int ND = D / 16, NK = D / 32;
+  constexpr int FB_BN = TILE;  // keys per iteration
+  constexpr int NI = FB_BN / 16;
   constexpr int KT = FB_BN * D * 2;
   constexpr int BMQ = 64;
   __shared__ __attribute__((aligned(1024))) char smem[4 * KT];  // [buf][K | V], both K-major halves
@@ -491,20 +501,20 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dq_kernel(AttnBwdArgs
     const char* tk = smem + cur * 2 * KT;
     const char* tv = tk + KT;
     if (!(a.causal && key0 > q0w + 15 + off)) {
-      f32x4_t s[4], dp[4];
+      f32x4_t s[NI], dp[NI];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) s[i] = dp[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < NI; ++i) s[i] = dp[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < NI; ++i) {
           s[i] = mfma16(frag_kmajor(tk + (kk >> 1) * (FB_BN * 128), i * 16, kk & 1, lane), qf[kk], s[i]);
           dp[i] = mfma16(frag_kmajor(tv + (kk >> 1) * (FB_BN * 128), i * 16, kk & 1, lane), df[kk], dp[i]);
         }
       }
       const bool need_mask = (key0 + FB_BN > kv_end) || (a.causal && key0 + FB_BN - 1 > q0w + off);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           bool ok = true;
@@ -516,7 +526,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dq_kernel(AttnBwdArgs
           dp[i][r] = p * (dp[i][r] - dq_);
         }
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
+      for (int s2 = 0; s2 < NI / 2; ++s2) {
         const float d0[4] = {dp[2 * s2][0], dp[2 * s2][1], dp[2 * s2][2], dp[2 * s2][3]};
         const float d1[4] = {dp[2 * s2 + 1][0], dp[2 * s2 + 1][1], dp[2 * s2 + 1][2], dp[2 * s2 + 1][3]};
         const mfma_bf16x8 dsf = pack8(d0, d1);
@@ -545,11 +555,15 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dq_kernel(AttnBwdArgs
 }
 
 // =============================================================================== launchers
+// D = 64 with long sequences: 128-wide key / query steps (same MFMA work per barrier as D = 128)
+static bool big_tile(int D, int S) { return D == 64 && S >= 1024; }
+
 void launch_flash_fwd(const AttnFwdArgs& a, int D, hipStream_t st) {
   const int nqb = (a.Sq + FA_BM - 1) / FA_BM;
-  const dim3 grid(nqb * a.Hq * a.B);
-  if (D == 128) hipLaunchKernelGGL(flash_fwd_kernel<128>, grid, dim3(FA_THREADS), 0, st, a);
-  else hipLaunchKernelGGL(flash_fwd_kernel<64>, grid, dim3(FA_THREADS), 0, st, a);
+  const dim3 grid(nqb * a.Hq * a.B), blk(FA_THREADS);
+  if (D == 128) hipLaunchKernelGGL((flash_fwd_kernel<128, 64>), grid, blk, 0, st, a);
+  else if (big_tile(D, a.Sk)) hipLaunchKernelGGL((flash_fwd_kernel<64, 128>), grid, blk, 0, st, a);
+  else hipLaunchKernelGGL((flash_fwd_kernel<64, 64>), grid, blk, 0, st, a);
 }
 
 void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, long sos, long soh,
@@ -563,14 +577,17 @@ void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, 
   else
     hipLaunchKernelGGL(flash_delta_kernel<64>, dgrid, dim3(256), 0, st, o, sob, sos, soh, a.dO, a.sdb, a.sds, a.sdh,
                        a.delta, a.B, a.Sq, a.Hq, a.lse_ld);
-  const dim3 gkv(((a.Sk + FB_BN - 1) / FB_BN) * a.Hkv * a.B);
-  const dim3 gq(((a.Sq + 63) / 64) * a.Hq * a.B);
+  const dim3 gkv(((a.Sk + FB_BN - 1) / FB_BN) * a.Hkv * a.B);  // dK/dV blocks own 64 keys at any D
+  const dim3 gq(((a.Sq + 63) / 64) * a.Hq * a.B), blk(FA_THREADS);
   if (D == 128) {
-    hipLaunchKernelGGL(flash_bwd_dkv_kernel<128>, gkv, dim3(FA_THREADS), 0, st, a);
-    hipLaunchKernelGGL(flash_bwd_dq_kernel<128>, gq, dim3(FA_THREADS), 0, st, a);
+    hipLaunchKernelGGL((flash_bwd_dkv_kernel<128, 64>), gkv, blk, 0, st, a);
+    hipLaunchKernelGGL((flash_bwd_dq_kernel<128, 64>), gq, blk, 0, st, a);
+  } else if (big_tile(D, a.Sq)) {
+    hipLaunchKernelGGL((flash_bwd_dkv_kernel<64, 128>), gkv, blk, 0, st, a);
+    hipLaunchKernelGGL((flash_bwd_dq_kernel<64, 128>), gq, blk, 0, st, a);
   } else {
-    hipLaunchKernelGGL(flash_bwd_dkv_kernel<64>, gkv, dim3(FA_THREADS), 0, st, a);
-    hipLaunchKernelGGL(flash_bwd_dq_kernel<64>, gq, dim3(FA_THREADS), 0, st, a);
+    hipLaunchKernelGGL((flash_bwd_dkv_kernel<64, 64>), gkv, blk, 0, st, a);
+    hipLaunchKernelGGL((flash_bwd_dq_kernel<64, 64>), gq, blk, 0, st, a);
   }
 }
 

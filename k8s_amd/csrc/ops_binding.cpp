@@ -389,7 +389,7 @@ std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, bool causal, c10::op
   TORCH_CHECK(Hkv > 0 && Hq % Hkv == 0, "Hq must be a multiple of Hkv");
   TORCH_CHECK(Sq > 0 && Sk > 0, "empty sequence");
   auto o = torch::empty({B, Sq, Hq, D}, q.options());
-  const long ld = (Sq + 63) / 64 * 64;  // padded rows: the backward stages 64-query slices with 16-B copies
+  const long ld = (Sq + 127) / 128 * 128;  // padded rows: the backward stages 64/128-query slices with 16-B copies
   auto lse = torch::empty({B, Hq, ld}, q.options().dtype(at::kFloat));
   k8s_amd::AttnFwdArgs a;
   a.q = cbf(q); a.k = cbf(k); a.v = cbf(v); a.o = bf(o); a.lse = f32(lse); a.kv_lens = kv_lens_ptr(kv_lens, B);
@@ -414,9 +414,9 @@ std::vector<Tensor> flash_bwd(Tensor dO, Tensor q, Tensor k, Tensor v, Tensor o,
   TORCH_CHECK(dO.sizes() == q.sizes() && o.sizes() == q.sizes(), "dO / o must match q");
   TORCH_CHECK(Hq % Hkv == 0, "Hq must be a multiple of Hkv");
   check_cuda(lse, "lse"); check_dtype(lse, at::kFloat, "lse");
-  const long ld = (Sq + 63) / 64 * 64;
+  const long ld = (Sq + 127) / 128 * 128;
   TORCH_CHECK(lse.dim() == 3 && lse.size(0) == B && lse.size(1) == Hq && lse.size(2) == ld,
-              "lse must be the [B, Hq, round_up(Sq, 64)] tensor flash_fwd returned");
+              "lse must be the [B, Hq, round_up(Sq, 128)] tensor flash_fwd returned");
   auto delta = torch::empty({B, Hq, ld}, q.options().dtype(at::kFloat));
   auto dq = torch::empty({B, Sq, Hq, D}, q.options());
   auto dk = torch::empty({B, Sk, Hkv, D}, q.options());

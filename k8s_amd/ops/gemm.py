@@ -104,14 +104,33 @@ def linear_fwd(x, w, b, act=None):
     return y, (pre if act == "gelu" else (y if act == "relu" else None))
 
 
-def linear_bwd(gy, x, w, saved, act, pw=None, store=None):
+_ADDMM_F32 = None  # does this torch build take addmm(..., out_dtype=float32) for bf16 inputs?
+
+
+def _blas_wgrad(g, x, out, accumulate):
+    """out (fp32) (+)= g^T x on hipBLASLt, fp32 accumulate straight into the slot when supported."""
+    global _ADDMM_F32
+    if _ADDMM_F32 is not False:
+        try:
+            torch.addmm(out, g.t(), x, out_dtype=torch.float32, beta=1.0 if accumulate else 0.0, out=out)
+            _ADDMM_F32 = True
+            return
+        except (RuntimeError, TypeError):
+            _ADDMM_F32 = False
+    d = torch.mm(g.t(), x)
+    out.add_(d) if accumulate else out.copy_(d)
+
+
+def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True):
     """dx and the parameter gradient. With (pw, store) on GPU the weight gradient is written
     (or accumulated) straight into the flat fp32 gradient slot; returns (dx, dw_or_None, db)."""
     g = _act_bwd(gy, saved, act)
     M, K = x.shape
     N = w.shape[0]
     db = None
-    if g.is_cuda and g.dtype == torch.bfloat16 and N % 8 == 0:
+    if not need_db:
+        pass
+    elif g.is_cuda and g.dtype == torch.bfloat16 and N % 8 == 0:
         db = _load().colsum(g.contiguous())
     else:
         db = g.float().sum(0)
@@ -130,8 +149,7 @@ def linear_bwd(gy, x, w, saved, act, pw=None, store=None):
                 mm(g, x, False, False, out=out, out_f32=True, accumulate=accumulate, splits=0)
 
             def blas_w(out, accumulate):
-                d = torch.mm(g.t(), x)
-                out.add_(d) if accumulate else out.copy_(d)
+                _blas_wgrad(g, x, out, accumulate)
 
             if autotune.choose("linear_wgrad|" + dims, [
                     ("hip", lambda: hip_w(torch.empty_like(pw.grad), False)),

@@ -235,7 +235,7 @@ class _Linear(torch.autograd.Function):
         g = _gemm()
         w = pw.weight if x2.dtype == pw.weight.dtype else pw.master.to(x2.dtype)
         gy2 = gy.reshape(-1, gy.shape[-1]).contiguous()
-        dx, dw, db = g.linear_bwd(gy2, x2, w, pre, ctx.act, pw=pw, store=pw.store)
+        dx, dw, db = g.linear_bwd(gy2, x2, w, pre, ctx.act, pw=pw, store=pw.store, need_db=pb is not None)
         if dw is not None:
             pw.store.deposit(pw, dw)
         if pb is not None:
@@ -262,9 +262,19 @@ class _Embedding(torch.autograd.Function):
         (ids,) = ctx.saved_tensors
         pw = ctx.pw
         V, D = pw.shape
-        dw = torch.zeros((V, D), device=gy.device, dtype=torch.float32)
-        dw.index_add_(0, ids.reshape(-1), gy.reshape(-1, D).float())
-        pw.store.deposit(pw, dw)
+        store = pw.store
+        slot = store.slot_for_write(pw)
+        if slot is not None:  # scatter-add straight into the flat fp32 gradient slot (no [V, D] temporary)
+            slot.zero_()
+            slot.index_add_(0, ids.reshape(-1), gy.reshape(-1, D).to(slot.dtype))
+            store.mark_written(pw)
+        elif pw.grad.dtype == torch.float32:  # tied weight already holds the other use's gradient
+            pw.grad.index_add_(0, ids.reshape(-1), gy.reshape(-1, D).float())
+            store._notify(pw)
+        else:
+            dw = torch.zeros((V, D), device=gy.device, dtype=torch.float32)
+            dw.index_add_(0, ids.reshape(-1), gy.reshape(-1, D).float())
+            store.deposit(pw, dw)
         return None, None, None, None
 
 

@@ -28,7 +28,7 @@ def bench(fn, it=20):
 def main():
     C = load()
     cases = [("bert_s128", 64, 128, 12, 12, 64, False), ("bert_s512", 16, 512, 12, 12, 64, False),
-             ("llama_s2048", 2, 2048, 32, 8, 128, True), ("llama_s4096", 1, 4096, 32, 8, 128, True),
+             ("llama_s2048", 2, 2048, 32, 8, 128, True), ("llama1b_s2048_d64", 2, 2048, 32, 8, 64, True), ("llama_s4096", 1, 4096, 32, 8, 128, True),
              ("mha_s4096_nc", 1, 4096, 32, 32, 128, False)]
     for name, B, S, Hq, Hkv, D, causal in cases:
         q = torch.randn(B, S, Hq, D, device="cuda").bfloat16()

@@ -25,6 +25,8 @@ CASES = [
     (2, 333, 4, 1, 128, True, None),
     (2, 192, 4, 4, 128, False, [1, 150]),
     (1, 64, 2, 2, 64, True, None),
+    (1, 1100, 4, 2, 64, True, None),        # D = 64 long sequence: 128-wide key / query tiles
+    (2, 1024, 2, 2, 64, False, [1024, 900]),
 ]
 
 
