@@ -112,7 +112,7 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": (ips / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": "bf16",
-            "data": "synthetic (random 224x224x3 images, random labels, random-init weights)",
+            "data": "synthetic (random %dx%dx3 images, random labels, random-init weights)" % (a.image, a.image),
             "config": {
                 "model": "resnet50-v1.5",
                 "global_batch": n * a.batch,

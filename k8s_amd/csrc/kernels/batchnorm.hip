@@ -487,6 +487,35 @@ void launch_bn_fwd_from_sums(const uint16_t* x, const uint16_t* res, const float
                      save_mean, save_invstd, gamma, beta, y, nvec, C / 8, (int)relu);
 }
 
+// Fold the conv-epilogue replicas [nrep][2][C] of (sum g*mask, sum g*mask*xhat) into sums / dgamma / dbeta.
+__global__ void __launch_bounds__(256) bn_bwd_fold_reps_kernel(const float* __restrict__ reps, int nrep, int C,
+                                                               float* __restrict__ sums, float* __restrict__ dgamma,
+                                                               float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f, b = 0.f;
+  for (int r = 0; r < nrep; ++r) {
+    a += reps[((long)r * 2) * C + c];
+    b += reps[((long)r * 2 + 1) * C + c];
+  }
+  sums[c] = a;
+  sums[C + c] = b;
+  if (dbeta) dbeta[c] = a;
+  if (dgamma) dgamma[c] = b;
+}
+
+// BN backward whose reduction already happened in the epilogue of the kernel that produced dy.
+void launch_bn_bwd_from_sums(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,
+                             const float* invstd, const float* gamma, const float* beta, bool relu_x, uint16_t* dx,
+                             uint16_t* dres, float* dgamma, float* dbeta, const float* reps, int nrep, float* sums,
+                             long M, int C, hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_fold_reps_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, reps, nrep, C, sums, dgamma,
+                     dbeta);
+  const long nvec = M * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(bn_elem_grid(nvec, C / 8)), dim3(BN_THREADS), 0, st, dy, x, y,
+                     mean, invstd, beta, (int)relu_x, gamma, sums, dx, dres, nvec, C / 8, C, 1.f / (float)M);
+}
+
 void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
                    const float* gamma, const float* beta, bool relu_x, uint16_t* dx, uint16_t* dres, float* dgamma,
                    float* dbeta, float* work, float* sums, long M, int C, hipStream_t st) {

@@ -212,6 +212,15 @@ struct Epi {
   float* stats;       // [STAT_REPL][2][N] fp32 per-column sum / sum of squares of the stored outputs
                       // (BN fusion) or null; tile row tm adds into replica tm % STAT_REPL so the atomics
                       // spread over STAT_REPL x 2N addresses instead of contending on 2N
+  // BatchNorm-BACKWARD statistics of the stored (bf16) output g, which is the gradient w.r.t. a BN output:
+  // bstats[rep][0][n] += sum_m g*mask, bstats[rep][1][n] += sum_m g*mask*xhat with xhat from the BN input bx
+  // and the ReLU mask from the BN output by (residual BN) or recomputed from bx (brelu_x). Replaces the
+  // separate reduction pass over g and x in the BN backward.
+  float* bstats;
+  const uint16_t* bx;
+  const uint16_t* by;
+  const float *bmean, *binvstd, *bgamma, *bbeta;
+  int brelu_x;
 };
 constexpr int STAT_REPL = 32;
 
@@ -396,13 +405,43 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r]);
           *reinterpret_cast<bf16x4_t*>(cp) = o;
+          if (E.bstats) {
+            const long off = (long)m * E.ldc + n;
+            const bf16x4_t xv = *reinterpret_cast<const bf16x4_t*>(E.bx + off);
+            bf16x4_t yv;
+            if (E.by) yv = *reinterpret_cast<const bf16x4_t*>(E.by + off);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float xh = (bf2f((uint16_t)xv[r]) - E.bmean[n + r]) * E.binvstd[n + r];
+              bool on = true;
+              if (E.by) on = bf2f((uint16_t)yv[r]) > 0.f;
+              else if (E.brelu_x) on = bf2f(f2bf(xh * E.bgamma[n + r] + E.bbeta[n + r])) > 0.f;
+              const float g = on ? bf2f((uint16_t)o[r]) : 0.f;
+              st_s[j][r] += g;
+              st_q[j][r] += g * xh;
+            }
+          }
         } else {
-          for (int r = 0; r < 4 && n + r < N; ++r) cp[r] = f2bf(v[r] + (E.mode == 1 ? bf2f(cp[r]) : 0.f));
+          for (int r = 0; r < 4 && n + r < N; ++r) {
+            const uint16_t o = f2bf(v[r] + (E.mode == 1 ? bf2f(cp[r]) : 0.f));
+            cp[r] = o;
+            if (E.bstats) {
+              const long off = (long)m * E.ldc + n + r;
+              const float xh = (bf2f(E.bx[off]) - E.bmean[n + r]) * E.binvstd[n + r];
+              bool on = true;
+              if (E.by) on = bf2f(E.by[off]) > 0.f;
+              else if (E.brelu_x) on = bf2f(f2bf(xh * E.bgamma[n + r] + E.bbeta[n + r])) > 0.f;
+              const float g = on ? bf2f(o) : 0.f;
+              st_s[j][r] += g;
+              st_q[j][r] += g * xh;
+            }
+          }
         }
       }
     }
   }
-  if (E.stats) {
+  float* const stat_out = E.stats ? E.stats : E.bstats;
+  if (stat_out) {
     // lanes with equal (lane >> 4) hold the same 4 columns: reduce over the 16 row lanes, then over the two
     // row-waves through LDS, so the block issues 4 full-wave atomic instructions (256 columns x {sum, sumsq})
     // instead of 128 quarter-empty ones -- float atomics cost ~50 ns per wave-instruction per CU.
@@ -432,7 +471,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
         float v = 0.f;
 #pragma unroll
         for (int w = 0; w < WM; ++w) v += red[(w * 2 + which) * BN + col];
-        atomicAdd(E.stats + (long)(tm % STAT_REPL) * 2 * N + (long)which * N + n, v);
+        atomicAdd(stat_out + (long)(tm % STAT_REPL) * 2 * N + (long)which * N + n, v);
       }
     }
   }
@@ -484,6 +523,10 @@ static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act,
   e.alpha = alpha;
   e.stats = nullptr;
   e.slab = 0;
+  e.bstats = nullptr;
+  e.bx = e.by = nullptr;
+  e.bmean = e.binvstd = e.bgamma = e.bbeta = nullptr;
+  e.brelu_x = 0;
   return e;
 }
 
@@ -521,13 +564,26 @@ long gemm_splitk_workspace(int M, int N, int splits) { return splits > 1 ? (long
 //  a_kmajor: A stored [M][K] (lda) else [K][M];  b_kmajor: B stored [N][K] (ldb) else [K][N]
 //  mode 0 store / 1 accumulate; with splits > 1 (fp32 C, plain epilogue) the K range is split over
 //  blockIdx.z, each split writes an fp32 slab of `ws` and a reduce kernel combines them into C.
+static void apply_bnbwd(Epi& e, const BnBwdEpi* bb) {
+  if (!bb) return;
+  e.bstats = bb->stats;
+  e.bx = bb->x;
+  e.by = bb->y;
+  e.bmean = bb->mean;
+  e.binvstd = bb->invstd;
+  e.bgamma = bb->gamma;
+  e.bbeta = bb->beta;
+  e.brelu_x = bb->relu_x;
+}
+
 void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                  long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
-                 float alpha, int splits, float* ws, hipStream_t st) {
+                 float alpha, int splits, float* ws, hipStream_t st, const BnBwdEpi* bnb) {
   splits = effective_splits(K, splits);
   const bool slab = splits > 1;
   Epi e = make_epi(slab ? (void*)ws : C, slab ? (long)N : ldc, c_f32, bias, act, pre, slab ? 3 : mode, alpha);
   e.slab = (long)M * N;
+  if (!slab) apply_bnbwd(e, bnb);
   if (a_kmajor && b_kmajor)
     launch(KMajor{A, lda, M}, KMajor{B, ldb, N}, e, M, N, K, splits, st);
   else if (a_kmajor && !b_kmajor)
@@ -543,11 +599,12 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
 // decode, any other C % 8 == 0 the per-unit one.
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int K,
                      int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
-                     int mode, float* stats, hipStream_t st) {
+                     int mode, float* stats, hipStream_t st, const BnBwdEpi* bnb) {
   const int M = N * Ho * Wo, RSC = R * S * C;
   KMajor b{w, (long)RSC, K, RSC};
   Epi e = make_epi(y, K, y_f32, bias, act, nullptr, mode, 1.f);
   e.stats = stats;
+  apply_bnbwd(e, bnb);
   if (C % 64 == 0) {
     ConvA a{x, N, H, W, C, Ho, Wo, S, stride, pad, dil, M,
             make_fastdiv(C), make_fastdiv(S), make_fastdiv(Ho * Wo), make_fastdiv(Wo)};

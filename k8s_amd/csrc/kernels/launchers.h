@@ -30,6 +30,10 @@ constexpr int kConvStatReplicas = 32;  // must match STAT_REPL in gemm.hip
 void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
                    const float* gamma, const float* beta, bool relu_x, uint16_t* dx, uint16_t* dres, float* dgamma,
                    float* dbeta, float* work, float* sums, long M, int C, hipStream_t st);
+void launch_bn_bwd_from_sums(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,
+                             const float* invstd, const float* gamma, const float* beta, bool relu_x, uint16_t* dx,
+                             uint16_t* dres, float* dgamma, float* dbeta, const float* reps, int nrep, float* sums,
+                             long M, int C, hipStream_t st);
 
 // norm.hip
 void launch_norm_fwd(bool rms, const uint16_t* x, const uint16_t* res, uint16_t* xsum, const float* gamma,
@@ -49,13 +53,23 @@ void launch_xent_bwd(const void* logits, bool bf16, const int64_t* labels, const
 
 // gemm.hip
 int gemm_choose_splits(int M, int N, int K);
+// BatchNorm-backward statistics computed in a GEMM / conv epilogue whose bf16 output is the gradient w.r.t.
+// a BN layer's output (see Epi::bstats in gemm.hip); stats = zeroed fp32 [kConvStatReplicas][2][N].
+struct BnBwdEpi {
+  float* stats;
+  const uint16_t* x;  // BN input
+  const uint16_t* y;  // BN output (ReLU mask of a residual BN) or null
+  const float *mean, *invstd, *gamma, *beta;
+  int relu_x;         // mask recomputed from x
+};
 void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                  long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
-                 float alpha, int splits, float* ws, hipStream_t st);
+                 float alpha, int splits, float* ws, hipStream_t st, const BnBwdEpi* bnb = nullptr);
 long gemm_splitk_workspace(int M, int N, int splits);  // fp32 elements of the split-K slab workspace
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int K,
                      int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
-                     int mode, float* stats, hipStream_t st);
+                     int mode, float* stats, hipStream_t st,
+                     const BnBwdEpi* bnb = nullptr);
 void launch_conv_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int C, int K, int R,
                        int S, int stride, int pad, int dil, int Ho, int Wo, int splits, bool accumulate, float* ws,
                        hipStream_t st);

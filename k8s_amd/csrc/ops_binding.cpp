@@ -124,7 +124,8 @@ std::vector<Tensor> bn_fwd_from_sums(Tensor x, c10::optional<Tensor> res, Tensor
 }
 
 std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor mean, Tensor invstd, Tensor gamma,
-                           Tensor beta, bool relu_x, Tensor dgamma, Tensor dbeta, bool want_dres) {
+                           Tensor beta, bool relu_x, Tensor dgamma, Tensor dbeta, bool want_dres,
+                           c10::optional<Tensor> reps) {
   check_cuda(dy, "dy"); check_cuda(x, "x");
   check_dtype(dy, at::kBFloat16, "dy"); check_dtype(x, at::kBFloat16, "x");
   TORCH_CHECK(dy.sizes() == x.sizes());
@@ -138,6 +139,16 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor 
   auto work = torch::empty({k8s_amd::bn_workspace_floats(M, C)}, gamma.options());
   auto sums = torch::empty({2 * C}, gamma.options());
   TORCH_CHECK(!(relu_x && y), "relu mask from x and y are exclusive");
+  if (reps) {  // (sum g*mask, sum g*mask*xhat) already accumulated by the epilogue that produced dy
+    TORCH_CHECK(reps->is_cuda() && reps->scalar_type() == at::kFloat && reps->is_contiguous() &&
+                    reps->numel() == (long)k8s_amd::kConvStatReplicas * 2 * C,
+                "reps must be fp32 [conv_stat_replicas, 2, C]");
+    k8s_amd::launch_bn_bwd_from_sums(cbf(dy), cbf(x), y ? cbf(*y) : nullptr, f32(mean), f32(invstd), f32(gamma),
+                                     f32(beta), relu_x, bf(dx), want_dres ? bf(dres) : nullptr, f32(dgamma),
+                                     f32(dbeta), f32(*reps), k8s_amd::kConvStatReplicas, f32(sums), M, C,
+                                     cur_stream());
+    return {dx, dres};
+  }
   k8s_amd::launch_bn_bwd(cbf(dy), cbf(x), y ? cbf(*y) : nullptr, f32(mean), f32(invstd), f32(gamma), f32(beta),
                          relu_x, bf(dx), want_dres ? bf(dres) : nullptr, f32(dgamma), f32(dbeta), f32(work), f32(sums), M, C,
                          cur_stream());
@@ -221,9 +232,33 @@ void check_bf16_operand(const Tensor& t, const char* name) {
 }
 
 // a: [M,K] if a_kmajor else [K,M];  b: [N,K] if b_kmajor else [K,N];  returns / writes C[M,N]
+// bnb = (stats [R,2,N] zeroed fp32, x, y|None, mean, invstd, gamma, beta, relu_x) for the BN-backward statistics
+// epilogue; x / y must be [M, N] bf16 matching the output.
+struct BnbHolder {
+  k8s_amd::BnBwdEpi e;
+  bool on = false;
+};
+BnbHolder parse_bnb(const c10::optional<std::vector<Tensor>>& t, c10::optional<bool> relu_x, long M, long N) {
+  BnbHolder h;
+  if (!t) return h;
+  TORCH_CHECK(t->size() == 7, "bnb = [stats, x, y, mean, invstd, gamma, beta] (y may be an empty tensor)");
+  const auto& v = *t;
+  TORCH_CHECK(v[0].numel() == (long)k8s_amd::kConvStatReplicas * 2 * N && v[0].scalar_type() == at::kFloat,
+              "bnb stats must be fp32 [conv_stat_replicas, 2, N]");
+  TORCH_CHECK(v[1].numel() == M * N && v[1].scalar_type() == at::kBFloat16 && v[1].is_contiguous(), "bnb x shape");
+  const bool has_y = v[2].defined() && v[2].numel() > 0;
+  if (has_y) TORCH_CHECK(v[2].numel() == M * N && v[2].scalar_type() == at::kBFloat16 && v[2].is_contiguous());
+  for (int i = 3; i < 7; ++i)
+    TORCH_CHECK(v[i].numel() == N && v[i].scalar_type() == at::kFloat && v[i].is_contiguous(), "bnb per-channel");
+  h.e = k8s_amd::BnBwdEpi{f32(v[0]), cbf(v[1]), has_y ? cbf(v[2]) : nullptr, f32(v[3]), f32(v[4]), f32(v[5]),
+                          f32(v[6]), (!has_y && relu_x.value_or(false)) ? 1 : 0};
+  h.on = true;
+  return h;
+}
+
 Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tensor> out, bool out_f32,
             c10::optional<Tensor> bias, int64_t act, c10::optional<Tensor> pre, bool accumulate, double alpha,
-            int64_t splits) {
+            int64_t splits, c10::optional<std::vector<Tensor>> bnb, c10::optional<bool> bnb_relu_x) {
   check_bf16_operand(a, "A");
   check_bf16_operand(b, "B");
   const long M = a_kmajor ? a.size(0) : a.size(1), K = a_kmajor ? a.size(1) : a.size(0);
@@ -252,16 +287,20 @@ Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tens
   }
   Tensor ws;
   if (sp > 1) ws = torch::empty({k8s_amd::gemm_splitk_workspace((int)M, (int)N, sp)}, a.options().dtype(at::kFloat));
+  BnbHolder bb = parse_bnb(bnb, bnb_relu_x, M, N);
+  TORCH_CHECK(!bb.on || (!out_f32 && sp == 1), "the BN-backward epilogue needs a bf16, non-split output");
   k8s_amd::launch_gemm(cbf(a), a.stride(0), a_kmajor, cbf(b), b.stride(0), b_kmajor, c.data_ptr(), N, out_f32,
                        (int)M, (int)N, (int)K, bias ? bias->data_ptr<float>() : nullptr, (int)act,
-                       pre ? bf(*pre) : nullptr, mode, (float)alpha, sp, sp > 1 ? f32(ws) : nullptr, cur_stream());
+                       pre ? bf(*pre) : nullptr, mode, (float)alpha, sp, sp > 1 ? f32(ws) : nullptr, cur_stream(),
+                       bb.on ? &bb.e : nullptr);
   return c;
 }
 
 static inline int conv_out(int in, int k, int st, int pad, int dil) { return (in + 2 * pad - dil * (k - 1) - 1) / st + 1; }
 
 Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, bool out_f32, c10::optional<Tensor> bias,
-                int64_t act, c10::optional<Tensor> stats) {
+                int64_t act, c10::optional<Tensor> stats, c10::optional<std::vector<Tensor>> bnb,
+                c10::optional<bool> bnb_relu_x) {
   check_cuda(x, "x"); check_cuda(w, "w");
   check_dtype(x, at::kBFloat16, "x"); check_dtype(w, at::kBFloat16, "w");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "x [N,H,W,C], w [K,R,S,C]");
@@ -275,9 +314,11 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, bo
   if (stats) TORCH_CHECK(stats->numel() == (long)k8s_amd::kConvStatReplicas * 2 * K &&
                              stats->scalar_type() == at::kFloat && stats->is_contiguous(),
                          "stats must be zeroed fp32 [conv_stat_replicas, 2, K]");
+  BnbHolder bb = parse_bnb(bnb, bnb_relu_x, (long)N * Ho * Wo, K);
+  TORCH_CHECK(!bb.on || (!out_f32 && !stats), "the BN-backward epilogue needs a bf16 output and no fwd stats");
   k8s_amd::launch_conv_fwd(cbf(x), cbf(w), y.data_ptr(), out_f32, N, H, W, C, K, R, S, (int)stride, (int)pad,
                            (int)dil, Ho, Wo, bias ? bias->data_ptr<float>() : nullptr, (int)act, 0,
-                           stats ? f32(*stats) : nullptr, cur_stream());
+                           stats ? f32(*stats) : nullptr, cur_stream(), bb.on ? &bb.e : nullptr);
   return y;
 }
 
@@ -471,20 +512,26 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_sumsq", &grad_sumsq);
   m.def("clip_factor", &clip_factor);
   m.def("bn_fwd", &bn_fwd);
-  m.def("bn_bwd", &bn_bwd);
+  m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("mean"), py::arg("invstd"),
+        py::arg("gamma"), py::arg("beta"), py::arg("relu_x"), py::arg("dgamma"), py::arg("dbeta"), py::arg("want_dres"),
+        py::arg("reps") = py::none());
   m.def("bn_fwd_from_sums", &bn_fwd_from_sums);
   m.def("norm_fwd", &norm_fwd);
   m.def("norm_bwd", &norm_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
-  m.def("gemm", &gemm);
+  m.def("gemm", &gemm, py::arg("a"), py::arg("a_kmajor"), py::arg("b"), py::arg("b_kmajor"), py::arg("out"),
+        py::arg("out_f32"), py::arg("bias"), py::arg("act"), py::arg("pre"), py::arg("accumulate"), py::arg("alpha"),
+        py::arg("splits"), py::arg("bnb") = py::none(), py::arg("bnb_relu_x") = py::none());
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("rope_", &rope_);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("relu_bwd", &relu_bwd);
   m.def("colsum", &colsum);
-  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
+        py::arg("out_f32"), py::arg("bias"), py::arg("act"), py::arg("stats"), py::arg("bnb") = py::none(),
+        py::arg("bnb_relu_x") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_dgrad_wtrans", &conv_dgrad_wtrans);
   m.def("flash_fwd", &flash_fwd);

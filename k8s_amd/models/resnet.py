@@ -31,12 +31,13 @@ class BN(nn.Module):
         self.register_buffer("running_var", torch.ones(c))
         self.momentum, self.eps = 0.1, 1e-5
 
-    def forward(self, x, residual=None, relu=True, res_link=None):
+    def forward(self, x, residual=None, relu=True, res_link=None, bwd_link=None):
         sums = None
         if isinstance(x, tuple):  # (conv output, fused statistics)
             x, sums = x
         return K.batch_norm_act(x, self.gamma, self.beta, self.running_mean, self.running_var, residual, relu,
-                                self.training, self.momentum, self.eps, sums=sums, res_link=res_link)
+                                self.training, self.momentum, self.eps, sums=sums, res_link=res_link,
+                                bwd_link=bwd_link)
 
 
 class Conv(nn.Module):
@@ -45,9 +46,10 @@ class Conv(nn.Module):
         self.w = store.new(name + ".weight", (cout, k, k, cin), init_kaiming_normal(cin * k * k))
         self.stride, self.pad = stride, k // 2
 
-    def forward(self, x, grad_link=None):
+    def forward(self, x, grad_link=None, bn_link=None):
         # BN statistics are accumulated in the conv epilogue (returned alongside y)
-        return K.conv2d_nhwc(x, self.w, self.stride, self.pad, with_stats=True, grad_link=grad_link)
+        return K.conv2d_nhwc(x, self.w, self.stride, self.pad, with_stats=True, grad_link=grad_link,
+                             bn_link=bn_link)
 
 
 class Bottleneck(nn.Module):
@@ -67,16 +69,21 @@ class Bottleneck(nn.Module):
             self.down = Conv(store, name + ".downsample.0", cin, cout, 1, stride)
             self.down_bn = BN(store, name + ".downsample.1", cout)
 
-    def forward(self, x):
+    def forward(self, x, in_link=None):
+        """Returns (out, link for the BN that produced out). ``in_link``: the BatchNorm that produced x (the
+        previous block's bn3); in an identity block conv1's dgrad output is x's complete gradient, so that
+        epilogue also reduces the previous bn3's backward statistics."""
         idn = x
+        identity = self.down is None and x.requires_grad
         # identity block: x's two gradient contributions (residual via bn3, main path via conv1) are summed
         # inside conv1's dgrad epilogue instead of by a separate elementwise add
-        link = K.GradLink() if (self.down is None and x.requires_grad) else None
-        y = self.bn1(self.conv1(x, grad_link=link))
-        y = self.bn2(self.conv2(y))
+        link = K.GradLink() if identity else None
+        l1, l2, l3 = K.BnBwdLink(), K.BnBwdLink(), K.BnBwdLink()
+        y = self.bn1(self.conv1(x, grad_link=link, bn_link=in_link if identity else None), bwd_link=l1)
+        y = self.bn2(self.conv2(y, bn_link=l1), bwd_link=l2)
         if self.down is not None:
             idn = self.down_bn(self.down(x), relu=False)
-        return self.bn3(self.conv3(y), residual=idn, relu=True, res_link=link)
+        return self.bn3(self.conv3(y, bn_link=l2), residual=idn, relu=True, res_link=link, bwd_link=l3), l3
 
 
 class ResNet(nn.Module):
@@ -122,8 +129,9 @@ class ResNet(nn.Module):
     def forward(self, x):
         y = self.bn1(self.conv1(x))
         y = K.max_pool_nhwc(y, 3, 2, 1)
+        link = None
         for b in self.blocks:
-            y = b(y)
+            y, link = b(y, link)
         y = K.global_avg_pool_nhwc(y)
         return K.linear(y, self.fc_w, self.fc_b)
 

@@ -92,23 +92,27 @@ def _wgrad_hip(C_, gy, x, out, stride, padding, acc):
         C_.conv_wgrad(x, gy, out, stride, padding, 1, 0, acc)
 
 
-def _dgrad_hip(C_, gy, w, padding, addend=None):
+def _dgrad_hip(C_, gy, w, padding, addend=None, bnb=None):
     """dx on our kernels; with ``addend`` (bf16, shape of dx) a 1x1 dgrad accumulates onto it in the GEMM
-    epilogue and returns it (the fused residual-gradient add)."""
+    epilogue and returns it (the fused residual-gradient add). ``bnb`` = (list, relu_x) from
+    BnBwdLink.epilogue_args: the epilogue also reduces the BN backward's statistics of dx."""
     K, R, S, C = w.shape
+    bl, brx = bnb if bnb is not None else (None, None)
     if R == 1 and S == 1 and padding == 0:
         N, H, W_, _ = gy.shape
         if addend is not None:
             C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, addend.view(-1, C), False, None, 0, None, True,
-                    1.0, 1)
+                    1.0, 1, bl, brx)
             return addend
         return C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, None, False, None, 0, None, False, 1.0,
-                       1).reshape(N, H, W_, C)
-    dx = C_.conv_fwd(gy, C_.conv_dgrad_wtrans(w), 1, R - 1 - padding, 1, False, None, 0, None)
+                       1, bl, brx).reshape(N, H, W_, C)
+    if addend is not None:  # (no 3x3 consumer needs both; keep the statistics exact: reduce after the add)
+        bl = None
+    dx = C_.conv_fwd(gy, C_.conv_dgrad_wtrans(w), 1, R - 1 - padding, 1, False, None, 0, None, bl, brx)
     return dx if addend is None else dx.add_(addend)
 
 
-def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None):
+def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, bn_link=None):
     """Returns dx (+ ``addend``, e.g. the residual branch's gradient of the same tensor, fused into the
     dgrad epilogue where our kernel runs) or None; deposits dw into ``p``'s flat gradient slot."""
     K, R, S, C = w.shape
@@ -145,7 +149,10 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None):
                     ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, True, False)[0].add_(addend))]) == "hip"
         if use_hip:
             STATS["hip_dgrad"] += 1
-            dx = _dgrad_hip(C_, gy, w, padding, addend)
+            bnb = None
+            if bn_link is not None and p is not None and (R == 1 or addend is None):
+                bnb = bn_link.epilogue_args(p.store, gy.device)
+            dx = _dgrad_hip(C_, gy, w, padding, addend, bnb)
         else:
             STATS["aten_dgrad"] += 1
             dx, _ = _aten_bwd(gy, x, w, stride, padding, True, False)

@@ -193,3 +193,54 @@ def test_maxpool_nhwc(cuda, shape, ksp):
     y.backward(dy)
     yr.backward(dy.float().permute(0, 3, 1, 2))
     assert _rel(x.grad, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+@pytest.mark.parametrize("mode", ["relu_x", "y", "none"])
+def test_gemm_bn_backward_statistics_epilogue(cuda, mode):
+    """The dgrad epilogue's BatchNorm-backward reductions (sum g*mask, sum g*mask*xhat) match a torch reduction
+    over the stored output; with accumulate the statistics are of the accumulated value."""
+    torch.manual_seed(11)
+    M, K, C = 1000, 256, 192
+    g = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(K, C, device=cuda) * 0.05).bfloat16()
+    x = torch.randn(M, C, device=cuda).bfloat16()
+    mean, invstd = torch.randn(C, device=cuda) * 0.1, torch.rand(C, device=cuda) + 0.5
+    gamma, beta = torch.rand(C, device=cuda) + 0.5, torch.randn(C, device=cuda) * 0.1
+    y = torch.relu(torch.randn(M, C, device=cuda)).bfloat16() if mode == "y" else torch.empty(0, device=cuda,
+                                                                                              dtype=torch.bfloat16)
+    R = _C().conv_stat_replicas
+    reps = torch.zeros(R, 2, C, device=cuda)
+    base = torch.randn(M, C, device=cuda).bfloat16()
+    out = base.clone()
+    _C().gemm(g, True, w, False, out, False, None, 0, None, True, 1.0, 1,
+              [reps, x, y, mean, invstd, gamma, beta], mode == "relu_x")
+    assert _rel(out, base.float() + g.float() @ w.float()) < 1e-2
+    xh = (x.float() - mean) * invstd
+    if mode == "y":
+        mask = (y.float() > 0).float()
+    elif mode == "relu_x":
+        mask = ((xh * gamma + beta).bfloat16().float() > 0).float()
+    else:
+        mask = torch.ones_like(xh)
+    ge = out.float() * mask
+    tot = reps.sum(0)
+    assert _rel(tot[0], ge.sum(0)) < 1e-3
+    assert _rel(tot[1], (ge * xh).sum(0)) < 1e-3
+
+
+def test_conv3x3_dgrad_bn_backward_statistics_epilogue(cuda):
+    torch.manual_seed(12)
+    N, H, W, C, K = 2, 14, 14, 64, 128
+    gy = torch.randn(N, H, W, K, device=cuda).bfloat16()
+    w = (torch.randn(K, 3, 3, C, device=cuda) * 0.05).bfloat16()
+    x = torch.randn(N, H, W, C, device=cuda).bfloat16()
+    mean, invstd = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    gamma, beta = torch.ones(C, device=cuda), torch.zeros(C, device=cuda)
+    reps = torch.zeros(_C().conv_stat_replicas, 2, C, device=cuda)
+    e = torch.empty(0, device=cuda, dtype=torch.bfloat16)
+    dx = _C().conv_fwd(gy, _C().conv_dgrad_wtrans(w), 1, 1, 1, False, None, 0, None,
+                       [reps, x, e, mean, invstd, gamma, beta], True)
+    m = (x.float() > 0).float()
+    ge = (dx.float() * m).reshape(-1, C)
+    assert _rel(reps.sum(0)[0], ge.sum(0)) < 1e-3
+    assert _rel(reps.sum(0)[1], (ge * x.float().reshape(-1, C)).sum(0)) < 1e-3
