@@ -328,10 +328,10 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
   }
 
   // ---- epilogue: lane holds C[m][n..n+3]
-  if (E.mode == 3) {  // this split's private fp32 slab, plain stores
-    E.c = reinterpret_cast<float*>(E.c) + (long)blockIdx.z * E.slab;
-    E.mode = 0;
-  }
+  // locals, not writes into the by-value kernarg struct: mutating E makes the compiler copy the whole
+  // (large) Epi into scratch memory
+  void* const ec = E.mode == 3 ? (void*)(reinterpret_cast<float*>(E.c) + (long)blockIdx.z * E.slab) : E.c;
+  const int emode = E.mode == 3 ? 0 : E.mode;  // mode 3 = this split's private fp32 slab, plain stores
   float st_s[4][4], st_q[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -380,24 +380,26 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
         }
       }
       if (E.out_f32) {
-        float* cp = reinterpret_cast<float*>(E.c) + (long)m * E.ldc + n;
-        if (E.mode == 2) {
+        float* cp = reinterpret_cast<float*>(ec) + (long)m * E.ldc + n;
+        if (emode == 2) {
           for (int r = 0; r < 4 && n + r < N; ++r) atomicAdd(cp + r, v[r]);
         } else if (full) {
           float4 o = make_float4(v[0], v[1], v[2], v[3]);
-          if (E.mode == 1) {
+          if (emode == 1) {
             const float4 old = *reinterpret_cast<const float4*>(cp);
             o.x += old.x; o.y += old.y; o.z += old.z; o.w += old.w;
           }
           *reinterpret_cast<float4*>(cp) = o;
         } else {
-          for (int r = 0; r < 4 && n + r < N; ++r) cp[r] = (E.mode == 1 ? cp[r] : 0.f) + v[r];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n + r < N) cp[r] = (emode == 1 ? cp[r] : 0.f) + v[r];
         }
       } else {
-        uint16_t* cp = reinterpret_cast<uint16_t*>(E.c) + (long)m * E.ldc + n;
+        uint16_t* cp = reinterpret_cast<uint16_t*>(ec) + (long)m * E.ldc + n;
         if (full) {
           bf16x4_t o;
-          if (E.mode == 1) {
+          if (emode == 1) {
             const bf16x4_t old = *reinterpret_cast<const bf16x4_t*>(cp);
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] += bf2f((uint16_t)old[r]);
@@ -422,8 +424,10 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
             }
           }
         } else {
-          for (int r = 0; r < 4 && n + r < N; ++r) {
-            const uint16_t o = f2bf(v[r] + (E.mode == 1 ? bf2f(cp[r]) : 0.f));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {  // static r: keeps st_s/st_q in registers (a dynamic bound spills them)
+            if (n + r >= N) continue;
+            const uint16_t o = f2bf(v[r] + (emode == 1 ? bf2f(cp[r]) : 0.f));
             cp[r] = o;
             if (E.bstats) {
               const long off = (long)m * E.ldc + n + r;

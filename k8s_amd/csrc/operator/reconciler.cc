@@ -304,7 +304,10 @@ void JobWorker::run() {
       bool del = false;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait_for(lk, interval_, [&] { return poked_ || deleted_ || stop_; });
+        // system_clock deadline: libstdc++ maps steady_clock waits to pthread_cond_clockwait, which GCC 11's
+        // ThreadSanitizer does not intercept (it then misreports the mutex as double-locked); a wall-clock
+        // jump only moves one resync tick
+        cv_.wait_until(lk, std::chrono::system_clock::now() + interval_, [&] { return poked_ || deleted_ || stop_; });
         if (stop_) break;
         del = deleted_;
         poked_ = false;

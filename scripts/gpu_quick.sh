@@ -4,7 +4,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 echo "pytest exit $rc" >> gpurun_out/pytest_gpu.log; tail -25 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 && grep metric gpurun_out/bench.log &&
