@@ -1,0 +1,153 @@
+"""HTTP front-end of the in-memory API server (``fakeapi.store.ApiStore``).
+
+Speaks the subset of the Kubernetes REST protocol the operator, the e2e
+binary, the kubelet and the ``tfjob`` CLI use: JSON bodies, Status error
+objects, ``?labelSelector=``, and ``?watch=true&resourceVersion=N`` streams
+delivered with chunked transfer encoding, one ``{"type","object"}`` JSON
+event per line (410 Gone as an ERROR event when the version is compacted).
+
+    python -m k8s_amd.fakeapi.server --port 8080
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import socket
+import threading
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from typing import Optional
+from urllib.parse import parse_qs, urlparse
+
+from k8s_amd.fakeapi.store import ApiStore
+
+
+class _Handler(BaseHTTPRequestHandler):
+    protocol_version = "HTTP/1.1"
+    store: ApiStore = None  # set per server class
+
+    def log_message(self, fmt, *args):  # quiet
+        pass
+
+    def _body(self) -> Optional[dict]:
+        n = int(self.headers.get("Content-Length") or 0)
+        if n <= 0:
+            return None
+        raw = self.rfile.read(n)
+        try:
+            return json.loads(raw)
+        except ValueError:
+            return None
+
+    def _send(self, code: int, body):
+        data = json.dumps(body).encode() if body is not None else b""
+        try:
+            self.send_response(code)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(data)))
+            self.end_headers()
+            self.wfile.write(data)
+        except (BrokenPipeError, ConnectionResetError):
+            pass  # the client went away (e.g. an operator shutting down mid-request)
+
+    def _dispatch(self, method):
+        u = urlparse(self.path)
+        q = {k: v[-1] for k, v in parse_qs(u.query).items()}
+        body = self._body() if method in ("POST", "PUT", "PATCH", "DELETE") else None
+        if method == "GET" and q.get("watch") in ("true", "1"):
+            return self._watch(q.get("resourceVersion") or None)
+        if u.path in ("/healthz", "/readyz", "/livez"):
+            data = b"ok"
+            self.send_response(200)
+            self.send_header("Content-Length", "2")
+            self.end_headers()
+            self.wfile.write(data)
+            return
+        if u.path == "/version":
+            return self._send(200, {"major": "1", "minor": "30", "gitVersion": "v1.30.0-k8s-amd-fake"})
+        code, out = self.store.handle_obj(method, self.path, body)
+        self._send(code, out)
+
+    def _chunk(self, data: bytes):
+        self.wfile.write(b"%x\r\n%s\r\n" % (len(data), data))
+        self.wfile.flush()
+
+    def _watch(self, rv):
+        self.send_response(200)
+        self.send_header("Content-Type", "application/json")
+        self.send_header("Transfer-Encoding", "chunked")
+        self.end_headers()
+        try:
+            for typ, obj in self.store.watch_from(self.path, rv):
+                if typ is None:
+                    continue  # heartbeat; a write failure below ends the stream
+                self._chunk((json.dumps({"type": typ, "object": obj}) + "\n").encode())
+                if typ == "ERROR":
+                    break
+            self.wfile.write(b"0\r\n\r\n")
+        except (BrokenPipeError, ConnectionResetError, OSError):
+            pass
+        self.close_connection = True
+
+    def do_GET(self):
+        self._dispatch("GET")
+
+    def do_POST(self):
+        self._dispatch("POST")
+
+    def do_PUT(self):
+        self._dispatch("PUT")
+
+    def do_PATCH(self):
+        self._dispatch("PATCH")
+
+    def do_DELETE(self):
+        self._dispatch("DELETE")
+
+
+class FakeApiServer:
+    """Run an ApiStore behind HTTP on 127.0.0.1:<port> in a background thread."""
+
+    def __init__(self, store: Optional[ApiStore] = None, port: int = 0, host: str = "127.0.0.1"):
+        self.store = store or ApiStore()
+        handler = type("Handler", (_Handler,), {"store": self.store})
+        self.httpd = ThreadingHTTPServer((host, port), handler)
+        self.httpd.daemon_threads = True
+        self.port = self.httpd.server_address[1]
+        self.url = "http://%s:%d" % (host, self.port)
+        self.thread = threading.Thread(target=self.httpd.serve_forever, daemon=True)
+
+    def start(self):
+        self.thread.start()
+        return self
+
+    def stop(self):
+        self.httpd.shutdown()
+        self.httpd.server_close()
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *a):
+        self.stop()
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="in-memory Kubernetes API server (k8s_amd test double)")
+    ap.add_argument("--port", type=int, default=8080)
+    ap.add_argument("--host", default="127.0.0.1")
+    a = ap.parse_args(argv)
+    srv = FakeApiServer(port=a.port, host=a.host)
+    print("fake API server on %s" % srv.url, flush=True)
+    srv.httpd.serve_forever()
+
+
+if __name__ == "__main__":
+    main()

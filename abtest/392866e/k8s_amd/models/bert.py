@@ -1,0 +1,146 @@
+"""BERT-base pretraining model (MLM + NSP) on the k8s_amd op set.
+
+BASELINE config 3: "BERT-base TfJob 8 WORKER data-parallel, fused Adam HIP
+kernel". Architecture = bert-base-uncased: vocab 30522 (padded to 30528 so
+every GEMM is MFMA-tile friendly; the 6 pad logits are excluded from the loss
+by the cross-entropy kernel's row stride), hidden 768, 12 layers, 12 heads,
+FFN 3072, GELU, post-LN, LayerNorm eps 1e-12, max 512 positions, 2 token
+types. MLM decoder weights are tied to the word embeddings (the flat store
+counts the two uses, ``Param.uses = 2``).
+
+Per layer the hot path is: fused QKV GEMM -> flash attention (key-padding
+mask) -> O GEMM (+bias) -> add & LayerNorm fused kernel -> FFN1 GEMM with
+bias+GELU epilogue -> FFN2 GEMM (+bias) -> add & LayerNorm.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+
+from k8s_amd.ops import nn as K
+from k8s_amd.ops.attention import attention
+from k8s_amd.parallel.flat import ParamStore, init_const, init_normal
+
+
+@dataclass
+class BertConfig:
+    vocab_size: int = 30522
+    hidden: int = 768
+    layers: int = 12
+    heads: int = 12
+    intermediate: int = 3072
+    max_position: int = 512
+    type_vocab: int = 2
+    eps: float = 1e-12
+    init_std: float = 0.02
+
+    @property
+    def padded_vocab(self) -> int:
+        return (self.vocab_size + 63) // 64 * 64
+
+
+BERT_BASE = BertConfig()
+BERT_TINY = BertConfig(vocab_size=1000, hidden=128, layers=2, heads=2, intermediate=512, max_position=128)
+
+
+class BertLayer(nn.Module):
+    def __init__(self, store: ParamStore, name: str, c: BertConfig):
+        super().__init__()
+        h, f = c.hidden, c.intermediate
+        std = init_normal(c.init_std)
+        self.c = c
+        self.qkv_w = store.new(name + ".attention.qkv.weight", (3 * h, h), std)
+        self.qkv_b = store.new(name + ".attention.qkv.bias", (3 * h,), init_const(0), decay=False, lowp=False)
+        self.o_w = store.new(name + ".attention.output.dense.weight", (h, h), std)
+        self.o_b = store.new(name + ".attention.output.dense.bias", (h,), init_const(0), decay=False, lowp=False)
+        self.ln1_g = store.new(name + ".attention.output.LayerNorm.weight", (h,), init_const(1), decay=False,
+                               lowp=False)
+        self.ln1_b = store.new(name + ".attention.output.LayerNorm.bias", (h,), init_const(0), decay=False,
+                               lowp=False)
+        self.f1_w = store.new(name + ".intermediate.dense.weight", (f, h), std)
+        self.f1_b = store.new(name + ".intermediate.dense.bias", (f,), init_const(0), decay=False, lowp=False)
+        self.f2_w = store.new(name + ".output.dense.weight", (h, f), std)
+        self.f2_b = store.new(name + ".output.dense.bias", (h,), init_const(0), decay=False, lowp=False)
+        self.ln2_g = store.new(name + ".output.LayerNorm.weight", (h,), init_const(1), decay=False, lowp=False)
+        self.ln2_b = store.new(name + ".output.LayerNorm.bias", (h,), init_const(0), decay=False, lowp=False)
+
+    def forward(self, x, B, S, kv_lens):
+        c = self.c
+        h, nh = c.hidden, c.heads
+        d = h // nh
+        qkv = K.linear(x, self.qkv_w, self.qkv_b)  # [T, 3h]
+        q, k, v = qkv.split([h, h, h], dim=-1)
+        o = attention(q.reshape(B, S, nh, d), k.reshape(B, S, nh, d), v.reshape(B, S, nh, d), causal=False,
+                      kv_lens=kv_lens)
+        a = K.linear(o.reshape(B * S, h), self.o_w, self.o_b)
+        x, _ = K.layer_norm(a, self.ln1_g, self.ln1_b, c.eps, residual=x)
+        f = K.linear(x, self.f1_w, self.f1_b, act="gelu")
+        f = K.linear(f, self.f2_w, self.f2_b)
+        x, _ = K.layer_norm(f, self.ln2_g, self.ln2_b, c.eps, residual=x)
+        return x
+
+
+class BertForPreTraining(nn.Module):
+    def __init__(self, store: ParamStore, c: BertConfig = BERT_BASE):
+        super().__init__()
+        self.store, self.c = store, c
+        h = c.hidden
+        std = init_normal(c.init_std)
+        self.word = store.new("bert.embeddings.word_embeddings.weight", (c.padded_vocab, h), std)
+        self.word.uses = 2  # embedding gather + tied MLM decoder
+        self.pos = store.new("bert.embeddings.position_embeddings.weight", (c.max_position, h), std)
+        self.typ = store.new("bert.embeddings.token_type_embeddings.weight", (c.type_vocab, h), std)
+        self.emb_ln_g = store.new("bert.embeddings.LayerNorm.weight", (h,), init_const(1), decay=False, lowp=False)
+        self.emb_ln_b = store.new("bert.embeddings.LayerNorm.bias", (h,), init_const(0), decay=False, lowp=False)
+        self.layers = nn.ModuleList([BertLayer(store, "bert.encoder.layer.%d" % i, c) for i in range(c.layers)])
+        self.pool_w = store.new("bert.pooler.dense.weight", (h, h), std)
+        self.pool_b = store.new("bert.pooler.dense.bias", (h,), init_const(0), decay=False, lowp=False)
+        self.mlm_w = store.new("cls.predictions.transform.dense.weight", (h, h), std)
+        self.mlm_b = store.new("cls.predictions.transform.dense.bias", (h,), init_const(0), decay=False, lowp=False)
+        self.mlm_ln_g = store.new("cls.predictions.transform.LayerNorm.weight", (h,), init_const(1), decay=False,
+                                  lowp=False)
+        self.mlm_ln_b = store.new("cls.predictions.transform.LayerNorm.bias", (h,), init_const(0), decay=False,
+                                  lowp=False)
+        self.dec_b = store.new("cls.predictions.bias", (c.padded_vocab,), init_const(0), decay=False, lowp=False)
+        self.nsp_w = store.new("cls.seq_relationship.weight", (64, h), std)  # 2 classes, padded to 64 rows
+        self.nsp_b = store.new("cls.seq_relationship.bias", (64,), init_const(0), decay=False, lowp=False)
+
+    def finalize(self, device, **kw):
+        self.store.finalize(device, **kw)
+        return self.to(device)
+
+    def forward(self, input_ids, token_type_ids, mlm_labels, nsp_labels, kv_lens=None, dtype=torch.bfloat16):
+        B, S = input_ids.shape
+        c = self.c
+        h = c.hidden
+        pos_ids = torch.arange(S, device=input_ids.device).expand(B, S)
+        e = (K.embedding(input_ids, self.word, dtype) + K.embedding(pos_ids, self.pos, dtype)
+             + K.embedding(token_type_ids, self.typ, dtype))
+        x = K.layer_norm(e.reshape(B * S, h), self.emb_ln_g, self.emb_ln_b, c.eps)
+        for layer in self.layers:
+            x = layer(x, B, S, kv_lens)
+        # MLM head on every token (labels -100 are ignored by the loss kernel)
+        t = K.linear(x, self.mlm_w, self.mlm_b, act="gelu")
+        t = K.layer_norm(t, self.mlm_ln_g, self.mlm_ln_b, c.eps)
+        logits = K.linear(t, self.word, self.dec_b)  # tied decoder, [T, padded_vocab]
+        mlm = K.cross_entropy(logits, mlm_labels.reshape(-1), valid=c.vocab_size)
+        # NSP head on [CLS]
+        cls = x.reshape(B, S, h)[:, 0].contiguous()
+        pooled = torch.tanh(K.linear(cls, self.pool_w, self.pool_b).float()).to(dtype)
+        nsp_logits = K.linear(pooled, self.nsp_w, self.nsp_b)
+        nsp = K.cross_entropy(nsp_logits, nsp_labels, valid=2)
+        return mlm + nsp, mlm, nsp
+
+
+def synthetic_batch(c: BertConfig, batch: int, seq: int, device, generator=None, mask_prob=0.15):
+    g = generator
+    ids = torch.randint(0, c.vocab_size, (batch, seq), device=device, generator=g)
+    tt = torch.zeros(batch, seq, dtype=torch.long, device=device)
+    tt[:, seq // 2:] = 1
+    sel = torch.rand(batch, seq, device=device, generator=g) < mask_prob
+    labels = torch.where(sel, ids, torch.full_like(ids, -100))
+    nsp = torch.randint(0, 2, (batch,), device=device, generator=g)
+    return ids, tt, labels, nsp

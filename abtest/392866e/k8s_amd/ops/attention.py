@@ -1,0 +1,94 @@
+"""Attention (K5) entry point.
+
+``attention(q, k, v, causal, kv_lens)`` with token-major layouts:
+q [B, S, Hq, D], k/v [B, S, Hkv, D] (GQA: Hq % Hkv == 0), bf16.
+
+GPU: the gfx950 flash-attention kernels (``csrc/kernels/attention.hip``:
+online-softmax forward writing the log-sum-exp, recompute backward with
+dK/dV in registers and atomically accumulated dQ). q/k/v may be strided
+views (e.g. column slices of the fused QKV projection) -- no copies. Head
+dims other than 64/128 and CPU tensors use an explicit matmul/softmax
+reference (no SDPA dispatch, so no Triton-built kernels run).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from k8s_amd.ops._ext import load as _load
+
+
+def _flash_ok(q, k, v) -> bool:
+    if not (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in (64, 128)):
+        return False
+    ok = all(t.stride(-1) == 1 and all(s % 8 == 0 for s in t.stride()[:3]) and t.data_ptr() % 16 == 0
+             for t in (q, k, v))
+    return ok and hasattr(_load(), "flash_fwd")  # _load() raises if the extension is missing on a GPU box
+
+
+def attention_reference(q, k, v, causal: bool, kv_lens: Optional[torch.Tensor] = None, scale: Optional[float] = None):
+    B, S, Hq, D = q.shape
+    Hkv = k.shape[2]
+    rep = Hq // Hkv
+    scale = scale or 1.0 / math.sqrt(D)
+    qh = q.permute(0, 2, 1, 3).float()
+    kh = k.permute(0, 2, 1, 3).float().repeat_interleave(rep, dim=1)
+    vh = v.permute(0, 2, 1, 3).float().repeat_interleave(rep, dim=1)
+    s = torch.matmul(qh, kh.transpose(-1, -2)) * scale
+    Sk = k.shape[1]
+    if causal:
+        mask = torch.ones(S, Sk, dtype=torch.bool, device=q.device).triu(1)
+        s = s.masked_fill(mask, float("-inf"))
+    if kv_lens is not None:
+        keymask = torch.arange(Sk, device=q.device)[None, :] >= kv_lens[:, None].to(q.device)
+        s = s.masked_fill(keymask[:, None, None, :], float("-inf"))
+    p = torch.softmax(s, -1)
+    o = torch.matmul(p, vh)
+    return o.permute(0, 2, 1, 3).to(q.dtype)
+
+
+class _Flash(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, causal, kv_lens, scale):
+        C = _load()
+        if kv_lens is not None:
+            kv_lens = kv_lens.to(device=q.device, dtype=torch.int32).contiguous()
+        o, lse = C.flash_fwd(q, k, v, causal, kv_lens, scale)
+        ctx.save_for_backward(q, k, v, o, lse, kv_lens if kv_lens is not None else torch.empty(0))
+        ctx.causal, ctx.scale, ctx.has_lens = causal, scale, kv_lens is not None
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, lens = ctx.saved_tensors
+        C = _load()
+        dq, dk, dv = C.flash_bwd(do.contiguous(), q, k, v, o, lse, ctx.causal, lens if ctx.has_lens else None,
+                                 ctx.scale)
+        return dq, dk, dv, None, None, None
+
+
+class _Reference(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, causal, kv_lens, scale):
+        ctx.save_for_backward(q, k, v)
+        ctx.causal, ctx.kv_lens, ctx.scale = causal, kv_lens, scale
+        with torch.no_grad():
+            return attention_reference(q, k, v, causal, kv_lens, scale)
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v = ctx.saved_tensors
+        with torch.enable_grad():
+            qq, kk, vv = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+            o = attention_reference(qq, kk, vv, ctx.causal, ctx.kv_lens, ctx.scale)
+            dq, dk, dv = torch.autograd.grad(o, (qq, kk, vv), do.float())
+        return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype), None, None, None
+
+
+def attention(q, k, v, causal: bool = False, kv_lens: Optional[torch.Tensor] = None, scale: Optional[float] = None):
+    scale = scale or 1.0 / math.sqrt(q.shape[-1])
+    if _flash_ok(q, k, v):
+        return _Flash.apply(q, k, v, causal, kv_lens, scale)
+    return _Reference.apply(q, k, v, causal, kv_lens, scale)

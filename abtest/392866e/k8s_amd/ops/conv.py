@@ -25,13 +25,6 @@ import torch.nn.functional as F
 from k8s_amd.ops import autotune
 from k8s_amd.ops._ext import load as _load
 
-import os
-
-# BatchNorm-backward statistics in the dgrad epilogue (ops.nn.BnBwdLink). Off by default: measured on
-# MI355X, the epilogue's extra loads cost more GEMM time than the separate reduction pass they replace
-# (ResNet-50 b256: 6700 vs 7200 img/s). K8S_AMD_BN_LINK=1 turns it on.
-BN_LINK = os.environ.get("K8S_AMD_BN_LINK", "0") == "1"
-
 STATS = {"hip_fwd": 0, "aten_fwd": 0, "hip_wgrad": 0, "aten_wgrad": 0, "hip_dgrad": 0, "aten_dgrad": 0}
 
 
@@ -99,27 +92,23 @@ def _wgrad_hip(C_, gy, x, out, stride, padding, acc):
         C_.conv_wgrad(x, gy, out, stride, padding, 1, 0, acc)
 
 
-def _dgrad_hip(C_, gy, w, padding, addend=None, bnb=None):
+def _dgrad_hip(C_, gy, w, padding, addend=None):
     """dx on our kernels; with ``addend`` (bf16, shape of dx) a 1x1 dgrad accumulates onto it in the GEMM
-    epilogue and returns it (the fused residual-gradient add). ``bnb`` = (list, relu_x) from
-    BnBwdLink.epilogue_args: the epilogue also reduces the BN backward's statistics of dx."""
+    epilogue and returns it (the fused residual-gradient add)."""
     K, R, S, C = w.shape
-    bl, brx = bnb if bnb is not None else (None, None)
     if R == 1 and S == 1 and padding == 0:
         N, H, W_, _ = gy.shape
         if addend is not None:
             C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, addend.view(-1, C), False, None, 0, None, True,
-                    1.0, 1, bl, brx)
+                    1.0, 1)
             return addend
         return C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, None, False, None, 0, None, False, 1.0,
-                       1, bl, brx).reshape(N, H, W_, C)
-    if addend is not None:  # (no 3x3 consumer needs both; keep the statistics exact: reduce after the add)
-        bl = None
-    dx = C_.conv_fwd(gy, C_.conv_dgrad_wtrans(w), 1, R - 1 - padding, 1, False, None, 0, None, bl, brx)
+                       1).reshape(N, H, W_, C)
+    dx = C_.conv_fwd(gy, C_.conv_dgrad_wtrans(w), 1, R - 1 - padding, 1, False, None, 0, None)
     return dx if addend is None else dx.add_(addend)
 
 
-def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, bn_link=None):
+def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None):
     """Returns dx (+ ``addend``, e.g. the residual branch's gradient of the same tensor, fused into the
     dgrad epilogue where our kernel runs) or None; deposits dw into ``p``'s flat gradient slot."""
     K, R, S, C = w.shape
@@ -156,10 +145,7 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, bn_link=No
                     ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, True, False)[0].add_(addend))]) == "hip"
         if use_hip:
             STATS["hip_dgrad"] += 1
-            bnb = None
-            if BN_LINK and bn_link is not None and p is not None and (R == 1 or addend is None):
-                bnb = bn_link.epilogue_args(p.store, gy.device)
-            dx = _dgrad_hip(C_, gy, w, padding, addend, bnb)
+            dx = _dgrad_hip(C_, gy, w, padding, addend)
         else:
             STATS["aten_dgrad"] += 1
             dx, _ = _aten_bwd(gy, x, w, stride, padding, True, False)

@@ -1,0 +1,151 @@
+"""GEMM entry points (K1) for linear layers, on the gfx950 MFMA kernel.
+
+``mm(a, b, a_kmajor, b_kmajor, ...)`` is the raw kernel (bf16 in, fp32 acc,
+bf16/fp32 out, bias / ReLU / GELU epilogue, fp32 accumulate, split-K
+atomics). ``linear_fwd`` / ``linear_bwd`` express a Linear layer's three
+products with it WITHOUT materialising any transpose:
+
+    fwd    y  = x . W^T          A = x   [M,K] K-major,  B = W [N,K] K-major
+    dgrad  dx = g . W            A = g   [M,N] K-major,  B = W [N,K] read N-major
+    wgrad  dW = g^T . x          A = g   read M-major,   B = x read N-major  (split-K, fp32 out
+                                                             straight into the flat gradient slot)
+
+Where the vendor library (hipBLASLt behind torch.matmul / addmm) can run the
+same plain product, ``ops.autotune`` times both once per shape and keeps the
+faster; fused epilogues the library lacks (GELU with the pre-activation side
+output, fp32 split-K accumulation straight into the flat gradient slot) are
+charged the extra elementwise / cast passes the library path needs, so the
+comparison is end to end. CPU tensors (and shapes the kernel does not take)
+use plain PyTorch.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from k8s_amd.ops import autotune
+from k8s_amd.ops._ext import load as _load
+
+ACT = {None: 0, "relu": 1, "gelu": 2}
+
+
+def hip_ok(*ts) -> bool:
+    return all(t.is_cuda and t.dtype == torch.bfloat16 for t in ts)
+
+
+def mm(a, b, a_kmajor=True, b_kmajor=True, out=None, out_f32=False, bias=None, act=None, pre=None,
+       accumulate=False, alpha=1.0, splits=1):
+    return _load().gemm(a, a_kmajor, b, b_kmajor, out, out_f32, bias, ACT[act], pre, accumulate, alpha, splits)
+
+
+def _shape_ok(M, N, K) -> bool:
+    return K % 64 == 0 and N % 8 == 0 and M % 8 == 0
+
+
+def _act_fwd(y, act):
+    if act is None:
+        return y
+    if act == "relu":
+        return torch.relu(y)
+    if act == "gelu":
+        return F.gelu(y, approximate="tanh")
+    raise ValueError(act)
+
+
+def _act_bwd(gy, pre_or_out, act):
+    if act is None:
+        return gy
+    if gy.is_cuda and gy.dtype == torch.bfloat16 and gy.numel() % 8 == 0 and act in ("relu", "gelu"):
+        C = _load()
+        g = gy.contiguous()
+        return C.relu_bwd(g, pre_or_out.contiguous()) if act == "relu" else C.gelu_bwd(g, pre_or_out.contiguous())
+    if act == "relu":
+        return gy * (pre_or_out > 0)
+    if act == "gelu":
+        x = pre_or_out.float()
+        k0, k1 = 0.7978845608028654, 0.044715
+        t = torch.tanh(k0 * (x + k1 * x ** 3))
+        d = 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k0 * (1 + 3 * k1 * x * x)
+        return (gy.float() * d).to(gy.dtype)
+    raise ValueError(act)
+
+
+def _blas_fwd(x, w, b, act):
+    y = torch.addmm(b.to(x.dtype), x, w.t()) if b is not None else torch.mm(x, w.t())
+    pre = y
+    y = _act_fwd(y, act)
+    return y, (pre if act == "gelu" else (y if act == "relu" else None))
+
+
+def _hip_fwd(x, w, b, act):
+    M, N = x.shape[0], w.shape[0]
+    pre = torch.empty((M, N), device=x.device, dtype=torch.bfloat16) if act == "gelu" else None
+    y = mm(x, w, True, True, bias=b, act=act, pre=pre)
+    return y, (pre if act == "gelu" else (y if act == "relu" else None))
+
+
+def linear_fwd(x, w, b, act=None):
+    """Returns (y, saved) where saved is what linear_bwd needs for the activation derivative."""
+    M, K = x.shape
+    N = w.shape[0]
+    if hip_ok(x, w) and _shape_ok(M, N, K) and x.stride(1) == 1:
+        key = "linear_fwd|%dx%dx%d|%s|%d" % (M, N, K, act, b is not None)
+        if autotune.choose(key, [("hip", lambda: _hip_fwd(x, w, b, act)),
+                                 ("blas", lambda: _blas_fwd(x, w, b, act))]) == "hip":
+            return _hip_fwd(x, w, b, act)
+        return _blas_fwd(x, w, b, act)
+    y = torch.matmul(x, w.t())
+    if b is not None:
+        y = y + b.to(y.dtype)
+    pre = y
+    y = _act_fwd(y, act)
+    return y, (pre if act == "gelu" else (y if act == "relu" else None))
+
+
+def linear_bwd(gy, x, w, saved, act, pw=None, store=None):
+    """dx and the parameter gradient. With (pw, store) on GPU the weight gradient is written
+    (or accumulated) straight into the flat fp32 gradient slot; returns (dx, dw_or_None, db)."""
+    g = _act_bwd(gy, saved, act)
+    M, K = x.shape
+    N = w.shape[0]
+    db = None
+    if g.is_cuda and g.dtype == torch.bfloat16 and N % 8 == 0:
+        db = _load().colsum(g.contiguous())
+    else:
+        db = g.float().sum(0)
+    if hip_ok(g, x, w) and _shape_ok(M, N, K) and N % 64 == 0:
+        g = g.contiguous()
+        dims = "%dx%dx%d" % (M, N, K)
+        if autotune.choose("linear_dgrad|" + dims, [("hip", lambda: mm(g, w, True, False)),
+                                                    ("blas", lambda: torch.mm(g, w))]) == "hip":
+            dx = mm(g, w, True, False)
+        else:
+            dx = torch.mm(g, w)
+        if pw is not None and store is not None and pw.grad.dtype == torch.float32:
+            acc = pw.written
+
+            def hip_w(out, accumulate):
+                mm(g, x, False, False, out=out, out_f32=True, accumulate=accumulate, splits=0)
+
+            def blas_w(out, accumulate):
+                d = torch.mm(g.t(), x)
+                out.add_(d) if accumulate else out.copy_(d)
+
+            if autotune.choose("linear_wgrad|" + dims, [
+                    ("hip", lambda: hip_w(torch.empty_like(pw.grad), False)),
+                    ("blas", lambda: blas_w(torch.empty_like(pw.grad), False))]) == "hip":
+                hip_w(pw.grad, acc)
+            else:
+                blas_w(pw.grad, acc)
+            if acc:
+                store._notify(pw)
+            else:
+                store.mark_written(pw)
+            return dx, None, db
+        dw = mm(g, x, False, False, out_f32=True, splits=0)
+        return dx, dw, db
+    dx = torch.matmul(g, w)
+    dw = torch.matmul(g.t(), x)
+    return dx, dw, db

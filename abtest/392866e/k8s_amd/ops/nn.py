@@ -1,0 +1,415 @@
+"""Autograd ops of k8s_amd: HIP kernels on GPU, fp32 references on CPU.
+
+Every op that owns parameters takes :class:`~k8s_amd.parallel.flat.Param`
+handles plus the store's ``anchor`` and deposits parameter gradients straight
+into the flat gradient buffer (see ``parallel/flat.py``); it returns ``None``
+for them to autograd.
+
+Layouts: convolution activations are NHWC ``[N, H, W, C]`` bf16 (channels
+last, what the MFMA implicit-GEMM and the NHWC BatchNorm kernels want);
+conv weights are KRSC ``[K, R, S, C]``; linear weights ``[out, in]``.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from k8s_amd.ops import reference as ref
+from k8s_amd.ops._ext import load as _load_ext
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def _C():
+    return _load_ext()
+
+
+# =========================================================================== convolution
+def _conv_impl():
+    from k8s_amd.ops import conv as _conv  # lazy: conv module selects HIP implicit-GEMM vs MIOpen oracle
+
+    return _conv
+
+
+def _zero_scratch(store, device, n):
+    from k8s_amd.parallel.flat import ZeroArena
+
+    arena = store.__dict__.get("zero_arena")
+    if arena is None or arena.device != torch.device(device):
+        arena = store.zero_arena = ZeroArena(device)
+    return arena.take(n)
+
+
+class GradLink:
+    """Carries one tensor's gradient from one autograd node to another that runs later in the backward
+    pass, so the sum of the two contributions is formed inside a kernel (e.g. a ResNet identity block:
+    the residual branch's dres is accumulated in conv1's dgrad epilogue instead of by a separate add)."""
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+
+class _Conv2dNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, p, stride, padding, with_stats, link=None):
+        impl = _conv_impl()
+        w = p.weight if x.dtype == p.weight.dtype else p.master.to(x.dtype)
+        sums = None
+        if with_stats and impl.fwd_uses_hip(x, w, stride, padding):
+            sums = _zero_scratch(p.store, x.device, _C().conv_stat_replicas * 2 * w.shape[0]).view(
+                _C().conv_stat_replicas, 2, w.shape[0])
+        y = impl.conv_fwd(x, w, stride, padding, sums)
+        ctx.save_for_backward(x)
+        ctx.p, ctx.stride, ctx.padding, ctx.link = p, stride, padding, link
+        ctx.x_requires_grad = x.requires_grad
+        if sums is not None:
+            ctx.mark_non_differentiable(sums)
+        return y, sums
+
+    @staticmethod
+    def backward(ctx, gy, _gsums=None):
+        (x,) = ctx.saved_tensors
+        p = ctx.p
+        impl = _conv_impl()
+        w = p.weight if x.dtype == p.weight.dtype else p.master.to(x.dtype)
+        gy = gy.contiguous()
+        addend = None
+        if ctx.link is not None:
+            addend, ctx.link.grad = ctx.link.grad, None
+        dx = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, ctx.x_requires_grad, p, addend=addend)
+        return dx, None, None, None, None, None, None
+
+
+def conv2d_nhwc(x: torch.Tensor, p, stride: int = 1, padding: int = 0, with_stats: bool = False,
+                grad_link: "GradLink" = None):
+    """NHWC convolution with KRSC weight ``p`` (no bias).
+
+    With ``with_stats`` returns ``(y, sums)``: ``sums`` = fp32 [2, K] per-channel sum / sum of squares of y
+    accumulated in the conv epilogue (None when the layer runs on the fallback path) -- the following
+    ``batch_norm_act(..., sums=sums)`` then needs no statistics pass. ``grad_link``: a gradient for x
+    deposited there by a later-backward node (``batch_norm_act(res_link=...)``) is added to dx in the dgrad."""
+    y, sums = _Conv2dNHWC.apply(x, p.store.anchor, p, stride, padding, with_stats, grad_link)
+    return (y, sums) if with_stats else y
+
+
+# =========================================================================== batchnorm + act
+class _BnAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, res, anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu, sums=None,
+                res_link=None):
+        x = x.contiguous()
+        if res is not None:
+            res = res.contiguous()
+        if _gpu(x) and sums is not None and training:
+            y, mean, invstd = _C().bn_fwd_from_sums(x, res, pg.master, pb.master, sums, run_mean, run_var, momentum,
+                                                    eps, relu)
+        elif _gpu(x):
+            y, mean, invstd = _C().bn_fwd(x, res, pg.master, pb.master, run_mean, run_var, training, momentum, eps,
+                                          relu)
+        else:
+            y, mean, invstd = ref.bn_fwd(x, res, pg.master, pb.master, run_mean, run_var, training, momentum, eps,
+                                         relu)
+        # without a residual the ReLU mask is recomputed from x in the backward kernels (no need to keep y)
+        keep_y = relu and (res is not None or not _gpu(x))
+        ctx.save_for_backward(x, y if keep_y else None, mean, invstd)
+        ctx.pg, ctx.pb, ctx.has_res, ctx.res_link = pg, pb, res is not None, res_link
+        ctx.relu_x = relu and not keep_y
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, invstd = ctx.saved_tensors
+        pg, pb = ctx.pg, ctx.pb
+        store = pg.store
+        dy = dy.contiguous()
+        if _gpu(x):
+            sg, sb = store.slot_for_write(pg), store.slot_for_write(pb)
+            dg = sg if sg is not None else torch.empty(pg.shape, device=x.device, dtype=torch.float32)
+            db = sb if sb is not None else torch.empty(pb.shape, device=x.device, dtype=torch.float32)
+            dx, dres = _C().bn_bwd(dy, x, y, mean, invstd, pg.master, pb.master, ctx.relu_x, dg, db, ctx.has_res)
+            if sg is not None:
+                store.mark_written(pg)
+            else:
+                store.deposit(pg, dg)
+            if sb is not None:
+                store.mark_written(pb)
+            else:
+                store.deposit(pb, db)
+        else:
+            dx, dres, dg, db = ref.bn_bwd(dy, x, y, mean, invstd, pg.master)
+            store.deposit(pg, dg)
+            store.deposit(pb, db)
+        if ctx.has_res and ctx.res_link is not None:  # hand dres to the node that adds it in a kernel
+            ctx.res_link.grad, dres = dres, None
+        return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None, None
+
+
+def batch_norm_act(x, pg, pb, run_mean, run_var, residual=None, relu=True, training=True, momentum=0.1,
+                   eps=1e-5, sums=None, res_link=None):
+    """y = act(BN(x) + residual) over the last (channel) dim of an NHWC tensor.
+
+    ``sums`` (fp32 [2, C] from ``conv2d_nhwc(..., with_stats=True)``) skips the statistics pass.
+    ``res_link``: the residual's gradient is handed to that GradLink (and NOT returned to autograd); the
+    node consuming the link must add it (``conv2d_nhwc(..., grad_link=link)`` on the same tensor)."""
+    return _BnAct.apply(x, residual, pg.store.anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu,
+                        sums, res_link)
+
+
+# =========================================================================== layernorm / rmsnorm
+class _Norm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, res, anchor, pg, pb, eps, rms):
+        x = x.contiguous()
+        if res is not None:
+            res = res.contiguous()
+        beta = pb.master if pb is not None else None
+        if _gpu(x):
+            y, mean, rstd, xsum = _C().norm_fwd(x, res, pg.master, beta, eps, rms)
+        else:
+            y, mean, rstd, xsum = ref.norm_fwd(x, res, pg.master, beta, eps, rms)
+        xin = xsum if res is not None else x
+        ctx.save_for_backward(xin, mean, rstd)
+        ctx.pg, ctx.pb, ctx.rms, ctx.has_res = pg, pb, rms, res is not None
+        if res is not None:
+            return y, xsum
+        return y, None
+
+    @staticmethod
+    def backward(ctx, dy, dxsum):
+        xin, mean, rstd = ctx.saved_tensors
+        pg, pb = ctx.pg, ctx.pb
+        store = pg.store
+        dy = dy.contiguous()
+        dres = dxsum.contiguous() if (dxsum is not None and ctx.has_res) else None
+        if _gpu(xin):
+            dg = torch.empty(pg.shape, device=xin.device, dtype=torch.float32)
+            db = torch.empty(pb.shape, device=xin.device, dtype=torch.float32) if pb is not None else None
+            dx = _C().norm_bwd(dy, xin, pg.master, mean, rstd, dres, dg, db, ctx.rms)
+        else:
+            dx, dg, db = ref.norm_bwd(dy, xin, pg.master, mean, rstd, dres, ctx.rms)
+        store.deposit(pg, dg)
+        if pb is not None:
+            store.deposit(pb, db)
+        return dx, (dx if ctx.has_res else None), None, None, None, None, None
+
+
+def layer_norm(x, pg, pb, eps=1e-12, residual=None):
+    """LayerNorm over the last dim; with ``residual`` returns (norm(x+res), x+res)."""
+    y, xsum = _Norm.apply(x, residual, pg.store.anchor, pg, pb, eps, False)
+    return (y, xsum) if residual is not None else y
+
+
+def rms_norm(x, pg, eps=1e-5, residual=None):
+    y, xsum = _Norm.apply(x, residual, pg.store.anchor, pg, None, eps, True)
+    return (y, xsum) if residual is not None else y
+
+
+# =========================================================================== linear
+def _gemm():
+    from k8s_amd.ops import gemm as _g
+
+    return _g
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, pw, pb, act):
+        g = _gemm()
+        w = pw.weight if x.dtype == pw.weight.dtype else pw.master.to(x.dtype)
+        x2 = x.reshape(-1, x.shape[-1])
+        b = pb.master if pb is not None else None
+        y, pre = g.linear_fwd(x2, w, b, act)
+        ctx.save_for_backward(x2, pre)
+        ctx.pw, ctx.pb, ctx.act, ctx.xshape = pw, pb, act, x.shape
+        return y.reshape(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, pre = ctx.saved_tensors
+        pw, pb = ctx.pw, ctx.pb
+        g = _gemm()
+        w = pw.weight if x2.dtype == pw.weight.dtype else pw.master.to(x2.dtype)
+        gy2 = gy.reshape(-1, gy.shape[-1]).contiguous()
+        dx, dw, db = g.linear_bwd(gy2, x2, w, pre, ctx.act, pw=pw, store=pw.store)
+        if dw is not None:
+            pw.store.deposit(pw, dw)
+        if pb is not None:
+            pb.store.deposit(pb, db)
+        return dx.reshape(ctx.xshape), None, None, None, None
+
+
+def linear(x, pw, pb=None, act: Optional[str] = None):
+    """y = act(x @ W^T + b); W [out, in] bf16 from the flat store."""
+    return _Linear.apply(x, pw.store.anchor, pw, pb, act)
+
+
+# =========================================================================== embedding
+class _Embedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, anchor, pw, dtype):
+        w = pw.weight if pw.weight.dtype == dtype else pw.master.to(dtype)
+        ctx.save_for_backward(ids)
+        ctx.pw = pw
+        return F.embedding(ids, w)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (ids,) = ctx.saved_tensors
+        pw = ctx.pw
+        V, D = pw.shape
+        dw = torch.zeros((V, D), device=gy.device, dtype=torch.float32)
+        dw.index_add_(0, ids.reshape(-1), gy.reshape(-1, D).float())
+        pw.store.deposit(pw, dw)
+        return None, None, None, None
+
+
+def embedding(ids, pw, dtype=torch.bfloat16):
+    return _Embedding.apply(ids, pw.store.anchor, pw, dtype)
+
+
+# =========================================================================== loss
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index, smoothing, valid):
+        # logits [R, Vpad]: only the first `valid` columns are classes (MFMA-friendly padded vocabularies)
+        logits = logits if logits.stride(-1) == 1 else logits.contiguous()
+        ctx.valid = valid
+        full = logits
+        if valid is not None and valid != logits.shape[1]:
+            logits = logits[:, :valid]
+        if _gpu(logits):
+            loss, lse = _C().xent_fwd(logits, labels, ignore_index, smoothing)
+        else:
+            loss, lse = ref.xent_fwd(logits, labels, ignore_index, smoothing)
+        nvalid = (labels != ignore_index).sum().clamp_min(1).float()
+        ctx.save_for_backward(full, labels, lse, nvalid)
+        ctx.ignore_index, ctx.smoothing = ignore_index, smoothing
+        return loss.sum() / nvalid
+
+    @staticmethod
+    def backward(ctx, gl):
+        full, labels, lse, nvalid = ctx.saved_tensors
+        dscale = (gl.float() / nvalid).reshape(1)
+        V = ctx.valid if ctx.valid is not None else full.shape[1]
+        if _gpu(full):
+            d = _C().xent_bwd(full, labels, lse, dscale, ctx.ignore_index, ctx.smoothing, V)
+        else:
+            d = torch.zeros_like(full)
+            d[:, :V] = ref.xent_bwd(full[:, :V], labels, lse, dscale, ctx.ignore_index, ctx.smoothing)
+        return d, None, None, None, None
+
+
+def cross_entropy(logits, labels, ignore_index: int = -100, smoothing: float = 0.0, valid: int = None):
+    """Mean softmax cross-entropy over valid rows of [R, V] logits (classes = first ``valid`` columns)."""
+    return _CrossEntropy.apply(logits.reshape(-1, logits.shape[-1]), labels.reshape(-1), ignore_index, smoothing,
+                               valid)
+
+
+# =========================================================================== pooling (NHWC)
+class _MaxPoolNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        y, idx = _C().maxpool_fwd(x.contiguous(), k, s, p)
+        ctx.save_for_backward(idx)
+        ctx.hw, ctx.ksp = x.shape[1:3], (k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        H, W = ctx.hw
+        return _C().maxpool_bwd(dy.contiguous(), idx, H, W, *ctx.ksp), None, None, None
+
+
+def max_pool_nhwc(x, k=3, s=2, p=1):
+    """NHWC max pooling; GPU: gfx950 kernel saving the winning window position as uint8 (gather backward)."""
+    if _gpu(x) and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0:
+        return _MaxPoolNHWC.apply(x, k, s, p)
+    y = F.max_pool2d(x.permute(0, 3, 1, 2), k, s, p)
+    return y.permute(0, 2, 3, 1).contiguous()
+
+
+def global_avg_pool_nhwc(x):
+    return x.mean(dim=(1, 2))
+
+
+# =========================================================================== transformer elementwise (K9)
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        gu = gu.contiguous()
+        F2 = gu.shape[-1] // 2
+        if _gpu(gu) and gu.dtype == torch.bfloat16 and F2 % 8 == 0:
+            y = _C().swiglu_fwd(gu)
+        else:
+            g, u = gu.float().split(F2, -1)
+            y = (torch.nn.functional.silu(g) * u).to(gu.dtype)
+        ctx.save_for_backward(gu)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (gu,) = ctx.saved_tensors
+        F2 = gu.shape[-1] // 2
+        dy = dy.contiguous()
+        if _gpu(gu) and gu.dtype == torch.bfloat16 and F2 % 8 == 0:
+            return _C().swiglu_bwd(gu, dy)
+        g, u = gu.float().split(F2, -1)
+        s = torch.sigmoid(g)
+        d = dy.float()
+        return torch.cat([d * u * s * (1 + g * (1 - s)), d * g * s], -1).to(gu.dtype)
+
+
+def swiglu(gu):
+    """silu(gate) * up over a fused [.., 2F] gate|up projection."""
+    return _SwiGLU.apply(gu)
+
+
+def rope_table(max_pos: int, dim: int, theta: float = 10000.0, device=None) -> torch.Tensor:
+    """[max_pos, dim/2, 2] fp32 (cos, sin), built once on the host side of the step."""
+    inv = 1.0 / (theta ** (torch.arange(0, dim, 2, dtype=torch.float64) / dim))
+    ang = torch.arange(max_pos, dtype=torch.float64)[:, None] * inv[None, :]
+    return torch.stack([ang.cos(), ang.sin()], -1).float().to(device)
+
+
+def _rope_ref(x, pos, table, inverse=False):
+    T = x.shape[0]
+    D = table.shape[1] * 2
+    xs = x.float().reshape(T, -1, D)
+    cs = table[pos.long()]  # [T, D/2, 2]
+    c, s = cs[..., 0][:, None, :], cs[..., 1][:, None, :]
+    if inverse:
+        s = -s
+    x1, x2 = xs[..., : D // 2], xs[..., D // 2:]
+    out = torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], -1)
+    return out.reshape(x.shape).to(x.dtype)
+
+
+class _Rope(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, pos, table):
+        ctx.save_for_backward(pos, table)
+        if _gpu(x) and x.dtype == torch.bfloat16:
+            y = x.contiguous().clone()
+            _C().rope_(y, pos, table, False)
+            return y
+        return _rope_ref(x, pos, table)
+
+    @staticmethod
+    def backward(ctx, dy):
+        pos, table = ctx.saved_tensors
+        if _gpu(dy) and dy.dtype == torch.bfloat16:
+            d = dy.contiguous().clone()
+            _C().rope_(d, pos, table, True)
+            return d, None, None
+        return _rope_ref(dy, pos, table, inverse=True), None, None
+
+
+def rope(x, pos, table):
+    """Rotary embedding of x [T, H*D] (token-major, rotate-half), pos [T] int32, table from ``rope_table``."""
+    return _Rope.apply(x, pos, table)

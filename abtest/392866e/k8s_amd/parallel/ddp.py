@@ -1,0 +1,121 @@
+"""Bucketed, backward-overlapped gradient all-reduce over RCCL (xGMI).
+
+Gradient buckets are contiguous ranges of the flat gradient buffer
+(``parallel/flat.py``) taken in REVERSE registration order, i.e. roughly the
+order backward produces them. When the last parameter of a bucket deposits
+its gradient, the bucket's all-reduce is enqueued immediately
+(``async_op=True``: RCCL runs on its own stream, ordered after the producing
+kernels), so communication overlaps the rest of backward. Buckets are always
+launched in index order so every rank issues the same collective sequence.
+
+Sizing for MI355X: a ring all-reduce over xGMI is per-link bound (~153 GB/s
+per link; RCCL spreads channels over the 7 links of a full 8-GPU mesh), and
+each collective has a fixed launch/latency cost of tens of microseconds. The
+default 64 MB bucket keeps that fixed cost below a few percent while still
+leaving several buckets to overlap for ResNet-50 (102 MB fp32 grads) and
+BERT-base (440 MB). With 288 GB of HBM there is no memory pressure to keep
+buckets small.
+
+Averaging is NOT done here: the optimizer kernel multiplies by 1/world in the
+same pass that applies the update.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from k8s_amd.parallel.flat import ALIGN, ParamStore, _round_up
+
+
+class _Bucket:
+    __slots__ = ("index", "lo", "hi", "params", "pending", "launched")
+
+    def __init__(self, index):
+        self.index = index
+        self.lo = None
+        self.hi = None
+        self.params = []
+        self.pending = 0
+        self.launched = False
+
+
+class GradReducer:
+    def __init__(self, store: ParamStore, group=None, bucket_mb: float = 64.0, enabled: Optional[bool] = None):
+        self.store = store
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.enabled = (self.world > 1) if enabled is None else enabled
+        elem = store.grad.element_size()
+        cap = max(ALIGN, int(bucket_mb * 1024 * 1024 / elem))
+        self.buckets: List[_Bucket] = []
+        cur = _Bucket(0)
+        for p in reversed(store.params):
+            lo, hi = p.offset, p.offset + _round_up(p.numel)
+            if cur.params and max(cur.hi, hi) - min(cur.lo, lo) > cap:
+                self.buckets.append(cur)
+                cur = _Bucket(len(self.buckets))
+            cur.params.append(p)
+            cur.lo = lo if cur.lo is None else min(cur.lo, lo)
+            cur.hi = hi if cur.hi is None else max(cur.hi, hi)
+        if cur.params:
+            self.buckets.append(cur)
+        self.bucket_of = {}
+        for b in self.buckets:
+            for p in b.params:
+                self.bucket_of[p.index] = b
+        self.works = []
+        self.next_launch = 0
+        store.hooks.append(self._on_deposit)
+
+    # ------------------------------------------------------------------ step protocol
+    def begin_step(self):
+        self.store.begin_step()
+        for b in self.buckets:
+            b.pending = sum(p.uses for p in b.params)
+            b.launched = False
+        self.works = []
+        self.next_launch = 0
+
+    def _on_deposit(self, p):
+        b = self.bucket_of.get(p.index)
+        if b is None:
+            return
+        b.pending -= 1
+        if self.enabled:
+            self._launch_ready()
+
+    def _launch_ready(self):
+        while self.next_launch < len(self.buckets):
+            b = self.buckets[self.next_launch]
+            if b.pending > 0:
+                return
+            self._launch(b)
+            self.next_launch += 1
+
+    def _launch(self, b: _Bucket):
+        if b.launched:
+            return
+        b.launched = True
+        t = self.store.grad[b.lo:b.hi]
+        self.works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+
+    def finish(self):
+        """Zero never-used gradients, flush remaining buckets, order the current stream after RCCL."""
+        for b in self.buckets:
+            if b.pending > 0:
+                for p in b.params:
+                    if not p.written:
+                        p.grad.zero_()
+                        p.written = True
+                b.pending = 0
+        if self.enabled:
+            self._launch_ready()
+            for w in self.works:
+                w.wait()
+        self.works = []
+
+    @property
+    def grad_scale(self) -> float:
+        return 1.0 / self.world if self.enabled else 1.0

@@ -1,0 +1,135 @@
+"""Process-group setup: one process per GPU, RCCL over xGMI.
+
+Two ways in:
+
+* ``torchrun``-style env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR /
+  MASTER_PORT) -- what ``bench.py`` is launched with.
+* ``TF_CONFIG`` -- what the operator injects into every replica
+  (`/root/reference/pkg/trainer/replicas.go:188-203`). ``rank_from_tf_config``
+  maps the cluster spec to a deterministic global rank order
+  (master -> 0, then worker 0..N-1, then ps 0..M-1; the chief named by the
+  TerminationPolicy is rank 0) and uses the MASTER service address as the
+  TCP-store rendezvous, so the operator's only contract with the workload
+  stays TF_CONFIG.
+"""
+from __future__ import annotations
+
+import datetime
+import json
+import os
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+ROLE_ORDER = ("master", "chief", "worker", "ps", "evaluator")
+
+
+@dataclass
+class RankInfo:
+    rank: int
+    world_size: int
+    local_rank: int
+    master_addr: str
+    master_port: int
+    role: str = "worker"
+    role_index: int = 0
+    compute_world: int = 1  # ranks that run the model (everything but ps)
+
+
+def resolve(addr: str) -> str:
+    """Map a TF_CONFIG "service:port" through $K8S_AMD_SERVICE_MAP (local kubelet's cluster-DNS stand-in)."""
+    m = os.environ.get("K8S_AMD_SERVICE_MAP")
+    if not m:
+        return addr
+    table = json.loads(m)
+    if addr in table:
+        return table[addr]
+    host = addr.rsplit(":", 1)[0]
+    return table.get(host, addr)
+
+
+def rank_from_tf_config(tf_config: str, port_offset: int = 1) -> RankInfo:
+    """Deterministic rank assignment from a TF_CONFIG JSON string.
+
+    Compute ranks (the collective group) are master/chief first, then workers;
+    PS tasks do not join the RCCL group (rank -1): in this framework the
+    parameter service is sharded over the compute ranks (parallel/ps.py) and
+    the PS replicas run the parameter/rendezvous server (ps_server/).
+    """
+    cfg = json.loads(tf_config)
+    cluster: Dict[str, List[str]] = cfg.get("cluster", {})
+    task = cfg.get("task", {})
+    ttype, tidx = task.get("type", "master").lower(), int(task.get("index", 0))
+    order = []
+    for role in ROLE_ORDER:
+        if role == "ps":
+            continue
+        for i, addr in enumerate(cluster.get(role, [])):
+            order.append((role, i, addr))
+    for role in sorted(cluster):  # unknown roles last, deterministic
+        if role not in ROLE_ORDER:
+            for i, addr in enumerate(cluster[role]):
+                order.append((role, i, addr))
+    if not order and not cluster.get("ps"):
+        raise ValueError("TF_CONFIG has an empty cluster")
+    keys = [(r, i) for r, i, _ in order]
+    if ttype == "ps":
+        rank = -1
+    elif (ttype, tidx) in keys:
+        rank = keys.index((ttype, tidx))
+    else:
+        raise ValueError("task %s:%d not in cluster %s" % (ttype, tidx, sorted(cluster)))
+    first = order[0][2] if order else cluster["ps"][0]
+    host, _, port = resolve(first).rpartition(":")
+    return RankInfo(rank=rank, world_size=len(order), local_rank=int(os.environ.get("LOCAL_RANK", 0)),
+                    master_addr=host or first, master_port=int(port or 2222) + port_offset, role=ttype,
+                    role_index=tidx, compute_world=len(order))
+
+
+def rank_from_env() -> Optional[RankInfo]:
+    if "WORLD_SIZE" in os.environ and "RANK" in os.environ:
+        ws = int(os.environ["WORLD_SIZE"])
+        return RankInfo(rank=int(os.environ["RANK"]), world_size=ws,
+                        local_rank=int(os.environ.get("LOCAL_RANK", 0)),
+                        master_addr=os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                        master_port=int(os.environ.get("MASTER_PORT", 29500)), compute_world=ws)
+    if "TF_CONFIG" in os.environ:
+        return rank_from_tf_config(os.environ["TF_CONFIG"])
+    return None
+
+
+def init_process_group(info: Optional[RankInfo] = None, backend: Optional[str] = None,
+                       timeout_s: float = 600.0) -> RankInfo:
+    """Initialise torch.distributed (nccl == RCCL on ROCm, gloo on CPU). Idempotent."""
+    info = info or rank_from_env() or RankInfo(0, 1, 0, "127.0.0.1", 29500)
+    if info.world_size > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(info.local_rank)
+        dist.init_process_group(backend=backend, init_method="tcp://%s:%d" % (info.master_addr, info.master_port),
+                                rank=info.rank, world_size=info.world_size,
+                                timeout=datetime.timedelta(seconds=timeout_s))
+    elif torch.cuda.is_available():
+        torch.cuda.set_device(info.local_rank)
+    return info
+
+
+def barrier():
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()
+
+
+def all_reduce_max(x: float, device) -> float:
+    if not (dist.is_available() and dist.is_initialized()):
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def destroy():
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Default parameter server for TfJob PS replicas (the IsDefaultPS path).
+
+CLI-compatible with the reference's default PS
+(`/root/reference/grpc_tensorflow_server/grpc_tensorflow_server.py:119-157`):
+
+    python grpc_tensorflow_server.py --cluster_spec "master|m-0:2222,ps|p-0:2222;p-1:2222" \\
+        --job_name ps --task_id 0 [--gpu_memory_fraction F] [--verbose]
+
+The operator ships this file in the ``cm-ps-<runtime id>`` ConfigMap
+(``grpcServerFilePath`` in the controller config) and runs it in every
+default-PS pod. Instead of a TF 1.x gRPC server it runs a small TCP task
+server that:
+
+* executes ops sent by other tasks on this task's device (what the smoke
+  workload's master uses to check every task runs a kernel), and
+* holds parameter shards for CPU-side push/pull (``put``/``get``/``add``
+  ops on named fp32 tensors) -- the GPU data plane uses RCCL instead
+  (``k8s_amd.parallel.ps``), this keeps the TF PS protocol shape for
+  small/CPU jobs and tests.
+
+The process blocks serving until it receives a ``shutdown`` message or
+SIGTERM (exit 0), mirroring ``server.join()``.
+The file is self-contained (stdlib + optional torch) because it is executed
+from a ConfigMap mount.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import socket
+import socketserver
+import struct
+import sys
+import threading
+
+
+def parse_cluster_spec(cluster_spec: str, job_name: str = "", task_id: int = 0):
+    """'job|h:p;h:p,job2|h:p' -> {job: [hosts]} with the reference's strict errors (:46-88)."""
+    cluster = {}
+    if not cluster_spec:
+        raise ValueError("Empty cluster_spec string")
+    for job_string in cluster_spec.split(","):
+        if not job_string:
+            raise ValueError("Empty job_string in cluster_spec")
+        parts = job_string.split("|")
+        if len(parts) != 2:
+            raise ValueError("Not exactly one instance of '|' in cluster_spec")
+        name, hosts = parts
+        if not name:
+            raise ValueError("Empty job_name in cluster_spec")
+        if name in cluster:
+            raise ValueError("Duplicate job_name in cluster_spec: %s" % name)
+        job_tasks = hosts.split(";")
+        if any(not t for t in job_tasks):
+            raise ValueError("Empty task string at position in cluster_spec")
+        cluster[name] = job_tasks
+    if job_name and job_name not in cluster:
+        raise ValueError("job_name %r not in cluster_spec" % job_name)
+    if job_name and not (0 <= task_id < len(cluster[job_name])):
+        raise ValueError("Invalid task_id: %d" % task_id)
+    return cluster
+
+
+def resolve(addr: str) -> str:
+    m = os.environ.get("K8S_AMD_SERVICE_MAP")
+    if m:
+        t = json.loads(m)
+        return t.get(addr) or t.get(addr.rsplit(":", 1)[0]) or addr
+    return addr
+
+
+# ----------------------------------------------------------------------------- wire protocol
+def send_msg(sock, obj):
+    data = json.dumps(obj).encode()
+    sock.sendall(struct.pack("!I", len(data)) + data)
+
+
+def recv_msg(sock):
+    hdr = b""
+    while len(hdr) < 4:
+        chunk = sock.recv(4 - len(hdr))
+        if not chunk:
+            return None
+        hdr += chunk
+    n = struct.unpack("!I", hdr)[0]
+    buf = b""
+    while len(buf) < n:
+        chunk = sock.recv(min(1 << 20, n - len(buf)))
+        if not chunk:
+            return None
+        buf += chunk
+    return json.loads(buf)
+
+
+def call(addr: str, obj, timeout: float = 30.0):
+    host, port = resolve(addr).rsplit(":", 1)
+    with socket.create_connection((host, int(port)), timeout=timeout) as s:
+        send_msg(s, obj)
+        return recv_msg(s)
+
+
+def _device():
+    try:
+        import torch
+
+        if torch.cuda.is_available() and os.environ.get("K8S_AMD_NO_GPU") != "1":
+            return torch, torch.device("cuda", 0)
+        return torch, torch.device("cpu")
+    except ImportError:
+        return None, None
+
+
+class TaskServer(socketserver.ThreadingTCPServer):
+    allow_reuse_address = True
+    daemon_threads = True
+
+    def __init__(self, addr, job, task, verbose=False):
+        self.job, self.task, self.verbose = job, task, verbose
+        self.params = {}
+        self.lock = threading.Lock()
+        super().__init__(addr, _TaskHandler)
+
+
+class _TaskHandler(socketserver.BaseRequestHandler):
+    def handle(self):
+        srv: TaskServer = self.server
+        while True:
+            msg = recv_msg(self.request)
+            if msg is None:
+                return
+            op = msg.get("op")
+            if srv.verbose:
+                print("[%s:%d] op=%s" % (srv.job, srv.task, op), flush=True)
+            if op == "multiply":  # the tf_smoke op: a * b on this task's device
+                torch, dev = _device()
+                if torch is not None:
+                    a = torch.tensor(msg["a"], dtype=torch.int32, device=dev)
+                    b = torch.tensor(msg["b"], dtype=torch.int32, device=dev)
+                    out = (a * b).cpu().tolist()
+                    where = str(dev)
+                else:
+                    out = [[x * y for x, y in zip(ra, rb)] for ra, rb in zip(msg["a"], msg["b"])]
+                    where = "cpu"
+                send_msg(self.request, {"ok": True, "result": out, "device": where,
+                                        "task": "/job:%s/task:%d" % (srv.job, srv.task)})
+            elif op == "put":
+                with srv.lock:
+                    srv.params[msg["name"]] = list(msg["value"])
+                send_msg(self.request, {"ok": True})
+            elif op == "add":  # push: accumulate a gradient-like update
+                with srv.lock:
+                    cur = srv.params.setdefault(msg["name"], [0.0] * len(msg["value"]))
+                    scale = float(msg.get("scale", 1.0))
+                    for i, v in enumerate(msg["value"]):
+                        cur[i] += scale * v
+                send_msg(self.request, {"ok": True})
+            elif op == "get":  # pull
+                with srv.lock:
+                    v = srv.params.get(msg["name"])
+                send_msg(self.request, {"ok": v is not None, "value": v})
+            elif op == "ping":
+                send_msg(self.request, {"ok": True, "task": "/job:%s/task:%d" % (srv.job, srv.task)})
+            elif op == "shutdown":
+                send_msg(self.request, {"ok": True})
+                threading.Thread(target=srv.shutdown, daemon=True).start()
+                return
+            else:
+                send_msg(self.request, {"ok": False, "error": "unknown op %r" % op})
+
+
+def serve(cluster, job_name, task_id, verbose=False) -> int:
+    addr = resolve(cluster[job_name][task_id])
+    host, port = addr.rsplit(":", 1)
+    bind_host = "127.0.0.1" if host in ("127.0.0.1", "localhost") else "0.0.0.0"
+    srv = TaskServer((bind_host, int(port)), job_name, task_id, verbose)
+    if threading.current_thread() is threading.main_thread():
+        signal.signal(signal.SIGTERM, lambda *a: threading.Thread(target=srv.shutdown, daemon=True).start())
+    print("Started server /job:%s/task:%d on %s" % (job_name, task_id, addr), flush=True)
+    srv.serve_forever()
+    srv.server_close()
+    return 0
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser(description="Run a default parameter server for a TfJob.")
+    p.add_argument("--cluster_spec", type=str, help="Cluster spec: 'job|host:port;host:port,job2|host:port'")
+    p.add_argument("--job_name", type=str, help="Job name: e.g., ps")
+    p.add_argument("--task_id", type=int, default=0, help="Task index, e.g., 0")
+    p.add_argument("--gpu_memory_fraction", type=float, default=1.0,
+                   help="Fraction of GPU memory allocated (per-process cap via torch)")
+    p.add_argument("--verbose", type=bool, default=False, help="Verbose mode")
+    a = p.parse_args(argv)
+    cluster = parse_cluster_spec(a.cluster_spec, a.job_name, a.task_id)
+    torch, dev = _device()
+    if torch is not None and dev is not None and dev.type == "cuda" and a.gpu_memory_fraction < 1.0:
+        torch.cuda.set_per_process_memory_fraction(a.gpu_memory_fraction, 0)
+    return serve(cluster, a.job_name, a.task_id, a.verbose)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

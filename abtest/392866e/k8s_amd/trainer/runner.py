@@ -1,0 +1,311 @@
+"""The TfJob workload: ``python -m k8s_amd.trainer``.
+
+What the operator launches in every replica's ``tensorflow`` container. Its
+only contract with the operator is the reference's: ``TF_CONFIG`` in the
+environment (`/root/reference/pkg/trainer/replicas.go:188-203`) and the
+process exit code (`/root/reference/pkg/trainer/training.go:45-73`):
+
+* role from ``TF_CONFIG.task``: MASTER/CHIEF/WORKER ranks form the RCCL group
+  (master -> rank 0, rendezvous on the master's service address); a PS task
+  runs the default parameter server until the master shuts it down;
+* data-parallel strategies: ``allreduce`` (bucketed RCCL all-reduce
+  overlapped with backward, ``parallel/ddp.py``) or ``ps`` (sharded parameter
+  service: reduce-scatter push / owner update / all-gather pull,
+  ``parallel/ps.py``);
+* exit codes: 0 success; 1 permanent (bad config, numerics, OOM -- the
+  reference treats OOMKilled as permanent); 128+ retryable (collective /
+  rendezvous / connection failures, SIGTERM): the operator restarts the
+  replica and it resumes from the latest checkpoint;
+* outputs (chief only): ``<logdir>/events.out.tfevents.*`` (TensorBoard),
+  ``<logdir>/metrics.jsonl`` (one JSON record per logged step, plus
+  ``start`` / ``step0`` / ``done`` events with wall-clock times so the
+  job-create -> step0 latency can be measured), and TF-style
+  ``<ckpt_dir>/model.ckpt-N`` checkpoints (``utils/checkpoint.py``).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import sys
+import time
+import traceback
+from typing import Optional
+
+import torch
+
+EXIT_OK = 0
+EXIT_PERMANENT = 1
+EXIT_RETRYABLE = 138  # 128 + 10: >= 128 is "retryable" in the operator's exit-code contract
+EXIT_SIGTERM = 143
+
+
+class RetryableError(RuntimeError):
+    pass
+
+
+def parse(argv=None):
+    from k8s_amd.models.registry import MODELS
+
+    ap = argparse.ArgumentParser(prog="python -m k8s_amd.trainer", description="k8s_amd TfJob trainer")
+    ap.add_argument("--model", default="resnet50", choices=MODELS)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--batch", type=int, default=None, help="per-rank batch (default: model preset)")
+    ap.add_argument("--seq", type=int, default=None)
+    ap.add_argument("--image", type=int, default=None)
+    ap.add_argument("--optimizer", default=None, choices=["sgd", "adam"])
+    ap.add_argument("--lr", type=float, default=None)
+    ap.add_argument("--weight-decay", type=float, default=None)
+    ap.add_argument("--warmup-steps", type=int, default=0, help="linear LR warmup")
+    ap.add_argument("--max-grad-norm", type=float, default=None)
+    ap.add_argument("--strategy", default="allreduce", choices=["allreduce", "ps"])
+    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
+    ap.add_argument("--logdir", default=os.environ.get("K8S_AMD_LOGDIR", ""))
+    ap.add_argument("--ckpt-dir", default=os.environ.get("K8S_AMD_CKPT_DIR", ""))
+    ap.add_argument("--ckpt-every", type=int, default=0)
+    ap.add_argument("--log-every", type=int, default=10)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--fresh-batches", action="store_true", help="draw a new synthetic batch every step")
+    ap.add_argument("--fail-at-step", type=int, default=-1, help="(testing) raise a retryable failure once")
+    return ap.parse_args(argv)
+
+
+_DEFAULT_BATCH = {"resnet50": 256, "resnet_tiny": 8, "bert_base": 64, "bert_tiny": 4, "llama3_8b": 2,
+                  "llama_1b": 4, "llama_tiny": 2}
+
+
+class _Metrics:
+    def __init__(self, logdir: str, enabled: bool):
+        self.enabled = enabled and bool(logdir)
+        self.tb = None
+        self.f = None
+        if self.enabled:
+            from k8s_amd.utils.tfevents import EventWriter
+
+            os.makedirs(logdir, exist_ok=True)
+            self.tb = EventWriter(logdir)
+            self.f = open(os.path.join(logdir, "metrics.jsonl"), "a")
+
+    def event(self, **rec):
+        rec.setdefault("time", time.time())
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if self.f:
+            self.f.write(line + "\n")
+            self.f.flush()
+
+    def scalars(self, step, values):
+        if self.tb:
+            self.tb.scalars(step, values)
+            self.tb.flush()
+
+    def close(self):
+        if self.tb:
+            self.tb.close()
+        if self.f:
+            self.f.close()
+
+
+def _shutdown_ps(tf_config: Optional[str]):
+    """The master tells the PS tasks to stop once training is done (real trainers exit 0 on all ranks)."""
+    if not tf_config:
+        return
+    from k8s_amd.parallel.dist import resolve
+    from k8s_amd.ps_server.grpc_tensorflow_server import call
+
+    cluster = json.loads(tf_config).get("cluster", {})
+    for addr in cluster.get("ps", []):
+        for _ in range(20):
+            try:
+                call(resolve(addr), {"op": "shutdown"}, timeout=5)
+                break
+            except OSError:
+                time.sleep(0.5)
+
+
+def _wait_for_ps(tf_config: Optional[str], timeout: float = 120.0):
+    """Liveness rendezvous with the PS tasks (the reference's workers block until the PS gRPC servers
+    answer); raises RetryableError when they never come up."""
+    if not tf_config:
+        return
+    from k8s_amd.parallel.dist import resolve
+    from k8s_amd.ps_server.grpc_tensorflow_server import call
+
+    end = time.time() + timeout
+    for addr in json.loads(tf_config).get("cluster", {}).get("ps", []):
+        while True:
+            try:
+                if call(resolve(addr), {"op": "ping"}, timeout=5).get("ok"):
+                    break
+            except OSError:
+                pass
+            if time.time() > end:
+                raise RetryableError("PS task %s unreachable" % addr)
+            time.sleep(0.2)
+
+
+def _run_ps(info, tf_config: str) -> int:
+    from k8s_amd.ps_server.grpc_tensorflow_server import serve
+
+    cluster = json.loads(tf_config).get("cluster", {})
+    return serve(cluster, "ps", info.role_index)
+
+
+def train(a) -> int:
+    from k8s_amd.models.registry import build
+    from k8s_amd.ops.optim import FusedAdam, FusedSGD
+    from k8s_amd.parallel import dist as kdist
+    from k8s_amd.parallel.ddp import GradReducer
+    from k8s_amd.parallel.ps import ShardedParameterService
+    from k8s_amd.utils import checkpoint as ckpt
+
+    t_start = time.time()
+    tf_config = os.environ.get("TF_CONFIG")
+    info = kdist.rank_from_env()
+    if info is not None and info.role == "ps" and tf_config:
+        return _run_ps(info, tf_config)
+    use_cuda = a.device == "cuda" or (a.device == "auto" and torch.cuda.is_available())
+    if a.device == "cuda" and not torch.cuda.is_available():
+        print("error: --device cuda but no GPU is visible", file=sys.stderr)
+        return EXIT_PERMANENT
+    try:
+        info = kdist.init_process_group(info, backend=("nccl" if use_cuda else "gloo"))
+    except (RuntimeError, OSError, ValueError) as e:  # rendezvous trouble is transient
+        raise RetryableError("process group init failed: %s" % e) from e
+    rank, world = max(info.rank, 0), info.world_size
+    chief = rank == 0
+    dev = torch.device("cuda", info.local_rank) if use_cuda else torch.device("cpu")
+    torch.manual_seed(a.seed + rank)
+    if chief:
+        _wait_for_ps(tf_config)
+    metrics = _Metrics(a.logdir, chief)
+    metrics.event(event="start", rank=rank, world=world, role=info.role, model=a.model, strategy=a.strategy,
+                  device=str(dev), start_time=t_start)
+
+    batch = a.batch or _DEFAULT_BATCH[a.model]
+    # the sharded parameter service needs the flat buffers divisible into world equal 64-aligned shards
+    from k8s_amd.parallel.flat import ALIGN
+
+    w = build(a.model, dev, batch, seq=a.seq, image=a.image, seed=a.seed, fixed_batch=not a.fresh_batches,
+              pad_to=world * ALIGN if a.strategy == "ps" else ALIGN, data_seed=a.seed * 7919 + rank)
+    opt_name = a.optimizer or w.optimizer
+    lr = a.lr if a.lr is not None else w.lr
+    if opt_name == "sgd":
+        wd = 5e-5 if a.weight_decay is None else a.weight_decay
+        opt = FusedSGD(w.store, lr=lr, momentum=0.9, weight_decay=wd, max_grad_norm=a.max_grad_norm)
+    else:
+        wd = 0.01 if a.weight_decay is None else a.weight_decay
+        opt = FusedAdam(w.store, lr=lr, weight_decay=wd, max_grad_norm=a.max_grad_norm)
+    if world > 1:  # identical initial weights everywhere
+        torch.distributed.broadcast(w.store.master, 0)
+        w.store.refresh_lowp()
+    if a.strategy == "ps":
+        svc = ShardedParameterService(w.store, opt, bucket_mb=a.bucket_mb)
+        begin, finish = svc.begin_step, (lambda lr_: svc.step(lr=lr_))
+    else:
+        red = GradReducer(w.store, bucket_mb=a.bucket_mb)
+        begin = red.begin_step
+
+        def finish(lr_):
+            red.finish()
+            opt.step(grad_scale=red.grad_scale, lr=lr_)
+        svc = None
+
+    # ---- restore
+    start_step = 0
+    if a.ckpt_dir:
+        base = ckpt.latest_checkpoint(a.ckpt_dir)
+        if base:
+            step0, tensors, meta = ckpt.load(base)
+            w.store.load_state_dict({k[len("params/"):]: v for k, v in tensors.items() if k.startswith("params/")})
+            bufs = dict(w.model.named_buffers())
+            for k, v in tensors.items():
+                if k.startswith("buffers/") and k[8:] in bufs:
+                    bufs[k[8:]].copy_(v)
+            osd = {k[len("optim/"):]: v.to(dev) for k, v in tensors.items() if k.startswith("optim/")}
+            osd["step"] = int(meta.get("optim_step", step0 + 1))
+            opt.load_state_dict(osd)
+            start_step = step0 + 1
+            metrics.event(event="restored", checkpoint=os.path.basename(base), step=step0)
+
+    def save(step):
+        if svc is not None:
+            svc.sync_state()
+        if not chief:
+            return
+        tensors = {"params/" + k: v for k, v in w.store.state_dict().items()}
+        tensors.update({"buffers/" + k: v for k, v in w.model.named_buffers()})
+        for k, v in opt.state_dict().items():
+            if torch.is_tensor(v):
+                tensors["optim/" + k] = v
+        base = ckpt.save(a.ckpt_dir, step, tensors, meta={"model": a.model, "optim_step": opt.step_count,
+                                                          "world": world})
+        metrics.event(event="checkpoint", step=step, path=base)
+
+    sync = torch.cuda.synchronize if use_cuda else (lambda: None)
+    t_last, n_last = time.time(), 0
+    loss_v = float("nan")
+    for step in range(start_step, a.steps):
+        if step == a.fail_at_step and a.ckpt_dir:
+            marker = os.path.join(a.ckpt_dir, ".injected_failure.%d" % rank)
+            if not os.path.exists(marker):
+                os.makedirs(a.ckpt_dir, exist_ok=True)
+                open(marker, "w").close()
+                raise RetryableError("injected failure at step %d" % step)
+        cur_lr = lr * min(1.0, (step + 1) / a.warmup_steps) if a.warmup_steps else lr
+        begin()
+        inputs = w.batch(step)
+        loss = w.loss(inputs)
+        loss.backward()
+        finish(cur_lr)
+        n_last += 1
+        if step == start_step or (step + 1) % a.log_every == 0 or step + 1 == a.steps:
+            loss_v = float(loss.detach().float().item())
+            if not (loss_v == loss_v and abs(loss_v) != float("inf")):
+                metrics.event(event="error", step=step, error="non-finite loss")
+                return EXIT_PERMANENT
+            sync()
+            now = time.time()
+            rate = n_last * w.units_per_step * world / max(now - t_last, 1e-9)
+            if step == start_step:
+                metrics.event(event="step0", step=step, loss=loss_v, since_start=now - t_start)
+            else:
+                metrics.event(event="step", step=step, loss=loss_v, lr=cur_lr,
+                              **{"%s_per_sec" % w.unit: round(rate, 2)})
+                metrics.scalars(step, {"loss": loss_v, "%s_per_sec" % w.unit: rate, "learning_rate": cur_lr})
+            t_last, n_last = now, 0
+        if a.ckpt_dir and a.ckpt_every and (step + 1) % a.ckpt_every == 0 and step + 1 < a.steps:
+            save(step)
+    if a.ckpt_dir and a.steps > start_step:
+        save(a.steps - 1)
+    kdist.barrier()
+    metrics.event(event="done", steps=a.steps, loss=loss_v, elapsed=time.time() - t_start)
+    metrics.close()
+    if chief:
+        _shutdown_ps(tf_config)
+    kdist.destroy()
+    return EXIT_OK
+
+
+def main(argv=None) -> int:
+    a = parse(argv)
+    signal.signal(signal.SIGTERM, lambda *_: os._exit(EXIT_SIGTERM))
+    try:
+        return train(a)
+    except RetryableError as e:
+        print("retryable failure: %s" % e, file=sys.stderr, flush=True)
+        return EXIT_RETRYABLE
+    except torch.cuda.OutOfMemoryError:
+        traceback.print_exc()
+        return EXIT_PERMANENT  # like OOMKilled: permanent
+    except (ConnectionError, TimeoutError) as e:
+        print("retryable failure: %r" % e, file=sys.stderr, flush=True)
+        return EXIT_RETRYABLE
+    except Exception as e:  # noqa: BLE001
+        msg = str(e)
+        traceback.print_exc()
+        if any(s in msg for s in ("NCCL", "RCCL", "Connection", "timed out", "Gloo", "gloo")):
+            return EXIT_RETRYABLE
+        return EXIT_PERMANENT

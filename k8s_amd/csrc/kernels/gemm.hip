@@ -26,6 +26,9 @@
 //    run on the same XCD (private L2).
 //  * epilogue: bias, ReLU / GELU(tanh), pre-activation side output, fp32 accumulate, split-K
 //    fp32 atomics (for the tall-K weight gradients).
+#include <stdexcept>
+#include <type_traits>
+
 #include "common.h"
 #include "launchers.h"
 #include "mfma.h"
@@ -238,7 +241,10 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 // WM x WN waves (WM * WN = 4), each owning a 64 x 64 piece: 128 x 128 tiles (2 x 2) in general, 256 x 64
 // (4 x 1) when N = 64 (the early ResNet convolutions and the stem) so no MFMA work is spent on padding.
 // Only K-major sources may sit on a 64-wide side (the MN-major swizzle assumes 256-B rows).
-template <class ASrc, class BSrc, int NBUF, int WM = 2, int WN = 2>
+// BNB: epilogue also reduces the BatchNorm-backward statistics (Epi::bstats). A separate instantiation:
+// compiled into every kernel, that code (7 more loads per output quad) costs ~30% on the plain GEMMs even
+// when disabled at run time.
+template <class ASrc, class BSrc, int NBUF, int WM = 2, int WN = 2, bool BNB = false>
 __global__ void __launch_bounds__(GEMM_THREADS, NBUF == 1 ? 3 : 2)
 gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
@@ -407,7 +413,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r]);
           *reinterpret_cast<bf16x4_t*>(cp) = o;
-          if (E.bstats) {
+          if constexpr (BNB) {
             const long off = (long)m * E.ldc + n;
             const bf16x4_t xv = *reinterpret_cast<const bf16x4_t*>(E.bx + off);
             bf16x4_t yv;
@@ -429,7 +435,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
             if (n + r >= N) continue;
             const uint16_t o = f2bf(v[r] + (emode == 1 ? bf2f(cp[r]) : 0.f));
             cp[r] = o;
-            if (E.bstats) {
+            if constexpr (BNB) {
               const long off = (long)m * E.ldc + n + r;
               const float xh = (bf2f(E.bx[off]) - E.bmean[n + r]) * E.binvstd[n + r];
               bool on = true;
@@ -444,7 +450,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
       }
     }
   }
-  float* const stat_out = E.stats ? E.stats : E.bstats;
+  float* const stat_out = BNB ? E.bstats : E.stats;
   if (stat_out) {
     // lanes with equal (lane >> 4) hold the same 4 columns: reduce over the 16 row lanes, then over the two
     // row-waves through LDS, so the block issues 4 full-wave atomic instructions (256 columns x {sum, sumsq})
@@ -489,16 +495,34 @@ static int effective_splits(int K, int splits) {
   return (K + kps - 1) / kps;
 }
 
+// operand pairs that produce a BatchNorm output gradient (the dgrads): the only BNB instantiations
+template <class ASrc, class BSrc>
+constexpr bool kBnbPair = (std::is_same_v<ASrc, KMajor> && std::is_same_v<BSrc, MNMajorK>) ||
+                          (std::is_same_v<ASrc, ConvA> && std::is_same_v<BSrc, KMajor>);
+
+template <class ASrc, class BSrc, int WM, int WN, bool BNB>
+static void launch_tiles2(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
+                          hipStream_t st) {
+  const int tiles = ((M + 64 * WM - 1) / (64 * WM)) * ((N + 64 * WN - 1) / (64 * WN));
+  if (kps <= 2 * BK)
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN, BNB>), dim3(tiles, 1, splits), dim3(GEMM_THREADS),
+                       0, st, a, b, e, M, N, K, kps);
+  else
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2, WM, WN, BNB>), dim3(tiles, 1, splits), dim3(GEMM_THREADS),
+                       0, st, a, b, e, M, N, K, kps);
+}
+
 template <class ASrc, class BSrc, int WM, int WN>
 static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
                          hipStream_t st) {
-  const int tiles = ((M + 64 * WM - 1) / (64 * WM)) * ((N + 64 * WN - 1) / (64 * WN));
-  if (kps <= 2 * BK)
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN>), dim3(tiles, 1, splits), dim3(GEMM_THREADS), 0, st,
-                       a, b, e, M, N, K, kps);
-  else
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2, WM, WN>), dim3(tiles, 1, splits), dim3(GEMM_THREADS), 0, st,
-                       a, b, e, M, N, K, kps);
+  if constexpr (kBnbPair<ASrc, BSrc>) {
+    if (e.bstats) {
+      launch_tiles2<ASrc, BSrc, WM, WN, true>(a, b, e, M, N, K, kps, splits, st);
+      return;
+    }
+  }
+  if (e.bstats) throw std::runtime_error("BatchNorm-backward epilogue requested for an operand pair without it");
+  launch_tiles2<ASrc, BSrc, WM, WN, false>(a, b, e, M, N, K, kps, splits, st);
 }
 
 template <class ASrc, class BSrc>

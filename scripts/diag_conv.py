@@ -7,7 +7,7 @@ import sys
 import traceback
 
 os.environ.setdefault("K8S_AMD_AUTOTUNE_CACHE", "none")
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.environ.get("K8S_AMD_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
