@@ -21,7 +21,9 @@ def load(build_if_missing: bool = False):
     if _C is not None:
         return _C
     try:
-        _C = importlib.import_module("k8s_amd._C")
+        from k8s_amd.utils.debug import maybe_wrap
+
+        _C = maybe_wrap(importlib.import_module("k8s_amd._C"))
         return _C
     except ImportError as e:  # pragma: no cover - depends on build state
         _ERR = e
@@ -29,7 +31,9 @@ def load(build_if_missing: bool = False):
             from k8s_amd import _build
 
             _build.build_kernels()
-            _C = importlib.import_module("k8s_amd._C")
+            from k8s_amd.utils.debug import maybe_wrap
+
+            _C = maybe_wrap(importlib.import_module("k8s_amd._C"))
             return _C
         raise ImportError(
             "k8s_amd native kernels are not built (k8s_amd/_C*.so missing): run "

@@ -20,7 +20,11 @@ process exit code (`/root/reference/pkg/trainer/training.go:45-73`):
   ``<logdir>/metrics.jsonl`` (one JSON record per logged step, plus
   ``start`` / ``step0`` / ``done`` events with wall-clock times so the
   job-create -> step0 latency can be measured), and TF-style
-  ``<ckpt_dir>/model.ckpt-N`` checkpoints (``utils/checkpoint.py``).
+  ``<ckpt_dir>/model.ckpt-N`` checkpoints (``utils/checkpoint.py``);
+* ``--hang-timeout S``: a watchdog exits 143 (retryable) when no step completes for S seconds (a wedged
+  collective); ``--trace 1|sync`` wraps the step phases in ROCTx ranges for ``rocprofv3 --marker-trace``
+  (``sync`` also logs per-phase milliseconds) -- ``utils/trace.py``. ``K8S_AMD_CHECK_NUMERICS=1`` /
+  ``K8S_AMD_SYNC_OPS=1`` turn on the kernel debug checks (``utils/debug.py``).
 """
 from __future__ import annotations
 
@@ -69,6 +73,11 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--fresh-batches", action="store_true", help="draw a new synthetic batch every step")
     ap.add_argument("--fail-at-step", type=int, default=-1, help="(testing) raise a retryable failure once")
+    ap.add_argument("--hang-timeout", type=float, default=float(os.environ.get("K8S_AMD_HANG_TIMEOUT", "0")),
+                    help="exit 143 (retryable) when no step completes for this many seconds (0: off)")
+    ap.add_argument("--hang-at-step", type=int, default=-1, help="(testing) stall forever at this step")
+    ap.add_argument("--trace", default=os.environ.get("K8S_AMD_TRACE", ""), choices=["", "0", "1", "sync"],
+                    help="ROCTx ranges per step phase (rocprofv3 --marker-trace); 'sync' also logs phase_ms")
     return ap.parse_args(argv)
 
 
@@ -160,6 +169,7 @@ def train(a) -> int:
     from k8s_amd.parallel.ddp import GradReducer
     from k8s_amd.parallel.ps import ShardedParameterService
     from k8s_amd.utils import checkpoint as ckpt
+    from k8s_amd.utils.trace import Tracer, Watchdog
 
     t_start = time.time()
     tf_config = os.environ.get("TF_CONFIG")
@@ -245,6 +255,9 @@ def train(a) -> int:
         metrics.event(event="checkpoint", step=step, path=base)
 
     sync = torch.cuda.synchronize if use_cuda else (lambda: None)
+    tracer = Tracer(enabled=a.trace not in ("", "0"), sync=(a.trace == "sync"), sync_fn=sync)
+    # the first step includes kernel autotuning / vendor-library tuning: the watchdog starts after it
+    watchdog = Watchdog(a.hang_timeout) if a.hang_timeout > 0 else None
     t_last, n_last = time.time(), 0
     loss_v = float("nan")
     for step in range(start_step, a.steps):
@@ -254,13 +267,24 @@ def train(a) -> int:
                 os.makedirs(a.ckpt_dir, exist_ok=True)
                 open(marker, "w").close()
                 raise RetryableError("injected failure at step %d" % step)
+        if step == a.hang_at_step:
+            time.sleep(1e9)  # (testing) a stalled collective
         cur_lr = lr * min(1.0, (step + 1) / a.warmup_steps) if a.warmup_steps else lr
-        begin()
-        inputs = w.batch(step)
-        loss = w.loss(inputs)
-        loss.backward()
-        finish(cur_lr)
+        with tracer.phase("step"):
+            begin()
+            with tracer.phase("data"):
+                inputs = w.batch(step)
+            with tracer.phase("forward"):
+                loss = w.loss(inputs)
+            with tracer.phase("backward"):
+                loss.backward()
+            with tracer.phase("reduce+update"):
+                finish(cur_lr)
         n_last += 1
+        if watchdog is not None:
+            if step == start_step:
+                watchdog.start()
+            watchdog.kick()
         if step == start_step or (step + 1) % a.log_every == 0 or step + 1 == a.steps:
             loss_v = float(loss.detach().float().item())
             if not (loss_v == loss_v and abs(loss_v) != float("inf")):
@@ -272,14 +296,17 @@ def train(a) -> int:
             if step == start_step:
                 metrics.event(event="step0", step=step, loss=loss_v, since_start=now - t_start)
             else:
+                extra = {"phase_ms": tracer.summary_ms()} if tracer.sync else {}
                 metrics.event(event="step", step=step, loss=loss_v, lr=cur_lr,
-                              **{"%s_per_sec" % w.unit: round(rate, 2)})
+                              **{"%s_per_sec" % w.unit: round(rate, 2)}, **extra)
                 metrics.scalars(step, {"loss": loss_v, "%s_per_sec" % w.unit: rate, "learning_rate": cur_lr})
             t_last, n_last = now, 0
         if a.ckpt_dir and a.ckpt_every and (step + 1) % a.ckpt_every == 0 and step + 1 < a.steps:
             save(step)
     if a.ckpt_dir and a.steps > start_step:
         save(a.steps - 1)
+    if watchdog is not None:
+        watchdog.stop()
     kdist.barrier()
     metrics.event(event="done", steps=a.steps, loss=loss_v, elapsed=time.time() - t_start)
     metrics.close()
