@@ -111,7 +111,7 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (ips / BASELINE_VALUE) if BASELINE_VALUE else None,
-            "dtype": "bf16",
+            "dtype": "bf16" if dev.type == "cuda" else "fp32",
             "data": "synthetic (random %dx%dx3 images, random labels, random-init weights)" % (a.image, a.image),
             "config": {
                 "model": "resnet50-v1.5",
