@@ -64,6 +64,10 @@ int main(int argc, char** argv) {
   fl.def("all-namespaces", "false", "Manage TfJobs in every namespace", true);
   fl.def("reconcile-interval", "8s", "Resync period of every TfJob (reference: 8s)");
   fl.def("leader-elect", "true", "Run leader election on Endpoints tf-operator", true);
+  // cmd/tf_operator/main.go:42-44 hard-codes 15s / 5s / 3s; kept as the defaults, settable for HA drills/tests
+  fl.def("lease-duration", "15s", "Leader-election lease duration");
+  fl.def("renew-deadline", "5s", "Leader-election renew deadline");
+  fl.def("retry-period", "3s", "Leader-election retry period");
   fl.def("create-crd", "true", "Register the tfjobs.tensorflow.org CRD at startup", true);
   std::string err = fl.parse(argc, argv);
   if (!err.empty()) {
@@ -143,6 +147,9 @@ int main(int argc, char** argv) {
   ec.ns = ns;
   ec.name = "tf-operator";
   ec.identity = pod;
+  ec.lease = std::chrono::milliseconds(parse_duration_ms(fl.str("lease-duration"), 15000));
+  ec.renew_deadline = std::chrono::milliseconds(parse_duration_ms(fl.str("renew-deadline"), 5000));
+  ec.retry = std::chrono::milliseconds(parse_duration_ms(fl.str("retry-period"), 3000));
   LeaderElector el(*api, ec);
   if (std::string e = el.check(); !e.empty()) {
     log_error("leader election config: %s", e.c_str());

@@ -59,7 +59,7 @@ def load_manifests(path: str) -> List[dict]:
 class LocalCluster:
     def __init__(self, gpus: Optional[List[int]] = None, port: int = 0, reconcile_interval: str = "500ms",
                  operator_bin: str = OPERATOR_BIN, log_dir: Optional[str] = None, extra_env=None,
-                 chaos_level: int = -1):
+                 chaos_level: int = -1, operator_args: Optional[List[str]] = None):
         self.log_dir = log_dir or tempfile.mkdtemp(prefix="k8s_amd_cluster_")
         self.server = FakeApiServer(port=port)
         self.client = ApiClient(self.server.url)
@@ -68,6 +68,7 @@ class LocalCluster:
         self.operator_bin = operator_bin
         self.reconcile_interval = reconcile_interval
         self.chaos_level = chaos_level
+        self.operator_args = list(operator_args or [])
         self.op_proc = None
         self.t_start = None
 
@@ -88,7 +89,7 @@ class LocalCluster:
         self.op_proc = subprocess.Popen(
             [self.operator_bin, "-controller_config_file", cfg_path, "-master", self.server.url,
              "-reconcile-interval", self.reconcile_interval, "-chaos-level", str(self.chaos_level),
-             "-alsologtostderr", "-v=1"],
+             "-alsologtostderr", "-v=1"] + self.operator_args,
             env=env, stdout=self.op_log, stderr=subprocess.STDOUT)
         # wait for the operator to register the CRD
         end = time.time() + 30

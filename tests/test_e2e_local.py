@@ -110,3 +110,40 @@ def test_cpp_e2e_binary_tap():
                             "--timeout", "90", "--num_jobs", "2"], capture_output=True, text=True, timeout=150)
         assert r.returncode == 0, r.stdout + r.stderr + c.operator_log()[-3000:]
         assert r.stdout.splitlines()[:2] == ["1..1", "ok 1 - Successfully ran TfJob"]
+
+
+def _leader(c):
+    ep = c.client.get("/api/v1/namespaces/default/endpoints/tf-operator")
+    return json.loads(ep["metadata"]["annotations"]["control-plane.alpha.kubernetes.io/leader"])
+
+
+def test_leader_election_failover():
+    """Two operator replicas (chart replicas=2): one leads on Endpoints tf-operator, the standby takes over when
+    the leader dies, and the new leader reconciles jobs (reference: cmd/tf_operator/main.go:125-148,
+    pkg/util/k8sutil/election/election.go:141-265)."""
+    fast = ["-lease-duration", "2s", "-renew-deadline", "1s", "-retry-period", "200ms"]
+    with LocalCluster(operator_args=fast) as c:
+        rec = _leader(c)
+        assert rec["holderIdentity"] == "tf-operator-local-0" and rec["leaseDurationSeconds"] == 2
+        env = dict(os.environ, MY_POD_NAMESPACE="default", MY_POD_NAME="tf-operator-local-1")
+        log1 = open(os.path.join(c.log_dir, "tf_operator_1.log"), "wb")
+        standby = subprocess.Popen([OPERATOR_BIN, "-master", c.url, "-reconcile-interval", "300ms"] + fast, env=env,
+                                   stdout=log1, stderr=subprocess.STDOUT)
+        try:
+            time.sleep(1.5)  # the leader keeps renewing: the standby must not steal the lease
+            assert standby.poll() is None
+            assert _leader(c)["holderIdentity"] == "tf-operator-local-0"
+            c.op_proc.kill()
+            c.op_proc.wait()
+            end = time.time() + 15
+            while _leader(c)["holderIdentity"] != "tf-operator-local-1" and time.time() < end:
+                time.sleep(0.1)
+            rec2 = _leader(c)
+            assert rec2["holderIdentity"] == "tf-operator-local-1"
+            assert rec2["leaderTransitions"] == rec.get("leaderTransitions", 0) + 1
+            c.create(_job("afterfailover", "exit 0"))
+            assert _wait_state(c, "afterfailover", {"Succeeded"})["status"]["state"] == "Succeeded"
+        finally:
+            standby.kill()
+            standby.wait()
+            log1.close()
