@@ -558,13 +558,32 @@ static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act,
   return e;
 }
 
-// Choose split-K so that small-MN / tall-K products (weight gradients) still fill 256 CUs.
+// Choose split-K for small-MN / tall-K products (weight gradients) with a wave-quantisation cost model:
+//   T(s) = ceil(tiles * s / slots) * ceil(ktiles / s)            -- block rounds x K tiles per block
+//        + s * M * N * 8 B / HBM BW / t_ktile                     -- fp32 slab write + reduce read per split
+// slots = resident blocks on 256 CUs (2 per CU double-buffered, 3 single-buffered). The previous rule
+// (double s until tiles * s >= 512) landed most ResNet-50 3x3 weight gradients on 576 blocks = 1.125
+// rounds; measured on MI355X (scripts/sweep_wgrad_splits.py) the model's choice is 1.3-1.5x faster there.
+// Up to 1024 splits: a single-tile product (64x64 1x1 weight gradient over 802816 rows) otherwise runs one
+// latency-bound block per CU.
 int gemm_choose_splits(int M, int N, int K) {
-  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const long tiles = (long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const int ktiles = (K + BK - 1) / BK;
-  int s = 1;
-  while (tiles * s < 512 && ktiles / (s * 2) >= 4 && s < 256) s *= 2;
-  return s;
+  const double slab_cost = (double)M * N * 8.0 / 5.0e12 / 2.0e-6;  // in units of one K tile (~2 us / block)
+  int best_s = 1;
+  double best = 1e30;
+  for (int s = 1; s <= 1024 && s <= ktiles; ++s) {
+    const int kpt = (ktiles + s - 1) / s;       // K tiles per split
+    if ((ktiles + kpt - 1) / kpt != s) continue;  // same kps as a smaller s
+    const long slots = kpt * BK <= 2 * BK ? 3 * 256 : 2 * 256;
+    const long rounds = (tiles * s + slots - 1) / slots;
+    const double t = (double)rounds * kpt + (s > 1 ? s * slab_cost : 0.0);
+    if (t < best * 0.999) {
+      best = t;
+      best_s = s;
+    }
+  }
+  return best_s;
 }
 
 // out[i] (+)= sum_z ws[z][i]  -- the split-K combine (float4 over MN, MN % 4 == 0)

@@ -10,6 +10,13 @@ skip tuning -- part of the job-create -> step 0 latency. Candidates must be
 side-effect free or write to scratch while tuning.
 
 ``K8S_AMD_AUTOTUNE=0`` disables tuning (always the first candidate = ours).
+
+Seed tables: ``ops/tuned/<arch>.json`` (e.g. ``gfx950.json``) hold choices measured on that
+GPU for the shipped benchmark configs and are consulted after the node cache. A fresh node
+then skips the timing runs -- and, more importantly, never builds the vendor (MIOpen)
+kernels of candidates that lost: on a cold MI355X those compiles are ~70 s of the
+job-create -> step 0 latency (profiles/r01_coldstart.md). ``K8S_AMD_AUTOTUNE_SEED=0``
+ignores the seed table.
 """
 from __future__ import annotations
 
@@ -30,7 +37,7 @@ def enabled() -> bool:
     return os.environ.get("K8S_AMD_AUTOTUNE", "1") != "0"
 
 
-CACHE_VERSION = "v1"  # bump when kernels / candidates change
+CACHE_VERSION = "v2"  # bump when kernels / candidates change
 
 
 def cache_path():
@@ -41,11 +48,34 @@ def cache_path():
     return None if p in ("", "none") else p
 
 
+SEED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
+
+
+def _arch() -> str:
+    try:
+        if torch.cuda.is_available():
+            return torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName.split(":")[0]
+    except (RuntimeError, AttributeError):
+        pass
+    return ""
+
+
+def seed_path(arch: str = None):
+    arch = _arch() if arch is None else arch
+    return os.path.join(SEED_DIR, arch + ".json") if arch else None
+
+
 def _load_cache():
     global _loaded
     if _loaded:
         return
     _loaded = True
+    sp = seed_path() if os.environ.get("K8S_AMD_AUTOTUNE_SEED", "1") != "0" else None
+    if sp and os.path.exists(sp):
+        try:
+            _cache.update(json.load(open(sp)))
+        except (ValueError, OSError):
+            pass
     p = cache_path()
     if p and os.path.exists(p):
         try:
@@ -83,22 +113,33 @@ def _time(fn, reps=3) -> float:
     return ts[len(ts) // 2]
 
 
+# A vendor candidate must beat ours (candidate 0) by this margin: near-ties flip between runs on timing noise,
+# and every vendor choice costs a kernel build (MIOpen) on a fresh node.
+MARGIN = float(os.environ.get("K8S_AMD_AUTOTUNE_MARGIN", "0.03"))
+
+
 def choose(key: str, candidates: Sequence[Tuple[str, Callable[[], object]]]) -> str:
     """Return the name of the fastest candidate for `key` (tuning on first use)."""
     _load_cache()
     name = _cache.get(key)
+    if name is not None and name not in [n for n, _ in candidates]:
+        name = None  # stale entry (candidate set changed)
     if name is None:
         if not enabled() or len(candidates) == 1 or not torch.cuda.is_available():
             name = candidates[0][0]
         else:
-            best, name = None, candidates[0][0]
+            times = {}
             for n, fn in candidates:
                 try:
-                    t = _time(fn)
+                    times[n] = _time(fn, reps=5)
                 except RuntimeError:
                     continue
-                if best is None or t < best:
-                    best, name = t, n
+            name = candidates[0][0]
+            if times:
+                best = min(times, key=times.get)
+                ours = times.get(name)
+                if ours is None or times[best] < ours * (1.0 - MARGIN):
+                    name = best
             with _lock:
                 _cache[key] = name
                 _save_cache()
