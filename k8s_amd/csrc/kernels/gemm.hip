@@ -224,6 +224,9 @@ struct Epi {
   const uint16_t* by;
   const float *bmean, *binvstd, *bgamma, *bbeta;
   int brelu_x;
+  // Sub-grid output (stride-s data gradient by output parity): GEMM row m = (n, i, j) over an rHo x rWo grid
+  // is stored at output row (n, i*rst + ra, j*rst + rb) of an rH x rW image. rst == 0: identity.
+  int rst, rHo, rWo, rH, rW, ra, rb;
 };
 constexpr int STAT_REPL = 32;
 
@@ -347,6 +350,13 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + wm * 64 + i * 16 + (lane & 15);
     if (m >= M) continue;
+    long orow = m;
+    if (E.rst) {
+      const int hw = E.rHo * E.rWo;
+      const int nimg = m / hw, rem = m - nimg * hw;
+      const int ii = rem / E.rWo, jj = rem - ii * E.rWo;
+      orow = ((long)nimg * E.rH + ii * E.rst + E.ra) * E.rW + jj * E.rst + E.rb;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int n = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
@@ -359,7 +369,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
           if (n + r < N) v[r] += E.bias[n + r];
       }
       if (E.pre) {
-        uint16_t* pp = E.pre + (long)m * E.ldc + n;
+        uint16_t* pp = E.pre + orow * E.ldc + n;
         if (full) {
           bf16x4_t o;
 #pragma unroll
@@ -386,7 +396,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
         }
       }
       if (E.out_f32) {
-        float* cp = reinterpret_cast<float*>(ec) + (long)m * E.ldc + n;
+        float* cp = reinterpret_cast<float*>(ec) + orow * E.ldc + n;
         if (emode == 2) {
           for (int r = 0; r < 4 && n + r < N; ++r) atomicAdd(cp + r, v[r]);
         } else if (full) {
@@ -402,7 +412,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
             if (n + r < N) cp[r] = (emode == 1 ? cp[r] : 0.f) + v[r];
         }
       } else {
-        uint16_t* cp = reinterpret_cast<uint16_t*>(ec) + (long)m * E.ldc + n;
+        uint16_t* cp = reinterpret_cast<uint16_t*>(ec) + orow * E.ldc + n;
         if (full) {
           bf16x4_t o;
           if (emode == 1) {
@@ -555,6 +565,7 @@ static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act,
   e.bx = e.by = nullptr;
   e.bmean = e.binvstd = e.bgamma = e.bbeta = nullptr;
   e.brelu_x = 0;
+  e.rst = e.rHo = e.rWo = e.rH = e.rW = e.ra = e.rb = 0;
   return e;
 }
 
@@ -564,15 +575,15 @@ static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act,
 // slots = resident blocks on 256 CUs (2 per CU double-buffered, 3 single-buffered). The previous rule
 // (double s until tiles * s >= 512) landed most ResNet-50 3x3 weight gradients on 576 blocks = 1.125
 // rounds; measured on MI355X (scripts/sweep_wgrad_splits.py) the model's choice is 1.3-1.5x faster there.
-// Up to 1024 splits: a single-tile product (64x64 1x1 weight gradient over 802816 rows) otherwise runs one
-// latency-bound block per CU.
+// At most 256 splits: measured with up to 1024, the single-tile 64x64 1x1 weight gradient got slower (134 ->
+// 189 us) -- the combine kernel's per-thread serial loop over the splits dominates.
 int gemm_choose_splits(int M, int N, int K) {
   const long tiles = (long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const int ktiles = (K + BK - 1) / BK;
   const double slab_cost = (double)M * N * 8.0 / 5.0e12 / 2.0e-6;  // in units of one K tile (~2 us / block)
   int best_s = 1;
   double best = 1e30;
-  for (int s = 1; s <= 1024 && s <= ktiles; ++s) {
+  for (int s = 1; s <= 256 && s <= ktiles; ++s) {
     const int kpt = (ktiles + s - 1) / s;       // K tiles per split
     if ((ktiles + kpt - 1) / kpt != s) continue;  // same kps as a smaller s
     const long slots = kpt * BK <= 2 * BK ? 3 * 256 : 2 * 256;
@@ -646,12 +657,22 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
 // decode, any other C % 8 == 0 the per-unit one.
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int K,
                      int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
-                     int mode, float* stats, hipStream_t st, const BnBwdEpi* bnb) {
+                     int mode, float* stats, hipStream_t st, const BnBwdEpi* bnb, const SubGrid* sg) {
   const int M = N * Ho * Wo, RSC = R * S * C;
   KMajor b{w, (long)RSC, K, RSC};
   Epi e = make_epi(y, K, y_f32, bias, act, nullptr, mode, 1.f);
   e.stats = stats;
   apply_bnbwd(e, bnb);
+  if (sg) {
+    if (bnb || stats) throw std::runtime_error("sub-grid output takes no statistics epilogue");
+    e.rst = sg->stride;
+    e.rHo = Ho;
+    e.rWo = Wo;
+    e.rH = sg->H;
+    e.rW = sg->W;
+    e.ra = sg->a;
+    e.rb = sg->b;
+  }
   if (C % 64 == 0) {
     ConvA a{x, N, H, W, C, Ho, Wo, S, stride, pad, dil, M,
             make_fastdiv(C), make_fastdiv(S), make_fastdiv(Ho * Wo), make_fastdiv(Wo)};

@@ -66,10 +66,15 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
                  long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
                  float alpha, int splits, float* ws, hipStream_t st, const BnBwdEpi* bnb = nullptr);
 long gemm_splitk_workspace(int M, int N, int splits);  // fp32 elements of the split-K slab workspace
+// Output written to the (a, b) parity sub-grid of an H x W image: GEMM row (n, i, j) -> (n, i*stride+a,
+// j*stride+b). Used for stride-s data gradients decomposed by output parity (ops/conv.py _dgrad_strided_hip).
+struct SubGrid {
+  int H, W, stride, a, b;
+};
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int K,
                      int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
                      int mode, float* stats, hipStream_t st,
-                     const BnBwdEpi* bnb = nullptr);
+                     const BnBwdEpi* bnb = nullptr, const SubGrid* sg = nullptr);
 void launch_conv_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int C, int K, int R,
                        int S, int stride, int pad, int dil, int Ho, int Wo, int splits, bool accumulate, float* ws,
                        hipStream_t st);

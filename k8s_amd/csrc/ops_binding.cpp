@@ -322,6 +322,27 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, bo
   return y;
 }
 
+// One output-parity piece of a stride-s data gradient: out[n, i*s+a, j*s+b, :] = conv(dy, wsub, stride 1, pad)
+// over an Hs x Ws grid (i < Hs, j < Ws). wsub [C, Tr, Ts, K] holds the taps of that parity
+// (ops/conv.py _dgrad_strided_hip builds it); out is the full bf16 dx [N, H, W, C].
+void conv_fwd_subgrid(Tensor x, Tensor w, int64_t pad, int64_t Hs, int64_t Ws, Tensor out, int64_t stride, int64_t a,
+                      int64_t b) {
+  check_cuda(x, "x"); check_cuda(w, "w"); check_cuda(out, "out");
+  check_dtype(x, at::kBFloat16, "x"); check_dtype(w, at::kBFloat16, "w"); check_dtype(out, at::kBFloat16, "out");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && out.dim() == 4 && out.is_contiguous());
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int K = w.size(0), R = w.size(1), S = w.size(2);
+  TORCH_CHECK(w.size(3) == C && C % 64 == 0 && K % 8 == 0, "sub-grid conv needs C % 64 == 0, K % 8 == 0");
+  TORCH_CHECK(out.size(0) == N && out.size(3) == K, "out shape");
+  const int OH = out.size(1), OW = out.size(2);
+  TORCH_CHECK(stride >= 1 && a >= 0 && a < stride && b >= 0 && b < stride, "parity out of range");
+  TORCH_CHECK(Hs >= 1 && Ws >= 1 && (Hs - 1) * stride + a < OH && (Ws - 1) * stride + b < OW,
+              "sub-grid exceeds the output image");
+  k8s_amd::SubGrid sg{OH, OW, (int)stride, (int)a, (int)b};
+  k8s_amd::launch_conv_fwd(cbf(x), cbf(w), out.data_ptr(), false, N, H, W, C, K, R, S, 1, (int)pad, 1, (int)Hs,
+                           (int)Ws, nullptr, 0, 0, nullptr, cur_stream(), nullptr, &sg);
+}
+
 // dw[K,R,S,C] fp32 (+)= dy^T . im2col(x)
 void conv_wgrad(Tensor x, Tensor dy, Tensor dw, int64_t stride, int64_t pad, int64_t dil, int64_t splits,
                 bool accumulate) {
@@ -533,6 +554,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out_f32"), py::arg("bias"), py::arg("act"), py::arg("stats"), py::arg("bnb") = py::none(),
         py::arg("bnb_relu_x") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_fwd_subgrid", &conv_fwd_subgrid);
   m.def("conv_dgrad_wtrans", &conv_dgrad_wtrans);
   m.def("flash_fwd", &flash_fwd);
   m.def("maxpool_fwd", &maxpool_fwd);

@@ -9,8 +9,11 @@ Activations NHWC bf16, weights KRSC bf16. Per product:
     dgrad  1x1, stride 1: dx = dy . w       plain GEMM, w read N-major (no transpose)
            RxS, stride 1: dx = conv(dy, w') w' = spatially flipped, in/out-swapped w
                                             (tiny per-step transform), pad' = R-1-pad
+           stride s     : split by output parity (a, b): each of the s*s sub-grids of dx is a stride-1
+                          conv of dy with the taps r = a + pad - s*d (d = row offset into dy), written
+                          through the GEMM epilogue's sub-grid row map; parities with no taps are zero
 
-Shapes outside those rules (stride-2 dgrad) and CPU
+Shapes outside those rules and CPU
 tensors run through ATen's convolution on a channels-last view (MIOpen on
 ROCm). Where both paths can run a shape, ``ops.autotune`` times them once on
 the real tensors (the vendor forward is charged for the extra BatchNorm
@@ -119,6 +122,50 @@ def _dgrad_hip(C_, gy, w, padding, addend=None, bnb=None):
     return dx if addend is None else dx.add_(addend)
 
 
+def _parity_taps(R, a, pad, stride):
+    """[(d, r)] sorted by d: taps r of an R-tap filter that reach output rows h = i*stride + a, read from dy
+    row i + d. None if the offsets are not contiguous (cannot be one stride-1 correlation)."""
+    taps = sorted(((a + pad - r) // stride, r) for r in range(R) if (a + pad - r) % stride == 0)
+    if taps and [d for d, _ in taps] != list(range(taps[0][0], taps[0][0] + len(taps))):
+        return None
+    return taps
+
+
+def strided_dgrad_ok(gy, w, stride, padding):
+    K, R, S, C = w.shape
+    if stride < 2 or K % 64 or C % 8:
+        return False
+    for a in range(stride):
+        for b in range(stride):
+            tr, ts = _parity_taps(R, a, padding, stride), _parity_taps(S, b, padding, stride)
+            if tr is None or ts is None:
+                return False
+            if tr and ts and tr[0][0] != ts[0][0]:
+                return False  # one pad for both dims
+    return True
+
+
+def _dgrad_strided_hip(C_, gy, w, stride, padding, H, W):
+    """dx [N, H, W, C] of a stride-s conv on our implicit-GEMM kernel, one launch per output parity."""
+    K, R, S, C = w.shape
+    N = gy.shape[0]
+    dx = torch.empty(N, H, W, C, device=gy.device, dtype=gy.dtype)
+    for a in range(stride):
+        tr = _parity_taps(R, a, padding, stride)
+        for b in range(stride):
+            ts = _parity_taps(S, b, padding, stride)
+            if not tr or not ts:
+                dx[:, a::stride, b::stride, :] = 0
+                continue
+            # gather the taps with views + stack (no host->device index tensor, so no stream sync)
+            wr = torch.stack([w[:, r] for _, r in tr], dim=1)                 # [K, Tr, S, C]
+            wsub = torch.stack([wr[:, :, s_] for _, s_ in ts], dim=2)         # [K, Tr, Ts, C]
+            wsub = wsub.permute(3, 1, 2, 0).contiguous()                      # [C, Tr, Ts, K]
+            Hs, Ws = (H - a + stride - 1) // stride, (W - b + stride - 1) // stride
+            C_.conv_fwd_subgrid(gy, wsub, -tr[0][0], Hs, Ws, dx, stride, a, b)
+    return dx
+
+
 def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, bn_link=None):
     """Returns dx (+ ``addend``, e.g. the residual branch's gradient of the same tensor, fused into the
     dgrad epilogue where our kernel runs) or None; deposits dw into ``p``'s flat gradient slot."""
@@ -154,6 +201,14 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, bn_link=No
                 use_hip = autotune.choose(_key("conv_dgrad_acc", x, w, stride, padding), [
                     ("hip", lambda: _dgrad_hip(C_, gy, w, padding, torch.empty_like(addend))),
                     ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, True, False)[0].add_(addend))]) == "hip"
+        elif hip and strided_dgrad_ok(gy, w, stride, padding):
+            H, W_ = x.shape[1], x.shape[2]
+            if autotune.choose(_key("conv_dgrad_s", x, w, stride, padding), [
+                    ("hip", lambda: _dgrad_strided_hip(C_, gy, w, stride, padding, H, W_)),
+                    ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, True, False))]) == "hip":
+                STATS["hip_dgrad"] += 1
+                dx = _dgrad_strided_hip(C_, gy, w, stride, padding, H, W_)
+                return _finish_dw(dx if addend is None else dx.add_(addend), dw_done, p, gy, x, w, stride, padding)
         if use_hip:
             STATS["hip_dgrad"] += 1
             bnb = None
@@ -165,6 +220,10 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, bn_link=No
             dx, _ = _aten_bwd(gy, x, w, stride, padding, True, False)
             if addend is not None:
                 dx = dx + addend
+    return _finish_dw(dx, dw_done, p, gy, x, w, stride, padding)
+
+
+def _finish_dw(dx, dw_done, p, gy, x, w, stride, padding):
     if not dw_done and p is not None:
         STATS["aten_wgrad"] += 1
         _, dw = _aten_bwd(gy, x, w, stride, padding, False, True)

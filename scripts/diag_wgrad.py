@@ -47,6 +47,10 @@ for (N, H, C, K, R, s, p) in DGRAD_S2:
     Ho = (H + 2 * p - R) // s + 1
     gy = torch.randn(N, Ho, Ho, K, device=dev, dtype=torch.bfloat16)
     t_aten = autotune._time(lambda: conv._aten_bwd(gy, x, w, s, p, True, False), reps=5)
+    t_hip = autotune._time(lambda: conv._dgrad_strided_hip(C_, gy, w, s, p, H, H), reps=5)
+    ref = conv._aten_bwd(gy, x, w, s, p, True, False)[0].float()
+    err = ((conv._dgrad_strided_hip(C_, gy, w, s, p, H, H).float() - ref).norm() / ref.norm()).item()
     fl = 2.0 * N * Ho * Ho * K * C * R * R
     print(json.dumps({"op": "dgrad_s2", "shape": [N, H, C, K, R, s, p], "aten_us": round(t_aten * 1e3, 1),
-                      "aten_tflops": round(fl / t_aten / 1e9)}), flush=True)
+                      "hip_us": round(t_hip * 1e3, 1), "aten_tflops": round(fl / t_aten / 1e9),
+                      "hip_tflops": round(fl / t_hip / 1e9), "relerr": round(err, 5)}), flush=True)

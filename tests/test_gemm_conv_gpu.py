@@ -244,3 +244,23 @@ def test_conv3x3_dgrad_bn_backward_statistics_epilogue(cuda):
     ge = (dx.float() * m).reshape(-1, C)
     assert _rel(reps.sum(0)[0], ge.sum(0)) < 1e-3
     assert _rel(reps.sum(0)[1], (ge * x.float().reshape(-1, C)).sum(0)) < 1e-3
+
+
+# stride-2 data gradients (ResNet-50 v1.5 strided 3x3 and 1x1 downsample, the 7x7 stem; odd sizes) on the
+# parity-decomposed implicit GEMM with the sub-grid epilogue
+@pytest.mark.parametrize("N,H,C,K,R,st,pad", [(4, 56, 128, 128, 3, 2, 1), (4, 28, 256, 512, 1, 2, 0),
+                                              (2, 15, 64, 128, 3, 2, 1), (2, 32, 8, 64, 7, 2, 3),
+                                              (3, 14, 512, 1024, 1, 2, 0)])
+def test_conv_dgrad_strided(cuda, N, H, C, K, R, st, pad):
+    from k8s_amd.ops import conv as kc
+
+    torch.manual_seed(7)
+    Ho = (H + 2 * pad - R) // st + 1
+    x = torch.randn(N, H, H, C, device=cuda).bfloat16()
+    w = (torch.randn(K, R, R, C, device=cuda) * 0.05).bfloat16()
+    dy = torch.randn(N, Ho, Ho, K, device=cuda).bfloat16()
+    assert kc.strided_dgrad_ok(dy, w, st, pad)
+    dx = kc._dgrad_strided_hip(_C(), dy, w, st, pad, H, H)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    F.conv2d(xr, w.float().permute(0, 3, 1, 2), None, st, pad).backward(dy.float().permute(0, 3, 1, 2))
+    assert _rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2

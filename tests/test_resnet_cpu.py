@@ -68,3 +68,37 @@ def test_resnet_tiny_gradients_match_plain_pytorch():
         g, r = p.grad.float(), ref[p.name]
         err = (g - r).abs().max().item()
         assert err <= 1e-3 * max(1.0, r.abs().max().item()), (p.name, err)
+
+
+def test_strided_dgrad_parity_taps():
+    """Output-parity decomposition of a stride-s data gradient (ops/conv.py): the taps of every parity,
+    emulated with stride-1 correlations on CPU, reproduce ATen's convolution_backward exactly."""
+    import torch.nn.functional as F
+
+    from k8s_amd.ops import conv
+
+    torch.manual_seed(0)
+    for (N, H, C, K, R, s, p) in [(2, 8, 16, 64, 3, 2, 1), (2, 9, 16, 64, 3, 2, 1), (2, 8, 16, 64, 1, 2, 0),
+                                  (1, 7, 8, 64, 7, 2, 3)]:
+        x, w = torch.randn(N, H, H, C), torch.randn(K, R, R, C)
+        Ho = (H + 2 * p - R) // s + 1
+        gy = torch.randn(N, Ho, Ho, K)
+        assert conv.strided_dgrad_ok(gy, w, s, p)
+        dx = torch.empty(N, H, H, C)
+        for a in range(s):
+            tr = conv._parity_taps(R, a, p, s)
+            for b in range(s):
+                ts = conv._parity_taps(R, b, p, s)
+                if not tr or not ts:
+                    dx[:, a::s, b::s] = 0
+                    continue
+                wr = torch.stack([w[:, r] for _, r in tr], dim=1)
+                wsub = torch.stack([wr[:, :, q] for _, q in ts], dim=2)  # [K, Tr, Ts, C]
+                Hs, Ws = (H - a + s - 1) // s, (H - b + s - 1) // s
+                lo = -tr[0][0]
+                xin = F.pad(gy.permute(0, 3, 1, 2), (lo, Ws - (Ho + lo - len(ts) + 1), lo, Hs - (Ho + lo - len(tr) + 1)))
+                dx[:, a::s, b::s] = F.conv2d(xin, wsub.permute(3, 0, 1, 2)).permute(0, 2, 3, 1)
+        ref = torch.ops.aten.convolution_backward(gy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2),
+                                                  w.permute(0, 3, 1, 2), None, [s, s], [p, p], [1, 1], False,
+                                                  [0, 0], 1, [True, False, False])[0].permute(0, 2, 3, 1)
+        assert (dx - ref).abs().max() < 1e-3
