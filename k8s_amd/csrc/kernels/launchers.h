@@ -9,11 +9,11 @@ namespace k8s_amd {
 
 // optim.hip
 void launch_sgd(float* p, float* mom, const void* g, bool g_bf16, uint16_t* pbf, long n, const uint8_t* decay_mask, float lr,
-                float mu, float wd, float scale, const float* scale_ptr, bool nesterov, bool first_step,
-                hipStream_t st);
+                float mu, float wd, float scale, const float* scale_ptr, const float* hyper, bool nesterov,
+                bool first_step, hipStream_t st);
 void launch_adam(float* p, float* m1, float* m2, const void* g, bool g_bf16, uint16_t* pbf, long n, const uint8_t* decay_mask,
-                 float lr, float b1, float b2, float eps, float wd, float scale, const float* scale_ptr, float bc1,
-                 float bc2, bool decoupled, hipStream_t st);
+                 float lr, float b1, float b2, float eps, float wd, float scale, const float* scale_ptr,
+                 const float* hyper, float bc1, float bc2, bool decoupled, hipStream_t st);
 void launch_sumsq(const void* g, bool g_bf16, long n, float* out, hipStream_t st);
 void launch_clip_factor(const float* stats, float max_norm, float* factor, hipStream_t st);
 

@@ -14,7 +14,10 @@
 //
 // An optional device-side scale pointer (gradient clip factor / loss-scale
 // inverse) keeps the step free of host synchronisation so the whole step can
-// be captured in a hipGraph.
+// be captured in a hipGraph. `hyper` (device fp32 [lr, step], optional) does
+// the same for the values that change every step: a captured graph replays
+// with the learning-rate schedule and Adam's bias correction read on device
+// (utils/graph.py).
 #include "common.h"
 #include "launchers.h"
 
@@ -46,8 +49,9 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* 
                                                   const GT* __restrict__ g, uint16_t* __restrict__ pbf,
                                                   long n4, const uint8_t* __restrict__ decay_mask, float lr, float mu, float wd,
                                                   float scale, const float* __restrict__ scale_ptr,
-                                                  int nesterov, int first_step) {
+                                                  const float* __restrict__ hyper, int nesterov, int first_step) {
   const float s = scale * (scale_ptr ? *scale_ptr : 1.f);
+  if (hyper) lr = hyper[0];
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n4; q += (long)gridDim.x * blockDim.x) {
     const long i = q * 4;
     float gv[4];
@@ -76,8 +80,14 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
                                                    uint16_t* __restrict__ pbf, long n4, const uint8_t* __restrict__ decay_mask,
                                                    float lr, float b1, float b2, float eps, float wd,
                                                    float scale, const float* __restrict__ scale_ptr,
-                                                   float bc1, float bc2, int decoupled) {
+                                                   const float* __restrict__ hyper, float bc1, float bc2,
+                                                   int decoupled) {
   const float s = scale * (scale_ptr ? *scale_ptr : 1.f);
+  if (hyper) {
+    lr = hyper[0];
+    bc1 = 1.f - powf(b1, hyper[1]);
+    bc2 = 1.f - powf(b2, hyper[1]);
+  }
   const float step1 = lr / bc1;
   const float rbc2 = 1.f / sqrtf(bc2);
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n4; q += (long)gridDim.x * blockDim.x) {
@@ -145,29 +155,29 @@ __global__ void clip_factor_kernel(const float* __restrict__ stats, float max_no
 
 // ---------------------------------------------------------------- launchers
 void launch_sgd(float* p, float* mom, const void* g, bool g_bf16, uint16_t* pbf, long n, const uint8_t* decay_mask,
-                float lr, float mu, float wd, float scale, const float* scale_ptr, bool nesterov,
+                float lr, float mu, float wd, float scale, const float* scale_ptr, const float* hyper, bool nesterov,
                 bool first_step, hipStream_t st) {
   const long n4 = n / 4;
   const int grid = stream_grid(n4, 256);
   if (g_bf16)
     hipLaunchKernelGGL(sgd_kernel<uint16_t>, dim3(grid), dim3(256), 0, st, p, mom, (const uint16_t*)g, pbf, n4,
-                       decay_mask, lr, mu, wd, scale, scale_ptr, (int)nesterov, (int)first_step);
+                       decay_mask, lr, mu, wd, scale, scale_ptr, hyper, (int)nesterov, (int)first_step);
   else
     hipLaunchKernelGGL(sgd_kernel<float>, dim3(grid), dim3(256), 0, st, p, mom, (const float*)g, pbf, n4, decay_mask,
-                       lr, mu, wd, scale, scale_ptr, (int)nesterov, (int)first_step);
+                       lr, mu, wd, scale, scale_ptr, hyper, (int)nesterov, (int)first_step);
 }
 
 void launch_adam(float* p, float* m1, float* m2, const void* g, bool g_bf16, uint16_t* pbf, long n, const uint8_t* decay_mask,
-                 float lr, float b1, float b2, float eps, float wd, float scale, const float* scale_ptr, float bc1,
-                 float bc2, bool decoupled, hipStream_t st) {
+                 float lr, float b1, float b2, float eps, float wd, float scale, const float* scale_ptr,
+                 const float* hyper, float bc1, float bc2, bool decoupled, hipStream_t st) {
   const long n4 = n / 4;
   const int grid = stream_grid(n4, 256);
   if (g_bf16)
     hipLaunchKernelGGL(adam_kernel<uint16_t>, dim3(grid), dim3(256), 0, st, p, m1, m2, (const uint16_t*)g, pbf, n4,
-                       decay_mask, lr, b1, b2, eps, wd, scale, scale_ptr, bc1, bc2, (int)decoupled);
+                       decay_mask, lr, b1, b2, eps, wd, scale, scale_ptr, hyper, bc1, bc2, (int)decoupled);
   else
     hipLaunchKernelGGL(adam_kernel<float>, dim3(grid), dim3(256), 0, st, p, m1, m2, (const float*)g, pbf, n4,
-                       decay_mask, lr, b1, b2, eps, wd, scale, scale_ptr, bc1, bc2, (int)decoupled);
+                       decay_mask, lr, b1, b2, eps, wd, scale, scale_ptr, hyper, bc1, bc2, (int)decoupled);
 }
 
 void launch_sumsq(const void* g, bool g_bf16, long n, float* out, hipStream_t st) {

@@ -39,8 +39,18 @@ const uint8_t* mask_ptr(const c10::optional<Tensor>& m, long n) {
   return m->data_ptr<uint8_t>();
 }
 
+// device fp32 [lr, step] read by the optimizer kernels instead of the host scalars (hipGraph replay)
+static const float* hyper_ptr(const c10::optional<Tensor>& h) {
+  if (!h) return nullptr;
+  check_cuda(*h, "hyper");
+  check_dtype(*h, at::kFloat, "hyper");
+  TORCH_CHECK(h->numel() >= 2 && h->is_contiguous(), "hyper must be a contiguous fp32 [lr, step] tensor");
+  return h->data_ptr<float>();
+}
+
 void fused_sgd(Tensor p, Tensor mom, Tensor g, c10::optional<Tensor> pbf, c10::optional<Tensor> decay_mask, double lr, double mu,
-               double wd, double scale, c10::optional<Tensor> scale_t, bool nesterov, bool first_step) {
+               double wd, double scale, c10::optional<Tensor> scale_t, bool nesterov, bool first_step,
+               c10::optional<Tensor> hyper) {
   check_cuda(p, "param"); check_cuda(mom, "momentum"); check_cuda(g, "grad");
   check_dtype(p, at::kFloat, "param"); check_dtype(mom, at::kFloat, "momentum");
   const long n = p.numel();
@@ -50,13 +60,13 @@ void fused_sgd(Tensor p, Tensor mom, Tensor g, c10::optional<Tensor> pbf, c10::o
   if (pbf) { check_cuda(*pbf, "param_bf16"); check_dtype(*pbf, at::kBFloat16, "param_bf16"); TORCH_CHECK(pbf->numel() == n); }
   const uint8_t* dm = mask_ptr(decay_mask, n);
   k8s_amd::launch_sgd(f32(p), f32(mom), g.data_ptr(), g.scalar_type() == at::kBFloat16, pbf ? bf(*pbf) : nullptr, n,
-                      dm, (float)lr, (float)mu, (float)wd, (float)scale, optf(scale_t), nesterov, first_step,
-                      cur_stream());
+                      dm, (float)lr, (float)mu, (float)wd, (float)scale, optf(scale_t), hyper_ptr(hyper), nesterov,
+                      first_step, cur_stream());
 }
 
 void fused_adam(Tensor p, Tensor m1, Tensor m2, Tensor g, c10::optional<Tensor> pbf, c10::optional<Tensor> decay_mask, double lr,
                 double b1, double b2, double eps, double wd, double scale, c10::optional<Tensor> scale_t, int64_t step,
-                bool decoupled) {
+                bool decoupled, c10::optional<Tensor> hyper) {
   check_cuda(p, "param"); check_cuda(m1, "exp_avg"); check_cuda(m2, "exp_avg_sq"); check_cuda(g, "grad");
   const long n = p.numel();
   TORCH_CHECK(n % 4 == 0, "flat buffer length must be a multiple of 4");
@@ -67,7 +77,7 @@ void fused_adam(Tensor p, Tensor m1, Tensor m2, Tensor g, c10::optional<Tensor> 
   const float bc2 = 1.f - std::pow((float)b2, (float)step);
   k8s_amd::launch_adam(f32(p), f32(m1), f32(m2), g.data_ptr(), g.scalar_type() == at::kBFloat16,
                        pbf ? bf(*pbf) : nullptr, n, mask_ptr(decay_mask, n), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd,
-                       (float)scale, optf(scale_t), bc1, bc2, decoupled, cur_stream());
+                       (float)scale, optf(scale_t), hyper_ptr(hyper), bc1, bc2, decoupled, cur_stream());
 }
 
 Tensor grad_sumsq(Tensor g) {
@@ -528,8 +538,12 @@ Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, int64
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "k8s_amd gfx950 (MI355X) HIP kernels";
-  m.def("fused_sgd", &fused_sgd);
-  m.def("fused_adam", &fused_adam);
+  m.def("fused_sgd", &fused_sgd, py::arg("p"), py::arg("mom"), py::arg("g"), py::arg("pbf"), py::arg("decay_mask"),
+        py::arg("lr"), py::arg("mu"), py::arg("wd"), py::arg("scale"), py::arg("scale_t"), py::arg("nesterov"),
+        py::arg("first_step"), py::arg("hyper") = py::none());
+  m.def("fused_adam", &fused_adam, py::arg("p"), py::arg("m1"), py::arg("m2"), py::arg("g"), py::arg("pbf"),
+        py::arg("decay_mask"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"),
+        py::arg("scale"), py::arg("scale_t"), py::arg("step"), py::arg("decoupled"), py::arg("hyper") = py::none());
   m.def("grad_sumsq", &grad_sumsq);
   m.def("clip_factor", &clip_factor);
   m.def("bn_fwd", &bn_fwd);

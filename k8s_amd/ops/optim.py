@@ -24,6 +24,22 @@ class _FlatOptimizer:
         self.weight_decay = weight_decay
         self.max_grad_norm = max_grad_norm
         self.step_count = 0
+        self.hyper: Optional[torch.Tensor] = None  # device [lr, step] (hipGraph replay), see use_device_hyper
+
+    def use_device_hyper(self):
+        """Kernels read lr (and Adam's step) from a device tensor instead of launch arguments, so a step
+        captured in a hipGraph replays with the current schedule (``utils/graph.StepGraph``)."""
+        if self.hyper is None:
+            self.hyper = torch.zeros(2, dtype=torch.float32, device=self.store.master.device)
+        return self.hyper
+
+    def set_hyper(self, lr: float, step: int):
+        self.hyper[0].fill_(float(lr))
+        self.hyper[1].fill_(float(step))
+
+    def prepare_replay(self, lr: float):
+        """Host bookkeeping + device hyperparameters for one replay of a captured step (mirrors ``step``)."""
+        raise NotImplementedError
 
     def _ranges(self, ranges: Optional[Sequence[Tuple[int, int]]]) -> List[Tuple[int, int]]:
         return [(0, self.store.total)] if ranges is None else list(ranges)
@@ -83,10 +99,16 @@ class FusedSGD(_FlatOptimizer):
             m = self.mom[lo:hi]
             if p.is_cuda:
                 _load_ext().fused_sgd(p, m, g, h, mask, lr, self.momentum, self.weight_decay, grad_scale, clip,
-                                      self.nesterov, first)
+                                      self.nesterov, first, self.hyper)
             else:
                 ref.sgd(p, m, g, h, mask, lr, self.momentum, self.weight_decay, grad_scale, clip, self.nesterov,
                         first)
+        self.step_count += 1
+
+    def prepare_replay(self, lr: float):
+        if self.step_count == 0:
+            raise RuntimeError("capture after at least one eager step (momentum initialisation)")
+        self.set_hyper(lr, self.step_count)
         self.step_count += 1
 
     def state_tensors(self):
@@ -120,10 +142,14 @@ class FusedAdam(_FlatOptimizer):
             a, b = self.m1[lo:hi], self.m2[lo:hi]
             if p.is_cuda:
                 _load_ext().fused_adam(p, a, b, g, h, mask, lr, self.b1, self.b2, self.eps, self.weight_decay,
-                                       grad_scale, clip, self.step_count, self.adamw)
+                                       grad_scale, clip, self.step_count, self.adamw, self.hyper)
             else:
                 ref.adam(p, a, b, g, h, mask, lr, self.b1, self.b2, self.eps, self.weight_decay, grad_scale, clip,
                          self.step_count, self.adamw)
+
+    def prepare_replay(self, lr: float):
+        self.step_count += 1
+        self.set_hyper(lr, self.step_count)
 
     def state_tensors(self):
         return [self.m1, self.m2]

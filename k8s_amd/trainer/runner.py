@@ -72,6 +72,8 @@ def parse(argv=None):
     ap.add_argument("--log-every", type=int, default=10)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--fresh-batches", action="store_true", help="draw a new synthetic batch every step")
+    ap.add_argument("--graph", action="store_true", default=os.environ.get("K8S_AMD_GRAPH", "0") == "1",
+                    help="capture the whole step in a hipGraph after warmup (single rank, all-reduce strategy)")
     ap.add_argument("--fail-at-step", type=int, default=-1, help="(testing) raise a retryable failure once")
     ap.add_argument("--hang-timeout", type=float, default=float(os.environ.get("K8S_AMD_HANG_TIMEOUT", "0")),
                     help="exit 143 (retryable) when no step completes for this many seconds (0: off)")
@@ -258,6 +260,24 @@ def train(a) -> int:
     tracer = Tracer(enabled=a.trace not in ("", "0"), sync=(a.trace == "sync"), sync_fn=sync)
     # the first step includes kernel autotuning / vendor-library tuning: the watchdog starts after it
     watchdog = Watchdog(a.hang_timeout) if a.hang_timeout > 0 else None
+    graph = None
+    from k8s_amd.utils import debug as kdebug
+
+    debug_on = any(kdebug.enabled_flags())
+    if a.graph and use_cuda and world == 1 and a.strategy == "allreduce" and not tracer.enabled and not debug_on:
+        from k8s_amd.utils.graph import StepGraph
+
+        def body(inputs, lr_):
+            begin()
+            loss_ = w.loss(inputs)
+            loss_.backward()
+            finish(lr_)
+            return loss_
+
+        graph = StepGraph(body, opt, warmup=2)
+    elif a.graph:
+        metrics.event(event="warning", message="--graph needs one GPU rank, --strategy allreduce, no --trace "
+                      "and no kernel debug mode")
     t_last, n_last = time.time(), 0
     loss_v = float("nan")
     for step in range(start_step, a.steps):
@@ -270,16 +290,19 @@ def train(a) -> int:
         if step == a.hang_at_step:
             time.sleep(1e9)  # (testing) a stalled collective
         cur_lr = lr * min(1.0, (step + 1) / a.warmup_steps) if a.warmup_steps else lr
-        with tracer.phase("step"):
-            begin()
-            with tracer.phase("data"):
-                inputs = w.batch(step)
-            with tracer.phase("forward"):
-                loss = w.loss(inputs)
-            with tracer.phase("backward"):
-                loss.backward()
-            with tracer.phase("reduce+update"):
-                finish(cur_lr)
+        if graph is not None:
+            loss = graph(w.batch(step), cur_lr)
+        else:
+            with tracer.phase("step"):
+                begin()
+                with tracer.phase("data"):
+                    inputs = w.batch(step)
+                with tracer.phase("forward"):
+                    loss = w.loss(inputs)
+                with tracer.phase("backward"):
+                    loss.backward()
+                with tracer.phase("reduce+update"):
+                    finish(cur_lr)
         n_last += 1
         if watchdog is not None:
             if step == start_step:
