@@ -105,6 +105,38 @@ bool LeaderElector::try_acquire_or_renew() {
   return leader_ = true;
 }
 
+// resourcelock/endpointslock.go RecordEvent: a Normal "LeaderElection" Event "<identity> <what>" on the
+// Endpoints lock (best effort: a failed POST does not affect the election).
+void LeaderElector::record_event(const std::string& what) {
+  static std::atomic<unsigned> seq{0};
+  const std::string now = now_rfc3339();
+  Json ev = Json::object();
+  ev["apiVersion"] = "v1";
+  ev["kind"] = "Event";
+  Json md = Json::object();
+  md["name"] = cfg_.name + "." + cfg_.identity + "." + std::to_string(std::time(nullptr)) + "." +
+               std::to_string(seq++);
+  md["namespace"] = cfg_.ns;
+  ev["metadata"] = md;
+  Json io = Json::object();
+  io["kind"] = "Endpoints";
+  io["namespace"] = cfg_.ns;
+  io["name"] = cfg_.name;
+  io["apiVersion"] = "v1";
+  ev["involvedObject"] = io;
+  ev["reason"] = "LeaderElection";
+  ev["message"] = cfg_.identity + " " + what;
+  ev["type"] = "Normal";
+  ev["firstTimestamp"] = now;
+  ev["lastTimestamp"] = now;
+  ev["count"] = 1;
+  Json src = Json::object();
+  src["component"] = "tf-operator";
+  ev["source"] = src;
+  ApiResult r = api_.post(core_path(cfg_.ns, "events"), ev);
+  if (!r.ok()) log_info("could not record leader-election event: %d", r.code);
+}
+
 void LeaderElector::run(const std::function<void()>& on_started, const std::function<void()>& on_stopped,
                         const std::atomic<bool>& stop) {
   std::mt19937 rng{std::random_device{}()};
@@ -113,6 +145,7 @@ void LeaderElector::run(const std::function<void()>& on_started, const std::func
     std::this_thread::sleep_for(std::chrono::milliseconds((long)(cfg_.retry.count() * jitter(rng))));
   if (stop) return;
   log_info("became leader: %s", cfg_.identity.c_str());
+  record_event("became leader");
   std::thread worker(on_started);
   worker.detach();
   auto last_ok = std::chrono::steady_clock::now();
@@ -126,6 +159,7 @@ void LeaderElector::run(const std::function<void()>& on_started, const std::func
     }
   }
   leader_ = false;
+  record_event("stopped leading");
   on_stopped();
 }
 

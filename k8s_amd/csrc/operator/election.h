@@ -44,6 +44,7 @@ class LeaderElector {
   void run(const std::function<void()>& on_started, const std::function<void()>& on_stopped,
            const std::atomic<bool>& stop);
   bool is_leader() const { return leader_; }
+  void record_event(const std::string& what);
 
  private:
   KubeApi& api_;
