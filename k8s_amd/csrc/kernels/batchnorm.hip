@@ -23,12 +23,22 @@ struct BnGeom {
   int grid_y;         // channel slices
 };
 
-static inline BnGeom bn_geom(int C) {
+// Reduction geometry. Every row-block writes a [C][2] fp32 partial that the final kernel reads back, so the
+// number of row-blocks is capped at M / 64 (partials <= ~6% of one pass over the data; the old fixed ~1024
+// row-blocks made the partials 16% of the traffic at 7x7x2048). Parallelism lost that way is recovered by
+// splitting the channels over more blocks (fewer threads per row, more rows per block iteration).
+static inline BnGeom bn_geom(int C, long M) {
   BnGeom g;
   g.cgroups = C / 8;
   g.tpr = g.cgroups < BN_THREADS ? g.cgroups : BN_THREADS;
+  long nbx = M / 64;
+  nbx = nbx < 1 ? 1 : (nbx > 1024 ? 1024 : nbx);
+  for (;;) {
+    g.grid_y = (g.cgroups + g.tpr - 1) / g.tpr;
+    if (nbx * g.grid_y >= 768 || g.tpr <= 8 || (g.tpr & 1)) break;
+    g.tpr /= 2;
+  }
   g.rows_per_iter = BN_THREADS / g.tpr;
-  g.grid_y = (g.cgroups + g.tpr - 1) / g.tpr;
   return g;
 }
 
@@ -426,8 +436,11 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t
 
 // ---------------------------------------------------------------- launchers
 static long bn_rows_per_block(long M, const BnGeom& g) {
-  // ~1024 blocks in total (4 per CU: enough loads in flight to cover HBM latency); >= 4 row trips per block
+  // ~1024 blocks in total (4 per CU: enough loads in flight to cover HBM latency), at most M / 64 row-blocks,
+  // >= 4 row trips per block
   long blocks_x = 1024 / g.grid_y;
+  const long cap = M / 64;
+  if (blocks_x > cap) blocks_x = cap;
   if (blocks_x < 1) blocks_x = 1;
   long rpb = (M + blocks_x - 1) / blocks_x;
   long minr = (long)g.rows_per_iter * 4;
@@ -450,7 +463,7 @@ static int bn_elem_grid(long nvec, int cgroups) {
 }
 
 int bn_workspace_floats(long M, int C) {
-  BnGeom g = bn_geom(C);
+  BnGeom g = bn_geom(C, M);
   long rpb = bn_rows_per_block(M, g);
   long nb = (M + rpb - 1) / rpb;
   return (int)(nb * C * 2);
@@ -460,7 +473,7 @@ void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, c
                    float* save_mean, float* save_invstd, float* run_mean, float* run_var, float* work, long M, int C,
                    float eps, float momentum, bool training, bool relu, hipStream_t st) {
   if (training) {
-    BnGeom g = bn_geom(C);
+    BnGeom g = bn_geom(C, M);
     long rpb = bn_rows_per_block(M, g);
     int nb = (int)((M + rpb - 1) / rpb);
     hipLaunchKernelGGL(bn_stats_kernel, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, x, M, C, g.tpr,
@@ -519,7 +532,7 @@ void launch_bn_bwd_from_sums(const uint16_t* dy, const uint16_t* x, const uint16
 void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
                    const float* gamma, const float* beta, bool relu_x, uint16_t* dx, uint16_t* dres, float* dgamma,
                    float* dbeta, float* work, float* sums, long M, int C, hipStream_t st) {
-  BnGeom g = bn_geom(C);
+  BnGeom g = bn_geom(C, M);
   long rpb = bn_rows_per_block(M, g);
   int nb = (int)((M + rpb - 1) / rpb);
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, dy, x, y, mean, invstd,
