@@ -1,4 +1,4 @@
-"""A/B of the GEMM block tile (128x128, 4 waves of 64x64 vs 256x128, 4 waves of 128x64) on BERT / Llama GEMMs
+"""A/B of the GEMM main loop: 128x128 tiles with two LDS buffers (K8S_AMD_GEMM_PIPE=0) vs 256x128 tiles, 8 waves,
 and ResNet-50 convolutions, same process, interleaved; also checks the 256x128 results against 128x128.
 
     python scripts/ab_gemm_tile.py
@@ -31,15 +31,15 @@ for name, M, N, K in GEMMS:
     res = {}
     outs = {}
     for tile in ("1", "2", "1", "2"):
-        os.environ["K8S_AMD_GEMM_TILE"] = tile
+        os.environ["K8S_AMD_GEMM_PIPE"] = {"1": "0", "2": "1"}[tile]
         fn = lambda: C.gemm(a, True, b, True, None, False, None, 0, None, False, 1.0, 1)  # noqa: E731
         res.setdefault(tile, []).append(t(fn))
         outs[tile] = fn()
     err = ((outs["1"].float() - outs["2"].float()).norm() / outs["1"].float().norm()).item()
     r = {k: min(v) for k, v in res.items()}
     fl = 2.0 * M * N * K
-    print(json.dumps({"gemm": name, "MNK": [M, N, K], "t128_us": round(r["1"] * 1e3, 1), "t256_us": round(r["2"] * 1e3, 1),
-                      "tf128": round(fl / r["1"] / 1e9), "tf256": round(fl / r["2"] / 1e9), "relerr": err}), flush=True)
+    print(json.dumps({"gemm": name, "MNK": [M, N, K], "t2buf_us": round(r["1"] * 1e3, 1), "t3stage_us": round(r["2"] * 1e3, 1),
+                      "tf2buf": round(fl / r["1"] / 1e9), "tf3stage": round(fl / r["2"] / 1e9), "relerr": err}), flush=True)
 CONVS = [(256, 56, 64, 64, 3, 1, 1), (256, 28, 128, 128, 3, 1, 1), (256, 14, 256, 256, 3, 1, 1),
          (256, 7, 512, 512, 3, 1, 1), (256, 56, 64, 256, 1, 1, 0), (256, 56, 256, 64, 1, 1, 0),
          (256, 28, 512, 128, 1, 1, 0), (256, 14, 256, 1024, 1, 1, 0), (256, 56, 128, 128, 3, 2, 1)]
@@ -48,7 +48,7 @@ for (N, H, Cin, K, R, s, p) in CONVS:
     w = (torch.randn(K, R, R, Cin, device=dev) * 0.05).bfloat16()
     res, outs = {}, {}
     for tile in ("1", "2", "1", "2"):
-        os.environ["K8S_AMD_GEMM_TILE"] = tile
+        os.environ["K8S_AMD_GEMM_PIPE"] = {"1": "0", "2": "1"}[tile]
         fn = lambda: C.conv_fwd(x, w, s, p, 1, False, None, 0, None)  # noqa: E731
         res.setdefault(tile, []).append(t(fn))
         outs[tile] = fn()
@@ -56,6 +56,6 @@ for (N, H, Cin, K, R, s, p) in CONVS:
     r = {k: min(v) for k, v in res.items()}
     Ho = (H + 2 * p - R) // s + 1
     fl = 2.0 * N * Ho * Ho * K * Cin * R * R
-    print(json.dumps({"conv": [N, H, Cin, K, R, s, p], "t128_us": round(r["1"] * 1e3, 1), "t256_us": round(r["2"] * 1e3, 1),
-                      "tf128": round(fl / r["1"] / 1e9), "tf256": round(fl / r["2"] / 1e9), "relerr": err}), flush=True)
-os.environ.pop("K8S_AMD_GEMM_TILE", None)
+    print(json.dumps({"conv": [N, H, Cin, K, R, s, p], "t2buf_us": round(r["1"] * 1e3, 1), "t3stage_us": round(r["2"] * 1e3, 1),
+                      "tf2buf": round(fl / r["1"] / 1e9), "tf3stage": round(fl / r["2"] / 1e9), "relerr": err}), flush=True)
+os.environ.pop("K8S_AMD_GEMM_PIPE", None)
