@@ -71,6 +71,19 @@ struct KMajor {
     if (k0 + c * 8 >= ktot) return g_zero_page;
     return p + (long)gr * ld + k0 + c * 8;
   }
+  // Hoisted per-thread cursor: row, swizzled chunk and the 64-bit row address are loop-invariant, a tile only
+  // adds k0 (rocprofv3 showed ~5 VALU instructions per MFMA with the per-tile derivation).
+  struct Cursor { const uint16_t* p; int c8; };
+  __device__ __forceinline__ Cursor cursor(int s, int r0) const {
+    const int row = s >> 3, cp = s & 7;
+    const int c = cp ^ ((row >> 1) & 7);
+    int gr = r0 + row;
+    gr = gr < rows ? gr : rows - 1;
+    return Cursor{p + (long)gr * ld + c * 8, c * 8};
+  }
+  __device__ __forceinline__ const void* at(const Cursor& q, int k0) const {
+    return k0 + q.c8 >= ktot ? (const void*)g_zero_page : (const void*)(q.p + k0);
+  }
   static constexpr bool kmajor = true;
 };
 
@@ -85,6 +98,10 @@ struct MNMajor {
     col = col < cols ? col : cols - 8;
     return p + (long)(k0 + krow) * ld + col;
   }
+  // no hoisted cursor: every tile re-derives the address from the slot index
+  struct Cursor { int s, base; };
+  __device__ __forceinline__ Cursor cursor(int s, int base) const { return Cursor{s, base}; }
+  __device__ __forceinline__ const void* at(const Cursor& c, int k0) const { return src(c.s, c.base, k0); }
   static constexpr bool kmajor = false;
 };
 
@@ -107,6 +124,26 @@ struct ConvA {
     const int hi = ho * stride - pad + r * dil, wi = wo * stride - pad + sx * dil;
     if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) return g_zero_page;
     return x + (((long)n * H + hi) * W + wi) * C + c0 + c * 8;
+  }
+  // Hoisted cursor: the output pixel (n, ho, wo) of a thread's rows is fixed for the whole K loop; a tile only
+  // decodes its (r, s, c0) -- wave-uniform, so scalar -- and bounds-checks the tap per lane.
+  struct Cursor { const uint16_t* p; int hs, ws; };
+  __device__ __forceinline__ Cursor cursor(int s, int r0) const {
+    const int row = s >> 3, cp = s & 7;
+    const int c = cp ^ ((row >> 1) & 7);
+    int m = r0 + row;
+    m = m < rows ? m : rows - 1;
+    const int n = fHW.div(m), rem = m - n * (Ho * Wo);
+    const int ho = fWo.div(rem), wo = rem - ho * Wo;
+    const int hs = ho * stride - pad, ws = wo * stride - pad;
+    return Cursor{x + (((long)n * H + hs) * W + ws) * C + c * 8, hs, ws};
+  }
+  __device__ __forceinline__ const void* at(const Cursor& q, int k0) const {
+    const int rs = fC.div(k0), c0 = k0 - rs * C;
+    const int r = fS.div(rs), sx = rs - r * S;
+    const int hi = q.hs + r * dil, wi = q.ws + sx * dil;
+    if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) return g_zero_page;
+    return q.p + ((long)(r * dil) * W + sx * dil) * C + c0;
   }
   static constexpr bool kmajor = true;
 };
@@ -134,6 +171,10 @@ struct ConvAG {
     if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) return g_zero_page;
     return x + (((long)n * H + hi) * W + wi) * C + c0;
   }
+  // no hoisted cursor: every tile re-derives the address from the slot index
+  struct Cursor { int s, base; };
+  __device__ __forceinline__ Cursor cursor(int s, int base) const { return Cursor{s, base}; }
+  __device__ __forceinline__ const void* at(const Cursor& c, int k0) const { return src(c.s, c.base, k0); }
   static constexpr bool kmajor = true;
 };
 
@@ -160,6 +201,10 @@ struct ConvWgB {
     if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) return g_zero_page;
     return x + (((long)n * H + hi) * W + wi) * C + c;
   }
+  // no hoisted cursor: every tile re-derives the address from the slot index
+  struct Cursor { int s, base; };
+  __device__ __forceinline__ Cursor cursor(int s, int base) const { return Cursor{s, base}; }
+  __device__ __forceinline__ const void* at(const Cursor& c, int k0) const { return src(c.s, c.base, k0); }
   static constexpr bool kmajor = false;
 };
 
@@ -174,6 +219,16 @@ struct MNMajorK {
     int col = c0 + u * 8;
     if (col >= cols || k0 + krow >= ktot) return g_zero_page;
     return p + (long)(k0 + krow) * ld + col;
+  }
+  struct Cursor { const uint16_t* p; int krow; };  // krow = -inf marks a padding column
+  __device__ __forceinline__ Cursor cursor(int s, int c0) const {
+    const int krow = s >> 4, up = s & 15;
+    const int u = up ^ mn_swz(krow);
+    const int col = c0 + u * 8;
+    return Cursor{p + (long)krow * ld + col, col >= cols ? -(1 << 30) : krow};
+  }
+  __device__ __forceinline__ const void* at(const Cursor& q, int k0) const {
+    return (q.krow < 0 || k0 + q.krow >= ktot) ? (const void*)g_zero_page : (const void*)(q.p + (long)k0 * ld);
   }
   static constexpr bool kmajor = false;
 };
@@ -285,18 +340,30 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);  // provably wave-uniform for the M0 (LDS base) operand
+  constexpr int RA = TA / (16 * GEMM_THREADS), RB = TB / (16 * GEMM_THREADS);
+  // hoisted cursors cost ~4 VGPRs per load slot: the 3-blocks/CU single-buffer kernels (170 VGPRs) with 12
+  // slots would spill, so they keep the per-tile derivation
+  constexpr bool HOIST = !(NBUF == 1 && RA + RB > 8);
+  typename ASrc::Cursor ca[HOIST ? RA : 1];
+  typename BSrc::Cursor cb[HOIST ? RB : 1];
+  if constexpr (HOIST) {
+#pragma unroll
+    for (int rd = 0; rd < RA; ++rd) ca[rd] = A.cursor(rd * GEMM_THREADS + tid, m0);
+#pragma unroll
+    for (int rd = 0; rd < RB; ++rd) cb[rd] = B.cursor(rd * GEMM_THREADS + tid, n0);
+  }
   auto stage = [&](int buf, int k0) {
     char* ta = smem + buf * (TA + TB);
     char* tb = ta + TA;
 #pragma unroll
-    for (int rd = 0; rd < TA / (16 * GEMM_THREADS); ++rd) {
-      const int s = rd * GEMM_THREADS + tid;
-      glds16(A.src(s, m0, k0), ta + (rd * GEMM_THREADS + wid_u * 64) * 16);
+    for (int rd = 0; rd < RA; ++rd) {
+      const void* g = HOIST ? A.at(ca[HOIST ? rd : 0], k0) : A.src(rd * GEMM_THREADS + tid, m0, k0);
+      glds16(g, ta + (rd * GEMM_THREADS + wid_u * 64) * 16);
     }
 #pragma unroll
-    for (int rd = 0; rd < TB / (16 * GEMM_THREADS); ++rd) {
-      const int s = rd * GEMM_THREADS + tid;
-      glds16(B.src(s, n0, k0), tb + (rd * GEMM_THREADS + wid_u * 64) * 16);
+    for (int rd = 0; rd < RB; ++rd) {
+      const void* g = HOIST ? B.at(cb[HOIST ? rd : 0], k0) : B.src(rd * GEMM_THREADS + tid, n0, k0);
+      glds16(g, tb + (rd * GEMM_THREADS + wid_u * 64) * 16);
     }
   };
 
