@@ -149,13 +149,17 @@ def _dgrad_strided_hip(C_, gy, w, stride, padding, H, W):
     """dx [N, H, W, C] of a stride-s conv on our implicit-GEMM kernel, one launch per output parity."""
     K, R, S, C = w.shape
     N = gy.shape[0]
-    dx = torch.empty(N, H, W, C, device=gy.device, dtype=gy.dtype)
+    parities = [(a, b) for a in range(stride) for b in range(stride)]
+    empty = [(a, b) for a, b in parities
+             if not _parity_taps(R, a, padding, stride) or not _parity_taps(S, b, padding, stride)]
+    # parities no tap reaches are zero: one contiguous memset beats strided fills of the sub-grids
+    # (1x1 stride-2: 3 of 4 parities; strided fills made that path 1.8x slower than MIOpen)
+    dx = (torch.zeros if empty else torch.empty)(N, H, W, C, device=gy.device, dtype=gy.dtype)
     for a in range(stride):
         tr = _parity_taps(R, a, padding, stride)
         for b in range(stride):
             ts = _parity_taps(S, b, padding, stride)
             if not tr or not ts:
-                dx[:, a::stride, b::stride, :] = 0
                 continue
             # gather the taps with views + stack (no host->device index tensor, so no stream sync)
             wr = torch.stack([w[:, r] for _, r in tr], dim=1)                 # [K, Tr, S, C]
