@@ -80,3 +80,32 @@ def test_test_runner_and_cleanup(tmp_path):
         assert "tfjob/runner-t1-" in r.stdout
         assert not c.client.get("/apis/tensorflow.org/v1alpha1/namespaces/default/tfjobs")["items"]
         assert not c.client.get("/api/v1/namespaces/default/services?labelSelector=tensorflow.org")["items"]
+
+
+def test_deploy_dryrun_commands(capsys):
+    """tools/deploy.py (py/deploy.py parity): helm install with the amd preset + image tag, rollout wait, helm test,
+    uninstall -- printed, not run, under --dryrun."""
+    from k8s_amd.tools import deploy
+
+    assert deploy.main(["--dryrun", "--namespace", "kubeflow", "setup", "--image", "reg.io/op:v1"]) == 0
+    out = capsys.readouterr().out
+    assert "kubectl get nodes -o json" in out
+    assert "helm upgrade --install tf-job" in out and "cloud=amd" in out and "image=reg.io/op:v1" in out
+    assert "rollout status deployment/tf-job-operator" in out
+    assert deploy.main(["--dryrun", "test"]) == 0 and "helm test tf-job" in capsys.readouterr().out
+    assert deploy.main(["--dryrun", "teardown"]) == 0 and "helm uninstall tf-job" in capsys.readouterr().out
+    nodes = {"items": [{"status": {"allocatable": {"amd.com/gpu": "8"}}}, {"status": {"allocatable": {}}}]}
+    assert deploy.gpu_capacity(json.dumps(nodes)) == 8
+
+
+def test_deploy_local_e2e(tmp_path):
+    import os
+
+    from k8s_amd.fakeapi.cluster import OPERATOR_BIN
+    from k8s_amd.tools import deploy
+
+    if not os.path.exists(OPERATOR_BIN):
+        pytest.skip("operator not built")
+    junit = str(tmp_path / "junit.xml")
+    assert deploy.main(["--timeout", "90", "--junit", junit, "local"]) == 0
+    assert 'failures="0"' in open(junit).read()
