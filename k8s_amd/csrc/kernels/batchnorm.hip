@@ -9,6 +9,8 @@
 //  bwd:  reduce : sum(dy_eff), sum(dy_eff * xhat)  with dy_eff = dy * (y > 0)
 //        final  : dgamma, dbeta (fp32, written straight into the flat grad bucket)
 //        apply  : dx = gamma*invstd*(dy_eff - sum_dy/M - xhat*sum_dyxh/M), dres = dy_eff
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -207,7 +209,10 @@ __global__ void bn_finalize_sums_kernel(const float* __restrict__ sums, int nrep
 
 // y = act((x - mean) * (gamma * invstd) + beta [+ res]).
 // The grid is sized so (gridDim.x * blockDim.x) % cgroups == 0: every thread then keeps ONE channel group
-// for the whole grid-stride loop and holds its 8 channels' parameters in registers.
+// for the whole grid-stride loop and holds its 8 channels' parameters in registers. U vectors per trip: all
+// U (or 2U with a residual) 16-B loads are issued before the first is used, so each wave keeps several HBM
+// requests in flight instead of one load -> use -> store chain per trip.
+template <int U>
 __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ res,
                                                               const float* __restrict__ mean,
@@ -217,6 +222,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(const uint16_t* __
                                                               uint16_t* __restrict__ y, long nvec, int cgroups,
                                                               int relu) {
   const long e0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long stride = (long)gridDim.x * blockDim.x;
   const int cg = (int)(e0 % cgroups);
   float mu[8], sc[8], bt[8];
 #pragma unroll
@@ -226,7 +232,29 @@ __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(const uint16_t* __
     sc[j] = gamma[c] * invstd[c];
     bt[j] = beta[c];
   }
-  for (long e = e0; e < nvec; e += (long)gridDim.x * blockDim.x) {
+  long e = e0;
+  for (; e + (U - 1) * stride < nvec; e += U * stride) {
+    bf16x8_t xv[U], rv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) xv[u] = *reinterpret_cast<const bf16x8_t*>(x + (e + u * stride) * 8);
+    if (res) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) rv[u] = *reinterpret_cast<const bf16x8_t*>(res + (e + u * stride) * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float o = (bf2f((uint16_t)xv[u][j]) - mu[j]) * sc[j] + bt[j];
+        if (res) o += bf2f((uint16_t)rv[u][j]);
+        if (relu) o = fmaxf(o, 0.f);
+        v[j] = o;
+      }
+      store8(y + (e + u * stride) * 8, v);
+    }
+  }
+  for (; e < nvec; e += stride) {
     float v[8];
     load8(x + e * 8, v);
     float rv[8];
@@ -386,6 +414,9 @@ __global__ void __launch_bounds__(256) bn_bwd_final_kernel(const float* __restri
   }
 }
 
+// dx = gamma*invstd*(dy_eff - mean(dy_eff) - xhat*mean(dy_eff*xhat)); dres = dy_eff. U vectors per trip
+// with every load of the trip issued up front (see bn_apply_kernel).
+template <int U>
 __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t* __restrict__ dy,
                                                                   const uint16_t* __restrict__ x,
                                                                   const uint16_t* __restrict__ y,
@@ -398,6 +429,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t
                                                                   uint16_t* __restrict__ dres, long nvec,
                                                                   int cgroups, int C, float inv_m) {
   const long e0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long stride = (long)gridDim.x * blockDim.x;
   const int cg = (int)(e0 % cgroups);  // fixed per thread: grid sized so (grid*block) % cgroups == 0
   float mu[8], is[8], sc[8], bt[8], k1[8], k2[8];
 #pragma unroll
@@ -410,29 +442,80 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t
     k1[j] = sums[c] * inv_m;      // mean(dy_eff)
     k2[j] = sums[C + c] * inv_m;  // mean(dy_eff * xhat)
   }
-  for (long e = e0; e < nvec; e += (long)gridDim.x * blockDim.x) {
+  // B = -gamma*invstd^2*mean(dy_eff*xhat), D = -gamma*invstd*mean(dy_eff) - B*mean: dx = sc*g + B*x + D
+  float B[8], D[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    B[j] = -sc[j] * is[j] * k2[j];
+    D[j] = -sc[j] * k1[j] - B[j] * mu[j];
+  }
+  auto one = [&](bf16x8_t gv, bf16x8_t xvv, bool has_y, bf16x8_t yv, long e) {
     float g[8], xv[8];
-    load8(dy + e * 8, g);
-    load8(x + e * 8, xv);
-    if (y) {
-      bf16x8_t yv = *reinterpret_cast<const bf16x8_t*>(y + e * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      g[j] = bf2f((uint16_t)gv[j]);
+      xv[j] = bf2f((uint16_t)xvv[j]);
+    }
+    if (has_y) {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (bf2f((uint16_t)yv[j]) <= 0.f) g[j] = 0.f;
-    } else if (relu_x) {
+    } else if (relu_x) {  // ReLU mask recomputed from x: no read of y (non-residual BN)
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (bf2f(f2bf((xv[j] - mu[j]) * sc[j] + bt[j])) <= 0.f) g[j] = 0.f;
     }
     if (dres) store8(dres + e * 8, g);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float xh = (xv[j] - mu[j]) * is[j];
-      xv[j] = sc[j] * (g[j] - k1[j] - xh * k2[j]);
-    }
+    for (int j = 0; j < 8; ++j) xv[j] = sc[j] * g[j] + B[j] * xv[j] + D[j];
     store8(dx + e * 8, xv);
+  };
+  long e = e0;
+  for (; e + (U - 1) * stride < nvec; e += U * stride) {
+    bf16x8_t gv[U], xv[U], yv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) yv[u] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      gv[u] = *reinterpret_cast<const bf16x8_t*>(dy + (e + u * stride) * 8);
+      xv[u] = *reinterpret_cast<const bf16x8_t*>(x + (e + u * stride) * 8);
+    }
+    if (y) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) yv[u] = *reinterpret_cast<const bf16x8_t*>(y + (e + u * stride) * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(gv[u], xv[u], y != nullptr, yv[u], e + u * stride);
+  }
+  for (; e < nvec; e += stride) {
+    const bf16x8_t gv = *reinterpret_cast<const bf16x8_t*>(dy + e * 8);
+    const bf16x8_t xv = *reinterpret_cast<const bf16x8_t*>(x + e * 8);
+    bf16x8_t yv = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (y) yv = *reinterpret_cast<const bf16x8_t*>(y + e * 8);
+    one(gv, xv, y != nullptr, yv, e);
   }
 }
+
+// Loads per trip for the per-element BN kernels. $K8S_AMD_BN_UNROLL (1, 2 or 4) exists for A/B runs; the
+// default stays 1: on the ResNet-50 b512 shapes one 16-B load per trip already streams 4.4-5.3 TB/s and 2 or 4
+// per trip measured 0-12 % slower (lower occupancy), ResNet-50 8151 / 8097 / 8028 img/s for U = 1 / 2 / 4
+// (profiles/r01_bn_unroll_ab.md).
+static int bn_unroll() {
+  static int u = [] {
+    const char* s = getenv("K8S_AMD_BN_UNROLL");
+    const int v = s ? atoi(s) : 1;
+    return (v == 2 || v == 4) ? v : 1;
+  }();
+  return u;
+}
+
+static void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* mean, const float* invstd,
+                            const float* gamma, const float* beta, uint16_t* y, long nvec, int cgroups, int relu,
+                            hipStream_t st);
+static void launch_bn_bwd_apply(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,
+                                const float* invstd, const float* beta, int relu_x, const float* gamma,
+                                const float* sums, uint16_t* dx, uint16_t* dres, long nvec, int cgroups, int C,
+                                float inv_m, hipStream_t st);
 
 // ---------------------------------------------------------------- launchers
 static long bn_rows_per_block(long M, const BnGeom& g) {
@@ -462,6 +545,45 @@ static int bn_elem_grid(long nvec, int cgroups) {
   return g;
 }
 
+static void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* mean, const float* invstd,
+                            const float* gamma, const float* beta, uint16_t* y, long nvec, int cgroups, int relu,
+                            hipStream_t st) {
+  const dim3 grid(bn_elem_grid(nvec, cgroups)), block(BN_THREADS);
+  switch (bn_unroll()) {
+    case 4:
+      hipLaunchKernelGGL(bn_apply_kernel<4>, grid, block, 0, st, x, res, mean, invstd, gamma, beta, y, nvec, cgroups,
+                         relu);
+      break;
+    case 2:
+      hipLaunchKernelGGL(bn_apply_kernel<2>, grid, block, 0, st, x, res, mean, invstd, gamma, beta, y, nvec, cgroups,
+                         relu);
+      break;
+    default:
+      hipLaunchKernelGGL(bn_apply_kernel<1>, grid, block, 0, st, x, res, mean, invstd, gamma, beta, y, nvec, cgroups,
+                         relu);
+  }
+}
+
+static void launch_bn_bwd_apply(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,
+                                const float* invstd, const float* beta, int relu_x, const float* gamma,
+                                const float* sums, uint16_t* dx, uint16_t* dres, long nvec, int cgroups, int C,
+                                float inv_m, hipStream_t st) {
+  const dim3 grid(bn_elem_grid(nvec, cgroups)), block(BN_THREADS);
+  switch (bn_unroll()) {
+    case 4:
+      hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid, block, 0, st, dy, x, y, mean, invstd, beta, relu_x, gamma,
+                         sums, dx, dres, nvec, cgroups, C, inv_m);
+      break;
+    case 2:
+      hipLaunchKernelGGL(bn_bwd_apply_kernel<2>, grid, block, 0, st, dy, x, y, mean, invstd, beta, relu_x, gamma,
+                         sums, dx, dres, nvec, cgroups, C, inv_m);
+      break;
+    default:
+      hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, block, 0, st, dy, x, y, mean, invstd, beta, relu_x, gamma,
+                         sums, dx, dres, nvec, cgroups, C, inv_m);
+  }
+}
+
 int bn_workspace_floats(long M, int C) {
   BnGeom g = bn_geom(C, M);
   long rpb = bn_rows_per_block(M, g);
@@ -485,8 +607,7 @@ void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, c
                        save_mean, save_invstd);
   }
   const long nvec = M * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(bn_elem_grid(nvec, C / 8)), dim3(BN_THREADS), 0, st, x, res,
-                     save_mean, save_invstd, gamma, beta, y, nvec, C / 8, (int)relu);
+  launch_bn_apply(x, res, save_mean, save_invstd, gamma, beta, y, nvec, C / 8, (int)relu, st);
 }
 
 void launch_bn_fwd_from_sums(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
@@ -496,8 +617,7 @@ void launch_bn_fwd_from_sums(const uint16_t* x, const uint16_t* res, const float
   hipLaunchKernelGGL(bn_finalize_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, nrep, C, (float)M, eps,
                      momentum, save_mean, save_invstd, run_mean, run_var);
   const long nvec = M * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(bn_elem_grid(nvec, C / 8)), dim3(BN_THREADS), 0, st, x, res,
-                     save_mean, save_invstd, gamma, beta, y, nvec, C / 8, (int)relu);
+  launch_bn_apply(x, res, save_mean, save_invstd, gamma, beta, y, nvec, C / 8, (int)relu, st);
 }
 
 // Fold the conv-epilogue replicas [nrep][2][C] of (sum g*mask, sum g*mask*xhat) into sums / dgamma / dbeta.
@@ -525,8 +645,8 @@ void launch_bn_bwd_from_sums(const uint16_t* dy, const uint16_t* x, const uint16
   hipLaunchKernelGGL(bn_bwd_fold_reps_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, reps, nrep, C, sums, dgamma,
                      dbeta);
   const long nvec = M * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(bn_elem_grid(nvec, C / 8)), dim3(BN_THREADS), 0, st, dy, x, y,
-                     mean, invstd, beta, (int)relu_x, gamma, sums, dx, dres, nvec, C / 8, C, 1.f / (float)M);
+  launch_bn_bwd_apply(dy, x, y, mean, invstd, beta, (int)relu_x, gamma, sums, dx, dres, nvec, C / 8, C,
+                      1.f / (float)M, st);
 }
 
 void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
@@ -539,8 +659,8 @@ void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, con
                      gamma, beta, (int)relu_x, M, C, g.tpr, g.rows_per_iter, rpb, work);
   hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, nb, C, sums, dgamma, dbeta);
   const long nvec = M * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(bn_elem_grid(nvec, C / 8)), dim3(BN_THREADS), 0, st, dy, x, y,
-                     mean, invstd, beta, (int)relu_x, gamma, sums, dx, dres, nvec, C / 8, C, 1.f / (float)M);
+  launch_bn_bwd_apply(dy, x, y, mean, invstd, beta, (int)relu_x, gamma, sums, dx, dres, nvec, C / 8, C,
+                      1.f / (float)M, st);
 }
 
 }  // namespace k8s_amd

@@ -28,8 +28,9 @@ def timeit(fn, reps=20):
     return s.elapsed_time(e) / reps
 
 
-SHAPES = [(256 * 112 * 112, 64), (256 * 56 * 56, 64), (256 * 56 * 56, 256), (256 * 28 * 28, 128),
-          (256 * 28 * 28, 512), (256 * 14 * 14, 1024), (256 * 7 * 7, 2048)]
+NB = int(os.environ.get("BN_BATCH", "256"))
+SHAPES = [(NB * 112 * 112, 64), (NB * 56 * 56, 64), (NB * 56 * 56, 256), (NB * 28 * 28, 128),
+          (NB * 28 * 28, 512), (NB * 14 * 14, 1024), (NB * 7 * 7, 2048)]
 for M, C in SHAPES:
     x = torch.randn(M, C, device=dev, dtype=torch.bfloat16)
     res = torch.randn(M, C, device=dev, dtype=torch.bfloat16)
