@@ -5,6 +5,8 @@
 // Backward as a GATHER: each thread owns 8 channels of one INPUT pixel and sums dy over the (at most
 // ceil(k/s)^2) output windows covering it whose recorded winner is this pixel -- no atomics, no zero fill,
 // every dx element written exactly once.
+#include <stdexcept>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -13,15 +15,17 @@ namespace k8s_amd {
 __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                           uint8_t* __restrict__ idx, int N, int H, int W, int C,
                                                           int Ho, int Wo, int k, int s, int p) {
+  // 32-bit index decode (the host guarantees total < 2^31): 64-bit division is a long software sequence on
+  // CDNA and dominated these bandwidth-bound kernels
   const int cv = C / 8;
-  const long total = (long)N * Ho * Wo * cv;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(e % cv) * 8;
-    long t = e / cv;
-    const int wo = (int)(t % Wo);
+  const int total = N * Ho * Wo * cv;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int c = (e % cv) * 8;
+    int t = e / cv;
+    const int wo = t % Wo;
     t /= Wo;
-    const int ho = (int)(t % Ho);
-    const int n = (int)(t / Ho);
+    const int ho = t % Ho;
+    const int n = t / Ho;
     float best[8];
     uint8_t arg[8];
 #pragma unroll
@@ -46,11 +50,11 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint16_t* __rest
           }
       }
     }
-    store8(y + e * 8, best);
+    store8(y + (long)e * 8, best);
     uint64_t packed = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) packed |= (uint64_t)arg[j] << (8 * j);
-    *reinterpret_cast<uint64_t*>(idx + e * 8) = packed;
+    *reinterpret_cast<uint64_t*>(idx + (long)e * 8) = packed;
   }
 }
 
@@ -59,14 +63,14 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const uint16_t* __rest
                                                           int N, int H, int W, int C, int Ho, int Wo, int k, int s,
                                                           int p) {
   const int cv = C / 8;
-  const long total = (long)N * H * W * cv;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(e % cv) * 8;
-    long t = e / cv;
-    const int w = (int)(t % W);
+  const int total = N * H * W * cv;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int c = (e % cv) * 8;
+    int t = e / cv;
+    const int w = t % W;
     t /= W;
-    const int h = (int)(t % H);
-    const int n = (int)(t / H);
+    const int h = t % H;
+    const int n = t / H;
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
@@ -91,13 +95,14 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const uint16_t* __rest
           if (((packed >> (8 * j)) & 0xff) == pos) acc[j] += g[j];
       }
     }
-    store8(dx + e * 8, acc);
+    store8(dx + (long)e * 8, acc);
   }
 }
 
 void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
                         int k, int s, int p, hipStream_t st) {
   const long total = (long)N * Ho * Wo * (C / 8);
+  if ((long)N * H * W * C / 8 >= (1L << 31)) throw std::runtime_error("maxpool: tensor too large for 32-bit indexing");
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, st, x, y, idx, N, H, W, C, Ho,
                      Wo, k, s, p);
 }
@@ -105,6 +110,7 @@ void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int
 void launch_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W, int C, int Ho,
                         int Wo, int k, int s, int p, hipStream_t st) {
   const long total = (long)N * H * W * (C / 8);
+  if (total >= (1L << 31)) throw std::runtime_error("maxpool: tensor too large for 32-bit indexing");
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, st, dy, idx, dx, N, H, W, C,
                      Ho, Wo, k, s, p);
 }

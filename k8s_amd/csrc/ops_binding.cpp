@@ -335,8 +335,10 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, bo
 // One output-parity piece of a stride-s data gradient: out[n, i*s+a, j*s+b, :] = conv(dy, wsub, stride 1, pad)
 // over an Hs x Ws grid (i < Hs, j < Ws). wsub [C, Tr, Ts, K] holds the taps of that parity
 // (ops/conv.py _dgrad_strided_hip builds it); out is the full bf16 dx [N, H, W, C].
+// out[n, i*stride + a, j*stride + b, :] (+)= conv(x, w)[n, i, j, :]: one output parity of a strided dgrad;
+// `accumulate` adds onto out in the epilogue (out already holds the residual branch's gradient).
 void conv_fwd_subgrid(Tensor x, Tensor w, int64_t pad, int64_t Hs, int64_t Ws, Tensor out, int64_t stride, int64_t a,
-                      int64_t b) {
+                      int64_t b, bool accumulate) {
   check_cuda(x, "x"); check_cuda(w, "w"); check_cuda(out, "out");
   check_dtype(x, at::kBFloat16, "x"); check_dtype(w, at::kBFloat16, "w"); check_dtype(out, at::kBFloat16, "out");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && out.dim() == 4 && out.is_contiguous());
@@ -350,7 +352,7 @@ void conv_fwd_subgrid(Tensor x, Tensor w, int64_t pad, int64_t Hs, int64_t Ws, T
               "sub-grid exceeds the output image");
   k8s_amd::SubGrid sg{OH, OW, (int)stride, (int)a, (int)b};
   k8s_amd::launch_conv_fwd(cbf(x), cbf(w), out.data_ptr(), false, N, H, W, C, K, R, S, 1, (int)pad, 1, (int)Hs,
-                           (int)Ws, nullptr, 0, 0, nullptr, cur_stream(), nullptr, &sg);
+                           (int)Ws, nullptr, 0, accumulate ? 1 : 0, nullptr, cur_stream(), nullptr, &sg);
 }
 
 // dw[K,R,S,C] fp32 (+)= dy^T . im2col(x)
@@ -568,7 +570,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out_f32"), py::arg("bias"), py::arg("act"), py::arg("stats"), py::arg("bnb") = py::none(),
         py::arg("bnb_relu_x") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
-  m.def("conv_fwd_subgrid", &conv_fwd_subgrid);
+  m.def("conv_fwd_subgrid", &conv_fwd_subgrid, py::arg("x"), py::arg("w"), py::arg("pad"), py::arg("Hs"),
+        py::arg("Ws"), py::arg("out"), py::arg("stride"), py::arg("a"), py::arg("b"), py::arg("accumulate") = false);
   m.def("conv_dgrad_wtrans", &conv_dgrad_wtrans);
   m.def("flash_fwd", &flash_fwd);
   m.def("maxpool_fwd", &maxpool_fwd);

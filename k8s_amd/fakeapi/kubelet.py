@@ -134,15 +134,39 @@ class LocalKubelet:
         return open(p).read() if os.path.exists(p) else ""
 
     # ------------------------------------------------------------------ services / volumes / env
+    def _service_port(self) -> int:
+        """A free 127.0.0.1 port P whose P+1 is free too and not handed out: workloads rendezvous on the
+        master service's port + 1 (parallel/dist.py), which must not land on another Service's port."""
+        import socket
+
+        taken = set(self.service_ports.values())
+        taken |= {p + 1 for p in taken}
+        for _ in range(64):
+            a = socket.socket()
+            try:
+                a.bind(("127.0.0.1", 0))
+                port = a.getsockname()[1]
+                if port in taken or port + 1 in taken or port + 1 > 65535:
+                    continue
+                b = socket.socket()
+                try:
+                    b.bind(("127.0.0.1", port + 1))
+                except OSError:
+                    continue
+                finally:
+                    b.close()
+                return port
+            finally:
+                a.close()
+        raise RuntimeError("no free port pair for a Service")
+
     def _service_map(self, ns) -> Dict[str, str]:
         out = {}
         for s in self.api.get(self._path(ns, "services")).get("items", []):
             name = s["metadata"]["name"]
             key = ns + "/" + name
             if key not in self.service_ports:
-                from k8s_amd.fakeapi.server import free_port
-
-                self.service_ports[key] = free_port()
+                self.service_ports[key] = self._service_port()
             out[name] = "127.0.0.1:%d" % self.service_ports[key]
             for port in s.get("spec", {}).get("ports", []):
                 out["%s:%s" % (name, port.get("port"))] = "127.0.0.1:%d" % self.service_ports[key]

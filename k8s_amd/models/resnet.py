@@ -78,11 +78,14 @@ class Bottleneck(nn.Module):
         # identity block: x's two gradient contributions (residual via bn3, main path via conv1) are summed
         # inside conv1's dgrad epilogue instead of by a separate elementwise add
         link = K.GradLink() if identity else None
+        # downsample block: x feeds conv1 and the downsample conv; their two dgrads are summed in the
+        # epilogue of whichever runs second (shared link) instead of by autograd's separate add
+        dlink = K.GradLink(shared=True) if (self.down is not None and x.requires_grad) else None
         l1, l2, l3 = K.BnBwdLink(), K.BnBwdLink(), K.BnBwdLink()
-        y = self.bn1(self.conv1(x, grad_link=link, bn_link=in_link if identity else None), bwd_link=l1)
+        y = self.bn1(self.conv1(x, grad_link=link or dlink, bn_link=in_link if identity else None), bwd_link=l1)
         y = self.bn2(self.conv2(y, bn_link=l1), bwd_link=l2)
         if self.down is not None:
-            idn = self.down_bn(self.down(x), relu=False)
+            idn = self.down_bn(self.down(x, grad_link=dlink), relu=False)
         return self.bn3(self.conv3(y, bn_link=l2), residual=idn, relu=True, res_link=link, bwd_link=l3), l3
 
 

@@ -145,16 +145,23 @@ def strided_dgrad_ok(gy, w, stride, padding):
     return True
 
 
-def _dgrad_strided_hip(C_, gy, w, stride, padding, H, W):
-    """dx [N, H, W, C] of a stride-s conv on our implicit-GEMM kernel, one launch per output parity."""
+def _dgrad_strided_hip(C_, gy, w, stride, padding, H, W, addend=None):
+    """dx [N, H, W, C] of a stride-s conv on our implicit-GEMM kernel, one launch per output parity.
+
+    With ``addend`` (bf16 [N, H, W, C], e.g. the gradient the block input already got from the other branch)
+    every parity accumulates onto it in the GEMM epilogue and it is returned: no memset for the parities no
+    tap reaches (they keep the addend) and no separate add pass."""
     K, R, S, C = w.shape
     N = gy.shape[0]
     parities = [(a, b) for a in range(stride) for b in range(stride)]
     empty = [(a, b) for a, b in parities
              if not _parity_taps(R, a, padding, stride) or not _parity_taps(S, b, padding, stride)]
-    # parities no tap reaches are zero: one contiguous memset beats strided fills of the sub-grids
-    # (1x1 stride-2: 3 of 4 parities; strided fills made that path 1.8x slower than MIOpen)
-    dx = (torch.zeros if empty else torch.empty)(N, H, W, C, device=gy.device, dtype=gy.dtype)
+    if addend is not None:
+        dx = addend
+    else:
+        # parities no tap reaches are zero: one contiguous memset beats strided fills of the sub-grids
+        # (1x1 stride-2: 3 of 4 parities; strided fills made that path 1.8x slower than MIOpen)
+        dx = (torch.zeros if empty else torch.empty)(N, H, W, C, device=gy.device, dtype=gy.dtype)
     for a in range(stride):
         tr = _parity_taps(R, a, padding, stride)
         for b in range(stride):
@@ -166,7 +173,7 @@ def _dgrad_strided_hip(C_, gy, w, stride, padding, H, W):
             wsub = torch.stack([wr[:, :, s_] for _, s_ in ts], dim=2)         # [K, Tr, Ts, C]
             wsub = wsub.permute(3, 1, 2, 0).contiguous()                      # [C, Tr, Ts, K]
             Hs, Ws = (H - a + stride - 1) // stride, (W - b + stride - 1) // stride
-            C_.conv_fwd_subgrid(gy, wsub, -tr[0][0], Hs, Ws, dx, stride, a, b)
+            C_.conv_fwd_subgrid(gy, wsub, -tr[0][0], Hs, Ws, dx, stride, a, b, addend is not None)
     return dx
 
 
@@ -207,12 +214,19 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, bn_link=No
                     ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, True, False)[0].add_(addend))]) == "hip"
         elif hip and strided_dgrad_ok(gy, w, stride, padding):
             H, W_ = x.shape[1], x.shape[2]
-            if autotune.choose(_key("conv_dgrad_s", x, w, stride, padding), [
+            if addend is None:
+                choice = autotune.choose(_key("conv_dgrad_s", x, w, stride, padding), [
                     ("hip", lambda: _dgrad_strided_hip(C_, gy, w, stride, padding, H, W_)),
-                    ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, True, False))]) == "hip":
+                    ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, True, False))])
+            else:  # the fused accumulate against the vendor dgrad + a separate add
+                scratch = torch.empty_like(addend)  # timing only: accumulates onto garbage, never read
+                choice = autotune.choose(_key("conv_dgrad_s_acc", x, w, stride, padding), [
+                    ("hip", lambda: _dgrad_strided_hip(C_, gy, w, stride, padding, H, W_, scratch)),
+                    ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, True, False)[0].add_(addend))])
+            if choice == "hip":
                 STATS["hip_dgrad"] += 1
-                dx = _dgrad_strided_hip(C_, gy, w, stride, padding, H, W_)
-                return _finish_dw(dx if addend is None else dx.add_(addend), dw_done, p, gy, x, w, stride, padding)
+                dx = _dgrad_strided_hip(C_, gy, w, stride, padding, H, W_, addend)
+                return _finish_dw(dx, dw_done, p, gy, x, w, stride, padding)
         if use_hip:
             STATS["hip_dgrad"] += 1
             bnb = None

@@ -47,11 +47,15 @@ def _zero_scratch(store, device, n):
 class GradLink:
     """Carries one tensor's gradient from one autograd node to another that runs later in the backward
     pass, so the sum of the two contributions is formed inside a kernel (e.g. a ResNet identity block:
-    the residual branch's dres is accumulated in conv1's dgrad epilogue instead of by a separate add)."""
-    __slots__ = ("grad",)
+    the residual branch's dres is accumulated in conv1's dgrad epilogue instead of by a separate add).
+    With ``shared=True`` the link joins two convolutions that read the same input (a ResNet downsample
+    block's conv1 and downsample conv): whichever backward runs first hands its dx over instead of returning
+    it, and the second accumulates it in its own dgrad epilogue -- correct in either autograd order."""
+    __slots__ = ("grad", "shared")
 
-    def __init__(self):
+    def __init__(self, shared: bool = False):
         self.grad = None
+        self.shared = shared
 
 
 class BnBwdLink:
@@ -100,6 +104,9 @@ class _Conv2dNHWC(torch.autograd.Function):
         addend = None
         if ctx.link is not None:
             addend, ctx.link.grad = ctx.link.grad, None
+            if addend is None and ctx.link.shared and ctx.x_requires_grad:  # first of the two readers of x
+                ctx.link.grad = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, True, p)
+                return None, None, None, None, None, None, None, None
         bn_link = ctx.bn_link if (ctx.bn_link is not None and ctx.bn_link.x is not None) else None
         dx = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, ctx.x_requires_grad, p, addend=addend, bn_link=bn_link)
         return dx, None, None, None, None, None, None, None

@@ -264,3 +264,24 @@ def test_conv_dgrad_strided(cuda, N, H, C, K, R, st, pad):
     xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
     F.conv2d(xr, w.float().permute(0, 3, 1, 2), None, st, pad).backward(dy.float().permute(0, 3, 1, 2))
     assert _rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+# the residual-gradient add fused into the strided dgrad: every parity accumulates onto the addend in the
+# GEMM epilogue; parities no tap reaches keep the addend unchanged
+@pytest.mark.parametrize("N,H,C,K,R,st,pad", [(4, 28, 256, 512, 1, 2, 0), (2, 15, 64, 128, 3, 2, 1),
+                                              (3, 14, 512, 1024, 1, 2, 0)])
+def test_conv_dgrad_strided_accumulate(cuda, N, H, C, K, R, st, pad):
+    from k8s_amd.ops import conv as kc
+
+    torch.manual_seed(11)
+    Ho = (H + 2 * pad - R) // st + 1
+    x = torch.randn(N, H, H, C, device=cuda).bfloat16()
+    w = (torch.randn(K, R, R, C, device=cuda) * 0.05).bfloat16()
+    dy = torch.randn(N, Ho, Ho, K, device=cuda).bfloat16()
+    addend = torch.randn(N, H, H, C, device=cuda).bfloat16()
+    ref_add = addend.float().clone()
+    out = kc._dgrad_strided_hip(_C(), dy, w, st, pad, H, H, addend)
+    assert out.data_ptr() == addend.data_ptr()
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    F.conv2d(xr, w.float().permute(0, 3, 1, 2), None, st, pad).backward(dy.float().permute(0, 3, 1, 2))
+    assert _rel(out, xr.grad.permute(0, 2, 3, 1) + ref_add) < 1e-2

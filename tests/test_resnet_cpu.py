@@ -102,3 +102,37 @@ def test_strided_dgrad_parity_taps():
                                                   w.permute(0, 3, 1, 2), None, [s, s], [p, p], [1, 1], False,
                                                   [0, 0], 1, [True, False, False])[0].permute(0, 2, 3, 1)
         assert (dx - ref).abs().max() < 1e-3
+
+
+def test_shared_grad_link_sums_both_readers_in_either_order():
+    """A downsample block's x feeds conv1 and the strided downsample conv through one shared GradLink: the
+    first backward hands its dx over, the second adds it in its dgrad. Whichever order autograd picks, x.grad
+    must equal the plain sum of both convolutions' input gradients."""
+    import torch.nn.functional as F
+
+    from k8s_amd.parallel.flat import init_kaiming_normal
+
+    for down_first in (False, True):
+        torch.manual_seed(3)
+        store = ParamStore()
+        pa = store.new("a.weight", (16, 1, 1, 8), init_kaiming_normal(8))
+        pb = store.new("b.weight", (16, 1, 1, 8), init_kaiming_normal(8))
+        store.finalize("cpu")
+        x = torch.randn(2, 8, 8, 8, requires_grad=True)
+        link = K.GradLink(shared=True)
+        store.begin_step()
+        if down_first:  # created later in forward -> runs earlier in backward
+            ya = K.conv2d_nhwc(x, pa, 1, 0, grad_link=link)
+            yb = K.conv2d_nhwc(x, pb, 2, 0, grad_link=link)
+        else:
+            yb = K.conv2d_nhwc(x, pb, 2, 0, grad_link=link)
+            ya = K.conv2d_nhwc(x, pa, 1, 0, grad_link=link)
+        ga, gb = torch.randn_like(ya), torch.randn_like(yb)
+        ((ya * ga).sum() + (yb * gb).sum()).backward()
+        assert link.grad is None  # consumed by the second reader
+        xr = x.detach().permute(0, 3, 1, 2).requires_grad_(True)
+        wa = pa.master.view(16, 1, 1, 8).permute(0, 3, 1, 2)
+        wb = pb.master.view(16, 1, 1, 8).permute(0, 3, 1, 2)
+        ((F.conv2d(xr, wa) * ga.permute(0, 3, 1, 2)).sum()
+         + (F.conv2d(xr, wb, stride=2) * gb.permute(0, 3, 1, 2)).sum()).backward()
+        torch.testing.assert_close(x.grad, xr.grad.permute(0, 2, 3, 1), rtol=1e-4, atol=1e-4)
