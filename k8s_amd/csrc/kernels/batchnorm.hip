@@ -207,6 +207,15 @@ __global__ void bn_finalize_sums_kernel(const float* __restrict__ sums, int nrep
   }
 }
 
+// Packed ReLU mask: bit j of byte e = (bf16(y[8e + j]) > 0). A residual BN's backward reads these M*C/8 bytes
+// instead of the bf16 output y (2 B/elem) in both its reduce and apply passes.
+__device__ __forceinline__ uint8_t relu_bits(const float (&v)[8]) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b |= (bf2f(f2bf(v[j])) > 0.f ? 1u : 0u) << j;
+  return (uint8_t)b;
+}
+
 // y = act((x - mean) * (gamma * invstd) + beta [+ res]).
 // The grid is sized so (gridDim.x * blockDim.x) % cgroups == 0: every thread then keeps ONE channel group
 // for the whole grid-stride loop and holds its 8 channels' parameters in registers. U vectors per trip: all
@@ -219,8 +228,8 @@ __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(const uint16_t* __
                                                               const float* __restrict__ invstd,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ beta,
-                                                              uint16_t* __restrict__ y, long nvec, int cgroups,
-                                                              int relu) {
+                                                              uint16_t* __restrict__ y, uint8_t* __restrict__ mask,
+                                                              long nvec, int cgroups, int relu) {
   const long e0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
   const long stride = (long)gridDim.x * blockDim.x;
   const int cg = (int)(e0 % cgroups);
@@ -252,6 +261,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(const uint16_t* __
         v[j] = o;
       }
       store8(y + (e + u * stride) * 8, v);
+      if (mask) mask[e + u * stride] = relu_bits(v);
     }
   }
   for (; e < nvec; e += stride) {
@@ -267,6 +277,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(const uint16_t* __
       v[j] = o;
     }
     store8(y + e * 8, v);
+    if (mask) mask[e] = relu_bits(v);
   }
 }
 
@@ -280,6 +291,9 @@ __global__ void bn_eval_prep_kernel(const float* __restrict__ run_mean, const fl
 }
 
 // Backward reduce: part[(bx*C + c)*2] = sum dy_eff, [+1] = sum dy_eff * xhat
+// MASK: the ReLU mask comes from the packed bit mask (a separate instantiation, so the y / relu_x variant keeps
+// its register budget and occupancy).
+template <bool MASK>
 __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy,
                                                                    const uint16_t* __restrict__ x,
                                                                    const uint16_t* __restrict__ y,
@@ -288,7 +302,8 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
                                                                    const float* __restrict__ gamma,
                                                                    const float* __restrict__ beta, int relu_x, long M,
                                                                    int C, int tpr, int rows_per_iter,
-                                                                   long rows_per_block, float* __restrict__ part) {
+                                                                   long rows_per_block, float* __restrict__ part,
+                                                                   const uint8_t* __restrict__ mask) {
   __shared__ float sh[2][BN_THREADS][9];
   const int t = threadIdx.x;
   const int r = t / tpr, cg_local = t % tpr;
@@ -321,7 +336,12 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
       for (int u = 0; u < 4; ++u) {
         float* g = g4[u];
         const float* xv = x4[u];
-        if (y) {
+        if constexpr (MASK) {
+          const uint32_t bits = mask[((row + u * rows_per_iter) * C + cg * 8) >> 3];
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (!((bits >> j) & 1u)) g[j] = 0.f;
+        } else if (y) {
           bf16x8_t yv = *reinterpret_cast<const bf16x8_t*>(y + (row + u * rows_per_iter) * C + cg * 8);
 #pragma unroll
           for (int j = 0; j < 8; ++j)
@@ -343,7 +363,12 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
       float g[8], xv[8];
       load8(dy + off, g);
       load8(x + off, xv);
-      if (y) {
+      if constexpr (MASK) {
+        const uint32_t bits = mask[off >> 3];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (!((bits >> j) & 1u)) g[j] = 0.f;
+      } else if (y) {
         bf16x8_t yv = *reinterpret_cast<const bf16x8_t*>(y + off);
 #pragma unroll
         for (int j = 0; j < 8; ++j)
@@ -427,7 +452,8 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t
                                                                   const float* __restrict__ sums,
                                                                   uint16_t* __restrict__ dx,
                                                                   uint16_t* __restrict__ dres, long nvec,
-                                                                  int cgroups, int C, float inv_m) {
+                                                                  int cgroups, int C, float inv_m,
+                                                                  const uint8_t* __restrict__ mask) {
   const long e0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
   const long stride = (long)gridDim.x * blockDim.x;
   const int cg = (int)(e0 % cgroups);  // fixed per thread: grid sized so (grid*block) % cgroups == 0
@@ -456,7 +482,12 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t
       g[j] = bf2f((uint16_t)gv[j]);
       xv[j] = bf2f((uint16_t)xvv[j]);
     }
-    if (has_y) {
+    if (mask) {
+      const uint32_t bits = mask[e];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (!((bits >> j) & 1u)) g[j] = 0.f;
+    } else if (has_y) {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (bf2f((uint16_t)yv[j]) <= 0.f) g[j] = 0.f;
@@ -510,12 +541,12 @@ static int bn_unroll() {
 }
 
 static void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* mean, const float* invstd,
-                            const float* gamma, const float* beta, uint16_t* y, long nvec, int cgroups, int relu,
-                            hipStream_t st);
+                            const float* gamma, const float* beta, uint16_t* y, uint8_t* mask, long nvec,
+                            int cgroups, int relu, hipStream_t st);
 static void launch_bn_bwd_apply(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,
                                 const float* invstd, const float* beta, int relu_x, const float* gamma,
                                 const float* sums, uint16_t* dx, uint16_t* dres, long nvec, int cgroups, int C,
-                                float inv_m, hipStream_t st);
+                                float inv_m, const uint8_t* mask, hipStream_t st);
 
 // ---------------------------------------------------------------- launchers
 static long bn_rows_per_block(long M, const BnGeom& g) {
@@ -546,41 +577,41 @@ static int bn_elem_grid(long nvec, int cgroups) {
 }
 
 static void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* mean, const float* invstd,
-                            const float* gamma, const float* beta, uint16_t* y, long nvec, int cgroups, int relu,
-                            hipStream_t st) {
+                            const float* gamma, const float* beta, uint16_t* y, uint8_t* mask, long nvec,
+                            int cgroups, int relu, hipStream_t st) {
   const dim3 grid(bn_elem_grid(nvec, cgroups)), block(BN_THREADS);
   switch (bn_unroll()) {
     case 4:
-      hipLaunchKernelGGL(bn_apply_kernel<4>, grid, block, 0, st, x, res, mean, invstd, gamma, beta, y, nvec, cgroups,
-                         relu);
+      hipLaunchKernelGGL(bn_apply_kernel<4>, grid, block, 0, st, x, res, mean, invstd, gamma, beta, y, mask, nvec,
+                         cgroups, relu);
       break;
     case 2:
-      hipLaunchKernelGGL(bn_apply_kernel<2>, grid, block, 0, st, x, res, mean, invstd, gamma, beta, y, nvec, cgroups,
-                         relu);
+      hipLaunchKernelGGL(bn_apply_kernel<2>, grid, block, 0, st, x, res, mean, invstd, gamma, beta, y, mask, nvec,
+                         cgroups, relu);
       break;
     default:
-      hipLaunchKernelGGL(bn_apply_kernel<1>, grid, block, 0, st, x, res, mean, invstd, gamma, beta, y, nvec, cgroups,
-                         relu);
+      hipLaunchKernelGGL(bn_apply_kernel<1>, grid, block, 0, st, x, res, mean, invstd, gamma, beta, y, mask, nvec,
+                         cgroups, relu);
   }
 }
 
 static void launch_bn_bwd_apply(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,
                                 const float* invstd, const float* beta, int relu_x, const float* gamma,
                                 const float* sums, uint16_t* dx, uint16_t* dres, long nvec, int cgroups, int C,
-                                float inv_m, hipStream_t st) {
+                                float inv_m, const uint8_t* mask, hipStream_t st) {
   const dim3 grid(bn_elem_grid(nvec, cgroups)), block(BN_THREADS);
   switch (bn_unroll()) {
     case 4:
       hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid, block, 0, st, dy, x, y, mean, invstd, beta, relu_x, gamma,
-                         sums, dx, dres, nvec, cgroups, C, inv_m);
+                         sums, dx, dres, nvec, cgroups, C, inv_m, mask);
       break;
     case 2:
       hipLaunchKernelGGL(bn_bwd_apply_kernel<2>, grid, block, 0, st, dy, x, y, mean, invstd, beta, relu_x, gamma,
-                         sums, dx, dres, nvec, cgroups, C, inv_m);
+                         sums, dx, dres, nvec, cgroups, C, inv_m, mask);
       break;
     default:
       hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, block, 0, st, dy, x, y, mean, invstd, beta, relu_x, gamma,
-                         sums, dx, dres, nvec, cgroups, C, inv_m);
+                         sums, dx, dres, nvec, cgroups, C, inv_m, mask);
   }
 }
 
@@ -593,7 +624,7 @@ int bn_workspace_floats(long M, int C) {
 
 void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta, uint16_t* y,
                    float* save_mean, float* save_invstd, float* run_mean, float* run_var, float* work, long M, int C,
-                   float eps, float momentum, bool training, bool relu, hipStream_t st) {
+                   float eps, float momentum, bool training, bool relu, hipStream_t st, uint8_t* mask) {
   if (training) {
     BnGeom g = bn_geom(C, M);
     long rpb = bn_rows_per_block(M, g);
@@ -607,17 +638,17 @@ void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, c
                        save_mean, save_invstd);
   }
   const long nvec = M * C / 8;
-  launch_bn_apply(x, res, save_mean, save_invstd, gamma, beta, y, nvec, C / 8, (int)relu, st);
+  launch_bn_apply(x, res, save_mean, save_invstd, gamma, beta, y, mask, nvec, C / 8, (int)relu, st);
 }
 
 void launch_bn_fwd_from_sums(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
                              uint16_t* y, const float* sums, int nrep, float* save_mean, float* save_invstd,
                              float* run_mean, float* run_var, long M, int C, float eps, float momentum, bool relu,
-                             hipStream_t st) {
+                             hipStream_t st, uint8_t* mask) {
   hipLaunchKernelGGL(bn_finalize_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, nrep, C, (float)M, eps,
                      momentum, save_mean, save_invstd, run_mean, run_var);
   const long nvec = M * C / 8;
-  launch_bn_apply(x, res, save_mean, save_invstd, gamma, beta, y, nvec, C / 8, (int)relu, st);
+  launch_bn_apply(x, res, save_mean, save_invstd, gamma, beta, y, mask, nvec, C / 8, (int)relu, st);
 }
 
 // Fold the conv-epilogue replicas [nrep][2][C] of (sum g*mask, sum g*mask*xhat) into sums / dgamma / dbeta.
@@ -641,26 +672,30 @@ __global__ void __launch_bounds__(256) bn_bwd_fold_reps_kernel(const float* __re
 void launch_bn_bwd_from_sums(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,
                              const float* invstd, const float* gamma, const float* beta, bool relu_x, uint16_t* dx,
                              uint16_t* dres, float* dgamma, float* dbeta, const float* reps, int nrep, float* sums,
-                             long M, int C, hipStream_t st) {
+                             long M, int C, hipStream_t st, const uint8_t* mask) {
   hipLaunchKernelGGL(bn_bwd_fold_reps_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, reps, nrep, C, sums, dgamma,
                      dbeta);
   const long nvec = M * C / 8;
   launch_bn_bwd_apply(dy, x, y, mean, invstd, beta, (int)relu_x, gamma, sums, dx, dres, nvec, C / 8, C,
-                      1.f / (float)M, st);
+                      1.f / (float)M, mask, st);
 }
 
 void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
                    const float* gamma, const float* beta, bool relu_x, uint16_t* dx, uint16_t* dres, float* dgamma,
-                   float* dbeta, float* work, float* sums, long M, int C, hipStream_t st) {
+                   float* dbeta, float* work, float* sums, long M, int C, hipStream_t st, const uint8_t* mask) {
   BnGeom g = bn_geom(C, M);
   long rpb = bn_rows_per_block(M, g);
   int nb = (int)((M + rpb - 1) / rpb);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, dy, x, y, mean, invstd,
-                     gamma, beta, (int)relu_x, M, C, g.tpr, g.rows_per_iter, rpb, work);
+  if (mask)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, dy, x, y, mean,
+                       invstd, gamma, beta, (int)relu_x, M, C, g.tpr, g.rows_per_iter, rpb, work, mask);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, dy, x, y, mean,
+                       invstd, gamma, beta, (int)relu_x, M, C, g.tpr, g.rows_per_iter, rpb, work, mask);
   hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, nb, C, sums, dgamma, dbeta);
   const long nvec = M * C / 8;
   launch_bn_bwd_apply(dy, x, y, mean, invstd, beta, (int)relu_x, gamma, sums, dx, dres, nvec, C / 8, C,
-                      1.f / (float)M, st);
+                      1.f / (float)M, mask, st);
 }
 
 }  // namespace k8s_amd

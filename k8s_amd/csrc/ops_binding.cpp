@@ -95,8 +95,19 @@ Tensor clip_factor(Tensor stats, double max_norm) {
 }
 
 // ------------------------------------------------------------------ batchnorm (NHWC)
+// want_mask: also return the packed ReLU mask (uint8 [M*C/8], bit j of byte e = y[8e+j] > 0) for the backward
+static Tensor relu_mask_for(const Tensor& x, bool want_mask) {
+  return want_mask ? torch::empty({x.numel() / 8}, x.options().dtype(at::kByte)) : Tensor();
+}
+
+static const uint8_t* cmask(const c10::optional<Tensor>& m) {
+  if (!m || !m->defined()) return nullptr;
+  TORCH_CHECK(m->is_cuda() && m->scalar_type() == at::kByte && m->is_contiguous(), "mask must be contiguous uint8");
+  return m->data_ptr<uint8_t>();
+}
+
 std::vector<Tensor> bn_fwd(Tensor x, c10::optional<Tensor> res, Tensor gamma, Tensor beta, Tensor run_mean,
-                           Tensor run_var, bool training, double momentum, double eps, bool relu) {
+                           Tensor run_var, bool training, double momentum, double eps, bool relu, bool want_mask) {
   check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x"); check_aligned(x, "x");
   const int C = (int)x.size(-1);
   TORCH_CHECK(C % 8 == 0, "channels must be a multiple of 8");
@@ -108,15 +119,18 @@ std::vector<Tensor> bn_fwd(Tensor x, c10::optional<Tensor> res, Tensor gamma, Te
   auto mean = torch::empty({C}, gamma.options());
   auto invstd = torch::empty({C}, gamma.options());
   Tensor work = training ? torch::empty({k8s_amd::bn_workspace_floats(M, C)}, gamma.options()) : mean;
+  Tensor mask = relu_mask_for(x, want_mask);
   k8s_amd::launch_bn_fwd(cbf(x), res ? cbf(*res) : nullptr, f32(gamma), f32(beta), bf(y), f32(mean), f32(invstd),
                          f32(run_mean), f32(run_var), f32(work), M, C, (float)eps, (float)momentum, training, relu,
-                         cur_stream());
+                         cur_stream(), want_mask ? mask.data_ptr<uint8_t>() : nullptr);
+  if (want_mask) return {y, mean, invstd, mask};
   return {y, mean, invstd};
 }
 
 // returns dx, dres (or empty), writes dgamma/dbeta into the given (flat-bucket view) tensors
 std::vector<Tensor> bn_fwd_from_sums(Tensor x, c10::optional<Tensor> res, Tensor gamma, Tensor beta, Tensor sums,
-                                     Tensor run_mean, Tensor run_var, double momentum, double eps, bool relu) {
+                                     Tensor run_mean, Tensor run_var, double momentum, double eps, bool relu,
+                                     bool want_mask) {
   check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x"); check_aligned(x, "x");
   const int C = (int)x.size(-1);
   TORCH_CHECK(C % 8 == 0, "channels must be a multiple of 8");
@@ -127,15 +141,17 @@ std::vector<Tensor> bn_fwd_from_sums(Tensor x, c10::optional<Tensor> res, Tensor
   auto y = torch::empty_like(x);
   auto mean = torch::empty({C}, gamma.options());
   auto invstd = torch::empty({C}, gamma.options());
+  Tensor mask = relu_mask_for(x, want_mask);
   k8s_amd::launch_bn_fwd_from_sums(cbf(x), res ? cbf(*res) : nullptr, f32(gamma), f32(beta), bf(y), f32(sums),
                                    nrep, f32(mean), f32(invstd), f32(run_mean), f32(run_var), M, C, (float)eps,
-                                   (float)momentum, relu, cur_stream());
+                                   (float)momentum, relu, cur_stream(), want_mask ? mask.data_ptr<uint8_t>() : nullptr);
+  if (want_mask) return {y, mean, invstd, mask};
   return {y, mean, invstd};
 }
 
 std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor mean, Tensor invstd, Tensor gamma,
                            Tensor beta, bool relu_x, Tensor dgamma, Tensor dbeta, bool want_dres,
-                           c10::optional<Tensor> reps) {
+                           c10::optional<Tensor> reps, c10::optional<Tensor> mask) {
   check_cuda(dy, "dy"); check_cuda(x, "x");
   check_dtype(dy, at::kBFloat16, "dy"); check_dtype(x, at::kBFloat16, "x");
   TORCH_CHECK(dy.sizes() == x.sizes());
@@ -149,6 +165,8 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor 
   auto work = torch::empty({k8s_amd::bn_workspace_floats(M, C)}, gamma.options());
   auto sums = torch::empty({2 * C}, gamma.options());
   TORCH_CHECK(!(relu_x && y), "relu mask from x and y are exclusive");
+  const uint8_t* mk = cmask(mask);
+  TORCH_CHECK(!mk || (!relu_x && mask->numel() == x.numel() / 8), "packed mask: M*C/8 bytes, exclusive with relu_x");
   if (reps) {  // (sum g*mask, sum g*mask*xhat) already accumulated by the epilogue that produced dy
     TORCH_CHECK(reps->is_cuda() && reps->scalar_type() == at::kFloat && reps->is_contiguous() &&
                     reps->numel() == (long)k8s_amd::kConvStatReplicas * 2 * C,
@@ -156,12 +174,12 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor 
     k8s_amd::launch_bn_bwd_from_sums(cbf(dy), cbf(x), y ? cbf(*y) : nullptr, f32(mean), f32(invstd), f32(gamma),
                                      f32(beta), relu_x, bf(dx), want_dres ? bf(dres) : nullptr, f32(dgamma),
                                      f32(dbeta), f32(*reps), k8s_amd::kConvStatReplicas, f32(sums), M, C,
-                                     cur_stream());
+                                     cur_stream(), mk);
     return {dx, dres};
   }
   k8s_amd::launch_bn_bwd(cbf(dy), cbf(x), y ? cbf(*y) : nullptr, f32(mean), f32(invstd), f32(gamma), f32(beta),
                          relu_x, bf(dx), want_dres ? bf(dres) : nullptr, f32(dgamma), f32(dbeta), f32(work), f32(sums), M, C,
-                         cur_stream());
+                         cur_stream(), mk);
   return {dx, dres};
 }
 
@@ -548,11 +566,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("scale"), py::arg("scale_t"), py::arg("step"), py::arg("decoupled"), py::arg("hyper") = py::none());
   m.def("grad_sumsq", &grad_sumsq);
   m.def("clip_factor", &clip_factor);
-  m.def("bn_fwd", &bn_fwd);
+  m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("run_mean"),
+        py::arg("run_var"), py::arg("training"), py::arg("momentum"), py::arg("eps"), py::arg("relu"),
+        py::arg("want_mask") = false);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("mean"), py::arg("invstd"),
         py::arg("gamma"), py::arg("beta"), py::arg("relu_x"), py::arg("dgamma"), py::arg("dbeta"), py::arg("want_dres"),
-        py::arg("reps") = py::none());
-  m.def("bn_fwd_from_sums", &bn_fwd_from_sums);
+        py::arg("reps") = py::none(), py::arg("mask") = py::none());
+  m.def("bn_fwd_from_sums", &bn_fwd_from_sums, py::arg("x"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
+        py::arg("sums"), py::arg("run_mean"), py::arg("run_var"), py::arg("momentum"), py::arg("eps"),
+        py::arg("relu"), py::arg("want_mask") = false);
   m.def("norm_fwd", &norm_fwd);
   m.def("norm_bwd", &norm_bwd);
   m.def("xent_fwd", &xent_fwd);

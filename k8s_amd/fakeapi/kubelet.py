@@ -76,6 +76,7 @@ class LocalKubelet:
         self.running: Dict[str, _Container] = {}  # pod name -> container
         self.pod_meta: Dict[str, dict] = {}  # pod name -> {"job":..., "ns":..., "restarts":..}
         self.service_ports: Dict[str, int] = {}
+        self._published: Dict[str, str] = {}
         self.failures: Dict[str, int] = {}  # job -> failed pods
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._loop, daemon=True)
@@ -160,6 +161,24 @@ class LocalKubelet:
                 a.close()
         raise RuntimeError("no free port pair for a Service")
 
+    def _service_map_file(self, ns) -> str:
+        return os.path.join(self.log_dir, "service-map-%s.json" % ns)
+
+    def _publish_service_map(self, ns) -> Dict[str, str]:
+        """Cluster DNS stand-in that stays current: the map is rewritten (atomically) on every sync, and pods
+        resolve through the file, so a pod started before a peer's Service existed still finds the peer
+        (the operator creates a replica's Job before the next replica's Service)."""
+        m = self._service_map(ns)
+        path = self._service_map_file(ns)
+        data = json.dumps(m, sort_keys=True)
+        if self._published.get(ns) != data:
+            tmp = path + ".tmp"
+            with open(tmp, "w") as f:
+                f.write(data)
+            os.replace(tmp, path)
+            self._published[ns] = data
+        return m
+
     def _service_map(self, ns) -> Dict[str, str]:
         out = {}
         for s in self.api.get(self._path(ns, "services")).get("items", []):
@@ -237,6 +256,7 @@ class LocalKubelet:
                 for ns in self._namespaces():
                     self._sync_jobs(ns)
                     self._sync_deployments(ns)
+                    self._publish_service_map(ns)
                 self._reap()
             except Exception as e:  # keep the node alive; log for the tests
                 import traceback
@@ -316,7 +336,8 @@ class LocalKubelet:
         for e in c.get("env") or []:
             if "value" in e:
                 env[e["name"]] = str(e["value"])
-        env["K8S_AMD_SERVICE_MAP"] = json.dumps(self._service_map(ns))
+        env["K8S_AMD_SERVICE_MAP"] = json.dumps(self._publish_service_map(ns))
+        env["K8S_AMD_SERVICE_MAP_FILE"] = self._service_map_file(ns)
         env["POD_NAME"], env["POD_NAMESPACE"] = pod_name, ns
         if gpus:
             env["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in gpus)

@@ -134,30 +134,37 @@ class _BnAct(torch.autograd.Function):
         x = x.contiguous()
         if res is not None:
             res = res.contiguous()
+        # residual + ReLU on the GPU: the forward also writes the packed ReLU mask (1 bit per element) that the
+        # backward's reduce and apply passes read instead of the bf16 output (saves ~2 B/elem per pass)
+        want_mask = relu and res is not None and _gpu(x)
+        mask = None
         if _gpu(x) and sums is not None and training:
-            y, mean, invstd = _C().bn_fwd_from_sums(x, res, pg.master, pb.master, sums, run_mean, run_var, momentum,
-                                                    eps, relu)
+            out = _C().bn_fwd_from_sums(x, res, pg.master, pb.master, sums, run_mean, run_var, momentum, eps, relu,
+                                        want_mask)
         elif _gpu(x):
-            y, mean, invstd = _C().bn_fwd(x, res, pg.master, pb.master, run_mean, run_var, training, momentum, eps,
-                                          relu)
+            out = _C().bn_fwd(x, res, pg.master, pb.master, run_mean, run_var, training, momentum, eps, relu,
+                              want_mask)
         else:
-            y, mean, invstd = ref.bn_fwd(x, res, pg.master, pb.master, run_mean, run_var, training, momentum, eps,
-                                         relu)
+            out = ref.bn_fwd(x, res, pg.master, pb.master, run_mean, run_var, training, momentum, eps, relu)
+        y, mean, invstd = out[0], out[1], out[2]
+        if want_mask:
+            mask = out[3]
         # without a residual the ReLU mask is recomputed from x in the backward kernels (no need to keep y)
-        keep_y = relu and (res is not None or not _gpu(x))
-        ctx.save_for_backward(x, y if keep_y else None, mean, invstd)
+        keep_y = relu and (res is not None or not _gpu(x)) and mask is None
+        ctx.save_for_backward(x, y if keep_y else None, mean, invstd, mask)
         ctx.pg, ctx.pb, ctx.has_res, ctx.res_link = pg, pb, res is not None, res_link
-        ctx.relu_x = relu and not keep_y
+        ctx.relu_x = relu and not keep_y and mask is None
         ctx.bwd_link = None
         if bwd_link is not None and _gpu(x) and training:
-            bwd_link.x, bwd_link.y, bwd_link.mean, bwd_link.invstd = x, (y if keep_y else None), mean, invstd
+            bwd_link.x, bwd_link.y, bwd_link.mean, bwd_link.invstd = x, (y if relu and res is not None else None), \
+                mean, invstd
             bwd_link.gamma, bwd_link.beta, bwd_link.relu_x = pg.master, pb.master, ctx.relu_x
             ctx.bwd_link = bwd_link
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, mean, invstd = ctx.saved_tensors
+        x, y, mean, invstd, mask = ctx.saved_tensors
         pg, pb = ctx.pg, ctx.pb
         store = pg.store
         dy = dy.contiguous()
@@ -170,7 +177,7 @@ class _BnAct(torch.autograd.Function):
                 reps, ctx.bwd_link.reps = ctx.bwd_link.reps, None
                 ctx.bwd_link.x = ctx.bwd_link.y = None  # drop the extra references to the saved activations
             dx, dres = _C().bn_bwd(dy, x, y, mean, invstd, pg.master, pb.master, ctx.relu_x, dg, db, ctx.has_res,
-                                   reps)
+                                   reps, mask)
             if sg is not None:
                 store.mark_written(pg)
             else:

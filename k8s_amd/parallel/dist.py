@@ -40,10 +40,11 @@ class RankInfo:
 
 def resolve(addr: str) -> str:
     """Map a TF_CONFIG "service:port" through $K8S_AMD_SERVICE_MAP (local kubelet's cluster-DNS stand-in)."""
-    m = os.environ.get("K8S_AMD_SERVICE_MAP")
-    if not m:
+    from k8s_amd.ps_server.grpc_tensorflow_server import _service_table
+
+    table = _service_table()
+    if not table:
         return addr
-    table = json.loads(m)
     if addr in table:
         return table[addr]
     host = addr.rsplit(":", 1)[0]

@@ -64,10 +64,23 @@ def parse_cluster_spec(cluster_spec: str, job_name: str = "", task_id: int = 0):
     return cluster
 
 
-def resolve(addr: str) -> str:
+def _service_table():
+    """The local kubelet's service map: the live file ($K8S_AMD_SERVICE_MAP_FILE, kept current by the kubelet)
+    when readable, else the snapshot in $K8S_AMD_SERVICE_MAP taken at container start."""
+    f = os.environ.get("K8S_AMD_SERVICE_MAP_FILE")
+    if f:
+        try:
+            with open(f) as fh:
+                return json.load(fh)
+        except (OSError, ValueError):
+            pass
     m = os.environ.get("K8S_AMD_SERVICE_MAP")
-    if m:
-        t = json.loads(m)
+    return json.loads(m) if m else None
+
+
+def resolve(addr: str) -> str:
+    t = _service_table()
+    if t:
         return t.get(addr) or t.get(addr.rsplit(":", 1)[0]) or addr
     return addr
 

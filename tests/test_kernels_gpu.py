@@ -170,3 +170,34 @@ def test_grad_clip(cuda):
     g[5] = float("nan")
     st = _C().grad_sumsq(g)
     assert _C().clip_factor(st, 1.0).item() == 0.0
+
+
+@pytest.mark.parametrize("C,M", [(64, 4096), (256, 1000), (2048, 98), (24, 333)])
+@pytest.mark.parametrize("from_sums", [False, True])
+def test_bn_packed_relu_mask(cuda, C, M, from_sums):
+    """Residual BN + ReLU: the forward's packed mask (bit j of byte e = y[8e+j] > 0) gives the backward the same
+    dx / dres / dgamma / dbeta as reading the bf16 output y."""
+    torch.manual_seed(1)
+    x = (torch.randn(M, C, device=cuda) * 2).bfloat16()
+    r = torch.randn(M, C, device=cuda).bfloat16()
+    g = torch.rand(C, device=cuda) + 0.5
+    b = torch.randn(C, device=cuda)
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    if from_sums:
+        xf = x.float()
+        sums = torch.zeros(_C().conv_stat_replicas, 2, C, device=cuda)
+        sums[0, 0], sums[0, 1] = xf.sum(0), (xf * xf).sum(0)
+        y, mean, invstd, mask = _C().bn_fwd_from_sums(x, r, g, b, sums, rm, rv, 0.1, 1e-5, True, True)
+    else:
+        y, mean, invstd, mask = _C().bn_fwd(x, r, g, b, rm, rv, True, 0.1, 1e-5, True, True)
+    assert mask.dtype == torch.uint8 and mask.numel() == M * C // 8
+    bits = ((mask.long().unsqueeze(-1) >> torch.arange(8, device=cuda)) & 1).reshape(M, C).bool()
+    assert torch.equal(bits, y.float() > 0)
+    dy = torch.randn(M, C, device=cuda).bfloat16()
+    dg1, db1, dg2, db2 = (torch.empty(C, device=cuda) for _ in range(4))
+    dx1, dres1 = _C().bn_bwd(dy, x, y, mean, invstd, g, b, False, dg1, db1, True)
+    dx2, dres2 = _C().bn_bwd(dy, x, None, mean, invstd, g, b, False, dg2, db2, True, None, mask)
+    assert torch.equal(dres1, dres2)
+    _close(dx2, dx1, 1e-2)
+    _close(dg2, dg1, 1e-4)
+    _close(db2, db1, 1e-4)

@@ -123,3 +123,21 @@ def test_two_rank_allreduce_and_sharded_ps_agree(tmp_path):
     for k in a:
         if k.startswith("params/") or k.startswith("optim/"):
             torch.testing.assert_close(a[k], b[k], rtol=1e-4, atol=1e-5, msg=k)
+
+
+def test_service_resolution_follows_the_live_map_file(tmp_path, monkeypatch):
+    """A pod started before a peer's Service existed must still resolve it: the local kubelet keeps
+    $K8S_AMD_SERVICE_MAP_FILE current and resolvers read it on every lookup (the env snapshot is a fallback)."""
+    import json
+
+    from k8s_amd.parallel import dist
+    from k8s_amd.ps_server import grpc_tensorflow_server as srv
+
+    f = tmp_path / "service-map-default.json"
+    monkeypatch.setenv("K8S_AMD_SERVICE_MAP", json.dumps({"a-master-x-0": "127.0.0.1:1000"}))
+    monkeypatch.setenv("K8S_AMD_SERVICE_MAP_FILE", str(f))
+    assert srv.resolve("a-ps-x-0:2222") == "a-ps-x-0:2222"  # no file yet: snapshot only
+    assert dist.resolve("a-master-x-0:2222") == "127.0.0.1:1000"
+    f.write_text(json.dumps({"a-master-x-0": "127.0.0.1:1000", "a-ps-x-0": "127.0.0.1:1002"}))
+    assert srv.resolve("a-ps-x-0:2222") == "127.0.0.1:1002"
+    assert dist.resolve("a-ps-x-0:2222") == "127.0.0.1:1002"
