@@ -85,8 +85,10 @@ def main(argv=None):
         opt.step(grad_scale=reducer.grad_scale)
         return loss
 
-    for _ in range(a.warmup):
+    for i in range(a.warmup):
         loss = step()
+        if info.rank == 0:  # progress on stderr (the first step may autotune unseen shapes for minutes)
+            print("warmup step %d/%d issued" % (i + 1, a.warmup), file=sys.stderr, flush=True)
     sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
     sync()
     kdist.barrier()

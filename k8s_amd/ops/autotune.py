@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import json
 import os
+import sys
 import threading
 from typing import Callable, Dict, Sequence, Tuple
 
@@ -143,6 +144,9 @@ def choose(key: str, candidates: Sequence[Tuple[str, Callable[[], object]]]) -> 
             with _lock:
                 _cache[key] = name
                 _save_cache()
+            if os.environ.get("K8S_AMD_AUTOTUNE_VERBOSE", "0") != "0":  # progress for long cold-start tuning
+                print("autotune %s -> %s %s" % (key, name, {n: round(t, 4) for n, t in times.items()}),
+                      file=sys.stderr, flush=True)
     st = STATS.setdefault(key.split("|")[0], {})
     st[name] = st.get(name, 0) + 1
     return name
