@@ -1,0 +1,388 @@
+// K1 large-tile GEMM for gfx950: 256 x 256 output tile, 8 waves, LDS-ring pipelined K loop.
+//
+//   C[M,N] (+)= alpha * op(A) . op(B) (+ bias, ReLU / GELU epilogue)   bf16 in, fp32 accumulate
+//
+// The hot path of the transformer linear layers (BERT / Llama-3-8B fwd, dgrad and wgrad) when the output has
+// enough 256 x 256 tiles to fill the chip (gemm256_eligible); the 128 x 128 kernel of gemm.hip (2 blocks/CU)
+// takes the rest and the convolutions.
+//
+// Design (cdna_hip_programming.md §5, MI355X_MICROARCH "Two waves per SIMD"):
+//  * 512 threads = 8 waves as 2 (M) x 4 (N); each wave owns a 128 x 64 piece = 8 x 4 tiles of
+//    v_mfma_f32_16x16x32_bf16 (128 accumulator VGPRs), ~200 VGPRs -> 2 waves per SIMD, 1 workgroup per CU.
+//  * K is streamed in 32-deep stages (A 256 x 32 + B 256 x 32 = 32 KB) through a 5-slot LDS ring (160 KB) by
+//    global_load_lds (16 B per lane, no VGPR round trip); each stage is issued THREE phases ahead of its use and
+//    the counted `s_waitcnt vmcnt(8)` never drains the ring inside the loop. (A first design staged whole
+//    64-deep K tiles in 2 buffers; with its operand DMA removed it ran 1.72 PF/s at 8192^3 against 1.24 with
+//    it: slabs issued one phase before use stalled it. See profiles/r02_gemm256.md.)
+//  * Half-phase stagger: waves 4-7 (the partner of wave w on its SIMD is w + 4) run one barrier behind waves
+//    0-3, so on every SIMD one wave's MFMA cluster overlaps its partner's LDS reads and DMA issue.
+//  * LDS images are lane-linear (global_load_lds writes base + lane*16): bank-conflict swizzles are applied to
+//    the per-lane SOURCE address and the same XOR on the read (rule 21). MN-major operands (dgrad's weight,
+//    both wgrad operands) are read in place with ds_read_b64_tr_b16: no transposes anywhere.
+//  * Operands swapped in the MFMA (B fragment as the instruction's A) so each lane holds 4 consecutive output
+//    columns; a plain bf16 output is staged through LDS and written as whole 16-B row segments.
+//  * XCD-aware bijective block remap + grouped (8 M-tiles) order: tiles sharing an A row panel / B column panel
+//    run on one XCD's L2.
+#include <cstdlib>
+#include <stdexcept>
+#include <type_traits>
+
+#include "common.h"
+#include "launchers.h"
+#include "mfma.h"
+
+namespace k8s_amd {
+
+namespace g256 {
+
+constexpr int THREADS = 512;
+
+__device__ __forceinline__ int mn128_swz(int r) { return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)); }
+
+struct Epi {
+  void* c;
+  long ldc;
+  const float* bias;  // [N] fp32 or null
+  uint16_t* pre;      // bf16 pre-activation copy (GELU backward) or null
+  int out_f32;
+  int act;            // 0 none, 1 relu, 2 gelu(tanh)
+  int accumulate;     // C += result
+  float alpha;
+};
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+__device__ __forceinline__ void barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// ---- epilogue shared by both 256 x 256 kernels: wave (wr, wc) holds acc[a][j] = C[m][n..n+3] with
+// m = m0 + wr*128 + a*16 + (lane & 15), n = n0 + wc*64 + j*16 + 4*(lane >> 4).
+__device__ __forceinline__ void epilogue256(const f32x4_t (&acc)[8][4], const Epi& E, char* smem, int M, int N,
+                                            int m0, int n0, int wid, int wr, int wc, int lane) {
+  const float alpha = E.alpha;
+  if (!E.out_f32 && !E.pre && !E.accumulate) {
+    // bf16 tile through LDS: each wave stages its 128 x 64 piece (16 KB) and stores whole 128-B row segments.
+    barrier();  // every wave is past its last LDS read of the K loop
+    uint16_t* st = reinterpret_cast<uint16_t*>(smem) + wid * (128 * 64);  // [128 rows][64 cols], row 128 B
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      const int lr = a * 16 + (lane & 15);  // wave-local row (ph*32 + i*16 == a*16)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int lc = j * 16 + 4 * (lane >> 4);
+        const int n = n0 + wc * 64 + lc;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[a][j][r] * alpha;
+          if (E.bias) v[r] += (n + r < N) ? E.bias[n + r] : 0.f;
+          if (E.act == 1) v[r] = fmaxf(v[r], 0.f);
+          else if (E.act == 2) v[r] = gelu_tanh(v[r]);
+        }
+        bf16x4_t o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r]);
+        // 16-B chunk (lc / 8) of row lr, XOR-swizzled by the row to spread the banks
+        const int ch = (lc >> 3) ^ (lr & 7);
+        *reinterpret_cast<bf16x4_t*>(reinterpret_cast<char*>(st) + lr * 128 + ch * 16 + (lc & 4) * 2) = o;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's staging writes landed (wave-private region)
+    asm volatile("" ::: "memory");
+    // 128 rows x 8 chunks of 16 B = 1024 chunks, 16 per lane
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int idx = it * 64 + lane;
+      const int lr = idx >> 3, ch = idx & 7;
+      const int m = m0 + wr * 128 + lr;
+      const int n = n0 + wc * 64 + ch * 8;
+      const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const char*>(st) + lr * 128 +
+                                                            ((ch ^ (lr & 7)) << 4));
+      if (m < M && n < N) {
+        uint16_t* cp = reinterpret_cast<uint16_t*>(E.c) + (long)m * E.ldc + n;
+        if (n + 8 <= N && (E.ldc & 7) == 0) {
+          *reinterpret_cast<bf16x8_t*>(cp) = v;
+        } else {
+          for (int r = 0; r < 8 && n + r < N; ++r) cp[r] = (uint16_t)v[r];
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int a = 0; a < 8; ++a) {
+    const int m = m0 + wr * 128 + a * 16 + (lane & 15);
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wc * 64 + j * 16 + 4 * (lane >> 4);
+      if (n >= N) continue;
+      const bool full = n + 3 < N;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = acc[a][j][r] * alpha;
+        if (E.bias) v[r] += (n + r < N) ? E.bias[n + r] : 0.f;
+      }
+      if (E.pre) {
+        uint16_t* pp = E.pre + (long)m * E.ldc + n;
+        if (full) {
+          bf16x4_t o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r]);
+          *reinterpret_cast<bf16x4_t*>(pp) = o;
+        } else {
+          for (int r = 0; r < 4 && n + r < N; ++r) pp[r] = f2bf(v[r]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (E.act == 1) v[r] = fmaxf(v[r], 0.f);
+        else if (E.act == 2) v[r] = gelu_tanh(v[r]);
+      }
+      if (E.out_f32) {
+        float* cp = reinterpret_cast<float*>(E.c) + (long)m * E.ldc + n;
+        if (full) {
+          float4 o = make_float4(v[0], v[1], v[2], v[3]);
+          if (E.accumulate) {
+            const float4 old = *reinterpret_cast<const float4*>(cp);
+            o.x += old.x; o.y += old.y; o.z += old.z; o.w += old.w;
+          }
+          *reinterpret_cast<float4*>(cp) = o;
+        } else {
+          for (int r = 0; r < 4 && n + r < N; ++r) cp[r] = (E.accumulate ? cp[r] : 0.f) + v[r];
+        }
+      } else {
+        uint16_t* cp = reinterpret_cast<uint16_t*>(E.c) + (long)m * E.ldc + n;
+        if (full) {
+          bf16x4_t o;
+          if (E.accumulate) {
+            const bf16x4_t old = *reinterpret_cast<const bf16x4_t*>(cp);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += bf2f((uint16_t)old[r]);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r]);
+          *reinterpret_cast<bf16x4_t*>(cp) = o;
+        } else {
+          for (int r = 0; r < 4 && n + r < N; ++r) cp[r] = f2bf(v[r] + (E.accumulate ? bf2f(cp[r]) : 0.f));
+        }
+      }
+    }
+  }
+}
+
+}  // namespace g256
+
+// ============================================================================ the kernel
+//   phase h: ds_read this wave's 8 A + 4 B fragments of stage h; issue stage h+3 into slot (h+3) % 5 (4 x 16 B
+//   per thread); vmcnt(8) = stage h+1 landed (two younger stages stay in flight); barrier; 32 MFMAs; barrier.
+//   RAW: stage h+1 is waited in phase h and read in phase h+1 (the barrier between makes every wave's DMA share
+//   visible). WAR: slot (h+3) % 5 last held stage h-2, whose reads finished >= 2 phases earlier (safe under the
+//   half-phase stagger, where one group runs one barrier behind the other).
+// Images (lane-linear DMA, swizzles on the source address and the read):
+//   K-major  [256 rows][32 k], 64-B rows: chunk c of row r at c ^ ((r >> 3) & 1) * 2 -> conflict-free b128 reads
+//   MN-major 4 sub-images [32 k][64 mn], 128-B rows: 16-B unit u of k-row r at u ^ h(r),
+//            h(r) = 2 * (((r >> 1) & 1) | ((r >> 3) & 1) << 1)        -> conflict-free ds_read_b64_tr_b16
+namespace g256r {
+constexpr int KS = 32;
+constexpr int STAGE_A = 256 * KS * 2;  // 16 KB
+constexpr int STAGE = 2 * STAGE_A;     // 32 KB
+constexpr int NSLOT = 5;
+constexpr int LDS_BYTES = NSLOT * STAGE;  // 160 KB
+
+__device__ __forceinline__ int km_swz(int r) { return ((r >> 3) & 1) << 1; }
+
+struct KMaj {
+  const uint16_t* p;
+  long ld;
+  int rows;
+  static constexpr bool kmajor = true;
+  // glds j (0, 1) of thread tid: 16 B of row s >> 2, chunk (s & 3) ^ swz, s = j * 512 + tid
+  __device__ __forceinline__ const uint16_t* cursor(int tid, int j, int o0) const {
+    const int sl = j * 512 + tid, row = sl >> 2, c = (sl & 3) ^ km_swz(row);
+    int r = o0 + row;
+    r = r < rows ? r : rows - 1;
+    return p + (long)r * ld + c * 8;
+  }
+  __device__ __forceinline__ long step() const { return KS; }
+  __device__ __forceinline__ static mfma_bf16x8 frag(const char* img, int rb, int lane) {
+    const int row = rb + (lane & 15), c = lane >> 4;
+    const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(img + row * 64 + ((c ^ km_swz(row)) << 4));
+    return __builtin_bit_cast(mfma_bf16x8, v);
+  }
+};
+
+struct MNMaj {
+  const uint16_t* p;
+  long ld;
+  int cols;
+  static constexpr bool kmajor = false;
+  // glds j of thread tid fills sub-image 2j + (tid >> 8): k-row s >> 3, 16-B unit (s & 7) ^ h(k-row), s = tid & 255
+  __device__ __forceinline__ const uint16_t* cursor(int tid, int j, int o0) const {
+    const int sub = 2 * j + (tid >> 8), sl = tid & 255, kr = sl >> 3;
+    const int lc = ((sl & 7) ^ g256::mn128_swz(kr)) * 8;
+    int c = o0 + sub * 64 + lc;
+    c = c < cols ? c : cols - 8;
+    return p + (long)kr * ld + c;
+  }
+  __device__ __forceinline__ long step() const { return (long)KS * ld; }
+  __device__ __forceinline__ static mfma_bf16x8 frag(const char* img, int rb, int lane) {
+    const char* sub = img + (rb >> 6) * 4096;
+    const int cb = rb & 63;
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+    const int u = (cb >> 3) + (pp >> 1);
+    const int r0 = 8 * g + q, r1 = r0 + 4;
+    const char* a0 = sub + r0 * 128 + ((u ^ g256::mn128_swz(r0)) << 4) + (pp & 1) * 8;
+    const char* a1 = sub + r1 * 128 + ((u ^ g256::mn128_swz(r1)) << 4) + (pp & 1) * 8;
+    return join8(tr16(a0), tr16(a1));
+  }
+};
+
+template <class AS, class BS, int DIAG = 0>
+__global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, g256::Epi E, int M, int N, int K) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+
+  const int tiles_m = (M + 255) >> 8, tiles_n = (N + 255) >> 8;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  int wg;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int group = 8 * tiles_n;
+  const int first_m = (wg / group) * 8;
+  const int gm = min(tiles_m - first_m, 8);
+  const int tm = first_m + (wg % group) % gm;
+  const int tn = (wg % group) / gm;
+  const int m0 = tm * 256, n0 = tn * 256;
+
+  const uint16_t* ca0 = A.cursor(tid, 0, m0);
+  const uint16_t* ca1 = A.cursor(tid, 1, m0);
+  const uint16_t* cb0 = B.cursor(tid, 0, n0);
+  const uint16_t* cb1 = B.cursor(tid, 1, n0);
+  const long sa = A.step(), sb = B.step();
+  const int dma_off = wid * 1024;
+  auto issue = [&](int slot) {
+    char* d = smem + slot * STAGE + dma_off;
+    glds16(ca0, d);
+    glds16(ca1, d + 8192);
+    glds16(cb0, d + STAGE_A);
+    glds16(cb1, d + STAGE_A + 8192);
+    ca0 += sa; ca1 += sa; cb0 += sb; cb1 += sb;
+  };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / KS;
+  issue(0);
+  if (nk > 1) issue(1);
+  if (nk > 2) issue(2);
+  if (nk > 2) vmwait<8>();
+  else if (nk > 1) vmwait<4>();
+  else vmwait<0>();
+  barrier();
+  const bool lag = wr == 1;  // half-phase stagger (header)
+  if (lag) barrier();
+
+  int slot = 0, islot = 3;  // slot of stage h, slot for stage h + 3
+  for (int h = 0; h < nk; ++h) {
+    const char* st = smem + slot * STAGE;
+    mfma_bf16x8 afr[8], bfr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = BS::frag(st + STAGE_A, wc * 64 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) afr[i] = AS::frag(st, wr * 128 + i * 16, lane);
+    if constexpr (DIAG == 0) {
+      if (h + 3 < nk) {
+        issue(islot);
+        vmwait<8>();
+      } else if (h + 2 < nk) {
+        vmwait<4>();
+      } else {
+        vmwait<0>();
+      }
+    }
+    barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], afr[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+    slot = slot == NSLOT - 1 ? 0 : slot + 1;
+    islot = islot == NSLOT - 1 ? 0 : islot + 1;
+  }
+  if (!lag) barrier();
+  epilogue256(acc, E, smem, M, N, m0, n0, wid, wr, wc, lane);
+}
+}  // namespace g256r
+
+namespace g256 {
+template <class AS, class BS>
+static void launch_ring(const AS& a, const BS& b, const Epi& e, int M, int N, int K, hipStream_t st) {
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  const char* dg = getenv("K8S_AMD_GEMM256_DIAG");
+  if (dg && atoi(dg) == 1)
+    hipLaunchKernelGGL((g256r::gemm256r_kernel<AS, BS, 1>), dim3(tiles), dim3(THREADS), 0, st, a, b, e, M, N, K);
+  else
+    hipLaunchKernelGGL((g256r::gemm256r_kernel<AS, BS>), dim3(tiles), dim3(THREADS), 0, st, a, b, e, M, N, K);
+}
+
+}  // namespace g256
+
+// Shape gate for the 256 x 256 kernel: K a multiple of 64, MN-major extents multiples of 8, and a wave-
+// quantisation cost model against the 128 x 128 kernel of gemm.hip (2 blocks/CU). Per output element the 256
+// kernel runs ~1.25x the 128 kernel's rate (measured, scripts/bench_gemm256.py), but with one 256-tile per CU
+// a 1.5-wave grid (e.g. 384 tiles) idles a third of the chip in its last round:
+//   t256 ~ ceil(T256 / 256) * 256^2 / 1.25     t128 ~ ceil(T128 / 512) * 2 * 128^2
+bool gemm256_eligible(int M, int N, int K, bool a_kmajor, bool b_kmajor) {
+  if (K % 64 != 0 || K < 64) return false;
+  if (!a_kmajor && M % 8 != 0) return false;
+  if (!b_kmajor && N % 8 != 0) return false;
+  if (N % 4 != 0) return false;
+  const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
+  const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+  const double c256 = (double)((t256 + 255) / 256) * 65536.0 / 1.25;
+  const double c128 = (double)((t128 + 511) / 512) * 32768.0;
+  return c256 <= c128;
+}
+
+void launch_gemm256(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
+                    long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre,
+                    bool accumulate, float alpha, hipStream_t st) {
+  if (K % 64 != 0) throw std::runtime_error("gemm256: K must be a multiple of 64");
+  g256::Epi e{C, ldc, bias, pre, c_f32 ? 1 : 0, act, accumulate ? 1 : 0, alpha};
+  using namespace g256r;
+  if (a_kmajor && b_kmajor)
+    g256::launch_ring(KMaj{A, lda, M}, KMaj{B, ldb, N}, e, M, N, K, st);
+  else if (a_kmajor && !b_kmajor)
+    g256::launch_ring(KMaj{A, lda, M}, MNMaj{B, ldb, N}, e, M, N, K, st);
+  else if (!a_kmajor && b_kmajor)
+    g256::launch_ring(MNMaj{A, lda, M}, KMaj{B, ldb, N}, e, M, N, K, st);
+  else
+    g256::launch_ring(MNMaj{A, lda, M}, MNMaj{B, ldb, N}, e, M, N, K, st);
+}
+
+}  // namespace k8s_amd

@@ -67,6 +67,11 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
                  long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
                  float alpha, int splits, float* ws, hipStream_t st, const BnBwdEpi* bnb = nullptr);
 long gemm_splitk_workspace(int M, int N, int splits);  // fp32 elements of the split-K slab workspace
+// gemm256.hip: 256 x 256-tile, 8-wave phased MFMA GEMM for the large (transformer) products
+bool gemm256_eligible(int M, int N, int K, bool a_kmajor, bool b_kmajor);
+void launch_gemm256(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
+                    long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre,
+                    bool accumulate, float alpha, hipStream_t st);
 // Output written to the (a, b) parity sub-grid of an H x W image: GEMM row (n, i, j) -> (n, i*stride+a,
 // j*stride+b). Used for stride-s data gradients decomposed by output parity (ops/conv.py _dgrad_strided_hip).
 struct SubGrid {

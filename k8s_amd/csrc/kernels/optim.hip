@@ -50,6 +50,9 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* 
                                                   long n4, const uint8_t* __restrict__ decay_mask, float lr, float mu, float wd,
                                                   float scale, const float* __restrict__ scale_ptr,
                                                   const float* __restrict__ hyper, int nesterov, int first_step) {
+  // a zero device factor = non-finite gradients (clip_factor_kernel): skip the step, leave every buffer
+  // bit-identical (NaN * 0 is NaN, so scaling by 0 would poison the momentum / moments / weights)
+  if (scale_ptr && *scale_ptr == 0.f) return;
   const float s = scale * (scale_ptr ? *scale_ptr : 1.f);
   if (hyper) lr = hyper[0];
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n4; q += (long)gridDim.x * blockDim.x) {
@@ -82,6 +85,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
                                                    float scale, const float* __restrict__ scale_ptr,
                                                    const float* __restrict__ hyper, float bc1, float bc2,
                                                    int decoupled) {
+  if (scale_ptr && *scale_ptr == 0.f) return;  // non-finite gradients: skipped step (see sgd_kernel)
   const float s = scale * (scale_ptr ? *scale_ptr : 1.f);
   if (hyper) {
     lr = hyper[0];
@@ -143,8 +147,8 @@ __global__ void __launch_bounds__(256) sumsq_kernel(const GT* __restrict__ g, lo
   }
 }
 
-// clip factor = min(1, max_norm / (sqrt(sumsq) + 1e-6)); 0 if non-finite grads (skip step semantics
-// are the caller's: a zero factor makes the update a pure decay step).
+// clip factor = min(1, max_norm / (sqrt(sumsq) + 1e-6)); 0 if non-finite grads: the update kernels then skip
+// the step entirely (no decay, no state change), like a loss-scaler's overflow skip.
 __global__ void clip_factor_kernel(const float* __restrict__ stats, float max_norm, float* __restrict__ factor) {
   float norm = sqrtf(stats[0]);
   float f = max_norm / (norm + 1e-6f);

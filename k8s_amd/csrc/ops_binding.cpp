@@ -4,6 +4,8 @@
 // before launching, so a mis-shaped call raises a Python exception instead of
 // faulting the GPU. Kernels are launched on PyTorch's current HIP stream so
 // they compose with torch ops, streams and hipGraph capture.
+#include <cstdlib>
+
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
@@ -284,6 +286,12 @@ BnbHolder parse_bnb(const c10::optional<std::vector<Tensor>>& t, c10::optional<b
   return h;
 }
 
+// K8S_AMD_GEMM256=0 routes every product to the 128 x 128 kernel (A/B comparisons, debugging)
+static bool gemm256_enabled() {
+  const char* e = std::getenv("K8S_AMD_GEMM256");  // per call: one process can A/B both kernels
+  return !(e && e[0] == '0');
+}
+
 Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tensor> out, bool out_f32,
             c10::optional<Tensor> bias, int64_t act, c10::optional<Tensor> pre, bool accumulate, double alpha,
             int64_t splits, c10::optional<std::vector<Tensor>> bnb, c10::optional<bool> bnb_relu_x) {
@@ -307,6 +315,12 @@ Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tens
   if (bias) TORCH_CHECK(bias->numel() == N && bias->scalar_type() == at::kFloat && bias->is_contiguous());
   if (pre) TORCH_CHECK(pre->numel() == M * N && pre->scalar_type() == at::kBFloat16 && pre->is_contiguous());
   const int mode = accumulate ? 1 : 0;
+  if (!bnb && gemm256_enabled() && k8s_amd::gemm256_eligible((int)M, (int)N, (int)K, a_kmajor, b_kmajor)) {
+    k8s_amd::launch_gemm256(cbf(a), a.stride(0), a_kmajor, cbf(b), b.stride(0), b_kmajor, c.data_ptr(), N, out_f32,
+                            (int)M, (int)N, (int)K, bias ? bias->data_ptr<float>() : nullptr, (int)act,
+                            pre ? bf(*pre) : nullptr, accumulate, (float)alpha, cur_stream());
+    return c;
+  }
   int sp = (int)splits;
   if (sp != 1 && out_f32 && !bias && act == 0 && !pre && N % 4 == 0) {
     if (sp <= 0) sp = k8s_amd::gemm_choose_splits((int)M, (int)N, (int)K);

@@ -136,30 +136,21 @@ class LocalKubelet:
 
     # ------------------------------------------------------------------ services / volumes / env
     def _service_port(self) -> int:
-        """A free 127.0.0.1 port P whose P+1 is free too and not handed out: workloads rendezvous on the
-        master service's port + 1 (parallel/dist.py), which must not land on another Service's port."""
+        """A free 127.0.0.1 port not handed out to another Service (the Service's ``tfPort`` stand-in; the
+        trainer's rendezvous listens on the master Service's own port, parallel/dist.py)."""
         import socket
 
         taken = set(self.service_ports.values())
-        taken |= {p + 1 for p in taken}
         for _ in range(64):
             a = socket.socket()
             try:
                 a.bind(("127.0.0.1", 0))
                 port = a.getsockname()[1]
-                if port in taken or port + 1 in taken or port + 1 > 65535:
-                    continue
-                b = socket.socket()
-                try:
-                    b.bind(("127.0.0.1", port + 1))
-                except OSError:
-                    continue
-                finally:
-                    b.close()
-                return port
             finally:
                 a.close()
-        raise RuntimeError("no free port pair for a Service")
+            if port not in taken:
+                return port
+        raise RuntimeError("no free port for a Service")
 
     def _service_map_file(self, ns) -> str:
         return os.path.join(self.log_dir, "service-map-%s.json" % ns)

@@ -1,34 +1,39 @@
-"""GEMM entry points (K1) for linear layers, on the gfx950 MFMA kernel.
+"""GEMM entry points (K1) for linear layers, on the gfx950 MFMA kernels.
 
 ``mm(a, b, a_kmajor, b_kmajor, ...)`` is the raw kernel (bf16 in, fp32 acc,
-bf16/fp32 out, bias / ReLU / GELU epilogue, fp32 accumulate, split-K
-atomics). ``linear_fwd`` / ``linear_bwd`` express a Linear layer's three
-products with it WITHOUT materialising any transpose:
+bf16/fp32 out, bias / ReLU / GELU epilogue, fp32 accumulate, split-K).
+``linear_fwd`` / ``linear_bwd`` express a Linear layer's three products with
+it WITHOUT materialising any transpose:
 
     fwd    y  = x . W^T          A = x   [M,K] K-major,  B = W [N,K] K-major
     dgrad  dx = g . W            A = g   [M,N] K-major,  B = W [N,K] read N-major
-    wgrad  dW = g^T . x          A = g   read M-major,   B = x read N-major  (split-K, fp32 out
-                                                             straight into the flat gradient slot)
+    wgrad  dW = g^T . x          A = g   read M-major,   B = x read N-major  (fp32 out straight into the
+                                                             flat gradient slot, accumulated for tied weights)
 
-Where the vendor library (hipBLASLt behind torch.matmul / addmm) can run the
-same plain product, ``ops.autotune`` times both once per shape and keeps the
-faster; fused epilogues the library lacks (GELU with the pre-activation side
-output, fp32 split-K accumulation straight into the flat gradient slot) are
-charged the extra elementwise / cast passes the library path needs, so the
-comparison is end to end. CPU tensors (and shapes the kernel does not take)
-use plain PyTorch.
+Every product runs on our kernels: the 256 x 256 LDS-ring kernel (csrc/kernels/gemm256.hip) when the output
+fills the chip, else the 128 x 128 kernel (gemm.hip); the choice is a wave-quantisation cost model in C++
+(``gemm256_eligible``), not a timing race against a vendor library. CPU tensors use plain PyTorch; GPU shapes
+the kernels do not take (K not a multiple of 64 on a K-major operand, odd M/N) go through PyTorch too and are
+counted in ``FALLBACKS`` (reported by the trainer), never silently.
 """
 from __future__ import annotations
 
-from typing import Optional
+import warnings
+from typing import Dict
 
 import torch
 import torch.nn.functional as F
 
-from k8s_amd.ops import autotune
 from k8s_amd.ops._ext import load as _load
 
 ACT = {None: 0, "relu": 1, "gelu": 2}
+FALLBACKS: Dict[str, int] = {}
+
+
+def _fallback(key: str):
+    if key not in FALLBACKS:
+        warnings.warn("k8s_amd GEMM: %s is outside the MFMA kernels' shape contract; using PyTorch" % key)
+    FALLBACKS[key] = FALLBACKS.get(key, 0) + 1
 
 
 def hip_ok(*ts) -> bool:
@@ -72,13 +77,6 @@ def _act_bwd(gy, pre_or_out, act):
     raise ValueError(act)
 
 
-def _blas_fwd(x, w, b, act):
-    y = torch.addmm(b.to(x.dtype), x, w.t()) if b is not None else torch.mm(x, w.t())
-    pre = y
-    y = _act_fwd(y, act)
-    return y, (pre if act == "gelu" else (y if act == "relu" else None))
-
-
 def _hip_fwd(x, w, b, act):
     M, N = x.shape[0], w.shape[0]
     pre = torch.empty((M, N), device=x.device, dtype=torch.bfloat16) if act == "gelu" else None
@@ -91,34 +89,15 @@ def linear_fwd(x, w, b, act=None):
     M, K = x.shape
     N = w.shape[0]
     if hip_ok(x, w) and _shape_ok(M, N, K) and x.stride(1) == 1:
-        key = "linear_fwd|%dx%dx%d|%s|%d" % (M, N, K, act, b is not None)
-        if autotune.choose(key, [("hip", lambda: _hip_fwd(x, w, b, act)),
-                                 ("blas", lambda: _blas_fwd(x, w, b, act))]) == "hip":
-            return _hip_fwd(x, w, b, act)
-        return _blas_fwd(x, w, b, act)
+        return _hip_fwd(x, w, b, act)
+    if x.is_cuda:
+        _fallback("linear_fwd %dx%dx%d" % (M, N, K))
     y = torch.matmul(x, w.t())
     if b is not None:
         y = y + b.to(y.dtype)
     pre = y
     y = _act_fwd(y, act)
     return y, (pre if act == "gelu" else (y if act == "relu" else None))
-
-
-_ADDMM_F32 = None  # does this torch build take addmm(..., out_dtype=float32) for bf16 inputs?
-
-
-def _blas_wgrad(g, x, out, accumulate):
-    """out (fp32) (+)= g^T x on hipBLASLt, fp32 accumulate straight into the slot when supported."""
-    global _ADDMM_F32
-    if _ADDMM_F32 is not False:
-        try:
-            torch.addmm(out, g.t(), x, out_dtype=torch.float32, beta=1.0 if accumulate else 0.0, out=out)
-            _ADDMM_F32 = True
-            return
-        except (RuntimeError, TypeError):
-            _ADDMM_F32 = False
-    d = torch.mm(g.t(), x)
-    out.add_(d) if accumulate else out.copy_(d)
 
 
 def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True):
@@ -136,27 +115,10 @@ def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True):
         db = g.float().sum(0)
     if hip_ok(g, x, w) and _shape_ok(M, N, K) and N % 64 == 0:
         g = g.contiguous()
-        dims = "%dx%dx%d" % (M, N, K)
-        if autotune.choose("linear_dgrad|" + dims, [("hip", lambda: mm(g, w, True, False)),
-                                                    ("blas", lambda: torch.mm(g, w))]) == "hip":
-            dx = mm(g, w, True, False)
-        else:
-            dx = torch.mm(g, w)
+        dx = mm(g, w, True, False)
         if pw is not None and store is not None and pw.grad.dtype == torch.float32:
             acc = pw.written
-
-            def hip_w(out, accumulate):
-                mm(g, x, False, False, out=out, out_f32=True, accumulate=accumulate, splits=0)
-
-            def blas_w(out, accumulate):
-                _blas_wgrad(g, x, out, accumulate)
-
-            if autotune.choose("linear_wgrad|" + dims, [
-                    ("hip", lambda: hip_w(torch.empty_like(pw.grad), False)),
-                    ("blas", lambda: blas_w(torch.empty_like(pw.grad), False))]) == "hip":
-                hip_w(pw.grad, acc)
-            else:
-                blas_w(pw.grad, acc)
+            mm(g, x, False, False, out=pw.grad, out_f32=True, accumulate=acc, splits=0)
             if acc:
                 store._notify(pw)
             else:
@@ -164,6 +126,8 @@ def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True):
             return dx, None, db
         dw = mm(g, x, False, False, out_f32=True, splits=0)
         return dx, dw, db
+    if g.is_cuda:
+        _fallback("linear_bwd %dx%dx%d" % (M, N, K))
     dx = torch.matmul(g, w)
     dw = torch.matmul(g.t(), x)
     return dx, dw, db

@@ -8,7 +8,7 @@ parallelism and gradient clipping are folded into the kernel's scale
 """
 from __future__ import annotations
 
-from typing import Callable, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -18,6 +18,9 @@ from k8s_amd.parallel.flat import ParamStore
 
 
 class _FlatOptimizer:
+    # attribute -> state_dict key of every flat fp32 state buffer
+    STATE: Dict[str, str] = {}
+
     def __init__(self, store: ParamStore, lr: float, weight_decay: float, max_grad_norm: Optional[float] = None):
         self.store = store
         self.lr = lr
@@ -25,6 +28,34 @@ class _FlatOptimizer:
         self.max_grad_norm = max_grad_norm
         self.step_count = 0
         self.hyper: Optional[torch.Tensor] = None  # device [lr, step] (hipGraph replay), see use_device_hyper
+        self.layout: Optional[List[Tuple[int, int, int]]] = None  # ZeRO-1 shard layout [(lo, hi, offset)]
+        for attr in self.STATE:
+            setattr(self, attr, torch.zeros_like(store.master))
+
+    # ---- ZeRO-1: optimizer state only for the shards this rank owns
+    def shard(self, ranges: Sequence[Tuple[int, int]]):
+        """Keep state only for ``ranges`` of the flat buffers (the parameter service's owned shards), packed
+        back to back: a rank then holds 1/world of the fp32 moments. ``step`` must be called with exactly
+        these ranges afterwards."""
+        layout, off = [], 0
+        for lo, hi in ranges:
+            layout.append((lo, hi, off))
+            off += hi - lo
+        self.layout = layout
+        for attr in self.STATE:
+            setattr(self, attr, torch.zeros(off, dtype=torch.float32, device=self.store.master.device))
+
+    def _st(self, t: torch.Tensor, lo: int, hi: int) -> torch.Tensor:
+        """State slice for flat range [lo, hi) (a sub-range of one owned shard when sharded)."""
+        if self.layout is None:
+            return t[lo:hi]
+        for a, b, off in self.layout:
+            if a <= lo and hi <= b:
+                return t[off + lo - a: off + hi - a]
+        raise ValueError("range [%d, %d) is not owned by this rank's optimizer shard" % (lo, hi))
+
+    def state_numel(self) -> int:
+        return sum(getattr(self, a).numel() for a in self.STATE)
 
     def use_device_hyper(self):
         """Kernels read lr (and Adam's step) from a device tensor instead of launch arguments, so a step
@@ -73,20 +104,37 @@ class _FlatOptimizer:
         f = min(1.0, self.max_grad_norm / (norm + 1e-6)) if bool(stats[1] == 0) else 0.0
         return torch.tensor([f])
 
-    def state_dict(self):
-        raise NotImplementedError
+    def state_tensors(self):
+        return [getattr(self, a) for a in self.STATE]
+
+    def state_dict(self, full: Optional[Dict[str, torch.Tensor]] = None):
+        """Flat state by key; when sharded pass ``full`` (attribute -> full-size tensor, gathered by the
+        parameter service) to get checkpointable whole-model tensors."""
+        d = {key: (full[attr] if full is not None else getattr(self, attr)) for attr, key in self.STATE.items()}
+        d["step"] = self.step_count
+        return d
 
     def load_state_dict(self, sd):
-        raise NotImplementedError
+        """Accepts whole-model flat tensors (a checkpoint); a sharded optimizer keeps its owned slices."""
+        for attr, key in self.STATE.items():
+            src, dst = sd[key], getattr(self, attr)
+            if self.layout is None:
+                dst.copy_(src.reshape(-1)[:dst.numel()])
+            else:
+                src = src.reshape(-1)
+                for lo, hi, off in self.layout:
+                    dst[off:off + hi - lo].copy_(src[lo:hi])
+        self.step_count = int(sd["step"])
 
 
 class FusedSGD(_FlatOptimizer):
+    STATE = {"mom": "momentum_buffer"}
+
     def __init__(self, store: ParamStore, lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=False,
                  max_grad_norm=None):
         super().__init__(store, lr, weight_decay, max_grad_norm)
         self.momentum = momentum
         self.nesterov = nesterov
-        self.mom = torch.zeros_like(store.master)
 
     def step(self, grad_scale: float = 1.0, lr: Optional[float] = None, ranges=None, stats_reduce=None):
         """Update the flat buffers (or only ``ranges`` of them: the shards this rank owns)."""
@@ -96,7 +144,7 @@ class FusedSGD(_FlatOptimizer):
         first = self.step_count == 0
         for lo, hi in ranges:
             p, g, h, mask = self._views(lo, hi)
-            m = self.mom[lo:hi]
+            m = self._st(self.mom, lo, hi)
             if p.is_cuda:
                 _load_ext().fused_sgd(p, m, g, h, mask, lr, self.momentum, self.weight_decay, grad_scale, clip,
                                       self.nesterov, first, self.hyper)
@@ -111,26 +159,17 @@ class FusedSGD(_FlatOptimizer):
         self.set_hyper(lr, self.step_count)
         self.step_count += 1
 
-    def state_tensors(self):
-        return [self.mom]
-
-    def state_dict(self):
-        return {"momentum_buffer": self.mom, "step": self.step_count}
-
-    def load_state_dict(self, sd):
-        self.mom.copy_(sd["momentum_buffer"])
-        self.step_count = int(sd["step"])
 
 
 class FusedAdam(_FlatOptimizer):
+    STATE = {"m1": "exp_avg", "m2": "exp_avg_sq"}
+
     def __init__(self, store: ParamStore, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
                  adamw=True, max_grad_norm=None):
         super().__init__(store, lr, weight_decay, max_grad_norm)
         self.b1, self.b2 = betas
         self.eps = eps
         self.adamw = adamw
-        self.m1 = torch.zeros_like(store.master)
-        self.m2 = torch.zeros_like(store.master)
 
     def step(self, grad_scale: float = 1.0, lr: Optional[float] = None, ranges=None, stats_reduce=None):
         lr = self.lr if lr is None else lr
@@ -139,7 +178,7 @@ class FusedAdam(_FlatOptimizer):
         self.step_count += 1
         for lo, hi in ranges:
             p, g, h, mask = self._views(lo, hi)
-            a, b = self.m1[lo:hi], self.m2[lo:hi]
+            a, b = self._st(self.m1, lo, hi), self._st(self.m2, lo, hi)
             if p.is_cuda:
                 _load_ext().fused_adam(p, a, b, g, h, mask, lr, self.b1, self.b2, self.eps, self.weight_decay,
                                        grad_scale, clip, self.step_count, self.adamw, self.hyper)
@@ -151,13 +190,3 @@ class FusedAdam(_FlatOptimizer):
         self.step_count += 1
         self.set_hyper(lr, self.step_count)
 
-    def state_tensors(self):
-        return [self.m1, self.m2]
-
-    def state_dict(self):
-        return {"exp_avg": self.m1, "exp_avg_sq": self.m2, "step": self.step_count}
-
-    def load_state_dict(self, sd):
-        self.m1.copy_(sd["exp_avg"])
-        self.m2.copy_(sd["exp_avg_sq"])
-        self.step_count = int(sd["step"])

@@ -117,7 +117,14 @@ def _decay_vec(mask, n, wd, device):
     return mask.to(device).repeat_interleave(64)[:n].float() * wd
 
 
+def _skipped(scale_t) -> bool:
+    """A zero clip factor marks non-finite gradients: the step is skipped, all buffers untouched."""
+    return scale_t is not None and float(scale_t.reshape(-1)[0]) == 0.0
+
+
 def sgd(p, mom, g, pbf, mask, lr, mu, wd, scale, scale_t, nesterov, first_step):
+    if _skipped(scale_t):
+        return
     s = scale * (float(scale_t.reshape(-1)[0]) if scale_t is not None else 1.0)
     d = g.float() * s + _decay_vec(mask, p.numel(), wd, p.device) * p
     m = d.clone() if first_step else mom * mu + d
@@ -128,6 +135,8 @@ def sgd(p, mom, g, pbf, mask, lr, mu, wd, scale, scale_t, nesterov, first_step):
 
 
 def adam(p, m1, m2, g, pbf, mask, lr, b1, b2, eps, wd, scale, scale_t, step, decoupled):
+    if _skipped(scale_t):
+        return
     s = scale * (float(scale_t.reshape(-1)[0]) if scale_t is not None else 1.0)
     w = _decay_vec(mask, p.numel(), wd, p.device)
     gr = g.float() * s

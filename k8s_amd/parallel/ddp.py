@@ -18,6 +18,14 @@ buckets small.
 
 Averaging is NOT done here: the optimizer kernel multiplies by 1/world in the
 same pass that applies the update.
+
+``comm_dtype=torch.bfloat16`` halves the bytes on xGMI without summing in
+bf16: a ready bucket is cast to bf16 and exchanged with one
+``all_to_all_single`` (the reduce-scatter, one direct hop over the full
+mesh); each rank sums its world received slices in fp32, rounds the reduced
+slice to bf16 once, and an ``all_gather_into_tensor`` returns the reduced
+bucket to every rank (expanded back into the fp32 gradient buffer). For
+Llama-3-8B that is 16 GB instead of 32 GB per step each way.
 """
 from __future__ import annotations
 
@@ -42,11 +50,15 @@ class _Bucket:
 
 
 class GradReducer:
-    def __init__(self, store: ParamStore, group=None, bucket_mb: float = 64.0, enabled: Optional[bool] = None):
+    def __init__(self, store: ParamStore, group=None, bucket_mb: float = 64.0, enabled: Optional[bool] = None,
+                 comm_dtype: torch.dtype = torch.float32):
         self.store = store
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self.enabled = (self.world > 1) if enabled is None else enabled
+        if comm_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("comm_dtype must be float32 or bfloat16")
+        self.comm_dtype = comm_dtype
         elem = store.grad.element_size()
         cap = max(ALIGN, int(bucket_mb * 1024 * 1024 / elem))
         self.buckets: List[_Bucket] = []
@@ -99,7 +111,13 @@ class GradReducer:
             return
         b.launched = True
         t = self.store.grad[b.lo:b.hi]
-        self.works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        if self.comm_dtype == torch.bfloat16 and (b.hi - b.lo) % self.world == 0:
+            send = t.to(torch.bfloat16)
+            recv = torch.empty_like(send)
+            self.works.append((b, send, recv, dist.all_to_all_single(recv, send, group=self.group, async_op=True)))
+        else:
+            self.works.append((b, None, None, dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group,
+                                                              async_op=True)))
 
     def finish(self):
         """Zero never-used gradients, flush remaining buckets, order the current stream after RCCL."""
@@ -112,8 +130,17 @@ class GradReducer:
                 b.pending = 0
         if self.enabled:
             self._launch_ready()
-            for w in self.works:
+            gathers = []
+            for b, send, recv, w in self.works:
                 w.wait()
+                if send is None:
+                    continue
+                n = (b.hi - b.lo) // self.world
+                red = recv.view(self.world, n).float().sum(0).to(torch.bfloat16)  # fp32 accumulate, one rounding
+                gathers.append((b, send, dist.all_gather_into_tensor(send, red, group=self.group, async_op=True)))
+            for b, full, w in gathers:
+                w.wait()
+                self.store.grad[b.lo:b.hi].copy_(full)
         self.works = []
 
     @property

@@ -51,13 +51,19 @@ def resolve(addr: str) -> str:
     return table.get(host, addr)
 
 
-def rank_from_tf_config(tf_config: str, port_offset: int = 1) -> RankInfo:
+def rank_from_tf_config(tf_config: str, port_offset: int = 0) -> RankInfo:
     """Deterministic rank assignment from a TF_CONFIG JSON string.
 
     Compute ranks (the collective group) are master/chief first, then workers;
     PS tasks do not join the RCCL group (rank -1): in this framework the
     parameter service is sharded over the compute ranks (parallel/ps.py) and
     the PS replicas run the parameter/rendezvous server (ps_server/).
+
+    The TCP-store rendezvous listens on the first compute task's own ``tfPort``
+    (``port_offset`` 0): that is the one port the operator's per-replica
+    ClusterIP Service forwards (`/root/reference/pkg/trainer/replicas.go:156-186`,
+    port ``tf-port``), and the trainer itself binds nothing else there. RCCL's
+    own bootstrap/data connections go pod-to-pod and need no Service.
     """
     cfg = json.loads(tf_config)
     cluster: Dict[str, List[str]] = cfg.get("cluster", {})

@@ -65,6 +65,8 @@ def parse(argv=None):
     ap.add_argument("--max-grad-norm", type=float, default=None)
     ap.add_argument("--strategy", default="allreduce", choices=["allreduce", "ps"])
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
+                    help="gradient transport: bf16 = all-to-all reduce-scatter with fp32 accumulation")
     ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
     ap.add_argument("--logdir", default=os.environ.get("K8S_AMD_LOGDIR", ""))
     ap.add_argument("--ckpt-dir", default=os.environ.get("K8S_AMD_CKPT_DIR", ""))
@@ -164,6 +166,52 @@ def _run_ps(info, tf_config: str) -> int:
     return serve(cluster, "ps", info.role_index)
 
 
+def _restore(a, w, opt, dev, chief: bool, world: int, metrics) -> int:
+    """Resume from the chief's latest checkpoint; returns the first step to run (0 without one)."""
+    from k8s_amd.utils import checkpoint as ckpt
+
+    meta_t = torch.tensor([-1, 0], dtype=torch.int64)  # [checkpoint step or -1, optimizer step]
+    tensors = {}
+    base = None
+    if chief and a.ckpt_dir:
+        base = ckpt.latest_checkpoint(a.ckpt_dir)
+        if base:
+            step0, tensors, meta = ckpt.load(base)
+            meta_t[0], meta_t[1] = step0, int(meta.get("optim_step", step0 + 1))
+    if world > 1:
+        mt = meta_t.to(dev)
+        torch.distributed.broadcast(mt, 0)
+        meta_t = mt.cpu()
+    step0 = int(meta_t[0])
+    if step0 < 0:
+        return 0
+
+    def bcast(t: torch.Tensor):
+        if world > 1:
+            torch.distributed.broadcast(t, 0)
+
+    params = {k[len("params/"):]: v for k, v in tensors.items() if k.startswith("params/")}
+    if chief:
+        w.store.load_state_dict(params)
+    bcast(w.store.master)
+    w.store.refresh_lowp()
+    for name, buf in w.model.named_buffers():
+        if chief and ("buffers/" + name) in tensors:
+            buf.copy_(tensors["buffers/" + name])
+        bcast(buf)
+    osd = {"step": int(meta_t[1])}
+    for attr, key in opt.STATE.items():
+        full = torch.zeros(w.store.total, dtype=torch.float32, device=dev)
+        if chief and ("optim/" + key) in tensors:
+            src = tensors["optim/" + key].reshape(-1)
+            full[:src.numel()].copy_(src)
+        bcast(full)
+        osd[key] = full
+    opt.load_state_dict(osd)
+    metrics.event(event="restored", checkpoint=os.path.basename(base) if base else None, step=step0)
+    return step0 + 1
+
+
 def train(a) -> int:
     from k8s_amd.models.registry import build
     from k8s_amd.ops.optim import FusedAdam, FusedSGD
@@ -213,11 +261,12 @@ def train(a) -> int:
     if world > 1:  # identical initial weights everywhere
         torch.distributed.broadcast(w.store.master, 0)
         w.store.refresh_lowp()
+    comm_dtype = torch.bfloat16 if a.grad_comm == "bf16" else torch.float32
     if a.strategy == "ps":
-        svc = ShardedParameterService(w.store, opt, bucket_mb=a.bucket_mb)
+        svc = ShardedParameterService(w.store, opt, bucket_mb=a.bucket_mb, comm_dtype=comm_dtype)
         begin, finish = svc.begin_step, (lambda lr_: svc.step(lr=lr_))
     else:
-        red = GradReducer(w.store, bucket_mb=a.bucket_mb)
+        red = GradReducer(w.store, bucket_mb=a.bucket_mb, comm_dtype=comm_dtype)
         begin = red.begin_step
 
         def finish(lr_):
@@ -225,31 +274,17 @@ def train(a) -> int:
             opt.step(grad_scale=red.grad_scale, lr=lr_)
         svc = None
 
-    # ---- restore
-    start_step = 0
-    if a.ckpt_dir:
-        base = ckpt.latest_checkpoint(a.ckpt_dir)
-        if base:
-            step0, tensors, meta = ckpt.load(base)
-            w.store.load_state_dict({k[len("params/"):]: v for k, v in tensors.items() if k.startswith("params/")})
-            bufs = dict(w.model.named_buffers())
-            for k, v in tensors.items():
-                if k.startswith("buffers/") and k[8:] in bufs:
-                    bufs[k[8:]].copy_(v)
-            osd = {k[len("optim/"):]: v.to(dev) for k, v in tensors.items() if k.startswith("optim/")}
-            osd["step"] = int(meta.get("optim_step", step0 + 1))
-            opt.load_state_dict(osd)
-            start_step = step0 + 1
-            metrics.event(event="restored", checkpoint=os.path.basename(base), step=step0)
+    # ---- restore: only the chief reads the checkpoint (--ckpt-dir may be pod-local), then every tensor and the
+    # start step are broadcast from it, so all ranks resume at the same step with identical weights and state
+    start_step = _restore(a, w, opt, dev, chief, world, metrics)
 
     def save(step):
-        if svc is not None:
-            svc.sync_state()
+        full = svc.full_optimizer_state() if svc is not None else None  # collective: every rank takes part
         if not chief:
             return
         tensors = {"params/" + k: v for k, v in w.store.state_dict().items()}
         tensors.update({"buffers/" + k: v for k, v in w.model.named_buffers()})
-        for k, v in opt.state_dict().items():
+        for k, v in opt.state_dict(full).items():
             if torch.is_tensor(v):
                 tensors["optim/" + k] = v
         base = ckpt.save(a.ckpt_dir, step, tensors, meta={"model": a.model, "optim_step": opt.step_count,
@@ -310,7 +345,12 @@ def train(a) -> int:
             watchdog.kick()
         if step == start_step or (step + 1) % a.log_every == 0 or step + 1 == a.steps:
             loss_v = float(loss.detach().float().item())
-            if not (loss_v == loss_v and abs(loss_v) != float("inf")):
+            bad = not (loss_v == loss_v and abs(loss_v) != float("inf"))
+            if world > 1:  # decided together: a rank that exits alone would leave its peers in a collective
+                flag = torch.tensor([1.0 if bad else 0.0], device=dev)
+                torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MAX)
+                bad = bool(flag.item() > 0)
+            if bad:
                 metrics.event(event="error", step=step, error="non-finite loss")
                 return EXIT_PERMANENT
             sync()
@@ -331,7 +371,10 @@ def train(a) -> int:
     if watchdog is not None:
         watchdog.stop()
     kdist.barrier()
-    metrics.event(event="done", steps=a.steps, loss=loss_v, elapsed=time.time() - t_start)
+    from k8s_amd.ops import gemm as kgemm
+
+    metrics.event(event="done", steps=a.steps, loss=loss_v, elapsed=time.time() - t_start,
+                  gemm_fallbacks=dict(kgemm.FALLBACKS))
     metrics.close()
     if chief:
         _shutdown_ps(tf_config)

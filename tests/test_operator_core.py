@@ -265,6 +265,27 @@ def test_replica_set_create():
     assert store.get("/apis/batch/v1/namespaces/default/jobs")[1]["items"] == []
 
 
+def test_rendezvous_port_is_exposed_by_the_master_service():
+    """The trainer's TCP-store rendezvous (parallel/dist.py) must dial a port the master's ClusterIP Service
+    forwards: a multi-replica TfJob on a real cluster reaches the master only through that Service."""
+    from k8s_amd.parallel.dist import rank_from_tf_config
+
+    store = ApiStore()
+    job = _seed(store, {"metadata": {"name": "dp"}, "spec": {"RuntimeId": "rid0", "replicaSpecs": [
+        {"replicas": 1, "tfPort": 2222, "tfReplicaType": "MASTER", "template": template(container())},
+        {"replicas": 3, "tfPort": 2222, "tfReplicaType": "WORKER", "template": template(container())}]}})
+    _reconciler(store, json.dumps(job)).reconcile()
+    _, svcs = store.get("/api/v1/namespaces/default/services")
+    _, jobs = store.get("/apis/batch/v1/namespaces/default/jobs")
+    ports = {s["metadata"]["name"]: {p["port"] for p in s["spec"]["ports"]} for s in svcs["items"]}
+    for j in jobs["items"]:
+        tfc = j["spec"]["template"]["spec"]["containers"][0]["env"][0]["value"]
+        info = rank_from_tf_config(tfc)
+        assert info.world_size == 4
+        assert info.master_addr == "dp-master-rid0-0"
+        assert info.master_port in ports[info.master_addr], (info.master_port, ports)
+
+
 def test_tensorboard_create():
     store = ApiStore()
     job = _seed(store, {"metadata": {"name": "some-job"}, "spec": {

@@ -1,0 +1,139 @@
+"""Data-parallel strategies on CPU with gloo, 2 and 4 ranks (the RCCL code paths, minus the device).
+
+* all-reduce (``GradReducer``) vs the sharded parameter service (``ShardedParameterService``, reduce-scatter
+  push / ZeRO-1 owner update / all-gather pull): same weights and optimizer state; bit-for-bit at 2 ranks
+  (a + b == b + a), to rounding at 4 (the two collectives sum in different orders).
+* bf16 gradient transport (all-to-all reduce-scatter + fp32 accumulation): close to the fp32 result, and the
+  fp32 summation is what keeps it close (a bf16 running sum would not be).
+* ZeRO-1: each rank holds 1/world of the optimizer moments.
+* non-finite gradients under gradient clipping skip the step on every rank, leaving all state bit-identical.
+"""
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from k8s_amd.fakeapi.server import free_port
+
+SHAPES = [(64, 33), (129,), (7, 5, 3), (256,), (16, 16), (1000,)]
+
+
+def _grads(rank, step, shapes):
+    g = torch.Generator().manual_seed(1000 * step + 17 * rank + 3)
+    return [torch.randn(s, generator=g) * (1.0 + rank) for s in shapes]
+
+
+def _worker(rank, world, port, strategy, comm, opt_name, steps, out_dir, nan_step):
+    from k8s_amd.ops.optim import FusedAdam, FusedSGD
+    from k8s_amd.parallel.ddp import GradReducer
+    from k8s_amd.parallel.flat import ALIGN, ParamStore, init_normal
+    from k8s_amd.parallel.ps import ShardedParameterService
+
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    store = ParamStore()
+    params = [store.new("p%d" % i, s, init_normal(0.5), decay=(i % 2 == 0)) for i, s in enumerate(SHAPES)]
+    store.finalize("cpu", pad_to=world * ALIGN, seed=5)
+    if opt_name == "sgd":
+        opt = FusedSGD(store, lr=0.05, momentum=0.9, weight_decay=1e-3, max_grad_norm=10.0)
+    else:
+        opt = FusedAdam(store, lr=0.01, weight_decay=0.01, max_grad_norm=10.0)
+    dtype = torch.bfloat16 if comm == "bf16" else torch.float32
+    if strategy == "ps":
+        svc = ShardedParameterService(store, opt, bucket_mb=0.002, comm_dtype=dtype)  # several buckets
+        begin, finish = svc.begin_step, (lambda: svc.step())
+    else:
+        red = GradReducer(store, bucket_mb=0.002, comm_dtype=dtype)
+        begin = red.begin_step
+
+        def finish():
+            red.finish()
+            opt.step(grad_scale=red.grad_scale)
+        svc = None
+    for step in range(steps):
+        begin()
+        gs = _grads(rank, step, SHAPES)
+        if step == nan_step and rank == world - 1:
+            gs[2][0, 0, 0] = float("nan")
+        for p, g in reversed(list(zip(params, gs))):  # backward order
+            store.deposit(p, g)
+        finish()
+    full = svc.full_optimizer_state() if svc is not None else None
+    if rank == 0:
+        sd = opt.state_dict(full)
+        torch.save({"master": store.master.clone(), "half": store.half.float().clone(),
+                    **{k: v.clone() for k, v in sd.items() if torch.is_tensor(v)},
+                    "state_numel": opt.state_numel(), "total": store.total},
+                   os.path.join(out_dir, "%s_%s_%s.pt" % (strategy, comm, opt_name)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(world, strategy, comm, opt_name, steps=4, nan_step=-1):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, free_port(), strategy, comm, opt_name, steps, d, nan_step), nprocs=world)
+        return torch.load(os.path.join(d, "%s_%s_%s.pt" % (strategy, comm, opt_name)), weights_only=True)
+
+
+def _reference(world, opt_name, steps):
+    """Single-process ground truth: the fp32 sum of every rank's gradient, one optimizer over everything."""
+    from k8s_amd.ops.optim import FusedAdam, FusedSGD
+    from k8s_amd.parallel.flat import ALIGN, ParamStore, init_normal
+
+    store = ParamStore()
+    params = [store.new("p%d" % i, s, init_normal(0.5), decay=(i % 2 == 0)) for i, s in enumerate(SHAPES)]
+    store.finalize("cpu", pad_to=world * ALIGN, seed=5)
+    if opt_name == "sgd":
+        opt = FusedSGD(store, lr=0.05, momentum=0.9, weight_decay=1e-3, max_grad_norm=10.0)
+    else:
+        opt = FusedAdam(store, lr=0.01, weight_decay=0.01, max_grad_norm=10.0)
+    for step in range(steps):
+        store.begin_step()
+        tot = [sum(_grads(r, step, SHAPES)[i] for r in range(world)) for i in range(len(SHAPES))]
+        for p, g in zip(params, tot):
+            store.deposit(p, g)
+        opt.step(grad_scale=1.0 / world)
+    return store.master.clone()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("opt_name", ["sgd", "adam"])
+def test_allreduce_and_sharded_ps_agree(world, opt_name):
+    a = _run(world, "allreduce", "fp32", opt_name)
+    b = _run(world, "ps", "fp32", opt_name)
+    keys = ["master", "half"] + (["momentum_buffer"] if opt_name == "sgd" else ["exp_avg", "exp_avg_sq"])
+    for k in keys:
+        if world == 2:
+            assert torch.equal(a[k], b[k]), k  # same two-term sums: bit-for-bit
+        else:
+            torch.testing.assert_close(a[k], b[k], rtol=1e-6, atol=1e-7, msg=k)
+    torch.testing.assert_close(a["master"], _reference(world, opt_name, 4), rtol=1e-5, atol=1e-6)
+    # ZeRO-1: the sharded run kept 1/world of the moments per rank
+    n_state = 1 if opt_name == "sgd" else 2
+    assert a["state_numel"] == n_state * a["total"]
+    assert b["state_numel"] == n_state * b["total"] // world
+
+
+@pytest.mark.parametrize("strategy", ["allreduce", "ps"])
+def test_bf16_gradient_transport_close_to_fp32(strategy):
+    world = 4
+    ref = _reference(world, "sgd", 4)
+    b = _run(world, strategy, "bf16", "sgd")
+    f = _run(world, strategy, "fp32", "sgd")
+    err_b = (b["master"] - ref).abs().max().item()
+    err_f = (f["master"] - ref).abs().max().item()
+    assert err_f < 1e-5
+    assert err_b < 5e-3, err_b  # one bf16 rounding per contribution, fp32 accumulation
+
+
+@pytest.mark.parametrize("strategy", ["allreduce", "ps"])
+def test_nonfinite_gradient_skips_step_everywhere(strategy):
+    """A NaN in one rank's gradient at the last step: the clip factor is 0 and the update is skipped, so the
+    final state equals a run that stopped one step earlier (bit for bit)."""
+    a = _run(2, strategy, "fp32", "adam", steps=4, nan_step=3)
+    b = _run(2, strategy, "fp32", "adam", steps=3)
+    for k in ("master", "exp_avg", "exp_avg_sq"):
+        assert torch.equal(a[k], b[k]), k

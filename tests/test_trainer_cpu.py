@@ -87,8 +87,17 @@ def test_bad_model_is_permanent_failure():
     assert 0 < p.returncode < 128
 
 
+def _distinct_ports(n):
+    ports = []
+    while len(ports) < n:
+        p = free_port()
+        if p not in ports:
+            ports.append(p)
+    return ports
+
+
 def _run_job(tmp_path, strategy, with_ps):
-    pm, pw, pp = free_port(), free_port(), free_port()
+    pm, pw, pp = _distinct_ports(3)
     cluster = {"master": ["127.0.0.1:%d" % pm], "worker": ["127.0.0.1:%d" % pw]}
     if with_ps:
         cluster["ps"] = ["127.0.0.1:%d" % pp]
