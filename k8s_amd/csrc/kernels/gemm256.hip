@@ -352,13 +352,15 @@ static void launch_ring(const AS& a, const BS& b, const Epi& e, int M, int N, in
 
 }  // namespace g256
 
-// Shape gate for the 256 x 256 kernel: K a multiple of 64, MN-major extents multiples of 8, and a wave-
+// Shape gate for the 256 x 256 kernel: K >= 768 and a multiple of 64, MN-major extents multiples of 8, and a wave-
 // quantisation cost model against the 128 x 128 kernel of gemm.hip (2 blocks/CU). Per output element the 256
 // kernel runs ~1.25x the 128 kernel's rate (measured, scripts/bench_gemm256.py), but with one 256-tile per CU
 // a 1.5-wave grid (e.g. 384 tiles) idles a third of the chip in its last round:
 //   t256 ~ ceil(T256 / 256) * 256^2 / 1.25     t128 ~ ceil(T128 / 512) * 2 * 128^2
 bool gemm256_eligible(int M, int N, int K, bool a_kmajor, bool b_kmajor) {
-  if (K % 64 != 0 || K < 64) return false;
+  // short reductions (ResNet's 1x1 convolutions as GEMMs, K = 64..512) leave the 5-stage ring mostly in its
+  // prologue/epilogue; the 128 x 128 kernel's single-buffered 3-blocks/CU variant is built for them
+  if (K % 64 != 0 || K < 768) return false;
   if (!a_kmajor && M % 8 != 0) return false;
   if (!b_kmajor && N % 8 != 0) return false;
   if (N % 4 != 0) return false;

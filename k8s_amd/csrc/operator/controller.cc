@@ -130,7 +130,29 @@ std::map<std::string, TfJobStatus> Controller::statuses() {
   return out;
 }
 
+void Controller::watchdog_loop() {
+  const long long limit = std::chrono::duration_cast<std::chrono::nanoseconds>(opts_.event_watchdog).count();
+  while (!stop_) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    const long long t0 = handler_started_ns_.load();
+    if (t0 && std::chrono::steady_clock::now().time_since_epoch().count() - t0 > limit) {
+      log_error("panicTimer: handling a TfJob event has taken longer than %lld ms; aborting",
+                (long long)opts_.event_watchdog.count());
+      std::abort();
+    }
+  }
+}
+
 std::string Controller::run() {
+  std::thread watchdog(&Controller::watchdog_loop, this);
+  struct Joiner {
+    Controller* c;
+    std::thread& t;
+    ~Joiner() {
+      c->stop_ = true;
+      t.join();
+    }
+  } joiner{this, watchdog};
   // initResource with retry (controller.go:86-96)
   while (!stop_) {
     std::string err = init_resource();
@@ -198,13 +220,10 @@ std::string Controller::run() {
       }
       if (!obj) continue;
       if (const Json* m = obj->find("metadata")) rv = get_str(*m, "resourceVersion");
-      // panicTimer equivalent: a single event handler must not wedge the controller
-      auto t0 = std::chrono::steady_clock::now();
+      // panicTimer: armed while the handler runs; the watchdog thread aborts a wedged handler
+      handler_started_ns_ = std::chrono::steady_clock::now().time_since_epoch().count();
       handle_event(type, *obj);
-      if (std::chrono::steady_clock::now() - t0 > opts_.event_watchdog) {
-        log_error("handling a TfJob event took longer than the watchdog; aborting");
-        std::abort();
-      }
+      handler_started_ns_ = 0;
     }
     w->close();
   }

@@ -60,7 +60,12 @@ class Controller {
   KubeApi& api_;
   ControllerConfig cfg_;
   ControllerOptions opts_;
+  void watchdog_loop();
+
   std::atomic<bool> stop_{false};
+  // panicTimer (pkg/controller/util.go:50-76): steady-clock ns at which the current event handler started,
+  // 0 when idle; a watchdog thread aborts the process while a handler is still running past event_watchdog
+  std::atomic<long long> handler_started_ns_{0};
   std::mutex mu_;
   std::map<std::string, std::unique_ptr<JobWorker>> jobs_;  // ns/name -> worker
   std::map<std::string, std::string> job_rvs_;               // ns/name -> resourceVersion

@@ -47,46 +47,98 @@ std::string LeaderElector::check() const {
   return "";
 }
 
-bool LeaderElector::try_acquire_or_renew() {
-  const std::string path = core_path(cfg_.ns, "endpoints", cfg_.name);
-  const std::string now = now_rfc3339();
+// MicroTime as the Lease API wants it (RFC3339 with microseconds)
+static std::string now_micro() {
+  using namespace std::chrono;
+  const auto t = system_clock::now();
+  const std::time_t s = system_clock::to_time_t(t);
+  const long us = (long)(duration_cast<microseconds>(t.time_since_epoch()).count() % 1000000);
+  std::tm tm;
+  gmtime_r(&s, &tm);
+  char buf[64];
+  strftime(buf, sizeof buf, "%Y-%m-%dT%H:%M:%S", &tm);
+  char out[96];
+  snprintf(out, sizeof out, "%s.%06ldZ", buf, us);
+  return out;
+}
+
+// Lock object <-> record. Endpoints: JSON in the leader annotation. Lease: the spec fields.
+static LeaderElectionRecord record_of(const Json& obj, bool lease) {
+  LeaderElectionRecord r;
+  if (lease) {
+    const Json* sp = obj.find("spec");
+    if (!sp) return r;
+    r.holder_identity = get_str(*sp, "holderIdentity");
+    if (const Json* v = sp->find("leaseDurationSeconds"); v && v->is_number()) r.lease_duration_seconds = (int)v->as_int();
+    r.acquire_time = get_str(*sp, "acquireTime");
+    r.renew_time = get_str(*sp, "renewTime");
+    if (const Json* v = sp->find("leaseTransitions"); v && v->is_number()) r.leader_transitions = (int)v->as_int();
+    return r;
+  }
+  const Json* md = obj.find("metadata");
+  if (md)
+    if (const Json* ann = md->find("annotations"); ann && ann->find(kLeaderAnnotation)) {
+      try {
+        r = LeaderElectionRecord::from_json(Json::parse(ann->at(kLeaderAnnotation).as_string()));
+      } catch (...) {
+      }
+    }
+  return r;
+}
+
+static void store_record(Json& obj, const LeaderElectionRecord& rec, bool lease) {
+  if (lease) {
+    Json sp = Json::object();
+    sp["holderIdentity"] = rec.holder_identity;
+    sp["leaseDurationSeconds"] = rec.lease_duration_seconds;
+    sp["acquireTime"] = rec.acquire_time;
+    sp["renewTime"] = rec.renew_time;
+    sp["leaseTransitions"] = rec.leader_transitions;
+    obj["spec"] = sp;
+  } else {
+    obj["metadata"]["annotations"][kLeaderAnnotation] = rec.to_json().dump();
+  }
+}
+
+bool LeaderElector::try_acquire_or_renew(int timeout_ms) {
+  const bool lease = cfg_.lock_type != "endpoints";
+  const std::string coll = lease ? group_path("coordination.k8s.io/v1", cfg_.ns, "leases")
+                                 : core_path(cfg_.ns, "endpoints");
+  const std::string path = coll + "/" + cfg_.name;
+  const std::string now = lease ? now_micro() : now_rfc3339();
+  RequestTimeout bound(timeout_ms);  // every API call below gives up by the caller's deadline
   LeaderElectionRecord rec;
   rec.holder_identity = cfg_.identity;
   rec.lease_duration_seconds = (int)(cfg_.lease.count() / 1000);
+  if (rec.lease_duration_seconds < 1) rec.lease_duration_seconds = 1;
   rec.acquire_time = now;
   rec.renew_time = now;
   ApiResult g = api_.get(path);
   if (g.not_found()) {
-    Json ep = Json::object();
-    ep["apiVersion"] = "v1";
-    ep["kind"] = "Endpoints";
+    Json obj = Json::object();
+    obj["apiVersion"] = lease ? "coordination.k8s.io/v1" : "v1";
+    obj["kind"] = lease ? "Lease" : "Endpoints";
     Json md = Json::object();
     md["name"] = cfg_.name;
     md["namespace"] = cfg_.ns;
-    Json ann = Json::object();
-    ann[kLeaderAnnotation] = rec.to_json().dump();
-    md["annotations"] = ann;
-    ep["metadata"] = md;
-    ApiResult c = api_.post(core_path(cfg_.ns, "endpoints"), ep);
-    if (!c.ok()) return false;
+    if (!lease) md["annotations"] = Json::object();
+    obj["metadata"] = md;
+    store_record(obj, rec, lease);
+    ApiResult c = api_.post(coll, obj);
+    if (!c.ok()) return leader_ = false;
     observed_ = rec;
     observed_time_ = std::chrono::steady_clock::now();
     return leader_ = true;
   }
   if (!g.ok()) return leader_ = false;
-  Json ep = g.body;
-  Json& md = ep["metadata"];
-  LeaderElectionRecord old;
-  if (const Json* ann = md.find("annotations"); ann && ann->find(kLeaderAnnotation)) {
-    try {
-      old = LeaderElectionRecord::from_json(Json::parse(ann->at(kLeaderAnnotation).as_string()));
-    } catch (...) {
-    }
-  }
+  Json obj = g.body;
+  LeaderElectionRecord old = record_of(obj, lease);
   if (old.to_json() != observed_.to_json()) {
     observed_ = old;
     observed_time_ = std::chrono::steady_clock::now();
   }
+  // the lease is judged by OUR clock since we last saw the record change (election.go:232-236), never by
+  // the holder's timestamps: no clock-skew assumptions between replicas
   const bool held_by_other = !old.holder_identity.empty() && old.holder_identity != cfg_.identity;
   if (held_by_other &&
       observed_time_ + std::chrono::seconds(old.lease_duration_seconds) > std::chrono::steady_clock::now())
@@ -97,8 +149,9 @@ bool LeaderElector::try_acquire_or_renew() {
   } else {
     rec.leader_transitions = old.leader_transitions + 1;
   }
-  md["annotations"][kLeaderAnnotation] = rec.to_json().dump();
-  ApiResult u = api_.put(path, ep);  // carries metadata.resourceVersion: optimistic CAS
+  if (!lease && !obj["metadata"].find("annotations")) obj["metadata"]["annotations"] = Json::object();
+  store_record(obj, rec, lease);
+  ApiResult u = api_.put(path, obj);  // carries metadata.resourceVersion: optimistic CAS
   if (!u.ok()) return leader_ = false;
   observed_ = rec;
   observed_time_ = std::chrono::steady_clock::now();
@@ -119,10 +172,10 @@ void LeaderElector::record_event(const std::string& what) {
   md["namespace"] = cfg_.ns;
   ev["metadata"] = md;
   Json io = Json::object();
-  io["kind"] = "Endpoints";
+  io["kind"] = cfg_.lock_type == "endpoints" ? "Endpoints" : "Lease";
   io["namespace"] = cfg_.ns;
   io["name"] = cfg_.name;
-  io["apiVersion"] = "v1";
+  io["apiVersion"] = cfg_.lock_type == "endpoints" ? "v1" : "coordination.k8s.io/v1";
   ev["involvedObject"] = io;
   ev["reason"] = "LeaderElection";
   ev["message"] = cfg_.identity + " " + what;
@@ -141,25 +194,35 @@ void LeaderElector::run(const std::function<void()>& on_started, const std::func
                         const std::atomic<bool>& stop) {
   std::mt19937 rng{std::random_device{}()};
   std::uniform_real_distribution<double> jitter(1.0, 1.2);
-  while (!stop && !try_acquire_or_renew())
+  // acquire: every attempt bounded by the retry period, then JitterUntil's sleep (election.go:175-189)
+  while (!stop && !try_acquire_or_renew((int)cfg_.retry.count()))
     std::this_thread::sleep_for(std::chrono::milliseconds((long)(cfg_.retry.count() * jitter(rng))));
   if (stop) return;
   log_info("became leader: %s", cfg_.identity.c_str());
   record_event("became leader");
   std::thread worker(on_started);
   worker.detach();
+  // renew: Poll(retry) until RenewDeadline passes without a successful renewal (election.go:192-208). Each
+  // attempt's API calls are bounded by the time left before that deadline, so a stalled API server makes the
+  // leader give up at renew_deadline -- strictly before a standby may take the lease (lease > renew_deadline).
   auto last_ok = std::chrono::steady_clock::now();
   while (!stop) {
     std::this_thread::sleep_for(cfg_.retry);
-    if (try_acquire_or_renew()) {
+    const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(
+        last_ok + cfg_.renew_deadline - std::chrono::steady_clock::now());
+    if (left.count() > 0 && try_acquire_or_renew((int)left.count())) {
       last_ok = std::chrono::steady_clock::now();
-    } else if (std::chrono::steady_clock::now() - last_ok > cfg_.renew_deadline) {
-      log_error("leader election lost");
+    } else if (std::chrono::steady_clock::now() - last_ok >= cfg_.renew_deadline) {
+      log_error("leader election lost: no renewal within the %lld ms renew deadline",
+                (long long)cfg_.renew_deadline.count());
       break;
     }
   }
   leader_ = false;
-  record_event("stopped leading");
+  {
+    RequestTimeout bound(1000);  // best effort: the API server may be the reason we lost the lease
+    record_event("stopped leading");
+  }
   on_stopped();
 }
 

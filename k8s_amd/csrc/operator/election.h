@@ -2,9 +2,14 @@
 //
 // Parity: /root/reference/pkg/util/k8sutil/election/election.go (acquire /
 // renew / tryAcquireOrRenew :141-265, lease > renew > 1.2 x retry check
-// :73-86) and resourcelock/endpointslock.go + interface.go (record stored as
-// JSON in the Endpoints annotation control-plane.alpha.kubernetes.io/leader).
-// The record format is unchanged so mixed deployments interoperate.
+// :73-86, renew Poll until RenewDeadline :192-208) and resourcelock/
+// endpointslock.go + interface.go (record stored as JSON in the Endpoints
+// annotation control-plane.alpha.kubernetes.io/leader; that record format is
+// unchanged so mixed deployments interoperate). Added: a coordination.k8s.io/v1
+// Lease lock (default), and renews whose API calls are bounded by the time
+// left before the renew deadline, so a hung API server cannot keep a leader
+// that can no longer renew (no split brain: the standby only acquires after a
+// full lease duration without renewals).
 #pragma once
 
 #include <atomic>
@@ -30,6 +35,9 @@ struct LeaderElectionRecord {
 struct ElectionConfig {
   std::string ns, name, identity;
   std::chrono::milliseconds lease{15000}, renew_deadline{5000}, retry{3000};
+  // "leases" (coordination.k8s.io/v1 Lease, the default of modern client-go) or "endpoints" (the reference's
+  // Endpoints annotation lock, pkg/util/k8sutil/election/resourcelock/endpointslock.go)
+  std::string lock_type = "leases";
 };
 
 class LeaderElector {
@@ -37,8 +45,9 @@ class LeaderElector {
   LeaderElector(KubeApi& api, ElectionConfig cfg);
   // error text if the durations are inconsistent (lease > renew > 1.2*retry)
   std::string check() const;
-  // one acquire/renew attempt; true if we hold the lock afterwards
-  bool try_acquire_or_renew();
+  // one acquire/renew attempt, every API call bounded by timeout_ms (-1: the client default); true if we hold
+  // the lock afterwards
+  bool try_acquire_or_renew(int timeout_ms = -1);
   // Blocks: acquire, run on_started (in this thread's caller's stead: a separate thread), renew until lost.
   // Returns when leadership is lost or stop is set.
   void run(const std::function<void()>& on_started, const std::function<void()>& on_stopped,

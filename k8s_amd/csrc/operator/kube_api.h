@@ -61,12 +61,35 @@ struct ClusterConfig {
   bool tls = true;
   bool insecure = false;
   std::string token;
-  std::string ca_file;
+  std::string ca_file, ca_data;      // PEM file / PEM text (kubeconfig certificate-authority[-data])
+  std::string cert_file, cert_data;  // client certificate (kubeconfig client-certificate[-data])
+  std::string key_file, key_data;    // client key (kubeconfig client-key[-data])
+  std::string tls_server_name;       // overrides the name checked against the server certificate
+  int connect_timeout_ms = 10000;    // TCP connect + TLS handshake
+  int timeout_ms = 30000;            // whole request (client-go's default REST timeout is similar)
+  std::string user_agent = "tf_operator-amd/0.3.0";
 };
 
-// $KUBECONFIG (current-context server + token), --master URL, or in-cluster service account.
+// $KUBECONFIG (current-context server + credentials: token / tokenFile, client certificates, inline *-data,
+// exec credential plugins), --master URL, or the in-cluster service account. Parity:
+// /root/reference/pkg/util/k8sutil/k8sutil.go:45-65 (clientcmd.BuildConfigFromFlags / InClusterConfig).
 ClusterConfig cluster_config_from_env(const std::string& master_url = "");
 ClusterConfig parse_master_url(const std::string& url);
+ClusterConfig cluster_config_from_kubeconfig(const std::string& text, const std::string& context = "");
+
+// Per-thread request deadline override (milliseconds) for the HTTP client, e.g. a leader-election renew that
+// must give up by the renew deadline: RequestTimeout t(remaining_ms); api.put(...);
+class RequestTimeout {
+ public:
+  explicit RequestTimeout(int ms);
+  ~RequestTimeout();
+  static int current();  // -1: none
+
+ private:
+  int prev_;
+};
+
+std::string base64_decode(const std::string& in);
 
 std::unique_ptr<KubeApi> make_http_api(const ClusterConfig& cfg);
 

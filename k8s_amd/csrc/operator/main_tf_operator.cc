@@ -3,13 +3,15 @@
 // Parity: /root/reference/cmd/tf_operator/main.go (flags :48-54, config
 // file :68-85, MY_POD_NAMESPACE / MY_POD_NAME :89-96, signal exit :98-103,
 // version :105-116, Endpoints leader election 15s/5s/3s :42-44,125-148,
-// controller run loop :153-169). The chaos monkey the reference left
+// controller run loop :153-169). Leader election defaults to a coordination.k8s.io/v1 Lease
+// (-leader-elect-resource-lock=endpoints keeps the reference's lock). The chaos monkey the reference left
 // commented out (:171-207) is implemented: -chaos-level N deletes a random
 // TfJob pod every 30/N seconds (fault injection for the exit-code/restart
 // state machine).
 #include <signal.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -69,6 +71,9 @@ int main(int argc, char** argv) {
   fl.def("renew-deadline", "5s", "Leader-election renew deadline");
   fl.def("retry-period", "3s", "Leader-election retry period");
   fl.def("create-crd", "true", "Register the tfjobs.tensorflow.org CRD at startup", true);
+  fl.def("leader-elect-resource-lock", "leases", "Leader-election lock: leases (coordination.k8s.io/v1) or endpoints");
+  fl.def("request-timeout", "30s", "Deadline of every API request (connect, TLS handshake, response)");
+  fl.def("event-watchdog", "60s", "Abort when one TfJob event handler runs longer (reference panicTimer: 1m)");
   std::string err = fl.parse(argc, argv);
   if (!err.empty()) {
     fprintf(stderr, "%s\nUsage of tf_operator:\n%s", err.c_str(), fl.usage().c_str());
@@ -115,12 +120,16 @@ int main(int argc, char** argv) {
     log_error("cluster config: %s", e.what());
     return 1;
   }
+  cc.timeout_ms = (int)parse_duration_ms(fl.str("request-timeout"), 30000);
+  cc.connect_timeout_ms = std::min(cc.connect_timeout_ms, cc.timeout_ms);
+  cc.user_agent = std::string("tf_operator-amd/") + kVersion + " (" + pod + ")";
   auto api = make_http_api(cc);
 
   ControllerOptions opts;
   opts.ns = fl.on("all-namespaces") ? "" : ns;
   opts.create_crd = fl.on("create-crd");
   opts.reconcile.interval = std::chrono::milliseconds(parse_duration_ms(fl.str("reconcile-interval"), 8000));
+  opts.event_watchdog = std::chrono::milliseconds(parse_duration_ms(fl.str("event-watchdog"), 60000));
   if (!cfg.grpc_server_file_path.empty()) {
     try {
       opts.reconcile.ps_server_source = read_file(cfg.grpc_server_file_path);
@@ -150,6 +159,11 @@ int main(int argc, char** argv) {
   ec.lease = std::chrono::milliseconds(parse_duration_ms(fl.str("lease-duration"), 15000));
   ec.renew_deadline = std::chrono::milliseconds(parse_duration_ms(fl.str("renew-deadline"), 5000));
   ec.retry = std::chrono::milliseconds(parse_duration_ms(fl.str("retry-period"), 3000));
+  ec.lock_type = fl.str("leader-elect-resource-lock");
+  if (ec.lock_type != "leases" && ec.lock_type != "endpoints") {
+    log_error("-leader-elect-resource-lock must be leases or endpoints");
+    return 1;
+  }
   LeaderElector el(*api, ec);
   if (std::string e = el.check(); !e.empty()) {
     log_error("leader election config: %s", e.c_str());

@@ -1,6 +1,8 @@
 // pybind11 module k8s_amd._operator: the C++ control-plane core exposed to
 // Python (tests, the tfjob CLI, the fake API server's defaulting path).
 // JSON crosses the boundary as strings.
+#include <algorithm>
+
 #include <pybind11/functional.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -129,6 +131,47 @@ PYBIND11_MODULE(_operator, m) {
     for (auto& d : yaml_parse_all(text)) a.push_back(d);
     return a.dump();
   });
+
+  // HTTP client probes (tests of the real transport: TLS verification, timeouts, keep-alive)
+  m.def("kubeconfig", [](const std::string& text, const std::string& context) {
+    ClusterConfig c = cluster_config_from_kubeconfig(text, context);
+    py::dict d;
+    d["host"] = c.host;
+    d["port"] = c.port;
+    d["tls"] = c.tls;
+    d["insecure"] = c.insecure;
+    d["token"] = c.token;
+    d["ca_file"] = c.ca_file;
+    d["ca_data"] = c.ca_data;
+    d["cert_file"] = c.cert_file;
+    d["cert_data"] = c.cert_data;
+    d["key_file"] = c.key_file;
+    d["key_data"] = c.key_data;
+    d["tls_server_name"] = c.tls_server_name;
+    return d;
+  }, py::arg("text"), py::arg("context") = "");
+  m.def("http_request", [](const std::string& url, const std::string& method, const std::string& path,
+                           const std::string& ca_data, const std::string& server_name, int timeout_ms, int repeat,
+                           const std::string& cert_data, const std::string& key_data) {
+    ClusterConfig c = parse_master_url(url);
+    c.ca_data = ca_data;
+    c.tls_server_name = server_name;
+    c.cert_data = cert_data;
+    c.key_data = key_data;
+    if (timeout_ms > 0) {
+      c.timeout_ms = timeout_ms;
+      c.connect_timeout_ms = timeout_ms;
+    }
+    auto api = make_http_api(c);
+    ApiResult r;
+    {
+      py::gil_scoped_release nogil;
+      for (int i = 0; i < std::max(1, repeat); ++i) r = api->request(method, path, nullptr, "application/json");
+    }
+    return py::make_tuple(r.code, r.error, r.body.is_null() ? std::string() : r.body.dump());
+  }, py::arg("url"), py::arg("method") = "GET", py::arg("path") = "/", py::arg("ca_data") = "",
+     py::arg("server_name") = "", py::arg("timeout_ms") = 0, py::arg("repeat") = 1, py::arg("cert_data") = "",
+     py::arg("key_data") = "");
 
   py::class_<PyReconciler>(m, "Reconciler")
       .def(py::init<py::function, std::string, std::string, std::string>(), py::arg("api"), py::arg("job"),

@@ -14,6 +14,7 @@ import argparse
 import json
 import socket
 import threading
+import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Optional
 from urllib.parse import parse_qs, urlparse
@@ -49,8 +50,25 @@ class _Handler(BaseHTTPRequestHandler):
         except (BrokenPipeError, ConnectionResetError):
             pass  # the client went away (e.g. an operator shutting down mid-request)
 
+    def _stall(self):
+        """Fault injection: hold a matching request until its stall window ends (the client has usually given
+        up by then), like an API server that stops answering."""
+        ua = self.headers.get("User-Agent", "")
+        for rule in list(self.server.stalls):
+            if time.time() < rule["until"] and self.path.startswith(rule["path_prefix"]) and \
+                    rule["user_agent"] in ua:
+                time.sleep(max(0.0, rule["until"] - time.time()))
+
     def _dispatch(self, method):
         u = urlparse(self.path)
+        if u.path == "/debug/stall" and method == "POST":
+            # {"seconds": S, "path_prefix": "/api", "user_agent": "tf-operator-local-0"}: stall matching requests
+            b = self._body() or {}
+            self.server.stalls.append({"until": time.time() + float(b.get("seconds", 5)),
+                                       "path_prefix": b.get("path_prefix", "/"),
+                                       "user_agent": b.get("user_agent", "")})
+            return self._send(200, {"stalls": len(self.server.stalls)})
+        self._stall()
         q = {k: v[-1] for k, v in parse_qs(u.query).items()}
         body = self._body() if method in ("POST", "PUT", "PATCH", "DELETE") else None
         if method == "GET" and q.get("watch") in ("true", "1"):
@@ -112,6 +130,7 @@ class FakeApiServer:
         handler = type("Handler", (_Handler,), {"store": self.store})
         self.httpd = ThreadingHTTPServer((host, port), handler)
         self.httpd.daemon_threads = True
+        self.httpd.stalls = []  # fault injection rules (POST /debug/stall, or stall() below)
         self.port = self.httpd.server_address[1]
         self.url = "http://%s:%d" % (host, self.port)
         self.thread = threading.Thread(target=self.httpd.serve_forever, daemon=True)
@@ -119,6 +138,11 @@ class FakeApiServer:
     def start(self):
         self.thread.start()
         return self
+
+    def stall(self, seconds: float, path_prefix: str = "/", user_agent: str = ""):
+        """Stop answering matching requests for ``seconds`` (requests arriving meanwhile hang until then)."""
+        self.httpd.stalls.append({"until": time.time() + seconds, "path_prefix": path_prefix,
+                                  "user_agent": user_agent})
 
     def stop(self):
         self.httpd.shutdown()

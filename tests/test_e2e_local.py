@@ -112,18 +112,26 @@ def test_cpp_e2e_binary_tap():
         assert r.stdout.splitlines()[:2] == ["1..1", "ok 1 - Successfully ran TfJob"]
 
 
-def _leader(c):
-    ep = c.client.get("/api/v1/namespaces/default/endpoints/tf-operator")
-    return json.loads(ep["metadata"]["annotations"]["control-plane.alpha.kubernetes.io/leader"])
+def _leader(c, lock="leases"):
+    """The election record as {holderIdentity, leaseDurationSeconds, leaderTransitions}, from either lock."""
+    if lock == "endpoints":
+        ep = c.client.get("/api/v1/namespaces/default/endpoints/tf-operator")
+        return json.loads(ep["metadata"]["annotations"]["control-plane.alpha.kubernetes.io/leader"])
+    sp = c.client.get("/apis/coordination.k8s.io/v1/namespaces/default/leases/tf-operator")["spec"]
+    return {"holderIdentity": sp["holderIdentity"], "leaseDurationSeconds": sp["leaseDurationSeconds"],
+            "leaderTransitions": sp.get("leaseTransitions", 0)}
 
 
-def test_leader_election_failover():
-    """Two operator replicas (chart replicas=2): one leads on Endpoints tf-operator, the standby takes over when
-    the leader dies, and the new leader reconciles jobs (reference: cmd/tf_operator/main.go:125-148,
+@pytest.mark.parametrize("lock", ["leases", "endpoints"])
+def test_leader_election_failover(lock):
+    """Two operator replicas (chart replicas=2): one leads on the tf-operator lock (a coordination.k8s.io/v1 Lease
+    by default, or the reference's Endpoints annotation), the standby takes over when the leader dies, and the new
+    leader reconciles jobs (reference: cmd/tf_operator/main.go:125-148,
     pkg/util/k8sutil/election/election.go:141-265)."""
-    fast = ["-lease-duration", "2s", "-renew-deadline", "1s", "-retry-period", "200ms"]
+    fast = ["-lease-duration", "2s", "-renew-deadline", "1s", "-retry-period", "200ms",
+            "-leader-elect-resource-lock", lock]
     with LocalCluster(operator_args=fast) as c:
-        rec = _leader(c)
+        rec = _leader(c, lock)
         assert rec["holderIdentity"] == "tf-operator-local-0" and rec["leaseDurationSeconds"] == 2
         env = dict(os.environ, MY_POD_NAMESPACE="default", MY_POD_NAME="tf-operator-local-1")
         log1 = open(os.path.join(c.log_dir, "tf_operator_1.log"), "wb")
@@ -132,13 +140,13 @@ def test_leader_election_failover():
         try:
             time.sleep(1.5)  # the leader keeps renewing: the standby must not steal the lease
             assert standby.poll() is None
-            assert _leader(c)["holderIdentity"] == "tf-operator-local-0"
+            assert _leader(c, lock)["holderIdentity"] == "tf-operator-local-0"
             c.op_proc.kill()
             c.op_proc.wait()
             end = time.time() + 15
-            while _leader(c)["holderIdentity"] != "tf-operator-local-1" and time.time() < end:
+            while _leader(c, lock)["holderIdentity"] != "tf-operator-local-1" and time.time() < end:
                 time.sleep(0.1)
-            rec2 = _leader(c)
+            rec2 = _leader(c, lock)
             assert rec2["holderIdentity"] == "tf-operator-local-1"
             assert rec2["leaderTransitions"] == rec.get("leaderTransitions", 0) + 1
             msgs = [e["message"] for e in c.client.get("/api/v1/namespaces/default/events").get("items", [])

@@ -1,0 +1,219 @@
+"""Operator behaviour under a misbehaving API server, and the real HTTP/TLS transport.
+
+client-go gives the reference operator request timeouts, keep-alive connections, TLS hostname verification and
+full kubeconfig credentials for free (pkg/util/k8sutil/k8sutil.go:45-65); its leader election gives up at the
+renew deadline (pkg/util/k8sutil/election/election.go:192-208) and its panicTimer aborts a wedged event handler
+(pkg/controller/util.go:50-76). These tests pin the same behaviour on the C++ operator:
+
+* a job worker recovers after the API server stalls (every request times out, then service resumes);
+* a stalled leader stops leading within the renew deadline and the standby takes over only afterwards;
+* TLS against a local ``openssl s_server`` with a self-signed CA succeeds, and fails on a hostname mismatch or an
+  unknown CA; kubeconfig inline ``*-data`` credentials decode.
+"""
+import base64
+import json
+import os
+import shutil
+import socket
+import subprocess
+import time
+
+import pytest
+
+from k8s_amd.fakeapi.cluster import OPERATOR_BIN, LocalCluster
+from k8s_amd.fakeapi.server import FakeApiServer, free_port
+
+needs_op = pytest.mark.skipif(not os.path.exists(OPERATOR_BIN), reason="bin/tf_operator not built")
+
+
+def _job(name, cmd):
+    return {"apiVersion": "tensorflow.org/v1alpha1", "kind": "TfJob", "metadata": {"name": name},
+            "spec": {"replicaSpecs": [{"replicas": 1, "tfReplicaType": "MASTER", "template": {"spec": {
+                "containers": [{"name": "tensorflow", "image": "busybox", "command": ["sh", "-c", cmd]}],
+                "restartPolicy": "OnFailure"}}}]}}
+
+
+def _wait(pred, timeout, step=0.05):
+    end = time.time() + timeout
+    while time.time() < end:
+        v = pred()
+        if v:
+            return v
+        time.sleep(step)
+    return None
+
+
+@needs_op
+def test_job_worker_recovers_after_api_stall():
+    with LocalCluster(operator_args=["-request-timeout", "500ms", "-leader-elect=false"]) as c:
+        marker = os.path.join(c.log_dir, "go")
+        c.create(_job("stall", "while [ ! -f %s ]; do sleep 0.1; done; exit 0" % marker))
+        assert _wait(lambda: c.get("stall").get("status", {}).get("phase") == "Running", 20)
+        c.server.stall(3.0, user_agent="tf-operator-local-0")  # the operator's requests hang for 3 s
+        open(marker, "w").close()
+        time.sleep(3.5)
+        assert c.op_proc.poll() is None, "operator died during the stall:\n" + c.operator_log()[-2000:]
+        done = _wait(lambda: c.get("stall").get("status", {}).get("phase") == "Done", 30)
+        assert done, json.dumps(c.get("stall").get("status")) + c.operator_log()[-2000:]
+        assert c.get("stall")["status"]["state"] == "Succeeded"
+        assert "timed out" in c.operator_log()  # the stalled reconciles failed by deadline, not by hanging
+
+
+@needs_op
+def test_stalled_leader_steps_down_before_standby_takes_over():
+    """Renewals bounded by the renew deadline: the leader whose API calls hang exits within renew_deadline (+ one
+    retry period), and the standby acquires only after the lease expired on its own clock: no overlap."""
+    renew, lease = 1.0, 3.0
+    args = ["-lease-duration", "%gs" % lease, "-renew-deadline", "%gs" % renew, "-retry-period", "200ms",
+            "-request-timeout", "30s"]  # the per-request default is far longer than the renew deadline
+    with LocalCluster(operator_args=args) as c:
+        lease_path = "/apis/coordination.k8s.io/v1/namespaces/default/leases/tf-operator"
+        holder = lambda: c.client.get(lease_path)["spec"]["holderIdentity"]  # noqa: E731
+        assert _wait(lambda: c.client.exists(lease_path) and holder() == "tf-operator-local-0", 10)
+        env = dict(os.environ, MY_POD_NAMESPACE="default", MY_POD_NAME="tf-operator-local-1")
+        log1 = open(os.path.join(c.log_dir, "tf_operator_1.log"), "wb")
+        standby = subprocess.Popen([OPERATOR_BIN, "-master", c.url, "-reconcile-interval", "300ms"] + args, env=env,
+                                   stdout=log1, stderr=subprocess.STDOUT)
+        try:
+            time.sleep(1.0)
+            assert holder() == "tf-operator-local-0"
+            t_stall = time.time()
+            c.server.stall(60.0, user_agent="tf-operator-local-0")
+            t_exit = None
+            t_acq = None
+            end = time.time() + 20
+            while time.time() < end and (t_exit is None or t_acq is None):
+                if t_exit is None and c.op_proc.poll() is not None:
+                    t_exit = time.time()
+                if t_acq is None and holder() == "tf-operator-local-1":
+                    t_acq = time.time()
+                time.sleep(0.02)
+            assert t_exit is not None, "stalled leader kept running:\n" + c.operator_log()[-2000:]
+            assert c.op_proc.returncode != 0  # leadership lost is fatal, as in the reference
+            assert t_exit - t_stall <= renew + 0.2 + 1.0, t_exit - t_stall
+            assert t_acq is not None, open(os.path.join(c.log_dir, "tf_operator_1.log")).read()[-2000:]
+            assert t_acq > t_exit, (t_acq - t_stall, t_exit - t_stall)  # never two leaders
+            assert "leader election lost" in c.operator_log()
+        finally:
+            standby.kill()
+            standby.wait()
+            log1.close()
+
+
+# ------------------------------------------------------------------------------------------------- TLS
+def _openssl(*args, cwd):
+    subprocess.run(["openssl", *args], cwd=cwd, check=True, capture_output=True)
+
+
+@pytest.fixture(scope="module")
+def pki(tmp_path_factory):
+    if not shutil.which("openssl"):
+        pytest.skip("openssl CLI not available")
+    d = str(tmp_path_factory.mktemp("pki"))
+    _openssl("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", "ca.key", "-out", "ca.pem", "-days", "2",
+             "-subj", "/CN=k8s-amd-test-ca", cwd=d)
+    with open(os.path.join(d, "ext.cnf"), "w") as f:
+        f.write("subjectAltName=DNS:localhost,IP:127.0.0.1\n")
+    _openssl("req", "-newkey", "rsa:2048", "-nodes", "-keyout", "srv.key", "-out", "srv.csr", "-subj", "/CN=localhost",
+             cwd=d)
+    _openssl("x509", "-req", "-in", "srv.csr", "-CA", "ca.pem", "-CAkey", "ca.key", "-CAcreateserial", "-out",
+             "srv.pem", "-days", "2", "-extfile", "ext.cnf", cwd=d)
+    # a second, unrelated CA
+    _openssl("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", "other.key", "-out", "other.pem", "-days",
+             "2", "-subj", "/CN=other-ca", cwd=d)
+    return d
+
+
+@pytest.fixture
+def tls_server(pki):
+    port = free_port()
+    p = subprocess.Popen(["openssl", "s_server", "-accept", "127.0.0.1:%d" % port, "-cert", "srv.pem", "-key",
+                          "srv.key", "-www", "-quiet"], cwd=pki, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    ok = _wait(lambda: socket.socket().connect_ex(("127.0.0.1", port)) == 0, 10)
+    if not ok:
+        p.kill()
+        pytest.skip("openssl s_server did not start")
+    yield port
+    p.kill()
+    p.wait()
+
+
+def _op():
+    from k8s_amd import _operator
+
+    return _operator
+
+
+def test_tls_verifies_ca_and_hostname(pki, tls_server):
+    op = _op()
+    ca = open(os.path.join(pki, "ca.pem")).read()
+    other = open(os.path.join(pki, "other.pem")).read()
+    url = "https://127.0.0.1:%d" % tls_server
+    code, err, _ = op.http_request(url, ca_data=ca, server_name="localhost", timeout_ms=5000)
+    assert code == 200, err
+    code, err, _ = op.http_request(url, ca_data=ca, timeout_ms=5000)  # IP SAN 127.0.0.1
+    assert code == 200, err
+    code, err, _ = op.http_request(url, ca_data=ca, server_name="wrong.example", timeout_ms=5000)
+    assert code == 0 and "TLS" in err and "mismatch" in err, err
+    code, err, _ = op.http_request(url, ca_data=other, server_name="localhost", timeout_ms=5000)
+    assert code == 0 and "TLS" in err, err
+
+
+def test_request_deadline_on_a_silent_server():
+    """A TCP peer that accepts but never answers: the request fails at its deadline instead of hanging."""
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(4)
+    try:
+        t0 = time.time()
+        code, err, _ = _op().http_request("http://127.0.0.1:%d" % srv.getsockname()[1], timeout_ms=400)
+        assert code == 0 and "timed out" in err, err
+        assert time.time() - t0 < 3.0
+    finally:
+        srv.close()
+
+
+def test_keepalive_reuses_connections():
+    with FakeApiServer() as s:
+        seen = set()
+        orig = s.httpd.RequestHandlerClass.handle_one_request
+
+        def spy(self):
+            seen.add(self.client_address)
+            return orig(self)
+
+        s.httpd.RequestHandlerClass.handle_one_request = spy
+        code, err, body = _op().http_request(s.url, path="/version", repeat=20)
+        assert code == 200, err
+        assert json.loads(body)["major"] == "1"
+        assert len(seen) == 1, seen  # 20 requests over one connection
+
+
+def test_kubeconfig_inline_credentials(tmp_path):
+    ca, crt, key = b"-----BEGIN CERTIFICATE-----\nCA\n", b"CRT", b"KEY"
+    kc = {
+        "apiVersion": "v1", "kind": "Config", "current-context": "amd",
+        "clusters": [{"name": "c1", "cluster": {"server": "https://10.0.0.1:6443",
+                                                 "certificate-authority-data": base64.b64encode(ca).decode(),
+                                                 "tls-server-name": "kubernetes"}}],
+        "contexts": [{"name": "amd", "context": {"cluster": "c1", "user": "u1"}}],
+        "users": [{"name": "u1", "user": {"client-certificate-data": base64.b64encode(crt).decode(),
+                                           "client-key-data": base64.b64encode(key).decode()}}],
+    }
+    d = _op().kubeconfig(json.dumps(kc))
+    assert (d["host"], d["port"], d["tls"]) == ("10.0.0.1", 6443, True)
+    assert d["ca_data"] == ca.decode() and d["cert_data"] == "CRT" and d["key_data"] == "KEY"
+    assert d["tls_server_name"] == "kubernetes"
+    # exec credential plugin
+    plug = tmp_path / "cred.sh"
+    plug.write_text("#!/bin/sh\necho '{\"apiVersion\":\"client.authentication.k8s.io/v1\",\"kind\":\"ExecCredential\","
+                    "\"status\":{\"token\":\"tok-'$CRED_SUFFIX'\"}}'\n")
+    plug.chmod(0o755)
+    kc["users"][0]["user"] = {"exec": {"apiVersion": "client.authentication.k8s.io/v1", "command": str(plug),
+                                       "env": [{"name": "CRED_SUFFIX", "value": "42"}]}}
+    assert _op().kubeconfig(json.dumps(kc))["token"] == "tok-42"
+    # tokenFile
+    tf = tmp_path / "token"
+    tf.write_text("file-token\n")
+    kc["users"][0]["user"] = {"tokenFile": str(tf)}
+    assert _op().kubeconfig(json.dumps(kc))["token"] == "file-token"
