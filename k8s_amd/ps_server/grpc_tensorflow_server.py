@@ -184,6 +184,10 @@ class _TaskHandler(socketserver.BaseRequestHandler):
                 send_msg(self.request, {"ok": False, "error": "unknown op %r" % op})
 
 
+def _bool_arg(v: str) -> bool:
+    return v.lower() == "true"
+
+
 def serve(cluster, job_name, task_id, verbose=False) -> int:
     addr = resolve(cluster[job_name][task_id])
     host, port = addr.rsplit(":", 1)
@@ -197,15 +201,22 @@ def serve(cluster, job_name, task_id, verbose=False) -> int:
     return 0
 
 
-def main(argv=None):
+def build_parser() -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(description="Run a default parameter server for a TfJob.")
     p.add_argument("--cluster_spec", type=str, help="Cluster spec: 'job|host:port;host:port,job2|host:port'")
     p.add_argument("--job_name", type=str, help="Job name: e.g., ps")
     p.add_argument("--task_id", type=int, default=0, help="Task index, e.g., 0")
     p.add_argument("--gpu_memory_fraction", type=float, default=1.0,
                    help="Fraction of GPU memory allocated (per-process cap via torch)")
-    p.add_argument("--verbose", type=bool, default=False, help="Verbose mode")
-    a = p.parse_args(argv)
+    # the reference registers type "bool" as `v.lower() == "true"` with nargs="?" / const=True
+    # (/root/reference/grpc_tensorflow_server/grpc_tensorflow_server.py:150-156): a bare --verbose is True,
+    # --verbose=true / --verbose True are True, --verbose False (or anything else) is False
+    p.add_argument("--verbose", type=_bool_arg, nargs="?", const=True, default=False, help="Verbose mode")
+    return p
+
+
+def main(argv=None):
+    a = build_parser().parse_args(argv)
     cluster = parse_cluster_spec(a.cluster_spec, a.job_name, a.task_id)
     torch, dev = _device()
     if torch is not None and dev is not None and dev.type == "cuda" and a.gpu_memory_fraction < 1.0:
