@@ -44,7 +44,7 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     # 1024 images per GPU (41 GB peak of 288 GB HBM, reported as peak_mem_gb): measured on MI355X 9102 img/s vs
     # 8913 at 768, 8498 at 512 and 7535 at 256 -- the 7x7 / 14x14 layers fill the 256 CUs only at large batch
-    # (profiles/r01_batch_sweep.md); the gfx950 autotune seed covers all four batches
+    # (profiles/r01_batch_sweep.md)
     ap.add_argument("--batch", type=int, default=1024, help="per-GPU batch")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
@@ -88,7 +88,7 @@ def main(argv=None):
 
     for i in range(a.warmup):
         loss = step()
-        if info.rank == 0:  # progress on stderr (the first step may autotune unseen shapes for minutes)
+        if info.rank == 0:  # progress on stderr (the first step JIT-loads kernels)
             print("warmup step %d/%d issued" % (i + 1, a.warmup), file=sys.stderr, flush=True)
     sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
     sync()
@@ -133,10 +133,10 @@ def main(argv=None):
         }
         print(json.dumps(out), flush=True)
         if dev.type == "cuda":
-            from k8s_amd.ops import autotune, conv
+            from k8s_amd.ops import conv, gemm
 
             print("conv paths: %s" % json.dumps(conv.STATS), file=sys.stderr)
-            print("autotune: %s" % json.dumps(autotune.choices(), sort_keys=True), file=sys.stderr)
+            print("gemm fallbacks: %s" % json.dumps(gemm.FALLBACKS), file=sys.stderr)
     kdist.destroy()
 
 

@@ -78,6 +78,20 @@ __device__ __forceinline__ void store8(uint16_t* p, const float (&o)[8]) {
   *reinterpret_cast<bf16x8_t*>(p) = v;
 }
 
+// Division by a runtime-invariant divisor as multiply-high + shift (valid for 0 <= n < 2^31).
+struct FastDiv {
+  uint32_t d, m, s;
+  __device__ __forceinline__ int div(int n) const { return (int)((__umulhi((uint32_t)n, m) + (uint32_t)n) >> s); }
+};
+inline FastDiv make_fastdiv(int d) {
+  FastDiv f;
+  f.d = (uint32_t)d;
+  f.s = 0;
+  while ((1u << f.s) < f.d) ++f.s;
+  f.m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << f.s) - f.d)) / f.d + 1);
+  return f;
+}
+
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 // Memory-bound launch sizing: cap at 256 CUs x 8 blocks and grid-stride.

@@ -41,20 +41,6 @@ constexpr int GEMM_THREADS = 256;
 // 16-byte zero line for out-of-image implicit-GEMM loads
 __device__ __attribute__((aligned(64))) uint16_t g_zero_page[64];
 
-// Division by a runtime-invariant divisor as multiply-high + shift (valid for 0 <= n < 2^31).
-struct FastDiv {
-  uint32_t d, m, s;
-  __device__ __forceinline__ int div(int n) const { return (int)((__umulhi((uint32_t)n, m) + (uint32_t)n) >> s); }
-};
-static inline FastDiv make_fastdiv(int d) {
-  FastDiv f;
-  f.d = (uint32_t)d;
-  f.s = 0;
-  while ((1u << f.s) < f.d) ++f.s;
-  f.m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << f.s) - f.d)) / f.d + 1);
-  return f;
-}
-
 // ----------------------------------------------------------------------------- operand sources
 // stage(): called for round 0..3, writes slot s = round*256 + tid of a 16 KB tile.
 struct KMajor {

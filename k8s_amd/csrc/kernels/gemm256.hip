@@ -217,11 +217,13 @@ struct KMaj {
     return p + (long)r * ld + c * 8;
   }
   __device__ __forceinline__ long step() const { return KS; }
-  __device__ __forceinline__ static mfma_bf16x8 frag(const char* img, int rb, int lane) {
+  // fragment in two steps: load() issues the LDS read, fin() yields the MFMA operand after the phase's wait
+  using Raw = bf16x8_t;
+  __device__ __forceinline__ static void load(Raw& r, const char* img, int rb, int lane) {
     const int row = rb + (lane & 15), c = lane >> 4;
-    const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(img + row * 64 + ((c ^ km_swz(row)) << 4));
-    return __builtin_bit_cast(mfma_bf16x8, v);
+    r = *reinterpret_cast<const bf16x8_t*>(img + row * 64 + ((c ^ km_swz(row)) << 4));
   }
+  __device__ __forceinline__ static mfma_bf16x8 fin(const Raw& r) { return __builtin_bit_cast(mfma_bf16x8, r); }
 };
 
 struct MNMaj {
@@ -238,17 +240,33 @@ struct MNMaj {
     return p + (long)kr * ld + c;
   }
   __device__ __forceinline__ long step() const { return (long)KS * ld; }
-  __device__ __forceinline__ static mfma_bf16x8 frag(const char* img, int rb, int lane) {
+  struct Raw {
+    short4_t lo, hi;
+  };
+  // transposed reads as inline asm (see tr16_asm): the destinations are tied to the phase's lgkmcnt wait
+  __device__ __forceinline__ static void load(Raw& r, const char* img, int rb, int lane) {
     const char* sub = img + (rb >> 6) * 4096;
     const int cb = rb & 63;
     const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
     const int u = (cb >> 3) + (pp >> 1);
     const int r0 = 8 * g + q, r1 = r0 + 4;
-    const char* a0 = sub + r0 * 128 + ((u ^ g256::mn128_swz(r0)) << 4) + (pp & 1) * 8;
-    const char* a1 = sub + r1 * 128 + ((u ^ g256::mn128_swz(r1)) << 4) + (pp & 1) * 8;
-    return join8(tr16(a0), tr16(a1));
+    tr16_asm(r.lo, sub + r0 * 128 + ((u ^ g256::mn128_swz(r0)) << 4) + (pp & 1) * 8);
+    tr16_asm(r.hi, sub + r1 * 128 + ((u ^ g256::mn128_swz(r1)) << 4) + (pp & 1) * 8);
   }
+  __device__ __forceinline__ static mfma_bf16x8 fin(const Raw& r) { return join8(r.lo, r.hi); }
 };
+
+// Ties every asm-read destination of a phase to one lgkmcnt(0) wait (no-op for compiler-read K-major frags).
+template <class S, int N>
+__device__ __forceinline__ void tie(typename S::Raw (&r)[N]) {
+  if constexpr (!S::kmajor) {
+    static_assert(N % 4 == 0, "tie groups of 4 fragments");
+#pragma unroll
+    for (int i = 0; i < N; i += 4)
+      K8S_LDS_TIE8("s_waitcnt lgkmcnt(0)", r[i].lo, r[i].hi, r[i + 1].lo, r[i + 1].hi, r[i + 2].lo, r[i + 2].hi,
+                   r[i + 3].lo, r[i + 3].hi);
+  }
+}
 
 template <class AS, class BS, int DIAG = 0>
 __global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, g256::Epi E, int M, int N, int K) {
@@ -308,11 +326,12 @@ __global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, 
   int slot = 0, islot = 3;  // slot of stage h, slot for stage h + 3
   for (int h = 0; h < nk; ++h) {
     const char* st = smem + slot * STAGE;
-    mfma_bf16x8 afr[8], bfr[4];
+    typename AS::Raw ar[8];
+    typename BS::Raw br[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bfr[j] = BS::frag(st + STAGE_A, wc * 64 + j * 16, lane);
+    for (int j = 0; j < 4; ++j) BS::load(br[j], st + STAGE_A, wc * 64 + j * 16, lane);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) afr[i] = AS::frag(st, wr * 128 + i * 16, lane);
+    for (int i = 0; i < 8; ++i) AS::load(ar[i], st, wr * 128 + i * 16, lane);
     if constexpr (DIAG == 0) {
       if (h + 3 < nk) {
         issue(islot);
@@ -324,6 +343,13 @@ __global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, 
       }
     }
     barrier();
+    tie<BS>(br);
+    tie<AS>(ar);
+    mfma_bf16x8 afr[8], bfr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = BS::fin(br[j]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) afr[i] = AS::fin(ar[i]);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 8; ++i)

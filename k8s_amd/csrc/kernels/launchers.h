@@ -84,6 +84,10 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, 
 void launch_conv_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int C, int K, int R,
                        int S, int stride, int pad, int dil, int Ho, int Wo, int splits, bool accumulate, float* ws,
                        hipStream_t st);
+// wgrad_stream.hip: tall-K weight gradient (few output tiles, millions of rows), fp32 atomics into dw
+bool wgrad_stream_eligible(int N, int Ho, int Wo, int C, int K, int R, int S);
+void launch_wgrad_stream(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int C, int K, int R,
+                         int S, int stride, int pad, int Ho, int Wo, bool accumulate, hipStream_t st);
 void launch_conv_dgrad_wtrans(const uint16_t* w, uint16_t* w2, int K, int R, int S, int C, hipStream_t st);
 
 // elementwise.hip

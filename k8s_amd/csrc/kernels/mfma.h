@@ -45,6 +45,21 @@ __device__ __forceinline__ short4_t tr16(const char* addr) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(addr));
 }
 
+// ds_read_b64_tr_b16 as inline asm. hipcc (ROCm 7.2) cannot prove that the builtin's read does not alias an
+// in-flight global_load_lds into the same LDS array and puts `s_waitcnt vmcnt(0)` in front of it, which drains a
+// counted LDS-DMA pipeline every K step (seen in the .s of gemm256r / wgrad_stream). The asm form is invisible to
+// that analysis: the caller's own vmcnt + barrier protocol orders it after the DMA, and its destination is not
+// ready until a following lds_tie() wait names it (cdna_hip_programming.md §5.7 item 1, form ii).
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(p);
+}
+__device__ __forceinline__ void tr16_asm(short4_t& r, const char* addr) {
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_addr(addr)));
+}
+// s_waitcnt lgkmcnt(0) that every listed register depends on (8 per statement; later statements after the wait)
+#define K8S_LDS_TIE8(w, a, b, c, d, e, f, g, h) \
+  asm volatile(w : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g), "+v"(h))
+
 __device__ __forceinline__ mfma_bf16x8 join8(short4_t lo, short4_t hi) {
   bf16x8_t v;
   v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];

@@ -397,6 +397,13 @@ void conv_wgrad(Tensor x, Tensor dy, Tensor dw, int64_t stride, int64_t pad, int
   TORCH_CHECK(dw.size(3) == C && C % 8 == 0 && K % 8 == 0);
   const int Ho = conv_out(H, R, stride, pad, dil), Wo = conv_out(W, S, stride, pad, dil);
   TORCH_CHECK(dy.size(0) == N && dy.size(1) == Ho && dy.size(2) == Wo && dy.size(3) == K, "dy shape mismatch");
+  const char* ws_env = std::getenv("K8S_AMD_WGRAD_STREAM");  // =0: generic split-K GEMM (A/B)
+  if (!(ws_env && ws_env[0] == '0') && dil == 1 && dy.is_contiguous() && x.is_contiguous() &&
+      k8s_amd::wgrad_stream_eligible(N, Ho, Wo, C, K, R, S)) {
+    k8s_amd::launch_wgrad_stream(cbf(x), cbf(dy), f32(dw), N, H, W, C, K, R, S, (int)stride, (int)pad, Ho, Wo,
+                                 accumulate, cur_stream());
+    return;
+  }
   int sp = splits <= 0 ? k8s_amd::gemm_choose_splits(K, R * S * C, N * Ho * Wo) : (int)splits;
   Tensor ws;
   if (sp > 1) ws = torch::empty({k8s_amd::gemm_splitk_workspace(K, R * S * C, sp)}, dw.options());
@@ -593,6 +600,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("norm_bwd", &norm_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
+  m.def("wgrad_stream_eligible", &k8s_amd::wgrad_stream_eligible, "tall-K weight-gradient kernel takes this shape");
   m.def("gemm", &gemm, py::arg("a"), py::arg("a_kmajor"), py::arg("b"), py::arg("b_kmajor"), py::arg("out"),
         py::arg("out_f32"), py::arg("bias"), py::arg("act"), py::arg("pre"), py::arg("accumulate"), py::arg("alpha"),
         py::arg("splits"), py::arg("bnb") = py::none(), py::arg("bnb_relu_x") = py::none());

@@ -1,22 +1,16 @@
 """Measured per-shape kernel selection ("measure, don't guess").
 
-For ops with more than one implementation (our MFMA implicit-GEMM vs the
-vendor path for the same conv shape, tile variants, ...) the first call of a
-shape times every candidate on the real tensors (cuda events, median of a few
-runs) and caches the winner for the process and in a JSON file
-(``$K8S_AMD_AUTOTUNE_CACHE``, default ``~/.cache/k8s_amd/autotune-v1.json``;
-``none`` disables the file) so restarted replicas and later jobs on the node
-skip tuning -- part of the job-create -> step 0 latency. Candidates must be
-side-effect free or write to scratch while tuning.
+For an op with more than one implementation (tile variants of one of our kernels, an experimental
+schedule, ...) the first call of a shape times every candidate on the real tensors (cuda events, median
+of a few runs) and caches the winner for the process and in a JSON file (``$K8S_AMD_AUTOTUNE_CACHE``,
+default ``~/.cache/k8s_amd/autotune-v3.json``; ``none`` disables the file). Candidates must be
+side-effect free or write to scratch while tuning. ``K8S_AMD_AUTOTUNE=0`` disables tuning (always the
+first candidate).
 
-``K8S_AMD_AUTOTUNE=0`` disables tuning (always the first candidate = ours).
-
-Seed tables: ``ops/tuned/<arch>.json`` (e.g. ``gfx950.json``) hold choices measured on that
-GPU for the shipped benchmark configs and are consulted after the node cache. A fresh node
-then skips the timing runs -- and, more importantly, never builds the vendor (MIOpen)
-kernels of candidates that lost: on a cold MI355X those compiles are ~70 s of the
-job-create -> step 0 latency (profiles/r01_coldstart.md). ``K8S_AMD_AUTOTUNE_SEED=0``
-ignores the seed table.
+Since round 2 no shipped op offers a vendor candidate (MIOpen / hipBLASLt): conv and linear always run
+our kernels for shapes inside their contract and count + warn on the rest (``conv.STATS``,
+``gemm.FALLBACKS``), so the seed tables of round 1 are gone. The A/B scripts under ``scripts/`` use
+``_time`` as their timer.
 """
 from __future__ import annotations
 
@@ -38,7 +32,7 @@ def enabled() -> bool:
     return os.environ.get("K8S_AMD_AUTOTUNE", "1") != "0"
 
 
-CACHE_VERSION = "v2"  # bump when kernels / candidates change
+CACHE_VERSION = "v3"  # bump when kernels / candidates change
 
 
 def cache_path():
@@ -49,34 +43,11 @@ def cache_path():
     return None if p in ("", "none") else p
 
 
-SEED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
-
-
-def _arch() -> str:
-    try:
-        if torch.cuda.is_available():
-            return torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName.split(":")[0]
-    except (RuntimeError, AttributeError):
-        pass
-    return ""
-
-
-def seed_path(arch: str = None):
-    arch = _arch() if arch is None else arch
-    return os.path.join(SEED_DIR, arch + ".json") if arch else None
-
-
 def _load_cache():
     global _loaded
     if _loaded:
         return
     _loaded = True
-    sp = seed_path() if os.environ.get("K8S_AMD_AUTOTUNE_SEED", "1") != "0" else None
-    if sp and os.path.exists(sp):
-        try:
-            _cache.update(json.load(open(sp)))
-        except (ValueError, OSError):
-            pass
     p = cache_path()
     if p and os.path.exists(p):
         try:
@@ -114,8 +85,8 @@ def _time(fn, reps=3) -> float:
     return ts[len(ts) // 2]
 
 
-# A vendor candidate must beat ours (candidate 0) by this margin: near-ties flip between runs on timing noise,
-# and every vendor choice costs a kernel build (MIOpen) on a fresh node.
+# Another candidate must beat the default (candidate 0) by this margin: near-ties flip between runs on
+# timing noise.
 MARGIN = float(os.environ.get("K8S_AMD_AUTOTUNE_MARGIN", "0.03"))
 
 

@@ -13,19 +13,22 @@ Activations NHWC bf16, weights KRSC bf16. Per product:
                           conv of dy with the taps r = a + pad - s*d (d = row offset into dy), written
                           through the GEMM epilogue's sub-grid row map; parities with no taps are zero
 
-Shapes outside those rules and CPU
-tensors run through ATen's convolution on a channels-last view (MIOpen on
-ROCm). Where both paths can run a shape, ``ops.autotune`` times them once on
-the real tensors (the vendor forward is charged for the extra BatchNorm
-statistics pass it implies) and the faster one is used from then on;
-``STATS`` / ``autotune.choices()`` show which path each layer takes.
+Every ResNet-50 shape runs on these kernels (plus the streaming tall-K weight gradient of
+``csrc/kernels/wgrad_stream.hip`` for the 1x1 / strided layers with few output tiles): there is no vendor
+candidate in the dispatch. Round 1 timed MIOpen against our kernels per shape; with the streaming weight
+gradient the whole-step difference of forcing our kernels everywhere measured at noise level (ResNet-50 b1024:
+8884/8869 vs 8967/8878 img/s, scripts/gpurun/bench_ab.sh) and a cold node no longer builds MIOpen kernels
+(~16 s of the job-create -> step 0 latency in round 1, profiles/r01_coldstart.md). Shapes outside the kernels'
+contract (C or K not a multiple of 8, dilation, CPU tensors) go through ATen's convolution on a channels-last
+view; on the GPU they are counted in ``STATS`` and warned about once.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn.functional as F
 
-from k8s_amd.ops import autotune
+import warnings
+
 from k8s_amd.ops._ext import load as _load
 
 import os
@@ -59,20 +62,21 @@ def _key(op, x, w, stride, padding):
 
 
 def fwd_uses_hip(x, w, stride, padding) -> bool:
-    """Whether the forward of this shape runs on our kernel (tuned against the vendor conv)."""
-    if not fwd_ok(x, w):
-        return False
-    C_ = _load()
-    K = w.shape[0]
+    """Whether the forward of this shape runs on our kernel (every shape inside its contract does)."""
+    return fwd_ok(x, w)
 
-    def hip():
-        st = torch.zeros(C_.conv_stat_replicas, 2, K, device=x.device)
-        C_.conv_fwd(x, w, stride, padding, 1, False, None, 0, st)
 
-    def aten():  # + one read of y: the statistics pass BatchNorm then has to run itself
-        _nhwc(F.conv2d(_nchw(x), _nchw(w), None, stride, padding)).view(-1, K).sum(0)
+_WARNED = set()
 
-    return autotune.choose(_key("conv_fwd", x, w, stride, padding), [("hip", hip), ("aten", aten)]) == "hip"
+
+def _vendor(op, x, w, stride, padding):
+    """Count (and on the GPU warn once about) a product that has to use ATen/MIOpen."""
+    STATS["aten_" + op] += 1
+    if x.is_cuda:
+        key = _key("conv_" + op, x, w, stride, padding)
+        if key not in _WARNED:
+            _WARNED.add(key)
+            warnings.warn("k8s_amd conv: %s is outside the MFMA kernels' shape contract; using ATen" % key)
 
 
 def conv_fwd(x, w, stride, padding, stats=None):
@@ -81,7 +85,7 @@ def conv_fwd(x, w, stride, padding, stats=None):
     if fwd_uses_hip(x, w, stride, padding):
         STATS["hip_fwd"] += 1
         return _load().conv_fwd(x, w, stride, padding, 1, False, None, 0, stats)
-    STATS["aten_fwd"] += 1
+    _vendor("fwd", x, w, stride, padding)
     return _nhwc(F.conv2d(_nchw(x), _nchw(w), None, stride, padding))
 
 
@@ -93,10 +97,13 @@ def _aten_bwd(gy, x, w, stride, padding, need_dx, need_dw):
 
 
 def _wgrad_hip(C_, gy, x, out, stride, padding, acc):
-    K, C = out.shape[0], out.shape[-1]
-    R, S = out.shape[1], out.shape[2]
-    if R == 1 and S == 1 and stride == 1 and padding == 0:
-        # 1x1 / stride 1: dW = dY^T . X as a plain tall-K GEMM (both operands read M-major, no im2col)
+    """dW (fp32, written or accumulated into ``out``): the streaming tall-K kernel where it applies (1x1 and
+    strided layers with few output tiles; decided in the binding), a plain split-K GEMM for other 1x1 / stride 1
+    layers (no im2col decode), else the implicit-GEMM split-K kernel."""
+    K, R, S, C = out.shape
+    N, Ho, Wo = gy.shape[0], gy.shape[1], gy.shape[2]
+    if (R == 1 and S == 1 and stride == 1 and padding == 0
+            and not C_.wgrad_stream_eligible(N, Ho, Wo, C, K, R, S)):
         C_.gemm(gy.reshape(-1, K), False, x.reshape(-1, C), False, out.view(K, C), True, None, 0, None, acc, 1.0, 0)
     else:
         C_.conv_wgrad(x, gy, out, stride, padding, 1, 0, acc)
@@ -186,55 +193,28 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, bn_link=No
     # ---- weight gradient
     dw_done = False
     if hip and C % 8 == 0 and K % 8 == 0 and p is not None and p.grad.dtype == torch.float32:
-        choice = autotune.choose(_key("conv_wgrad", x, w, stride, padding), [
-            ("hip", lambda: _wgrad_hip(C_, gy, x, torch.empty(w.shape, device=w.device, dtype=torch.float32),
-                                       stride, padding, False)),
-            ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, False, True))])
-        if choice == "hip":
-            STATS["hip_wgrad"] += 1
-            acc = p.written
-            _wgrad_hip(C_, gy, x, p.grad.view(w.shape), stride, padding, acc)
-            if acc:
-                p.store._notify(p)
-            else:
-                p.store.mark_written(p)
-            dw_done = True
+        STATS["hip_wgrad"] += 1
+        acc = p.written
+        _wgrad_hip(C_, gy, x, p.grad.view(w.shape), stride, padding, acc)
+        if acc:
+            p.store._notify(p)
+        else:
+            p.store.mark_written(p)
+        dw_done = True
     # ---- data gradient
     dx = None
     if need_dx:
-        use_hip = False
         if hip and stride == 1 and K % 64 == 0 and C % 8 == 0:
-            if addend is None:
-                use_hip = autotune.choose(_key("conv_dgrad", x, w, stride, padding), [
-                    ("hip", lambda: _dgrad_hip(C_, gy, w, padding)),
-                    ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, True, False))]) == "hip"
-            else:  # compare the fused accumulate against the vendor dgrad + a separate add
-                use_hip = autotune.choose(_key("conv_dgrad_acc", x, w, stride, padding), [
-                    ("hip", lambda: _dgrad_hip(C_, gy, w, padding, torch.empty_like(addend))),
-                    ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, True, False)[0].add_(addend))]) == "hip"
-        elif hip and strided_dgrad_ok(gy, w, stride, padding):
-            H, W_ = x.shape[1], x.shape[2]
-            if addend is None:
-                choice = autotune.choose(_key("conv_dgrad_s", x, w, stride, padding), [
-                    ("hip", lambda: _dgrad_strided_hip(C_, gy, w, stride, padding, H, W_)),
-                    ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, True, False))])
-            else:  # the fused accumulate against the vendor dgrad + a separate add
-                scratch = torch.empty_like(addend)  # timing only: accumulates onto garbage, never read
-                choice = autotune.choose(_key("conv_dgrad_s_acc", x, w, stride, padding), [
-                    ("hip", lambda: _dgrad_strided_hip(C_, gy, w, stride, padding, H, W_, scratch)),
-                    ("aten", lambda: _aten_bwd(gy, x, w, stride, padding, True, False)[0].add_(addend))])
-            if choice == "hip":
-                STATS["hip_dgrad"] += 1
-                dx = _dgrad_strided_hip(C_, gy, w, stride, padding, H, W_, addend)
-                return _finish_dw(dx, dw_done, p, gy, x, w, stride, padding)
-        if use_hip:
             STATS["hip_dgrad"] += 1
             bnb = None
             if BN_LINK and bn_link is not None and p is not None and (R == 1 or addend is None):
                 bnb = bn_link.epilogue_args(p.store, gy.device)
             dx = _dgrad_hip(C_, gy, w, padding, addend, bnb)
+        elif hip and strided_dgrad_ok(gy, w, stride, padding):
+            STATS["hip_dgrad"] += 1
+            dx = _dgrad_strided_hip(C_, gy, w, stride, padding, x.shape[1], x.shape[2], addend)
         else:
-            STATS["aten_dgrad"] += 1
+            _vendor("dgrad", x, w, stride, padding)
             dx, _ = _aten_bwd(gy, x, w, stride, padding, True, False)
             if addend is not None:
                 dx = dx + addend
@@ -243,7 +223,7 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, bn_link=No
 
 def _finish_dw(dx, dw_done, p, gy, x, w, stride, padding):
     if not dw_done and p is not None:
-        STATS["aten_wgrad"] += 1
+        _vendor("wgrad", x, w, stride, padding)
         _, dw = _aten_bwd(gy, x, w, stride, padding, False, True)
         p.store.deposit(p, dw)
     return dx

@@ -113,9 +113,13 @@ def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True):
         db = _load().colsum(g.contiguous())
     else:
         db = g.float().sum(0)
-    if hip_ok(g, x, w) and _shape_ok(M, N, K) and N % 64 == 0:
+    if hip_ok(g, x, w) and _shape_ok(M, N, K):
         g = g.contiguous()
-        dx = mm(g, w, True, False)
+        if N % 64:  # dgrad reduces over N: zero-pad it to the kernel's 64-deep k-step (e.g. a 1000-class head)
+            Np = (N + 63) // 64 * 64
+            dx = mm(torch.nn.functional.pad(g, (0, Np - N)), torch.nn.functional.pad(w, (0, 0, 0, Np - N)), True, False)
+        else:
+            dx = mm(g, w, True, False)
         if pw is not None and store is not None and pw.grad.dtype == torch.float32:
             acc = pw.written
             mm(g, x, False, False, out=pw.grad, out_f32=True, accumulate=acc, splits=0)

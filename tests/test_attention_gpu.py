@@ -27,6 +27,8 @@ CASES = [
     (1, 64, 2, 2, 64, True, None),
     (1, 1100, 4, 2, 64, True, None),        # D = 64 long sequence: 128-wide key / query tiles
     (2, 1024, 2, 2, 64, False, [1024, 900]),
+    (1, 4096, 32, 8, 128, True, None),      # Llama-3-8B attention at the benchmarked sequence length
+    (1, 2048, 12, 12, 64, False, None),     # BERT-style heads at a long sequence
 ]
 
 

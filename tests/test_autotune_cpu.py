@@ -1,4 +1,4 @@
-"""ops/autotune.py: the shipped gfx950 seed table and the margin a vendor candidate must win by."""
+"""ops/autotune.py: the node cache and the margin a non-default candidate must win by."""
 import json
 import os
 
@@ -15,26 +15,23 @@ def fresh(monkeypatch):
     return autotune
 
 
-def test_seed_table_loaded_for_gfx950(fresh, monkeypatch):
-    monkeypatch.setattr(fresh, "_arch", lambda: "gfx950")
-    seed = json.load(open(os.path.join(fresh.SEED_DIR, "gfx950.json")))
-    assert any(k.startswith("conv_fwd|256x56x56x64|") for k in seed)  # the ResNet-50 b256 benchmark shapes
-    assert set(seed.values()) <= {"hip", "aten", "blas"}
+def test_node_cache_round_trip(fresh, monkeypatch, tmp_path):
+    p = tmp_path / "cache.json"
+    monkeypatch.setenv("K8S_AMD_AUTOTUNE_CACHE", str(p))
+    p.write_text(json.dumps({"op|x": "b"}))
     fresh._load_cache()
-    assert all(fresh._cache[k] == v for k, v in seed.items())
+    assert fresh.choices() == {"op|x": "b"}
+    assert fresh.choose("op|x", [("a", lambda: 0), ("b", lambda: 0)]) == "b"
 
 
-def test_seed_can_be_disabled(fresh, monkeypatch):
-    monkeypatch.setattr(fresh, "_arch", lambda: "gfx950")
-    monkeypatch.setenv("K8S_AMD_AUTOTUNE_SEED", "0")
-    fresh._load_cache()
-    assert fresh._cache == {}
+def test_no_vendor_seed_tables_ship():
+    """Round 2 retired MIOpen / hipBLASLt from the dispatch: nothing may pin a vendor kernel per shape."""
+    assert not os.path.exists(os.path.join(os.path.dirname(autotune.__file__), "tuned"))
 
 
-def test_vendor_needs_margin(fresh, monkeypatch):
+def test_candidate_needs_margin(fresh, monkeypatch):
     monkeypatch.setattr(fresh.torch.cuda, "is_available", lambda: True)
     monkeypatch.setattr(fresh, "_time", lambda fn, reps=5: fn())
-    monkeypatch.setattr(fresh, "_arch", lambda: "")
     assert fresh.choose("op|a", [("hip", lambda: 1.0), ("aten", lambda: 0.98)]) == "hip"  # within 3 %
     assert fresh.choose("op|b", [("hip", lambda: 1.0), ("aten", lambda: 0.90)]) == "aten"
     assert fresh.choose("op|c", [("hip", lambda: 1.0), ("aten", lambda: 2.0)]) == "hip"

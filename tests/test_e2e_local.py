@@ -149,9 +149,14 @@ def test_leader_election_failover(lock):
             rec2 = _leader(c, lock)
             assert rec2["holderIdentity"] == "tf-operator-local-1"
             assert rec2["leaderTransitions"] == rec.get("leaderTransitions", 0) + 1
-            msgs = [e["message"] for e in c.client.get("/api/v1/namespaces/default/events").get("items", [])
-                    if e.get("reason") == "LeaderElection"]
-            assert "tf-operator-local-0 became leader" in msgs and "tf-operator-local-1 became leader" in msgs
+            def msgs():
+                return [e["message"] for e in c.client.get("/api/v1/namespaces/default/events").get("items", [])
+                        if e.get("reason") == "LeaderElection"]
+
+            end = time.time() + 10  # the event is posted right after the lock write: poll, do not race it
+            while "tf-operator-local-1 became leader" not in msgs() and time.time() < end:
+                time.sleep(0.1)
+            assert "tf-operator-local-0 became leader" in msgs() and "tf-operator-local-1 became leader" in msgs()
             c.create(_job("afterfailover", "exit 0"))
             assert _wait_state(c, "afterfailover", {"Succeeded"})["status"]["state"] == "Succeeded"
         finally:

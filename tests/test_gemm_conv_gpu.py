@@ -285,3 +285,23 @@ def test_conv_dgrad_strided_accumulate(cuda, N, H, C, K, R, st, pad):
     xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
     F.conv2d(xr, w.float().permute(0, 3, 1, 2), None, st, pad).backward(dy.float().permute(0, 3, 1, 2))
     assert _rel(out, xr.grad.permute(0, 2, 3, 1) + ref_add) < 1e-2
+
+
+def test_linear_head_1000_classes_no_fallback(cuda):
+    """The ResNet-50 fc (N = 1000, not a multiple of the 64-deep k-step of the dgrad product) stays on our
+    kernels: dgrad zero-pads N, fwd / wgrad need only N % 8."""
+    from k8s_amd.ops import gemm
+
+    torch.manual_seed(3)
+    M, N, K = 256, 1000, 2048
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) * 0.02).bfloat16()
+    gy = torch.randn(M, N, device=cuda).bfloat16()
+    before = dict(gemm.FALLBACKS)
+    y, saved = gemm.linear_fwd(x, w, None)
+    dx, dw, db = gemm.linear_bwd(gy, x, w, saved, None)
+    assert gemm.FALLBACKS == before
+    assert _rel(y, x.float() @ w.float().t()) < 1e-2
+    assert _rel(dx, gy.float() @ w.float()) < 1e-2
+    assert _rel(dw, gy.float().t() @ x.float()) < 1e-2
+    assert _rel(db, gy.float().sum(0)) < 1e-2
