@@ -288,7 +288,7 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 // BNB: epilogue also reduces the BatchNorm-backward statistics (Epi::bstats). A separate instantiation:
 // compiled into every kernel, that code (7 more loads per output quad) costs ~30% on the plain GEMMs even
 // when disabled at run time.
-template <class ASrc, class BSrc, int NBUF, int WM = 2, int WN = 2, bool BNB = false>
+template <class ASrc, class BSrc, int NBUF, int WM = 2, int WN = 2, bool BNB = false, bool LEAN = false>
 __global__ void __launch_bounds__(GEMM_THREADS, NBUF == 1 ? 3 : 2)
 gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
@@ -327,9 +327,9 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
 
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);  // provably wave-uniform for the M0 (LDS base) operand
   constexpr int RA = TA / (16 * GEMM_THREADS), RB = TB / (16 * GEMM_THREADS);
-  // hoisted cursors cost ~4 VGPRs per load slot: the 3-blocks/CU single-buffer kernels (170 VGPRs) with 12
-  // slots would spill, so they keep the per-tile derivation
-  constexpr bool HOIST = !(NBUF == 1 && RA + RB > 8);
+  // hoisted cursors cost ~4 VGPRs per load slot and pay off over many K tiles: the 3-blocks/CU single-buffer
+  // kernels (<= 2 K tiles, 168-VGPR budget) keep the per-tile derivation
+  constexpr bool HOIST = NBUF != 1;
   typename ASrc::Cursor ca[HOIST ? RA : 1];
   typename BSrc::Cursor cb[HOIST ? RB : 1];
   if constexpr (HOIST) {
@@ -394,119 +394,202 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
   // (large) Epi into scratch memory
   void* const ec = E.mode == 3 ? (void*)(reinterpret_cast<float*>(E.c) + (long)blockIdx.z * E.slab) : E.c;
   const int emode = E.mode == 3 ? 0 : E.mode;  // mode 3 = this split's private fp32 slab, plain stores
+  // LEAN (bf16 C, no bias / activation / pre-activation copy, mode store or accumulate; the convolution forward
+  // and the data gradients): the tile goes through LDS and leaves as 16-B row-contiguous stores, and none of the
+  // general epilogue's run-time branches are compiled in (the general instantiations are ~85 KB of code, more
+  // than the instruction cache). LDS image [BM][BN] bf16, 16-B chunk c of row r at c ^ (r % (BN / 8)).
+  uint16_t* const ctile = reinterpret_cast<uint16_t*>(smem);
+  constexpr int CPR = BN / 8;  // 16-B chunks per tile row
   float st_s[4][4], st_q[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) st_s[j][r] = st_q[j][r] = 0.f;
+  if constexpr (LEAN) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
-    if (m >= M) continue;
-    long orow = m;
-    if (E.rst) {
-      const int hw = E.rHo * E.rWo;
-      const int nimg = m / hw, rem = m - nimg * hw;
-      const int ii = rem / E.rWo, jj = rem - ii * E.rWo;
-      orow = ((long)nimg * E.rH + ii * E.rst + E.ra) * E.rW + jj * E.rst + E.rb;
+    for (int i = 0; i < 4; ++i) {
+      const int row = wm * 64 + i * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = wn * 64 + j * 16 + (lane >> 4) * 4;
+        bf16x4_t o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(acc[i][j][r] * E.alpha);
+        *reinterpret_cast<bf16x4_t*>(ctile + row * BN + (((col >> 3) ^ (row % CPR)) << 3) + (col & 4)) = o;
+      }
     }
+    __syncthreads();
+    // copy-out: thread t always handles 16-B chunk c = t % CPR of its rows (GEMM_THREADS % CPR == 0), so it
+    // also accumulates the BN statistics of those 8 columns from the bf16 values it stores
+    const bool want_stats = E.stats != nullptr;
+    float ps[8], pq[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
-      if (n >= N) continue;
-      float v[4] = {acc[i][j][0] * E.alpha, acc[i][j][1] * E.alpha, acc[i][j][2] * E.alpha, acc[i][j][3] * E.alpha};
-      const bool full = (n + 3 < N);
-      if (E.bias) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (n + r < N) v[r] += E.bias[n + r];
+    for (int r = 0; r < 8; ++r) ps[r] = pq[r] = 0.f;
+    constexpr int CHUNKS = BM * CPR;
+#pragma unroll 2
+    for (int q = tid; q < CHUNKS; q += GEMM_THREADS) {
+      const int row = q / CPR, c = q % CPR;
+      const int m = m0 + row, n = n0 + c * 8;
+      if (m >= M || n >= N) continue;
+      long orow = m;
+      if (E.rst) {
+        const int hw = E.rHo * E.rWo;
+        const int nimg = m / hw, rem = m - nimg * hw;
+        const int ii = rem / E.rWo, jj = rem - ii * E.rWo;
+        orow = ((long)nimg * E.rH + ii * E.rst + E.ra) * E.rW + jj * E.rst + E.rb;
       }
-      if (E.pre) {
-        uint16_t* pp = E.pre + orow * E.ldc + n;
-        if (full) {
-          bf16x4_t o;
+      bf16x8_t o = *reinterpret_cast<const bf16x8_t*>(ctile + row * BN + ((c ^ (row % CPR)) << 3));
+      uint16_t* cp = reinterpret_cast<uint16_t*>(ec) + orow * E.ldc + n;
+      if (emode == 1) {  // accumulate onto bf16 C: the staged value is already bf16 (two roundings, <= 1 ulp more)
+        const bf16x8_t old = *reinterpret_cast<const bf16x8_t*>(cp);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r]);
-          *reinterpret_cast<bf16x4_t*>(pp) = o;
-        } else {
-          for (int r = 0; r < 4 && n + r < N; ++r) pp[r] = f2bf(v[r]);
+        for (int r = 0; r < 8; ++r) o[r] = (short)f2bf(bf2f((uint16_t)o[r]) + bf2f((uint16_t)old[r]));
+      }
+      *reinterpret_cast<bf16x8_t*>(cp) = o;
+      if (want_stats) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float v = bf2f((uint16_t)o[r]);
+          ps[r] += v;
+          pq[r] += v * v;
         }
       }
-      if (E.act == 1) {
+    }
+    if (want_stats) {
+      // partials [GEMM_THREADS][16] in LDS, then thread (which, col) sums the GEMM_THREADS / CPR partials of its
+      // column: one atomic per (column, sum | sum of squares) per block
+      __syncthreads();
+      float* part = reinterpret_cast<float*>(smem);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-      } else if (E.act == 2) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+      for (int r = 0; r < 8; ++r) {
+        part[tid * 16 + r] = ps[r];
+        part[tid * 16 + 8 + r] = pq[r];
       }
-      if (E.stats) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float vr = E.out_f32 ? v[r] : bf2f(f2bf(v[r]));  // statistics of what is stored
-          const bool ok = n + r < N;
-          st_s[j][r] += ok ? vr : 0.f;
-          st_q[j][r] += ok ? vr * vr : 0.f;
+      __syncthreads();
+      if (tid < 2 * BN) {
+        const int col = tid % BN, which = tid / BN;
+        const int n = n0 + col;
+        if (n < N) {
+          const int c = col >> 3, r = col & 7;
+          float v = 0.f;
+#pragma unroll 4
+          for (int t = c; t < GEMM_THREADS; t += CPR) v += part[t * 16 + which * 8 + r];
+          atomicAdd(E.stats + (long)(tm % STAT_REPL) * 2 * N + (long)which * N + n, v);
         }
       }
-      if (E.out_f32) {
-        float* cp = reinterpret_cast<float*>(ec) + orow * E.ldc + n;
-        if (emode == 2) {
-          for (int r = 0; r < 4 && n + r < N; ++r) atomicAdd(cp + r, v[r]);
-        } else if (full) {
-          float4 o = make_float4(v[0], v[1], v[2], v[3]);
-          if (emode == 1) {
-            const float4 old = *reinterpret_cast<const float4*>(cp);
-            o.x += old.x; o.y += old.y; o.z += old.z; o.w += old.w;
-          }
-          *reinterpret_cast<float4*>(cp) = o;
-        } else {
+    }
+    return;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+      if (m >= M) continue;
+      long orow = m;
+      if (E.rst) {
+        const int hw = E.rHo * E.rWo;
+        const int nimg = m / hw, rem = m - nimg * hw;
+        const int ii = rem / E.rWo, jj = rem - ii * E.rWo;
+        orow = ((long)nimg * E.rH + ii * E.rst + E.ra) * E.rW + jj * E.rst + E.rb;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
+        if (n >= N) continue;
+        float v[4] = {acc[i][j][0] * E.alpha, acc[i][j][1] * E.alpha, acc[i][j][2] * E.alpha,
+                      acc[i][j][3] * E.alpha};
+        const bool full = (n + 3 < N);
+        if (E.bias) {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (n + r < N) cp[r] = (emode == 1 ? cp[r] : 0.f) + v[r];
+            if (n + r < N) v[r] += E.bias[n + r];
         }
-      } else {
-        uint16_t* cp = reinterpret_cast<uint16_t*>(ec) + orow * E.ldc + n;
-        if (full) {
-          bf16x4_t o;
-          if (emode == 1) {
-            const bf16x4_t old = *reinterpret_cast<const bf16x4_t*>(cp);
+        if (E.pre) {
+          uint16_t* pp = E.pre + orow * E.ldc + n;
+          if (full) {
+            bf16x4_t o;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] += bf2f((uint16_t)old[r]);
+            for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r]);
+            *reinterpret_cast<bf16x4_t*>(pp) = o;
+          } else {
+            for (int r = 0; r < 4 && n + r < N; ++r) pp[r] = f2bf(v[r]);
           }
+        }
+        if (E.act == 1) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r]);
-          *reinterpret_cast<bf16x4_t*>(cp) = o;
-          if constexpr (BNB) {
-            const long off = (long)m * E.ldc + n;
-            const bf16x4_t xv = *reinterpret_cast<const bf16x4_t*>(E.bx + off);
-            bf16x4_t yv;
-            if (E.by) yv = *reinterpret_cast<const bf16x4_t*>(E.by + off);
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        } else if (E.act == 2) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float xh = (bf2f((uint16_t)xv[r]) - E.bmean[n + r]) * E.binvstd[n + r];
-              bool on = true;
-              if (E.by) on = bf2f((uint16_t)yv[r]) > 0.f;
-              else if (E.brelu_x) on = bf2f(f2bf(xh * E.bgamma[n + r] + E.bbeta[n + r])) > 0.f;
-              const float g = on ? bf2f((uint16_t)o[r]) : 0.f;
-              st_s[j][r] += g;
-              st_q[j][r] += g * xh;
+          for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+        }
+        if (E.stats) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float vr = E.out_f32 ? v[r] : bf2f(f2bf(v[r]));  // statistics of what is stored
+            const bool ok = n + r < N;
+            st_s[j][r] += ok ? vr : 0.f;
+            st_q[j][r] += ok ? vr * vr : 0.f;
+          }
+        }
+        if (E.out_f32) {
+          float* cp = reinterpret_cast<float*>(ec) + orow * E.ldc + n;
+          if (emode == 2) {
+            for (int r = 0; r < 4 && n + r < N; ++r) atomicAdd(cp + r, v[r]);
+          } else if (full) {
+            float4 o = make_float4(v[0], v[1], v[2], v[3]);
+            if (emode == 1) {
+              const float4 old = *reinterpret_cast<const float4*>(cp);
+              o.x += old.x; o.y += old.y; o.z += old.z; o.w += old.w;
             }
+            *reinterpret_cast<float4*>(cp) = o;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < N) cp[r] = (emode == 1 ? cp[r] : 0.f) + v[r];
           }
         } else {
+          uint16_t* cp = reinterpret_cast<uint16_t*>(ec) + orow * E.ldc + n;
+          if (full) {
+            bf16x4_t o;
+            if (emode == 1) {
+              const bf16x4_t old = *reinterpret_cast<const bf16x4_t*>(cp);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {  // static r: keeps st_s/st_q in registers (a dynamic bound spills them)
-            if (n + r >= N) continue;
-            const uint16_t o = f2bf(v[r] + (emode == 1 ? bf2f(cp[r]) : 0.f));
-            cp[r] = o;
+              for (int r = 0; r < 4; ++r) v[r] += bf2f((uint16_t)old[r]);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r]);
+            *reinterpret_cast<bf16x4_t*>(cp) = o;
             if constexpr (BNB) {
-              const long off = (long)m * E.ldc + n + r;
-              const float xh = (bf2f(E.bx[off]) - E.bmean[n + r]) * E.binvstd[n + r];
-              bool on = true;
-              if (E.by) on = bf2f(E.by[off]) > 0.f;
-              else if (E.brelu_x) on = bf2f(f2bf(xh * E.bgamma[n + r] + E.bbeta[n + r])) > 0.f;
-              const float g = on ? bf2f(o) : 0.f;
-              st_s[j][r] += g;
-              st_q[j][r] += g * xh;
+              const long off = (long)m * E.ldc + n;
+              const bf16x4_t xv = *reinterpret_cast<const bf16x4_t*>(E.bx + off);
+              bf16x4_t yv;
+              if (E.by) yv = *reinterpret_cast<const bf16x4_t*>(E.by + off);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float xh = (bf2f((uint16_t)xv[r]) - E.bmean[n + r]) * E.binvstd[n + r];
+                bool on = true;
+                if (E.by) on = bf2f((uint16_t)yv[r]) > 0.f;
+                else if (E.brelu_x) on = bf2f(f2bf(xh * E.bgamma[n + r] + E.bbeta[n + r])) > 0.f;
+                const float g = on ? bf2f((uint16_t)o[r]) : 0.f;
+                st_s[j][r] += g;
+                st_q[j][r] += g * xh;
+              }
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {  // static r: keeps st_s/st_q in registers (a dynamic bound spills them)
+              if (n + r >= N) continue;
+              const uint16_t o = f2bf(v[r] + (emode == 1 ? bf2f(cp[r]) : 0.f));
+              cp[r] = o;
+              if constexpr (BNB) {
+                const long off = (long)m * E.ldc + n + r;
+                const float xh = (bf2f(E.bx[off]) - E.bmean[n + r]) * E.binvstd[n + r];
+                bool on = true;
+                if (E.by) on = bf2f(E.by[off]) > 0.f;
+                else if (E.brelu_x) on = bf2f(f2bf(xh * E.bgamma[n + r] + E.bbeta[n + r])) > 0.f;
+                const float g = on ? bf2f(o) : 0.f;
+                st_s[j][r] += g;
+                st_q[j][r] += g * xh;
+              }
             }
           }
         }
@@ -515,20 +598,15 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
   }
   float* const stat_out = BNB ? E.bstats : E.stats;
   if (stat_out) {
-    // lanes with equal (lane >> 4) hold the same 4 columns: reduce over the 16 row lanes, then over the two
-    // row-waves through LDS, so the block issues 4 full-wave atomic instructions (256 columns x {sum, sumsq})
-    // instead of 128 quarter-empty ones -- float atomics cost ~50 ns per wave-instruction per CU.
+    // lanes with equal (lane >> 4) hold the same 4 columns: reduce over the 16 row lanes (DPP), then over the
+    // row-waves through LDS, so the block issues 2 * BN / 64 full-wave atomic instructions instead of 128
+    // quarter-empty ones -- float atomics cost ~50 ns per wave-instruction per CU.
     float* red = reinterpret_cast<float*>(smem);  // [wm][2][BN]; the K loop's last barrier freed the tiles
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float a = st_s[j][r], b = st_q[j][r];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          a += __shfl_xor(a, o, 64);
-          b += __shfl_xor(b, o, 64);
-        }
+        const float a = row16_sum(st_s[j][r]), b = row16_sum(st_q[j][r]);
         if ((lane & 15) == 0) {
           const int col = wn * 64 + j * 16 + (lane >> 4) * 4 + r;
           red[(wm * 2 + 0) * BN + col] = a;
@@ -563,16 +641,34 @@ template <class ASrc, class BSrc>
 constexpr bool kBnbPair = (std::is_same_v<ASrc, KMajor> && std::is_same_v<BSrc, MNMajorK>) ||
                           (std::is_same_v<ASrc, ConvA> && std::is_same_v<BSrc, KMajor>);
 
-template <class ASrc, class BSrc, int WM, int WN, bool BNB>
-static void launch_tiles2(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
+template <class ASrc, class BSrc, int WM, int WN, bool BNB, bool LEAN>
+static void launch_tiles3(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
                           hipStream_t st) {
   const int tiles = ((M + 64 * WM - 1) / (64 * WM)) * ((N + 64 * WN - 1) / (64 * WN));
   if (kps <= 2 * BK)
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN, BNB>), dim3(tiles, 1, splits), dim3(GEMM_THREADS),
-                       0, st, a, b, e, M, N, K, kps);
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN, BNB, LEAN>), dim3(tiles, 1, splits),
+                       dim3(GEMM_THREADS), 0, st, a, b, e, M, N, K, kps);
   else
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2, WM, WN, BNB>), dim3(tiles, 1, splits), dim3(GEMM_THREADS),
-                       0, st, a, b, e, M, N, K, kps);
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2, WM, WN, BNB, LEAN>), dim3(tiles, 1, splits),
+                       dim3(GEMM_THREADS), 0, st, a, b, e, M, N, K, kps);
+}
+
+// the lean epilogue applies: bf16 C (16-B aligned rows), no bias / activation / pre-activation copy / atomics
+static bool lean_epi(const Epi& e, int N) {
+  return !e.out_f32 && !e.bias && !e.pre && e.act == 0 && (e.mode == 0 || e.mode == 1) && (e.ldc & 7) == 0 &&
+         (N & 7) == 0 && (reinterpret_cast<uintptr_t>(e.c) & 15) == 0;
+}
+
+template <class ASrc, class BSrc, int WM, int WN, bool BNB>
+static void launch_tiles2(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
+                          hipStream_t st) {
+  if constexpr (!BNB && !std::is_same_v<BSrc, ConvWgB>) {
+    if (lean_epi(e, N)) {
+      launch_tiles3<ASrc, BSrc, WM, WN, false, true>(a, b, e, M, N, K, kps, splits, st);
+      return;
+    }
+  }
+  launch_tiles3<ASrc, BSrc, WM, WN, BNB, false>(a, b, e, M, N, K, kps, splits, st);
 }
 
 template <class ASrc, class BSrc, int WM, int WN>

@@ -60,6 +60,21 @@ __device__ __forceinline__ void tr16_asm(short4_t& r, const char* addr) {
 #define K8S_LDS_TIE8(w, a, b, c, d, e, f, g, h) \
   asm volatile(w : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g), "+v"(h))
 
+// Sum over each 16-lane DPP row (lanes 16q .. 16q+15); every lane of the row gets the total. Four DPP adds
+// (quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror) instead of four ds_bpermute round trips
+// through the LDS crossbar, which is what __shfl_xor compiles to.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_mov<0xB1>(v);
+  v += dpp_mov<0x4E>(v);
+  v += dpp_mov<0x141>(v);
+  v += dpp_mov<0x140>(v);
+  return v;
+}
+
 __device__ __forceinline__ mfma_bf16x8 join8(short4_t lo, short4_t hi) {
   bf16x8_t v;
   v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
