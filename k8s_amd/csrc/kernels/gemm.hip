@@ -258,11 +258,11 @@ struct Epi {
                       // spread over STAT_REPL x 2N addresses instead of contending on 2N
   // BatchNorm-BACKWARD statistics of the stored (bf16) output g, which is the gradient w.r.t. a BN output:
   // bstats[rep][0][n] += sum_m g*mask, bstats[rep][1][n] += sum_m g*mask*xhat with xhat from the BN input bx
-  // and the ReLU mask from the BN output by (residual BN) or recomputed from bx (brelu_x). Replaces the
-  // separate reduction pass over g and x in the BN backward.
+  // and the ReLU mask from the packed bits bmask (residual BN), recomputed from bx (brelu_x), or all ones.
+  // Replaces the BN backward's separate reduction pass over g and x (lean epilogue only).
   float* bstats;
   const uint16_t* bx;
-  const uint16_t* by;
+  const uint8_t* bmask;
   const float *bmean, *binvstd, *bgamma, *bbeta;
   int brelu_x;
   // Sub-grid output (stride-s data gradient by output parity): GEMM row m = (n, i, j) over an rHo x rWo grid
@@ -285,10 +285,8 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 // WM x WN waves (WM * WN = 4), each owning a 64 x 64 piece: 128 x 128 tiles (2 x 2) in general, 256 x 64
 // (4 x 1) when N = 64 (the early ResNet convolutions and the stem) so no MFMA work is spent on padding.
 // Only K-major sources may sit on a 64-wide side (the MN-major swizzle assumes 256-B rows).
-// BNB: epilogue also reduces the BatchNorm-backward statistics (Epi::bstats). A separate instantiation:
-// compiled into every kernel, that code (7 more loads per output quad) costs ~30% on the plain GEMMs even
-// when disabled at run time.
-template <class ASrc, class BSrc, int NBUF, int WM = 2, int WN = 2, bool BNB = false, bool LEAN = false>
+// LEAN: the staged bf16 epilogue (also the only one with the BN-statistics reductions, forward and backward).
+template <class ASrc, class BSrc, int NBUF, int WM = 2, int WN = 2, bool LEAN = false>
 __global__ void __launch_bounds__(GEMM_THREADS, NBUF == 1 ? 3 : 2)
 gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
@@ -420,11 +418,25 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
     }
     __syncthreads();
     // copy-out: thread t always handles 16-B chunk c = t % CPR of its rows (GEMM_THREADS % CPR == 0), so it
-    // also accumulates the BN statistics of those 8 columns from the bf16 values it stores
-    const bool want_stats = E.stats != nullptr;
+    // also accumulates the BN statistics of those 8 columns from the bf16 values it stores: forward
+    // (sum, sum of squares) for Epi::stats, or backward (sum g*mask, sum g*mask*xhat) for Epi::bstats
+    float* const stat_out = E.stats ? E.stats : E.bstats;
+    const bool bwd = E.bstats != nullptr;
     float ps[8], pq[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) ps[r] = pq[r] = 0.f;
+    float bmu[8], bis[8], bsc[8], bbt[8];  // this thread's 8 channels (BN backward)
+    if (bwd) {
+      const int n = n0 + (tid % CPR) * 8;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int cn = n + r < N ? n + r : N - 1;
+        bmu[r] = E.bmean[cn];
+        bis[r] = E.binvstd[cn];
+        bsc[r] = E.brelu_x ? E.bgamma[cn] * bis[r] : 0.f;
+        bbt[r] = E.brelu_x ? E.bbeta[cn] : 0.f;
+      }
+    }
     constexpr int CHUNKS = BM * CPR;
 #pragma unroll 2
     for (int q = tid; q < CHUNKS; q += GEMM_THREADS) {
@@ -446,7 +458,21 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
         for (int r = 0; r < 8; ++r) o[r] = (short)f2bf(bf2f((uint16_t)o[r]) + bf2f((uint16_t)old[r]));
       }
       *reinterpret_cast<bf16x8_t*>(cp) = o;
-      if (want_stats) {
+      if (bwd) {
+        const long off = orow * E.ldc + n;
+        const bf16x8_t xv = *reinterpret_cast<const bf16x8_t*>(E.bx + off);
+        const uint32_t bits = E.bmask ? (uint32_t)E.bmask[off >> 3] : 0xFFu;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float xh = (bf2f((uint16_t)xv[r]) - bmu[r]) * bis[r];
+          bool on = (bits >> r) & 1u;
+          // the forward's ReLU decision, bit for bit: relu(bf16((x - mean) * gamma * invstd + beta)) > 0
+          if (E.brelu_x) on = bf2f(f2bf((bf2f((uint16_t)xv[r]) - bmu[r]) * bsc[r] + bbt[r])) > 0.f;
+          const float g = on ? bf2f((uint16_t)o[r]) : 0.f;
+          ps[r] += g;
+          pq[r] += g * xh;
+        }
+      } else if (stat_out) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           const float v = bf2f((uint16_t)o[r]);
@@ -455,7 +481,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
         }
       }
     }
-    if (want_stats) {
+    if (stat_out) {
       // partials [GEMM_THREADS][16] in LDS, then thread (which, col) sums the GEMM_THREADS / CPR partials of its
       // column: one atomic per (column, sum | sum of squares) per block
       __syncthreads();
@@ -474,7 +500,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
           float v = 0.f;
 #pragma unroll 4
           for (int t = c; t < GEMM_THREADS; t += CPR) v += part[t * 16 + which * 8 + r];
-          atomicAdd(E.stats + (long)(tm % STAT_REPL) * 2 * N + (long)which * N + n, v);
+          atomicAdd(stat_out + (long)(tm % STAT_REPL) * 2 * N + (long)which * N + n, v);
         }
       }
     }
@@ -558,45 +584,19 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r]);
             *reinterpret_cast<bf16x4_t*>(cp) = o;
-            if constexpr (BNB) {
-              const long off = (long)m * E.ldc + n;
-              const bf16x4_t xv = *reinterpret_cast<const bf16x4_t*>(E.bx + off);
-              bf16x4_t yv;
-              if (E.by) yv = *reinterpret_cast<const bf16x4_t*>(E.by + off);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const float xh = (bf2f((uint16_t)xv[r]) - E.bmean[n + r]) * E.binvstd[n + r];
-                bool on = true;
-                if (E.by) on = bf2f((uint16_t)yv[r]) > 0.f;
-                else if (E.brelu_x) on = bf2f(f2bf(xh * E.bgamma[n + r] + E.bbeta[n + r])) > 0.f;
-                const float g = on ? bf2f((uint16_t)o[r]) : 0.f;
-                st_s[j][r] += g;
-                st_q[j][r] += g * xh;
-              }
-            }
           } else {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {  // static r: keeps st_s/st_q in registers (a dynamic bound spills them)
               if (n + r >= N) continue;
               const uint16_t o = f2bf(v[r] + (emode == 1 ? bf2f(cp[r]) : 0.f));
               cp[r] = o;
-              if constexpr (BNB) {
-                const long off = (long)m * E.ldc + n + r;
-                const float xh = (bf2f(E.bx[off]) - E.bmean[n + r]) * E.binvstd[n + r];
-                bool on = true;
-                if (E.by) on = bf2f(E.by[off]) > 0.f;
-                else if (E.brelu_x) on = bf2f(f2bf(xh * E.bgamma[n + r] + E.bbeta[n + r])) > 0.f;
-                const float g = on ? bf2f(o) : 0.f;
-                st_s[j][r] += g;
-                st_q[j][r] += g * xh;
-              }
             }
           }
         }
       }
     }
   }
-  float* const stat_out = BNB ? E.bstats : E.stats;
+  float* const stat_out = E.stats;
   if (stat_out) {
     // lanes with equal (lane >> 4) hold the same 4 columns: reduce over the 16 row lanes (DPP), then over the
     // row-waves through LDS, so the block issues 2 * BN / 64 full-wave atomic instructions instead of 128
@@ -636,21 +636,16 @@ static int effective_splits(int K, int splits) {
   return (K + kps - 1) / kps;
 }
 
-// operand pairs that produce a BatchNorm output gradient (the dgrads): the only BNB instantiations
-template <class ASrc, class BSrc>
-constexpr bool kBnbPair = (std::is_same_v<ASrc, KMajor> && std::is_same_v<BSrc, MNMajorK>) ||
-                          (std::is_same_v<ASrc, ConvA> && std::is_same_v<BSrc, KMajor>);
-
-template <class ASrc, class BSrc, int WM, int WN, bool BNB, bool LEAN>
-static void launch_tiles3(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
+template <class ASrc, class BSrc, int WM, int WN, bool LEAN>
+static void launch_tiles2(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
                           hipStream_t st) {
   const int tiles = ((M + 64 * WM - 1) / (64 * WM)) * ((N + 64 * WN - 1) / (64 * WN));
   if (kps <= 2 * BK)
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN, BNB, LEAN>), dim3(tiles, 1, splits),
-                       dim3(GEMM_THREADS), 0, st, a, b, e, M, N, K, kps);
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN, LEAN>), dim3(tiles, 1, splits), dim3(GEMM_THREADS),
+                       0, st, a, b, e, M, N, K, kps);
   else
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2, WM, WN, BNB, LEAN>), dim3(tiles, 1, splits),
-                       dim3(GEMM_THREADS), 0, st, a, b, e, M, N, K, kps);
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2, WM, WN, LEAN>), dim3(tiles, 1, splits), dim3(GEMM_THREADS),
+                       0, st, a, b, e, M, N, K, kps);
 }
 
 // the lean epilogue applies: bf16 C (16-B aligned rows), no bias / activation / pre-activation copy / atomics
@@ -659,28 +654,16 @@ static bool lean_epi(const Epi& e, int N) {
          (N & 7) == 0 && (reinterpret_cast<uintptr_t>(e.c) & 15) == 0;
 }
 
-template <class ASrc, class BSrc, int WM, int WN, bool BNB>
-static void launch_tiles2(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
-                          hipStream_t st) {
-  if constexpr (!BNB && !std::is_same_v<BSrc, ConvWgB>) {
-    if (lean_epi(e, N)) {
-      launch_tiles3<ASrc, BSrc, WM, WN, false, true>(a, b, e, M, N, K, kps, splits, st);
-      return;
-    }
-  }
-  launch_tiles3<ASrc, BSrc, WM, WN, BNB, false>(a, b, e, M, N, K, kps, splits, st);
-}
-
 template <class ASrc, class BSrc, int WM, int WN>
 static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
                          hipStream_t st) {
-  if constexpr (kBnbPair<ASrc, BSrc>) {
-    if (e.bstats) {
+  if constexpr (!std::is_same_v<BSrc, ConvWgB>) {
+    if (lean_epi(e, N)) {
       launch_tiles2<ASrc, BSrc, WM, WN, true>(a, b, e, M, N, K, kps, splits, st);
       return;
     }
   }
-  if (e.bstats) throw std::runtime_error("BatchNorm-backward epilogue requested for an operand pair without it");
+  if (e.bstats) throw std::runtime_error("the BatchNorm-backward epilogue needs a plain bf16 output (lean epilogue)");
   launch_tiles2<ASrc, BSrc, WM, WN, false>(a, b, e, M, N, K, kps, splits, st);
 }
 
@@ -711,7 +694,8 @@ static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act,
   e.stats = nullptr;
   e.slab = 0;
   e.bstats = nullptr;
-  e.bx = e.by = nullptr;
+  e.bx = nullptr;
+  e.bmask = nullptr;
   e.bmean = e.binvstd = e.bgamma = e.bbeta = nullptr;
   e.brelu_x = 0;
   e.rst = e.rHo = e.rWo = e.rH = e.rW = e.ra = e.rb = 0;
@@ -775,7 +759,7 @@ static void apply_bnbwd(Epi& e, const BnBwdEpi* bb) {
   if (!bb) return;
   e.bstats = bb->stats;
   e.bx = bb->x;
-  e.by = bb->y;
+  e.bmask = bb->mask;
   e.bmean = bb->mean;
   e.binvstd = bb->invstd;
   e.bgamma = bb->gamma;

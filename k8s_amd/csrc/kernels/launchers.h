@@ -59,7 +59,7 @@ int gemm_choose_splits(int M, int N, int K);
 struct BnBwdEpi {
   float* stats;
   const uint16_t* x;  // BN input
-  const uint16_t* y;  // BN output (ReLU mask of a residual BN) or null
+  const uint8_t* mask;  // packed ReLU mask of a residual BN (bit j of byte e = element 8e + j) or null
   const float *mean, *invstd, *gamma, *beta;
   int relu_x;         // mask recomputed from x
 };

@@ -262,8 +262,9 @@ void check_bf16_operand(const Tensor& t, const char* name) {
 }
 
 // a: [M,K] if a_kmajor else [K,M];  b: [N,K] if b_kmajor else [K,N];  returns / writes C[M,N]
-// bnb = (stats [R,2,N] zeroed fp32, x, y|None, mean, invstd, gamma, beta, relu_x) for the BN-backward statistics
-// epilogue; x / y must be [M, N] bf16 matching the output.
+// bnb = (stats [R,2,N] zeroed fp32, x, mask|empty, mean, invstd, gamma, beta) + relu_x for the BN-backward
+// statistics epilogue; x is the BN input ([M, N] bf16 matching the output), mask the packed ReLU bits of a
+// residual BN's output (uint8 [M*N/8]).
 struct BnbHolder {
   k8s_amd::BnBwdEpi e;
   bool on = false;
@@ -271,17 +272,20 @@ struct BnbHolder {
 BnbHolder parse_bnb(const c10::optional<std::vector<Tensor>>& t, c10::optional<bool> relu_x, long M, long N) {
   BnbHolder h;
   if (!t) return h;
-  TORCH_CHECK(t->size() == 7, "bnb = [stats, x, y, mean, invstd, gamma, beta] (y may be an empty tensor)");
+  TORCH_CHECK(t->size() == 7, "bnb = [stats, x, mask, mean, invstd, gamma, beta] (mask may be an empty tensor)");
   const auto& v = *t;
   TORCH_CHECK(v[0].numel() == (long)k8s_amd::kConvStatReplicas * 2 * N && v[0].scalar_type() == at::kFloat,
               "bnb stats must be fp32 [conv_stat_replicas, 2, N]");
   TORCH_CHECK(v[1].numel() == M * N && v[1].scalar_type() == at::kBFloat16 && v[1].is_contiguous(), "bnb x shape");
-  const bool has_y = v[2].defined() && v[2].numel() > 0;
-  if (has_y) TORCH_CHECK(v[2].numel() == M * N && v[2].scalar_type() == at::kBFloat16 && v[2].is_contiguous());
+  const bool has_mask = v[2].defined() && v[2].numel() > 0;
+  if (has_mask)
+    TORCH_CHECK(v[2].numel() == M * N / 8 && v[2].scalar_type() == at::kByte && v[2].is_contiguous(),
+                "bnb mask must be uint8 [M*N/8]");
   for (int i = 3; i < 7; ++i)
     TORCH_CHECK(v[i].numel() == N && v[i].scalar_type() == at::kFloat && v[i].is_contiguous(), "bnb per-channel");
-  h.e = k8s_amd::BnBwdEpi{f32(v[0]), cbf(v[1]), has_y ? cbf(v[2]) : nullptr, f32(v[3]), f32(v[4]), f32(v[5]),
-                          f32(v[6]), (!has_y && relu_x.value_or(false)) ? 1 : 0};
+  TORCH_CHECK(!(has_mask && relu_x.value_or(false)), "bnb: mask and relu_x are exclusive");
+  h.e = k8s_amd::BnBwdEpi{f32(v[0]), cbf(v[1]), has_mask ? v[2].data_ptr<uint8_t>() : nullptr, f32(v[3]),
+                          f32(v[4]), f32(v[5]), f32(v[6]), relu_x.value_or(false) ? 1 : 0};
   h.on = true;
   return h;
 }

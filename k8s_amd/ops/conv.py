@@ -33,9 +33,12 @@ from k8s_amd.ops._ext import load as _load
 
 import os
 
-# BatchNorm-backward statistics in the dgrad epilogue (ops.nn.BnBwdLink). Off by default: measured on
-# MI355X, the epilogue's extra loads cost more GEMM time than the separate reduction pass they replace
-# (ResNet-50 b256: 6700 vs 7200 img/s). K8S_AMD_BN_LINK=1 turns it on.
+# BatchNorm-backward statistics in the dgrad epilogue (ops.nn.BnBwdLink): the lean (LDS-staged) epilogue's
+# copy-out pass reads the BN input next to the gradient it stores and reduces (sum g*m, sum g*m*xhat), replacing
+# the BN backward's separate reduction pass over (dy, x). Off by default: measured on MI355X (ResNet-50 b1024,
+# scripts/gpurun/prof_ab.sh) it removes 8.1 ms/step of reduction passes but adds 10.3 ms/step to the dgrads --
+# the x reads sit exposed at the end of every block instead of streaming -- 9.51k vs 9.72k img/s.
+# K8S_AMD_BN_LINK=1 turns it on.
 BN_LINK = os.environ.get("K8S_AMD_BN_LINK", "0") == "1"
 
 STATS = {"hip_fwd": 0, "aten_fwd": 0, "hip_wgrad": 0, "aten_wgrad": 0, "hip_dgrad": 0, "aten_dgrad": 0}

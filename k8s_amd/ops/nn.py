@@ -63,18 +63,18 @@ class BnBwdLink:
     output) also accumulate the BN backward's two channel reductions in its epilogue; the BN backward then
     runs only the apply pass. The BN forward fills in what the epilogue needs; ``reps`` is set by the
     producing kernel (left None when the vendor path ran, and the BN backward reduces itself)."""
-    __slots__ = ("x", "y", "mean", "invstd", "gamma", "beta", "relu_x", "reps")
+    __slots__ = ("x", "mask", "mean", "invstd", "gamma", "beta", "relu_x", "reps")
 
     def __init__(self):
-        self.x = self.y = self.mean = self.invstd = self.gamma = self.beta = self.reps = None
+        self.x = self.mask = self.mean = self.invstd = self.gamma = self.beta = self.reps = None
         self.relu_x = False
 
     def epilogue_args(self, store, device):
         """(bnb list for the kernel binding, relu_x), allocating the zeroed replica buffer into ``reps``."""
         C = self.x.shape[-1]
         self.reps = _zero_scratch(store, device, _C().conv_stat_replicas * 2 * C).view(_C().conv_stat_replicas, 2, C)
-        y = self.y if self.y is not None else torch.empty(0, device=device, dtype=torch.bfloat16)
-        return [self.reps, self.x, y, self.mean, self.invstd, self.gamma, self.beta], self.relu_x
+        mask = self.mask if self.mask is not None else torch.empty(0, device=device, dtype=torch.uint8)
+        return [self.reps, self.x, mask, self.mean, self.invstd, self.gamma, self.beta], self.relu_x
 
 
 class _Conv2dNHWC(torch.autograd.Function):
@@ -156,8 +156,7 @@ class _BnAct(torch.autograd.Function):
         ctx.relu_x = relu and not keep_y and mask is None
         ctx.bwd_link = None
         if bwd_link is not None and _gpu(x) and training:
-            bwd_link.x, bwd_link.y, bwd_link.mean, bwd_link.invstd = x, (y if relu and res is not None else None), \
-                mean, invstd
+            bwd_link.x, bwd_link.mask, bwd_link.mean, bwd_link.invstd = x, mask, mean, invstd
             bwd_link.gamma, bwd_link.beta, bwd_link.relu_x = pg.master, pb.master, ctx.relu_x
             ctx.bwd_link = bwd_link
         return y
@@ -175,7 +174,7 @@ class _BnAct(torch.autograd.Function):
             reps = None
             if ctx.bwd_link is not None:
                 reps, ctx.bwd_link.reps = ctx.bwd_link.reps, None
-                ctx.bwd_link.x = ctx.bwd_link.y = None  # drop the extra references to the saved activations
+                ctx.bwd_link.x = ctx.bwd_link.mask = None  # drop the extra references to the saved activations
             dx, dres = _C().bn_bwd(dy, x, y, mean, invstd, pg.master, pb.master, ctx.relu_x, dg, db, ctx.has_res,
                                    reps, mask)
             if sg is not None:
