@@ -1,20 +1,46 @@
 // K3: NHWC BatchNorm (training statistics) fused with residual add + ReLU.
 //
-// Activations are [M = N*H*W, C] bf16 rows (channels_last). Every kernel
-// reads/writes 16-B bf16x8 vectors; a thread owns 8 consecutive channels.
+// Activations are [M = N*H*W, C] bf16 rows (channels_last); every pass reads / writes 16-B bf16x8 vectors.
 //
-//  fwd:  stats  : per-block Welford/Chan partials (count-weighted mean, M2)
-//        final  : combine partials -> mean, invstd; update running stats
-//        apply  : y = relu(x*scale + shift [+ res])    (scale/shift per channel)
-//  bwd:  reduce : sum(dy_eff), sum(dy_eff * xhat)  with dy_eff = dy * (y > 0)
-//        final  : dgamma, dbeta (fp32, written straight into the flat grad bucket)
-//        apply  : dx = gamma*invstd*(dy_eff - sum_dy/M - xhat*sum_dyxh/M), dres = dy_eff
+//  fwd:  statistics: from the producing conv's epilogue (bn_finalize_sums) or a stats pass + final
+//        -> mean, invstd, and the per-channel affine pair (scale = gamma*invstd, shift = beta - mean*scale)
+//        apply  : y = relu(fma(x, scale, shift) [+ res])  (+ packed ReLU mask bits for a residual BN)
+//  bwd:  reduce : sum(dy_eff), sum(dy_eff * xhat)  with dy_eff = dy * relu'(y)
+//        final  : dgamma, dbeta (fp32, straight into the flat grad bucket) and the per-channel triple
+//                 (sc, B, D): dx = sc*dy_eff + B*x + D
+//        apply  : dx (and dres = dy_eff for a residual BN)
+//
+// The per-element passes (apply) are launched flat: ONE 16-B vector per thread, one 256-thread block per 4 KB
+// of the tensor, no grid-stride loop. Measured on MI355X (scripts/microbench/stream_bw.hip, read-1-write-1 over
+// 2 GB): that shape streams 6.25 TB/s where grid-stride loops reach 4.8-5.5 TB/s (2048-8192 blocks, 1-4 vectors
+// per trip, temporal or non-temporal) -- short-lived waves dispatched in address order keep the DRAM pages hot.
+// Per-thread channel parameters are therefore precomputed per channel (2-4 floats instead of 4-6 + math).
 #include <cstdlib>
+#include <stdexcept>
 
 #include "common.h"
 #include "launchers.h"
 
 namespace k8s_amd {
+
+// The forward's affine pair; the backward recomputes it with the same operations, so the ReLU decision
+// relu_on(x) below is bit-identical in every pass that makes it.
+__device__ __forceinline__ void bn_affine_regs(float gamma, float beta, float mean, float invstd, float& scale,
+                                               float& shift) {
+  scale = gamma * invstd;
+  shift = __builtin_fmaf(-mean, scale, beta);
+}
+__device__ __forceinline__ void bn_affine(float gamma, float beta, float mean, float invstd, float* scale,
+                                          float* shift) {
+  float a, b;
+  bn_affine_regs(gamma, beta, mean, invstd, a, b);
+  *scale = a;
+  *shift = b;
+}
+// y > 0 for a non-residual BN + ReLU, from its input: the stored bf16 of fma(x, scale, shift) is positive
+__device__ __forceinline__ bool relu_on(float x, float scale, float shift) {
+  return bf2f(f2bf(__builtin_fmaf(x, scale, shift))) > 0.f;
+}
 
 constexpr int BN_THREADS = 256;
 
@@ -153,7 +179,10 @@ __global__ void __launch_bounds__(256) bn_stats_final_kernel(const float* __rest
                                                              float* __restrict__ mean_out,
                                                              float* __restrict__ invstd_out,
                                                              float* __restrict__ run_mean,
-                                                             float* __restrict__ run_var) {
+                                                             float* __restrict__ run_var,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta,
+                                                             float* __restrict__ params) {
   __shared__ float sh[3][FIN_RG][FIN_CH];
   const int cl = threadIdx.x % FIN_CH, rg = threadIdx.x / FIN_CH;
   const int c = blockIdx.x * FIN_CH + cl;
@@ -176,6 +205,7 @@ __global__ void __launch_bounds__(256) bn_stats_final_kernel(const float* __rest
     const float var = m2 / cnt;
     mean_out[c] = mean;
     invstd_out[c] = rsqrtf(var + eps);
+    bn_affine(gamma[c], beta[c], mean, invstd_out[c], params + c, params + C + c);
     if (run_mean) {
       const float unbiased = cnt > 1.f ? m2 / (cnt - 1.f) : var;
       run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
@@ -188,7 +218,9 @@ __global__ void __launch_bounds__(256) bn_stats_final_kernel(const float* __rest
 // epilogue (gemm.hip, Epi::stats): no extra pass over the activation.
 __global__ void bn_finalize_sums_kernel(const float* __restrict__ sums, int nrep, int C, float count, float eps,
                                         float momentum, float* __restrict__ mean_out, float* __restrict__ invstd_out,
-                                        float* __restrict__ run_mean, float* __restrict__ run_var) {
+                                        float* __restrict__ run_mean, float* __restrict__ run_var,
+                                        const float* __restrict__ gamma, const float* __restrict__ beta,
+                                        float* __restrict__ params) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float s = 0.f, q = 0.f;
@@ -200,6 +232,7 @@ __global__ void bn_finalize_sums_kernel(const float* __restrict__ sums, int nrep
   const float var = fmaxf(q / count - mean * mean, 0.f);
   mean_out[c] = mean;
   invstd_out[c] = rsqrtf(var + eps);
+  bn_affine(gamma[c], beta[c], mean, invstd_out[c], params + c, params + C + c);
   if (run_mean) {
     const float unbiased = count > 1.f ? var * count / (count - 1.f) : var;
     run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
@@ -208,86 +241,58 @@ __global__ void bn_finalize_sums_kernel(const float* __restrict__ sums, int nrep
 }
 
 // Packed ReLU mask: bit j of byte e = (bf16(y[8e + j]) > 0). A residual BN's backward reads these M*C/8 bytes
-// instead of the bf16 output y (2 B/elem) in both its reduce and apply passes.
-__device__ __forceinline__ uint8_t relu_bits(const float (&v)[8]) {
+// instead of the bf16 output y (2 B/elem) in both its reduce and apply passes. A bf16 is > 0 iff its int16 bit
+// pattern is > 0 (NaN aside).
+__device__ __forceinline__ uint8_t relu_bits(const bf16x8_t& o) {
   uint32_t b = 0;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) b |= (bf2f(f2bf(v[j])) > 0.f ? 1u : 0u) << j;
+  for (int j = 0; j < 8; ++j) b |= (o[j] > 0 ? 1u : 0u) << j;
   return (uint8_t)b;
 }
 
-// y = act((x - mean) * (gamma * invstd) + beta [+ res]).
-// The grid is sized so (gridDim.x * blockDim.x) % cgroups == 0: every thread then keeps ONE channel group
-// for the whole grid-stride loop and holds its 8 channels' parameters in registers. U vectors per trip: all
-// U (or 2U with a residual) 16-B loads are issued before the first is used, so each wave keeps several HBM
-// requests in flight instead of one load -> use -> store chain per trip.
-template <int U>
-__global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(const uint16_t* __restrict__ x,
-                                                              const uint16_t* __restrict__ res,
-                                                              const float* __restrict__ mean,
-                                                              const float* __restrict__ invstd,
-                                                              const float* __restrict__ gamma,
-                                                              const float* __restrict__ beta,
-                                                              uint16_t* __restrict__ y, uint8_t* __restrict__ mask,
-                                                              long nvec, int cgroups, int relu) {
-  const long e0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  const long stride = (long)gridDim.x * blockDim.x;
-  const int cg = (int)(e0 % cgroups);
-  float mu[8], sc[8], bt[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c = cg * 8 + j;
-    mu[j] = mean[c];
-    sc[j] = gamma[c] * invstd[c];
-    bt[j] = beta[c];
-  }
-  long e = e0;
-  for (; e + (U - 1) * stride < nvec; e += U * stride) {
-    bf16x8_t xv[U], rv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) xv[u] = *reinterpret_cast<const bf16x8_t*>(x + (e + u * stride) * 8);
-    if (res) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) rv[u] = *reinterpret_cast<const bf16x8_t*>(res + (e + u * stride) * 8);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float o = (bf2f((uint16_t)xv[u][j]) - mu[j]) * sc[j] + bt[j];
-        if (res) o += bf2f((uint16_t)rv[u][j]);
-        if (relu) o = fmaxf(o, 0.f);
-        v[j] = o;
-      }
-      store8(y + (e + u * stride) * 8, v);
-      if (mask) mask[e + u * stride] = relu_bits(v);
-    }
-  }
-  for (; e < nvec; e += stride) {
-    float v[8];
-    load8(x + e * 8, v);
-    float rv[8];
-    if (res) load8(res + e * 8, rv);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float o = (v[j] - mu[j]) * sc[j] + bt[j];
-      if (res) o += rv[j];
-      if (relu) o = fmaxf(o, 0.f);
-      v[j] = o;
-    }
-    store8(y + e * 8, v);
-    if (mask) mask[e] = relu_bits(v);
-  }
+__device__ __forceinline__ void load_f8(const float* p, float (&o)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+  o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
 }
 
-// Eval-mode: same apply with running stats (mean/invstd precomputed on host side kernel below).
-__global__ void bn_eval_prep_kernel(const float* __restrict__ run_mean, const float* __restrict__ run_var, int C,
-                                    float eps, float* __restrict__ mean, float* __restrict__ invstd) {
+// y = act(fma(x, scale, shift) [+ res]); params = [scale | shift] (fp32 [2][C]). One vector per thread.
+__global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(const uint16_t* __restrict__ x,
+                                                              const uint16_t* __restrict__ res,
+                                                              const float* __restrict__ params,
+                                                              uint16_t* __restrict__ y, uint8_t* __restrict__ mask,
+                                                              int nvec, int C, FastDiv fcg, int relu) {
+  const int e = blockIdx.x * BN_THREADS + threadIdx.x;
+  if (e >= nvec) return;
+  const int cgroups = C >> 3;
+  const int c0 = (e - fcg.div(e) * cgroups) * 8;
+  const bf16x8_t xv = *reinterpret_cast<const bf16x8_t*>(x + (long)e * 8);
+  bf16x8_t rv;
+  if (res) rv = *reinterpret_cast<const bf16x8_t*>(res + (long)e * 8);
+  float sc[8], sh[8], v[8];
+  load_f8(params + c0, sc);
+  load_f8(params + C + c0, sh);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float o = __builtin_fmaf(bf2f((uint16_t)xv[j]), sc[j], sh[j]);
+    if (res) o += bf2f((uint16_t)rv[j]);
+    v[j] = relu ? fmaxf(o, 0.f) : o;
+  }
+  const bf16x8_t ov = pack_bf16x8(v);
+  *reinterpret_cast<bf16x8_t*>(y + (long)e * 8) = ov;
+  if (mask) mask[e] = relu_bits(ov);
+}
+
+// Eval mode: the affine pair from the running statistics.
+__global__ void bn_eval_prep_kernel(const float* __restrict__ run_mean, const float* __restrict__ run_var,
+                                    const float* __restrict__ gamma, const float* __restrict__ beta, int C, float eps,
+                                    float* __restrict__ mean, float* __restrict__ invstd,
+                                    float* __restrict__ params) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   mean[c] = run_mean[c];
   invstd[c] = rsqrtf(run_var[c] + eps);
+  bn_affine(gamma[c], beta[c], mean[c], invstd[c], params + c, params + C + c);
 }
 
 // Backward reduce: part[(bx*C + c)*2] = sum dy_eff, [+1] = sum dy_eff * xhat
@@ -318,8 +323,9 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
     sd[j] = sx[j] = 0.f;
     mu[j] = active ? mean[cg * 8 + j] : 0.f;
     is[j] = active ? invstd[cg * 8 + j] : 0.f;
-    sc[j] = (active && relu_x) ? gamma[cg * 8 + j] * is[j] : 0.f;
-    bt[j] = (active && relu_x) ? beta[cg * 8 + j] : 0.f;
+    sc[j] = 0.f;
+    bt[j] = 0.f;
+    if (active && relu_x) bn_affine_regs(gamma[cg * 8 + j], beta[cg * 8 + j], mu[j], is[j], sc[j], bt[j]);
   }
   if (active) {
     // 4 rows per trip: 8-12 independent 16-B loads in flight per thread before any is used
@@ -349,7 +355,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
         } else if (relu_x) {
 #pragma unroll
           for (int j = 0; j < 8; ++j)
-            if (bf2f(f2bf((xv[j] - mu[j]) * sc[j] + bt[j])) <= 0.f) g[j] = 0.f;
+            if (!relu_on(xv[j], sc[j], bt[j])) g[j] = 0.f;
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -376,7 +382,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
       } else if (relu_x) {  // ReLU mask recomputed from x: no read of y (non-residual BN)
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          if (bf2f(f2bf((xv[j] - mu[j]) * sc[j] + bt[j])) <= 0.f) g[j] = 0.f;
+          if (!relu_on(xv[j], sc[j], bt[j])) g[j] = 0.f;
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -439,114 +445,108 @@ __global__ void __launch_bounds__(256) bn_bwd_final_kernel(const float* __restri
   }
 }
 
-// dx = gamma*invstd*(dy_eff - mean(dy_eff) - xhat*mean(dy_eff*xhat)); dres = dy_eff. U vectors per trip
-// with every load of the trip issued up front (see bn_apply_kernel).
-template <int U>
+// Backward per-channel constants from the two reductions (sum dy_eff, sum dy_eff*xhat), M rows:
+//   params = [sc | B | D | shift]:  dx = sc*dy_eff + B*x + D,  shift = the forward's affine shift (relu_x)
+__device__ __forceinline__ void bn_bwd_consts(int c, int C, float s_dy, float s_dyxh, float inv_m,
+                                              const float* __restrict__ mean, const float* __restrict__ invstd,
+                                              const float* __restrict__ gamma, const float* __restrict__ beta,
+                                              float* __restrict__ params) {
+  float sc, shift;
+  bn_affine_regs(gamma[c], beta ? beta[c] : 0.f, mean[c], invstd[c], sc, shift);
+  const float k1 = s_dy * inv_m, k2 = s_dyxh * inv_m;  // mean(dy_eff), mean(dy_eff * xhat)
+  const float B = -sc * invstd[c] * k2;
+  params[c] = sc;
+  params[C + c] = B;
+  params[2 * C + c] = -sc * k1 - B * mean[c];
+  params[3 * C + c] = shift;
+}
+
+__global__ void __launch_bounds__(256) bn_bwd_final_kernel(const float* __restrict__ part, int nblocks, int C,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                           float inv_m, const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           float* __restrict__ params) {
+  __shared__ float sh[2][FIN_RG][FIN_CH];
+  const int cl = threadIdx.x % FIN_CH, rg = threadIdx.x / FIN_CH;
+  const int c = blockIdx.x * FIN_CH + cl;
+  float a = 0.f, b2 = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int i = rg; i < nblocks; i += FIN_RG) {
+      const float2 v = *reinterpret_cast<const float2*>(part + ((long)i * C + c) * 2);
+      a += v.x;
+      b2 += v.y;
+    }
+  }
+  sh[0][rg][cl] = a;
+  sh[1][rg][cl] = b2;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    for (int r = 1; r < FIN_RG; ++r) {
+      a += sh[0][r][cl];
+      b2 += sh[1][r][cl];
+    }
+    if (dbeta) dbeta[c] = a;
+    if (dgamma) dgamma[c] = b2;
+    bn_bwd_consts(c, C, a, b2, inv_m, mean, invstd, gamma, beta, params);
+  }
+}
+
+// Fold the conv-epilogue replicas [nrep][2][C] of (sum g*mask, sum g*mask*xhat) into dgamma / dbeta / params.
+__global__ void __launch_bounds__(256) bn_bwd_fold_reps_kernel(const float* __restrict__ reps, int nrep, int C,
+                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                               float inv_m, const float* __restrict__ mean,
+                                                               const float* __restrict__ invstd,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta,
+                                                               float* __restrict__ params) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f, b = 0.f;
+  for (int r = 0; r < nrep; ++r) {
+    a += reps[((long)r * 2) * C + c];
+    b += reps[((long)r * 2 + 1) * C + c];
+  }
+  if (dbeta) dbeta[c] = a;
+  if (dgamma) dgamma[c] = b;
+  bn_bwd_consts(c, C, a, b, inv_m, mean, invstd, gamma, beta, params);
+}
+
+// dx = sc*dy_eff + B*x + D; dres = dy_eff. dy_eff = dy masked by the packed bits (residual BN), by relu_on(x)
+// (non-residual BN + ReLU) or not at all. One vector per thread (see the header).
 __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t* __restrict__ dy,
                                                                   const uint16_t* __restrict__ x,
-                                                                  const uint16_t* __restrict__ y,
-                                                                  const float* __restrict__ mean,
-                                                                  const float* __restrict__ invstd,
-                                                                  const float* __restrict__ beta, int relu_x,
-                                                                  const float* __restrict__ gamma,
-                                                                  const float* __restrict__ sums,
+                                                                  const uint8_t* __restrict__ mask,
+                                                                  const float* __restrict__ params, int relu_x,
                                                                   uint16_t* __restrict__ dx,
-                                                                  uint16_t* __restrict__ dres, long nvec,
-                                                                  int cgroups, int C, float inv_m,
-                                                                  const uint8_t* __restrict__ mask) {
-  const long e0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  const long stride = (long)gridDim.x * blockDim.x;
-  const int cg = (int)(e0 % cgroups);  // fixed per thread: grid sized so (grid*block) % cgroups == 0
-  float mu[8], is[8], sc[8], bt[8], k1[8], k2[8];
+                                                                  uint16_t* __restrict__ dres, int nvec, int C,
+                                                                  FastDiv fcg) {
+  const int e = blockIdx.x * BN_THREADS + threadIdx.x;
+  if (e >= nvec) return;
+  const int cgroups = C >> 3;
+  const int c0 = (e - fcg.div(e) * cgroups) * 8;
+  const bf16x8_t gv = *reinterpret_cast<const bf16x8_t*>(dy + (long)e * 8);
+  const bf16x8_t xv = *reinterpret_cast<const bf16x8_t*>(x + (long)e * 8);
+  const uint32_t bits = mask ? (uint32_t)mask[e] : 0xFFu;
+  float sc[8], B[8], D[8], g[8], o[8];
+  load_f8(params + c0, sc);
+  load_f8(params + C + c0, B);
+  load_f8(params + 2 * C + c0, D);
+  float sh[8];
+  if (relu_x) load_f8(params + 3 * C + c0, sh);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int c = cg * 8 + j;
-    mu[j] = mean[c];
-    is[j] = invstd[c];
-    sc[j] = gamma[c] * is[j];
-    bt[j] = beta ? beta[c] : 0.f;
-    k1[j] = sums[c] * inv_m;      // mean(dy_eff)
-    k2[j] = sums[C + c] * inv_m;  // mean(dy_eff * xhat)
+    const float xf = bf2f((uint16_t)xv[j]);
+    bool on = (bits >> j) & 1u;
+    if (relu_x) on = relu_on(xf, sc[j], sh[j]);
+    g[j] = on ? bf2f((uint16_t)gv[j]) : 0.f;
+    o[j] = __builtin_fmaf(sc[j], g[j], __builtin_fmaf(B[j], xf, D[j]));
   }
-  // B = -gamma*invstd^2*mean(dy_eff*xhat), D = -gamma*invstd*mean(dy_eff) - B*mean: dx = sc*g + B*x + D
-  float B[8], D[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    B[j] = -sc[j] * is[j] * k2[j];
-    D[j] = -sc[j] * k1[j] - B[j] * mu[j];
-  }
-  auto one = [&](bf16x8_t gv, bf16x8_t xvv, bool has_y, bf16x8_t yv, long e) {
-    float g[8], xv[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      g[j] = bf2f((uint16_t)gv[j]);
-      xv[j] = bf2f((uint16_t)xvv[j]);
-    }
-    if (mask) {
-      const uint32_t bits = mask[e];
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (!((bits >> j) & 1u)) g[j] = 0.f;
-    } else if (has_y) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (bf2f((uint16_t)yv[j]) <= 0.f) g[j] = 0.f;
-    } else if (relu_x) {  // ReLU mask recomputed from x: no read of y (non-residual BN)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (bf2f(f2bf((xv[j] - mu[j]) * sc[j] + bt[j])) <= 0.f) g[j] = 0.f;
-    }
-    if (dres) store8(dres + e * 8, g);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) xv[j] = sc[j] * g[j] + B[j] * xv[j] + D[j];
-    store8(dx + e * 8, xv);
-  };
-  long e = e0;
-  for (; e + (U - 1) * stride < nvec; e += U * stride) {
-    bf16x8_t gv[U], xv[U], yv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) yv[u] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      gv[u] = *reinterpret_cast<const bf16x8_t*>(dy + (e + u * stride) * 8);
-      xv[u] = *reinterpret_cast<const bf16x8_t*>(x + (e + u * stride) * 8);
-    }
-    if (y) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) yv[u] = *reinterpret_cast<const bf16x8_t*>(y + (e + u * stride) * 8);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) one(gv[u], xv[u], y != nullptr, yv[u], e + u * stride);
-  }
-  for (; e < nvec; e += stride) {
-    const bf16x8_t gv = *reinterpret_cast<const bf16x8_t*>(dy + e * 8);
-    const bf16x8_t xv = *reinterpret_cast<const bf16x8_t*>(x + e * 8);
-    bf16x8_t yv = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (y) yv = *reinterpret_cast<const bf16x8_t*>(y + e * 8);
-    one(gv, xv, y != nullptr, yv, e);
-  }
+  if (dres) *reinterpret_cast<bf16x8_t*>(dres + (long)e * 8) = pack_bf16x8(g);
+  *reinterpret_cast<bf16x8_t*>(dx + (long)e * 8) = pack_bf16x8(o);
 }
-
-// Loads per trip for the per-element BN kernels. $K8S_AMD_BN_UNROLL (1, 2 or 4) exists for A/B runs; the
-// default stays 1: on the ResNet-50 b512 shapes one 16-B load per trip already streams 4.4-5.3 TB/s and 2 or 4
-// per trip measured 0-12 % slower (lower occupancy), ResNet-50 8151 / 8097 / 8028 img/s for U = 1 / 2 / 4
-// (profiles/r01_bn_unroll_ab.md).
-static int bn_unroll() {
-  static int u = [] {
-    const char* s = getenv("K8S_AMD_BN_UNROLL");
-    const int v = s ? atoi(s) : 1;
-    return (v == 2 || v == 4) ? v : 1;
-  }();
-  return u;
-}
-
-static void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* mean, const float* invstd,
-                            const float* gamma, const float* beta, uint16_t* y, uint8_t* mask, long nvec,
-                            int cgroups, int relu, hipStream_t st);
-static void launch_bn_bwd_apply(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,
-                                const float* invstd, const float* beta, int relu_x, const float* gamma,
-                                const float* sums, uint16_t* dx, uint16_t* dres, long nvec, int cgroups, int C,
-                                float inv_m, const uint8_t* mask, hipStream_t st);
 
 // ---------------------------------------------------------------- launchers
 static long bn_rows_per_block(long M, const BnGeom& g) {
@@ -563,58 +563,6 @@ static long bn_rows_per_block(long M, const BnGeom& g) {
   return rpb;
 }
 
-// grid for the per-element kernels: (grid * BN_THREADS) % cgroups == 0 keeps each thread on one channel group
-static int bn_elem_grid(long nvec, int cgroups) {
-  int g = stream_grid(nvec, BN_THREADS);
-  if ((BN_THREADS % cgroups) != 0) {
-    // cgroups does not divide the block: round the grid up to a multiple of cgroups / gcd(cgroups, BN_THREADS)
-    int a = cgroups, b = BN_THREADS;
-    while (b) { int t = a % b; a = b; b = t; }
-    const int step = cgroups / a;
-    g = (g + step - 1) / step * step;
-  }
-  return g;
-}
-
-static void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* mean, const float* invstd,
-                            const float* gamma, const float* beta, uint16_t* y, uint8_t* mask, long nvec,
-                            int cgroups, int relu, hipStream_t st) {
-  const dim3 grid(bn_elem_grid(nvec, cgroups)), block(BN_THREADS);
-  switch (bn_unroll()) {
-    case 4:
-      hipLaunchKernelGGL(bn_apply_kernel<4>, grid, block, 0, st, x, res, mean, invstd, gamma, beta, y, mask, nvec,
-                         cgroups, relu);
-      break;
-    case 2:
-      hipLaunchKernelGGL(bn_apply_kernel<2>, grid, block, 0, st, x, res, mean, invstd, gamma, beta, y, mask, nvec,
-                         cgroups, relu);
-      break;
-    default:
-      hipLaunchKernelGGL(bn_apply_kernel<1>, grid, block, 0, st, x, res, mean, invstd, gamma, beta, y, mask, nvec,
-                         cgroups, relu);
-  }
-}
-
-static void launch_bn_bwd_apply(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,
-                                const float* invstd, const float* beta, int relu_x, const float* gamma,
-                                const float* sums, uint16_t* dx, uint16_t* dres, long nvec, int cgroups, int C,
-                                float inv_m, const uint8_t* mask, hipStream_t st) {
-  const dim3 grid(bn_elem_grid(nvec, cgroups)), block(BN_THREADS);
-  switch (bn_unroll()) {
-    case 4:
-      hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid, block, 0, st, dy, x, y, mean, invstd, beta, relu_x, gamma,
-                         sums, dx, dres, nvec, cgroups, C, inv_m, mask);
-      break;
-    case 2:
-      hipLaunchKernelGGL(bn_bwd_apply_kernel<2>, grid, block, 0, st, dy, x, y, mean, invstd, beta, relu_x, gamma,
-                         sums, dx, dres, nvec, cgroups, C, inv_m, mask);
-      break;
-    default:
-      hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, block, 0, st, dy, x, y, mean, invstd, beta, relu_x, gamma,
-                         sums, dx, dres, nvec, cgroups, C, inv_m, mask);
-  }
-}
-
 int bn_workspace_floats(long M, int C) {
   BnGeom g = bn_geom(C, M);
   long rpb = bn_rows_per_block(M, g);
@@ -622,9 +570,18 @@ int bn_workspace_floats(long M, int C) {
   return (int)(nb * C * 2);
 }
 
+static void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* params, uint16_t* y, uint8_t* mask,
+                            long M, int C, bool relu, hipStream_t st) {
+  const long nvec = M * C / 8;
+  if (nvec >= (1L << 31)) throw std::runtime_error("BatchNorm tensor too large (>= 2^31 vectors)");
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(cdiv(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, x, res, params, y,
+                     mask, (int)nvec, C, make_fastdiv(C / 8), (int)relu);
+}
+
 void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta, uint16_t* y,
-                   float* save_mean, float* save_invstd, float* run_mean, float* run_var, float* work, long M, int C,
-                   float eps, float momentum, bool training, bool relu, hipStream_t st, uint8_t* mask) {
+                   float* save_mean, float* save_invstd, float* run_mean, float* run_var, float* work, float* params,
+                   long M, int C, float eps, float momentum, bool training, bool relu, hipStream_t st,
+                   uint8_t* mask) {
   if (training) {
     BnGeom g = bn_geom(C, M);
     long rpb = bn_rows_per_block(M, g);
@@ -632,70 +589,67 @@ void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, c
     hipLaunchKernelGGL(bn_stats_kernel, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, x, M, C, g.tpr,
                        g.rows_per_iter, rpb, work);
     hipLaunchKernelGGL(bn_stats_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, nb, M, rpb, C, eps,
-                       momentum, save_mean, save_invstd, run_mean, run_var);
+                       momentum, save_mean, save_invstd, run_mean, run_var, gamma, beta, params);
   } else {
-    hipLaunchKernelGGL(bn_eval_prep_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, run_mean, run_var, C, eps,
-                       save_mean, save_invstd);
+    hipLaunchKernelGGL(bn_eval_prep_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, run_mean, run_var, gamma, beta, C,
+                       eps, save_mean, save_invstd, params);
   }
-  const long nvec = M * C / 8;
-  launch_bn_apply(x, res, save_mean, save_invstd, gamma, beta, y, mask, nvec, C / 8, (int)relu, st);
+  launch_bn_apply(x, res, params, y, mask, M, C, relu, st);
 }
 
 void launch_bn_fwd_from_sums(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
                              uint16_t* y, const float* sums, int nrep, float* save_mean, float* save_invstd,
-                             float* run_mean, float* run_var, long M, int C, float eps, float momentum, bool relu,
-                             hipStream_t st, uint8_t* mask) {
+                             float* run_mean, float* run_var, float* params, long M, int C, float eps, float momentum,
+                             bool relu, hipStream_t st, uint8_t* mask) {
   hipLaunchKernelGGL(bn_finalize_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, nrep, C, (float)M, eps,
-                     momentum, save_mean, save_invstd, run_mean, run_var);
-  const long nvec = M * C / 8;
-  launch_bn_apply(x, res, save_mean, save_invstd, gamma, beta, y, mask, nvec, C / 8, (int)relu, st);
+                     momentum, save_mean, save_invstd, run_mean, run_var, gamma, beta, params);
+  launch_bn_apply(x, res, params, y, mask, M, C, relu, st);
 }
 
-// Fold the conv-epilogue replicas [nrep][2][C] of (sum g*mask, sum g*mask*xhat) into sums / dgamma / dbeta.
-__global__ void __launch_bounds__(256) bn_bwd_fold_reps_kernel(const float* __restrict__ reps, int nrep, int C,
-                                                               float* __restrict__ sums, float* __restrict__ dgamma,
-                                                               float* __restrict__ dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float a = 0.f, b = 0.f;
-  for (int r = 0; r < nrep; ++r) {
-    a += reps[((long)r * 2) * C + c];
-    b += reps[((long)r * 2 + 1) * C + c];
-  }
-  sums[c] = a;
-  sums[C + c] = b;
-  if (dbeta) dbeta[c] = a;
-  if (dgamma) dgamma[c] = b;
+static void launch_bn_bwd_apply(const uint16_t* dy, const uint16_t* x, const uint8_t* mask, const float* params,
+                                bool relu_x, uint16_t* dx, uint16_t* dres, long M, int C, hipStream_t st) {
+  const long nvec = M * C / 8;
+  if (nvec >= (1L << 31)) throw std::runtime_error("BatchNorm tensor too large (>= 2^31 vectors)");
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(cdiv(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, dy, x, mask, params,
+                     (int)relu_x, dx, dres, (int)nvec, C, make_fastdiv(C / 8));
 }
 
 // BN backward whose reduction already happened in the epilogue of the kernel that produced dy.
-void launch_bn_bwd_from_sums(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,
-                             const float* invstd, const float* gamma, const float* beta, bool relu_x, uint16_t* dx,
-                             uint16_t* dres, float* dgamma, float* dbeta, const float* reps, int nrep, float* sums,
-                             long M, int C, hipStream_t st, const uint8_t* mask) {
-  hipLaunchKernelGGL(bn_bwd_fold_reps_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, reps, nrep, C, sums, dgamma,
-                     dbeta);
-  const long nvec = M * C / 8;
-  launch_bn_bwd_apply(dy, x, y, mean, invstd, beta, (int)relu_x, gamma, sums, dx, dres, nvec, C / 8, C,
-                      1.f / (float)M, mask, st);
+void launch_bn_bwd_from_sums(const uint16_t* dy, const uint16_t* x, const float* mean, const float* invstd,
+                             const float* gamma, const float* beta, bool relu_x, uint16_t* dx, uint16_t* dres,
+                             float* dgamma, float* dbeta, const float* reps, int nrep, float* params, long M, int C,
+                             hipStream_t st, const uint8_t* mask) {
+  hipLaunchKernelGGL(bn_bwd_fold_reps_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, reps, nrep, C, dgamma, dbeta,
+                     1.f / (float)M, mean, invstd, gamma, beta, params);
+  launch_bn_bwd_apply(dy, x, mask, params, relu_x, dx, dres, M, C, st);
 }
 
-void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
-                   const float* gamma, const float* beta, bool relu_x, uint16_t* dx, uint16_t* dres, float* dgamma,
-                   float* dbeta, float* work, float* sums, long M, int C, hipStream_t st, const uint8_t* mask) {
+void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, const float* invstd, const float* gamma,
+                   const float* beta, bool relu_x, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta,
+                   float* work, float* params, long M, int C, hipStream_t st, const uint8_t* mask) {
   BnGeom g = bn_geom(C, M);
   long rpb = bn_rows_per_block(M, g);
   int nb = (int)((M + rpb - 1) / rpb);
   if (mask)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, dy, x, y, mean,
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, dy, x, nullptr, mean,
                        invstd, gamma, beta, (int)relu_x, M, C, g.tpr, g.rows_per_iter, rpb, work, mask);
   else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, dy, x, y, mean,
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, dy, x, nullptr, mean,
                        invstd, gamma, beta, (int)relu_x, M, C, g.tpr, g.rows_per_iter, rpb, work, mask);
-  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, nb, C, sums, dgamma, dbeta);
-  const long nvec = M * C / 8;
-  launch_bn_bwd_apply(dy, x, y, mean, invstd, beta, (int)relu_x, gamma, sums, dx, dres, nvec, C / 8, C,
-                      1.f / (float)M, mask, st);
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, nb, C, dgamma, dbeta,
+                     1.f / (float)M, mean, invstd, gamma, beta, params);
+  launch_bn_bwd_apply(dy, x, mask, params, relu_x, dx, dres, M, C, st);
+}
+
+__global__ void __launch_bounds__(BN_THREADS) relu_mask_kernel(const uint16_t* __restrict__ y,
+                                                               uint8_t* __restrict__ mask, int nvec) {
+  const int e = blockIdx.x * BN_THREADS + threadIdx.x;
+  if (e < nvec) mask[e] = relu_bits(*reinterpret_cast<const bf16x8_t*>(y + (long)e * 8));
+}
+
+void launch_relu_mask(const uint16_t* y, uint8_t* mask, long nvec, hipStream_t st) {
+  if (nvec >= (1L << 31)) throw std::runtime_error("tensor too large (>= 2^31 vectors)");
+  hipLaunchKernelGGL(relu_mask_kernel, dim3(cdiv(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, y, mask, (int)nvec);
 }
 
 }  // namespace k8s_amd

@@ -21,12 +21,18 @@ __device__ __forceinline__ float bf2f(uint16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }
 
-// round-to-nearest-even, NaN preserved as quiet NaN
-__device__ __forceinline__ uint16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16v8_t;
+typedef __attribute__((ext_vector_type(8))) float f32x8_t;
+
+// fp32 -> bf16, round-to-nearest-even, NaN kept as a quiet NaN: gfx950's v_cvt_pk_bf16_f32 (one instruction per
+// PAIR of values) instead of the 7-instruction integer rounding sequence -- the per-element passes (BatchNorm,
+// GEMM epilogues) were VALU-bound on that sequence at ~4.5 TB/s
+__device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+
+// 8 floats -> 8 bf16 (4 v_cvt_pk_bf16_f32)
+__device__ __forceinline__ bf16x8_t pack_bf16x8(const float (&o)[8]) {
+  const f32x8_t f = {o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7]};
+  return __builtin_bit_cast(bf16x8_t, __builtin_convertvector(f, bf16v8_t));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -72,10 +78,7 @@ __device__ __forceinline__ void load8(const uint16_t* p, float (&o)[8]) {
 }
 
 __device__ __forceinline__ void store8(uint16_t* p, const float (&o)[8]) {
-  bf16x8_t v;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(o[j]);
-  *reinterpret_cast<bf16x8_t*>(p) = v;
+  *reinterpret_cast<bf16x8_t*>(p) = pack_bf16x8(o);
 }
 
 // Division by a runtime-invariant divisor as multiply-high + shift (valid for 0 <= n < 2^31).

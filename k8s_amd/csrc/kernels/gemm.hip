@@ -433,8 +433,9 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
         const int cn = n + r < N ? n + r : N - 1;
         bmu[r] = E.bmean[cn];
         bis[r] = E.binvstd[cn];
+        // the BN forward's affine pair (batchnorm.hip bn_affine_regs), so the ReLU decision below is bit-identical
         bsc[r] = E.brelu_x ? E.bgamma[cn] * bis[r] : 0.f;
-        bbt[r] = E.brelu_x ? E.bbeta[cn] : 0.f;
+        bbt[r] = E.brelu_x ? __builtin_fmaf(-bmu[r], bsc[r], E.bbeta[cn]) : 0.f;
       }
     }
     constexpr int CHUNKS = BM * CPR;
@@ -466,8 +467,8 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
         for (int r = 0; r < 8; ++r) {
           const float xh = (bf2f((uint16_t)xv[r]) - bmu[r]) * bis[r];
           bool on = (bits >> r) & 1u;
-          // the forward's ReLU decision, bit for bit: relu(bf16((x - mean) * gamma * invstd + beta)) > 0
-          if (E.brelu_x) on = bf2f(f2bf((bf2f((uint16_t)xv[r]) - bmu[r]) * bsc[r] + bbt[r])) > 0.f;
+          // the forward's ReLU decision, bit for bit: bf16(fma(x, scale, shift)) > 0
+          if (E.brelu_x) on = bf2f(f2bf(__builtin_fmaf(bf2f((uint16_t)xv[r]), bsc[r], bbt[r]))) > 0.f;
           const float g = on ? bf2f((uint16_t)o[r]) : 0.f;
           ps[r] += g;
           pq[r] += g * xh;

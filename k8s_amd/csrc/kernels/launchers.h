@@ -19,22 +19,25 @@ void launch_clip_factor(const float* stats, float max_norm, float* factor, hipSt
 
 // batchnorm.hip
 int bn_workspace_floats(long M, int C);
+// params: fp32 workspace, [2][C] for the forward (scale, shift), [4][C] for the backward (sc, B, D, shift)
 void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta, uint16_t* y,
-                   float* save_mean, float* save_invstd, float* run_mean, float* run_var, float* work, long M, int C,
-                   float eps, float momentum, bool training, bool relu, hipStream_t st, uint8_t* mask = nullptr);
+                   float* save_mean, float* save_invstd, float* run_mean, float* run_var, float* work, float* params,
+                   long M, int C, float eps, float momentum, bool training, bool relu, hipStream_t st,
+                   uint8_t* mask = nullptr);
 void launch_bn_fwd_from_sums(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
                              uint16_t* y, const float* sums, int nrep, float* save_mean, float* save_invstd,
-                             float* run_mean, float* run_var, long M, int C, float eps, float momentum, bool relu,
-                             hipStream_t st, uint8_t* mask = nullptr);
+                             float* run_mean, float* run_var, float* params, long M, int C, float eps, float momentum,
+                             bool relu, hipStream_t st, uint8_t* mask = nullptr);
 constexpr int kConvStatReplicas = 32;  // must match STAT_REPL in gemm.hip
-void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
-                   const float* gamma, const float* beta, bool relu_x, uint16_t* dx, uint16_t* dres, float* dgamma,
-                   float* dbeta, float* work, float* sums, long M, int C, hipStream_t st,
-                   const uint8_t* mask = nullptr);
-void launch_bn_bwd_from_sums(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,
-                             const float* invstd, const float* gamma, const float* beta, bool relu_x, uint16_t* dx,
-                             uint16_t* dres, float* dgamma, float* dbeta, const float* reps, int nrep, float* sums,
-                             long M, int C, hipStream_t st, const uint8_t* mask = nullptr);
+void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, const float* invstd, const float* gamma,
+                   const float* beta, bool relu_x, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta,
+                   float* work, float* params, long M, int C, hipStream_t st, const uint8_t* mask = nullptr);
+void launch_bn_bwd_from_sums(const uint16_t* dy, const uint16_t* x, const float* mean, const float* invstd,
+                             const float* gamma, const float* beta, bool relu_x, uint16_t* dx, uint16_t* dres,
+                             float* dgamma, float* dbeta, const float* reps, int nrep, float* params, long M, int C,
+                             hipStream_t st, const uint8_t* mask = nullptr);
+// packed ReLU bits of a bf16 tensor (bit j of byte e = y[8e + j] > 0), nvec = numel / 8
+void launch_relu_mask(const uint16_t* y, uint8_t* mask, long nvec, hipStream_t st);
 
 // norm.hip
 void launch_norm_fwd(bool rms, const uint16_t* x, const uint16_t* res, uint16_t* xsum, const float* gamma,

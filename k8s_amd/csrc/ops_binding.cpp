@@ -120,16 +120,16 @@ std::vector<Tensor> bn_fwd(Tensor x, c10::optional<Tensor> res, Tensor gamma, Te
   auto y = torch::empty_like(x);
   auto mean = torch::empty({C}, gamma.options());
   auto invstd = torch::empty({C}, gamma.options());
+  auto params = torch::empty({2 * C}, gamma.options());
   Tensor work = training ? torch::empty({k8s_amd::bn_workspace_floats(M, C)}, gamma.options()) : mean;
   Tensor mask = relu_mask_for(x, want_mask);
   k8s_amd::launch_bn_fwd(cbf(x), res ? cbf(*res) : nullptr, f32(gamma), f32(beta), bf(y), f32(mean), f32(invstd),
-                         f32(run_mean), f32(run_var), f32(work), M, C, (float)eps, (float)momentum, training, relu,
-                         cur_stream(), want_mask ? mask.data_ptr<uint8_t>() : nullptr);
+                         f32(run_mean), f32(run_var), f32(work), f32(params), M, C, (float)eps, (float)momentum,
+                         training, relu, cur_stream(), want_mask ? mask.data_ptr<uint8_t>() : nullptr);
   if (want_mask) return {y, mean, invstd, mask};
   return {y, mean, invstd};
 }
 
-// returns dx, dres (or empty), writes dgamma/dbeta into the given (flat-bucket view) tensors
 std::vector<Tensor> bn_fwd_from_sums(Tensor x, c10::optional<Tensor> res, Tensor gamma, Tensor beta, Tensor sums,
                                      Tensor run_mean, Tensor run_var, double momentum, double eps, bool relu,
                                      bool want_mask) {
@@ -143,14 +143,19 @@ std::vector<Tensor> bn_fwd_from_sums(Tensor x, c10::optional<Tensor> res, Tensor
   auto y = torch::empty_like(x);
   auto mean = torch::empty({C}, gamma.options());
   auto invstd = torch::empty({C}, gamma.options());
+  auto params = torch::empty({2 * C}, gamma.options());
   Tensor mask = relu_mask_for(x, want_mask);
   k8s_amd::launch_bn_fwd_from_sums(cbf(x), res ? cbf(*res) : nullptr, f32(gamma), f32(beta), bf(y), f32(sums),
-                                   nrep, f32(mean), f32(invstd), f32(run_mean), f32(run_var), M, C, (float)eps,
-                                   (float)momentum, relu, cur_stream(), want_mask ? mask.data_ptr<uint8_t>() : nullptr);
+                                   nrep, f32(mean), f32(invstd), f32(run_mean), f32(run_var), f32(params), M, C,
+                                   (float)eps, (float)momentum, relu, cur_stream(),
+                                   want_mask ? mask.data_ptr<uint8_t>() : nullptr);
   if (want_mask) return {y, mean, invstd, mask};
   return {y, mean, invstd};
 }
 
+// returns dx, dres (or empty), writes dgamma/dbeta into the given (flat-bucket view) tensors. The ReLU of the
+// forward comes from the packed `mask` (residual BN), is recomputed from x (`relu_x`), or -- given the BN output
+// `y` -- is packed from y first (compatibility; the trainer passes the mask).
 std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor mean, Tensor invstd, Tensor gamma,
                            Tensor beta, bool relu_x, Tensor dgamma, Tensor dbeta, bool want_dres,
                            c10::optional<Tensor> reps, c10::optional<Tensor> mask) {
@@ -161,26 +166,32 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor 
   const long M = x.numel() / C;
   TORCH_CHECK(dgamma.numel() == C && dbeta.numel() == C && dgamma.is_contiguous() && dbeta.is_contiguous());
   check_dtype(dgamma, at::kFloat, "dgamma");
-  if (y) { check_cuda(*y, "y"); TORCH_CHECK(y->sizes() == x.sizes()); }
+  TORCH_CHECK(!(relu_x && y), "relu mask from x and y are exclusive");
+  Tensor ymask;
+  if (y) {
+    check_cuda(*y, "y");
+    TORCH_CHECK(y->sizes() == x.sizes() && !mask, "y: same shape as x, exclusive with mask");
+    ymask = torch::empty({x.numel() / 8}, x.options().dtype(at::kByte));
+    k8s_amd::launch_relu_mask(cbf(y->contiguous()), ymask.data_ptr<uint8_t>(), x.numel() / 8, cur_stream());
+  }
   auto dx = torch::empty_like(x);
   Tensor dres = want_dres ? torch::empty_like(x) : Tensor();
-  auto work = torch::empty({k8s_amd::bn_workspace_floats(M, C)}, gamma.options());
-  auto sums = torch::empty({2 * C}, gamma.options());
-  TORCH_CHECK(!(relu_x && y), "relu mask from x and y are exclusive");
-  const uint8_t* mk = cmask(mask);
-  TORCH_CHECK(!mk || (!relu_x && mask->numel() == x.numel() / 8), "packed mask: M*C/8 bytes, exclusive with relu_x");
+  auto params = torch::empty({4 * C}, gamma.options());
+  const uint8_t* mk = y ? ymask.data_ptr<uint8_t>() : cmask(mask);
+  TORCH_CHECK(!mk || (!relu_x && (y || mask->numel() == x.numel() / 8)),
+              "packed mask: M*C/8 bytes, exclusive with relu_x");
   if (reps) {  // (sum g*mask, sum g*mask*xhat) already accumulated by the epilogue that produced dy
     TORCH_CHECK(reps->is_cuda() && reps->scalar_type() == at::kFloat && reps->is_contiguous() &&
                     reps->numel() == (long)k8s_amd::kConvStatReplicas * 2 * C,
                 "reps must be fp32 [conv_stat_replicas, 2, C]");
-    k8s_amd::launch_bn_bwd_from_sums(cbf(dy), cbf(x), y ? cbf(*y) : nullptr, f32(mean), f32(invstd), f32(gamma),
-                                     f32(beta), relu_x, bf(dx), want_dres ? bf(dres) : nullptr, f32(dgamma),
-                                     f32(dbeta), f32(*reps), k8s_amd::kConvStatReplicas, f32(sums), M, C,
-                                     cur_stream(), mk);
+    k8s_amd::launch_bn_bwd_from_sums(cbf(dy), cbf(x), f32(mean), f32(invstd), f32(gamma), f32(beta), relu_x, bf(dx),
+                                     want_dres ? bf(dres) : nullptr, f32(dgamma), f32(dbeta), f32(*reps),
+                                     k8s_amd::kConvStatReplicas, f32(params), M, C, cur_stream(), mk);
     return {dx, dres};
   }
-  k8s_amd::launch_bn_bwd(cbf(dy), cbf(x), y ? cbf(*y) : nullptr, f32(mean), f32(invstd), f32(gamma), f32(beta),
-                         relu_x, bf(dx), want_dres ? bf(dres) : nullptr, f32(dgamma), f32(dbeta), f32(work), f32(sums), M, C,
+  auto work = torch::empty({k8s_amd::bn_workspace_floats(M, C)}, gamma.options());
+  k8s_amd::launch_bn_bwd(cbf(dy), cbf(x), f32(mean), f32(invstd), f32(gamma), f32(beta), relu_x, bf(dx),
+                         want_dres ? bf(dres) : nullptr, f32(dgamma), f32(dbeta), f32(work), f32(params), M, C,
                          cur_stream(), mk);
   return {dx, dres};
 }

@@ -282,8 +282,10 @@ def _bn_bwd_sums_ref(g, x, mean, invstd, gamma, beta, mask_bits=None, relu_x=Fal
     if mask_bits is not None:
         bits = mask_bits.reshape(-1, 1).int()
         on = ((bits >> torch.arange(8, device=x.device).int()) & 1).reshape(-1, C).bool()
-    elif relu_x:
-        on = ((xf - mean) * (gamma * invstd) + beta).bfloat16().float() > 0
+    elif relu_x:  # the BN forward's decision: bf16(fma(x, scale, shift)) > 0, fma emulated in fp64
+        sc = gamma * invstd
+        sh = (-mean.double() * sc.double() + beta.double()).float()
+        on = (xf.double() * sc.double() + sh.double()).float().bfloat16().float() > 0
     else:
         on = torch.ones_like(xf, dtype=torch.bool)
     ge = torch.where(on, g, torch.zeros_like(g))
