@@ -20,6 +20,8 @@
 // Both operands are consumed "MN-major" (the reduction index m is the row of dy and of x), through
 // ds_read_b64_tr_b16 transposed fragment reads of v_mfma_f32_16x16x32_bf16.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "common.h"
@@ -29,8 +31,7 @@
 namespace k8s_amd {
 namespace wgs {
 
-constexpr int THREADS = 256;  // 4 waves as 2 (k) x 2 (c)
-constexpr int KS = 64;        // rows of the reduction per stage
+constexpr int KS = 64;  // rows of the reduction per stage
 
 __device__ __attribute__((aligned(64))) uint16_t g_zero16[64];
 
@@ -86,14 +87,22 @@ struct Args {
   int chunks;
 };
 
-// NSLOT: ring depth (KT = 128: 3 slots = 72 KB, KT = 64: 4 slots = 64 KB -> two workgroups per CU either way)
-template <int KT, int CT, int NSLOT>
-__global__ void __launch_bounds__(THREADS, 2) wgrad_stream_kernel(Args a) {
+// Tile KT (dW rows = dy columns) x CT (dW columns = im2col columns), WK x WC waves each owning a
+// (KT / WK) x (CT / WC) piece, NSLOT-deep ring of 64-row stages:
+//   <128,  64, 2, 2, 3>: 256 threads, 72 KB ring, 2 workgroups / CU -- 43.7 FLOP per L2->LDS byte
+//   <128, 128, 2, 2, 2>: 256 threads, 64 KB ring, 2 workgroups / CU -- 64 FLOP / B
+//   <256, 128, 4, 2, 3>: 512 threads, 144 KB ring, 1 workgroup / CU -- 87 FLOP / B
+// L2 feeds LDS at ~70 GB/s per CU (MI355X_MICROARCH, "Indexed rows: gather into LDS"), so the FLOP/B of the
+// tile caps the compute-bound (3x3) weight gradients at ~0.78 / 1.15 / 1.56 PFLOP/s.
+//   <64, 64, 2, 2, 4>: K = 64 layers, 64 KB ring.
+template <int KT, int CT, int WK, int WC, int NSLOT>
+__global__ void __launch_bounds__(WK * WC * 64, WK * WC == 8 ? 1 : 2) wgrad_stream_kernel(Args a) {
+  constexpr int THREADS = WK * WC * 64;
   constexpr int IMG_A = KS * KT * 2, IMG_B = KS * CT * 2, STAGE = IMG_A + IMG_B;
   __shared__ __attribute__((aligned(1024))) char smem[NSLOT * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wk = wid >> 1, wc = wid & 1;
+  const int wk = wid / WC, wc = wid % WC;
 
   // tiles that share a chunk go to one XCD (bid % 8) and run back to back (bid / 8)
   const int T = a.tiles_k * a.tiles_c;
@@ -115,6 +124,8 @@ __global__ void __launch_bounds__(THREADS, 2) wgrad_stream_kernel(Args a) {
   constexpr int LA = KS * UA / THREADS, LB = KS * UB / THREADS;  // glds per thread per stage
   static_assert(LA >= 1 && LB >= 1, "tile too small for 256 threads");
   const int dma_off = wid * 1024;
+  static_assert(KT == 64 || KT == 128 || KT == 256, "KT");
+  static_assert(CT == 64 || CT == 128, "CT");
   auto src_a = [&](int j, int m0) -> const void* {
     const int sl = j * THREADS + tid, row = sl / UA, up = sl % UA;
     const int u = KT == 64 ? (up ^ swz128(row)) : (up ^ swz256(row));
@@ -145,7 +156,7 @@ __global__ void __launch_bounds__(THREADS, 2) wgrad_stream_kernel(Args a) {
   };
   constexpr int PER = LA + LB;  // glds per thread per stage
 
-  constexpr int RT = KT / 32, CTT = CT / 32;  // 16-wide tiles per wave: (KT/2)/16, (CT/2)/16
+  constexpr int RT = KT / WK / 16, CTT = CT / WC / 16;  // 16-wide tiles per wave
   f32x4_t acc[RT][CTT];
 #pragma unroll
   for (int i = 0; i < RT; ++i)
@@ -169,9 +180,9 @@ __global__ void __launch_bounds__(THREADS, 2) wgrad_stream_kernel(Args a) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
-      for (int i = 0; i < RT; ++i) tr_load<KT>(ar[kk * RT + i], st, wk * (KT / 2) + i * 16, kk, lane);
+      for (int i = 0; i < RT; ++i) tr_load<KT>(ar[kk * RT + i], st, wk * (KT / WK) + i * 16, kk, lane);
 #pragma unroll
-      for (int j = 0; j < CTT; ++j) tr_load<CT>(br[kk * CTT + j], st + IMG_A, wc * (CT / 2) + j * 16, kk, lane);
+      for (int j = 0; j < CTT; ++j) tr_load<CT>(br[kk * CTT + j], st + IMG_A, wc * (CT / WC) + j * 16, kk, lane);
     }
     static_assert((2 * RT) % 4 == 0 && (2 * CTT) % 4 == 0, "tie groups of 4");
 #pragma unroll
@@ -192,14 +203,14 @@ __global__ void __launch_bounds__(THREADS, 2) wgrad_stream_kernel(Args a) {
                                                               join8(ar[kk * RT + i].lo, ar[kk * RT + i].hi),
                                                               acc[i][j], 0, 0, 0);
   }
-  // acc[i][j]: lane holds dW[k = k0 + wk*KT/2 + i*16 + (lane & 15)][col0 + wc*CT/2 + j*16 + 4*(lane >> 4) + r]
+  // acc[i][j]: lane holds dW[k = k0 + wk*KT/WK + i*16 + (lane & 15)][col0 + wc*CT/WC + j*16 + 4*(lane >> 4) + r]
 #pragma unroll
   for (int i = 0; i < RT; ++i) {
-    const int k = k0 + wk * (KT / 2) + i * 16 + (lane & 15);
+    const int k = k0 + wk * (KT / WK) + i * 16 + (lane & 15);
     if (k >= a.dy.K) continue;
 #pragma unroll
     for (int j = 0; j < CTT; ++j) {
-      const int cl = wc * (CT / 2) + j * 16 + 4 * (lane >> 4);
+      const int cl = wc * (CT / WC) + j * 16 + 4 * (lane >> 4);
       if (c0 + cl >= a.xs.C) continue;
       float* d = a.dw + (long)k * a.RSC + col0 + cl;
 #pragma unroll
@@ -210,12 +221,36 @@ __global__ void __launch_bounds__(THREADS, 2) wgrad_stream_kernel(Args a) {
 
 }  // namespace wgs
 
-// Shapes this kernel takes: C % 64 == 0 (a tile's columns inside one tap), K % 64 == 0, few output tiles.
+// Tile choice: 128 x 64 (64 x 64 for K = 64), or $K8S_AMD_WGS_TILE ("128x64", "128x128", "256x128", "64x64")
+// for A/B runs.
+struct WgsTile {
+  int KT, CT;
+};
+static WgsTile wgs_tile(int K, int RSC) {
+  if (const char* e = getenv("K8S_AMD_WGS_TILE")) {
+    int kt = 0, ct = 0;
+    if (sscanf(e, "%dx%d", &kt, &ct) == 2 && K % kt == 0 && RSC % ct == 0 &&
+        ((kt == 128 && (ct == 64 || ct == 128)) || (kt == 256 && ct == 128) || (kt == 64 && ct == 64)))
+      return WgsTile{kt, ct};
+  }
+  // measured (scripts/bench_wgrad_tiles.py, b1024): the larger tiles are not faster on the shapes this kernel
+  // keeps (their rings leave one or two workgroups per CU); they stay selectable for A/B runs
+  if (K % 128 == 0) return WgsTile{128, 64};
+  return WgsTile{64, 64};
+}
+
+// Shapes this kernel takes: C % 64 == 0 (a tile's columns inside one tap), K % 64 == 0, and a 64-wide side of
+// dW (K == 64 or R*S*C == 64: the memory-bound ResNet-50 layers at 56 x 56). Measured at batch 1024
+// (scripts/bench_wgrad_tiles.py, profiles/r02_wgrad_tiles.jsonl) the generic split-K kernel is 5-60 % faster on
+// every other ResNet-50 weight gradient, the 3x3 ones included ($K8S_AMD_WGS_ANY=1 lifts the restriction).
 bool wgrad_stream_eligible(int N, int Ho, int Wo, int C, int K, int R, int S) {
   if (C % 64 != 0 || K % 64 != 0) return false;
-  const long tiles = (long)(K / (K >= 128 ? 128 : 64)) * ((long)R * S * C / 64);
+  const WgsTile t = wgs_tile(K, R * S * C);
+  const long tiles = (long)(K / t.KT) * ((long)R * S * C / t.CT);
   const long rows = (long)N * Ho * Wo;
-  return tiles <= 96 && rows >= 64L * 64;
+  const char* any = getenv("K8S_AMD_WGS_ANY");
+  const bool narrow = K == 64 || R * S * C == 64 || (any && any[0] == '1');
+  return narrow && tiles <= 96 && rows >= 64L * 64;
 }
 
 void launch_wgrad_stream(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int C, int K, int R,
@@ -231,23 +266,28 @@ void launch_wgrad_stream(const uint16_t* x, const uint16_t* dy, float* dw, int N
   a.dw = dw;
   a.RSC = RSC;
   a.S = S;
-  const int KT = K >= 128 ? 128 : 64;
-  a.tiles_k = K / KT;
-  a.tiles_c = RSC / 64;
+  const WgsTile t = wgs_tile(K, RSC);
+  a.tiles_k = K / t.KT;
+  a.tiles_c = RSC / t.CT;
   const int T = a.tiles_k * a.tiles_c;
   const int steps = (M + KS - 1) / KS;
-  // ~4 workgroups per CU in total, at least 8 k-steps each (prologue amortised), chunks a multiple of 8 so the
-  // tiles of one chunk share an XCD
-  int chunks = (4 * 256 + T - 1) / T;
+  // ~4 (256-thread) or ~2 (512-thread) workgroups per CU in total, at least 8 k-steps each (prologue amortised),
+  // chunks a multiple of 8 so the tiles of one chunk share an XCD
+  const int per_cu = t.KT == 256 ? 2 : 4;
+  int chunks = (per_cu * 256 + T - 1) / T;
   chunks = (chunks + 7) / 8 * 8;
   chunks = std::max(8, std::min(chunks, (steps + 7) / 8));
   a.chunk_steps = (steps + chunks - 1) / chunks;
   a.chunks = (steps + a.chunk_steps - 1) / a.chunk_steps;
   const int grid = ((a.chunks + 7) / 8) * 8 * T;
-  if (KT == 128)
-    hipLaunchKernelGGL((wgrad_stream_kernel<128, 64, 3>), dim3(grid), dim3(THREADS), 0, st, a);
+  if (t.KT == 256)
+    hipLaunchKernelGGL((wgrad_stream_kernel<256, 128, 4, 2, 3>), dim3(grid), dim3(512), 0, st, a);
+  else if (t.KT == 128 && t.CT == 128)
+    hipLaunchKernelGGL((wgrad_stream_kernel<128, 128, 2, 2, 2>), dim3(grid), dim3(256), 0, st, a);
+  else if (t.KT == 128)
+    hipLaunchKernelGGL((wgrad_stream_kernel<128, 64, 2, 2, 3>), dim3(grid), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((wgrad_stream_kernel<64, 64, 4>), dim3(grid), dim3(THREADS), 0, st, a);
+    hipLaunchKernelGGL((wgrad_stream_kernel<64, 64, 2, 2, 4>), dim3(grid), dim3(256), 0, st, a);
 }
 
 }  // namespace k8s_amd

@@ -53,6 +53,7 @@ def main():
             "conv_stats": lambda: C_.conv_fwd(x, w, 1, 0, 1, False, None, 0, st),
             "conv": lambda: C_.conv_fwd(x, w, 1, 0, 1, False, None, 0, None),
             "gemm": lambda: C_.gemm(x.view(M, C), True, w.view(K, C), True, None, False, None, 0, None, False, 1.0, 1),
+            "blas": lambda: torch.mm(x.view(M, C), w.view(K, C).t()),  # hipBLASLt reference point
             "copy": lambda: torch.empty(M, K, device=dev, dtype=torch.bfloat16).copy_(
                 x.view(M, C)[:, :1].expand(M, K)),
         }
