@@ -409,8 +409,8 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
   }
   const int key = kw + li;
   if (key < a.Sk) {
-    uint16_t* dkp = a.dk + (((long)b * a.Sk + key) * a.Hkv + hk) * D;
-    uint16_t* dvp = a.dv + (((long)b * a.Sk + key) * a.Hkv + hk) * D;
+    uint16_t* dkp = a.dk + b * a.sgkb + key * a.sgks + hk * a.sgkh;
+    uint16_t* dvp = a.dv + b * a.sgvb + key * a.sgvs + hk * a.sgvh;
 #pragma unroll
     for (int d = 0; d < ND; ++d) {
       bf16x4_t x, y;
@@ -543,7 +543,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dq_kernel(AttnBwdArgs
     __syncthreads();
   }
   if (qi < a.Sq) {
-    uint16_t* dqp = a.dq + (((long)b * a.Sq + qi) * a.Hq + h) * D;
+    uint16_t* dqp = a.dq + b * a.sgqb + qi * a.sgqs + h * a.sgqh;
 #pragma unroll
     for (int d = 0; d < ND; ++d) {
       bf16x4_t x;

@@ -118,10 +118,12 @@ struct AttnBwdArgs {
   const uint16_t *q, *k, *v, *dO;
   const float* lse;
   float* delta;       // [B, Hq, lse_ld] scratch
-  uint16_t* dq;       // [B, Sq, Hq, D]
-  uint16_t *dk, *dv;  // [B, Sk, Hkv, D]
+  uint16_t* dq;       // [B, Sq, Hq, D] at strides (sgqb, sgqs, sgqh)
+  uint16_t *dk, *dv;  // [B, Sk, Hkv, D] at strides (sgkb, sgks, sgkh) / (sgvb, sgvs, sgvh)
   const int* kv_lens;
   long sqb, sqs, sqh, skb, sks, skh, svb, svs, svh, sdb, sds, sdh;
+  // output strides: a packed [B*S, (Hq + 2*Hkv) * D] gradient of a fused QKV projection is written in place
+  long sgqb, sgqs, sgqh, sgkb, sgks, sgkh, sgvb, sgvs, sgvh;
   long lse_ld;
   int B, Sq, Sk, Hq, Hkv, causal;
   float scale_log2, scale;

@@ -454,6 +454,8 @@ Tensor swiglu_bwd(Tensor gu, Tensor dy) {
   k8s_amd::launch_swiglu_bwd(cbf(gu), cbf(dy), bf(dgu), gu.numel() / F2, (int)(F2 / 2), cur_stream());
   return dgu;
 }
+// in place on x [T, H*D]: contiguous, or a 2-D column slice of a wider row-major tensor (row stride = its
+// leading dimension -- the q and k heads of a packed QKV projection rotated without a copy)
 void rope_(Tensor x, Tensor pos, Tensor table, bool inverse) {
   check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x");
   check_cuda(pos, "pos"); check_dtype(pos, at::kInt, "pos");
@@ -461,9 +463,20 @@ void rope_(Tensor x, Tensor pos, Tensor table, bool inverse) {
   const int D = (int)table.size(1) * 2;
   TORCH_CHECK(D % 16 == 0, "head dim must be a multiple of 16");
   const long T = pos.numel();
-  TORCH_CHECK(x.numel() % (T * D) == 0, "x must be [T, H*D]");
-  const int H = (int)(x.numel() / (T * D));
-  k8s_amd::launch_rope(bf(x), (long)H * D, pos.data_ptr<int>(), f32(table), T, H, D, inverse, cur_stream());
+  long ld;
+  int H;
+  if (x.is_contiguous()) {
+    TORCH_CHECK(x.numel() % (T * D) == 0, "x must be [T, H*D]");
+    H = (int)(x.numel() / (T * D));
+    ld = (long)H * D;
+  } else {
+    TORCH_CHECK(x.dim() == 2 && x.size(0) == T && x.stride(1) == 1 && x.size(1) % D == 0 && x.stride(0) % 8 == 0,
+                "strided x must be a [T, H*D] column slice with unit column stride");
+    check_aligned(x, "x");
+    H = (int)(x.size(1) / D);
+    ld = x.stride(0);
+  }
+  k8s_amd::launch_rope(bf(x), ld, pos.data_ptr<int>(), f32(table), T, H, D, inverse, cur_stream());
 }
 Tensor gelu_bwd(Tensor dy, Tensor pre) {
   check_cuda(dy, "dy"); check_cuda(pre, "pre");
@@ -532,8 +545,11 @@ std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, bool causal, c10::op
   return {o, lse};
 }
 
+// dq / dk / dv are new contiguous tensors, or -- with `dqkv` given -- views into that [B*S, (Hq + 2*Hkv) * D]
+// buffer laid out like the packed QKV projection q / k / v were sliced from (q at column 0, k at Hq*D, v at
+// (Hq + Hkv)*D): the fused projection's gradient is written in place, no concatenation afterwards.
 std::vector<Tensor> flash_bwd(Tensor dO, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal,
-                              c10::optional<Tensor> kv_lens, double scale) {
+                              c10::optional<Tensor> kv_lens, double scale, c10::optional<Tensor> dqkv) {
   const long D = q.size(-1);
   TORCH_CHECK(D == 64 || D == 128, "head dim must be 64 or 128");
   check_attn_operand(q, "q", D); check_attn_operand(k, "k", D); check_attn_operand(v, "v", D);
@@ -546,9 +562,21 @@ std::vector<Tensor> flash_bwd(Tensor dO, Tensor q, Tensor k, Tensor v, Tensor o,
   TORCH_CHECK(lse.dim() == 3 && lse.size(0) == B && lse.size(1) == Hq && lse.size(2) == ld,
               "lse must be the [B, Hq, round_up(Sq, 128)] tensor flash_fwd returned");
   auto delta = torch::empty({B, Hq, ld}, q.options().dtype(at::kFloat));
-  auto dq = torch::empty({B, Sq, Hq, D}, q.options());
-  auto dk = torch::empty({B, Sk, Hkv, D}, q.options());
-  auto dv = torch::empty({B, Sk, Hkv, D}, q.options());
+  Tensor dq, dk, dv;
+  if (dqkv) {
+    TORCH_CHECK(Sq == Sk, "packed QKV gradient needs self-attention (Sq == Sk)");
+    const long W = (Hq + 2 * Hkv) * D;
+    check_cuda(*dqkv, "dqkv"); check_dtype(*dqkv, at::kBFloat16, "dqkv");
+    TORCH_CHECK(dqkv->is_contiguous() && dqkv->numel() == B * Sq * W, "dqkv must be contiguous [B*S, (Hq+2*Hkv)*D]");
+    auto g = dqkv->view({B, Sq, Hq + 2 * Hkv, D});
+    dq = g.narrow(2, 0, Hq);
+    dk = g.narrow(2, Hq, Hkv);
+    dv = g.narrow(2, Hq + Hkv, Hkv);
+  } else {
+    dq = torch::empty({B, Sq, Hq, D}, q.options());
+    dk = torch::empty({B, Sk, Hkv, D}, q.options());
+    dv = torch::empty({B, Sk, Hkv, D}, q.options());
+  }
   k8s_amd::AttnBwdArgs a;
   a.q = cbf(q); a.k = cbf(k); a.v = cbf(v); a.dO = cbf(dO); a.lse = f32(lse); a.delta = f32(delta);
   a.dq = bf(dq); a.dk = bf(dk); a.dv = bf(dv); a.kv_lens = kv_lens_ptr(kv_lens, B);
@@ -557,6 +585,10 @@ std::vector<Tensor> flash_bwd(Tensor dO, Tensor q, Tensor k, Tensor v, Tensor o,
   a.skb = k.stride(0); a.sks = k.stride(1); a.skh = k.stride(2);
   a.svb = v.stride(0); a.svs = v.stride(1); a.svh = v.stride(2);
   a.sdb = dO.stride(0); a.sds = dO.stride(1); a.sdh = dO.stride(2);
+  a.sgqb = dq.stride(0); a.sgqs = dq.stride(1); a.sgqh = dq.stride(2);
+  a.sgkb = dk.stride(0); a.sgks = dk.stride(1); a.sgkh = dk.stride(2);
+  a.sgvb = dv.stride(0); a.sgvs = dv.stride(1); a.sgvh = dv.stride(2);
+  TORCH_CHECK(dq.stride(3) == 1 && dk.stride(3) == 1 && dv.stride(3) == 1, "gradient rows must be contiguous");
   a.B = B; a.Sq = Sq; a.Sk = Sk; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal;
   a.scale_log2 = (float)(scale * 1.4426950408889634);
   a.scale = (float)scale;
@@ -635,7 +667,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_fwd", &flash_fwd);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
-  m.def("flash_bwd", &flash_bwd);
+  m.def("flash_bwd", &flash_bwd, py::arg("dO"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
+        py::arg("lse"), py::arg("causal"), py::arg("kv_lens"), py::arg("scale"), py::arg("dqkv") = py::none());
   m.attr("conv_stat_replicas") = k8s_amd::kConvStatReplicas;
   m.attr("arch") = "gfx950";
 }

@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from k8s_amd.ops import nn as K
-from k8s_amd.ops.attention import attention
+from k8s_amd.ops.attention import attention_qkv
 from k8s_amd.parallel.flat import ParamStore, init_const, init_normal
 
 
@@ -72,9 +72,7 @@ class BertLayer(nn.Module):
         h, nh = c.hidden, c.heads
         d = h // nh
         qkv = K.linear(x, self.qkv_w, self.qkv_b)  # [T, 3h]
-        q, k, v = qkv.split([h, h, h], dim=-1)
-        o = attention(q.reshape(B, S, nh, d), k.reshape(B, S, nh, d), v.reshape(B, S, nh, d), causal=False,
-                      kv_lens=kv_lens)
+        o = attention_qkv(qkv, B, S, nh, nh, d, causal=False, kv_lens=kv_lens)  # packed QKV gradient in place
         a = K.linear(o.reshape(B * S, h), self.o_w, self.o_b)
         x, _ = K.layer_norm(a, self.ln1_g, self.ln1_b, c.eps, residual=x)
         f = K.linear(x, self.f1_w, self.f1_b, act="gelu")

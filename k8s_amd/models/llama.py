@@ -23,7 +23,7 @@ import torch
 import torch.nn as nn
 
 from k8s_amd.ops import nn as K
-from k8s_amd.ops.attention import attention
+from k8s_amd.ops.attention import attention_qkv
 from k8s_amd.parallel.flat import ParamStore, init_const, init_normal
 
 
@@ -78,11 +78,8 @@ class LlamaLayer(nn.Module):
         else:
             hn, res = K.rms_norm(x, self.attn_norm, c.eps, residual=res)
         qkv = K.linear(hn, self.qkv)
-        q, k, v = qkv.split([c.heads * d, c.kv_heads * d, c.kv_heads * d], dim=-1)
-        q = K.rope(q, pos, table)
-        k = K.rope(k, pos, table)
-        o = attention(q.reshape(B, S, c.heads, d), k.reshape(B, S, c.kv_heads, d),
-                      v.reshape(B, S, c.kv_heads, d), causal=True)
+        # rotary q/k, causal GQA flash attention and the packed QKV gradient in one op (no split/cat/copies)
+        o = attention_qkv(qkv, B, S, c.heads, c.kv_heads, d, causal=True, rope=(pos, table))
         a = K.linear(o.reshape(B * S, c.heads * d), self.o)
         hn, res = K.rms_norm(a, self.mlp_norm, c.eps, residual=res)
         gu = K.linear(hn, self.gate_up)

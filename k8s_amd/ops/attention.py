@@ -92,3 +92,62 @@ def attention(q, k, v, causal: bool = False, kv_lens: Optional[torch.Tensor] = N
     if _flash_ok(q, k, v):
         return _Flash.apply(q, k, v, causal, kv_lens, scale)
     return _Reference.apply(q, k, v, causal, kv_lens, scale)
+
+
+class _FlashQKV(torch.autograd.Function):
+    """Self-attention straight off a fused QKV projection [T = B*S, (H + 2*Hkv)*D]: q / k / v are strided views,
+    the optional rotary embedding rotates the q and k columns of one copy in place, and the backward writes the
+    packed gradient in place (flash_bwd ``dqkv``) and un-rotates it in place -- no split / concatenation / rope
+    copies on either pass."""
+
+    @staticmethod
+    def forward(ctx, qkv, B, S, H, Hkv, D, causal, kv_lens, scale, pos, table):
+        C = _load()
+        if kv_lens is not None:
+            kv_lens = kv_lens.to(device=qkv.device, dtype=torch.int32).contiguous()
+        x = qkv.contiguous()
+        if pos is not None:
+            x = x.clone() if x.data_ptr() == qkv.data_ptr() else x
+            C.rope_(x[:, : (H + Hkv) * D], pos, table, False)
+        g = x.view(B, S, H + 2 * Hkv, D)
+        q, k, v = g.narrow(2, 0, H), g.narrow(2, H, Hkv), g.narrow(2, H + Hkv, Hkv)
+        o, lse = C.flash_fwd(q, k, v, causal, kv_lens, scale)
+        ctx.save_for_backward(x, o, lse, kv_lens if kv_lens is not None else torch.empty(0),
+                              pos if pos is not None else torch.empty(0), table if table is not None else torch.empty(0))
+        ctx.meta = (B, S, H, Hkv, D, causal, scale, kv_lens is not None, pos is not None)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        x, o, lse, lens, pos, table = ctx.saved_tensors
+        B, S, H, Hkv, D, causal, scale, has_lens, has_rope = ctx.meta
+        C = _load()
+        g = x.view(B, S, H + 2 * Hkv, D)
+        q, k, v = g.narrow(2, 0, H), g.narrow(2, H, Hkv), g.narrow(2, H + Hkv, Hkv)
+        dqkv = torch.empty_like(x)
+        C.flash_bwd(do.contiguous(), q, k, v, o, lse, causal, lens if has_lens else None, scale, dqkv)
+        if has_rope:
+            C.rope_(dqkv[:, : (H + Hkv) * D], pos, table, True)
+        return dqkv, None, None, None, None, None, None, None, None, None, None
+
+
+def attention_qkv(qkv, B: int, S: int, heads: int, kv_heads: int, head_dim: int, causal: bool = False,
+                  kv_lens: Optional[torch.Tensor] = None, rope: Optional[tuple] = None,
+                  scale: Optional[float] = None):
+    """Self-attention of a packed QKV projection ``qkv`` [B*S, (heads + 2*kv_heads) * head_dim] (q heads, then k,
+    then v); ``rope`` = (pos [B*S] int32, table) applies rotary embeddings to q and k. Returns o [B, S, heads, D].
+    GPU bf16: one fused path (``_FlashQKV``); otherwise the split + ``attention`` reference composition."""
+    D = head_dim
+    scale = scale or 1.0 / math.sqrt(D)
+    W = (heads + 2 * kv_heads) * D
+    if qkv.is_cuda and qkv.dtype == torch.bfloat16 and D in (64, 128) and qkv.shape[-1] == W and \
+            W % 8 == 0 and qkv.is_contiguous():
+        pos, table = rope if rope is not None else (None, None)
+        return _FlashQKV.apply(qkv, B, S, heads, kv_heads, D, causal, kv_lens, scale, pos, table)
+    q, k, v = qkv.split([heads * D, kv_heads * D, kv_heads * D], dim=-1)
+    if rope is not None:
+        from k8s_amd.ops import nn as _nn
+
+        q, k = _nn.rope(q, rope[0], rope[1]), _nn.rope(k, rope[0], rope[1])
+    return attention(q.reshape(B, S, heads, D), k.reshape(B, S, kv_heads, D), v.reshape(B, S, kv_heads, D),
+                     causal=causal, kv_lens=kv_lens, scale=scale)

@@ -70,3 +70,36 @@ def test_flash_lse(cuda):
     s = torch.einsum("bqhd,bkhd->bhqk", q.float(), k.float()) * 0.1
     ref = torch.logsumexp(s, -1) / math.log(2.0)  # the kernel stores log2-domain lse
     _close(lse[..., :S], ref, 1e-3, "lse")
+
+
+@pytest.mark.parametrize("B,S,H,Hkv,D,causal,rope,lens", [
+    (2, 128, 12, 12, 64, False, False, True),    # BERT-style, key padding
+    (1, 512, 32, 8, 128, True, True, False),     # Llama-style GQA + rotary
+])
+def test_attention_qkv_packed_matches_split(cuda, B, S, H, Hkv, D, causal, rope, lens):
+    """attention_qkv (strided q/k/v views of the fused projection, in-place rotary, packed dqkv written in place)
+    against the fp32 split + rope + reference-attention composition, forward and the packed gradient."""
+    from k8s_amd.ops import nn as K
+    from k8s_amd.ops.attention import attention_qkv, attention_reference
+
+    torch.manual_seed(7)
+    W = (H + 2 * Hkv) * D
+    qkv = (torch.randn(B * S, W, device=cuda) * 0.5).bfloat16().requires_grad_(True)
+    pos = torch.arange(S, device=cuda, dtype=torch.int32).repeat(B)
+    table = K.rope_table(S, D, device=cuda)
+    kv_lens = torch.tensor([S - 17 * (i + 1) for i in range(B)], device=cuda, dtype=torch.int32) if lens else None
+    o = attention_qkv(qkv, B, S, H, Hkv, D, causal=causal, kv_lens=kv_lens,
+                      rope=(pos, table) if rope else None)
+    go = torch.randn_like(o)
+    (g,) = torch.autograd.grad(o, qkv, go)
+
+    xr = qkv.detach().float().requires_grad_(True)
+    q, k, v = xr.split([H * D, Hkv * D, Hkv * D], dim=-1)
+    if rope:
+        q, k = K._rope_ref(q, pos, table), K._rope_ref(k, pos, table)
+    ref = attention_reference(q.reshape(B, S, H, D), k.reshape(B, S, Hkv, D), v.reshape(B, S, Hkv, D), causal,
+                              kv_lens)
+    (gr,) = torch.autograd.grad(ref, xr, go.float())
+    rel = lambda a, b: ((a.float() - b.float()).norm() / b.float().norm()).item()  # noqa: E731
+    assert rel(o, ref) < 2e-2
+    assert rel(g, gr) < 3e-2

@@ -25,8 +25,19 @@ def test_templates_balanced():
                 yaml.safe_load(_read(root, "values.yaml")) if f == "values.yaml" else None
 
 
+def _render_values(text, values):
+    """The `{{ .Values.a.b | quote }}` placeholders of a template, filled from values.yaml (no helm binary here)."""
+    def sub(m):
+        v = values
+        for k in m.group(1).split("."):
+            v = v[k]
+        return json.dumps(str(v)) if m.group(2) else str(v)
+    return re.sub(r"\{\{\s*\.Values\.([\w.]+)\s*(\|\s*quote)?\s*\}\}", sub, text)
+
+
 def test_amd_preset_controller_config():
-    t = _read(CHART, "templates", "config.yaml")
+    values = yaml.safe_load(_read(CHART, "values.yaml"))
+    t = _render_values(_read(CHART, "templates", "config.yaml"), values)
     body = t.split("controller_config_file.yaml: |\n", 1)[1].split("{{-", 1)[0]
     body = "\n".join(line[4:] for line in body.splitlines())
     cfg = json.loads(op.controller_config(json.dumps(yaml.safe_load(body))))
@@ -34,6 +45,7 @@ def test_amd_preset_controller_config():
     acc = cfg["Accelerators"]["amd.com/gpu"]
     assert {v["MountPath"] for v in acc["Volumes"]} >= {"/opt/rocm", "/dev/kfd", "/dev/dri"}
     assert {"Name": "HSA_ENABLE_IPC_MODE_LEGACY", "Value": "0"} in acc["EnvVars"]
+    assert {"Name": "NCCL_MIN_NCHANNELS", "Value": str(values["rccl"]["minChannels"])} in acc["EnvVars"]
     assert cfg["GrpcServerFilePath"].endswith("grpc_tensorflow_server.py")
 
 
