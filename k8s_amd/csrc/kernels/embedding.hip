@@ -1,0 +1,143 @@
+// K9: token-embedding gather (sum of up to 3 tables: BERT word + position + token type; Llama: 1) and its
+// scatter-add backward into the fp32 flat-gradient slots.
+//
+//   fwd: out[t][:] = sum_i W_i[row_i(t)][:]            (bf16 tables, fp32 sum, bf16 out)
+//   bwd: dW_i[row_i(t)][:] += g[t][:]                    (fp32 atomics straight into the gradient slot)
+// row_i(t) = ids_i[t] (int64), or t % S for a position table (no [B, S] position-id tensor).
+// Flat launches, one 16-B vector (8 columns) of one token per thread (batchnorm.hip header: the streaming
+// shape MI355X serves fastest). Tables with at most 4 rows (BERT's token types) are reduced per thread over a
+// run of tokens in registers first: every token adding into the same 2 rows would serialize the atomics on a
+// handful of addresses (MI355X_MICROARCH "Global float atomics": one hot row is ~14x slower).
+#include <stdexcept>
+
+#include "common.h"
+#include "launchers.h"
+
+namespace k8s_amd {
+
+struct EmbTab {
+  const uint16_t* w;    // [V][D] bf16 (forward)
+  float* g;             // [V][D] fp32 gradient slot (backward)
+  const int64_t* ids;   // [T] or null for a position table
+  int V;
+};
+struct EmbArgs {
+  EmbTab t[3];
+  int ntab, T, D, S;  // S: sequence length (position rows = t % S)
+};
+
+__device__ __forceinline__ int emb_row(const EmbTab& e, int t, int S) {
+  if (!e.ids) return t % S;
+  const long r = e.ids[t];
+  return (int)(r < 0 ? 0 : (r >= e.V ? e.V - 1 : r));  // out-of-range ids clamp (torch raises; we never fault)
+}
+
+__global__ void __launch_bounds__(256) embed_fwd_kernel(EmbArgs a, uint16_t* __restrict__ out, int nvec) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= nvec) return;
+  const int cv = a.D >> 3;
+  const int t = e / cv, c = (e - t * cv) * 8;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    if (i >= a.ntab) break;
+    const int row = emb_row(a.t[i], t, a.S);
+    float v[8];
+    load8(a.t[i].w + (long)row * a.D + c, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+  }
+  store8(out + (long)e * 8, acc);
+}
+
+// large tables: one token's 8 columns per thread, 8 fp32 atomics per table
+__global__ void __launch_bounds__(256) embed_bwd_kernel(EmbArgs a, const uint16_t* __restrict__ g, int nvec,
+                                                        int tab_mask) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= nvec) return;
+  const int cv = a.D >> 3;
+  const int t = e / cv, c = (e - t * cv) * 8;
+  float v[8];
+  load8(g + (long)e * 8, v);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    if (i >= a.ntab || !((tab_mask >> i) & 1)) continue;
+    float* dst = a.t[i].g + (long)emb_row(a.t[i], t, a.S) * a.D + c;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(dst + j, v[j]);
+  }
+}
+
+// small tables (V <= 4): thread = (run of RUN tokens, 8 columns); per-row sums in registers, then V*8 atomics
+constexpr int EMB_RUN = 64;
+__global__ void __launch_bounds__(256) embed_bwd_small_kernel(EmbArgs a, const uint16_t* __restrict__ g, int tab,
+                                                              int nthreads) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= nthreads) return;
+  const int cv = a.D >> 3;
+  const int run = e / cv, c = (e - run * cv) * 8;
+  const EmbTab& tb = a.t[tab];
+  float acc[4][8];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[r][j] = 0.f;
+  const int t0 = run * EMB_RUN, t1 = min(a.T, t0 + EMB_RUN);
+  for (int t = t0; t < t1; ++t) {
+    const int row = emb_row(tb, t, a.S);
+    float v[8];
+    load8(g + (long)t * a.D + c, v);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (row == r) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[r][j] += v[j];
+      }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (r >= tb.V) break;
+    float* dst = tb.g + (long)r * a.D + c;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(dst + j, acc[r][j]);
+  }
+}
+
+static EmbArgs emb_args(const EmbTable* tabs, int ntab, int T, int D, int S) {
+  if (ntab < 1 || ntab > 3) throw std::runtime_error("embedding: 1 to 3 tables");
+  if (D % 8 != 0) throw std::runtime_error("embedding: width must be a multiple of 8");
+  if ((long)T * (D / 8) >= (1L << 31)) throw std::runtime_error("embedding: too many elements");
+  EmbArgs a;
+  for (int i = 0; i < 3; ++i) a.t[i] = EmbTab{nullptr, nullptr, nullptr, 1};
+  for (int i = 0; i < ntab; ++i) a.t[i] = EmbTab{tabs[i].w, tabs[i].g, tabs[i].ids, tabs[i].V};
+  a.ntab = ntab;
+  a.T = T;
+  a.D = D;
+  a.S = S;
+  return a;
+}
+
+void launch_embed_fwd(const EmbTable* tabs, int ntab, int T, int D, int S, uint16_t* out, hipStream_t st) {
+  const EmbArgs a = emb_args(tabs, ntab, T, D, S);
+  const int nvec = T * (D / 8);
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3(cdiv(nvec, 256)), dim3(256), 0, st, a, out, nvec);
+}
+
+void launch_embed_bwd(const EmbTable* tabs, int ntab, int T, int D, int S, const uint16_t* g, hipStream_t st) {
+  const EmbArgs a = emb_args(tabs, ntab, T, D, S);
+  const int nvec = T * (D / 8);
+  int big = 0;
+  for (int i = 0; i < ntab; ++i) {
+    if (tabs[i].V <= 4) {
+      const int nthreads = cdiv(T, EMB_RUN) * (D / 8);
+      hipLaunchKernelGGL(embed_bwd_small_kernel, dim3(cdiv(nthreads, 256)), dim3(256), 0, st, a, g, i, nthreads);
+    } else {
+      big |= 1 << i;
+    }
+  }
+  if (big) hipLaunchKernelGGL(embed_bwd_kernel, dim3(cdiv(nvec, 256)), dim3(256), 0, st, a, g, nvec, big);
+}
+
+}  // namespace k8s_amd

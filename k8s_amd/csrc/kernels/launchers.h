@@ -131,6 +131,20 @@ struct AttnBwdArgs {
 void launch_flash_fwd(const AttnFwdArgs& a, int D, hipStream_t st);
 void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, long sos, long soh, hipStream_t st);
 
+// ---- embedding.hip: sum of up to 3 table gathers (fwd) / fp32 atomic scatter-add into gradient slots (bwd)
+struct EmbTable {
+  const uint16_t* w;   // [V][D] bf16 table (forward)
+  float* g;            // [V][D] fp32 gradient (backward; accumulated into)
+  const int64_t* ids;  // [T] row ids, or null: row = token % S (position table)
+  int V;
+};
+void launch_embed_fwd(const EmbTable* tabs, int ntab, int T, int D, int S, uint16_t* out, hipStream_t st);
+void launch_embed_bwd(const EmbTable* tabs, int ntab, int T, int D, int S, const uint16_t* g, hipStream_t st);
+
+// ---- NHWC average pooling over H*W (pool.hip): y[n][c] = mean_hw x[n][hw][c] (fp32 accumulate, bf16 out)
+void launch_avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st);
+void launch_avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st);
+
 // ---- NHWC max pooling (pool.hip): idx = winning window position per output element (uint8)
 void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
                         int k, int s, int p, hipStream_t st);

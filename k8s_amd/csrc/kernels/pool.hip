@@ -114,4 +114,65 @@ void launch_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, in
                      p, (int)total, make_fastdiv(C / 8), make_fastdiv(W), make_fastdiv(H));
 }
 
+// Global average pool (the ResNet head): thread = (image, 8 channels) summing HW rows in fp32; backward writes
+// dy / HW to every pixel, one 16-B vector per thread.
+__global__ void __launch_bounds__(256) avgpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                          int N, int HW, int C, float inv) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int cv = C >> 3;
+  if (e >= N * cv) return;
+  const int n = e / cv, c = (e - n * cv) * 8;
+  const uint16_t* p = x + (long)n * HW * C + c;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  int i = 0;
+  for (; i + 3 < HW; i += 4) {  // 4 rows in flight
+    float v[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load8(p + (long)(i + u) * C, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[u][j];
+  }
+  for (; i < HW; ++i) {
+    float v[8];
+    load8(p + (long)i * C, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] *= inv;
+  store8(y + (long)n * C + c, acc);
+}
+
+__global__ void __launch_bounds__(256) avgpool_bwd_kernel(const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx,
+                                                          int total, int HW, int C, FastDiv fcv, FastDiv fhw,
+                                                          float inv) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= total) return;
+  const int cv = C >> 3;
+  const int pix = fcv.div(e), c = (e - pix * cv) * 8;
+  const int n = fhw.div(pix);
+  float v[8];
+  load8(dy + (long)n * C + c, v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] *= inv;
+  store8(dx + (long)e * 8, v);
+}
+
+void launch_avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st) {
+  if (C % 8 != 0) throw std::runtime_error("avgpool: C must be a multiple of 8");
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(cdiv((long)N * (C / 8), 256)), dim3(256), 0, st, x, y, N, HW, C,
+                     1.f / (float)HW);
+}
+
+void launch_avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st) {
+  const long total = (long)N * HW * (C / 8);
+  if (C % 8 != 0 || total >= (1L << 31)) throw std::runtime_error("avgpool: C % 8 != 0 or tensor too large");
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, dy, dx, (int)total, HW, C,
+                     make_fastdiv(C / 8), make_fastdiv(HW), 1.f / (float)HW);
+}
+
 }  // namespace k8s_amd

@@ -457,7 +457,7 @@ Tensor swiglu_bwd(Tensor gu, Tensor dy) {
 // in place on x [T, H*D]: contiguous, or a 2-D column slice of a wider row-major tensor (row stride = its
 // leading dimension -- the q and k heads of a packed QKV projection rotated without a copy)
 void rope_(Tensor x, Tensor pos, Tensor table, bool inverse) {
-  check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.is_cuda(), "x must be a GPU tensor"); check_dtype(x, at::kBFloat16, "x");
   check_cuda(pos, "pos"); check_dtype(pos, at::kInt, "pos");
   check_cuda(table, "table"); check_dtype(table, at::kFloat, "table");
   const int D = (int)table.size(1) * 2;
@@ -622,6 +622,72 @@ Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, int64
   return dx;
 }
 
+// ------------------------------------------------------------------ embedding (sum of gathers) / avg pool
+// tables: list of (weight bf16 [V, D], ids int64 [T] or None = position table) ; returns bf16 [T, D]
+Tensor embed_fwd(std::vector<Tensor> weights, std::vector<c10::optional<Tensor>> ids, int64_t T, int64_t S) {
+  TORCH_CHECK(!weights.empty() && weights.size() <= 3 && weights.size() == ids.size(), "1-3 tables, one ids each");
+  const long D = weights[0].size(1);
+  k8s_amd::EmbTable tabs[3];
+  for (size_t i = 0; i < weights.size(); ++i) {
+    const Tensor& w = weights[i];
+    check_cuda(w, "weight"); check_dtype(w, at::kBFloat16, "weight");
+    TORCH_CHECK(w.dim() == 2 && w.size(1) == D && D % 8 == 0, "tables must be [V, D] with one D % 8 == 0");
+    const int64_t* ip = nullptr;
+    if (ids[i]) {
+      check_cuda(*ids[i], "ids"); check_dtype(*ids[i], at::kLong, "ids");
+      TORCH_CHECK(ids[i]->numel() == T, "ids must have T entries");
+      ip = ids[i]->data_ptr<int64_t>();
+    } else {
+      TORCH_CHECK(S > 0 && T % S == 0 && w.size(0) >= S, "position table needs T % S == 0 and >= S rows");
+    }
+    tabs[i] = k8s_amd::EmbTable{cbf(w), nullptr, ip, (int)w.size(0)};
+  }
+  auto out = torch::empty({T, D}, weights[0].options());
+  k8s_amd::launch_embed_fwd(tabs, (int)weights.size(), (int)T, (int)D, (int)S, bf(out), cur_stream());
+  return out;
+}
+
+// grads: fp32 [V, D] slots accumulated into (zero them first for a fresh gradient)
+void embed_bwd(Tensor g, std::vector<Tensor> grads, std::vector<c10::optional<Tensor>> ids, int64_t S) {
+  check_cuda(g, "g"); check_dtype(g, at::kBFloat16, "g");
+  TORCH_CHECK(!grads.empty() && grads.size() <= 3 && grads.size() == ids.size(), "1-3 tables, one ids each");
+  const long T = g.size(0), D = g.size(1);
+  k8s_amd::EmbTable tabs[3];
+  for (size_t i = 0; i < grads.size(); ++i) {
+    const Tensor& gr = grads[i];
+    check_cuda(gr, "grad"); check_dtype(gr, at::kFloat, "grad");
+    TORCH_CHECK(gr.dim() == 2 && gr.size(1) == D, "grad slots must be [V, D]");
+    const int64_t* ip = nullptr;
+    if (ids[i]) {
+      check_cuda(*ids[i], "ids"); check_dtype(*ids[i], at::kLong, "ids");
+      TORCH_CHECK(ids[i]->numel() == T);
+      ip = ids[i]->data_ptr<int64_t>();
+    } else {
+      TORCH_CHECK(S > 0 && T % S == 0 && gr.size(0) >= S, "position table needs T % S == 0");
+    }
+    tabs[i] = k8s_amd::EmbTable{nullptr, f32(gr), ip, (int)gr.size(0)};
+  }
+  k8s_amd::launch_embed_bwd(tabs, (int)grads.size(), (int)T, (int)D, (int)S, cbf(g), cur_stream());
+}
+
+Tensor avgpool_fwd(Tensor x) {
+  check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "x must be NHWC with C % 8 == 0");
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  auto y = torch::empty({N, C}, x.options());
+  k8s_amd::launch_avgpool_fwd(cbf(x), bf(y), N, HW, C, cur_stream());
+  return y;
+}
+
+Tensor avgpool_bwd(Tensor dy, int64_t H, int64_t W) {
+  check_cuda(dy, "dy"); check_dtype(dy, at::kBFloat16, "dy");
+  TORCH_CHECK(dy.dim() == 2 && dy.size(1) % 8 == 0, "dy must be [N, C] with C % 8 == 0");
+  const int N = dy.size(0), C = dy.size(1);
+  auto dx = torch::empty({N, H, W, C}, dy.options());
+  k8s_amd::launch_avgpool_bwd(cbf(dy), bf(dx), N, (int)(H * W), C, cur_stream());
+  return dx;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -666,6 +732,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad_wtrans", &conv_dgrad_wtrans);
   m.def("flash_fwd", &flash_fwd);
   m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("embed_fwd", &embed_fwd);
+  m.def("embed_bwd", &embed_bwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("flash_bwd", &flash_bwd, py::arg("dO"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("causal"), py::arg("kv_lens"), py::arg("scale"), py::arg("dqkv") = py::none());

@@ -114,9 +114,8 @@ class BertForPreTraining(nn.Module):
         B, S = input_ids.shape
         c = self.c
         h = c.hidden
-        pos_ids = torch.arange(S, device=input_ids.device).expand(B, S)
-        e = (K.embedding(input_ids, self.word, dtype) + K.embedding(pos_ids, self.pos, dtype)
-             + K.embedding(token_type_ids, self.typ, dtype))
+        # word + position + token-type lookups summed in one gather pass (scatter-add backward)
+        e = K.embedding_sum([(input_ids, self.word), (None, self.pos), (token_type_ids, self.typ)], S, dtype)
         x = K.layer_norm(e.reshape(B * S, h), self.emb_ln_g, self.emb_ln_b, c.eps)
         for layer in self.layers:
             x = layer(x, B, S, kv_lens)

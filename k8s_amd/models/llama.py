@@ -107,7 +107,7 @@ class LlamaForCausalLM(nn.Module):
         B, S = input_ids.shape
         c = self.c
         pos = torch.arange(S, device=input_ids.device, dtype=torch.int32).repeat(B)
-        x = K.embedding(input_ids, self.embed, dtype).reshape(B * S, c.hidden)
+        x = K.embedding_sum([(input_ids, self.embed)], S, dtype).reshape(B * S, c.hidden)
         res = None
         for layer in self.layers:
             x, res = layer(x, res, B, S, pos, self.table)

@@ -296,6 +296,70 @@ def linear(x, pw, pb=None, act: Optional[str] = None):
 
 
 # =========================================================================== embedding
+class _EmbeddingSum(torch.autograd.Function):
+    """sum_i W_i[row_i(t)] over 1-3 tables on the GPU (csrc/kernels/embedding.hip): gather + sum in one pass, the
+    backward scatter-adds (fp32 atomics) straight into each table's flat fp32 gradient slot. ``ids`` None = a
+    position table (row = token % S)."""
+
+    @staticmethod
+    def forward(ctx, anchor, S, dtype, *flat):
+        ids = list(flat[0::2])
+        pws = list(flat[1::2])
+        T = next(i.numel() for i in ids if i is not None) if any(i is not None for i in ids) else None
+        ws = [pw.weight if pw.weight.dtype == dtype else pw.master.to(dtype) for pw in pws]
+        ids_c = [i.reshape(-1).contiguous() if i is not None else None for i in ids]
+        out = _C().embed_fwd(ws, ids_c, T, S)
+        ctx.save_for_backward(*[i if i is not None else torch.empty(0) for i in ids_c])
+        ctx.has_ids = [i is not None for i in ids_c]
+        ctx.pws, ctx.S = pws, S
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        saved = ctx.saved_tensors
+        ids = [t if h else None for t, h in zip(saved, ctx.has_ids)]
+        g = g.contiguous()
+        grads, finish = [], []
+        for pw in ctx.pws:
+            store = pw.store
+            slot = store.slot_for_write(pw)
+            if slot is not None:  # first writer: zero the slot, scatter-add into it
+                slot.zero_()
+                grads.append(slot.view(pw.shape))
+                finish.append(lambda pw=pw: pw.store.mark_written(pw))
+            elif pw.grad.dtype == torch.float32:  # tied weight already holds the other use's gradient
+                grads.append(pw.grad.view(pw.shape))
+                finish.append(lambda pw=pw: pw.store._notify(pw))
+            else:
+                tmp = torch.zeros(pw.shape, device=g.device, dtype=torch.float32)
+                grads.append(tmp)
+                finish.append(lambda pw=pw, tmp=tmp: pw.store.deposit(pw, tmp))
+        _C().embed_bwd(g, grads, ids, ctx.S)
+        for f in finish:
+            f()
+        return (None, None, None) + (None,) * (2 * len(ctx.pws))
+
+
+def embedding_sum(tables, S: int = 0, dtype=torch.bfloat16):
+    """Sum of embedding lookups: ``tables`` = [(ids [B, S] int64 or None for positions 0..S-1, param), ...] (1-3),
+    returns [B*S, D]. One fused HIP gather (and scatter-add backward) on the GPU; aten gathers on the CPU."""
+    ids0 = next(i for i, _ in tables if i is not None)
+    pw0 = tables[0][1]
+    if _gpu(pw0.master) and pw0.shape[1] % 8 == 0 and len(tables) <= 3:
+        flat = []
+        for i, pw in tables:
+            flat += [i, pw]
+        return _EmbeddingSum.apply(pw0.store.anchor, S or ids0.shape[-1], dtype, *flat)
+    T = ids0.numel()
+    out = None
+    for i, pw in tables:
+        if i is None:
+            i = torch.arange(S or ids0.shape[-1], device=ids0.device).repeat(T // (S or ids0.shape[-1]))
+        e = embedding(i.reshape(-1), pw, dtype)
+        out = e if out is None else out + e
+    return out
+
+
 class _Embedding(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, anchor, pw, dtype):
@@ -391,7 +455,21 @@ def max_pool_nhwc(x, k=3, s=2, p=1):
     return y.permute(0, 2, 3, 1).contiguous()
 
 
+class _AvgPoolNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.hw = x.shape[1:3]
+        return _C().avgpool_fwd(x.contiguous())
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _C().avgpool_bwd(dy.contiguous(), *ctx.hw)
+
+
 def global_avg_pool_nhwc(x):
+    """[N, H, W, C] -> [N, C] mean; GPU bf16: one HIP pass each way (pool.hip), fp32 accumulation."""
+    if _gpu(x) and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0:
+        return _AvgPoolNHWC.apply(x)
     return x.mean(dim=(1, 2))
 
 

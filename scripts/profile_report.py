@@ -12,7 +12,7 @@ import re
 
 CATS = [
     ("BatchNorm", r"k8s_amd::bn_|relu_mask"),
-    ("weight gradient", r"wgrad_stream|ConvWgB|MNMajorK, k8s_amd::MNMajorK|splitk_reduce"),
+    ("weight gradient", r"wgrad_stream|ConvWgB|MNMajorK, k8s_amd::MNMajorK|MNMaj, k8s_amd::g256r::MNMaj|splitk_reduce"),
     ("conv / GEMM fwd + dgrad", r"gemm_bf16_kernel|gemm256|conv_dgrad_wtrans"),
     ("pooling", r"pool"),
     ("optimizer / loss", r"sgd_|adam_|xent|sumsq|clip"),

@@ -201,3 +201,45 @@ def test_bn_packed_relu_mask(cuda, C, M, from_sums):
     _close(dx2, dx1, 1e-2)
     _close(dg2, dg1, 1e-4)
     _close(db2, db1, 1e-4)
+
+
+def test_embedding_sum_gather_and_scatter(cuda):
+    """BERT-style word + position + token-type lookup (embedding.hip) vs torch gathers; the backward's fp32
+    scatter-adds (incl. the 2-row token-type table's register-reduced path) vs index_add_."""
+    from k8s_amd.ops import nn as K
+    from k8s_amd.parallel.flat import ParamStore, init_normal
+
+    torch.manual_seed(3)
+    B, S, D, V = 4, 96, 256, 1000
+    store = ParamStore()
+    word = store.new("word", (V, D), init_normal(0.5))
+    pos = store.new("pos", (128, D), init_normal(0.5))
+    typ = store.new("typ", (2, D), init_normal(0.5))
+    store.finalize(cuda)
+    ids = torch.randint(0, V, (B, S), device=cuda)
+    tt = torch.randint(0, 2, (B, S), device=cuda)
+    out = K.embedding_sum([(ids, word), (None, pos), (tt, typ)], S)
+    pids = torch.arange(S, device=cuda).repeat(B)
+    ref = (word.master[ids.reshape(-1)].bfloat16().float() + pos.master[pids].bfloat16().float()
+           + typ.master[tt.reshape(-1)].bfloat16().float())
+    assert ((out.float() - ref).abs().max() / ref.abs().max()).item() < 1e-2
+    g = torch.randn_like(out)
+    out.backward(g)
+    gf = g.float()
+    for p, rows in ((word, ids.reshape(-1)), (pos, pids), (typ, tt.reshape(-1))):
+        want = torch.zeros(p.shape, device=cuda).index_add_(0, rows, gf)
+        got = p.grad.view(p.shape)
+        assert ((got - want).norm() / want.norm()).item() < 1e-5, p.name
+
+
+def test_global_avg_pool_nhwc(cuda):
+    from k8s_amd.ops import nn as K
+
+    torch.manual_seed(4)
+    x = torch.randn(8, 7, 7, 2048, device=cuda).bfloat16().requires_grad_(True)
+    y = K.global_avg_pool_nhwc(x)
+    ref = x.float().mean(dim=(1, 2))
+    assert ((y.float() - ref).abs().max()).item() < 1e-2
+    g = torch.randn_like(y)
+    (dx,) = torch.autograd.grad(y, x, g)
+    assert ((dx.float() - (g.float() / 49)[:, None, None, :]).abs().max()).item() < 1e-3
