@@ -286,14 +286,20 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 // (4 x 1) when N = 64 (the early ResNet convolutions and the stem) so no MFMA work is spent on padding.
 // Only K-major sources may sit on a 64-wide side (the MN-major swizzle assumes 256-B rows).
 // LEAN: the staged bf16 epilogue (also the only one with the BN-statistics reductions, forward and backward).
-template <class ASrc, class BSrc, int NBUF, int WM = 2, int WN = 2, bool LEAN = false>
-__global__ void __launch_bounds__(GEMM_THREADS, NBUF == 1 ? 3 : 2)
+// BNB (lean only): the epilogue also reduces the BatchNorm-backward statistics (Epi::bstats); the BN input tile
+// x[m0:m0+BM][n0:n0+BN] is DMA'd into LDS during the K loop -- into the idle buffer of the last K step (NBUF = 2)
+// or a second 32 KB region issued with the first stage (NBUF = 1) -- so the copy-out reads it from LDS.
+template <class ASrc, class BSrc, int NBUF, int WM = 2, int WN = 2, bool LEAN = false, bool BNB = false>
+__global__ void __launch_bounds__(GEMM_THREADS, (NBUF == 1 && !BNB) ? 3 : 2)
 gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
   constexpr int TA = BM * BK * 2, TB = BN * BK * 2;  // operand tile bytes
   static_assert(WM * WN == 4, "4 waves");
   static_assert((WM == 2 || ASrc::kmajor) && (WN == 2 || BSrc::kmajor), "MN-major operands need a 128 side");
-  __shared__ __attribute__((aligned(1024))) char smem[NBUF * (TA + TB)];  // [buf][A|B]
+  static_assert(!BNB || LEAN, "the BN-backward reduction lives in the lean epilogue");
+  static_assert(BM * BN * 2 <= TA + TB, "the x (and C) tile fits one operand buffer");
+  constexpr int NREG = (NBUF == 1 && BNB) ? 2 : NBUF;  // 32 KB LDS regions
+  __shared__ __attribute__((aligned(1024))) char smem[NREG * (TA + TB)];  // [buf][A|B]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
 
@@ -351,8 +357,26 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
     }
   };
 
+  constexpr int CPR = BN / 8;  // 16-B chunks per output-tile row
+  // BN input tile -> LDS, lane-linear: slot q (= the copy-out's chunk index) at byte q * 16
+  auto stage_x = [&](char* dst) {
+#pragma unroll
+    for (int rd = 0; rd < BM * CPR / GEMM_THREADS; ++rd) {
+      const int q = rd * GEMM_THREADS + tid, row = q / CPR, c = q % CPR;
+      const int m = min(m0 + row, M - 1), n = n0 + c * 8;
+      const void* g = n < N ? (const void*)(E.bx + (long)m * E.ldc + n) : (const void*)g_zero_page;
+      glds16(g, dst + (rd * GEMM_THREADS + wid_u * 64) * 16);
+    }
+  };
+  int xbuf = -1;  // LDS region holding the x tile (BNB)
   if (nt > 0) {
     stage(0, kbeg);
+    if constexpr (BNB && NBUF == 1) {
+      if (E.bstats) {
+        stage_x(smem + (TA + TB));
+        xbuf = 1;
+      }
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -366,6 +390,11 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
       }
     } else if (t + 1 < nt) {
       stage(cur ^ 1, kbeg + (t + 1) * BK);
+    } else if constexpr (BNB) {  // last K step: the other buffer is idle
+      if (E.bstats) {
+        stage_x(smem + (cur ^ 1) * (TA + TB));
+        xbuf = cur ^ 1;
+      }
     }
     const char* ta = smem + cur * (TA + TB);
     const char* tb = ta + TA;
@@ -396,8 +425,9 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
   // and the data gradients): the tile goes through LDS and leaves as 16-B row-contiguous stores, and none of the
   // general epilogue's run-time branches are compiled in (the general instantiations are ~85 KB of code, more
   // than the instruction cache). LDS image [BM][BN] bf16, 16-B chunk c of row r at c ^ (r % (BN / 8)).
-  uint16_t* const ctile = reinterpret_cast<uint16_t*>(smem);
-  constexpr int CPR = BN / 8;  // 16-B chunks per tile row
+  // the C tile goes to region 0, or region 1 when the x tile sits in region 0 (NBUF = 2, even step count)
+  uint16_t* const ctile = reinterpret_cast<uint16_t*>(smem + (xbuf == 0 ? (TA + TB) : 0));
+  const uint16_t* const xtile = reinterpret_cast<const uint16_t*>(smem + (xbuf < 0 ? 0 : xbuf) * (TA + TB));
   float st_s[4][4], st_q[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -461,7 +491,8 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
       *reinterpret_cast<bf16x8_t*>(cp) = o;
       if (bwd) {
         const long off = orow * E.ldc + n;
-        const bf16x8_t xv = *reinterpret_cast<const bf16x8_t*>(E.bx + off);
+        const bf16x8_t xv = BNB ? *reinterpret_cast<const bf16x8_t*>(xtile + q * 8)
+                                : *reinterpret_cast<const bf16x8_t*>(E.bx + off);
         const uint32_t bits = E.bmask ? (uint32_t)E.bmask[off >> 3] : 0xFFu;
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
@@ -637,16 +668,16 @@ static int effective_splits(int K, int splits) {
   return (K + kps - 1) / kps;
 }
 
-template <class ASrc, class BSrc, int WM, int WN, bool LEAN>
+template <class ASrc, class BSrc, int WM, int WN, bool LEAN, bool BNB>
 static void launch_tiles2(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
                           hipStream_t st) {
   const int tiles = ((M + 64 * WM - 1) / (64 * WM)) * ((N + 64 * WN - 1) / (64 * WN));
   if (kps <= 2 * BK)
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN, LEAN>), dim3(tiles, 1, splits), dim3(GEMM_THREADS),
-                       0, st, a, b, e, M, N, K, kps);
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN, LEAN, BNB>), dim3(tiles, 1, splits),
+                       dim3(GEMM_THREADS), 0, st, a, b, e, M, N, K, kps);
   else
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2, WM, WN, LEAN>), dim3(tiles, 1, splits), dim3(GEMM_THREADS),
-                       0, st, a, b, e, M, N, K, kps);
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2, WM, WN, LEAN, BNB>), dim3(tiles, 1, splits),
+                       dim3(GEMM_THREADS), 0, st, a, b, e, M, N, K, kps);
 }
 
 // the lean epilogue applies: bf16 C (16-B aligned rows), no bias / activation / pre-activation copy / atomics
@@ -655,17 +686,30 @@ static bool lean_epi(const Epi& e, int N) {
          (N & 7) == 0 && (reinterpret_cast<uintptr_t>(e.c) & 15) == 0;
 }
 
+// operand pairs that produce a BatchNorm output gradient (the dgrads): the only BN-backward instantiations
+template <class ASrc, class BSrc>
+constexpr bool kBnbPair = (std::is_same_v<ASrc, KMajor> && std::is_same_v<BSrc, MNMajorK>) ||
+                          (std::is_same_v<ASrc, ConvA> && std::is_same_v<BSrc, KMajor>);
+
 template <class ASrc, class BSrc, int WM, int WN>
 static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
                          hipStream_t st) {
   if constexpr (!std::is_same_v<BSrc, ConvWgB>) {
     if (lean_epi(e, N)) {
-      launch_tiles2<ASrc, BSrc, WM, WN, true>(a, b, e, M, N, K, kps, splits, st);
+      if constexpr (kBnbPair<ASrc, BSrc>) {
+        if (e.bstats) {
+          if (e.rst || splits != 1) throw std::runtime_error("BN-backward epilogue: identity rows, no split-K");
+          launch_tiles2<ASrc, BSrc, WM, WN, true, true>(a, b, e, M, N, K, kps, splits, st);
+          return;
+        }
+      }
+      if (e.bstats) throw std::runtime_error("BN-backward epilogue requested for an operand pair without it");
+      launch_tiles2<ASrc, BSrc, WM, WN, true, false>(a, b, e, M, N, K, kps, splits, st);
       return;
     }
   }
   if (e.bstats) throw std::runtime_error("the BatchNorm-backward epilogue needs a plain bf16 output (lean epilogue)");
-  launch_tiles2<ASrc, BSrc, WM, WN, false>(a, b, e, M, N, K, kps, splits, st);
+  launch_tiles2<ASrc, BSrc, WM, WN, false, false>(a, b, e, M, N, K, kps, splits, st);
 }
 
 template <class ASrc, class BSrc>

@@ -34,11 +34,12 @@ from k8s_amd.ops._ext import load as _load
 import os
 
 # BatchNorm-backward statistics in the dgrad epilogue (ops.nn.BnBwdLink): the lean (LDS-staged) epilogue's
-# copy-out pass reads the BN input next to the gradient it stores and reduces (sum g*m, sum g*m*xhat), replacing
-# the BN backward's separate reduction pass over (dy, x). Off by default: measured on MI355X (ResNet-50 b1024,
-# scripts/gpurun/prof_ab.sh) it removes 8.1 ms/step of reduction passes but adds 10.3 ms/step to the dgrads --
-# the x reads sit exposed at the end of every block instead of streaming -- 9.51k vs 9.72k img/s.
-# K8S_AMD_BN_LINK=1 turns it on.
+# copy-out pass reduces (sum g*m, sum g*m*xhat) from the gradient it stores and the BN input tile, which is
+# DMA'd into LDS during the K loop; this replaces the BN backward's separate reduction pass over (dy, x). Off by
+# default: measured on MI355X (ResNet-50 b1024, scripts/gpurun/prof_ab.sh) it removes 6.1 ms/step of reduction
+# passes but adds 9.0 ms/step to the dgrads -- ~10 VALU per element on the critical path of the short-K
+# products (the single-buffer 1x1 dgrads run 2.3x slower) -- 10.61k vs 11.00k img/s. K8S_AMD_BN_LINK=1 turns
+# it on.
 BN_LINK = os.environ.get("K8S_AMD_BN_LINK", "0") == "1"
 
 STATS = {"hip_fwd": 0, "aten_fwd": 0, "hip_wgrad": 0, "aten_wgrad": 0, "hip_dgrad": 0, "aten_dgrad": 0}
