@@ -18,7 +18,9 @@ box, CPU or MI355X:
   (cluster DNS stand-in, see ``k8s_amd.parallel.dist``).
 * volumes: configMap volumes are materialised in a scratch dir; command/args
   paths under a mountPath are rewritten to it; hostPath mounts likewise.
-* Deployments (TensorBoard) are marked available without a process.
+* Deployments: a TensorBoard Deployment (container command ``tensorboard --logdir ...``) runs the
+  ``k8s_amd.tools.tensorboard`` stand-in on the 127.0.0.1 port of the Service that selects it, with the
+  logdir rewritten through its volumes; other Deployments are marked available without a process.
 * fault injection: ``kill_pod(name, exit_code)`` ends a container with a
   chosen exit code.
 """
@@ -74,6 +76,7 @@ class LocalKubelet:
         self.extra_env = dict(extra_env or {})
         self.max_restarts = max_restarts
         self.running: Dict[str, _Container] = {}  # pod name -> container
+        self.deploy_procs: Dict[str, subprocess.Popen] = {}  # ns/deployment -> TensorBoard stand-in
         self.pod_meta: Dict[str, dict] = {}  # pod name -> {"job":..., "ns":..., "restarts":..}
         self.service_ports: Dict[str, int] = {}
         self._published: Dict[str, str] = {}
@@ -92,6 +95,8 @@ class LocalKubelet:
         self._thread.join(timeout=10)
         for c in list(self.running.values()):
             self._kill(c.proc)
+        for p in list(self.deploy_procs.values()):
+            self._kill(p)
 
     def __enter__(self):
         return self.start()
@@ -257,12 +262,58 @@ class LocalKubelet:
             self._stop.wait(self.poll)
 
     def _sync_deployments(self, ns):
-        for d in self.api.get(self._path(ns, "deployments", group="apps/v1")).get("items", []):
+        deps = self.api.get(self._path(ns, "deployments", group="apps/v1")).get("items", [])
+        live = set()
+        for d in deps:
+            key = ns + "/" + d["metadata"]["name"]
+            live.add(key)
+            if self._is_tensorboard(d) and (key not in self.deploy_procs or self.deploy_procs[key].poll() is not None):
+                if not self._start_tensorboard(ns, d, key):
+                    continue  # its Service is not there yet: retried on the next sync
             want = d.get("spec", {}).get("replicas", 1)
             st = d.get("status") or {}
             if st.get("availableReplicas") != want:
                 d["status"] = {"replicas": want, "availableReplicas": want, "readyReplicas": want}
                 self.api.request("PUT", self._path(ns, "deployments", d["metadata"]["name"], "apps/v1"), d)
+        for key in [k for k in self.deploy_procs if k.startswith(ns + "/") and k not in live]:
+            self._kill(self.deploy_procs.pop(key))  # Deployment deleted (job deleted / garbage collected)
+
+    @staticmethod
+    def _tb_container(d):
+        cs = (((d.get("spec") or {}).get("template") or {}).get("spec") or {}).get("containers") or []
+        return next((c for c in cs if os.path.basename((c.get("command") or [""])[0]) == "tensorboard"), None)
+
+    def _is_tensorboard(self, d) -> bool:
+        return self._tb_container(d) is not None
+
+    def _start_tensorboard(self, ns, d, key) -> bool:
+        tmpl = d["spec"]["template"]
+        labels = (tmpl.get("metadata") or {}).get("labels") or {}
+        svc = None
+        for s in self.api.get(self._path(ns, "services")).get("items", []):
+            sel = (s.get("spec") or {}).get("selector") or {}
+            if sel and all(labels.get(k) == v for k, v in sel.items()):
+                svc = s["metadata"]["name"]
+                break
+        if svc is None:
+            return False
+        self._publish_service_map(ns)
+        port = self.service_ports[ns + "/" + svc]
+        c = self._tb_container(d)
+        mounts = self._materialise_volumes(ns, d["metadata"]["name"], tmpl.get("spec") or {}, c)
+        argv = list(c.get("command") or [])[1:] + list(c.get("args") or [])
+        logdir = argv[argv.index("--logdir") + 1] if "--logdir" in argv else "."
+        cmd = [sys.executable, "-m", "k8s_amd.tools.tensorboard", "--logdir", self._rewrite(logdir, mounts),
+               "--host", "127.0.0.1", "--port", str(port)]
+        env = dict(os.environ)
+        env["PYTHONPATH"] = REPO + os.pathsep + env.get("PYTHONPATH", "")
+        log_path = os.path.join(self.log_dir, d["metadata"]["name"] + ".log")
+        with open(log_path, "ab") as logf:
+            logf.write(("$ %s\n" % " ".join(shlex.quote(x) for x in cmd)).encode())
+            logf.flush()
+            self.deploy_procs[key] = subprocess.Popen(cmd, env=env, stdout=logf, stderr=subprocess.STDOUT, cwd=REPO,
+                                                      start_new_session=True)
+        return True
 
     def _sync_jobs(self, ns):
         jobs = self.api.get(self._path(ns, "jobs", group="batch/v1")).get("items", [])

@@ -79,7 +79,8 @@ def frame(record: bytes) -> bytes:
 
 
 def read_records(path: str):
-    """Parse a TFRecord file back (verifying both CRCs); yields payloads."""
+    """Parse a TFRecord file back (verifying both CRCs); yields payloads. A record still being written (short
+    read) ends the iteration."""
     with open(path, "rb") as f:
         while True:
             h = f.read(12)
@@ -89,10 +90,80 @@ def read_records(path: str):
             if masked_crc(h[:8]) != lc:
                 raise ValueError("length crc mismatch")
             data = f.read(n)
-            (dc,) = struct.unpack("<I", f.read(4))
+            tail = f.read(4)
+            if len(data) < n or len(tail) < 4:
+                return
+            (dc,) = struct.unpack("<I", tail)
             if masked_crc(data) != dc:
                 raise ValueError("data crc mismatch")
             yield data
+
+
+def _read_varint(b: bytes, i: int):
+    n = shift = 0
+    while True:
+        c = b[i]
+        i += 1
+        n |= (c & 0x7F) << shift
+        if not c & 0x80:
+            return n, i
+        shift += 7
+
+
+def _fields(b: bytes):
+    """(field number, wire type, value) of one protobuf message: varint -> int, fixed64/32 -> raw bytes,
+    length-delimited -> bytes."""
+    i = 0
+    while i < len(b):
+        key, i = _read_varint(b, i)
+        f, w = key >> 3, key & 7
+        if w == 0:
+            v, i = _read_varint(b, i)
+        elif w == 1:
+            v, i = b[i:i + 8], i + 8
+        elif w == 5:
+            v, i = b[i:i + 4], i + 4
+        elif w == 2:
+            n, i = _read_varint(b, i)
+            v, i = b[i:i + n], i + n
+        else:
+            raise ValueError("unsupported wire type %d" % w)
+        yield f, w, v
+
+
+def decode_event(data: bytes) -> dict:
+    """Event{wall_time=1 double, step=2 int64, file_version=3 string, summary=5 Summary{value=1 repeated
+    Value{tag=1 string, simple_value=2 float}}} -> {"wall_time", "step", "file_version"?, "scalars"}."""
+    ev = {"wall_time": 0.0, "step": 0, "scalars": {}}
+    for f, w, v in _fields(data):
+        if f == 1 and w == 1:
+            ev["wall_time"] = struct.unpack("<d", v)[0]
+        elif f == 2 and w == 0:
+            ev["step"] = v
+        elif f == 3 and w == 2:
+            ev["file_version"] = v.decode()
+        elif f == 5 and w == 2:
+            for sf, sw, sv in _fields(v):
+                if sf != 1 or sw != 2:
+                    continue
+                tag, val = None, None
+                for vf, vw, vv in _fields(sv):
+                    if vf == 1 and vw == 2:
+                        tag = vv.decode()
+                    elif vf == 2 and vw == 5:
+                        val = struct.unpack("<f", vv)[0]
+                if tag is not None and val is not None:
+                    ev["scalars"][tag] = val
+    return ev
+
+
+def read_events(path: str):
+    """Decoded events of one file (CRC-checked); stops cleanly at a partially written tail record."""
+    try:
+        for rec in read_records(path):
+            yield decode_event(rec)
+    except (ValueError, struct.error):
+        return
 
 
 class EventWriter:
