@@ -26,6 +26,7 @@
 //    run on the same XCD (private L2).
 //  * epilogue: bias, ReLU / GELU(tanh), pre-activation side output, fp32 accumulate, split-K
 //    fp32 atomics (for the tall-K weight gradients).
+#include <cstdlib>
 #include <stdexcept>
 #include <type_traits>
 
@@ -70,6 +71,8 @@ struct KMajor {
   __device__ __forceinline__ const void* at(const Cursor& q, int k0) const {
     return k0 + q.c8 >= ktot ? (const void*)g_zero_page : (const void*)(q.p + k0);
   }
+  // per-K-step uniform part of the address (identity here; see ConvA)
+  __device__ __forceinline__ int tap(int k0) const { return k0; }
   static constexpr bool kmajor = true;
 };
 
@@ -88,6 +91,8 @@ struct MNMajor {
   struct Cursor { int s, base; };
   __device__ __forceinline__ Cursor cursor(int s, int base) const { return Cursor{s, base}; }
   __device__ __forceinline__ const void* at(const Cursor& c, int k0) const { return src(c.s, c.base, k0); }
+  // per-K-step uniform part of the address (identity here; see ConvA)
+  __device__ __forceinline__ int tap(int k0) const { return k0; }
   static constexpr bool kmajor = false;
 };
 
@@ -124,12 +129,21 @@ struct ConvA {
     const int hs = ho * stride - pad, ws = wo * stride - pad;
     return Cursor{x + (((long)n * H + hs) * W + ws) * C + c * 8, hs, ws};
   }
-  __device__ __forceinline__ const void* at(const Cursor& q, int k0) const {
+  // The (r, s, c0) decode of a K step is wave-uniform: done once per stage (tap) instead of once per load -- the
+  // four loads' repeated scalar divisions were ~120 SALU per K step in the ISA, issued ahead of the MFMAs.
+  struct Tap {
+    int dh, dw;
+    long off;
+  };
+  __device__ __forceinline__ Tap tap(int k0) const {
     const int rs = fC.div(k0), c0 = k0 - rs * C;
     const int r = fS.div(rs), sx = rs - r * S;
-    const int hi = q.hs + r * dil, wi = q.ws + sx * dil;
+    return Tap{r * dil, sx * dil, ((long)(r * dil) * W + sx * dil) * C + c0};
+  }
+  __device__ __forceinline__ const void* at(const Cursor& q, const Tap& t) const {
+    const int hi = q.hs + t.dh, wi = q.ws + t.dw;
     if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) return g_zero_page;
-    return q.p + ((long)(r * dil) * W + sx * dil) * C + c0;
+    return q.p + t.off;
   }
   static constexpr bool kmajor = true;
 };
@@ -161,6 +175,8 @@ struct ConvAG {
   struct Cursor { int s, base; };
   __device__ __forceinline__ Cursor cursor(int s, int base) const { return Cursor{s, base}; }
   __device__ __forceinline__ const void* at(const Cursor& c, int k0) const { return src(c.s, c.base, k0); }
+  // per-K-step uniform part of the address (identity here; see ConvA)
+  __device__ __forceinline__ int tap(int k0) const { return k0; }
   static constexpr bool kmajor = true;
 };
 
@@ -191,6 +207,8 @@ struct ConvWgB {
   struct Cursor { int s, base; };
   __device__ __forceinline__ Cursor cursor(int s, int base) const { return Cursor{s, base}; }
   __device__ __forceinline__ const void* at(const Cursor& c, int k0) const { return src(c.s, c.base, k0); }
+  // per-K-step uniform part of the address (identity here; see ConvA)
+  __device__ __forceinline__ int tap(int k0) const { return k0; }
   static constexpr bool kmajor = false;
 };
 
@@ -216,6 +234,8 @@ struct MNMajorK {
   __device__ __forceinline__ const void* at(const Cursor& q, int k0) const {
     return (q.krow < 0 || k0 + q.krow >= ktot) ? (const void*)g_zero_page : (const void*)(q.p + (long)k0 * ld);
   }
+  // per-K-step uniform part of the address (identity here; see ConvA)
+  __device__ __forceinline__ int tap(int k0) const { return k0; }
   static constexpr bool kmajor = false;
 };
 
@@ -268,6 +288,7 @@ struct Epi {
   // Sub-grid output (stride-s data gradient by output parity): GEMM row m = (n, i, j) over an rHo x rWo grid
   // is stored at output row (n, i*rst + ra, j*rst + rb) of an rH x rW image. rst == 0: identity.
   int rst, rHo, rWo, rH, rW, ra, rb;
+  int late_nt;  // K steps from which the next step's loads are issued behind the first MFMA half
 };
 constexpr int STAT_REPL = 32;
 
@@ -345,15 +366,20 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
   auto stage = [&](int buf, int k0) {
     char* ta = smem + buf * (TA + TB);
     char* tb = ta + TA;
+    if constexpr (HOIST) {
+      const auto tpa = A.tap(k0);
+      const auto tpb = B.tap(k0);
 #pragma unroll
-    for (int rd = 0; rd < RA; ++rd) {
-      const void* g = HOIST ? A.at(ca[HOIST ? rd : 0], k0) : A.src(rd * GEMM_THREADS + tid, m0, k0);
-      glds16(g, ta + (rd * GEMM_THREADS + wid_u * 64) * 16);
-    }
+      for (int rd = 0; rd < RA; ++rd) glds16(A.at(ca[rd], tpa), ta + (rd * GEMM_THREADS + wid_u * 64) * 16);
 #pragma unroll
-    for (int rd = 0; rd < RB; ++rd) {
-      const void* g = HOIST ? B.at(cb[HOIST ? rd : 0], k0) : B.src(rd * GEMM_THREADS + tid, n0, k0);
-      glds16(g, tb + (rd * GEMM_THREADS + wid_u * 64) * 16);
+      for (int rd = 0; rd < RB; ++rd) glds16(B.at(cb[rd], tpb), tb + (rd * GEMM_THREADS + wid_u * 64) * 16);
+    } else {
+#pragma unroll
+      for (int rd = 0; rd < RA; ++rd)
+        glds16(A.src(rd * GEMM_THREADS + tid, m0, k0), ta + (rd * GEMM_THREADS + wid_u * 64) * 16);
+#pragma unroll
+      for (int rd = 0; rd < RB; ++rd)
+        glds16(B.src(rd * GEMM_THREADS + tid, n0, k0), tb + (rd * GEMM_THREADS + wid_u * 64) * 16);
     }
   };
 
@@ -369,6 +395,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
     }
   };
   int xbuf = -1;  // LDS region holding the x tile (BNB)
+  const bool late = nt >= E.late_nt;
   if (nt > 0) {
     stage(0, kbeg);
     if constexpr (BNB && NBUF == 1) {
@@ -388,13 +415,8 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
       }
-    } else if (t + 1 < nt) {
+    } else if (!late && t + 1 < nt) {
       stage(cur ^ 1, kbeg + (t + 1) * BK);
-    } else if constexpr (BNB) {  // last K step: the other buffer is idle
-      if (E.bstats) {
-        stage_x(smem + (cur ^ 1) * (TA + TB));
-        xbuf = cur ^ 1;
-      }
     }
     const char* ta = smem + cur * (TA + TB);
     const char* tb = ta + TA;
@@ -411,6 +433,19 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfv[j], af[i], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
+      if (NBUF == 2 && kk == 0) {
+        // long K loops: the next K step's loads are issued behind the first half's MFMAs (their address
+        // arithmetic then runs while the matrix pipe is busy instead of delaying the MFMAs); short ones keep them
+        // ahead of the MFMAs (more time in flight). The buffer they fill was released by the previous barrier.
+        if (late && t + 1 < nt) {
+          stage(cur ^ 1, kbeg + (t + 1) * BK);
+        } else if constexpr (BNB) {  // last K step: the other buffer is idle
+          if (E.bstats) {
+            stage_x(smem + (cur ^ 1) * (TA + TB));
+            xbuf = cur ^ 1;
+          }
+        }
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -744,6 +779,14 @@ static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act,
   e.bmean = e.binvstd = e.bgamma = e.bbeta = nullptr;
   e.brelu_x = 0;
   e.rst = e.rHo = e.rWo = e.rH = e.rW = e.ra = e.rb = 0;
+  // $K8S_AMD_GEMM_LATE_NT (A/B knob), default off: issuing the next step's loads behind the first MFMA half sped
+  // up the isolated 56x56 / 28x28 3x3 convolutions 7-12 % but the ResNet-50 step lost 1.5 % at any threshold
+  // (b1024: 11.00k img/s never late, 10.84k from 8 K steps, 10.80k always; scripts/gpurun/bench_ab.sh)
+  static const int late_nt = [] {
+    const char* v = getenv("K8S_AMD_GEMM_LATE_NT");
+    return v ? atoi(v) : (1 << 30);
+  }();
+  e.late_nt = late_nt;
   return e;
 }
 
@@ -898,6 +941,33 @@ __global__ void conv_dgrad_wtrans_kernel(const uint16_t* __restrict__ w, uint16_
 void launch_conv_dgrad_wtrans(const uint16_t* w, uint16_t* w2, int K, int R, int S, int C, hipStream_t st) {
   const long total = (long)K * R * S * C;
   hipLaunchKernelGGL(conv_dgrad_wtrans_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, st, w, w2, K, R, S, C);
+}
+
+// Stride-s data gradient, per-parity sub-weights in one launch: parity p (grid.y) gets
+//   out[off_p + (c * T_p + t) * K + k] = w[k][rs_p[t]][c]          ([C][T_p][K], T_p = its taps, rs = r*S + s)
+// replacing a stack / permute / contiguous chain of ATen copies per parity (ops/conv.py _dgrad_strided_hip).
+__global__ void conv_dgrad_wsub_kernel(const uint16_t* __restrict__ w, uint16_t* __restrict__ out, int K, int RS,
+                                       int C, DgradTaps taps) {
+  const int p = blockIdx.y;
+  const int T = taps.n[p];
+  const long total = (long)C * T * K;
+  uint16_t* o = out + taps.off[p];
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int k = (int)(i % K);
+    const long ct = i / K;
+    const int t = (int)(ct % T);
+    const int c = (int)(ct / T);
+    o[i] = w[((long)k * RS + taps.rs[p][t]) * C + c];
+  }
+}
+
+void launch_conv_dgrad_wsub(const uint16_t* w, uint16_t* out, int K, int RS, int C, const DgradTaps& taps, int np,
+                            hipStream_t st) {
+  int maxt = 1;
+  for (int p = 0; p < np; ++p) maxt = taps.n[p] > maxt ? taps.n[p] : maxt;
+  const long total = (long)C * maxt * K;
+  hipLaunchKernelGGL(conv_dgrad_wsub_kernel, dim3(stream_grid(total, 256), np), dim3(256), 0, st, w, out, K, RS, C,
+                     taps);
 }
 
 }  // namespace k8s_amd

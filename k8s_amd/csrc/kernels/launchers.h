@@ -92,6 +92,14 @@ bool wgrad_stream_eligible(int N, int Ho, int Wo, int C, int K, int R, int S);
 void launch_wgrad_stream(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int C, int K, int R,
                          int S, int stride, int pad, int Ho, int Wo, bool accumulate, hipStream_t st);
 void launch_conv_dgrad_wtrans(const uint16_t* w, uint16_t* w2, int K, int R, int S, int C, hipStream_t st);
+// per-output-parity sub-weights of a stride-s dgrad (up to 16 parities x 16 taps), packed at off[p]
+struct DgradTaps {
+  int n[16];
+  long off[16];
+  int rs[16][16];
+};
+void launch_conv_dgrad_wsub(const uint16_t* w, uint16_t* out, int K, int RS, int C, const DgradTaps& taps, int np,
+                            hipStream_t st);
 
 // elementwise.hip
 void launch_swiglu_fwd(const uint16_t* gu, uint16_t* y, long T, int F, hipStream_t st);

@@ -426,6 +426,32 @@ void conv_wgrad(Tensor x, Tensor dy, Tensor dw, int64_t stride, int64_t pad, int
                              sp, accumulate, sp > 1 ? f32(ws) : nullptr, cur_stream());
 }
 
+// taps: per parity, the list of r*S + s tap indices (row-major over its [Tr][Ts] grid); returns one packed bf16
+// buffer with parity p's [C, T_p, K] sub-weight at the element offset offsets[p]
+std::vector<Tensor> conv_dgrad_wsub(Tensor w, std::vector<std::vector<int64_t>> taps) {
+  check_cuda(w, "w"); check_dtype(w, at::kBFloat16, "w");
+  const int K = w.size(0), R = w.size(1), S = w.size(2), C = w.size(3);
+  TORCH_CHECK(!taps.empty() && taps.size() <= 16, "1-16 parities");
+  k8s_amd::DgradTaps t{};
+  long off = 0;
+  std::vector<int64_t> offs;
+  for (size_t p = 0; p < taps.size(); ++p) {
+    TORCH_CHECK(!taps[p].empty() && taps[p].size() <= 16, "1-16 taps per parity");
+    t.n[p] = (int)taps[p].size();
+    t.off[p] = off;
+    offs.push_back(off);
+    for (size_t i = 0; i < taps[p].size(); ++i) {
+      TORCH_CHECK(taps[p][i] >= 0 && taps[p][i] < R * S, "tap index out of range");
+      t.rs[p][i] = (int)taps[p][i];
+    }
+    off += (long)C * t.n[p] * K;
+    off = (off + 7) / 8 * 8;  // keep every parity's sub-weight 16-B aligned
+  }
+  auto out = torch::empty({off}, w.options());
+  k8s_amd::launch_conv_dgrad_wsub(cbf(w), bf(out), K, R * S, C, t, (int)taps.size(), cur_stream());
+  return {out, torch::tensor(offs)};
+}
+
 Tensor conv_dgrad_wtrans(Tensor w) {
   check_cuda(w, "w"); check_dtype(w, at::kBFloat16, "w");
   const int K = w.size(0), R = w.size(1), S = w.size(2), C = w.size(3);
@@ -730,6 +756,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd_subgrid", &conv_fwd_subgrid, py::arg("x"), py::arg("w"), py::arg("pad"), py::arg("Hs"),
         py::arg("Ws"), py::arg("out"), py::arg("stride"), py::arg("a"), py::arg("b"), py::arg("accumulate") = false);
   m.def("conv_dgrad_wtrans", &conv_dgrad_wtrans);
+  m.def("conv_dgrad_wsub", &conv_dgrad_wsub);
   m.def("flash_fwd", &flash_fwd);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("embed_fwd", &embed_fwd);

@@ -173,18 +173,17 @@ def _dgrad_strided_hip(C_, gy, w, stride, padding, H, W, addend=None):
         # parities no tap reaches are zero: one contiguous memset beats strided fills of the sub-grids
         # (1x1 stride-2: 3 of 4 parities; strided fills made that path 1.8x slower than MIOpen)
         dx = (torch.zeros if empty else torch.empty)(N, H, W, C, device=gy.device, dtype=gy.dtype)
-    for a in range(stride):
-        tr = _parity_taps(R, a, padding, stride)
-        for b in range(stride):
-            ts = _parity_taps(S, b, padding, stride)
-            if not tr or not ts:
-                continue
-            # gather the taps with views + stack (no host->device index tensor, so no stream sync)
-            wr = torch.stack([w[:, r] for _, r in tr], dim=1)                 # [K, Tr, S, C]
-            wsub = torch.stack([wr[:, :, s_] for _, s_ in ts], dim=2)         # [K, Tr, Ts, C]
-            wsub = wsub.permute(3, 1, 2, 0).contiguous()                      # [C, Tr, Ts, K]
-            Hs, Ws = (H - a + stride - 1) // stride, (W - b + stride - 1) // stride
-            C_.conv_fwd_subgrid(gy, wsub, -tr[0][0], Hs, Ws, dx, stride, a, b, addend is not None)
+    live = [(a, b, _parity_taps(R, a, padding, stride), _parity_taps(S, b, padding, stride))
+            for a in range(stride) for b in range(stride)]
+    live = [(a, b, tr, ts) for a, b, tr, ts in live if tr and ts]
+    # every parity's [C, Tr, Ts, K] sub-weight gathered by one kernel (taps r*S + s, row-major over Tr x Ts)
+    packed, offs = C_.conv_dgrad_wsub(w, [[r * S + s_ for _, r in tr for _, s_ in ts] for _, _, tr, ts in live])
+    offs = offs.tolist()
+    for i, (a, b, tr, ts) in enumerate(live):
+        n = C * len(tr) * len(ts) * K
+        wsub = packed[offs[i]:offs[i] + n].view(C, len(tr), len(ts), K)
+        Hs, Ws = (H - a + stride - 1) // stride, (W - b + stride - 1) // stride
+        C_.conv_fwd_subgrid(gy, wsub, -tr[0][0], Hs, Ws, dx, stride, a, b, addend is not None)
     return dx
 
 

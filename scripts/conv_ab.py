@@ -18,6 +18,8 @@ from k8s_amd.ops._ext import load  # noqa: E402
 # (name, H, C, K): 1x1 stride-1 convs at batch N -> GEMM M = N*H*H, N = K, K = C
 CASES = [("s0.conv3", 56, 64, 256), ("s0.conv1", 56, 256, 64), ("s1.conv3", 28, 128, 512),
          ("s2.conv3", 14, 256, 1024), ("s2.conv1", 14, 1024, 256), ("s0.c1b0", 56, 64, 64)]
+# 3x3 stride-1 convs (name, H, C, K): PMC_ONLY=100 + index runs one of these 10x
+CASES3 = [("s0.conv2", 56, 64, 64), ("s1.conv2", 28, 128, 128), ("s2.conv2", 14, 256, 256), ("s3.conv2", 7, 512, 512)]
 
 
 def timed(fn, reps=7):
@@ -42,6 +44,15 @@ def main():
     C_ = load()
     dev = torch.device("cuda")
     only = os.environ.get("PMC_ONLY")
+    if only is not None and int(only) >= 100:
+        name, H, C, K = CASES3[int(only) - 100]
+        x = torch.randn(a.batch, H, H, C, device=dev, dtype=torch.bfloat16)
+        w = (torch.randn(K, 3, 3, C, device=dev) * 0.05).bfloat16()
+        st = torch.zeros(C_.conv_stat_replicas, 2, K, device=dev)
+        for _ in range(10):
+            C_.conv_fwd(x, w, 1, 1, 1, False, None, 0, st)
+        torch.cuda.synchronize()
+        return
     for i, (name, H, C, K) in enumerate(CASES):
         if only is not None and int(only) != i:
             continue
@@ -69,6 +80,15 @@ def main():
             out[k + "_ms"] = round(t, 4)
             out[k + "_tbps"] = round(nbytes / t / 1e9, 2)
         print(json.dumps(out), flush=True)
+    if only is None:
+        for name, H, C, K in CASES3:
+            x = torch.randn(a.batch, H, H, C, device=dev, dtype=torch.bfloat16)
+            w = (torch.randn(K, 3, 3, C, device=dev) * 0.05).bfloat16()
+            st = torch.zeros(C_.conv_stat_replicas, 2, K, device=dev)
+            t = timed(lambda: C_.conv_fwd(x, w, 1, 1, 1, False, None, 0, st))
+            flops = 2.0 * a.batch * H * H * K * 9 * C
+            print(json.dumps({"case": name + " 3x3", "conv_stats_ms": round(t, 4),
+                              "tflops": round(flops / t / 1e9, 1)}), flush=True)
 
 
 if __name__ == "__main__":
