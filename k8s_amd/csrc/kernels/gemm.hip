@@ -203,10 +203,29 @@ struct ConvWgB {
     if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) return g_zero_page;
     return x + (((long)n * H + hi) * W + wi) * C + c;
   }
-  // no hoisted cursor: every tile re-derives the address from the slot index
-  struct Cursor { int s, base; };
-  __device__ __forceinline__ Cursor cursor(int s, int base) const { return Cursor{s, base}; }
-  __device__ __forceinline__ const void* at(const Cursor& c, int k0) const { return src(c.s, c.base, k0); }
+  // Hoisted cursor: a thread's column (r, s, c) -- and so its tap offsets -- is fixed for the whole K loop; a K
+  // step only decodes its row m = k0 + krow into (n, ho, wo) (two multiply-high divisions).
+  struct Cursor {
+    int krow, dh, dw, coff;  // dh/dw: r*dil - pad, s*dil - pad; krow < 0 marks a padding column
+  };
+  __device__ __forceinline__ Cursor cursor(int s, int c0) const {
+    const int krow = s >> 4, up = s & 15;
+    const int u = up ^ mn_swz(krow);
+    const int col = c0 + u * 8;
+    if (col >= cols) return Cursor{-(1 << 30), 0, 0, 0};
+    const int rs = fC.div(col), c = col - rs * C;
+    const int r = fS.div(rs), sx = rs - r * S;
+    return Cursor{krow, r * dil - pad, sx * dil - pad, c};
+  }
+  __device__ __forceinline__ const void* at(const Cursor& q, int k0) const {
+    const int m = k0 + q.krow;
+    if (q.krow < 0 || m >= mtot) return g_zero_page;
+    const int n = fHW.div(m), rem = m - n * (Ho * Wo);
+    const int ho = fWo.div(rem), wo = rem - ho * Wo;
+    const int hi = ho * stride + q.dh, wi = wo * stride + q.dw;
+    if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) return g_zero_page;
+    return x + (((long)n * H + hi) * W + wi) * C + q.coff;
+  }
   // per-K-step uniform part of the address (identity here; see ConvA)
   __device__ __forceinline__ int tap(int k0) const { return k0; }
   static constexpr bool kmajor = false;
@@ -437,8 +456,8 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
         // long K loops: the next K step's loads are issued behind the first half's MFMAs (their address
         // arithmetic then runs while the matrix pipe is busy instead of delaying the MFMAs); short ones keep them
         // ahead of the MFMAs (more time in flight). The buffer they fill was released by the previous barrier.
-        if (late && t + 1 < nt) {
-          stage(cur ^ 1, kbeg + (t + 1) * BK);
+        if (t + 1 < nt) {
+          if (late) stage(cur ^ 1, kbeg + (t + 1) * BK);
         } else if constexpr (BNB) {  // last K step: the other buffer is idle
           if (E.bstats) {
             stage_x(smem + (cur ^ 1) * (TA + TB));

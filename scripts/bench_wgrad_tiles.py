@@ -22,7 +22,7 @@ SHAPES = [  # H(in), C, K, R, stride, pad
     (56, 256, 128, 1, 1, 0), (56, 256, 512, 1, 2, 0), (28, 512, 256, 1, 1, 0), (28, 512, 1024, 1, 2, 0),
     (14, 1024, 512, 1, 1, 0), (14, 1024, 2048, 1, 2, 0),
 ]
-TILES = [t for t in os.environ.get("WGS_TILES", "128x64,128x128,256x128,64x64").split(",") if t]
+TILES = [t for t in os.environ.get("WGS_TILES", "128x64,128x128,256x128,64x64").split(",") if "x" in t]
 
 
 def timed(fn, reps=5):
