@@ -153,6 +153,11 @@ void launch_embed_bwd(const EmbTable* tabs, int ntab, int T, int D, int S, const
 void launch_avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st);
 void launch_avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st);
 
+// ---- stem.hip: 7x7 / stride-2 stem as a 4x4 conv over the 2x2 space-to-depth image (16 channels)
+void launch_stem_s2d_input(const uint16_t* x, int N, int H, int W, int Cin, int pad, uint16_t* out, hipStream_t st);
+void launch_stem_w_s2d(const uint16_t* w7, int K, int R, int Cw, uint16_t* w4, hipStream_t st);
+void launch_stem_dw_s2d(const float* dw4, int K, int R, int Cw, float* dw7, hipStream_t st);
+
 // ---- NHWC max pooling (pool.hip): idx = winning window position per output element (uint8)
 void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
                         int k, int s, int p, hipStream_t st);

@@ -696,6 +696,31 @@ void embed_bwd(Tensor g, std::vector<Tensor> grads, std::vector<c10::optional<Te
   k8s_amd::launch_embed_bwd(tabs, (int)grads.size(), (int)T, (int)D, (int)S, cbf(g), cur_stream());
 }
 
+// ------------------------------------------------------------------ space-to-depth stem
+Tensor stem_s2d_input(Tensor x, int64_t pad) {
+  check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) <= 8, "x must be NHWC with <= 8 channels");
+  const int N = x.size(0), H = x.size(1), W = x.size(2);
+  auto out = torch::empty({N, (H + 2 * pad) / 2, (W + 2 * pad) / 2, 16}, x.options());
+  k8s_amd::launch_stem_s2d_input(cbf(x), N, H, W, (int)x.size(3), (int)pad, bf(out), cur_stream());
+  return out;
+}
+Tensor stem_w_s2d(Tensor w7) {
+  check_cuda(w7, "w7"); check_dtype(w7, at::kBFloat16, "w7");
+  TORCH_CHECK(w7.dim() == 4 && w7.size(1) == w7.size(2), "w7 must be [K, R, R, C]");
+  const int K = w7.size(0), R = w7.size(1), Rs = (R + 1) / 2;
+  auto w4 = torch::empty({K, Rs, Rs, 16}, w7.options());
+  k8s_amd::launch_stem_w_s2d(cbf(w7), K, R, (int)w7.size(3), bf(w4), cur_stream());
+  return w4;
+}
+void stem_dw_s2d(Tensor dw4, Tensor dw7) {
+  check_cuda(dw4, "dw4"); check_cuda(dw7, "dw7");
+  check_dtype(dw4, at::kFloat, "dw4"); check_dtype(dw7, at::kFloat, "dw7");
+  const int K = dw7.size(0), R = dw7.size(1), Rs = (R + 1) / 2;
+  TORCH_CHECK(dw4.numel() == (long)K * Rs * Rs * 16, "dw4 must be [K, Rs, Rs, 16]");
+  k8s_amd::launch_stem_dw_s2d(f32(dw4), K, R, (int)dw7.size(3), f32(dw7), cur_stream());
+}
+
 Tensor avgpool_fwd(Tensor x) {
   check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x");
   TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "x must be NHWC with C % 8 == 0");
@@ -762,6 +787,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("stem_s2d_input", &stem_s2d_input);
+  m.def("stem_w_s2d", &stem_w_s2d);
+  m.def("stem_dw_s2d", &stem_dw_s2d);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("flash_bwd", &flash_bwd, py::arg("dO"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),

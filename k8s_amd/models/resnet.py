@@ -91,9 +91,11 @@ class Bottleneck(nn.Module):
 
 class ResNet(nn.Module):
     def __init__(self, store: ParamStore, layers: List[int] = (3, 4, 6, 3), num_classes: int = 1000,
-                 in_ch: int = 3, width: int = 64):
+                 in_ch: int = 3, width: int = 64, stem_s2d: bool = True):
         super().__init__()
         self.store = store
+        # GPU: the 7x7/s2 stem runs as a 4x4 conv over the space-to-depth image (ops.nn.stem_conv_s2d)
+        self.stem_s2d = stem_s2d
         # the stem reads a channel-padded image (3 -> 8 channels, zeros) so every NHWC row is 16-B aligned
         self.in_ch = in_ch
         self.stem_ch = (in_ch + 7) // 8 * 8
@@ -122,15 +124,22 @@ class ResNet(nn.Module):
             self.store.refresh_lowp()
         return self.to(device)
 
-    def prepare_input(self, images_nhwc: torch.Tensor) -> torch.Tensor:
-        """[N, H, W, 3] -> [N, H, W, 8] bf16 (zero channel padding)."""
+    def prepare_input(self, images_nhwc: torch.Tensor, s2d: bool = None) -> torch.Tensor:
+        """[N, H, W, 3] -> the stem's input: on the GPU (bf16) the [N, H/2+3, W/2+3, 16] space-to-depth image
+        of ``stem_conv_s2d``; otherwise (or ``s2d=False``) [N, H, W, 8] (zero channel padding)."""
+        use = self.stem_s2d if s2d is None else s2d
+        if use and images_nhwc.is_cuda and images_nhwc.dtype == torch.bfloat16 and self.conv1.w.shape[1] == 7:
+            return K.stem_s2d_input(images_nhwc, pad=3)
         if images_nhwc.shape[-1] == self.stem_ch:
             return images_nhwc
         pad = self.stem_ch - images_nhwc.shape[-1]
         return torch.nn.functional.pad(images_nhwc, (0, pad))
 
     def forward(self, x):
-        y = self.bn1(self.conv1(x))
+        if x.shape[-1] == 16 and self.stem_s2d and x.is_cuda:  # space-to-depth stem (prepare_input)
+            y = self.bn1(K.stem_conv_s2d(x, self.conv1.w))
+        else:
+            y = self.bn1(self.conv1(x))
         y = K.max_pool_nhwc(y, 3, 2, 1)
         link = None
         for b in self.blocks:

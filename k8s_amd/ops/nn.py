@@ -129,6 +129,56 @@ def conv2d_nhwc(x: torch.Tensor, p, stride: int = 1, padding: int = 0, with_stat
     return (y, sums) if with_stats else y
 
 
+class _StemS2D(torch.autograd.Function):
+    """The 7x7 / stride-2 / pad-3 stem as a 4x4 / stride-1 conv over the 2x2 space-to-depth image
+    (csrc/kernels/stem.hip): the master weight stays [K, 7, 7, C]; forward maps it to [K, 4, 4, 16], backward maps
+    the 4x4 weight gradient back into the parameter's flat fp32 slot. The image needs no gradient."""
+
+    @staticmethod
+    def forward(ctx, xs, anchor, p):
+        C_ = _C()
+        w7 = p.weight if p.weight.dtype == xs.dtype else p.master.to(xs.dtype)
+        w4 = C_.stem_w_s2d(w7.contiguous())
+        sums = _zero_scratch(p.store, xs.device, C_.conv_stat_replicas * 2 * w4.shape[0]).view(
+            C_.conv_stat_replicas, 2, w4.shape[0])
+        y = C_.conv_fwd(xs, w4, 1, 0, 1, False, None, 0, sums)
+        _conv_impl().STATS["hip_fwd"] += 1
+        ctx.save_for_backward(xs)
+        ctx.p, ctx.kshape = p, tuple(w4.shape)
+        ctx.mark_non_differentiable(sums)
+        ctx.set_materialize_grads(False)
+        return y, sums
+
+    @staticmethod
+    def backward(ctx, gy, _gsums=None):
+        (xs,) = ctx.saved_tensors
+        p, C_ = ctx.p, _C()
+        dw4 = torch.empty(ctx.kshape, device=xs.device, dtype=torch.float32)
+        _conv_impl()._wgrad_hip(C_, gy.contiguous(), xs, dw4, 1, 0, False)
+        _conv_impl().STATS["hip_wgrad"] += 1
+        store = p.store
+        slot = store.slot_for_write(p)
+        if slot is not None:
+            C_.stem_dw_s2d(dw4, slot.view(p.shape))
+            store.mark_written(p)
+        else:
+            tmp = torch.empty(p.shape, device=xs.device, dtype=torch.float32)
+            C_.stem_dw_s2d(dw4, tmp)
+            store.deposit(p, tmp)
+        return None, None, None
+
+
+def stem_conv_s2d(xs, p):
+    """(y, BN statistics) of the 7x7/s2 stem weight ``p`` applied to a space-to-depth image ``xs`` [N, H/2+3,
+    W/2+3, 16] (``stem_s2d_input``); GPU only."""
+    return _StemS2D.apply(xs, p.store.anchor, p)
+
+
+def stem_s2d_input(images, pad: int = 3):
+    """[N, H, W, <= 8] bf16 image -> [N, (H+2*pad)/2, (W+2*pad)/2, 16] space-to-depth input of ``stem_conv_s2d``."""
+    return _C().stem_s2d_input(images.contiguous(), pad)
+
+
 # =========================================================================== batchnorm + act
 class _BnAct(torch.autograd.Function):
     @staticmethod

@@ -51,14 +51,17 @@ def test_resnet_gradients_match_plain_pytorch_gpu(cuda):
     store = ParamStore()
     m = ResNet(store, (2, 2, 1, 1), 10, width=64).finalize(cuda, seed=3)
     m.train()
-    x = m.prepare_input(torch.randn(8, 64, 64, 3, device=cuda).bfloat16())
+    images = torch.randn(8, 64, 64, 3, device=cuda).bfloat16()
+    x = m.prepare_input(images)  # the space-to-depth stem input on the GPU
+    assert x.shape[-1] == 16
+    x8 = m.prepare_input(images, s2d=False)  # the plain 7x7 stem's input for the reference twin
     y = torch.randint(0, 10, (8,), device=cuda)
     store.begin_step()
     loss = K.cross_entropy(m(x), y)
     loss.backward()
     store.zero_unwritten()
-    ref_loss, ref = reference_grads(m, store, x, y)
-    _, stock = reference_grads(m, store, x, y, autocast_bf16=True)  # stock bf16 autocast: the noise floor
+    ref_loss, ref = reference_grads(m, store, x8, y)
+    _, stock = reference_grads(m, store, x8, y, autocast_bf16=True)  # stock bf16 autocast: the noise floor
     assert abs(loss.float().item() - ref_loss.item()) < 3e-2 * max(1.0, abs(ref_loss.item()))
     bad = []
     for p in store.params:
@@ -68,3 +71,34 @@ def test_resnet_gradients_match_plain_pytorch_gpu(cuda):
         if err > 2.0 * floor + 0.03:
             bad.append((p.name, round(err, 3), round(floor, 3)))
     assert not bad, bad
+
+
+def test_stem_space_to_depth_matches_7x7(cuda):
+    """stem_conv_s2d (4x4 conv over the 2x2 space-to-depth image) vs the 7x7 / stride-2 / pad-3 convolution of
+    the same weight: forward output and the weight gradient mapped back to the 7x7 layout."""
+    import torch.nn.functional as F
+
+    from k8s_amd.parallel.flat import ParamStore, init_normal
+
+    torch.manual_seed(2)
+    store = ParamStore()
+    p = store.new("conv1.weight", (64, 7, 7, 8), init_normal(0.05))
+    store.finalize(cuda)
+    with torch.no_grad():
+        p.master[..., 3:].zero_()
+    store.refresh_lowp()
+    img = torch.randn(4, 32, 32, 3, device=cuda).bfloat16()
+    xs = K.stem_s2d_input(img)
+    assert xs.shape == (4, 19, 19, 16)
+    store.begin_step()
+    y, _ = K.stem_conv_s2d(xs, p)
+    g = torch.randn_like(y)
+    y.backward(g)
+    w = p.master.detach().bfloat16().float().permute(0, 3, 1, 2)[:, :3].clone().requires_grad_(True)
+    ref = F.conv2d(img.float().permute(0, 3, 1, 2), w, None, 2, 3)
+    ref.backward(g.float().permute(0, 3, 1, 2))
+    rel = lambda a, b: ((a.float() - b.float()).norm() / b.float().norm()).item()  # noqa: E731
+    assert rel(y.permute(0, 3, 1, 2), ref) < 1e-2
+    dw = p.grad.view(p.shape)
+    assert rel(dw[..., :3].permute(0, 3, 1, 2), w.grad) < 1e-2
+    assert dw[..., 3:].abs().max().item() == 0.0
