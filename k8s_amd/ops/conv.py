@@ -41,6 +41,9 @@ import os
 # products (the single-buffer 1x1 dgrads run 2.3x slower) -- 10.61k vs 11.00k img/s. K8S_AMD_BN_LINK=1 turns
 # it on.
 BN_LINK = os.environ.get("K8S_AMD_BN_LINK", "0") == "1"
+# ... or only for dgrads whose reduction (R*S*K) is at least this long, where the epilogue's extra work is small
+# next to the K loop (K8S_AMD_BN_LINK_MIN_K; 0 = off)
+BN_LINK_MIN_K = int(os.environ.get("K8S_AMD_BN_LINK_MIN_K", "0"))
 
 STATS = {"hip_fwd": 0, "aten_fwd": 0, "hip_wgrad": 0, "aten_wgrad": 0, "hip_dgrad": 0, "aten_dgrad": 0}
 
@@ -210,7 +213,8 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, bn_link=No
         if hip and stride == 1 and K % 64 == 0 and C % 8 == 0:
             STATS["hip_dgrad"] += 1
             bnb = None
-            if BN_LINK and bn_link is not None and p is not None and (R == 1 or addend is None):
+            link_on = BN_LINK or (BN_LINK_MIN_K > 0 and R * S * K >= BN_LINK_MIN_K)
+            if link_on and bn_link is not None and p is not None and (R == 1 or addend is None):
                 bnb = bn_link.epilogue_args(p.store, gy.device)
             dx = _dgrad_hip(C_, gy, w, padding, addend, bnb)
         elif hip and strided_dgrad_ok(gy, w, stride, padding):
