@@ -599,4 +599,26 @@ void launch_relu_mask(const uint16_t* y, uint8_t* mask, long nvec, hipStream_t s
   hipLaunchKernelGGL(relu_mask_kernel, dim3(cdiv(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, y, mask, (int)nvec);
 }
 
+// out = bit ? src : 0: a residual gradient handed over as (dy, ReLU mask) materialised for a consumer whose
+// epilogue cannot read the pair itself (GEMM Epi::addmask covers the 1x1 identity-block dgrad)
+__global__ void __launch_bounds__(BN_THREADS) mask_apply_kernel(const uint16_t* __restrict__ src,
+                                                                const uint8_t* __restrict__ mask,
+                                                                uint16_t* __restrict__ out, int nvec) {
+  const int e = blockIdx.x * BN_THREADS + threadIdx.x;
+  if (e >= nvec) return;
+  bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(src + (long)e * 8);
+  const uint32_t bits = mask[e];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) v[r] = ((bits >> r) & 1u) ? v[r] : (short)0;
+  *reinterpret_cast<bf16x8_t*>(out + (long)e * 8) = v;
+}
+
+void launch_mask_apply(const uint16_t* src, const uint8_t* mask, uint16_t* out, long n, hipStream_t st) {
+  if (n % 8) throw std::runtime_error("mask_apply: element count must be a multiple of 8");
+  const long nvec = n / 8;
+  if (nvec >= (1L << 31)) throw std::runtime_error("tensor too large (>= 2^31 vectors)");
+  hipLaunchKernelGGL(mask_apply_kernel, dim3(cdiv(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, src, mask, out,
+                     (int)nvec);
+}
+
 }  // namespace k8s_amd

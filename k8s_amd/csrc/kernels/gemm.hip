@@ -308,6 +308,12 @@ struct Epi {
   // is stored at output row (n, i*rst + ra, j*rst + rb) of an rH x rW image. rst == 0: identity.
   int rst, rHo, rWo, rH, rW, ra, rb;
   int late_nt;  // K steps from which the next step's loads are issued behind the first MFMA half
+  // accumulate (mode 1, lean epilogue) onto addsrc instead of C's old value, with the elements whose packed bit in
+  // addmask is clear taken as zero: C = acc + (bit ? addsrc : 0). A ResNet identity block's input gradient is
+  // conv1's dgrad plus the block output's gradient masked by its ReLU -- read here from dy and the forward's
+  // 1-bit mask instead of from a materialised residual gradient.
+  const uint16_t* addsrc;
+  const uint8_t* addmask;
 };
 constexpr int STAT_REPL = 32;
 
@@ -538,7 +544,13 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
       bf16x8_t o = *reinterpret_cast<const bf16x8_t*>(ctile + row * BN + ((c ^ (row % CPR)) << 3));
       uint16_t* cp = reinterpret_cast<uint16_t*>(ec) + orow * E.ldc + n;
       if (emode == 1) {  // accumulate onto bf16 C: the staged value is already bf16 (two roundings, <= 1 ulp more)
-        const bf16x8_t old = *reinterpret_cast<const bf16x8_t*>(cp);
+        const long aoff = orow * E.ldc + n;
+        bf16x8_t old = *reinterpret_cast<const bf16x8_t*>(E.addsrc ? E.addsrc + aoff : cp);
+        if (E.addmask) {
+          const uint32_t abits = E.addmask[aoff >> 3];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) old[r] = ((abits >> r) & 1u) ? old[r] : (short)0;
+        }
 #pragma unroll
         for (int r = 0; r < 8; ++r) o[r] = (short)f2bf(bf2f((uint16_t)o[r]) + bf2f((uint16_t)old[r]));
       }
@@ -763,6 +775,7 @@ static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int 
     }
   }
   if (e.bstats) throw std::runtime_error("the BatchNorm-backward epilogue needs a plain bf16 output (lean epilogue)");
+  if (e.addsrc || e.addmask) throw std::runtime_error("a separate (masked) addend needs the lean epilogue");
   launch_tiles2<ASrc, BSrc, WM, WN, false, false>(a, b, e, M, N, K, kps, splits, st);
 }
 
@@ -798,6 +811,8 @@ static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act,
   e.bmean = e.binvstd = e.bgamma = e.bbeta = nullptr;
   e.brelu_x = 0;
   e.rst = e.rHo = e.rWo = e.rH = e.rW = e.ra = e.rb = 0;
+  e.addsrc = nullptr;
+  e.addmask = nullptr;
   // $K8S_AMD_GEMM_LATE_NT (A/B knob), default off: issuing the next step's loads behind the first MFMA half sped
   // up the isolated 56x56 / 28x28 3x3 convolutions 7-12 % but the ResNet-50 step lost 1.5 % at any threshold
   // (b1024: 11.00k img/s never late, 10.84k from 8 K steps, 10.80k always; scripts/gpurun/bench_ab.sh)
@@ -876,12 +891,17 @@ static void apply_bnbwd(Epi& e, const BnBwdEpi* bb) {
 
 void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                  long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
-                 float alpha, int splits, float* ws, hipStream_t st, const BnBwdEpi* bnb) {
+                 float alpha, int splits, float* ws, hipStream_t st, const BnBwdEpi* bnb, const AddEpi* add) {
   splits = effective_splits(K, splits);
   const bool slab = splits > 1;
   Epi e = make_epi(slab ? (void*)ws : C, slab ? (long)N : ldc, c_f32, bias, act, pre, slab ? 3 : mode, alpha);
   e.slab = (long)M * N;
   if (!slab) apply_bnbwd(e, bnb);
+  if (add) {
+    if (slab || mode != 1) throw std::runtime_error("a separate addend needs accumulate mode and no split-K");
+    e.addsrc = add->src;
+    e.addmask = add->mask;
+  }
   if (a_kmajor && b_kmajor)
     launch(KMajor{A, lda, M}, KMajor{B, ldb, N}, e, M, N, K, splits, st);
   else if (a_kmajor && !b_kmajor)

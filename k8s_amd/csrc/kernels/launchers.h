@@ -66,9 +66,18 @@ struct BnBwdEpi {
   const float *mean, *invstd, *gamma, *beta;
   int relu_x;         // mask recomputed from x
 };
+// accumulate-mode addend read from src (same layout as C) instead of C, elements with a clear bit in the packed
+// mask (bit j of byte e = element 8e + j; null = all set) taken as zero (see Epi::addsrc in gemm.hip)
+struct AddEpi {
+  const uint16_t* src;
+  const uint8_t* mask;
+};
 void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                  long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
-                 float alpha, int splits, float* ws, hipStream_t st, const BnBwdEpi* bnb = nullptr);
+                 float alpha, int splits, float* ws, hipStream_t st, const BnBwdEpi* bnb = nullptr,
+                 const AddEpi* add = nullptr);
+// out = bit ? src : 0 per element (bf16, n % 8 == 0; mask packed as above)
+void launch_mask_apply(const uint16_t* src, const uint8_t* mask, uint16_t* out, long n, hipStream_t st);
 long gemm_splitk_workspace(int M, int N, int splits);  // fp32 elements of the split-K slab workspace
 // gemm256.hip: 256 x 256-tile, 8-wave phased MFMA GEMM for the large (transformer) products
 bool gemm256_eligible(int M, int N, int K, bool a_kmajor, bool b_kmajor);

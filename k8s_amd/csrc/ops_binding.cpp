@@ -301,15 +301,33 @@ BnbHolder parse_bnb(const c10::optional<std::vector<Tensor>>& t, c10::optional<b
   return h;
 }
 
-// K8S_AMD_GEMM256=0 routes every product to the 128 x 128 kernel (A/B comparisons, debugging)
-static bool gemm256_enabled() {
-  const char* e = std::getenv("K8S_AMD_GEMM256");  // per call: one process can A/B both kernels
-  return !(e && e[0] == '0');
+// K8S_AMD_GEMM256=0 routes every product to the 128 x 128 kernel, =2 every product the 256 x 256 kernel can take
+// (A/B comparisons, debugging); read per call, so one process can A/B both kernels
+static int gemm256_mode() {
+  const char* e = std::getenv("K8S_AMD_GEMM256");
+  return e ? atoi(e) : 1;
+}
+static bool use_gemm256(long M, long N, long K, bool a_kmajor, bool b_kmajor) {
+  const int m = gemm256_mode();
+  if (m == 2)
+    return K % 64 == 0 && N % 4 == 0 && (a_kmajor || M % 8 == 0) && (b_kmajor || N % 8 == 0);
+  return m != 0 && k8s_amd::gemm256_eligible((int)M, (int)N, (int)K, a_kmajor, b_kmajor);
+}
+
+Tensor mask_apply(Tensor src, Tensor mask) {
+  check_cuda(src, "src");
+  check_dtype(src, at::kBFloat16, "src");
+  TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == at::kByte && mask.is_contiguous() &&
+                  mask.numel() * 8 == src.numel(), "mask: packed uint8, one bit per element");
+  Tensor out = torch::empty_like(src);
+  k8s_amd::launch_mask_apply(cbf(src), mask.data_ptr<uint8_t>(), bf(out), src.numel(), cur_stream());
+  return out;
 }
 
 Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tensor> out, bool out_f32,
             c10::optional<Tensor> bias, int64_t act, c10::optional<Tensor> pre, bool accumulate, double alpha,
-            int64_t splits, c10::optional<std::vector<Tensor>> bnb, c10::optional<bool> bnb_relu_x) {
+            int64_t splits, c10::optional<std::vector<Tensor>> bnb, c10::optional<bool> bnb_relu_x,
+            c10::optional<Tensor> add_src, c10::optional<Tensor> add_mask) {
   check_bf16_operand(a, "A");
   check_bf16_operand(b, "B");
   const long M = a_kmajor ? a.size(0) : a.size(1), K = a_kmajor ? a.size(1) : a.size(0);
@@ -330,7 +348,21 @@ Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tens
   if (bias) TORCH_CHECK(bias->numel() == N && bias->scalar_type() == at::kFloat && bias->is_contiguous());
   if (pre) TORCH_CHECK(pre->numel() == M * N && pre->scalar_type() == at::kBFloat16 && pre->is_contiguous());
   const int mode = accumulate ? 1 : 0;
-  if (!bnb && gemm256_enabled() && k8s_amd::gemm256_eligible((int)M, (int)N, (int)K, a_kmajor, b_kmajor)) {
+  k8s_amd::AddEpi add{nullptr, nullptr};
+  if (add_src) {
+    TORCH_CHECK(accumulate && !out_f32, "add_src: a bf16 accumulate-mode output");
+    TORCH_CHECK(add_src->is_cuda() && add_src->scalar_type() == at::kBFloat16 && add_src->is_contiguous() &&
+                    add_src->numel() == M * N, "add_src must be a contiguous bf16 tensor of the output's size");
+    add.src = cbf(*add_src);
+    if (add_mask) {
+      TORCH_CHECK(add_mask->is_cuda() && add_mask->scalar_type() == at::kByte && add_mask->is_contiguous() &&
+                      add_mask->numel() * 8 == M * N, "add_mask: packed uint8, one bit per output element");
+      add.mask = add_mask->data_ptr<uint8_t>();
+    }
+  } else {
+    TORCH_CHECK(!add_mask, "add_mask needs add_src");
+  }
+  if (!bnb && !add_src && use_gemm256(M, N, K, a_kmajor, b_kmajor)) {
     k8s_amd::launch_gemm256(cbf(a), a.stride(0), a_kmajor, cbf(b), b.stride(0), b_kmajor, c.data_ptr(), N, out_f32,
                             (int)M, (int)N, (int)K, bias ? bias->data_ptr<float>() : nullptr, (int)act,
                             pre ? bf(*pre) : nullptr, accumulate, (float)alpha, cur_stream());
@@ -349,7 +381,7 @@ Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tens
   k8s_amd::launch_gemm(cbf(a), a.stride(0), a_kmajor, cbf(b), b.stride(0), b_kmajor, c.data_ptr(), N, out_f32,
                        (int)M, (int)N, (int)K, bias ? bias->data_ptr<float>() : nullptr, (int)act,
                        pre ? bf(*pre) : nullptr, mode, (float)alpha, sp, sp > 1 ? f32(ws) : nullptr, cur_stream(),
-                       bb.on ? &bb.e : nullptr);
+                       bb.on ? &bb.e : nullptr, add_src ? &add : nullptr);
   return c;
 }
 
@@ -767,7 +799,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_stream_eligible", &k8s_amd::wgrad_stream_eligible, "tall-K weight-gradient kernel takes this shape");
   m.def("gemm", &gemm, py::arg("a"), py::arg("a_kmajor"), py::arg("b"), py::arg("b_kmajor"), py::arg("out"),
         py::arg("out_f32"), py::arg("bias"), py::arg("act"), py::arg("pre"), py::arg("accumulate"), py::arg("alpha"),
-        py::arg("splits"), py::arg("bnb") = py::none(), py::arg("bnb_relu_x") = py::none());
+        py::arg("splits"), py::arg("bnb") = py::none(), py::arg("bnb_relu_x") = py::none(),
+        py::arg("add_src") = py::none(), py::arg("add_mask") = py::none());
+  m.def("mask_apply", &mask_apply, "out = bit ? src : 0 (packed 1-bit mask per element)");
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("rope_", &rope_);

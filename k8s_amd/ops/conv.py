@@ -122,14 +122,22 @@ def _dgrad_hip(C_, gy, w, padding, addend=None, bnb=None):
     BnBwdLink.epilogue_args: the epilogue also reduces the BN backward's statistics of dx."""
     K, R, S, C = w.shape
     bl, brx = bnb if bnb is not None else (None, None)
+    masked = addend is not None and not torch.is_tensor(addend)  # nn.MaskedGrad: (dy, packed ReLU mask)
     if R == 1 and S == 1 and padding == 0:
         N, H, W_, _ = gy.shape
+        if masked:  # the epilogue reads dy and the mask bits itself: no materialised residual gradient
+            out = torch.empty(N, H, W_, C, device=gy.device, dtype=gy.dtype)
+            C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, out.view(-1, C), False, None, 0, None, True,
+                    1.0, 1, bl, brx, addend.dy.view(-1, C), addend.mask)
+            return out
         if addend is not None:
             C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, addend.view(-1, C), False, None, 0, None, True,
                     1.0, 1, bl, brx)
             return addend
         return C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, None, False, None, 0, None, False, 1.0,
                        1, bl, brx).reshape(N, H, W_, C)
+    if masked:
+        addend = addend.materialize()
     if addend is not None:  # (no 3x3 consumer needs both; keep the statistics exact: reduce after the add)
         bl = None
     dx = C_.conv_fwd(gy, C_.conv_dgrad_wtrans(w), 1, R - 1 - padding, 1, False, None, 0, None, bl, brx)
@@ -196,6 +204,9 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, bn_link=No
     K, R, S, C = w.shape
     C_ = _load() if gy.is_cuda else None
     hip = _hip(gy, x, w)
+    if addend is not None and not torch.is_tensor(addend) and not (
+            hip and stride == 1 and K % 64 == 0 and C % 8 == 0):
+        addend = addend.materialize()  # only the stride-1 dgrad on our kernels takes the (dy, mask) pair
     # ---- weight gradient
     dw_done = False
     if hip and C % 8 == 0 and K % 8 == 0 and p is not None and p.grad.dtype == torch.float32:

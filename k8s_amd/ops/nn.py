@@ -11,6 +11,7 @@ conv weights are KRSC ``[K, R, S, C]``; linear weights ``[out, in]``.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -44,6 +45,10 @@ def _zero_scratch(store, device, n):
     return arena.take(n)
 
 
+# K8S_AMD_MASKED_RES_GRAD=0: the residual BN backward writes dres and the linked dgrad accumulates onto it (A/B)
+MASKED_RES_GRAD = os.environ.get("K8S_AMD_MASKED_RES_GRAD", "1") != "0"
+
+
 class GradLink:
     """Carries one tensor's gradient from one autograd node to another that runs later in the backward
     pass, so the sum of the two contributions is formed inside a kernel (e.g. a ResNet identity block:
@@ -56,6 +61,20 @@ class GradLink:
     def __init__(self, shared: bool = False):
         self.grad = None
         self.shared = shared
+
+
+class MaskedGrad:
+    """A residual gradient handed over unmaterialised: ``dy`` masked by the packed 1-bit ReLU ``mask`` of the BN
+    forward (bit j of byte e = element 8e + j). The 1x1 dgrad that receives it reads the pair in its epilogue
+    (GEMM add_src / add_mask), so the BN backward writes no dres tensor (2 B/element) and the dgrad reads 1/8 B
+    of mask more than it would have read of dres."""
+    __slots__ = ("dy", "mask")
+
+    def __init__(self, dy, mask):
+        self.dy, self.mask = dy, mask
+
+    def materialize(self):
+        return _C().mask_apply(self.dy, self.mask)
 
 
 class BnBwdLink:
@@ -228,8 +247,12 @@ class _BnAct(torch.autograd.Function):
             if ctx.bwd_link is not None:
                 reps, ctx.bwd_link.reps = ctx.bwd_link.reps, None
                 ctx.bwd_link.x = ctx.bwd_link.mask = None  # drop the extra references to the saved activations
-            dx, dres = _C().bn_bwd(dy, x, y, mean, invstd, pg.master, pb.master, ctx.relu_x, dg, db, ctx.has_res,
-                                   reps, mask)
+            # residual gradient for a linked consumer: (dy, mask) instead of a written dres tensor
+            handoff = ctx.has_res and ctx.res_link is not None and mask is not None and MASKED_RES_GRAD
+            dx, dres = _C().bn_bwd(dy, x, y, mean, invstd, pg.master, pb.master, ctx.relu_x, dg, db,
+                                   ctx.has_res and not handoff, reps, mask)
+            if handoff:
+                dres = MaskedGrad(dy, mask)
             if sg is not None:
                 store.mark_written(pg)
             else:

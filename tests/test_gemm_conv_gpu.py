@@ -319,6 +319,36 @@ def test_dgrad_bn_backward_epilogue(cuda, mode, accumulate):
     assert _rel(s, s_ref) < 1e-4 and _rel(q, q_ref) < 1e-4
 
 
+def _unpack_bits(mask, shape):
+    bits = mask.reshape(-1, 1).int()
+    return ((bits >> torch.arange(8, device=mask.device).int()) & 1).reshape(shape).bool()
+
+
+@pytest.mark.parametrize("with_mask", [True, False])
+def test_gemm_masked_addend_epilogue(cuda, with_mask):
+    """1x1 dgrad accumulating onto a separate addend masked by packed ReLU bits (identity-block residual
+    gradient read as (dy, mask) instead of a materialised dres): out = gy.w + (bit ? dy : 0)."""
+    torch.manual_seed(7)
+    C_ = _C()
+    M, K, C = 3000, 128, 192
+    gy = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(K, C, device=cuda) * 0.1).bfloat16()
+    dy = torch.randn(M, C, device=cuda).bfloat16()
+    mask = torch.randint(0, 256, (M * C // 8,), device=cuda, dtype=torch.uint8)
+    out = torch.full((M, C), 7.0, device=cuda, dtype=torch.bfloat16)  # overwritten, never read
+    C_.gemm(gy, True, w, False, out, False, None, 0, None, True, 1.0, 1, None, None, dy,
+            mask if with_mask else None)
+    on = _unpack_bits(mask, (M, C)) if with_mask else torch.ones(M, C, dtype=torch.bool, device=cuda)
+    ref = gy.float() @ w.float() + torch.where(on, dy.float(), torch.zeros_like(dy.float()))
+    assert _rel(out, ref) < 1e-2
+    # the same as the two-step form: materialise bit ? dy : 0, then accumulate onto it in place
+    if with_mask:
+        dres = C_.mask_apply(dy, mask)
+        assert torch.equal(dres.float(), torch.where(on, dy.float(), torch.zeros_like(dy.float())))
+        C_.gemm(gy, True, w, False, dres, False, None, 0, None, True, 1.0, 1)
+        assert torch.equal(dres, out)
+
+
 def test_conv3x3_dgrad_bn_backward_epilogue(cuda):
     """3x3 stride-1 dgrad (conv of dy with the flipped weights) with the BN-backward epilogue (relu_x)."""
     torch.manual_seed(5)
