@@ -97,8 +97,8 @@ def main(argv=None):
             if rank == 0:
                 print(json.dumps({"op": op, "bytes": nbytes, "n": n, "dtype": str(dtype).split(".")[-1],
                                   "backend": dist.get_backend() if dist.is_initialized() else "none",
-                                  "us": round(dt * 1e6, 1), "algbw_GBs": round(algbw, 2),
-                                  "busbw_GBs": round(algbw * bus_factor(op, n), 2)}), flush=True)
+                                  "us": round(dt * 1e6, 1), "algbw_GBs": round(algbw, 4),
+                                  "busbw_GBs": round(algbw * bus_factor(op, n), 4)}), flush=True)
             del buf, out
     kdist.destroy()
 

@@ -31,13 +31,13 @@ class BN(nn.Module):
         self.register_buffer("running_var", torch.ones(c))
         self.momentum, self.eps = 0.1, 1e-5
 
-    def forward(self, x, residual=None, relu=True, res_link=None, bwd_link=None):
+    def forward(self, x, residual=None, relu=True, res_link=None, bwd_link=None, dy_link=None):
         sums = None
         if isinstance(x, tuple):  # (conv output, fused statistics)
             x, sums = x
         return K.batch_norm_act(x, self.gamma, self.beta, self.running_mean, self.running_var, residual, relu,
                                 self.training, self.momentum, self.eps, sums=sums, res_link=res_link,
-                                bwd_link=bwd_link)
+                                bwd_link=bwd_link, dy_link=dy_link)
 
 
 class Conv(nn.Module):
@@ -84,9 +84,13 @@ class Bottleneck(nn.Module):
         l1, l2, l3 = K.BnBwdLink(), K.BnBwdLink(), K.BnBwdLink()
         y = self.bn1(self.conv1(x, grad_link=link or dlink, bn_link=in_link if identity else None), bwd_link=l1)
         y = self.bn2(self.conv2(y, bn_link=l1), bwd_link=l2)
+        # downsample block: bn3's ReLU mask is applied by the downsample BN's backward as it reads dy
+        mlink = None
         if self.down is not None:
-            idn = self.down_bn(self.down(x, grad_link=dlink), relu=False)
-        return self.bn3(self.conv3(y, bn_link=l2), residual=idn, relu=True, res_link=link, bwd_link=l3), l3
+            mlink = K.MaskLink()
+            idn = self.down_bn(self.down(x, grad_link=dlink), relu=False, dy_link=mlink)
+        return self.bn3(self.conv3(y, bn_link=l2), residual=idn, relu=True, res_link=link or mlink,
+                        bwd_link=l3), l3
 
 
 class ResNet(nn.Module):

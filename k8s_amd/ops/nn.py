@@ -77,6 +77,17 @@ class MaskedGrad:
         return _C().mask_apply(self.dy, self.mask)
 
 
+class MaskLink:
+    """Joins a residual BN (ReLU, packed mask) to the plain BN that produced its residual input (a ResNet
+    downsample branch): the residual BN's backward passes its incoming dy through unchanged as the residual's
+    gradient and leaves its ReLU mask here; the plain BN's backward applies the mask while it reads dy (its
+    reduce and apply kernels' mask path), so the masked gradient is never written out."""
+    __slots__ = ("mask",)
+
+    def __init__(self):
+        self.mask = None
+
+
 class BnBwdLink:
     """Lets the kernel that produces a BatchNorm's output gradient (the dgrad of the conv that consumed the BN
     output) also accumulate the BN backward's two channel reductions in its epilogue; the BN backward then
@@ -202,7 +213,7 @@ def stem_s2d_input(images, pad: int = 3):
 class _BnAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu, sums=None,
-                res_link=None, bwd_link=None):
+                res_link=None, bwd_link=None, dy_link=None):
         x = x.contiguous()
         if res is not None:
             res = res.contiguous()
@@ -226,6 +237,7 @@ class _BnAct(torch.autograd.Function):
         ctx.save_for_backward(x, y if keep_y else None, mean, invstd, mask)
         ctx.pg, ctx.pb, ctx.has_res, ctx.res_link = pg, pb, res is not None, res_link
         ctx.relu_x = relu and not keep_y and mask is None
+        ctx.dy_link = dy_link if (dy_link is not None and not relu and res is None) else None
         ctx.bwd_link = None
         if bwd_link is not None and _gpu(x) and training:
             bwd_link.x, bwd_link.mask, bwd_link.mean, bwd_link.invstd = x, mask, mean, invstd
@@ -239,6 +251,9 @@ class _BnAct(torch.autograd.Function):
         pg, pb = ctx.pg, ctx.pb
         store = pg.store
         dy = dy.contiguous()
+        if ctx.dy_link is not None and ctx.dy_link.mask is not None:  # dy arrives unmasked: apply the mask here
+            mask, ctx.dy_link.mask = ctx.dy_link.mask, None
+        mask_out = isinstance(ctx.res_link, MaskLink) and mask is not None and ctx.has_res and MASKED_RES_GRAD
         if _gpu(x):
             sg, sb = store.slot_for_write(pg), store.slot_for_write(pb)
             dg = sg if sg is not None else torch.empty(pg.shape, device=x.device, dtype=torch.float32)
@@ -248,11 +263,15 @@ class _BnAct(torch.autograd.Function):
                 reps, ctx.bwd_link.reps = ctx.bwd_link.reps, None
                 ctx.bwd_link.x = ctx.bwd_link.mask = None  # drop the extra references to the saved activations
             # residual gradient for a linked consumer: (dy, mask) instead of a written dres tensor
-            handoff = ctx.has_res and ctx.res_link is not None and mask is not None and MASKED_RES_GRAD
+            handoff = (isinstance(ctx.res_link, GradLink) and ctx.has_res and mask is not None and
+                       MASKED_RES_GRAD)
             dx, dres = _C().bn_bwd(dy, x, y, mean, invstd, pg.master, pb.master, ctx.relu_x, dg, db,
-                                   ctx.has_res and not handoff, reps, mask)
+                                   ctx.has_res and not (handoff or mask_out), reps, mask)
             if handoff:
                 dres = MaskedGrad(dy, mask)
+            elif mask_out:  # the producing plain BN masks dy itself (MaskLink)
+                dres = dy
+                ctx.res_link.mask = mask
             if sg is not None:
                 store.mark_written(pg)
             else:
@@ -265,22 +284,23 @@ class _BnAct(torch.autograd.Function):
             dx, dres, dg, db = ref.bn_bwd(dy, x, y, mean, invstd, pg.master)
             store.deposit(pg, dg)
             store.deposit(pb, db)
-        if ctx.has_res and ctx.res_link is not None:  # hand dres to the node that adds it in a kernel
+        if ctx.has_res and isinstance(ctx.res_link, GradLink):  # hand dres to the node that adds it in a kernel
             ctx.res_link.grad, dres = dres, None
         return (dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None, None,
-                None)
+                None, None)
 
 
 def batch_norm_act(x, pg, pb, run_mean, run_var, residual=None, relu=True, training=True, momentum=0.1,
-                   eps=1e-5, sums=None, res_link=None, bwd_link=None):
+                   eps=1e-5, sums=None, res_link=None, bwd_link=None, dy_link=None):
     """y = act(BN(x) + residual) over the last (channel) dim of an NHWC tensor.
 
     ``sums`` (fp32 [2, C] from ``conv2d_nhwc(..., with_stats=True)``) skips the statistics pass.
     ``res_link``: the residual's gradient is handed to that GradLink (and NOT returned to autograd); the
     node consuming the link must add it (``conv2d_nhwc(..., grad_link=link)`` on the same tensor).
-    ``bwd_link``: a BnBwdLink handed to the consumer of y (``conv2d_nhwc(y, ..., bn_link=link)``)."""
+    ``bwd_link``: a BnBwdLink handed to the consumer of y (``conv2d_nhwc(y, ..., bn_link=link)``).
+    ``res_link`` may also be a MaskLink whose ``dy_link`` end is the plain BN that produced ``residual``."""
     return _BnAct.apply(x, residual, pg.store.anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu,
-                        sums, res_link, bwd_link)
+                        sums, res_link, bwd_link, dy_link)
 
 
 # =========================================================================== layernorm / rmsnorm
