@@ -51,7 +51,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default=None)
-    ap.add_argument("--variants", nargs="*", default=[], help="extra ENV=VALUE arms, e.g. K8S_AMD_GEMM256_STAGGER=0")
+    ap.add_argument("--variants", nargs="*", default=[], help="extra ENV=VALUE[,ENV=VALUE] arms, e.g. K8S_AMD_GEMM256_KERNEL=quad,K8S_AMD_GEMM256_QVAR=1")
     a = ap.parse_args()
     groups = [a.only] if a.only else list(LAYERS)
     for grp in groups:
@@ -71,15 +71,18 @@ def main():
                 for _ in range(a.rounds):
                     to.append(timeit(ours))
                     tb.append(timeit(blas))
-                    for v in a.variants:  # ENV=VALUE A/B arms of our kernel, same process
-                        k_, v_ = v.split("=")
-                        old = os.environ.get(k_)
-                        os.environ[k_] = v_
+                    for v in a.variants:  # ENV=VALUE[,ENV=VALUE] A/B arms of our kernel, same process
+                        saved = {}
+                        for kv in v.split(","):
+                            k_, v_ = kv.split("=")
+                            saved[k_] = os.environ.get(k_)
+                            os.environ[k_] = v_
                         tv[v].append(timeit(ours))
-                        if old is None:
-                            os.environ.pop(k_)
-                        else:
-                            os.environ[k_] = old
+                        for k_, old in saved.items():
+                            if old is None:
+                                os.environ.pop(k_)
+                            else:
+                                os.environ[k_] = old
                 ref = blas().float()
                 got = ours().float()
                 err = ((got - ref).norm() / ref.norm()).item()
