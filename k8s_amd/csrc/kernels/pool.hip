@@ -77,6 +77,31 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const uint16_t* __rest
   // output windows covering (h, w): ho*s - p <= h <= ho*s - p + k - 1
   const int ho0 = max(0, (h + p - k + s) / s), ho1 = min(Ho - 1, (h + p) / s);
   const int wo0 = max(0, (w + p - k + s) / s), wo1 = min(Wo - 1, (w + p) / s);
+  if (k <= 2 * s) {
+    // at most 2 x 2 covering windows (the ResNet stem's 3x3 / s2): every window's winner bytes and dy vector are
+    // loaded up front (8 independent loads in flight) instead of a dependent idx -> dy round trip per window
+    uint64_t pk[4];
+    float g[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ho = ho0 + (q >> 1), wo = wo0 + (q & 1);
+      const bool ok = ho <= ho1 && wo <= wo1;
+      const long o = (((long)n * Ho + (ok ? ho : ho0)) * Wo + (ok ? wo : wo0)) * C + c;
+      pk[q] = *reinterpret_cast<const uint64_t*>(idx + o);  // (clamped in-bounds address when !ok: not used)
+      load8(dy + o, g[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ho = ho0 + (q >> 1), wo = wo0 + (q & 1);
+      if (ho > ho1 || wo > wo1) continue;
+      const uint8_t pos = (uint8_t)((h - (ho * s - p)) * k + (w - (wo * s - p)));
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (((pk[q] >> (8 * j)) & 0xff) == pos) acc[j] += g[q][j];
+    }
+    store8(dx + (long)e * 8, acc);
+    return;
+  }
   for (int ho = ho0; ho <= ho1; ++ho) {
     const int dh = h - (ho * s - p);
     for (int wo = wo0; wo <= wo1; ++wo) {

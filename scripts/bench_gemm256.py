@@ -4,7 +4,7 @@ interleaved rounds in ONE process on uniform random [-1, 1) bf16 operands (cdna_
 Every Llama-3-8B (M = 4096 tokens) and BERT-base (M = 8192 tokens) linear product in its three forms:
     fwd   y  = x . W^T   (A K-major,  B K-major)     torch: x @ W.t()
     dgrad dx = g . W     (A K-major,  B N-major)     torch: g @ W
-    wgrad dW = g^T . x   (A M-major,  B N-major)     torch: g.t() @ x   (fp32 out for ours, as in training)
+    wgrad dW = g^T . x   (A M-major,  B N-major)     torch: g.t() @ x   (fp32 out, split-K chosen as in training)
 
     python scripts/bench_gemm256.py [--rounds 5] [--only llama|bert|square] > gemm256.jsonl
 """
@@ -63,7 +63,7 @@ def main():
                         lambda: x @ w.t(), 2.0 * M * N * K),
                 "dgrad": (lambda: C.gemm(g, True, w, False, None, False, None, 0, None, False, 1.0, 1),
                           lambda: g @ w, 2.0 * M * N * K),
-                "wgrad": (lambda: C.gemm(g, False, x, False, dw, True, None, 0, None, False, 1.0, 1),
+                "wgrad": (lambda: C.gemm(g, False, x, False, dw, True, None, 0, None, False, 1.0, 0),
                           lambda: g.t() @ x, 2.0 * M * N * K),
             }
             for form, (ours, blas, flop) in forms.items():

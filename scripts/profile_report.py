@@ -1,6 +1,11 @@
 """Markdown summary of a rocprofv3 kernel_stats.csv (+ optional per-layer roofline JSONL) for profiles/.
 
     python scripts/profile_report.py STATS.csv --steps 6 [--roofline roofline.jsonl] [--title ...] > profiles/x.md
+    python scripts/profile_report.py TRACE_kernel_trace.csv --step-marker adam_kernel ...   (steady state only)
+
+With ``--step-marker`` the input is a kernel TRACE and only the dispatches between the first and the last
+dispatch matching the marker (one optimizer launch per step) are counted: start-up work (weight init fills,
+first-step copies) stays out of the per-step numbers.
 
 Kernels are grouped into categories (BatchNorm, conv/GEMM forward+dgrad, weight gradient, pooling, optimizer,
 vendor/ATen) so the step-time split is visible at a glance; ``k8s_amd::`` share = GPU time in our kernels.
@@ -29,15 +34,36 @@ def categorize(name):
     return "other k8s_amd"
 
 
+def steady_rows(trace, marker):
+    """kernel_stats-shaped rows from the dispatches between the first and last step-marker dispatch."""
+    disp = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
+    idx = [i for i, r in enumerate(disp) if re.search(marker, r["Kernel_Name"])]
+    if len(idx) < 2:
+        raise SystemExit("need >= 2 dispatches matching %r (found %d)" % (marker, len(idx)))
+    agg = {}
+    for r in disp[idx[0] + 1:idx[-1] + 1]:
+        d = agg.setdefault(r["Kernel_Name"], [0, 0.0])
+        d[0] += 1
+        d[1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    rows = [{"Name": n, "Calls": c, "TotalDurationNs": t, "AverageNs": t / c} for n, (c, t) in agg.items()]
+    return rows, float(len(idx) - 1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("stats")
-    ap.add_argument("--steps", type=float, required=True, help="profiled steps (warmup + timed) in the trace")
+    ap.add_argument("--steps", type=float, help="profiled steps (warmup + timed) in the trace")
+    ap.add_argument("--step-marker", help="regex of the one-per-step kernel; input is then a kernel_trace.csv")
     ap.add_argument("--roofline")
     ap.add_argument("--title", default="Kernel profile")
     ap.add_argument("--top", type=int, default=20)
     a = ap.parse_args()
-    rows = list(csv.DictReader(open(a.stats)))
+    if a.step_marker:
+        rows, a.steps = steady_rows(a.stats, a.step_marker)
+    else:
+        if a.steps is None:
+            ap.error("--steps is required with a kernel_stats.csv")
+        rows = list(csv.DictReader(open(a.stats)))
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     ours = sum(float(r["TotalDurationNs"]) for r in rows if r["Name"].startswith(("void k8s_amd::", "k8s_amd::")))
     print("# %s\n" % a.title)

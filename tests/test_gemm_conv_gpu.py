@@ -178,7 +178,7 @@ def test_elementwise_kernels(cuda):
 
 
 @pytest.mark.parametrize("shape,ksp", [((2, 112, 112, 64), (3, 2, 1)), ((3, 9, 7, 16), (3, 2, 1)),
-                                       ((2, 8, 8, 8), (2, 2, 0))])
+                                       ((2, 8, 8, 8), (2, 2, 0)), ((2, 10, 10, 8), (3, 1, 1))])
 def test_maxpool_nhwc(cuda, shape, ksp):
     from k8s_amd.ops import nn as K
 

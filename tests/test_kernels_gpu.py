@@ -160,13 +160,18 @@ def test_fused_adam(cuda, decoupled):
     _close(m2, B, 1e-6)
 
 
-def test_grad_clip(cuda):
-    g = torch.randn(64 * 100, device=cuda)
+@pytest.mark.parametrize("n", [64 * 100, 64 * (1 << 18) + 192])  # tail-only; 4-vector trips + tail
+def test_grad_clip(cuda, n):
+    g = torch.randn(n, device=cuda)
     st = _C().grad_sumsq(g)
     _close(st, ref.grad_sumsq(g), 1e-4)
     f = _C().clip_factor(st, 1.0)
     norm = g.norm().item()
     assert abs(f.item() - min(1.0, 1.0 / (norm + 1e-6))) < 1e-5
+    g[n // 3] = float("inf")
+    st = _C().grad_sumsq(g)
+    assert _C().clip_factor(st, 1.0).item() == 0.0
+    g[n // 3] = 0.0
     g[5] = float("nan")
     st = _C().grad_sumsq(g)
     assert _C().clip_factor(st, 1.0).item() == 0.0
