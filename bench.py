@@ -59,7 +59,7 @@ def main(argv=None):
     n = info.world_size
     if n != a.gpus and info.rank == 0:
         print("warning: --gpus %d but world size %d" % (a.gpus, n), file=sys.stderr)
-    dev = torch.device("cuda", info.local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    dev = torch.device("cuda", info.device_index) if torch.cuda.is_available() else torch.device("cpu")
     torch.manual_seed(1234 + info.rank)
 
     store = ParamStore()

@@ -37,6 +37,15 @@ class RankInfo:
     role_index: int = 0
     compute_world: int = 1  # ranks that run the model (everything but ps)
 
+    @property
+    def device_index(self) -> int:
+        """The GPU this rank drives: its local rank. ``K8S_AMD_GPU_OVERSUBSCRIBE=1`` wraps it modulo the visible
+        devices, so several ranks can share one GPU for a rehearsal of the multi-rank path on a 1-GPU box
+        (with ``K8S_AMD_DIST_BACKEND=gloo``: RCCL refuses two ranks on one device)."""
+        if os.environ.get("K8S_AMD_GPU_OVERSUBSCRIBE") == "1" and torch.cuda.is_available():
+            return self.local_rank % max(1, torch.cuda.device_count())
+        return self.local_rank
+
 
 def resolve(addr: str) -> str:
     """Map a TF_CONFIG "service:port" through $K8S_AMD_SERVICE_MAP (local kubelet's cluster-DNS stand-in)."""
@@ -109,18 +118,19 @@ def rank_from_env() -> Optional[RankInfo]:
 
 def init_process_group(info: Optional[RankInfo] = None, backend: Optional[str] = None,
                        timeout_s: float = 600.0) -> RankInfo:
-    """Initialise torch.distributed (nccl == RCCL on ROCm, gloo on CPU). Idempotent."""
+    """Initialise torch.distributed (nccl == RCCL on ROCm, gloo on CPU; ``K8S_AMD_DIST_BACKEND`` overrides the
+    default). Idempotent."""
     info = info or rank_from_env() or RankInfo(0, 1, 0, "127.0.0.1", 29500)
     if info.world_size > 1 and not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
-            torch.cuda.set_device(info.local_rank)
+            backend = os.environ.get("K8S_AMD_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        if torch.cuda.is_available():
+            torch.cuda.set_device(info.device_index)
         dist.init_process_group(backend=backend, init_method="tcp://%s:%d" % (info.master_addr, info.master_port),
                                 rank=info.rank, world_size=info.world_size,
                                 timeout=datetime.timedelta(seconds=timeout_s))
     elif torch.cuda.is_available():
-        torch.cuda.set_device(info.local_rank)
+        torch.cuda.set_device(info.device_index)
     return info
 
 

@@ -236,7 +236,7 @@ def train(a) -> int:
         raise RetryableError("process group init failed: %s" % e) from e
     rank, world = max(info.rank, 0), info.world_size
     chief = rank == 0
-    dev = torch.device("cuda", info.local_rank) if use_cuda else torch.device("cpu")
+    dev = torch.device("cuda", info.device_index) if use_cuda else torch.device("cpu")
     torch.manual_seed(a.seed + rank)
     if chief:
         _wait_for_ps(tf_config)

@@ -51,7 +51,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default=None)
-    ap.add_argument("--variants", nargs="*", default=[], help="extra ENV=VALUE[,ENV=VALUE] arms, e.g. K8S_AMD_GEMM256_KERNEL=quad,K8S_AMD_GEMM256_QVAR=1")
+    ap.add_argument("--variants", nargs="*", default=[], help="extra ENV=VALUE[,ENV=VALUE] arms, e.g. K8S_AMD_GEMM256=0 (force the 128 x 128 kernel)")
     a = ap.parse_args()
     groups = [a.only] if a.only else list(LAYERS)
     for grp in groups:

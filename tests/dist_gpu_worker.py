@@ -1,0 +1,51 @@
+"""Worker for tests/test_dist_gpu.py (not collected): DP training of resnet_tiny on the GPU kernels with the
+bucketed GradReducer, then every rank's fp32 master weights and momentum are compared with rank 0's."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from k8s_amd.models.resnet import resnet_tiny  # noqa: E402
+from k8s_amd.ops import nn as K  # noqa: E402
+from k8s_amd.ops.optim import FusedSGD  # noqa: E402
+from k8s_amd.parallel import dist as kdist  # noqa: E402
+from k8s_amd.parallel.ddp import GradReducer  # noqa: E402
+from k8s_amd.parallel.flat import ParamStore  # noqa: E402
+
+
+def main():
+    info = kdist.init_process_group()
+    gpu = torch.cuda.is_available()
+    dev = torch.device("cuda", info.device_index) if gpu else torch.device("cpu")  # CPU: a dry run of this script
+    store = ParamStore()
+    model = resnet_tiny(store).finalize(dev)
+    torch.distributed.broadcast(store.master, 0)
+    store.refresh_lowp()
+    red = GradReducer(store, bucket_mb=0.01)  # many buckets: every hook / overlap path runs
+    opt = FusedSGD(store, lr=0.05, momentum=0.9, weight_decay=1e-4)
+    g = torch.Generator(device="cpu").manual_seed(100 + info.rank)  # different data per rank
+    for _ in range(3):
+        x = torch.randn(8, 32, 32, 3, generator=g).to(dev, torch.bfloat16 if gpu else torch.float32)
+        y = torch.randint(0, 10, (8,), generator=g).to(dev)
+        red.begin_step()
+        loss = K.cross_entropy(model(model.prepare_input(x).contiguous()), y)
+        loss.backward()
+        red.finish()
+        opt.step(grad_scale=red.grad_scale)
+    if gpu:
+        torch.cuda.synchronize()
+    state = torch.cat([store.master, opt.mom if hasattr(opt, "mom") else store.master]).cpu()
+    ref = state.clone()
+    torch.distributed.broadcast(ref, 0)
+    same = torch.tensor([int(torch.equal(state, ref))])
+    torch.distributed.all_reduce(same, op=torch.distributed.ReduceOp.MIN)
+    if info.rank == 0:
+        print("{\"replicas_identical\": %d, \"world\": %d, \"loss\": %.5f}" % (int(same), info.world_size,
+                                                                              float(loss.detach())), flush=True)
+    kdist.destroy()
+
+
+if __name__ == "__main__":
+    main()
