@@ -34,7 +34,10 @@ elements, so a bucket's push starts as soon as every parameter overlapping it
 has deposited -- overlapped with the rest of backward like ``GradReducer``.
 
 PS replicas of a TfJob (``--job_name ps``) run the default PS server
-(rendezvous / liveness / shutdown; ``ps_server/``).
+(rendezvous / liveness / shutdown; ``ps_server/``) and are the variable store
+of record: the chief pushes versioned snapshots of the weights, optimizer
+state and buffers to them, sharded over the PS tasks, and a restarted job
+resumes from the newest committed snapshot (``parallel/ps_vars.py``).
 """
 from __future__ import annotations
 

@@ -17,7 +17,14 @@ server that:
 * holds parameter shards for CPU-side push/pull (``put``/``get``/``add``
   ops on named fp32 tensors) -- the GPU data plane uses RCCL instead
   (``k8s_amd.parallel.ps``), this keeps the TF PS protocol shape for
-  small/CPU jobs and tests.
+  small/CPU jobs and tests, and
+* is the trainer's VARIABLE STORE OF RECORD (``k8s_amd.parallel.ps_vars``):
+  ``vput`` / ``vcommit`` / ``vinfo`` / ``vget`` move raw fp32 shards of the
+  flat master weights, optimizer state and buffers (binary payload after a
+  JSON header, no re-encoding). The chief pushes a versioned snapshot every
+  ``--ps-sync-every`` steps; a restarted job pulls the newest committed
+  snapshot from the PS tasks, as TF workers re-read their variables from
+  ``/job:ps`` (workers stay stateless).
 
 The process blocks serving until it receives a ``shutdown`` message or
 SIGTERM (exit 0), mirroring ``server.join()``.
@@ -35,6 +42,7 @@ import socketserver
 import struct
 import sys
 import threading
+from typing import Optional
 
 
 def parse_cluster_spec(cluster_spec: str, job_name: str = "", task_id: int = 0):
@@ -108,11 +116,39 @@ def recv_msg(sock):
     return json.loads(buf)
 
 
-def call(addr: str, obj, timeout: float = 30.0):
+def recv_exact(sock, n: int) -> Optional[bytearray]:
+    """n raw bytes (a variable shard payload) or None if the peer closed first."""
+    buf = bytearray(n)
+    view, got = memoryview(buf), 0
+    while got < n:
+        k = sock.recv_into(view[got:], min(8 << 20, n - got))
+        if not k:
+            return None
+        got += k
+    return buf
+
+
+def send_blob(sock, hdr: dict, payload) -> None:
+    """JSON header carrying ``nbytes`` followed by the raw payload (bytes / memoryview), no re-encoding."""
+    mv = memoryview(payload).cast("B")
+    send_msg(sock, dict(hdr, nbytes=mv.nbytes))
+    sock.sendall(mv)
+
+
+def call(addr: str, obj, timeout: float = 30.0, payload=None, want_payload: bool = False):
+    """One request/response round trip. ``payload``: raw bytes sent after the header; ``want_payload``: returns
+    (reply header, raw bytes) for replies that carry ``nbytes``."""
     host, port = resolve(addr).rsplit(":", 1)
     with socket.create_connection((host, int(port)), timeout=timeout) as s:
-        send_msg(s, obj)
-        return recv_msg(s)
+        if payload is not None:
+            send_blob(s, obj, payload)
+        else:
+            send_msg(s, obj)
+        rep = recv_msg(s)
+        if not want_payload:
+            return rep
+        data = recv_exact(s, int(rep.get("nbytes", 0))) if rep is not None and rep.get("nbytes") else None
+        return rep, data
 
 
 def _device():
@@ -133,6 +169,10 @@ class TaskServer(socketserver.ThreadingTCPServer):
     def __init__(self, addr, job, task, verbose=False):
         self.job, self.task, self.verbose = job, task, verbose
         self.params = {}
+        # variable store of record (parallel/ps_vars.py): (name, lo) -> [version, raw little-endian fp32 bytes];
+        # `committed` is the newest version whose every shard on this task has landed (readers pull only that)
+        self.shards = {}
+        self.committed = -1
         self.lock = threading.Lock()
         super().__init__(addr, _TaskHandler)
 
@@ -174,6 +214,34 @@ class _TaskHandler(socketserver.BaseRequestHandler):
                 with srv.lock:
                     v = srv.params.get(msg["name"])
                 send_msg(self.request, {"ok": v is not None, "value": v})
+            elif op == "vput":  # one variable shard (raw fp32 payload) for snapshot `version`
+                data = recv_exact(self.request, int(msg["nbytes"]))
+                if data is None:
+                    return
+                with srv.lock:
+                    srv.shards[(msg["name"], int(msg["lo"]))] = [int(msg["version"]), data]
+                send_msg(self.request, {"ok": True})
+            elif op == "vcommit":  # every shard of `version` has been put: make it the readable snapshot
+                v = int(msg["version"])
+                with srv.lock:
+                    names = msg.get("names")
+                    ok = all(srv.shards.get((n, int(lo)), [None])[0] == v for n, lo in names) if names else True
+                    if ok:
+                        srv.committed = max(srv.committed, v)
+                        srv.meta = msg.get("meta", {})
+                send_msg(self.request, {"ok": ok, "committed": srv.committed})
+            elif op == "vinfo":
+                with srv.lock:
+                    send_msg(self.request, {"ok": True, "committed": srv.committed,
+                                            "meta": getattr(srv, "meta", {}),
+                                            "shards": sorted([n, lo] for n, lo in srv.shards)})
+            elif op == "vget":
+                with srv.lock:
+                    ent = srv.shards.get((msg["name"], int(msg["lo"])))
+                if ent is None:
+                    send_msg(self.request, {"ok": False, "error": "no shard %s@%s" % (msg["name"], msg["lo"])})
+                else:
+                    send_blob(self.request, {"ok": True, "version": ent[0]}, ent[1])
             elif op == "ping":
                 send_msg(self.request, {"ok": True, "task": "/job:%s/task:%d" % (srv.job, srv.task)})
             elif op == "shutdown":

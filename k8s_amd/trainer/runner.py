@@ -71,6 +71,10 @@ def parse(argv=None):
     ap.add_argument("--logdir", default=os.environ.get("K8S_AMD_LOGDIR", ""))
     ap.add_argument("--ckpt-dir", default=os.environ.get("K8S_AMD_CKPT_DIR", ""))
     ap.add_argument("--ckpt-every", type=int, default=0)
+    ap.add_argument("--ps-sync-every", type=int, default=-1,
+                    help="push a variable snapshot to the TfJob's PS tasks every N steps (the PS tasks are the "
+                         "variable store of record; a restarted job resumes from them). -1: 100 when TF_CONFIG "
+                         "has PS tasks, 0: never")
     ap.add_argument("--log-every", type=int, default=10)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--fresh-batches", action="store_true", help="draw a new synthetic batch every step")
@@ -166,18 +170,29 @@ def _run_ps(info, tf_config: str) -> int:
     return serve(cluster, "ps", info.role_index)
 
 
-def _restore(a, w, opt, dev, chief: bool, world: int, metrics) -> int:
-    """Resume from the chief's latest checkpoint; returns the first step to run (0 without one)."""
+def _restore(a, w, opt, dev, chief: bool, world: int, metrics, psv=None) -> int:
+    """Resume from the newest of: the chief's latest checkpoint, the PS tasks' latest committed variable snapshot
+    (``parallel/ps_vars.py``); returns the first step to run (0 without either)."""
     from k8s_amd.utils import checkpoint as ckpt
 
-    meta_t = torch.tensor([-1, 0], dtype=torch.int64)  # [checkpoint step or -1, optimizer step]
-    tensors = {}
-    base = None
+    meta_t = torch.tensor([-1, 0], dtype=torch.int64)  # [restored step or -1, optimizer step]
+    tensors, flat = {}, None
+    base = source = None
     if chief and a.ckpt_dir:
         base = ckpt.latest_checkpoint(a.ckpt_dir)
         if base:
             step0, tensors, meta = ckpt.load(base)
             meta_t[0], meta_t[1] = step0, int(meta.get("optim_step", step0 + 1))
+            source = "checkpoint"
+    if chief and psv is not None:
+        try:
+            v, meta = psv.latest()
+            if v > int(meta_t[0]) and meta.get("total") == w.store.total:
+                flat = psv.pull(v)
+                meta_t[0], meta_t[1] = v, int(meta.get("optim_step", v + 1))
+                source = "ps"
+        except OSError as e:  # PS unreachable: fall back to the checkpoint
+            metrics.event(event="warning", message="PS variable snapshot unavailable: %s" % e)
     if world > 1:
         mt = meta_t.to(dev)
         torch.distributed.broadcast(mt, 0)
@@ -190,25 +205,35 @@ def _restore(a, w, opt, dev, chief: bool, world: int, metrics) -> int:
         if world > 1:
             torch.distributed.broadcast(t, 0)
 
-    params = {k[len("params/"):]: v for k, v in tensors.items() if k.startswith("params/")}
-    if chief:
-        w.store.load_state_dict(params)
+    if chief and flat is not None:
+        w.store.master.copy_(flat["params"].to(w.store.master.device))
+    elif chief:
+        w.store.load_state_dict({k[len("params/"):]: v for k, v in tensors.items() if k.startswith("params/")})
     bcast(w.store.master)
     w.store.refresh_lowp()
     for name, buf in w.model.named_buffers():
-        if chief and ("buffers/" + name) in tensors:
-            buf.copy_(tensors["buffers/" + name])
+        key = "buffers/" + name
+        if chief and flat is not None and key in flat:
+            buf.copy_(flat[key].view(buf.shape))
+        elif chief and key in tensors:
+            buf.copy_(tensors[key])
         bcast(buf)
     osd = {"step": int(meta_t[1])}
     for attr, key in opt.STATE.items():
         full = torch.zeros(w.store.total, dtype=torch.float32, device=dev)
-        if chief and ("optim/" + key) in tensors:
-            src = tensors["optim/" + key].reshape(-1)
+        src = None
+        if chief and flat is not None:
+            src = flat.get("optim/" + key)
+        elif chief:
+            src = tensors.get("optim/" + key)
+        if src is not None:
+            src = src.reshape(-1)
             full[:src.numel()].copy_(src)
         bcast(full)
         osd[key] = full
     opt.load_state_dict(osd)
-    metrics.event(event="restored", checkpoint=os.path.basename(base) if base else None, step=step0)
+    metrics.event(event="restored", source=source if chief else None,
+                  checkpoint=os.path.basename(base) if (base and source == "checkpoint") else None, step=step0)
     return step0 + 1
 
 
@@ -276,7 +301,14 @@ def train(a) -> int:
 
     # ---- restore: only the chief reads the checkpoint (--ckpt-dir may be pod-local), then every tensor and the
     # start step are broadcast from it, so all ranks resume at the same step with identical weights and state
-    start_step = _restore(a, w, opt, dev, chief, world, metrics)
+    ps_addrs = json.loads(tf_config).get("cluster", {}).get("ps", []) if tf_config else []
+    sync_every = a.ps_sync_every if a.ps_sync_every >= 0 else (100 if ps_addrs else 0)
+    psv = None
+    if chief and ps_addrs and sync_every > 0:
+        from k8s_amd.parallel.ps_vars import PsVariables
+
+        psv = PsVariables(ps_addrs)
+    start_step = _restore(a, w, opt, dev, chief, world, metrics, psv)
 
     def save(step):
         full = svc.full_optimizer_state() if svc is not None else None  # collective: every rank takes part
@@ -290,6 +322,18 @@ def train(a) -> int:
         base = ckpt.save(a.ckpt_dir, step, tensors, meta={"model": a.model, "optim_step": opt.step_count,
                                                           "world": world})
         metrics.event(event="checkpoint", step=step, path=base)
+
+    def ps_push(step):
+        """Variable snapshot to the PS tasks (collective for the sharded optimizer state, like save())."""
+        full = svc.full_optimizer_state() if svc is not None else None
+        if psv is None:
+            return
+        snap = {"params": w.store.master}
+        snap.update({"buffers/" + k: v for k, v in w.model.named_buffers()})
+        for k, v in opt.state_dict(full).items():
+            if torch.is_tensor(v):
+                snap["optim/" + k] = v
+        psv.push(step, snap, meta={"optim_step": opt.step_count, "total": w.store.total, "model": a.model})
 
     sync = torch.cuda.synchronize if use_cuda else (lambda: None)
     tracer = Tracer(enabled=a.trace not in ("", "0"), sync=(a.trace == "sync"), sync_fn=sync)
@@ -315,59 +359,72 @@ def train(a) -> int:
                       "and no kernel debug mode")
     t_last, n_last = time.time(), 0
     loss_v = float("nan")
-    for step in range(start_step, a.steps):
-        if step == a.fail_at_step and a.ckpt_dir:
-            marker = os.path.join(a.ckpt_dir, ".injected_failure.%d" % rank)
-            if not os.path.exists(marker):
-                os.makedirs(a.ckpt_dir, exist_ok=True)
-                open(marker, "w").close()
-                raise RetryableError("injected failure at step %d" % step)
-        if step == a.hang_at_step:
-            time.sleep(1e9)  # (testing) a stalled collective
-        cur_lr = lr * min(1.0, (step + 1) / a.warmup_steps) if a.warmup_steps else lr
-        if graph is not None:
-            loss = graph(w.batch(step), cur_lr)
-        else:
-            with tracer.phase("step"):
-                begin()
-                with tracer.phase("data"):
-                    inputs = w.batch(step)
-                with tracer.phase("forward"):
-                    loss = w.loss(inputs)
-                with tracer.phase("backward"):
-                    loss.backward()
-                with tracer.phase("reduce+update"):
-                    finish(cur_lr)
-        n_last += 1
-        if watchdog is not None:
-            if step == start_step:
-                watchdog.start()
-            watchdog.kick()
-        if step == start_step or (step + 1) % a.log_every == 0 or step + 1 == a.steps:
-            loss_v = float(loss.detach().float().item())
-            bad = not (loss_v == loss_v and abs(loss_v) != float("inf"))
-            if world > 1:  # decided together: a rank that exits alone would leave its peers in a collective
-                flag = torch.tensor([1.0 if bad else 0.0], device=dev)
-                torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MAX)
-                bad = bool(flag.item() > 0)
-            if bad:
-                metrics.event(event="error", step=step, error="non-finite loss")
-                return EXIT_PERMANENT
-            sync()
-            now = time.time()
-            rate = n_last * w.units_per_step * world / max(now - t_last, 1e-9)
-            if step == start_step:
-                metrics.event(event="step0", step=step, loss=loss_v, since_start=now - t_start)
+    try:
+        for step in range(start_step, a.steps):
+            if step == a.fail_at_step and a.ckpt_dir:
+                marker = os.path.join(a.ckpt_dir, ".injected_failure.%d" % rank)
+                if not os.path.exists(marker):
+                    os.makedirs(a.ckpt_dir, exist_ok=True)
+                    open(marker, "w").close()
+                    raise RetryableError("injected failure at step %d" % step)
+            if step == a.hang_at_step:
+                time.sleep(1e9)  # (testing) a stalled collective
+            cur_lr = lr * min(1.0, (step + 1) / a.warmup_steps) if a.warmup_steps else lr
+            if graph is not None:
+                loss = graph(w.batch(step), cur_lr)
             else:
-                extra = {"phase_ms": tracer.summary_ms()} if tracer.sync else {}
-                metrics.event(event="step", step=step, loss=loss_v, lr=cur_lr,
-                              **{"%s_per_sec" % w.unit: round(rate, 2)}, **extra)
-                metrics.scalars(step, {"loss": loss_v, "%s_per_sec" % w.unit: rate, "learning_rate": cur_lr})
-            t_last, n_last = now, 0
-        if a.ckpt_dir and a.ckpt_every and (step + 1) % a.ckpt_every == 0 and step + 1 < a.steps:
-            save(step)
+                with tracer.phase("step"):
+                    begin()
+                    with tracer.phase("data"):
+                        inputs = w.batch(step)
+                    with tracer.phase("forward"):
+                        loss = w.loss(inputs)
+                    with tracer.phase("backward"):
+                        loss.backward()
+                    with tracer.phase("reduce+update"):
+                        finish(cur_lr)
+            n_last += 1
+            if watchdog is not None:
+                if step == start_step:
+                    watchdog.start()
+                watchdog.kick()
+            if step == start_step or (step + 1) % a.log_every == 0 or step + 1 == a.steps:
+                loss_v = float(loss.detach().float().item())
+                bad = not (loss_v == loss_v and abs(loss_v) != float("inf"))
+                if world > 1:  # decided together: a rank that exits alone would leave its peers in a collective
+                    flag = torch.tensor([1.0 if bad else 0.0], device=dev)
+                    torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MAX)
+                    bad = bool(flag.item() > 0)
+                if bad:
+                    metrics.event(event="error", step=step, error="non-finite loss")
+                    return EXIT_PERMANENT
+                sync()
+                now = time.time()
+                rate = n_last * w.units_per_step * world / max(now - t_last, 1e-9)
+                if step == start_step:
+                    metrics.event(event="step0", step=step, loss=loss_v, since_start=now - t_start)
+                else:
+                    extra = {"phase_ms": tracer.summary_ms()} if tracer.sync else {}
+                    metrics.event(event="step", step=step, loss=loss_v, lr=cur_lr,
+                                  **{"%s_per_sec" % w.unit: round(rate, 2)}, **extra)
+                    metrics.scalars(step, {"loss": loss_v, "%s_per_sec" % w.unit: rate, "learning_rate": cur_lr})
+                t_last, n_last = now, 0
+            if a.ckpt_dir and a.ckpt_every and (step + 1) % a.ckpt_every == 0 and step + 1 < a.steps:
+                save(step)
+            if sync_every and ps_addrs and ((step + 1) % sync_every == 0 or step + 1 == a.steps):
+                ps_push(step)
+    except RetryableError:
+        if psv is not None:  # let the last snapshot reach the PS tasks: the restarted job resumes from it
+            try:
+                psv.wait()
+            except Exception:  # noqa: BLE001 -- the original failure is what gets reported
+                pass
+        raise
     if a.ckpt_dir and a.steps > start_step:
         save(a.steps - 1)
+    if psv is not None:
+        psv.wait()  # the last snapshot is committed before the PS tasks are told to stop
+        metrics.event(event="ps_snapshot", step=psv.pushed)
     if watchdog is not None:
         watchdog.stop()
     kdist.barrier()

@@ -150,3 +150,75 @@ def test_service_resolution_follows_the_live_map_file(tmp_path, monkeypatch):
     f.write_text(json.dumps({"a-master-x-0": "127.0.0.1:1000", "a-ps-x-0": "127.0.0.1:1002"}))
     assert srv.resolve("a-ps-x-0:2222") == "127.0.0.1:1002"
     assert dist.resolve("a-ps-x-0:2222") == "127.0.0.1:1002"
+
+
+def test_ps_tasks_hold_the_variables_and_a_restarted_job_resumes_from_them(tmp_path):
+    """1 MASTER + 1 WORKER + 2 PS: the chief pushes a versioned snapshot (weights, Adam state, BN buffers) to the
+    PS tasks every 2 steps, sharded over them; both compute ranks then fail (retryable) at step 4 with NO
+    checkpoint on disk, and the restarted ranks resume from the PS tasks' committed snapshot (step 3) -- the TF
+    PS semantics (variables live on /job:ps, workers are stateless). The result equals an uninterrupted run."""
+    from k8s_amd.ps_server.grpc_tensorflow_server import call
+
+    pm, pw, p0, p1, rm, rw = _distinct_ports(6)
+    cluster = {"master": ["127.0.0.1:%d" % pm], "worker": ["127.0.0.1:%d" % pw],
+               "ps": ["127.0.0.1:%d" % p0, "127.0.0.1:%d" % p1]}
+    run = str(tmp_path / "run")
+    common = ["--model", "resnet_tiny", "--steps", "6", "--ckpt-dir", run, "--log-every", "1", "--optimizer",
+              "adam", "--lr", "0.01", "--ps-sync-every", "2"]
+
+    def tfc(role, i, cl=cluster):
+        return {"cluster": cl, "task": {"type": role, "index": i}, "environment": "cloud"}
+
+    ps = [_trainer(common, tfc("ps", 0)), _trainer(common, tfc("ps", 1))]
+    try:
+        first = [_trainer(common + ["--fail-at-step", "4"], tfc("master", 0)),
+                 _trainer(common + ["--fail-at-step", "4"], tfc("worker", 0))]
+        for p in first:
+            out, _ = p.communicate(timeout=300)
+            assert p.returncode >= 128, out
+        assert ckpt.latest_checkpoint(run) is None  # nothing on disk: only the PS tasks hold the state
+        for addr in cluster["ps"]:
+            info = call(addr, {"op": "vinfo"})
+            assert info["committed"] == 3, info
+            assert {n for n, _ in info["shards"]} >= {"params", "optim/exp_avg", "optim/exp_avg_sq"}
+        again = [_trainer(common + ["--fail-at-step", "4"], tfc("master", 0)),
+                 _trainer(common + ["--fail-at-step", "4"], tfc("worker", 0))]  # markers: no second failure
+        outs = []
+        for p in again:
+            out, _ = p.communicate(timeout=300)
+            outs.append(out)
+            assert p.returncode == 0, out
+        ev = _events(outs[0])
+        restored = [e for e in ev if e["event"] == "restored"]
+        assert restored and restored[0]["source"] == "ps" and restored[0]["step"] == 3, restored
+        assert [e for e in ev if e["event"] == "step0"][0]["step"] == 4
+        for p in ps:  # the master shuts the PS tasks down after its last snapshot
+            out, _ = p.communicate(timeout=120)
+            assert p.returncode == 0, out
+    finally:
+        for p in ps:
+            if p.poll() is None:
+                p.kill()
+    # an uninterrupted 2-rank run reaches the same weights and optimizer state
+    ref_cluster = {"master": ["127.0.0.1:%d" % rm], "worker": ["127.0.0.1:%d" % rw]}
+    ref = str(tmp_path / "ref")
+    rargs = [a if a != run else ref for a in common]
+    procs = [_trainer(rargs, tfc("master", 0, ref_cluster)), _trainer(rargs, tfc("worker", 0, ref_cluster))]
+    for p in procs:
+        out, _ = p.communicate(timeout=300)
+        assert p.returncode == 0, out
+    _, a, _ = ckpt.load(ckpt.latest_checkpoint(ref))
+    _, b, _ = ckpt.load(ckpt.latest_checkpoint(run))
+    for k in a:
+        if k.startswith(("params/", "optim/", "buffers/")):
+            torch.testing.assert_close(a[k], b[k], rtol=1e-5, atol=1e-6, msg=k)
+
+
+def test_ps_shard_ranges_cover_and_align():
+    from k8s_amd.parallel.ps_vars import shard_ranges
+
+    for n, parts in [(1000, 3), (64, 4), (5, 2), (4096 * 7 + 3, 5)]:
+        r = shard_ranges(n, parts)
+        assert len(r) == parts and r[0][0] == 0 and r[-1][1] == n
+        assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+        assert all(lo % 64 == 0 for lo, _ in r if lo < n)
