@@ -550,12 +550,21 @@ Tensor relu_bwd(Tensor dy, Tensor y) {
   k8s_amd::launch_relu_bwd(cbf(dy), cbf(y), bf(dx), dy.numel(), cur_stream());
   return dx;
 }
-Tensor colsum(Tensor x) {
+// column sums of a [R, C] bf16 matrix in fp32; `out` (optional, fp32 [C] contiguous, e.g. a bias's flat gradient
+// slot) is written in place instead of a new tensor
+Tensor colsum(Tensor x, c10::optional<Tensor> out_) {
   check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x");
   const int C = (int)x.size(-1);
   TORCH_CHECK(C % 8 == 0);
   const long R = x.numel() / C;
-  auto out = torch::empty({C}, x.options().dtype(at::kFloat));
+  Tensor out;
+  if (out_) {
+    out = *out_;
+    TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() == C,
+                "colsum out: contiguous fp32 [C]");
+  } else {
+    out = torch::empty({C}, x.options().dtype(at::kFloat));
+  }
   auto work = torch::empty({k8s_amd::colsum_workspace_floats(R, C)}, out.options());
   k8s_amd::launch_colsum(cbf(x), R, C, f32(work), f32(out), false, cur_stream());
   return out;
@@ -807,7 +816,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_", &rope_);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("relu_bwd", &relu_bwd);
-  m.def("colsum", &colsum);
+  m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none());
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
         py::arg("out_f32"), py::arg("bias"), py::arg("act"), py::arg("stats"), py::arg("bnb") = py::none(),
         py::arg("bnb_relu_x") = py::none());

@@ -71,13 +71,16 @@ class BertLayer(nn.Module):
         c = self.c
         h, nh = c.hidden, c.heads
         d = h // nh
-        qkv = K.linear(x, self.qkv_w, self.qkv_b)  # [T, 3h]
+        # x is read by the QKV GEMM and, as the residual, by LN1 (likewise LN1's output by FFN1 and LN2): each
+        # GradLink sums the two gradient contributions in the GEMM's dgrad epilogue instead of a separate add
+        l1, l2 = K.GradLink(), K.GradLink()
+        qkv = K.linear(x, self.qkv_w, self.qkv_b, grad_link=l1)  # [T, 3h]
         o = attention_qkv(qkv, B, S, nh, nh, d, causal=False, kv_lens=kv_lens)  # packed QKV gradient in place
         a = K.linear(o.reshape(B * S, h), self.o_w, self.o_b)
-        x, _ = K.layer_norm(a, self.ln1_g, self.ln1_b, c.eps, residual=x)
-        f = K.linear(x, self.f1_w, self.f1_b, act="gelu")
+        x, _ = K.layer_norm(a, self.ln1_g, self.ln1_b, c.eps, residual=x, res_link=l1)
+        f = K.linear(x, self.f1_w, self.f1_b, act="gelu", grad_link=l2)
         f = K.linear(f, self.f2_w, self.f2_b)
-        x, _ = K.layer_norm(f, self.ln2_g, self.ln2_b, c.eps, residual=x)
+        x, _ = K.layer_norm(f, self.ln2_g, self.ln2_b, c.eps, residual=x, res_link=l2)
         return x
 
 

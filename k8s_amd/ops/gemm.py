@@ -100,9 +100,12 @@ def linear_fwd(x, w, b, act=None):
     return y, (pre if act == "gelu" else (y if act == "relu" else None))
 
 
-def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True):
+def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True, dx_addend=None, pb=None):
     """dx and the parameter gradient. With (pw, store) on GPU the weight gradient is written
-    (or accumulated) straight into the flat fp32 gradient slot; returns (dx, dw_or_None, db)."""
+    (or accumulated) straight into the flat fp32 gradient slot; returns (dx, dw_or_None, db).
+    ``dx_addend`` (bf16, x's shape): another gradient contribution of x, accumulated in the dgrad epilogue (it is
+    overwritten and returned as dx). With ``pb`` the bias gradient goes straight into its flat slot on first use
+    (db is then returned as None)."""
     g = _act_bwd(gy, saved, act)
     M, K = x.shape
     N = w.shape[0]
@@ -110,16 +113,24 @@ def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True):
     if not need_db:
         pass
     elif g.is_cuda and g.dtype == torch.bfloat16 and N % 8 == 0:
-        db = _load().colsum(g.contiguous())
+        slot = store.slot_for_write(pb) if (pb is not None and store is not None) else None
+        db = _load().colsum(g.contiguous(), slot)
+        if slot is not None:
+            store.mark_written(pb)
+            db = None
     else:
         db = g.float().sum(0)
     if hip_ok(g, x, w) and _shape_ok(M, N, K):
         g = g.contiguous()
+        acc = dx_addend is not None and dx_addend.is_contiguous() and dx_addend.dtype == torch.bfloat16
         if N % 64:  # dgrad reduces over N: zero-pad it to the kernel's 64-deep k-step (e.g. a 1000-class head)
             Np = (N + 63) // 64 * 64
-            dx = mm(torch.nn.functional.pad(g, (0, Np - N)), torch.nn.functional.pad(w, (0, 0, 0, Np - N)), True, False)
+            dx = mm(torch.nn.functional.pad(g, (0, Np - N)), torch.nn.functional.pad(w, (0, 0, 0, Np - N)), True, False,
+                    out=dx_addend if acc else None, accumulate=acc)
         else:
-            dx = mm(g, w, True, False)
+            dx = mm(g, w, True, False, out=dx_addend if acc else None, accumulate=acc)
+        if dx_addend is not None and not acc:
+            dx = dx + dx_addend
         if pw is not None and store is not None and pw.grad.dtype == torch.float32:
             acc = pw.written
             mm(g, x, False, False, out=pw.grad, out_f32=True, accumulate=acc, splits=0)
@@ -133,5 +144,7 @@ def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True):
     if g.is_cuda:
         _fallback("linear_bwd %dx%dx%d" % (M, N, K))
     dx = torch.matmul(g, w)
+    if dx_addend is not None:
+        dx = dx + dx_addend.reshape(dx.shape).to(dx.dtype)
     dw = torch.matmul(g.t(), x)
     return dx, dw, db

@@ -306,7 +306,9 @@ def batch_norm_act(x, pg, pb, run_mean, run_var, residual=None, relu=True, train
 # =========================================================================== layernorm / rmsnorm
 class _Norm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, anchor, pg, pb, eps, rms):
+    def forward(ctx, x, res, anchor, pg, pb, eps, rms, res_link=None):
+        # an unused second output (x + res) must not get a materialised zero gradient (one [T, D] fill per norm)
+        ctx.set_materialize_grads(False)
         x = x.contiguous()
         if res is not None:
             res = res.contiguous()
@@ -318,6 +320,7 @@ class _Norm(torch.autograd.Function):
         xin = xsum if res is not None else x
         ctx.save_for_backward(xin, mean, rstd)
         ctx.pg, ctx.pb, ctx.rms, ctx.has_res = pg, pb, rms, res is not None
+        ctx.res_link = res_link if res is not None else None
         if res is not None:
             return y, xsum
         return y, None
@@ -327,28 +330,53 @@ class _Norm(torch.autograd.Function):
         xin, mean, rstd = ctx.saved_tensors
         pg, pb = ctx.pg, ctx.pb
         store = pg.store
+        if dy is None:
+            dy = torch.zeros(xin.shape, device=xin.device, dtype=xin.dtype)
         dy = dy.contiguous()
         dres = dxsum.contiguous() if (dxsum is not None and ctx.has_res) else None
         if _gpu(xin):
-            dg = torch.empty(pg.shape, device=xin.device, dtype=torch.float32)
-            db = torch.empty(pb.shape, device=xin.device, dtype=torch.float32) if pb is not None else None
+            # gamma / beta gradients straight into their flat fp32 slots on first use (no temporary + copy)
+            sg = store.slot_for_write(pg)
+            sb = store.slot_for_write(pb) if pb is not None else None
+            dg = sg.view(pg.shape) if sg is not None else torch.empty(pg.shape, device=xin.device,
+                                                                       dtype=torch.float32)
+            db = None
+            if pb is not None:
+                db = sb.view(pb.shape) if sb is not None else torch.empty(pb.shape, device=xin.device,
+                                                                           dtype=torch.float32)
             dx = _C().norm_bwd(dy, xin, pg.master, mean, rstd, dres, dg, db, ctx.rms)
+            store.mark_written(pg) if sg is not None else store.deposit(pg, dg)
+            if pb is not None:
+                store.mark_written(pb) if sb is not None else store.deposit(pb, db)
         else:
             dx, dg, db = ref.norm_bwd(dy, xin, pg.master, mean, rstd, dres, ctx.rms)
-        store.deposit(pg, dg)
-        if pb is not None:
-            store.deposit(pb, db)
-        return dx, (dx if ctx.has_res else None), None, None, None, None, None
+            store.deposit(pg, dg)
+            if pb is not None:
+                store.deposit(pb, db)
+        dres_out = None
+        if ctx.has_res:
+            dres_out = dx
+            link = ctx.res_link
+            if link is not None:
+                if link.grad is None:  # the residual's other consumer (a linear) runs later: it adds dx in its
+                    link.grad = dx     # dgrad epilogue and returns the sum, so nothing is returned here
+                    dres_out = None
+                else:  # that linear already ran and handed its dgrad over: form the sum here
+                    dres_out = dx + link.grad
+                    link.grad = None
+        return dx, dres_out, None, None, None, None, None, None
 
 
-def layer_norm(x, pg, pb, eps=1e-12, residual=None):
-    """LayerNorm over the last dim; with ``residual`` returns (norm(x+res), x+res)."""
-    y, xsum = _Norm.apply(x, residual, pg.store.anchor, pg, pb, eps, False)
+def layer_norm(x, pg, pb, eps=1e-12, residual=None, res_link=None):
+    """LayerNorm over the last dim; with ``residual`` returns (norm(x+res), x+res). ``res_link`` (a GradLink
+    shared with the linear that also reads ``residual``): the two gradient contributions of ``residual`` are
+    summed in that linear's dgrad epilogue instead of by a separate add."""
+    y, xsum = _Norm.apply(x, residual, pg.store.anchor, pg, pb, eps, False, res_link)
     return (y, xsum) if residual is not None else y
 
 
-def rms_norm(x, pg, eps=1e-5, residual=None):
-    y, xsum = _Norm.apply(x, residual, pg.store.anchor, pg, None, eps, True)
+def rms_norm(x, pg, eps=1e-5, residual=None, res_link=None):
+    y, xsum = _Norm.apply(x, residual, pg.store.anchor, pg, None, eps, True, res_link)
     return (y, xsum) if residual is not None else y
 
 
@@ -361,14 +389,14 @@ def _gemm():
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, anchor, pw, pb, act):
+    def forward(ctx, x, anchor, pw, pb, act, grad_link=None):
         g = _gemm()
         w = pw.weight if x.dtype == pw.weight.dtype else pw.master.to(x.dtype)
         x2 = x.reshape(-1, x.shape[-1])
         b = pb.master if pb is not None else None
         y, pre = g.linear_fwd(x2, w, b, act)
         ctx.save_for_backward(x2, pre)
-        ctx.pw, ctx.pb, ctx.act, ctx.xshape = pw, pb, act, x.shape
+        ctx.pw, ctx.pb, ctx.act, ctx.xshape, ctx.grad_link = pw, pb, act, x.shape, grad_link
         return y.reshape(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -378,17 +406,26 @@ class _Linear(torch.autograd.Function):
         g = _gemm()
         w = pw.weight if x2.dtype == pw.weight.dtype else pw.master.to(x2.dtype)
         gy2 = gy.reshape(-1, gy.shape[-1]).contiguous()
-        dx, dw, db = g.linear_bwd(gy2, x2, w, pre, ctx.act, pw=pw, store=pw.store, need_db=pb is not None)
+        link = ctx.grad_link
+        addend = None
+        if link is not None and link.grad is not None:  # x's other gradient contribution, handed over (GradLink)
+            addend = link.grad.reshape(x2.shape)
+            link.grad = None
+        dx, dw, db = g.linear_bwd(gy2, x2, w, pre, ctx.act, pw=pw, store=pw.store, need_db=pb is not None,
+                                  dx_addend=addend, pb=pb)
         if dw is not None:
             pw.store.deposit(pw, dw)
-        if pb is not None:
+        if pb is not None and db is not None:  # None: written straight into its slot
             pb.store.deposit(pb, db)
-        return dx.reshape(ctx.xshape), None, None, None, None
+        if link is not None and addend is None:  # ran first: hand dx to the norm backward, which forms the sum
+            link.grad = dx.reshape(ctx.xshape)
+            return None, None, None, None, None, None
+        return dx.reshape(ctx.xshape), None, None, None, None, None
 
 
-def linear(x, pw, pb=None, act: Optional[str] = None):
-    """y = act(x @ W^T + b); W [out, in] bf16 from the flat store."""
-    return _Linear.apply(x, pw.store.anchor, pw, pb, act)
+def linear(x, pw, pb=None, act: Optional[str] = None, grad_link=None):
+    """y = act(x @ W^T + b); W [out, in] bf16 from the flat store. ``grad_link``: see ``layer_norm``."""
+    return _Linear.apply(x, pw.store.anchor, pw, pb, act, grad_link)
 
 
 # =========================================================================== embedding
