@@ -124,11 +124,20 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const uint16_t* __r
   if (cg < cv) {
     const long r0 = blockIdx.x * rpb;
     const long r1 = r0 + rpb < R ? r0 + rpb : R;
-    for (long r = r0 + rg; r < r1; r += 8) {
-      float v[8];
-      load8(x + r * C + cg * 8, v);
+    // 4 rows per trip, all loads issued before the adds (clamped address + zero weight past the end: no
+    // per-load branch, which would serialise the loads behind vmcnt(0) waits)
+    for (long r = r0 + rg; r < r1; r += 32) {
+      float v[4][8], wgt[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s[j] += v[j];
+      for (int u = 0; u < 4; ++u) {
+        const long rr = r + 8 * u;
+        wgt[u] = rr < r1 ? 1.f : 0.f;
+        load8(x + (rr < r1 ? rr : r1 - 1) * C + cg * 8, v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += v[u][j] * wgt[u];
     }
   }
   __shared__ float sh[8][32][9];
@@ -144,12 +153,28 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const uint16_t* __r
   }
 }
 
-__global__ void colsum_fold_kernel(const float* __restrict__ part, int P, int C, float* __restrict__ out, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// fold of the P partial rows: block = 64 columns x 4 partial-row groups (a wave each), LDS combine. P is up to
+// 256 rows of L2-resident partials: 4 waves x P/4 independent loads per lane instead of one lane walking all P.
+__global__ void __launch_bounds__(256) colsum_fold_kernel(const float* __restrict__ part, int P, int C,
+                                                          float* __restrict__ out, int accumulate) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), pg = threadIdx.x >> 6;
   float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(long)p * C + c];
-  out[c] = accumulate ? out[c] + s : s;
+  if (c < C) {
+    int p = pg;
+    for (; p + 12 < P; p += 16) {  // 4 loads in flight per lane
+      const float a = part[(long)p * C + c], b = part[(long)(p + 4) * C + c];
+      const float d = part[(long)(p + 8) * C + c], e = part[(long)(p + 12) * C + c];
+      s += (a + b) + (d + e);
+    }
+    for (; p < P; p += 4) s += part[(long)p * C + c];
+  }
+  __shared__ float sh[4][64];
+  sh[pg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (pg == 0 && c < C) {
+    s = (sh[0][threadIdx.x] + sh[1][threadIdx.x]) + (sh[2][threadIdx.x] + sh[3][threadIdx.x]);
+    out[c] = accumulate ? out[c] + s : s;
+  }
 }
 
 // ----------------------------------------------------------------------------- launchers
@@ -170,18 +195,19 @@ void launch_gelu_bwd(const uint16_t* dy, const uint16_t* pre, uint16_t* dx, long
 void launch_relu_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n, hipStream_t st) {
   hipLaunchKernelGGL(relu_bwd_kernel, dim3(stream_grid(n / 8, 256)), dim3(256), 0, st, dy, y, dx, n / 8);
 }
-int colsum_workspace_floats(long R, int C) {
-  long nb = (R + 255) / 256;
-  if (nb > 256) nb = 256;
-  return (int)(nb * C);
+// Row blocks of 32 rows (4 per thread, 8 row groups), at most 256 of them: a [8192, 768] gradient launches
+// 256 x 3 = 768 blocks (was 32 x 3 with 256-row blocks: 96 blocks on 256 CUs, 0.9 TB/s).
+static long colsum_row_blocks(long R) {
+  long nb = (R + 31) / 32;
+  return nb > 256 ? 256 : nb;
 }
+int colsum_workspace_floats(long R, int C) { return (int)(colsum_row_blocks(R) * C); }
 void launch_colsum(const uint16_t* x, long R, int C, float* work, float* out, bool accumulate, hipStream_t st) {
-  long nb = (R + 255) / 256;
-  if (nb > 256) nb = 256;
+  const long nb = colsum_row_blocks(R);
   const long rpb = (R + nb - 1) / nb;
   dim3 g((unsigned)nb, (unsigned)((C / 8 + 31) / 32));
   hipLaunchKernelGGL(colsum_partial_kernel, g, dim3(256), 0, st, x, R, C, rpb, work);
-  hipLaunchKernelGGL(colsum_fold_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, work, (int)nb, C, out, (int)accumulate);
+  hipLaunchKernelGGL(colsum_fold_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, work, (int)nb, C, out, (int)accumulate);
 }
 
 }  // namespace k8s_amd

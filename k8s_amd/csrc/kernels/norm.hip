@@ -6,9 +6,10 @@
 // per 256-thread block. Optional fused residual add (x = a + r, sum written
 // out) covers the transformer "add & norm" step.
 //
-// Backward: per-row dx in registers; dgamma/dbeta are per-block partial sums
-// over the block's rows ([nblocks, D] fp32) folded by a column-reduce kernel,
-// so no float atomics are needed and results are reproducible.
+// Backward: per-row dx in registers (one wave per row); dgamma/dbeta are
+// per-64-row-block partial sums ([nblocks, 2, D] fp32) from a column kernel,
+// folded by a column-reduce kernel, so no float atomics are needed and results
+// are reproducible.
 #include "common.h"
 #include "launchers.h"
 
@@ -82,89 +83,135 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(const uint16_t* __restric
 }
 
 // rows_per_block rows per block (waves stride over rows); writes partial dgamma/dbeta per block.
+// Backward as two independent launches (measured: the former one-kernel form, 8 rows per wave in sequence with a
+// dy/x re-read for the second pass and per-block dgamma/dbeta partials, ran 0.9-1.7 TB/s: latency-bound, 2
+// waves per CU on Llama-3-8B's 4096 rows):
+//  * norm_bwd_dx_kernel: one wave per row, all of the row's dy / x (/ dres) loads issued up front and kept in
+//    registers as raw bf16 across both passes -> every row in flight at once;
+//  * norm_bwd_param_kernel: dgamma / dbeta column partials over 64-row blocks (8 columns per thread, 4 rows per
+//    trip, mean / rstd broadcast per row), folded by norm_colsum_kernel.
 template <int CPL, bool RMS>
-__global__ void __launch_bounds__(256) norm_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
-                                                       const float* __restrict__ gamma, const float* __restrict__ mean,
-                                                       const float* __restrict__ rstd, const uint16_t* __restrict__ dres,
-                                                       uint16_t* __restrict__ dx, float* __restrict__ part, long R,
-                                                       int D, int rows_per_block) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+__global__ void __launch_bounds__(256) norm_bwd_dx_kernel(const uint16_t* __restrict__ dy,
+                                                          const uint16_t* __restrict__ x,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd,
+                                                          const uint16_t* __restrict__ dres,
+                                                          uint16_t* __restrict__ dx, long R, int D) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * NORM_WAVES + (threadIdx.x >> 6);
+  if (row >= R) return;
   const int nch = D / 8;
-  float pg[CPL][8], pb[CPL][8];
+  bf16x8_t gr[CPL], xr[CPL];
 #pragma unroll
-  for (int c = 0; c < CPL; ++c)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) pg[c][j] = pb[c][j] = 0.f;
-  const long r0 = (long)blockIdx.x * rows_per_block;
-  for (long row = r0 + w; row < r0 + rows_per_block && row < R; row += NORM_WAVES) {
-    const float mu = RMS ? 0.f : mean[row];
-    const float rs = rstd[row];
-    float a = 0.f, b = 0.f;  // sum(dy*gamma), sum(dy*gamma*xhat)
-    // pass 1: row reductions + parameter-gradient partials (kept in registers across rows)
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      const int ch = lane + c * 64;
-      if (ch < nch) {
-        float g[8], xh[8];
-        load8(dy + row * D + ch * 8, g);
-        load8(x + row * D + ch * 8, xh);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = ch * 8 + j;
-          xh[j] = (xh[j] - mu) * rs;
-          pg[c][j] += g[j] * xh[j];
-          pb[c][j] += g[j];
-          const float gg = g[j] * gamma[k];
-          a += gg;
-          b += gg * xh[j];
-        }
-      }
-    }
-    a = wave_sum(a) / D;
-    b = wave_sum(b) / D;
-    // pass 2: re-read the (L1/L2-hot) row and write dx
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      const int ch = lane + c * 64;
-      if (ch < nch) {
-        float g[8], xh[8], o[8];
-        load8(dy + row * D + ch * 8, g);
-        load8(x + row * D + ch * 8, xh);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = ch * 8 + j;
-          const float xn = (xh[j] - mu) * rs;
-          o[j] = rs * (g[j] * gamma[k] - (RMS ? 0.f : a) - xn * b);
-        }
-        if (dres) {
-          float r[8];
-          load8(dres + row * D + ch * 8, r);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += r[j];
-        }
-        store8(dx + row * D + ch * 8, o);
-      }
-    }
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + c * 64;
+    const int cc = ch < nch ? ch : nch - 1;  // clamped (unused) load instead of a branch per chunk
+    gr[c] = *reinterpret_cast<const bf16x8_t*>(dy + row * D + cc * 8);
+    xr[c] = *reinterpret_cast<const bf16x8_t*>(x + row * D + cc * 8);
   }
-  // block partials: waves write their own slice [blockIdx][w][D] then a column reduce folds waves too
+  const float mu = RMS ? 0.f : mean[row];
+  const float rs = rstd[row];
+  float a = 0.f, b = 0.f;  // sum(dy*gamma), sum(dy*gamma*xhat)
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
     const int ch = lane + c * 64;
     if (ch < nch) {
-      float* pgp = part + (((long)blockIdx.x * NORM_WAVES + w) * 2) * D + ch * 8;
-      float* pbp = pgp + D;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        pgp[j] = pg[c][j];
-        pbp[j] = pb[c][j];
+        const float gg = bf2f((uint16_t)gr[c][j]) * gamma[ch * 8 + j];
+        a += gg;
+        b += gg * ((bf2f((uint16_t)xr[c][j]) - mu) * rs);
       }
+    }
+  }
+  a = wave_sum(a) / D;
+  b = wave_sum(b) / D;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xn = (bf2f((uint16_t)xr[c][j]) - mu) * rs;
+        o[j] = rs * (bf2f((uint16_t)gr[c][j]) * gamma[ch * 8 + j] - (RMS ? 0.f : a) - xn * b);
+      }
+      if (dres) {
+        float r[8];
+        load8(dres + row * D + ch * 8, r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += r[j];
+      }
+      store8(dx + row * D + ch * 8, o);
+    }
+  }
+}
+
+constexpr int NORM_PARAM_ROWS = 64;  // rows per column-partial block
+
+// part[blockIdx.x][0][k] = sum dy * xhat, part[blockIdx.x][1][k] = sum dy over the block's rows; block = 32 column
+// chunks (256 columns) x 8 row groups, LDS combine of the row groups
+template <bool RMS>
+__global__ void __launch_bounds__(256) norm_bwd_param_kernel(const uint16_t* __restrict__ dy,
+                                                             const uint16_t* __restrict__ x,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ rstd,
+                                                             float* __restrict__ part, long R, int D) {
+  const int nch = D / 8;
+  const int ch = blockIdx.y * 32 + (threadIdx.x & 31), rg = threadIdx.x >> 5;
+  float pg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (ch < nch) {
+    const long r0 = (long)blockIdx.x * NORM_PARAM_ROWS;
+    const long r1 = r0 + NORM_PARAM_ROWS < R ? r0 + NORM_PARAM_ROWS : R;
+    for (long r = r0 + rg; r < r1; r += 32) {  // 4 rows per trip, loads first (clamped, zero-weighted tail)
+      float g[4][8], xv[4][8], mu[4], rs[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long rr = r + 8 * u < r1 ? r + 8 * u : r1 - 1;
+        load8(dy + rr * D + ch * 8, g[u]);
+        load8(x + rr * D + ch * 8, xv[u]);
+        mu[u] = RMS ? 0.f : mean[rr];
+        rs[u] = r + 8 * u < r1 ? rstd[rr] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float wgt = r + 8 * u < r1 ? 1.f : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          pg[j] += g[u][j] * ((xv[u][j] - mu[u]) * rs[u]);
+          pb[j] += g[u][j] * wgt;
+        }
+      }
+    }
+  }
+  __shared__ float sh[2][8][32][9];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sh[0][rg][threadIdx.x & 31][j] = pg[j];
+    sh[1][rg][threadIdx.x & 31][j] = pb[j];
+  }
+  __syncthreads();
+  if (rg == 0 && ch < nch) {
+    for (int q = 1; q < 8; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        pg[j] += sh[0][q][threadIdx.x][j];
+        pb[j] += sh[1][q][threadIdx.x][j];
+      }
+    float* pgp = part + ((long)blockIdx.x * 2) * D + ch * 8;
+    float* pbp = pgp + D;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      pgp[j] = pg[j];
+      pbp[j] = pb[j];
     }
   }
 }
 
 // fold partial rows: part [P][2][D] -> dgamma[D], dbeta[D]. Block = 32 columns x 8 row slices (coalesced
-// 128-B rows, 4 independent loads in flight per thread), LDS combine of the slices. P is ~1k partials: a
-// thread-per-column serial loop here was latency-bound at ~260 us per call.
+// 128-B rows, 4 independent loads in flight per thread), LDS combine of the slices. P = R / 64 partial rows; a
+// thread-per-column serial loop here was latency-bound at ~260 us per call with ~1k partials.
 __global__ void __launch_bounds__(256) norm_colsum_kernel(const float* __restrict__ part, int P, int D,
                                                           float* __restrict__ dgamma, float* __restrict__ dbeta) {
   __shared__ float sh[2][8][33];
@@ -236,28 +283,20 @@ void launch_norm_fwd(bool rms, const uint16_t* x, const uint16_t* res, uint16_t*
     norm_fwd_dispatch<false>(cpl, g, st, x, res, xsum, gamma, beta, y, mean, rstd, R, D, eps);
 }
 
-int norm_bwd_blocks(long R) {
-  long b = (R + 31) / 32;  // 32 rows per block
-  if (b > 256) b = 256;
-  if (b < 1) b = 1;
-  return (int)b;
-}
+static int norm_param_blocks(long R) { return (int)((R + NORM_PARAM_ROWS - 1) / NORM_PARAM_ROWS); }
 
-int norm_workspace_floats(long R, int D) { return norm_bwd_blocks(R) * NORM_WAVES * 2 * D; }
+int norm_workspace_floats(long R, int D) { return norm_param_blocks(R) * 2 * D; }
 
 void launch_norm_bwd(bool rms, const uint16_t* dy, const uint16_t* x, const float* gamma, const float* mean,
                      const float* rstd, const uint16_t* dres, uint16_t* dx, float* dgamma, float* dbeta, float* work,
                      long R, int D, hipStream_t st) {
-  const int nb = norm_bwd_blocks(R);
-  const int rpb = (int)((R + nb - 1) / nb);
   const int cpl = norm_cpl(D);
-#define NB(C)                                                                                                    \
-  if (rms)                                                                                                       \
-    hipLaunchKernelGGL((norm_bwd_kernel<C, true>), dim3(nb), dim3(256), 0, st, dy, x, gamma, mean, rstd, dres, dx, \
-                       work, R, D, rpb);                                                                         \
-  else                                                                                                           \
-    hipLaunchKernelGGL((norm_bwd_kernel<C, false>), dim3(nb), dim3(256), 0, st, dy, x, gamma, mean, rstd, dres,    \
-                       dx, work, R, D, rpb);
+  const dim3 g(cdiv(R, NORM_WAVES));
+#define NB(C)                                                                                                     \
+  if (rms)                                                                                                        \
+    hipLaunchKernelGGL((norm_bwd_dx_kernel<C, true>), g, dim3(256), 0, st, dy, x, gamma, mean, rstd, dres, dx, R, D); \
+  else                                                                                                            \
+    hipLaunchKernelGGL((norm_bwd_dx_kernel<C, false>), g, dim3(256), 0, st, dy, x, gamma, mean, rstd, dres, dx, R, D);
   switch (cpl) {
     case 1: NB(1); break;
     case 2: NB(2); break;
@@ -266,7 +305,13 @@ void launch_norm_bwd(bool rms, const uint16_t* dy, const uint16_t* x, const floa
     default: NB(16); break;
   }
 #undef NB
-  hipLaunchKernelGGL(norm_colsum_kernel, dim3(cdiv(D, 32)), dim3(256), 0, st, work, nb * NORM_WAVES, D, dgamma,
+  const int nb = norm_param_blocks(R);
+  const dim3 gp(nb, cdiv(D / 8, 32));
+  if (rms)
+    hipLaunchKernelGGL(norm_bwd_param_kernel<true>, gp, dim3(256), 0, st, dy, x, mean, rstd, work, R, D);
+  else
+    hipLaunchKernelGGL(norm_bwd_param_kernel<false>, gp, dim3(256), 0, st, dy, x, mean, rstd, work, R, D);
+  hipLaunchKernelGGL(norm_colsum_kernel, dim3(cdiv(D, 32)), dim3(256), 0, st, work, nb, D, dgamma,
                      rms ? nullptr : dbeta);
 }
 

@@ -1,0 +1,10 @@
+#!/bin/bash
+# GPU job: kernel + transformer tests, then BERT-base / Llama-1B / Llama-3-8B trainer throughput.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_kernels_gpu.py tests/test_transformer_grads_gpu.py tests/test_models_gpu.py > gpurun_out/kq_test.log 2>&1 || { tail -40 gpurun_out/kq_test.log; exit 1; }
+tail -1 gpurun_out/kq_test.log
+timeout -k 10 300 python -m k8s_amd.trainer --model bert_base --batch 64 --seq 128 --steps 30 --log-every 10 > gpurun_out/train_bert.log 2>&1 && grep '"step"' gpurun_out/train_bert.log | tail -1 | cut -c1-160 &&
+timeout -k 10 300 python -m k8s_amd.trainer --model llama_1b --batch 2 --seq 2048 --steps 20 --log-every 5 --max-grad-norm 1.0 > gpurun_out/train_llama1b.log 2>&1 && grep '"step"' gpurun_out/train_llama1b.log | tail -1 | cut -c1-160 &&
+timeout -k 10 500 python -m k8s_amd.trainer --model llama3_8b --batch 1 --seq 4096 --steps 8 --log-every 2 --max-grad-norm 1.0 > gpurun_out/train_llama8b.log 2>&1 && grep '"step"' gpurun_out/train_llama8b.log | tail -1 | cut -c1-160

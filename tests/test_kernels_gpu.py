@@ -82,9 +82,9 @@ def test_bn_from_conv_sums_and_relu_from_x(cuda, C, M):
 @pytest.mark.parametrize("D", [768, 4096, 1024, 136])
 @pytest.mark.parametrize("rms", [False, True])
 @pytest.mark.parametrize("res", [False, True])
-def test_norm_fwd_bwd(cuda, D, rms, res):
+@pytest.mark.parametrize("R", [257, 2100])  # one partial block / many, ragged tails
+def test_norm_fwd_bwd(cuda, D, rms, res, R):
     torch.manual_seed(1)
-    R = 257
     x = torch.randn(R, D, device=cuda).bfloat16()
     r = torch.randn(R, D, device=cuda).bfloat16() if res else None
     g = torch.rand(D, device=cuda) + 0.5
