@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import sys
 import time
 
 import torch
@@ -111,10 +112,13 @@ def main(argv=None):
     ap.add_argument("--seq", type=int, default=None)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-find", action="store_true",
+                    help="cudnn.benchmark off: MIOpen immediate mode (heuristic solution per shape, no Find search) "
+                         "-- the only way a cold box compiles the batch-1024 kernels inside a GPU-call limit")
     a = ap.parse_args(argv)
     batch = a.batch or {"resnet50": 256, "bert_base": 64, "llama_1b": 2, "llama3_8b": 1}[a.model]
     seq = a.seq or {"bert_base": 128}.get(a.model, 2048)
-    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.benchmark = not a.no_find
     m, opt, loss_fn, units, unit = build(a.model, batch, seq)
 
     def step():
@@ -124,9 +128,10 @@ def main(argv=None):
         opt.step()
         return loss
 
-    for _ in range(a.warmup):
+    for i in range(a.warmup):
         step()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        print("warmup step %d/%d done" % (i + 1, a.warmup), file=sys.stderr, flush=True)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss = step()
@@ -136,7 +141,8 @@ def main(argv=None):
                       "unit": "%s/s" % unit, "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
                       "ms_per_step": round(1000 * dt / a.steps, 3), "batch": batch,
                       "seq": seq if unit == "tokens" else None, "final_loss": round(float(loss), 4),
-                      "stack": "torch %s (MIOpen / hipBLASLt / SDPA / fused optim)" % torch.__version__}), flush=True)
+                      "stack": "torch %s (MIOpen / hipBLASLt / SDPA / fused optim)" % torch.__version__,
+                      "miopen_find": not a.no_find}), flush=True)
 
 
 if __name__ == "__main__":
