@@ -50,9 +50,11 @@ struct Epi {
   float alpha;
 };
 
+// GELU(tanh) = x * sigmoid(2u): v_exp_f32 + v_rcp_f32 (see gemm.hip's gelu_tanh)
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+  const float u = k0 * (x + k1 * x * x * x);
+  return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-2.8853900817779268f * u));
 }
 
 __device__ __forceinline__ void barrier() {
