@@ -82,13 +82,15 @@ class Bottleneck(nn.Module):
         # epilogue of whichever runs second (shared link) instead of by autograd's separate add
         dlink = K.GradLink(shared=True) if (self.down is not None and x.requires_grad) else None
         l1, l2, l3 = K.BnBwdLink(), K.BnBwdLink(), K.BnBwdLink()
-        y = self.bn1(self.conv1(x, grad_link=link or dlink, bn_link=in_link if identity else None), bwd_link=l1)
-        y = self.bn2(self.conv2(y, bn_link=l1), bwd_link=l2)
-        # downsample block: bn3's ReLU mask is applied by the downsample BN's backward as it reads dy
+        # downsample block: bn3's ReLU mask is applied by the downsample BN's backward as it reads dy. The branch is
+        # built FIRST so autograd (highest sequence number first) runs its backward LAST: the stride-2 1x1 dgrad
+        # then accumulates onto conv1's dx (shared GradLink) instead of zero-filling the 3 parities it never writes
         mlink = None
         if self.down is not None:
             mlink = K.MaskLink()
             idn = self.down_bn(self.down(x, grad_link=dlink), relu=False, dy_link=mlink)
+        y = self.bn1(self.conv1(x, grad_link=link or dlink, bn_link=in_link if identity else None), bwd_link=l1)
+        y = self.bn2(self.conv2(y, bn_link=l1), bwd_link=l2)
         return self.bn3(self.conv3(y, bn_link=l2), residual=idn, relu=True, res_link=link or mlink,
                         bwd_link=l3), l3
 
