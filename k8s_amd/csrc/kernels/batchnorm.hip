@@ -224,7 +224,9 @@ __global__ void bn_finalize_sums_kernel(const float* __restrict__ sums, int nrep
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float s = 0.f, q = 0.f;
-  for (int r = 0; r < nrep; ++r) {  // replicas written by the conv epilogue
+  // replicas written by the conv epilogue: all 2 x nrep loads in flight (a rolled loop waited ~32 round trips)
+#pragma unroll 16
+  for (int r = 0; r < nrep; ++r) {
     s += sums[(long)r * 2 * C + c];
     q += sums[(long)r * 2 * C + C + c];
   }
@@ -412,7 +414,7 @@ __global__ void __launch_bounds__(256) bn_bwd_final_kernel(const float* __restri
   const int c = blockIdx.x * FIN_CH + cl;
   float a = 0.f, b2 = 0.f;
   if (c < C) {
-#pragma unroll 4
+#pragma unroll 16
     for (int i = rg; i < nblocks; i += FIN_RG) {
       const float2 v = *reinterpret_cast<const float2*>(part + ((long)i * C + c) * 2);
       a += v.x;
