@@ -900,7 +900,8 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, l
                                      int accumulate) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < mn4; i += (long)gridDim.x * blockDim.x) {
     float4 acc = accumulate ? reinterpret_cast<const float4*>(out)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int z = 0; z < splits; ++z) {
+#pragma unroll 8
+    for (int z = 0; z < splits; ++z) {  // slab loads of up to 8 splits in flight
       const float4 v = reinterpret_cast<const float4*>(ws)[(long)z * mn4 + i];
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
