@@ -123,6 +123,61 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const uint16_t* __rest
   store8(dx + (long)e * 8, acc);
 }
 
+// 3x3 / stride 2 / pad 1 (the ResNet stem) backward by 2x2 input-pixel cells: the cell (2k..2k+1, 2j..2j+1) is
+// covered by exactly the windows (k..k+1, j..j+1), so one thread loads those 4 windows' winner bytes and dy
+// vectors ONCE for its 4 pixels (24 B of L2 reads per 16-B output instead of 4 x 24 B when every pixel thread
+// loads its own covering windows) and writes the 4 pixels. Window position of pixel (h, w) in window (ho, wo):
+// (h - 2ho + 1) * 3 + (w - 2wo + 1).
+__global__ void __launch_bounds__(256) maxpool_bwd_3s2_kernel(const uint16_t* __restrict__ dy,
+                                                              const uint8_t* __restrict__ idx,
+                                                              uint16_t* __restrict__ dx, int H, int W, int C, int Ho,
+                                                              int Wo, int Hc, int Wc, int total, FastDiv fcv,
+                                                              FastDiv fWc, FastDiv fHc) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= total) return;
+  const int cv = C >> 3;
+  int t = fcv.div(e);
+  const int c = (e - t * cv) * 8;
+  int t2 = fWc.div(t);
+  const int j = t - t2 * Wc;
+  const int n = fHc.div(t2);
+  const int k = t2 - n * Hc;
+  uint64_t pk[2][2];
+  float g[2][2][8];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const bool ok = k + a < Ho && j + b < Wo;
+      const long o = (((long)n * Ho + (ok ? k + a : k)) * Wo + (ok ? j + b : j)) * C + c;
+      pk[a][b] = ok ? *reinterpret_cast<const uint64_t*>(idx + o) : ~0ull;  // 0xff: matches no position
+      load8(dy + o, g[a][b]);
+    }
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int dw = 0; dw < 2; ++dw) {
+      const int h = 2 * k + dh, w = 2 * j + dw;
+      if (h >= H || w >= W) continue;
+      float acc[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          // pixel (h, w) lies in window (k + a, j + b) iff its offset inside the window is in 0..2
+          const int oh = h - 2 * (k + a) + 1, ow = w - 2 * (j + b) + 1;
+          if (oh < 0 || oh > 2 || ow < 0 || ow > 2) continue;  // compile-time after unrolling
+          const uint8_t pos = (uint8_t)(oh * 3 + ow);
+#pragma unroll
+          for (int r = 0; r < 8; ++r)
+            if (((pk[a][b] >> (8 * r)) & 0xff) == pos) acc[r] += g[a][b][r];
+        }
+      store8(dx + (((long)n * H + h) * W + w) * C + c, acc);
+    }
+}
+
 void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
                         int k, int s, int p, hipStream_t st) {
   const long total = (long)N * Ho * Wo * (C / 8);
@@ -135,6 +190,13 @@ void launch_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, in
                         int Wo, int k, int s, int p, hipStream_t st) {
   const long total = (long)N * H * W * (C / 8);
   if (total >= (1L << 31)) throw std::runtime_error("maxpool: tensor too large for 32-bit indexing");
+  if (k == 3 && s == 2 && p == 1) {
+    const int Hc = (H + 1) / 2, Wc = (W + 1) / 2;
+    const long cells = (long)N * Hc * Wc * (C / 8);
+    hipLaunchKernelGGL(maxpool_bwd_3s2_kernel, dim3(cdiv(cells, 256)), dim3(256), 0, st, dy, idx, dx, H, W, C, Ho,
+                       Wo, Hc, Wc, (int)cells, make_fastdiv(C / 8), make_fastdiv(Wc), make_fastdiv(Hc));
+    return;
+  }
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, dy, idx, dx, H, W, C, Ho, Wo, k, s,
                      p, (int)total, make_fastdiv(C / 8), make_fastdiv(W), make_fastdiv(H));
 }
