@@ -342,8 +342,11 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 // XEPI (lean only): bias / ReLU / GELU / pre-activation copy in the staged epilogue (the transformer linears'
 // forward); its own instantiation so the convolutions' lean kernels stay as small as before (the extra epilogue
 // code compiled into every lean kernel cost ResNet-50 1.1 %, measured new/old/new/old on one box).
+// F32S (general epilogue only): fp32 outputs without bias / activation / statistics / row remap -- the weight
+// gradients and their split-K slabs -- go through LDS and leave as whole 256-B row segments; its own instantiation
+// for the weight-gradient operand pairs.
 template <class ASrc, class BSrc, int NBUF, int WM = 2, int WN = 2, bool LEAN = false, bool BNB = false,
-          bool XEPI = false>
+          bool XEPI = false, bool F32S = false>
 __global__ void __launch_bounds__(GEMM_THREADS, (NBUF == 1 && !BNB) ? 3 : 2)
 gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
@@ -633,6 +636,47 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
     }
     return;
   } else {
+    if constexpr (F32S && WM == 2 && WN == 2) {
+      if (E.out_f32 && emode != 2 && !E.bias && !E.pre && E.act == 0 && !E.stats && !E.rst && (E.ldc & 3) == 0 &&
+          (N & 3) == 0) {
+        __syncthreads();  // every wave is past its last K-loop LDS read
+        // wave (wm, wn): its 64 x 64 piece in two 32-row halves, [32 rows][64 cols] fp32 (8 KB, wave-private)
+        float* const st = reinterpret_cast<float*>(smem) + (wm * WN + wn) * (32 * 64);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          if (h) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of the first half are done
+            asm volatile("" ::: "memory");
+          }
+#pragma unroll
+          for (int i2 = 0; i2 < 2; ++i2) {
+            const int lr = i2 * 16 + (lane & 15);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int ch = (j * 4 + (lane >> 4)) ^ (lr & 15);  // 16-B chunk, XOR-swizzled by the row
+              *reinterpret_cast<f32x4_t*>(reinterpret_cast<char*>(st) + lr * 256 + ch * 16) =
+                  acc[2 * h + i2][j] * E.alpha;
+            }
+          }
+          __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the staging writes landed
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int it = 0; it < 8; ++it) {
+            const int idx = it * 64 + lane;
+            const int lr = idx >> 4, ch = idx & 15;
+            const int m = m0 + wm * 64 + h * 32 + lr, n = n0 + wn * 64 + ch * 4;
+            f32x4_t v = *reinterpret_cast<const f32x4_t*>(reinterpret_cast<const char*>(st) + lr * 256 +
+                                                          ((ch ^ (lr & 15)) << 4));
+            if (m < M && n < N) {
+              float* cp = reinterpret_cast<float*>(ec) + (long)m * E.ldc + n;
+              if (emode == 1) v += *reinterpret_cast<const f32x4_t*>(cp);
+              *reinterpret_cast<f32x4_t*>(cp) = v;
+            }
+          }
+        }
+        return;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + wm * 64 + i * 16 + (lane & 15);
@@ -763,21 +807,26 @@ static int effective_splits(int K, int splits) {
   return (K + kps - 1) / kps;
 }
 
-template <class ASrc, class BSrc, int WM, int WN, bool LEAN, bool BNB, bool XEPI = false>
+template <class ASrc, class BSrc, int WM, int WN, bool LEAN, bool BNB, bool XEPI = false, bool F32S = false>
 static void launch_tiles2(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
                           hipStream_t st) {
   const int tiles = ((M + 64 * WM - 1) / (64 * WM)) * ((N + 64 * WN - 1) / (64 * WN));
   if (kps <= 2 * BK)
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN, LEAN, BNB, XEPI>), dim3(tiles, 1, splits),
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN, LEAN, BNB, XEPI, F32S>), dim3(tiles, 1, splits),
                        dim3(GEMM_THREADS), 0, st, a, b, e, M, N, K, kps);
   else
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2, WM, WN, LEAN, BNB, XEPI>), dim3(tiles, 1, splits),
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2, WM, WN, LEAN, BNB, XEPI, F32S>), dim3(tiles, 1, splits),
                        dim3(GEMM_THREADS), 0, st, a, b, e, M, N, K, kps);
 }
 
 // the lean epilogue applies: bf16 C (16-B aligned rows), store or accumulate, no atomics; bias / ReLU / GELU /
 // pre-activation copy in store mode on identity rows without statistics (the transformer linears: measured on
 // BERT-base's QKV / FFN1 forward 81 / 105 us per call through the general per-lane epilogue)
+// K8S_AMD_F32S=0 keeps the weight gradients on the per-lane fp32 epilogue (A/B switch; read per call)
+static bool f32s_on() {
+  const char* v = getenv("K8S_AMD_F32S");
+  return !(v && v[0] == '0');
+}
 static bool epi_extra(const Epi& e) { return e.bias || e.pre || e.act != 0; }
 static bool lean_epi(const Epi& e, int N, bool allow_extra) {
   if (epi_extra(e) && (!allow_extra || e.mode != 0 || e.rst || e.stats || e.bstats || e.addsrc ||
@@ -819,6 +868,15 @@ static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int 
   }
   if (e.bstats) throw std::runtime_error("the BatchNorm-backward epilogue needs a plain bf16 output (lean epilogue)");
   if (e.addsrc || e.addmask) throw std::runtime_error("a separate (masked) addend needs the lean epilogue");
+  // weight gradients (both operands MN-major: dense or im2col) with an fp32 output or split-K slab
+  constexpr bool kWgrad = std::is_same_v<ASrc, MNMajorK> &&
+                          (std::is_same_v<BSrc, MNMajorK> || std::is_same_v<BSrc, ConvWgB>);
+  if constexpr (kWgrad && WM == 2 && WN == 2) {
+    if (e.out_f32 && e.mode != 2 && !epi_extra(e) && !e.stats && !e.rst && f32s_on()) {
+      launch_tiles2<ASrc, BSrc, WM, WN, false, false, false, true>(a, b, e, M, N, K, kps, splits, st);
+      return;
+    }
+  }
   launch_tiles2<ASrc, BSrc, WM, WN, false, false>(a, b, e, M, N, K, kps, splits, st);
 }
 

@@ -122,6 +122,47 @@ __device__ __forceinline__ void epilogue256(const f32x4_t (&acc)[8][4], const Ep
     }
     return;
   }
+  if (E.out_f32 && !E.pre && !E.bias && E.act == 0 && (E.ldc & 3) == 0) {
+    // fp32 tile (the weight gradients, written or accumulated into the flat fp32 slots) through LDS in two
+    // 64-row halves per wave (16 KB each, wave-private): the copy-out stores whole 256-B row segments (4 rows per
+    // wave-instruction) instead of 16 rows x 64 B per instruction from the MFMA fragment layout.
+    barrier();  // every wave is past its last LDS read of the K loop
+    float* st = reinterpret_cast<float*>(smem) + wid * (64 * 64);  // [64 rows][64 cols], 256-B rows
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if (half) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of the first half are done
+        asm volatile("" ::: "memory");
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int lr = a * 16 + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int ch = (j * 4 + (lane >> 4)) ^ (lr & 15);  // 16-B chunk, XOR-swizzled by the row
+          const f32x4_t v = acc[half * 4 + a][j] * alpha;
+          *reinterpret_cast<f32x4_t*>(reinterpret_cast<char*>(st) + lr * 256 + ch * 16) = v;
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the staging writes landed (wave-private region)
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int idx = it * 64 + lane;
+        const int lr = idx >> 4, ch = idx & 15;
+        const int m = m0 + wr * 128 + half * 64 + lr;
+        const int n = n0 + wc * 64 + ch * 4;
+        f32x4_t v = *reinterpret_cast<const f32x4_t*>(reinterpret_cast<const char*>(st) + lr * 256 +
+                                                      ((ch ^ (lr & 15)) << 4));
+        if (m < M && n < N) {  // N % 4 == 0 (gemm256_eligible)
+          float* cp = reinterpret_cast<float*>(E.c) + (long)m * E.ldc + n;
+          if (E.accumulate) v += *reinterpret_cast<const f32x4_t*>(cp);
+          *reinterpret_cast<f32x4_t*>(cp) = v;
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
     const int m = m0 + wr * 128 + a * 16 + (lane & 15);
