@@ -46,7 +46,7 @@ void launch_norm_fwd(bool rms, const uint16_t* x, const uint16_t* res, uint16_t*
 int norm_workspace_floats(long R, int D);
 void launch_norm_bwd(bool rms, const uint16_t* dy, const uint16_t* x, const float* gamma, const float* mean,
                      const float* rstd, const uint16_t* dres, uint16_t* dx, float* dgamma, float* dbeta, float* work,
-                     long R, int D, hipStream_t st);
+                     long R, int D, hipStream_t st, float* dsum = nullptr);
 
 // xent.hip
 void launch_xent_fwd(const void* logits, bool bf16, const int64_t* labels, long R, long V, long ld, float* loss,

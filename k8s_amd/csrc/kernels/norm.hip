@@ -10,6 +10,8 @@
 // per-64-row-block partial sums ([nblocks, 2, D] fp32) from a column kernel,
 // folded by a column-reduce kernel, so no float atomics are needed and results
 // are reproducible.
+#include <stdexcept>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -97,7 +99,8 @@ __global__ void __launch_bounds__(256) norm_bwd_dx_kernel(const uint16_t* __rest
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ rstd,
                                                           const uint16_t* __restrict__ dres,
-                                                          uint16_t* __restrict__ dx, long R, int D) {
+                                                          uint16_t* __restrict__ dx, float* __restrict__ rowab, long R,
+                                                          int D) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * NORM_WAVES + (threadIdx.x >> 6);
   if (row >= R) return;
@@ -127,6 +130,10 @@ __global__ void __launch_bounds__(256) norm_bwd_dx_kernel(const uint16_t* __rest
   }
   a = wave_sum(a) / D;
   b = wave_sum(b) / D;
+  if (rowab && lane == 0) {  // the row's dx coefficients, for the column sums of dx (upstream linear's bias grad)
+    rowab[2 * row] = a;
+    rowab[2 * row + 1] = b;
+  }
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
     const int ch = lane + c * 64;
@@ -152,15 +159,24 @@ constexpr int NORM_PARAM_ROWS = 64;  // rows per column-partial block
 
 // part[blockIdx.x][0][k] = sum dy * xhat, part[blockIdx.x][1][k] = sum dy over the block's rows; block = 32 column
 // chunks (256 columns) x 8 row groups, LDS combine of the row groups
+// With rowab (the dx kernel's per-row a, b): also part[..][2][k] = sum dx, dx recomputed from dy, x and the row
+// coefficients -- the bias gradient of the linear whose output this norm read (no separate column-sum pass).
 template <bool RMS>
 __global__ void __launch_bounds__(256) norm_bwd_param_kernel(const uint16_t* __restrict__ dy,
                                                              const uint16_t* __restrict__ x,
                                                              const float* __restrict__ mean,
                                                              const float* __restrict__ rstd,
+                                                             const float* __restrict__ rowab,
+                                                             const float* __restrict__ gamma,
                                                              float* __restrict__ part, long R, int D) {
   const int nch = D / 8;
   const int ch = blockIdx.y * 32 + (threadIdx.x & 31), rg = threadIdx.x >> 5;
-  float pg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float pg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pb[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pd[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float gm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (rowab && ch < nch) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gm[j] = gamma[ch * 8 + j];
+  }
   if (ch < nch) {
     const long r0 = (long)blockIdx.x * NORM_PARAM_ROWS;
     const long r1 = r0 + NORM_PARAM_ROWS < R ? r0 + NORM_PARAM_ROWS : R;
@@ -183,13 +199,24 @@ __global__ void __launch_bounds__(256) norm_bwd_param_kernel(const uint16_t* __r
           pb[j] += g[u][j] * wgt;
         }
       }
+      if (rowab) {  // sum dx = rs * (dy * gamma - a - xhat * b) (rs = 0 on the clamped tail rows)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const long rr = r + 8 * u < r1 ? r + 8 * u : r1 - 1;
+          const float ra = RMS ? 0.f : rowab[2 * rr], rb = rowab[2 * rr + 1];
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            pd[j] += rs[u] * (g[u][j] * gm[j] - ra - (xv[u][j] - mu[u]) * rs[u] * rb);
+        }
+      }
     }
   }
-  __shared__ float sh[2][8][32][9];
+  __shared__ float sh[3][8][32][9];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     sh[0][rg][threadIdx.x & 31][j] = pg[j];
     sh[1][rg][threadIdx.x & 31][j] = pb[j];
+    sh[2][rg][threadIdx.x & 31][j] = pd[j];
   }
   __syncthreads();
   if (rg == 0 && ch < nch) {
@@ -198,13 +225,16 @@ __global__ void __launch_bounds__(256) norm_bwd_param_kernel(const uint16_t* __r
       for (int j = 0; j < 8; ++j) {
         pg[j] += sh[0][q][threadIdx.x][j];
         pb[j] += sh[1][q][threadIdx.x][j];
+        pd[j] += sh[2][q][threadIdx.x][j];
       }
-    float* pgp = part + ((long)blockIdx.x * 2) * D + ch * 8;
+    float* pgp = part + ((long)blockIdx.x * 3) * D + ch * 8;
     float* pbp = pgp + D;
+    float* pdp = pbp + D;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       pgp[j] = pg[j];
       pbp[j] = pb[j];
+      pdp[j] = pd[j];
     }
   }
 }
@@ -213,42 +243,49 @@ __global__ void __launch_bounds__(256) norm_bwd_param_kernel(const uint16_t* __r
 // 128-B rows, 4 independent loads in flight per thread), LDS combine of the slices. P = R / 64 partial rows; a
 // thread-per-column serial loop here was latency-bound at ~260 us per call with ~1k partials.
 __global__ void __launch_bounds__(256) norm_colsum_kernel(const float* __restrict__ part, int P, int D,
-                                                          float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  __shared__ float sh[2][8][33];
+                                                          float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                          float* __restrict__ dsum) {
+  __shared__ float sh[3][8][33];
   const int col = threadIdx.x & 31, sl = threadIdx.x >> 5;
   const int k = blockIdx.x * 32 + col;
-  float a = 0.f, b = 0.f;
+  float a = 0.f, b = 0.f, d = 0.f;
   if (k < D) {
     int p = sl;
     for (; p + 24 < P; p += 32) {
-      float av[4], bv[4];
+      float av[4], bv[4], dv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        av[u] = part[((long)(p + 8 * u) * 2) * D + k];
-        bv[u] = part[((long)(p + 8 * u) * 2 + 1) * D + k];
+        av[u] = part[((long)(p + 8 * u) * 3) * D + k];
+        bv[u] = part[((long)(p + 8 * u) * 3 + 1) * D + k];
+        dv[u] = dsum ? part[((long)(p + 8 * u) * 3 + 2) * D + k] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         a += av[u];
         b += bv[u];
+        d += dv[u];
       }
     }
     for (; p < P; p += 8) {
-      a += part[((long)p * 2) * D + k];
-      b += part[((long)p * 2 + 1) * D + k];
+      a += part[((long)p * 3) * D + k];
+      b += part[((long)p * 3 + 1) * D + k];
+      if (dsum) d += part[((long)p * 3 + 2) * D + k];
     }
   }
   sh[0][sl][col] = a;
   sh[1][sl][col] = b;
+  sh[2][sl][col] = d;
   __syncthreads();
   if (sl == 0 && k < D) {
 #pragma unroll
     for (int i = 1; i < 8; ++i) {
       a += sh[0][i][col];
       b += sh[1][i][col];
+      d += sh[2][i][col];
     }
     if (dgamma) dgamma[k] = a;
     if (dbeta) dbeta[k] = b;
+    if (dsum) dsum[k] = d;
   }
 }
 
@@ -285,18 +322,24 @@ void launch_norm_fwd(bool rms, const uint16_t* x, const uint16_t* res, uint16_t*
 
 static int norm_param_blocks(long R) { return (int)((R + NORM_PARAM_ROWS - 1) / NORM_PARAM_ROWS); }
 
-int norm_workspace_floats(long R, int D) { return norm_param_blocks(R) * 2 * D; }
+// [nblocks][3][D] partials + [R][2] row coefficients
+int norm_workspace_floats(long R, int D) { return (int)(norm_param_blocks(R) * 3L * D + 2 * R); }
 
 void launch_norm_bwd(bool rms, const uint16_t* dy, const uint16_t* x, const float* gamma, const float* mean,
                      const float* rstd, const uint16_t* dres, uint16_t* dx, float* dgamma, float* dbeta, float* work,
-                     long R, int D, hipStream_t st) {
+                     long R, int D, hipStream_t st, float* dsum) {
+  if (dsum && dres) throw std::runtime_error("norm_bwd: the dx column sums exclude a residual gradient");
   const int cpl = norm_cpl(D);
   const dim3 g(cdiv(R, NORM_WAVES));
+  const int nb = norm_param_blocks(R);
+  float* const rowab = dsum ? work + (long)nb * 3 * D : nullptr;
 #define NB(C)                                                                                                     \
   if (rms)                                                                                                        \
-    hipLaunchKernelGGL((norm_bwd_dx_kernel<C, true>), g, dim3(256), 0, st, dy, x, gamma, mean, rstd, dres, dx, R, D); \
+    hipLaunchKernelGGL((norm_bwd_dx_kernel<C, true>), g, dim3(256), 0, st, dy, x, gamma, mean, rstd, dres, dx, \
+                       rowab, R, D);                                                                             \
   else                                                                                                            \
-    hipLaunchKernelGGL((norm_bwd_dx_kernel<C, false>), g, dim3(256), 0, st, dy, x, gamma, mean, rstd, dres, dx, R, D);
+    hipLaunchKernelGGL((norm_bwd_dx_kernel<C, false>), g, dim3(256), 0, st, dy, x, gamma, mean, rstd, dres, dx, \
+                       rowab, R, D);
   switch (cpl) {
     case 1: NB(1); break;
     case 2: NB(2); break;
@@ -305,14 +348,15 @@ void launch_norm_bwd(bool rms, const uint16_t* dy, const uint16_t* x, const floa
     default: NB(16); break;
   }
 #undef NB
-  const int nb = norm_param_blocks(R);
   const dim3 gp(nb, cdiv(D / 8, 32));
   if (rms)
-    hipLaunchKernelGGL(norm_bwd_param_kernel<true>, gp, dim3(256), 0, st, dy, x, mean, rstd, work, R, D);
+    hipLaunchKernelGGL(norm_bwd_param_kernel<true>, gp, dim3(256), 0, st, dy, x, mean, rstd, rowab, gamma, work, R,
+                       D);
   else
-    hipLaunchKernelGGL(norm_bwd_param_kernel<false>, gp, dim3(256), 0, st, dy, x, mean, rstd, work, R, D);
+    hipLaunchKernelGGL(norm_bwd_param_kernel<false>, gp, dim3(256), 0, st, dy, x, mean, rstd, rowab, gamma, work, R,
+                       D);
   hipLaunchKernelGGL(norm_colsum_kernel, dim3(cdiv(D, 32)), dim3(256), 0, st, work, nb, D, dgamma,
-                     rms ? nullptr : dbeta);
+                     rms ? nullptr : dbeta, dsum);
 }
 
 }  // namespace k8s_amd

@@ -216,8 +216,10 @@ std::vector<Tensor> norm_fwd(Tensor x, c10::optional<Tensor> res, Tensor gamma, 
   return {y, mean, rstd, xsum};
 }
 
+// dsum (optional, fp32 [D]): also the column sums of dx -- the bias gradient of the linear that produced x's
+// first summand (no residual gradient allowed)
 Tensor norm_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tensor rstd, c10::optional<Tensor> dres,
-                Tensor dgamma, c10::optional<Tensor> dbeta, bool rms) {
+                Tensor dgamma, c10::optional<Tensor> dbeta, bool rms, c10::optional<Tensor> dsum) {
   check_cuda(dy, "dy"); check_cuda(x, "x");
   check_dtype(dy, at::kBFloat16, "dy");
   TORCH_CHECK(dy.sizes() == x.sizes());
@@ -226,11 +228,13 @@ Tensor norm_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tensor rstd, c10
   TORCH_CHECK(dgamma.numel() == D && dgamma.is_contiguous());
   if (!rms) TORCH_CHECK(dbeta.has_value() && dbeta->numel() == D);
   if (dres) TORCH_CHECK(dres->sizes() == x.sizes() && dres->is_contiguous());
+  if (dsum) TORCH_CHECK(!dres && dsum->is_cuda() && dsum->scalar_type() == at::kFloat && dsum->is_contiguous() &&
+                            dsum->numel() == D, "dsum: contiguous fp32 [D], no residual gradient");
   auto dx = torch::empty_like(x);
   auto work = torch::empty({k8s_amd::norm_workspace_floats(R, D)}, gamma.options());
   k8s_amd::launch_norm_bwd(rms, cbf(dy), cbf(x), f32(gamma), f32(mean), f32(rstd), dres ? cbf(*dres) : nullptr,
                            bf(dx), f32(dgamma), dbeta ? dbeta->data_ptr<float>() : nullptr, f32(work), R, D,
-                           cur_stream());
+                           cur_stream(), dsum ? dsum->data_ptr<float>() : nullptr);
   return dx;
 }
 
@@ -802,7 +806,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("sums"), py::arg("run_mean"), py::arg("run_var"), py::arg("momentum"), py::arg("eps"),
         py::arg("relu"), py::arg("want_mask") = false);
   m.def("norm_fwd", &norm_fwd);
-  m.def("norm_bwd", &norm_bwd);
+  m.def("norm_bwd", &norm_bwd, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
+        py::arg("dres"), py::arg("dgamma"), py::arg("dbeta"), py::arg("rms"), py::arg("dsum") = py::none());
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
   m.def("wgrad_stream_eligible", &k8s_amd::wgrad_stream_eligible, "tall-K weight-gradient kernel takes this shape");

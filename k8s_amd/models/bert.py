@@ -74,13 +74,15 @@ class BertLayer(nn.Module):
         # x is read by the QKV GEMM and, as the residual, by LN1 (likewise LN1's output by FFN1 and LN2): each
         # GradLink sums the two gradient contributions in the GEMM's dgrad epilogue instead of a separate add
         l1, l2 = K.GradLink(), K.GradLink()
+        # and the O / FFN2 bias gradients come from the LayerNorm backward that reads their outputs (BiasLink)
+        b1, b2 = K.BiasLink(), K.BiasLink()
         qkv = K.linear(x, self.qkv_w, self.qkv_b, grad_link=l1)  # [T, 3h]
         o = attention_qkv(qkv, B, S, nh, nh, d, causal=False, kv_lens=kv_lens)  # packed QKV gradient in place
-        a = K.linear(o.reshape(B * S, h), self.o_w, self.o_b)
-        x, _ = K.layer_norm(a, self.ln1_g, self.ln1_b, c.eps, residual=x, res_link=l1)
+        a = K.linear(o.reshape(B * S, h), self.o_w, self.o_b, bias_link=b1)
+        x, _ = K.layer_norm(a, self.ln1_g, self.ln1_b, c.eps, residual=x, res_link=l1, bias_link=b1)
         f = K.linear(x, self.f1_w, self.f1_b, act="gelu", grad_link=l2)
-        f = K.linear(f, self.f2_w, self.f2_b)
-        x, _ = K.layer_norm(f, self.ln2_g, self.ln2_b, c.eps, residual=x, res_link=l2)
+        f = K.linear(f, self.f2_w, self.f2_b, bias_link=b2)
+        x, _ = K.layer_norm(f, self.ln2_g, self.ln2_b, c.eps, residual=x, res_link=l2, bias_link=b2)
         return x
 
 

@@ -63,6 +63,16 @@ class GradLink:
         self.shared = shared
 
 
+class BiasLink:
+    """Joins a linear (``linear(..., bias_link=l)``) to the LayerNorm that reads its output (``layer_norm(y, ...,
+    bias_link=l)``): the norm's backward also emits the column sums of the gradient it returns for y -- that
+    linear's bias gradient -- from its parameter-gradient kernel, so the linear skips its column-sum pass."""
+    __slots__ = ("pb", "done")
+
+    def __init__(self):
+        self.pb, self.done = None, False
+
+
 class MaskedGrad:
     """A residual gradient handed over unmaterialised: ``dy`` masked by the packed 1-bit ReLU ``mask`` of the BN
     forward (bit j of byte e = element 8e + j). The 1x1 dgrad that receives it reads the pair in its epilogue
@@ -306,7 +316,7 @@ def batch_norm_act(x, pg, pb, run_mean, run_var, residual=None, relu=True, train
 # =========================================================================== layernorm / rmsnorm
 class _Norm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, anchor, pg, pb, eps, rms, res_link=None):
+    def forward(ctx, x, res, anchor, pg, pb, eps, rms, res_link=None, bias_link=None):
         # an unused second output (x + res) must not get a materialised zero gradient (one [T, D] fill per norm)
         ctx.set_materialize_grads(False)
         x = x.contiguous()
@@ -321,6 +331,7 @@ class _Norm(torch.autograd.Function):
         ctx.save_for_backward(xin, mean, rstd)
         ctx.pg, ctx.pb, ctx.rms, ctx.has_res = pg, pb, rms, res is not None
         ctx.res_link = res_link if res is not None else None
+        ctx.bias_link = bias_link
         if res is not None:
             return y, xsum
         return y, None
@@ -344,10 +355,20 @@ class _Norm(torch.autograd.Function):
             if pb is not None:
                 db = sb.view(pb.shape) if sb is not None else torch.empty(pb.shape, device=xin.device,
                                                                            dtype=torch.float32)
-            dx = _C().norm_bwd(dy, xin, pg.master, mean, rstd, dres, dg, db, ctx.rms)
+            bl = ctx.bias_link
+            lpb = bl.pb if (bl is not None and dres is None) else None
+            dsum = None
+            if lpb is not None:  # the producing linear's bias gradient (column sums of dx) from the same pass
+                ss = store.slot_for_write(lpb) if lpb.store is store else None
+                dsum = ss.view(lpb.shape) if ss is not None else torch.empty(lpb.shape, device=xin.device,
+                                                                             dtype=torch.float32)
+            dx = _C().norm_bwd(dy, xin, pg.master, mean, rstd, dres, dg, db, ctx.rms, dsum=dsum)
             store.mark_written(pg) if sg is not None else store.deposit(pg, dg)
             if pb is not None:
                 store.mark_written(pb) if sb is not None else store.deposit(pb, db)
+            if lpb is not None:
+                lpb.store.mark_written(lpb) if ss is not None else lpb.store.deposit(lpb, dsum)
+                bl.done = True
         else:
             dx, dg, db = ref.norm_bwd(dy, xin, pg.master, mean, rstd, dres, ctx.rms)
             store.deposit(pg, dg)
@@ -364,14 +385,14 @@ class _Norm(torch.autograd.Function):
                 else:  # that linear already ran and handed its dgrad over: form the sum here
                     dres_out = dx + link.grad
                     link.grad = None
-        return dx, dres_out, None, None, None, None, None, None
+        return dx, dres_out, None, None, None, None, None, None, None
 
 
-def layer_norm(x, pg, pb, eps=1e-12, residual=None, res_link=None):
+def layer_norm(x, pg, pb, eps=1e-12, residual=None, res_link=None, bias_link=None):
     """LayerNorm over the last dim; with ``residual`` returns (norm(x+res), x+res). ``res_link`` (a GradLink
     shared with the linear that also reads ``residual``): the two gradient contributions of ``residual`` are
-    summed in that linear's dgrad epilogue instead of by a separate add."""
-    y, xsum = _Norm.apply(x, residual, pg.store.anchor, pg, pb, eps, False, res_link)
+    summed in that linear's dgrad epilogue instead of by a separate add. ``bias_link``: see ``BiasLink``."""
+    y, xsum = _Norm.apply(x, residual, pg.store.anchor, pg, pb, eps, False, res_link, bias_link)
     return (y, xsum) if residual is not None else y
 
 
@@ -389,7 +410,7 @@ def _gemm():
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, anchor, pw, pb, act, grad_link=None):
+    def forward(ctx, x, anchor, pw, pb, act, grad_link=None, bias_link=None):
         g = _gemm()
         w = pw.weight if x.dtype == pw.weight.dtype else pw.master.to(x.dtype)
         x2 = x.reshape(-1, x.shape[-1])
@@ -397,6 +418,9 @@ class _Linear(torch.autograd.Function):
         y, pre = g.linear_fwd(x2, w, b, act)
         ctx.save_for_backward(x2, pre)
         ctx.pw, ctx.pb, ctx.act, ctx.xshape, ctx.grad_link = pw, pb, act, x.shape, grad_link
+        ctx.bias_link = bias_link
+        if bias_link is not None and act is None:
+            bias_link.pb = pb
         return y.reshape(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -411,21 +435,23 @@ class _Linear(torch.autograd.Function):
         if link is not None and link.grad is not None:  # x's other gradient contribution, handed over (GradLink)
             addend = link.grad.reshape(x2.shape)
             link.grad = None
-        dx, dw, db = g.linear_bwd(gy2, x2, w, pre, ctx.act, pw=pw, store=pw.store, need_db=pb is not None,
-                                  dx_addend=addend, pb=pb)
+        db_done = ctx.bias_link is not None and ctx.bias_link.done  # the reading norm produced it
+        dx, dw, db = g.linear_bwd(gy2, x2, w, pre, ctx.act, pw=pw, store=pw.store,
+                                  need_db=pb is not None and not db_done, dx_addend=addend, pb=pb)
         if dw is not None:
             pw.store.deposit(pw, dw)
         if pb is not None and db is not None:  # None: written straight into its slot
             pb.store.deposit(pb, db)
         if link is not None and addend is None:  # ran first: hand dx to the norm backward, which forms the sum
             link.grad = dx.reshape(ctx.xshape)
-            return None, None, None, None, None, None
-        return dx.reshape(ctx.xshape), None, None, None, None, None
+            return None, None, None, None, None, None, None
+        return dx.reshape(ctx.xshape), None, None, None, None, None, None
 
 
-def linear(x, pw, pb=None, act: Optional[str] = None, grad_link=None):
-    """y = act(x @ W^T + b); W [out, in] bf16 from the flat store. ``grad_link``: see ``layer_norm``."""
-    return _Linear.apply(x, pw.store.anchor, pw, pb, act, grad_link)
+def linear(x, pw, pb=None, act: Optional[str] = None, grad_link=None, bias_link=None):
+    """y = act(x @ W^T + b); W [out, in] bf16 from the flat store. ``grad_link``: see ``layer_norm``;
+    ``bias_link``: see ``BiasLink``."""
+    return _Linear.apply(x, pw.store.anchor, pw, pb, act, grad_link, bias_link)
 
 
 # =========================================================================== embedding

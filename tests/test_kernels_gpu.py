@@ -104,6 +104,11 @@ def test_norm_fwd_bwd(cuda, D, rms, res, R):
     _close(dg, dgr, 2e-2)
     if not rms:
         _close(db, dbr, 2e-2)
+    if not res:  # the dx column sums (the producing linear's bias gradient) from the parameter kernel
+        dsum = torch.empty(D, device=cuda)
+        dx2 = _C().norm_bwd(dy, xin, g, mean, rstd, None, dg, db, rms, dsum=dsum)
+        assert torch.equal(dx2, dx)
+        _close(dsum, dxr.float().sum(0), 2e-2)
 
 
 @pytest.mark.parametrize("R,V,dt", [(64, 1000, torch.bfloat16), (8, 30522, torch.bfloat16), (16, 1003, torch.float32),
