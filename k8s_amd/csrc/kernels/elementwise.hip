@@ -153,6 +153,66 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const uint16_t* __r
   }
 }
 
+// Activation backward fused with the column sums of its output (the bias gradient of the linear whose activation
+// it is): g = dy * act'(pre) stored bf16 and summed per column exactly as colsum_partial_kernel sums a stored
+// tensor (ACT 1 ReLU with pre = the ReLU output, 2 GELU(tanh) with pre = the pre-activation).
+template <int ACT>
+__global__ void __launch_bounds__(256) act_bwd_colsum_partial_kernel(const uint16_t* __restrict__ dy,
+                                                                     const uint16_t* __restrict__ pre,
+                                                                     uint16_t* __restrict__ g, long R, int C, long rpb,
+                                                                     float* __restrict__ part) {
+  const int cv = C / 8;
+  const int cg = blockIdx.y * 32 + (threadIdx.x & 31);
+  const int rg = threadIdx.x >> 5;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (cg < cv) {
+    const long r0 = blockIdx.x * rpb;
+    const long r1 = r0 + rpb < R ? r0 + rpb : R;
+    for (long r = r0 + rg; r < r1; r += 32) {
+      float d[4][8], x[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long rr = r + 8 * u < r1 ? r + 8 * u : r1 - 1;
+        load8(dy + rr * C + cg * 8, d[u]);
+        load8(pre + rr * C + cg * 8, x[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float gd;
+          if (ACT == 1) {
+            gd = x[u][j] > 0.f ? 1.f : 0.f;
+          } else {
+            const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+            const float t = tanhf(k0 * (x[u][j] + k1 * x[u][j] * x[u][j] * x[u][j]));
+            gd = 0.5f * (1.f + t) + 0.5f * x[u][j] * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x[u][j] * x[u][j]);
+          }
+          o[j] = d[u][j] * gd;
+        }
+        const bf16x8_t ob = pack_bf16x8(o);
+        if (r + 8 * u < r1) {
+          *reinterpret_cast<bf16x8_t*>(g + (r + 8 * u) * C + cg * 8) = ob;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s[j] += bf2f((uint16_t)ob[j]);
+        }
+      }
+    }
+  }
+  __shared__ float sh[8][32][9];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sh[rg][threadIdx.x & 31][j] = s[j];
+  __syncthreads();
+  if (rg == 0 && cg < cv) {
+    for (int q = 1; q < 8; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += sh[q][threadIdx.x][j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part[(long)blockIdx.x * C + cg * 8 + j] = s[j];
+  }
+}
+
 // fold of the P partial rows: block = 64 columns x 4 partial-row groups (a wave each), LDS combine. P is up to
 // 256 rows of L2-resident partials: 4 waves x P/4 independent loads per lane instead of one lane walking all P.
 __global__ void __launch_bounds__(256) colsum_fold_kernel(const float* __restrict__ part, int P, int C,
@@ -202,6 +262,17 @@ static long colsum_row_blocks(long R) {
   return nb > 256 ? 256 : nb;
 }
 int colsum_workspace_floats(long R, int C) { return (int)(colsum_row_blocks(R) * C); }
+void launch_act_bwd_colsum(int act, const uint16_t* dy, const uint16_t* pre, uint16_t* g, long R, int C, float* work,
+                           float* out, bool accumulate, hipStream_t st) {
+  const long nb = colsum_row_blocks(R);
+  const long rpb = (R + nb - 1) / nb;
+  dim3 grid((unsigned)nb, (unsigned)((C / 8 + 31) / 32));
+  if (act == 1)
+    hipLaunchKernelGGL(act_bwd_colsum_partial_kernel<1>, grid, dim3(256), 0, st, dy, pre, g, R, C, rpb, work);
+  else
+    hipLaunchKernelGGL(act_bwd_colsum_partial_kernel<2>, grid, dim3(256), 0, st, dy, pre, g, R, C, rpb, work);
+  hipLaunchKernelGGL(colsum_fold_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, work, (int)nb, C, out, (int)accumulate);
+}
 void launch_colsum(const uint16_t* x, long R, int C, float* work, float* out, bool accumulate, hipStream_t st) {
   const long nb = colsum_row_blocks(R);
   const long rpb = (R + nb - 1) / nb;

@@ -119,6 +119,9 @@ void launch_gelu_bwd(const uint16_t* dy, const uint16_t* pre, uint16_t* dx, long
 void launch_relu_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n, hipStream_t st);
 int colsum_workspace_floats(long R, int C);
 void launch_colsum(const uint16_t* x, long R, int C, float* work, float* out, bool accumulate, hipStream_t st);
+// g = dy * act'(pre) (1 ReLU, pre = its output; 2 GELU(tanh), pre = the pre-activation) and out = column sums of g
+void launch_act_bwd_colsum(int act, const uint16_t* dy, const uint16_t* pre, uint16_t* g, long R, int C, float* work,
+                           float* out, bool accumulate, hipStream_t st);
 
 // ---- K5 flash attention (attention.hip). q [B,Sq,Hq,D], k/v [B,Sk,Hkv,D] (strided, last dim contiguous)
 struct AttnFwdArgs {

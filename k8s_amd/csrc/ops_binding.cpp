@@ -574,6 +574,29 @@ Tensor colsum(Tensor x, c10::optional<Tensor> out_) {
   return out;
 }
 
+// activation backward + the column sums of its result (a linear's bias gradient); returns [g, db]
+std::vector<Tensor> act_bwd_colsum(Tensor dy, Tensor pre, int64_t act, c10::optional<Tensor> out_) {
+  check_cuda(dy, "dy"); check_cuda(pre, "pre");
+  check_dtype(dy, at::kBFloat16, "dy"); check_dtype(pre, at::kBFloat16, "pre");
+  TORCH_CHECK(act == 1 || act == 2, "act: 1 ReLU, 2 GELU(tanh)");
+  TORCH_CHECK(dy.sizes() == pre.sizes() && dy.is_contiguous() && pre.is_contiguous());
+  const int C = (int)dy.size(-1);
+  TORCH_CHECK(C % 8 == 0);
+  const long R = dy.numel() / C;
+  Tensor out;
+  if (out_) {
+    out = *out_;
+    TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() == C,
+                "act_bwd_colsum out: contiguous fp32 [C]");
+  } else {
+    out = torch::empty({C}, dy.options().dtype(at::kFloat));
+  }
+  auto g = torch::empty_like(dy);
+  auto work = torch::empty({k8s_amd::colsum_workspace_floats(R, C)}, out.options());
+  k8s_amd::launch_act_bwd_colsum((int)act, cbf(dy), cbf(pre), bf(g), R, C, f32(work), f32(out), false, cur_stream());
+  return {g, out};
+}
+
 // ------------------------------------------------------------------ flash attention (K5)
 void check_attn_operand(const Tensor& t, const char* name, long D) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
@@ -820,6 +843,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("rope_", &rope_);
   m.def("gelu_bwd", &gelu_bwd);
+  m.def("act_bwd_colsum", &act_bwd_colsum, py::arg("dy"), py::arg("pre"), py::arg("act"),
+        py::arg("out") = py::none());
   m.def("relu_bwd", &relu_bwd);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none());
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),

@@ -106,10 +106,21 @@ def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True, dx_adden
     ``dx_addend`` (bf16, x's shape): another gradient contribution of x, accumulated in the dgrad epilogue (it is
     overwritten and returned as dx). With ``pb`` the bias gradient goes straight into its flat slot on first use
     (db is then returned as None)."""
-    g = _act_bwd(gy, saved, act)
     M, K = x.shape
     N = w.shape[0]
     db = None
+    if (need_db and act in ("relu", "gelu") and gy.is_cuda and gy.dtype == torch.bfloat16 and N % 8 == 0
+            and saved is not None and saved.dtype == torch.bfloat16):
+        # activation backward and the bias gradient (its column sums) in one pass
+        slot = store.slot_for_write(pb) if (pb is not None and store is not None) else None
+        g, db = _load().act_bwd_colsum(gy.reshape(-1, N).contiguous(), saved.reshape(-1, N).contiguous(), ACT[act],
+                                       slot)
+        if slot is not None:
+            store.mark_written(pb)
+            db = None
+        need_db = False
+    else:
+        g = _act_bwd(gy, saved, act)
     if not need_db:
         pass
     elif g.is_cuda and g.dtype == torch.bfloat16 and N % 8 == 0:

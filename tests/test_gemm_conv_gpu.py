@@ -369,3 +369,20 @@ def test_conv3x3_dgrad_bn_backward_epilogue(cuda):
     assert _rel(dx, ref.permute(0, 2, 3, 1)) < 1e-2
     s_ref, q_ref = _bn_bwd_sums_ref(dx, x, mean, invstd, gamma, beta, None, True)
     assert _rel(reps[:, 0].sum(0), s_ref) < 1e-4 and _rel(reps[:, 1].sum(0), q_ref) < 1e-4
+
+
+@pytest.mark.parametrize("act", [1, 2])
+@pytest.mark.parametrize("R,C", [(8192, 3072), (1000, 776), (37, 64)])
+def test_act_bwd_colsum(cuda, act, R, C):
+    """activation backward fused with its column sums (a linear's bias gradient) vs the separate kernels."""
+    torch.manual_seed(4)
+    dy = torch.randn(R, C, device=cuda).bfloat16()
+    pre = torch.randn(R, C, device=cuda).bfloat16()
+    y = torch.relu(pre) if act == 1 else pre
+    g, db = _C().act_bwd_colsum(dy, y, act)
+    ref = _C().relu_bwd(dy, y) if act == 1 else _C().gelu_bwd(dy, pre)
+    assert torch.equal(g, ref)
+    assert _rel(db, ref.float().sum(0)) < 1e-4
+    out = torch.empty(C, device=cuda)
+    g2, db2 = _C().act_bwd_colsum(dy, y, act, out)
+    assert db2.data_ptr() == out.data_ptr() and torch.equal(db2, db)
