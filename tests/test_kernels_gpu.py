@@ -213,14 +213,16 @@ def test_bn_packed_relu_mask(cuda, C, M, from_sums):
     _close(db2, db1, 1e-4)
 
 
-def test_embedding_sum_gather_and_scatter(cuda):
+@pytest.mark.parametrize("B", [4, 40])  # position rows summed in the tail loop only / in 8-token trips too
+def test_embedding_sum_gather_and_scatter(cuda, B):
     """BERT-style word + position + token-type lookup (embedding.hip) vs torch gathers; the backward's fp32
-    scatter-adds (incl. the 2-row token-type table's register-reduced path) vs index_add_."""
+    scatter-adds (incl. the 2-row token-type table's register-reduced path and the position table's
+    owner-per-row path) vs index_add_."""
     from k8s_amd.ops import nn as K
     from k8s_amd.parallel.flat import ParamStore, init_normal
 
     torch.manual_seed(3)
-    B, S, D, V = 4, 96, 256, 1000
+    S, D, V = 96, 256, 1000
     store = ParamStore()
     word = store.new("word", (V, D), init_normal(0.5))
     pos = store.new("pos", (128, D), init_normal(0.5))
