@@ -125,6 +125,8 @@ __global__ void __launch_bounds__(256) xent_bwd_kernel(const T* __restrict__ log
     if (i == lab) p -= on;
     store1<T>(dx + i, p * sc);
   }
+  // padded columns [V, ld) of the gradient are written here, so the caller never zero-fills the whole matrix
+  for (long i = V + threadIdx.x; i < ld; i += 256) store1<T>(dx + i, 0.f);
 }
 
 void launch_xent_fwd(const void* logits, bool bf16, const int64_t* labels, long R, long V, long ld, float* loss,

@@ -261,7 +261,7 @@ Tensor xent_bwd(Tensor logits, Tensor labels, Tensor lse, Tensor dscale, int64_t
   TORCH_CHECK(V > 0 && V <= Vpad);
   TORCH_CHECK(dscale.numel() == 1 || dscale.numel() == R);
   auto d = dscale.to(at::kFloat).contiguous();
-  auto dl = V == Vpad ? torch::empty({R, Vpad}, logits.options()) : torch::zeros({R, Vpad}, logits.options());
+  auto dl = torch::empty({R, Vpad}, logits.options());  // the kernel zeroes the pad columns itself
   k8s_amd::launch_xent_bwd(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, labels.data_ptr<int64_t>(),
                            f32(lse), f32(d), d.numel() == R, R, V, Vpad, dl.data_ptr(), ignore_index,
                            (float)smoothing, cur_stream());

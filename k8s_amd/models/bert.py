@@ -36,6 +36,9 @@ class BertConfig:
     type_vocab: int = 2
     eps: float = 1e-12
     init_std: float = 0.02
+    # masked-LM slots per sequence (``max_predictions_per_seq`` of the original pretraining data): the MLM head runs
+    # on the gathered masked positions only; 0 = head on every token with dense [B, S] labels
+    max_predictions: int = 20
 
     @property
     def padded_vocab(self) -> int:
@@ -43,7 +46,8 @@ class BertConfig:
 
 
 BERT_BASE = BertConfig()
-BERT_TINY = BertConfig(vocab_size=1000, hidden=128, layers=2, heads=2, intermediate=512, max_position=128)
+BERT_TINY = BertConfig(vocab_size=1000, hidden=128, layers=2, heads=2, intermediate=512, max_position=128,
+                       max_predictions=12)
 
 
 class BertLayer(nn.Module):
@@ -115,7 +119,11 @@ class BertForPreTraining(nn.Module):
         self.store.finalize(device, **kw)
         return self.to(device)
 
-    def forward(self, input_ids, token_type_ids, mlm_labels, nsp_labels, kv_lens=None, dtype=torch.bfloat16):
+    def forward(self, input_ids, token_type_ids, mlm_labels, nsp_labels, mlm_positions=None, kv_lens=None,
+                dtype=torch.bfloat16):
+        """``mlm_positions`` [B, P] (with ``mlm_labels`` [B, P], -100 on unused slots) runs the MLM head on those rows
+        only, as BERT pretraining does (the head's gradient is zero on every unlabelled row, so loss and gradients
+        equal the every-token head's); without it ``mlm_labels`` is dense [B, S]."""
         B, S = input_ids.shape
         c = self.c
         h = c.hidden
@@ -124,8 +132,12 @@ class BertForPreTraining(nn.Module):
         x = K.layer_norm(e.reshape(B * S, h), self.emb_ln_g, self.emb_ln_b, c.eps)
         for layer in self.layers:
             x = layer(x, B, S, kv_lens)
-        # MLM head on every token (labels -100 are ignored by the loss kernel)
-        t = K.linear(x, self.mlm_w, self.mlm_b, act="gelu")
+        if mlm_positions is not None:
+            rows = (mlm_positions + torch.arange(B, device=x.device).unsqueeze(1) * S).reshape(-1)
+            xm = x.index_select(0, rows)  # [B * P, h]; backward scatters into the encoder output gradient
+        else:
+            xm = x  # MLM head on every token (labels -100 are ignored by the loss kernel)
+        t = K.linear(xm, self.mlm_w, self.mlm_b, act="gelu")
         t = K.layer_norm(t, self.mlm_ln_g, self.mlm_ln_b, c.eps)
         logits = K.linear(t, self.word, self.dec_b)  # tied decoder, [T, padded_vocab]
         mlm = K.cross_entropy(logits, mlm_labels.reshape(-1), valid=c.vocab_size)
@@ -138,11 +150,33 @@ class BertForPreTraining(nn.Module):
 
 
 def synthetic_batch(c: BertConfig, batch: int, seq: int, device, generator=None, mask_prob=0.15):
+    """Random pretraining batch. With ``c.max_predictions`` it has the original data format: per sequence
+    min(max_predictions, max(1, round(seq * mask_prob))) masked positions (sorted, never [CLS] at 0), padded to
+    max_predictions slots with position 0 / label -100; returns (ids, token_types, labels [B, P], nsp, positions).
+    Otherwise a Bernoulli mask with dense labels [B, S]; returns (ids, token_types, labels, nsp)."""
     g = generator
     ids = torch.randint(0, c.vocab_size, (batch, seq), device=device, generator=g)
     tt = torch.zeros(batch, seq, dtype=torch.long, device=device)
     tt[:, seq // 2:] = 1
+    nsp = torch.randint(0, 2, (batch,), device=device, generator=g)
+    if c.max_predictions:
+        P = c.max_predictions
+        n = min(P, max(1, int(round(seq * mask_prob))), seq - 1)
+        pick = torch.rand(batch, seq - 1, device=device, generator=g).argsort(dim=1)[:, :n] + 1
+        pos = torch.zeros(batch, P, dtype=torch.long, device=device)
+        pos[:, :n] = pick.sort(dim=1).values
+        labels = torch.full((batch, P), -100, dtype=torch.long, device=device)
+        labels[:, :n] = ids.gather(1, pos[:, :n])
+        return ids, tt, labels, nsp, pos
     sel = torch.rand(batch, seq, device=device, generator=g) < mask_prob
     labels = torch.where(sel, ids, torch.full_like(ids, -100))
-    nsp = torch.randint(0, 2, (batch,), device=device, generator=g)
     return ids, tt, labels, nsp
+
+
+def dense_mlm_labels(labels, positions, seq: int):
+    """[B, P] slot labels at ``positions`` -> dense [B, S] labels (-100 elsewhere), for every-token references."""
+    B = labels.shape[0]
+    out = torch.full((B, seq), -100, dtype=labels.dtype, device=labels.device)
+    keep = labels != -100
+    out[torch.arange(B, device=labels.device).unsqueeze(1).expand_as(labels)[keep], positions[keep]] = labels[keep]
+    return out

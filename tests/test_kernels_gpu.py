@@ -129,6 +129,24 @@ def test_xent(cuda, R, V, dt, smooth):
     _close(d, dr, 2e-2 if dt == torch.bfloat16 else 1e-5)
 
 
+def test_xent_padded_vocab(cuda):
+    """logits [R, Vpad] with the classes in the first V columns: the gradient's pad columns come back zero even when
+    the output buffer starts as garbage (the binding allocates it uninitialised)."""
+    torch.manual_seed(5)
+    R, V, Vpad = 32, 30522, 30528
+    full = (torch.randn(R, Vpad, device=cuda) * 4).bfloat16()
+    lab = torch.randint(0, V, (R,), device=cuda)
+    loss, lse = _C().xent_fwd(full[:, :V], lab, -100, 0.0)
+    _, lser = ref.xent_fwd(full[:, :V].contiguous(), lab, -100, 0.0)
+    _close(lse, lser, 1e-4)
+    ds = torch.tensor([1.0], device=cuda)
+    torch.full((R * Vpad * 4,), float("nan"), device=cuda)  # dirty the caching allocator's free blocks
+    d = _C().xent_bwd(full, lab, lse, ds, -100, 0.0, V)
+    assert d.shape == (R, Vpad)
+    assert torch.equal(d[:, V:], torch.zeros_like(d[:, V:]))
+    _close(d[:, :V], ref.xent_bwd(full[:, :V].contiguous(), lab, lser, ds, -100, 0.0), 2e-2)
+
+
 @pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("nesterov", [False, True])
 def test_fused_sgd(cuda, gdt, nesterov):

@@ -144,21 +144,30 @@ def _bert_twin(m, store, ids, tt, mlm_labels, nsp_labels, kv_lens, autocast):
     return loss.item(), {k: v.grad for k, v in P.items()}
 
 
-def test_bert_tiny_gradients_match_fp32_twin(cuda):
-    from k8s_amd.models.bert import BERT_TINY, BertForPreTraining, synthetic_batch
+@pytest.mark.parametrize("gathered", [True, False])
+def test_bert_tiny_gradients_match_fp32_twin(cuda, gathered):
+    """gathered: MLM head on the masked-position slots (pretraining data format); the twin runs the head on every
+    token with the equivalent dense labels, so the two must agree on loss and every gradient."""
+    import dataclasses
+
+    from k8s_amd.models.bert import BERT_TINY, BertForPreTraining, dense_mlm_labels, synthetic_batch
     from k8s_amd.parallel.flat import ParamStore
 
     torch.manual_seed(0)
+    cfg = BERT_TINY if gathered else dataclasses.replace(BERT_TINY, max_predictions=0)
     store = ParamStore()
-    m = BertForPreTraining(store, BERT_TINY).finalize(cuda, seed=11)
+    m = BertForPreTraining(store, cfg).finalize(cuda, seed=11)
     g = torch.Generator(device=cuda).manual_seed(4)
-    ids, tt, labels, nsp = synthetic_batch(BERT_TINY, 4, 128, cuda, generator=g, mask_prob=0.3)
+    batch = synthetic_batch(cfg, 4, 128, cuda, generator=g, mask_prob=0.3 if not gathered else 0.08)
+    ids, tt, labels, nsp = batch[:4]
+    pos = batch[4] if gathered else None
+    dense = dense_mlm_labels(labels, pos, 128) if gathered else labels
     kv_lens = torch.tensor([128, 100, 64, 128], device=cuda, dtype=torch.int32)
     store.begin_step()
-    loss, _, _ = m(ids, tt, labels, nsp, kv_lens=kv_lens)
+    loss, _, _ = m(ids, tt, labels, nsp, pos, kv_lens=kv_lens)
     loss.backward()
     store.zero_unwritten()
-    ref_loss, ref = _bert_twin(m, store, ids, tt, labels, nsp, kv_lens, autocast=False)
-    _, stock = _bert_twin(m, store, ids, tt, labels, nsp, kv_lens, autocast=True)
+    ref_loss, ref = _bert_twin(m, store, ids, tt, dense, nsp, kv_lens, autocast=False)
+    _, stock = _bert_twin(m, store, ids, tt, dense, nsp, kv_lens, autocast=True)
     # padded key rows of the [CLS]-only NSP head see no gradient in either path; pad decoder columns neither
     _check(store, loss.float().item(), ref_loss, ref, stock)
