@@ -44,6 +44,10 @@ __device__ __forceinline__ int v_swz(int r) {
   return D == 128 ? mn_swz(r) : (mn_swz(r) & 7);
 }
 
+// 2^x on v_exp_f32 alone: exp2f adds a denormal-range rescale (compare, select, ldexp) around every call;
+// softmax probabilities below 2^-126 flush to zero, and -inf still gives 0
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // XCD-aware bijective remap of a linear block id (blocks sharing K/V land on the same XCD / L2)
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
@@ -180,13 +184,13 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
         const float mn = fmaxf(m[qs], mx);
-        const float alpha = exp2f(m[qs] - mn);
+        const float alpha = fexp2(m[qs] - mn);
         float rs = 0.f;
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float p = exp2f(s[i][qs][r] - mn);
+            const float p = fexp2(s[i][qs][r] - mn);
             s[i][qs][r] = p;
             rs += p;
           }
@@ -379,7 +383,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
         for (int r = 0; r < 4; ++r) {
           const int qi = q0 + qs * 16 + g * 4 + r;
           const bool ok = qi < a.Sq && key < kv_end && !(a.causal && key > qi + off);
-          const float p = ok ? exp2f(sv[qs][r] * a.scale_log2 - l4[r]) : 0.f;
+          const float p = ok ? fexp2(sv[qs][r] * a.scale_log2 - l4[r]) : 0.f;
           sv[qs][r] = p;
           dp[qs][r] = ok ? p * (dp[qs][r] - d4[r]) : 0.f;  // padded rows of lse / delta are uninitialised
         }
@@ -522,7 +526,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dq_kernel(AttnBwdArgs
             const int key = key0 + i * 16 + g * 4 + r;
             ok = key < kv_end && !(a.causal && key > qi + off);
           }
-          const float p = ok ? exp2f(s[i][r] * a.scale_log2 - lq) : 0.f;
+          const float p = ok ? fexp2(s[i][r] * a.scale_log2 - lq) : 0.f;
           dp[i][r] = p * (dp[i][r] - dq_);
         }
 #pragma unroll
