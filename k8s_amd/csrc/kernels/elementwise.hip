@@ -10,7 +10,12 @@
 
 namespace k8s_amd {
 
-__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+__device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+// tanh(u) = 1 - 2 / (1 + 2^(2u log2 e)) on v_exp_f32 / v_rcp_f32 (libm tanhf is a long polynomial + branch path);
+// saturates to +-1 for large |u|, absolute error ~1e-7 near 0
+__device__ __forceinline__ float ftanh(float u) {
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(2.8853900817779268f * u));
+}
 
 // gu: [T, 2F] (gate in [:, :F], up in [:, F:]) -> y: [T, F]
 __global__ void __launch_bounds__(256) swiglu_fwd_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ y,
@@ -44,7 +49,7 @@ __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restr
     load8(dy + t * F + c, d);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float s = 1.f / (1.f + __expf(-g[j]));
+      const float s = __builtin_amdgcn_rcpf(1.f + __expf(-g[j]));
       const float sl = g[j] * s;
       du[j] = d[j] * sl;
       dg[j] = d[j] * u[j] * (s * (1.f + g[j] * (1.f - s)));
@@ -93,7 +98,7 @@ __global__ void __launch_bounds__(256) gelu_bwd_kernel(const uint16_t* __restric
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float u = k0 * (x[j] + k1 * x[j] * x[j] * x[j]);
-      const float t = tanhf(u);
+      const float t = ftanh(u);
       const float g = 0.5f * (1.f + t) + 0.5f * x[j] * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x[j] * x[j]);
       d[j] *= g;
     }
@@ -186,7 +191,7 @@ __global__ void __launch_bounds__(256) act_bwd_colsum_partial_kernel(const uint1
             gd = x[u][j] > 0.f ? 1.f : 0.f;
           } else {
             const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-            const float t = tanhf(k0 * (x[u][j] + k1 * x[u][j] * x[u][j] * x[u][j]));
+            const float t = ftanh(k0 * (x[u][j] + k1 * x[u][j] * x[u][j] * x[u][j]));
             gd = 0.5f * (1.f + t) + 0.5f * x[u][j] * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x[u][j] * x[u][j]);
           }
           o[j] = d[u][j] * gd;
