@@ -58,6 +58,60 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint16_t* __rest
   *reinterpret_cast<uint64_t*>(idx + (long)e * 8) = packed;
 }
 
+// k x k window known at compile time (the stem's 3 x 3): all k*k input vectors are loaded up front (clamped
+// in-bounds addresses, out-of-image taps masked afterwards) so the loads are in flight together instead of one
+// load -> compare round trip per tap; taps are compared in the same (dh, dw) order, so ties pick the same winner
+template <int K>
+__global__ void __launch_bounds__(256) maxpool_fwd_k_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                            uint8_t* __restrict__ idx, int H, int W, int C, int Ho,
+                                                            int Wo, int s, int p, int total, FastDiv fcv, FastDiv fWo,
+                                                            FastDiv fHo) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= total) return;
+  const int cv = C >> 3;
+  int t = fcv.div(e);
+  const int c = (e - t * cv) * 8;
+  int t2 = fWo.div(t);
+  const int wo = t - t2 * Wo;
+  const int n = fHo.div(t2);
+  const int ho = t2 - n * Ho;
+  const int h0 = ho * s - p, w0 = wo * s - p;
+  float v[K * K][8];
+#pragma unroll
+  for (int dh = 0; dh < K; ++dh)
+#pragma unroll
+    for (int dw = 0; dw < K; ++dw) {
+      const int h = min(max(h0 + dh, 0), H - 1), w = min(max(w0 + dw, 0), W - 1);
+      load8(x + (((long)n * H + h) * W + w) * C + c, v[dh * K + dw]);
+    }
+  float best[8];
+  uint8_t arg[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    best[j] = -INFINITY;
+    arg[j] = 255;
+  }
+#pragma unroll
+  for (int dh = 0; dh < K; ++dh)
+#pragma unroll
+    for (int dw = 0; dw < K; ++dw) {
+      if ((unsigned)(h0 + dh) >= (unsigned)H || (unsigned)(w0 + dw) >= (unsigned)W) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float u = v[dh * K + dw][j];
+        if (u > best[j] || (u != u && best[j] == best[j])) {  // NaN propagates like torch
+          best[j] = u;
+          arg[j] = (uint8_t)(dh * K + dw);
+        }
+      }
+    }
+  store8(y + (long)e * 8, best);
+  uint64_t packed = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) packed |= (uint64_t)arg[j] << (8 * j);
+  *reinterpret_cast<uint64_t*>(idx + (long)e * 8) = packed;
+}
+
 __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const uint16_t* __restrict__ dy,
                                                           const uint8_t* __restrict__ idx, uint16_t* __restrict__ dx,
                                                           int H, int W, int C, int Ho, int Wo, int k, int s, int p,
@@ -182,6 +236,11 @@ void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int
                         int k, int s, int p, hipStream_t st) {
   const long total = (long)N * Ho * Wo * (C / 8);
   if ((long)N * H * W * C / 8 >= (1L << 31)) throw std::runtime_error("maxpool: tensor too large for 32-bit indexing");
+  if (k == 3) {
+    hipLaunchKernelGGL(maxpool_fwd_k_kernel<3>, dim3(cdiv(total, 256)), dim3(256), 0, st, x, y, idx, H, W, C, Ho, Wo,
+                       s, p, (int)total, make_fastdiv(C / 8), make_fastdiv(Wo), make_fastdiv(Ho));
+    return;
+  }
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, x, y, idx, H, W, C, Ho, Wo, k, s,
                      p, (int)total, make_fastdiv(C / 8), make_fastdiv(Wo), make_fastdiv(Ho));
 }
