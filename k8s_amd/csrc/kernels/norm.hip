@@ -30,6 +30,22 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(const uint16_t* __restric
   if (row >= R) return;
   const int nch = D / 8;
   float v[CPL][8];
+  // the affine parameters are loaded with the row (in flight together) rather than after the two reductions,
+  // where they were a dependent L2 round trip at the end of every wave (one wave per row = a single round of waves);
+  // rows of up to 2048 only: at CPL 8 the extra 64-128 registers would cost waves per SIMD
+  constexpr bool kPre = CPL <= 4;
+  float gm[kPre ? CPL : 1][8], bt[kPre ? CPL : 1][8];
+  if constexpr (kPre) {
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int cc = min(lane + c * 64, nch - 1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        gm[c][j] = gamma[cc * 8 + j];
+        bt[c][j] = RMS ? 0.f : beta[cc * 8 + j];
+      }
+    }
+  }
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
@@ -76,8 +92,12 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(const uint16_t* __restric
       float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int k = ch * 8 + j;
-        o[j] = (v[c][j] - mean) * rstd * gamma[k] + (RMS ? 0.f : beta[k]);
+        if constexpr (kPre) {
+          o[j] = (v[c][j] - mean) * rstd * gm[c][j] + bt[c][j];
+        } else {
+          const int k = ch * 8 + j;
+          o[j] = (v[c][j] - mean) * rstd * gamma[k] + (RMS ? 0.f : beta[k]);
+        }
       }
       store8(y + row * D + ch * 8, o);
     }
@@ -105,13 +125,15 @@ __global__ void __launch_bounds__(256) norm_bwd_dx_kernel(const uint16_t* __rest
   const long row = (long)blockIdx.x * NORM_WAVES + (threadIdx.x >> 6);
   if (row >= R) return;
   const int nch = D / 8;
-  bf16x8_t gr[CPL], xr[CPL];
+  bf16x8_t gr[CPL], xr[CPL], rr[CPL];
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
     const int ch = lane + c * 64;
     const int cc = ch < nch ? ch : nch - 1;  // clamped (unused) load instead of a branch per chunk
     gr[c] = *reinterpret_cast<const bf16x8_t*>(dy + row * D + cc * 8);
     xr[c] = *reinterpret_cast<const bf16x8_t*>(x + row * D + cc * 8);
+    // the residual gradient addend too: loaded after the reductions it was a dependent round trip per wave
+    if (dres) rr[c] = *reinterpret_cast<const bf16x8_t*>(dres + row * D + cc * 8);
   }
   const float mu = RMS ? 0.f : mean[row];
   const float rs = rstd[row];
@@ -145,10 +167,8 @@ __global__ void __launch_bounds__(256) norm_bwd_dx_kernel(const uint16_t* __rest
         o[j] = rs * (bf2f((uint16_t)gr[c][j]) * gamma[ch * 8 + j] - (RMS ? 0.f : a) - xn * b);
       }
       if (dres) {
-        float r[8];
-        load8(dres + row * D + ch * 8, r);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] += r[j];
+        for (int j = 0; j < 8; ++j) o[j] += bf2f((uint16_t)rr[c][j]);
       }
       store8(dx + row * D + ch * 8, o);
     }
