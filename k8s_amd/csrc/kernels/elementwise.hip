@@ -18,45 +18,43 @@ __device__ __forceinline__ float ftanh(float u) {
 }
 
 // gu: [T, 2F] (gate in [:, :F], up in [:, F:]) -> y: [T, F]
+// Flat launches, one 16-B vector per thread: grid (T rows, F/8 / 256 column blocks), so no 64-bit index division
+// (the former grid-stride form divided by F/8 per vector)
 __global__ void __launch_bounds__(256) swiglu_fwd_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ y,
                                                          long T, int F) {
-  const int fv = F / 8;
-  const long total = T * fv;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const long t = e / fv;
-    const int c = (int)(e - t * fv) * 8;
-    float g[8], u[8], o[8];
-    load8(gu + t * 2 * F + c, g);
-    load8(gu + t * 2 * F + F + c, u);
+  const int cvec = blockIdx.y * 256 + threadIdx.x;
+  if (cvec >= F / 8) return;
+  const long t = blockIdx.x;
+  const int c = cvec * 8;
+  float g[8], u[8], o[8];
+  load8(gu + t * 2 * F + c, g);
+  load8(gu + t * 2 * F + F + c, u);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = silu(g[j]) * u[j];
-    store8(y + t * F + c, o);
-  }
+  for (int j = 0; j < 8; ++j) o[j] = silu(g[j]) * u[j];
+  store8(y + t * F + c, o);
 }
 
 // dgu[:, :F] = dy * u * silu'(g),  dgu[:, F:] = dy * silu(g)
 __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restrict__ gu,
                                                          const uint16_t* __restrict__ dy, uint16_t* __restrict__ dgu,
                                                          long T, int F) {
-  const int fv = F / 8;
-  const long total = T * fv;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const long t = e / fv;
-    const int c = (int)(e - t * fv) * 8;
-    float g[8], u[8], d[8], dg[8], du[8];
-    load8(gu + t * 2 * F + c, g);
-    load8(gu + t * 2 * F + F + c, u);
-    load8(dy + t * F + c, d);
+  const int cvec = blockIdx.y * 256 + threadIdx.x;
+  if (cvec >= F / 8) return;
+  const long t = blockIdx.x;
+  const int c = cvec * 8;
+  float g[8], u[8], d[8], dg[8], du[8];
+  load8(gu + t * 2 * F + c, g);
+  load8(gu + t * 2 * F + F + c, u);
+  load8(dy + t * F + c, d);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float s = __builtin_amdgcn_rcpf(1.f + __expf(-g[j]));
-      const float sl = g[j] * s;
-      du[j] = d[j] * sl;
-      dg[j] = d[j] * u[j] * (s * (1.f + g[j] * (1.f - s)));
-    }
-    store8(dgu + t * 2 * F + c, dg);
-    store8(dgu + t * 2 * F + F + c, du);
+  for (int j = 0; j < 8; ++j) {
+    const float s = __builtin_amdgcn_rcpf(1.f + __expf(-g[j]));
+    const float sl = g[j] * s;
+    du[j] = d[j] * sl;
+    dg[j] = d[j] * u[j] * (s * (1.f + g[j] * (1.f - s)));
   }
+  store8(dgu + t * 2 * F + c, dg);
+  store8(dgu + t * 2 * F + F + c, du);
 }
 
 // x: [T, H, D] bf16 (row stride ld elements between tokens), pos: [T] int32, table: [maxpos, D/2] (cos, sin)
@@ -244,10 +242,10 @@ __global__ void __launch_bounds__(256) colsum_fold_kernel(const float* __restric
 
 // ----------------------------------------------------------------------------- launchers
 void launch_swiglu_fwd(const uint16_t* gu, uint16_t* y, long T, int F, hipStream_t st) {
-  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(stream_grid(T * F / 8, 256)), dim3(256), 0, st, gu, y, T, F);
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(T, cdiv(F / 8, 256)), dim3(256), 0, st, gu, y, T, F);
 }
 void launch_swiglu_bwd(const uint16_t* gu, const uint16_t* dy, uint16_t* dgu, long T, int F, hipStream_t st) {
-  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(stream_grid(T * F / 8, 256)), dim3(256), 0, st, gu, dy, dgu, T, F);
+  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(T, cdiv(F / 8, 256)), dim3(256), 0, st, gu, dy, dgu, T, F);
 }
 void launch_rope(uint16_t* x, long ld, const int* pos, const float* table, long T, int H, int D, bool inverse,
                  hipStream_t st) {

@@ -146,11 +146,12 @@ def test_conv_fwd_bn_stats_epilogue(cuda, case):
     assert _rel(tot[1], (yf * yf).sum(0)) < 1e-3
 
 
-def test_elementwise_kernels(cuda):
+@pytest.mark.parametrize("F2", [2 * 256, 2 * 2056])
+def test_elementwise_kernels(cuda, F2):
     from k8s_amd.ops import nn as K
 
     torch.manual_seed(8)
-    T, F2 = 96, 2 * 256
+    T = 96
     gu = torch.randn(T, F2, device=cuda).bfloat16()
     y = _C().swiglu_fwd(gu)
     g, u = gu.float().split(F2 // 2, -1)
