@@ -222,6 +222,7 @@ std::string Controller::run() {
       if (const Json* m = obj->find("metadata")) rv = get_str(*m, "resourceVersion");
       // panicTimer: armed while the handler runs; the watchdog thread aborts a wedged handler
       handler_started_ns_ = std::chrono::steady_clock::now().time_since_epoch().count();
+      if (opts_.inject_handler_stall.count() > 0) std::this_thread::sleep_for(opts_.inject_handler_stall);
       handle_event(type, *obj);
       handler_started_ns_ = 0;
     }

@@ -30,6 +30,7 @@ struct ControllerOptions {
   std::chrono::milliseconds crd_poll{500};
   std::chrono::milliseconds crd_timeout{60000};
   std::chrono::milliseconds event_watchdog{60000};  // panicTimer: abort if one event takes longer
+  std::chrono::milliseconds inject_handler_stall{0};  // fault injection: every event handler sleeps this long
   bool create_crd = true;
 };
 

@@ -74,6 +74,7 @@ int main(int argc, char** argv) {
   fl.def("leader-elect-resource-lock", "leases", "Leader-election lock: leases (coordination.k8s.io/v1) or endpoints");
   fl.def("request-timeout", "30s", "Deadline of every API request (connect, TLS handshake, response)");
   fl.def("event-watchdog", "60s", "Abort when one TfJob event handler runs longer (reference panicTimer: 1m)");
+  fl.def("inject-handler-stall", "0s", "DO NOT USE IN PRODUCTION - fault injection: stall every TfJob event handler this long");
   std::string err = fl.parse(argc, argv);
   if (!err.empty()) {
     fprintf(stderr, "%s\nUsage of tf_operator:\n%s", err.c_str(), fl.usage().c_str());
@@ -130,6 +131,7 @@ int main(int argc, char** argv) {
   opts.create_crd = fl.on("create-crd");
   opts.reconcile.interval = std::chrono::milliseconds(parse_duration_ms(fl.str("reconcile-interval"), 8000));
   opts.event_watchdog = std::chrono::milliseconds(parse_duration_ms(fl.str("event-watchdog"), 60000));
+  opts.inject_handler_stall = std::chrono::milliseconds(parse_duration_ms(fl.str("inject-handler-stall"), 0));
   if (!cfg.grpc_server_file_path.empty()) {
     try {
       opts.reconcile.ps_server_source = read_file(cfg.grpc_server_file_path);

@@ -217,3 +217,23 @@ def test_kubeconfig_inline_credentials(tmp_path):
     tf.write_text("file-token\n")
     kc["users"][0]["user"] = {"tokenFile": str(tf)}
     assert _op().kubeconfig(json.dumps(kc))["token"] == "file-token"
+
+
+@needs_op
+def test_panic_timer_aborts_a_wedged_event_handler():
+    """The reference's panicTimer (pkg/controller/util.go:50-76) fires while the handler is still running: with every
+    event handler stalled (fault injection) past -event-watchdog, the operator aborts instead of hanging; a stall
+    below the limit is tolerated and the job still runs to completion."""
+    with LocalCluster(operator_args=["-leader-elect=false", "-event-watchdog", "2s",
+                                     "-inject-handler-stall", "100ms"]) as c:
+        c.create(_job("slowhandler", "exit 0"))
+        assert _wait(lambda: c.get("slowhandler").get("status", {}).get("phase") == "Done", 30), c.operator_log()[-2000:]
+        assert c.op_proc.poll() is None and "panicTimer" not in c.operator_log()
+    with LocalCluster(operator_args=["-leader-elect=false", "-event-watchdog", "300ms",
+                                     "-inject-handler-stall", "5s"]) as c:
+        t0 = time.time()
+        c.create(_job("wedged", "exit 0"))
+        assert _wait(lambda: c.op_proc.poll() is not None, 10), "operator still running with a wedged handler"
+        assert time.time() - t0 < 4.0  # aborted while the 5 s stall was still in progress
+        assert c.op_proc.returncode in (-6, 134), c.op_proc.returncode
+        assert "panicTimer" in c.operator_log()
