@@ -168,29 +168,28 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
 #pragma unroll
       for (int qs = 0; qs < 2; ++qs) {
         const int qi = q0w + qs * 16 + li;
+        // max over the raw scores (scale_log2 > 0 commutes with max), the scale folded into the exponent's fma
         float mx = -INFINITY;
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float x = s[i][qs][r] * a.scale_log2;
             if (need_mask) {
               const int key = key0 + i * 16 + g * 4 + r;
-              if (key >= kv_end || (a.causal && key > qi + off)) x = -INFINITY;
+              if (key >= kv_end || (a.causal && key > qi + off)) s[i][qs][r] = -INFINITY;
             }
-            s[i][qs][r] = x;
-            mx = fmaxf(mx, x);
+            mx = fmaxf(mx, s[i][qs][r]);
           }
         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mn = fmaxf(m[qs], mx);
+        const float mn = fmaxf(m[qs], mx * a.scale_log2);
         const float alpha = fexp2(m[qs] - mn);
         float rs = 0.f;
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float p = fexp2(s[i][qs][r] - mn);
+            const float p = fexp2(fmaf(s[i][qs][r], a.scale_log2, -mn));
             s[i][qs][r] = p;
             rs += p;
           }
