@@ -194,11 +194,14 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
             rs += p;
           }
         l[qs] = l[qs] * alpha + rs;
+        // rescale only when some row's running max moved (wave-uniform branch; late key tiles rarely move it)
+        if (__any(mn != m[qs])) {
+#pragma unroll
+          for (int d = 0; d < ND; ++d)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) oacc[d][qs][r] *= alpha;
+        }
         m[qs] = mn;
-#pragma unroll
-        for (int d = 0; d < ND; ++d)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) oacc[d][qs][r] *= alpha;
       }
       // ---- O^T += V^T P^T (k = keys in the permuted order of the S^T accumulators)
 #pragma unroll
