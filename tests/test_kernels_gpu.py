@@ -231,8 +231,9 @@ def test_bn_packed_relu_mask(cuda, C, M, from_sums):
     _close(db2, db1, 1e-4)
 
 
-@pytest.mark.parametrize("B", [4, 40])  # position rows summed in the tail loop only / in 8-token trips too
-def test_embedding_sum_gather_and_scatter(cuda, B):
+# position rows summed in the tail loop only / in 8-token trips too; 150 tokens: a partial token run
+@pytest.mark.parametrize("B,S", [(4, 96), (40, 96), (3, 50)])
+def test_embedding_sum_gather_and_scatter(cuda, B, S):
     """BERT-style word + position + token-type lookup (embedding.hip) vs torch gathers; the backward's fp32
     scatter-adds (incl. the 2-row token-type table's register-reduced path and the position table's
     owner-per-row path) vs index_add_."""
@@ -240,7 +241,7 @@ def test_embedding_sum_gather_and_scatter(cuda, B):
     from k8s_amd.parallel.flat import ParamStore, init_normal
 
     torch.manual_seed(3)
-    S, D, V = 96, 256, 1000
+    D, V = 256, 1000
     store = ParamStore()
     word = store.new("word", (V, D), init_normal(0.5))
     pos = store.new("pos", (128, D), init_normal(0.5))
