@@ -16,6 +16,8 @@ void launch_adam(float* p, float* m1, float* m2, const void* g, bool g_bf16, uin
                  const float* hyper, float bc1, float bc2, bool decoupled, hipStream_t st);
 void launch_sumsq(const void* g, bool g_bf16, long n, float* out, hipStream_t st);
 void launch_clip_factor(const float* stats, float max_norm, float* factor, hipStream_t st);
+void launch_slice_sum(const uint16_t* in, long n, int world, float* out, uint16_t* out_bf, hipStream_t st);
+void launch_cast_bf16(const float* in, uint16_t* out, long n, hipStream_t st);
 
 // batchnorm.hip
 int bn_workspace_floats(long M, int C);

@@ -175,7 +175,64 @@ __global__ void clip_factor_kernel(const float* __restrict__ stats, float max_no
   factor[0] = f;
 }
 
+// ---------------------------------------------------------------- bf16 gradient transport (parallel/ddp.py, ps.py)
+// Sum of the `world` bf16 chunks [world][n] an all-to-all delivered for one gradient bucket, in rank order with fp32
+// accumulation (deterministic, the same sum on every owner), into fp32 `out` (the owner's gradient slice) and/or
+// bf16 `out_bf` (the reduced slice an all-gather returns to every rank). One pass, 16-B loads: replaces
+// recv.float().sum(0).to(bf16) (an fp32 copy of the whole receive buffer plus two more passes).
+__global__ void __launch_bounds__(256) slice_sum_kernel(const uint16_t* __restrict__ in, long n, int world,
+                                                        float* __restrict__ out, uint16_t* __restrict__ out_bf) {
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q * 8 < n; q += (long)gridDim.x * blockDim.x) {
+    const long i = q * 8;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (i + 8 <= n && (n & 7) == 0) {
+      for (int r = 0; r < world; ++r) {
+        const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(in + (long)r * n + i);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += bf2f((uint16_t)v[j]);
+      }
+      if (out) {
+        *reinterpret_cast<float4*>(out + i) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        *reinterpret_cast<float4*>(out + i + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+      }
+      if (out_bf) *reinterpret_cast<bf16x8_t*>(out_bf + i) = pack_bf16x8(acc);
+    } else {  // ragged slice length: element by element
+      for (int j = 0; j < 8 && i + j < n; ++j) {
+        float a = 0.f;
+        for (int r = 0; r < world; ++r) a += bf2f(in[(long)r * n + i + j]);
+        if (out) out[i + j] = a;
+        if (out_bf) out_bf[i + j] = f2bf(a);
+      }
+    }
+  }
+}
+
+// fp32 -> bf16 (round to nearest even) of a gradient bucket before the all-to-all, 16-B stores
+__global__ void __launch_bounds__(256) cast_bf16_kernel(const float* __restrict__ in, uint16_t* __restrict__ out,
+                                                        long n) {
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q * 8 < n; q += (long)gridDim.x * blockDim.x) {
+    const long i = q * 8;
+    if (i + 8 <= n && (n & 7) == 0) {
+      const float4 a = *reinterpret_cast<const float4*>(in + i), b = *reinterpret_cast<const float4*>(in + i + 4);
+      const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      *reinterpret_cast<bf16x8_t*>(out + i) = pack_bf16x8(v);
+    } else {
+      for (int j = 0; j < 8 && i + j < n; ++j) out[i + j] = f2bf(in[i + j]);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- launchers
+void launch_slice_sum(const uint16_t* in, long n, int world, float* out, uint16_t* out_bf, hipStream_t st) {
+  const int grid = stream_grid((n + 7) / 8, 256);
+  hipLaunchKernelGGL(slice_sum_kernel, dim3(grid), dim3(256), 0, st, in, n, world, out, out_bf);
+}
+
+void launch_cast_bf16(const float* in, uint16_t* out, long n, hipStream_t st) {
+  const int grid = stream_grid((n + 7) / 8, 256);
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid), dim3(256), 0, st, in, out, n);
+}
+
 void launch_sgd(float* p, float* mom, const void* g, bool g_bf16, uint16_t* pbf, long n, const uint8_t* decay_mask,
                 float lr, float mu, float wd, float scale, const float* scale_ptr, const float* hyper, bool nesterov,
                 bool first_step, hipStream_t st) {

@@ -96,6 +96,38 @@ Tensor clip_factor(Tensor stats, double max_norm) {
   return f;
 }
 
+// ------------------------------------------------------------------ bf16 gradient transport
+// recv: bf16 [world * n] (all-to-all receive buffer of one bucket) -> fp32 out [n] and/or bf16 out_bf [n]
+void slice_sum(Tensor recv, int64_t world, c10::optional<Tensor> out, c10::optional<Tensor> out_bf) {
+  check_cuda(recv, "recv"); check_dtype(recv, at::kBFloat16, "recv");
+  TORCH_CHECK(recv.is_contiguous() && world > 0 && recv.numel() % world == 0, "recv must be [world * n]");
+  const long n = recv.numel() / world;
+  float* o = nullptr;
+  uint16_t* ob = nullptr;
+  if (out && out->defined()) {
+    check_dtype(*out, at::kFloat, "out");
+    TORCH_CHECK(out->is_contiguous() && out->numel() == n, "out must be [n] fp32");
+    o = f32(*out);
+  }
+  if (out_bf && out_bf->defined()) {
+    check_dtype(*out_bf, at::kBFloat16, "out_bf");
+    TORCH_CHECK(out_bf->is_contiguous() && out_bf->numel() == n, "out_bf must be [n] bf16");
+    ob = reinterpret_cast<uint16_t*>(out_bf->data_ptr());
+  }
+  TORCH_CHECK(o || ob, "slice_sum: no output");
+  k8s_amd::launch_slice_sum(reinterpret_cast<const uint16_t*>(recv.data_ptr()), n, (int)world, o, ob, cur_stream());
+}
+
+Tensor cast_bf16(Tensor x, c10::optional<Tensor> out) {
+  check_cuda(x, "x"); check_dtype(x, at::kFloat, "x");
+  TORCH_CHECK(x.is_contiguous(), "x must be contiguous");
+  Tensor o = (out && out->defined()) ? *out : torch::empty({x.numel()}, x.options().dtype(at::kBFloat16));
+  check_dtype(o, at::kBFloat16, "out");
+  TORCH_CHECK(o.is_contiguous() && o.numel() == x.numel(), "out size mismatch");
+  k8s_amd::launch_cast_bf16(f32(x), reinterpret_cast<uint16_t*>(o.data_ptr()), x.numel(), cur_stream());
+  return o;
+}
+
 // ------------------------------------------------------------------ batchnorm (NHWC)
 // want_mask: also return the packed ReLU mask (uint8 [M*C/8], bit j of byte e = y[8e+j] > 0) for the backward
 static Tensor relu_mask_for(const Tensor& x, bool want_mask) {
@@ -819,6 +851,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("scale"), py::arg("scale_t"), py::arg("step"), py::arg("decoupled"), py::arg("hyper") = py::none());
   m.def("grad_sumsq", &grad_sumsq);
   m.def("clip_factor", &clip_factor);
+  m.def("slice_sum", &slice_sum, py::arg("recv"), py::arg("world"), py::arg("out") = py::none(),
+        py::arg("out_bf") = py::none(), "fp32 rank-order sum of an all-to-all's bf16 chunks");
+  m.def("cast_bf16", &cast_bf16, py::arg("x"), py::arg("out") = py::none());
   m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("run_mean"),
         py::arg("run_var"), py::arg("training"), py::arg("momentum"), py::arg("eps"), py::arg("relu"),
         py::arg("want_mask") = false);

@@ -31,6 +31,9 @@ class Workload:
 
 
 MODELS = ("resnet50", "resnet_tiny", "bert_base", "bert_tiny", "llama3_8b", "llama_1b", "llama_tiny")
+# each model's default optimizer family (Workload.optimizer), known before the model is built
+MODEL_OPTIMIZER = {"resnet50": "sgd", "resnet_tiny": "sgd", "bert_base": "adam", "bert_tiny": "adam",
+                   "llama3_8b": "adam", "llama_1b": "adam", "llama_tiny": "adam"}
 
 
 def build(name: str, device, batch: int, seq: Optional[int] = None, image: Optional[int] = None,

@@ -20,12 +20,17 @@ Averaging is NOT done here: the optimizer kernel multiplies by 1/world in the
 same pass that applies the update.
 
 ``comm_dtype=torch.bfloat16`` halves the bytes on xGMI without summing in
-bf16: a ready bucket is cast to bf16 and exchanged with one
+bf16: a ready bucket is cast to bf16 (HIP kernel) and exchanged with one
 ``all_to_all_single`` (the reduce-scatter, one direct hop over the full
-mesh); each rank sums its world received slices in fp32, rounds the reduced
-slice to bf16 once, and an ``all_gather_into_tensor`` returns the reduced
-bucket to every rank (expanded back into the fp32 gradient buffer). For
-Llama-3-8B that is 16 GB instead of 32 GB per step each way.
+mesh); each rank sums its world received slices in fp32 (``slice_sum``, rank
+order), rounds the reduced slice to bf16 once, and an
+``all_gather_into_tensor`` returns the reduced bucket to every rank (expanded
+back into the fp32 gradient buffer). For Llama-3-8B that is 16 GB instead of
+32 GB per step each way. On the GPU the sum, the all-gather and the expansion
+of a bucket are all enqueued when its exchange is issued -- on a side stream
+that waits for the exchange device-side -- so they overlap the rest of
+backward; ``finish()`` only joins that stream. (The ZeRO-1 sharded service,
+``parallel/ps.py``, needs no all-gather of gradients at all.)
 """
 from __future__ import annotations
 
@@ -35,6 +40,7 @@ import torch
 import torch.distributed as dist
 
 from k8s_amd.parallel.flat import ALIGN, ParamStore, _round_up
+from k8s_amd.parallel.ps import cast_bf16, slice_sum
 
 
 class _Bucket:
@@ -79,6 +85,8 @@ class GradReducer:
                 self.bucket_of[p.index] = b
         self.works = []
         self.next_launch = 0
+        self.side = torch.cuda.Stream(store.grad.device) if (store.grad.is_cuda and self.enabled) else None
+        self.side_busy = False
         store.hooks.append(self._on_deposit)
 
     # ------------------------------------------------------------------ step protocol
@@ -112,9 +120,25 @@ class GradReducer:
         b.launched = True
         t = self.store.grad[b.lo:b.hi]
         if self.comm_dtype == torch.bfloat16 and (b.hi - b.lo) % self.world == 0:
-            send = t.to(torch.bfloat16)
+            send = cast_bf16(t)
             recv = torch.empty_like(send)
-            self.works.append((b, send, recv, dist.all_to_all_single(recv, send, group=self.group, async_op=True)))
+            w = dist.all_to_all_single(recv, send, group=self.group, async_op=True)
+            if self.side is None:
+                self.works.append((b, send, recv, w))
+                return
+            n = (b.hi - b.lo) // self.world
+            me = dist.get_rank(self.group)
+            with torch.cuda.stream(self.side):  # everything below waits for the exchange on the device only
+                w.wait()
+                # the reduced slice lands in this rank's own chunk of `send` (already on the wire), then the
+                # all-gather fills the other chunks in place and the bucket is expanded back to fp32
+                red = send[me * n:(me + 1) * n]
+                slice_sum(recv, self.world, None, red)
+                dist.all_gather_into_tensor(send, red, group=self.group, async_op=True).wait()
+                t.copy_(send)
+            send.record_stream(self.side)
+            recv.record_stream(self.side)
+            self.side_busy = True
         else:
             self.works.append((b, None, None, dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group,
                                                               async_op=True)))
@@ -136,11 +160,15 @@ class GradReducer:
                 if send is None:
                     continue
                 n = (b.hi - b.lo) // self.world
-                red = recv.view(self.world, n).float().sum(0).to(torch.bfloat16)  # fp32 accumulate, one rounding
+                red = torch.empty(n, dtype=torch.bfloat16, device=recv.device)
+                slice_sum(recv, self.world, None, red)  # fp32 accumulate in rank order, one rounding
                 gathers.append((b, send, dist.all_gather_into_tensor(send, red, group=self.group, async_op=True)))
             for b, full, w in gathers:
                 w.wait()
                 self.store.grad[b.lo:b.hi].copy_(full)
+            if self.side_busy:
+                torch.cuda.current_stream(self.store.grad.device).wait_stream(self.side)
+                self.side_busy = False
         self.works = []
 
     @property

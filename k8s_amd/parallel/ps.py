@@ -22,11 +22,21 @@ Two push transports:
 * ``comm_dtype=float32``: ``reduce_scatter_tensor`` in place (the output IS
   this rank's slice of the bucket).
 * ``comm_dtype=bfloat16`` (Llama-scale models): each bucket is cast to bf16
-  and exchanged with ONE ``all_to_all_single`` -- on a fully connected 8-GPU
-  xGMI mesh that is a direct one-hop exchange over all 7 links -- and the
-  world received slices are summed in fp32 on the owner. Half the bytes of
+  (``cast_bf16`` HIP kernel) and exchanged with ONE ``all_to_all_single`` --
+  on a fully connected 8-GPU xGMI mesh that is a direct one-hop exchange over
+  all 7 links -- and the world received slices are summed in fp32 on the
+  owner (``slice_sum`` HIP kernel, rank order, one pass). Half the bytes of
   the fp32 push, with fp32 accumulation (the only rounding is each rank's
-  contribution to bf16 once).
+  contribution to bf16 once). On the GPU the sum is enqueued on a side stream
+  behind the bucket's exchange the moment the exchange is issued (the stream
+  waits on the collective device-side), so it overlaps the rest of backward
+  instead of running after it.
+
+This service is also the all-reduce strategy's ZeRO-1 mode (``--zero``,
+``trainer/runner.py``): reduce-scatter + owner update + all-gather moves the
+same bytes over xGMI as an all-reduce, and each rank runs the optimizer and
+holds its fp32 state for 1/world of the model (Llama-3-8B: 96 GB of Adam
+state and the 42 ms update pass, per rank, divided by 8).
 
 Buckets are fixed ranges of the flat buffer taken from the END (backward
 produces the last layers' gradients first), each a multiple of world*64
@@ -46,6 +56,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 import torch.distributed as dist
 
+from k8s_amd.ops._ext import load as _load_ext
 from k8s_amd.parallel.flat import ALIGN, ParamStore, _round_up
 
 
@@ -92,6 +103,9 @@ class ShardedParameterService:
         self.sharded = zero1 and self.world > 1
         if self.sharded:
             optimizer.shard(self.owned_ranges)
+        # bf16 pushes on the GPU: the owner's fp32 sum runs on this stream, device-ordered behind each exchange
+        self.side = (torch.cuda.Stream(store.grad.device) if store.grad.is_cuda and self.world > 1 else None)
+        self.side_busy = False
         store.hooks.append(self._on_deposit)
 
     # ---------------------------------------------------------------- shards
@@ -127,9 +141,19 @@ class ShardedParameterService:
             return
         g = self.store.grad[b.lo:b.hi]
         if self.comm_dtype == torch.bfloat16:
-            send = g.to(torch.bfloat16)
+            send = cast_bf16(g)
             recv = torch.empty_like(send)
-            self.a2a.append((b, send, recv, dist.all_to_all_single(recv, send, group=self.group, async_op=True)))
+            w = dist.all_to_all_single(recv, send, group=self.group, async_op=True)
+            if self.side is not None:
+                lo, hi = self.shard(b)
+                with torch.cuda.stream(self.side):
+                    w.wait()  # device-side: the side stream waits for this bucket's exchange, the host does not
+                    _load_ext().slice_sum(recv, self.world, self.store.grad[lo:hi], None)
+                send.record_stream(self.side)
+                recv.record_stream(self.side)
+                self.side_busy = True
+            else:
+                self.a2a.append((b, send, recv, w))
         else:
             lo, hi = self.shard(b)  # in place: the output is this rank's slice of the input
             self.works.append(dist.reduce_scatter_tensor(self.store.grad[lo:hi], g, group=self.group,
@@ -143,8 +167,11 @@ class ShardedParameterService:
             w.wait()
             lo, hi = self.shard(b)
             # fp32 accumulation of the world bf16 contributions, in rank order (deterministic)
-            torch.sum(recv.view(self.world, hi - lo).float(), dim=0, out=self.store.grad[lo:hi])
+            slice_sum(recv, self.world, self.store.grad[lo:hi])
         self.a2a = []
+        if self.side_busy:
+            torch.cuda.current_stream(self.store.grad.device).wait_stream(self.side)
+            self.side_busy = False
 
     def step(self, lr: Optional[float] = None):
         """Finish the pushes, update the owned shards, pull the new weights."""
@@ -177,23 +204,54 @@ class ShardedParameterService:
             w.wait()
 
     # ---------------------------------------------------------------- checkpoint support
-    def full_optimizer_state(self) -> Dict[str, torch.Tensor]:
-        """Whole-model optimizer state (attribute -> full-size flat tensor) gathered from the owners; every
-        rank must call it (collective). Unsharded: the optimizer's own tensors."""
+    def gather_state(self, dst: int = 0) -> Optional[Dict[str, torch.Tensor]]:
+        """Whole-model optimizer state (attribute -> fp32 [total] tensor in host memory) on rank ``dst``, None on
+        the others; every rank must call it (collective). Bucket by bucket: the owners' slices are gathered into
+        one bucket-sized device buffer on ``dst`` and copied into (pinned) host memory, so no rank ever holds a
+        full-size device copy of a state tensor (an all-gather of every state onto every rank was
+        ~64 GB per GPU for Llama-3-8B). Unsharded: the optimizer's own tensors, copied to host on ``dst``."""
         if not self.sharded:
-            return {a: getattr(self.opt, a) for a in self.opt.STATE}
-        out = {}
+            if self.rank != dst:
+                return None
+            return {a: getattr(self.opt, a).detach().to("cpu") for a in self.opt.STATE}
+        dev = self.store.master.device
+        out = {} if self.rank == dst else None
+        stage = None
         for attr in self.opt.STATE:
             compact = getattr(self.opt, attr)
-            full = torch.zeros(self.store.total, dtype=compact.dtype, device=compact.device)
-            works = []
+            if out is not None:
+                out[attr] = torch.empty(self.store.total, dtype=torch.float32,
+                                        pin_memory=dev.type == "cuda")
             for b, (lo, hi, off) in zip(self.buckets, self.opt.layout):
-                works.append(dist.all_gather_into_tensor(full[b.lo:b.hi], compact[off:off + hi - lo],
-                                                         group=self.group, async_op=True))
-            for w in works:
-                w.wait()
-            out[attr] = full
+                n = hi - lo
+                glist = None
+                if out is not None:
+                    if stage is None or stage.numel() < b.hi - b.lo:
+                        stage = torch.empty(b.hi - b.lo, dtype=torch.float32, device=dev)
+                    glist = [stage[r * n:(r + 1) * n] for r in range(self.world)]
+                dist.gather(compact[off:off + n], glist, dst=dst, group=self.group)
+                if out is not None:
+                    out[attr][b.lo:b.hi].copy_(stage[:b.hi - b.lo])
         return out
+
+    def scatter_state(self, full: Optional[Dict[str, torch.Tensor]], src: int = 0):
+        """Inverse of ``gather_state``: rank ``src`` holds whole-model state tensors (host or device, attribute
+        -> [>= total]); every rank receives only the slices it owns, bucket by bucket (collective)."""
+        if not self.sharded:
+            raise RuntimeError("scatter_state is for the sharded (ZeRO-1) optimizer")
+        dev = self.store.master.device
+        stage = None
+        for attr in self.opt.STATE:
+            compact = getattr(self.opt, attr)
+            for b, (lo, hi, off) in zip(self.buckets, self.opt.layout):
+                n = hi - lo
+                slist = None
+                if self.rank == src:
+                    if stage is None or stage.numel() < b.hi - b.lo:
+                        stage = torch.empty(b.hi - b.lo, dtype=torch.float32, device=dev)
+                    stage[:b.hi - b.lo].copy_(full[attr].reshape(-1)[b.lo:b.hi])
+                    slist = [stage[r * n:(r + 1) * n] for r in range(self.world)]
+                dist.scatter(compact[off:off + n], slist, src=src, group=self.group)
 
     def sync_state(self):
         """Kept for callers of the unsharded service: gather the owners' state onto every rank."""
@@ -201,3 +259,23 @@ class ShardedParameterService:
             return
         for t in self.opt.state_tensors():
             self._pull(t)
+
+
+def cast_bf16(g: torch.Tensor) -> torch.Tensor:
+    """fp32 -> bf16 copy of a gradient bucket (HIP kernel on the GPU)."""
+    if g.is_cuda:
+        return _load_ext().cast_bf16(g.contiguous())
+    return g.to(torch.bfloat16)
+
+
+def slice_sum(recv: torch.Tensor, world: int, out: Optional[torch.Tensor] = None,
+              out_bf: Optional[torch.Tensor] = None):
+    """Rank-order fp32 sum of the ``world`` bf16 chunks of ``recv`` into ``out`` (fp32) and/or ``out_bf``."""
+    if recv.is_cuda:
+        _load_ext().slice_sum(recv, world, out, out_bf)
+        return
+    s = recv.view(world, -1).float().sum(0)
+    if out is not None:
+        out.copy_(s)
+    if out_bf is not None:
+        out_bf.copy_(s.to(torch.bfloat16))

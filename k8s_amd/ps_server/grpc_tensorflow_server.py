@@ -14,17 +14,21 @@ server that:
 
 * executes ops sent by other tasks on this task's device (what the smoke
   workload's master uses to check every task runs a kernel), and
-* holds parameter shards for CPU-side push/pull (``put``/``get``/``add``
-  ops on named fp32 tensors) -- the GPU data plane uses RCCL instead
-  (``k8s_amd.parallel.ps``), this keeps the TF PS protocol shape for
-  small/CPU jobs and tests, and
 * is the trainer's VARIABLE STORE OF RECORD (``k8s_amd.parallel.ps_vars``):
-  ``vput`` / ``vcommit`` / ``vinfo`` / ``vget`` move raw fp32 shards of the
-  flat master weights, optimizer state and buffers (binary payload after a
-  JSON header, no re-encoding). The chief pushes a versioned snapshot every
-  ``--ps-sync-every`` steps; a restarted job pulls the newest committed
-  snapshot from the PS tasks, as TF workers re-read their variables from
-  ``/job:ps`` (workers stay stateless).
+  ``vput`` / ``vcommit`` / ``vgc`` / ``vinfo`` / ``vget`` move raw fp32 shards
+  of the flat master weights, optimizer state and buffers (binary payload
+  after a JSON header, no re-encoding). The chief pushes a versioned snapshot
+  every ``--ps-sync-every`` steps; a restarted job pulls the newest snapshot
+  committed on EVERY PS task, as TF workers re-read their variables from
+  ``/job:ps`` (workers stay stateless). The per-step gradient exchange is not
+  here: it rides RCCL between the GPU ranks (``k8s_amd.parallel.ps``).
+
+Snapshots are two-phase and multi-versioned: every shard is stored under its
+version (a ``vput`` of version v+1 never overwrites version v's bytes),
+``vcommit`` makes a version readable on one task only after all its shards
+landed there, and the chief drops older versions (``vgc``) only after the new
+one is committed on every task. A chief that dies mid-push therefore leaves
+the previous snapshot intact and readable on every task.
 
 The process blocks serving until it receives a ``shutdown`` message or
 SIGTERM (exit 0), mirroring ``server.join()``.
@@ -168,11 +172,10 @@ class TaskServer(socketserver.ThreadingTCPServer):
 
     def __init__(self, addr, job, task, verbose=False):
         self.job, self.task, self.verbose = job, task, verbose
-        self.params = {}
-        # variable store of record (parallel/ps_vars.py): (name, lo) -> [version, raw little-endian fp32 bytes];
-        # `committed` is the newest version whose every shard on this task has landed (readers pull only that)
+        # variable store of record (parallel/ps_vars.py): (version, push id, name, lo) -> raw little-endian fp32
+        # bytes; `committed`: version -> (push id, metadata) of every version whose shards all landed on this task
         self.shards = {}
-        self.committed = -1
+        self.committed = {}
         self.lock = threading.Lock()
         super().__init__(addr, _TaskHandler)
 
@@ -199,49 +202,46 @@ class _TaskHandler(socketserver.BaseRequestHandler):
                     where = "cpu"
                 send_msg(self.request, {"ok": True, "result": out, "device": where,
                                         "task": "/job:%s/task:%d" % (srv.job, srv.task)})
-            elif op == "put":
-                with srv.lock:
-                    srv.params[msg["name"]] = list(msg["value"])
-                send_msg(self.request, {"ok": True})
-            elif op == "add":  # push: accumulate a gradient-like update
-                with srv.lock:
-                    cur = srv.params.setdefault(msg["name"], [0.0] * len(msg["value"]))
-                    scale = float(msg.get("scale", 1.0))
-                    for i, v in enumerate(msg["value"]):
-                        cur[i] += scale * v
-                send_msg(self.request, {"ok": True})
-            elif op == "get":  # pull
-                with srv.lock:
-                    v = srv.params.get(msg["name"])
-                send_msg(self.request, {"ok": v is not None, "value": v})
-            elif op == "vput":  # one variable shard (raw fp32 payload) for snapshot `version`
+            elif op == "vput":  # one variable shard (raw fp32 payload) of push `push` of snapshot `version`
                 data = recv_exact(self.request, int(msg["nbytes"]))
                 if data is None:
                     return
-                with srv.lock:
-                    srv.shards[(msg["name"], int(msg["lo"]))] = [int(msg["version"]), data]
+                v, push = int(msg["version"]), str(msg.get("push", ""))
+                with srv.lock:  # keyed by push id: a re-push of a version never touches a committed copy
+                    srv.shards[(v, push, msg["name"], int(msg["lo"]))] = data
                 send_msg(self.request, {"ok": True})
-            elif op == "vcommit":  # every shard of `version` has been put: make it the readable snapshot
-                v = int(msg["version"])
+            elif op == "vcommit":  # every shard of this push has landed on this task: make it readable here
+                v, push = int(msg["version"]), str(msg.get("push", ""))
                 with srv.lock:
-                    names = msg.get("names")
-                    ok = all(srv.shards.get((n, int(lo)), [None])[0] == v for n, lo in names) if names else True
+                    names = msg.get("names") or []
+                    ok = all((v, push, n, int(lo)) in srv.shards for n, lo in names)
                     if ok:
-                        srv.committed = max(srv.committed, v)
-                        srv.meta = msg.get("meta", {})
-                send_msg(self.request, {"ok": ok, "committed": srv.committed})
+                        srv.committed[v] = (push, msg.get("meta", {}))
+                send_msg(self.request, {"ok": ok, "committed": sorted(srv.committed)})
+            elif op == "vgc":  # `keep` is committed on every task: drop older versions and stale partial pushes
+                keep = int(msg["keep"])
+                with srv.lock:
+                    live = srv.committed.get(keep, (None,))[0]
+                    for key in [k for k in srv.shards if k[0] < keep or (k[0] == keep and k[1] != live)]:
+                        del srv.shards[key]
+                    for v in [v for v in srv.committed if v < keep]:
+                        del srv.committed[v]
+                send_msg(self.request, {"ok": True, "committed": sorted(srv.committed)})
             elif op == "vinfo":
                 with srv.lock:
-                    send_msg(self.request, {"ok": True, "committed": srv.committed,
-                                            "meta": getattr(srv, "meta", {}),
-                                            "shards": sorted([n, lo] for n, lo in srv.shards)})
+                    send_msg(self.request, {"ok": True, "committed": sorted(srv.committed),
+                                            "meta": {str(v): m for v, (_, m) in srv.committed.items()},
+                                            "shards": sorted([v, n, lo] for v, _, n, lo in srv.shards)})
             elif op == "vget":
+                v = int(msg["version"])
                 with srv.lock:
-                    ent = srv.shards.get((msg["name"], int(msg["lo"])))
-                if ent is None:
-                    send_msg(self.request, {"ok": False, "error": "no shard %s@%s" % (msg["name"], msg["lo"])})
+                    ent = srv.committed.get(v)
+                    data = srv.shards.get((v, ent[0], msg["name"], int(msg["lo"]))) if ent else None
+                if data is None:
+                    send_msg(self.request, {"ok": False, "error": "no committed shard %s@%s of version %d"
+                                            % (msg["name"], msg["lo"], v)})
                 else:
-                    send_blob(self.request, {"ok": True, "version": ent[0]}, ent[1])
+                    send_blob(self.request, {"ok": True, "version": v}, data)
             elif op == "ping":
                 send_msg(self.request, {"ok": True, "task": "/job:%s/task:%d" % (srv.job, srv.task)})
             elif op == "shutdown":
@@ -284,7 +284,11 @@ def build_parser() -> argparse.ArgumentParser:
 
 
 def main(argv=None):
-    a = build_parser().parse_args(argv)
+    # unknown flags are ignored, as the reference does (parse_known_args,
+    # /root/reference/grpc_tensorflow_server/grpc_tensorflow_server.py:159): a PS pod must not crash on an extra flag
+    a, unknown = build_parser().parse_known_args(argv)
+    if unknown:
+        print("ignoring unknown flags: %s" % " ".join(unknown), file=sys.stderr, flush=True)
     cluster = parse_cluster_spec(a.cluster_spec, a.job_name, a.task_id)
     torch, dev = _device()
     if torch is not None and dev is not None and dev.type == "cuda" and a.gpu_memory_fraction < 1.0:

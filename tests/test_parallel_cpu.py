@@ -26,7 +26,7 @@ def _grads(rank, step, shapes):
     return [torch.randn(s, generator=g) * (1.0 + rank) for s in shapes]
 
 
-def _worker(rank, world, port, strategy, comm, opt_name, steps, out_dir, nan_step):
+def _worker(rank, world, port, strategy, comm, opt_name, steps, out_dir, nan_step, clip=10.0):
     from k8s_amd.ops.optim import FusedAdam, FusedSGD
     from k8s_amd.parallel.ddp import GradReducer
     from k8s_amd.parallel.flat import ALIGN, ParamStore, init_normal
@@ -38,9 +38,9 @@ def _worker(rank, world, port, strategy, comm, opt_name, steps, out_dir, nan_ste
     params = [store.new("p%d" % i, s, init_normal(0.5), decay=(i % 2 == 0)) for i, s in enumerate(SHAPES)]
     store.finalize("cpu", pad_to=world * ALIGN, seed=5)
     if opt_name == "sgd":
-        opt = FusedSGD(store, lr=0.05, momentum=0.9, weight_decay=1e-3, max_grad_norm=10.0)
+        opt = FusedSGD(store, lr=0.05, momentum=0.9, weight_decay=1e-3, max_grad_norm=clip)
     else:
-        opt = FusedAdam(store, lr=0.01, weight_decay=0.01, max_grad_norm=10.0)
+        opt = FusedAdam(store, lr=0.01, weight_decay=0.01, max_grad_norm=clip)
     dtype = torch.bfloat16 if comm == "bf16" else torch.float32
     if strategy == "ps":
         svc = ShardedParameterService(store, opt, bucket_mb=0.002, comm_dtype=dtype)  # several buckets
@@ -61,7 +61,7 @@ def _worker(rank, world, port, strategy, comm, opt_name, steps, out_dir, nan_ste
         for p, g in reversed(list(zip(params, gs))):  # backward order
             store.deposit(p, g)
         finish()
-    full = svc.full_optimizer_state() if svc is not None else None
+    full = svc.gather_state() if svc is not None else None
     if rank == 0:
         sd = opt.state_dict(full)
         torch.save({"master": store.master.clone(), "half": store.half.float().clone(),
@@ -72,9 +72,10 @@ def _worker(rank, world, port, strategy, comm, opt_name, steps, out_dir, nan_ste
     dist.destroy_process_group()
 
 
-def _run(world, strategy, comm, opt_name, steps=4, nan_step=-1):
+def _run(world, strategy, comm, opt_name, steps=4, nan_step=-1, clip=10.0):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, free_port(), strategy, comm, opt_name, steps, d, nan_step), nprocs=world)
+        mp.spawn(_worker, args=(world, free_port(), strategy, comm, opt_name, steps, d, nan_step, clip),
+                 nprocs=world)
         return torch.load(os.path.join(d, "%s_%s_%s.pt" % (strategy, comm, opt_name)), weights_only=True)
 
 
@@ -137,3 +138,89 @@ def test_nonfinite_gradient_skips_step_everywhere(strategy):
     b = _run(2, strategy, "fp32", "adam", steps=3)
     for k in ("master", "exp_avg", "exp_avg_sq"):
         assert torch.equal(a[k], b[k]), k
+
+
+def _reference_bf16(world, opt_name, steps, round_sum, clip=None):
+    """Ground truth of the bf16 transport: every rank's contribution rounded to bf16 once, summed in fp32 in RANK
+    ORDER (what slice_sum does on the owner); ``round_sum``: the all-reduce strategy also rounds the reduced slice
+    to bf16 for its all-gather."""
+    from k8s_amd.ops.optim import FusedAdam, FusedSGD
+    from k8s_amd.parallel.flat import ALIGN, ParamStore, init_normal
+
+    store = ParamStore()
+    params = [store.new("p%d" % i, s, init_normal(0.5), decay=(i % 2 == 0)) for i, s in enumerate(SHAPES)]
+    store.finalize("cpu", pad_to=world * ALIGN, seed=5)
+    if opt_name == "sgd":
+        opt = FusedSGD(store, lr=0.05, momentum=0.9, weight_decay=1e-3, max_grad_norm=clip)
+    else:
+        opt = FusedAdam(store, lr=0.01, weight_decay=0.01, max_grad_norm=clip)
+    for step in range(steps):
+        store.begin_step()
+        per = [_grads(r, step, SHAPES) for r in range(world)]
+        for i, p in enumerate(params):
+            acc = torch.zeros(p.shape)
+            for r in range(world):
+                acc = acc + per[r][i].to(torch.bfloat16).float()
+            if round_sum:
+                acc = acc.to(torch.bfloat16).float()
+            store.deposit(p, acc)
+        opt.step(grad_scale=1.0 / world)
+    return store.master.clone()
+
+
+@pytest.mark.parametrize("world", [4, 8])
+@pytest.mark.parametrize("strategy", ["allreduce", "ps"])
+def test_bf16_transport_bit_exact_against_rank_order_reference(world, strategy):
+    """4- and 8-rank runs bit-exact against the single-process reference. The bf16
+    transport sums in a fixed (rank) order, so its result is reproducible to the bit: Adam, 4 steps. (No gradient
+    clipping here: the sharded clip norm is an all-reduce of per-shard partial sums, whose order differs from a
+    single-process norm in the last bit.)"""
+    got = _run(world, strategy, "bf16", "adam", clip=None)
+    ref = _reference_bf16(world, "adam", 4, round_sum=(strategy == "allreduce"))
+    assert torch.equal(got["master"], ref), (got["master"] - ref).abs().max()
+
+
+def _gather_worker(rank, world, port, out_dir):
+    from k8s_amd.ops.optim import FusedAdam
+    from k8s_amd.parallel.flat import ALIGN, ParamStore, init_normal
+    from k8s_amd.parallel.ps import ShardedParameterService
+
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    store = ParamStore()
+    [store.new("p%d" % i, s, init_normal(0.5)) for i, s in enumerate(SHAPES)]
+    store.finalize("cpu", pad_to=world * ALIGN, seed=5)
+    opt = FusedAdam(store, lr=0.01)
+    svc = ShardedParameterService(store, opt, bucket_mb=0.002)
+    for attr in opt.STATE:  # each rank's owned slices hold a recognisable pattern
+        for lo, hi, off in opt.layout:
+            getattr(opt, attr)[off:off + hi - lo] = torch.arange(lo, hi, dtype=torch.float32) * (
+                1.0 if attr == "m1" else -1.0)
+    full = svc.gather_state(dst=0)
+    if rank == 0:
+        n = store.total
+        assert torch.equal(full["m1"], torch.arange(n, dtype=torch.float32))
+        assert torch.equal(full["m2"], -torch.arange(n, dtype=torch.float32))
+        assert not full["m1"].is_cuda  # host memory, never a full-size device copy
+    else:
+        assert full is None
+    for attr in opt.STATE:
+        getattr(opt, attr).zero_()
+    src = {a: full[a] * 2 for a in full} if rank == 0 else None
+    svc.scatter_state(src, src=0)
+    for attr in opt.STATE:
+        for lo, hi, off in opt.layout:
+            want = torch.arange(lo, hi, dtype=torch.float32) * (2.0 if attr == "m1" else -2.0)
+            assert torch.equal(getattr(opt, attr)[off:off + hi - lo], want)
+    open(os.path.join(out_dir, "ok%d" % rank), "w").close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_state_gathers_to_one_rank_and_scatters_back():
+    """checkpoints / PS snapshots gather the ZeRO-1 optimizer state to the chief only
+    (bucket by bucket, into host memory), and a restore scatters each rank only its owned slices."""
+    world = 4
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_gather_worker, args=(world, free_port(), d), nprocs=world)
+        assert sorted(os.listdir(d)) == ["ok%d" % r for r in range(world)]

@@ -179,8 +179,8 @@ def test_ps_tasks_hold_the_variables_and_a_restarted_job_resumes_from_them(tmp_p
         assert ckpt.latest_checkpoint(run) is None  # nothing on disk: only the PS tasks hold the state
         for addr in cluster["ps"]:
             info = call(addr, {"op": "vinfo"})
-            assert info["committed"] == 3, info
-            assert {n for n, _ in info["shards"]} >= {"params", "optim/exp_avg", "optim/exp_avg_sq"}
+            assert info["committed"] == [3], info  # older versions were dropped once 3 was committed everywhere
+            assert {n for _, n, _ in info["shards"]} >= {"params", "optim/exp_avg", "optim/exp_avg_sq"}
         again = [_trainer(common + ["--fail-at-step", "4"], tfc("master", 0)),
                  _trainer(common + ["--fail-at-step", "4"], tfc("worker", 0))]  # markers: no second failure
         outs = []
@@ -222,3 +222,87 @@ def test_ps_shard_ranges_cover_and_align():
         assert len(r) == parts and r[0][0] == 0 and r[-1][1] == n
         assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
         assert all(lo % 64 == 0 for lo, _ in r if lo < n)
+
+
+def _ps_tasks(n):
+    """n in-process default-PS task servers on free ports; returns (addresses, servers)."""
+    import threading
+
+    from k8s_amd.ps_server.grpc_tensorflow_server import TaskServer
+
+    srvs, addrs = [], []
+    for j in range(n):
+        port = free_port()
+        s = TaskServer(("127.0.0.1", port), "ps", j)
+        threading.Thread(target=s.serve_forever, daemon=True).start()
+        srvs.append(s)
+        addrs.append("127.0.0.1:%d" % port)
+    return addrs, srvs
+
+
+def test_ps_snapshot_survives_a_chief_that_dies_mid_push():
+    """a push of version v+1 must never destroy the committed version v. Three crash points
+    of the two-phase push -- some shards of v+1 put on one task only, v+1 committed on one task only, v+1 committed
+    everywhere but the old version not yet dropped -- each leave a whole snapshot readable on every task."""
+    from k8s_amd.parallel.ps_vars import PsVariables, shard_ranges
+    from k8s_amd.ps_server.grpc_tensorflow_server import call
+
+    addrs, srvs = _ps_tasks(2)
+    try:
+        psv = PsVariables(addrs)
+        v1 = {"params": torch.arange(1000, dtype=torch.float32), "optim/m": torch.full((300,), 2.0)}
+        psv.push(1, v1, meta={"total": 1000})
+        psv.wait()
+        assert psv.latest()[0] == 1
+
+        # (1) the chief dies in phase 1: part of version 2 reached task 0 only
+        lo, hi = shard_ranges(1000, 2)[0]
+        a = (torch.arange(1000, dtype=torch.float32) * -1).numpy()
+        assert call(addrs[0], {"op": "vput", "name": "params", "lo": lo, "n": hi - lo, "version": 2},
+                    payload=memoryview(a[lo:hi]))["ok"]
+        v, meta = psv.latest()
+        assert v == 1 and meta["total"] == 1000
+        got = psv.pull(1)
+        assert torch.equal(got["params"], v1["params"]) and torch.equal(got["optim/m"], v1["optim/m"])
+
+        # (2) the chief dies in phase 2: version 2 committed on task 0 only
+        assert call(addrs[0], {"op": "vcommit", "version": 2, "names": [["params", lo]], "meta": {}})["ok"]
+        assert psv.latest()[0] == 1
+        assert torch.equal(psv.pull(1)["params"], v1["params"])
+
+        # (3) the chief dies between phase 2 and the old version's GC: both versions readable, newest wins
+        v2 = {"params": torch.arange(1000, dtype=torch.float32) + 0.5, "optim/m": torch.full((300,), 3.0)}
+
+        def die(stage):
+            raise SystemExit("chief killed after %s" % stage)
+
+        psv.fault_hook = die
+        psv.push(2, v2, meta={"total": 1000})
+        with pytest.raises(SystemExit):
+            psv.wait()
+        assert psv.latest()[0] == 2
+        assert torch.equal(psv.pull(2)["params"], v2["params"])
+        assert torch.equal(psv.pull(1)["params"], v1["params"])  # not dropped: GC never ran
+
+        # a later complete push drops everything older than itself
+        psv.fault_hook = None
+        psv.push(3, v2, meta={"total": 1000})
+        psv.wait()
+        for addr in addrs:
+            assert call(addr, {"op": "vinfo"})["committed"] == [3]
+        with pytest.raises(RuntimeError):
+            psv.pull(1)
+    finally:
+        for s in srvs:
+            s.shutdown()
+            s.server_close()
+
+
+def test_default_ps_ignores_unknown_flags():
+    """The reference's default PS parses with parse_known_args (grpc_tensorflow_server.py:159): extra flags from a
+    user's PS template must not crash the pod."""
+    from k8s_amd.ps_server import grpc_tensorflow_server as srv
+
+    a, unknown = srv.build_parser().parse_known_args(
+        ["--cluster_spec", "ps|127.0.0.1:1", "--job_name", "ps", "--task_id", "0", "--log_dir", "/tmp/x", "--foo"])
+    assert a.job_name == "ps" and unknown == ["--log_dir", "/tmp/x", "--foo"]
