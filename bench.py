@@ -23,7 +23,16 @@ import os
 import sys
 import time
 
-import torch
+# RCCL / HIP environment, set before anything initialises the GPU (the first HIP call happens in
+# kdist.init_process_group -> torch.cuda.set_device). The KFD on the MI355X hosts this runs on only supports
+# dmabuf-based peer memory: without HSA_ENABLE_IPC_MODE_LEGACY=0 RCCL's intra-node transport and CUDA-IPC tensor
+# sharing fail with `hipIpcGetMemHandle: invalid argument` (observed on these hosts; the same requirement is in
+# charts/tf-job-operator/values.yaml `ipcModeLegacy` and the task environment notes). setdefault: an operator-set
+# value wins. RCCL's channel count is left to its own MI3xx tuning (charts/... `minChannels` is a knob, not a
+# requirement).
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import torch  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -103,6 +112,9 @@ def main(argv=None):
     dt = time.perf_counter() - t0
     dt_max = kdist.all_reduce_max(dt, dev)
     final_loss = float(loss.detach().float().item())
+    # data-parallel sanity (outside the timed region): every replica must hold the same weights
+    csum = float(store.master.double().sum().item())
+    identical = kdist.all_reduce_max(csum, dev) == -kdist.all_reduce_max(-csum, dev)
     ips = n * a.batch * a.steps / dt_max
     if info.rank == 0:
         out = {
@@ -129,6 +141,7 @@ def main(argv=None):
                 "bucket_mb": a.bucket_mb,
             },
             "final_loss": round(final_loss, 4),
+            "replicas_identical": identical,
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if dev.type == "cuda" else None,
         }
         print(json.dumps(out), flush=True)

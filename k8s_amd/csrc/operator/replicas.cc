@@ -1,3 +1,4 @@
+#include <cstdlib>
 #include "replicas.h"
 
 #include <algorithm>
@@ -158,6 +159,42 @@ Json make_replica_service(const TfJob& job, const TfReplicaSpec& r, int index) {
   return svc;
 }
 
+// GPUs the `tensorflow` container of a replica template asks for: limits (else requests) of every resource whose
+// name contains "gpu" (amd.com/gpu, nvidia.com/gpu, alpha.kubernetes.io/nvidia-gpu).
+static int64_t template_gpus(const TfReplicaSpec& r) {
+  if (!r.tmpl) return 0;
+  const Json* spec = r.tmpl->find("spec");
+  const Json* cons = spec ? spec->find("containers") : nullptr;
+  if (!cons || !cons->is_array()) return 0;
+  for (const auto& c : cons->as_array()) {
+    if (get_str(c, "name") != kTensorflowContainer) continue;
+    const Json* res = c.find("resources");
+    if (!res || !res->is_object()) return 0;
+    for (const char* which : {"limits", "requests"}) {
+      const Json* m = res->find(which);
+      if (!m || !m->is_object()) continue;
+      int64_t n = 0;
+      for (const auto& kv : m->as_object()) {
+        if (kv.first.find("gpu") == std::string::npos) continue;
+        if (kv.second.is_number()) n += kv.second.as_int();
+        else if (kv.second.is_string()) n += std::atoll(kv.second.as_string().c_str());
+      }
+      if (n > 0) return n;
+    }
+    return 0;
+  }
+  return 0;
+}
+
+// TFJOB_TASK_GPUS: {"master": n, "worker": n, "ps": n} -- the GPUs per task of every replica type, so a trainer
+// replica that drives several local GPUs (one process per GPU) can place its processes in the global rank order
+// without a registration round (TF_CONFIG itself stays byte-identical to the reference's).
+std::string task_gpus_json(const TfJob& job) {
+  Json j = Json::object();
+  for (const auto& r : job.spec.replica_specs) j[lower(r.type)] = template_gpus(r);
+  return j.dump();
+}
+
 Json make_replica_job(const TfJob& job, const TfReplicaSpec& r, int index, const ClusterSpec& cs,
                       const std::string& ps_script_path) {
   Labels l = task_labels(job, r.type, index);
@@ -186,6 +223,7 @@ Json make_replica_job(const TfJob& job, const TfReplicaSpec& r, int index, const
   if (!tl.is_object()) tl = Json::object();
   for (auto& kv : l) tl[kv.first] = kv.second;
   const std::string tfc = tf_config_json(cs, lower(r.type), index);
+  const std::string gpus = task_gpus_json(job);
   if (Json* cons = pspec.find("containers"); cons && cons->is_array()) {
     for (auto& c : cons->as_array()) {
       if (get_str(c, "name") != kTensorflowContainer) continue;
@@ -193,6 +231,10 @@ Json make_replica_job(const TfJob& job, const TfReplicaSpec& r, int index, const
       ev["name"] = "TF_CONFIG";
       ev["value"] = tfc;
       c["env"].push_back(ev);
+      Json eg = Json::object();
+      eg["name"] = "TFJOB_TASK_GPUS";
+      eg["value"] = gpus;
+      c["env"].push_back(eg);
     }
   }
   Json jspec = Json::object();

@@ -70,6 +70,7 @@ class LocalKubelet:
         self.ns = namespace
         self.gpu_pool = list(gpus or [])
         self.gpu_used: Dict[str, List[int]] = {}
+        self.gpu_history: Dict[str, List[int]] = {}  # every allocation ever made (tests)
         self.log_dir = log_dir or tempfile.mkdtemp(prefix="k8s_amd_kubelet_")
         os.makedirs(self.log_dir, exist_ok=True)
         self.poll = poll
@@ -243,6 +244,7 @@ class LocalKubelet:
         if len(free) < n:
             return None  # unschedulable for now (Pending)
         self.gpu_used[pod_name] = free[:n]
+        self.gpu_history[pod_name] = free[:n]
         return free[:n]
 
     # ------------------------------------------------------------------ reconcile loop

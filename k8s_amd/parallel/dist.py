@@ -17,6 +17,9 @@ from __future__ import annotations
 import datetime
 import json
 import os
+
+# dmabuf IPC (see bench.py): must be in the environment before the first HIP call of this process
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -60,13 +63,48 @@ def resolve(addr: str) -> str:
     return table.get(host, addr)
 
 
-def rank_from_tf_config(tf_config: str, port_offset: int = 0) -> RankInfo:
+def local_device_count() -> int:
+    """GPUs this container was given, WITHOUT initialising the GPU (a process that has touched HIP must not be the
+    one that forks the per-GPU trainers): the kubelet's / device plugin's visibility list when set, else the
+    runtime's device count (``torch.cuda.device_count`` does not initialise HIP on this image), else 1."""
+    for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+        v = os.environ.get(k)
+        if v is not None and v.strip():
+            return len([d for d in v.split(",") if d.strip()])
+    if os.environ.get("K8S_AMD_NO_GPU") == "1":
+        return 1
+    try:
+        return max(1, torch.cuda.device_count())
+    except Exception:  # noqa: BLE001
+        return 1
+
+
+def task_gpus_table() -> Optional[Dict[str, int]]:
+    """``TFJOB_TASK_GPUS`` (set by the operator next to TF_CONFIG): GPUs per task of every replica type."""
+    v = os.environ.get("TFJOB_TASK_GPUS")
+    if not v:
+        return None
+    try:
+        return {str(k).lower(): int(n) for k, n in json.loads(v).items()}
+    except (ValueError, TypeError, AttributeError):
+        return None
+
+
+def rank_from_tf_config(tf_config: str, port_offset: int = 0, local_rank: Optional[int] = None,
+                        task_gpus: Optional[Dict[str, int]] = None) -> RankInfo:
     """Deterministic rank assignment from a TF_CONFIG JSON string.
 
     Compute ranks (the collective group) are master/chief first, then workers;
     PS tasks do not join the RCCL group (rank -1): in this framework the
     parameter service is sharded over the compute ranks (parallel/ps.py) and
     the PS replicas run the parameter/rendezvous server (ps_server/).
+
+    A task given n > 1 GPUs runs n processes, one per GPU (``trainer/runner.py`` forks them, ``LOCAL_RANK`` i):
+    the reference's single MASTER pod with ``--num-gpus=N`` (`/root/reference/examples/gke/TF on GKE.ipynb`
+    lines 976, 988; in-graph replication, `/root/reference/tf_job_design_doc.md:101-103`) becomes N ranks.
+    Task t's processes take global ranks ``sum(n of the tasks before t) + i``; the world is the sum over tasks.
+    ``task_gpus`` (role -> GPUs per task, from the operator's ``TFJOB_TASK_GPUS``) gives every task's n; without
+    it every compute task is assumed to have this container's device count.
 
     The TCP-store rendezvous listens on the first compute task's own ``tfPort``
     (``port_offset`` 0): that is the one port the operator's per-replica
@@ -91,17 +129,32 @@ def rank_from_tf_config(tf_config: str, port_offset: int = 0) -> RankInfo:
     if not order and not cluster.get("ps"):
         raise ValueError("TF_CONFIG has an empty cluster")
     keys = [(r, i) for r, i, _ in order]
+    if local_rank is None:
+        local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    table = task_gpus if task_gpus is not None else task_gpus_table()
+    mine = local_device_count()
+
+    def procs(role):  # processes a task of this role runs (a CPU-only task: one)
+        if table is None:
+            return mine
+        return max(1, int(table.get(role, mine)))
+
+    counts = [procs(r) for r, _, _ in order]
     if ttype == "ps":
         rank = -1
     elif (ttype, tidx) in keys:
-        rank = keys.index((ttype, tidx))
+        k = keys.index((ttype, tidx))
+        if local_rank >= counts[k]:
+            raise ValueError("local rank %d but task %s:%d runs %d processes" % (local_rank, ttype, tidx, counts[k]))
+        rank = sum(counts[:k]) + local_rank
     else:
         raise ValueError("task %s:%d not in cluster %s" % (ttype, tidx, sorted(cluster)))
     first = order[0][2] if order else cluster["ps"][0]
     host, _, port = resolve(first).rpartition(":")
-    return RankInfo(rank=rank, world_size=len(order), local_rank=int(os.environ.get("LOCAL_RANK", 0)),
+    world = sum(counts)
+    return RankInfo(rank=rank, world_size=world, local_rank=local_rank,
                     master_addr=host or first, master_port=int(port or 2222) + port_offset, role=ttype,
-                    role_index=tidx, compute_world=len(order))
+                    role_index=tidx, compute_world=world)
 
 
 def rank_from_env() -> Optional[RankInfo]:

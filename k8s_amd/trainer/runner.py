@@ -466,8 +466,8 @@ def train(a) -> int:
     kdist.barrier()
     from k8s_amd.ops import gemm as kgemm
 
-    metrics.event(event="done", steps=a.steps, loss=loss_v, elapsed=time.time() - t_start,
-                  gemm_fallbacks=dict(kgemm.FALLBACKS))
+    metrics.event(event="done", steps=a.steps, loss=loss_v, elapsed=time.time() - t_start, rank=rank,
+                  weights_sum=float(w.store.master.double().sum().item()), gemm_fallbacks=dict(kgemm.FALLBACKS))
     metrics.close()
     if chief:
         _shutdown_ps(tf_config)
@@ -475,7 +475,72 @@ def train(a) -> int:
     return EXIT_OK
 
 
+def _replica_processes() -> int:
+    """Processes this replica runs: one per GPU it was given, when TF_CONFIG makes it a compute task (the PS and
+    single-GPU replicas run in this process)."""
+    if os.environ.get("K8S_AMD_REPLICA_CHILD") == "1" or "RANK" in os.environ:
+        return 1
+    tfc = os.environ.get("TF_CONFIG")
+    if not tfc:
+        return 1
+    try:
+        ttype = json.loads(tfc).get("task", {}).get("type", "master").lower()
+    except ValueError:
+        return 1
+    if ttype == "ps":
+        return 1
+    from k8s_amd.parallel.dist import local_device_count, task_gpus_table
+
+    n = local_device_count()
+    table = task_gpus_table()
+    if table is not None and ttype in table:
+        n = max(1, min(n, table[ttype])) if table[ttype] > 0 else 1
+    return n
+
+
+def _run_replica_children(n: int, argv) -> int:
+    """One trainer process per local GPU (LOCAL_RANK i drives visible device i), started BEFORE anything touches
+    the GPU; returns the replica's exit code: 0 when every child succeeded, else a failing child's code (a
+    retryable one, >= 128, wins so the operator restarts the replica). When one child fails the others get a grace
+    period to finish, then SIGTERM (they would otherwise wait forever in a collective)."""
+    import subprocess
+
+    argv = list(sys.argv[1:] if argv is None else argv)
+    procs = []
+    for i in range(n):
+        env = dict(os.environ, LOCAL_RANK=str(i), LOCAL_WORLD_SIZE=str(n), K8S_AMD_REPLICA_CHILD="1")
+        procs.append(subprocess.Popen([sys.executable, "-m", "k8s_amd.trainer"] + argv, env=env))
+
+    def forward(signum, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signum)
+
+    signal.signal(signal.SIGTERM, forward)
+    codes = [None] * n
+    deadline = None
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None and p.poll() is not None:
+                rc = p.returncode
+                codes[i] = 128 - rc if rc < 0 else rc  # killed by signal s -> 128 + s
+                if codes[i] != 0 and deadline is None:
+                    deadline = time.time() + 30.0
+        if deadline is not None and time.time() > deadline:
+            forward(signal.SIGTERM, None)
+            deadline = time.time() + 1e9
+        time.sleep(0.1)
+    bad = [c for c in codes if c != 0]
+    if not bad:
+        return EXIT_OK
+    retry = [c for c in bad if c >= 128]
+    return retry[0] if retry else bad[0]
+
+
 def main(argv=None) -> int:
+    n = _replica_processes()
+    if n > 1:
+        return _run_replica_children(n, argv)
     a = parse(argv)
     signal.signal(signal.SIGTERM, lambda *_: os._exit(EXIT_SIGTERM))
     try:

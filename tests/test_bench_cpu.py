@@ -40,6 +40,18 @@ def test_bench_two_ranks_json_contract():
     assert r["final_loss"] == r["final_loss"]
 
 
+def test_bench_eight_ranks_like_the_driver():
+    """the driver's 8-GPU launch (torch.distributed.run, 8 ranks, one per GPU) rehearsed
+    with 8 gloo ranks on the CPU: one JSON line, dp8, the whole-job value, identical replicas after the steps."""
+    recs = _run("bench.py", ["--gpus", "8", "--steps", "2", "--warmup", "1", "--batch", "2", "--image", "32"],
+                nproc=8, timeout=600)
+    assert len(recs) == 1, recs
+    r = recs[0]
+    assert r["n_gpus"] == 8 and r["config"]["parallelism"] == "dp8" and r["config"]["global_batch"] == 16
+    assert abs(r["value"] - 16 * 2 / (r["ms_per_step"] * 2 / 1000.0)) / r["value"] < 0.02
+    assert r["replicas_identical"] is True
+
+
 def test_collectives_bench_busbw():
     recs = _run("benchmarks/collectives.py", ["--device", "cpu", "--sizes-mb", "0.25", "--iters", "2",
                                               "--warmup", "1"])

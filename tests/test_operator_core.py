@@ -253,7 +253,10 @@ def test_replica_set_create():
         assert s["spec"]["ports"] == [{"name": "tf-port", "port": 10}] and s["spec"]["selector"] == labels
         assert j["spec"]["completions"] == 1 and j["spec"]["parallelism"] == 1
         cs = j["spec"]["template"]["spec"]["containers"]
-        assert len(cs) == 1 and len(cs[0]["env"]) == 1 and cs[0]["env"][0]["name"] == "TF_CONFIG"
+        # TF_CONFIG (byte-compatible with the reference) plus our TFJOB_TASK_GPUS (GPUs per task of every replica
+        # type, for replicas that drive several local GPUs; the reference's test pins only TF_CONFIG)
+        assert len(cs) == 1 and [e["name"] for e in cs[0]["env"]] == ["TF_CONFIG", "TFJOB_TASK_GPUS"]
+        assert json.loads(cs[0]["env"][1]["value"]) == {"ps": 0}
         tfc = json.loads(cs[0]["env"][0]["value"])
         # reference test sees an empty cluster because its job was never set up; ours is derived from the spec
         assert tfc == {"cluster": {"ps": ["some-job-ps-some-runtime-0:10", "some-job-ps-some-runtime-1:10"]},
