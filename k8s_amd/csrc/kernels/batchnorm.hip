@@ -556,6 +556,15 @@ void launch_bn_fwd_from_sums(const uint16_t* x, const uint16_t* res, const float
   launch_bn_apply(x, res, params, y, mask, M, C, relu, st);
 }
 
+// Statistics finalize only (mean, invstd, running stats, [scale | shift]): the apply happens in the consuming
+// convolution's operand load (gemm.hip XForm, normalize on load).
+void launch_bn_finalize_sums(const float* gamma, const float* beta, const float* sums, int nrep, float* save_mean,
+                             float* save_invstd, float* run_mean, float* run_var, float* params, long M, int C,
+                             float eps, float momentum, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, nrep, C, (float)M, eps,
+                     momentum, save_mean, save_invstd, run_mean, run_var, gamma, beta, params);
+}
+
 static void launch_bn_bwd_apply(const uint16_t* dy, const uint16_t* x, const uint8_t* mask, const float* params,
                                 bool relu_x, uint16_t* dx, uint16_t* dres, long M, int C, hipStream_t st) {
   const long nvec = M * C / 8;

@@ -42,6 +42,33 @@ constexpr int GEMM_THREADS = 256;
 // 16-byte zero line for out-of-image implicit-GEMM loads
 __device__ __attribute__((aligned(64))) uint16_t g_zero_page[64];
 
+// BatchNorm + ReLU applied to an operand as it is staged into LDS ("normalize on load"): the operand is a BN
+// layer's raw input x and the GEMM consumes z = relu(fma(x, scale, shift)) -- bit-identical to what
+// batchnorm.hip's bn_apply_kernel would have written -- so the BN forward's apply pass (read x, write z) and the z
+// tensor disappear. p = fp32 [2][C] (scale | shift, from bn_finalize); an operand element's channel is its K index
+// (A, K-major) or its column (B, MN-major) modulo C. Zero padding (taps outside the image, split-K / tile tails)
+// stays zero: those loads are recognised by their zero-page source address and not transformed.
+struct XForm {
+  const float* p;
+  int C;
+  FastDiv fC;
+};
+
+__device__ __forceinline__ bf16x8_t bn_relu8(const bf16x8_t& v, const float (&sc)[8], const float (&sh)[8],
+                                             bool valid) {
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = fmaxf(__builtin_fmaf(bf2f((uint16_t)v[j]), sc[j], sh[j]), 0.f);
+  const bf16x8_t r = pack_bf16x8(o);
+  return valid ? r : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+}
+
+__device__ __forceinline__ void load_f8g(const float* p, float (&o)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+  o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+
 // ----------------------------------------------------------------------------- operand sources
 // stage(): called for round 0..3, writes slot s = round*256 + tid of a 16 KB tile.
 struct KMajor {
@@ -73,6 +100,8 @@ struct KMajor {
   }
   // per-K-step uniform part of the address (identity here; see ConvA)
   __device__ __forceinline__ int tap(int k0) const { return k0; }
+  // channel of K index k0 (a 1x1 convolution's activation: K is the channel)
+  __device__ __forceinline__ int chan0(int k0) const { return k0; }
   static constexpr bool kmajor = true;
 };
 
@@ -145,6 +174,8 @@ struct ConvA {
     if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) return g_zero_page;
     return q.p + t.off;
   }
+  // channel of K index k0 = (r, s, c0): c0 (a K step lies inside one tap, C % 64 == 0)
+  __device__ __forceinline__ int chan0(int k0) const { return k0 - fC.div(k0) * C; }
   static constexpr bool kmajor = true;
 };
 
@@ -345,10 +376,14 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 // F32S (general epilogue only): fp32 outputs without bias / activation / statistics / row remap -- the weight
 // gradients and their split-K slabs -- go through LDS and leave as whole 256-B row segments; its own instantiation
 // for the weight-gradient operand pairs.
+// XF (normalize on load, see XForm): 1 = the A operand (K-major: a convolution's activation), 2 = the B operand
+// (MN-major: a weight gradient's im2col / activation operand) is loaded through VGPRs, transformed and written to
+// its LDS slot by ds_write instead of by LDS-DMA (same lane-linear image, same swizzle). The staging registers of
+// the next K step are filled behind this step's MFMAs and written after them, before the step's barrier.
 template <class ASrc, class BSrc, int NBUF, int WM = 2, int WN = 2, bool LEAN = false, bool BNB = false,
-          bool XEPI = false, bool F32S = false>
-__global__ void __launch_bounds__(GEMM_THREADS, (NBUF == 1 && !BNB) ? 3 : 2)
-gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
+          bool XEPI = false, bool F32S = false, int XF = 0>
+__global__ void __launch_bounds__(GEMM_THREADS, (NBUF == 1 && !BNB && XF == 0) ? 3 : 2)
+gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XForm X) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
   constexpr int TA = BM * BK * 2, TB = BN * BK * 2;  // operand tile bytes
   static_assert(WM * WN == 4, "4 waves");
@@ -399,23 +434,95 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
 #pragma unroll
     for (int rd = 0; rd < RB; ++rd) cb[rd] = B.cursor(rd * GEMM_THREADS + tid, n0);
   }
+  static_assert(XF == 0 || (XF == 1 && ASrc::kmajor) || (XF == 2 && !BSrc::kmajor),
+                "normalize-on-load: K-major A or MN-major B");
+  // LDS-DMA staging of the operands that are not transformed
   auto stage = [&](int buf, int k0) {
     char* ta = smem + buf * (TA + TB);
     char* tb = ta + TA;
     if constexpr (HOIST) {
       const auto tpa = A.tap(k0);
       const auto tpb = B.tap(k0);
+      if constexpr (XF != 1) {
 #pragma unroll
-      for (int rd = 0; rd < RA; ++rd) glds16(A.at(ca[rd], tpa), ta + (rd * GEMM_THREADS + wid_u * 64) * 16);
+        for (int rd = 0; rd < RA; ++rd) glds16(A.at(ca[rd], tpa), ta + (rd * GEMM_THREADS + wid_u * 64) * 16);
+      }
+      if constexpr (XF != 2) {
 #pragma unroll
-      for (int rd = 0; rd < RB; ++rd) glds16(B.at(cb[rd], tpb), tb + (rd * GEMM_THREADS + wid_u * 64) * 16);
+        for (int rd = 0; rd < RB; ++rd) glds16(B.at(cb[rd], tpb), tb + (rd * GEMM_THREADS + wid_u * 64) * 16);
+      }
     } else {
+      if constexpr (XF != 1) {
 #pragma unroll
-      for (int rd = 0; rd < RA; ++rd)
-        glds16(A.src(rd * GEMM_THREADS + tid, m0, k0), ta + (rd * GEMM_THREADS + wid_u * 64) * 16);
+        for (int rd = 0; rd < RA; ++rd)
+          glds16(A.src(rd * GEMM_THREADS + tid, m0, k0), ta + (rd * GEMM_THREADS + wid_u * 64) * 16);
+      }
+      if constexpr (XF != 2) {
 #pragma unroll
-      for (int rd = 0; rd < RB; ++rd)
-        glds16(B.src(rd * GEMM_THREADS + tid, n0, k0), tb + (rd * GEMM_THREADS + wid_u * 64) * 16);
+        for (int rd = 0; rd < RB; ++rd)
+          glds16(B.src(rd * GEMM_THREADS + tid, n0, k0), tb + (rd * GEMM_THREADS + wid_u * 64) * 16);
+      }
+    }
+  };
+  // ---- normalize on load: the transformed operand goes global -> VGPR (xload) -> transform -> LDS (xstore)
+  constexpr int RX = XF == 1 ? RA : (XF == 2 ? RB : 1);
+  bf16x8_t xr[RX];
+  bool xok[RX];
+  float xsc[8], xsh[8];
+  // a thread's 16-B slots all cover the same 8 channels: K-major chunk (tid & 7) ^ ((tid >> 4) & 7) of the K step
+  // (A), or MN-major unit (tid & 15) ^ mn_swz(tid >> 4) of the tile's columns (B) -- fixed for the whole kernel
+  if constexpr (XF == 2) {
+    const int col = n0 + (((tid & 15) ^ mn_swz(tid >> 4)) << 3);
+    const int ch = col < N ? col - X.fC.div(col) * X.C : 0;
+    load_f8g(X.p + ch, xsc);
+    load_f8g(X.p + X.C + ch, xsh);
+  }
+  auto xload = [&](int k0) {
+    if constexpr (XF == 1) {
+      const int ch = A.chan0(k0) + (((tid & 7) ^ ((tid >> 4) & 7)) << 3);
+      load_f8g(X.p + ch, xsc);
+      load_f8g(X.p + X.C + ch, xsh);
+      if constexpr (HOIST) {
+        const auto tpa = A.tap(k0);
+#pragma unroll
+        for (int rd = 0; rd < RA; ++rd) {
+          const void* q = A.at(ca[rd], tpa);
+          xok[rd] = q != (const void*)g_zero_page;
+          xr[rd] = *reinterpret_cast<const bf16x8_t*>(q);
+        }
+      } else {
+#pragma unroll
+        for (int rd = 0; rd < RA; ++rd) {
+          const void* q = A.src(rd * GEMM_THREADS + tid, m0, k0);
+          xok[rd] = q != (const void*)g_zero_page;
+          xr[rd] = *reinterpret_cast<const bf16x8_t*>(q);
+        }
+      }
+    } else if constexpr (XF == 2) {
+      if constexpr (HOIST) {
+        const auto tpb = B.tap(k0);
+#pragma unroll
+        for (int rd = 0; rd < RB; ++rd) {
+          const void* q = B.at(cb[rd], tpb);
+          xok[rd] = q != (const void*)g_zero_page;
+          xr[rd] = *reinterpret_cast<const bf16x8_t*>(q);
+        }
+      } else {
+#pragma unroll
+        for (int rd = 0; rd < RB; ++rd) {
+          const void* q = B.src(rd * GEMM_THREADS + tid, n0, k0);
+          xok[rd] = q != (const void*)g_zero_page;
+          xr[rd] = *reinterpret_cast<const bf16x8_t*>(q);
+        }
+      }
+    }
+  };
+  auto xstore = [&](int buf) {
+    if constexpr (XF != 0) {
+      char* t = smem + buf * (TA + TB) + (XF == 1 ? 0 : TA);
+#pragma unroll
+      for (int rd = 0; rd < RX; ++rd)
+        *reinterpret_cast<bf16x8_t*>(t + (rd * GEMM_THREADS + tid) * 16) = bn_relu8(xr[rd], xsc, xsh, xok[rd]);
     }
   };
 
@@ -431,9 +538,10 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
     }
   };
   int xbuf = -1;  // LDS region holding the x tile (BNB)
-  const bool late = nt >= E.late_nt;
+  const bool late = XF == 0 && nt >= E.late_nt;
   if (nt > 0) {
     stage(0, kbeg);
+    xload(kbeg);
     if constexpr (BNB && NBUF == 1) {
       if (E.bstats) {
         stage_x(smem + (TA + TB));
@@ -441,6 +549,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    xstore(0);
     __syncthreads();
   }
   for (int t = 0; t < nt; ++t) {
@@ -448,11 +557,14 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
     if (NBUF == 1) {
       if (t > 0) {  // the previous tile's reads are done (barrier at the end of the last iteration)
         stage(0, kbeg + t * BK);
+        xload(kbeg + t * BK);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        xstore(0);
         __syncthreads();
       }
     } else if (!late && t + 1 < nt) {
       stage(cur ^ 1, kbeg + (t + 1) * BK);
+      xload(kbeg + (t + 1) * BK);
     }
     const char* ta = smem + cur * (TA + TB);
     const char* tb = ta + TA;
@@ -484,6 +596,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split) {
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (NBUF == 2 && t + 1 < nt) xstore(cur ^ 1);  // the idle buffer: its last reader finished before the last barrier
     __syncthreads();
   }
 
@@ -807,16 +920,17 @@ static int effective_splits(int K, int splits) {
   return (K + kps - 1) / kps;
 }
 
-template <class ASrc, class BSrc, int WM, int WN, bool LEAN, bool BNB, bool XEPI = false, bool F32S = false>
+template <class ASrc, class BSrc, int WM, int WN, bool LEAN, bool BNB, bool XEPI = false, bool F32S = false,
+          int XF = 0>
 static void launch_tiles2(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
-                          hipStream_t st) {
+                          hipStream_t st, const XForm& x = XForm{nullptr, 0, FastDiv{}}) {
   const int tiles = ((M + 64 * WM - 1) / (64 * WM)) * ((N + 64 * WN - 1) / (64 * WN));
   if (kps <= 2 * BK)
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN, LEAN, BNB, XEPI, F32S>), dim3(tiles, 1, splits),
-                       dim3(GEMM_THREADS), 0, st, a, b, e, M, N, K, kps);
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN, LEAN, BNB, XEPI, F32S, XF>), dim3(tiles, 1, splits),
+                       dim3(GEMM_THREADS), 0, st, a, b, e, M, N, K, kps, x);
   else
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2, WM, WN, LEAN, BNB, XEPI, F32S>), dim3(tiles, 1, splits),
-                       dim3(GEMM_THREADS), 0, st, a, b, e, M, N, K, kps);
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2, WM, WN, LEAN, BNB, XEPI, F32S, XF>), dim3(tiles, 1, splits),
+                       dim3(GEMM_THREADS), 0, st, a, b, e, M, N, K, kps, x);
 }
 
 // the lean epilogue applies: bf16 C (16-B aligned rows), store or accumulate, no atomics; bias / ReLU / GELU /
@@ -843,7 +957,25 @@ constexpr bool kBnbPair = (std::is_same_v<ASrc, KMajor> && std::is_same_v<BSrc, 
 
 template <class ASrc, class BSrc, int WM, int WN>
 static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
-                         hipStream_t st) {
+                         hipStream_t st, const XForm* xf = nullptr) {
+  // normalize-on-load instantiations: the convolution forward (A = the BN input, lean epilogue with statistics) and
+  // the weight gradients (B = the BN input, fp32 output or split-K slab through the F32S epilogue)
+  if (xf) {
+    if constexpr (std::is_same_v<ASrc, ConvA> && std::is_same_v<BSrc, KMajor>) {
+      if (lean_epi(e, N, false) && !e.bstats && !e.rst && !e.addsrc) {
+        launch_tiles2<ASrc, BSrc, WM, WN, true, false, false, false, 1>(a, b, e, M, N, K, kps, splits, st, *xf);
+        return;
+      }
+    }
+    if constexpr (std::is_same_v<ASrc, MNMajorK> && (std::is_same_v<BSrc, ConvWgB> || std::is_same_v<BSrc, MNMajorK>) &&
+                  WM == 2 && WN == 2) {
+      if (e.out_f32 && e.mode != 2 && !epi_extra(e) && !e.stats && !e.rst) {
+        launch_tiles2<ASrc, BSrc, WM, WN, false, false, false, true, 2>(a, b, e, M, N, K, kps, splits, st, *xf);
+        return;
+      }
+    }
+    throw std::runtime_error("normalize-on-load: no instantiation for this operand pair / epilogue");
+  }
   // the linear forward (both operands K-major) is the one pair with a bias / activation epilogue instantiation
   constexpr bool kXepi = std::is_same_v<ASrc, KMajor> && std::is_same_v<BSrc, KMajor>;
   if constexpr (kXepi) {
@@ -881,16 +1013,17 @@ static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int 
 }
 
 template <class ASrc, class BSrc>
-static void launch(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int splits, hipStream_t st) {
+static void launch(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int splits, hipStream_t st,
+                   const XForm* xf = nullptr) {
   const int kps = ((K + splits - 1) / splits + BK - 1) / BK * BK;
   splits = (K + kps - 1) / kps;
   if constexpr (ASrc::kmajor && BSrc::kmajor) {
     if (N <= 64) {  // 256 x 64 tiles: no half-empty 128-wide column tile
-      launch_tiles<ASrc, BSrc, 4, 1>(a, b, e, M, N, K, kps, splits, st);
+      launch_tiles<ASrc, BSrc, 4, 1>(a, b, e, M, N, K, kps, splits, st, xf);
       return;
     }
   }
-  launch_tiles<ASrc, BSrc, 2, 2>(a, b, e, M, N, K, kps, splits, st);
+  launch_tiles<ASrc, BSrc, 2, 2>(a, b, e, M, N, K, kps, splits, st, xf);
 }
 
 static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act, uint16_t* pre, int mode,
@@ -993,7 +1126,8 @@ static void apply_bnbwd(Epi& e, const BnBwdEpi* bb) {
 
 void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                  long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
-                 float alpha, int splits, float* ws, hipStream_t st, const BnBwdEpi* bnb, const AddEpi* add) {
+                 float alpha, int splits, float* ws, hipStream_t st, const BnBwdEpi* bnb, const AddEpi* add,
+                 const float* xform_b, int xform_c) {
   splits = effective_splits(K, splits);
   const bool slab = splits > 1;
   Epi e = make_epi(slab ? (void*)ws : C, slab ? (long)N : ldc, c_f32, bias, act, pre, slab ? 3 : mode, alpha);
@@ -1004,7 +1138,11 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
     e.addsrc = add->src;
     e.addmask = add->mask;
   }
-  if (a_kmajor && b_kmajor)
+  if (xform_b) {  // B = relu(bn(x)) normalised on load: the plain (1x1) weight gradient
+    if (a_kmajor || b_kmajor) throw std::runtime_error("normalize-on-load GEMM: MN-major A and B");
+    const XForm xf{xform_b, xform_c, make_fastdiv(xform_c)};
+    launch(MNMajorK{A, lda, M, K}, MNMajorK{B, ldb, N, K}, e, M, N, K, splits, st, &xf);
+  } else if (a_kmajor && b_kmajor)
     launch(KMajor{A, lda, M}, KMajor{B, ldb, N}, e, M, N, K, splits, st);
   else if (a_kmajor && !b_kmajor)
     launch(KMajor{A, lda, M}, MNMajorK{B, ldb, N, K}, e, M, N, K, splits, st);
@@ -1019,7 +1157,8 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
 // decode, any other C % 8 == 0 the per-unit one.
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int K,
                      int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
-                     int mode, float* stats, hipStream_t st, const BnBwdEpi* bnb, const SubGrid* sg) {
+                     int mode, float* stats, hipStream_t st, const BnBwdEpi* bnb, const SubGrid* sg,
+                     const float* xform) {
   const int M = N * Ho * Wo, RSC = R * S * C;
   KMajor b{w, (long)RSC, K, RSC};
   Epi e = make_epi(y, K, y_f32, bias, act, nullptr, mode, 1.f);
@@ -1035,10 +1174,16 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, 
     e.ra = sg->a;
     e.rb = sg->b;
   }
+  if (xform && C % 64 != 0) throw std::runtime_error("normalize-on-load convolution needs C % 64 == 0");
   if (C % 64 == 0) {
     ConvA a{x, N, H, W, C, Ho, Wo, S, stride, pad, dil, M,
             make_fastdiv(C), make_fastdiv(S), make_fastdiv(Ho * Wo), make_fastdiv(Wo)};
-    launch(a, b, e, M, K, RSC, 1, st);
+    if (xform) {
+      const XForm xf{xform, C, make_fastdiv(C)};
+      launch(a, b, e, M, K, RSC, 1, st, &xf);
+    } else {
+      launch(a, b, e, M, K, RSC, 1, st);
+    }
   } else {
     ConvAG a{x, N, H, W, C, Ho, Wo, S, stride, pad, dil, M, RSC,
              make_fastdiv(C), make_fastdiv(S), make_fastdiv(Ho * Wo), make_fastdiv(Wo)};
@@ -1049,7 +1194,7 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, 
 // Weight gradient: dw[K][R*S*C] fp32 (+)= dY^T . im2col(x); split-K through fp32 slabs in `ws`
 void launch_conv_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int C, int K, int R,
                        int S, int stride, int pad, int dil, int Ho, int Wo, int splits, bool accumulate, float* ws,
-                       hipStream_t st) {
+                       hipStream_t st, const float* xform) {
   const int M = N * Ho * Wo;  // reduction dim
   MNMajorK a{dy, (long)K, K, M};
   ConvWgB b{x, N, H, W, C, Ho, Wo, S, stride, pad, dil, R * S * C, M,
@@ -1060,7 +1205,12 @@ void launch_conv_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int N, 
   Epi e = make_epi(slab ? (void*)ws : (void*)dw, (long)RSC, true, nullptr, 0, nullptr, slab ? 3 : (accumulate ? 1 : 0),
                    1.f);
   e.slab = (long)K * RSC;
-  launch(a, b, e, K, RSC, M, splits, st);
+  if (xform) {
+    const XForm xf{xform, C, make_fastdiv(C)};
+    launch(a, b, e, K, RSC, M, splits, st, &xf);
+  } else {
+    launch(a, b, e, K, RSC, M, splits, st);
+  }
   if (slab) splitk_reduce(ws, splits, (long)K * RSC, dw, accumulate, st);
 }
 

@@ -30,6 +30,9 @@ void launch_bn_fwd_from_sums(const uint16_t* x, const uint16_t* res, const float
                              uint16_t* y, const float* sums, int nrep, float* save_mean, float* save_invstd,
                              float* run_mean, float* run_var, float* params, long M, int C, float eps, float momentum,
                              bool relu, hipStream_t st, uint8_t* mask = nullptr);
+void launch_bn_finalize_sums(const float* gamma, const float* beta, const float* sums, int nrep, float* save_mean,
+                             float* save_invstd, float* run_mean, float* run_var, float* params, long M, int C,
+                             float eps, float momentum, hipStream_t st);
 constexpr int kConvStatReplicas = 32;  // must match STAT_REPL in gemm.hip
 void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, const float* invstd, const float* gamma,
                    const float* beta, bool relu_x, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta,
@@ -77,7 +80,7 @@ struct AddEpi {
 void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                  long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
                  float alpha, int splits, float* ws, hipStream_t st, const BnBwdEpi* bnb = nullptr,
-                 const AddEpi* add = nullptr);
+                 const AddEpi* add = nullptr, const float* xform_b = nullptr, int xform_c = 0);
 // out = bit ? src : 0 per element (bf16, n % 8 == 0; mask packed as above)
 void launch_mask_apply(const uint16_t* src, const uint8_t* mask, uint16_t* out, long n, hipStream_t st);
 long gemm_splitk_workspace(int M, int N, int splits);  // fp32 elements of the split-K slab workspace
@@ -94,10 +97,12 @@ struct SubGrid {
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int K,
                      int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
                      int mode, float* stats, hipStream_t st,
-                     const BnBwdEpi* bnb = nullptr, const SubGrid* sg = nullptr);
+                     const BnBwdEpi* bnb = nullptr, const SubGrid* sg = nullptr, const float* xform = nullptr);
+// xform (here and in launch_gemm / launch_wgrad_stream): fp32 [2][C] BatchNorm (scale | shift): the activation
+// operand x is consumed as relu(x * scale + shift), normalised as it is loaded (gemm.hip XForm)
 void launch_conv_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int C, int K, int R,
                        int S, int stride, int pad, int dil, int Ho, int Wo, int splits, bool accumulate, float* ws,
-                       hipStream_t st);
+                       hipStream_t st, const float* xform = nullptr);
 // wgrad_stream.hip: tall-K weight gradient (few output tiles, millions of rows), fp32 atomics into dw
 bool wgrad_stream_eligible(int N, int Ho, int Wo, int C, int K, int R, int S);
 void launch_wgrad_stream(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int C, int K, int R,

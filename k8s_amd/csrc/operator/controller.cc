@@ -1,3 +1,4 @@
+#include <random>
 #include "controller.h"
 
 #include <cstdlib>
@@ -143,6 +144,35 @@ void Controller::watchdog_loop() {
   }
 }
 
+bool Controller::relist(std::string& rv) {
+  std::map<std::string, std::string> before;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    before = job_rvs_;
+  }
+  ApiResult l = api_.get(list_path());
+  if (!l.ok()) {
+    log_warn("relist failed: HTTP %d", l.code);
+    return false;
+  }
+  std::map<std::string, bool> seen;
+  if (const Json* items = l.body.find("items"); items && items->is_array())
+    for (auto& it : items->as_array()) {
+      TfJob j = tfjob_from_json(it);
+      seen[j.ns() + "/" + j.name()] = true;
+      handle_event("ADDED", it);  // idempotent for a job that already has a worker
+    }
+  for (auto& kv : before)
+    if (!seen.count(kv.first)) {
+      std::lock_guard<std::mutex> g(mu_);
+      auto jt = jobs_.find(kv.first);
+      if (jt != jobs_.end()) jt->second->request_delete();
+      job_rvs_.erase(kv.first);
+    }
+  if (const Json* m = l.body.find("metadata")) rv = get_str(*m, "resourceVersion");
+  return true;
+}
+
 std::string Controller::run() {
   std::thread watchdog(&Controller::watchdog_loop, this);
   struct Joiner {
@@ -168,15 +198,33 @@ std::string Controller::run() {
     log_error("%s; retrying", err.c_str());
     std::this_thread::sleep_for(std::chrono::seconds(1));
   }
+  std::mt19937 rng(std::random_device{}());
+  using clock = std::chrono::steady_clock;
+  auto last_relist = clock::now();
   while (!stop_) {
     std::string err;
-    auto w = api_.watch(list_path() + "?watch=true&resourceVersion=" + rv, err);
+    const long tmin = std::max<long>(1, (long)(opts_.watch_timeout.count() / 1000));
+    const long timeout_s = std::uniform_int_distribution<long>(tmin, 2 * tmin - 1 > tmin ? 2 * tmin - 1 : tmin)(rng);
+    auto w = api_.watch(list_path() + "?watch=true&resourceVersion=" + rv + "&timeoutSeconds=" +
+                            std::to_string(timeout_s), err);
     if (!w) {
       log_warn("watch failed: %s; retrying", err.c_str());
       std::this_thread::sleep_for(std::chrono::seconds(1));
       continue;
     }
+    // the server ends this watch after timeout_s; still open past the grace = nobody is on the other end
+    const auto dead_after = clock::now() + std::chrono::seconds(timeout_s) + opts_.watch_idle_grace;
     while (!stop_) {
+      if (clock::now() > dead_after) {
+        log_warn("watch open %lds past its timeoutSeconds=%ld: half-open connection, re-watching from rv=%s",
+                 (long)(opts_.watch_idle_grace.count() / 1000), timeout_s, rv.c_str());
+        break;
+      }
+      if (opts_.resync_period.count() > 0 && clock::now() - last_relist > opts_.resync_period) {
+        last_relist = clock::now();
+        log_v(1, "periodic resync: relisting TfJobs");
+        if (relist(rv)) break;  // re-watch from the list's resourceVersion
+      }
       Json ev;
       if (!w->next(ev, 1000, err)) {
         log_v(1, "watch stream ended: %s; re-watching from %s", err.c_str(), rv.c_str());
@@ -191,28 +239,8 @@ std::string Controller::run() {
         if (code == 410) {
           // resourceVersion too old: relist and diff (removed jobs are deleted, new ones started)
           log_warn("watch 410 Gone at rv=%s: relisting", rv.c_str());
-          std::map<std::string, std::string> before;
-          {
-            std::lock_guard<std::mutex> g(mu_);
-            before = job_rvs_;
-          }
-          ApiResult l = api_.get(list_path());
-          if (!l.ok()) break;
-          std::map<std::string, bool> seen;
-          if (const Json* items = l.body.find("items"); items && items->is_array())
-            for (auto& it : items->as_array()) {
-              TfJob j = tfjob_from_json(it);
-              seen[j.ns() + "/" + j.name()] = true;
-              handle_event("ADDED", it);
-            }
-          for (auto& kv : before)
-            if (!seen.count(kv.first)) {
-              std::lock_guard<std::mutex> g(mu_);
-              auto jt = jobs_.find(kv.first);
-              if (jt != jobs_.end()) jt->second->request_delete();
-              job_rvs_.erase(kv.first);
-            }
-          if (const Json* m = l.body.find("metadata")) rv = get_str(*m, "resourceVersion");
+          relist(rv);
+          last_relist = clock::now();
           break;
         }
         log_error("watch ERROR event: %s", obj ? obj->dump().c_str() : "");

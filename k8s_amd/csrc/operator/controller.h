@@ -32,6 +32,14 @@ struct ControllerOptions {
   std::chrono::milliseconds event_watchdog{60000};  // panicTimer: abort if one event takes longer
   std::chrono::milliseconds inject_handler_stall{0};  // fault injection: every event handler sleeps this long
   bool create_crd = true;
+  // Watch liveness (controller.go:292-361 re-watches on EOF; client-go's reflector asks the server to end every
+  // watch after a random 5-10 min timeoutSeconds). Each watch asks for timeoutSeconds in [watch_timeout,
+  // 2 * watch_timeout); a stream still open watch_idle_grace after that is a half-open connection (dropped by a
+  // NAT / load balancer without a FIN) and is closed and re-established from the last resourceVersion.
+  std::chrono::milliseconds watch_timeout{300000};
+  std::chrono::milliseconds watch_idle_grace{30000};
+  // full relist + diff (the 410 path) this often, so an event lost anywhere is still picked up (0 = off)
+  std::chrono::milliseconds resync_period{300000};
 };
 
 Json crd_manifest();  // the CustomResourceDefinition the operator installs
@@ -57,6 +65,8 @@ class Controller {
  private:
   std::string list_path() const { return tfjobs_path(opts_.ns); }
   void reap_finished();
+  // relist every TfJob, start the new ones, delete the vanished ones; updates rv. false on an API error.
+  bool relist(std::string& rv);
 
   KubeApi& api_;
   ControllerConfig cfg_;

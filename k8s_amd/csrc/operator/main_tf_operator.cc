@@ -75,6 +75,9 @@ int main(int argc, char** argv) {
   fl.def("request-timeout", "30s", "Deadline of every API request (connect, TLS handshake, response)");
   fl.def("event-watchdog", "60s", "Abort when one TfJob event handler runs longer (reference panicTimer: 1m)");
   fl.def("inject-handler-stall", "0s", "DO NOT USE IN PRODUCTION - fault injection: stall every TfJob event handler this long");
+  fl.def("watch-timeout", "5m", "Each TfJob watch asks the server to end it after a random timeoutSeconds in [t, 2t)");
+  fl.def("watch-idle-grace", "30s", "A watch still open this long past its timeoutSeconds is half-open: re-watch");
+  fl.def("resync-period", "5m", "Full relist of the TfJobs this often (0: never), so a lost watch event is recovered");
   std::string err = fl.parse(argc, argv);
   if (!err.empty()) {
     fprintf(stderr, "%s\nUsage of tf_operator:\n%s", err.c_str(), fl.usage().c_str());
@@ -132,6 +135,9 @@ int main(int argc, char** argv) {
   opts.reconcile.interval = std::chrono::milliseconds(parse_duration_ms(fl.str("reconcile-interval"), 8000));
   opts.event_watchdog = std::chrono::milliseconds(parse_duration_ms(fl.str("event-watchdog"), 60000));
   opts.inject_handler_stall = std::chrono::milliseconds(parse_duration_ms(fl.str("inject-handler-stall"), 0));
+  opts.watch_timeout = std::chrono::milliseconds(parse_duration_ms(fl.str("watch-timeout"), 300000));
+  opts.watch_idle_grace = std::chrono::milliseconds(parse_duration_ms(fl.str("watch-idle-grace"), 30000));
+  opts.resync_period = std::chrono::milliseconds(parse_duration_ms(fl.str("resync-period"), 300000));
   if (!cfg.grpc_server_file_path.empty()) {
     try {
       opts.reconcile.ps_server_source = read_file(cfg.grpc_server_file_path);

@@ -185,6 +185,33 @@ std::vector<Tensor> bn_fwd_from_sums(Tensor x, c10::optional<Tensor> res, Tensor
   return {y, mean, invstd};
 }
 
+// BatchNorm statistics of a conv output from its epilogue sums, WITHOUT the apply pass: returns (mean, invstd,
+// params = fp32 [2][C] scale | shift) for a consumer that normalises on load (conv_fwd / conv_wgrad / gemm xform).
+std::vector<Tensor> bn_finalize(Tensor sums, Tensor gamma, Tensor beta, Tensor run_mean, Tensor run_var,
+                                int64_t count, double momentum, double eps) {
+  const int C = (int)gamma.numel();
+  check_dtype(gamma, at::kFloat, "gamma");
+  TORCH_CHECK(sums.is_cuda() && sums.numel() % (2 * C) == 0 && sums.scalar_type() == at::kFloat &&
+                  sums.is_contiguous(), "sums must be fp32 [R, 2, C]");
+  TORCH_CHECK(beta.numel() == C && run_mean.numel() == C && run_var.numel() == C);
+  const int nrep = (int)(sums.numel() / (2 * C));
+  auto mean = torch::empty({C}, gamma.options());
+  auto invstd = torch::empty({C}, gamma.options());
+  auto params = torch::empty({2 * C}, gamma.options());
+  k8s_amd::launch_bn_finalize_sums(f32(gamma), f32(beta), f32(sums), nrep, f32(mean), f32(invstd), f32(run_mean),
+                                   f32(run_var), f32(params), (long)count, C, (float)eps, (float)momentum,
+                                   cur_stream());
+  return {mean, invstd, params};
+}
+
+static const float* xform_ptr(const c10::optional<Tensor>& xf, long C) {
+  if (!xf || !xf->defined()) return nullptr;
+  TORCH_CHECK(xf->is_cuda() && xf->scalar_type() == at::kFloat && xf->is_contiguous() && xf->numel() == 2 * C,
+              "xform must be fp32 [2 * C] (BatchNorm scale | shift)");
+  TORCH_CHECK(C % 8 == 0, "xform channels must be a multiple of 8");
+  return xf->data_ptr<float>();
+}
+
 // returns dx, dres (or empty), writes dgamma/dbeta into the given (flat-bucket view) tensors. The ReLU of the
 // forward comes from the packed `mask` (residual BN), is recomputed from x (`relu_x`), or -- given the BN output
 // `y` -- is packed from y first (compatibility; the trainer passes the mask).
@@ -363,7 +390,8 @@ Tensor mask_apply(Tensor src, Tensor mask) {
 Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tensor> out, bool out_f32,
             c10::optional<Tensor> bias, int64_t act, c10::optional<Tensor> pre, bool accumulate, double alpha,
             int64_t splits, c10::optional<std::vector<Tensor>> bnb, c10::optional<bool> bnb_relu_x,
-            c10::optional<Tensor> add_src, c10::optional<Tensor> add_mask) {
+            c10::optional<Tensor> add_src, c10::optional<Tensor> add_mask, c10::optional<Tensor> xform_b,
+            int64_t xform_c) {
   check_bf16_operand(a, "A");
   check_bf16_operand(b, "B");
   const long M = a_kmajor ? a.size(0) : a.size(1), K = a_kmajor ? a.size(1) : a.size(0);
@@ -398,7 +426,10 @@ Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tens
   } else {
     TORCH_CHECK(!add_mask, "add_mask needs add_src");
   }
-  if (!bnb && !add_src && use_gemm256(M, N, K, a_kmajor, b_kmajor)) {
+  const float* xfb = xform_ptr(xform_b, xform_c);
+  if (xfb) TORCH_CHECK(!a_kmajor && !b_kmajor && out_f32 && !bias && act == 0 && !pre && !bnb && !add_src &&
+                           N % xform_c == 0, "normalize-on-load GEMM: the plain weight-gradient form only");
+  if (!xfb && !bnb && !add_src && use_gemm256(M, N, K, a_kmajor, b_kmajor)) {
     k8s_amd::launch_gemm256(cbf(a), a.stride(0), a_kmajor, cbf(b), b.stride(0), b_kmajor, c.data_ptr(), N, out_f32,
                             (int)M, (int)N, (int)K, bias ? bias->data_ptr<float>() : nullptr, (int)act,
                             pre ? bf(*pre) : nullptr, accumulate, (float)alpha, cur_stream());
@@ -417,7 +448,7 @@ Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tens
   k8s_amd::launch_gemm(cbf(a), a.stride(0), a_kmajor, cbf(b), b.stride(0), b_kmajor, c.data_ptr(), N, out_f32,
                        (int)M, (int)N, (int)K, bias ? bias->data_ptr<float>() : nullptr, (int)act,
                        pre ? bf(*pre) : nullptr, mode, (float)alpha, sp, sp > 1 ? f32(ws) : nullptr, cur_stream(),
-                       bb.on ? &bb.e : nullptr, add_src ? &add : nullptr);
+                       bb.on ? &bb.e : nullptr, add_src ? &add : nullptr, xfb, (int)xform_c);
   return c;
 }
 
@@ -425,7 +456,7 @@ static inline int conv_out(int in, int k, int st, int pad, int dil) { return (in
 
 Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, bool out_f32, c10::optional<Tensor> bias,
                 int64_t act, c10::optional<Tensor> stats, c10::optional<std::vector<Tensor>> bnb,
-                c10::optional<bool> bnb_relu_x) {
+                c10::optional<bool> bnb_relu_x, c10::optional<Tensor> xform) {
   check_cuda(x, "x"); check_cuda(w, "w");
   check_dtype(x, at::kBFloat16, "x"); check_dtype(w, at::kBFloat16, "w");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "x [N,H,W,C], w [K,R,S,C]");
@@ -441,9 +472,12 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, bo
                          "stats must be zeroed fp32 [conv_stat_replicas, 2, K]");
   BnbHolder bb = parse_bnb(bnb, bnb_relu_x, (long)N * Ho * Wo, K);
   TORCH_CHECK(!bb.on || (!out_f32 && !stats), "the BN-backward epilogue needs a bf16 output and no fwd stats");
+  const float* xf = xform_ptr(xform, C);
+  if (xf) TORCH_CHECK(C % 64 == 0 && !out_f32 && !bias && act == 0 && !bb.on,
+                      "normalize-on-load convolution: C % 64 == 0, bf16 output, no bias / activation");
   k8s_amd::launch_conv_fwd(cbf(x), cbf(w), y.data_ptr(), out_f32, N, H, W, C, K, R, S, (int)stride, (int)pad,
                            (int)dil, Ho, Wo, bias ? bias->data_ptr<float>() : nullptr, (int)act, 0,
-                           stats ? f32(*stats) : nullptr, cur_stream(), bb.on ? &bb.e : nullptr);
+                           stats ? f32(*stats) : nullptr, cur_stream(), bb.on ? &bb.e : nullptr, nullptr, xf);
   return y;
 }
 
@@ -472,7 +506,7 @@ void conv_fwd_subgrid(Tensor x, Tensor w, int64_t pad, int64_t Hs, int64_t Ws, T
 
 // dw[K,R,S,C] fp32 (+)= dy^T . im2col(x)
 void conv_wgrad(Tensor x, Tensor dy, Tensor dw, int64_t stride, int64_t pad, int64_t dil, int64_t splits,
-                bool accumulate) {
+                bool accumulate, c10::optional<Tensor> xform) {
   check_cuda(x, "x"); check_cuda(dy, "dy"); check_cuda(dw, "dw");
   check_dtype(x, at::kBFloat16, "x"); check_dtype(dy, at::kBFloat16, "dy"); check_dtype(dw, at::kFloat, "dw");
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
@@ -480,8 +514,9 @@ void conv_wgrad(Tensor x, Tensor dy, Tensor dw, int64_t stride, int64_t pad, int
   TORCH_CHECK(dw.size(3) == C && C % 8 == 0 && K % 8 == 0);
   const int Ho = conv_out(H, R, stride, pad, dil), Wo = conv_out(W, S, stride, pad, dil);
   TORCH_CHECK(dy.size(0) == N && dy.size(1) == Ho && dy.size(2) == Wo && dy.size(3) == K, "dy shape mismatch");
+  const float* xf = xform_ptr(xform, C);
   const char* ws_env = std::getenv("K8S_AMD_WGRAD_STREAM");  // =0: generic split-K GEMM (A/B)
-  if (!(ws_env && ws_env[0] == '0') && dil == 1 && dy.is_contiguous() && x.is_contiguous() &&
+  if (!xf && !(ws_env && ws_env[0] == '0') && dil == 1 && dy.is_contiguous() && x.is_contiguous() &&
       k8s_amd::wgrad_stream_eligible(N, Ho, Wo, C, K, R, S)) {
     k8s_amd::launch_wgrad_stream(cbf(x), cbf(dy), f32(dw), N, H, W, C, K, R, S, (int)stride, (int)pad, Ho, Wo,
                                  accumulate, cur_stream());
@@ -490,8 +525,9 @@ void conv_wgrad(Tensor x, Tensor dy, Tensor dw, int64_t stride, int64_t pad, int
   int sp = splits <= 0 ? k8s_amd::gemm_choose_splits(K, R * S * C, N * Ho * Wo) : (int)splits;
   Tensor ws;
   if (sp > 1) ws = torch::empty({k8s_amd::gemm_splitk_workspace(K, R * S * C, sp)}, dw.options());
+  if (xf) TORCH_CHECK(C % 64 == 0, "normalize-on-load weight gradient needs C % 64 == 0");
   k8s_amd::launch_conv_wgrad(cbf(x), cbf(dy), f32(dw), N, H, W, C, K, R, S, (int)stride, (int)pad, (int)dil, Ho, Wo,
-                             sp, accumulate, sp > 1 ? f32(ws) : nullptr, cur_stream());
+                             sp, accumulate, sp > 1 ? f32(ws) : nullptr, cur_stream(), xf);
 }
 
 // taps: per parity, the list of r*S + s tap indices (row-major over its [Tr][Ts] grid); returns one packed bf16
@@ -872,7 +908,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm, py::arg("a"), py::arg("a_kmajor"), py::arg("b"), py::arg("b_kmajor"), py::arg("out"),
         py::arg("out_f32"), py::arg("bias"), py::arg("act"), py::arg("pre"), py::arg("accumulate"), py::arg("alpha"),
         py::arg("splits"), py::arg("bnb") = py::none(), py::arg("bnb_relu_x") = py::none(),
-        py::arg("add_src") = py::none(), py::arg("add_mask") = py::none());
+        py::arg("add_src") = py::none(), py::arg("add_mask") = py::none(), py::arg("xform_b") = py::none(),
+        py::arg("xform_c") = 0);
+  m.def("bn_finalize", &bn_finalize, py::arg("sums"), py::arg("gamma"), py::arg("beta"), py::arg("run_mean"),
+        py::arg("run_var"), py::arg("count"), py::arg("momentum"), py::arg("eps"));
   m.def("mask_apply", &mask_apply, "out = bit ? src : 0 (packed 1-bit mask per element)");
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
@@ -884,8 +923,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none());
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
         py::arg("out_f32"), py::arg("bias"), py::arg("act"), py::arg("stats"), py::arg("bnb") = py::none(),
-        py::arg("bnb_relu_x") = py::none());
-  m.def("conv_wgrad", &conv_wgrad);
+        py::arg("bnb_relu_x") = py::none(), py::arg("xform") = py::none());
+  m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
+        py::arg("dil"), py::arg("splits"), py::arg("accumulate"), py::arg("xform") = py::none());
   m.def("conv_fwd_subgrid", &conv_fwd_subgrid, py::arg("x"), py::arg("w"), py::arg("pad"), py::arg("Hs"),
         py::arg("Ws"), py::arg("out"), py::arg("stride"), py::arg("a"), py::arg("b"), py::arg("accumulate") = false);
   m.def("conv_dgrad_wtrans", &conv_dgrad_wtrans);

@@ -89,10 +89,18 @@ class Bottleneck(nn.Module):
         if self.down is not None:
             mlink = K.MaskLink()
             idn = self.down_bn(self.down(x, grad_link=dlink), relu=False, dy_link=mlink)
-        y = self.bn1(self.conv1(x, grad_link=link or dlink, bn_link=in_link if identity else None), bwd_link=l1)
-        y = self.bn2(self.conv2(y, bn_link=l1), bwd_link=l2)
-        return self.bn3(self.conv3(y, bn_link=l2), residual=idn, relu=True, res_link=link or mlink,
-                        bwd_link=l3), l3
+        t = self.conv1(x, grad_link=link or dlink, bn_link=in_link if identity else None)
+        # bn1 / bn2 + ReLU: normalised on load by the consuming convolution (ops.nn.bn_relu_conv, no apply pass)
+        # or applied by the BN kernel; ops.nn.BN_ONLOAD picks which
+        if K.BN_ONLOAD == "all":
+            t = K.bn_relu_conv(t, self.bn1, self.conv2)
+        else:
+            t = self.conv2(self.bn1(t, bwd_link=l1), bn_link=l1)
+        if K.BN_ONLOAD in ("all", "1x1"):
+            t = K.bn_relu_conv(t, self.bn2, self.conv3)
+        else:
+            t = self.conv3(self.bn2(t, bwd_link=l2), bn_link=l2)
+        return self.bn3(t, residual=idn, relu=True, res_link=link or mlink, bwd_link=l3), l3
 
 
 class ResNet(nn.Module):

@@ -103,17 +103,20 @@ def _aten_bwd(gy, x, w, stride, padding, need_dx, need_dw):
     return (_nhwc(dx) if dx is not None else None), (dw.permute(0, 2, 3, 1) if dw is not None else None)
 
 
-def _wgrad_hip(C_, gy, x, out, stride, padding, acc):
+def _wgrad_hip(C_, gy, x, out, stride, padding, acc, xform=None):
     """dW (fp32, written or accumulated into ``out``): the streaming tall-K kernel where it applies (1x1 and
     strided layers with few output tiles; decided in the binding), a plain split-K GEMM for other 1x1 / stride 1
-    layers (no im2col decode), else the implicit-GEMM split-K kernel."""
+    layers (no im2col decode), else the implicit-GEMM split-K kernel. ``xform`` (fp32 [2, C] BatchNorm scale |
+    shift): the activation operand is relu(x * scale + shift), normalised as the GEMM loads it (the streaming
+    kernel has no such path: those shapes take the GEMMs)."""
     K, R, S, C = out.shape
     N, Ho, Wo = gy.shape[0], gy.shape[1], gy.shape[2]
     if (R == 1 and S == 1 and stride == 1 and padding == 0
-            and not C_.wgrad_stream_eligible(N, Ho, Wo, C, K, R, S)):
-        C_.gemm(gy.reshape(-1, K), False, x.reshape(-1, C), False, out.view(K, C), True, None, 0, None, acc, 1.0, 0)
+            and (xform is not None or not C_.wgrad_stream_eligible(N, Ho, Wo, C, K, R, S))):
+        C_.gemm(gy.reshape(-1, K), False, x.reshape(-1, C), False, out.view(K, C), True, None, 0, None, acc, 1.0, 0,
+                xform_b=xform, xform_c=C if xform is not None else 0)
     else:
-        C_.conv_wgrad(x, gy, out, stride, padding, 1, 0, acc)
+        C_.conv_wgrad(x, gy, out, stride, padding, 1, 0, acc, xform=xform)
 
 
 def _dgrad_hip(C_, gy, w, padding, addend=None, bnb=None):
@@ -198,12 +201,17 @@ def _dgrad_strided_hip(C_, gy, w, stride, padding, H, W, addend=None):
     return dx
 
 
-def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, bn_link=None):
+def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, bn_link=None, xform=None):
     """Returns dx (+ ``addend``, e.g. the residual branch's gradient of the same tensor, fused into the
-    dgrad epilogue where our kernel runs) or None; deposits dw into ``p``'s flat gradient slot."""
+    dgrad epilogue where our kernel runs) or None; deposits dw into ``p``'s flat gradient slot. ``xform``: the
+    convolution's input is relu(bn(x)) normalised on load (see ``_wgrad_hip``); dx is then the gradient w.r.t.
+    that normalised input."""
     K, R, S, C = w.shape
     C_ = _load() if gy.is_cuda else None
     hip = _hip(gy, x, w)
+    if xform is not None and not (hip and C % 64 == 0 and K % 8 == 0 and p is not None
+                                  and p.grad.dtype == torch.float32):
+        raise RuntimeError("normalize-on-load weight gradient outside the kernels' contract")
     if addend is not None and not torch.is_tensor(addend) and not (
             hip and stride == 1 and K % 64 == 0 and C % 8 == 0):
         addend = addend.materialize()  # only the stride-1 dgrad on our kernels takes the (dy, mask) pair
@@ -212,7 +220,7 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, bn_link=No
     if hip and C % 8 == 0 and K % 8 == 0 and p is not None and p.grad.dtype == torch.float32:
         STATS["hip_wgrad"] += 1
         acc = p.written
-        _wgrad_hip(C_, gy, x, p.grad.view(w.shape), stride, padding, acc)
+        _wgrad_hip(C_, gy, x, p.grad.view(w.shape), stride, padding, acc, xform)
         if acc:
             p.store._notify(p)
         else:

@@ -300,6 +300,77 @@ class _BnAct(torch.autograd.Function):
                 None, None)
 
 
+# Which BatchNorm + ReLU outputs of a ResNet bottleneck are normalised on load by the convolution that consumes them
+# (``bn_relu_conv``) instead of being written by an apply pass: "1x1" = bn2 -> conv3 (default), "all" = also
+# bn1 -> the 3x3 conv2, "0" = none. (The 3x3 consumer re-applies the transform to each input element once per tap:
+# 9x the VALU work of an apply pass, inside a compute-bound product.)
+BN_ONLOAD = os.environ.get("K8S_AMD_BN_ONLOAD", "1x1")
+
+
+def _bn_param_grads(store, pg, pb, device):
+    sg, sb = store.slot_for_write(pg), store.slot_for_write(pb)
+    dg = sg if sg is not None else torch.empty(pg.shape, device=device, dtype=torch.float32)
+    db = sb if sb is not None else torch.empty(pb.shape, device=device, dtype=torch.float32)
+
+    def finish():
+        store.mark_written(pg) if sg is not None else store.deposit(pg, dg)
+        store.mark_written(pb) if sb is not None else store.deposit(pb, db)
+
+    return dg, db, finish
+
+
+class _BnReluConv(torch.autograd.Function):
+    """conv(relu(BN(x)), w) for a training-mode BatchNorm whose statistics came from x's producing conv epilogue
+    (``sums``): the BN is finalised to per-channel (scale, shift) and APPLIED INSIDE THE CONVOLUTION'S OPERAND LOAD
+    (gemm.hip XForm) -- the z = relu(BN(x)) tensor is never written, saving the apply pass (read x, write z) and
+    z's memory. Backward: the weight gradient normalises x on load the same way; the data gradient gives dz, and
+    the BN backward (reduce + apply, ReLU mask recomputed from x bit-exactly) turns it into dx.
+    Returns (y, y's BN statistics sums) like ``conv2d_nhwc(..., with_stats=True)``."""
+
+    @staticmethod
+    def forward(ctx, x, sums, anchor, pg, pb, run_mean, run_var, momentum, eps, pw, stride, padding):
+        C_ = _C()
+        x = x.contiguous()
+        M = x.numel() // x.shape[-1]
+        mean, invstd, params = C_.bn_finalize(sums, pg.master, pb.master, run_mean, run_var, M, momentum, eps)
+        w = pw.weight
+        ysums = _zero_scratch(pw.store, x.device, C_.conv_stat_replicas * 2 * w.shape[0]).view(
+            C_.conv_stat_replicas, 2, w.shape[0])
+        y = C_.conv_fwd(x, w, stride, padding, 1, False, None, 0, ysums, xform=params)
+        _conv_impl().STATS["hip_fwd"] += 1
+        ctx.save_for_backward(x, mean, invstd, params)
+        ctx.pg, ctx.pb, ctx.pw, ctx.stride, ctx.padding = pg, pb, pw, stride, padding
+        ctx.x_requires_grad = x.requires_grad
+        ctx.mark_non_differentiable(ysums)
+        ctx.set_materialize_grads(False)
+        return y, ysums
+
+    @staticmethod
+    def backward(ctx, gy, _gsums=None):
+        x, mean, invstd, params = ctx.saved_tensors
+        pg, pb, pw = ctx.pg, ctx.pb, ctx.pw
+        impl = _conv_impl()
+        gy = gy.contiguous()
+        dz = impl.conv_bwd(gy, x, pw.weight, ctx.stride, ctx.padding, True, pw, xform=params)
+        dg, db, finish = _bn_param_grads(pg.store, pg, pb, x.device)
+        dx, _ = _C().bn_bwd(dz, x, None, mean, invstd, pg.master, pb.master, True, dg, db, False)
+        finish()
+        return (dx if ctx.x_requires_grad else None,) + (None,) * 11
+
+
+def bn_relu_conv(t, bn, conv):
+    """``conv(bn(t))`` for ``t = (x, sums)`` from ``conv2d_nhwc(..., with_stats=True)``, a training-mode ReLU
+    BatchNorm ``bn`` (models/resnet.BN) and a convolution ``conv`` (models/resnet.Conv): normalised on load
+    (``_BnReluConv``) where the kernels take it, else the separate BN apply + conv. Returns (y, y's sums)."""
+    x, sums = t if isinstance(t, tuple) else (t, None)
+    w = conv.w
+    if (sums is not None and bn.training and _gpu(x) and x.dtype == torch.bfloat16 and x.shape[-1] % 64 == 0
+            and w.weight.dtype == torch.bfloat16 and w.shape[0] % 8 == 0 and w.grad.dtype == torch.float32):
+        return _BnReluConv.apply(x, sums, w.store.anchor, bn.gamma, bn.beta, bn.running_mean, bn.running_var,
+                                 bn.momentum, bn.eps, w, conv.stride, conv.pad)
+    return conv(bn(t))
+
+
 def batch_norm_act(x, pg, pb, run_mean, run_var, residual=None, relu=True, training=True, momentum=0.1,
                    eps=1e-5, sums=None, res_link=None, bwd_link=None, dy_link=None):
     """y = act(BN(x) + residual) over the last (channel) dim of an NHWC tensor.

@@ -16,27 +16,41 @@ from k8s_amd.parallel.flat import ParamStore  # noqa: E402
 
 
 def main():
+    mode = sys.argv[1] if len(sys.argv) > 1 else "allreduce-fp32"
     info = kdist.init_process_group()
     gpu = torch.cuda.is_available()
     dev = torch.device("cuda", info.device_index) if gpu else torch.device("cpu")  # CPU: a dry run of this script
     store = ParamStore()
-    model = resnet_tiny(store).finalize(dev)
+    model = resnet_tiny(store).finalize(dev, pad_to=64 * info.world_size)
     torch.distributed.broadcast(store.master, 0)
     store.refresh_lowp()
-    red = GradReducer(store, bucket_mb=0.01)  # many buckets: every hook / overlap path runs
     opt = FusedSGD(store, lr=0.05, momentum=0.9, weight_decay=1e-4)
+    if mode.startswith("zero"):  # ZeRO-1 sharded service (reduce-scatter / all-to-all push, owner update, pull)
+        from k8s_amd.parallel.ps import ShardedParameterService
+
+        svc = ShardedParameterService(store, opt, bucket_mb=0.01,
+                                      comm_dtype=torch.bfloat16 if mode.endswith("bf16") else torch.float32)
+        begin, finish = svc.begin_step, svc.step
+    else:  # many buckets: every hook / overlap path runs
+        red = GradReducer(store, bucket_mb=0.01,
+                          comm_dtype=torch.bfloat16 if mode.endswith("bf16") else torch.float32)
+        begin = red.begin_step
+
+        def finish():
+            red.finish()
+            opt.step(grad_scale=red.grad_scale)
     g = torch.Generator(device="cpu").manual_seed(100 + info.rank)  # different data per rank
     for _ in range(3):
         x = torch.randn(8, 32, 32, 3, generator=g).to(dev, torch.bfloat16 if gpu else torch.float32)
         y = torch.randint(0, 10, (8,), generator=g).to(dev)
-        red.begin_step()
+        begin()
         loss = K.cross_entropy(model(model.prepare_input(x).contiguous()), y)
         loss.backward()
-        red.finish()
-        opt.step(grad_scale=red.grad_scale)
+        finish()
     if gpu:
         torch.cuda.synchronize()
-    state = torch.cat([store.master, opt.mom if hasattr(opt, "mom") else store.master]).cpu()
+    # the sharded optimizer keeps different (owned) state slices per rank: compare the weights only
+    state = (store.master if mode.startswith("zero") else torch.cat([store.master, opt.mom])).cpu()
     ref = state.clone()
     torch.distributed.broadcast(ref, 0)
     same = torch.tensor([int(torch.equal(state, ref))])

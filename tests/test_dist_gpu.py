@@ -29,8 +29,11 @@ def _torchrun(script, args, nproc=2, timeout=240):
     return [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
 
 
-def test_dp_replicas_stay_identical_on_gpu():
-    (rec,) = _torchrun("tests/dist_gpu_worker.py", [])
+@pytest.mark.parametrize("mode", ["allreduce-fp32", "allreduce-bf16", "zero-bf16"])
+def test_dp_replicas_stay_identical_on_gpu(mode):
+    """All-reduce (fp32, and bf16 transport with its side-stream sum / all-gather / expansion) and the ZeRO-1
+    service with the bf16 all-to-all push: after 3 steps every rank holds the same weights."""
+    (rec,) = _torchrun("tests/dist_gpu_worker.py", [mode])
     assert rec["world"] == 2 and rec["replicas_identical"] == 1
     assert rec["loss"] == rec["loss"]
 

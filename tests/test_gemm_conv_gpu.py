@@ -387,3 +387,127 @@ def test_act_bwd_colsum(cuda, act, R, C):
     out = torch.empty(C, device=cuda)
     g2, db2 = _C().act_bwd_colsum(dy, y, act, out)
     assert db2.data_ptr() == out.data_ptr() and torch.equal(db2, db)
+
+
+# ----------------------------------------------------------------------------- normalize on load (gemm.hip XForm)
+def _bn_params(C, device, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    scale = (torch.rand(C, generator=g) * 1.5 + 0.25) * torch.where(torch.rand(C, generator=g) < 0.2, -1.0, 1.0)
+    shift = torch.randn(C, generator=g) * 0.5
+    return torch.cat([scale, shift]).float().to(device).contiguous()
+
+
+def _bn_relu_ref(x, params):
+    """z as batchnorm.hip's apply writes it, bf16(relu(fma(x, scale, shift))): the fma through float64 (the product
+    of two floats is exact there; the sum's double rounding can differ from a true fma in rare last bits)"""
+    C = x.shape[-1]
+    z = (x.double() * params[:C].double() + params[C:].double()).float().clamp_min(0.0)
+    return z.bfloat16()
+
+
+XF_CASES = [
+    # N, H, W, C, K, R, stride, pad
+    (4, 14, 14, 64, 64, 3, 1, 1),       # 3x3, padded taps stay zero
+    (2, 28, 28, 128, 128, 3, 2, 1),     # strided 3x3 (ResNet stage-entry conv2)
+    (8, 14, 14, 64, 256, 1, 1, 0),      # 1x1, K = 64: the single-buffer kernel (ResNet conv3 at stage 1)
+    (3, 7, 7, 512, 2048, 1, 1, 0),      # 1x1, long K: the double-buffered kernel
+    (2, 9, 11, 64, 72, 3, 1, 1),        # ragged M / N tails
+    (16, 8, 8, 128, 64, 1, 1, 0),       # N = 64: the 256 x 64 tile
+]
+
+
+@pytest.mark.parametrize("case", XF_CASES)
+def test_conv_fwd_normalize_on_load(cuda, case):
+    """conv(relu(bn(x))) with the BN applied in the A-operand load equals conv of the materialised z (what the BN
+    apply pass would have written), statistics epilogue included."""
+    N, H, W, C, K, R, st, pad = case
+    torch.manual_seed(5)
+    x = (torch.randn(N, H, W, C, device=cuda) * 2 + 0.3).bfloat16()
+    w = (torch.randn(K, R, R, C, device=cuda) * 0.05).bfloat16()
+    p = _bn_params(C, cuda, 1)
+    reps = _C().conv_stat_replicas
+    s1 = torch.zeros(reps, 2, K, device=cuda)
+    y = _C().conv_fwd(x, w, st, pad, 1, False, None, 0, s1, xform=p)
+    z = _bn_relu_ref(x, p)
+    s2 = torch.zeros(reps, 2, K, device=cuda)
+    y2 = _C().conv_fwd(z, w, st, pad, 1, False, None, 0, s2)
+    # same kernel arithmetic on (almost always) the same operand bits: a rare 1-ulp z difference (see _bn_relu_ref)
+    # moves a few outputs by ~1 bf16 ulp at most
+    d = (y.float() - y2.float()).abs()
+    assert (d > 0).float().mean().item() < 1e-3 and d.max().item() <= 0.02 * y2.float().abs().max().item(), d.max()
+    ref = F.conv2d(z.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, st, pad).permute(0, 2, 3, 1)
+    assert _rel(y, ref) < 1e-2
+    torch.testing.assert_close(s1.sum(0), s2.sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("case", XF_CASES + [(2, 56, 56, 64, 64, 3, 1, 1)])
+def test_conv_wgrad_normalize_on_load(cuda, case):
+    """dW with the activation operand normalised on load (implicit-GEMM B, or the plain 1x1 GEMM with split-K
+    slabs) vs an fp32 reference on the materialised z."""
+    N, H, W, C, K, R, st, pad = case
+    torch.manual_seed(6)
+    x = (torch.randn(N, H, W, C, device=cuda) * 2 + 0.3).bfloat16()
+    Ho = (H + 2 * pad - R) // st + 1
+    Wo = (W + 2 * pad - R) // st + 1
+    dy = torch.randn(N, Ho, Wo, K, device=cuda).bfloat16()
+    p = _bn_params(C, cuda, 2)
+    z = _bn_relu_ref(x, p)
+    zr = z.float().permute(0, 3, 1, 2)
+    wr = torch.zeros(K, C, R, R, device=cuda, requires_grad=True)
+    F.conv2d(zr, wr, None, st, pad).backward(dy.float().permute(0, 3, 1, 2))
+    ref = wr.grad.permute(0, 2, 3, 1)
+    dw = torch.empty(K, R, R, C, device=cuda)
+    _C().conv_wgrad(x, dy, dw, st, pad, 1, 0, False, xform=p)
+    assert _rel(dw, ref) < 5e-3
+    if R == 1 and st == 1:
+        dw2 = torch.full((K, C), 7.0, device=cuda)
+        _C().gemm(dy.reshape(-1, K), False, x.reshape(-1, C), False, dw2, True, None, 0, None, False, 1.0, 0,
+                  xform_b=p, xform_c=C)
+        assert _rel(dw2, ref.reshape(K, C)) < 5e-3
+        base = torch.randn(K, C, device=cuda)
+        dw3 = base.clone()
+        _C().gemm(dy.reshape(-1, K), False, x.reshape(-1, C), False, dw3, True, None, 0, None, True, 1.0, 1,
+                  xform_b=p, xform_c=C)
+        assert _rel(dw3 - base, ref.reshape(K, C)) < 5e-3
+
+
+def test_bn_relu_conv_matches_separate_ops(cuda):
+    """ops.nn.bn_relu_conv (BN applied in the conv's loads) vs batch_norm_act + conv2d_nhwc on the same inputs:
+    outputs, statistics, input gradient, conv weight / BN parameter gradients and running statistics."""
+    from k8s_amd.models.resnet import BN, Conv
+    from k8s_amd.ops import nn as K
+    from k8s_amd.parallel.flat import ParamStore
+
+    def build():
+        store = ParamStore()
+        pre = Conv(store, "pre", 64, 128, 1)
+        bn = BN(store, "bn", 128)
+        conv = Conv(store, "conv", 128, 128, 3, 2)
+        store.finalize(cuda, seed=11)
+        gen = torch.Generator(device=cuda).manual_seed(12)  # the same BN affine in both builds
+        with torch.no_grad():
+            bn.gamma.master.uniform_(0.5, 1.5, generator=gen)
+            bn.beta.master.normal_(0.0, 0.3, generator=gen)
+        return store, pre, bn.to(cuda), conv
+
+    torch.manual_seed(7)
+    x0 = torch.randn(4, 16, 16, 64, device=cuda).bfloat16().requires_grad_(True)
+    g = torch.randn(4, 8, 8, 128, device=cuda).bfloat16()
+    outs = []
+    for fused in (True, False):
+        store, pre, bn, conv = build()
+        store.begin_step()
+        x = x0.detach().clone().requires_grad_(True)
+        t = pre(x)
+        y, s = K.bn_relu_conv(t, bn, conv) if fused else conv(bn(t))
+        y.backward(g)
+        store.zero_unwritten()
+        outs.append((y.detach(), s.detach().sum(0), x.grad, store.grad.clone(), bn.running_mean.clone(),
+                     bn.running_var.clone()))
+    (y1, s1, dx1, g1, rm1, rv1), (y2, s2, dx2, g2, rm2, rv2) = outs
+    assert torch.equal(y1, y2)
+    torch.testing.assert_close(s1, s2, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(rm1, rm2)
+    torch.testing.assert_close(rv1, rv2)
+    assert _rel(dx1, dx2) < 1e-2
+    assert _rel(g1, g2) < 1e-2

@@ -274,3 +274,22 @@ def test_global_avg_pool_nhwc(cuda):
     g = torch.randn_like(y)
     (dx,) = torch.autograd.grad(y, x, g)
     assert ((dx.float() - (g.float() / 49)[:, None, None, :]).abs().max()).item() < 1e-3
+
+
+@pytest.mark.parametrize("world,n", [(2, 64 * 1000), (8, 64 * 4097), (8, 999), (3, 8 * 77)])
+def test_slice_sum_and_cast_bf16(cuda, world, n):
+    """bf16 gradient transport kernels (parallel/ddp.py, ps.py): the fp32->bf16 pack matches torch's rounding and
+    the owner's sum of the world received chunks is the fp32 rank-order sum (bitwise), both outputs."""
+    torch.manual_seed(world)
+    g = torch.randn(world * n, device=cuda) * 3
+    send = _C().cast_bf16(g)
+    assert torch.equal(send, g.to(torch.bfloat16))
+    out = torch.empty(n, device=cuda)
+    out_bf = torch.empty(n, device=cuda, dtype=torch.bfloat16)
+    _C().slice_sum(send, world, out, out_bf)
+    chunks = send.view(world, n).float()
+    want = torch.zeros(n, device=cuda)
+    for r in range(world):
+        want = want + chunks[r]
+    assert torch.equal(out, want)
+    assert torch.equal(out_bf, want.to(torch.bfloat16))
