@@ -130,9 +130,16 @@ def build_kernels(force=False, jobs=None) -> str:
     n = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=n) as ex:
         logs = [(j, fut.result()) for j, fut in [(j, ex.submit(_run, j)) for j in jobs_list]]
-    _check_resources(logs)
+    try:
+        _check_resources(logs)
+    except RuntimeError:
+        for j in jobs_list:  # a spilling object must not survive to be linked by the next (incremental) build
+            o = j[j.index("-o") + 1]
+            if os.path.exists(o):
+                os.remove(o)
+        raise
     out = os.path.join(ROOT, "_C" + _ext_suffix())
-    if force or jobs_list or not os.path.exists(out):
+    if force or jobs_list or not os.path.exists(out) or _newer(out, objs):
         libs = ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64"]
         tmp = out + ".tmp"
         _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", *objs, "-o", tmp, "-L", tlib, *libs,

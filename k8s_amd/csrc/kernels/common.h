@@ -14,6 +14,7 @@ constexpr int kWave = 64;
 typedef __attribute__((ext_vector_type(8))) short bf16x8_t;   // 8 bf16 = 16 B
 typedef __attribute__((ext_vector_type(4))) short bf16x4_t;   // 4 bf16 = 8 B
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 typedef uint16_t bf16_raw;
 
@@ -22,6 +23,7 @@ __device__ __forceinline__ float bf2f(uint16_t v) {
 }
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16v8_t;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16v4_t;
 typedef __attribute__((ext_vector_type(8))) float f32x8_t;
 
 // fp32 -> bf16, round-to-nearest-even, NaN kept as a quiet NaN: gfx950's v_cvt_pk_bf16_f32 (one instruction per

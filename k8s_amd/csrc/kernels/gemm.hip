@@ -626,16 +626,25 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
 #pragma unroll
       for (int r = 0; r < 4; ++r) bj[j][r] = (XEPI && E.bias && n + r < N) ? E.bias[n + r] : 0.f;
     }
+    // alpha is 1 for every convolution and data gradient: the scaling pass runs only when it is not (one
+    // wave-uniform branch instead of 64 multiplies per lane on every tile)
+    if (XEPI || E.alpha != 1.f) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            acc[i][j][r] = XEPI ? __builtin_fmaf(acc[i][j][r], E.alpha, bj[j][r]) : acc[i][j][r] * E.alpha;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = wm * 64 + i * 16 + (lane & 15);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col = wn * 64 + j * 16 + (lane >> 4) * 4;
-        bf16x4_t o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          o[r] = (short)f2bf(XEPI ? __builtin_fmaf(acc[i][j][r], E.alpha, bj[j][r]) : acc[i][j][r] * E.alpha);
+        // 4 fp32 -> 4 bf16: two v_cvt_pk_bf16_f32, no per-element packing
+        const bf16x4_t o = __builtin_bit_cast(bf16x4_t, __builtin_convertvector(acc[i][j], bf16v4_t));
         *reinterpret_cast<bf16x4_t*>(ctile + row * BN + (((col >> 3) ^ (row % CPR)) << 3) + (col & 4)) = o;
       }
     }
@@ -662,6 +671,47 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
       }
     }
     constexpr int CHUNKS = BM * CPR;
+    // fast path (convolution forward with statistics, plain data gradients): identity rows, store mode, no BN
+    // backward. A thread's chunk column is fixed and its rows advance by GEMM_THREADS / CPR per trip, so the
+    // output pointer is one 64-bit add per trip; the statistics use packed fp32 adds / FMAs on the unpacked pairs.
+    if (!BNB && !XEPI && !E.rst && emode == 0 && !bwd) {
+      constexpr int RSTEP = GEMM_THREADS / CPR;
+      const int c = tid % CPR, row0 = tid / CPR;
+      const int n = n0 + c * 8;
+      if (n < N) {
+        const long ldc = E.ldc;
+        uint16_t* cp = reinterpret_cast<uint16_t*>(ec) + (long)(m0 + row0) * ldc + n;
+        const uint16_t* lp = ctile + row0 * BN;
+        f32x2_t s2[4], q2[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s2[r] = q2[r] = f32x2_t{0.f, 0.f};
+#pragma unroll 4
+        for (int row = row0; row < BM; row += RSTEP) {
+          if (m0 + row < M) {
+            const bf16x8_t o = *reinterpret_cast<const bf16x8_t*>(lp + ((c ^ (row % CPR)) << 3));
+            *reinterpret_cast<bf16x8_t*>(cp) = o;
+            if (stat_out) {
+              const uint32_t* w = reinterpret_cast<const uint32_t*>(&o);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {  // pair r = elements (2r, 2r+1): bf16 -> fp32 is a shift / a mask
+                const f32x2_t v = {__uint_as_float(w[r] << 16), __uint_as_float(w[r] & 0xFFFF0000u)};
+                s2[r] += v;
+                q2[r] = __builtin_elementwise_fma(v, v, q2[r]);
+              }
+            }
+          }
+          cp += (long)RSTEP * ldc;
+          lp += RSTEP * BN;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ps[2 * r] = s2[r][0];
+          ps[2 * r + 1] = s2[r][1];
+          pq[2 * r] = q2[r][0];
+          pq[2 * r + 1] = q2[r][1];
+        }
+      }
+    } else
 #pragma unroll 2
     for (int q = tid; q < CHUNKS; q += GEMM_THREADS) {
       const int row = q / CPR, c = q % CPR;
@@ -961,7 +1011,7 @@ static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int 
   // normalize-on-load instantiations: the convolution forward (A = the BN input, lean epilogue with statistics) and
   // the weight gradients (B = the BN input, fp32 output or split-K slab through the F32S epilogue)
   if (xf) {
-    if constexpr (std::is_same_v<ASrc, ConvA> && std::is_same_v<BSrc, KMajor>) {
+    if constexpr ((std::is_same_v<ASrc, ConvA> || std::is_same_v<ASrc, KMajor>) && std::is_same_v<BSrc, KMajor>) {
       if (lean_epi(e, N, false) && !e.bstats && !e.rst && !e.addsrc) {
         launch_tiles2<ASrc, BSrc, WM, WN, true, false, false, false, 1>(a, b, e, M, N, K, kps, splits, st, *xf);
         return;
@@ -1175,7 +1225,17 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, 
     e.rb = sg->b;
   }
   if (xform && C % 64 != 0) throw std::runtime_error("normalize-on-load convolution needs C % 64 == 0");
-  if (C % 64 == 0) {
+  if (R == 1 && S == 1 && stride == 1 && pad == 0 && !sg && C % 64 == 0) {
+    // a plain 1x1 convolution is the GEMM y[M][K] = x[M][C] . w[K][C]^T: the K-major source needs no im2col
+    // decode (ConvA's per-row (n, ho, wo) cursors were ~1/4 of the VALU of these memory-bound kernels)
+    KMajor a{x, (long)C, M};
+    if (xform) {
+      const XForm xf{xform, C, make_fastdiv(C)};
+      launch(a, b, e, M, K, RSC, 1, st, &xf);
+    } else {
+      launch(a, b, e, M, K, RSC, 1, st);
+    }
+  } else if (C % 64 == 0) {
     ConvA a{x, N, H, W, C, Ho, Wo, S, stride, pad, dil, M,
             make_fastdiv(C), make_fastdiv(S), make_fastdiv(Ho * Wo), make_fastdiv(Wo)};
     if (xform) {

@@ -101,20 +101,29 @@ void Controller::handle_event(const std::string& type, const Json& obj) {
   if (job.status.state == "Failed" && !jobs_.count(key)) return;
   auto it = jobs_.find(key);
   if (it != jobs_.end() && !it->second->finished()) {
-    if (type == "MODIFIED") it->second->update(job);
-    return;
+    if (job_uids_[key] == job.uid() || job.uid().empty()) {
+      if (type == "MODIFIED") it->second->update(job);
+      return;
+    }
+    // same name, new object (deleted and re-created while no watch event reached us): retire the old worker
+    log_info("TfJob %s was re-created (uid %s -> %s)", key.c_str(), job_uids_[key].c_str(), job.uid().c_str());
+    it->second->request_delete();
   }
   if (type == "ADDED" || type == "MODIFIED") {
     log_info("Starting TfJob %s (phase=%s)", key.c_str(), job.status.phase.c_str());
     auto tj = std::make_unique<TrainingJob>(api_, job, cfg_, opts_.reconcile);
     jobs_[key] = std::make_unique<JobWorker>(std::move(tj), opts_.reconcile.interval);
+    job_uids_[key] = job.uid();
   }
 }
 
 void Controller::reap_finished() {
   std::lock_guard<std::mutex> g(mu_);
   for (auto it = jobs_.begin(); it != jobs_.end();) {
-    if (it->second->finished() && !job_rvs_.count(it->first)) it = jobs_.erase(it);
+    if (it->second->finished() && !job_rvs_.count(it->first)) {
+      job_uids_.erase(it->first);
+      it = jobs_.erase(it);
+    }
     else ++it;
   }
 }

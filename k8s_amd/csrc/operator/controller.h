@@ -80,6 +80,7 @@ class Controller {
   std::mutex mu_;
   std::map<std::string, std::unique_ptr<JobWorker>> jobs_;  // ns/name -> worker
   std::map<std::string, std::string> job_rvs_;               // ns/name -> resourceVersion
+  std::map<std::string, std::string> job_uids_;              // ns/name -> uid of the object its worker runs
 };
 
 }  // namespace tfop

@@ -1,3 +1,4 @@
+#include <vector>
 #include "election.h"
 
 #include <ctime>
@@ -101,60 +102,77 @@ static void store_record(Json& obj, const LeaderElectionRecord& rec, bool lease)
 }
 
 bool LeaderElector::try_acquire_or_renew(int timeout_ms) {
-  const bool lease = cfg_.lock_type != "endpoints";
-  const std::string coll = lease ? group_path("coordination.k8s.io/v1", cfg_.ns, "leases")
-                                 : core_path(cfg_.ns, "endpoints");
-  const std::string path = coll + "/" + cfg_.name;
-  const std::string now = lease ? now_micro() : now_rfc3339();
+  // lock objects this elector holds: the Lease, the Endpoints annotation, or both (client-go's
+  // "endpointsleases" MultiLock: an operator that takes BOTH is mutually exclusive with an older operator that
+  // only knows either one, so a rolling upgrade from an Endpoints-lock or a Lease-lock release cannot produce two
+  // leaders)
+  std::vector<bool> kinds;
+  if (cfg_.lock_type == "endpoints") kinds = {false};
+  else if (cfg_.lock_type == "leases") kinds = {true};
+  else kinds = {false, true};
   RequestTimeout bound(timeout_ms);  // every API call below gives up by the caller's deadline
-  LeaderElectionRecord rec;
-  rec.holder_identity = cfg_.identity;
-  rec.lease_duration_seconds = (int)(cfg_.lease.count() / 1000);
-  if (rec.lease_duration_seconds < 1) rec.lease_duration_seconds = 1;
-  rec.acquire_time = now;
-  rec.renew_time = now;
-  ApiResult g = api_.get(path);
-  if (g.not_found()) {
-    Json obj = Json::object();
-    obj["apiVersion"] = lease ? "coordination.k8s.io/v1" : "v1";
-    obj["kind"] = lease ? "Lease" : "Endpoints";
-    Json md = Json::object();
-    md["name"] = cfg_.name;
-    md["namespace"] = cfg_.ns;
-    if (!lease) md["annotations"] = Json::object();
-    obj["metadata"] = md;
-    store_record(obj, rec, lease);
-    ApiResult c = api_.post(coll, obj);
-    if (!c.ok()) return leader_ = false;
-    observed_ = rec;
-    observed_time_ = std::chrono::steady_clock::now();
-    return leader_ = true;
+  struct Held {
+    bool lease;
+    std::string coll, path;
+    ApiResult got;
+    LeaderElectionRecord old;
+  };
+  std::vector<Held> locks;
+  const auto now_steady = std::chrono::steady_clock::now();
+  for (bool lease : kinds) {
+    Held h;
+    h.lease = lease;
+    h.coll = lease ? group_path("coordination.k8s.io/v1", cfg_.ns, "leases") : core_path(cfg_.ns, "endpoints");
+    h.path = h.coll + "/" + cfg_.name;
+    h.got = api_.get(h.path);
+    if (!h.got.ok() && !h.got.not_found()) return leader_ = false;
+    if (h.got.ok()) h.old = record_of(h.got.body, lease);
+    LeaderElectionRecord& seen = lease ? observed_lease_ : observed_;
+    auto& seen_time = lease ? observed_lease_time_ : observed_time_;
+    if (h.old.to_json() != seen.to_json()) {
+      seen = h.old;
+      seen_time = now_steady;
+    }
+    // the lease is judged by OUR clock since we last saw the record change (election.go:232-236), never by
+    // the holder's timestamps: no clock-skew assumptions between replicas
+    const bool held_by_other = !h.old.holder_identity.empty() && h.old.holder_identity != cfg_.identity;
+    if (held_by_other && seen_time + std::chrono::seconds(h.old.lease_duration_seconds) > now_steady)
+      return leader_ = false;
+    locks.push_back(std::move(h));
   }
-  if (!g.ok()) return leader_ = false;
-  Json obj = g.body;
-  LeaderElectionRecord old = record_of(obj, lease);
-  if (old.to_json() != observed_.to_json()) {
-    observed_ = old;
-    observed_time_ = std::chrono::steady_clock::now();
+  for (auto& h : locks) {
+    const std::string now = h.lease ? now_micro() : now_rfc3339();
+    LeaderElectionRecord rec;
+    rec.holder_identity = cfg_.identity;
+    rec.lease_duration_seconds = std::max(1, (int)(cfg_.lease.count() / 1000));
+    rec.acquire_time = now;
+    rec.renew_time = now;
+    if (h.got.not_found()) {
+      Json obj = Json::object();
+      obj["apiVersion"] = h.lease ? "coordination.k8s.io/v1" : "v1";
+      obj["kind"] = h.lease ? "Lease" : "Endpoints";
+      Json md = Json::object();
+      md["name"] = cfg_.name;
+      md["namespace"] = cfg_.ns;
+      if (!h.lease) md["annotations"] = Json::object();
+      obj["metadata"] = md;
+      store_record(obj, rec, h.lease);
+      if (!api_.post(h.coll, obj).ok()) return leader_ = false;
+    } else {
+      if (h.old.holder_identity == cfg_.identity) {
+        rec.acquire_time = h.old.acquire_time;
+        rec.leader_transitions = h.old.leader_transitions;
+      } else {
+        rec.leader_transitions = h.old.leader_transitions + 1;
+      }
+      Json obj = h.got.body;
+      if (!h.lease && !obj["metadata"].find("annotations")) obj["metadata"]["annotations"] = Json::object();
+      store_record(obj, rec, h.lease);
+      if (!api_.put(h.path, obj).ok()) return leader_ = false;  // carries resourceVersion: optimistic CAS
+    }
+    (h.lease ? observed_lease_ : observed_) = rec;
+    (h.lease ? observed_lease_time_ : observed_time_) = std::chrono::steady_clock::now();
   }
-  // the lease is judged by OUR clock since we last saw the record change (election.go:232-236), never by
-  // the holder's timestamps: no clock-skew assumptions between replicas
-  const bool held_by_other = !old.holder_identity.empty() && old.holder_identity != cfg_.identity;
-  if (held_by_other &&
-      observed_time_ + std::chrono::seconds(old.lease_duration_seconds) > std::chrono::steady_clock::now())
-    return leader_ = false;
-  if (old.holder_identity == cfg_.identity) {
-    rec.acquire_time = old.acquire_time;
-    rec.leader_transitions = old.leader_transitions;
-  } else {
-    rec.leader_transitions = old.leader_transitions + 1;
-  }
-  if (!lease && !obj["metadata"].find("annotations")) obj["metadata"]["annotations"] = Json::object();
-  store_record(obj, rec, lease);
-  ApiResult u = api_.put(path, obj);  // carries metadata.resourceVersion: optimistic CAS
-  if (!u.ok()) return leader_ = false;
-  observed_ = rec;
-  observed_time_ = std::chrono::steady_clock::now();
   return leader_ = true;
 }
 
@@ -172,10 +190,10 @@ void LeaderElector::record_event(const std::string& what) {
   md["namespace"] = cfg_.ns;
   ev["metadata"] = md;
   Json io = Json::object();
-  io["kind"] = cfg_.lock_type == "endpoints" ? "Endpoints" : "Lease";
+  io["kind"] = cfg_.lock_type == "leases" ? "Lease" : "Endpoints";
   io["namespace"] = cfg_.ns;
   io["name"] = cfg_.name;
-  io["apiVersion"] = cfg_.lock_type == "endpoints" ? "v1" : "coordination.k8s.io/v1";
+  io["apiVersion"] = cfg_.lock_type == "leases" ? "coordination.k8s.io/v1" : "v1";
   ev["involvedObject"] = io;
   ev["reason"] = "LeaderElection";
   ev["message"] = cfg_.identity + " " + what;

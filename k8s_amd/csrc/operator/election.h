@@ -5,11 +5,14 @@
 // :73-86, renew Poll until RenewDeadline :192-208) and resourcelock/
 // endpointslock.go + interface.go (record stored as JSON in the Endpoints
 // annotation control-plane.alpha.kubernetes.io/leader; that record format is
-// unchanged so mixed deployments interoperate). Added: a coordination.k8s.io/v1
-// Lease lock (default), and renews whose API calls are bounded by the time
-// left before the renew deadline, so a hung API server cannot keep a leader
-// that can no longer renew (no split brain: the standby only acquires after a
-// full lease duration without renewals).
+// unchanged). Added: a coordination.k8s.io/v1 Lease lock, the default
+// "endpointsleases" multi-lock that takes and renews BOTH objects (client-go's
+// migration lock: mutually exclusive with an operator that only knows the
+// Endpoints lock -- the reference, round 1 -- or only the Lease, so a rolling
+// upgrade cannot run two leaders), and renews whose API calls are bounded by
+// the time left before the renew deadline, so a hung API server cannot keep a
+// leader that can no longer renew (no split brain: the standby only acquires
+// after a full lease duration without renewals).
 #pragma once
 
 #include <atomic>
@@ -35,9 +38,9 @@ struct LeaderElectionRecord {
 struct ElectionConfig {
   std::string ns, name, identity;
   std::chrono::milliseconds lease{15000}, renew_deadline{5000}, retry{3000};
-  // "leases" (coordination.k8s.io/v1 Lease, the default of modern client-go) or "endpoints" (the reference's
-  // Endpoints annotation lock, pkg/util/k8sutil/election/resourcelock/endpointslock.go)
-  std::string lock_type = "leases";
+  // "endpointsleases" (both locks, the default), "leases" (coordination.k8s.io/v1 Lease only) or "endpoints"
+  // (the reference's Endpoints annotation lock, pkg/util/k8sutil/election/resourcelock/endpointslock.go)
+  std::string lock_type = "endpointsleases";
 };
 
 class LeaderElector {
@@ -58,8 +61,10 @@ class LeaderElector {
  private:
   KubeApi& api_;
   ElectionConfig cfg_;
-  LeaderElectionRecord observed_;
+  LeaderElectionRecord observed_;  // the Endpoints record (or the only lock's)
   std::chrono::steady_clock::time_point observed_time_;
+  LeaderElectionRecord observed_lease_;  // the Lease record
+  std::chrono::steady_clock::time_point observed_lease_time_;
   bool leader_ = false;
 };
 

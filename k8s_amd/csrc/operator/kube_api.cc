@@ -728,7 +728,12 @@ class HttpKubeApi : public KubeApi {
       Reader r(*c, dl);
       Head h;
       if (!read_head(r, h, res.error)) {
-        if (pooled && !r.got_any() && !r.expired()) continue;  // closed by the server while idle
+        // a pooled connection the server closed while idle: the request was written but no byte came back, so
+        // the server may or may not have processed it. Replay only what is safe to run twice (Go's transport:
+        // idempotent methods); a POST (create, event) is reported and retried by its caller's own logic, which
+        // tolerates AlreadyExists.
+        const bool replayable = method == "GET" || method == "HEAD" || method == "PUT" || method == "DELETE";
+        if (pooled && replayable && !r.got_any() && !r.expired()) continue;
         return res;
       }
       std::string payload;

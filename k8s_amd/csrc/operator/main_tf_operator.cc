@@ -71,7 +71,7 @@ int main(int argc, char** argv) {
   fl.def("renew-deadline", "5s", "Leader-election renew deadline");
   fl.def("retry-period", "3s", "Leader-election retry period");
   fl.def("create-crd", "true", "Register the tfjobs.tensorflow.org CRD at startup", true);
-  fl.def("leader-elect-resource-lock", "leases", "Leader-election lock: leases (coordination.k8s.io/v1) or endpoints");
+  fl.def("leader-elect-resource-lock", "endpointsleases", "Leader-election lock: endpointsleases (both: safe across upgrades from either), leases (coordination.k8s.io/v1) or endpoints");
   fl.def("request-timeout", "30s", "Deadline of every API request (connect, TLS handshake, response)");
   fl.def("event-watchdog", "60s", "Abort when one TfJob event handler runs longer (reference panicTimer: 1m)");
   fl.def("inject-handler-stall", "0s", "DO NOT USE IN PRODUCTION - fault injection: stall every TfJob event handler this long");
@@ -168,8 +168,8 @@ int main(int argc, char** argv) {
   ec.renew_deadline = std::chrono::milliseconds(parse_duration_ms(fl.str("renew-deadline"), 5000));
   ec.retry = std::chrono::milliseconds(parse_duration_ms(fl.str("retry-period"), 3000));
   ec.lock_type = fl.str("leader-elect-resource-lock");
-  if (ec.lock_type != "leases" && ec.lock_type != "endpoints") {
-    log_error("-leader-elect-resource-lock must be leases or endpoints");
+  if (ec.lock_type != "leases" && ec.lock_type != "endpoints" && ec.lock_type != "endpointsleases") {
+    log_error("-leader-elect-resource-lock must be endpointsleases, leases or endpoints");
     return 1;
   }
   LeaderElector el(*api, ec);

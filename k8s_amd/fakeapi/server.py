@@ -72,7 +72,7 @@ class _Handler(BaseHTTPRequestHandler):
         q = {k: v[-1] for k, v in parse_qs(u.query).items()}
         body = self._body() if method in ("POST", "PUT", "PATCH", "DELETE") else None
         if method == "GET" and q.get("watch") in ("true", "1"):
-            return self._watch(q.get("resourceVersion") or None)
+            return self._watch(q.get("resourceVersion") or None, float(q.get("timeoutSeconds") or 0))
         if u.path in ("/healthz", "/readyz", "/livez"):
             data = b"ok"
             self.send_response(200)
@@ -89,13 +89,24 @@ class _Handler(BaseHTTPRequestHandler):
         self.wfile.write(b"%x\r\n%s\r\n" % (len(data), data))
         self.wfile.flush()
 
-    def _watch(self, rv):
+    def _watch(self, rv, timeout_s=0.0):
+        """Chunked watch stream; ends after ``timeout_s`` (``?timeoutSeconds=``) like the real API server. A watch
+        open when a black-hole fault is injected (``FakeApiServer.blackhole_watches``) goes silent for good -- no
+        events, no end of stream, the socket left open -- as a connection a NAT / load balancer dropped without
+        telling either side."""
+        started = time.time()
         self.send_response(200)
         self.send_header("Content-Type", "application/json")
         self.send_header("Transfer-Encoding", "chunked")
         self.end_headers()
         try:
             for typ, obj in self.store.watch_from(self.path, rv):
+                if started < self.server.blackhole_before:
+                    while not self.server.stopping:  # half-open: hold the socket, never write again
+                        time.sleep(0.2)
+                    return
+                if timeout_s and time.time() - started >= timeout_s:
+                    break
                 if typ is None:
                     continue  # heartbeat; a write failure below ends the stream
                 self._chunk((json.dumps({"type": typ, "object": obj}) + "\n").encode())
@@ -131,6 +142,8 @@ class FakeApiServer:
         self.httpd = ThreadingHTTPServer((host, port), handler)
         self.httpd.daemon_threads = True
         self.httpd.stalls = []  # fault injection rules (POST /debug/stall, or stall() below)
+        self.httpd.blackhole_before = 0.0  # watches opened before this time are black holes (blackhole_watches)
+        self.httpd.stopping = False
         self.port = self.httpd.server_address[1]
         self.url = "http://%s:%d" % (host, self.port)
         self.thread = threading.Thread(target=self.httpd.serve_forever, daemon=True)
@@ -144,7 +157,13 @@ class FakeApiServer:
         self.httpd.stalls.append({"until": time.time() + seconds, "path_prefix": path_prefix,
                                   "user_agent": user_agent})
 
+    def blackhole_watches(self):
+        """Every watch open right now silently stops: no more events and no end of stream (a half-open TCP
+        connection); watches opened afterwards work normally."""
+        self.httpd.blackhole_before = time.time()
+
     def stop(self):
+        self.httpd.stopping = True
         self.httpd.shutdown()
         self.httpd.server_close()
 

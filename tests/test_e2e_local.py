@@ -163,3 +163,33 @@ def test_leader_election_failover(lock):
             standby.kill()
             standby.wait()
             log1.close()
+
+
+def test_half_open_watch_is_replaced_and_later_jobs_still_run():
+    """a watch connection that silently stops (dropped by a NAT / load balancer: no events,
+    no end of stream) must not blind the operator. Every watch asks for timeoutSeconds (randomised in [t, 2t)); a
+    stream still open past that + a grace is closed and re-established from the last resourceVersion, so a TfJob
+    created after the stall still reaches Done (reference: controller.go:292-361 re-watches on EOF)."""
+    with LocalCluster(operator_args=["-watch-timeout", "2s", "-watch-idle-grace", "1s", "-resync-period", "0"]) as c:
+        c.create(os.path.join(REPO, "examples", "tf_job.yaml"))
+        _wait_state(c, "example-job", {"Succeeded"})
+        c.server.blackhole_watches()  # the operator's open watch goes silent for good
+        with open(os.path.join(REPO, "examples", "tf_job.yaml")) as f:
+            text = f.read().replace('name: "example-job"', 'name: "after-stall"')
+        assert "after-stall" in text
+        path = os.path.join(c.log_dir, "after_stall.yaml")
+        with open(path, "w") as f:
+            f.write(text)
+        c.create(path)
+        _wait_state(c, "after-stall", {"Succeeded"}, timeout=60)
+        assert "half-open connection" in c.operator_log()
+
+
+def test_periodic_resync_recovers_a_lost_event():
+    """With the watch black-holed and a long watch timeout, the periodic full relist (-resync-period) still picks
+    up a TfJob whose ADDED event never arrived."""
+    with LocalCluster(operator_args=["-watch-timeout", "10m", "-resync-period", "2s"]) as c:
+        time.sleep(1.0)  # the operator's first watch is open
+        c.server.blackhole_watches()
+        c.create(os.path.join(REPO, "examples", "tf_job.yaml"))
+        _wait_state(c, "example-job", {"Succeeded"}, timeout=60)
