@@ -674,13 +674,18 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
     // fast path (convolution forward with statistics, plain data gradients): identity rows, store mode, no BN
     // backward. A thread's chunk column is fixed and its rows advance by GEMM_THREADS / CPR per trip, so the
     // output pointer is one 64-bit add per trip; the statistics use packed fp32 adds / FMAs on the unpacked pairs.
-    if (!BNB && !XEPI && !E.rst && emode == 0 && !bwd) {
+    if (!BNB && !XEPI && !E.rst && !bwd) {
       constexpr int RSTEP = GEMM_THREADS / CPR;
       const int c = tid % CPR, row0 = tid / CPR;
       const int n = n0 + c * 8;
       if (n < N) {
         const long ldc = E.ldc;
-        uint16_t* cp = reinterpret_cast<uint16_t*>(ec) + (long)(m0 + row0) * ldc + n;
+        const long off0 = (long)(m0 + row0) * ldc + n;
+        uint16_t* cp = reinterpret_cast<uint16_t*>(ec) + off0;
+        // accumulate mode: the addend (C's old value, or addsrc masked by addmask -- a ResNet identity block's
+        // residual gradient) walks with the output
+        const uint16_t* ap = emode == 1 ? (E.addsrc ? E.addsrc + off0 : cp) : nullptr;
+        const uint8_t* mp = emode == 1 && E.addmask ? E.addmask + (off0 >> 3) : nullptr;
         const uint16_t* lp = ctile + row0 * BN;
         f32x2_t s2[4], q2[4];
 #pragma unroll
@@ -688,7 +693,16 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
 #pragma unroll 4
         for (int row = row0; row < BM; row += RSTEP) {
           if (m0 + row < M) {
-            const bf16x8_t o = *reinterpret_cast<const bf16x8_t*>(lp + ((c ^ (row % CPR)) << 3));
+            bf16x8_t o = *reinterpret_cast<const bf16x8_t*>(lp + ((c ^ (row % CPR)) << 3));
+            if (ap) {  // one extra bf16 rounding on top of the staged value (<= 1 ulp), as the general path
+              const bf16x8_t old = *reinterpret_cast<const bf16x8_t*>(ap);
+              const uint32_t bits = mp ? (uint32_t)*mp : 0xFFu;
+              float f[8];
+#pragma unroll
+              for (int r = 0; r < 8; ++r)
+                f[r] = bf2f((uint16_t)o[r]) + (((bits >> r) & 1u) ? bf2f((uint16_t)old[r]) : 0.f);
+              o = pack_bf16x8(f);
+            }
             *reinterpret_cast<bf16x8_t*>(cp) = o;
             if (stat_out) {
               const uint32_t* w = reinterpret_cast<const uint32_t*>(&o);
@@ -702,6 +716,8 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
           }
           cp += (long)RSTEP * ldc;
           lp += RSTEP * BN;
+          if (ap) ap += (long)RSTEP * ldc;
+          if (mp) mp += ((long)RSTEP * ldc) >> 3;
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {

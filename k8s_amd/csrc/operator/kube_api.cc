@@ -1,4 +1,7 @@
+#include <ctime>
+#include <signal.h>
 #include "kube_api.h"
+#include "log.h"
 
 #include <arpa/inet.h>
 #include <fcntl.h>
@@ -132,7 +135,14 @@ std::string base64_decode(const std::string& in) {
 }
 
 // ---- exec credential plugin (client.authentication.k8s.io ExecCredential): run the command, read
-// status.{token, clientCertificateData, clientKeyData} from its stdout
+// status.{token, clientCertificateData, clientKeyData, expirationTimestamp} from its stdout. A plugin that has not
+// finished within out.exec_timeout_ms is killed (a hung plugin must not block the operator forever).
+static long long parse_rfc3339(const std::string& t) {
+  struct tm tmv = {};
+  if (t.size() < 19 || !strptime(t.c_str(), "%Y-%m-%dT%H:%M:%S", &tmv)) return 0;
+  return (long long)timegm(&tmv);
+}
+
 static void run_exec_plugin(const Json& ex, ClusterConfig& out) {
   std::vector<std::string> argv{get_str(ex, "command")};
   if (argv[0].empty()) throw std::runtime_error("kubeconfig exec: no command");
@@ -162,11 +172,28 @@ static void run_exec_plugin(const Json& ex, ClusterConfig& out) {
   ::close(pfd[1]);
   std::string text;
   char buf[4096];
-  long n;
-  while ((n = ::read(pfd[0], buf, sizeof buf)) > 0) text.append(buf, (size_t)n);
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(out.exec_timeout_ms);
+  bool timed_out = false;
+  for (;;) {
+    const long left = (long)std::chrono::duration_cast<std::chrono::milliseconds>(
+                          deadline - std::chrono::steady_clock::now()).count();
+    if (left <= 0) {
+      timed_out = true;
+      break;
+    }
+    struct pollfd p{pfd[0], POLLIN, 0};
+    const int pr = poll(&p, 1, (int)std::min<long>(left, 1000));
+    if (pr < 0 && errno != EINTR) break;
+    if (pr <= 0) continue;
+    const long n = ::read(pfd[0], buf, sizeof buf);
+    if (n <= 0) break;
+    text.append(buf, (size_t)n);
+  }
   ::close(pfd[0]);
+  if (timed_out) kill(pid, SIGKILL);
   int status = 0;
   waitpid(pid, &status, 0);
+  if (timed_out) throw std::runtime_error("kubeconfig exec plugin " + argv[0] + " timed out");
   if (!WIFEXITED(status) || WEXITSTATUS(status) != 0)
     throw std::runtime_error("kubeconfig exec plugin " + argv[0] + " failed");
   Json cred = Json::parse(text);
@@ -175,6 +202,12 @@ static void run_exec_plugin(const Json& ex, ClusterConfig& out) {
   if (std::string t = get_str(*st, "token"); !t.empty()) out.token = t;
   if (std::string c = get_str(*st, "clientCertificateData"); !c.empty()) out.cert_data = c;
   if (std::string k = get_str(*st, "clientKeyData"); !k.empty()) out.key_data = k;
+  out.token_expiry = parse_rfc3339(get_str(*st, "expirationTimestamp"));
+}
+
+void refresh_exec_credential(ClusterConfig& cfg) {
+  if (cfg.exec_config.empty()) return;
+  run_exec_plugin(Json::parse(cfg.exec_config), cfg);
 }
 
 ClusterConfig cluster_config_from_kubeconfig(const std::string& text, const std::string& context) {
@@ -216,7 +249,12 @@ ClusterConfig cluster_config_from_kubeconfig(const std::string& text, const std:
           if (std::string d = get_str(*uu, "client-certificate-data"); !d.empty()) out.cert_data = base64_decode(d);
           out.key_file = get_str(*uu, "client-key");
           if (std::string d = get_str(*uu, "client-key-data"); !d.empty()) out.key_data = base64_decode(d);
-          if (const Json* ex = uu->find("exec"); ex && ex->is_object()) run_exec_plugin(*ex, out);
+          if (std::string tf = get_str(*uu, "tokenFile"); !tf.empty()) out.token_file = tf;
+          if (const Json* ex = uu->find("exec"); ex && ex->is_object()) {
+            out.exec_config = ex->dump();
+            if (const char* t = getenv("K8S_AMD_EXEC_TIMEOUT_MS"); t && atoi(t) > 0) out.exec_timeout_ms = atoi(t);
+            run_exec_plugin(*ex, out);
+          }
         }
         break;
       }
@@ -239,6 +277,7 @@ ClusterConfig cluster_config_from_env(const std::string& master_url) {
   try {
     c.token = read_file(sa + "token");
     while (!c.token.empty() && isspace((unsigned char)c.token.back())) c.token.pop_back();
+    c.token_file = sa + "token";  // bound service-account tokens are rotated by the kubelet: re-read
   } catch (...) {
   }
   c.ca_file = sa + "ca.crt";
@@ -708,16 +747,53 @@ class HttpKubeApi : public KubeApi {
 
   ApiResult request(const std::string& method, const std::string& path, const Json* body,
                     const std::string& ctype) override {
+    ApiResult res = request_once(method, path, body, ctype, false);
+    // 401 with a refreshable credential: refresh it once and replay (the server rejected the request, it did
+    // not run it)
+    if (res.code == 401 && (!cfg_.exec_config.empty() || !cfg_.token_file.empty()))
+      res = request_once(method, path, body, ctype, true);
+    return res;
+  }
+
+  // the bearer token to send: an exec-plugin token is re-fetched shortly before its expiry (or when forced by a
+  // 401), a token file re-read every minute (client-go's cached token source does the same)
+  std::string token(bool force) {
+    std::lock_guard<std::mutex> g(cred_mu_);
+    const long long now = (long long)time(nullptr);
+    if (!cfg_.exec_config.empty() && (force || (cfg_.token_expiry > 0 && now >= cfg_.token_expiry - 60))) {
+      try {
+        refresh_exec_credential(cfg_);
+        log_info("exec credential refreshed (expires %lld)", cfg_.token_expiry);
+      } catch (const std::exception& e) {
+        log_error("exec credential refresh failed: %s", e.what());
+      }
+    }
+    if (!cfg_.token_file.empty() && (force || now - token_read_ >= 60)) {
+      try {
+        std::string t = read_file(cfg_.token_file);
+        while (!t.empty() && isspace((unsigned char)t.back())) t.pop_back();
+        if (!t.empty()) cfg_.token = t;
+      } catch (...) {
+      }
+      token_read_ = now;
+    }
+    return cfg_.token;
+  }
+
+  ApiResult request_once(const std::string& method, const std::string& path, const Json* body,
+                         const std::string& ctype, bool force_refresh) {
     const int ovr = RequestTimeout::current();
     const Deadline dl = Deadline::in_ms(ovr >= 0 ? ovr : cfg_.timeout_ms);
     const std::string b = body ? body->dump() : "";
-    const std::string req = build_request(cfg_, method, path, b, ctype, true);
+    ClusterConfig rc = cfg_view();
+    rc.token = token(force_refresh);
+    const std::string req = build_request(rc, method, path, b, ctype, true);
     ApiResult res;
     for (int attempt = 0; attempt < 2; ++attempt) {
       bool pooled = false;
       std::unique_ptr<Conn> c = take(pooled);
       if (!c) {
-        c = std::make_unique<Conn>(cfg_);
+        c = std::make_unique<Conn>(cfg_view());
         if (!c->open(dl, res.error)) return res;
       }
       if (!c->write_all(req, dl)) {
@@ -777,9 +853,11 @@ class HttpKubeApi : public KubeApi {
 
   std::unique_ptr<WatchStream> watch(const std::string& path, std::string& err) override {
     const Deadline dl = Deadline::in_ms(cfg_.timeout_ms);
-    auto c = std::make_unique<Conn>(cfg_);
+    auto c = std::make_unique<Conn>(cfg_view());
     if (!c->open(dl, err)) return nullptr;
-    if (!c->write_all(build_request(cfg_, "GET", path, "", "", true), dl)) {
+    ClusterConfig wc = cfg_view();
+    wc.token = token(false);
+    if (!c->write_all(build_request(wc, "GET", path, "", "", true), dl)) {
       err = "write failed";
       return nullptr;
     }
@@ -814,7 +892,14 @@ class HttpKubeApi : public KubeApi {
     if (idle_.size() < kMaxIdle) idle_.push_back(std::move(c));
   }
 
+  ClusterConfig cfg_view() {
+    std::lock_guard<std::mutex> g(cred_mu_);
+    return cfg_;
+  }
+
   ClusterConfig cfg_;
+  std::mutex cred_mu_;        // cfg_'s credentials change on refresh
+  long long token_read_ = 0;  // last read of cfg_.token_file
   std::mutex mu_;
   std::vector<std::unique_ptr<Conn>> idle_;
 };

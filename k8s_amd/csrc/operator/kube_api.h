@@ -65,6 +65,13 @@ struct ClusterConfig {
   std::string cert_file, cert_data;  // client certificate (kubeconfig client-certificate[-data])
   std::string key_file, key_data;    // client key (kubeconfig client-key[-data])
   std::string tls_server_name;       // overrides the name checked against the server certificate
+  // credential refresh (client-go re-runs an exec plugin when its token expires or a request gets 401, and
+  // re-reads a rotated service-account / tokenFile token): the exec block as JSON, the token's expiry (unix
+  // seconds from status.expirationTimestamp, 0 = none), the token file
+  std::string exec_config;
+  long long token_expiry = 0;
+  std::string token_file;
+  int exec_timeout_ms = 30000;       // an exec plugin that has not answered by then is killed
   int connect_timeout_ms = 10000;    // TCP connect + TLS handshake
   int timeout_ms = 30000;            // whole request (client-go's default REST timeout is similar)
   std::string user_agent = "tf_operator-amd/0.3.0";
@@ -76,6 +83,8 @@ struct ClusterConfig {
 ClusterConfig cluster_config_from_env(const std::string& master_url = "");
 ClusterConfig parse_master_url(const std::string& url);
 ClusterConfig cluster_config_from_kubeconfig(const std::string& text, const std::string& context = "");
+// (Re)run the exec credential plugin of cfg.exec_config into cfg.token / cert / key / token_expiry.
+void refresh_exec_credential(ClusterConfig& cfg);
 
 // Per-thread request deadline override (milliseconds) for the HTTP client, e.g. a leader-election renew that
 // must give up by the renew deadline: RequestTimeout t(remaining_ms); api.put(...);

@@ -1,6 +1,8 @@
 // pybind11 module k8s_amd._operator: the C++ control-plane core exposed to
 // Python (tests, the tfjob CLI, the fake API server's defaulting path).
 // JSON crosses the boundary as strings.
+#include <chrono>
+#include <thread>
 #include <algorithm>
 
 #include <pybind11/functional.h>
@@ -150,6 +152,26 @@ PYBIND11_MODULE(_operator, m) {
     d["tls_server_name"] = c.tls_server_name;
     return d;
   }, py::arg("text"), py::arg("context") = "");
+  // n requests through a client configured from a kubeconfig (credentials: token / tokenFile / exec plugin with
+  // refresh), the server address overridden by `url`; returns the HTTP codes
+  m.def("kubeconfig_requests", [](const std::string& text, const std::string& url, const std::string& path, int n,
+                                  int interval_ms) {
+    ClusterConfig c = cluster_config_from_kubeconfig(text, "");
+    ClusterConfig u = parse_master_url(url);
+    c.host = u.host;
+    c.port = u.port;
+    c.tls = u.tls;
+    auto api = make_http_api(c);
+    std::vector<int> codes;
+    {
+      py::gil_scoped_release nogil;
+      for (int i = 0; i < n; ++i) {
+        if (i && interval_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(interval_ms));
+        codes.push_back(api->request("GET", path, nullptr, "application/json").code);
+      }
+    }
+    return codes;
+  }, py::arg("text"), py::arg("url"), py::arg("path") = "/version", py::arg("n") = 1, py::arg("interval_ms") = 0);
   m.def("http_request", [](const std::string& url, const std::string& method, const std::string& path,
                            const std::string& ca_data, const std::string& server_name, int timeout_ms, int repeat,
                            const std::string& cert_data, const std::string& key_data) {

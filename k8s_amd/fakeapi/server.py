@@ -69,6 +69,15 @@ class _Handler(BaseHTTPRequestHandler):
                                        "user_agent": b.get("user_agent", "")})
             return self._send(200, {"stalls": len(self.server.stalls)})
         self._stall()
+        accept = self.server.accept_token
+        if accept is not None:  # bearer-token check (credential refresh tests)
+            auth = self.headers.get("Authorization", "")
+            tok = auth[len("Bearer "):] if auth.startswith("Bearer ") else ""
+            if not accept(tok):
+                self.server.rejected.append(tok)
+                return self._send(401, {"kind": "Status", "apiVersion": "v1", "status": "Failure",
+                                        "reason": "Unauthorized", "code": 401})
+            self.server.accepted.append(tok)
         q = {k: v[-1] for k, v in parse_qs(u.query).items()}
         body = self._body() if method in ("POST", "PUT", "PATCH", "DELETE") else None
         if method == "GET" and q.get("watch") in ("true", "1"):
@@ -143,6 +152,8 @@ class FakeApiServer:
         self.httpd.daemon_threads = True
         self.httpd.stalls = []  # fault injection rules (POST /debug/stall, or stall() below)
         self.httpd.blackhole_before = 0.0  # watches opened before this time are black holes (blackhole_watches)
+        self.httpd.accept_token = None  # callable(token) -> bool: reject other bearer tokens with 401
+        self.httpd.accepted, self.httpd.rejected = [], []
         self.httpd.stopping = False
         self.port = self.httpd.server_address[1]
         self.url = "http://%s:%d" % (host, self.port)

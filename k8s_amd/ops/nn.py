@@ -351,9 +351,14 @@ class _BnReluConv(torch.autograd.Function):
         pg, pb, pw = ctx.pg, ctx.pb, ctx.pw
         impl = _conv_impl()
         gy = gy.contiguous()
-        dz = impl.conv_bwd(gy, x, pw.weight, ctx.stride, ctx.padding, True, pw, xform=params)
+        # the data gradient dz is the BN output's gradient: its epilogue may also reduce the BN backward's channel
+        # sums (BnBwdLink; ops/conv.py decides by the product's K), then the BN backward runs only its apply pass
+        link = BnBwdLink()
+        link.x, link.mean, link.invstd, link.gamma, link.beta, link.relu_x = (x, mean, invstd, pg.master,
+                                                                               pb.master, True)
+        dz = impl.conv_bwd(gy, x, pw.weight, ctx.stride, ctx.padding, True, pw, xform=params, bn_link=link)
         dg, db, finish = _bn_param_grads(pg.store, pg, pb, x.device)
-        dx, _ = _C().bn_bwd(dz, x, None, mean, invstd, pg.master, pb.master, True, dg, db, False)
+        dx, _ = _C().bn_bwd(dz, x, None, mean, invstd, pg.master, pb.master, True, dg, db, False, link.reps)
         finish()
         return (dx if ctx.x_requires_grad else None,) + (None,) * 11
 

@@ -237,3 +237,63 @@ def test_panic_timer_aborts_a_wedged_event_handler():
         assert time.time() - t0 < 4.0  # aborted while the 5 s stall was still in progress
         assert c.op_proc.returncode in (-6, 134), c.op_proc.returncode
         assert "panicTimer" in c.operator_log()
+
+
+def _exec_kubeconfig(plug):
+    return json.dumps({
+        "apiVersion": "v1", "kind": "Config", "current-context": "amd",
+        "clusters": [{"name": "c1", "cluster": {"server": "http://127.0.0.1:1"}}],
+        "contexts": [{"name": "amd", "context": {"cluster": "c1", "user": "u1"}}],
+        "users": [{"name": "u1", "user": {"exec": {"apiVersion": "client.authentication.k8s.io/v1",
+                                                   "command": str(plug)}}}]})
+
+
+def _counting_plugin(tmp_path, expiry_s):
+    """An exec plugin printing token tok-<n> (n = its run count), expiring expiry_s seconds from now (0: none)."""
+    cnt = tmp_path / "runs"
+    cnt.write_text("0")
+    plug = tmp_path / "cred.sh"
+    exp = ('$(date -u -d "+%d seconds" +%%Y-%%m-%%dT%%H:%%M:%%SZ)' % expiry_s) if expiry_s else ""
+    status = '"token":"tok-\'$n\'"' + (',"expirationTimestamp":"\'"%s"\'"' % exp if expiry_s else "")
+    plug.write_text("#!/bin/sh\nn=$(( $(cat %s) + 1 ))\necho $n > %s\n"
+                    "echo '{\"apiVersion\":\"client.authentication.k8s.io/v1\",\"kind\":\"ExecCredential\","
+                    "\"status\":{%s}}'\n" % (cnt, cnt, status))
+    plug.chmod(0o755)
+    return plug, cnt
+
+
+def test_exec_credential_is_refreshed_before_expiry_and_on_401(tmp_path):
+    """an exec-plugin token is re-fetched when it is about to expire (status.expirationTimestamp)
+    and when the API server answers 401; a plugin that hangs is killed after a timeout."""
+    from k8s_amd.fakeapi.server import FakeApiServer
+
+    srv = FakeApiServer().start()
+    try:
+        # short-lived token: every request is within the 60 s refresh margin, so the plugin runs again each time
+        plug, cnt = _counting_plugin(tmp_path, expiry_s=5)
+        srv.httpd.accept_token = lambda t: t.startswith("tok-")
+        codes = _op().kubeconfig_requests(_exec_kubeconfig(plug), srv.url, n=3)
+        assert codes == [200, 200, 200]
+        assert int(cnt.read_text()) >= 3 and len(set(srv.httpd.accepted)) >= 2, srv.httpd.accepted
+        # no expiry, but the server rejects the first token: one 401, a forced refresh, the replay succeeds
+        plug, cnt = _counting_plugin(tmp_path, expiry_s=0)
+        srv.httpd.accept_token = lambda t: t == "tok-2"
+        srv.httpd.accepted.clear()
+        srv.httpd.rejected.clear()
+        codes = _op().kubeconfig_requests(_exec_kubeconfig(plug), srv.url, n=2)
+        assert codes == [200, 200], (codes, srv.httpd.rejected)
+        assert srv.httpd.rejected == ["tok-1"] and int(cnt.read_text()) == 2
+    finally:
+        srv.stop()
+    # a hung plugin is killed after the exec timeout instead of blocking start-up forever
+    hang = tmp_path / "hang.sh"
+    hang.write_text("#!/bin/sh\nsleep 30\n")
+    hang.chmod(0o755)
+    os.environ["K8S_AMD_EXEC_TIMEOUT_MS"] = "500"
+    try:
+        t0 = time.time()
+        with pytest.raises(RuntimeError, match="timed out"):
+            _op().kubeconfig(_exec_kubeconfig(hang))
+        assert time.time() - t0 < 5
+    finally:
+        del os.environ["K8S_AMD_EXEC_TIMEOUT_MS"]
