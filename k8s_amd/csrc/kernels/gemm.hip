@@ -991,7 +991,15 @@ template <class ASrc, class BSrc, int WM, int WN, bool LEAN, bool BNB, bool XEPI
 static void launch_tiles2(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
                           hipStream_t st, const XForm& x = XForm{nullptr, 0, FastDiv{}}) {
   const int tiles = ((M + 64 * WM - 1) / (64 * WM)) * ((N + 64 * WN - 1) / (64 * WN));
-  if (kps <= 2 * BK)
+  // single-buffered (3 blocks / CU) up to this K range: $K8S_AMD_GEMM_SINGLEBUF_MAXK (A/B knob). Measured on the
+  // ResNet-50 b1024 step (scripts/gpurun/env_ab.sh, one box, 2 rounds): 128 -> 12.20k img/s, 256 -> 12.46k,
+  // 512 -> 12.57k, 1024 -> 12.57k, 2304 -> 12.54k, all -> 12.44k: a third block per CU hides more load latency than
+  // a second LDS buffer does on these short / memory-bound K loops
+  static const int single_max = [] {
+    const char* v = getenv("K8S_AMD_GEMM_SINGLEBUF_MAXK");
+    return v ? atoi(v) : 8 * BK;
+  }();
+  if (kps <= single_max)
     hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN, LEAN, BNB, XEPI, F32S, XF>), dim3(tiles, 1, splits),
                        dim3(GEMM_THREADS), 0, st, a, b, e, M, N, K, kps, x);
   else
