@@ -29,9 +29,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from k8s_amd.fakeapi.cluster import LocalCluster  # noqa: E402
 
 
-def _manifest(name, model, steps, logdir, gpu):
+def _manifest(name, model, steps, logdir, gpu, log_every=1):
     c = {"image": "k8s-amd/trainer:rocm7-gfx950", "name": "tensorflow",
-         "args": ["--model", model, "--steps", str(steps), "--log-every", "1", "--logdir", logdir]}
+         "args": ["--model", model, "--steps", str(steps), "--log-every", str(log_every), "--logdir", logdir]}
     if gpu:
         c["resources"] = {"limits": {"amd.com/gpu": 1}}
     else:
@@ -41,7 +41,7 @@ def _manifest(name, model, steps, logdir, gpu):
                                        "template": {"spec": {"containers": [c], "restartPolicy": "OnFailure"}}}]}}
 
 
-def _events(path):
+def _events(path, all_steps=None):
     out = {}
     if os.path.exists(path):
         for line in open(path):
@@ -50,6 +50,8 @@ def _events(path):
             except ValueError:
                 continue
             out.setdefault(r.get("event"), r)
+            if all_steps is not None and r.get("event") == "step":
+                all_steps.append(r)
     return out
 
 
@@ -59,6 +61,9 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--model", default=None)
     ap.add_argument("--timeout", type=float, default=600)
+    ap.add_argument("--log-every", type=int, default=1,
+                    help="trainer log interval; with --steps 30 --log-every 10 the record also carries the TfJob "
+                         "path's steady-state throughput (the trainer's per-interval rate, default batch = bench's)")
     a = ap.parse_args(argv)
     try:
         import torch
@@ -74,10 +79,11 @@ def main(argv=None):
             name = "latency-%d" % i
             logdir = os.path.join(work, name)
             t0 = time.time()
-            c.create(_manifest(name, model, a.steps, logdir, gpu))
+            c.create(_manifest(name, model, a.steps, logdir, gpu, a.log_every))
             job = c.wait(name, timeout=a.timeout)
             t_done = time.time()
-            ev = _events(os.path.join(logdir, "metrics.jsonl"))
+            steps_ev = []
+            ev = _events(os.path.join(logdir, "metrics.jsonl"), steps_ev)
             state = job.get("status", {}).get("state")
             if state != "Succeeded" or "step0" not in ev:
                 print(json.dumps({"error": "job %s ended %s" % (name, state), "events": list(ev)}), flush=True)
@@ -86,10 +92,13 @@ def main(argv=None):
             results.append({"create_to_step0_s": ev["step0"]["time"] - t0, "create_to_trainer_start_s": start - t0,
                             "trainer_start_to_step0_s": ev["step0"]["time"] - start,
                             "create_to_succeeded_s": t_done - t0})
+            rates = [v for r in steps_ev for k, v in r.items() if k.endswith("_per_sec")]
+            if len(rates) >= 2:  # the first interval includes the warm-up steps after step 0
+                results[-1]["tfjob_steady_rate"] = statistics.median(rates[1:])
             c.delete(name)
             print(json.dumps({"run": i, **{k: round(v, 3) for k, v in results[-1].items()}}), file=sys.stderr,
                   flush=True)
-    med = {k: round(statistics.median(r[k] for r in results), 3) for k in results[0]}
+    med = {k: round(statistics.median(r[k] for r in results if k in r), 3) for k in results[0]}
     print(json.dumps({"metric": "TfJob create -> step0 latency", "value": med["create_to_step0_s"], "unit": "s",
                       "higher_is_better": False, "runs": a.runs, "model": model, "gpu": gpu, "median": med,
                       "all": results}), flush=True)

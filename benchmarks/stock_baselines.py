@@ -112,10 +112,16 @@ def main(argv=None):
     ap.add_argument("--seq", type=int, default=None)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--miopen-find-mode", default=None,
+                    help="MIOPEN_FIND_MODE for the run (e.g. FAST: heuristic-ranked short Find; NORMAL: full Find)")
     ap.add_argument("--no-find", action="store_true",
                     help="cudnn.benchmark off: MIOpen immediate mode (heuristic solution per shape, no Find search) "
                          "-- the only way a cold box compiles the batch-1024 kernels inside a GPU-call limit")
     a = ap.parse_args(argv)
+    if a.miopen_find_mode:
+        import os
+
+        os.environ["MIOPEN_FIND_MODE"] = a.miopen_find_mode  # read by MIOpen at its first convolution
     batch = a.batch or {"resnet50": 256, "bert_base": 64, "llama_1b": 2, "llama3_8b": 1}[a.model]
     seq = a.seq or {"bert_base": 128}.get(a.model, 2048)
     torch.backends.cudnn.benchmark = not a.no_find
@@ -142,7 +148,7 @@ def main(argv=None):
                       "ms_per_step": round(1000 * dt / a.steps, 3), "batch": batch,
                       "seq": seq if unit == "tokens" else None, "final_loss": round(float(loss), 4),
                       "stack": "torch %s (MIOpen / hipBLASLt / SDPA / fused optim)" % torch.__version__,
-                      "miopen_find": not a.no_find}), flush=True)
+                      "miopen_find": not a.no_find, "miopen_find_mode": a.miopen_find_mode}), flush=True)
 
 
 if __name__ == "__main__":

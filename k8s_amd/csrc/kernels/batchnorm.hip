@@ -301,6 +301,10 @@ __global__ void bn_eval_prep_kernel(const float* __restrict__ run_mean, const fl
 // Rows are visited grid-stride (block bx takes row groups bx, bx + G, ... of rows_per_iter rows each): the
 // blocks resident at any time then sweep one narrow window of the tensors front to back, which streams at
 // 5.5-5.7 TB/s on MI355X against ~4.9 for one long contiguous run per block (scripts/microbench/stream_bw.hip).
+// (Round 3 tried a flat variant -- short-lived blocks over 8 x 256-vector contiguous chunks, 6.0-6.3 TB/s in
+// scripts/microbench/read_bw.hip -- with per-block partials and a parallel fold: 85.8 vs 81.7 ms per ResNet-50
+// step, the fold of tens of thousands of partials plus the extra launches eating the bandwidth gain; with
+// same-address atomics into 32 replicas instead, 88.1 vs 82.2. Not kept.)
 // MASK: the ReLU mask comes from the packed bit mask (a separate instantiation, so the relu_x variant keeps its
 // register budget and occupancy).
 template <bool MASK>
@@ -435,26 +439,6 @@ __global__ void __launch_bounds__(256) bn_bwd_final_kernel(const float* __restri
   }
 }
 
-// Fold the conv-epilogue replicas [nrep][2][C] of (sum g*mask, sum g*mask*xhat) into dgamma / dbeta / params.
-__global__ void __launch_bounds__(256) bn_bwd_fold_reps_kernel(const float* __restrict__ reps, int nrep, int C,
-                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                               float inv_m, const float* __restrict__ mean,
-                                                               const float* __restrict__ invstd,
-                                                               const float* __restrict__ gamma,
-                                                               const float* __restrict__ beta,
-                                                               float* __restrict__ params) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float a = 0.f, b = 0.f;
-  for (int r = 0; r < nrep; ++r) {
-    a += reps[((long)r * 2) * C + c];
-    b += reps[((long)r * 2 + 1) * C + c];
-  }
-  if (dbeta) dbeta[c] = a;
-  if (dgamma) dgamma[c] = b;
-  bn_bwd_consts(c, C, a, b, inv_m, mean, invstd, gamma, beta, params);
-}
-
 // dx = sc*dy_eff + B*x + D; dres = dy_eff. dy_eff = dy masked by the packed bits (residual BN), by relu_on(x)
 // (non-residual BN + ReLU) or not at all. One vector per thread (see the header).
 __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t* __restrict__ dy,
@@ -571,16 +555,6 @@ static void launch_bn_bwd_apply(const uint16_t* dy, const uint16_t* x, const uin
   if (nvec >= (1L << 31)) throw std::runtime_error("BatchNorm tensor too large (>= 2^31 vectors)");
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(cdiv(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, dy, x, mask, params,
                      (int)relu_x, dx, dres, (int)nvec, C, make_fastdiv(C / 8));
-}
-
-// BN backward whose reduction already happened in the epilogue of the kernel that produced dy.
-void launch_bn_bwd_from_sums(const uint16_t* dy, const uint16_t* x, const float* mean, const float* invstd,
-                             const float* gamma, const float* beta, bool relu_x, uint16_t* dx, uint16_t* dres,
-                             float* dgamma, float* dbeta, const float* reps, int nrep, float* params, long M, int C,
-                             hipStream_t st, const uint8_t* mask) {
-  hipLaunchKernelGGL(bn_bwd_fold_reps_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, reps, nrep, C, dgamma, dbeta,
-                     1.f / (float)M, mean, invstd, gamma, beta, params);
-  launch_bn_bwd_apply(dy, x, mask, params, relu_x, dx, dres, M, C, st);
 }
 
 void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, const float* invstd, const float* gamma,

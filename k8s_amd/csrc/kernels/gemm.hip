@@ -326,15 +326,6 @@ struct Epi {
   float* stats;       // [STAT_REPL][2][N] fp32 per-column sum / sum of squares of the stored outputs
                       // (BN fusion) or null; tile row tm adds into replica tm % STAT_REPL so the atomics
                       // spread over STAT_REPL x 2N addresses instead of contending on 2N
-  // BatchNorm-BACKWARD statistics of the stored (bf16) output g, which is the gradient w.r.t. a BN output:
-  // bstats[rep][0][n] += sum_m g*mask, bstats[rep][1][n] += sum_m g*mask*xhat with xhat from the BN input bx
-  // and the ReLU mask from the packed bits bmask (residual BN), recomputed from bx (brelu_x), or all ones.
-  // Replaces the BN backward's separate reduction pass over g and x (lean epilogue only).
-  float* bstats;
-  const uint16_t* bx;
-  const uint8_t* bmask;
-  const float *bmean, *binvstd, *bgamma, *bbeta;
-  int brelu_x;
   // Sub-grid output (stride-s data gradient by output parity): GEMM row m = (n, i, j) over an rHo x rWo grid
   // is stored at output row (n, i*rst + ra, j*rst + rb) of an rH x rW image. rst == 0: identity.
   int rst, rHo, rWo, rH, rW, ra, rb;
@@ -366,10 +357,9 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 // WM x WN waves (WM * WN = 4), each owning a 64 x 64 piece: 128 x 128 tiles (2 x 2) in general, 256 x 64
 // (4 x 1) when N = 64 (the early ResNet convolutions and the stem) so no MFMA work is spent on padding.
 // Only K-major sources may sit on a 64-wide side (the MN-major swizzle assumes 256-B rows).
-// LEAN: the staged bf16 epilogue (also the only one with the BN-statistics reductions, forward and backward).
-// BNB (lean only): the epilogue also reduces the BatchNorm-backward statistics (Epi::bstats); the BN input tile
-// x[m0:m0+BM][n0:n0+BN] is DMA'd into LDS during the K loop -- into the idle buffer of the last K step (NBUF = 2)
-// or a second 32 KB region issued with the first stage (NBUF = 1) -- so the copy-out reads it from LDS.
+// LEAN: the staged bf16 epilogue (also the only one with the BN-statistics reduction).
+// (Rounds 2-3 also had a BatchNorm-BACKWARD statistics epilogue for the data gradients, the BN input tile DMA'd
+// into LDS beside the operands; it measured a net loss on ResNet-50 both rounds and was removed -- ops/conv.py.)
 // XEPI (lean only): bias / ReLU / GELU / pre-activation copy in the staged epilogue (the transformer linears'
 // forward); its own instantiation so the convolutions' lean kernels stay as small as before (the extra epilogue
 // code compiled into every lean kernel cost ResNet-50 1.1 %, measured new/old/new/old on one box).
@@ -380,18 +370,16 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 // (MN-major: a weight gradient's im2col / activation operand) is loaded through VGPRs, transformed and written to
 // its LDS slot by ds_write instead of by LDS-DMA (same lane-linear image, same swizzle). The staging registers of
 // the next K step are filled behind this step's MFMAs and written after them, before the step's barrier.
-template <class ASrc, class BSrc, int NBUF, int WM = 2, int WN = 2, bool LEAN = false, bool BNB = false,
-          bool XEPI = false, bool F32S = false, int XF = 0>
-__global__ void __launch_bounds__(GEMM_THREADS, (NBUF == 1 && !BNB && XF == 0) ? 3 : 2)
+template <class ASrc, class BSrc, int NBUF, int WM = 2, int WN = 2, bool LEAN = false, bool XEPI = false,
+          bool F32S = false, int XF = 0>
+__global__ void __launch_bounds__(GEMM_THREADS, (NBUF == 1 && (XF == 0 || (XF == 1 && WM == 2))) ? 3 : 2)
 gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XForm X) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
   constexpr int TA = BM * BK * 2, TB = BN * BK * 2;  // operand tile bytes
   static_assert(WM * WN == 4, "4 waves");
   static_assert((WM == 2 || ASrc::kmajor) && (WN == 2 || BSrc::kmajor), "MN-major operands need a 128 side");
-  static_assert(!BNB || LEAN, "the BN-backward reduction lives in the lean epilogue");
-  static_assert(BM * BN * 2 <= TA + TB, "the x (and C) tile fits one operand buffer");
-  constexpr int NREG = (NBUF == 1 && BNB) ? 2 : NBUF;  // 32 KB LDS regions
-  __shared__ __attribute__((aligned(1024))) char smem[NREG * (TA + TB)];  // [buf][A|B]
+  static_assert(BM * BN * 2 <= TA + TB, "the C tile fits one operand buffer");
+  __shared__ __attribute__((aligned(1024))) char smem[NBUF * (TA + TB)];  // [buf][A|B]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
 
@@ -527,27 +515,10 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
   };
 
   constexpr int CPR = BN / 8;  // 16-B chunks per output-tile row
-  // BN input tile -> LDS, lane-linear: slot q (= the copy-out's chunk index) at byte q * 16
-  auto stage_x = [&](char* dst) {
-#pragma unroll
-    for (int rd = 0; rd < BM * CPR / GEMM_THREADS; ++rd) {
-      const int q = rd * GEMM_THREADS + tid, row = q / CPR, c = q % CPR;
-      const int m = min(m0 + row, M - 1), n = n0 + c * 8;
-      const void* g = n < N ? (const void*)(E.bx + (long)m * E.ldc + n) : (const void*)g_zero_page;
-      glds16(g, dst + (rd * GEMM_THREADS + wid_u * 64) * 16);
-    }
-  };
-  int xbuf = -1;  // LDS region holding the x tile (BNB)
   const bool late = XF == 0 && nt >= E.late_nt;
   if (nt > 0) {
     stage(0, kbeg);
     xload(kbeg);
-    if constexpr (BNB && NBUF == 1) {
-      if (E.bstats) {
-        stage_x(smem + (TA + TB));
-        xbuf = 1;
-      }
-    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     xstore(0);
     __syncthreads();
@@ -585,14 +556,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
         // long K loops: the next K step's loads are issued behind the first half's MFMAs (their address
         // arithmetic then runs while the matrix pipe is busy instead of delaying the MFMAs); short ones keep them
         // ahead of the MFMAs (more time in flight). The buffer they fill was released by the previous barrier.
-        if (t + 1 < nt) {
-          if (late) stage(cur ^ 1, kbeg + (t + 1) * BK);
-        } else if constexpr (BNB) {  // last K step: the other buffer is idle
-          if (E.bstats) {
-            stage_x(smem + (cur ^ 1) * (TA + TB));
-            xbuf = cur ^ 1;
-          }
-        }
+        if (late && t + 1 < nt) stage(cur ^ 1, kbeg + (t + 1) * BK);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -609,9 +573,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
   // and the data gradients): the tile goes through LDS and leaves as 16-B row-contiguous stores, and none of the
   // general epilogue's run-time branches are compiled in (the general instantiations are ~85 KB of code, more
   // than the instruction cache). LDS image [BM][BN] bf16, 16-B chunk c of row r at c ^ (r % (BN / 8)).
-  // the C tile goes to region 0, or region 1 when the x tile sits in region 0 (NBUF = 2, even step count)
-  uint16_t* const ctile = reinterpret_cast<uint16_t*>(smem + (xbuf == 0 ? (TA + TB) : 0));
-  const uint16_t* const xtile = reinterpret_cast<const uint16_t*>(smem + (xbuf < 0 ? 0 : xbuf) * (TA + TB));
+  uint16_t* const ctile = reinterpret_cast<uint16_t*>(smem);
   float st_s[4][4], st_q[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -650,31 +612,16 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
     }
     __syncthreads();
     // copy-out: thread t always handles 16-B chunk c = t % CPR of its rows (GEMM_THREADS % CPR == 0), so it
-    // also accumulates the BN statistics of those 8 columns from the bf16 values it stores: forward
-    // (sum, sum of squares) for Epi::stats, or backward (sum g*mask, sum g*mask*xhat) for Epi::bstats
-    float* const stat_out = E.stats ? E.stats : E.bstats;
-    const bool bwd = E.bstats != nullptr;
+    // also accumulates the BN statistics (sum, sum of squares) of those 8 columns from the bf16 values it stores
+    float* const stat_out = E.stats;
     float ps[8], pq[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) ps[r] = pq[r] = 0.f;
-    float bmu[8], bis[8], bsc[8], bbt[8];  // this thread's 8 channels (BN backward)
-    if (bwd) {
-      const int n = n0 + (tid % CPR) * 8;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int cn = n + r < N ? n + r : N - 1;
-        bmu[r] = E.bmean[cn];
-        bis[r] = E.binvstd[cn];
-        // the BN forward's affine pair (batchnorm.hip bn_affine_regs), so the ReLU decision below is bit-identical
-        bsc[r] = E.brelu_x ? E.bgamma[cn] * bis[r] : 0.f;
-        bbt[r] = E.brelu_x ? __builtin_fmaf(-bmu[r], bsc[r], E.bbeta[cn]) : 0.f;
-      }
-    }
     constexpr int CHUNKS = BM * CPR;
-    // fast path (convolution forward with statistics, plain data gradients): identity rows, store mode, no BN
-    // backward. A thread's chunk column is fixed and its rows advance by GEMM_THREADS / CPR per trip, so the
+    // fast path (convolution forward with statistics, plain and accumulating data gradients): identity rows. A
+    // thread's chunk column is fixed and its rows advance by GEMM_THREADS / CPR per trip, so the
     // output pointer is one 64-bit add per trip; the statistics use packed fp32 adds / FMAs on the unpacked pairs.
-    if (!BNB && !XEPI && !E.rst && !bwd) {
+    if (!XEPI && !E.rst) {
       constexpr int RSTEP = GEMM_THREADS / CPR;
       const int c = tid % CPR, row0 = tid / CPR;
       const int n = n0 + c * 8;
@@ -766,22 +713,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
         for (int r = 0; r < 8; ++r) o[r] = (short)f2bf(bf2f((uint16_t)o[r]) + bf2f((uint16_t)old[r]));
       }
       *reinterpret_cast<bf16x8_t*>(cp) = o;
-      if (bwd) {
-        const long off = orow * E.ldc + n;
-        const bf16x8_t xv = BNB ? *reinterpret_cast<const bf16x8_t*>(xtile + q * 8)
-                                : *reinterpret_cast<const bf16x8_t*>(E.bx + off);
-        const uint32_t bits = E.bmask ? (uint32_t)E.bmask[off >> 3] : 0xFFu;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const float xh = (bf2f((uint16_t)xv[r]) - bmu[r]) * bis[r];
-          bool on = (bits >> r) & 1u;
-          // the forward's ReLU decision, bit for bit: bf16(fma(x, scale, shift)) > 0
-          if (E.brelu_x) on = bf2f(f2bf(__builtin_fmaf(bf2f((uint16_t)xv[r]), bsc[r], bbt[r]))) > 0.f;
-          const float g = on ? bf2f((uint16_t)o[r]) : 0.f;
-          ps[r] += g;
-          pq[r] += g * xh;
-        }
-      } else if (stat_out) {
+      if (stat_out) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           const float v = bf2f((uint16_t)o[r]);
@@ -979,6 +911,18 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
 }
 
 // ----------------------------------------------------------------------------- host side
+// Single-buffered (3 blocks / CU) kernel up to this K range per block, double-buffered (2 blocks / CU) above:
+// $K8S_AMD_GEMM_SINGLEBUF_MAXK (A/B knob). Measured on the ResNet-50 b1024 step (scripts/gpurun/env_ab.sh, one box,
+// 2 rounds): 128 -> 12.20k img/s, 256 -> 12.46k, 512 -> 12.57k, 1024 -> 12.57k, 2304 -> 12.54k, all -> 12.44k: a
+// third block per CU hides more load latency than a second LDS buffer does on these short / memory-bound K loops.
+static int single_buf_maxk() {
+  static const int v = [] {
+    const char* e = getenv("K8S_AMD_GEMM_SINGLEBUF_MAXK");
+    return e ? atoi(e) : 8 * BK;
+  }();
+  return v;
+}
+
 // splits actually launched for a requested count (each split a whole number of BK tiles)
 static int effective_splits(int K, int splits) {
   if (splits <= 1) return 1;
@@ -986,24 +930,15 @@ static int effective_splits(int K, int splits) {
   return (K + kps - 1) / kps;
 }
 
-template <class ASrc, class BSrc, int WM, int WN, bool LEAN, bool BNB, bool XEPI = false, bool F32S = false,
-          int XF = 0>
+template <class ASrc, class BSrc, int WM, int WN, bool LEAN, bool XEPI = false, bool F32S = false, int XF = 0>
 static void launch_tiles2(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
                           hipStream_t st, const XForm& x = XForm{nullptr, 0, FastDiv{}}) {
   const int tiles = ((M + 64 * WM - 1) / (64 * WM)) * ((N + 64 * WN - 1) / (64 * WN));
-  // single-buffered (3 blocks / CU) up to this K range: $K8S_AMD_GEMM_SINGLEBUF_MAXK (A/B knob). Measured on the
-  // ResNet-50 b1024 step (scripts/gpurun/env_ab.sh, one box, 2 rounds): 128 -> 12.20k img/s, 256 -> 12.46k,
-  // 512 -> 12.57k, 1024 -> 12.57k, 2304 -> 12.54k, all -> 12.44k: a third block per CU hides more load latency than
-  // a second LDS buffer does on these short / memory-bound K loops
-  static const int single_max = [] {
-    const char* v = getenv("K8S_AMD_GEMM_SINGLEBUF_MAXK");
-    return v ? atoi(v) : 8 * BK;
-  }();
-  if (kps <= single_max)
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN, LEAN, BNB, XEPI, F32S, XF>), dim3(tiles, 1, splits),
+  if (kps <= single_buf_maxk())
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN, LEAN, XEPI, F32S, XF>), dim3(tiles, 1, splits),
                        dim3(GEMM_THREADS), 0, st, a, b, e, M, N, K, kps, x);
   else
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2, WM, WN, LEAN, BNB, XEPI, F32S, XF>), dim3(tiles, 1, splits),
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2, WM, WN, LEAN, XEPI, F32S, XF>), dim3(tiles, 1, splits),
                        dim3(GEMM_THREADS), 0, st, a, b, e, M, N, K, kps, x);
 }
 
@@ -1017,17 +952,12 @@ static bool f32s_on() {
 }
 static bool epi_extra(const Epi& e) { return e.bias || e.pre || e.act != 0; }
 static bool lean_epi(const Epi& e, int N, bool allow_extra) {
-  if (epi_extra(e) && (!allow_extra || e.mode != 0 || e.rst || e.stats || e.bstats || e.addsrc ||
+  if (epi_extra(e) && (!allow_extra || e.mode != 0 || e.rst || e.stats || e.addsrc ||
                        (reinterpret_cast<uintptr_t>(e.pre) & 15) != 0))
     return false;
   return !e.out_f32 && (e.mode == 0 || e.mode == 1) && (e.ldc & 7) == 0 && (N & 7) == 0 &&
          (reinterpret_cast<uintptr_t>(e.c) & 15) == 0;
 }
-
-// operand pairs that produce a BatchNorm output gradient (the dgrads): the only BN-backward instantiations
-template <class ASrc, class BSrc>
-constexpr bool kBnbPair = (std::is_same_v<ASrc, KMajor> && std::is_same_v<BSrc, MNMajorK>) ||
-                          (std::is_same_v<ASrc, ConvA> && std::is_same_v<BSrc, KMajor>);
 
 template <class ASrc, class BSrc, int WM, int WN>
 static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
@@ -1036,15 +966,15 @@ static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int 
   // the weight gradients (B = the BN input, fp32 output or split-K slab through the F32S epilogue)
   if (xf) {
     if constexpr ((std::is_same_v<ASrc, ConvA> || std::is_same_v<ASrc, KMajor>) && std::is_same_v<BSrc, KMajor>) {
-      if (lean_epi(e, N, false) && !e.bstats && !e.rst && !e.addsrc) {
-        launch_tiles2<ASrc, BSrc, WM, WN, true, false, false, false, 1>(a, b, e, M, N, K, kps, splits, st, *xf);
+      if (lean_epi(e, N, false) && !e.rst && !e.addsrc) {
+        launch_tiles2<ASrc, BSrc, WM, WN, true, false, false, 1>(a, b, e, M, N, K, kps, splits, st, *xf);
         return;
       }
     }
     if constexpr (std::is_same_v<ASrc, MNMajorK> && (std::is_same_v<BSrc, ConvWgB> || std::is_same_v<BSrc, MNMajorK>) &&
                   WM == 2 && WN == 2) {
       if (e.out_f32 && e.mode != 2 && !epi_extra(e) && !e.stats && !e.rst) {
-        launch_tiles2<ASrc, BSrc, WM, WN, false, false, false, true, 2>(a, b, e, M, N, K, kps, splits, st, *xf);
+        launch_tiles2<ASrc, BSrc, WM, WN, false, false, true, 2>(a, b, e, M, N, K, kps, splits, st, *xf);
         return;
       }
     }
@@ -1054,36 +984,27 @@ static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int 
   constexpr bool kXepi = std::is_same_v<ASrc, KMajor> && std::is_same_v<BSrc, KMajor>;
   if constexpr (kXepi) {
     if (epi_extra(e) && lean_epi(e, N, true)) {
-      launch_tiles2<ASrc, BSrc, WM, WN, true, false, true>(a, b, e, M, N, K, kps, splits, st);
+      launch_tiles2<ASrc, BSrc, WM, WN, true, true>(a, b, e, M, N, K, kps, splits, st);
       return;
     }
   }
   if constexpr (!std::is_same_v<BSrc, ConvWgB>) {
     if (lean_epi(e, N, false)) {
-      if constexpr (kBnbPair<ASrc, BSrc>) {
-        if (e.bstats) {
-          if (e.rst || splits != 1) throw std::runtime_error("BN-backward epilogue: identity rows, no split-K");
-          launch_tiles2<ASrc, BSrc, WM, WN, true, true>(a, b, e, M, N, K, kps, splits, st);
-          return;
-        }
-      }
-      if (e.bstats) throw std::runtime_error("BN-backward epilogue requested for an operand pair without it");
-      launch_tiles2<ASrc, BSrc, WM, WN, true, false>(a, b, e, M, N, K, kps, splits, st);
+      launch_tiles2<ASrc, BSrc, WM, WN, true>(a, b, e, M, N, K, kps, splits, st);
       return;
     }
   }
-  if (e.bstats) throw std::runtime_error("the BatchNorm-backward epilogue needs a plain bf16 output (lean epilogue)");
   if (e.addsrc || e.addmask) throw std::runtime_error("a separate (masked) addend needs the lean epilogue");
   // weight gradients (both operands MN-major: dense or im2col) with an fp32 output or split-K slab
   constexpr bool kWgrad = std::is_same_v<ASrc, MNMajorK> &&
                           (std::is_same_v<BSrc, MNMajorK> || std::is_same_v<BSrc, ConvWgB>);
   if constexpr (kWgrad && WM == 2 && WN == 2) {
     if (e.out_f32 && e.mode != 2 && !epi_extra(e) && !e.stats && !e.rst && f32s_on()) {
-      launch_tiles2<ASrc, BSrc, WM, WN, false, false, false, true>(a, b, e, M, N, K, kps, splits, st);
+      launch_tiles2<ASrc, BSrc, WM, WN, false, false, true>(a, b, e, M, N, K, kps, splits, st);
       return;
     }
   }
-  launch_tiles2<ASrc, BSrc, WM, WN, false, false>(a, b, e, M, N, K, kps, splits, st);
+  launch_tiles2<ASrc, BSrc, WM, WN, false>(a, b, e, M, N, K, kps, splits, st);
 }
 
 template <class ASrc, class BSrc>
@@ -1113,11 +1034,6 @@ static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act,
   e.alpha = alpha;
   e.stats = nullptr;
   e.slab = 0;
-  e.bstats = nullptr;
-  e.bx = nullptr;
-  e.bmask = nullptr;
-  e.bmean = e.binvstd = e.bgamma = e.bbeta = nullptr;
-  e.brelu_x = 0;
   e.rst = e.rHo = e.rWo = e.rH = e.rW = e.ra = e.rb = 0;
   e.addsrc = nullptr;
   e.addmask = nullptr;
@@ -1149,7 +1065,8 @@ int gemm_choose_splits(int M, int N, int K) {
   for (int s = 1; s <= 256 && s <= ktiles; ++s) {
     const int kpt = (ktiles + s - 1) / s;       // K tiles per split
     if ((ktiles + kpt - 1) / kpt != s) continue;  // same kps as a smaller s
-    const long slots = kpt * BK <= 2 * BK ? 3 * 256 : 2 * 256;
+    static const bool old_model = getenv("K8S_AMD_SPLITK_OLD") && getenv("K8S_AMD_SPLITK_OLD")[0] == '1';  // A/B
+    const long slots = kpt * BK <= (old_model ? 2 * BK : single_buf_maxk()) ? 3 * 256 : 2 * 256;
     const long rounds = (tiles * s + slots - 1) / slots;
     const double t = (double)rounds * kpt + (s > 1 ? s * slab_cost : 0.0);
     if (t < best * 0.999) {
@@ -1186,27 +1103,14 @@ long gemm_splitk_workspace(int M, int N, int splits) { return splits > 1 ? (long
 //  a_kmajor: A stored [M][K] (lda) else [K][M];  b_kmajor: B stored [N][K] (ldb) else [K][N]
 //  mode 0 store / 1 accumulate; with splits > 1 (fp32 C, plain epilogue) the K range is split over
 //  blockIdx.z, each split writes an fp32 slab of `ws` and a reduce kernel combines them into C.
-static void apply_bnbwd(Epi& e, const BnBwdEpi* bb) {
-  if (!bb) return;
-  e.bstats = bb->stats;
-  e.bx = bb->x;
-  e.bmask = bb->mask;
-  e.bmean = bb->mean;
-  e.binvstd = bb->invstd;
-  e.bgamma = bb->gamma;
-  e.bbeta = bb->beta;
-  e.brelu_x = bb->relu_x;
-}
-
 void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                  long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
-                 float alpha, int splits, float* ws, hipStream_t st, const BnBwdEpi* bnb, const AddEpi* add,
+                 float alpha, int splits, float* ws, hipStream_t st, const AddEpi* add,
                  const float* xform_b, int xform_c) {
   splits = effective_splits(K, splits);
   const bool slab = splits > 1;
   Epi e = make_epi(slab ? (void*)ws : C, slab ? (long)N : ldc, c_f32, bias, act, pre, slab ? 3 : mode, alpha);
   e.slab = (long)M * N;
-  if (!slab) apply_bnbwd(e, bnb);
   if (add) {
     if (slab || mode != 1) throw std::runtime_error("a separate addend needs accumulate mode and no split-K");
     e.addsrc = add->src;
@@ -1231,15 +1135,14 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
 // decode, any other C % 8 == 0 the per-unit one.
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int K,
                      int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
-                     int mode, float* stats, hipStream_t st, const BnBwdEpi* bnb, const SubGrid* sg,
+                     int mode, float* stats, hipStream_t st, const SubGrid* sg,
                      const float* xform) {
   const int M = N * Ho * Wo, RSC = R * S * C;
   KMajor b{w, (long)RSC, K, RSC};
   Epi e = make_epi(y, K, y_f32, bias, act, nullptr, mode, 1.f);
   e.stats = stats;
-  apply_bnbwd(e, bnb);
   if (sg) {
-    if (bnb || stats) throw std::runtime_error("sub-grid output takes no statistics epilogue");
+    if (stats) throw std::runtime_error("sub-grid output takes no statistics epilogue");
     e.rst = sg->stride;
     e.rHo = Ho;
     e.rWo = Wo;

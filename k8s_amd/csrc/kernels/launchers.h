@@ -37,10 +37,6 @@ constexpr int kConvStatReplicas = 32;  // must match STAT_REPL in gemm.hip
 void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, const float* invstd, const float* gamma,
                    const float* beta, bool relu_x, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta,
                    float* work, float* params, long M, int C, hipStream_t st, const uint8_t* mask = nullptr);
-void launch_bn_bwd_from_sums(const uint16_t* dy, const uint16_t* x, const float* mean, const float* invstd,
-                             const float* gamma, const float* beta, bool relu_x, uint16_t* dx, uint16_t* dres,
-                             float* dgamma, float* dbeta, const float* reps, int nrep, float* params, long M, int C,
-                             hipStream_t st, const uint8_t* mask = nullptr);
 // packed ReLU bits of a bf16 tensor (bit j of byte e = y[8e + j] > 0), nvec = numel / 8
 void launch_relu_mask(const uint16_t* y, uint8_t* mask, long nvec, hipStream_t st);
 
@@ -62,15 +58,6 @@ void launch_xent_bwd(const void* logits, bool bf16, const int64_t* labels, const
 
 // gemm.hip
 int gemm_choose_splits(int M, int N, int K);
-// BatchNorm-backward statistics computed in a GEMM / conv epilogue whose bf16 output is the gradient w.r.t.
-// a BN layer's output (see Epi::bstats in gemm.hip); stats = zeroed fp32 [kConvStatReplicas][2][N].
-struct BnBwdEpi {
-  float* stats;
-  const uint16_t* x;  // BN input
-  const uint8_t* mask;  // packed ReLU mask of a residual BN (bit j of byte e = element 8e + j) or null
-  const float *mean, *invstd, *gamma, *beta;
-  int relu_x;         // mask recomputed from x
-};
 // accumulate-mode addend read from src (same layout as C) instead of C, elements with a clear bit in the packed
 // mask (bit j of byte e = element 8e + j; null = all set) taken as zero (see Epi::addsrc in gemm.hip)
 struct AddEpi {
@@ -79,8 +66,8 @@ struct AddEpi {
 };
 void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                  long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
-                 float alpha, int splits, float* ws, hipStream_t st, const BnBwdEpi* bnb = nullptr,
-                 const AddEpi* add = nullptr, const float* xform_b = nullptr, int xform_c = 0);
+                 float alpha, int splits, float* ws, hipStream_t st, const AddEpi* add = nullptr,
+                 const float* xform_b = nullptr, int xform_c = 0);
 // out = bit ? src : 0 per element (bf16, n % 8 == 0; mask packed as above)
 void launch_mask_apply(const uint16_t* src, const uint8_t* mask, uint16_t* out, long n, hipStream_t st);
 long gemm_splitk_workspace(int M, int N, int splits);  // fp32 elements of the split-K slab workspace
@@ -96,8 +83,7 @@ struct SubGrid {
 };
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int K,
                      int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
-                     int mode, float* stats, hipStream_t st,
-                     const BnBwdEpi* bnb = nullptr, const SubGrid* sg = nullptr, const float* xform = nullptr);
+                     int mode, float* stats, hipStream_t st, const SubGrid* sg = nullptr, const float* xform = nullptr);
 // xform (here and in launch_gemm / launch_wgrad_stream): fp32 [2][C] BatchNorm (scale | shift): the activation
 // operand x is consumed as relu(x * scale + shift), normalised as it is loaded (gemm.hip XForm)
 void launch_conv_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int C, int K, int R,

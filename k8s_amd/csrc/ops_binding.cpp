@@ -217,7 +217,7 @@ static const float* xform_ptr(const c10::optional<Tensor>& xf, long C) {
 // `y` -- is packed from y first (compatibility; the trainer passes the mask).
 std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor mean, Tensor invstd, Tensor gamma,
                            Tensor beta, bool relu_x, Tensor dgamma, Tensor dbeta, bool want_dres,
-                           c10::optional<Tensor> reps, c10::optional<Tensor> mask) {
+                           c10::optional<Tensor> mask) {
   check_cuda(dy, "dy"); check_cuda(x, "x");
   check_dtype(dy, at::kBFloat16, "dy"); check_dtype(x, at::kBFloat16, "x");
   TORCH_CHECK(dy.sizes() == x.sizes());
@@ -239,15 +239,6 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor 
   const uint8_t* mk = y ? ymask.data_ptr<uint8_t>() : cmask(mask);
   TORCH_CHECK(!mk || (!relu_x && (y || mask->numel() == x.numel() / 8)),
               "packed mask: M*C/8 bytes, exclusive with relu_x");
-  if (reps) {  // (sum g*mask, sum g*mask*xhat) already accumulated by the epilogue that produced dy
-    TORCH_CHECK(reps->is_cuda() && reps->scalar_type() == at::kFloat && reps->is_contiguous() &&
-                    reps->numel() == (long)k8s_amd::kConvStatReplicas * 2 * C,
-                "reps must be fp32 [conv_stat_replicas, 2, C]");
-    k8s_amd::launch_bn_bwd_from_sums(cbf(dy), cbf(x), f32(mean), f32(invstd), f32(gamma), f32(beta), relu_x, bf(dx),
-                                     want_dres ? bf(dres) : nullptr, f32(dgamma), f32(dbeta), f32(*reps),
-                                     k8s_amd::kConvStatReplicas, f32(params), M, C, cur_stream(), mk);
-    return {dx, dres};
-  }
   auto work = torch::empty({k8s_amd::bn_workspace_floats(M, C)}, gamma.options());
   k8s_amd::launch_bn_bwd(cbf(dy), cbf(x), f32(mean), f32(invstd), f32(gamma), f32(beta), relu_x, bf(dx),
                          want_dres ? bf(dres) : nullptr, f32(dgamma), f32(dbeta), f32(work), f32(params), M, C,
@@ -336,34 +327,6 @@ void check_bf16_operand(const Tensor& t, const char* name) {
 }
 
 // a: [M,K] if a_kmajor else [K,M];  b: [N,K] if b_kmajor else [K,N];  returns / writes C[M,N]
-// bnb = (stats [R,2,N] zeroed fp32, x, mask|empty, mean, invstd, gamma, beta) + relu_x for the BN-backward
-// statistics epilogue; x is the BN input ([M, N] bf16 matching the output), mask the packed ReLU bits of a
-// residual BN's output (uint8 [M*N/8]).
-struct BnbHolder {
-  k8s_amd::BnBwdEpi e;
-  bool on = false;
-};
-BnbHolder parse_bnb(const c10::optional<std::vector<Tensor>>& t, c10::optional<bool> relu_x, long M, long N) {
-  BnbHolder h;
-  if (!t) return h;
-  TORCH_CHECK(t->size() == 7, "bnb = [stats, x, mask, mean, invstd, gamma, beta] (mask may be an empty tensor)");
-  const auto& v = *t;
-  TORCH_CHECK(v[0].numel() == (long)k8s_amd::kConvStatReplicas * 2 * N && v[0].scalar_type() == at::kFloat,
-              "bnb stats must be fp32 [conv_stat_replicas, 2, N]");
-  TORCH_CHECK(v[1].numel() == M * N && v[1].scalar_type() == at::kBFloat16 && v[1].is_contiguous(), "bnb x shape");
-  const bool has_mask = v[2].defined() && v[2].numel() > 0;
-  if (has_mask)
-    TORCH_CHECK(v[2].numel() == M * N / 8 && v[2].scalar_type() == at::kByte && v[2].is_contiguous(),
-                "bnb mask must be uint8 [M*N/8]");
-  for (int i = 3; i < 7; ++i)
-    TORCH_CHECK(v[i].numel() == N && v[i].scalar_type() == at::kFloat && v[i].is_contiguous(), "bnb per-channel");
-  TORCH_CHECK(!(has_mask && relu_x.value_or(false)), "bnb: mask and relu_x are exclusive");
-  h.e = k8s_amd::BnBwdEpi{f32(v[0]), cbf(v[1]), has_mask ? v[2].data_ptr<uint8_t>() : nullptr, f32(v[3]),
-                          f32(v[4]), f32(v[5]), f32(v[6]), relu_x.value_or(false) ? 1 : 0};
-  h.on = true;
-  return h;
-}
-
 // K8S_AMD_GEMM256=0 routes every product to the 128 x 128 kernel, =2 every product the 256 x 256 kernel can take
 // (A/B comparisons, debugging); read per call, so one process can A/B both kernels
 static int gemm256_mode() {
@@ -389,8 +352,7 @@ Tensor mask_apply(Tensor src, Tensor mask) {
 
 Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tensor> out, bool out_f32,
             c10::optional<Tensor> bias, int64_t act, c10::optional<Tensor> pre, bool accumulate, double alpha,
-            int64_t splits, c10::optional<std::vector<Tensor>> bnb, c10::optional<bool> bnb_relu_x,
-            c10::optional<Tensor> add_src, c10::optional<Tensor> add_mask, c10::optional<Tensor> xform_b,
+            int64_t splits, c10::optional<Tensor> add_src, c10::optional<Tensor> add_mask, c10::optional<Tensor> xform_b,
             int64_t xform_c) {
   check_bf16_operand(a, "A");
   check_bf16_operand(b, "B");
@@ -427,9 +389,9 @@ Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tens
     TORCH_CHECK(!add_mask, "add_mask needs add_src");
   }
   const float* xfb = xform_ptr(xform_b, xform_c);
-  if (xfb) TORCH_CHECK(!a_kmajor && !b_kmajor && out_f32 && !bias && act == 0 && !pre && !bnb && !add_src &&
+  if (xfb) TORCH_CHECK(!a_kmajor && !b_kmajor && out_f32 && !bias && act == 0 && !pre && !add_src &&
                            N % xform_c == 0, "normalize-on-load GEMM: the plain weight-gradient form only");
-  if (!xfb && !bnb && !add_src && use_gemm256(M, N, K, a_kmajor, b_kmajor)) {
+  if (!xfb && !add_src && use_gemm256(M, N, K, a_kmajor, b_kmajor)) {
     k8s_amd::launch_gemm256(cbf(a), a.stride(0), a_kmajor, cbf(b), b.stride(0), b_kmajor, c.data_ptr(), N, out_f32,
                             (int)M, (int)N, (int)K, bias ? bias->data_ptr<float>() : nullptr, (int)act,
                             pre ? bf(*pre) : nullptr, accumulate, (float)alpha, cur_stream());
@@ -443,20 +405,17 @@ Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tens
   }
   Tensor ws;
   if (sp > 1) ws = torch::empty({k8s_amd::gemm_splitk_workspace((int)M, (int)N, sp)}, a.options().dtype(at::kFloat));
-  BnbHolder bb = parse_bnb(bnb, bnb_relu_x, M, N);
-  TORCH_CHECK(!bb.on || (!out_f32 && sp == 1), "the BN-backward epilogue needs a bf16, non-split output");
   k8s_amd::launch_gemm(cbf(a), a.stride(0), a_kmajor, cbf(b), b.stride(0), b_kmajor, c.data_ptr(), N, out_f32,
                        (int)M, (int)N, (int)K, bias ? bias->data_ptr<float>() : nullptr, (int)act,
                        pre ? bf(*pre) : nullptr, mode, (float)alpha, sp, sp > 1 ? f32(ws) : nullptr, cur_stream(),
-                       bb.on ? &bb.e : nullptr, add_src ? &add : nullptr, xfb, (int)xform_c);
+                       add_src ? &add : nullptr, xfb, (int)xform_c);
   return c;
 }
 
 static inline int conv_out(int in, int k, int st, int pad, int dil) { return (in + 2 * pad - dil * (k - 1) - 1) / st + 1; }
 
 Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, bool out_f32, c10::optional<Tensor> bias,
-                int64_t act, c10::optional<Tensor> stats, c10::optional<std::vector<Tensor>> bnb,
-                c10::optional<bool> bnb_relu_x, c10::optional<Tensor> xform) {
+                int64_t act, c10::optional<Tensor> stats, c10::optional<Tensor> xform) {
   check_cuda(x, "x"); check_cuda(w, "w");
   check_dtype(x, at::kBFloat16, "x"); check_dtype(w, at::kBFloat16, "w");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "x [N,H,W,C], w [K,R,S,C]");
@@ -470,14 +429,12 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, bo
   if (stats) TORCH_CHECK(stats->numel() == (long)k8s_amd::kConvStatReplicas * 2 * K &&
                              stats->scalar_type() == at::kFloat && stats->is_contiguous(),
                          "stats must be zeroed fp32 [conv_stat_replicas, 2, K]");
-  BnbHolder bb = parse_bnb(bnb, bnb_relu_x, (long)N * Ho * Wo, K);
-  TORCH_CHECK(!bb.on || (!out_f32 && !stats), "the BN-backward epilogue needs a bf16 output and no fwd stats");
   const float* xf = xform_ptr(xform, C);
-  if (xf) TORCH_CHECK(C % 64 == 0 && !out_f32 && !bias && act == 0 && !bb.on,
+  if (xf) TORCH_CHECK(C % 64 == 0 && !out_f32 && !bias && act == 0,
                       "normalize-on-load convolution: C % 64 == 0, bf16 output, no bias / activation");
   k8s_amd::launch_conv_fwd(cbf(x), cbf(w), y.data_ptr(), out_f32, N, H, W, C, K, R, S, (int)stride, (int)pad,
                            (int)dil, Ho, Wo, bias ? bias->data_ptr<float>() : nullptr, (int)act, 0,
-                           stats ? f32(*stats) : nullptr, cur_stream(), bb.on ? &bb.e : nullptr, nullptr, xf);
+                           stats ? f32(*stats) : nullptr, cur_stream(), nullptr, xf);
   return y;
 }
 
@@ -501,7 +458,7 @@ void conv_fwd_subgrid(Tensor x, Tensor w, int64_t pad, int64_t Hs, int64_t Ws, T
               "sub-grid exceeds the output image");
   k8s_amd::SubGrid sg{OH, OW, (int)stride, (int)a, (int)b};
   k8s_amd::launch_conv_fwd(cbf(x), cbf(w), out.data_ptr(), false, N, H, W, C, K, R, S, 1, (int)pad, 1, (int)Hs,
-                           (int)Ws, nullptr, 0, accumulate ? 1 : 0, nullptr, cur_stream(), nullptr, &sg);
+                           (int)Ws, nullptr, 0, accumulate ? 1 : 0, nullptr, cur_stream(), &sg);
 }
 
 // dw[K,R,S,C] fp32 (+)= dy^T . im2col(x)
@@ -895,7 +852,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("want_mask") = false);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("mean"), py::arg("invstd"),
         py::arg("gamma"), py::arg("beta"), py::arg("relu_x"), py::arg("dgamma"), py::arg("dbeta"), py::arg("want_dres"),
-        py::arg("reps") = py::none(), py::arg("mask") = py::none());
+        py::arg("mask") = py::none());
   m.def("bn_fwd_from_sums", &bn_fwd_from_sums, py::arg("x"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
         py::arg("sums"), py::arg("run_mean"), py::arg("run_var"), py::arg("momentum"), py::arg("eps"),
         py::arg("relu"), py::arg("want_mask") = false);
@@ -907,7 +864,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_stream_eligible", &k8s_amd::wgrad_stream_eligible, "tall-K weight-gradient kernel takes this shape");
   m.def("gemm", &gemm, py::arg("a"), py::arg("a_kmajor"), py::arg("b"), py::arg("b_kmajor"), py::arg("out"),
         py::arg("out_f32"), py::arg("bias"), py::arg("act"), py::arg("pre"), py::arg("accumulate"), py::arg("alpha"),
-        py::arg("splits"), py::arg("bnb") = py::none(), py::arg("bnb_relu_x") = py::none(),
+        py::arg("splits"),
         py::arg("add_src") = py::none(), py::arg("add_mask") = py::none(), py::arg("xform_b") = py::none(),
         py::arg("xform_c") = 0);
   m.def("bn_finalize", &bn_finalize, py::arg("sums"), py::arg("gamma"), py::arg("beta"), py::arg("run_mean"),
@@ -922,8 +879,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("relu_bwd", &relu_bwd);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none());
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
-        py::arg("out_f32"), py::arg("bias"), py::arg("act"), py::arg("stats"), py::arg("bnb") = py::none(),
-        py::arg("bnb_relu_x") = py::none(), py::arg("xform") = py::none());
+        py::arg("out_f32"), py::arg("bias"), py::arg("act"), py::arg("stats"),
+        py::arg("xform") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
         py::arg("dil"), py::arg("splits"), py::arg("accumulate"), py::arg("xform") = py::none());
   m.def("conv_fwd_subgrid", &conv_fwd_subgrid, py::arg("x"), py::arg("w"), py::arg("pad"), py::arg("Hs"),

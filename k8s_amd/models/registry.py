@@ -38,7 +38,7 @@ MODEL_OPTIMIZER = {"resnet50": "sgd", "resnet_tiny": "sgd", "bert_base": "adam",
 
 def build(name: str, device, batch: int, seq: Optional[int] = None, image: Optional[int] = None,
           seed: int = 0, grad_dtype=torch.float32, fixed_batch: bool = True, pad_to: int = 64,
-          data_seed: Optional[int] = None) -> Workload:
+          data_seed: Optional[int] = None, mlm_every_token: bool = False) -> Workload:
     """Construct ``name`` on ``device`` with per-rank ``batch``. ``fixed_batch`` reuses one synthetic batch
     (what a throughput benchmark wants); otherwise every step draws a new one."""
     device = torch.device(device)
@@ -79,6 +79,10 @@ def build(name: str, device, batch: int, seq: Optional[int] = None, image: Optio
         from k8s_amd.models import bert as M
 
         cfg = M.BERT_BASE if name == "bert_base" else M.BERT_TINY
+        if mlm_every_token:  # the MLM head on every token (dense labels), like HF BertForPreTraining
+            import dataclasses
+
+            cfg = dataclasses.replace(cfg, max_predictions=0)
         seq = seq or (128 if name == "bert_base" else 32)
         model = M.BertForPreTraining(store, cfg).finalize(device, grad_dtype=grad_dtype, seed=seed, pad_to=pad_to)
 

@@ -31,13 +31,13 @@ class BN(nn.Module):
         self.register_buffer("running_var", torch.ones(c))
         self.momentum, self.eps = 0.1, 1e-5
 
-    def forward(self, x, residual=None, relu=True, res_link=None, bwd_link=None, dy_link=None):
+    def forward(self, x, residual=None, relu=True, res_link=None, dy_link=None):
         sums = None
         if isinstance(x, tuple):  # (conv output, fused statistics)
             x, sums = x
         return K.batch_norm_act(x, self.gamma, self.beta, self.running_mean, self.running_var, residual, relu,
                                 self.training, self.momentum, self.eps, sums=sums, res_link=res_link,
-                                bwd_link=bwd_link, dy_link=dy_link)
+                                dy_link=dy_link)
 
 
 class Conv(nn.Module):
@@ -46,10 +46,9 @@ class Conv(nn.Module):
         self.w = store.new(name + ".weight", (cout, k, k, cin), init_kaiming_normal(cin * k * k))
         self.stride, self.pad = stride, k // 2
 
-    def forward(self, x, grad_link=None, bn_link=None):
+    def forward(self, x, grad_link=None):
         # BN statistics are accumulated in the conv epilogue (returned alongside y)
-        return K.conv2d_nhwc(x, self.w, self.stride, self.pad, with_stats=True, grad_link=grad_link,
-                             bn_link=bn_link)
+        return K.conv2d_nhwc(x, self.w, self.stride, self.pad, with_stats=True, grad_link=grad_link)
 
 
 class Bottleneck(nn.Module):
@@ -69,10 +68,7 @@ class Bottleneck(nn.Module):
             self.down = Conv(store, name + ".downsample.0", cin, cout, 1, stride)
             self.down_bn = BN(store, name + ".downsample.1", cout)
 
-    def forward(self, x, in_link=None):
-        """Returns (out, link for the BN that produced out). ``in_link``: the BatchNorm that produced x (the
-        previous block's bn3); in an identity block conv1's dgrad output is x's complete gradient, so that
-        epilogue also reduces the previous bn3's backward statistics."""
+    def forward(self, x):
         idn = x
         identity = self.down is None and x.requires_grad
         # identity block: x's two gradient contributions (residual via bn3, main path via conv1) are summed
@@ -81,7 +77,6 @@ class Bottleneck(nn.Module):
         # downsample block: x feeds conv1 and the downsample conv; their two dgrads are summed in the
         # epilogue of whichever runs second (shared link) instead of by autograd's separate add
         dlink = K.GradLink(shared=True) if (self.down is not None and x.requires_grad) else None
-        l1, l2, l3 = K.BnBwdLink(), K.BnBwdLink(), K.BnBwdLink()
         # downsample block: bn3's ReLU mask is applied by the downsample BN's backward as it reads dy. The branch is
         # built FIRST so autograd (highest sequence number first) runs its backward LAST: the stride-2 1x1 dgrad
         # then accumulates onto conv1's dx (shared GradLink) instead of zero-filling the 3 parities it never writes
@@ -89,18 +84,18 @@ class Bottleneck(nn.Module):
         if self.down is not None:
             mlink = K.MaskLink()
             idn = self.down_bn(self.down(x, grad_link=dlink), relu=False, dy_link=mlink)
-        t = self.conv1(x, grad_link=link or dlink, bn_link=in_link if identity else None)
+        t = self.conv1(x, grad_link=link or dlink)
         # bn1 / bn2 + ReLU: normalised on load by the consuming convolution (ops.nn.bn_relu_conv, no apply pass)
         # or applied by the BN kernel; ops.nn.BN_ONLOAD picks which
         if K.BN_ONLOAD == "all":
             t = K.bn_relu_conv(t, self.bn1, self.conv2)
         else:
-            t = self.conv2(self.bn1(t, bwd_link=l1), bn_link=l1)
+            t = self.conv2(self.bn1(t))
         if K.BN_ONLOAD in ("all", "1x1"):
             t = K.bn_relu_conv(t, self.bn2, self.conv3)
         else:
-            t = self.conv3(self.bn2(t, bwd_link=l2), bn_link=l2)
-        return self.bn3(t, residual=idn, relu=True, res_link=link or mlink, bwd_link=l3), l3
+            t = self.conv3(self.bn2(t))
+        return self.bn3(t, residual=idn, relu=True, res_link=link or mlink)
 
 
 class ResNet(nn.Module):
@@ -155,9 +150,8 @@ class ResNet(nn.Module):
         else:
             y = self.bn1(self.conv1(x))
         y = K.max_pool_nhwc(y, 3, 2, 1)
-        link = None
         for b in self.blocks:
-            y, link = b(y, link)
+            y = b(y)
         y = K.global_avg_pool_nhwc(y)
         return K.linear(y, self.fc_w, self.fc_b)
 

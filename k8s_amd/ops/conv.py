@@ -33,17 +33,9 @@ from k8s_amd.ops._ext import load as _load
 
 import os
 
-# BatchNorm-backward statistics in the dgrad epilogue (ops.nn.BnBwdLink): the lean (LDS-staged) epilogue's
-# copy-out pass reduces (sum g*m, sum g*m*xhat) from the gradient it stores and the BN input tile, which is
-# DMA'd into LDS during the K loop; this replaces the BN backward's separate reduction pass over (dy, x). Off by
-# default: measured on MI355X (ResNet-50 b1024, scripts/gpurun/prof_ab.sh) it removes 6.1 ms/step of reduction
-# passes but adds 9.0 ms/step to the dgrads -- ~10 VALU per element on the critical path of the short-K
-# products (the single-buffer 1x1 dgrads run 2.3x slower) -- 10.61k vs 11.00k img/s. K8S_AMD_BN_LINK=1 turns
-# it on.
-BN_LINK = os.environ.get("K8S_AMD_BN_LINK", "0") == "1"
-# ... or only for dgrads whose reduction (R*S*K) is at least this long, where the epilogue's extra work is small
-# next to the K loop (K8S_AMD_BN_LINK_MIN_K; 0 = off)
-BN_LINK_MIN_K = int(os.environ.get("K8S_AMD_BN_LINK_MIN_K", "0"))
+# (Round 2 built a BatchNorm-backward statistics epilogue for the data gradients -- the BN backward's reduction
+# pass computed in the dgrad that produces its input; it measured a net loss twice, 10.61k vs 11.00k img/s in round 2
+# and 12.02k vs 12.20k with only the long-K dgrads in round 3 (scripts/gpurun/env_ab.sh), and was removed.)
 
 STATS = {"hip_fwd": 0, "aten_fwd": 0, "hip_wgrad": 0, "aten_wgrad": 0, "hip_dgrad": 0, "aten_dgrad": 0}
 
@@ -119,31 +111,27 @@ def _wgrad_hip(C_, gy, x, out, stride, padding, acc, xform=None):
         C_.conv_wgrad(x, gy, out, stride, padding, 1, 0, acc, xform=xform)
 
 
-def _dgrad_hip(C_, gy, w, padding, addend=None, bnb=None):
+def _dgrad_hip(C_, gy, w, padding, addend=None):
     """dx on our kernels; with ``addend`` (bf16, shape of dx) a 1x1 dgrad accumulates onto it in the GEMM
-    epilogue and returns it (the fused residual-gradient add). ``bnb`` = (list, relu_x) from
-    BnBwdLink.epilogue_args: the epilogue also reduces the BN backward's statistics of dx."""
+    epilogue and returns it (the fused residual-gradient add)."""
     K, R, S, C = w.shape
-    bl, brx = bnb if bnb is not None else (None, None)
     masked = addend is not None and not torch.is_tensor(addend)  # nn.MaskedGrad: (dy, packed ReLU mask)
     if R == 1 and S == 1 and padding == 0:
         N, H, W_, _ = gy.shape
         if masked:  # the epilogue reads dy and the mask bits itself: no materialised residual gradient
             out = torch.empty(N, H, W_, C, device=gy.device, dtype=gy.dtype)
             C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, out.view(-1, C), False, None, 0, None, True,
-                    1.0, 1, bl, brx, addend.dy.view(-1, C), addend.mask)
+                    1.0, 1, add_src=addend.dy.view(-1, C), add_mask=addend.mask)
             return out
         if addend is not None:
             C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, addend.view(-1, C), False, None, 0, None, True,
-                    1.0, 1, bl, brx)
+                    1.0, 1)
             return addend
         return C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, None, False, None, 0, None, False, 1.0,
-                       1, bl, brx).reshape(N, H, W_, C)
+                       1).reshape(N, H, W_, C)
     if masked:
         addend = addend.materialize()
-    if addend is not None:  # (no 3x3 consumer needs both; keep the statistics exact: reduce after the add)
-        bl = None
-    dx = C_.conv_fwd(gy, C_.conv_dgrad_wtrans(w), 1, R - 1 - padding, 1, False, None, 0, None, bl, brx)
+    dx = C_.conv_fwd(gy, C_.conv_dgrad_wtrans(w), 1, R - 1 - padding, 1, False, None, 0, None)
     return dx if addend is None else dx.add_(addend)
 
 
@@ -201,7 +189,7 @@ def _dgrad_strided_hip(C_, gy, w, stride, padding, H, W, addend=None):
     return dx
 
 
-def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, bn_link=None, xform=None):
+def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, xform=None):
     """Returns dx (+ ``addend``, e.g. the residual branch's gradient of the same tensor, fused into the
     dgrad epilogue where our kernel runs) or None; deposits dw into ``p``'s flat gradient slot. ``xform``: the
     convolution's input is relu(bn(x)) normalised on load (see ``_wgrad_hip``); dx is then the gradient w.r.t.
@@ -231,11 +219,7 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, bn_link=No
     if need_dx:
         if hip and stride == 1 and K % 64 == 0 and C % 8 == 0:
             STATS["hip_dgrad"] += 1
-            bnb = None
-            link_on = BN_LINK or (BN_LINK_MIN_K > 0 and R * S * K >= BN_LINK_MIN_K)
-            if link_on and bn_link is not None and p is not None and (R == 1 or addend is None):
-                bnb = bn_link.epilogue_args(p.store, gy.device)
-            dx = _dgrad_hip(C_, gy, w, padding, addend, bnb)
+            dx = _dgrad_hip(C_, gy, w, padding, addend)
         elif hip and strided_dgrad_ok(gy, w, stride, padding):
             STATS["hip_dgrad"] += 1
             dx = _dgrad_strided_hip(C_, gy, w, stride, padding, x.shape[1], x.shape[2], addend)

@@ -98,28 +98,9 @@ class MaskLink:
         self.mask = None
 
 
-class BnBwdLink:
-    """Lets the kernel that produces a BatchNorm's output gradient (the dgrad of the conv that consumed the BN
-    output) also accumulate the BN backward's two channel reductions in its epilogue; the BN backward then
-    runs only the apply pass. The BN forward fills in what the epilogue needs; ``reps`` is set by the
-    producing kernel (left None when the vendor path ran, and the BN backward reduces itself)."""
-    __slots__ = ("x", "mask", "mean", "invstd", "gamma", "beta", "relu_x", "reps")
-
-    def __init__(self):
-        self.x = self.mask = self.mean = self.invstd = self.gamma = self.beta = self.reps = None
-        self.relu_x = False
-
-    def epilogue_args(self, store, device):
-        """(bnb list for the kernel binding, relu_x), allocating the zeroed replica buffer into ``reps``."""
-        C = self.x.shape[-1]
-        self.reps = _zero_scratch(store, device, _C().conv_stat_replicas * 2 * C).view(_C().conv_stat_replicas, 2, C)
-        mask = self.mask if self.mask is not None else torch.empty(0, device=device, dtype=torch.uint8)
-        return [self.reps, self.x, mask, self.mean, self.invstd, self.gamma, self.beta], self.relu_x
-
-
 class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, anchor, p, stride, padding, with_stats, link=None, bn_link=None):
+    def forward(ctx, x, anchor, p, stride, padding, with_stats, link=None):
         impl = _conv_impl()
         w = p.weight if x.dtype == p.weight.dtype else p.master.to(x.dtype)
         sums = None
@@ -128,7 +109,7 @@ class _Conv2dNHWC(torch.autograd.Function):
                 _C().conv_stat_replicas, 2, w.shape[0])
         y = impl.conv_fwd(x, w, stride, padding, sums)
         ctx.save_for_backward(x)
-        ctx.p, ctx.stride, ctx.padding, ctx.link, ctx.bn_link = p, stride, padding, link, bn_link
+        ctx.p, ctx.stride, ctx.padding, ctx.link = p, stride, padding, link
         ctx.x_requires_grad = x.requires_grad
         if sums is not None:
             ctx.mark_non_differentiable(sums)
@@ -149,23 +130,20 @@ class _Conv2dNHWC(torch.autograd.Function):
             addend, ctx.link.grad = ctx.link.grad, None
             if addend is None and ctx.link.shared and ctx.x_requires_grad:  # first of the two readers of x
                 ctx.link.grad = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, True, p)
-                return None, None, None, None, None, None, None, None
-        bn_link = ctx.bn_link if (ctx.bn_link is not None and ctx.bn_link.x is not None) else None
-        dx = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, ctx.x_requires_grad, p, addend=addend, bn_link=bn_link)
-        return dx, None, None, None, None, None, None, None
+                return None, None, None, None, None, None, None
+        dx = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, ctx.x_requires_grad, p, addend=addend)
+        return dx, None, None, None, None, None, None
 
 
 def conv2d_nhwc(x: torch.Tensor, p, stride: int = 1, padding: int = 0, with_stats: bool = False,
-                grad_link: "GradLink" = None, bn_link: "BnBwdLink" = None):
+                grad_link: "GradLink" = None):
     """NHWC convolution with KRSC weight ``p`` (no bias).
 
     With ``with_stats`` returns ``(y, sums)``: ``sums`` = fp32 [2, K] per-channel sum / sum of squares of y
     accumulated in the conv epilogue (None when the layer runs on the fallback path) -- the following
     ``batch_norm_act(..., sums=sums)`` then needs no statistics pass. ``grad_link``: a gradient for x
-    deposited there by a later-backward node (``batch_norm_act(res_link=...)``) is added to dx in the dgrad.
-    ``bn_link``: x is the output of that BatchNorm and dx its complete gradient -- the dgrad epilogue also
-    computes the BN backward's reductions."""
-    y, sums = _Conv2dNHWC.apply(x, p.store.anchor, p, stride, padding, with_stats, grad_link, bn_link)
+    deposited there by a later-backward node (``batch_norm_act(res_link=...)``) is added to dx in the dgrad."""
+    y, sums = _Conv2dNHWC.apply(x, p.store.anchor, p, stride, padding, with_stats, grad_link)
     return (y, sums) if with_stats else y
 
 
@@ -223,7 +201,7 @@ def stem_s2d_input(images, pad: int = 3):
 class _BnAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu, sums=None,
-                res_link=None, bwd_link=None, dy_link=None):
+                res_link=None, dy_link=None):
         x = x.contiguous()
         if res is not None:
             res = res.contiguous()
@@ -248,11 +226,6 @@ class _BnAct(torch.autograd.Function):
         ctx.pg, ctx.pb, ctx.has_res, ctx.res_link = pg, pb, res is not None, res_link
         ctx.relu_x = relu and not keep_y and mask is None
         ctx.dy_link = dy_link if (dy_link is not None and not relu and res is None) else None
-        ctx.bwd_link = None
-        if bwd_link is not None and _gpu(x) and training:
-            bwd_link.x, bwd_link.mask, bwd_link.mean, bwd_link.invstd = x, mask, mean, invstd
-            bwd_link.gamma, bwd_link.beta, bwd_link.relu_x = pg.master, pb.master, ctx.relu_x
-            ctx.bwd_link = bwd_link
         return y
 
     @staticmethod
@@ -268,15 +241,11 @@ class _BnAct(torch.autograd.Function):
             sg, sb = store.slot_for_write(pg), store.slot_for_write(pb)
             dg = sg if sg is not None else torch.empty(pg.shape, device=x.device, dtype=torch.float32)
             db = sb if sb is not None else torch.empty(pb.shape, device=x.device, dtype=torch.float32)
-            reps = None
-            if ctx.bwd_link is not None:
-                reps, ctx.bwd_link.reps = ctx.bwd_link.reps, None
-                ctx.bwd_link.x = ctx.bwd_link.mask = None  # drop the extra references to the saved activations
             # residual gradient for a linked consumer: (dy, mask) instead of a written dres tensor
             handoff = (isinstance(ctx.res_link, GradLink) and ctx.has_res and mask is not None and
                        MASKED_RES_GRAD)
             dx, dres = _C().bn_bwd(dy, x, y, mean, invstd, pg.master, pb.master, ctx.relu_x, dg, db,
-                                   ctx.has_res and not (handoff or mask_out), reps, mask)
+                                   ctx.has_res and not (handoff or mask_out), mask)
             if handoff:
                 dres = MaskedGrad(dy, mask)
             elif mask_out:  # the producing plain BN masks dy itself (MaskLink)
@@ -297,7 +266,7 @@ class _BnAct(torch.autograd.Function):
         if ctx.has_res and isinstance(ctx.res_link, GradLink):  # hand dres to the node that adds it in a kernel
             ctx.res_link.grad, dres = dres, None
         return (dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None, None,
-                None, None)
+                None)
 
 
 # Which BatchNorm + ReLU outputs of a ResNet bottleneck are normalised on load by the convolution that consumes them
@@ -351,14 +320,9 @@ class _BnReluConv(torch.autograd.Function):
         pg, pb, pw = ctx.pg, ctx.pb, ctx.pw
         impl = _conv_impl()
         gy = gy.contiguous()
-        # the data gradient dz is the BN output's gradient: its epilogue may also reduce the BN backward's channel
-        # sums (BnBwdLink; ops/conv.py decides by the product's K), then the BN backward runs only its apply pass
-        link = BnBwdLink()
-        link.x, link.mean, link.invstd, link.gamma, link.beta, link.relu_x = (x, mean, invstd, pg.master,
-                                                                               pb.master, True)
-        dz = impl.conv_bwd(gy, x, pw.weight, ctx.stride, ctx.padding, True, pw, xform=params, bn_link=link)
+        dz = impl.conv_bwd(gy, x, pw.weight, ctx.stride, ctx.padding, True, pw, xform=params)
         dg, db, finish = _bn_param_grads(pg.store, pg, pb, x.device)
-        dx, _ = _C().bn_bwd(dz, x, None, mean, invstd, pg.master, pb.master, True, dg, db, False, link.reps)
+        dx, _ = _C().bn_bwd(dz, x, None, mean, invstd, pg.master, pb.master, True, dg, db, False)
         finish()
         return (dx if ctx.x_requires_grad else None,) + (None,) * 11
 
@@ -377,16 +341,15 @@ def bn_relu_conv(t, bn, conv):
 
 
 def batch_norm_act(x, pg, pb, run_mean, run_var, residual=None, relu=True, training=True, momentum=0.1,
-                   eps=1e-5, sums=None, res_link=None, bwd_link=None, dy_link=None):
+                   eps=1e-5, sums=None, res_link=None, dy_link=None):
     """y = act(BN(x) + residual) over the last (channel) dim of an NHWC tensor.
 
     ``sums`` (fp32 [2, C] from ``conv2d_nhwc(..., with_stats=True)``) skips the statistics pass.
     ``res_link``: the residual's gradient is handed to that GradLink (and NOT returned to autograd); the
     node consuming the link must add it (``conv2d_nhwc(..., grad_link=link)`` on the same tensor).
-    ``bwd_link``: a BnBwdLink handed to the consumer of y (``conv2d_nhwc(y, ..., bn_link=link)``).
     ``res_link`` may also be a MaskLink whose ``dy_link`` end is the plain BN that produced ``residual``."""
     return _BnAct.apply(x, residual, pg.store.anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu,
-                        sums, res_link, bwd_link, dy_link)
+                        sums, res_link, dy_link)
 
 
 # =========================================================================== layernorm / rmsnorm

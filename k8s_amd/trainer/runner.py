@@ -74,6 +74,9 @@ def parse(argv=None):
                          "Adam with world > 1 (the optimizer is ~19%% of a Llama-3-8B step), off for SGD (ResNet's "
                          "update is 0.1%% of the step and its all-gather would be exposed)")
     ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
+    ap.add_argument("--mlm-head", default="gathered", choices=["gathered", "every-token"],
+                    help="BERT: MLM head on the masked-position slots (the original pretraining data format) or on "
+                         "every token (HF BertForPreTraining's layout; same loss and gradients, more head FLOPs)")
     ap.add_argument("--logdir", default=os.environ.get("K8S_AMD_LOGDIR", ""))
     ap.add_argument("--ckpt-dir", default=os.environ.get("K8S_AMD_CKPT_DIR", ""))
     ap.add_argument("--ckpt-every", type=int, default=0)
@@ -306,7 +309,8 @@ def train(a) -> int:
 
     # the sharded parameter service needs the flat buffers divisible into world equal 64-aligned shards
     w = build(a.model, dev, batch, seq=a.seq, image=a.image, seed=a.seed, fixed_batch=not a.fresh_batches,
-              pad_to=world * ALIGN if sharded else ALIGN, data_seed=a.seed * 7919 + rank)
+              pad_to=world * ALIGN if sharded else ALIGN, data_seed=a.seed * 7919 + rank,
+              mlm_every_token=a.mlm_head == "every-token")
     lr = a.lr if a.lr is not None else w.lr
     if opt_name == "sgd":
         wd = 5e-5 if a.weight_decay is None else a.weight_decay

@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
-from k8s_amd.ops import autotune  # noqa: E402
+from k8s_amd.utils.timing import time_ms  # noqa: E402
 from k8s_amd.ops._ext import load  # noqa: E402
 
 C = load()
@@ -19,7 +19,7 @@ dev = torch.device("cuda")
 
 
 def t(fn):
-    return autotune._time(fn, reps=7)
+    return time_ms(fn, reps=7)
 
 
 GEMMS = [("bert_qkv", 8192, 2304, 768), ("bert_ffn1", 8192, 3072, 768), ("bert_ffn2", 8192, 768, 3072),

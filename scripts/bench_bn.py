@@ -50,10 +50,10 @@ for M, C in SHAPES:
         out[name + "_GBs"] = round(nb * (2 if r is None else 3) / t / 1e6)
     y, mean, invstd = C_.bn_fwd_from_sums(x, res, g, b, sums, rm, rv, 0.1, 1e-5, True)
     dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
-    t = timeit(lambda: C_.bn_bwd(dy, x, None, mean, invstd, g, b, True, dg, db, False, None))
+    t = timeit(lambda: C_.bn_bwd(dy, x, None, mean, invstd, g, b, True, dg, db, False))
     out["bwd_relux_us"] = round(t * 1e3, 1)
     out["bwd_relux_GBs"] = round(nb * 5 / t / 1e6)  # reduce: dy, x; apply: dy, x, dx
-    t = timeit(lambda: C_.bn_bwd(dy, x, y, mean, invstd, g, b, False, dg, db, True, None))
+    t = timeit(lambda: C_.bn_bwd(dy, x, y, mean, invstd, g, b, False, dg, db, True))
     out["bwd_res_us"] = round(t * 1e3, 1)
     out["bwd_res_GBs"] = round(nb * 8 / t / 1e6)  # reduce: dy, x, y; apply: dy, x, y, dx, dres
     print(json.dumps(out), flush=True)

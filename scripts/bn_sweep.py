@@ -53,10 +53,9 @@ def child():
         t = timed(lambda: C_.bn_fwd_from_sums(x, r, g, b, sums, rm, rv, 0.1, 1e-5, True, res))
         nb = M * C * (4 + (2.125 if res else 0))
         out[name + ".fwd"] = round(nb / t / 1e9, 2)
-        reps = torch.zeros(C_.conv_stat_replicas, 2, C, device=dev)
         dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
-        t = timed(lambda: C_.bn_bwd(y, x, None, mean, invstd, g, b, not res, dg, db, res, reps, mask))
-        nb = M * C * (6 + (2.125 if res else 0))
+        t = timed(lambda: C_.bn_bwd(y, x, None, mean, invstd, g, b, not res, dg, db, res, mask))
+        nb = M * C * (10 + (2.125 if res else 0))  # reduce reads dy, x; apply reads dy, x, writes dx (+ dres)
         out[name + ".bwd"] = round(nb / t / 1e9, 2)
         del x, r, y
         torch.cuda.empty_cache()

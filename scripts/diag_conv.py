@@ -12,7 +12,7 @@ sys.path.insert(0, os.environ.get("K8S_AMD_ROOT") or os.path.dirname(os.path.dir
 import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
-from k8s_amd.ops import autotune  # noqa: E402
+from k8s_amd.utils.timing import time_ms  # noqa: E402
 from k8s_amd.ops import conv  # noqa: E402
 from k8s_amd.ops._ext import load  # noqa: E402
 
@@ -40,7 +40,7 @@ for (N, H, C, K, R, s, p) in SHAPES:
     res = {}
     for name, fn in (("hip", hip), ("aten", aten)):
         try:
-            res[name] = autotune._time(fn, reps=5)
+            res[name] = time_ms(fn, reps=5)
         except Exception as e:  # noqa: BLE001
             res[name] = "ERR " + repr(e)[:300]
             traceback.print_exc()

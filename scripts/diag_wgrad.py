@@ -12,7 +12,8 @@ sys.path.insert(0, os.environ.get("K8S_AMD_ROOT") or os.path.dirname(os.path.dir
 
 import torch  # noqa: E402
 
-from k8s_amd.ops import autotune, conv  # noqa: E402
+from k8s_amd.ops import conv  # noqa: E402
+from k8s_amd.utils.timing import time_ms  # noqa: E402
 from k8s_amd.ops._ext import load  # noqa: E402
 
 C_ = load()
@@ -29,8 +30,8 @@ for (N, H, C, K, R, s, p) in WGRAD:
     Ho = (H + 2 * p - R) // s + 1
     gy = torch.randn(N, Ho, Ho, K, device=dev, dtype=torch.bfloat16)
     out = torch.empty(K, R, R, C, device=dev, dtype=torch.float32)
-    t_hip = autotune._time(lambda: conv._wgrad_hip(C_, gy, x, out, s, p, False), reps=5)
-    t_aten = autotune._time(lambda: conv._aten_bwd(gy, x, w, s, p, False, True), reps=5)
+    t_hip = time_ms(lambda: conv._wgrad_hip(C_, gy, x, out, s, p, False), reps=5)
+    t_aten = time_ms(lambda: conv._aten_bwd(gy, x, w, s, p, False, True), reps=5)
     conv._wgrad_hip(C_, gy, x, out, s, p, False)
     ref = conv._aten_bwd(gy, x, w, s, p, False, True)[1].float()
     err = ((out - ref).abs().max() / ref.abs().max()).item()
@@ -46,8 +47,8 @@ for (N, H, C, K, R, s, p) in DGRAD_S2:
     w = torch.randn(K, R, R, C, device=dev, dtype=torch.bfloat16) * 0.05
     Ho = (H + 2 * p - R) // s + 1
     gy = torch.randn(N, Ho, Ho, K, device=dev, dtype=torch.bfloat16)
-    t_aten = autotune._time(lambda: conv._aten_bwd(gy, x, w, s, p, True, False), reps=5)
-    t_hip = autotune._time(lambda: conv._dgrad_strided_hip(C_, gy, w, s, p, H, H), reps=5)
+    t_aten = time_ms(lambda: conv._aten_bwd(gy, x, w, s, p, True, False), reps=5)
+    t_hip = time_ms(lambda: conv._dgrad_strided_hip(C_, gy, w, s, p, H, H), reps=5)
     ref = conv._aten_bwd(gy, x, w, s, p, True, False)[0].float()
     err = ((conv._dgrad_strided_hip(C_, gy, w, s, p, H, H).float() - ref).norm() / ref.norm()).item()
     fl = 2.0 * N * Ho * Ho * K * C * R * R

@@ -119,7 +119,7 @@ def main():
             mask = out[3] if mask_out else None
             dg, db = torch.empty(K, device=dev), torch.empty(K, device=dev)
             relu_x = relu and not mask_out
-            t = timed(lambda: C_.bn_bwd(gy, y, None, mean, invstd, g, b, relu_x, dg, db, bnk == "res", None, mask),
+            t = timed(lambda: C_.bn_bwd(gy, y, None, mean, invstd, g, b, relu_x, dg, db, bnk == "res", mask),
                       a.reps)
             # reduce: dy + x (+ mask); apply: dy + x (+ mask) -> dx (+ dres)
             nbytes = elems * (4 + 4 + 2 + (2 if bnk == "res" else 0) + (0.25 if mask_out else 0))

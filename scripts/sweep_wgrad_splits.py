@@ -11,7 +11,7 @@ sys.path.insert(0, os.environ.get("K8S_AMD_ROOT") or os.path.dirname(os.path.dir
 
 import torch  # noqa: E402
 
-from k8s_amd.ops import autotune  # noqa: E402
+from k8s_amd.utils.timing import time_ms  # noqa: E402
 from k8s_amd.ops._ext import load  # noqa: E402
 
 C_ = load()
@@ -37,12 +37,12 @@ for (N, H, C, K, R, s, p) in SHAPES:
                                  None, False, 1.0, sp)
         else:
             fn = lambda: C_.conv_wgrad(x, gy, out, s, p, 1, sp, False)  # noqa
-        res[sp] = round(autotune._time(fn, reps=5) * 1e3, 1)
+        res[sp] = round(time_ms(fn, reps=5) * 1e3, 1)
     if R == 1 and s == 1:
         C_.gemm(gy.reshape(-1, K), False, x.reshape(-1, C), False, out.view(K, C), True, None, 0, None, False, 1.0, 0)
     else:
         C_.conv_wgrad(x, gy, out, s, p, 1, 0, False)
-    t_auto = round(autotune._time(
+    t_auto = round(time_ms(
         (lambda: C_.gemm(gy.reshape(-1, K), False, x.reshape(-1, C), False, out.view(K, C), True, None, 0, None, False,
                          1.0, 0)) if (R == 1 and s == 1) else (lambda: C_.conv_wgrad(x, gy, out, s, p, 1, 0, False)),
         reps=5) * 1e3, 1)

@@ -199,24 +199,6 @@ def test_maxpool_nhwc(cuda, shape, ksp):
     assert _rel(x.grad, xr.grad.permute(0, 2, 3, 1)) < 1e-2
 
 
-def test_conv3x3_dgrad_bn_backward_statistics_epilogue(cuda):
-    torch.manual_seed(12)
-    N, H, W, C, K = 2, 14, 14, 64, 128
-    gy = torch.randn(N, H, W, K, device=cuda).bfloat16()
-    w = (torch.randn(K, 3, 3, C, device=cuda) * 0.05).bfloat16()
-    x = torch.randn(N, H, W, C, device=cuda).bfloat16()
-    mean, invstd = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
-    gamma, beta = torch.ones(C, device=cuda), torch.zeros(C, device=cuda)
-    reps = torch.zeros(_C().conv_stat_replicas, 2, C, device=cuda)
-    e = torch.empty(0, device=cuda, dtype=torch.bfloat16)
-    dx = _C().conv_fwd(gy, _C().conv_dgrad_wtrans(w), 1, 1, 1, False, None, 0, None,
-                       [reps, x, e, mean, invstd, gamma, beta], True)
-    m = (x.float() > 0).float()
-    ge = (dx.float() * m).reshape(-1, C)
-    assert _rel(reps.sum(0)[0], ge.sum(0)) < 1e-3
-    assert _rel(reps.sum(0)[1], (ge * x.float().reshape(-1, C)).sum(0)) < 1e-3
-
-
 # stride-2 data gradients (ResNet-50 v1.5 strided 3x3 and 1x1 downsample, the 7x7 stem; odd sizes) on the
 # parity-decomposed implicit GEMM with the sub-grid epilogue
 @pytest.mark.parametrize("N,H,C,K,R,st,pad", [(4, 56, 128, 128, 3, 2, 1), (4, 28, 256, 512, 1, 2, 0),
@@ -278,51 +260,6 @@ def test_linear_head_1000_classes_no_fallback(cuda):
     assert _rel(db, gy.float().sum(0)) < 1e-2
 
 
-def _bn_bwd_sums_ref(g, x, mean, invstd, gamma, beta, mask_bits=None, relu_x=False):
-    """(sum g*m, sum g*m*xhat) per channel in fp32 from the bf16 gradient g the kernel stored."""
-    C = x.shape[-1]
-    g, xf = g.float().reshape(-1, C), x.float().reshape(-1, C)
-    xh = (xf - mean) * invstd
-    if mask_bits is not None:
-        bits = mask_bits.reshape(-1, 1).int()
-        on = ((bits >> torch.arange(8, device=x.device).int()) & 1).reshape(-1, C).bool()
-    elif relu_x:  # the BN forward's decision: bf16(fma(x, scale, shift)) > 0, fma emulated in fp64
-        sc = gamma * invstd
-        sh = (-mean.double() * sc.double() + beta.double()).float()
-        on = (xf.double() * sc.double() + sh.double()).float().bfloat16().float() > 0
-    else:
-        on = torch.ones_like(xf, dtype=torch.bool)
-    ge = torch.where(on, g, torch.zeros_like(g))
-    return ge.sum(0), (ge * xh).sum(0)
-
-
-@pytest.mark.parametrize("mode", ["mask", "relu_x", "plain"])
-@pytest.mark.parametrize("accumulate", [False, True])
-def test_dgrad_bn_backward_epilogue(cuda, mode, accumulate):
-    """1x1 dgrad (KMajor x MNMajor GEMM) whose lean epilogue also reduces the BN backward's two channel sums."""
-    torch.manual_seed(4)
-    C_ = _C()
-    M, K, C = 3000, 128, 192
-    gy = torch.randn(M, K, device=cuda).bfloat16()
-    w = (torch.randn(K, C, device=cuda) * 0.1).bfloat16()
-    x = torch.randn(M, C, device=cuda).bfloat16()
-    mean, invstd = torch.randn(C, device=cuda) * 0.1, torch.rand(C, device=cuda) + 0.5
-    gamma, beta = torch.randn(C, device=cuda), torch.randn(C, device=cuda) * 0.1
-    mask = torch.randint(0, 256, (M * C // 8,), device=cuda, dtype=torch.uint8) if mode == "mask" else \
-        torch.empty(0, device=cuda, dtype=torch.uint8)
-    reps = torch.zeros(C_.conv_stat_replicas, 2, C, device=cuda)
-    out = torch.randn(M, C, device=cuda).bfloat16() if accumulate else None
-    base = out.clone() if accumulate else None
-    g = C_.gemm(gy, True, w, False, out, False, None, 0, None, accumulate, 1.0, 1,
-                [reps, x, mask, mean, invstd, gamma, beta], mode == "relu_x")
-    ref_g = gy.float() @ w.float() + (base.float() if accumulate else 0)
-    assert _rel(g, ref_g) < 1e-2
-    s_ref, q_ref = _bn_bwd_sums_ref(g, x, mean, invstd, gamma, beta, mask if mode == "mask" else None,
-                                    mode == "relu_x")
-    s, q = reps[:, 0].sum(0), reps[:, 1].sum(0)
-    assert _rel(s, s_ref) < 1e-4 and _rel(q, q_ref) < 1e-4
-
-
 def _unpack_bits(mask, shape):
     bits = mask.reshape(-1, 1).int()
     return ((bits >> torch.arange(8, device=mask.device).int()) & 1).reshape(shape).bool()
@@ -340,8 +277,7 @@ def test_gemm_masked_addend_epilogue(cuda, with_mask):
     dy = torch.randn(M, C, device=cuda).bfloat16()
     mask = torch.randint(0, 256, (M * C // 8,), device=cuda, dtype=torch.uint8)
     out = torch.full((M, C), 7.0, device=cuda, dtype=torch.bfloat16)  # overwritten, never read
-    C_.gemm(gy, True, w, False, out, False, None, 0, None, True, 1.0, 1, None, None, dy,
-            mask if with_mask else None)
+    C_.gemm(gy, True, w, False, out, False, None, 0, None, True, 1.0, 1, dy, mask if with_mask else None)
     on = _unpack_bits(mask, (M, C)) if with_mask else torch.ones(M, C, dtype=torch.bool, device=cuda)
     ref = gy.float() @ w.float() + torch.where(on, dy.float(), torch.zeros_like(dy.float()))
     assert _rel(out, ref) < 1e-2
@@ -351,25 +287,6 @@ def test_gemm_masked_addend_epilogue(cuda, with_mask):
         assert torch.equal(dres.float(), torch.where(on, dy.float(), torch.zeros_like(dy.float())))
         C_.gemm(gy, True, w, False, dres, False, None, 0, None, True, 1.0, 1)
         assert torch.equal(dres, out)
-
-
-def test_conv3x3_dgrad_bn_backward_epilogue(cuda):
-    """3x3 stride-1 dgrad (conv of dy with the flipped weights) with the BN-backward epilogue (relu_x)."""
-    torch.manual_seed(5)
-    C_ = _C()
-    N, H, K, C = 4, 14, 64, 128
-    gy = torch.randn(N, H, H, K, device=cuda).bfloat16()
-    w = (torch.randn(K, 3, 3, C, device=cuda) * 0.05).bfloat16()
-    x = torch.randn(N, H, H, C, device=cuda).bfloat16()
-    mean, invstd = torch.randn(C, device=cuda) * 0.1, torch.rand(C, device=cuda) + 0.5
-    gamma, beta = torch.randn(C, device=cuda), torch.randn(C, device=cuda) * 0.1
-    reps = torch.zeros(C_.conv_stat_replicas, 2, C, device=cuda)
-    dx = C_.conv_fwd(gy, C_.conv_dgrad_wtrans(w), 1, 1, 1, False, None, 0, None,
-                     [reps, x, torch.empty(0, device=cuda, dtype=torch.uint8), mean, invstd, gamma, beta], True)
-    ref = F.conv_transpose2d(gy.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, 1, 1)
-    assert _rel(dx, ref.permute(0, 2, 3, 1)) < 1e-2
-    s_ref, q_ref = _bn_bwd_sums_ref(dx, x, mean, invstd, gamma, beta, None, True)
-    assert _rel(reps[:, 0].sum(0), s_ref) < 1e-4 and _rel(reps[:, 1].sum(0), q_ref) < 1e-4
 
 
 @pytest.mark.parametrize("act", [1, 2])

@@ -224,7 +224,7 @@ def test_bn_packed_relu_mask(cuda, C, M, from_sums):
     dy = torch.randn(M, C, device=cuda).bfloat16()
     dg1, db1, dg2, db2 = (torch.empty(C, device=cuda) for _ in range(4))
     dx1, dres1 = _C().bn_bwd(dy, x, y, mean, invstd, g, b, False, dg1, db1, True)
-    dx2, dres2 = _C().bn_bwd(dy, x, None, mean, invstd, g, b, False, dg2, db2, True, None, mask)
+    dx2, dres2 = _C().bn_bwd(dy, x, None, mean, invstd, g, b, False, dg2, db2, True, mask)
     assert torch.equal(dres1, dres2)
     _close(dx2, dx1, 1e-2)
     _close(dg2, dg1, 1e-4)
