@@ -258,13 +258,25 @@ __device__ __forceinline__ void load_f8(const float* p, float (&o)[8]) {
   o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
 }
 
+// Block -> 4-KB chunk order of the flat passes (see stream_order_mode below). rev 0: address order. rev 1 / 2: the tensor as
+// 8 contiguous bands swept concurrently (consecutive blocks in different bands), each descending (1) or ascending
+// (2) -- the shape in which the XCD-remapped GEMMs write their outputs (8 row bands in parallel, ascending).
+__device__ __forceinline__ int bn_block_order(int b, int nb, int rev) {
+  if (!rev) return b;
+  const int band = b & 7, q = nb >> 3, r = nb & 7;
+  const int size = q + (band < r ? 1 : 0);
+  const int start = band < r ? band * (q + 1) : r * (q + 1) + (band - r) * q;
+  const int local = b >> 3;
+  return rev == 1 ? start + size - 1 - local : start + local;
+}
+
 // y = act(fma(x, scale, shift) [+ res]); params = [scale | shift] (fp32 [2][C]). One vector per thread.
 __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ res,
                                                               const float* __restrict__ params,
                                                               uint16_t* __restrict__ y, uint8_t* __restrict__ mask,
-                                                              int nvec, int C, FastDiv fcg, int relu) {
-  const int e = blockIdx.x * BN_THREADS + threadIdx.x;
+                                                              int nvec, int C, FastDiv fcg, int relu, int rev) {
+  const int e = bn_block_order(blockIdx.x, gridDim.x, rev) * BN_THREADS + threadIdx.x;
   if (e >= nvec) return;
   const int cgroups = C >> 3;
   const int c0 = (e - fcg.div(e) * cgroups) * 8;
@@ -316,13 +328,12 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
                                                                    const float* __restrict__ beta, int relu_x, long M,
                                                                    int C, int tpr, int rows_per_iter,
                                                                    float* __restrict__ part,
-                                                                   const uint8_t* __restrict__ mask) {
+                                                                   const uint8_t* __restrict__ mask, int rev) {
   __shared__ float sh[2][BN_THREADS][9];
   const int t = threadIdx.x;
   const int r = t / tpr, cg_local = t % tpr;
   const int cg = blockIdx.y * tpr + cg_local;
   const bool active = (r < rows_per_iter) && (cg * 8 < C);
-  const long stride = (long)gridDim.x * rows_per_iter;
   float sd[8], sx[8], mu[8], is[8], sc[8], bt[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -344,15 +355,28 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
       sx[j] += g * (xv - mu[j]) * is[j];
     }
   };
+  // rev: the rows as 8 bands (block bx sweeps band bx & 7), each visited descending -- the reverse of the
+  // producing GEMM's write order (bn_block_order)
+  long M_ = M, base = 0, nblk = gridDim.x, bx = blockIdx.x;
+  if (rev) {
+    const long bandlen = (M + 7) / 8, band = bx & 7;
+    base = band * bandlen;
+    M_ = M - base < bandlen ? M - base : bandlen;
+    if (M_ < 0) M_ = 0;
+    nblk = gridDim.x / 8;
+    bx = bx >> 3;
+  }
+  const long stride = nblk * rows_per_iter;
   if (active) {
-    long row = (long)blockIdx.x * rows_per_iter + r;
+    long row = bx * rows_per_iter + r;
     // 4 row groups per trip: every 16-B load (and mask byte) of the trip is issued before any is used
-    for (; row + 3 * stride < M; row += 4 * stride) {
+    for (; row + 3 * stride < M_; row += 4 * stride) {
       bf16x8_t g4[4], x4[4];
       uint32_t b4[4] = {0xFFu, 0xFFu, 0xFFu, 0xFFu};
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const long off = (row + u * stride) * C + cg * 8;
+        const long rw = row + u * stride;
+        const long off = (rev ? base + M_ - 1 - rw : rw) * C + cg * 8;
         g4[u] = *reinterpret_cast<const bf16x8_t*>(dy + off);
         x4[u] = *reinterpret_cast<const bf16x8_t*>(x + off);
         if constexpr (MASK) b4[u] = mask[off >> 3];
@@ -360,8 +384,8 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
 #pragma unroll
       for (int u = 0; u < 4; ++u) one(g4[u], x4[u], b4[u]);
     }
-    for (; row < M; row += stride) {
-      const long off = row * C + cg * 8;
+    for (; row < M_; row += stride) {
+      const long off = (rev ? base + M_ - 1 - row : row) * C + cg * 8;
       one(*reinterpret_cast<const bf16x8_t*>(dy + off), *reinterpret_cast<const bf16x8_t*>(x + off),
           MASK ? (uint32_t)mask[off >> 3] : 0xFFu);
     }
@@ -447,8 +471,8 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t
                                                                   const float* __restrict__ params, int relu_x,
                                                                   uint16_t* __restrict__ dx,
                                                                   uint16_t* __restrict__ dres, int nvec, int C,
-                                                                  FastDiv fcg) {
-  const int e = blockIdx.x * BN_THREADS + threadIdx.x;
+                                                                  FastDiv fcg, int rev) {
+  const int e = bn_block_order(blockIdx.x, gridDim.x, rev) * BN_THREADS + threadIdx.x;
   if (e >= nvec) return;
   const int cgroups = C >> 3;
   const int c0 = (e - fcg.div(e) * cgroups) * 8;
@@ -474,6 +498,34 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t
 }
 
 // ---------------------------------------------------------------- launchers
+// Traversal order of the streaming passes, chosen so that each pass starts where its producer stopped: the bytes
+// the producer touched last are still in the 256 MiB Infinity Cache (a line stays resident while it plus every
+// byte streamed since its last use fits, MI355X_MICROARCH.md "Infinity Cache"). The XCD-remapped GEMMs write their
+// outputs as 8 row bands in parallel, each ascending; so the passes sweep 8 bands concurrently too
+// (bn_block_order), in the direction opposite to their producer's.
+// $K8S_AMD_STREAM_ORDER: 0 = plain address order everywhere; 1 (default) = fixed BatchNorm directions (forward
+// apply descending behind its ascending conv, backward reduce descending behind its dgrad, backward apply
+// ascending behind the reduce); 2 = every streaming launch (BN passes, bf16-output GEMMs / convolutions)
+// alternates direction with the previous one (stream_dir). Measured (ResNet-50 b1024, scripts/gpurun/env_ab.sh):
+// 12.36-12.38k img/s plain, 12.61-12.64k with the fixed BatchNorm directions, 12.51-12.53k alternating everything
+// (the GEMMs' reversed tile order costs more than the producer-consumer reuse it buys).
+int stream_order_mode() {
+  static const int v = [] {
+    const char* e = getenv("K8S_AMD_STREAM_ORDER");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+static int g_stream_dir = 0;
+int stream_dir(int fixed) {
+  const int mode = stream_order_mode();
+  if (mode == 0) return 0;
+  if (mode == 1) return fixed;
+  g_stream_dir ^= 1;
+  return g_stream_dir;
+}
+int stream_dir_gemm() { return stream_order_mode() == 2 ? stream_dir(0) : 0; }
+
 static long bn_rows_per_block(long M, const BnGeom& g) {
   // ~1024 blocks in total (4 per CU: enough loads in flight to cover HBM latency), at most M / 64 row-blocks,
   // >= 4 row trips per block
@@ -493,6 +545,7 @@ static int bn_reduce_blocks(long M, const BnGeom& g) {
   long nb = 1024 / g.grid_y;
   const long groups = (M + g.rows_per_iter - 1) / g.rows_per_iter;
   if (nb > groups) nb = groups;
+  if (stream_order_mode()) nb = nb < 8 ? 8 : nb & ~7L;  // banded order: a multiple of 8 blocks (one band each)
   return (int)(nb < 1 ? 1 : nb);
 }
 
@@ -509,7 +562,8 @@ static void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float*
   const long nvec = M * C / 8;
   if (nvec >= (1L << 31)) throw std::runtime_error("BatchNorm tensor too large (>= 2^31 vectors)");
   hipLaunchKernelGGL(bn_apply_kernel, dim3(cdiv(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, x, res, params, y,
-                     mask, (int)nvec, C, make_fastdiv(C / 8), (int)relu);
+                     mask, (int)nvec, C, make_fastdiv(C / 8), (int)relu,
+                     stream_order_mode() ? (stream_dir(1) ? 1 : 2) : 0);
 }
 
 void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta, uint16_t* y,
@@ -554,7 +608,8 @@ static void launch_bn_bwd_apply(const uint16_t* dy, const uint16_t* x, const uin
   const long nvec = M * C / 8;
   if (nvec >= (1L << 31)) throw std::runtime_error("BatchNorm tensor too large (>= 2^31 vectors)");
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(cdiv(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, dy, x, mask, params,
-                     (int)relu_x, dx, dres, (int)nvec, C, make_fastdiv(C / 8));
+                     (int)relu_x, dx, dres, (int)nvec, C, make_fastdiv(C / 8),
+                     stream_order_mode() ? (stream_dir(0) ? 1 : 2) : 0);
 }
 
 void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, const float* invstd, const float* gamma,
@@ -562,12 +617,13 @@ void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, con
                    float* work, float* params, long M, int C, hipStream_t st, const uint8_t* mask) {
   BnGeom g = bn_geom(C, M);
   const int nb = bn_reduce_blocks(M, g);
+  const int rdir = stream_dir(1);
   if (mask)
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, dy, x, mean, invstd,
-                       gamma, beta, (int)relu_x, M, C, g.tpr, g.rows_per_iter, work, mask);
+                       gamma, beta, (int)relu_x, M, C, g.tpr, g.rows_per_iter, work, mask, rdir);
   else
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, dy, x, mean, invstd,
-                       gamma, beta, (int)relu_x, M, C, g.tpr, g.rows_per_iter, work, mask);
+                       gamma, beta, (int)relu_x, M, C, g.tpr, g.rows_per_iter, work, mask, rdir);
   hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, nb, C, dgamma, dbeta,
                      1.f / (float)M, mean, invstd, gamma, beta, params);
   launch_bn_bwd_apply(dy, x, mask, params, relu_x, dx, dres, M, C, st);

@@ -336,6 +336,7 @@ struct Epi {
   // 1-bit mask instead of from a materialised residual gradient.
   const uint16_t* addsrc;
   const uint8_t* addmask;
+  int rev;  // tiles of each XCD's band in descending order (stream_order_mode 2: start where the producer stopped)
 };
 constexpr int STAT_REPL = 32;
 
@@ -390,7 +391,8 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
   int wg;
   {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int local = E.rev ? q + (xcd < r ? 1 : 0) - 1 - (bid >> 3) : (bid >> 3);
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
   }
   const int group = 8 * tiles_n;
   const int first_m = (wg / group) * 8;
@@ -1037,6 +1039,7 @@ static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act,
   e.rst = e.rHo = e.rWo = e.rH = e.rW = e.ra = e.rb = 0;
   e.addsrc = nullptr;
   e.addmask = nullptr;
+  e.rev = 0;
   // $K8S_AMD_GEMM_LATE_NT (A/B knob), default off: issuing the next step's loads behind the first MFMA half sped
   // up the isolated 56x56 / 28x28 3x3 convolutions 7-12 % but the ResNet-50 step lost 1.5 % at any threshold
   // (b1024: 11.00k img/s never late, 10.84k from 8 K steps, 10.80k always; scripts/gpurun/bench_ab.sh)
@@ -1111,6 +1114,7 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
   const bool slab = splits > 1;
   Epi e = make_epi(slab ? (void*)ws : C, slab ? (long)N : ldc, c_f32, bias, act, pre, slab ? 3 : mode, alpha);
   e.slab = (long)M * N;
+  if (!c_f32) e.rev = stream_dir_gemm();  // activation-streaming products (not the fp32 weight gradients)
   if (add) {
     if (slab || mode != 1) throw std::runtime_error("a separate addend needs accumulate mode and no split-K");
     e.addsrc = add->src;
@@ -1141,6 +1145,7 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, 
   KMajor b{w, (long)RSC, K, RSC};
   Epi e = make_epi(y, K, y_f32, bias, act, nullptr, mode, 1.f);
   e.stats = stats;
+  if (!sg && !y_f32) e.rev = stream_dir_gemm();
   if (sg) {
     if (stats) throw std::runtime_error("sub-grid output takes no statistics epilogue");
     e.rst = sg->stride;

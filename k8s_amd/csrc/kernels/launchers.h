@@ -141,6 +141,12 @@ struct AttnBwdArgs {
   int B, Sq, Sk, Hq, Hkv, causal;
   float scale_log2, scale;
 };
+// Streaming-order state (batchnorm.hip): direction (0 ascending, 1 descending, as 8 concurrent bands) of the next
+// streaming launch; `fixed` is the direction used in the fixed-BatchNorm mode.
+int stream_order_mode();
+int stream_dir(int fixed);
+int stream_dir_gemm();
+
 void launch_flash_fwd(const AttnFwdArgs& a, int D, hipStream_t st);
 void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, long sos, long soh, hipStream_t st);
 
