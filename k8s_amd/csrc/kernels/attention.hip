@@ -15,6 +15,10 @@
 //                    with the SAME permutation through ds_read_b64_tr_b16 -- no register shuffle,
 //                    no LDS round trip for P.
 //   writes O (bf16) and lse2 = m + log2(l) (fp32, [B, Hq, Sq]) for the backward.
+//   (Round 3 measured two 8-wave v_mfma_f32_32x32x16_bf16 forwards against this kernel at Llama-3-8B s4096 D128:
+//   one phase per 64-key tile, register-staged K/V -- 519 TF/s causal / 829 non-causal vs 596 / 833; and a
+//   ping-pong with group B one barrier behind group A so the softmax VALU of one wave overlaps its partner's PV
+//   MFMAs -- 519 / 787 vs 667 / 842 after the masking fix below. Neither kept.)
 //
 // Backward (FA2 order, dK/dV kernel: one block = 64 keys of one KV head, looping over every query tile
 // of every query head of its GQA group, so dK/dV accumulate in VGPRs without atomics):
@@ -26,6 +30,7 @@
 //   so no fp32 atomics; delta = rowsum(dO * O) is a tiny kernel ahead of both. lse / delta rows are padded
 //   to a multiple of 64 so a query tile's 256 B of each can be staged by one global_load_lds.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "launchers.h"
@@ -169,17 +174,18 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
       for (int qs = 0; qs < 2; ++qs) {
         const int qi = q0w + qs * 16 + li;
         // max over the raw scores (scale_log2 > 0 commutes with max), the scale folded into the exponent's fma
+        if (need_mask) {  // wave-uniform; one compare per score against min(kv_end - 1, causal diagonal)
+          const int klim = a.causal ? min(kv_end - 1, qi + off) : kv_end - 1;
+#pragma unroll
+          for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[i][qs][r] = key0 + i * 16 + g * 4 + r > klim ? -INFINITY : s[i][qs][r];
+        }
         float mx = -INFINITY;
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            if (need_mask) {
-              const int key = key0 + i * 16 + g * 4 + r;
-              if (key >= kv_end || (a.causal && key > qi + off)) s[i][qs][r] = -INFINITY;
-            }
-            mx = fmaxf(mx, s[i][qs][r]);
-          }
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[i][qs][r]);
         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
         const float mn = fmaxf(m[qs], mx * a.scale_log2);
@@ -250,6 +256,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
     if (g == 0) a.lse[((long)b * a.Hq + h) * a.lse_ld + qi] = lt > 0.f ? m[qs] + log2f(lt) : INFINITY;
   }
 }
+
 
 // =============================================================================== backward
 // delta[b, h, q] = sum_d dO * O  (D/8 lanes per row, 8 elements per lane); rows of stride lse_ld
@@ -435,13 +442,14 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
 // double-buffered in LDS, S^T = K Q^T and dP^T = V dO^T recomputed (lane: query = li, keys 4g+r), and
 // dQ^T += K^T dS^T with dS^T consumed in place (permuted k) and K^T read transposed from the K tile.
 // No atomics: each block owns its queries.
-template <int D, int TILE>
-__global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dq_kernel(AttnBwdArgs a) {
+template <int D, int TILE, int QS>
+__global__ void __launch_bounds__(FA_THREADS, (QS == 2 && D * TILE >= 8192) ? 1 : 2) flash_bwd_dq_kernel(AttnBwdArgs a) {
   constexpr int ND = D / 16, NK = D / 32;
   constexpr int FB_BN = TILE;  // keys per iteration
   constexpr int NI = FB_BN / 16;
   constexpr int KT = FB_BN * D * 2;
-  constexpr int BMQ = 64;
+  constexpr int QW = 16 * QS;     // queries per wave (QS 16-query sets share every K / V / K^T fragment read)
+  constexpr int BMQ = 4 * QW;
   __shared__ __attribute__((aligned(1024))) char smem[4 * KT];  // [buf][K | V], both K-major halves
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
@@ -453,7 +461,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dq_kernel(AttnBwdArgs
   const int h = (wg / nqb) % a.Hq;
   const int b = wg / (nqb * a.Hq);
   const int hk = h / (a.Hq / a.Hkv);
-  const int q0 = qb * BMQ, q0w = q0 + wid * 16, qi = q0w + li;
+  const int q0 = qb * BMQ, q0w = q0 + wid * QW;
   const int off = a.Sk - a.Sq;
   int kv_end = a.Sk;
   if (a.kv_lens) kv_end = min(kv_end, a.kv_lens[b]);
@@ -466,24 +474,32 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dq_kernel(AttnBwdArgs
   const uint16_t* kp = a.k + (long)b * a.skb + (long)hk * a.skh;
   const uint16_t* vp = a.v + (long)b * a.svb + (long)hk * a.svh;
 
-  mfma_bf16x8 qf[NK], df[NK];
-#pragma unroll
-  for (int kk = 0; kk < NK; ++kk) {
-    bf16x8_t x = {0, 0, 0, 0, 0, 0, 0, 0}, y = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (qi < a.Sq) {
-      x = *reinterpret_cast<const bf16x8_t*>(qp + (long)qi * a.sqs + kk * 32 + g * 8);
-      y = *reinterpret_cast<const bf16x8_t*>(dop + (long)qi * a.sds + kk * 32 + g * 8);
-    }
-    qf[kk] = __builtin_bit_cast(mfma_bf16x8, x);
-    df[kk] = __builtin_bit_cast(mfma_bf16x8, y);
-  }
+  // query of set qs on this lane: q0w + 16 qs + li
+  mfma_bf16x8 qf[QS][NK], df[QS][NK];
+  float lq[QS], dq_[QS];
   const long lrow = ((long)b * a.Hq + h) * a.lse_ld;
-  const float lq = qi < a.Sq ? a.lse[lrow + qi] : INFINITY;
-  const float dq_ = qi < a.Sq ? a.delta[lrow + qi] : 0.f;
-
-  f32x4_t acc[ND];
 #pragma unroll
-  for (int i = 0; i < ND; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int qs = 0; qs < QS; ++qs) {
+    const int qi = q0w + 16 * qs + li;
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      bf16x8_t x = {0, 0, 0, 0, 0, 0, 0, 0}, y = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (qi < a.Sq) {
+        x = *reinterpret_cast<const bf16x8_t*>(qp + (long)qi * a.sqs + kk * 32 + g * 8);
+        y = *reinterpret_cast<const bf16x8_t*>(dop + (long)qi * a.sds + kk * 32 + g * 8);
+      }
+      qf[qs][kk] = __builtin_bit_cast(mfma_bf16x8, x);
+      df[qs][kk] = __builtin_bit_cast(mfma_bf16x8, y);
+    }
+    lq[qs] = qi < a.Sq ? a.lse[lrow + qi] : INFINITY;
+    dq_[qs] = qi < a.Sq ? a.delta[lrow + qi] : 0.f;
+  }
+
+  f32x4_t acc[QS][ND];
+#pragma unroll
+  for (int qs = 0; qs < QS; ++qs)
+#pragma unroll
+    for (int i = 0; i < ND; ++i) acc[qs][i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   auto stage = [&](int buf, int key0) {
     char* tk = smem + buf * 2 * KT;
@@ -506,56 +522,82 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dq_kernel(AttnBwdArgs
     if (t + 1 < ntiles) stage(cur ^ 1, key0 + FB_BN);
     const char* tk = smem + cur * 2 * KT;
     const char* tv = tk + KT;
-    if (!(a.causal && key0 > q0w + 15 + off)) {
-      f32x4_t s[NI], dp[NI];
+    if (!(a.causal && key0 > q0w + QW - 1 + off)) {
+      f32x4_t s[NI][QS], dp[NI][QS];
 #pragma unroll
-      for (int i = 0; i < NI; ++i) s[i] = dp[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int qs = 0; qs < QS; ++qs) s[i][qs] = dp[i][qs] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-          s[i] = mfma16(frag_kmajor(tk + (kk >> 1) * (FB_BN * 128), i * 16, kk & 1, lane), qf[kk], s[i]);
-          dp[i] = mfma16(frag_kmajor(tv + (kk >> 1) * (FB_BN * 128), i * 16, kk & 1, lane), df[kk], dp[i]);
+          const mfma_bf16x8 kf = frag_kmajor(tk + (kk >> 1) * (FB_BN * 128), i * 16, kk & 1, lane);
+          const mfma_bf16x8 vf = frag_kmajor(tv + (kk >> 1) * (FB_BN * 128), i * 16, kk & 1, lane);
+#pragma unroll
+          for (int qs = 0; qs < QS; ++qs) {
+            s[i][qs] = mfma16(kf, qf[qs][kk], s[i][qs]);
+            dp[i][qs] = mfma16(vf, df[qs][kk], dp[i][qs]);
+          }
         }
       }
-      const bool need_mask = (key0 + FB_BN > kv_end) || (a.causal && key0 + FB_BN - 1 > q0w + off);
+      // masked scores -> -inf before the exponent (exp2(-inf) = 0): a select per score in masked tiles only, no
+      // branch around each exponent (the per-element `ok ? exp : 0` form compiled to 72 exec-mask branches)
+      if ((key0 + FB_BN > kv_end) || (a.causal && key0 + FB_BN - 1 > q0w + off)) {
+#pragma unroll
+        for (int qs = 0; qs < QS; ++qs) {
+          const int qi = q0w + 16 * qs + li;
+          const int klim = a.causal ? min(kv_end - 1, qi + off) : kv_end - 1;
+#pragma unroll
+          for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[i][qs][r] = key0 + i * 16 + g * 4 + r > klim ? -INFINITY : s[i][qs][r];
+        }
+      }
 #pragma unroll
       for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          bool ok = true;
-          if (need_mask) {
-            const int key = key0 + i * 16 + g * 4 + r;
-            ok = key < kv_end && !(a.causal && key > qi + off);
+        for (int qs = 0; qs < QS; ++qs)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float p = fexp2(s[i][qs][r] * a.scale_log2 - lq[qs]);
+            dp[i][qs][r] = p * (dp[i][qs][r] - dq_[qs]);
           }
-          const float p = ok ? fexp2(s[i][r] * a.scale_log2 - lq) : 0.f;
-          dp[i][r] = p * (dp[i][r] - dq_);
-        }
 #pragma unroll
       for (int s2 = 0; s2 < NI / 2; ++s2) {
-        const float d0[4] = {dp[2 * s2][0], dp[2 * s2][1], dp[2 * s2][2], dp[2 * s2][3]};
-        const float d1[4] = {dp[2 * s2 + 1][0], dp[2 * s2 + 1][1], dp[2 * s2 + 1][2], dp[2 * s2 + 1][3]};
-        const mfma_bf16x8 dsf = pack8(d0, d1);
+        mfma_bf16x8 dsf[QS];
+#pragma unroll
+        for (int qs = 0; qs < QS; ++qs) {
+          const float d0[4] = {dp[2 * s2][qs][0], dp[2 * s2][qs][1], dp[2 * s2][qs][2], dp[2 * s2][qs][3]};
+          const float d1[4] = {dp[2 * s2 + 1][qs][0], dp[2 * s2 + 1][qs][1], dp[2 * s2 + 1][qs][2],
+                               dp[2 * s2 + 1][qs][3]};
+          dsf[qs] = pack8(d0, d1);
+        }
         const int r0 = 32 * s2 + 4 * g + q_, r1 = r0 + 16;
 #pragma unroll
         for (int d = 0; d < ND; ++d) {
           const int dc = d * 16 + pp * 4;
           const mfma_bf16x8 kt = join8(tr16(kh_addr(tk, FB_BN, r0, dc)), tr16(kh_addr(tk, FB_BN, r1, dc)));
-          acc[d] = mfma16(kt, dsf, acc[d]);
+#pragma unroll
+          for (int qs = 0; qs < QS; ++qs) acc[qs][d] = mfma16(kt, dsf[qs], acc[qs][d]);
         }
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  if (qi < a.Sq) {
-    uint16_t* dqp = a.dq + b * a.sgqb + qi * a.sgqs + h * a.sgqh;
 #pragma unroll
-    for (int d = 0; d < ND; ++d) {
-      bf16x4_t x;
+  for (int qs = 0; qs < QS; ++qs) {
+    const int qi = q0w + 16 * qs + li;
+    if (qi < a.Sq) {
+      uint16_t* dqp = a.dq + b * a.sgqb + qi * a.sgqs + h * a.sgqh;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) x[r] = (short)f2bf(acc[d][r] * a.scale);
-      *reinterpret_cast<bf16x4_t*>(dqp + d * 16 + g * 4) = x;
+      for (int d = 0; d < ND; ++d) {
+        bf16x4_t x;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = (short)f2bf(acc[qs][d][r] * a.scale);
+        *reinterpret_cast<bf16x4_t*>(dqp + d * 16 + g * 4) = x;
+      }
     }
   }
 }
@@ -563,6 +605,8 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dq_kernel(AttnBwdArgs
 // =============================================================================== launchers
 // D = 64 with long sequences: 128-wide key / query steps (same MFMA work per barrier as D = 128)
 static bool big_tile(int D, int S) { return D == 64 && S >= 1024; }
+
+
 
 void launch_flash_fwd(const AttnFwdArgs& a, int D, hipStream_t st) {
   const int nqb = (a.Sq + FA_BM - 1) / FA_BM;
@@ -584,16 +628,28 @@ void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, 
     hipLaunchKernelGGL(flash_delta_kernel<64>, dgrid, dim3(256), 0, st, o, sob, sos, soh, a.dO, a.sdb, a.sds, a.sdh,
                        a.delta, a.B, a.Sq, a.Hq, a.lse_ld);
   const dim3 gkv(((a.Sk + FB_BN - 1) / FB_BN) * a.Hkv * a.B);  // dK/dV blocks own 64 keys at any D
-  const dim3 gq(((a.Sq + 63) / 64) * a.Hq * a.B), blk(FA_THREADS);
+  // dQ: QS = 2 (32 queries per wave, 128 per block) when the grid still fills the chip. With D x TILE = 8192
+  // (D = 128, or D = 64 on 128-key tiles) that form needs ~320 VGPRs (one wave per SIMD); $K8S_AMD_FA_DQ_QS2=1
+  // selects it there too (A/B).
+  static const bool qs2_big = [] {
+    const char* e = getenv("K8S_AMD_FA_DQ_QS2");
+    return e && e[0] == '1';
+  }();
+  const bool small = D == 64 && !big_tile(D, a.Sq);
+  const bool qs2 = (small || qs2_big) && (long)((a.Sq + 127) / 128) * a.Hq * a.B >= 512;
+  const dim3 gq(((a.Sq + (qs2 ? 127 : 63)) / (qs2 ? 128 : 64)) * a.Hq * a.B), blk(FA_THREADS);
   if (D == 128) {
     hipLaunchKernelGGL((flash_bwd_dkv_kernel<128, 64>), gkv, blk, 0, st, a);
-    hipLaunchKernelGGL((flash_bwd_dq_kernel<128, 64>), gq, blk, 0, st, a);
+    if (qs2) hipLaunchKernelGGL((flash_bwd_dq_kernel<128, 64, 2>), gq, blk, 0, st, a);
+    else hipLaunchKernelGGL((flash_bwd_dq_kernel<128, 64, 1>), gq, blk, 0, st, a);
   } else if (big_tile(D, a.Sq)) {
     hipLaunchKernelGGL((flash_bwd_dkv_kernel<64, 128>), gkv, blk, 0, st, a);
-    hipLaunchKernelGGL((flash_bwd_dq_kernel<64, 128>), gq, blk, 0, st, a);
+    if (qs2) hipLaunchKernelGGL((flash_bwd_dq_kernel<64, 128, 2>), gq, blk, 0, st, a);
+    else hipLaunchKernelGGL((flash_bwd_dq_kernel<64, 128, 1>), gq, blk, 0, st, a);
   } else {
     hipLaunchKernelGGL((flash_bwd_dkv_kernel<64, 64>), gkv, blk, 0, st, a);
-    hipLaunchKernelGGL((flash_bwd_dq_kernel<64, 64>), gq, blk, 0, st, a);
+    if (qs2) hipLaunchKernelGGL((flash_bwd_dq_kernel<64, 64, 2>), gq, blk, 0, st, a);
+    else hipLaunchKernelGGL((flash_bwd_dq_kernel<64, 64, 1>), gq, blk, 0, st, a);
   }
 }
 

@@ -1125,11 +1125,11 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
     const XForm xf{xform_b, xform_c, make_fastdiv(xform_c)};
     launch(MNMajorK{A, lda, M, K}, MNMajorK{B, ldb, N, K}, e, M, N, K, splits, st, &xf);
   } else if (a_kmajor && b_kmajor)
-    launch(KMajor{A, lda, M}, KMajor{B, ldb, N}, e, M, N, K, splits, st);
+    launch(KMajor{A, lda, M, K}, KMajor{B, ldb, N, K}, e, M, N, K, splits, st);
   else if (a_kmajor && !b_kmajor)
-    launch(KMajor{A, lda, M}, MNMajorK{B, ldb, N, K}, e, M, N, K, splits, st);
+    launch(KMajor{A, lda, M, K}, MNMajorK{B, ldb, N, K}, e, M, N, K, splits, st);
   else if (!a_kmajor && b_kmajor)
-    launch(MNMajorK{A, lda, M, K}, KMajor{B, ldb, N}, e, M, N, K, splits, st);
+    launch(MNMajorK{A, lda, M, K}, KMajor{B, ldb, N, K}, e, M, N, K, splits, st);
   else
     launch(MNMajorK{A, lda, M, K}, MNMajorK{B, ldb, N, K}, e, M, N, K, splits, st);
   if (slab) splitk_reduce(ws, splits, (long)M * N, reinterpret_cast<float*>(C), mode == 1, st);

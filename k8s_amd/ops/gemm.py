@@ -134,12 +134,8 @@ def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True, dx_adden
     if hip_ok(g, x, w) and _shape_ok(M, N, K):
         g = g.contiguous()
         acc = dx_addend is not None and dx_addend.is_contiguous() and dx_addend.dtype == torch.bfloat16
-        if N % 64:  # dgrad reduces over N: zero-pad it to the kernel's 64-deep k-step (e.g. a 1000-class head)
-            Np = (N + 63) // 64 * 64
-            dx = mm(torch.nn.functional.pad(g, (0, Np - N)), torch.nn.functional.pad(w, (0, 0, 0, Np - N)), True, False,
-                    out=dx_addend if acc else None, accumulate=acc)
-        else:
-            dx = mm(g, w, True, False, out=dx_addend if acc else None, accumulate=acc)
+        # dgrad reduces over N; a ragged N (e.g. the 1000-class head) is masked by the kernel's K tail (zeros)
+        dx = mm(g, w, True, False, out=dx_addend if acc else None, accumulate=acc)
         if dx_addend is not None and not acc:
             dx = dx + dx_addend
         if pw is not None and store is not None and pw.grad.dtype == torch.float32:
