@@ -497,6 +497,214 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t
   *reinterpret_cast<bf16x8_t*>(dx + (long)e * 8) = pack_bf16x8(o);
 }
 
+
+// ---------------------------------------------------------------- stem: BatchNorm + ReLU + 3x3 / s2 / p1 max pool
+// The ResNet stem's bn1 -> ReLU -> max pool as one pass each way, so the 112 x 112 x 64 BN output is never stored:
+//  forward : each thread owns 8 channels of one pooled pixel, normalises its 9 window taps on load
+//            (z = bf16(relu(fma(x, scale, shift))), bit-identical to bn_apply_kernel's output) and keeps the max
+//            and the winner's window position (uint8, as maxpool_fwd_k_kernel; ties -> first tap)
+//  backward: the max-pool gradient of an input pixel (sum of dy over the covering windows whose winner it is)
+//            is GATHERED inside the BatchNorm backward's reduce and apply passes, by 2 x 2 input cells (the four
+//            windows covering a cell are loaded once for its 4 pixels, as maxpool_bwd_3s2_kernel), rounded to bf16
+//            as the stored gradient would be, and masked by the ReLU recomputed from x.
+// HBM bytes per step at ResNet-50 b1024 (x = 1.64 GB): forward 1 read of x + the pooled write instead of read x,
+// write z, read z; backward 2 reads of x + the dx write instead of writing dz and reading it twice with x.
+__global__ void __launch_bounds__(BN_THREADS) bn_relu_maxpool_fwd_kernel(
+    const uint16_t* __restrict__ x, const float* __restrict__ params, uint16_t* __restrict__ y,
+    uint8_t* __restrict__ idx, int H, int W, int C, int Ho, int Wo, int total, FastDiv fcv, FastDiv fWo, FastDiv fHo) {
+  const int e = blockIdx.x * BN_THREADS + threadIdx.x;
+  if (e >= total) return;
+  const int cv = C >> 3;
+  const int t = fcv.div(e);
+  const int c = (e - t * cv) * 8;
+  const int t2 = fWo.div(t);
+  const int wo = t - t2 * Wo;
+  const int n = fHo.div(t2);
+  const int ho = t2 - n * Ho;
+  const int h0 = 2 * ho - 1, w0 = 2 * wo - 1;
+  float sc[8], sh[8];
+  load_f8(params + c, sc);
+  load_f8(params + C + c, sh);
+  bf16x8_t v[9];
+#pragma unroll
+  for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+    for (int dw = 0; dw < 3; ++dw) {
+      const int h = min(max(h0 + dh, 0), H - 1), w = min(max(w0 + dw, 0), W - 1);
+      v[dh * 3 + dw] = *reinterpret_cast<const bf16x8_t*>(x + (((long)n * H + h) * W + w) * C + c);
+    }
+  float best[8];
+  uint32_t arg[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    best[j] = -INFINITY;
+    arg[j] = 255;
+  }
+#pragma unroll
+  for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+    for (int dw = 0; dw < 3; ++dw) {
+      if ((unsigned)(h0 + dh) >= (unsigned)H || (unsigned)(w0 + dw) >= (unsigned)W) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float z = bf2f(f2bf(fmaxf(__builtin_fmaf(bf2f((uint16_t)v[dh * 3 + dw][j]), sc[j], sh[j]), 0.f)));
+        if (z > best[j] || (z != z && best[j] == best[j])) {
+          best[j] = z;
+          arg[j] = (uint32_t)(dh * 3 + dw);
+        }
+      }
+    }
+  store8(y + (long)e * 8, best);
+  uint64_t packed = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) packed |= (uint64_t)arg[j] << (8 * j);
+  *reinterpret_cast<uint64_t*>(idx + (long)e * 8) = packed;
+}
+
+// dz of the 4 pixels of input cell (n, kc, jc), channels c .. c+7: the max-pool gradient (bf16-rounded)
+struct PoolCell {
+  float dz[2][2][8];
+};
+__device__ __forceinline__ void pool_cell_grad(const uint16_t* __restrict__ dpool, const uint8_t* __restrict__ idx,
+                                               int n, int kc, int jc, int c, int C, int Ho, int Wo, PoolCell& pc) {
+  uint64_t pk[2][2];
+  float g[2][2][8];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const bool ok = kc + a < Ho && jc + b < Wo;
+      const long o = (((long)n * Ho + (ok ? kc + a : kc)) * Wo + (ok ? jc + b : jc)) * C + c;
+      pk[a][b] = ok ? *reinterpret_cast<const uint64_t*>(idx + o) : ~0ull;  // 0xff matches no position
+      load8(dpool + o, g[a][b]);
+    }
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int dw = 0; dw < 2; ++dw) {
+      float acc[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          // pixel (2kc + dh, 2jc + dw) lies in window (kc + a, jc + b) iff its offset there is in 0..2
+          const int oh = dh - 2 * a + 1, ow = dw - 2 * b + 1;
+          if (oh < 0 || oh > 2 || ow < 0 || ow > 2) continue;  // compile-time after unrolling
+          const uint32_t pos = (uint32_t)(oh * 3 + ow);
+#pragma unroll
+          for (int r = 0; r < 8; ++r)
+            if (((pk[a][b] >> (8 * r)) & 0xff) == pos) acc[r] += g[a][b][r];
+        }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) pc.dz[dh][dw][r] = bf2f(f2bf(acc[r]));
+    }
+}
+
+// Backward reduce over input cells: part[(bx * C + c) * 2 + {0, 1}] = sum dz_eff, sum dz_eff * xhat (the layout of
+// bn_bwd_reduce_kernel, finished by bn_bwd_final_kernel). Block = (256 / cv) cells x cv channel groups, cell-strided.
+__global__ void __launch_bounds__(BN_THREADS) pool_bn_bwd_reduce_kernel(
+    const uint16_t* __restrict__ dpool, const uint8_t* __restrict__ idx, const uint16_t* __restrict__ x,
+    const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ beta, int H, int W, int C, int Ho, int Wo, int Hc, int Wc, int ncells,
+    float* __restrict__ part, FastDiv fWc, FastDiv fHc) {
+  __shared__ float sh[2][BN_THREADS][9];
+  const int t = threadIdx.x, cv = C >> 3;
+  const int cg = t % cv, cl = t / cv, cpb = BN_THREADS / cv;
+  const int c = cg * 8;
+  float sd[8], sx[8], mu[8], is[8], sc[8], bt[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sd[j] = sx[j] = 0.f;
+    mu[j] = mean[c + j];
+    is[j] = invstd[c + j];
+    bn_affine_regs(gamma[c + j], beta[c + j], mu[j], is[j], sc[j], bt[j]);
+  }
+  for (int cell = blockIdx.x * cpb + cl; cell < ncells; cell += gridDim.x * cpb) {
+    const int r2 = fWc.div(cell), jc = cell - r2 * Wc, n = fHc.div(r2), kc = r2 - n * Hc;
+    PoolCell pc;
+    pool_cell_grad(dpool, idx, n, kc, jc, c, C, Ho, Wo, pc);
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int dw = 0; dw < 2; ++dw) {
+        const int h = 2 * kc + dh, w = 2 * jc + dw;
+        if (h >= H || w >= W) continue;
+        const bf16x8_t xv = *reinterpret_cast<const bf16x8_t*>(x + (((long)n * H + h) * W + w) * C + c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xf = bf2f((uint16_t)xv[j]);
+          const float g = relu_on(xf, sc[j], bt[j]) ? pc.dz[dh][dw][j] : 0.f;
+          sd[j] += g;
+          sx[j] += g * (xf - mu[j]) * is[j];
+        }
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sh[0][t][j] = sd[j];
+    sh[1][t][j] = sx[j];
+  }
+  __syncthreads();
+  if (cl == 0) {
+    for (int rr = 1; rr < cpb; ++rr) {
+      const int o = rr * cv + cg;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sd[j] += sh[0][o][j];
+        sx[j] += sh[1][o][j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const long i = ((long)blockIdx.x * C + c + j) * 2;
+      part[i] = sd[j];
+      part[i + 1] = sx[j];
+    }
+  }
+}
+
+// dx = sc * dz_eff + B * x + D for the 4 pixels of one cell, 8 channels per thread (params = [sc | B | D | shift])
+__global__ void __launch_bounds__(BN_THREADS) pool_bn_bwd_apply_kernel(
+    const uint16_t* __restrict__ dpool, const uint8_t* __restrict__ idx, const uint16_t* __restrict__ x,
+    const float* __restrict__ params, uint16_t* __restrict__ dx, int H, int W, int C, int Ho, int Wo, int total,
+    FastDiv fcv, FastDiv fWc, FastDiv fHc) {
+  const int e = blockIdx.x * BN_THREADS + threadIdx.x;
+  if (e >= total) return;
+  const int cv = C >> 3;
+  const int t = fcv.div(e);
+  const int c = (e - t * cv) * 8;
+  const int t2 = fWc.div(t);
+  const int jc = t - t2 * (int)fWc.d;
+  const int n = fHc.div(t2);
+  const int kc = t2 - n * (int)fHc.d;
+  PoolCell pc;
+  pool_cell_grad(dpool, idx, n, kc, jc, c, C, Ho, Wo, pc);
+  float sc[8], B[8], D[8], shf[8];
+  load_f8(params + c, sc);
+  load_f8(params + C + c, B);
+  load_f8(params + 2 * C + c, D);
+  load_f8(params + 3 * C + c, shf);
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int dw = 0; dw < 2; ++dw) {
+      const int h = 2 * kc + dh, w = 2 * jc + dw;
+      if (h >= H || w >= W) continue;
+      const long o = (((long)n * H + h) * W + w) * C + c;
+      const bf16x8_t xv = *reinterpret_cast<const bf16x8_t*>(x + o);
+      float r[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xf = bf2f((uint16_t)xv[j]);
+        const float g = relu_on(xf, sc[j], shf[j]) ? pc.dz[dh][dw][j] : 0.f;
+        r[j] = __builtin_fmaf(sc[j], g, __builtin_fmaf(B[j], xf, D[j]));
+      }
+      store8(dx + o, r);
+    }
+}
+
 // ---------------------------------------------------------------- launchers
 // Traversal order of the streaming passes, chosen so that each pass starts where its producer stopped: the bytes
 // the producer touched last are still in the 256 MiB Infinity Cache (a line stays resident while it plus every
@@ -627,6 +835,44 @@ void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, con
   hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, nb, C, dgamma, dbeta,
                      1.f / (float)M, mean, invstd, gamma, beta, params);
   launch_bn_bwd_apply(dy, x, mask, params, relu_x, dx, dres, M, C, st);
+}
+
+// ---- stem BatchNorm + ReLU + 3x3 / s2 / p1 max pool (see bn_relu_maxpool_fwd_kernel)
+void launch_bn_relu_maxpool_fwd(const uint16_t* x, const float* gamma, const float* beta, const float* sums, int nrep,
+                                float* save_mean, float* save_invstd, float* run_mean, float* run_var, float* params,
+                                uint16_t* y, uint8_t* idx, int N, int H, int W, int C, float eps, float momentum,
+                                hipStream_t st) {
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;  // (H + 2 - 3) / 2 + 1
+  const long total = (long)N * Ho * Wo * (C / 8);
+  if ((long)N * H * W * C / 8 >= (1L << 31)) throw std::runtime_error("bn_relu_maxpool: tensor too large");
+  hipLaunchKernelGGL(bn_finalize_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, nrep, C,
+                     (float)((long)N * H * W), eps, momentum, save_mean, save_invstd, run_mean, run_var, gamma, beta,
+                     params);
+  hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel, dim3(cdiv(total, BN_THREADS)), dim3(BN_THREADS), 0, st, x, params,
+                     y, idx, H, W, C, Ho, Wo, (int)total, make_fastdiv(C / 8), make_fastdiv(Wo), make_fastdiv(Ho));
+}
+
+int pool_bn_workspace_floats(int C) { return 4096 * C * 2; }
+
+void launch_pool_bn_bwd(const uint16_t* dpool, const uint8_t* idx, const uint16_t* x, const float* mean,
+                        const float* invstd, const float* gamma, const float* beta, uint16_t* dx, float* dgamma,
+                        float* dbeta, float* work, float* params, int N, int H, int W, int C, hipStream_t st) {
+  if (C % 8 || BN_THREADS % (C / 8)) throw std::runtime_error("pool_bn_bwd: C / 8 must divide 256");
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2, Hc = (H + 1) / 2, Wc = (W + 1) / 2;
+  const long ncells = (long)N * Hc * Wc;
+  if (ncells * (C / 8) >= (1L << 31)) throw std::runtime_error("pool_bn_bwd: tensor too large");
+  const int cpb = BN_THREADS / (C / 8);
+  long nb = (ncells + cpb - 1) / cpb;
+  nb = nb > 4096 ? 4096 : nb;  // ~16 blocks per CU: enough loads in flight (a 1024-block grid ran at half the roof)
+  hipLaunchKernelGGL(pool_bn_bwd_reduce_kernel, dim3((unsigned)nb), dim3(BN_THREADS), 0, st, dpool, idx, x, mean,
+                     invstd, gamma, beta, H, W, C, Ho, Wo, Hc, Wc, (int)ncells, work, make_fastdiv(Wc),
+                     make_fastdiv(Hc));
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, (int)nb, C, dgamma, dbeta,
+                     1.f / (float)((long)N * H * W), mean, invstd, gamma, beta, params);
+  const long total = ncells * (C / 8);
+  hipLaunchKernelGGL(pool_bn_bwd_apply_kernel, dim3(cdiv(total, BN_THREADS)), dim3(BN_THREADS), 0, st, dpool, idx, x,
+                     params, dx, H, W, C, Ho, Wo, (int)total, make_fastdiv(C / 8), make_fastdiv(Wc),
+                     make_fastdiv(Hc));
 }
 
 __global__ void __launch_bounds__(BN_THREADS) relu_mask_kernel(const uint16_t* __restrict__ y,

@@ -1094,7 +1094,7 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, l
   }
 }
 
-static void splitk_reduce(const float* ws, int splits, long mn, float* out, bool accumulate, hipStream_t st) {
+void splitk_reduce(const float* ws, int splits, long mn, float* out, bool accumulate, hipStream_t st) {
   const long mn4 = mn / 4;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(stream_grid(mn4, 256)), dim3(256), 0, st, ws, splits, mn4, out,
                      accumulate ? 1 : 0);

@@ -141,6 +141,18 @@ struct AttnBwdArgs {
   int B, Sq, Sk, Hq, Hkv, causal;
   float scale_log2, scale;
 };
+// ResNet stem BatchNorm + ReLU + 3x3 / s2 / p1 max pool, fused (batchnorm.hip): forward from the conv's epilogue sums
+// (params = fp32 [2][C] scale | shift, idx = winner byte per pooled element); backward into dx of the conv output
+// (params = fp32 [4][C] workspace, work = pool_bn_workspace_floats(C))
+void launch_bn_relu_maxpool_fwd(const uint16_t* x, const float* gamma, const float* beta, const float* sums, int nrep,
+                                float* save_mean, float* save_invstd, float* run_mean, float* run_var, float* params,
+                                uint16_t* y, uint8_t* idx, int N, int H, int W, int C, float eps, float momentum,
+                                hipStream_t st);
+int pool_bn_workspace_floats(int C);
+void launch_pool_bn_bwd(const uint16_t* dpool, const uint8_t* idx, const uint16_t* x, const float* mean,
+                        const float* invstd, const float* gamma, const float* beta, uint16_t* dx, float* dgamma,
+                        float* dbeta, float* work, float* params, int N, int H, int W, int C, hipStream_t st);
+
 // Streaming-order state (batchnorm.hip): direction (0 ascending, 1 descending, as 8 concurrent bands) of the next
 // streaming launch; `fixed` is the direction used in the fixed-BatchNorm mode.
 int stream_order_mode();
@@ -167,6 +179,16 @@ void launch_avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, 
 // ---- stem.hip: 7x7 / stride-2 stem as a 4x4 conv over the 2x2 space-to-depth image (16 channels)
 void launch_stem_s2d_input(const uint16_t* x, int N, int H, int W, int Cin, int pad, uint16_t* out, hipStream_t st);
 void launch_stem_w_s2d(const uint16_t* w7, int K, int R, int Cw, uint16_t* w4, hipStream_t st);
+// the s2d stem conv (K = 64, 4x4 taps, 16 channels) LDS-tiled, BN statistics into stats [kConvStatReplicas][2][64]
+bool stem_conv_fwd_ok(int K, int R, int C, int Wo);
+void launch_stem_conv_fwd(const uint16_t* xs, const uint16_t* w4, uint16_t* y, float* stats, int N, int Hs, int Ws,
+                          hipStream_t st);
+// out[i] (+)= sum over `splits` fp32 slabs of mn elements (gemm.hip)
+void splitk_reduce(const float* ws, int splits, long mn, float* out, bool accumulate, hipStream_t st);
+// the s2d stem weight gradient (LDS-tiled, persistent blocks; ws = stem_wgrad_blocks(N, Hs) x 64 x 256 fp32 partials)
+int stem_wgrad_blocks(int N, int Hs);
+void launch_stem_wgrad(const uint16_t* xs, const uint16_t* dy, float* ws, float* dw4, int N, int Hs, int Ws,
+                       hipStream_t st);
 void launch_stem_dw_s2d(const float* dw4, int K, int R, int Cw, float* dw7, hipStream_t st);
 
 // ---- NHWC max pooling (pool.hip): idx = winning window position per output element (uint8)

@@ -204,6 +204,51 @@ std::vector<Tensor> bn_finalize(Tensor sums, Tensor gamma, Tensor beta, Tensor r
   return {mean, invstd, params};
 }
 
+// ResNet stem: BatchNorm (statistics from the conv epilogue sums) + ReLU + 3x3 / s2 / p1 max pool in one pass; the
+// BN output is never stored. Returns (pooled y, winner idx, mean, invstd).
+std::vector<Tensor> bn_relu_maxpool(Tensor x, Tensor sums, Tensor gamma, Tensor beta, Tensor run_mean, Tensor run_var,
+                                    double momentum, double eps) {
+  check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(), "x must be a contiguous NHWC tensor");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0, "C / 8 must divide 256");
+  check_dtype(gamma, at::kFloat, "gamma");
+  TORCH_CHECK(gamma.numel() == C && beta.numel() == C && run_mean.numel() == C && run_var.numel() == C);
+  TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kFloat && sums.is_contiguous() && sums.numel() % (2 * C) == 0,
+              "sums must be fp32 [R, 2, C]");
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+  auto y = torch::empty({N, Ho, Wo, C}, x.options());
+  auto idx = torch::empty({N, Ho, Wo, C}, x.options().dtype(at::kByte));
+  auto mean = torch::empty({C}, gamma.options());
+  auto invstd = torch::empty({C}, gamma.options());
+  auto params = torch::empty({2 * C}, gamma.options());
+  k8s_amd::launch_bn_relu_maxpool_fwd(cbf(x), f32(gamma), f32(beta), f32(sums), (int)(sums.numel() / (2 * C)),
+                                      f32(mean), f32(invstd), f32(run_mean), f32(run_var), f32(params), bf(y),
+                                      idx.data_ptr<uint8_t>(), N, H, W, C, (float)eps, (float)momentum, cur_stream());
+  return {y, idx, mean, invstd};
+}
+
+// Backward of bn_relu_maxpool: dx of the conv output; dgamma / dbeta written into the given fp32 tensors.
+Tensor pool_bn_bwd(Tensor dpool, Tensor idx, Tensor x, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta,
+                   Tensor dgamma, Tensor dbeta) {
+  check_cuda(dpool, "dpool"); check_dtype(dpool, at::kBFloat16, "dpool");
+  check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x");
+  check_dtype(idx, at::kByte, "idx");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous() && dpool.is_contiguous() && idx.is_contiguous());
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(dpool.sizes() == idx.sizes() && dpool.size(0) == N && dpool.size(1) == (H + 1) / 2 &&
+                  dpool.size(2) == (W + 1) / 2 && dpool.size(3) == C, "dpool / idx shape mismatch");
+  TORCH_CHECK(dgamma.numel() == C && dbeta.numel() == C && dgamma.is_contiguous() && dbeta.is_contiguous());
+  check_dtype(dgamma, at::kFloat, "dgamma"); check_dtype(dbeta, at::kFloat, "dbeta");
+  auto dx = torch::empty_like(x);
+  auto params = torch::empty({4 * C}, gamma.options());
+  auto work = torch::empty({k8s_amd::pool_bn_workspace_floats(C)}, gamma.options());
+  k8s_amd::launch_pool_bn_bwd(cbf(dpool), idx.data_ptr<uint8_t>(), cbf(x), f32(mean), f32(invstd), f32(gamma),
+                              f32(beta), bf(dx), f32(dgamma), f32(dbeta), f32(work), f32(params), N, H, W, C,
+                              cur_stream());
+  return dx;
+}
+
 static const float* xform_ptr(const c10::optional<Tensor>& xf, long C) {
   if (!xf || !xf->defined()) return nullptr;
   TORCH_CHECK(xf->is_cuda() && xf->scalar_type() == at::kFloat && xf->is_contiguous() && xf->numel() == 2 * C,
@@ -807,6 +852,32 @@ Tensor stem_w_s2d(Tensor w7) {
   k8s_amd::launch_stem_w_s2d(cbf(w7), K, R, (int)w7.size(3), bf(w4), cur_stream());
   return w4;
 }
+// the s2d stem convolution on its LDS-tiled kernel (stem.hip): y [N, Hs-3, Ws-3, 64] + BN statistics into `stats`
+Tensor stem_conv_fwd(Tensor xs, Tensor w4, Tensor stats) {
+  check_cuda(xs, "xs"); check_dtype(xs, at::kBFloat16, "xs"); check_dtype(w4, at::kBFloat16, "w4");
+  TORCH_CHECK(xs.dim() == 4 && xs.size(3) == 16 && xs.is_contiguous(), "xs must be a contiguous [N, Hs, Ws, 16] image");
+  TORCH_CHECK(w4.dim() == 4 && w4.is_contiguous() && k8s_amd::stem_conv_fwd_ok((int)w4.size(0), (int)w4.size(1),
+              (int)w4.size(3), (int)xs.size(2) - 3) && w4.size(2) == 4, "stem conv: w4 [64, 4, 4, 16], Wo % 16 == 0");
+  TORCH_CHECK(stats.is_cuda() && stats.scalar_type() == at::kFloat && stats.is_contiguous() &&
+              stats.numel() == (long)k8s_amd::kConvStatReplicas * 2 * 64, "stats must be zeroed fp32 [R, 2, 64]");
+  const int N = xs.size(0), Hs = xs.size(1), Ws = xs.size(2);
+  auto y = torch::empty({N, Hs - 3, Ws - 3, 64}, xs.options());
+  k8s_amd::launch_stem_conv_fwd(cbf(xs), cbf(w4), bf(y), f32(stats), N, Hs, Ws, cur_stream());
+  return y;
+}
+
+// the s2d stem weight gradient (stem.hip): dw4 fp32 [64, 4, 4, 16] from the image xs and the output gradient dy
+void stem_wgrad(Tensor xs, Tensor dy, Tensor dw4) {
+  check_cuda(xs, "xs"); check_dtype(xs, at::kBFloat16, "xs"); check_dtype(dy, at::kBFloat16, "dy");
+  TORCH_CHECK(xs.dim() == 4 && xs.size(3) == 16 && xs.is_contiguous() && dy.is_contiguous(), "xs [N, Hs, Ws, 16]");
+  const int N = xs.size(0), Hs = xs.size(1), Ws = xs.size(2);
+  TORCH_CHECK(dy.dim() == 4 && dy.size(0) == N && dy.size(1) == Hs - 3 && dy.size(2) == Ws - 3 && dy.size(3) == 64 &&
+              k8s_amd::stem_conv_fwd_ok(64, 4, 16, Ws - 3), "dy [N, Hs-3, Ws-3, 64], Wo % 16 == 0");
+  TORCH_CHECK(dw4.is_cuda() && dw4.scalar_type() == at::kFloat && dw4.is_contiguous() && dw4.numel() == 64 * 256);
+  auto ws = torch::empty({(long)k8s_amd::stem_wgrad_blocks(N, Hs) * 64 * 256}, dw4.options());
+  k8s_amd::launch_stem_wgrad(cbf(xs), cbf(dy), f32(ws), f32(dw4), N, Hs, Ws, cur_stream());
+}
+
 void stem_dw_s2d(Tensor dw4, Tensor dw7) {
   check_cuda(dw4, "dw4"); check_cuda(dw7, "dw7");
   check_dtype(dw4, at::kFloat, "dw4"); check_dtype(dw7, at::kFloat, "dw7");
@@ -890,11 +961,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad_wsub", &conv_dgrad_wsub);
   m.def("flash_fwd", &flash_fwd);
   m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("bn_relu_maxpool", &bn_relu_maxpool, py::arg("x"), py::arg("sums"), py::arg("gamma"), py::arg("beta"),
+        py::arg("run_mean"), py::arg("run_var"), py::arg("momentum"), py::arg("eps"));
+  m.def("pool_bn_bwd", &pool_bn_bwd, py::arg("dpool"), py::arg("idx"), py::arg("x"), py::arg("mean"),
+        py::arg("invstd"), py::arg("gamma"), py::arg("beta"), py::arg("dgamma"), py::arg("dbeta"));
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("stem_s2d_input", &stem_s2d_input);
   m.def("stem_w_s2d", &stem_w_s2d);
+  m.def("stem_conv_fwd", &stem_conv_fwd);
+  m.def("stem_wgrad", &stem_wgrad);
   m.def("stem_dw_s2d", &stem_dw_s2d);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("maxpool_bwd", &maxpool_bwd);

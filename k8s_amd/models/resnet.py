@@ -146,10 +146,11 @@ class ResNet(nn.Module):
 
     def forward(self, x):
         if x.shape[-1] == 16 and self.stem_s2d and x.is_cuda:  # space-to-depth stem (prepare_input)
-            y = self.bn1(K.stem_conv_s2d(x, self.conv1.w))
+            t = K.stem_conv_s2d(x, self.conv1.w)
         else:
-            y = self.bn1(self.conv1(x))
-        y = K.max_pool_nhwc(y, 3, 2, 1)
+            t = self.conv1(x)
+        # bn1 + ReLU + 3x3/s2 max pool: one fused pass each way on the GPU (the 112x112 BN output is never stored)
+        y = K.bn_relu_maxpool(t, self.bn1) if K.STEM_POOL_FUSED else K.max_pool_nhwc(self.bn1(t), 3, 2, 1)
         for b in self.blocks:
             y = b(y)
         y = K.global_avg_pool_nhwc(y)

@@ -159,7 +159,10 @@ class _StemS2D(torch.autograd.Function):
         w4 = C_.stem_w_s2d(w7.contiguous())
         sums = _zero_scratch(p.store, xs.device, C_.conv_stat_replicas * 2 * w4.shape[0]).view(
             C_.conv_stat_replicas, 2, w4.shape[0])
-        y = C_.conv_fwd(xs, w4, 1, 0, 1, False, None, 0, sums)
+        if STEM_CONV and tuple(w4.shape) == (64, 4, 4, 16) and (xs.shape[2] - 3) % 16 == 0 and xs.shape[2] - 3 <= 112:
+            y = C_.stem_conv_fwd(xs.contiguous(), w4, sums)  # LDS-tiled input window (stem.hip)
+        else:
+            y = C_.conv_fwd(xs, w4, 1, 0, 1, False, None, 0, sums)
         _conv_impl().STATS["hip_fwd"] += 1
         ctx.save_for_backward(xs)
         ctx.p, ctx.kshape = p, tuple(w4.shape)
@@ -172,7 +175,10 @@ class _StemS2D(torch.autograd.Function):
         (xs,) = ctx.saved_tensors
         p, C_ = ctx.p, _C()
         dw4 = torch.empty(ctx.kshape, device=xs.device, dtype=torch.float32)
-        _conv_impl()._wgrad_hip(C_, gy.contiguous(), xs, dw4, 1, 0, False)
+        if STEM_CONV and ctx.kshape == (64, 4, 4, 16) and (xs.shape[2] - 3) % 16 == 0 and xs.shape[2] - 3 <= 112:
+            C_.stem_wgrad(xs.contiguous(), gy.contiguous(), dw4)  # LDS-tiled persistent kernel (stem.hip)
+        else:
+            _conv_impl()._wgrad_hip(C_, gy.contiguous(), xs, dw4, 1, 0, False)
         _conv_impl().STATS["hip_wgrad"] += 1
         store = p.store
         slot = store.slot_for_write(p)
@@ -274,6 +280,10 @@ class _BnAct(torch.autograd.Function):
 # bn1 -> the 3x3 conv2, "0" = none. (The 3x3 consumer re-applies the transform to each input element once per tap:
 # 9x the VALU work of an apply pass, inside a compute-bound product.)
 BN_ONLOAD = os.environ.get("K8S_AMD_BN_ONLOAD", "1x1")
+# the s2d stem conv on its LDS-tiled kernel (stem.hip); K8S_AMD_STEM_CONV=0: the generic implicit GEMM (A/B)
+STEM_CONV = os.environ.get("K8S_AMD_STEM_CONV", "1") != "0"
+# ResNet stem bn1 + ReLU + max pool fused (bn_relu_maxpool); K8S_AMD_STEM_POOL_FUSED=0 runs them separately (A/B)
+STEM_POOL_FUSED = os.environ.get("K8S_AMD_STEM_POOL_FUSED", "1") != "0"
 
 
 def _bn_param_grads(store, pg, pb, device):
@@ -651,6 +661,42 @@ def max_pool_nhwc(x, k=3, s=2, p=1):
         return _MaxPoolNHWC.apply(x, k, s, p)
     y = F.max_pool2d(x.permute(0, 3, 1, 2), k, s, p)
     return y.permute(0, 2, 3, 1).contiguous()
+
+
+class _BnReluMaxPool(torch.autograd.Function):
+    """max_pool(relu(BN(x)), 3, 2, 1) for the ResNet stem in one pass each way (batchnorm.hip
+    bn_relu_maxpool_fwd_kernel / pool_bn_bwd_*): the BN output is never stored; the backward gathers the
+    max-pool gradient inside the BatchNorm backward's reduce and apply passes. Statistics from the conv epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, sums, anchor, pg, pb, run_mean, run_var, momentum, eps):
+        x = x.contiguous()
+        y, idx, mean, invstd = _C().bn_relu_maxpool(x, sums, pg.master, pb.master, run_mean, run_var, momentum, eps)
+        ctx.save_for_backward(x, idx, mean, invstd)
+        ctx.pg, ctx.pb = pg, pb
+        ctx.mark_non_differentiable(idx)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, idx, mean, invstd = ctx.saved_tensors
+        pg, pb = ctx.pg, ctx.pb
+        dg, db, finish = _bn_param_grads(pg.store, pg, pb, x.device)
+        dx = _C().pool_bn_bwd(dy.contiguous(), idx, x, mean, invstd, pg.master, pb.master, dg, db)
+        finish()
+        return (dx,) + (None,) * 8
+
+
+def bn_relu_maxpool(t, bn):
+    """``max_pool_nhwc(bn(t), 3, 2, 1)`` for ``t = (x, sums)`` from a conv with the statistics epilogue and a
+    training-mode ReLU BatchNorm ``bn`` (models/resnet.BN): fused on the GPU where the kernels take the shape, else
+    the separate BN + max pool."""
+    x, sums = t if isinstance(t, tuple) else (t, None)
+    if (sums is not None and bn.training and _gpu(x) and x.dtype == torch.bfloat16 and x.dim() == 4
+            and x.shape[-1] % 8 == 0 and 256 % (x.shape[-1] // 8) == 0):
+        return _BnReluMaxPool.apply(x, sums, bn.gamma.store.anchor, bn.gamma, bn.beta, bn.running_mean,
+                                    bn.running_var, bn.momentum, bn.eps)
+    return max_pool_nhwc(bn(t), 3, 2, 1)
 
 
 class _AvgPoolNHWC(torch.autograd.Function):

@@ -293,3 +293,44 @@ def test_slice_sum_and_cast_bf16(cuda, world, n):
         want = want + chunks[r]
     assert torch.equal(out, want)
     assert torch.equal(out_bf, want.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("N,H,W,C", [(4, 32, 30, 64), (2, 31, 17, 64), (3, 12, 12, 32)])
+def test_bn_relu_maxpool_fused_vs_fp32(cuda, N, H, W, C):
+    """Stem BN + ReLU + 3x3/s2/p1 max pool in one pass (and its backward gathering the pool gradient inside the BN
+    backward) against an fp32 reference: batch statistics, z = bf16(relu(BN(x))) (the stored activation the
+    separate kernels would write, so max-pool ties resolve alike), max_pool2d autograd for the pool gradient, then
+    the training-mode BatchNorm backward formula."""
+    torch.manual_seed(11)
+    x = (torch.randn(N, H, W, C, device=cuda) * 2 + 0.3).bfloat16()
+    g = torch.rand(C, device=cuda) + 0.5
+    b = torch.randn(C, device=cuda) * 0.5
+    xf = x.float().reshape(-1, C)
+    M = xf.shape[0]
+    sums = torch.stack([xf.sum(0), (xf * xf).sum(0)]).reshape(1, 2, C).contiguous()
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    y, idx, mean, invstd = _C().bn_relu_maxpool(x, sums, g, b, rm, rv, 0.1, 1e-5)
+    assert y.shape == (N, (H + 1) // 2, (W + 1) // 2, C)
+    var = xf.var(0, unbiased=False)
+    _close(mean, xf.mean(0), 1e-4)
+    _close(invstd, torch.rsqrt(var + 1e-5), 1e-3)
+    sc = g * invstd
+    sh = b - mean * sc
+    pre = (x.float() * sc + sh).bfloat16().float()
+    z = torch.relu(pre)
+    zr = z.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    yr = torch.nn.functional.max_pool2d(zr, 3, 2, 1)
+    assert torch.equal(y.float().permute(0, 3, 1, 2), yr.detach().bfloat16().float())
+    dy = torch.randn_like(y)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    dz = zr.grad.permute(0, 2, 3, 1).bfloat16().float() * (pre > 0)
+    dz = dz.reshape(-1, C)
+    xhat = (xf - mean) * invstd
+    dbr, dgr = dz.sum(0), (dz * xhat).sum(0)
+    dxr = (g * invstd) * (dz - dbr / M - xhat * dgr / M)
+    dg, db = torch.empty(C, device=cuda), torch.empty(C, device=cuda)
+    dx = _C().pool_bn_bwd(dy, idx, x, mean, invstd, g, b, dg, db)
+    _close(db, dbr, 1e-3)
+    _close(dg, dgr, 1e-3)
+    rel = ((dx.float().reshape(-1, C) - dxr).norm() / dxr.norm()).item()
+    assert rel < 1e-2, rel

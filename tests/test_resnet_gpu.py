@@ -102,3 +102,42 @@ def test_stem_space_to_depth_matches_7x7(cuda):
     dw = p.grad.view(p.shape)
     assert rel(dw[..., :3].permute(0, 3, 1, 2), w.grad) < 1e-2
     assert dw[..., 3:].abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 224, 224), (3, 64, 64), (2, 70, 64)])
+def test_stem_conv_kernel_matches_generic(cuda, N, H, W):
+    """The LDS-tiled s2d stem convolution (stem.hip) vs the generic implicit-GEMM conv of the same 4x4 weight:
+    outputs and the BatchNorm statistics of the stored values (H = 70: 35 output rows, a partial last row tile)."""
+    torch.manual_seed(3)
+    C = K._C()
+    img = torch.randn(N, H, W, 3, device=cuda).bfloat16()
+    xs = K.stem_s2d_input(img)
+    w4 = (torch.randn(64, 4, 4, 16, device=cuda) * 0.1).bfloat16()
+    R = C.conv_stat_replicas
+    s1, s2 = torch.zeros(R, 2, 64, device=cuda), torch.zeros(R, 2, 64, device=cuda)
+    y1 = C.stem_conv_fwd(xs, w4, s1)
+    y2 = C.conv_fwd(xs, w4, 1, 0, 1, False, None, 0, s2)
+    assert y1.shape == y2.shape
+    assert ((y1.float() - y2.float()).norm() / y2.float().norm()).item() < 5e-3
+    t1, t2 = s1.sum(0), s2.sum(0)
+    assert ((t1 - t2).abs().max() / t2.abs().max()).item() < 1e-3
+    yf = y1.float().reshape(-1, 64)
+    assert ((t1[0] - yf.sum(0)).abs().max() / yf.sum(0).abs().max()).item() < 1e-3
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 224, 224), (3, 70, 64)])
+def test_stem_wgrad_kernel_matches_generic(cuda, N, H, W):
+    """The LDS-tiled persistent s2d stem weight gradient (stem.hip) vs the generic split-K implicit GEMM."""
+    from k8s_amd.ops import conv as convmod
+
+    torch.manual_seed(4)
+    C = K._C()
+    img = torch.randn(N, H, W, 3, device=cuda).bfloat16()
+    xs = K.stem_s2d_input(img)
+    Ho, Wo = xs.shape[1] - 3, xs.shape[2] - 3
+    dy = torch.randn(N, Ho, Wo, 64, device=cuda).bfloat16()
+    d1 = torch.empty(64, 4, 4, 16, device=cuda)
+    d2 = torch.empty(64, 4, 4, 16, device=cuda)
+    C.stem_wgrad(xs, dy, d1)
+    convmod._wgrad_hip(C, dy, xs, d2, 1, 0, False)
+    assert ((d1 - d2).norm() / d2.norm()).item() < 1e-3
