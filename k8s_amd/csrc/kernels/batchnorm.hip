@@ -825,7 +825,11 @@ void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, con
                    float* work, float* params, long M, int C, hipStream_t st, const uint8_t* mask) {
   BnGeom g = bn_geom(C, M);
   const int nb = bn_reduce_blocks(M, g);
-  const int rdir = stream_dir(1);
+  static const bool masked_plain = [] {  // $K8S_AMD_BN_MASKED_PLAIN=1: residual-BN reduce in address order (A/B)
+    const char* e = getenv("K8S_AMD_BN_MASKED_PLAIN");
+    return e && e[0] == '1';
+  }();
+  const int rdir = (mask && masked_plain) ? 0 : stream_dir(1);
   if (mask)
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, dy, x, mean, invstd,
                        gamma, beta, (int)relu_x, M, C, g.tpr, g.rows_per_iter, work, mask, rdir);

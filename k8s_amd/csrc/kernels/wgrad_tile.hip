@@ -6,7 +6,7 @@
 // empty with 64 output channels, and every 16-B tap unit of im2col(x) is gathered from L2 nine times. Here
 // persistent blocks (2 per CU) sweep tiles of RT = 4 output rows: the (RT + 2)-row zero-padded input window and
 // the RT dy rows are staged in LDS once per tile and both MFMA operands are read from them transposed
-// (ds_read_b64_tr_b16: 4 pixels x 16 channels per 16 lanes); each block keeps its fp32 partial of the whole
+// (ds_read_b64_tr_b16: 4 pixels x 16 channels per 16 lanes), staged by LDS-DMA; each block keeps its fp32 partial of the whole
 // 64 x 576 gradient in accumulator registers (wave w: output columns 144 w .. 144 w + 143) until its last tile,
 // and splitk_reduce sums the blocks' partials into dw.
 //   LDS images: [position][64 ch] bf16, 128-B rows, 16-B chunk c of row p at c ^ (p & 7) (window and dy alike).
@@ -21,6 +21,7 @@ namespace k8s_amd {
 
 namespace wg3 {
 constexpr int RT = 4, C = 64, NQ = 9 * C;  // 576 output columns (tap, channel)
+__device__ __attribute__((aligned(64))) uint16_t g_wg3_zero[64];  // source of the zero padding
 
 __device__ __forceinline__ int off(int p, int ch16) { return p * 128 + ((ch16 ^ (p & 7)) << 4); }
 
@@ -44,41 +45,34 @@ __global__ void __launch_bounds__(256, 2) wgrad3x3_c64_kernel(const uint16_t* __
 
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int n = t / tiles_per_img, h0 = (t % tiles_per_img) * RT;
-    // ---- stage: window rows h0 - 1 .. h0 + RT, columns -1 .. W (zeros outside the image), dy rows h0 .. h0+RT-1,
-    // in batches of 4 chunks per thread (the 144 accumulator registers leave no room for the whole tile in flight;
-    // the CU's other block computes meanwhile)
+    // ---- stage by LDS-DMA (global_load_lds, 16 B per lane, no VGPR round trip): window rows h0 - 1 .. h0 + RT,
+    // columns -1 .. W (the zero page outside the image), then the RT dy rows. Chunk c of an image lands at LDS byte
+    // 16 c (lane-linear per wave instruction); its source is logical chunk (c & 7) ^ (position & 7) of the position
+    // (the read-side swizzle of off()).
     {
-      constexpr int NW = (WIN * 8 + 255) / 256, ND = (PX * 8 + 255) / 256, NT = NW + ND;
+      constexpr int NW = (WIN * 8 + 255) / 256, ND = (PX * 8 + 255) / 256;
 #pragma unroll 1
-      for (int i0 = 0; i0 < NT; i0 += 4) {
-        bf16x8_t v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int i = i0 + u;
-          v[u] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-          if (i < NW) {
-            const int c = i * 256 + tid, p = c >> 3, ch = c & 7;
-            const int wr = p / WP, wc = p - wr * WP, h = h0 - 1 + wr, w = wc - 1;
-            if (c < WIN * 8 && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W)
-              v[u] = *reinterpret_cast<const bf16x8_t*>(x + (((long)n * H + h) * W + w) * C + ch * 8);
-          } else if (i < NT) {
-            const int c = (i - NW) * 256 + tid, h = h0 + (c >> 3) / W;
-            if (c < PX * 8 && h < H)
-              v[u] = *reinterpret_cast<const bf16x8_t*>(dy + (((long)n * H + h0) * W) * C + (long)c * 8);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int i = i0 + u;
-          if (i < NW) {
-            const int c = i * 256 + tid;
-            if (c < WIN * 8) *reinterpret_cast<bf16x8_t*>(xw + off(c >> 3, c & 7)) = v[u];
-          } else if (i < NT) {
-            const int c = (i - NW) * 256 + tid;
-            if (c < PX * 8) *reinterpret_cast<bf16x8_t*>(dl + off(c >> 3, c & 7)) = v[u];
-          }
+      for (int i = 0; i < NW; ++i) {
+        const int c = i * 256 + tid;
+        if (c < WIN * 8) {  // lanes past the image stay inactive (they would write into the dy image)
+          const int p = c >> 3, lc = (c & 7) ^ (p & 7);
+          const int wr = p / WP, wc = p - wr * WP, h = h0 - 1 + wr, w = wc - 1;
+          const bool in = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+          const void* src = in ? (const void*)(x + (((long)n * H + h) * W + w) * C + lc * 8) : (const void*)g_wg3_zero;
+          glds16(src, xw + (i * 256 + wid * 64) * 16);
         }
       }
+#pragma unroll 1
+      for (int i = 0; i < ND; ++i) {
+        const int c = i * 256 + tid;
+        if (c < PX * 8) {
+          const int p = c >> 3, lc = (c & 7) ^ (p & 7);
+          const bool in = h0 + p / W < H;
+          const void* src = in ? (const void*)(dy + (((long)n * H + h0) * W + p) * C + lc * 8) : (const void*)g_wg3_zero;
+          glds16(src, dl + (i * 256 + wid * 64) * 16);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
 #pragma unroll 1

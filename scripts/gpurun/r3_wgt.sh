@@ -1,8 +1,8 @@
 #!/bin/bash
-# GPU job (round 3): tiled stage-1 3x3 weight gradient -- tests, A/B on the headline bench, profile.
+# GPU job (round 3): tiled stage-1 3x3 weight gradient (LDS-DMA staging) -- tests, A/B on the headline bench, profile.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gemm_conv_gpu.py tests/test_resnet_gpu.py tests/test_models_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/wgt_tests.log 2>&1 || { tail -40 gpurun_out/wgt_tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gemm_conv_gpu.py tests/test_resnet_gpu.py tests/test_models_gpu.py tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/wgt_tests.log 2>&1 || { tail -40 gpurun_out/wgt_tests.log; exit 1; }
 tail -1 gpurun_out/wgt_tests.log
-bash scripts/gpurun/env_ab.sh "K8S_AMD_WGRAD_TILE=0" "K8S_AMD_WGRAD_TILE=1" || exit 1
+bash scripts/gpurun/env_ab.sh "K8S_AMD_WGRAD_TILE=0" "" "K8S_AMD_BN_MASKED_PLAIN=1" || exit 1
 bash scripts/gpurun/r3_prof.sh
