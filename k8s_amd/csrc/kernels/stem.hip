@@ -67,7 +67,8 @@ __global__ void stem_dw_s2d_kernel(const float* __restrict__ dw4, int K, int R, 
 // y[n][h][w][k] = sum_{i,j<4, c<16} xs[n][h+i][w+j][c] * w4[k][i][j][c]  (4x4 / stride 1 over the s2d image), with the
 // BatchNorm statistics of the stored bf16 outputs. The generic implicit-GEMM kernel gathers every 16-B tap unit
 // from L2 (256 taps x channels per output pixel, 16x re-read); here a block stages the (RT + 3)-row input window of
-// RT whole output rows in LDS once and builds the MFMA operands from it (forward 940 -> 741 us at ResNet-50 b1024).
+// RT whole output rows in LDS once (LDS-DMA) and builds the MFMA operands from it (forward 940 -> 741 us at
+// ResNet-50 b1024 with register staging).
 //   block: 4 waves, wave w = output row r0 + w, all Wo (<= 112, % 16 == 0) pixels as Wo / 16 pixel tiles
 //   MFMA:  C^T[k][px] += W[k][32 taps*ch] . im2col^T  (v_mfma_f32_16x16x32_bf16, A = weight rows from LDS,
 //          B = 16 B of one position's channel half per lane) -> a lane holds 4 consecutive output channels of one
@@ -98,20 +99,24 @@ __global__ void __launch_bounds__(256, 2) stem_conv_fwd_kernel(const uint16_t* _
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int n = blockIdx.x / tiles_per_img, r0 = (blockIdx.x % tiles_per_img) * STEM_RT;
   constexpr int Wo = NMT * 16;
-  // ---- stage the input window (rows r0 .. r0 + RT + 2, contiguous in xs) and the weights
+  // ---- stage the input window (rows r0 .. r0 + RT + 2, contiguous in xs) and the weights by LDS-DMA: chunk c of
+  // an image lands at byte 16 c, its source is the logical chunk the read-side swizzle maps there
   const int rows = min(STEM_RT + 3, Hs - r0);
   const int nch = rows * Ws * 2;  // 16-B chunks
   const uint16_t* src = xs + ((long)n * Hs + r0) * Ws * 16;
-  for (int c = tid; c < nch; c += 256) {
-    const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(src + (long)c * 8);
-    *reinterpret_cast<bf16x8_t*>(xw + stem_xoff(c >> 1, c & 1)) = v;
+#pragma unroll 1
+  for (int c = tid; c - tid < nch; c += 256) {
+    if (c < nch) {
+      const int pos = c >> 1, lh = (c & 1) ^ ((pos >> 3) & 1);
+      glds16(src + (long)pos * 16 + lh * 8, xw + __builtin_amdgcn_readfirstlane(c - lane) * 16);
+    }
   }
-#pragma unroll
+#pragma unroll 1
   for (int i = 0; i < STEM_K * 32 / 256; ++i) {
-    const int c = i * 256 + tid, k = c >> 5, ch = c & 31;
-    const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(w4 + (long)c * 8);
-    *reinterpret_cast<bf16x8_t*>(wl + k * 512 + ((ch ^ (k & 15)) << 4)) = v;
+    const int c = i * 256 + tid, k = c >> 5, lc = (c & 31) ^ (k & 15);
+    glds16(w4 + (long)k * 256 + lc * 8, wl + __builtin_amdgcn_readfirstlane(c - lane) * 16);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   f32x4_t acc[4][NMT];
@@ -222,8 +227,8 @@ void launch_stem_conv_fwd(const uint16_t* xs, const uint16_t* w4, uint16_t* y, f
 // ---------------------------------------------------------------- the s2d stem weight gradient, LDS-tiled
 // dw4[k][i][j][c] = sum_{n,h,w} dy[n][h][w][k] * xs[n][h+i][w+j][c]: a 64 x 256 product reduced over all N*Ho*Wo
 // output pixels. Persistent blocks (2 per CU) sweep tiles of RT = 2 output rows; per tile the input window
-// [RT + 3][Ws][16] and the dy rows [RT * Wo][64] are staged in LDS (the next tile's through registers behind this
-// tile's MFMAs), both operands are read transposed (ds_read_b64_tr_b16: 4 pixels x 16 channels per 16 lanes), and
+// [RT + 3][Ws][16] and the dy rows [RT * Wo][64] are staged in LDS by LDS-DMA (register staging with the next
+// tile prefetched behind the MFMAs measured 668 us at b1024), both operands are read transposed (ds_read_b64_tr_b16: 4 pixels x 16 channels per 16 lanes), and
 // the block's fp32 partial stays in 64 accumulator registers per lane until its last tile; the partials are
 // summed by splitk_reduce. (The generic split-K implicit GEMM gathers every 16-B tap unit from L2 and fills only
 // half of its 128-row tiles with the 64 output channels.)
@@ -231,7 +236,7 @@ void launch_stem_conv_fwd(const uint16_t* xs, const uint16_t* w4, uint16_t* y, f
 constexpr int SWG_RT = 2;
 constexpr int SWG_WIN = (SWG_RT + 3) * (STEM_WMAX + 3) * 32;   // 20,960 B
 constexpr int SWG_DY = SWG_RT * STEM_WMAX * 128;               // 32 KB
-constexpr int SWG_PFX = (SWG_WIN / 16 + 255) / 256, SWG_PFD = SWG_DY / 16 / 256;
+__device__ __attribute__((aligned(64))) uint16_t g_stem_zero[64];  // source of dy rows past the image
 
 __device__ __forceinline__ int swg_dyoff(int px, int ch16) { return px * 128 + ((ch16 ^ (px & 7)) << 4); }
 
@@ -245,37 +250,30 @@ __global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(const uint16_t* __re
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int li = lane & 15, G = lane >> 4, q4 = li >> 2, p4 = li & 3;
   constexpr int Wo = NMT * 16, PX = SWG_RT * Wo, NKS = PX / 32;
-  bf16x8_t px_[SWG_PFX], pd[SWG_PFD];
-  int nch = 0, npx = 0;
-  auto fetch = [&](int t) {
+  // stage tile t by LDS-DMA (chunk c of an image at byte 16 c, sourced from the logical chunk the read swizzle maps
+  // there; dy rows past Ho from the zero page); the CU's other blocks compute while one stages
+  auto stage = [&](int t) {
     const int n = t / tiles_per_img, r0 = (t % tiles_per_img) * SWG_RT;
-    nch = min(SWG_RT + 3, Hs - r0) * Ws * 2;
-    npx = min(SWG_RT, Ho - r0) * Wo;
+    const int nch = min(SWG_RT + 3, Hs - r0) * Ws * 2;
+    const int npx = min(SWG_RT, Ho - r0) * Wo;
     const uint16_t* sx = xs + ((long)n * Hs + r0) * Ws * 16;
     const uint16_t* sd = dy + (((long)n * Ho + r0) * Wo) * STEM_K;
-#pragma unroll
-    for (int i = 0; i < SWG_PFX; ++i) {
-      const int c = i * 256 + tid;
-      if (c < nch) px_[i] = *reinterpret_cast<const bf16x8_t*>(sx + (long)c * 8);
+#pragma unroll 1
+    for (int c = tid; c - tid < nch; c += 256) {
+      if (c < nch) {
+        const int pos = c >> 1, lh = (c & 1) ^ ((pos >> 3) & 1);
+        glds16(sx + (long)pos * 16 + lh * 8, xw + __builtin_amdgcn_readfirstlane(c - lane) * 16);
+      }
     }
-#pragma unroll
-    for (int i = 0; i < SWG_PFD; ++i) {
-      const int c = i * 256 + tid;  // 16-B chunk: pixel c >> 3, channels 8 (c & 7) ..
-      pd[i] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-      if ((c >> 3) < npx) pd[i] = *reinterpret_cast<const bf16x8_t*>(sd + (long)c * 8);
+#pragma unroll 1
+    for (int c = tid; c - tid < PX * 8; c += 256) {
+      if (c < PX * 8) {
+        const int px = c >> 3, lc = (c & 7) ^ (px & 7);
+        glds16(px < npx ? (const void*)(sd + (long)px * STEM_K + lc * 8) : (const void*)g_stem_zero,
+               dl + __builtin_amdgcn_readfirstlane(c - lane) * 16);
+      }
     }
-  };
-  auto stash = [&]() {
-#pragma unroll
-    for (int i = 0; i < SWG_PFX; ++i) {
-      const int c = i * 256 + tid;
-      if (c < nch) *reinterpret_cast<bf16x8_t*>(xw + stem_xoff(c >> 1, c & 1)) = px_[i];
-    }
-#pragma unroll
-    for (int i = 0; i < SWG_PFD; ++i) {
-      const int c = i * 256 + tid;
-      if (c < PX * 8) *reinterpret_cast<bf16x8_t*>(dl + swg_dyoff(c >> 3, c & 7)) = pd[i];
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
   f32x4_t acc[4][4];  // [k tile][q tile]: lane holds out[16 kt + 4 G + r][64 wid + 16 qt + li]
 #pragma unroll
@@ -283,15 +281,9 @@ __global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(const uint16_t* __re
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  int t = blockIdx.x;
-  if (t < ntiles) {
-    fetch(t);
-    stash();
-  }
-  __syncthreads();
-  for (; t < ntiles; t += gridDim.x) {
-    const int tn = t + gridDim.x;
-    if (tn < ntiles) fetch(tn);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    stage(t);
+    __syncthreads();
 #pragma unroll 1
     for (int ks = 0; ks < NKS; ++ks) {
       // k-step: pixels 32 ks + 8 G + (0..7) of the tile (row-major over RT x Wo; 8-pixel runs never straddle a row)
@@ -318,11 +310,7 @@ __global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(const uint16_t* __re
         for (int kt = 0; kt < 4; ++kt) acc[kt][qt] = mfma16(af[kt], bf, acc[kt][qt]);
       }
     }
-    __syncthreads();  // every wave is done with this tile's LDS
-    if (tn < ntiles) {
-      stash();
-      __syncthreads();
-    }
+    __syncthreads();  // every wave is done with this tile's LDS before the next stage
   }
   float* out = ws + (long)blockIdx.x * (STEM_K * 256);
 #pragma unroll

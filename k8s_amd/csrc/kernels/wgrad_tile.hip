@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(256, 2) wgrad3x3_c64_kernel(const uint16_t* __
           const int wr = p / WP, wc = p - wr * WP, h = h0 - 1 + wr, w = wc - 1;
           const bool in = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
           const void* src = in ? (const void*)(x + (((long)n * H + h) * W + w) * C + lc * 8) : (const void*)g_wg3_zero;
-          glds16(src, xw + (i * 256 + wid * 64) * 16);
+          glds16(src, xw + __builtin_amdgcn_readfirstlane(i * 256 + wid * 64) * 16);
         }
       }
 #pragma unroll 1
@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(256, 2) wgrad3x3_c64_kernel(const uint16_t* __
           const int p = c >> 3, lc = (c & 7) ^ (p & 7);
           const bool in = h0 + p / W < H;
           const void* src = in ? (const void*)(dy + (((long)n * H + h0) * W + p) * C + lc * 8) : (const void*)g_wg3_zero;
-          glds16(src, dl + (i * 256 + wid * 64) * 16);
+          glds16(src, dl + __builtin_amdgcn_readfirstlane(i * 256 + wid * 64) * 16);
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
