@@ -185,11 +185,12 @@ void launch_stem_conv_fwd(const uint16_t* xs, const uint16_t* w4, uint16_t* y, f
                           hipStream_t st);
 // out[i] (+)= sum over `splits` fp32 slabs of mn elements (gemm.hip)
 void splitk_reduce(const float* ws, int splits, long mn, float* out, bool accumulate, hipStream_t st);
-// LDS-tiled 3x3 / s1 / p1 weight gradient for C = K = 64 (ResNet stage 1), ws = wgrad3x3_c64_blocks x 64 x 576 fp32
-bool wgrad3x3_c64_ok(int C, int K, int R, int S, int stride, int pad, int W);
-int wgrad3x3_c64_blocks(int N, int H);
-void launch_wgrad3x3_c64(const uint16_t* x, const uint16_t* dy, float* ws, float* dw, int N, int H, int W,
-                         bool accumulate, hipStream_t st);
+// LDS-tiled 3x3 / s1 / p1 weight gradient (wgrad_tile.hip), C == K in 64 pieces; ws = wgrad3x3_tiled_workspace floats
+bool wgrad3x3_tiled_ok(int C, int K, int R, int S, int stride, int pad, int W);
+int wgrad3x3_tiled_blocks(int N, int H, int W, int C);
+long wgrad3x3_tiled_workspace(int N, int H, int W, int C);
+void launch_wgrad3x3_tiled(const uint16_t* x, const uint16_t* dy, float* ws, float* dw, int N, int H, int W, int C,
+                           bool accumulate, hipStream_t st);
 // the s2d stem weight gradient (LDS-tiled, persistent blocks; ws = stem_wgrad_blocks(N, Hs) x 64 x 256 fp32 partials)
 int stem_wgrad_blocks(int N, int Hs);
 void launch_stem_wgrad(const uint16_t* xs, const uint16_t* dy, float* ws, float* dw4, int N, int Hs, int Ws,

@@ -226,7 +226,7 @@ void launch_stem_conv_fwd(const uint16_t* xs, const uint16_t* w4, uint16_t* y, f
 
 // ---------------------------------------------------------------- the s2d stem weight gradient, LDS-tiled
 // dw4[k][i][j][c] = sum_{n,h,w} dy[n][h][w][k] * xs[n][h+i][w+j][c]: a 64 x 256 product reduced over all N*Ho*Wo
-// output pixels. Persistent blocks (2 per CU) sweep tiles of RT = 2 output rows; per tile the input window
+// output pixels. Persistent blocks (3 per CU) sweep tiles of RT = 2 output rows; per tile the input window
 // [RT + 3][Ws][16] and the dy rows [RT * Wo][64] are staged in LDS by LDS-DMA (register staging with the next
 // tile prefetched behind the MFMAs measured 668 us at b1024), both operands are read transposed (ds_read_b64_tr_b16: 4 pixels x 16 channels per 16 lanes), and
 // the block's fp32 partial stays in 64 accumulator registers per lane until its last tile; the partials are
@@ -241,7 +241,7 @@ __device__ __attribute__((aligned(64))) uint16_t g_stem_zero[64];  // source of 
 __device__ __forceinline__ int swg_dyoff(int px, int ch16) { return px * 128 + ((ch16 ^ (px & 7)) << 4); }
 
 template <int NMT>  // Wo / 16
-__global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(const uint16_t* __restrict__ xs,
+__global__ void __launch_bounds__(256, 3) stem_wgrad_kernel(const uint16_t* __restrict__ xs,
                                                            const uint16_t* __restrict__ dy, float* __restrict__ ws,
                                                            int Hs, int Ws, int Ho, int tiles_per_img, int ntiles) {
   __shared__ __attribute__((aligned(1024))) char smem[SWG_WIN + SWG_DY];
@@ -323,7 +323,7 @@ __global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(const uint16_t* __re
 
 int stem_wgrad_blocks(int N, int Hs) {
   const long ntiles = (long)N * ((Hs - 3 + SWG_RT - 1) / SWG_RT);
-  return (int)std::min<long>(ntiles, 512);
+  return (int)std::min<long>(ntiles, 768);  // persistent: 3 blocks per CU (47 KB LDS, ~130 VGPRs)
 }
 
 void launch_stem_wgrad(const uint16_t* xs, const uint16_t* dy, float* ws, float* dw4, int N, int Hs, int Ws,

@@ -1,15 +1,18 @@
-// LDS-tiled weight gradient of the ResNet-50 stage-1 3x3 convolution (C = K = 64, 56 x 56, stride 1, pad 1).
+// LDS-tiled weight gradient of the ResNet-50 stride-1 3x3 convolutions (C = K = 64 / 128 / 256 at 56 / 28 / 14
+// pixels square, pad 1).
 //
-//   dw[k][r][s][c] = sum_{n,h,w} dy[n][h][w][k] * x[n][h + r - 1][w + s - 1][c]        (a 64 x 576 product,
-//                                                                                     reduced over N*H*W pixels)
-// The generic split-K implicit GEMM (gemm.hip ConvWgB) ran this shape at ~270 TF/s: its 128-row tiles are half
-// empty with 64 output channels, and every 16-B tap unit of im2col(x) is gathered from L2 nine times. Here
-// persistent blocks (2 per CU) sweep tiles of RT = 4 output rows: the (RT + 2)-row zero-padded input window and
-// the RT dy rows are staged in LDS once per tile and both MFMA operands are read from them transposed
-// (ds_read_b64_tr_b16: 4 pixels x 16 channels per 16 lanes), staged by LDS-DMA; each block keeps its fp32 partial of the whole
-// 64 x 576 gradient in accumulator registers (wave w: output columns 144 w .. 144 w + 143) until its last tile,
-// and splitk_reduce sums the blocks' partials into dw.
+//   dw[k][r][s][c] = sum_{n,h,w} dy[n][h][w][k] * x[n][h + r - 1][w + s - 1][c]
+// The generic split-K implicit GEMM (gemm.hip ConvWgB) gathers every 16-B tap unit of im2col(x) from L2 nine
+// times and, at K = 64, fills half of its 128-row tiles (~270 TF/s at stage 1). Here the product is cut into
+// 64 x 576 pieces -- output channels k0 .. k0 + 63 x (9 taps x input channels c0 .. c0 + 63), one piece per
+// blockIdx.y -- and persistent blocks (2 per CU) sweep tiles of RT output rows: per tile the (RT + 2)-row
+// zero-padded input window of the 64-channel slice and the RT dy rows of the 64-output slice are staged in LDS by
+// LDS-DMA, both MFMA operands are read from them transposed (ds_read_b64_tr_b16: 4 pixels x 16 channels per 16
+// lanes), and each block keeps its fp32 partial of the piece in accumulator registers (wave w: output columns
+// 144 w .. 144 w + 143) until its last tile; wg3_reduce1/2 sum the blocks' partials into dw.
 //   LDS images: [position][64 ch] bf16, 128-B rows, 16-B chunk c of row p at c ^ (p & 7) (window and dy alike).
+//   tile: RT rows x W pixels, RT * W = 224 (7 k-steps of 32 pixels; a tile may run past the image: zero dy rows;
+//   the W = 16 test shape: 2 rows)
 #include <algorithm>
 #include <stdexcept>
 
@@ -20,24 +23,25 @@
 namespace k8s_amd {
 
 namespace wg3 {
-constexpr int RT = 4, C = 64, NQ = 9 * C;  // 576 output columns (tap, channel)
+constexpr int CS = 64, NQ = 9 * CS;  // a piece: 64 output channels x 576 (tap, input channel) columns
 __device__ __attribute__((aligned(64))) uint16_t g_wg3_zero[64];  // source of the zero padding
 
 __device__ __forceinline__ int off(int p, int ch16) { return p * 128 + ((ch16 ^ (p & 7)) << 4); }
 
-template <int W>
-__global__ void __launch_bounds__(256, 2) wgrad3x3_c64_kernel(const uint16_t* __restrict__ x,
-                                                             const uint16_t* __restrict__ dy, float* __restrict__ ws,
-                                                             int H, int tiles_per_img, int ntiles) {
+template <int W, int RT>
+__global__ void __launch_bounds__(256, 2) wgrad3x3_kernel(const uint16_t* __restrict__ x,
+                                                         const uint16_t* __restrict__ dy, float* __restrict__ ws,
+                                                         int H, int C, int K, int tiles_per_img, int ntiles) {
   constexpr int WP = W + 2, WIN = (RT + 2) * WP, PX = RT * W, NKS = PX / 32;
-  static_assert(W % 8 == 0 && PX % 32 == 0, "8-pixel runs inside one row, whole 32-pixel k steps");
+  static_assert(PX % 32 == 0, "whole 32-pixel k steps");
   __shared__ __attribute__((aligned(1024))) char smem[(WIN + PX) * 128];
   char* const xw = smem;
   char* const dl = smem + WIN * 128;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int li = lane & 15, G = lane >> 4, q4 = li >> 2, p4 = li & 3;
+  const int cpieces = C / CS, k0 = (blockIdx.y / cpieces) * CS, c0 = (blockIdx.y % cpieces) * CS;
 
-  f32x4_t acc[4][9];  // [k tile][q tile 9 wid + j]: lane holds dw[16 kt + 4 G + r][16 (9 wid + j) + li]
+  f32x4_t acc[4][9];  // [k tile][q tile 9 wid + j]: lane holds piece[16 kt + 4 G + r][16 (9 wid + j) + li]
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -58,7 +62,8 @@ __global__ void __launch_bounds__(256, 2) wgrad3x3_c64_kernel(const uint16_t* __
           const int p = c >> 3, lc = (c & 7) ^ (p & 7);
           const int wr = p / WP, wc = p - wr * WP, h = h0 - 1 + wr, w = wc - 1;
           const bool in = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-          const void* src = in ? (const void*)(x + (((long)n * H + h) * W + w) * C + lc * 8) : (const void*)g_wg3_zero;
+          const void* src =
+              in ? (const void*)(x + (((long)n * H + h) * W + w) * C + c0 + lc * 8) : (const void*)g_wg3_zero;
           glds16(src, xw + __builtin_amdgcn_readfirstlane(i * 256 + wid * 64) * 16);
         }
       }
@@ -68,7 +73,8 @@ __global__ void __launch_bounds__(256, 2) wgrad3x3_c64_kernel(const uint16_t* __
         if (c < PX * 8) {
           const int p = c >> 3, lc = (c & 7) ^ (p & 7);
           const bool in = h0 + p / W < H;
-          const void* src = in ? (const void*)(dy + (((long)n * H + h0) * W + p) * C + lc * 8) : (const void*)g_wg3_zero;
+          const void* src =
+              in ? (const void*)(dy + (((long)n * H + h0) * W + p) * K + k0 + lc * 8) : (const void*)g_wg3_zero;
           glds16(src, dl + __builtin_amdgcn_readfirstlane(i * 256 + wid * 64) * 16);
         }
       }
@@ -77,7 +83,7 @@ __global__ void __launch_bounds__(256, 2) wgrad3x3_c64_kernel(const uint16_t* __
     __syncthreads();
 #pragma unroll 1
     for (int ks = 0; ks < NKS; ++ks) {
-      const int pb = 32 * ks + 8 * G;  // this lane group's 8 pixels of the k step (one row: W % 8 == 0)
+      const int pb = 32 * ks + 8 * G;  // this lane group's 8 pixels of the k step
       mfma_bf16x8 af[4];               // dy^T: row = output channel 16 kt + li, k = 8 pixels
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
@@ -86,15 +92,17 @@ __global__ void __launch_bounds__(256, 2) wgrad3x3_c64_kernel(const uint16_t* __
         const short4_t hi = tr16(dl + off(pb + 4 + q4, ch16) + (p4 & 1) * 8);
         af[kt] = join8(lo, hi);
       }
-      const int r0 = pb / W, c0 = pb - r0 * W;  // output row / column of the group's first pixel
+      // window positions of this lane's two pixels (pb + q4, pb + 4 + q4) at tap (0, 0)
+      const int pa = pb + q4, pc = pb + 4 + q4;
+      const int ra = pa / W, rc = pc / W;
+      const int posa = ra * WP + (pa - ra * W), posc = rc * WP + (pc - rc * W);
 #pragma unroll
       for (int j = 0; j < 9; ++j) {
         const int qt = 9 * wid + j, tap = qt >> 2, cq = qt & 3, tr = tap / 3, ts = tap - tr * 3;
-        // X: rows = the 8 pixels' window positions shifted by the tap, column = channel 16 cq + 4 p4 ..
-        const int pos = (r0 + tr) * WP + c0 + ts + q4;
+        const int toff = tr * WP + ts;
         const int ch16 = 2 * cq + (p4 >> 1);
-        const short4_t lo = tr16(xw + off(pos, ch16) + (p4 & 1) * 8);
-        const short4_t hi = tr16(xw + off(pos + 4, ch16) + (p4 & 1) * 8);
+        const short4_t lo = tr16(xw + off(posa + toff, ch16) + (p4 & 1) * 8);
+        const short4_t hi = tr16(xw + off(posc + toff, ch16) + (p4 & 1) * 8);
         const mfma_bf16x8 bf = join8(lo, hi);
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) acc[kt][j] = mfma16(af[kt], bf, acc[kt][j]);
@@ -102,7 +110,7 @@ __global__ void __launch_bounds__(256, 2) wgrad3x3_c64_kernel(const uint16_t* __
     }
     __syncthreads();  // every wave is done with this tile's LDS before the next stage
   }
-  float* out = ws + (long)blockIdx.x * (C * NQ);
+  float* out = ws + ((long)blockIdx.y * gridDim.x + blockIdx.x) * (CS * NQ);
 #pragma unroll
   for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
@@ -110,27 +118,97 @@ __global__ void __launch_bounds__(256, 2) wgrad3x3_c64_kernel(const uint16_t* __
 #pragma unroll
       for (int r = 0; r < 4; ++r) out[(kt * 16 + G * 4 + r) * NQ + (9 * wid + j) * 16 + li] = acc[kt][j][r];
 }
-}  // namespace wg3
 
-bool wgrad3x3_c64_ok(int C, int K, int R, int S, int stride, int pad, int W) {
-  return C == 64 && K == 64 && R == 3 && S == 3 && stride == 1 && pad == 1 && (W == 56 || W == 16);
+// Two-pass deterministic sum of the nb per-block partials of every piece: pass 1 (blockIdx.y = slab group s of SG)
+// sums slabs s, s + SG, ... into part[s]; pass 2 sums the SG group partials and scatters the piece into
+// dw[k0 + kk][tap][c0 + cc] (+)=. (One pass with a 512-slab serial loop per output ran 125 us at stage 1.)
+__global__ void __launch_bounds__(256) wg3_reduce1_kernel(const float* __restrict__ ws, int nb, int pieces, int SG,
+                                                          float* __restrict__ part) {
+  const long n4 = (long)pieces * CS * NQ / 4;
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;  // float4 index over [pieces][64][576]
+  if (e >= n4) return;
+  const int piece = (int)(e / (CS * NQ / 4));
+  const long rem4 = e - (long)piece * (CS * NQ / 4);
+  const float4* src = reinterpret_cast<const float4*>(ws) + (long)piece * nb * (CS * NQ / 4) + rem4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+  for (int b = blockIdx.y; b < nb; b += SG) {
+    const float4 v = src[(long)b * (CS * NQ / 4)];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  reinterpret_cast<float4*>(part)[(long)blockIdx.y * n4 + e] = s;
 }
 
-int wgrad3x3_c64_blocks(int N, int H) { return (int)std::min<long>((long)N * ((H + wg3::RT - 1) / wg3::RT), 512); }
+__global__ void __launch_bounds__(256) wg3_reduce2_kernel(const float* __restrict__ part, int SG, int C, int pieces,
+                                                          float* __restrict__ dw, int accumulate) {
+  const long n4 = (long)pieces * CS * NQ / 4;
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n4) return;
+  const int piece = (int)(e / (CS * NQ / 4));
+  const int rem = (int)(e - (long)piece * (CS * NQ / 4)) * 4;
+  const int kk = rem / NQ, q = rem - kk * NQ, tap = q / CS, cc = q - tap * CS;
+  const int cpieces = C / CS, k0 = (piece / cpieces) * CS, c0 = (piece % cpieces) * CS;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int g = 0; g < SG; ++g) {
+    const float4 v = reinterpret_cast<const float4*>(part)[(long)g * n4 + e];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  float4* d = reinterpret_cast<float4*>(dw + ((long)(k0 + kk) * 9 + tap) * C + c0 + cc);
+  if (accumulate) {
+    const float4 o = *d;
+    s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
+  }
+  *d = s;
+}
+}  // namespace wg3
 
-void launch_wgrad3x3_c64(const uint16_t* x, const uint16_t* dy, float* ws, float* dw, int N, int H, int W,
-                         bool accumulate, hipStream_t st) {
-  const int tpi = (H + wg3::RT - 1) / wg3::RT;
+// stride-1 / pad-1 3x3, C == K in {64, 128, 256} with the matching square image side (56 / 28 / 14), or the small
+// W = 16 test shape at 64 channels
+bool wgrad3x3_tiled_ok(int C, int K, int R, int S, int stride, int pad, int W) {
+  if (R != 3 || S != 3 || stride != 1 || pad != 1 || C != K) return false;
+  return (C == 64 && (W == 56 || W == 16)) || (C == 128 && W == 28) || (C == 256 && W == 14);
+}
+
+static int wg3_rt(int W) { return W == 56 ? 4 : W == 28 ? 8 : W == 16 ? 2 : 16; }
+
+int wgrad3x3_tiled_blocks(int N, int H, int W, int C) {
+  const int pieces = (C / wg3::CS) * (C / wg3::CS);
+  const long tiles = (long)N * ((H + wg3_rt(W) - 1) / wg3_rt(W));
+  return (int)std::max<long>(1, std::min<long>(tiles, std::max(512 / pieces, 32)));
+}
+
+static int wg3_groups(int nb) { return std::max(1, nb / 16); }
+
+long wgrad3x3_tiled_workspace(int N, int H, int W, int C) {
+  const long pieces = (long)(C / wg3::CS) * (C / wg3::CS);
+  const int nb = wgrad3x3_tiled_blocks(N, H, W, C);
+  return pieces * (nb + wg3_groups(nb)) * wg3::CS * wg3::NQ;  // block partials + slab-group partials
+}
+
+void launch_wgrad3x3_tiled(const uint16_t* x, const uint16_t* dy, float* ws, float* dw, int N, int H, int W, int C,
+                           bool accumulate, hipStream_t st) {
+  const int rt = wg3_rt(W), tpi = (H + rt - 1) / rt;
   const long ntiles = (long)N * tpi;
-  if (ntiles >= (1L << 31)) throw std::runtime_error("wgrad3x3_c64: too many tiles");
-  const int nb = wgrad3x3_c64_blocks(N, H);
+  if (ntiles >= (1L << 31)) throw std::runtime_error("wgrad3x3_tiled: too many tiles");
+  const int pieces = (C / wg3::CS) * (C / wg3::CS);
+  const int nb = wgrad3x3_tiled_blocks(N, H, W, C);
+  const dim3 grid(nb, pieces), blk(256);
   if (W == 56)
-    hipLaunchKernelGGL(wg3::wgrad3x3_c64_kernel<56>, dim3(nb), dim3(256), 0, st, x, dy, ws, H, tpi, (int)ntiles);
+    hipLaunchKernelGGL((wg3::wgrad3x3_kernel<56, 4>), grid, blk, 0, st, x, dy, ws, H, C, C, tpi, (int)ntiles);
+  else if (W == 28)
+    hipLaunchKernelGGL((wg3::wgrad3x3_kernel<28, 8>), grid, blk, 0, st, x, dy, ws, H, C, C, tpi, (int)ntiles);
   else if (W == 16)
-    hipLaunchKernelGGL(wg3::wgrad3x3_c64_kernel<16>, dim3(nb), dim3(256), 0, st, x, dy, ws, H, tpi, (int)ntiles);
+    hipLaunchKernelGGL((wg3::wgrad3x3_kernel<16, 2>), grid, blk, 0, st, x, dy, ws, H, C, C, tpi, (int)ntiles);
+  else if (W == 14)
+    hipLaunchKernelGGL((wg3::wgrad3x3_kernel<14, 16>), grid, blk, 0, st, x, dy, ws, H, C, C, tpi, (int)ntiles);
   else
-    throw std::runtime_error("wgrad3x3_c64: W must be 56 or 16");
-  splitk_reduce(ws, nb, (long)wg3::C * wg3::NQ, dw, accumulate, st);
+    throw std::runtime_error("wgrad3x3_tiled: unsupported width");
+  const long n4 = (long)pieces * wg3::CS * wg3::NQ / 4;
+  const int SG = wg3_groups(nb);
+  float* part = ws + (long)pieces * nb * wg3::CS * wg3::NQ;
+  hipLaunchKernelGGL(wg3::wg3_reduce1_kernel, dim3(cdiv(n4, 256), SG), dim3(256), 0, st, ws, nb, pieces, SG, part);
+  hipLaunchKernelGGL(wg3::wg3_reduce2_kernel, dim3(cdiv(n4, 256)), dim3(256), 0, st, part, SG, C, pieces, dw,
+                     accumulate ? 1 : 0);
 }
 
 }  // namespace k8s_amd

@@ -518,11 +518,11 @@ void conv_wgrad(Tensor x, Tensor dy, Tensor dw, int64_t stride, int64_t pad, int
   const int Ho = conv_out(H, R, stride, pad, dil), Wo = conv_out(W, S, stride, pad, dil);
   TORCH_CHECK(dy.size(0) == N && dy.size(1) == Ho && dy.size(2) == Wo && dy.size(3) == K, "dy shape mismatch");
   const float* xf = xform_ptr(xform, C);
-  const char* wt_env = std::getenv("K8S_AMD_WGRAD_TILE");  // =0: the stage-1 3x3 shape on the generic kernel (A/B)
+  const char* wt_env = std::getenv("K8S_AMD_WGRAD_TILE");  // =0: these 3x3 shapes on the generic kernels (A/B)
   if (!xf && !(wt_env && wt_env[0] == '0') && dil == 1 && dy.is_contiguous() && x.is_contiguous() && Ho == H &&
-      Wo == W && k8s_amd::wgrad3x3_c64_ok(C, K, R, S, (int)stride, (int)pad, W)) {
-    auto wsp = torch::empty({(long)k8s_amd::wgrad3x3_c64_blocks(N, H) * 64 * 576}, dw.options());
-    k8s_amd::launch_wgrad3x3_c64(cbf(x), cbf(dy), f32(wsp), f32(dw), N, H, W, accumulate, cur_stream());
+      Wo == W && H == W && k8s_amd::wgrad3x3_tiled_ok(C, K, R, S, (int)stride, (int)pad, W)) {
+    auto wsp = torch::empty({k8s_amd::wgrad3x3_tiled_workspace(N, H, W, C)}, dw.options());
+    k8s_amd::launch_wgrad3x3_tiled(cbf(x), cbf(dy), f32(wsp), f32(dw), N, H, W, C, accumulate, cur_stream());
     return;
   }
   const char* ws_env = std::getenv("K8S_AMD_WGRAD_STREAM");  // =0: generic split-K GEMM (A/B)

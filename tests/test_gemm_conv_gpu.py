@@ -432,17 +432,17 @@ def test_bn_relu_conv_matches_separate_ops(cuda):
     assert _rel(g1, g2) < 1e-2
 
 
-@pytest.mark.parametrize("N,H,W", [(2, 56, 56), (3, 13, 16)])
+@pytest.mark.parametrize("N,H,W,C", [(2, 56, 56, 64), (3, 13, 16, 64), (2, 28, 28, 128), (3, 14, 14, 256)])
 @pytest.mark.parametrize("accumulate", [False, True])
-def test_wgrad3x3_c64_tiled_vs_fp32(cuda, N, H, W, accumulate):
-    """LDS-tiled stage-1 3x3 weight gradient (wgrad_tile.hip; C = K = 64, stride 1, pad 1) against the fp32 weight
-    gradient of the same convolution (H = 13: a partial last row tile)."""
+def test_wgrad3x3_tiled_vs_fp32(cuda, N, H, W, C, accumulate):
+    """LDS-tiled 3x3 weight gradient (wgrad_tile.hip; C = K in 64-channel pieces, stride 1, pad 1) against the fp32
+    weight gradient of the same convolution (H = 13 / 14: tiles running past the image)."""
     torch.manual_seed(5)
-    x = torch.randn(N, H, W, 64, device=cuda).bfloat16()
-    dy = torch.randn(N, H, W, 64, device=cuda).bfloat16()
-    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (64, 64, 3, 3), dy.float().permute(0, 3, 1, 2),
+    x = torch.randn(N, H, W, C, device=cuda).bfloat16()
+    dy = torch.randn(N, H, W, C, device=cuda).bfloat16()
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (C, C, 3, 3), dy.float().permute(0, 3, 1, 2),
                                       1, 1).permute(0, 2, 3, 1)
-    base = torch.randn(64, 3, 3, 64, device=cuda) if accumulate else torch.zeros(64, 3, 3, 64, device=cuda)
+    base = torch.randn(C, 3, 3, C, device=cuda) if accumulate else torch.zeros(C, 3, 3, C, device=cuda)
     dw = base.clone()
     _C().conv_wgrad(x, dy, dw, 1, 1, 1, 0, accumulate, None)
     assert _rel(dw, ref + (base if accumulate else 0)) < 1e-3
