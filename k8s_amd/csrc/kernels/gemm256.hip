@@ -48,6 +48,7 @@ struct Epi {
   int act;            // 0 none, 1 relu, 2 gelu(tanh)
   int accumulate;     // C += result
   float alpha;
+  long slab;          // split-K: split z writes plain fp32 at c + z * slab (0: no split)
 };
 
 // GELU(tanh) = x * sigmoid(2u): v_exp_f32 + v_rcp_f32 (see gemm.hip's gelu_tanh)
@@ -312,7 +313,8 @@ __device__ __forceinline__ void tie(typename S::Raw (&r)[N]) {
 }
 
 template <class AS, class BS, int DIAG = 0>
-__global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, g256::Epi E, int M, int N, int K) {
+__global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, g256::Epi E, int M, int N, int K,
+                                                                   int kps) {
   using namespace g256;
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -334,10 +336,13 @@ __global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, 
   const int tn = (wg % group) / gm;
   const int m0 = tm * 256, n0 = tn * 256;
 
-  const uint16_t* ca0 = A.cursor(tid, 0, m0);
-  const uint16_t* ca1 = A.cursor(tid, 1, m0);
-  const uint16_t* cb0 = B.cursor(tid, 0, n0);
-  const uint16_t* cb1 = B.cursor(tid, 1, n0);
+  // split-K (blockIdx.y): this block reduces K range [koff, koff + kps) into its own fp32 slab
+  const long koff = (long)blockIdx.y * kps;
+  if (E.slab) E.c = reinterpret_cast<float*>(E.c) + blockIdx.y * E.slab;
+  const uint16_t* ca0 = A.cursor(tid, 0, m0) + (AS::kmajor ? koff : koff * A.ld);
+  const uint16_t* ca1 = A.cursor(tid, 1, m0) + (AS::kmajor ? koff : koff * A.ld);
+  const uint16_t* cb0 = B.cursor(tid, 0, n0) + (BS::kmajor ? koff : koff * B.ld);
+  const uint16_t* cb1 = B.cursor(tid, 1, n0) + (BS::kmajor ? koff : koff * B.ld);
   const long sa = A.step(), sb = B.step();
   const int dma_off = wid * 1024;
   auto issue = [&](int slot) {
@@ -355,7 +360,7 @@ __global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, 
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = K / KS;
+  const int nk = (int)(min((long)K, koff + kps) - koff) / KS;
   issue(0);
   if (nk > 1) issue(1);
   if (nk > 2) issue(2);
@@ -410,13 +415,15 @@ __global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, 
 
 namespace g256 {
 template <class AS, class BS>
-static void launch_ring(const AS& a, const BS& b, const Epi& e, int M, int N, int K, hipStream_t st) {
+static void launch_ring(const AS& a, const BS& b, const Epi& e, int M, int N, int K, int splits, hipStream_t st) {
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  const int kps = K / splits;  // a multiple of 64 (gemm256_choose_splits)
+  const dim3 grid(tiles, splits);
   const char* dg = getenv("K8S_AMD_GEMM256_DIAG");
   if (dg && atoi(dg) == 1)
-    hipLaunchKernelGGL((g256r::gemm256r_kernel<AS, BS, 1>), dim3(tiles), dim3(THREADS), 0, st, a, b, e, M, N, K);
+    hipLaunchKernelGGL((g256r::gemm256r_kernel<AS, BS, 1>), grid, dim3(THREADS), 0, st, a, b, e, M, N, K, kps);
   else
-    hipLaunchKernelGGL((g256r::gemm256r_kernel<AS, BS>), dim3(tiles), dim3(THREADS), 0, st, a, b, e, M, N, K);
+    hipLaunchKernelGGL((g256r::gemm256r_kernel<AS, BS>), grid, dim3(THREADS), 0, st, a, b, e, M, N, K, kps);
 }
 
 }  // namespace g256
@@ -440,20 +447,40 @@ bool gemm256_eligible(int M, int N, int K, bool a_kmajor, bool b_kmajor) {
   return c256 <= c128;
 }
 
+// Split-K for the tall-K fp32 products (weight gradients of small output, e.g. ResNet's 1x1 layers: 256 x 1024
+// outputs over 200k pixels): the smallest split count that puts >= 192 blocks on the chip, each split a multiple of
+// 64 deep and >= 1024 (the ring's prologue / epilogue), at most 64 splits. 1 when the tiles alone fill the chip.
+int gemm256_choose_splits(int M, int N, int K) {
+  const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
+  int best = 1;
+  for (int s = 2; s <= 64; ++s) {
+    if (tiles * (s / 2) >= 192) break;  // the previous s already filled the chip
+    if (K % (64 * s) != 0 || K / s < 1024) continue;
+    best = s;
+    if (tiles * s >= 192) break;
+  }
+  return best;
+}
+
 void launch_gemm256(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                     long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre,
-                    bool accumulate, float alpha, hipStream_t st) {
+                    bool accumulate, float alpha, hipStream_t st, int splits, float* ws) {
   if (K % 64 != 0) throw std::runtime_error("gemm256: K must be a multiple of 64");
-  g256::Epi e{C, ldc, bias, pre, c_f32 ? 1 : 0, act, accumulate ? 1 : 0, alpha};
+  if (splits < 1) splits = 1;
+  if (splits > 1 && (!c_f32 || bias || act || pre || !ws || K % (64 * splits) != 0 || ldc != N))
+    throw std::runtime_error("gemm256 split-K: plain fp32 output, K % (64 * splits) == 0, a workspace");
+  g256::Epi e{splits > 1 ? (void*)ws : C, ldc, bias, pre, c_f32 ? 1 : 0, act, (splits == 1 && accumulate) ? 1 : 0,
+              alpha, splits > 1 ? (long)M * N : 0};
   using namespace g256r;
   if (a_kmajor && b_kmajor)
-    g256::launch_ring(KMaj{A, lda, M}, KMaj{B, ldb, N}, e, M, N, K, st);
+    g256::launch_ring(KMaj{A, lda, M}, KMaj{B, ldb, N}, e, M, N, K, splits, st);
   else if (a_kmajor && !b_kmajor)
-    g256::launch_ring(KMaj{A, lda, M}, MNMaj{B, ldb, N}, e, M, N, K, st);
+    g256::launch_ring(KMaj{A, lda, M}, MNMaj{B, ldb, N}, e, M, N, K, splits, st);
   else if (!a_kmajor && b_kmajor)
-    g256::launch_ring(MNMaj{A, lda, M}, KMaj{B, ldb, N}, e, M, N, K, st);
+    g256::launch_ring(MNMaj{A, lda, M}, KMaj{B, ldb, N}, e, M, N, K, splits, st);
   else
-    g256::launch_ring(MNMaj{A, lda, M}, MNMaj{B, ldb, N}, e, M, N, K, st);
+    g256::launch_ring(MNMaj{A, lda, M}, MNMaj{B, ldb, N}, e, M, N, K, splits, st);
+  if (splits > 1) splitk_reduce(ws, splits, (long)M * N, reinterpret_cast<float*>(C), accumulate, st);
 }
 
 }  // namespace k8s_amd

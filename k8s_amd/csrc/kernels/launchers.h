@@ -73,9 +73,11 @@ void launch_mask_apply(const uint16_t* src, const uint8_t* mask, uint16_t* out, 
 long gemm_splitk_workspace(int M, int N, int splits);  // fp32 elements of the split-K slab workspace
 // gemm256.hip: 256 x 256-tile, 8-wave phased MFMA GEMM for the large (transformer) products
 bool gemm256_eligible(int M, int N, int K, bool a_kmajor, bool b_kmajor);
+// split count for the tall-K fp32 products on the 256 x 256 kernel (1 = none)
+int gemm256_choose_splits(int M, int N, int K);
 void launch_gemm256(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                     long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre,
-                    bool accumulate, float alpha, hipStream_t st);
+                    bool accumulate, float alpha, hipStream_t st, int splits = 1, float* ws = nullptr);
 // Output written to the (a, b) parity sub-grid of an H x W image: GEMM row (n, i, j) -> (n, i*stride+a,
 // j*stride+b). Used for stride-s data gradients decomposed by output parity (ops/conv.py _dgrad_strided_hip).
 struct SubGrid {

@@ -443,6 +443,24 @@ Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tens
                             pre ? bf(*pre) : nullptr, accumulate, (float)alpha, cur_stream());
     return c;
   }
+  // tall-K fp32 products whose output is too small for the 256 x 256 kernel alone (the ResNet 1x1 weight gradients):
+  // split-K on the 256 kernel ($K8S_AMD_G256_SPLITK=0: the 128 x 128 split-K kernel, A/B)
+  static const bool g256_splitk = [] {
+    const char* e = std::getenv("K8S_AMD_G256_SPLITK");
+    return !(e && e[0] == '0');
+  }();
+  if (g256_splitk && !xfb && !add_src && splits != 1 && out_f32 && !bias && act == 0 && !pre && gemm256_mode() != 0 &&
+      K % 64 == 0 && (a_kmajor || M % 8 == 0) && (b_kmajor || N % 8 == 0) && N % 4 == 0) {
+    const int s256 = k8s_amd::gemm256_choose_splits((int)M, (int)N, (int)K);
+    const long t256 = ((M + 255) / 256) * ((N + 255) / 256);
+    if (s256 > 1 && t256 * s256 >= 128) {
+      auto ws = torch::empty({(long)s256 * M * N}, c.options());
+      k8s_amd::launch_gemm256(cbf(a), a.stride(0), a_kmajor, cbf(b), b.stride(0), b_kmajor, c.data_ptr(), N, true,
+                              (int)M, (int)N, (int)K, nullptr, 0, nullptr, accumulate, (float)alpha, cur_stream(), s256,
+                              f32(ws));
+      return c;
+    }
+  }
   int sp = (int)splits;
   if (sp != 1 && out_f32 && !bias && act == 0 && !pre && N % 4 == 0) {
     if (sp <= 0) sp = k8s_amd::gemm_choose_splits((int)M, (int)N, (int)K);

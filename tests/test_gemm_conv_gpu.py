@@ -446,3 +446,20 @@ def test_wgrad3x3_tiled_vs_fp32(cuda, N, H, W, C, accumulate):
     dw = base.clone()
     _C().conv_wgrad(x, dy, dw, 1, 1, 1, 0, accumulate, None)
     assert _rel(dw, ref + (base if accumulate else 0)) < 1e-3
+
+
+@pytest.mark.parametrize("M,N,K,ak,bk", [(256, 1024, 200704, False, False), (512, 128, 65536, False, False),
+                                         (256, 512, 32768, True, False)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_gemm256_splitk(cuda, M, N, K, ak, bk, accumulate):
+    """Tall-K fp32 products on the 256 x 256 kernel with split-K (the ResNet 1x1 weight-gradient shapes)."""
+    torch.manual_seed(6)
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    b = torch.randn(N, K, device=cuda).bfloat16()
+    ref = a.float() @ b.float().t()
+    A = a if ak else a.t().contiguous()
+    B = b if bk else b.t().contiguous()
+    base = torch.randn(M, N, device=cuda) if accumulate else None
+    out = base.clone() if accumulate else None
+    c = _C().gemm(A, ak, B, bk, out, True, None, 0, None, accumulate, 1.0, 0)
+    assert _rel(c, ref + (base if accumulate else 0)) < 2e-3
