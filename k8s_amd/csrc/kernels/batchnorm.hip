@@ -260,9 +260,11 @@ __device__ __forceinline__ void load_f8(const float* p, float (&o)[8]) {
 
 // Block -> 4-KB chunk order of the flat passes (see stream_order_mode below). rev 0: address order. rev 1 / 2: the tensor as
 // 8 contiguous bands swept concurrently (consecutive blocks in different bands), each descending (1) or ascending
-// (2) -- the shape in which the XCD-remapped GEMMs write their outputs (8 row bands in parallel, ascending).
+// (2) -- the shape in which the XCD-remapped GEMMs write their outputs (8 row bands in parallel, ascending); rev 3:
+// plain descending address order.
 __device__ __forceinline__ int bn_block_order(int b, int nb, int rev) {
   if (!rev) return b;
+  if (rev == 3) return nb - 1 - b;  // plain descending
   const int band = b & 7, q = nb >> 3, r = nb & 7;
   const int size = q + (band < r ? 1 : 0);
   const int start = band < r ? band * (q + 1) : r * (q + 1) + (band - r) * q;
@@ -812,12 +814,13 @@ void launch_bn_finalize_sums(const float* gamma, const float* beta, const float*
 }
 
 static void launch_bn_bwd_apply(const uint16_t* dy, const uint16_t* x, const uint8_t* mask, const float* params,
-                                bool relu_x, uint16_t* dx, uint16_t* dres, long M, int C, hipStream_t st) {
+                                bool relu_x, uint16_t* dx, uint16_t* dres, long M, int C, hipStream_t st,
+                                int order = -1) {
   const long nvec = M * C / 8;
   if (nvec >= (1L << 31)) throw std::runtime_error("BatchNorm tensor too large (>= 2^31 vectors)");
+  if (order < 0) order = stream_order_mode() ? (stream_dir(0) ? 1 : 2) : 0;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(cdiv(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, dy, x, mask, params,
-                     (int)relu_x, dx, dres, (int)nvec, C, make_fastdiv(C / 8),
-                     stream_order_mode() ? (stream_dir(0) ? 1 : 2) : 0);
+                     (int)relu_x, dx, dres, (int)nvec, C, make_fastdiv(C / 8), order);
 }
 
 void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, const float* invstd, const float* gamma,
@@ -825,9 +828,11 @@ void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, con
                    float* work, float* params, long M, int C, hipStream_t st, const uint8_t* mask) {
   BnGeom g = bn_geom(C, M);
   const int nb = bn_reduce_blocks(M, g);
-  static const bool masked_plain = [] {  // $K8S_AMD_BN_MASKED_PLAIN=1: residual-BN reduce in address order (A/B)
+  // $K8S_AMD_BN_MASKED_PLAIN (A/B): 1 = residual-BN reduce in address order; 2 = that, and its apply in descending
+  // address order behind it
+  static const int masked_plain = [] {
     const char* e = getenv("K8S_AMD_BN_MASKED_PLAIN");
-    return e && e[0] == '1';
+    return e ? atoi(e) : 0;
   }();
   const int rdir = (mask && masked_plain) ? 0 : stream_dir(1);
   if (mask)
@@ -838,7 +843,7 @@ void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, con
                        gamma, beta, (int)relu_x, M, C, g.tpr, g.rows_per_iter, work, mask, rdir);
   hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, nb, C, dgamma, dbeta,
                      1.f / (float)M, mean, invstd, gamma, beta, params);
-  launch_bn_bwd_apply(dy, x, mask, params, relu_x, dx, dres, M, C, st);
+  launch_bn_bwd_apply(dy, x, mask, params, relu_x, dx, dres, M, C, st, (mask && masked_plain == 2) ? 3 : -1);
 }
 
 // ---- stem BatchNorm + ReLU + 3x3 / s2 / p1 max pool (see bn_relu_maxpool_fwd_kernel)
