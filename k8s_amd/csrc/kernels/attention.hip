@@ -30,6 +30,7 @@
 //   so no fp32 atomics; delta = rowsum(dO * O) is a tiny kernel ahead of both. lse / delta rows are padded
 //   to a multiple of 64 so a query tile's 256 B of each can be staged by one global_load_lds.
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "common.h"
@@ -127,19 +128,37 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
   for (int i = 0; i < ND; ++i) oacc[i][0] = oacc[i][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   float m[2] = {-1e30f, -1e30f}, l[2] = {0.f, 0.f};
 
+  // Staging geometry, fixed across tiles: round rd moves K unit s = rd * 256 + tid (tile row, element offset inside
+  // the row) and V unit s. The element offsets row * stride + column are computed once -- for full tiles and, rows
+  // clamped to Sk - 1, for the block's last tile -- so every LDS-DMA source is one 64-bit add off a wave-uniform tile
+  // base (the per-tile index math was ~40 % of the loop's VALU; rocprofv3: 5.5 VALU per MFMA).
+  constexpr int NRD = KT / (16 * FA_THREADS);
+  int koff[NRD], voff[NRD], koffL[NRD], voffL[NRD];
+  {
+    const int lim = a.Sk - 1 - (ntiles > 0 ? (ntiles - 1) * FA_BN : 0);  // last tile's highest valid row
+#pragma unroll
+    for (int rd = 0; rd < NRD; ++rd) {
+      const int s_ = rd * FA_THREADS + tid;
+      const int per_half = FA_BN * 8, half = s_ / per_half, rem = s_ - half * per_half;
+      const int kr = rem >> 3, kc = half * 64 + (((rem & 7) ^ ((kr >> 1) & 7)) * 8);  // kh_src's image
+      const int vr = s_ / UPR, vc = ((s_ - vr * UPR) ^ v_swz<D>(vr)) * 8;
+      koff[rd] = kr * (int)a.sks + kc;
+      voff[rd] = vr * (int)a.svs + vc;
+      koffL[rd] = min(kr, lim) * (int)a.sks + kc;
+      voffL[rd] = min(vr, lim) * (int)a.svs + vc;
+    }
+  }
   auto stage = [&](int buf, int key0) {
     char* tk = smem + buf * 2 * KT;
     char* tv = tk + KT;
+    const uint16_t* kt = kp + (long)key0 * a.sks;
+    const uint16_t* vt = vp + (long)key0 * a.svs;
+    const bool last = key0 + FA_BN > a.Sk;
 #pragma unroll
-    for (int rd = 0; rd < KT / (16 * FA_THREADS); ++rd) {
-      const int s = rd * FA_THREADS + tid;
+    for (int rd = 0; rd < NRD; ++rd) {
       const size_t wb = (size_t)(rd * FA_THREADS + wid_u * 64) * 16;  // this wave's 1 KB of the round
-      glds16(kh_src(kp, a.sks, FA_BN, key0, a.Sk, s), tk + wb);
-      const int krow = s / UPR, up = s - krow * UPR;
-      const int u = up ^ v_swz<D>(krow);
-      int gr = key0 + krow;
-      gr = gr < a.Sk ? gr : a.Sk - 1;
-      glds16(vp + (long)gr * a.svs + u * 8, tv + wb);
+      glds16(kt + (last ? koffL[rd] : koff[rd]), tk + wb);
+      glds16(vt + (last ? voffL[rd] : voff[rd]), tv + wb);
     }
   };
 
@@ -148,12 +167,16 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  for (int t = 0; t < ntiles; ++t) {
+  // one key tile; MASKED: causal / key-length masking and whole-tile skips (only the block's last tiles need it,
+  // so the main loop carries no masking code -- as one loop, the compiler if-converted the mask selects into every
+  // tile)
+  auto tile = [&](const int t, auto masked_tag) {
+    constexpr bool MASKED = decltype(masked_tag)::value;
     const int cur = t & 1, key0 = t * FA_BN;
     if (t + 1 < ntiles) stage(cur ^ 1, key0 + FA_BN);
     const char* tk = smem + cur * 2 * KT;
     const char* tv = tk + KT;
-    const bool skip = a.causal && key0 > q0w + 31 + off;  // whole tile masked for this wave
+    const bool skip = MASKED && a.causal && key0 > q0w + 31 + off;  // whole tile masked for this wave
     if (!skip) {
       // ---- S^T = K Q^T
       f32x4_t s[NI][2];
@@ -169,7 +192,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
         }
       }
       // ---- online softmax (per query column = lane & 15)
-      const bool need_mask = (key0 + FA_BN > kv_end) || (a.causal && key0 + FA_BN - 1 > q0w + off);
+      const bool need_mask = MASKED && ((key0 + FA_BN > kv_end) || (a.causal && key0 + FA_BN - 1 > q0w + off));
 #pragma unroll
       for (int qs = 0; qs < 2; ++qs) {
         const int qi = q0w + qs * 16 + li;
@@ -234,7 +257,15 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-  }
+  };
+  // tiles whose every key is valid for every query of the block: below kv_end and (causal) at or below the block's
+  // first query's diagonal
+  int tfull = kv_end / FA_BN;
+  if (a.causal) tfull = min(tfull, max(0, q0 + off + 1) / FA_BN);
+  tfull = min(tfull, ntiles);
+  int t = 0;
+  for (; t < tfull; ++t) tile(t, std::false_type{});
+  for (; t < ntiles; ++t) tile(t, std::true_type{});
 
   // ---- epilogue: O = O^T / l, lse2 = m + log2(l)
   uint16_t* op = a.o + (long)b * a.sob + (long)h * a.soh;
