@@ -369,17 +369,38 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
         vf[kk] = __builtin_bit_cast(mfma_bf16x8, y);
       }
     }
-    auto stage = [&](int buf, int it) {
-      const int h = hk * rep + it / per_head, q0 = (qt0 + it % per_head) * FB_BM;
+    // per-thread staging offsets of the Q / dO units (kh_src's image without the row clamp; only a ragged last
+    // query tile takes the clamped path)
+    constexpr int NRQ = TQ / (16 * FA_THREADS);
+    int qoff[NRQ], doff[NRQ];
+#pragma unroll
+    for (int rd = 0; rd < NRQ; ++rd) {
+      const int s_ = rd * FA_THREADS + tid, half = s_ / (FB_BM * 8), rem = s_ - half * (FB_BM * 8);
+      const int row = rem >> 3, col = half * 64 + (((rem & 7) ^ ((row >> 1) & 7)) * 8);
+      qoff[rd] = row * (int)a.sqs + col;
+      doff[rd] = row * (int)a.sds + col;
+    }
+    auto stage = [&](int buf, int h, int q0) {
       const uint16_t* qp = a.q + (long)b * a.sqb + (long)h * a.sqh;
       const uint16_t* dop = a.dO + (long)b * a.sdb + (long)h * a.sdh;
       char* base = smem + buf * STAGE;
+      if (q0 + FB_BM <= a.Sq) {
+        const uint16_t* qt = qp + (long)q0 * a.sqs;
+        const uint16_t* dt = dop + (long)q0 * a.sds;
 #pragma unroll
-      for (int rd = 0; rd < TQ / (16 * FA_THREADS); ++rd) {
-        const int s = rd * FA_THREADS + tid;
-        const size_t wb = (size_t)(rd * FA_THREADS + wid_u * 64) * 16;
-        glds16(kh_src(qp, a.sqs, FB_BM, q0, a.Sq, s), base + wb);
-        glds16(kh_src(dop, a.sds, FB_BM, q0, a.Sq, s), base + TQ + wb);
+        for (int rd = 0; rd < NRQ; ++rd) {
+          const size_t wb = (size_t)(rd * FA_THREADS + wid_u * 64) * 16;
+          glds16(qt + qoff[rd], base + wb);
+          glds16(dt + doff[rd], base + TQ + wb);
+        }
+      } else {
+#pragma unroll
+        for (int rd = 0; rd < NRQ; ++rd) {
+          const int s = rd * FA_THREADS + tid;
+          const size_t wb = (size_t)(rd * FA_THREADS + wid_u * 64) * 16;
+          glds16(kh_src(qp, a.sqs, FB_BM, q0, a.Sq, s), base + wb);
+          glds16(kh_src(dop, a.sds, FB_BM, q0, a.Sq, s), base + TQ + wb);
+        }
       }
       if (wid_u == 0) {  // lse | delta of the tile's queries (rows padded to lse_ld, so never out of bounds)
         constexpr int L4 = FB_BM / 4;  // lanes per 4-float row piece
@@ -389,17 +410,22 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
         glds16(src, base + 2 * TQ);
       }
     };
-    stage(0, 0);
+    stage(0, hk * rep, qt0 * FB_BM);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const int key = kw + li;
+    // (head, query tile) walk by counters (no per-step division)
+    int hh = hk * rep, qt = qt0;
     for (int it = 0; it < total; ++it) {
-      const int cur = it & 1;
-      if (it + 1 < total) stage(cur ^ 1, it + 1);
+      const int cur = it & 1, q0 = qt * FB_BM;
+      if (++qt == nqt) {
+        qt = qt0;
+        ++hh;
+      }
+      if (it + 1 < total) stage(cur ^ 1, hh, qt * FB_BM);
       const char* tq = smem + cur * STAGE;
       const char* tdo = tq + TQ;
       const float* tl = reinterpret_cast<const float*>(tq + 2 * TQ);
-      const int q0 = (qt0 + it % per_head) * FB_BM;
       // ---- S = Q K^T, dP = dO V^T
       f32x4_t sv[NQ], dp[NQ];
 #pragma unroll
@@ -415,17 +441,28 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
         }
       }
       // ---- P = exp2(S c - lse2), dS = P (dP - delta)
+      const bool need_mask = q0 + FB_BM > a.Sq || k0 + FB_BN > kv_end || (a.causal && k0 + FB_BN - 1 > q0 + off);
 #pragma unroll
       for (int qs = 0; qs < NQ; ++qs) {
-        const f32x4_t l4 = *reinterpret_cast<const f32x4_t*>(tl + qs * 16 + g * 4);
-        const f32x4_t d4 = *reinterpret_cast<const f32x4_t*>(tl + FB_BM + qs * 16 + g * 4);
+        f32x4_t l4 = *reinterpret_cast<const f32x4_t*>(tl + qs * 16 + g * 4);
+        f32x4_t d4 = *reinterpret_cast<const f32x4_t*>(tl + FB_BM + qs * 16 + g * 4);
+        // masked scores -> -inf (exp2 -> 0) and their lse / delta -> 0 (padded rows are uninitialised): cheap
+        // selects in a uniform branch taken only by diagonal / ragged steps, one exponent path for every step
+        if (need_mask) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int qi = q0 + qs * 16 + g * 4 + r;
+            const bool ok = qi < a.Sq && key < kv_end && !(a.causal && key > qi + off);
+            sv[qs][r] = ok ? sv[qs][r] : -INFINITY;
+            l4[r] = ok ? l4[r] : 0.f;
+            d4[r] = ok ? d4[r] : 0.f;
+          }
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int qi = q0 + qs * 16 + g * 4 + r;
-          const bool ok = qi < a.Sq && key < kv_end && !(a.causal && key > qi + off);
-          const float p = ok ? fexp2(sv[qs][r] * a.scale_log2 - l4[r]) : 0.f;
+          const float p = fexp2(sv[qs][r] * a.scale_log2 - l4[r]);
           sv[qs][r] = p;
-          dp[qs][r] = ok ? p * (dp[qs][r] - d4[r]) : 0.f;  // padded rows of lse / delta are uninitialised
+          dp[qs][r] = p * (dp[qs][r] - d4[r]);
         }
       }
       // ---- dV^T += dO^T P, dK^T += Q^T dS   (k = queries in the permuted order of the accumulators)
