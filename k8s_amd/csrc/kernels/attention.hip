@@ -98,7 +98,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
   const int h = (wg / nqb) % a.Hq;
   const int b = wg / (nqb * a.Hq);
   const int hk = h / (a.Hq / a.Hkv);
-  const int q0 = qb * FA_BM, q0w = q0 + wid * 32;
+  const int q0 = qb * FA_BM, q0w = q0 + wid_u * 32;  // wave-uniform (SGPR): per-wave skip / mask tests branch on scc
   const int off = a.Sk - a.Sq;
   int kv_end = a.Sk;
   if (a.kv_lens) kv_end = min(kv_end, a.kv_lens[b]);
@@ -338,7 +338,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
   const int hk = (wg / nkb) % a.Hkv;
   const int b = wg / (nkb * a.Hkv);
   const int rep = a.Hq / a.Hkv;
-  const int k0 = kb * FB_BN, kw = k0 + wid * 16;
+  const int k0 = kb * FB_BN, kw = k0 + wid_u * 16;
   const int off = a.Sk - a.Sq;
   int kv_end = a.Sk;
   if (a.kv_lens) kv_end = min(kv_end, a.kv_lens[b]);
@@ -529,7 +529,7 @@ __global__ void __launch_bounds__(FA_THREADS, (QS == 2 && D * TILE >= 8192) ? 1 
   const int h = (wg / nqb) % a.Hq;
   const int b = wg / (nqb * a.Hq);
   const int hk = h / (a.Hq / a.Hkv);
-  const int q0 = qb * BMQ, q0w = q0 + wid * QW;
+  const int q0 = qb * BMQ, q0w = q0 + wid * QW;  // (wid, not wid_u: a scalar skip branch made the compiler copy all of acc on every tile)
   const int off = a.Sk - a.Sq;
   int kv_end = a.Sk;
   if (a.kv_lens) kv_end = min(kv_end, a.kv_lens[b]);
@@ -569,14 +569,35 @@ __global__ void __launch_bounds__(FA_THREADS, (QS == 2 && D * TILE >= 8192) ? 1 
 #pragma unroll
     for (int i = 0; i < ND; ++i) acc[qs][i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  // per-thread staging offsets (kh_src's image without the row clamp; only a ragged last key tile is clamped)
+  constexpr int NRK = KT / (16 * FA_THREADS);
+  int kof[NRK], vof[NRK];
+#pragma unroll
+  for (int rd = 0; rd < NRK; ++rd) {
+    const int s_ = rd * FA_THREADS + tid, half = s_ / (FB_BN * 8), rem = s_ - half * (FB_BN * 8);
+    const int row = rem >> 3, col = half * 64 + (((rem & 7) ^ ((row >> 1) & 7)) * 8);
+    kof[rd] = row * (int)a.sks + col;
+    vof[rd] = row * (int)a.svs + col;
+  }
   auto stage = [&](int buf, int key0) {
     char* tk = smem + buf * 2 * KT;
+    if (key0 + FB_BN <= a.Sk) {
+      const uint16_t* kt = kp + (long)key0 * a.sks;
+      const uint16_t* vt = vp + (long)key0 * a.svs;
 #pragma unroll
-    for (int rd = 0; rd < KT / (16 * FA_THREADS); ++rd) {
-      const int s = rd * FA_THREADS + tid;
-      const size_t wb = (size_t)(rd * FA_THREADS + wid_u * 64) * 16;
-      glds16(kh_src(kp, a.sks, FB_BN, key0, a.Sk, s), tk + wb);
-      glds16(kh_src(vp, a.svs, FB_BN, key0, a.Sk, s), tk + KT + wb);
+      for (int rd = 0; rd < NRK; ++rd) {
+        const size_t wb = (size_t)(rd * FA_THREADS + wid_u * 64) * 16;
+        glds16(kt + kof[rd], tk + wb);
+        glds16(vt + vof[rd], tk + KT + wb);
+      }
+    } else {
+#pragma unroll
+      for (int rd = 0; rd < NRK; ++rd) {
+        const int s = rd * FA_THREADS + tid;
+        const size_t wb = (size_t)(rd * FA_THREADS + wid_u * 64) * 16;
+        glds16(kh_src(kp, a.sks, FB_BN, key0, a.Sk, s), tk + wb);
+        glds16(kh_src(vp, a.svs, FB_BN, key0, a.Sk, s), tk + KT + wb);
+      }
     }
   };
   if (ntiles > 0) {
