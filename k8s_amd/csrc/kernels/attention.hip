@@ -45,9 +45,26 @@ constexpr int FB_BN = 64;
 // per barrier: 64 keys / queries at D = 128, 128 at D = 64.
 // (host side picks TILE = 128 for D = 64 only when the sequence is long enough to keep the grid full)
 
+// 16-B unit swizzles of the attention LDS tiles, chosen so every fragment read is bank-conflict free on gfx950
+// (ds_read_b128: 4 lane groups of 16; ds_read_b64_tr_b16: 2 groups of 32; 64 banks). The transposed reads take
+// rows 4g + q_ (+16, +32 s2) per 32-lane group: 8 rows whose swizzles must pick 8 different unit pairs. The GEMM
+// tiles' swizzles (mn_swz, row/2 mod 8) give those rows only 4 distinct pairs (2-way conflicts on every transposed
+// read; rocprofv3 measured 31 % LDS bank-conflict cycles in the forward).
+// V tile ([keys][D] rows of 2D bytes, read transposed in the forward's O^T += V^T P^T)
 template <int D>
 __device__ __forceinline__ int v_swz(int r) {
-  return D == 128 ? mn_swz(r) : (mn_swz(r) & 7);
+  return D == 128 ? 2 * (r & 7) : 2 * ((r >> 1) & 3);
+}
+// K-major-halves tiles ([rows][64] halves of 128-B rows): read as MFMA fragments (ds_read_b128) AND transposed
+// (dK/dV: Q^T, dO^T; dQ: K^T)
+__device__ __forceinline__ int kh_swz(int row) { return row & 6; }
+
+// operand fragment of a K-major-halves tile: row rb + (lane & 15), k = kk*32 + 8*(lane>>4) .. +7
+__device__ __forceinline__ mfma_bf16x8 frag_kh(const char* tile, int rb, int kk, int lane) {
+  const int row = rb + (lane & 15);
+  const int c = kk * 4 + (lane >> 4);
+  const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(tile + row * 128 + ((c ^ kh_swz(row)) << 4));
+  return __builtin_bit_cast(mfma_bf16x8, v);
 }
 
 // 2^x on v_exp_f32 alone: exp2f adds a denormal-range rescale (compare, select, ldexp) around every call;
@@ -64,7 +81,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // Byte address of (row, column d .. d+3) for the transposed reads.
 __device__ __forceinline__ const char* kh_addr(const char* tile, int rows, int row, int d) {
   const int half = d >> 6, c = (d & 63) >> 3;
-  return tile + half * rows * 128 + row * 128 + ((c ^ ((row >> 1) & 7)) << 4) + (d & 7) * 2;
+  return tile + half * rows * 128 + row * 128 + ((c ^ kh_swz(row)) << 4) + (d & 7) * 2;
 }
 
 // global source of unit s (16 B) of a K-major-halves tile with `rows` rows starting at row0
@@ -73,7 +90,7 @@ __device__ __forceinline__ const uint16_t* kh_src(const uint16_t* base, long rst
   const int per_half = rows * 8;
   const int half = s / per_half, rem = s - half * per_half;
   const int row = rem >> 3, cp = rem & 7;
-  const int c = cp ^ ((row >> 1) & 7);
+  const int c = cp ^ kh_swz(row);
   int gr = row0 + row;
   gr = gr < nrows ? gr : nrows - 1;
   return base + (long)gr * rstride + half * 64 + c * 8;
@@ -140,7 +157,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
     for (int rd = 0; rd < NRD; ++rd) {
       const int s_ = rd * FA_THREADS + tid;
       const int per_half = FA_BN * 8, half = s_ / per_half, rem = s_ - half * per_half;
-      const int kr = rem >> 3, kc = half * 64 + (((rem & 7) ^ ((kr >> 1) & 7)) * 8);  // kh_src's image
+      const int kr = rem >> 3, kc = half * 64 + (((rem & 7) ^ kh_swz(kr)) * 8);  // kh_src's image
       const int vr = s_ / UPR, vc = ((s_ - vr * UPR) ^ v_swz<D>(vr)) * 8;
       koff[rd] = kr * (int)a.sks + kc;
       voff[rd] = vr * (int)a.svs + vc;
@@ -186,7 +203,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
       for (int kk = 0; kk < NK; ++kk) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-          const mfma_bf16x8 kf = frag_kmajor(tk + (kk >> 1) * (FA_BN * 128), i * 16, kk & 1, lane);
+          const mfma_bf16x8 kf = frag_kh(tk + (kk >> 1) * (FA_BN * 128), i * 16, kk & 1, lane);
           s[i][0] = mfma16(kf, qf[0][kk], s[i][0]);
           s[i][1] = mfma16(kf, qf[1][kk], s[i][1]);
         }
@@ -376,7 +393,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
 #pragma unroll
     for (int rd = 0; rd < NRQ; ++rd) {
       const int s_ = rd * FA_THREADS + tid, half = s_ / (FB_BM * 8), rem = s_ - half * (FB_BM * 8);
-      const int row = rem >> 3, col = half * 64 + (((rem & 7) ^ ((row >> 1) & 7)) * 8);
+      const int row = rem >> 3, col = half * 64 + (((rem & 7) ^ kh_swz(row)) * 8);
       qoff[rd] = row * (int)a.sqs + col;
       doff[rd] = row * (int)a.sds + col;
     }
@@ -434,8 +451,8 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
       for (int kk = 0; kk < NK; ++kk) {
 #pragma unroll
         for (int qs = 0; qs < NQ; ++qs) {
-          const mfma_bf16x8 qa = frag_kmajor(tq + (kk >> 1) * (FB_BM * 128), qs * 16, kk & 1, lane);
-          const mfma_bf16x8 da = frag_kmajor(tdo + (kk >> 1) * (FB_BM * 128), qs * 16, kk & 1, lane);
+          const mfma_bf16x8 qa = frag_kh(tq + (kk >> 1) * (FB_BM * 128), qs * 16, kk & 1, lane);
+          const mfma_bf16x8 da = frag_kh(tdo + (kk >> 1) * (FB_BM * 128), qs * 16, kk & 1, lane);
           sv[qs] = mfma16(qa, kf[kk], sv[qs]);
           dp[qs] = mfma16(da, vf[kk], dp[qs]);
         }
@@ -575,7 +592,7 @@ __global__ void __launch_bounds__(FA_THREADS, (QS == 2 && D * TILE >= 8192) ? 1 
 #pragma unroll
   for (int rd = 0; rd < NRK; ++rd) {
     const int s_ = rd * FA_THREADS + tid, half = s_ / (FB_BN * 8), rem = s_ - half * (FB_BN * 8);
-    const int row = rem >> 3, col = half * 64 + (((rem & 7) ^ ((row >> 1) & 7)) * 8);
+    const int row = rem >> 3, col = half * 64 + (((rem & 7) ^ kh_swz(row)) * 8);
     kof[rd] = row * (int)a.sks + col;
     vof[rd] = row * (int)a.svs + col;
   }
@@ -621,8 +638,8 @@ __global__ void __launch_bounds__(FA_THREADS, (QS == 2 && D * TILE >= 8192) ? 1 
       for (int kk = 0; kk < NK; ++kk) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-          const mfma_bf16x8 kf = frag_kmajor(tk + (kk >> 1) * (FB_BN * 128), i * 16, kk & 1, lane);
-          const mfma_bf16x8 vf = frag_kmajor(tv + (kk >> 1) * (FB_BN * 128), i * 16, kk & 1, lane);
+          const mfma_bf16x8 kf = frag_kh(tk + (kk >> 1) * (FB_BN * 128), i * 16, kk & 1, lane);
+          const mfma_bf16x8 vf = frag_kh(tv + (kk >> 1) * (FB_BN * 128), i * 16, kk & 1, lane);
 #pragma unroll
           for (int qs = 0; qs < QS; ++qs) {
             s[i][qs] = mfma16(kf, qf[qs][kk], s[i][qs]);
