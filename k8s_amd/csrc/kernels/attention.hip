@@ -349,11 +349,13 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
 
   const int nkb = (a.Sk + FB_BN - 1) / FB_BN;
-  const int nwg = nkb * a.Hkv * a.B;
+  const int nsp = a.dkv_split;  // blocks per (key block, KV head): contiguous chunks of its (head, query tile) walk
+  const int nwg = nkb * a.Hkv * a.B * nsp;
   const int wg = xcd_remap(blockIdx.x, nwg);
-  const int kb = wg % nkb;
-  const int hk = (wg / nkb) % a.Hkv;
-  const int b = wg / (nkb * a.Hkv);
+  const int sp = wg % nsp;  // the chunks of one key block dispatch together (heavy causal key blocks first)
+  const int kb = (wg / nsp) % nkb;
+  const int hk = (wg / (nsp * nkb)) % a.Hkv;
+  const int b = wg / (nsp * nkb * a.Hkv);
   const int rep = a.Hq / a.Hkv;
   const int k0 = kb * FB_BN, kw = k0 + wid_u * 16;
   const int off = a.Sk - a.Sq;
@@ -371,7 +373,10 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
   const int nqt = (a.Sq + FB_BM - 1) / FB_BM;
   const int per_head = nqt - qt0;
   const int total = (k0 < kv_end && per_head > 0) ? rep * per_head : 0;
-  if (total > 0) {
+  // this block's chunk [it0, it1) of the walk; causal key blocks differ in work by up to Sq / 64 x, so one block
+  // per key block left the chip waiting on the first ones (load imbalance, not throughput, bounded the kernel)
+  const int it0 = (int)((long)total * sp / nsp), it1 = (int)((long)total * (sp + 1) / nsp);
+  if (it1 > it0) {
     mfma_bf16x8 kf[NK], vf[NK];
     {
       const int key = kw + li;
@@ -427,19 +432,19 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
         glds16(src, base + 2 * TQ);
       }
     };
-    stage(0, hk * rep, qt0 * FB_BM);
+    int hh = hk * rep + it0 / per_head, qt = qt0 + it0 % per_head;
+    stage(0, hh, qt * FB_BM);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const int key = kw + li;
     // (head, query tile) walk by counters (no per-step division)
-    int hh = hk * rep, qt = qt0;
-    for (int it = 0; it < total; ++it) {
-      const int cur = it & 1, q0 = qt * FB_BM;
+    for (int it = it0; it < it1; ++it) {
+      const int cur = (it - it0) & 1, q0 = qt * FB_BM;
       if (++qt == nqt) {
         qt = qt0;
         ++hh;
       }
-      if (it + 1 < total) stage(cur ^ 1, hh, qt * FB_BM);
+      if (it + 1 < it1) stage(cur ^ 1, hh, qt * FB_BM);
       const char* tq = smem + cur * STAGE;
       const char* tdo = tq + TQ;
       const float* tl = reinterpret_cast<const float*>(tq + 2 * TQ);
@@ -506,7 +511,16 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
     }
   }
   const int key = kw + li;
-  if (key < a.Sk) {
+  if (key < a.Sk && nsp > 1) {  // fp32 partials [split][dk | dv][b][hk][key][D], summed by flash_dkv_reduce_kernel
+    const long plane = (long)a.B * a.Hkv * a.Sk * D;
+    float* wk = a.dkv_ws + (long)sp * 2 * plane + (((long)b * a.Hkv + hk) * a.Sk + key) * D;
+    float* wv = wk + plane;
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      *reinterpret_cast<f32x4_t*>(wk + d * 16 + g * 4) = dka[d];
+      *reinterpret_cast<f32x4_t*>(wv + d * 16 + g * 4) = dva[d];
+    }
+  } else if (key < a.Sk) {
     uint16_t* dkp = a.dk + b * a.sgkb + key * a.sgks + hk * a.sgkh;
     uint16_t* dvp = a.dv + b * a.sgvb + key * a.sgvs + hk * a.sgvh;
 #pragma unroll
@@ -521,6 +535,40 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_dkv_kernel(AttnBwdArg
       *reinterpret_cast<bf16x4_t*>(dvp + d * 16 + g * 4) = y;
     }
   }
+}
+
+// sum of the dK / dV chunk partials (fp32), dK scaled, written as bf16 at the gradient strides; 8 columns per thread
+template <int D>
+__global__ void __launch_bounds__(256) flash_dkv_reduce_kernel(AttnBwdArgs a) {
+  constexpr int CPR = D / 8;  // 8-column pieces per row
+  const long rows = (long)a.B * a.Hkv * a.Sk;
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= rows * CPR) return;
+  const long row = t / CPR;
+  const int c = (int)(t - row * CPR) * 8;
+  const int key = (int)(row % a.Sk);
+  const int hk = (int)((row / a.Sk) % a.Hkv);
+  const int b = (int)(row / ((long)a.Sk * a.Hkv));
+  const long plane = rows * D;
+  const float* src = a.dkv_ws + row * D + c;
+  f32x4_t k0 = {0.f, 0.f, 0.f, 0.f}, k1 = k0, v0 = k0, v1 = k0;
+  for (int sp = 0; sp < a.dkv_split; ++sp) {
+    const float* pk = src + (long)sp * 2 * plane;
+    k0 += *reinterpret_cast<const f32x4_t*>(pk);
+    k1 += *reinterpret_cast<const f32x4_t*>(pk + 4);
+    v0 += *reinterpret_cast<const f32x4_t*>(pk + plane);
+    v1 += *reinterpret_cast<const f32x4_t*>(pk + plane + 4);
+  }
+  bf16x8_t xk, xv;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    xk[r] = (short)f2bf(k0[r] * a.scale);
+    xk[4 + r] = (short)f2bf(k1[r] * a.scale);
+    xv[r] = (short)f2bf(v0[r]);
+    xv[4 + r] = (short)f2bf(v1[r]);
+  }
+  *reinterpret_cast<bf16x8_t*>(a.dk + b * a.sgkb + key * a.sgks + hk * a.sgkh + c) = xk;
+  *reinterpret_cast<bf16x8_t*>(a.dv + b * a.sgvb + key * a.sgvs + hk * a.sgvh + c) = xv;
 }
 
 // ---- dQ: one block = 4 waves x 16 queries of one head (the forward's structure): K/V tiles of 64 keys
@@ -714,6 +762,23 @@ static bool big_tile(int D, int S) { return D == 64 && S >= 1024; }
 
 
 
+// dK/dV chunks per key block: causal key blocks carry from 1 to Sq / 64 query tiles of work, so with one block per
+// key block the first ones ran long after the rest of the chip had drained. Split each key block's (head, query tile)
+// walk into chunks (fp32 partials + a reduce pass) while the grid stays small enough for the partials to be cheap.
+// $K8S_AMD_FA_DKV_SPLIT overrides (1 = unsplit).
+int flash_dkv_splits(int B, int Sq, int Sk, int Hkv, int causal) {
+  static const int env = [] {
+    const char* e = getenv("K8S_AMD_FA_DKV_SPLIT");
+    return e ? atoi(e) : 0;
+  }();
+  if (env > 0) return std::min(env, 8);
+  if (!causal) return 1;
+  const long nblk = (long)((Sk + FB_BN - 1) / FB_BN) * Hkv * B;
+  const int per_block = (Sq + 63) / 64;  // query tiles of the heaviest key block (per query head)
+  if (per_block < 8) return 1;
+  return nblk >= 2048 ? 1 : (nblk >= 1024 ? 2 : 4);
+}
+
 void launch_flash_fwd(const AttnFwdArgs& a, int D, hipStream_t st) {
   const int nqb = (a.Sq + FA_BM - 1) / FA_BM;
   const dim3 grid(nqb * a.Hq * a.B), blk(FA_THREADS);
@@ -733,7 +798,8 @@ void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, 
   else
     hipLaunchKernelGGL(flash_delta_kernel<64>, dgrid, dim3(256), 0, st, o, sob, sos, soh, a.dO, a.sdb, a.sds, a.sdh,
                        a.delta, a.B, a.Sq, a.Hq, a.lse_ld);
-  const dim3 gkv(((a.Sk + FB_BN - 1) / FB_BN) * a.Hkv * a.B);  // dK/dV blocks own 64 keys at any D
+  // dK/dV blocks own 64 keys at any D, split into a.dkv_split chunks (flash_dkv_splits)
+  const dim3 gkv(((a.Sk + FB_BN - 1) / FB_BN) * a.Hkv * a.B * a.dkv_split);
   // dQ: QS = 2 (32 queries per wave, 128 per block) when the grid still fills the chip. With D x TILE = 8192
   // (D = 128, or D = 64 on 128-key tiles) that form needs ~320 VGPRs (one wave per SIMD); $K8S_AMD_FA_DQ_QS2=1
   // selects it there too (A/B).
@@ -756,6 +822,12 @@ void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, 
     hipLaunchKernelGGL((flash_bwd_dkv_kernel<64, 64>), gkv, blk, 0, st, a);
     if (qs2) hipLaunchKernelGGL((flash_bwd_dq_kernel<64, 64, 2>), gq, blk, 0, st, a);
     else hipLaunchKernelGGL((flash_bwd_dq_kernel<64, 64, 1>), gq, blk, 0, st, a);
+  }
+  if (a.dkv_split > 1) {
+    const long n = (long)a.B * a.Hkv * a.Sk * (D / 8);
+    const dim3 rg((unsigned)((n + 255) / 256));
+    if (D == 128) hipLaunchKernelGGL(flash_dkv_reduce_kernel<128>, rg, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(flash_dkv_reduce_kernel<64>, rg, dim3(256), 0, st, a);
   }
 }
 

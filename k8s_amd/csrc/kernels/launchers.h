@@ -142,7 +142,11 @@ struct AttnBwdArgs {
   long lse_ld;
   int B, Sq, Sk, Hq, Hkv, causal;
   float scale_log2, scale;
+  // dK/dV split into dkv_split chunks per key block (flash_dkv_splits): fp32 partials [dkv_split][2][B][Hkv][Sk][D]
+  int dkv_split = 1;
+  float* dkv_ws = nullptr;
 };
+int flash_dkv_splits(int B, int Sq, int Sk, int Hkv, int causal);
 // ResNet stem BatchNorm + ReLU + 3x3 / s2 / p1 max pool, fused (batchnorm.hip): forward from the conv's epilogue sums
 // (params = fp32 [2][C] scale | shift, idx = winner byte per pooled element); backward into dx of the conv output
 // (params = fp32 [4][C] workspace, work = pool_bn_workspace_floats(C))

@@ -782,6 +782,12 @@ std::vector<Tensor> flash_bwd(Tensor dO, Tensor q, Tensor k, Tensor v, Tensor o,
   a.B = B; a.Sq = Sq; a.Sk = Sk; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal;
   a.scale_log2 = (float)(scale * 1.4426950408889634);
   a.scale = (float)scale;
+  a.dkv_split = k8s_amd::flash_dkv_splits((int)B, (int)Sq, (int)Sk, (int)Hkv, causal);
+  Tensor dkv_ws;
+  if (a.dkv_split > 1) {
+    dkv_ws = torch::empty({a.dkv_split, 2, B, Hkv, Sk, D}, q.options().dtype(at::kFloat));
+    a.dkv_ws = f32(dkv_ws);
+  }
   k8s_amd::launch_flash_bwd(a, (int)D, cbf(o), o.stride(0), o.stride(1), o.stride(2), cur_stream());
   return {dq, dk, dv};
 }
