@@ -29,6 +29,10 @@ CASES = [
     (2, 1024, 2, 2, 64, False, [1024, 900]),
     (1, 4096, 32, 8, 128, True, None),      # Llama-3-8B attention at the benchmarked sequence length
     (1, 2048, 12, 12, 64, False, None),     # BERT-style heads at a long sequence
+    # causal dK/dV split into chunks (fp32 partials + reduce): GQA group of 3 (chunks straddle query heads), key
+    # lengths (key blocks past kv_len have empty chunks), ragged last query tile
+    (2, 700, 6, 2, 128, True, [700, 333]),
+    (1, 600, 2, 2, 64, True, [450]),
 ]
 
 
