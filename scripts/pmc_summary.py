@@ -15,6 +15,8 @@ def main():
     ap.add_argument("csv", nargs="+")
     ap.add_argument("--match", default="", help="regex on the kernel name")
     ap.add_argument("--cus", type=int, default=256)
+    # GRBM_GUI_ACTIVE comes back summed over the XCDs (8 on MI355X): divide for the kernel's cycle count
+    ap.add_argument("--xcds", type=int, default=8)
     args = ap.parse_args()
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     for path in args.csv:
@@ -34,7 +36,9 @@ def main():
             print(f"  {c:28s} {m[c]:.4g}")
         g = m.get("GRBM_GUI_ACTIVE")
         if g and "SQ_VALU_MFMA_BUSY_CYCLES" in m:
-            print(f"  -> MFMA busy {m['SQ_VALU_MFMA_BUSY_CYCLES'] / (g * args.cus * 4):.1%} of SIMD-cycles")
+            cyc = g / args.xcds
+            print(f"  -> MFMA busy {m['SQ_VALU_MFMA_BUSY_CYCLES'] / (cyc * args.cus * 4):.1%} of SIMD-cycles "
+                  f"({cyc:.4g} cycles per pass)")
         if "SQ_LDS_BANK_CONFLICT" in m and m.get("SQ_LDS_IDX_ACTIVE"):
             print(f"  -> LDS bank-conflict cycles {m['SQ_LDS_BANK_CONFLICT'] / m['SQ_LDS_IDX_ACTIVE']:.1%} of LDS-array cycles")
         if m.get("SQ_INSTS_MFMA"):
