@@ -21,7 +21,8 @@
 //   MFMAs -- 519 / 787 vs 667 / 842 after the masking fix below. Neither kept. Later in round 3, same-box A/Bs:
 //   8-wave / 256-query blocks (each K/V tile staged once per 256 queries) with a 3-stage ring 258 us causal / 312 us
 //   non-causal, with 2 stages 235 / 291, vs this kernel 205 / 302 (scripts/gpurun/r3_attn7.sh); the row sums of P
-//   on the matrix cores (ones^T P^T, 4 extra MFMAs per tile instead of 32 v_add_f32) measured neutral.)
+//   on the matrix cores (ones^T P^T, 4 extra MFMAs per tile instead of 32 v_add_f32) measured neutral; an
+//   unconditional rescale (one basic block per tile for the scheduler) 196 / 305 vs 188-194 / 294 us.)
 //
 // Backward (FA2 order, dK/dV kernel: one block = 64 keys of one KV head, looping over every query tile
 // of every query head of its GQA group, so dK/dV accumulate in VGPRs without atomics):
