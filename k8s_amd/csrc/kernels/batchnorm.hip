@@ -273,9 +273,12 @@ __device__ __forceinline__ int bn_block_order(int b, int nb, int rev) {
 }
 
 // y = act(fma(x, scale, shift) [+ res]); params = [scale | shift] (fp32 [2][C]). One vector per thread.
+// rparams: the residual is itself a BatchNorm input (a ResNet downsample branch) -- res is normalised here with its own
+// [scale | shift] instead of by a separate apply pass that writes and re-reads the normalised tensor.
 __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ res,
                                                               const float* __restrict__ params,
+                                                              const float* __restrict__ rparams,
                                                               uint16_t* __restrict__ y, uint8_t* __restrict__ mask,
                                                               int nvec, int C, FastDiv fcg, int relu, int rev) {
   const int e = bn_block_order(blockIdx.x, gridDim.x, rev) * BN_THREADS + threadIdx.x;
@@ -288,11 +291,23 @@ __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(const uint16_t* __
   float sc[8], sh[8], v[8];
   load_f8(params + c0, sc);
   load_f8(params + C + c0, sh);
+  if (rparams) {
+    float rsc[8], rsh[8];
+    load_f8(rparams + c0, rsc);
+    load_f8(rparams + C + c0, rsh);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float o = __builtin_fmaf(bf2f((uint16_t)xv[j]), sc[j], sh[j]);
-    if (res) o += bf2f((uint16_t)rv[j]);
-    v[j] = relu ? fmaxf(o, 0.f) : o;
+    for (int j = 0; j < 8; ++j) {
+      const float o = __builtin_fmaf(bf2f((uint16_t)xv[j]), sc[j], sh[j]) +
+                      __builtin_fmaf(bf2f((uint16_t)rv[j]), rsc[j], rsh[j]);
+      v[j] = relu ? fmaxf(o, 0.f) : o;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float o = __builtin_fmaf(bf2f((uint16_t)xv[j]), sc[j], sh[j]);
+      if (res) o += bf2f((uint16_t)rv[j]);
+      v[j] = relu ? fmaxf(o, 0.f) : o;
+    }
   }
   const bf16x8_t ov = pack_bf16x8(v);
   *reinterpret_cast<bf16x8_t*>(y + (long)e * 8) = ov;
@@ -768,11 +783,11 @@ int bn_workspace_floats(long M, int C) {
 }
 
 static void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* params, uint16_t* y, uint8_t* mask,
-                            long M, int C, bool relu, hipStream_t st) {
+                            long M, int C, bool relu, hipStream_t st, const float* rparams = nullptr) {
   const long nvec = M * C / 8;
   if (nvec >= (1L << 31)) throw std::runtime_error("BatchNorm tensor too large (>= 2^31 vectors)");
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(cdiv(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, x, res, params, y,
-                     mask, (int)nvec, C, make_fastdiv(C / 8), (int)relu,
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(cdiv(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, x, res, params, rparams,
+                     y, mask, (int)nvec, C, make_fastdiv(C / 8), (int)relu,
                      stream_order_mode() ? (stream_dir(1) ? 1 : 2) : 0);
 }
 
@@ -802,6 +817,22 @@ void launch_bn_fwd_from_sums(const uint16_t* x, const uint16_t* res, const float
   hipLaunchKernelGGL(bn_finalize_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, nrep, C, (float)M, eps,
                      momentum, save_mean, save_invstd, run_mean, run_var, gamma, beta, params);
   launch_bn_apply(x, res, params, y, mask, M, C, relu, st);
+}
+
+// y = relu(BN(x) + BN_r(xr)), both BatchNorms' statistics from their convs' epilogue sums (a ResNet downsample
+// block's bn3 and downsample BN): the downsample BN's output is never written (it was stored by its own apply pass
+// and read back once by bn3's). mask = the packed ReLU mask of y.
+void launch_bn_fwd_from_sums_dual(const uint16_t* x, const float* gamma, const float* beta, const float* sums,
+                                  int nrep, float* save_mean, float* save_invstd, float* run_mean, float* run_var,
+                                  float* params, const uint16_t* xr, const float* gamma_r, const float* beta_r,
+                                  const float* sums_r, int nrep_r, float* save_mean_r, float* save_invstd_r,
+                                  float* run_mean_r, float* run_var_r, float* params_r, uint16_t* y, uint8_t* mask,
+                                  long M, int C, float eps, float momentum, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, nrep, C, (float)M, eps,
+                     momentum, save_mean, save_invstd, run_mean, run_var, gamma, beta, params);
+  hipLaunchKernelGGL(bn_finalize_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums_r, nrep_r, C, (float)M, eps,
+                     momentum, save_mean_r, save_invstd_r, run_mean_r, run_var_r, gamma_r, beta_r, params_r);
+  launch_bn_apply(x, xr, params, y, mask, M, C, true, st, params_r);
 }
 
 // Statistics finalize only (mean, invstd, running stats, [scale | shift]): the apply happens in the consuming

@@ -30,6 +30,12 @@ void launch_bn_fwd_from_sums(const uint16_t* x, const uint16_t* res, const float
                              uint16_t* y, const float* sums, int nrep, float* save_mean, float* save_invstd,
                              float* run_mean, float* run_var, float* params, long M, int C, float eps, float momentum,
                              bool relu, hipStream_t st, uint8_t* mask = nullptr);
+void launch_bn_fwd_from_sums_dual(const uint16_t* x, const float* gamma, const float* beta, const float* sums,
+                                  int nrep, float* save_mean, float* save_invstd, float* run_mean, float* run_var,
+                                  float* params, const uint16_t* xr, const float* gamma_r, const float* beta_r,
+                                  const float* sums_r, int nrep_r, float* save_mean_r, float* save_invstd_r,
+                                  float* run_mean_r, float* run_var_r, float* params_r, uint16_t* y, uint8_t* mask,
+                                  long M, int C, float eps, float momentum, hipStream_t st);
 void launch_bn_finalize_sums(const float* gamma, const float* beta, const float* sums, int nrep, float* save_mean,
                              float* save_invstd, float* run_mean, float* run_var, float* params, long M, int C,
                              float eps, float momentum, hipStream_t st);

@@ -185,6 +185,35 @@ std::vector<Tensor> bn_fwd_from_sums(Tensor x, c10::optional<Tensor> res, Tensor
   return {y, mean, invstd};
 }
 
+// y = relu(BN(x) + BN_r(xr)) with both BatchNorms' statistics from conv epilogue sums (ResNet downsample block:
+// bn3 + the downsample BN in one apply pass). Returns (y, mean, invstd, packed ReLU mask, mean_r, invstd_r).
+std::vector<Tensor> bn_fwd_from_sums_dual(Tensor x, Tensor sums, Tensor gamma, Tensor beta, Tensor run_mean,
+                                          Tensor run_var, Tensor xr, Tensor sums_r, Tensor gamma_r, Tensor beta_r,
+                                          Tensor run_mean_r, Tensor run_var_r, double momentum, double eps) {
+  check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x"); check_aligned(x, "x");
+  check_cuda(xr, "xr"); check_dtype(xr, at::kBFloat16, "xr"); check_aligned(xr, "xr");
+  TORCH_CHECK(x.is_contiguous() && xr.is_contiguous() && xr.sizes() == x.sizes(), "x / xr: same contiguous shape");
+  const int C = (int)x.size(-1);
+  TORCH_CHECK(C % 8 == 0, "channels must be a multiple of 8");
+  const long M = x.numel() / C;
+  for (const Tensor* t : {&gamma, &beta, &run_mean, &run_var, &gamma_r, &beta_r, &run_mean_r, &run_var_r})
+    TORCH_CHECK(t->numel() == C && t->scalar_type() == at::kFloat && t->is_cuda(), "per-channel fp32 vectors of C");
+  for (const Tensor* t : {&sums, &sums_r})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() % (2 * C) == 0,
+                "sums must be fp32 [R, 2, C]");
+  auto y = torch::empty_like(x);
+  auto mean = torch::empty({C}, gamma.options()), invstd = torch::empty({C}, gamma.options());
+  auto mean_r = torch::empty({C}, gamma.options()), invstd_r = torch::empty({C}, gamma.options());
+  auto params = torch::empty({2 * C}, gamma.options()), params_r = torch::empty({2 * C}, gamma.options());
+  Tensor mask = relu_mask_for(x, true);
+  k8s_amd::launch_bn_fwd_from_sums_dual(
+      cbf(x), f32(gamma), f32(beta), f32(sums), (int)(sums.numel() / (2 * C)), f32(mean), f32(invstd), f32(run_mean),
+      f32(run_var), f32(params), cbf(xr), f32(gamma_r), f32(beta_r), f32(sums_r), (int)(sums_r.numel() / (2 * C)),
+      f32(mean_r), f32(invstd_r), f32(run_mean_r), f32(run_var_r), f32(params_r), bf(y), mask.data_ptr<uint8_t>(), M,
+      C, (float)eps, (float)momentum, cur_stream());
+  return {y, mean, invstd, mask, mean_r, invstd_r};
+}
+
 // BatchNorm statistics of a conv output from its epilogue sums, WITHOUT the apply pass: returns (mean, invstd,
 // params = fp32 [2][C] scale | shift) for a consumer that normalises on load (conv_fwd / conv_wgrad / gemm xform).
 std::vector<Tensor> bn_finalize(Tensor sums, Tensor gamma, Tensor beta, Tensor run_mean, Tensor run_var,
@@ -970,6 +999,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("splits"),
         py::arg("add_src") = py::none(), py::arg("add_mask") = py::none(), py::arg("xform_b") = py::none(),
         py::arg("xform_c") = 0);
+  m.def("bn_fwd_from_sums_dual", &bn_fwd_from_sums_dual, "relu(BN(x) + BN_r(xr)), statistics from conv sums");
   m.def("bn_finalize", &bn_finalize, py::arg("sums"), py::arg("gamma"), py::arg("beta"), py::arg("run_mean"),
         py::arg("run_var"), py::arg("count"), py::arg("momentum"), py::arg("eps"));
   m.def("mask_apply", &mask_apply, "out = bit ? src : 0 (packed 1-bit mask per element)");

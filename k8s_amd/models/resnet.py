@@ -80,10 +80,14 @@ class Bottleneck(nn.Module):
         # downsample block: bn3's ReLU mask is applied by the downsample BN's backward as it reads dy. The branch is
         # built FIRST so autograd (highest sequence number first) runs its backward LAST: the stride-2 1x1 dgrad
         # then accumulates onto conv1's dx (shared GradLink) instead of zero-filling the 3 parities it never writes
-        mlink = None
+        mlink = dn = None
         if self.down is not None:
             mlink = K.MaskLink()
-            idn = self.down_bn(self.down(x, grad_link=dlink), relu=False, dy_link=mlink)
+            dn = self.down(x, grad_link=dlink)
+            # bn3 + downsample BN in one apply pass where the fused kernel applies (ops.nn.bn_act_dual)
+            fuse = K.BN_DUAL and isinstance(dn, tuple) and dn[1] is not None and self.training and dn[0].is_cuda
+            if not fuse:
+                idn = self.down_bn(dn, relu=False, dy_link=mlink)
         t = self.conv1(x, grad_link=link or dlink)
         # bn1 / bn2 + ReLU: normalised on load by the consuming convolution (ops.nn.bn_relu_conv, no apply pass)
         # or applied by the BN kernel; ops.nn.BN_ONLOAD picks which
@@ -95,6 +99,11 @@ class Bottleneck(nn.Module):
             t = K.bn_relu_conv(t, self.bn2, self.conv3)
         else:
             t = self.conv3(self.bn2(t))
+        if dn is not None and fuse:
+            y = K.bn_act_dual(t, self.bn3, dn, self.down_bn)
+            if y is not None:
+                return y
+            idn = self.down_bn(dn, relu=False, dy_link=mlink)
         return self.bn3(t, residual=idn, relu=True, res_link=link or mlink)
 
 

@@ -699,6 +699,58 @@ def bn_relu_maxpool(t, bn):
     return max_pool_nhwc(bn(t), 3, 2, 1)
 
 
+# ResNet downsample blocks: bn3 and the downsample BN in one apply pass (bn_act_dual); K8S_AMD_BN_DUAL=0 runs them
+# separately (A/B)
+BN_DUAL = os.environ.get("K8S_AMD_BN_DUAL", "1") != "0"
+
+
+class _BnActDual(torch.autograd.Function):
+    """relu(BN(x) + BN_r(xr)) for a ResNet downsample block (bn3 over conv3's output, the downsample BN over the
+    downsample conv's output), statistics of both from their convs' epilogue sums (batchnorm.hip
+    launch_bn_fwd_from_sums_dual). The downsample BN's output is never written: as a separate pass it was stored
+    (2 B / element) and read back once by bn3's apply. Backward: both BatchNorm backwards read the same dy through the
+    packed ReLU mask of y (what the MaskLink hand-over of the separate path does)."""
+
+    @staticmethod
+    def forward(ctx, x, sums, xr, sums_r, anchor, pg, pb, run_mean, run_var, pgr, pbr, run_mean_r, run_var_r,
+                momentum, eps):
+        x, xr = x.contiguous(), xr.contiguous()
+        y, mean, invstd, mask, mean_r, invstd_r = _C().bn_fwd_from_sums_dual(
+            x, sums, pg.master, pb.master, run_mean, run_var, xr, sums_r, pgr.master, pbr.master, run_mean_r,
+            run_var_r, momentum, eps)
+        ctx.save_for_backward(x, xr, mean, invstd, mask, mean_r, invstd_r)
+        ctx.p = (pg, pb, pgr, pbr)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, xr, mean, invstd, mask, mean_r, invstd_r = ctx.saved_tensors
+        pg, pb, pgr, pbr = ctx.p
+        dy = dy.contiguous()
+        C_ = _C()
+        dg, db, finish = _bn_param_grads(pg.store, pg, pb, x.device)
+        dx, _ = C_.bn_bwd(dy, x, None, mean, invstd, pg.master, pb.master, False, dg, db, False, mask)
+        finish()
+        dg, db, finish = _bn_param_grads(pgr.store, pgr, pbr, x.device)
+        dxr, _ = C_.bn_bwd(dy, xr, None, mean_r, invstd_r, pgr.master, pbr.master, False, dg, db, False, mask)
+        finish()
+        return (dx, None, dxr) + (None,) * 12
+
+
+def bn_act_dual(t, bn, tr, bn_r):
+    """``relu(bn(t) + bn_r(tr))`` for ``t`` / ``tr`` = (conv output, epilogue sums) pairs and training-mode
+    BatchNorms (models/resnet.BN); None when the fused kernel does not apply (caller runs the separate BNs)."""
+    if not BN_DUAL or not (isinstance(t, tuple) and isinstance(tr, tuple)):
+        return None
+    (x, sums), (xr, sums_r) = t, tr
+    if (sums is None or sums_r is None or not (bn.training and bn_r.training) or not _gpu(x)
+            or x.dtype != torch.bfloat16 or xr.shape != x.shape or x.shape[-1] % 8 != 0):
+        return None
+    return _BnActDual.apply(x, sums, xr, sums_r, bn.gamma.store.anchor, bn.gamma, bn.beta, bn.running_mean,
+                            bn.running_var, bn_r.gamma, bn_r.beta, bn_r.running_mean, bn_r.running_var, bn.momentum,
+                            bn.eps)
+
+
 class _AvgPoolNHWC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
