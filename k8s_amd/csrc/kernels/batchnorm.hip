@@ -336,7 +336,10 @@ __global__ void bn_eval_prep_kernel(const float* __restrict__ run_mean, const fl
 // same-address atomics into 32 replicas instead, 88.1 vs 82.2. Not kept.)
 // MASK: the ReLU mask comes from the packed bit mask (a separate instantiation, so the relu_x variant keeps its
 // register budget and occupancy).
-template <bool MASK>
+// DUAL (with MASK): a second BatchNorm input x2 (mean2 / invstd2) fed by the same masked dy -- the ResNet downsample
+// block's bn3 and downsample BN after their fused forward -- reduced in the same sweep (dy and the mask read once);
+// part2 gets (sum dy_eff, sum dy_eff * xhat2).
+template <bool MASK, bool DUAL = false>
 __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy,
                                                                    const uint16_t* __restrict__ x,
                                                                    const float* __restrict__ mean,
@@ -345,13 +348,18 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
                                                                    const float* __restrict__ beta, int relu_x, long M,
                                                                    int C, int tpr, int rows_per_iter,
                                                                    float* __restrict__ part,
-                                                                   const uint8_t* __restrict__ mask, int rev) {
-  __shared__ float sh[2][BN_THREADS][9];
+                                                                   const uint8_t* __restrict__ mask, int rev,
+                                                                   const uint16_t* __restrict__ x2 = nullptr,
+                                                                   const float* __restrict__ mean2 = nullptr,
+                                                                   const float* __restrict__ invstd2 = nullptr,
+                                                                   float* __restrict__ part2 = nullptr) {
+  __shared__ float sh[DUAL ? 3 : 2][BN_THREADS][9];
   const int t = threadIdx.x;
   const int r = t / tpr, cg_local = t % tpr;
   const int cg = blockIdx.y * tpr + cg_local;
   const bool active = (r < rows_per_iter) && (cg * 8 < C);
   float sd[8], sx[8], mu[8], is[8], sc[8], bt[8];
+  float sx2[DUAL ? 8 : 1], mu2[DUAL ? 8 : 1], is2[DUAL ? 8 : 1];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     sd[j] = sx[j] = 0.f;
@@ -360,6 +368,11 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
     sc[j] = 0.f;
     bt[j] = 0.f;
     if (active && relu_x) bn_affine_regs(gamma[cg * 8 + j], beta[cg * 8 + j], mu[j], is[j], sc[j], bt[j]);
+    if constexpr (DUAL) {
+      sx2[j] = 0.f;
+      mu2[j] = active ? mean2[cg * 8 + j] : 0.f;
+      is2[j] = active ? invstd2[cg * 8 + j] : 0.f;
+    }
   }
   auto one = [&](const bf16x8_t& gv, const bf16x8_t& xw, uint32_t bits) {
 #pragma unroll
@@ -370,6 +383,15 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
       const float g = on ? bf2f((uint16_t)gv[j]) : 0.f;
       sd[j] += g;
       sx[j] += g * (xv - mu[j]) * is[j];
+    }
+  };
+  auto two = [&](const bf16x8_t& gv, const bf16x8_t& xw, uint32_t bits) {  // DUAL: the second input's term
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if constexpr (DUAL) {
+        const float g = ((bits >> j) & 1u) ? bf2f((uint16_t)gv[j]) : 0.f;
+        sx2[j] += g * (bf2f((uint16_t)xw[j]) - mu2[j]) * is2[j];
+      }
     }
   };
   // rev: the rows as 8 bands (block bx sweeps band bx & 7), each visited descending -- the reverse of the
@@ -388,7 +410,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
     long row = bx * rows_per_iter + r;
     // 4 row groups per trip: every 16-B load (and mask byte) of the trip is issued before any is used
     for (; row + 3 * stride < M_; row += 4 * stride) {
-      bf16x8_t g4[4], x4[4];
+      bf16x8_t g4[4], x4[4], y4[DUAL ? 4 : 1];
       uint32_t b4[4] = {0xFFu, 0xFFu, 0xFFu, 0xFFu};
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -396,21 +418,28 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
         const long off = (rev ? base + M_ - 1 - rw : rw) * C + cg * 8;
         g4[u] = *reinterpret_cast<const bf16x8_t*>(dy + off);
         x4[u] = *reinterpret_cast<const bf16x8_t*>(x + off);
+        if constexpr (DUAL) y4[u] = *reinterpret_cast<const bf16x8_t*>(x2 + off);
         if constexpr (MASK) b4[u] = mask[off >> 3];
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) one(g4[u], x4[u], b4[u]);
+      for (int u = 0; u < 4; ++u) {
+        one(g4[u], x4[u], b4[u]);
+        if constexpr (DUAL) two(g4[u], y4[u], b4[u]);
+      }
     }
     for (; row < M_; row += stride) {
       const long off = (rev ? base + M_ - 1 - row : row) * C + cg * 8;
-      one(*reinterpret_cast<const bf16x8_t*>(dy + off), *reinterpret_cast<const bf16x8_t*>(x + off),
-          MASK ? (uint32_t)mask[off >> 3] : 0xFFu);
+      const bf16x8_t gv = *reinterpret_cast<const bf16x8_t*>(dy + off);
+      const uint32_t bits = MASK ? (uint32_t)mask[off >> 3] : 0xFFu;
+      one(gv, *reinterpret_cast<const bf16x8_t*>(x + off), bits);
+      if constexpr (DUAL) two(gv, *reinterpret_cast<const bf16x8_t*>(x2 + off), bits);
     }
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     sh[0][t][j] = sd[j];
     sh[1][t][j] = sx[j];
+    if constexpr (DUAL) sh[DUAL ? 2 : 0][t][j] = sx2[j];
   }
   __syncthreads();
   if (r == 0 && cg * 8 < C) {
@@ -420,6 +449,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
       for (int j = 0; j < 8; ++j) {
         sd[j] += sh[0][o][j];
         sx[j] += sh[1][o][j];
+        if constexpr (DUAL) sx2[j] += sh[DUAL ? 2 : 0][o][j];
       }
     }
 #pragma unroll
@@ -427,6 +457,10 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_reduce_kernel(const uint16_
       const long idx = ((long)blockIdx.x * C + cg * 8 + j) * 2;
       part[idx] = sd[j];
       part[idx + 1] = sx[j];
+      if constexpr (DUAL) {
+        part2[idx] = sd[j];
+        part2[idx + 1] = sx2[j];
+      }
     }
   }
 }
@@ -512,6 +546,41 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t
   }
   if (dres) *reinterpret_cast<bf16x8_t*>(dres + (long)e * 8) = pack_bf16x8(g);
   *reinterpret_cast<bf16x8_t*>(dx + (long)e * 8) = pack_bf16x8(o);
+}
+
+// Both BatchNorm backwards of a fused downsample-block forward (bn_apply_kernel with rparams): one masked dy, two
+// inputs, two gradients; dy and the mask read once.
+__global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_dual_kernel(
+    const uint16_t* __restrict__ dy, const uint8_t* __restrict__ mask, const uint16_t* __restrict__ x,
+    const float* __restrict__ params, uint16_t* __restrict__ dx, const uint16_t* __restrict__ x2,
+    const float* __restrict__ params2, uint16_t* __restrict__ dx2, int nvec, int C, FastDiv fcg, int rev) {
+  const int e = bn_block_order(blockIdx.x, gridDim.x, rev) * BN_THREADS + threadIdx.x;
+  if (e >= nvec) return;
+  const int c0 = (e - fcg.div(e) * (C >> 3)) * 8;
+  const bf16x8_t gv = *reinterpret_cast<const bf16x8_t*>(dy + (long)e * 8);
+  const bf16x8_t xv = *reinterpret_cast<const bf16x8_t*>(x + (long)e * 8);
+  const bf16x8_t yv = *reinterpret_cast<const bf16x8_t*>(x2 + (long)e * 8);
+  const uint32_t bits = mask[e];
+  float g[8], o[8];
+  {
+    float sc[8], B[8], D[8];
+    load_f8(params + c0, sc);
+    load_f8(params + C + c0, B);
+    load_f8(params + 2 * C + c0, D);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      g[j] = ((bits >> j) & 1u) ? bf2f((uint16_t)gv[j]) : 0.f;
+      o[j] = __builtin_fmaf(sc[j], g[j], __builtin_fmaf(B[j], bf2f((uint16_t)xv[j]), D[j]));
+    }
+    *reinterpret_cast<bf16x8_t*>(dx + (long)e * 8) = pack_bf16x8(o);
+  }
+  float sc[8], B[8], D[8];
+  load_f8(params2 + c0, sc);
+  load_f8(params2 + C + c0, B);
+  load_f8(params2 + 2 * C + c0, D);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = __builtin_fmaf(sc[j], g[j], __builtin_fmaf(B[j], bf2f((uint16_t)yv[j]), D[j]));
+  *reinterpret_cast<bf16x8_t*>(dx2 + (long)e * 8) = pack_bf16x8(o);
 }
 
 
@@ -875,6 +944,29 @@ void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, con
   hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, nb, C, dgamma, dbeta,
                      1.f / (float)M, mean, invstd, gamma, beta, params);
   launch_bn_bwd_apply(dy, x, mask, params, relu_x, dx, dres, M, C, st, (mask && masked_plain == 2) ? 3 : -1);
+}
+
+// Backward of launch_bn_fwd_from_sums_dual: both BatchNorms' (dgamma, dbeta, dx) from one masked dy in one reduce
+// sweep and one apply pass (work / work2: bn_workspace_floats each; params / params2: fp32 [4][C] each).
+void launch_bn_bwd_dual(const uint16_t* dy, const uint8_t* mask, const uint16_t* x, const float* mean,
+                        const float* invstd, const float* gamma, const float* beta, uint16_t* dx, float* dgamma,
+                        float* dbeta, float* work, float* params, const uint16_t* x2, const float* mean2,
+                        const float* invstd2, const float* gamma2, const float* beta2, uint16_t* dx2, float* dgamma2,
+                        float* dbeta2, float* work2, float* params2, long M, int C, hipStream_t st) {
+  BnGeom g = bn_geom(C, M);
+  const int nb = bn_reduce_blocks(M, g);
+  const int rdir = stream_dir(1);
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, true>), dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, dy, x, mean,
+                     invstd, gamma, beta, 0, M, C, g.tpr, g.rows_per_iter, work, mask, rdir, x2, mean2, invstd2, work2);
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, nb, C, dgamma, dbeta,
+                     1.f / (float)M, mean, invstd, gamma, beta, params);
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work2, nb, C, dgamma2, dbeta2,
+                     1.f / (float)M, mean2, invstd2, gamma2, beta2, params2);
+  const long nvec = M * C / 8;
+  if (nvec >= (1L << 31)) throw std::runtime_error("BatchNorm tensor too large (>= 2^31 vectors)");
+  hipLaunchKernelGGL(bn_bwd_apply_dual_kernel, dim3(cdiv(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, dy, mask, x,
+                     params, dx, x2, params2, dx2, (int)nvec, C, make_fastdiv(C / 8),
+                     stream_order_mode() ? (stream_dir(0) ? 1 : 2) : 0);
 }
 
 // ---- stem BatchNorm + ReLU + 3x3 / s2 / p1 max pool (see bn_relu_maxpool_fwd_kernel)

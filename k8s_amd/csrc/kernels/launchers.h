@@ -36,6 +36,11 @@ void launch_bn_fwd_from_sums_dual(const uint16_t* x, const float* gamma, const f
                                   const float* sums_r, int nrep_r, float* save_mean_r, float* save_invstd_r,
                                   float* run_mean_r, float* run_var_r, float* params_r, uint16_t* y, uint8_t* mask,
                                   long M, int C, float eps, float momentum, hipStream_t st);
+void launch_bn_bwd_dual(const uint16_t* dy, const uint8_t* mask, const uint16_t* x, const float* mean,
+                        const float* invstd, const float* gamma, const float* beta, uint16_t* dx, float* dgamma,
+                        float* dbeta, float* work, float* params, const uint16_t* x2, const float* mean2,
+                        const float* invstd2, const float* gamma2, const float* beta2, uint16_t* dx2, float* dgamma2,
+                        float* dbeta2, float* work2, float* params2, long M, int C, hipStream_t st);
 void launch_bn_finalize_sums(const float* gamma, const float* beta, const float* sums, int nrep, float* save_mean,
                              float* save_invstd, float* run_mean, float* run_var, float* params, long M, int C,
                              float eps, float momentum, hipStream_t st);

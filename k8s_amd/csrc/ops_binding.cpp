@@ -320,6 +320,33 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor 
   return {dx, dres};
 }
 
+// Backward of bn_fwd_from_sums_dual: (dx, dx2) and both BatchNorms' dgamma / dbeta from one masked dy (dy and the
+// packed ReLU mask read once per pass).
+std::vector<Tensor> bn_bwd_dual(Tensor dy, Tensor mask, Tensor x, Tensor mean, Tensor invstd, Tensor gamma,
+                                Tensor beta, Tensor dgamma, Tensor dbeta, Tensor x2, Tensor mean2, Tensor invstd2,
+                                Tensor gamma2, Tensor beta2, Tensor dgamma2, Tensor dbeta2) {
+  for (const Tensor* t : {&dy, &x, &x2}) {
+    check_cuda(*t, "dy / x / x2"); check_dtype(*t, at::kBFloat16, "dy / x / x2");
+    TORCH_CHECK(t->is_contiguous() && t->sizes() == x.sizes(), "dy / x / x2: same contiguous shape");
+  }
+  const int C = (int)x.size(-1);
+  const long M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "channels must be a multiple of 8");
+  for (const Tensor* t : {&mean, &invstd, &gamma, &beta, &dgamma, &dbeta, &mean2, &invstd2, &gamma2, &beta2, &dgamma2,
+                          &dbeta2})
+    TORCH_CHECK(t->numel() == C && t->scalar_type() == at::kFloat && t->is_contiguous(), "per-channel fp32 of C");
+  TORCH_CHECK(mask.numel() == x.numel() / 8, "packed mask: M*C/8 bytes");
+  auto dx = torch::empty_like(x), dx2 = torch::empty_like(x);
+  auto params = torch::empty({4 * C}, gamma.options()), params2 = torch::empty({4 * C}, gamma.options());
+  auto work = torch::empty({k8s_amd::bn_workspace_floats(M, C)}, gamma.options());
+  auto work2 = torch::empty({k8s_amd::bn_workspace_floats(M, C)}, gamma.options());
+  k8s_amd::launch_bn_bwd_dual(cbf(dy), cmask(mask), cbf(x), f32(mean), f32(invstd), f32(gamma), f32(beta), bf(dx),
+                              f32(dgamma), f32(dbeta), f32(work), f32(params), cbf(x2), f32(mean2), f32(invstd2),
+                              f32(gamma2), f32(beta2), bf(dx2), f32(dgamma2), f32(dbeta2), f32(work2), f32(params2), M,
+                              C, cur_stream());
+  return {dx, dx2};
+}
+
 // ------------------------------------------------------------------ layernorm / rmsnorm
 std::vector<Tensor> norm_fwd(Tensor x, c10::optional<Tensor> res, Tensor gamma, c10::optional<Tensor> beta, double eps,
                              bool rms) {
@@ -999,6 +1026,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("splits"),
         py::arg("add_src") = py::none(), py::arg("add_mask") = py::none(), py::arg("xform_b") = py::none(),
         py::arg("xform_c") = 0);
+  m.def("bn_bwd_dual", &bn_bwd_dual, "both BatchNorm backwards of bn_fwd_from_sums_dual from one masked dy");
   m.def("bn_fwd_from_sums_dual", &bn_fwd_from_sums_dual, "relu(BN(x) + BN_r(xr)), statistics from conv sums");
   m.def("bn_finalize", &bn_finalize, py::arg("sums"), py::arg("gamma"), py::arg("beta"), py::arg("run_mean"),
         py::arg("run_var"), py::arg("count"), py::arg("momentum"), py::arg("eps"));

@@ -702,6 +702,8 @@ def bn_relu_maxpool(t, bn):
 # ResNet downsample blocks: bn3 and the downsample BN in one apply pass (bn_act_dual); K8S_AMD_BN_DUAL=0 runs them
 # separately (A/B)
 BN_DUAL = os.environ.get("K8S_AMD_BN_DUAL", "1") != "0"
+# ... and their backwards in one reduce sweep + one apply pass (K8S_AMD_BN_DUAL_BWD=0: two bn_bwd calls, A/B)
+BN_DUAL_BWD = os.environ.get("K8S_AMD_BN_DUAL_BWD", "1") != "0"
 
 
 class _BnActDual(torch.autograd.Function):
@@ -729,11 +731,15 @@ class _BnActDual(torch.autograd.Function):
         dy = dy.contiguous()
         C_ = _C()
         dg, db, finish = _bn_param_grads(pg.store, pg, pb, x.device)
-        dx, _ = C_.bn_bwd(dy, x, None, mean, invstd, pg.master, pb.master, False, dg, db, False, mask)
+        dgr, dbr, finish_r = _bn_param_grads(pgr.store, pgr, pbr, x.device)
+        if BN_DUAL_BWD:  # one reduce sweep and one apply pass for both (dy and the mask read once per pass)
+            dx, dxr = C_.bn_bwd_dual(dy, mask, x, mean, invstd, pg.master, pb.master, dg, db, xr, mean_r, invstd_r,
+                                     pgr.master, pbr.master, dgr, dbr)
+        else:
+            dx, _ = C_.bn_bwd(dy, x, None, mean, invstd, pg.master, pb.master, False, dg, db, False, mask)
+            dxr, _ = C_.bn_bwd(dy, xr, None, mean_r, invstd_r, pgr.master, pbr.master, False, dgr, dbr, False, mask)
         finish()
-        dg, db, finish = _bn_param_grads(pgr.store, pgr, pbr, x.device)
-        dxr, _ = C_.bn_bwd(dy, xr, None, mean_r, invstd_r, pgr.master, pbr.master, False, dg, db, False, mask)
-        finish()
+        finish_r()
         return (dx, None, dxr) + (None,) * 12
 
 
