@@ -928,13 +928,9 @@ void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, con
                    float* work, float* params, long M, int C, hipStream_t st, const uint8_t* mask) {
   BnGeom g = bn_geom(C, M);
   const int nb = bn_reduce_blocks(M, g);
-  // $K8S_AMD_BN_MASKED_PLAIN (A/B): 1 = residual-BN reduce in address order; 2 = that, and its apply in descending
-  // address order behind it
-  static const int masked_plain = [] {
-    const char* e = getenv("K8S_AMD_BN_MASKED_PLAIN");
-    return e ? atoi(e) : 0;
-  }();
-  const int rdir = (mask && masked_plain) ? 0 : stream_dir(1);
+  // (round 3: the residual-BN reduce in address order, and its apply descending behind it, measured slower than
+  // the producer-opposite banded order -- 12.92k vs 13.06k img/s -- and were dropped)
+  const int rdir = stream_dir(1);
   if (mask)
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(nb, g.grid_y), dim3(BN_THREADS), 0, st, dy, x, mean, invstd,
                        gamma, beta, (int)relu_x, M, C, g.tpr, g.rows_per_iter, work, mask, rdir);
@@ -943,7 +939,7 @@ void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, con
                        gamma, beta, (int)relu_x, M, C, g.tpr, g.rows_per_iter, work, mask, rdir);
   hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, nb, C, dgamma, dbeta,
                      1.f / (float)M, mean, invstd, gamma, beta, params);
-  launch_bn_bwd_apply(dy, x, mask, params, relu_x, dx, dres, M, C, st, (mask && masked_plain == 2) ? 3 : -1);
+  launch_bn_bwd_apply(dy, x, mask, params, relu_x, dx, dres, M, C, st);
 }
 
 // Backward of launch_bn_fwd_from_sums_dual: both BatchNorms' (dgamma, dbeta, dx) from one masked dy in one reduce
