@@ -62,12 +62,59 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+def _launch_local_ranks(a, argv) -> int:
+    """``--gpus N`` (N > 1) without a launcher: start N local rank processes ourselves, one per GPU, BEFORE this
+    process touches the GPU (the pattern of trainer/runner.py ``_run_replica_children``). Each child gets
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT like torch.distributed.run would set; rank 0's JSON
+    line goes straight to our stdout. Returns the first non-zero child exit code (0 when all succeed); when one rank
+    fails the others get a grace period, then SIGTERM (they would otherwise wait in a collective forever)."""
+    import signal
+    import subprocess
+
+    from k8s_amd.fakeapi.server import free_port
+
+    port = free_port()
+    script = os.path.abspath(__file__)
+    argv = list(sys.argv[1:] if argv is None else argv)
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script] + argv, env=env))
+
+    def forward(signum, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signum)
+
+    signal.signal(signal.SIGTERM, forward)
+    codes = [None] * len(procs)
+    deadline = None
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None and p.poll() is not None:
+                codes[i] = 128 - p.returncode if p.returncode < 0 else p.returncode
+                if codes[i] != 0 and deadline is None:
+                    deadline = time.time() + 30.0
+        if deadline is not None and time.time() > deadline:
+            forward(signal.SIGTERM, None)
+            deadline = float("inf")
+        time.sleep(0.05)
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
 def main(argv=None):
     a = parse(argv)
+    if a.gpus > 1 and "RANK" not in os.environ and "WORLD_SIZE" not in os.environ:
+        return _launch_local_ranks(a, argv)
     info = kdist.init_process_group()
     n = info.world_size
-    if n != a.gpus and info.rank == 0:
-        print("warning: --gpus %d but world size %d" % (a.gpus, n), file=sys.stderr)
+    if n != a.gpus:
+        # fail closed: a number measured on a different world than the one asked for must not be reported
+        print("error: --gpus %d but the process group has world size %d" % (a.gpus, n), file=sys.stderr)
+        kdist.destroy()
+        return 2
     dev = torch.device("cuda", info.device_index) if torch.cuda.is_available() else torch.device("cpu")
     torch.manual_seed(1234 + info.rank)
 
@@ -86,12 +133,28 @@ def main(argv=None):
     x = model.prepare_input(images).contiguous()
     labels = torch.randint(0, 1000, (a.batch,), device=dev)
 
-    def step():
+    # comm_exposed_ms: per step, the time from the end of backward to the end of reducer.finish() (the collective
+    # work backward did not hide). On the GPU from events recorded on the compute stream (no host sync inside the
+    # timed loop; read after it); on the CPU (gloo, synchronous) from the host clock.
+    marks = []
+
+    def step(timed=False):
         reducer.begin_step()
         logits = model(x)
         loss = K.cross_entropy(logits, labels)
         loss.backward()
-        reducer.finish()
+        if timed and dev.type == "cuda":
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            reducer.finish()
+            e1.record()
+            marks.append((e0, e1))
+        elif timed:
+            t = time.perf_counter()
+            reducer.finish()
+            marks.append(time.perf_counter() - t)
+        else:
+            reducer.finish()
         opt.step(grad_scale=reducer.grad_scale)
         return loss
 
@@ -105,12 +168,17 @@ def main(argv=None):
     sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        loss = step()
+        loss = step(timed=True)
     sync()
     kdist.barrier()
     sync()
     dt = time.perf_counter() - t0
     dt_max = kdist.all_reduce_max(dt, dev)
+    if dev.type == "cuda":
+        exposed = [e0.elapsed_time(e1) for e0, e1 in marks]
+    else:
+        exposed = [1000.0 * t for t in marks]
+    exposed_ms = kdist.all_reduce_max(sum(exposed) / max(1, len(exposed)), dev)
     final_loss = float(loss.detach().float().item())
     # data-parallel sanity (outside the timed region): every replica must hold the same weights
     csum = float(store.master.double().sum().item())
@@ -142,6 +210,8 @@ def main(argv=None):
             },
             "final_loss": round(final_loss, 4),
             "replicas_identical": identical,
+            "comm_exposed_ms": round(exposed_ms, 3),
+            "grad_comm_fallbacks": dict(reducer.fallbacks),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if dev.type == "cuda" else None,
         }
         print(json.dumps(out), flush=True)
@@ -154,4 +224,4 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -87,7 +87,14 @@ class GradReducer:
         self.next_launch = 0
         self.side = torch.cuda.Stream(store.grad.device) if (store.grad.is_cuda and self.enabled) else None
         self.side_busy = False
+        self.padded = 0  # bf16 exchanges zero-padded to a multiple of the world (counted, reported by bench.py)
         store.hooks.append(self._on_deposit)
+
+    @property
+    def fallbacks(self):
+        """Transport deviations from the requested ``comm_dtype`` (none: a ragged bucket is padded, not demoted to
+        fp32); reported next to the GEMM fallbacks so the multi-GPU harness never changes transport silently."""
+        return {"bf16_padded_buckets": self.padded} if self.padded else {}
 
     # ------------------------------------------------------------------ step protocol
     def begin_step(self):
@@ -119,14 +126,20 @@ class GradReducer:
             return
         b.launched = True
         t = self.store.grad[b.lo:b.hi]
-        if self.comm_dtype == torch.bfloat16 and (b.hi - b.lo) % self.world == 0:
-            send = cast_bf16(t)
+        if self.comm_dtype == torch.bfloat16:
+            length = b.hi - b.lo
+            if length % self.world == 0:
+                send = cast_bf16(t)
+            else:  # a world that does not divide the 64-element alignment (e.g. 7 ranks): zero-padded exchange
+                send = torch.zeros(_round_up(length, self.world), dtype=torch.bfloat16, device=t.device)
+                send[:length].copy_(cast_bf16(t))
+                self.padded += 1
             recv = torch.empty_like(send)
             w = dist.all_to_all_single(recv, send, group=self.group, async_op=True)
             if self.side is None:
                 self.works.append((b, send, recv, w))
                 return
-            n = (b.hi - b.lo) // self.world
+            n = send.numel() // self.world
             me = dist.get_rank(self.group)
             with torch.cuda.stream(self.side):  # everything below waits for the exchange on the device only
                 w.wait()
@@ -135,7 +148,7 @@ class GradReducer:
                 red = send[me * n:(me + 1) * n]
                 slice_sum(recv, self.world, None, red)
                 dist.all_gather_into_tensor(send, red, group=self.group, async_op=True).wait()
-                t.copy_(send)
+                t.copy_(send[:length])
             send.record_stream(self.side)
             recv.record_stream(self.side)
             self.side_busy = True
@@ -159,13 +172,13 @@ class GradReducer:
                 w.wait()
                 if send is None:
                     continue
-                n = (b.hi - b.lo) // self.world
+                n = send.numel() // self.world
                 red = torch.empty(n, dtype=torch.bfloat16, device=recv.device)
                 slice_sum(recv, self.world, None, red)  # fp32 accumulate in rank order, one rounding
                 gathers.append((b, send, dist.all_gather_into_tensor(send, red, group=self.group, async_op=True)))
             for b, full, w in gathers:
                 w.wait()
-                self.store.grad[b.lo:b.hi].copy_(full)
+                self.store.grad[b.lo:b.hi].copy_(full[:b.hi - b.lo])
             if self.side_busy:
                 torch.cuda.current_stream(self.store.grad.device).wait_stream(self.side)
                 self.side_busy = False

@@ -12,14 +12,21 @@ from k8s_amd.fakeapi.server import free_port
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(script, args, nproc=2, timeout=300):
+def _env(**extra):
     env = dict(os.environ)
     env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "TF_CONFIG"):
         env.pop(k, None)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(REPO, script)] + args
-    r = subprocess.run(cmd, env=env, cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+    env.update(extra)
+    return env
+
+
+def _run(script, args, nproc=2, timeout=300, launcher=True):
+    cmd = [sys.executable, os.path.join(REPO, script)] + args
+    if launcher:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(REPO, script)] + args
+    r = subprocess.run(cmd, env=_env(), cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                        timeout=timeout)
     assert r.returncode == 0, r.stdout + r.stderr
     return [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
@@ -40,16 +47,30 @@ def test_bench_two_ranks_json_contract():
     assert r["final_loss"] == r["final_loss"]
 
 
-def test_bench_eight_ranks_like_the_driver():
-    """the driver's 8-GPU launch (torch.distributed.run, 8 ranks, one per GPU) rehearsed
-    with 8 gloo ranks on the CPU: one JSON line, dp8, the whole-job value, identical replicas after the steps."""
+def test_bench_eight_ranks_without_a_launcher():
+    """``python bench.py --gpus 8`` with no torchrun starts its 8 local ranks itself (before
+    any GPU call), rehearsed with 8 gloo ranks on the CPU: one JSON line, dp8, the whole-job value, identical
+    replicas after the steps, and the exposed-communication time."""
     recs = _run("bench.py", ["--gpus", "8", "--steps", "2", "--warmup", "1", "--batch", "2", "--image", "32"],
-                nproc=8, timeout=600)
+                timeout=600, launcher=False)
     assert len(recs) == 1, recs
     r = recs[0]
     assert r["n_gpus"] == 8 and r["config"]["parallelism"] == "dp8" and r["config"]["global_batch"] == 16
     assert abs(r["value"] - 16 * 2 / (r["ms_per_step"] * 2 / 1000.0)) / r["value"] < 0.02
     assert r["replicas_identical"] is True
+    assert r["comm_exposed_ms"] >= 0 and r["grad_comm_fallbacks"] == {}
+
+
+def test_bench_world_mismatch_fails_closed():
+    """A world that is not the one asked for (here a single-rank env with --gpus 2) exits non-zero and prints no
+    JSON line, instead of reporting a 1-GPU number as a 2-GPU one."""
+    env = _env(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup",
+                        "0", "--batch", "2", "--image", "32"], env=env, cwd=REPO, stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=300)
+    assert r.returncode != 0
+    assert not [line for line in r.stdout.splitlines() if line.startswith("{")]
+    assert "world size 1" in r.stderr
 
 
 def test_collectives_bench_busbw():

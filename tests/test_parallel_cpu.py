@@ -168,10 +168,11 @@ def _reference_bf16(world, opt_name, steps, round_sum, clip=None):
     return store.master.clone()
 
 
-@pytest.mark.parametrize("world", [4, 8])
+@pytest.mark.parametrize("world", [3, 4, 8])
 @pytest.mark.parametrize("strategy", ["allreduce", "ps"])
 def test_bf16_transport_bit_exact_against_rank_order_reference(world, strategy):
-    """4- and 8-rank runs bit-exact against the single-process reference. The bf16
+    """4- and 8-rank runs bit-exact against the single-process reference; 3 ranks (a world
+    that does not divide the 64-element bucket alignment) take the zero-padded exchange, not an fp32 fallback. The bf16
     transport sums in a fixed (rank) order, so its result is reproducible to the bit: Adam, 4 steps. (No gradient
     clipping here: the sharded clip norm is an all-reduce of per-shard partial sums, whose order differs from a
     single-process norm in the last bit.)"""
