@@ -23,6 +23,7 @@
 //    columns; a plain bf16 output is staged through LDS and written as whole 16-B row segments.
 //  * XCD-aware bijective block remap + grouped (8 M-tiles) order: tiles sharing an A row panel / B column panel
 //    run on one XCD's L2.
+#include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
 #include <type_traits>
@@ -312,9 +313,96 @@ __device__ __forceinline__ void tie(typename S::Raw (&r)[N]) {
   }
 }
 
+// XCD-aware bijective remap of block b of n (blocks b and b + 8 share an XCD): consecutive results share one
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+  const int xcd = b & 7, q = n >> 3, r = n & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+// Stream-K tail (g256::Plan): blocks [0, full) each own one whole tile (the full waves); the remaining tiles are split
+// `sk` ways along K, one block per (tile, split), so a 1.5-wave grid runs as 1 + 1/sk waves instead of 2.
+struct SkArgs {
+  int full;      // tiles computed whole (a multiple of the CU count), in tile order [0, full)
+  int sk;        // K splits of each remaining tile (1: none)
+  float* slabs;  // [tail tiles][sk][256 x 256] fp32 partials, fragment-native order
+  int* sync;     // [tail tiles][1 + sk]: arrival ticket, then one published flag per split (self-resetting)
+};
+
+// Deterministic in-kernel split-K fix-up of one stream-K tile (cdna_hip_programming.md §5 "In-launch split-K
+// reduction", §6 Guideline 16). Each split takes an arrival ticket FIRST; every split but the last arriver writes
+// its fp32 partial (plain 16-B stores, fragment-native order: coalesced both ways), drains, and publishes it with an
+// agent-scope release + a flag; the last arriver waits only for blocks that already took a ticket (they are running
+// and never wait themselves: no residency assumption), acquires, and sums the partials in a FIXED order -- for two
+// splits own + other (IEEE addition commutes: bit-identical whoever arrives last), for more splits every split's
+// slab in split order (the reducer writes its own too) -- then resets the ticket and flags for the next launch and
+// runs the normal epilogue. Returns true in the reducer (which goes on to the epilogue).
+__device__ __forceinline__ bool sk_fixup(f32x4_t (&acc)[8][4], const SkArgs& SK, int slot, int split, char* smem,
+                                      int tid) {
+  const int sk = SK.sk;
+  int* cnt = SK.sync + (long)slot * (1 + sk);
+  int* flg = cnt + 1;
+  int* bcast = reinterpret_cast<int*>(smem + g256r::LDS_BYTES - 16);  // the K loop's reads are all done
+  __syncthreads();
+  if (tid == 0) bcast[0] = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const bool last = bcast[0] == sk - 1;
+  // this tile's slabs through one buffer resource: the lane offset is one VGPR (tid * 16 B) and each 8 KB piece's
+  // offset an SGPR, so the 32 stores / loads add no address registers next to the 128 accumulators
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(SK.slabs + (long)slot * sk * 65536, (short)0, sk * 262144, 0x00020000);
+  const int voff = tid * 16;
+  if (!last || sk > 2) {
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(acc[a][j], rs, voff, split * 262144 + (a * 4 + j) * 8192, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep: the compiler may drop the fence's own wait
+      __hip_atomic_store(flg + split, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!last) return false;
+  }
+  if (tid == 0) {
+    for (int z = 0; z < sk; ++z)
+      if (z != split)
+        while (__hip_atomic_load(flg + z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // slab reads in chunks of 8 x 16 B per lane (the sched_barrier keeps the compiler from hoisting all 32 loads of
+  // a slab ahead of the adds: 128 more live VGPRs next to the accumulators would spill)
+  for (int z = sk == 2 ? 1 - split : 0; z < sk; z += (sk == 2 ? 2 : 1)) {
+    const bool assign = sk > 2 && z == 0;
+#pragma unroll
+    for (int a = 0; a < 8; a += 2) {
+      f32x4_t v[2][4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          v[i][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, z * 262144 + ((a + i) * 4 + j) * 8192, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[a + i][j] = assign ? v[i][j] : acc[a + i][j] + v[i][j];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (tid == 0) {  // every split has taken its ticket and published: reset for the next launch (stream-ordered)
+    __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int z = 0; z < sk; ++z) __hip_atomic_store(flg + z, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return true;
+}
+
 template <class AS, class BS, int DIAG = 0>
 __global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, g256::Epi E, int M, int N, int K,
-                                                                   int kps) {
+                                                                   int kps, SkArgs SK) {
   using namespace g256;
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -322,12 +410,15 @@ __global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, 
   const int wr = wid >> 2, wc = wid & 3;
 
   const int tiles_m = (M + 255) >> 8, tiles_n = (N + 255) >> 8;
-  const int nwg = tiles_m * tiles_n;
   const int bid = blockIdx.x;
-  int wg;
-  {
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  int wg, split = 0, sk_slot = -1;
+  if (bid < SK.full) {
+    wg = xcd_remap(bid, SK.full);
+  } else {  // stream-K tail: a tile's splits are consecutive after the remap, so they share an XCD's L2
+    const int j = xcd_remap(bid - SK.full, gridDim.x - SK.full);
+    sk_slot = j / SK.sk;
+    split = j - sk_slot * SK.sk;
+    wg = SK.full + sk_slot;
   }
   const int group = 8 * tiles_n;
   const int first_m = (wg / group) * 8;
@@ -336,8 +427,10 @@ __global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, 
   const int tn = (wg % group) / gm;
   const int m0 = tm * 256, n0 = tn * 256;
 
-  // split-K (blockIdx.y): this block reduces K range [koff, koff + kps) into its own fp32 slab
-  const long koff = (long)blockIdx.y * kps;
+  // split-K: blockIdx.y (tall-K products, fp32 slabs combined by splitk_reduce) or the stream-K split; this block
+  // reduces K range [koff, koff + kps)
+  if (bid < SK.full && SK.sk > 1) kps = K;  // a whole tile of a stream-K launch: the full K range
+  const long koff = (long)(blockIdx.y + split) * kps;
   if (E.slab) E.c = reinterpret_cast<float*>(E.c) + blockIdx.y * E.slab;
   const uint16_t* ca0 = A.cursor(tid, 0, m0) + (AS::kmajor ? koff : koff * A.ld);
   const uint16_t* ca1 = A.cursor(tid, 1, m0) + (AS::kmajor ? koff : koff * A.ld);
@@ -409,24 +502,58 @@ __global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, 
     islot = islot == NSLOT - 1 ? 0 : islot + 1;
   }
   if (!lag) barrier();
+  if (sk_slot >= 0 && !sk_fixup(acc, SK, sk_slot, split, smem, tid)) return;
   epilogue256(acc, E, smem, M, N, m0, n0, wid, wr, wc, lane);
 }
 }  // namespace g256r
 
 namespace g256 {
 template <class AS, class BS>
-static void launch_ring(const AS& a, const BS& b, const Epi& e, int M, int N, int K, int splits, hipStream_t st) {
+static void launch_ring(const AS& a, const BS& b, const Epi& e, int M, int N, int K, int splits,
+                        const Gemm256Plan& plan, float* sk_slabs, int* sk_sync, hipStream_t st) {
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
-  const int kps = K / splits;  // a multiple of 64 (gemm256_choose_splits)
-  const dim3 grid(tiles, splits);
+  g256r::SkArgs sk{tiles, 1, nullptr, nullptr};
+  int kps = K / splits;  // a multiple of 64 (gemm256_choose_splits)
+  int blocks = tiles;
+  if (splits == 1 && plan.sk > 1) {
+    sk = g256r::SkArgs{plan.full, plan.sk, sk_slabs, sk_sync};
+    kps = plan.kps;
+    blocks = plan.full + (tiles - plan.full) * plan.sk;
+  }
+  const dim3 grid(blocks, splits);
   const char* dg = getenv("K8S_AMD_GEMM256_DIAG");
   if (dg && atoi(dg) == 1)
-    hipLaunchKernelGGL((g256r::gemm256r_kernel<AS, BS, 1>), grid, dim3(THREADS), 0, st, a, b, e, M, N, K, kps);
+    hipLaunchKernelGGL((g256r::gemm256r_kernel<AS, BS, 1>), grid, dim3(THREADS), 0, st, a, b, e, M, N, K, kps, sk);
   else
-    hipLaunchKernelGGL((g256r::gemm256r_kernel<AS, BS>), grid, dim3(THREADS), 0, st, a, b, e, M, N, K, kps);
+    hipLaunchKernelGGL((g256r::gemm256r_kernel<AS, BS>), grid, dim3(THREADS), 0, st, a, b, e, M, N, K, kps, sk);
 }
 
 }  // namespace g256
+
+// Stream-K tail plan for a grid of 256 x 256 tiles on 256 CUs (one block per CU): with T = w * 256 + r tiles and
+// 0 < r <= 128, the last r tiles are split sk = min(256 / r, 4) ways along K (each split a multiple of 64 deep and
+// >= 512), so the tail costs ~1/sk of a wave (+ the fix-up) instead of a whole one. Not for grids of 8+ waves (the
+// tail is then a small fraction) or when the split would be too shallow.
+Gemm256Plan gemm256_plan(int M, int N, int K) {
+  Gemm256Plan p;
+  p.tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  p.full = p.tiles;
+  p.sk = 1;
+  p.kps = K;
+  constexpr int P = 256;
+  const int waves = p.tiles / P, r = p.tiles % P;
+  if (r == 0 || waves >= 8 || r > P / 2) return p;
+  int s = std::min(P / r, 4);
+  while (s > 1 && (K % (64 * s) != 0 || K / s < 512)) --s;
+  if (s > 1) {
+    p.full = waves * P;
+    p.sk = s;
+    p.kps = K / s;
+  }
+  return p;
+}
+long gemm256_sk_slab_floats(const Gemm256Plan& p) { return p.sk > 1 ? (long)(p.tiles - p.full) * p.sk * 65536 : 0; }
+long gemm256_sk_sync_ints(const Gemm256Plan& p) { return p.sk > 1 ? (long)(p.tiles - p.full) * (1 + p.sk) : 0; }
 
 // Shape gate for the 256 x 256 kernel: K >= 768 and a multiple of 64, MN-major extents multiples of 8, and a wave-
 // quantisation cost model against the 128 x 128 kernel of gemm.hip (2 blocks/CU). Per output element the 256
@@ -440,9 +567,11 @@ bool gemm256_eligible(int M, int N, int K, bool a_kmajor, bool b_kmajor) {
   if (!a_kmajor && M % 8 != 0) return false;
   if (!b_kmajor && N % 8 != 0) return false;
   if (N % 4 != 0) return false;
-  const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
+  const Gemm256Plan plan = gemm256_plan(M, N, K);
   const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
-  const double c256 = (double)((t256 + 255) / 256) * 65536.0 / 1.25;
+  // waves of 256 tiles, the stream-K tail counted as 1/sk of a wave (+5 % for its fix-up)
+  const double w256 = plan.sk > 1 ? plan.full / 256 + 1.05 / plan.sk : (double)((plan.tiles + 255) / 256);
+  const double c256 = w256 * 65536.0 / 1.25;
   const double c128 = (double)((t128 + 511) / 512) * 32768.0;
   return c256 <= c128;
 }
@@ -464,22 +593,25 @@ int gemm256_choose_splits(int M, int N, int K) {
 
 void launch_gemm256(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                     long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre,
-                    bool accumulate, float alpha, hipStream_t st, int splits, float* ws) {
+                    bool accumulate, float alpha, hipStream_t st, int splits, float* ws, float* sk_slabs,
+                    int* sk_sync) {
   if (K % 64 != 0) throw std::runtime_error("gemm256: K must be a multiple of 64");
   if (splits < 1) splits = 1;
   if (splits > 1 && (!c_f32 || bias || act || pre || !ws || K % (64 * splits) != 0 || ldc != N))
     throw std::runtime_error("gemm256 split-K: plain fp32 output, K % (64 * splits) == 0, a workspace");
   g256::Epi e{splits > 1 ? (void*)ws : C, ldc, bias, pre, c_f32 ? 1 : 0, act, (splits == 1 && accumulate) ? 1 : 0,
               alpha, splits > 1 ? (long)M * N : 0};
+  Gemm256Plan plan = gemm256_plan(M, N, K);
+  if (splits > 1 || !sk_slabs || !sk_sync) plan.sk = 1;  // tall-K split, or no stream-K workspace given
   using namespace g256r;
   if (a_kmajor && b_kmajor)
-    g256::launch_ring(KMaj{A, lda, M}, KMaj{B, ldb, N}, e, M, N, K, splits, st);
+    g256::launch_ring(KMaj{A, lda, M}, KMaj{B, ldb, N}, e, M, N, K, splits, plan, sk_slabs, sk_sync, st);
   else if (a_kmajor && !b_kmajor)
-    g256::launch_ring(KMaj{A, lda, M}, MNMaj{B, ldb, N}, e, M, N, K, splits, st);
+    g256::launch_ring(KMaj{A, lda, M}, MNMaj{B, ldb, N}, e, M, N, K, splits, plan, sk_slabs, sk_sync, st);
   else if (!a_kmajor && b_kmajor)
-    g256::launch_ring(MNMaj{A, lda, M}, KMaj{B, ldb, N}, e, M, N, K, splits, st);
+    g256::launch_ring(MNMaj{A, lda, M}, KMaj{B, ldb, N}, e, M, N, K, splits, plan, sk_slabs, sk_sync, st);
   else
-    g256::launch_ring(MNMaj{A, lda, M}, MNMaj{B, ldb, N}, e, M, N, K, splits, st);
+    g256::launch_ring(MNMaj{A, lda, M}, MNMaj{B, ldb, N}, e, M, N, K, splits, plan, sk_slabs, sk_sync, st);
   if (splits > 1) splitk_reduce(ws, splits, (long)M * N, reinterpret_cast<float*>(C), accumulate, st);
 }
 

@@ -86,9 +86,17 @@ long gemm_splitk_workspace(int M, int N, int splits);  // fp32 elements of the s
 bool gemm256_eligible(int M, int N, int K, bool a_kmajor, bool b_kmajor);
 // split count for the tall-K fp32 products on the 256 x 256 kernel (1 = none)
 int gemm256_choose_splits(int M, int N, int K);
+// stream-K tail plan (gemm256.hip): tiles [full, tiles) are split sk ways along K (sk == 1: none), kps deep each
+struct Gemm256Plan {
+  int tiles, full, sk, kps;
+};
+Gemm256Plan gemm256_plan(int M, int N, int K);
+long gemm256_sk_slab_floats(const Gemm256Plan& p);  // fp32 partial slabs the stream-K tail needs
+long gemm256_sk_sync_ints(const Gemm256Plan& p);    // zeroed ints (ticket + flags) it needs; left zeroed after
 void launch_gemm256(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                     long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre,
-                    bool accumulate, float alpha, hipStream_t st, int splits = 1, float* ws = nullptr);
+                    bool accumulate, float alpha, hipStream_t st, int splits = 1, float* ws = nullptr,
+                    float* sk_slabs = nullptr, int* sk_sync = nullptr);
 // Output written to the (a, b) parity sub-grid of an H x W image: GEMM row (n, i, j) -> (n, i*stride+a,
 // j*stride+b). Used for stride-s data gradients decomposed by output parity (ops/conv.py _dgrad_strided_hip).
 struct SubGrid {

@@ -39,6 +39,7 @@ Controller::~Controller() {
   std::lock_guard<std::mutex> g(mu_);
   for (auto& kv : jobs_) kv.second->stop();
   jobs_.clear();
+  retiring_.clear();  // each finishes its requested delete, then joins
 }
 
 static bool crd_established(const Json& crd) {
@@ -108,6 +109,8 @@ void Controller::handle_event(const std::string& type, const Json& obj) {
     // same name, new object (deleted and re-created while no watch event reached us): retire the old worker
     log_info("TfJob %s was re-created (uid %s -> %s)", key.c_str(), job_uids_[key].c_str(), job.uid().c_str());
     it->second->request_delete();
+    retiring_.push_back(std::move(it->second));  // keeps running its delete; reaped by reap_finished
+    jobs_.erase(it);
   }
   if (type == "ADDED" || type == "MODIFIED") {
     log_info("Starting TfJob %s (phase=%s)", key.c_str(), job.status.phase.c_str());
@@ -118,13 +121,26 @@ void Controller::handle_event(const std::string& type, const Json& obj) {
 }
 
 void Controller::reap_finished() {
-  std::lock_guard<std::mutex> g(mu_);
-  for (auto it = jobs_.begin(); it != jobs_.end();) {
-    if (it->second->finished() && !job_rvs_.count(it->first)) {
-      job_uids_.erase(it->first);
-      it = jobs_.erase(it);
+  std::vector<std::unique_ptr<JobWorker>> done;  // joined after mu_ is released
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto it = jobs_.begin(); it != jobs_.end();) {
+      if (it->second->finished() && !job_rvs_.count(it->first)) {
+        job_uids_.erase(it->first);
+        done.push_back(std::move(it->second));
+        it = jobs_.erase(it);
+      } else {
+        ++it;
+      }
     }
-    else ++it;
+    for (auto it = retiring_.begin(); it != retiring_.end();) {
+      if ((*it)->finished()) {
+        done.push_back(std::move(*it));
+        it = retiring_.erase(it);
+      } else {
+        ++it;
+      }
+    }
   }
 }
 

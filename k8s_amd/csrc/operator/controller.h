@@ -16,6 +16,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "kube_api.h"
 #include "reconciler.h"
@@ -81,6 +82,9 @@ class Controller {
   std::map<std::string, std::unique_ptr<JobWorker>> jobs_;  // ns/name -> worker
   std::map<std::string, std::string> job_rvs_;               // ns/name -> resourceVersion
   std::map<std::string, std::string> job_uids_;              // ns/name -> uid of the object its worker runs
+  // workers of deleted-and-re-created TfJobs: still deleting the old object's children on their own thread;
+  // reaped (joined) once finished, never destroyed under mu_ while running
+  std::vector<std::unique_ptr<JobWorker>> retiring_;
 };
 
 }  // namespace tfop

@@ -1,6 +1,9 @@
 #include <ctime>
 #include <signal.h>
 #include "kube_api.h"
+
+#include <condition_variable>
+#include <thread>
 #include "log.h"
 
 #include <arpa/inet.h>
@@ -756,17 +759,22 @@ class HttpKubeApi : public KubeApi {
   }
 
   // the bearer token to send: an exec-plugin token is re-fetched shortly before its expiry (or when forced by a
-  // 401), a token file re-read every minute (client-go's cached token source does the same)
-  std::string token(bool force) {
-    std::lock_guard<std::mutex> g(cred_mu_);
+  // 401), a token file re-read every minute (client-go's cached token source does the same).
+  // The plugin never runs under cred_mu_ (every request and the leader-election renew take that lock): one refresh
+  // at a time runs on a background thread and swaps the new credentials in under the lock. A request waits for it
+  // only when its token is unusable (expired, or rejected with a 401), and then at most `wait_ms` (the request's
+  // own deadline); otherwise it goes out with the cached token. A failed refresh backs off (1 s doubling to 60 s)
+  // and the cached token stays in use.
+  std::string token(bool force, int wait_ms) {
+    std::unique_lock<std::mutex> lk(cred_mu_);
     const long long now = (long long)time(nullptr);
-    if (!cfg_.exec_config.empty() && (force || (cfg_.token_expiry > 0 && now >= cfg_.token_expiry - 60))) {
-      try {
-        refresh_exec_credential(cfg_);
-        log_info("exec credential refreshed (expires %lld)", cfg_.token_expiry);
-      } catch (const std::exception& e) {
-        log_error("exec credential refresh failed: %s", e.what());
-      }
+    if (!cfg_.exec_config.empty()) {
+      const bool near = cfg_.token_expiry > 0 && now >= cfg_.token_expiry - 60;
+      const bool unusable = force || cfg_.token.empty() || (cfg_.token_expiry > 0 && now >= cfg_.token_expiry);
+      if ((force || near) && !refreshing_ && (force || mono_ms() >= retry_after_ms_)) start_refresh();
+      const int w = wait_ms < 0 ? cfg_.exec_timeout_ms + 1000 : wait_ms;  // -1: a request without a deadline
+      if (unusable && refreshing_ && w > 0)
+        refresh_cv_.wait_for(lk, std::chrono::milliseconds(w), [&] { return !refreshing_; });
     }
     if (!cfg_.token_file.empty() && (force || now - token_read_ >= 60)) {
       try {
@@ -780,13 +788,22 @@ class HttpKubeApi : public KubeApi {
     return cfg_.token;
   }
 
+  ~HttpKubeApi() override {
+    std::thread t;
+    {
+      std::lock_guard<std::mutex> g(cred_mu_);
+      t.swap(refresher_);
+    }
+    if (t.joinable()) t.join();
+  }
+
   ApiResult request_once(const std::string& method, const std::string& path, const Json* body,
                          const std::string& ctype, bool force_refresh) {
     const int ovr = RequestTimeout::current();
     const Deadline dl = Deadline::in_ms(ovr >= 0 ? ovr : cfg_.timeout_ms);
     const std::string b = body ? body->dump() : "";
     ClusterConfig rc = cfg_view();
-    rc.token = token(force_refresh);
+    rc.token = token(force_refresh, (int)dl.left_ms());
     const std::string req = build_request(rc, method, path, b, ctype, true);
     ApiResult res;
     for (int attempt = 0; attempt < 2; ++attempt) {
@@ -856,7 +873,7 @@ class HttpKubeApi : public KubeApi {
     auto c = std::make_unique<Conn>(cfg_view());
     if (!c->open(dl, err)) return nullptr;
     ClusterConfig wc = cfg_view();
-    wc.token = token(false);
+    wc.token = token(false, (int)dl.left_ms());
     if (!c->write_all(build_request(wc, "GET", path, "", "", true), dl)) {
       err = "write failed";
       return nullptr;
@@ -897,8 +914,52 @@ class HttpKubeApi : public KubeApi {
     return cfg_;
   }
 
+  static long long mono_ms() {
+    return std::chrono::duration_cast<std::chrono::milliseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+
+  // with cred_mu_ held and no refresh running: run the exec plugin on the (single) refresher thread
+  void start_refresh() {
+    if (refresher_.joinable()) refresher_.join();  // the previous refresher has already cleared refreshing_
+    refreshing_ = true;
+    ClusterConfig job;
+    job.exec_config = cfg_.exec_config;
+    job.exec_timeout_ms = cfg_.exec_timeout_ms;
+    refresher_ = std::thread([this, job]() mutable {
+      std::string err;
+      try {
+        job.token_expiry = 0;
+        refresh_exec_credential(job);
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
+      std::lock_guard<std::mutex> g(cred_mu_);
+      if (err.empty()) {
+        if (!job.token.empty()) cfg_.token = job.token;
+        if (!job.cert_data.empty()) cfg_.cert_data = job.cert_data;
+        if (!job.key_data.empty()) cfg_.key_data = job.key_data;
+        cfg_.token_expiry = job.token_expiry;
+        backoff_ms_ = 0;
+        retry_after_ms_ = 0;
+        log_info("exec credential refreshed (expires %lld)", cfg_.token_expiry);
+      } else {
+        backoff_ms_ = backoff_ms_ ? std::min<long long>(2 * backoff_ms_, 60000) : 1000;
+        retry_after_ms_ = mono_ms() + backoff_ms_;
+        log_error("exec credential refresh failed: %s (cached token kept; next try in %lld ms)", err.c_str(),
+                  backoff_ms_);
+      }
+      refreshing_ = false;
+      refresh_cv_.notify_all();
+    });
+  }
+
   ClusterConfig cfg_;
   std::mutex cred_mu_;        // cfg_'s credentials change on refresh
+  std::condition_variable refresh_cv_;
+  bool refreshing_ = false;   // an exec-plugin run is in flight on refresher_
+  std::thread refresher_;
+  long long backoff_ms_ = 0, retry_after_ms_ = 0;
   long long token_read_ = 0;  // last read of cfg_.token_file
   std::mutex mu_;
   std::vector<std::unique_ptr<Conn>> idle_;

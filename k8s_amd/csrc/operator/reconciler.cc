@@ -187,6 +187,12 @@ bool TrainingJob::update_status() {
       ApiResult g = call("GET", tfjobs_path(job_.ns(), job_.name()));
       if (!g.ok()) return false;
       TfJob cur = tfjob_from_json(g.body);
+      if (!job_.uid().empty() && cur.uid() != job_.uid()) {
+        // the name now belongs to a re-created object: never write this (old) job's spec / status onto it
+        log_warn("Job %s: uid changed (%s -> %s); dropping the status write of the old object", key().c_str(),
+                 job_.uid().c_str(), cur.uid().c_str());
+        return false;
+      }
       want.metadata = cur.metadata.clone();
       continue;
     }
@@ -308,8 +314,8 @@ void JobWorker::run() {
         // ThreadSanitizer does not intercept (it then misreports the mutex as double-locked); a wall-clock
         // jump only moves one resync tick
         cv_.wait_until(lk, std::chrono::system_clock::now() + interval_, [&] { return poked_ || deleted_ || stop_; });
-        if (stop_) break;
-        del = deleted_;
+        del = deleted_;  // a requested delete is carried out even when a stop arrives with it (retired workers)
+        if (stop_ && !del) break;
         poked_ = false;
         upd.swap(pending_update_);
       }

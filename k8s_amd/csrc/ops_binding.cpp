@@ -7,6 +7,9 @@
 #include <cstdlib>
 
 #include <torch/extension.h>
+
+#include <map>
+#include <mutex>
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
 
@@ -441,6 +444,25 @@ static bool use_gemm256(long M, long N, long K, bool a_kmajor, bool b_kmajor) {
   return m != 0 && k8s_amd::gemm256_eligible((int)M, (int)N, (int)K, a_kmajor, b_kmajor);
 }
 
+// $K8S_AMD_GEMM256_SK=0 turns the stream-K tail off (A/B knob, read per call; tests run both sides)
+static bool sk_enabled() {
+  const char* e = std::getenv("K8S_AMD_GEMM256_SK");
+  return !(e && e[0] == '0');
+}
+
+// Zero-initialised int words for the stream-K tickets / flags, one buffer per device, grown on demand. The kernel
+// leaves every word it used at zero again, so no per-call clear is needed. GEMMs run on one compute stream, so one
+// buffer per device is never used by two launches at once.
+static int* sk_sync_words(long n, const c10::Device& dev) {
+  static std::mutex mu;
+  static std::map<int, Tensor> bufs;
+  std::lock_guard<std::mutex> g(mu);
+  Tensor& t = bufs[dev.index()];
+  if (!t.defined() || t.numel() < n)
+    t = torch::zeros({std::max<long>(n, 1 << 16)}, torch::TensorOptions().dtype(at::kInt).device(dev));
+  return t.data_ptr<int>();
+}
+
 Tensor mask_apply(Tensor src, Tensor mask) {
   check_cuda(src, "src");
   check_dtype(src, at::kBFloat16, "src");
@@ -494,9 +516,19 @@ Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tens
   if (xfb) TORCH_CHECK(!a_kmajor && !b_kmajor && out_f32 && !bias && act == 0 && !pre && !add_src &&
                            N % xform_c == 0, "normalize-on-load GEMM: the plain weight-gradient form only");
   if (!xfb && !add_src && use_gemm256(M, N, K, a_kmajor, b_kmajor)) {
+    // stream-K tail of a partial-wave grid: fp32 partial slabs (caching allocator, stream-ordered) and the
+    // self-resetting ticket / flag words
+    const k8s_amd::Gemm256Plan plan = k8s_amd::gemm256_plan((int)M, (int)N, (int)K);
+    Tensor slabs;
+    int* sync = nullptr;
+    if (plan.sk > 1 && sk_enabled()) {
+      slabs = torch::empty({k8s_amd::gemm256_sk_slab_floats(plan)}, a.options().dtype(at::kFloat));
+      sync = sk_sync_words(k8s_amd::gemm256_sk_sync_ints(plan), a.device());
+    }
     k8s_amd::launch_gemm256(cbf(a), a.stride(0), a_kmajor, cbf(b), b.stride(0), b_kmajor, c.data_ptr(), N, out_f32,
                             (int)M, (int)N, (int)K, bias ? bias->data_ptr<float>() : nullptr, (int)act,
-                            pre ? bf(*pre) : nullptr, accumulate, (float)alpha, cur_stream());
+                            pre ? bf(*pre) : nullptr, accumulate, (float)alpha, cur_stream(), 1, nullptr,
+                            sync ? f32(slabs) : nullptr, sync);
     return c;
   }
   // tall-K fp32 products whose output is too small for the 256 x 256 kernel alone (the ResNet 1x1 weight gradients):

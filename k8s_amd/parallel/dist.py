@@ -90,6 +90,21 @@ def task_gpus_table() -> Optional[Dict[str, int]]:
         return None
 
 
+def own_task_processes(role: str) -> int:
+    """Processes THIS task runs (one per GPU): its role's entry in ``TFJOB_TASK_GPUS`` when the operator set one,
+    else this container's device count. The world size every rank computes (``rank_from_tf_config``) uses the same
+    table, so a task whose container sees fewer GPUs than the table says would leave the rendezvous one rank short
+    until its timeout: that is refused here, up front, with the two numbers."""
+    mine = local_device_count()
+    table = task_gpus_table()
+    if table is None or role not in table:
+        return mine
+    want = max(1, int(table[role]))
+    if want > mine:
+        raise ValueError("TFJOB_TASK_GPUS gives a %s task %d GPUs but this container sees %d" % (role, want, mine))
+    return want
+
+
 def rank_from_tf_config(tf_config: str, port_offset: int = 0, local_rank: Optional[int] = None,
                         task_gpus: Optional[Dict[str, int]] = None) -> RankInfo:
     """Deterministic rank assignment from a TF_CONFIG JSON string.
@@ -140,6 +155,9 @@ def rank_from_tf_config(tf_config: str, port_offset: int = 0, local_rank: Option
         return max(1, int(table.get(role, mine)))
 
     counts = [procs(r) for r, _, _ in order]
+    if table is not None and ttype in table and ttype != "ps" and procs(ttype) > mine:
+        raise ValueError("TFJOB_TASK_GPUS gives a %s task %d GPUs but this container sees %d"
+                         % (ttype, procs(ttype), mine))
     if ttype == "ps":
         rank = -1
     elif (ttype, tidx) in keys:

@@ -65,14 +65,15 @@ def parse(argv=None):
     ap.add_argument("--max-grad-norm", type=float, default=None)
     ap.add_argument("--strategy", default="allreduce", choices=["allreduce", "ps"])
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    # Both multi-GPU side-stream paths below are opt-in (the examples for configs 3/4 turn them on): they have run on
+    # gloo and on 2 ranks sharing one GPU, not yet on RCCL with one rank per GPU.
     ap.add_argument("--grad-comm", default="auto", choices=["auto", "fp32", "bf16"],
-                    help="gradient transport: bf16 = all-to-all reduce-scatter with fp32 accumulation; auto = bf16 "
-                         "for the Llama models (16 GB instead of 32 GB per step on Llama-3-8B), fp32 otherwise")
+                    help="gradient transport: bf16 = all-to-all reduce-scatter with fp32 accumulation (16 GB instead "
+                         "of 32 GB per step on Llama-3-8B); auto = fp32")
     ap.add_argument("--zero", default="auto", choices=["auto", "0", "1"],
-                    help="ZeRO-1 for --strategy allreduce: reduce-scatter + owner update + all-gather (same xGMI "
-                         "bytes as an all-reduce; optimizer state and update pass / world per rank). auto = on for "
-                         "Adam with world > 1 (the optimizer is ~19%% of a Llama-3-8B step), off for SGD (ResNet's "
-                         "update is 0.1%% of the step and its all-gather would be exposed)")
+                    help="ZeRO-1 for --strategy allreduce: reduce-scatter + owner update (fp32 master and moments "
+                         "stay 1/world per rank) + bf16 all-gather of the updated weights (same xGMI bytes as an "
+                         "all-reduce; optimizer state and update pass / world per rank). auto = off")
     ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
     ap.add_argument("--mlm-head", default="gathered", choices=["gathered", "every-token"],
                     help="BERT: MLM head on the masked-position slots (the original pretraining data format) or on "
@@ -299,9 +300,9 @@ def train(a) -> int:
 
     batch = a.batch or _DEFAULT_BATCH[a.model]
     opt_name = a.optimizer or MODEL_OPTIMIZER[a.model]
-    zero = a.zero == "1" or (a.zero == "auto" and world > 1 and opt_name == "adam")
+    zero = a.zero == "1"
     sharded = a.strategy == "ps" or (zero and world > 1)
-    comm = a.grad_comm if a.grad_comm != "auto" else ("bf16" if a.model.startswith("llama") else "fp32")
+    comm = a.grad_comm if a.grad_comm != "auto" else "fp32"
     metrics = _Metrics(a.logdir, chief)
     metrics.event(event="start", rank=rank, world=world, role=info.role, model=a.model, strategy=a.strategy,
                   device=str(dev), start_time=t_start, zero1=bool(sharded and world > 1), grad_comm=comm,
@@ -493,13 +494,9 @@ def _replica_processes() -> int:
         return 1
     if ttype == "ps":
         return 1
-    from k8s_amd.parallel.dist import local_device_count, task_gpus_table
+    from k8s_amd.parallel.dist import own_task_processes
 
-    n = local_device_count()
-    table = task_gpus_table()
-    if table is not None and ttype in table:
-        n = max(1, min(n, table[ttype])) if table[ttype] > 0 else 1
-    return n
+    return own_task_processes(ttype)
 
 
 def _run_replica_children(n: int, argv) -> int:
@@ -542,7 +539,11 @@ def _run_replica_children(n: int, argv) -> int:
 
 
 def main(argv=None) -> int:
-    n = _replica_processes()
+    try:
+        n = _replica_processes()
+    except ValueError as e:  # the operator's GPU table and this container's devices disagree: not retryable
+        print("error: %s" % e, file=sys.stderr, flush=True)
+        return EXIT_PERMANENT
     if n > 1:
         return _run_replica_children(n, argv)
     a = parse(argv)

@@ -193,3 +193,34 @@ def test_periodic_resync_recovers_a_lost_event():
         c.server.blackhole_watches()
         c.create(os.path.join(REPO, "examples", "tf_job.yaml"))
         _wait_state(c, "example-job", {"Succeeded"}, timeout=60)
+
+
+def test_deleted_and_recreated_job_while_the_watch_is_blind():
+    """a TfJob deleted and re-created under the same name while no watch event reaches the
+    operator (watch black-holed; only the periodic relist sees it) is a new object (new uid). The old worker is
+    retired -- it still deletes the old object's children, off the controller lock -- and never writes the old spec
+    or status onto the new object; the new object gets its own RuntimeId and runs to completion."""
+    with LocalCluster(operator_args=["-watch-timeout", "10m", "-resync-period", "1s"]) as c:
+        marker = os.path.join(c.log_dir, "never")
+        c.create(_job("again", "while [ ! -f %s ]; do sleep 0.1; done; exit 0" % marker))
+        end = time.time() + 30
+        while c.get("again").get("status", {}).get("phase") != "Running" and time.time() < end:
+            time.sleep(0.1)
+        old = c.get("again")
+        assert old["status"]["phase"] == "Running", old.get("status")
+        c.server.blackhole_watches()
+        c.delete("again")
+        c.create(_job("again", "exit 0"))
+        j = _wait_state(c, "again", {"Succeeded"}, timeout=60)
+        assert j["metadata"]["uid"] != old["metadata"]["uid"]
+        assert j["spec"]["RuntimeId"] != old["spec"]["RuntimeId"]
+        assert "was re-created" in c.operator_log()
+        # nothing of the old runtime is left
+        end = time.time() + 20
+        while time.time() < end:
+            left = [o["metadata"]["name"] for o in c.client.get("/apis/batch/v1/namespaces/default/jobs")["items"]
+                    if old["spec"]["RuntimeId"] in o["metadata"]["name"]]
+            if not left:
+                break
+            time.sleep(0.2)
+        assert not left, left

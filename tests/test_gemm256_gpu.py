@@ -93,3 +93,68 @@ def test_gemm256_long_k(cuda):
     ref = a.float() @ b.float().t()
     c = _C().gemm(a, True, b, True, None, True, None, 0, None, False, 1.0, 1)
     assert _rel(c, ref) < 1e-3
+
+
+# stream-K tail (gemm256_plan): T = w * 256 + r tiles with r <= 128 run the last r tiles split sk ways along K with
+# the in-kernel fixed-order fix-up. (M, N, K) -> tiles, sk: 16x24 = 384 -> 2 (Llama QKV); 8x16 = 128 -> 2 (a single
+# partial wave); 16x21 = 336 -> 3; 16x20 = 320 -> 4; ragged edges on a 2-split tail.
+SK_SHAPES = [(4096, 6144, 4096), (2048, 4096, 2048), (4096, 5376, 3072), (4096, 5120, 4096), (4000, 6136, 2048)]
+
+
+def _sk_env(monkeypatch, on):
+    monkeypatch.setenv("K8S_AMD_GEMM256_SK", "1" if on else "0")
+
+
+@pytest.mark.parametrize("M,N,K", SK_SHAPES)
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, False)])
+def test_gemm256_stream_k_tail_matches_fp32(cuda, monkeypatch, M, N, K, ak, bk):
+    """the stream-K tail against an fp32 PyTorch product, bf16 and fp32 outputs; the
+    result is deterministic (bit-identical over repeated launches, whichever split arrives last)."""
+    torch.manual_seed(3)
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    b = torch.randn(N, K, device=cuda).bfloat16()
+    ref = a.float() @ b.float().t()
+    A = a if ak else a.t().contiguous()
+    B = b if bk else b.t().contiguous()
+    _sk_env(monkeypatch, True)
+    c = _C().gemm(A, ak, B, bk, None, True, None, 0, None, False, 1.0, 1)
+    assert _rel(c, ref) < 1e-4
+    for _ in range(3):
+        assert torch.equal(_C().gemm(A, ak, B, bk, None, True, None, 0, None, False, 1.0, 1), c)
+    cb = _C().gemm(A, ak, B, bk, None, False, None, 0, None, False, 1.0, 1)
+    assert _rel(cb, ref) < 1e-2
+    _sk_env(monkeypatch, False)  # the whole-tile path agrees to fp32 rounding
+    c0 = _C().gemm(A, ak, B, bk, None, True, None, 0, None, False, 1.0, 1)
+    assert _rel(c0, c) < 1e-5
+
+
+@pytest.mark.parametrize("act", [0, 2])
+def test_gemm256_stream_k_tail_epilogues(cuda, monkeypatch, act):
+    """The fix-up hands the summed tile to the normal epilogue: bias + GELU + pre-activation copy, and an fp32
+    accumulate into an existing buffer with alpha, on a 2-split tail."""
+    torch.manual_seed(4)
+    M, N, K = 4096, 6144, 4096
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) * 0.02).bfloat16()
+    bvec = torch.randn(N, device=cuda)
+    _sk_env(monkeypatch, True)
+    pre = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    y = _C().gemm(a, True, w, True, None, False, bvec, act, pre, False, 1.0, 1)
+    p_ref = a.float() @ w.float().t() + bvec
+    y_ref = F.gelu(p_ref, approximate="tanh") if act == 2 else p_ref
+    assert _rel(pre, p_ref) < 1e-2 and _rel(y, y_ref) < 1e-2
+    out = torch.full((M, N), -1.5, device=cuda)
+    _C().gemm(a, True, w, True, out, True, None, 0, None, True, 0.5, 1)
+    assert _rel(out + 1.5, 0.5 * (a.float() @ w.float().t())) < 1e-4
+
+
+def test_gemm256_stream_k_sync_words_reset(cuda, monkeypatch):
+    """Back-to-back launches of different stream-K plans reuse the ticket / flag words: every launch must leave
+    them zero (a stale ticket would make a split skip its fix-up and write a partial tile)."""
+    torch.manual_seed(5)
+    _sk_env(monkeypatch, True)
+    for M, N, K in SK_SHAPES[:4] * 2:
+        a = torch.randn(M, K, device=cuda).bfloat16()
+        b = torch.randn(N, K, device=cuda).bfloat16()
+        c = _C().gemm(a, True, b, True, None, True, None, 0, None, False, 1.0, 1)
+        assert _rel(c, a.float() @ b.float().t()) < 1e-4, (M, N, K)

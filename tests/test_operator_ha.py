@@ -271,10 +271,11 @@ def test_exec_credential_is_refreshed_before_expiry_and_on_401(tmp_path):
 
     srv = FakeApiServer().start()
     try:
-        # short-lived token: every request is within the 60 s refresh margin, so the plugin runs again each time
+        # short-lived token: every request is within the 60 s refresh margin, so the plugin runs again (in the
+        # background, the still-valid cached token goes out meanwhile) before each next request
         plug, cnt = _counting_plugin(tmp_path, expiry_s=5)
         srv.httpd.accept_token = lambda t: t.startswith("tok-")
-        codes = _op().kubeconfig_requests(_exec_kubeconfig(plug), srv.url, n=3)
+        codes = _op().kubeconfig_requests(_exec_kubeconfig(plug), srv.url, n=3, interval_ms=400)
         assert codes == [200, 200, 200]
         assert int(cnt.read_text()) >= 3 and len(set(srv.httpd.accepted)) >= 2, srv.httpd.accepted
         # no expiry, but the server rejects the first token: one 401, a forced refresh, the replay succeeds
@@ -299,3 +300,35 @@ def test_exec_credential_is_refreshed_before_expiry_and_on_401(tmp_path):
         assert time.time() - t0 < 5
     finally:
         del os.environ["K8S_AMD_EXEC_TIMEOUT_MS"]
+
+
+def test_slow_exec_plugin_does_not_block_requests(tmp_path):
+    """the exec plugin never runs under the credential lock. With a token inside its refresh
+    margin and a plugin that takes 2 s, requests keep going out with the cached (still valid) token while ONE
+    refresh runs in the background -- so a leader-election renew (15 s lease, 5 s renew deadline) is never held up
+    by a slow plugin -- and the new token is used once it arrives."""
+    from k8s_amd.fakeapi.server import FakeApiServer
+
+    runs = tmp_path / "runs"
+    runs.write_text("")
+    plug = tmp_path / "slow.sh"
+    plug.write_text("#!/bin/sh\necho x >> %s\nn=$(wc -l < %s)\n[ $n -gt 1 ] && sleep 2\n"
+                    "exp=$(date -u -d '+30 seconds' +%%Y-%%m-%%dT%%H:%%M:%%SZ)\n"
+                    "echo '{\"apiVersion\":\"client.authentication.k8s.io/v1\",\"kind\":\"ExecCredential\","
+                    "\"status\":{\"token\":\"tok-'$n'\",\"expirationTimestamp\":\"'$exp'\"}}'\n" % (runs, runs))
+    plug.chmod(0o755)
+    srv = FakeApiServer().start()
+    try:
+        srv.httpd.accept_token = lambda t: t.startswith("tok-")
+        t0 = time.time()
+        codes = _op().kubeconfig_requests(_exec_kubeconfig(plug), srv.url, n=12, interval_ms=250)
+        took = time.time() - t0
+        assert codes == [200] * 12
+        # 12 requests 250 ms apart ~ 2.75 s (+ the first, synchronous plugin run); a blocking refresh would add
+        # 2 s per request inside the margin
+        assert took < 6.0, took
+        assert srv.httpd.accepted[0] == "tok-1" and "tok-2" in srv.httpd.accepted, srv.httpd.accepted
+        # one refresh at a time: at most the initial run + two sequential 2 s refreshes started in ~3 s
+        assert len(runs.read_text().split()) <= 3
+    finally:
+        srv.stop()
