@@ -336,7 +336,8 @@ struct SkArgs {
 // splits own + other (IEEE addition commutes: bit-identical whoever arrives last), for more splits every split's
 // slab in split order (the reducer writes its own too) -- then resets the ticket and flags for the next launch and
 // runs the normal epilogue. Returns true in the reducer (which goes on to the epilogue).
-__device__ __forceinline__ bool sk_fixup(f32x4_t (&acc)[8][4], const SkArgs& SK, int slot, int split, char* smem,
+template <int NJ = 4, int NT = 512>
+__device__ __forceinline__ bool sk_fixup(f32x4_t (&acc)[8][NJ], const SkArgs& SK, int slot, int split, char* smem,
                                       int tid) {
   const int sk = SK.sk;
   int* cnt = SK.sync + (long)slot * (1 + sk);
@@ -355,8 +356,8 @@ __device__ __forceinline__ bool sk_fixup(f32x4_t (&acc)[8][4], const SkArgs& SK,
 #pragma unroll
     for (int a = 0; a < 8; ++a)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        __builtin_amdgcn_raw_buffer_store_b128(acc[a][j], rs, voff, split * 262144 + (a * 4 + j) * 8192, 0);
+      for (int j = 0; j < NJ; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(acc[a][j], rs, voff, split * 262144 + (a * NJ + j) * NT * 16, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
@@ -379,17 +380,18 @@ __device__ __forceinline__ bool sk_fixup(f32x4_t (&acc)[8][4], const SkArgs& SK,
   for (int z = sk == 2 ? 1 - split : 0; z < sk; z += (sk == 2 ? 2 : 1)) {
     const bool assign = sk > 2 && z == 0;
 #pragma unroll
-    for (int a = 0; a < 8; a += 2) {
-      f32x4_t v[2][4];
+    for (int a = 0; a < 8; a += 8 / NJ) {
+      constexpr int R = 8 / NJ;  // accumulator rows per chunk: 8 loads of 16 B per lane
+      f32x4_t v[R][NJ];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < R; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          v[i][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, z * 262144 + ((a + i) * 4 + j) * 8192, 0);
+        for (int j = 0; j < NJ; ++j)
+          v[i][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, z * 262144 + ((a + i) * NJ + j) * NT * 16, 0);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < R; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[a + i][j] = assign ? v[i][j] : acc[a + i][j] + v[i][j];
+        for (int j = 0; j < NJ; ++j) acc[a + i][j] = assign ? v[i][j] : acc[a + i][j] + v[i][j];
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -506,6 +508,7 @@ __global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, 
   epilogue256(acc, E, smem, M, N, m0, n0, wid, wr, wc, lane);
 }
 }  // namespace g256r
+
 
 namespace g256 {
 template <class AS, class BS>

@@ -51,6 +51,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--forms", default="fwd,dgrad,wgrad", help="comma list of fwd,dgrad,wgrad")
     ap.add_argument("--variants", nargs="*", default=[], help="extra ENV=VALUE[,ENV=VALUE] arms, e.g. K8S_AMD_GEMM256=0 (force the 128 x 128 kernel)")
     a = ap.parse_args()
     groups = [a.only] if a.only else list(LAYERS)
@@ -67,6 +68,8 @@ def main():
                           lambda: g.t() @ x, 2.0 * M * N * K),
             }
             for form, (ours, blas, flop) in forms.items():
+                if form not in a.forms.split(","):
+                    continue
                 to, tb, tv = [], [], {v: [] for v in a.variants}
                 for _ in range(a.rounds):
                     to.append(timeit(ours))
