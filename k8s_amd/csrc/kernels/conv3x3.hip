@@ -1,0 +1,260 @@
+// K2: staged-window 3 x 3 / stride-1 / pad-1 NHWC convolution for gfx950 (the ResNet-50 bottleneck conv2 of every
+// block but the stage-entry ones, forward and -- with spatially flipped, in/out-swapped weights -- data gradient).
+//
+//   y[n][h][w][k] = sum_{r,s,c} x[n][h + r - 1][w + s - 1][c] * wt[k][r][s][c]
+//
+// The implicit GEMM of gemm.hip (ConvA) gathers im2col(x) through L2: every input element is fetched into LDS nine
+// times, one 16-B LDS-DMA piece per (pixel, tap, 8 channels). Here a block owns RT whole image rows (RT * W output
+// pixels) x KT output channels and stages the zero-padded (RT + 2) x (W + 2) input WINDOW of each 64-channel slice
+// once; the nine taps read the MFMA A operand from that window at a shifted position. The slice's weights stream per
+// tap ([KT][64] bf16, double-buffered, the next tap's DMA behind this tap's MFMAs).
+//
+// XF (BatchNorm + ReLU normalised on load, see gemm.hip XForm): after the window lands, each thread rewrites its
+// window chunks in place as relu(x * scale + shift) -- ONCE per staged element, not once per tap (the implicit GEMM's
+// on-load path re-applied it nine times) -- leaving the zero padding zero. The BN apply pass of bn1 (read x, write z)
+// and the z tensor then disappear from the ResNet forward.
+//
+// Layout / tiling:
+//  * 256 threads = 4 waves as 2 (pixels) x 2 (channels); wave piece = MF x 16 pixels x KT / 2 channels, MF x NF
+//    tiles of v_mfma_f32_16x16x32_bf16 (operands swapped: each lane ends with 4 consecutive output channels).
+//  * LDS images [position][64 ch] (window) and [row][64 ch] (weights), 128-B rows, 16-B chunk c of row p stored at
+//    c ^ ((p >> 1) & 7): the 16 lanes of a fragment read 16 consecutive positions -> conflict-free ds_read_b128.
+//  * epilogue: the bf16 tile goes through LDS, leaves as 16-B row segments, and the per-channel sum / sum of squares
+//    of the stored values are accumulated for the following BatchNorm (the [STAT_REPL][2][K] layout of gemm.hip).
+//  * ~60-71 KB LDS, <= 128 VGPRs: 2 blocks per CU, so one block's window staging overlaps the other's MFMAs.
+#include <stdexcept>
+
+#include "common.h"
+#include "launchers.h"
+#include "mfma.h"
+
+namespace k8s_amd {
+
+namespace c3 {
+constexpr int THREADS = 256;
+constexpr int STAT_REPL = 32;  // = gemm.hip STAT_REPL = kConvStatReplicas
+__device__ __attribute__((aligned(64))) uint16_t g_c3_zero[64];  // source of the zero padding
+
+__device__ __forceinline__ int swz(int p) { return (p >> 1) & 7; }
+
+template <int W, int RT, int KT, bool XF>
+struct Geo {
+  static constexpr int WP = W + 2, WIN = (RT + 2) * WP, P = RT * W;
+  static constexpr int MF = (P + 31) / 32, NF = KT / 32;
+  static constexpr int WIN_B = WIN * 128, WT_B = KT * 128;
+  static constexpr int STAGE_B = 32 * MF * KT * 2;  // epilogue C tile
+  static constexpr int LDS = (WIN_B + 2 * WT_B) > STAGE_B ? (WIN_B + 2 * WT_B) : STAGE_B;
+  static_assert(LDS >= THREADS * 16 * 4, "room for the statistics partials");
+};
+
+template <int W, int RT, int KT, bool XF>
+__global__ void __launch_bounds__(THREADS, 2) conv3x3_kernel(const uint16_t* __restrict__ x,
+                                                            const uint16_t* __restrict__ wt, uint16_t* __restrict__ y,
+                                                            float* __restrict__ stats, const float* __restrict__ xf,
+                                                            int H, int C, int K, int tiles_per_img) {
+  using G = Geo<W, RT, KT, XF>;
+  constexpr int WP = G::WP, WIN = G::WIN, P = G::P, MF = G::MF, NF = G::NF;
+  __shared__ __attribute__((aligned(1024))) char smem[G::LDS];
+  char* const win = smem;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tile = blockIdx.x;
+  const int n = tile / tiles_per_img, h0 = (tile - n * tiles_per_img) * RT;
+  const int k0 = blockIdx.y * KT;
+
+  // this lane's window position (tap (0, 0)) for each of its MF pixel fragments; padding rows of the last fragment
+  // read position 0 (their outputs are never stored)
+  int pos0[MF];
+#pragma unroll
+  for (int f = 0; f < MF; ++f) {
+    const int m = (wm * MF + f) * 16 + (lane & 15);
+    const int row = m / W, col = m - row * W;
+    pos0[f] = m < P ? row * WP + col : 0;
+  }
+  f32x4_t acc[MF][NF];
+#pragma unroll
+  for (int f = 0; f < MF; ++f)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[f][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // a thread's window chunks c = i * 256 + tid all hold the same logical 8 channels (256 % 16 == 0)
+  const int lchunk = (tid & 7) ^ ((tid >> 4) & 7);
+  auto stage_w = [&](int tap, int c0, int slot) {
+    char* d = smem + G::WIN_B + slot * G::WT_B;
+#pragma unroll
+    for (int i = 0; i < KT * 8 / THREADS; ++i) {
+      const int c = i * THREADS + tid, row = c >> 3, lc = (c & 7) ^ swz(row);
+      glds16(wt + ((long)(k0 + row) * 9 + tap) * C + c0 + lc * 8, d + (i * THREADS + wid * 64) * 16);
+    }
+  };
+
+  const int nslices = C >> 6;
+  for (int cs = 0; cs < nslices; ++cs) {
+    const int c0 = cs * 64;
+    if (cs) __syncthreads();  // every wave is done with the previous slice's window and weights
+    // ---- window rows h0 - 1 .. h0 + RT, columns -1 .. W (zero page outside the image), by LDS-DMA
+#pragma unroll 1
+    for (int i = 0; i < (WIN * 8 + THREADS - 1) / THREADS; ++i) {
+      const int c = i * THREADS + tid;
+      if (c < WIN * 8) {  // lanes past the window stay inactive (they would write into the weight slots)
+        const int p = c >> 3, wr = p / WP, wc = p - wr * WP, h = h0 - 1 + wr, w = wc - 1;
+        const bool in = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+        const void* src = in ? (const void*)(x + (((long)n * H + h) * W + w) * C + c0 + lchunk * 8)
+                             : (const void*)g_c3_zero;
+        glds16(src, win + __builtin_amdgcn_readfirstlane(i * THREADS + wid * 64) * 16);
+      }
+    }
+    stage_w(0, c0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if constexpr (XF) {  // relu(x * scale + shift) in place, once per staged element; padding stays zero
+      float sc[8], sh[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sc[j] = xf[c0 + lchunk * 8 + j];
+        sh[j] = xf[C + c0 + lchunk * 8 + j];
+      }
+#pragma unroll 1
+      for (int i = 0; i < (WIN * 8 + THREADS - 1) / THREADS; ++i) {
+        const int c = i * THREADS + tid;
+        if (c < WIN * 8) {
+          const int p = c >> 3, wr = p / WP, wc = p - wr * WP, h = h0 - 1 + wr, w = wc - 1;
+          if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
+            bf16x8_t* q = reinterpret_cast<bf16x8_t*>(win + c * 16);
+            const bf16x8_t v = *q;
+            float o[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = fmaxf(__builtin_fmaf(bf2f((uint16_t)v[j]), sc[j], sh[j]), 0.f);
+            *q = pack_bf16x8(o);
+          }
+        }
+      }
+      __syncthreads();
+    }
+#pragma unroll 1
+    for (int t = 0; t < 9; ++t) {
+      if (t + 1 < 9) stage_w(t + 1, c0, (t + 1) & 1);  // its slot was last read in tap t - 1 (barrier since)
+      const int tr = t / 3, toff = tr * WP + (t - tr * 3);
+      const char* ws = smem + G::WIN_B + (t & 1) * G::WT_B;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ch = kk * 4 + (lane >> 4);
+        mfma_bf16x8 af[MF], bfr[NF];
+#pragma unroll
+        for (int f = 0; f < MF; ++f) {
+          const int p = pos0[f] + toff;
+          af[f] = __builtin_bit_cast(mfma_bf16x8,
+                                     *reinterpret_cast<const bf16x8_t*>(win + p * 128 + ((ch ^ swz(p)) << 4)));
+        }
+#pragma unroll
+        for (int j = 0; j < NF; ++j) {
+          const int r = wn * (KT / 2) + j * 16 + (lane & 15);
+          bfr[j] = __builtin_bit_cast(mfma_bf16x8,
+                                      *reinterpret_cast<const bf16x8_t*>(ws + r * 128 + ((ch ^ swz(r)) << 4)));
+        }
+#pragma unroll
+        for (int f = 0; f < MF; ++f)
+#pragma unroll
+          for (int j = 0; j < NF; ++j) acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[f], acc[f][j], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tap t + 1's weights landed
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: [32 MF][KT] bf16 tile in LDS (16-B chunk c of row r at c ^ (r % CPR)), 16-B copy-out with the BN
+  // statistics of the stored values
+  constexpr int CPR = KT / 8;
+  uint16_t* const ctile = reinterpret_cast<uint16_t*>(smem);
+#pragma unroll
+  for (int f = 0; f < MF; ++f) {
+    const int row = (wm * MF + f) * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int col = wn * (KT / 2) + j * 16 + (lane >> 4) * 4;
+      const bf16x4_t o = __builtin_bit_cast(bf16x4_t, __builtin_convertvector(acc[f][j], bf16v4_t));
+      *reinterpret_cast<bf16x4_t*>(ctile + row * KT + (((col >> 3) ^ (row % CPR)) << 3) + (col & 4)) = o;
+    }
+  }
+  __syncthreads();
+  constexpr int RSTEP = THREADS / CPR;
+  const int c = tid % CPR, row0 = tid / CPR;
+  f32x2_t s2[4], q2[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) s2[r] = q2[r] = f32x2_t{0.f, 0.f};
+#pragma unroll 2
+  for (int m = row0; m < P; m += RSTEP) {
+    const int hr = m / W, h = h0 + hr;
+    if (h < H) {
+      const bf16x8_t o = *reinterpret_cast<const bf16x8_t*>(ctile + m * KT + ((c ^ (m % CPR)) << 3));
+      *reinterpret_cast<bf16x8_t*>(y + (((long)n * H + h) * W + (m - hr * W)) * K + k0 + c * 8) = o;
+      if (stats) {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(&o);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const f32x2_t v = {__uint_as_float(w[r] << 16), __uint_as_float(w[r] & 0xFFFF0000u)};
+          s2[r] += v;
+          q2[r] = __builtin_elementwise_fma(v, v, q2[r]);
+        }
+      }
+    }
+  }
+  if (stats) {
+    __syncthreads();
+    float* part = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      part[tid * 16 + 2 * r] = s2[r][0];
+      part[tid * 16 + 2 * r + 1] = s2[r][1];
+      part[tid * 16 + 8 + 2 * r] = q2[r][0];
+      part[tid * 16 + 8 + 2 * r + 1] = q2[r][1];
+    }
+    __syncthreads();
+    if (tid < 2 * KT) {
+      const int col = tid % KT, which = tid / KT, cc = col >> 3, r = col & 7;
+      float v = 0.f;
+#pragma unroll 4
+      for (int t = cc; t < THREADS; t += CPR) v += part[t * 16 + which * 8 + r];
+      atomicAdd(stats + (long)(tile % STAT_REPL) * 2 * K + (long)which * K + k0 + col, v);
+    }
+  }
+}
+
+template <int W, int RT, int KT, bool XF>
+static void launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const float* xf, int N, int H,
+                   int C, int K, hipStream_t st) {
+  const int tpi = (H + RT - 1) / RT;
+  hipLaunchKernelGGL((conv3x3_kernel<W, RT, KT, XF>), dim3(N * tpi, K / KT), dim3(THREADS), 0, st, x, w, y, stats, xf,
+                     H, C, K, tpi);
+}
+
+template <int W, int RT, int KT>
+static void launch_x(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const float* xf, int N, int H,
+                     int C, int K, hipStream_t st) {
+  if (xf) launch<W, RT, KT, true>(x, w, y, stats, xf, N, H, C, K, st);
+  else launch<W, RT, KT, false>(x, w, y, stats, xf, N, H, C, K, st);
+}
+}  // namespace c3
+
+// Shapes the staged-window kernel takes: 3 x 3, stride 1, pad 1, dilation 1, square 56 / 28 / 14 images (the
+// stride-1 ResNet-50 3 x 3 layers and their data gradients), C and K multiples of 64 (K = 64 at 56 x 56, else a
+// multiple of 128), bf16 output without bias / activation. $K8S_AMD_CONV3X3=0 keeps them on the implicit GEMM (A/B;
+// read per call, both sides tested).
+bool conv3x3_eligible(int H, int W, int C, int K, int R, int S, int stride, int pad, int dil) {
+  const char* e = getenv("K8S_AMD_CONV3X3");
+  if (e && e[0] == '0') return false;
+  if (R != 3 || S != 3 || stride != 1 || pad != 1 || dil != 1 || H != W || C % 64 != 0) return false;
+  if (W == 56) return K == 64;
+  return (W == 28 || W == 14) && K % 128 == 0;
+}
+
+void launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const float* xform, int N,
+                    int H, int W, int C, int K, hipStream_t st) {
+  if (W == 56 && K == 64) c3::launch_x<56, 4, 64>(x, w, y, stats, xform, N, H, C, K, st);
+  else if (W == 28 && K % 128 == 0) c3::launch_x<28, 8, 128>(x, w, y, stats, xform, N, H, C, K, st);
+  else if (W == 14 && K % 128 == 0) c3::launch_x<14, 14, 128>(x, w, y, stats, xform, N, H, C, K, st);
+  else throw std::runtime_error("conv3x3: shape outside the staged-window kernel's contract");
+}
+
+}  // namespace k8s_amd

@@ -1141,6 +1141,10 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, 
                      int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
                      int mode, float* stats, hipStream_t st, const SubGrid* sg,
                      const float* xform) {
+  if (!sg && !y_f32 && !bias && act == 0 && mode == 0 && conv3x3_eligible(H, W, C, K, R, S, stride, pad, dil)) {
+    launch_conv3x3(x, w, reinterpret_cast<uint16_t*>(y), stats, xform, N, H, W, C, K, st);  // staged window
+    return;
+  }
   const int M = N * Ho * Wo, RSC = R * S * C;
   KMajor b{w, (long)RSC, K, RSC};
   Epi e = make_epi(y, K, y_f32, bias, act, nullptr, mode, 1.f);

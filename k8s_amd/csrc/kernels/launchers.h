@@ -82,6 +82,11 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
 // out = bit ? src : 0 per element (bf16, n % 8 == 0; mask packed as above)
 void launch_mask_apply(const uint16_t* src, const uint8_t* mask, uint16_t* out, long n, hipStream_t st);
 long gemm_splitk_workspace(int M, int N, int splits);  // fp32 elements of the split-K slab workspace
+// conv3x3.hip: staged-window 3 x 3 / stride-1 / pad-1 NHWC convolution (optional BN + ReLU on load: xform =
+// fp32 [2][C] scale | shift), bf16 output, optional BN statistics [kConvStatReplicas][2][K]
+bool conv3x3_eligible(int H, int W, int C, int K, int R, int S, int stride, int pad, int dil);
+void launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const float* xform, int N,
+                    int H, int W, int C, int K, hipStream_t st);
 // gemm256.hip: 256 x 256-tile, 8-wave phased MFMA GEMM for the large (transformer) products
 bool gemm256_eligible(int M, int N, int K, bool a_kmajor, bool b_kmajor);
 // split count for the tall-K fp32 products on the 256 x 256 kernel (1 = none)

@@ -444,12 +444,6 @@ static bool use_gemm256(long M, long N, long K, bool a_kmajor, bool b_kmajor) {
   return m != 0 && k8s_amd::gemm256_eligible((int)M, (int)N, (int)K, a_kmajor, b_kmajor);
 }
 
-// $K8S_AMD_GEMM256_SK=0 turns the stream-K tail off (A/B knob, read per call; tests run both sides)
-static bool sk_enabled() {
-  const char* e = std::getenv("K8S_AMD_GEMM256_SK");
-  return !(e && e[0] == '0');
-}
-
 // Zero-initialised int words for the stream-K tickets / flags, one buffer per device, grown on demand. The kernel
 // leaves every word it used at zero again, so no per-call clear is needed. GEMMs run on one compute stream, so one
 // buffer per device is never used by two launches at once.
@@ -521,7 +515,7 @@ Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tens
     const k8s_amd::Gemm256Plan plan = k8s_amd::gemm256_plan((int)M, (int)N, (int)K);
     Tensor slabs;
     int* sync = nullptr;
-    if (plan.sk > 1 && sk_enabled()) {
+    if (plan.sk > 1) {
       slabs = torch::empty({k8s_amd::gemm256_sk_slab_floats(plan)}, a.options().dtype(at::kFloat));
       sync = sk_sync_words(k8s_amd::gemm256_sk_sync_ints(plan), a.device());
     }
