@@ -159,7 +159,32 @@ def cmd_describe(c: ApiClient, a, out) -> int:
     out.write("Pods:\n")
     for p in _pods(c, a.namespace, a.name):
         out.write("  %s  %s\n" % (p["metadata"]["name"], (p.get("status") or {}).get("phase", "")))
+    out.write("Events:\n")
+    evs = job_events(c, a.namespace, a.name, md.get("uid"))
+    if not evs:
+        out.write("  <none>\n")
+    else:
+        out.write("  %-8s %-10s %-6s %-24s %s\n" % ("Type", "Reason", "Count", "Last seen", "Message"))
+        for e in evs:
+            out.write("  %-8s %-10s %-6s %-24s %s\n" % (e.get("type", ""), e.get("reason", ""), e.get("count", 1),
+                                                        e.get("lastTimestamp", ""), e.get("message", "")))
     return 0
+
+
+def job_events(c: ApiClient, namespace: str, name: str, uid=None):
+    """core/v1 Events whose involvedObject is this TfJob (the operator's Created / Running / Succeeded / Failed),
+    oldest first; with ``uid`` only those of that incarnation of the name."""
+    try:
+        items = c.get("/api/v1/namespaces/%s/events" % namespace).get("items") or []
+    except ApiError:
+        return []
+    out = []
+    for e in items:
+        io = e.get("involvedObject") or {}
+        if io.get("kind") == "TfJob" and io.get("name") == name and (not uid or io.get("uid") in (None, uid)):
+            out.append(e)
+    out.sort(key=lambda e: (e.get("firstTimestamp") or "", int((e.get("metadata") or {}).get("resourceVersion") or 0)))
+    return out
 
 
 def cmd_wait(c: ApiClient, a, out) -> int:

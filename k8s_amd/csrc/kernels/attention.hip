@@ -769,13 +769,7 @@ static bool big_tile(int D, int S) { return D == 64 && S >= 1024; }
 // dK/dV chunks per key block: causal key blocks carry from 1 to Sq / 64 query tiles of work, so with one block per
 // key block the first ones ran long after the rest of the chip had drained. Split each key block's (head, query tile)
 // walk into chunks (fp32 partials + a reduce pass) while the grid stays small enough for the partials to be cheap.
-// $K8S_AMD_FA_DKV_SPLIT overrides (1 = unsplit).
 int flash_dkv_splits(int B, int Sq, int Sk, int Hkv, int causal) {
-  static const int env = [] {
-    const char* e = getenv("K8S_AMD_FA_DKV_SPLIT");
-    return e ? atoi(e) : 0;
-  }();
-  if (env > 0) return std::min(env, 8);
   if (!causal) return 1;
   const long nblk = (long)((Sk + FB_BN - 1) / FB_BN) * Hkv * B;
   const int per_block = (Sq + 63) / 64;  // query tiles of the heaviest key block (per query head)
@@ -806,23 +800,17 @@ void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, 
   // dK/dV blocks own 64 keys at any D, split into a.dkv_split chunks (flash_dkv_splits)
   const dim3 gkv(((a.Sk + FB_BN - 1) / FB_BN) * a.Hkv * a.B * a.dkv_split);
   // dQ: QS = 2 (32 queries per wave, 128 per block) when the grid still fills the chip. With D x TILE = 8192
-  // (D = 128, or D = 64 on 128-key tiles) that form needs ~320 VGPRs (one wave per SIMD); $K8S_AMD_FA_DQ_QS2=1
-  // selects it there too (A/B).
-  static const bool qs2_big = [] {
-    const char* e = getenv("K8S_AMD_FA_DQ_QS2");
-    return e && e[0] == '1';
-  }();
+  // (D = 128, or D = 64 on 128-key tiles) that form needs ~320 VGPRs (one wave per SIMD) and measured slower there
+  // (round 3), so those keep QS = 1.
   const bool small = D == 64 && !big_tile(D, a.Sq);
-  const bool qs2 = (small || qs2_big) && (long)((a.Sq + 127) / 128) * a.Hq * a.B >= 512;
+  const bool qs2 = small && (long)((a.Sq + 127) / 128) * a.Hq * a.B >= 512;
   const dim3 gq(((a.Sq + (qs2 ? 127 : 63)) / (qs2 ? 128 : 64)) * a.Hq * a.B), blk(FA_THREADS);
   if (D == 128) {
     hipLaunchKernelGGL((flash_bwd_dkv_kernel<128, 64>), gkv, blk, 0, st, a);
-    if (qs2) hipLaunchKernelGGL((flash_bwd_dq_kernel<128, 64, 2>), gq, blk, 0, st, a);
-    else hipLaunchKernelGGL((flash_bwd_dq_kernel<128, 64, 1>), gq, blk, 0, st, a);
+    hipLaunchKernelGGL((flash_bwd_dq_kernel<128, 64, 1>), gq, blk, 0, st, a);
   } else if (big_tile(D, a.Sq)) {
     hipLaunchKernelGGL((flash_bwd_dkv_kernel<64, 128>), gkv, blk, 0, st, a);
-    if (qs2) hipLaunchKernelGGL((flash_bwd_dq_kernel<64, 128, 2>), gq, blk, 0, st, a);
-    else hipLaunchKernelGGL((flash_bwd_dq_kernel<64, 128, 1>), gq, blk, 0, st, a);
+    hipLaunchKernelGGL((flash_bwd_dq_kernel<64, 128, 1>), gq, blk, 0, st, a);
   } else {
     hipLaunchKernelGGL((flash_bwd_dkv_kernel<64, 64>), gkv, blk, 0, st, a);
     if (qs2) hipLaunchKernelGGL((flash_bwd_dq_kernel<64, 64, 2>), gq, blk, 0, st, a);

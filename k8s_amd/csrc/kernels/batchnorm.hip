@@ -797,28 +797,12 @@ __global__ void __launch_bounds__(BN_THREADS) pool_bn_bwd_apply_kernel(
 // byte streamed since its last use fits, MI355X_MICROARCH.md "Infinity Cache"). The XCD-remapped GEMMs write their
 // outputs as 8 row bands in parallel, each ascending; so the passes sweep 8 bands concurrently too
 // (bn_block_order), in the direction opposite to their producer's.
-// $K8S_AMD_STREAM_ORDER: 0 = plain address order everywhere; 1 (default) = fixed BatchNorm directions (forward
-// apply descending behind its ascending conv, backward reduce descending behind its dgrad, backward apply
-// ascending behind the reduce); 2 = every streaming launch (BN passes, bf16-output GEMMs / convolutions)
-// alternates direction with the previous one (stream_dir). Measured (ResNet-50 b1024, scripts/gpurun/env_ab.sh):
-// 12.36-12.38k img/s plain, 12.61-12.64k with the fixed BatchNorm directions, 12.51-12.53k alternating everything
-// (the GEMMs' reversed tile order costs more than the producer-consumer reuse it buys).
-int stream_order_mode() {
-  static const int v = [] {
-    const char* e = getenv("K8S_AMD_STREAM_ORDER");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-static int g_stream_dir = 0;
-int stream_dir(int fixed) {
-  const int mode = stream_order_mode();
-  if (mode == 0) return 0;
-  if (mode == 1) return fixed;
-  g_stream_dir ^= 1;
-  return g_stream_dir;
-}
-int stream_dir_gemm() { return stream_order_mode() == 2 ? stream_dir(0) : 0; }
+// Measured (ResNet-50 b1024, scripts/gpurun/env_ab.sh, round 3): 12.36-12.38k img/s in plain address order,
+// 12.61-12.64k with these fixed BatchNorm directions (forward apply descending behind its ascending conv, backward
+// reduce descending behind its dgrad, backward apply ascending behind the reduce), 12.51-12.53k when every streaming
+// launch, the GEMMs included, alternated direction (the GEMMs' reversed tile order costs more than the reuse buys).
+int stream_order_mode() { return 1; }
+int stream_dir(int fixed) { return fixed; }
 
 static long bn_rows_per_block(long M, const BnGeom& g) {
   // ~1024 blocks in total (4 per CU: enough loads in flight to cover HBM latency), at most M / 64 row-blocks,

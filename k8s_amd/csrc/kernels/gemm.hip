@@ -329,14 +329,12 @@ struct Epi {
   // Sub-grid output (stride-s data gradient by output parity): GEMM row m = (n, i, j) over an rHo x rWo grid
   // is stored at output row (n, i*rst + ra, j*rst + rb) of an rH x rW image. rst == 0: identity.
   int rst, rHo, rWo, rH, rW, ra, rb;
-  int late_nt;  // K steps from which the next step's loads are issued behind the first MFMA half
   // accumulate (mode 1, lean epilogue) onto addsrc instead of C's old value, with the elements whose packed bit in
   // addmask is clear taken as zero: C = acc + (bit ? addsrc : 0). A ResNet identity block's input gradient is
   // conv1's dgrad plus the block output's gradient masked by its ReLU -- read here from dy and the forward's
   // 1-bit mask instead of from a materialised residual gradient.
   const uint16_t* addsrc;
   const uint8_t* addmask;
-  int rev;  // tiles of each XCD's band in descending order (stream_order_mode 2: start where the producer stopped)
 };
 constexpr int STAT_REPL = 32;
 
@@ -391,8 +389,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
   int wg;
   {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    const int local = E.rev ? q + (xcd < r ? 1 : 0) - 1 - (bid >> 3) : (bid >> 3);
-    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
   const int group = 8 * tiles_n;
   const int first_m = (wg / group) * 8;
@@ -517,7 +514,6 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
   };
 
   constexpr int CPR = BN / 8;  // 16-B chunks per output-tile row
-  const bool late = XF == 0 && nt >= E.late_nt;
   if (nt > 0) {
     stage(0, kbeg);
     xload(kbeg);
@@ -535,7 +531,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
         xstore(0);
         __syncthreads();
       }
-    } else if (!late && t + 1 < nt) {
+    } else if (t + 1 < nt) {
       stage(cur ^ 1, kbeg + (t + 1) * BK);
       xload(kbeg + (t + 1) * BK);
     }
@@ -554,12 +550,6 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfv[j], af[i], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
-      if (NBUF == 2 && kk == 0) {
-        // long K loops: the next K step's loads are issued behind the first half's MFMAs (their address
-        // arithmetic then runs while the matrix pipe is busy instead of delaying the MFMAs); short ones keep them
-        // ahead of the MFMAs (more time in flight). The buffer they fill was released by the previous barrier.
-        if (late && t + 1 < nt) stage(cur ^ 1, kbeg + (t + 1) * BK);
-      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (NBUF == 2 && t + 1 < nt) xstore(cur ^ 1);  // the idle buffer: its last reader finished before the last barrier
@@ -913,17 +903,12 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
 }
 
 // ----------------------------------------------------------------------------- host side
-// Single-buffered (3 blocks / CU) kernel up to this K range per block, double-buffered (2 blocks / CU) above:
-// $K8S_AMD_GEMM_SINGLEBUF_MAXK (A/B knob). Measured on the ResNet-50 b1024 step (scripts/gpurun/env_ab.sh, one box,
-// 2 rounds): 128 -> 12.20k img/s, 256 -> 12.46k, 512 -> 12.57k, 1024 -> 12.57k, 2304 -> 12.54k, all -> 12.44k: a
-// third block per CU hides more load latency than a second LDS buffer does on these short / memory-bound K loops.
-static int single_buf_maxk() {
-  static const int v = [] {
-    const char* e = getenv("K8S_AMD_GEMM_SINGLEBUF_MAXK");
-    return e ? atoi(e) : 8 * BK;
-  }();
-  return v;
-}
+// Single-buffered (3 blocks / CU) kernel up to this K range per block, double-buffered (2 blocks / CU) above.
+// Measured on the ResNet-50 b1024 step (round 1, one box, 2 rounds): 128 -> 12.20k img/s, 256 -> 12.46k,
+// 512 -> 12.57k, 1024 -> 12.57k, 2304 -> 12.54k, all -> 12.44k: a third block per CU hides more load latency than a
+// second LDS buffer does on these short / memory-bound K loops.
+constexpr int kSingleBufMaxK = 8 * BK;
+static int single_buf_maxk() { return kSingleBufMaxK; }
 
 // splits actually launched for a requested count (each split a whole number of BK tiles)
 static int effective_splits(int K, int splits) {
@@ -947,11 +932,6 @@ static void launch_tiles2(const ASrc& a, const BSrc& b, const Epi& e, int M, int
 // the lean epilogue applies: bf16 C (16-B aligned rows), store or accumulate, no atomics; bias / ReLU / GELU /
 // pre-activation copy in store mode on identity rows without statistics (the transformer linears: measured on
 // BERT-base's QKV / FFN1 forward 81 / 105 us per call through the general per-lane epilogue)
-// K8S_AMD_F32S=0 keeps the weight gradients on the per-lane fp32 epilogue (A/B switch; read per call)
-static bool f32s_on() {
-  const char* v = getenv("K8S_AMD_F32S");
-  return !(v && v[0] == '0');
-}
 static bool epi_extra(const Epi& e) { return e.bias || e.pre || e.act != 0; }
 static bool lean_epi(const Epi& e, int N, bool allow_extra) {
   if (epi_extra(e) && (!allow_extra || e.mode != 0 || e.rst || e.stats || e.addsrc ||
@@ -1001,7 +981,7 @@ static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int 
   constexpr bool kWgrad = std::is_same_v<ASrc, MNMajorK> &&
                           (std::is_same_v<BSrc, MNMajorK> || std::is_same_v<BSrc, ConvWgB>);
   if constexpr (kWgrad && WM == 2 && WN == 2) {
-    if (e.out_f32 && e.mode != 2 && !epi_extra(e) && !e.stats && !e.rst && f32s_on()) {
+    if (e.out_f32 && e.mode != 2 && !epi_extra(e) && !e.stats && !e.rst) {
       launch_tiles2<ASrc, BSrc, WM, WN, false, false, true>(a, b, e, M, N, K, kps, splits, st);
       return;
     }
@@ -1039,15 +1019,8 @@ static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act,
   e.rst = e.rHo = e.rWo = e.rH = e.rW = e.ra = e.rb = 0;
   e.addsrc = nullptr;
   e.addmask = nullptr;
-  e.rev = 0;
-  // $K8S_AMD_GEMM_LATE_NT (A/B knob), default off: issuing the next step's loads behind the first MFMA half sped
-  // up the isolated 56x56 / 28x28 3x3 convolutions 7-12 % but the ResNet-50 step lost 1.5 % at any threshold
-  // (b1024: 11.00k img/s never late, 10.84k from 8 K steps, 10.80k always; scripts/gpurun/bench_ab.sh)
-  static const int late_nt = [] {
-    const char* v = getenv("K8S_AMD_GEMM_LATE_NT");
-    return v ? atoi(v) : (1 << 30);
-  }();
-  e.late_nt = late_nt;
+  // (Issuing the next K step's loads behind the first MFMA half sped up the isolated 56x56 / 28x28 3x3 convolutions
+  // 7-12 % but cost the ResNet-50 step 1.5 % at any K threshold -- round 2, scripts/gpurun/bench_ab.sh; removed.)
   return e;
 }
 
@@ -1068,8 +1041,7 @@ int gemm_choose_splits(int M, int N, int K) {
   for (int s = 1; s <= 256 && s <= ktiles; ++s) {
     const int kpt = (ktiles + s - 1) / s;       // K tiles per split
     if ((ktiles + kpt - 1) / kpt != s) continue;  // same kps as a smaller s
-    static const bool old_model = getenv("K8S_AMD_SPLITK_OLD") && getenv("K8S_AMD_SPLITK_OLD")[0] == '1';  // A/B
-    const long slots = kpt * BK <= (old_model ? 2 * BK : single_buf_maxk()) ? 3 * 256 : 2 * 256;
+    const long slots = kpt * BK <= single_buf_maxk() ? 3 * 256 : 2 * 256;
     const long rounds = (tiles * s + slots - 1) / slots;
     const double t = (double)rounds * kpt + (s > 1 ? s * slab_cost : 0.0);
     if (t < best * 0.999) {
@@ -1114,7 +1086,6 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
   const bool slab = splits > 1;
   Epi e = make_epi(slab ? (void*)ws : C, slab ? (long)N : ldc, c_f32, bias, act, pre, slab ? 3 : mode, alpha);
   e.slab = (long)M * N;
-  if (!c_f32) e.rev = stream_dir_gemm();  // activation-streaming products (not the fp32 weight gradients)
   if (add) {
     if (slab || mode != 1) throw std::runtime_error("a separate addend needs accumulate mode and no split-K");
     e.addsrc = add->src;
@@ -1149,7 +1120,6 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, 
   KMajor b{w, (long)RSC, K, RSC};
   Epi e = make_epi(y, K, y_f32, bias, act, nullptr, mode, 1.f);
   e.stats = stats;
-  if (!sg && !y_f32) e.rev = stream_dir_gemm();
   if (sg) {
     if (stats) throw std::runtime_error("sub-grid output takes no statistics epilogue");
     e.rst = sg->stride;

@@ -402,7 +402,7 @@ __device__ __forceinline__ bool sk_fixup(f32x4_t (&acc)[8][NJ], const SkArgs& SK
   return true;
 }
 
-template <class AS, class BS, int DIAG = 0>
+template <class AS, class BS>
 __global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, g256::Epi E, int M, int N, int K,
                                                                    int kps, SkArgs SK) {
   using namespace g256;
@@ -475,15 +475,13 @@ __global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, 
     for (int j = 0; j < 4; ++j) BS::load(br[j], st + STAGE_A, wc * 64 + j * 16, lane);
 #pragma unroll
     for (int i = 0; i < 8; ++i) AS::load(ar[i], st, wr * 128 + i * 16, lane);
-    if constexpr (DIAG == 0) {
-      if (h + 3 < nk) {
-        issue(islot);
-        vmwait<8>();
-      } else if (h + 2 < nk) {
-        vmwait<4>();
-      } else {
-        vmwait<0>();
-      }
+    if (h + 3 < nk) {
+      issue(islot);
+      vmwait<8>();
+    } else if (h + 2 < nk) {
+      vmwait<4>();
+    } else {
+      vmwait<0>();
     }
     barrier();
     tie<BS>(br);
@@ -524,11 +522,7 @@ static void launch_ring(const AS& a, const BS& b, const Epi& e, int M, int N, in
     blocks = plan.full + (tiles - plan.full) * plan.sk;
   }
   const dim3 grid(blocks, splits);
-  const char* dg = getenv("K8S_AMD_GEMM256_DIAG");
-  if (dg && atoi(dg) == 1)
-    hipLaunchKernelGGL((g256r::gemm256r_kernel<AS, BS, 1>), grid, dim3(THREADS), 0, st, a, b, e, M, N, K, kps, sk);
-  else
-    hipLaunchKernelGGL((g256r::gemm256r_kernel<AS, BS>), grid, dim3(THREADS), 0, st, a, b, e, M, N, K, kps, sk);
+  hipLaunchKernelGGL((g256r::gemm256r_kernel<AS, BS>), grid, dim3(THREADS), 0, st, a, b, e, M, N, K, kps, sk);
 }
 
 }  // namespace g256

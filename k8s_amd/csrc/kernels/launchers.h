@@ -187,7 +187,6 @@ void launch_pool_bn_bwd(const uint16_t* dpool, const uint8_t* idx, const uint16_
 // streaming launch; `fixed` is the direction used in the fixed-BatchNorm mode.
 int stream_order_mode();
 int stream_dir(int fixed);
-int stream_dir_gemm();
 
 void launch_flash_fwd(const AttnFwdArgs& a, int D, hipStream_t st);
 void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, long sos, long soh, hipStream_t st);
@@ -220,7 +219,7 @@ bool wgrad3x3_tiled_ok(int C, int K, int R, int S, int stride, int pad, int W);
 int wgrad3x3_tiled_blocks(int N, int H, int W, int C);
 long wgrad3x3_tiled_workspace(int N, int H, int W, int C);
 void launch_wgrad3x3_tiled(const uint16_t* x, const uint16_t* dy, float* ws, float* dw, int N, int H, int W, int C,
-                           bool accumulate, hipStream_t st);
+                           bool accumulate, hipStream_t st, const float* xform = nullptr);
 // the s2d stem weight gradient (LDS-tiled, persistent blocks; ws = stem_wgrad_blocks(N, Hs) x 64 x 256 fp32 partials)
 int stem_wgrad_blocks(int N, int Hs);
 void launch_stem_wgrad(const uint16_t* xs, const uint16_t* dy, float* ws, float* dw4, int N, int Hs, int Ws,

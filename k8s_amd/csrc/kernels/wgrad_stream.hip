@@ -221,20 +221,13 @@ __global__ void __launch_bounds__(WK * WC * 64, WK * WC == 8 ? 1 : 2) wgrad_stre
 
 }  // namespace wgs
 
-// Tile choice: 128 x 64 (64 x 64 for K = 64), or $K8S_AMD_WGS_TILE ("128x64", "128x128", "256x128", "64x64")
-// for A/B runs.
+// Tile choice: 128 x 64 (64 x 64 for K = 64). Measured (scripts/bench_wgrad_tiles.py, b1024): 128 x 128, 256 x 128
+// are not faster on the shapes this kernel keeps (their rings leave one or two workgroups per CU).
 struct WgsTile {
   int KT, CT;
 };
 static WgsTile wgs_tile(int K, int RSC) {
-  if (const char* e = getenv("K8S_AMD_WGS_TILE")) {
-    int kt = 0, ct = 0;
-    if (sscanf(e, "%dx%d", &kt, &ct) == 2 && K % kt == 0 && RSC % ct == 0 &&
-        ((kt == 128 && (ct == 64 || ct == 128)) || (kt == 256 && ct == 128) || (kt == 64 && ct == 64)))
-      return WgsTile{kt, ct};
-  }
-  // measured (scripts/bench_wgrad_tiles.py, b1024): the larger tiles are not faster on the shapes this kernel
-  // keeps (their rings leave one or two workgroups per CU); they stay selectable for A/B runs
+  (void)RSC;
   if (K % 128 == 0) return WgsTile{128, 64};
   return WgsTile{64, 64};
 }
@@ -242,14 +235,13 @@ static WgsTile wgs_tile(int K, int RSC) {
 // Shapes this kernel takes: C % 64 == 0 (a tile's columns inside one tap), K % 64 == 0, and a 64-wide side of
 // dW (K == 64 or R*S*C == 64: the memory-bound ResNet-50 layers at 56 x 56). Measured at batch 1024
 // (scripts/bench_wgrad_tiles.py, profiles/r02_wgrad_tiles.jsonl) the generic split-K kernel is 5-60 % faster on
-// every other ResNet-50 weight gradient, the 3x3 ones included ($K8S_AMD_WGS_ANY=1 lifts the restriction).
+// every other ResNet-50 weight gradient, the 3x3 ones included.
 bool wgrad_stream_eligible(int N, int Ho, int Wo, int C, int K, int R, int S) {
   if (C % 64 != 0 || K % 64 != 0) return false;
   const WgsTile t = wgs_tile(K, R * S * C);
   const long tiles = (long)(K / t.KT) * ((long)R * S * C / t.CT);
   const long rows = (long)N * Ho * Wo;
-  const char* any = getenv("K8S_AMD_WGS_ANY");
-  const bool narrow = K == 64 || R * S * C == 64 || (any && any[0] == '1');
+  const bool narrow = K == 64 || R * S * C == 64;
   return narrow && tiles <= 96 && rows >= 64L * 64;
 }
 
@@ -271,20 +263,16 @@ void launch_wgrad_stream(const uint16_t* x, const uint16_t* dy, float* dw, int N
   a.tiles_c = RSC / t.CT;
   const int T = a.tiles_k * a.tiles_c;
   const int steps = (M + KS - 1) / KS;
-  // ~4 (256-thread) or ~2 (512-thread) workgroups per CU in total, at least 8 k-steps each (prologue amortised),
-  // chunks a multiple of 8 so the tiles of one chunk share an XCD
-  const int per_cu = t.KT == 256 ? 2 : 4;
+  // ~4 workgroups per CU in total, at least 8 k-steps each (prologue amortised), chunks a multiple of 8 so the
+  // tiles of one chunk share an XCD
+  const int per_cu = 4;
   int chunks = (per_cu * 256 + T - 1) / T;
   chunks = (chunks + 7) / 8 * 8;
   chunks = std::max(8, std::min(chunks, (steps + 7) / 8));
   a.chunk_steps = (steps + chunks - 1) / chunks;
   a.chunks = (steps + a.chunk_steps - 1) / a.chunk_steps;
   const int grid = ((a.chunks + 7) / 8) * 8 * T;
-  if (t.KT == 256)
-    hipLaunchKernelGGL((wgrad_stream_kernel<256, 128, 4, 2, 3>), dim3(grid), dim3(512), 0, st, a);
-  else if (t.KT == 128 && t.CT == 128)
-    hipLaunchKernelGGL((wgrad_stream_kernel<128, 128, 2, 2, 2>), dim3(grid), dim3(256), 0, st, a);
-  else if (t.KT == 128)
+  if (t.KT == 128)
     hipLaunchKernelGGL((wgrad_stream_kernel<128, 64, 2, 2, 3>), dim3(grid), dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL((wgrad_stream_kernel<64, 64, 2, 2, 4>), dim3(grid), dim3(256), 0, st, a);

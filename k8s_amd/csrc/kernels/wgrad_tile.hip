@@ -28,10 +28,14 @@ __device__ __attribute__((aligned(64))) uint16_t g_wg3_zero[64];  // source of t
 
 __device__ __forceinline__ int off(int p, int ch16) { return p * 128 + ((ch16 ^ (p & 7)) << 4); }
 
-template <int W, int RT>
+// XF: the activation operand is relu(x * scale + shift) (BatchNorm normalised on load, xf = fp32 [2][C] scale |
+// shift): each thread rewrites its staged window chunks in place once per tile, the zero padding left zero (the
+// forward's conv3x3.hip does the same, so the bn1 apply pass is gone from both directions).
+template <int W, int RT, bool XF = false>
 __global__ void __launch_bounds__(256, 2) wgrad3x3_kernel(const uint16_t* __restrict__ x,
                                                          const uint16_t* __restrict__ dy, float* __restrict__ ws,
-                                                         int H, int C, int K, int tiles_per_img, int ntiles) {
+                                                         int H, int C, int K, int tiles_per_img, int ntiles,
+                                                         const float* __restrict__ xf) {
   constexpr int WP = W + 2, WIN = (RT + 2) * WP, PX = RT * W, NKS = PX / 32;
   static_assert(PX % 32 == 0, "whole 32-pixel k steps");
   __shared__ __attribute__((aligned(1024))) char smem[(WIN + PX) * 128];
@@ -81,6 +85,33 @@ __global__ void __launch_bounds__(256, 2) wgrad3x3_kernel(const uint16_t* __rest
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
+    if constexpr (XF) {
+      // a thread's window chunks c = i * 256 + tid all hold logical channels 8 * ((tid & 7) ^ ((tid >> 3) & 7)) + 0..7
+      // (scale / shift re-read per tile from L1: kept live across the K loop they spill the 255-VGPR kernel)
+      float xsc[8], xsh[8];
+      const int ch = c0 + 8 * ((tid & 7) ^ ((tid >> 3) & 7));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xsc[j] = xf[ch + j];
+        xsh[j] = xf[C + ch + j];
+      }
+#pragma unroll 1
+      for (int i = 0; i < (WIN * 8 + 255) / 256; ++i) {
+        const int c = i * 256 + tid;
+        if (c < WIN * 8) {
+          const int p = c >> 3, wr = p / WP, wc = p - wr * WP, h = h0 - 1 + wr, w = wc - 1;
+          if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
+            bf16x8_t* q = reinterpret_cast<bf16x8_t*>(xw + c * 16);
+            const bf16x8_t v = *q;
+            float o[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = fmaxf(__builtin_fmaf(bf2f((uint16_t)v[j]), xsc[j], xsh[j]), 0.f);
+            *q = pack_bf16x8(o);
+          }
+        }
+      }
+      __syncthreads();
+    }
 #pragma unroll 1
     for (int ks = 0; ks < NKS; ++ks) {
       const int pb = 32 * ks + 8 * G;  // this lane group's 8 pixels of the k step
@@ -185,24 +216,28 @@ long wgrad3x3_tiled_workspace(int N, int H, int W, int C) {
   return pieces * (nb + wg3_groups(nb)) * wg3::CS * wg3::NQ;  // block partials + slab-group partials
 }
 
+template <int W, int RT>
+static void wg3_launch(dim3 grid, hipStream_t st, const uint16_t* x, const uint16_t* dy, float* ws, int H, int C,
+                       int tpi, int ntiles, const float* xf) {
+  if (xf)
+    hipLaunchKernelGGL((wg3::wgrad3x3_kernel<W, RT, true>), grid, dim3(256), 0, st, x, dy, ws, H, C, C, tpi, ntiles, xf);
+  else
+    hipLaunchKernelGGL((wg3::wgrad3x3_kernel<W, RT>), grid, dim3(256), 0, st, x, dy, ws, H, C, C, tpi, ntiles, xf);
+}
+
 void launch_wgrad3x3_tiled(const uint16_t* x, const uint16_t* dy, float* ws, float* dw, int N, int H, int W, int C,
-                           bool accumulate, hipStream_t st) {
+                           bool accumulate, hipStream_t st, const float* xform) {
   const int rt = wg3_rt(W), tpi = (H + rt - 1) / rt;
   const long ntiles = (long)N * tpi;
   if (ntiles >= (1L << 31)) throw std::runtime_error("wgrad3x3_tiled: too many tiles");
   const int pieces = (C / wg3::CS) * (C / wg3::CS);
   const int nb = wgrad3x3_tiled_blocks(N, H, W, C);
-  const dim3 grid(nb, pieces), blk(256);
-  if (W == 56)
-    hipLaunchKernelGGL((wg3::wgrad3x3_kernel<56, 4>), grid, blk, 0, st, x, dy, ws, H, C, C, tpi, (int)ntiles);
-  else if (W == 28)
-    hipLaunchKernelGGL((wg3::wgrad3x3_kernel<28, 8>), grid, blk, 0, st, x, dy, ws, H, C, C, tpi, (int)ntiles);
-  else if (W == 16)
-    hipLaunchKernelGGL((wg3::wgrad3x3_kernel<16, 2>), grid, blk, 0, st, x, dy, ws, H, C, C, tpi, (int)ntiles);
-  else if (W == 14)
-    hipLaunchKernelGGL((wg3::wgrad3x3_kernel<14, 16>), grid, blk, 0, st, x, dy, ws, H, C, C, tpi, (int)ntiles);
-  else
-    throw std::runtime_error("wgrad3x3_tiled: unsupported width");
+  const dim3 grid(nb, pieces);
+  if (W == 56) wg3_launch<56, 4>(grid, st, x, dy, ws, H, C, tpi, (int)ntiles, xform);
+  else if (W == 28) wg3_launch<28, 8>(grid, st, x, dy, ws, H, C, tpi, (int)ntiles, xform);
+  else if (W == 16) wg3_launch<16, 2>(grid, st, x, dy, ws, H, C, tpi, (int)ntiles, xform);
+  else if (W == 14) wg3_launch<14, 16>(grid, st, x, dy, ws, H, C, tpi, (int)ntiles, xform);
+  else throw std::runtime_error("wgrad3x3_tiled: unsupported width");
   const long n4 = (long)pieces * wg3::CS * wg3::NQ / 4;
   const int SG = wg3_groups(nb);
   float* part = ws + (long)pieces * nb * wg3::CS * wg3::NQ;

@@ -2,6 +2,7 @@
 
 #include <random>
 
+#include "election.h"
 #include "log.h"
 
 namespace tfop {
@@ -71,11 +72,14 @@ void TrainingJob::setup() {
       status_.phase = "Failed";
       status_.state = "Failed";
       setup_ok_ = false;
+      record_event("Warning", "Failed", "TfJob " + job_.name() + " cannot run: " + err);
     } else {
       status_.phase = "Creating";
       status_.state = "Running";
       status_.append_condition("Creating", "replica resources are being created");
       setup_ok_ = true;
+      record_event("Normal", "Created", "Creating the replica resources of TfJob " + job_.name() + " (RuntimeId " +
+                                            job_.spec.runtime_id + ")");
     }
     return;
   }
@@ -132,6 +136,7 @@ void TrainingJob::create_resources() {
   if (all && status_.phase == "Creating") {
     status_.phase = "Running";
     status_.append_condition("Running", "all replica resources created");
+    record_event("Normal", "Running", "All replica resources of TfJob " + job_.name() + " exist");
   }
 }
 
@@ -202,7 +207,55 @@ bool TrainingJob::update_status() {
   return false;
 }
 
-void TrainingJob::reconcile() {
+void TrainingJob::record_event(const std::string& type, const std::string& reason, const std::string& message) {
+  const std::string key = reason + "\n" + message;
+  const std::string now = now_rfc3339();
+  const std::string ns = job_.ns();
+  auto it = events_.find(key);
+  if (it != events_.end()) {  // seen before: count + 1 on the stored object (carries its resourceVersion)
+    Json ev = it->second.clone();
+    ev["count"] = (long long)(ev.find("count") && ev.at("count").is_number() ? ev.at("count").as_int() : 1) + 1;
+    ev["lastTimestamp"] = now;
+    const std::string name = ev.find("metadata") ? get_str(ev.at("metadata"), "name") : "";
+    ApiResult r = call("PUT", core_path(ns, "events", name), &ev);
+    if (r.ok()) it->second = r.body;
+    else log_v(1, "job %s: could not update event %s: HTTP %d", key.c_str(), name.c_str(), r.code);
+    return;
+  }
+  Json ev = Json::object();
+  ev["apiVersion"] = "v1";
+  ev["kind"] = "Event";
+  Json md = Json::object();
+  md["name"] = job_.name() + "." + rand_string(8);  // kubectl-style <object>.<unique suffix>
+  md["namespace"] = ns;
+  ev["metadata"] = md;
+  Json io = Json::object();
+  io["apiVersion"] = "tensorflow.org/v1alpha1";
+  io["kind"] = "TfJob";
+  io["name"] = job_.name();
+  io["namespace"] = ns;
+  if (!job_.uid().empty()) io["uid"] = job_.uid();
+  ev["involvedObject"] = io;
+  ev["type"] = type;
+  ev["reason"] = reason;
+  ev["message"] = message;
+  ev["firstTimestamp"] = now;
+  ev["lastTimestamp"] = now;
+  ev["count"] = 1;
+  Json src = Json::object();
+  src["component"] = "tf-operator";
+  ev["source"] = src;
+  ApiResult r = call("POST", core_path(ns, "events"), &ev);
+  if (r.ok()) events_[key] = r.body.is_object() ? r.body : ev;
+  else log_v(1, "job %s: could not record event %s: HTTP %d", this->key().c_str(), reason.c_str(), r.code);
+}
+
+// Phase / state transitions are recorded as Events where they happen (README.md:466-476 phases and states):
+// Created (setup done, resources being created), Running (every replica resource exists), Succeeded / Failed (the
+// chief's outcome, or a spec that cannot run)
+void TrainingJob::reconcile() { reconcile_once(); }
+
+void TrainingJob::reconcile_once() {
   if (status_.phase.empty() || !setup_ok_) {
     const bool first = status_.phase.empty();
     setup();
@@ -220,11 +273,14 @@ void TrainingJob::reconcile() {
       status_.phase = "Done";
       status_.state = "Failed";
       status_.append_condition("Done", "chief replica failed");
+      record_event("Warning", "Failed", "TfJob " + job_.name() + " failed: the " + chief_type() + " replica failed");
     } else if (state == "Succeeded") {
       log_info("Master succeeded Job: %s.", job_.name().c_str());
       status_.phase = "Done";
       status_.state = "Succeeded";
       status_.append_condition("Done", "chief replica succeeded");
+      record_event("Normal", "Succeeded", "TfJob " + job_.name() + " succeeded: the " + chief_type() +
+                                              " replica exited 0");
     }
   }
   update_status();

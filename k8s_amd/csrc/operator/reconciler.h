@@ -22,6 +22,7 @@
 #include <condition_variable>
 #include <deque>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <set>
@@ -65,9 +66,14 @@ class TrainingJob {
 
  private:
   ApiResult call(const std::string& method, const std::string& path, const Json* body = nullptr);
+  // core/v1 Event on this TfJob (involvedObject = the TfJob): POSTed the first time a (reason, message) pair
+  // occurs, then updated in place with count + 1 and a new lastTimestamp (client-go EventCorrelator's dedup).
+  // Best effort: a failed write never affects reconciliation.
+  void record_event(const std::string& type, const std::string& reason, const std::string& message);
   bool create_if_absent(const std::string& collection, const std::string& name, const Json& obj, bool* created);
   void create_resources();
   void get_status(std::string& state, std::vector<TfReplicaStatus>& out);
+  void reconcile_once();
   bool update_status();
 
   KubeApi& api_;
@@ -79,6 +85,7 @@ class TrainingJob {
   bool tensorboard_ = false;
   bool setup_ok_ = false;
   std::set<std::string> existing_;  // objects known to exist (kind/name)
+  std::map<std::string, Json> events_;  // reason + "\n" + message -> the last stored Event object
   int api_calls_ = 0;
 };
 

@@ -526,12 +526,8 @@ Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tens
     return c;
   }
   // tall-K fp32 products whose output is too small for the 256 x 256 kernel alone (the ResNet 1x1 weight gradients):
-  // split-K on the 256 kernel ($K8S_AMD_G256_SPLITK=0: the 128 x 128 split-K kernel, A/B)
-  static const bool g256_splitk = [] {
-    const char* e = std::getenv("K8S_AMD_G256_SPLITK");
-    return !(e && e[0] == '0');
-  }();
-  if (g256_splitk && !xfb && !add_src && splits != 1 && out_f32 && !bias && act == 0 && !pre && gemm256_mode() != 0 &&
+  // split-K on the 256 kernel
+  if (!xfb && !add_src && splits != 1 && out_f32 && !bias && act == 0 && !pre && gemm256_mode() != 0 &&
       K % 64 == 0 && (a_kmajor || M % 8 == 0) && (b_kmajor || N % 8 == 0) && N % 4 == 0) {
     const int s256 = k8s_amd::gemm256_choose_splits((int)M, (int)N, (int)K);
     const long t256 = ((M + 255) / 256) * ((N + 255) / 256);
@@ -618,15 +614,13 @@ void conv_wgrad(Tensor x, Tensor dy, Tensor dw, int64_t stride, int64_t pad, int
   const int Ho = conv_out(H, R, stride, pad, dil), Wo = conv_out(W, S, stride, pad, dil);
   TORCH_CHECK(dy.size(0) == N && dy.size(1) == Ho && dy.size(2) == Wo && dy.size(3) == K, "dy shape mismatch");
   const float* xf = xform_ptr(xform, C);
-  const char* wt_env = std::getenv("K8S_AMD_WGRAD_TILE");  // =0: these 3x3 shapes on the generic kernels (A/B)
-  if (!xf && !(wt_env && wt_env[0] == '0') && dil == 1 && dy.is_contiguous() && x.is_contiguous() && Ho == H &&
+  if (dil == 1 && dy.is_contiguous() && x.is_contiguous() && Ho == H &&
       Wo == W && H == W && k8s_amd::wgrad3x3_tiled_ok(C, K, R, S, (int)stride, (int)pad, W)) {
     auto wsp = torch::empty({k8s_amd::wgrad3x3_tiled_workspace(N, H, W, C)}, dw.options());
-    k8s_amd::launch_wgrad3x3_tiled(cbf(x), cbf(dy), f32(wsp), f32(dw), N, H, W, C, accumulate, cur_stream());
+    k8s_amd::launch_wgrad3x3_tiled(cbf(x), cbf(dy), f32(wsp), f32(dw), N, H, W, C, accumulate, cur_stream(), xf);
     return;
   }
-  const char* ws_env = std::getenv("K8S_AMD_WGRAD_STREAM");  // =0: generic split-K GEMM (A/B)
-  if (!xf && !(ws_env && ws_env[0] == '0') && dil == 1 && dy.is_contiguous() && x.is_contiguous() &&
+  if (!xf && dil == 1 && dy.is_contiguous() && x.is_contiguous() &&
       k8s_amd::wgrad_stream_eligible(N, Ho, Wo, C, K, R, S)) {
     k8s_amd::launch_wgrad_stream(cbf(x), cbf(dy), f32(dw), N, H, W, C, K, R, S, (int)stride, (int)pad, Ho, Wo,
                                  accumulate, cur_stream());
@@ -1068,6 +1062,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
         py::arg("out_f32"), py::arg("bias"), py::arg("act"), py::arg("stats"),
         py::arg("xform") = py::none());
+  m.def("conv3x3_staged_ok", [](int H, int W, int C, int K, int R, int S, int stride, int pad) {
+    // the staged-window forward / data gradient (conv3x3.hip) and the tiled weight gradient (wgrad_tile.hip) both
+    // take this layer: BatchNorm + ReLU can be normalised on load in all three products
+    return k8s_amd::conv3x3_eligible(H, W, C, K, R, S, stride, pad, 1) &&
+           k8s_amd::conv3x3_eligible(H, W, K, C, R, S, stride, pad, 1) &&
+           k8s_amd::wgrad3x3_tiled_ok(C, K, R, S, stride, pad, W);
+  });
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
         py::arg("dil"), py::arg("splits"), py::arg("accumulate"), py::arg("xform") = py::none());
   m.def("conv_fwd_subgrid", &conv_fwd_subgrid, py::arg("x"), py::arg("w"), py::arg("pad"), py::arg("Hs"),

@@ -89,16 +89,10 @@ class Bottleneck(nn.Module):
             if not fuse:
                 idn = self.down_bn(dn, relu=False, dy_link=mlink)
         t = self.conv1(x, grad_link=link or dlink)
-        # bn1 / bn2 + ReLU: normalised on load by the consuming convolution (ops.nn.bn_relu_conv, no apply pass)
-        # or applied by the BN kernel; ops.nn.BN_ONLOAD picks which
-        if K.BN_ONLOAD == "all":
-            t = K.bn_relu_conv(t, self.bn1, self.conv2)
-        else:
-            t = self.conv2(self.bn1(t))
-        if K.BN_ONLOAD in ("all", "1x1"):
-            t = K.bn_relu_conv(t, self.bn2, self.conv3)
-        else:
-            t = self.conv3(self.bn2(t))
+        # bn1 / bn2 + ReLU: normalised on load by the consuming convolution where its kernels take it
+        # (ops.nn.bn_relu_conv: no apply pass, no z tensor), else applied by the BN kernel
+        t = K.bn_relu_conv(t, self.bn1, self.conv2)
+        t = K.bn_relu_conv(t, self.bn2, self.conv3)
         if dn is not None and fuse:
             y = K.bn_act_dual(t, self.bn3, dn, self.down_bn)
             if y is not None:
@@ -159,7 +153,7 @@ class ResNet(nn.Module):
         else:
             t = self.conv1(x)
         # bn1 + ReLU + 3x3/s2 max pool: one fused pass each way on the GPU (the 112x112 BN output is never stored)
-        y = K.bn_relu_maxpool(t, self.bn1) if K.STEM_POOL_FUSED else K.max_pool_nhwc(self.bn1(t), 3, 2, 1)
+        y = K.bn_relu_maxpool(t, self.bn1)
         for b in self.blocks:
             y = b(y)
         y = K.global_avg_pool_nhwc(y)

@@ -13,8 +13,8 @@ it WITHOUT materialising any transpose:
 Every product runs on our kernels: the 256 x 256 LDS-ring kernel (csrc/kernels/gemm256.hip) when the output
 fills the chip, else the 128 x 128 kernel (gemm.hip); the choice is a wave-quantisation cost model in C++
 (``gemm256_eligible``), not a timing race against a vendor library. CPU tensors use plain PyTorch; GPU shapes
-the kernels do not take (K not a multiple of 64 on a K-major operand, odd M/N) go through PyTorch too and are
-counted in ``FALLBACKS`` (reported by the trainer), never silently.
+the kernels do not take (K not a multiple of 8, N not a multiple of 4) go through PyTorch too and are counted in
+``FALLBACKS`` (reported by the trainer), never silently; M and the K tail are masked in-kernel.
 """
 from __future__ import annotations
 
@@ -46,7 +46,11 @@ def mm(a, b, a_kmajor=True, b_kmajor=True, out=None, out_f32=False, bias=None, a
 
 
 def _shape_ok(M, N, K) -> bool:
-    return K % 64 == 0 and N % 8 == 0 and M % 8 == 0
+    """The kernels' contract for a Linear layer's products: any M (the row tails are masked in-kernel); the K-major
+    reduction dims (K forward, N in the data gradient) and the MN-major extents (N and K in the weight gradient)
+    in whole 16-B units -- K % 8 and N % 8 -- and N % 4 for the forward epilogue. A backward with N % 8 != 0 runs on
+    zero-padded copies (``linear_bwd``), so only K % 8 is required there."""
+    return K % 8 == 0 and N % 4 == 0
 
 
 def _act_fwd(y, act):
@@ -133,6 +137,18 @@ def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True, dx_adden
         db = g.float().sum(0)
     if hip_ok(g, x, w) and _shape_ok(M, N, K):
         g = g.contiguous()
+        if N % 8:  # ragged N (e.g. 12 classes): zero-pad g's columns and w's rows to whole 16-B units
+            n8 = (N + 7) // 8 * 8
+            g = F.pad(g, (0, n8 - N))
+            w = F.pad(w, (0, 0, 0, n8 - N))
+            dx = mm(g, w, True, False)
+            if dx_addend is not None:
+                dx = dx + dx_addend.reshape(dx.shape).to(dx.dtype)
+            dw = mm(g, x, False, False, out_f32=True, splits=0)[:N]
+            if pw is not None and store is not None and pw.grad.dtype == torch.float32:
+                store.deposit(pw, dw)
+                return dx, None, db
+            return dx, dw, db
         acc = dx_addend is not None and dx_addend.is_contiguous() and dx_addend.dtype == torch.bfloat16
         # dgrad reduces over N; a ragged N (e.g. the 1000-class head) is masked by the kernel's K tail (zeros)
         dx = mm(g, w, True, False, out=dx_addend if acc else None, accumulate=acc)

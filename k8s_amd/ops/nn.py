@@ -45,10 +45,6 @@ def _zero_scratch(store, device, n):
     return arena.take(n)
 
 
-# K8S_AMD_MASKED_RES_GRAD=0: the residual BN backward writes dres and the linked dgrad accumulates onto it (A/B)
-MASKED_RES_GRAD = os.environ.get("K8S_AMD_MASKED_RES_GRAD", "1") != "0"
-
-
 class GradLink:
     """Carries one tensor's gradient from one autograd node to another that runs later in the backward
     pass, so the sum of the two contributions is formed inside a kernel (e.g. a ResNet identity block:
@@ -159,7 +155,7 @@ class _StemS2D(torch.autograd.Function):
         w4 = C_.stem_w_s2d(w7.contiguous())
         sums = _zero_scratch(p.store, xs.device, C_.conv_stat_replicas * 2 * w4.shape[0]).view(
             C_.conv_stat_replicas, 2, w4.shape[0])
-        if STEM_CONV and tuple(w4.shape) == (64, 4, 4, 16) and (xs.shape[2] - 3) % 16 == 0 and xs.shape[2] - 3 <= 112:
+        if tuple(w4.shape) == (64, 4, 4, 16) and (xs.shape[2] - 3) % 16 == 0 and xs.shape[2] - 3 <= 112:
             y = C_.stem_conv_fwd(xs.contiguous(), w4, sums)  # LDS-tiled input window (stem.hip)
         else:
             y = C_.conv_fwd(xs, w4, 1, 0, 1, False, None, 0, sums)
@@ -175,7 +171,7 @@ class _StemS2D(torch.autograd.Function):
         (xs,) = ctx.saved_tensors
         p, C_ = ctx.p, _C()
         dw4 = torch.empty(ctx.kshape, device=xs.device, dtype=torch.float32)
-        if STEM_CONV and ctx.kshape == (64, 4, 4, 16) and (xs.shape[2] - 3) % 16 == 0 and xs.shape[2] - 3 <= 112:
+        if ctx.kshape == (64, 4, 4, 16) and (xs.shape[2] - 3) % 16 == 0 and xs.shape[2] - 3 <= 112:
             C_.stem_wgrad(xs.contiguous(), gy.contiguous(), dw4)  # LDS-tiled persistent kernel (stem.hip)
         else:
             _conv_impl()._wgrad_hip(C_, gy.contiguous(), xs, dw4, 1, 0, False)
@@ -242,14 +238,13 @@ class _BnAct(torch.autograd.Function):
         dy = dy.contiguous()
         if ctx.dy_link is not None and ctx.dy_link.mask is not None:  # dy arrives unmasked: apply the mask here
             mask, ctx.dy_link.mask = ctx.dy_link.mask, None
-        mask_out = isinstance(ctx.res_link, MaskLink) and mask is not None and ctx.has_res and MASKED_RES_GRAD
+        mask_out = isinstance(ctx.res_link, MaskLink) and mask is not None and ctx.has_res
         if _gpu(x):
             sg, sb = store.slot_for_write(pg), store.slot_for_write(pb)
             dg = sg if sg is not None else torch.empty(pg.shape, device=x.device, dtype=torch.float32)
             db = sb if sb is not None else torch.empty(pb.shape, device=x.device, dtype=torch.float32)
             # residual gradient for a linked consumer: (dy, mask) instead of a written dres tensor
-            handoff = (isinstance(ctx.res_link, GradLink) and ctx.has_res and mask is not None and
-                       MASKED_RES_GRAD)
+            handoff = isinstance(ctx.res_link, GradLink) and ctx.has_res and mask is not None
             dx, dres = _C().bn_bwd(dy, x, y, mean, invstd, pg.master, pb.master, ctx.relu_x, dg, db,
                                    ctx.has_res and not (handoff or mask_out), mask)
             if handoff:
@@ -276,14 +271,11 @@ class _BnAct(torch.autograd.Function):
 
 
 # Which BatchNorm + ReLU outputs of a ResNet bottleneck are normalised on load by the convolution that consumes them
-# (``bn_relu_conv``) instead of being written by an apply pass: "1x1" = bn2 -> conv3 (default), "all" = also
-# bn1 -> the 3x3 conv2, "0" = none. (The 3x3 consumer re-applies the transform to each input element once per tap:
-# 9x the VALU work of an apply pass, inside a compute-bound product.)
-BN_ONLOAD = os.environ.get("K8S_AMD_BN_ONLOAD", "1x1")
-# the s2d stem conv on its LDS-tiled kernel (stem.hip); K8S_AMD_STEM_CONV=0: the generic implicit GEMM (A/B)
-STEM_CONV = os.environ.get("K8S_AMD_STEM_CONV", "1") != "0"
-# ResNet stem bn1 + ReLU + max pool fused (bn_relu_maxpool); K8S_AMD_STEM_POOL_FUSED=0 runs them separately (A/B)
-STEM_POOL_FUSED = os.environ.get("K8S_AMD_STEM_POOL_FUSED", "1") != "0"
+# (``bn_relu_conv``) instead of being written by an apply pass. Default "3x3": bn2 -> the 1x1 conv3 everywhere, and
+# bn1 -> the 3x3 conv2 wherever the staged-window kernels take the layer (stride 1: conv3x3.hip forward,
+# wgrad_tile.hip weight gradient, both transforming each staged element once -- not once per tap, as the implicit
+# GEMM's on-load path did, which measured 12.48k vs 13.39k img/s in round 3 and was removed). "1x1" = bn2 only (A/B).
+BN_ONLOAD = os.environ.get("K8S_AMD_BN_ONLOAD", "3x3")
 
 
 def _bn_param_grads(store, pg, pb, device):
@@ -337,14 +329,26 @@ class _BnReluConv(torch.autograd.Function):
         return (dx if ctx.x_requires_grad else None,) + (None,) * 11
 
 
+def onload_ok(x, conv) -> bool:
+    """Whether ``conv`` can consume relu(BN(x)) normalised on load in all three of its products: a 1x1 stride-1
+    convolution (the GEMM operand paths), or a 3x3 one the staged-window kernels take (``BN_ONLOAD == "3x3"``)."""
+    K_, R, S, C = conv.w.shape
+    if R == 1 and S == 1:
+        return conv.stride == 1 and conv.pad == 0
+    return (BN_ONLOAD == "3x3" and x.dim() == 4 and
+            bool(_C().conv3x3_staged_ok(x.shape[1], x.shape[2], C, K_, R, S, conv.stride, conv.pad)))
+
+
 def bn_relu_conv(t, bn, conv):
     """``conv(bn(t))`` for ``t = (x, sums)`` from ``conv2d_nhwc(..., with_stats=True)``, a training-mode ReLU
     BatchNorm ``bn`` (models/resnet.BN) and a convolution ``conv`` (models/resnet.Conv): normalised on load
-    (``_BnReluConv``) where the kernels take it, else the separate BN apply + conv. Returns (y, y's sums)."""
+    (``_BnReluConv``) where the kernels take it (``onload_ok``), else the separate BN apply + conv. Returns (y, y's
+    sums)."""
     x, sums = t if isinstance(t, tuple) else (t, None)
     w = conv.w
     if (sums is not None and bn.training and _gpu(x) and x.dtype == torch.bfloat16 and x.shape[-1] % 64 == 0
-            and w.weight.dtype == torch.bfloat16 and w.shape[0] % 8 == 0 and w.grad.dtype == torch.float32):
+            and w.weight.dtype == torch.bfloat16 and w.shape[0] % 8 == 0 and w.grad.dtype == torch.float32
+            and onload_ok(x, conv)):
         return _BnReluConv.apply(x, sums, w.store.anchor, bn.gamma, bn.beta, bn.running_mean, bn.running_var,
                                  bn.momentum, bn.eps, w, conv.stride, conv.pad)
     return conv(bn(t))
@@ -699,11 +703,10 @@ def bn_relu_maxpool(t, bn):
     return max_pool_nhwc(bn(t), 3, 2, 1)
 
 
-# ResNet downsample blocks: bn3 and the downsample BN in one apply pass (bn_act_dual); K8S_AMD_BN_DUAL=0 runs them
-# separately (A/B)
-BN_DUAL = os.environ.get("K8S_AMD_BN_DUAL", "1") != "0"
-# ... and their backwards in one reduce sweep + one apply pass (K8S_AMD_BN_DUAL_BWD=0: two bn_bwd calls, A/B)
-BN_DUAL_BWD = os.environ.get("K8S_AMD_BN_DUAL_BWD", "1") != "0"
+# ResNet downsample blocks: bn3 and the downsample BN in one apply pass (bn_act_dual), their backwards in one reduce
+# sweep + one apply pass (measured round 3: 13.27k -> 13.41k and 13.40k -> 13.56k img/s). tests/test_resnet_gpu.py
+# switches BN_DUAL off to check the fused path against the separate BatchNorms.
+BN_DUAL = True
 
 
 class _BnActDual(torch.autograd.Function):
@@ -732,12 +735,9 @@ class _BnActDual(torch.autograd.Function):
         C_ = _C()
         dg, db, finish = _bn_param_grads(pg.store, pg, pb, x.device)
         dgr, dbr, finish_r = _bn_param_grads(pgr.store, pgr, pbr, x.device)
-        if BN_DUAL_BWD:  # one reduce sweep and one apply pass for both (dy and the mask read once per pass)
-            dx, dxr = C_.bn_bwd_dual(dy, mask, x, mean, invstd, pg.master, pb.master, dg, db, xr, mean_r, invstd_r,
-                                     pgr.master, pbr.master, dgr, dbr)
-        else:
-            dx, _ = C_.bn_bwd(dy, x, None, mean, invstd, pg.master, pb.master, False, dg, db, False, mask)
-            dxr, _ = C_.bn_bwd(dy, xr, None, mean_r, invstd_r, pgr.master, pbr.master, False, dgr, dbr, False, mask)
+        # one reduce sweep and one apply pass for both (dy and the mask read once per pass)
+        dx, dxr = C_.bn_bwd_dual(dy, mask, x, mean, invstd, pg.master, pb.master, dg, db, xr, mean_r, invstd_r,
+                                 pgr.master, pbr.master, dgr, dbr)
         finish()
         finish_r()
         return (dx, None, dxr) + (None,) * 12

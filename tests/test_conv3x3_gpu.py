@@ -81,3 +81,50 @@ def test_conv3x3_data_gradient(cuda, monkeypatch, on, H, C, K):
     xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
     F.conv2d(xr, w.float().permute(0, 3, 1, 2), padding=1).backward(gy.float().permute(0, 3, 1, 2))
     assert _rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+@pytest.mark.parametrize("H,C", [(56, 64), (28, 128), (14, 256)])
+def test_wgrad_tile_bn_relu_on_load(cuda, H, C):
+    """The tiled 3x3 weight gradient with the activation operand normalised on load (wgrad_tile.hip XF): against the
+    fp32 weight gradient of the conv of relu(x * scale + shift), padding untransformed (shift > 0)."""
+    torch.manual_seed(3)
+    N = 2
+    x = torch.randn(N, H, H, C, device=cuda).bfloat16()
+    dy = torch.randn(N, H, H, C, device=cuda).bfloat16()
+    scale = torch.rand(C, device=cuda) + 0.5
+    shift = torch.rand(C, device=cuda) * 0.5 + 0.1
+    params = torch.stack([scale, shift]).contiguous()
+    dw = torch.empty(C, 3, 3, C, device=cuda)
+    _C().conv_wgrad(x, dy, dw, 1, 1, 1, 0, False, xform=params)
+    z = torch.relu(x.float() * scale + shift).bfloat16().float().permute(0, 3, 1, 2)
+    wr = torch.zeros(C, C, 3, 3, device=cuda, requires_grad=True)
+    F.conv2d(z, wr, padding=1).backward(dy.float().permute(0, 3, 1, 2))
+    assert _rel(dw, wr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+def test_resnet_bottleneck_onload_matches_apply_path(cuda, monkeypatch):
+    """A stride-1 bottleneck at stage-1 width on the default (bn1 normalised on load by the staged kernels) against
+    the same block with bn1 applied by the BN kernel (``K8S_AMD_BN_ONLOAD=1x1``): outputs, input gradient and every
+    parameter gradient agree to bf16 rounding."""
+    from k8s_amd.models import resnet
+    from k8s_amd.ops import nn as K
+    from k8s_amd.parallel.flat import ParamStore
+
+    outs = {}
+    for mode in ("3x3", "1x1"):
+        monkeypatch.setattr(K, "BN_ONLOAD", mode)
+        torch.manual_seed(4)
+        store = ParamStore()
+        blk = resnet.Bottleneck(store, "b", 256, 64, 1, False)
+        store.finalize(cuda, seed=11)
+        store.by_name["b.bn3.weight"].master.fill_(1.0)  # zero-init gamma would cut the main path off
+        blk.to(cuda)
+        x = torch.randn(4, 56, 56, 256, device=cuda).bfloat16().requires_grad_(True)
+        store.begin_step()
+        y = blk(x)
+        y.float().square().mean().backward()
+        outs[mode] = (y.detach().float(), x.grad.float(), store.grad.clone())
+    a, b = outs["3x3"], outs["1x1"]
+    assert _rel(a[0], b[0]) < 1e-2
+    assert _rel(a[1], b[1]) < 2e-2
+    assert _rel(a[2], b[2]) < 2e-2

@@ -224,3 +224,48 @@ def test_deleted_and_recreated_job_while_the_watch_is_blind():
                 break
             time.sleep(0.2)
         assert not left, left
+
+
+def test_tfjob_events_are_recorded_in_order():
+    """the operator writes core/v1 Events on the TfJob (involvedObject = the TfJob, with its
+    uid) at each phase / state transition -- Created, Running, Succeeded -- each exactly once (a repeat would bump
+    ``count`` on the same Event), Normal type; ``tfjob describe`` renders them. A spec that cannot run gets a Warning
+    ``Failed`` event carrying the reason."""
+    from k8s_amd import cli
+
+    with LocalCluster() as c:
+        c.create(_job("evjob", "exit 0"))
+        j = _wait_state(c, "evjob", {"Succeeded"})
+        end = time.time() + 10
+        while time.time() < end:
+            evs = cli.job_events(c.client, "default", "evjob")
+            if [e["reason"] for e in evs][-1:] == ["Succeeded"]:
+                break
+            time.sleep(0.2)
+        assert [e["reason"] for e in evs] == ["Created", "Running", "Succeeded"], evs
+        for e in evs:
+            assert e["type"] == "Normal" and e["count"] == 1 and e["source"]["component"] == "tf-operator"
+            io = e["involvedObject"]
+            assert (io["kind"], io["name"], io["uid"]) == ("TfJob", "evjob", j["metadata"]["uid"])
+        import io as _io
+
+        buf = _io.StringIO()
+
+        class A:
+            namespace, name = "default", "evjob"
+
+        assert cli.cmd_describe(c.client, A, buf) == 0
+        text = buf.getvalue()
+        assert "Events:" in text and "Succeeded" in text and "Created" in text
+        # a spec that cannot run: no tensorflow container -> Failed at setup, Warning event with the reason
+        bad = _job("evbad", "exit 0")
+        bad["spec"]["replicaSpecs"][0]["template"]["spec"]["containers"][0]["name"] = "other"
+        c.create(bad)
+        end = time.time() + 30
+        while time.time() < end:
+            evs = cli.job_events(c.client, "default", "evbad")
+            if evs:
+                break
+            time.sleep(0.2)
+        assert [(e["type"], e["reason"]) for e in evs] == [("Warning", "Failed")], evs
+        assert "tensorflow" in evs[0]["message"]

@@ -158,3 +158,45 @@ def test_gemm256_stream_k_sync_words_reset(cuda, monkeypatch):
         b = torch.randn(N, K, device=cuda).bfloat16()
         c = _C().gemm(a, True, b, True, None, True, None, 0, None, False, 1.0, 1)
         assert _rel(c, a.float() @ b.float().t()) < 1e-4, (M, N, K)
+
+
+@pytest.mark.parametrize("M", [4, 12, 1000])
+@pytest.mark.parametrize("N", [4, 12, 1000])
+def test_linear_ragged_rows_and_columns_on_our_kernels(cuda, M, N):
+    """ragged M / N (a batch-4 classifier head, 12 classes) run on our GEMM kernels -- the row
+    tails masked in-kernel, a ragged N zero-padded to 16-B units in the backward -- with no PyTorch fallback, against
+    fp32 PyTorch: forward with bias, data gradient, and the weight gradient written into the flat fp32 slot."""
+    from k8s_amd.ops import gemm
+
+    torch.manual_seed(6)
+    Kd = 2048
+    x = torch.randn(M, Kd, device=cuda).bfloat16()
+    w = (torch.randn(N, Kd, device=cuda) * 0.02).bfloat16()
+    b = torch.randn(N, device=cuda)
+    before = dict(gemm.FALLBACKS)
+    y, saved = gemm.linear_fwd(x, w, b)
+    ref = x.float() @ w.float().t() + b
+    assert _rel(y, ref) < 1e-2
+    gy = torch.randn(M, N, device=cuda).bfloat16()
+    dx, dw, db = gemm.linear_bwd(gy, x, w, saved, None)
+    assert _rel(dx, gy.float() @ w.float()) < 1e-2
+    assert _rel(dw, gy.float().t() @ x.float()) < 1e-2
+    assert _rel(db, gy.float().sum(0)) < 1e-2
+    assert gemm.FALLBACKS == before, gemm.FALLBACKS
+
+
+@pytest.mark.parametrize("mode", ["0", "2"])
+def test_gemm256_mode_switch_sides(cuda, monkeypatch, mode):
+    """$K8S_AMD_GEMM256: 0 routes every product to the 128 x 128 kernel, 2 every product the 256 x 256 kernel can
+    take -- both non-default sides against fp32, all three operand forms."""
+    monkeypatch.setenv("K8S_AMD_GEMM256", mode)
+    torch.manual_seed(7)
+    M, N, K = 2048, 1536, 1024
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    b = torch.randn(N, K, device=cuda).bfloat16()
+    ref = a.float() @ b.float().t()
+    for ak, bk in [(True, True), (True, False), (False, False)]:
+        A = a if ak else a.t().contiguous()
+        B = b if bk else b.t().contiguous()
+        c = _C().gemm(A, ak, B, bk, None, True, None, 0, None, False, 1.0, 1)
+        assert _rel(c, ref) < 1e-4, (ak, bk)

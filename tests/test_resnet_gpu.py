@@ -1,6 +1,7 @@
 """End-to-end ResNet step on the GPU through the HIP kernels, checked against the CPU fp32 path."""
 import pytest
 import torch
+import torch.nn.functional as F
 
 from k8s_amd.models.resnet import resnet_tiny
 from k8s_amd.ops import nn as K
@@ -105,31 +106,29 @@ def test_stem_space_to_depth_matches_7x7(cuda):
 
 
 @pytest.mark.parametrize("N,H,W", [(2, 224, 224), (3, 64, 64), (2, 70, 64)])
-def test_stem_conv_kernel_matches_generic(cuda, N, H, W):
-    """The LDS-tiled s2d stem convolution (stem.hip) vs the generic implicit-GEMM conv of the same 4x4 weight:
-    outputs and the BatchNorm statistics of the stored values (H = 70: 35 output rows, a partial last row tile)."""
+def test_stem_conv_kernel_matches_fp32(cuda, N, H, W):
+    """The LDS-tiled s2d stem convolution (stem.hip) against the fp32 PyTorch conv of the same s2d input and 4x4
+    weight, and its BatchNorm statistics against the sums of the stored bf16 outputs (H = 70: 35 output rows, a
+    partial last row tile)."""
     torch.manual_seed(3)
     C = K._C()
     img = torch.randn(N, H, W, 3, device=cuda).bfloat16()
     xs = K.stem_s2d_input(img)
     w4 = (torch.randn(64, 4, 4, 16, device=cuda) * 0.1).bfloat16()
-    R = C.conv_stat_replicas
-    s1, s2 = torch.zeros(R, 2, 64, device=cuda), torch.zeros(R, 2, 64, device=cuda)
+    s1 = torch.zeros(C.conv_stat_replicas, 2, 64, device=cuda)
     y1 = C.stem_conv_fwd(xs, w4, s1)
-    y2 = C.conv_fwd(xs, w4, 1, 0, 1, False, None, 0, s2)
-    assert y1.shape == y2.shape
-    assert ((y1.float() - y2.float()).norm() / y2.float().norm()).item() < 5e-3
-    t1, t2 = s1.sum(0), s2.sum(0)
-    assert ((t1 - t2).abs().max() / t2.abs().max()).item() < 1e-3
+    ref = F.conv2d(xs.float().permute(0, 3, 1, 2), w4.float().permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+    assert y1.shape == ref.shape
+    assert ((y1.float() - ref).norm() / ref.norm()).item() < 5e-3
+    t1 = s1.sum(0)
     yf = y1.float().reshape(-1, 64)
     assert ((t1[0] - yf.sum(0)).abs().max() / yf.sum(0).abs().max()).item() < 1e-3
+    assert ((t1[1] - (yf * yf).sum(0)).abs().max() / (yf * yf).sum(0).max()).item() < 1e-3
 
 
 @pytest.mark.parametrize("N,H,W", [(2, 224, 224), (3, 70, 64)])
-def test_stem_wgrad_kernel_matches_generic(cuda, N, H, W):
-    """The LDS-tiled persistent s2d stem weight gradient (stem.hip) vs the generic split-K implicit GEMM."""
-    from k8s_amd.ops import conv as convmod
-
+def test_stem_wgrad_kernel_matches_fp32(cuda, N, H, W):
+    """The LDS-tiled persistent s2d stem weight gradient (stem.hip) against the fp32 PyTorch weight gradient."""
     torch.manual_seed(4)
     C = K._C()
     img = torch.randn(N, H, W, 3, device=cuda).bfloat16()
@@ -137,14 +136,14 @@ def test_stem_wgrad_kernel_matches_generic(cuda, N, H, W):
     Ho, Wo = xs.shape[1] - 3, xs.shape[2] - 3
     dy = torch.randn(N, Ho, Wo, 64, device=cuda).bfloat16()
     d1 = torch.empty(64, 4, 4, 16, device=cuda)
-    d2 = torch.empty(64, 4, 4, 16, device=cuda)
     C.stem_wgrad(xs, dy, d1)
-    convmod._wgrad_hip(C, dy, xs, d2, 1, 0, False)
-    assert ((d1 - d2).norm() / d2.norm()).item() < 1e-3
+    ref = torch.nn.grad.conv2d_weight(xs.float().permute(0, 3, 1, 2), (64, 16, 4, 4),
+                                      dy.float().permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+    assert ((d1 - ref).norm() / ref.norm()).item() < 1e-3
 
 
 def test_downsample_bn_dual_matches_separate(cuda):
-    """bn3 + downsample BN fused into one apply pass (ops.nn.bn_act_dual, K8S_AMD_BN_DUAL) vs the separate BNs with
+    """bn3 + downsample BN fused into one apply pass (ops.nn.bn_act_dual, ops.nn.BN_DUAL) vs the separate BNs with
     the MaskLink hand-over, both against the fp32 torch twin with non-trivial BN affines (bn3 starts at gamma 0 in
     the model): the fused path's gradient error may not exceed the separate path's beyond bf16 noise, and both
     update the same running statistics. (The two bf16 paths round differently -- the fused pass adds the downsample
@@ -188,7 +187,9 @@ def test_downsample_bn_dual_matches_separate(cuda):
     l1, e1, s1 = run(True)
     l0, e0, s0 = run(False)
     assert abs(l1 - l0) < 1e-2 * max(1.0, abs(l0)), (l1, l0)
-    bad = [(n, round(e1[n], 4), round(e0[n], 4)) for n in e0 if e1[n] > 1.5 * e0[n] + 0.02]
+    # relative bound only (floored at 0.1 %, far below bf16 gradient noise): no absolute slack that could hide a
+    # wrong gradient on a small-norm parameter
+    bad = [(n, round(e1[n], 4), round(e0[n], 4)) for n in e0 if e1[n] > 1.5 * max(e0[n], 1e-3)]
     assert not bad, bad
     for n, r in s0.items():
         # the first block's inputs are identical in both runs; later blocks see the other rounding of the residual

@@ -2,8 +2,8 @@
 
 Shapes are ResNet-50 layers (1x1 at 56x56 / 28x28, strided 1x1 downsample, 3x3 stride 1 / 2) at a reduced batch,
 with ragged row counts (N*Ho*Wo not a multiple of the 64-row step) and accumulation. The trainer sends only the
-narrow (K or R*S*C = 64) layers here; K8S_AMD_WGS_ANY=1 opens the kernel to every case, and every tile variant
-($K8S_AMD_WGS_TILE) the shape divides into is checked."""
+narrow (K or R*S*C = 64) layers here (128 x 64 tiles at K % 128 == 0, else 64 x 64); the cases it does not take
+are skipped.""" 
 import pytest
 import torch
 import torch.nn.functional as F
@@ -15,7 +15,6 @@ CASES = [  # N, H, C, K, R, stride, pad
     (8, 56, 256, 512, 1, 2, 0), (6, 28, 512, 128, 1, 1, 0), (6, 28, 128, 512, 1, 1, 0),
     (16, 56, 128, 128, 3, 2, 1), (7, 57, 64, 64, 3, 1, 1), (4, 14, 256, 256, 3, 1, 1),
 ]
-TILES = ["128x64", "128x128", "256x128", "64x64"]
 
 
 def _ref_dw(x, gy, K, C, R, stride, pad):
@@ -25,23 +24,20 @@ def _ref_dw(x, gy, K, C, R, stride, pad):
     return dw.permute(0, 2, 3, 1).contiguous()  # KRSC
 
 
-@pytest.mark.parametrize("tile", TILES)
+CASES += [(8, 56, 64, 128, 1, 1, 0), (6, 28, 64, 512, 1, 1, 0)]  # K % 128 == 0 with C = 64: the 128 x 64 tile
+
+
 @pytest.mark.parametrize("N,H,C,K,R,stride,pad", CASES)
-def test_wgrad_stream_matches_fp32(cuda, monkeypatch, N, H, C, K, R, stride, pad, tile):
+def test_wgrad_stream_matches_fp32(cuda, N, H, C, K, R, stride, pad):
     from k8s_amd.ops._ext import load
 
-    kt, ct = map(int, tile.split("x"))
-    if K % kt or (R * R * C) % ct:
-        pytest.skip("tile does not divide the shape")
-    monkeypatch.setenv("K8S_AMD_WGS_ANY", "1")
-    monkeypatch.setenv("K8S_AMD_WGS_TILE", tile)
     C_ = load()
     torch.manual_seed(0)
     x = torch.randn(N, H, H, C, device=cuda).bfloat16()
     Ho = (H + 2 * pad - R) // stride + 1
     gy = torch.randn(N, Ho, Ho, K, device=cuda).bfloat16()
     if not C_.wgrad_stream_eligible(N, Ho, Ho, C, K, R, R):
-        pytest.skip("more output tiles than the streaming kernel takes")
+        pytest.skip("not a shape the streaming kernel takes")
     ref = _ref_dw(x, gy, K, C, R, stride, pad)
     dw = torch.full((K, R, R, C), float("nan"), device=cuda)  # must be fully overwritten
     C_.conv_wgrad(x, gy, dw, stride, pad, 1, 0, False)
