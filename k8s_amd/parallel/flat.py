@@ -58,7 +58,10 @@ class Param:
 
     @property
     def weight(self) -> torch.Tensor:
-        """The tensor compute kernels consume: bf16 copy for MFMA weights, fp32 master otherwise."""
+        """The tensor compute kernels consume: bf16 copy for MFMA weights, fp32 master otherwise. With a bf16 pull in
+        flight (ZeRO-1, parallel/ps.py) the first read of a weight waits for its bucket(s) only."""
+        if self.store.pending:
+            self.store.wait_param(self)
         return self.half if self.half is not None else self.master
 
     def __repr__(self):
@@ -138,6 +141,9 @@ class ParamStore:
         self.total = 0
         self.hooks: List[Callable[[Param], None]] = []
         self.finalized = False
+        # in-flight pull collectives (bucket index -> async work) and param index -> its buckets (parallel/ps.py)
+        self.pending: Dict[int, object] = {}
+        self.pending_of: Dict[int, list] = {}
 
     # ---- construction
     def new(self, name: str, shape, init: Callable, decay: bool = True, lowp: bool = True) -> Param:
@@ -183,6 +189,25 @@ class ParamStore:
         self.refresh_lowp()
         self.finalized = True
         return self
+
+    # ---- pull bookkeeping (ZeRO-1 bf16 pull)
+    def set_pending(self, works: Dict[int, object], buckets_of: Dict[int, list]):
+        self.wait_pending()
+        self.pending = dict(works)
+        self.pending_of = buckets_of
+
+    def wait_param(self, p: Param):
+        """Order the current stream after the pull of ``p``'s bucket(s) (device-side wait for RCCL; blocking for
+        gloo), once per bucket."""
+        for b in self.pending_of.get(p.index, ()):
+            w = self.pending.pop(b.index, None)
+            if w is not None:
+                w.wait()
+
+    def wait_pending(self):
+        works, self.pending = self.pending, {}
+        for w in works.values():
+            w.wait()
 
     def refresh_lowp(self):
         if self.half is not None:

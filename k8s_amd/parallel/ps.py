@@ -14,8 +14,17 @@ RCCL collectives over xGMI:
     update = the fused SGD/Adam kernel on the owned slices only; the optimizer
              keeps fp32 state for those slices only (ZeRO-1: 1/world of the
              moments per rank -- the PS role really holds the state)
-    pull   = all-gather of the updated fp32 master slices; the bf16 working
-             copy is refreshed locally
+    pull   = bf16 all-gather of the updated working-copy slices (the owner's
+             optimizer kernel writes its slice of the bf16 copy in the same
+             pass as the update), bucket by bucket and overlapped with the next
+             forward: each bucket is waited for by the first layer that reads
+             one of its weights (``Param.weight``). The fp32 master stays
+             sharded -- each rank keeps only its owned slices current -- except
+             for the parameters the kernels read in fp32 (norm / BN affines,
+             biases: a few hundred K values), which come back in one small fp32
+             all-gather. Checkpoints and PS snapshots gather the master on
+             demand (``sync_master``). On the CPU (fp32 compute reads the
+             master) the pull is the full fp32 all-gather.
 
 Two push transports:
 
@@ -71,7 +80,7 @@ class _Range:
 
 class ShardedParameterService:
     def __init__(self, store: ParamStore, optimizer, group=None, bucket_mb: float = 64.0,
-                 comm_dtype: torch.dtype = torch.float32, zero1: bool = True):
+                 comm_dtype: torch.dtype = torch.float32, zero1: bool = True, pull: str = "auto"):
         self.store, self.opt, self.group = store, optimizer, group
         init = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(group) if init else 1
@@ -107,6 +116,17 @@ class ShardedParameterService:
         self.side = (torch.cuda.Stream(store.grad.device) if store.grad.is_cuda and self.world > 1 else None)
         self.side_busy = False
         store.hooks.append(self._on_deposit)
+        # pull: "lowp" = bf16 working copy + fp32 non-lowp parameters (GPU default), "fp32" = the full fp32 master
+        if pull not in ("auto", "lowp", "fp32"):
+            raise ValueError("pull must be auto, lowp or fp32")
+        if pull == "auto":
+            pull = "lowp" if (store.master.is_cuda and store.half is not None) else "fp32"
+        if pull == "lowp" and store.half is None:
+            raise ValueError("the bf16 pull needs a low-precision working copy")
+        self.pull = pull if self.sharded else "fp32"
+        self.master_stale = False  # non-owned master slices are not current (bf16 pull)
+        if self.pull == "lowp":
+            self._build_f32_pack()
 
     # ---------------------------------------------------------------- shards
     def shard(self, bk: _Range) -> Tuple[int, int]:
@@ -119,6 +139,7 @@ class ShardedParameterService:
 
     # ---------------------------------------------------------------- step protocol
     def begin_step(self):
+        self.store.wait_pending()  # every bucket of the last pull, read by this step's forward or not
         self.store.begin_step()
         for b in self.buckets:
             b.pending = sum(p.uses for p in b.params)
@@ -173,6 +194,67 @@ class ShardedParameterService:
             torch.cuda.current_stream(self.store.grad.device).wait_stream(self.side)
             self.side_busy = False
 
+    # ---------------------------------------------------------------- bf16 pull
+    def _build_f32_pack(self):
+        """Index plan of the small fp32 pull: the elements of the parameters the kernels read in fp32 (``lowp=False``),
+        per bucket and owning rank, padded to the largest rank's count so one ``all_gather_into_tensor`` moves all of
+        them: rank r sends ``master[send_idx]`` (its owned elements, padded with a repeat), everyone receives
+        [world][total] and scatters the valid entries back (``recv_pos`` -> ``dst_idx``)."""
+        s = self.store
+        flag = torch.zeros(s.total, dtype=torch.bool)
+        for p in s.params:
+            if not p.lowp:
+                flag[p.offset:p.offset + p.numel] = True
+        per_rank = [[] for _ in range(self.world)]
+        width = 0
+        for b in self.buckets:
+            n = (b.hi - b.lo) // self.world
+            parts = [torch.nonzero(flag[b.lo + r * n:b.lo + (r + 1) * n]).flatten() + b.lo + r * n
+                     for r in range(self.world)]
+            m = max(len(t) for t in parts)
+            for r in range(self.world):
+                t = parts[r]
+                pad = t[:1].repeat(m - len(t)) if len(t) else torch.full((m,), b.lo + r * n, dtype=torch.long)
+                per_rank[r].append((torch.cat([t, pad]) if m else t, len(t)))
+            width += m
+        self.f32_width = width
+        dev = s.master.device
+        self.f32_send_idx = torch.cat([t for t, _ in per_rank[self.rank]]).to(dev) if width else None
+        pos, dst = [], []
+        for r in range(self.world):
+            off = r * width
+            for t, valid in per_rank[r]:
+                pos.append(torch.arange(off, off + valid))
+                dst.append(t[:valid])
+                off += len(t)
+        self.f32_recv_pos = torch.cat(pos).to(dev) if width else None
+        self.f32_dst_idx = torch.cat(dst).to(dev) if width else None
+
+    def _pull_lowp(self):
+        """bf16 all-gather of every bucket's working copy (async; waited lazily by ``Param.weight`` or at
+        ``begin_step``), and the fp32 all-gather of the non-lowp parameters (waited here: a few hundred K values)."""
+        s = self.store
+        pending = {}
+        for b in self.buckets:  # ascending offsets: the first layers' weights are requested first
+            lo, hi = self.shard(b)
+            pending[b.index] = dist.all_gather_into_tensor(s.half[b.lo:b.hi], s.half[lo:hi], group=self.group,
+                                                           async_op=True)
+        s.set_pending(pending, self.buckets_of)
+        if self.f32_width:
+            send = s.master.index_select(0, self.f32_send_idx)
+            recv = torch.empty(self.world * self.f32_width, dtype=send.dtype, device=send.device)
+            dist.all_gather_into_tensor(recv, send, group=self.group)
+            s.master.index_copy_(0, self.f32_dst_idx, recv.index_select(0, self.f32_recv_pos))
+        self.master_stale = True
+
+    def sync_master(self):
+        """Make the whole fp32 master current on every rank (checkpoints, PS snapshots, end-of-run checks):
+        the full fp32 all-gather the bf16 pull skips every step. Collective."""
+        if self.world > 1 and self.master_stale:
+            self.store.wait_pending()
+            self._pull(self.store.master)
+            self.master_stale = False
+
     def step(self, lr: Optional[float] = None):
         """Finish the pushes, update the owned shards, pull the new weights."""
         s = self.store
@@ -191,9 +273,12 @@ class ShardedParameterService:
                 dist.all_reduce(stats, group=self.group)
         self.opt.step(grad_scale=1.0 / self.world, lr=lr, ranges=self.owned_ranges, stats_reduce=reduce)
         if self.world > 1:
-            # fp32 master (biases / norm parameters are read from it) then the bf16 copy locally
-            self._pull(s.master)
-            s.refresh_lowp()
+            if self.pull == "lowp":
+                self._pull_lowp()
+            else:
+                # fp32 master (the CPU's fp32 compute reads it) then the bf16 copy locally
+                self._pull(s.master)
+                s.refresh_lowp()
 
     def _pull(self, buf: torch.Tensor):
         works = []

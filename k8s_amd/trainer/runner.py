@@ -347,7 +347,10 @@ def train(a) -> int:
     start_step = _restore(a, w, opt, dev, chief, world, metrics, psv, svc)
 
     def save(step):
-        # sharded optimizer state gathered to the chief only, bucket by bucket, into host memory (collective)
+        # sharded optimizer state gathered to the chief only, bucket by bucket, into host memory (collective); the
+        # fp32 master made current everywhere first (the bf16 pull keeps only each rank's owned slices current)
+        if svc is not None:
+            svc.sync_master()
         full = svc.gather_state() if svc is not None else None
         if not chief:
             return
@@ -362,6 +365,8 @@ def train(a) -> int:
 
     def ps_push(step):
         """Variable snapshot to the PS tasks (collective for the sharded optimizer state, like save())."""
+        if svc is not None:
+            svc.sync_master()
         full = svc.gather_state() if svc is not None else None
         if psv is None:
             return
@@ -468,6 +473,8 @@ def train(a) -> int:
         metrics.event(event="ps_snapshot", step=psv.pushed)
     if watchdog is not None:
         watchdog.stop()
+    if svc is not None:
+        svc.sync_master()
     kdist.barrier()
     from k8s_amd.ops import gemm as kgemm
 

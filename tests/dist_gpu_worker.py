@@ -28,8 +28,10 @@ def main():
     if mode.startswith("zero"):  # ZeRO-1 sharded service (reduce-scatter / all-to-all push, owner update, pull)
         from k8s_amd.parallel.ps import ShardedParameterService
 
+        # "zero-fp32pull-*": the fp32-master pull; otherwise the GPU default, the bf16 working-copy pull
         svc = ShardedParameterService(store, opt, bucket_mb=0.01,
-                                      comm_dtype=torch.bfloat16 if mode.endswith("bf16") else torch.float32)
+                                      comm_dtype=torch.bfloat16 if mode.endswith("bf16") else torch.float32,
+                                      pull="fp32" if "fp32pull" in mode else "auto")
         begin, finish = svc.begin_step, svc.step
     else:  # many buckets: every hook / overlap path runs
         red = GradReducer(store, bucket_mb=0.01,
@@ -47,6 +49,10 @@ def main():
         loss = K.cross_entropy(model(model.prepare_input(x).contiguous()), y)
         loss.backward()
         finish()
+    pull = "none"
+    if mode.startswith("zero"):
+        pull = svc.pull
+        svc.sync_master()  # the bf16 pull keeps only the owned fp32 master slices current
     if gpu:
         torch.cuda.synchronize()
     # the sharded optimizer keeps different (owned) state slices per rank: compare the weights only
@@ -56,8 +62,9 @@ def main():
     same = torch.tensor([int(torch.equal(state, ref))])
     torch.distributed.all_reduce(same, op=torch.distributed.ReduceOp.MIN)
     if info.rank == 0:
-        print("{\"replicas_identical\": %d, \"world\": %d, \"loss\": %.5f}" % (int(same), info.world_size,
-                                                                              float(loss.detach())), flush=True)
+        print("{\"replicas_identical\": %d, \"world\": %d, \"loss\": %.5f, \"pull\": \"%s\", \"wsum\": %r}"
+              % (int(same), info.world_size, float(loss.detach()), pull, float(store.master.double().sum())),
+              flush=True)
     kdist.destroy()
 
 

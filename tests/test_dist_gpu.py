@@ -38,6 +38,16 @@ def test_dp_replicas_stay_identical_on_gpu(mode):
     assert rec["loss"] == rec["loss"]
 
 
+def test_zero_bf16_pull_matches_fp32_pull_on_gpu():
+    """The ZeRO-1 bf16 working-copy pull (the GPU default: bucket-wise bf16 all-gather waited per bucket by the next
+    forward, fp32 master sharded) trains bit-identically to the fp32-master pull on the GPU kernels."""
+    (a,) = _torchrun("tests/dist_gpu_worker.py", ["zero-bf16"])
+    (b,) = _torchrun("tests/dist_gpu_worker.py", ["zero-fp32pull-bf16"])
+    assert (a["pull"], b["pull"]) == ("lowp", "fp32")
+    assert a["replicas_identical"] == 1 and b["replicas_identical"] == 1
+    assert a["wsum"] == b["wsum"] and a["loss"] == b["loss"]
+
+
 def test_bench_two_ranks_on_gpu():
     (r,) = _torchrun("bench.py", ["--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "16", "--image", "64"])
     assert r["n_gpus"] == 2 and r["dtype"] == "bf16" and r["config"]["parallelism"] == "dp2"

@@ -26,7 +26,7 @@ def _grads(rank, step, shapes):
     return [torch.randn(s, generator=g) * (1.0 + rank) for s in shapes]
 
 
-def _worker(rank, world, port, strategy, comm, opt_name, steps, out_dir, nan_step, clip=10.0):
+def _worker(rank, world, port, strategy, comm, opt_name, steps, out_dir, nan_step, clip=10.0, pull="auto"):
     from k8s_amd.ops.optim import FusedAdam, FusedSGD
     from k8s_amd.parallel.ddp import GradReducer
     from k8s_amd.parallel.flat import ALIGN, ParamStore, init_normal
@@ -35,7 +35,7 @@ def _worker(rank, world, port, strategy, comm, opt_name, steps, out_dir, nan_ste
     torch.set_num_threads(1)
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
     store = ParamStore()
-    params = [store.new("p%d" % i, s, init_normal(0.5), decay=(i % 2 == 0)) for i, s in enumerate(SHAPES)]
+    params = [store.new("p%d" % i, s, init_normal(0.5), decay=(i % 2 == 0), lowp=(i % 3 != 2)) for i, s in enumerate(SHAPES)]
     store.finalize("cpu", pad_to=world * ALIGN, seed=5)
     if opt_name == "sgd":
         opt = FusedSGD(store, lr=0.05, momentum=0.9, weight_decay=1e-3, max_grad_norm=clip)
@@ -43,7 +43,7 @@ def _worker(rank, world, port, strategy, comm, opt_name, steps, out_dir, nan_ste
         opt = FusedAdam(store, lr=0.01, weight_decay=0.01, max_grad_norm=clip)
     dtype = torch.bfloat16 if comm == "bf16" else torch.float32
     if strategy == "ps":
-        svc = ShardedParameterService(store, opt, bucket_mb=0.002, comm_dtype=dtype)  # several buckets
+        svc = ShardedParameterService(store, opt, bucket_mb=0.002, comm_dtype=dtype, pull=pull)  # several buckets
         begin, finish = svc.begin_step, (lambda: svc.step())
     else:
         red = GradReducer(store, bucket_mb=0.002, comm_dtype=dtype)
@@ -61,20 +61,28 @@ def _worker(rank, world, port, strategy, comm, opt_name, steps, out_dir, nan_ste
         for p, g in reversed(list(zip(params, gs))):  # backward order
             store.deposit(p, g)
         finish()
+    stale_ok = True
+    if svc is not None and svc.pull == "lowp" and world > 1:
+        # before sync_master: the bf16 copy is whole, the fp32 master current on this rank's owned slices and on the
+        # fp32-read (lowp=False) parameters only
+        store.wait_pending()
+        ref_half = store.half.clone()
+        svc.sync_master()
+        stale_ok = torch.equal(ref_half, store.half) and torch.equal(store.half, store.master.to(torch.bfloat16))
     full = svc.gather_state() if svc is not None else None
     if rank == 0:
         sd = opt.state_dict(full)
         torch.save({"master": store.master.clone(), "half": store.half.float().clone(),
                     **{k: v.clone() for k, v in sd.items() if torch.is_tensor(v)},
-                    "state_numel": opt.state_numel(), "total": store.total},
+                    "state_numel": opt.state_numel(), "total": store.total, "stale_ok": stale_ok},
                    os.path.join(out_dir, "%s_%s_%s.pt" % (strategy, comm, opt_name)))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run(world, strategy, comm, opt_name, steps=4, nan_step=-1, clip=10.0):
+def _run(world, strategy, comm, opt_name, steps=4, nan_step=-1, clip=10.0, pull="auto"):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, free_port(), strategy, comm, opt_name, steps, d, nan_step, clip),
+        mp.spawn(_worker, args=(world, free_port(), strategy, comm, opt_name, steps, d, nan_step, clip, pull),
                  nprocs=world)
         return torch.load(os.path.join(d, "%s_%s_%s.pt" % (strategy, comm, opt_name)), weights_only=True)
 
@@ -85,7 +93,7 @@ def _reference(world, opt_name, steps):
     from k8s_amd.parallel.flat import ALIGN, ParamStore, init_normal
 
     store = ParamStore()
-    params = [store.new("p%d" % i, s, init_normal(0.5), decay=(i % 2 == 0)) for i, s in enumerate(SHAPES)]
+    params = [store.new("p%d" % i, s, init_normal(0.5), decay=(i % 2 == 0), lowp=(i % 3 != 2)) for i, s in enumerate(SHAPES)]
     store.finalize("cpu", pad_to=world * ALIGN, seed=5)
     if opt_name == "sgd":
         opt = FusedSGD(store, lr=0.05, momentum=0.9, weight_decay=1e-3, max_grad_norm=10.0)
@@ -148,7 +156,7 @@ def _reference_bf16(world, opt_name, steps, round_sum, clip=None):
     from k8s_amd.parallel.flat import ALIGN, ParamStore, init_normal
 
     store = ParamStore()
-    params = [store.new("p%d" % i, s, init_normal(0.5), decay=(i % 2 == 0)) for i, s in enumerate(SHAPES)]
+    params = [store.new("p%d" % i, s, init_normal(0.5), decay=(i % 2 == 0), lowp=(i % 3 != 2)) for i, s in enumerate(SHAPES)]
     store.finalize("cpu", pad_to=world * ALIGN, seed=5)
     if opt_name == "sgd":
         opt = FusedSGD(store, lr=0.05, momentum=0.9, weight_decay=1e-3, max_grad_norm=clip)
@@ -225,3 +233,17 @@ def test_sharded_state_gathers_to_one_rank_and_scatters_back():
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_gather_worker, args=(world, free_port(), d), nprocs=world)
         assert sorted(os.listdir(d)) == ["ok%d" % r for r in range(world)]
+
+
+@pytest.mark.parametrize("world", [4, 8])
+@pytest.mark.parametrize("comm", ["fp32", "bf16"])
+def test_bf16_pull_bit_exact_against_fp32_pull(world, comm):
+    """the ZeRO-1 bf16 pull (working copy all-gathered bucket by bucket, fp32 master kept
+    sharded, fp32 all-gather only for the lowp=False parameters) ends bit-identical to the fp32-master pull after
+    several Adam steps: master (after sync_master), bf16 copy and the gathered optimizer state; and before the sync
+    the bf16 copy already equals bf16(master) everywhere."""
+    a = _run(world, "ps", comm, "adam", steps=5, pull="lowp")
+    b = _run(world, "ps", comm, "adam", steps=5, pull="fp32")
+    assert a["stale_ok"]
+    for k in ("master", "half", "exp_avg", "exp_avg_sq"):
+        assert torch.equal(a[k], b[k]), k
