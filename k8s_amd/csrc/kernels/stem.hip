@@ -254,7 +254,9 @@ __global__ void __launch_bounds__(256, 3) stem_wgrad_kernel(const uint16_t* __re
   // there; dy rows past Ho from the zero page); the CU's other blocks compute while one stages
   auto stage = [&](int t) {
     const int n = t / tiles_per_img, r0 = (t % tiles_per_img) * SWG_RT;
-    const int nch = min(SWG_RT + 3, Hs - r0) * Ws * 2;
+    // the whole window, rows past the image from the zero page: a partial last tile multiplies its zero dy rows by
+    // these window rows, and stale LDS there (a NaN bit pattern from an earlier kernel) would make 0 * NaN = NaN
+    const int nch = (SWG_RT + 3) * Ws * 2, nvalid = min(SWG_RT + 3, Hs - r0) * Ws * 2;
     const int npx = min(SWG_RT, Ho - r0) * Wo;
     const uint16_t* sx = xs + ((long)n * Hs + r0) * Ws * 16;
     const uint16_t* sd = dy + (((long)n * Ho + r0) * Wo) * STEM_K;
@@ -262,7 +264,8 @@ __global__ void __launch_bounds__(256, 3) stem_wgrad_kernel(const uint16_t* __re
     for (int c = tid; c - tid < nch; c += 256) {
       if (c < nch) {
         const int pos = c >> 1, lh = (c & 1) ^ ((pos >> 3) & 1);
-        glds16(sx + (long)pos * 16 + lh * 8, xw + __builtin_amdgcn_readfirstlane(c - lane) * 16);
+        glds16(c < nvalid ? (const void*)(sx + (long)pos * 16 + lh * 8) : (const void*)g_stem_zero,
+               xw + __builtin_amdgcn_readfirstlane(c - lane) * 16);
       }
     }
 #pragma unroll 1

@@ -89,8 +89,8 @@ class Bottleneck(nn.Module):
             if not fuse:
                 idn = self.down_bn(dn, relu=False, dy_link=mlink)
         t = self.conv1(x, grad_link=link or dlink)
-        # bn1 / bn2 + ReLU: normalised on load by the consuming convolution where its kernels take it
-        # (ops.nn.bn_relu_conv: no apply pass, no z tensor), else applied by the BN kernel
+        # bn1 / bn2 + ReLU: normalised on load by the consuming convolution where ops.nn.BN_ONLOAD and its kernels
+        # take it (ops.nn.bn_relu_conv: no apply pass, no z tensor), else applied by the BN kernel
         t = K.bn_relu_conv(t, self.bn1, self.conv2)
         t = K.bn_relu_conv(t, self.bn2, self.conv3)
         if dn is not None and fuse:

@@ -271,11 +271,14 @@ class _BnAct(torch.autograd.Function):
 
 
 # Which BatchNorm + ReLU outputs of a ResNet bottleneck are normalised on load by the convolution that consumes them
-# (``bn_relu_conv``) instead of being written by an apply pass. Default "3x3": bn2 -> the 1x1 conv3 everywhere, and
-# bn1 -> the 3x3 conv2 wherever the staged-window kernels take the layer (stride 1: conv3x3.hip forward,
-# wgrad_tile.hip weight gradient, both transforming each staged element once -- not once per tap, as the implicit
-# GEMM's on-load path did, which measured 12.48k vs 13.39k img/s in round 3 and was removed). "1x1" = bn2 only (A/B).
-BN_ONLOAD = os.environ.get("K8S_AMD_BN_ONLOAD", "3x3")
+# (``bn_relu_conv``) instead of being written by an apply pass. Default "1x1": bn2 -> the 1x1 conv3 everywhere.
+# "3x3" also normalises bn1 in the 3x3 conv2 wherever the staged-window kernels take the layer (stride 1:
+# conv3x3.hip forward, wgrad_tile.hip weight gradient, each transforming a staged element once, not once per tap as
+# the round-3 implicit-GEMM path did). Measured round 4 (ResNet-50 b1024, one box, rocprofv3 per-kernel diff,
+# profiles/r04_bn1_onload_diff.txt): it removes 11 of 32 apply passes (-0.78 ms / step) but the in-LDS transform pass
+# costs the staged forward +0.36 ms and the tiled weight gradient +0.71 ms (a VALU / LDS phase between the window
+# DMA and the MFMAs): 13.78-13.84k vs 13.85-13.87k img/s, so it stays opt-in.
+BN_ONLOAD = os.environ.get("K8S_AMD_BN_ONLOAD", "1x1")
 
 
 def _bn_param_grads(store, pg, pb, device):

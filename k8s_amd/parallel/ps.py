@@ -305,8 +305,9 @@ class ShardedParameterService:
         for attr in self.opt.STATE:
             compact = getattr(self.opt, attr)
             if out is not None:
-                out[attr] = torch.empty(self.store.total, dtype=torch.float32,
-                                        pin_memory=dev.type == "cuda")
+                # pageable host memory: a page-locked allocation of the whole state per call (Llama-3-8B with Adam:
+                # ~64 GB) cost more than the faster copies it buys, and ps_vars keeps the result until its push ends
+                out[attr] = torch.empty(self.store.total, dtype=torch.float32)
             for b, (lo, hi, off) in zip(self.buckets, self.opt.layout):
                 n = hi - lo
                 glist = None
