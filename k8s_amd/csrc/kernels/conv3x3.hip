@@ -17,11 +17,23 @@
 // Layout / tiling:
 //  * 256 threads = 4 waves as 2 (pixels) x 2 (channels); wave piece = MF x 16 pixels x KT / 2 channels, MF x NF
 //    tiles of v_mfma_f32_16x16x32_bf16 (operands swapped: each lane ends with 4 consecutive output channels).
+//  * window: row wr (image row h0 - 1 + wr) at positions wr * WP + 8 + [0, W), WP = W rounded up to a multiple of 8
+//    (64 / 32 / 16); the positions between rows are zero and serve as the left and right padding. Output pixel m =
+//    (r, c) reads position pw + dr * WP + ds at tap (dr, ds), pw = r * WP + 7 + c. Because WP % 8 == 0 the swizzle
+//    below is the same for all three dr, so a lane's A address is computed once per ds and the dr taps are
+//    immediate offsets of the same ds_read_b128.
 //  * LDS images [position][64 ch] (window) and [row][64 ch] (weights), 128-B rows, 16-B chunk c of row p stored at
-//    c ^ ((p >> 1) & 7): the 16 lanes of a fragment read 16 consecutive positions -> conflict-free ds_read_b128.
+//    c ^ (p & 6): with fragment lane group j reading chunk 4 kk + j, every ds_read_b128 lane group of 16 consecutive
+//    positions -- starting at ANY position -- hits 16 distinct 16-B bank slots (searched exhaustively; the
+//    (p >> 1) & 7 XOR of gemm.hip is conflict-free only for 16-aligned runs and cost 37-41 % of the LDS cycles here).
+//    A fragment crossing a row end jumps by WP - W positions: 8 at W = 56 (still conflict-free), 4 / 2 at 28 / 14.
+//  * NS weight slots: tap g + NS - 1 streams in while tap g computes.
+//  * measured (profiles/r04_conv3x3_pmc.txt): 1.10-1.24x the implicit GEMM; the 56 x 56 layer runs at 28 % MFMA busy
+//    and an ablation of its phases (staging, LDS reads, epilogue) shows no single one dominating -- the two blocks per
+//    CU overlap their phases poorly. The swizzle, address and weight-ring changes above moved it by < 1 %.
 //  * epilogue: the bf16 tile goes through LDS, leaves as 16-B row segments, and the per-channel sum / sum of squares
 //    of the stored values are accumulated for the following BatchNorm (the [STAT_REPL][2][K] layout of gemm.hip).
-//  * ~60-71 KB LDS, <= 128 VGPRs: 2 blocks per CU, so one block's window staging overlaps the other's MFMAs.
+//  * <= 80 KB LDS: 2 blocks per CU, so one block's window staging overlaps the other's MFMAs.
 #include <stdexcept>
 
 #include "common.h"
@@ -33,18 +45,22 @@ namespace k8s_amd {
 namespace c3 {
 constexpr int THREADS = 256;
 constexpr int STAT_REPL = 32;  // = gemm.hip STAT_REPL = kConvStatReplicas
-__device__ __attribute__((aligned(64))) uint16_t g_c3_zero[64];  // source of the zero padding
+__device__ __attribute__((aligned(64))) uint16_t g_c3_zero[64];  // source of the rows outside the image
 
-__device__ __forceinline__ int swz(int p) { return (p >> 1) & 7; }
+__device__ __forceinline__ int swz(int p) { return p & 6; }
 
 template <int W, int RT, int KT, bool XF>
 struct Geo {
-  static constexpr int WP = W + 2, WIN = (RT + 2) * WP, P = RT * W;
+  static constexpr int WP = (W + 7) / 8 * 8 + (W % 8 == 0 ? 8 : 0), P = RT * W;
+  static constexpr int NPOS = (RT + 2) * WP + 8;  // + the right padding of the last row
   static constexpr int MF = (P + 31) / 32, NF = KT / 32;
-  static constexpr int WIN_B = WIN * 128, WT_B = KT * 128;
+  static constexpr int WIN_B = NPOS * 128, WT_B = KT * 128;
+  static constexpr int NS = WIN_B + 3 * WT_B <= 80 * 1024 ? 3 : 2;  // 2 blocks per CU
   static constexpr int STAGE_B = 32 * MF * KT * 2;  // epilogue C tile
-  static constexpr int LDS = (WIN_B + 2 * WT_B) > STAGE_B ? (WIN_B + 2 * WT_B) : STAGE_B;
+  static constexpr int LDS = (WIN_B + NS * WT_B) > STAGE_B ? (WIN_B + NS * WT_B) : STAGE_B;
+  static_assert(WIN_B + NS * WT_B <= 80 * 1024, "two blocks per CU");
   static_assert(LDS >= THREADS * 16 * 4, "room for the statistics partials");
+  static_assert(WP % 8 == 0 && WP > W, "pitch");
 };
 
 template <int W, int RT, int KT, bool XF>
@@ -53,7 +69,8 @@ __global__ void __launch_bounds__(THREADS, 2) conv3x3_kernel(const uint16_t* __r
                                                             float* __restrict__ stats, const float* __restrict__ xf,
                                                             int H, int C, int K, int tiles_per_img) {
   using G = Geo<W, RT, KT, XF>;
-  constexpr int WP = G::WP, WIN = G::WIN, P = G::P, MF = G::MF, NF = G::NF;
+  constexpr int WP = G::WP, NPOS = G::NPOS, P = G::P, MF = G::MF, NF = G::NF, NS = G::NS;
+  constexpr int WOPS = KT * 8 / THREADS;  // weight DMA instructions per thread per tap
   __shared__ __attribute__((aligned(1024))) char smem[G::LDS];
   char* const win = smem;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -63,103 +80,162 @@ __global__ void __launch_bounds__(THREADS, 2) conv3x3_kernel(const uint16_t* __r
   const int n = tile / tiles_per_img, h0 = (tile - n * tiles_per_img) * RT;
   const int k0 = blockIdx.y * KT;
 
-  // this lane's window position (tap (0, 0)) for each of its MF pixel fragments; padding rows of the last fragment
-  // read position 0 (their outputs are never stored)
-  int pos0[MF];
+  // window position of this lane's pixel for each fragment at tap (0, 0); pad lanes of a last fragment (m >= P, only
+  // when P % 32 != 0) read what lies past the window -- their output rows are never stored
+  int pw[MF];
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
-    const int m = (wm * MF + f) * 16 + (lane & 15);
-    const int row = m / W, col = m - row * W;
-    pos0[f] = m < P ? row * WP + col : 0;
+    const int m = (wm * MF + f) * 16 + (lane & 15), r = m / W;
+    pw[f] = r * WP + 7 + (m - r * W);
   }
+  int boff[2][NF];  // B operand byte offsets in a weight slot
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int r = wn * (KT / 2) + j * 16 + (lane & 15), ch = kk * 4 + (lane >> 4);
+      boff[kk][j] = r * 128 + ((ch ^ swz(r)) << 4);
+    }
   f32x4_t acc[MF][NF];
 #pragma unroll
   for (int f = 0; f < MF; ++f)
 #pragma unroll
     for (int j = 0; j < NF; ++j) acc[f][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // a thread's window chunks c = i * 256 + tid all hold the same logical 8 channels (256 % 16 == 0)
-  const int lchunk = (tid & 7) ^ ((tid >> 4) & 7);
+  // the padding positions (everything that is not image data) are zeroed once; the DMA never writes them
+#pragma unroll 1
+  for (int c = tid; c < NPOS * 8; c += THREADS) {
+    const int q = (c >> 3) - 8;
+    if (q < 0 || q - q / WP * WP >= W || q >= (RT + 2) * WP)
+      *reinterpret_cast<bf16x8_t*>(win + c * 16) = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  // window DMA: row wr, instruction i covers positions wr * WP + 8 + 8 i + [0, 8) (lane-linear 16-B pieces); the
+  // logical chunk of a lane is fixed because every instruction's first position is a multiple of 8
+  constexpr int IPR = (W * 8 + 63) / 64, NWI = (RT + 2) * IPR;
+  const int lch = (lane & 7) ^ ((lane >> 3) & 6);
+  auto load_window = [&](int c0) {
+#pragma unroll 1
+    for (int wi = wid; wi < NWI; wi += THREADS / 64) {
+      const int wr = wi / IPR, i = wi - wr * IPR, px = i * 8 + (lane >> 3), h = h0 - 1 + wr;
+      if (px < W) {
+        const void* src = (unsigned)h < (unsigned)H ? (const void*)(x + (((long)n * H + h) * W + px) * C + c0 + lch * 8)
+                                                    : (const void*)g_c3_zero;
+        glds16(src, win + (wr * WP + 8 + i * 8) * 128);
+      }
+    }
+  };
+  auto transform_window = [&](int c0) {  // XF: relu(x * scale + shift) in place, once per staged image element
+    const int lc = (tid & 7) ^ ((tid >> 3) & 6);  // logical chunk of LDS chunk c = k * 256 + tid
+    float sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = xf[c0 + lc * 8 + j];
+      sh[j] = xf[C + c0 + lc * 8 + j];
+    }
+#pragma unroll 1
+    for (int c = tid; c < NPOS * 8; c += THREADS) {
+      const int q = (c >> 3) - 8, wr = q / WP, h = h0 - 1 + wr;
+      if (q >= 0 && q - wr * WP < W && wr < RT + 2 && (unsigned)h < (unsigned)H) {
+        bf16x8_t* qp = reinterpret_cast<bf16x8_t*>(win + c * 16);
+        const bf16x8_t v = *qp;
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = fmaxf(__builtin_fmaf(bf2f((uint16_t)v[j]), sc[j], sh[j]), 0.f);
+        *qp = pack_bf16x8(o);
+      }
+    }
+    __syncthreads();
+  };
   auto stage_w = [&](int tap, int c0, int slot) {
     char* d = smem + G::WIN_B + slot * G::WT_B;
 #pragma unroll
-    for (int i = 0; i < KT * 8 / THREADS; ++i) {
+    for (int i = 0; i < WOPS; ++i) {
       const int c = i * THREADS + tid, row = c >> 3, lc = (c & 7) ^ swz(row);
       glds16(wt + ((long)(k0 + row) * 9 + tap) * C + c0 + lc * 8, d + (i * THREADS + wid * 64) * 16);
     }
   };
+  // steps g = slice * 9 + 3 ds + dr visit the taps ds-major; tap_of(k) for k = g % 9
+  auto tap_of = [](int k) { return (k % 3) * 3 + k / 3; };
 
-  const int nslices = C >> 6;
-  for (int cs = 0; cs < nslices; ++cs) {
-    const int c0 = cs * 64;
-    if (cs) __syncthreads();  // every wave is done with the previous slice's window and weights
-    // ---- window rows h0 - 1 .. h0 + RT, columns -1 .. W (zero page outside the image), by LDS-DMA
+  const int nsteps = (C >> 6) * 9;
+  load_window(0);
+#pragma unroll
+  for (int g = 0; g < NS - 1; ++g)
+    if (g < nsteps) stage_w(tap_of(g), 0, g);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if constexpr (XF) transform_window(0);
 #pragma unroll 1
-    for (int i = 0; i < (WIN * 8 + THREADS - 1) / THREADS; ++i) {
-      const int c = i * THREADS + tid;
-      if (c < WIN * 8) {  // lanes past the window stay inactive (they would write into the weight slots)
-        const int p = c >> 3, wr = p / WP, wc = p - wr * WP, h = h0 - 1 + wr, w = wc - 1;
-        const bool in = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-        const void* src = in ? (const void*)(x + (((long)n * H + h) * W + w) * C + c0 + lchunk * 8)
-                             : (const void*)g_c3_zero;
-        glds16(src, win + __builtin_amdgcn_readfirstlane(i * THREADS + wid * 64) * 16);
-      }
+  for (int cs = 0; cs < (C >> 6); ++cs) {
+    if (cs) {  // next 64-channel slice: every wave is past the previous slice's last tap (barrier)
+      load_window(cs * 64);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if constexpr (XF) transform_window(cs * 64);
     }
-    stage_w(0, c0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if constexpr (XF) {  // relu(x * scale + shift) in place, once per staged element; padding stays zero
-      float sc[8], sh[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        sc[j] = xf[c0 + lchunk * 8 + j];
-        sh[j] = xf[C + c0 + lchunk * 8 + j];
-      }
 #pragma unroll 1
-      for (int i = 0; i < (WIN * 8 + THREADS - 1) / THREADS; ++i) {
-        const int c = i * THREADS + tid;
-        if (c < WIN * 8) {
-          const int p = c >> 3, wr = p / WP, wc = p - wr * WP, h = h0 - 1 + wr, w = wc - 1;
-          if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
-            bf16x8_t* q = reinterpret_cast<bf16x8_t*>(win + c * 16);
-            const bf16x8_t v = *q;
-            float o[8];
+    for (int ds = 0; ds < 3; ++ds) {
+      int aoff[2][MF];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) o[j] = fmaxf(__builtin_fmaf(bf2f((uint16_t)v[j]), sc[j], sh[j]), 0.f);
-            *q = pack_bf16x8(o);
+      for (int f = 0; f < MF; ++f) {
+        const int p = pw[f] + ds;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) aoff[kk][f] = p * 128 + (((kk * 4 + (lane >> 4)) ^ swz(p)) << 4);
+      }
+#pragma unroll
+      for (int dr = 0; dr < 3; ++dr) {
+        const int g = cs * 9 + ds * 3 + dr, gp = g + NS - 1;
+        if (gp < nsteps) stage_w(tap_of(gp % 9), gp / 9 * 64, gp % NS);  // slot last read in step g - 1
+        const char* ws = smem + G::WIN_B + (NS == 3 ? dr : g & 1) * G::WT_B;  // NS = 3: g % 3 == dr
+        const char* wa = win + dr * WP * 128;
+        if constexpr (NF == 2) {
+          // both k-halves' fragments read up front, the first half's MFMAs waiting only for their own reads (the
+          // compiler's own order waited for every read before the next: LDS latency exposed at 2 waves per SIMD)
+          mfma_bf16x8 af[2][MF], bfr[2][NF];
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+            for (int f = 0; f < MF; ++f)
+              af[kk][f] = __builtin_bit_cast(mfma_bf16x8, *reinterpret_cast<const bf16x8_t*>(wa + aoff[kk][f]));
+#pragma unroll
+            for (int j = 0; j < NF; ++j)
+              bfr[kk][j] = __builtin_bit_cast(mfma_bf16x8, *reinterpret_cast<const bf16x8_t*>(ws + boff[kk][j]));
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            if (kk == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(MF + NF) : "memory");
+            else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int f = 0; f < MF; ++f)
+#pragma unroll
+              for (int j = 0; j < NF; ++j)
+                acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[kk][j], af[kk][f], acc[f][j], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        } else {  // 112 accumulator VGPRs: no room for a second fragment set
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            mfma_bf16x8 af[MF], bfr[NF];
+#pragma unroll
+            for (int f = 0; f < MF; ++f)
+              af[f] = __builtin_bit_cast(mfma_bf16x8, *reinterpret_cast<const bf16x8_t*>(wa + aoff[kk][f]));
+#pragma unroll
+            for (int j = 0; j < NF; ++j)
+              bfr[j] = __builtin_bit_cast(mfma_bf16x8, *reinterpret_cast<const bf16x8_t*>(ws + boff[kk][j]));
+#pragma unroll
+            for (int f = 0; f < MF; ++f)
+#pragma unroll
+              for (int j = 0; j < NF; ++j)
+                acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[f], acc[f][j], 0, 0, 0);
           }
         }
+        // step g + 1's weights landed (step g + NS - 1's may still be in flight)
+        if (NS > 2 && gp < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WOPS * (NS - 2)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
       }
-      __syncthreads();
-    }
-#pragma unroll 1
-    for (int t = 0; t < 9; ++t) {
-      if (t + 1 < 9) stage_w(t + 1, c0, (t + 1) & 1);  // its slot was last read in tap t - 1 (barrier since)
-      const int tr = t / 3, toff = tr * WP + (t - tr * 3);
-      const char* ws = smem + G::WIN_B + (t & 1) * G::WT_B;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int ch = kk * 4 + (lane >> 4);
-        mfma_bf16x8 af[MF], bfr[NF];
-#pragma unroll
-        for (int f = 0; f < MF; ++f) {
-          const int p = pos0[f] + toff;
-          af[f] = __builtin_bit_cast(mfma_bf16x8,
-                                     *reinterpret_cast<const bf16x8_t*>(win + p * 128 + ((ch ^ swz(p)) << 4)));
-        }
-#pragma unroll
-        for (int j = 0; j < NF; ++j) {
-          const int r = wn * (KT / 2) + j * 16 + (lane & 15);
-          bfr[j] = __builtin_bit_cast(mfma_bf16x8,
-                                      *reinterpret_cast<const bf16x8_t*>(ws + r * 128 + ((ch ^ swz(r)) << 4)));
-        }
-#pragma unroll
-        for (int f = 0; f < MF; ++f)
-#pragma unroll
-          for (int j = 0; j < NF; ++j) acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[f], acc[f][j], 0, 0, 0);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tap t + 1's weights landed
-      __syncthreads();
     }
   }
 
