@@ -539,14 +539,14 @@ Gemm256Plan gemm256_plan(int M, int N, int K) {
   p.kps = K;
   constexpr int P = 256;
   const int waves = p.tiles / P, r = p.tiles % P;
-  if (r == 0 || waves >= 8 || r > P / 2) return p;
+  // sub-wave grids (waves == 0, e.g. BERT's M = 8192 x N = 768 products, 96 tiles) stay on the 128 x 128 kernel:
+  // split 2 ways onto this kernel they measured 72-82 us per call in the BERT step against 51-62 us there
+  // (profiles/r04_bert_b64.md, first run)
+  if (r == 0 || waves == 0 || waves >= 8 || r > P / 2) return p;
   const char* e = getenv("K8S_AMD_GEMM256_SK");  // =0: no stream-K tail (A/B knob, read per call; tests run both)
   if (e && e[0] == '0') return p;
   int s = std::min(P / r, 4);
   while (s > 1 && (K % (64 * s) != 0 || K / s < 512)) --s;
-  // a grid below one wave takes the tail only if the splits then fill most of the chip (a few tiles of a tall-K
-  // product need far more than 4 splits: the split-K path / the 128 x 128 kernel take those)
-  if (waves == 0 && r * s < 192) s = 1;
   if (s > 1) {
     p.full = waves * P;
     p.sk = s;

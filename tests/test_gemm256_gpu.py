@@ -96,9 +96,9 @@ def test_gemm256_long_k(cuda):
 
 
 # stream-K tail (gemm256_plan): T = w * 256 + r tiles with r <= 128 run the last r tiles split sk ways along K with
-# the in-kernel fixed-order fix-up. (M, N, K) -> tiles, sk: 16x24 = 384 -> 2 (Llama QKV); 8x16 = 128 -> 2 (a single
-# partial wave); 16x21 = 336 -> 3; 16x20 = 320 -> 4; ragged edges on a 2-split tail.
-SK_SHAPES = [(4096, 6144, 4096), (2048, 4096, 2048), (4096, 5376, 3072), (4096, 5120, 4096), (4000, 6136, 2048)]
+# the in-kernel fixed-order fix-up. (M, N, K) -> tiles, sk: 16x24 = 384 -> 2 (Llama QKV); 16x18 = 288 -> 4 at
+# K = 2048; 16x21 = 336 -> 3; 16x20 = 320 -> 4; ragged edges on a 2-split tail. Sub-wave grids take no tail.
+SK_SHAPES = [(4096, 6144, 4096), (4096, 4608, 2048), (4096, 5376, 3072), (4096, 5120, 4096), (4000, 6136, 2048)]
 
 
 def _sk_env(monkeypatch, on):
