@@ -527,6 +527,187 @@ static void launch_ring(const AS& a, const BS& b, const Epi& e, int M, int N, in
 
 }  // namespace g256
 
+// ============================================================================ 4-wave NT kernel
+// The forward (both operands K-major) form of a plain bf16 product, on the schedule hipBLASLt's MT256x256x64 kernel
+// uses on gfx950 (its disassembly: 4 waves, 128 MFMAs + 32 ds_read_b128 + 16 LDS-DMA per 64-deep stage, 2 stages,
+// accumulators in AGPRs): the ring kernel above reaches 0.78-0.85x hipBLASLt on this form only
+// (profiles/r04_gemm_all_vs_hipblaslt.jsonl) with 2x its L2 requests -- its 32-deep stages read half cache lines
+// of a K-major row per DMA piece.
+//  * 256 threads = 4 waves as 2 x 2, each wave a 128 x 128 piece = 8 x 8 tiles of v_mfma_f32_16x16x32_bf16: 0.25
+//    LDS reads per MFMA (the 8-wave ring: 0.375). The 64 accumulators live in AGPRs: the MFMAs are inline asm with
+//    "+a" operands (the builtin's register choice moved the 256 accumulator registers between AGPRs and VGPRs every
+//    phase in a first 4-wave version, 0.97 vs 1.25 PF/s).
+//  * 64-deep stages (A 256 x 64 + B 256 x 64 = 64 KB), 2 in LDS; a row's 64 k are one 128-B line, read by 8 lanes of
+//    one DMA instruction. Stage s + 2 is issued right after the barrier in the middle of stage s, a whole stage
+//    (128 MFMAs per wave, one wave per SIMD) ahead of its wait.
+//  * fragments double-buffered in VGPRs: the k-half read while the other half's 64 MFMAs run.
+//  * LDS images [256 rows][64 k], 128-B rows, 16-B chunk c of row r at c ^ (r & 6): conflict-free ds_read_b128 for
+//    16-row fragment groups (the conv3x3 swizzle); a lane's row & 6 is lane & 6, so every fragment address is one
+//    of two per-lane bases plus an immediate.
+namespace g4 {
+constexpr int THREADS = 256, KS = 64;
+constexpr int STAGE_A = 256 * KS * 2;  // 32 KB
+constexpr int STAGE = 2 * STAGE_A;     // 64 KB
+constexpr int LDS_BYTES = 2 * STAGE;   // 128 KB
+
+#define K8S_G4_MFMA(acc, b, a) \
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a))
+
+__global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __restrict__ A, long lda,
+                                                             const uint16_t* __restrict__ B, long ldb,
+                                                             uint16_t* __restrict__ C, long ldc, int M, int N, int K,
+                                                             float alpha) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+
+  const int tiles_m = M >> 8, tiles_n = N >> 8;
+  const int wg = g256r::xcd_remap(blockIdx.x, gridDim.x);
+  const int group = 8 * tiles_n;
+  const int first_m = (wg / group) * 8;
+  const int gm = min(tiles_m - first_m, 8);
+  const int m0 = (first_m + (wg % group) % gm) * 256, n0 = ((wg % group) / gm) * 256;
+
+  // DMA (buffer_load ... lds: the per-instruction row offset in an SGPR, no per-lane address arithmetic):
+  // instruction q = wid + 4 i of an operand's stage covers rows 8 q .. 8 q + 7 (1 KB of LDS); lane l loads row
+  // 8 q + l / 8, logical chunk (l & 7) ^ (row & 6) = (l & 7) ^ ((l >> 3) & 6)
+  const int drow = wid * 8 + (lane >> 3), lch = (lane & 7) ^ ((lane >> 3) & 6);
+  const __amdgpu_buffer_rsrc_t rsa =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)m0 * lda), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)n0 * ldb), (short)0, 0x7fffffff, 0x00020000);
+  const int va = (drow * (int)lda + lch * 8) * 2, vb = (drow * (int)ldb + lch * 8) * 2;
+  const int sa = 64 * (int)lda, sb = 64 * (int)ldb;  // bytes between instruction i and i + 1 (32 rows)
+  // piece p (0-7: A instruction p, 8-15: B instruction p - 8) of stage t into buffer dbuf
+  auto dma = [&](int p, int t, int dbuf) {
+    char* d = smem + dbuf * STAGE + wid * 1024 + (p & 7) * 4096 + (p >> 3) * STAGE_A;
+    auto* l = (__attribute__((address_space(3))) void*)d;
+    if (p < 8) __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, l, 16, va, p * sa + t * (KS * 2), 0, 0);
+    else __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, l, 16, vb, (p - 8) * sb + t * (KS * 2), 0, 0);
+  };
+  // fragment f of the wave's A piece: row wr * 128 + 16 f + (lane & 15), chunk 4 kk + (lane >> 4)
+  const int li = lane & 15, g = lane >> 4, sw = lane & 6;
+  const int ra = (wr * 128 + li) * 128, rb = STAGE_A + (wc * 128 + li) * 128;
+  const int co0 = (g ^ sw) << 4, co1 = ((4 + g) ^ sw) << 4;
+  auto frag = [&](int buf, int kk, int off) {
+    return __builtin_bit_cast(
+        mfma_bf16x8, *reinterpret_cast<const bf16x8_t*>(smem + buf * STAGE + (kk ? co1 : co0) + off));
+  };
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int f = 0; f < 8; ++f)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[f][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // MFMAs [lo, hi) of the 64 on (af, bf), one other instruction after every second MFMA (the interleave of
+  // hipBLASLt's loop): op slot k < 16 reads the next k-half's fragment k (A k/2 or B k/2) into (na, nb) when `rd`;
+  // slot k >= 16 issues DMA piece k - 16 of stage `dt` into buffer `dbuf` when `dm`. rd_c / dm_c are
+  // std::integral_constant<bool, ...>, so the sequence carries no branches.
+  auto mm = [&](int lo, int hi, const mfma_bf16x8 (&af)[8], const mfma_bf16x8 (&bf)[8], mfma_bf16x8 (&na)[8],
+                mfma_bf16x8 (&nb)[8], auto rd_c, int nbuf, int nkk, auto dm_c, int dt, int dbuf) {
+    constexpr bool rd = decltype(rd_c)::value, dm = decltype(dm_c)::value;
+#pragma unroll
+    for (int x = lo; x < hi; ++x) {
+      K8S_G4_MFMA(acc[x >> 3][x & 7], bf[x & 7], af[x >> 3]);
+      if (x & 1) {
+        const int k = x >> 1;
+        if constexpr (rd) {
+          if (k < 16) {
+            if (k & 1) nb[k >> 1] = frag(nbuf, nkk, rb + (k >> 1) * 2048);
+            else na[k >> 1] = frag(nbuf, nkk, ra + (k >> 1) * 2048);
+          }
+        }
+        if constexpr (dm) {
+          if (k >= 16) dma(k - 16, dt, dbuf);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+
+  const int nst = K / KS;
+#pragma unroll
+  for (int p = 0; p < 16; ++p) dma(p, 0, 0);
+  if (nst > 1) {
+#pragma unroll
+    for (int p = 0; p < 16; ++p) dma(p, 1, 1);
+    g256::vmwait<16>();  // stage 0 landed, stage 1 in flight
+  } else {
+    g256::vmwait<0>();
+  }
+  g256::barrier();
+  mfma_bf16x8 a0[8], b0[8], a1[8], b1[8];
+#pragma unroll
+  for (int f = 0; f < 8; ++f) {
+    a0[f] = frag(0, 0, ra + f * 2048);
+    b0[f] = frag(0, 0, rb + f * 2048);
+  }
+  // first k-half of stage s (+ its second half's reads), the stage's hand-over -- stage s + 1 landed and visible,
+  // every wave done with stage s's buffer -- with the last two MFMAs of the half around it
+  auto first = [&](int s) {
+    mm(0, 62, a0, b0, a1, b1, T_{}, s & 1, 1, F_{}, 0, 0);
+    g256::vmwait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mm(62, 63, a0, b0, a1, b1, F_{}, 0, 0, F_{}, 0, 0);
+    g256::barrier();
+    mm(63, 64, a0, b0, a1, b1, F_{}, 0, 0, F_{}, 0, 0);
+  };
+  int s = 0;
+  for (; s + 2 < nst; ++s) {
+    first(s);
+    mm(0, 64, a1, b1, a0, b0, T_{}, (s & 1) ^ 1, 0, T_{}, s + 2, s & 1);  // + stage s + 1's reads, stage s + 2's DMA
+  }
+  if (s + 1 < nst) {  // stage nst - 2: no DMA left
+    first(s);
+    mm(0, 64, a1, b1, a0, b0, T_{}, (s & 1) ^ 1, 0, F_{}, 0, 0);
+    ++s;
+  }
+  mm(0, 64, a0, b0, a1, b1, T_{}, s & 1, 1, F_{}, 0, 0);  // the last stage
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  mm(0, 64, a1, b1, a0, b0, F_{}, 0, 0, F_{}, 0, 0);
+
+  // epilogue: each wave stages its 128 x 128 bf16 piece (32 KB, wave-private; 256-B rows, 16-B chunk c of row r at
+  // c ^ (r & 15)) and stores whole 16-B row segments
+  g256::barrier();  // every wave is past its last fragment read
+  char* stg = smem + wid * 32768;
+#pragma unroll
+  for (int f = 0; f < 8; ++f) {
+    const int lr = f * 16 + li;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int lc = j * 16 + 4 * g;
+      bf16x4_t o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(acc[f][j][r] * alpha);
+      *reinterpret_cast<bf16x4_t*>(stg + lr * 256 + (((lc >> 3) ^ (lr & 15)) << 4) + (lc & 4) * 2) = o;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private region: no barrier needed
+#pragma unroll 4
+  for (int it = 0; it < 32; ++it) {
+    const int idx = it * 64 + lane, lr = idx >> 4, ch = idx & 15;
+    const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(stg + lr * 256 + ((ch ^ (lr & 15)) << 4));
+    *reinterpret_cast<bf16x8_t*>(C + (long)(m0 + wr * 128 + lr) * ldc + n0 + wc * 128 + ch * 8) = v;
+  }
+}
+#undef K8S_G4_MFMA
+}  // namespace g4
+
+// The 4-wave NT kernel's contract: both operands K-major, whole 256 x 256 tiles (M, N % 256), K % 64, 16-B aligned
+// rows, a plain bf16 output (no bias / activation / pre-activation / accumulate, alpha allowed), no split and no
+// stream-K tail, and at least one wave of tiles. $K8S_AMD_GEMM_W4=0 keeps such products on the ring kernel (A/B;
+// read per call, both sides tested).
+static bool w4_ok(bool a_kmajor, bool b_kmajor, bool c_f32, int M, int N, int K, long lda, long ldb, long ldc,
+                  const float* bias, int act, const uint16_t* pre, bool accumulate, int splits, int sk) {
+  const char* e = getenv("K8S_AMD_GEMM_W4");
+  if (e && e[0] == '0') return false;
+  return a_kmajor && b_kmajor && !c_f32 && !bias && act == 0 && !pre && !accumulate && splits == 1 && sk == 1 &&
+         M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && (lda | ldb | ldc) % 8 == 0 && (M / 256) * (N / 256) >= 256;
+}
+
 // Stream-K tail plan for a grid of 256 x 256 tiles on 256 CUs (one block per CU): with T = w * 256 + r tiles and
 // 0 < r <= 128, the last r tiles are split sk = min(256 / r, 4) ways along K (each split a multiple of 64 deep and
 // >= 512), so the tail costs ~1/sk of a wave (+ the fix-up) instead of a whole one. Not for grids of 8+ waves (the
@@ -606,6 +787,11 @@ void launch_gemm256(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* 
   Gemm256Plan plan = gemm256_plan(M, N, K);
   if (splits > 1 || !sk_slabs || !sk_sync) plan.sk = 1;  // tall-K split, or no stream-K workspace given
   using namespace g256r;
+  if (w4_ok(a_kmajor, b_kmajor, c_f32, M, N, K, lda, ldb, ldc, bias, act, pre, accumulate, splits, plan.sk)) {
+    hipLaunchKernelGGL(g4::gemm_w4_kernel, dim3((M / 256) * (N / 256)), dim3(g4::THREADS), 0, st, A, lda, B, ldb,
+                       reinterpret_cast<uint16_t*>(C), ldc, M, N, K, alpha);
+    return;
+  }
   if (a_kmajor && b_kmajor)
     g256::launch_ring(KMaj{A, lda, M}, KMaj{B, ldb, N}, e, M, N, K, splits, plan, sk_slabs, sk_sync, st);
   else if (a_kmajor && !b_kmajor)

@@ -1,9 +1,17 @@
 #!/bin/bash
-# GPU job (round 4): 4-wave (one wave per SIMD, 128 x 128 per wave) NT GEMM vs the 8-wave ring vs hipBLASLt.
+# GPU job (round 4): 4-wave AGPR NT GEMM -- tests vs fp32, then the transformer products against hipBLASLt.
 set -o pipefail
-export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gemm256_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r4_w4_tests.log 2>&1 || { tail -40 gpurun_out/r4_w4_tests.log; exit 1; }
-tail -2 gpurun_out/r4_w4_tests.log
-timeout -k 10 400 python -u scripts/bench_gemm256.py --rounds 3 --only llama --forms fwd --variants K8S_AMD_G256_W4=0 > gpurun_out/r4_w4_llama.jsonl 2> gpurun_out/r4_w4_llama.err || { tail -30 gpurun_out/r4_w4_llama.err; exit 1; }
-cut -c1-260 gpurun_out/r4_w4_llama.jsonl
+timeout -k 10 300 python -u -m pytest tests/test_gemm256_gpu.py -x -q --timeout 120 --timeout-method thread -k "w4 or stream_k" > gpurun_out/r4_w4b_tests.log 2>&1 || { tail -30 gpurun_out/r4_w4b_tests.log; exit 1; }
+tail -1 gpurun_out/r4_w4b_tests.log
+timeout -k 10 400 python -u scripts/bench_gemm256.py --rounds 5 --only llama > gpurun_out/r4_w4b.jsonl 2> gpurun_out/r4_w4b.err || { tail -30 gpurun_out/r4_w4b.err; exit 1; }
+K8S_AMD_GEMM_W4=0 timeout -k 10 400 python -u scripts/bench_gemm256.py --rounds 5 --only square > gpurun_out/r4_w4b_sq0.jsonl 2>> gpurun_out/r4_w4b.err || { tail -30 gpurun_out/r4_w4b.err; exit 1; }
+timeout -k 10 400 python -u scripts/bench_gemm256.py --rounds 5 --only square > gpurun_out/r4_w4b_sq1.jsonl 2>> gpurun_out/r4_w4b.err || { tail -30 gpurun_out/r4_w4b.err; exit 1; }
+python3 - <<'PY'
+import json
+for fn in ["gpurun_out/r4_w4b.jsonl", "gpurun_out/r4_w4b_sq0.jsonl", "gpurun_out/r4_w4b_sq1.jsonl"]:
+    print(fn)
+    for l in open(fn):
+        r = json.loads(l)
+        print("%-6s %-8s %-6s %6.1f us ours %5d TF  blas %5d TF  x%.3f" % (r["group"], r["layer"], r["form"], r["ours_us"], r["ours_tf"], r["blas_tf"], r["speedup"]))
+PY
