@@ -336,13 +336,13 @@ struct SkArgs {
 // splits own + other (IEEE addition commutes: bit-identical whoever arrives last), for more splits every split's
 // slab in split order (the reducer writes its own too) -- then resets the ticket and flags for the next launch and
 // runs the normal epilogue. Returns true in the reducer (which goes on to the epilogue).
-template <int NJ = 4, int NT = 512>
+template <int NJ = 4, int NT = 512, int LDS = LDS_BYTES>
 __device__ __forceinline__ bool sk_fixup(f32x4_t (&acc)[8][NJ], const SkArgs& SK, int slot, int split, char* smem,
                                       int tid) {
   const int sk = SK.sk;
   int* cnt = SK.sync + (long)slot * (1 + sk);
   int* flg = cnt + 1;
-  int* bcast = reinterpret_cast<int*>(smem + g256r::LDS_BYTES - 16);  // the K loop's reads are all done
+  int* bcast = reinterpret_cast<int*>(smem + LDS - 16);  // the K loop's reads are all done
   __syncthreads();
   if (tid == 0) bcast[0] = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
@@ -556,14 +556,26 @@ constexpr int LDS_BYTES = 2 * STAGE;   // 128 KB
 __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __restrict__ A, long lda,
                                                              const uint16_t* __restrict__ B, long ldb,
                                                              uint16_t* __restrict__ C, long ldc, int M, int N, int K,
-                                                             float alpha) {
+                                                             float alpha, int kps, g256r::SkArgs SK) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 1, wc = wid & 1;
 
   const int tiles_m = M >> 8, tiles_n = N >> 8;
-  const int wg = g256r::xcd_remap(blockIdx.x, gridDim.x);
+  // whole tiles [0, SK.full), then the stream-K tail: (tile, split) pairs of K range kps (as gemm256r_kernel)
+  const int bid = blockIdx.x;
+  int wg, split = 0, sk_slot = -1;
+  if (bid < SK.full) {
+    wg = g256r::xcd_remap(bid, SK.full);
+    kps = K;
+  } else {
+    const int j = g256r::xcd_remap(bid - SK.full, gridDim.x - SK.full);
+    sk_slot = j / SK.sk;
+    split = j - sk_slot * SK.sk;
+    wg = SK.full + sk_slot;
+  }
+  const long koff = (long)split * kps;
   const int group = 8 * tiles_n;
   const int first_m = (wg / group) * 8;
   const int gm = min(tiles_m - first_m, 8);
@@ -574,9 +586,9 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
   // 8 q + l / 8, logical chunk (l & 7) ^ (row & 6) = (l & 7) ^ ((l >> 3) & 6)
   const int drow = wid * 8 + (lane >> 3), lch = (lane & 7) ^ ((lane >> 3) & 6);
   const __amdgpu_buffer_rsrc_t rsa =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)m0 * lda), (short)0, 0x7fffffff, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)m0 * lda + koff), (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsb =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)n0 * ldb), (short)0, 0x7fffffff, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)n0 * ldb + koff), (short)0, 0x7fffffff, 0x00020000);
   const int va = (drow * (int)lda + lch * 8) * 2, vb = (drow * (int)ldb + lch * 8) * 2;
   const int sa = 64 * (int)lda, sb = 64 * (int)ldb;  // bytes between instruction i and i + 1 (32 rows)
   // piece p (0-7: A instruction p, 8-15: B instruction p - 8) of stage t into buffer dbuf
@@ -629,7 +641,7 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
   using T_ = std::true_type;
   using F_ = std::false_type;
 
-  const int nst = K / KS;
+  const int nst = kps / KS;
 #pragma unroll
   for (int p = 0; p < 16; ++p) dma(p, 0, 0);
   if (nst > 1) {
@@ -670,6 +682,43 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   mm(0, 64, a1, b1, a0, b0, F_{}, 0, 0, F_{}, 0, 0);
 
+  // stream-K tail: every split stores its fp32 partial (fragment-native order, the slab layout of sk_fixup), takes a
+  // ticket and publishes; the last arriver sums the tile's slabs in split order inside the epilogue -- fixed order,
+  // so bit-identical whoever arrives last. The accumulators are only read here (updating them in place would pull
+  // all 256 out of the AGPRs).
+  const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+      SK.slabs + (long)(sk_slot < 0 ? 0 : sk_slot) * SK.sk * 65536, (short)0, SK.sk * 262144, 0x00020000);
+  if (sk_slot >= 0) {
+    const int sk = SK.sk;
+    int* cnt = SK.sync + (long)sk_slot * (1 + sk);
+    int* flg = cnt + 1;
+    int* bcast = reinterpret_cast<int*>(smem + LDS_BYTES - 16);
+#pragma unroll
+    for (int f = 0; f < 8; ++f)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(acc[f][j], srs, tid * 16, split * 262144 + (f * 8 + j) * THREADS * 16,
+                                               0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // also: every wave is past its last fragment read (bcast lives in the stage buffers)
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(flg + split, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      bcast[0] = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (bcast[0] != sk - 1) return;
+    if (tid == 0) {  // the others published before taking their tickets
+      for (int z = 0; z < sk; ++z)
+        while (__hip_atomic_load(flg + z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reset for the next launch
+      for (int z = 0; z < sk; ++z) __hip_atomic_store(flg + z, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+  }
   // epilogue: each wave stages its 128 x 128 bf16 piece (32 KB, wave-private; 256-B rows, 16-B chunk c of row r at
   // c ^ (r & 15)) and stores whole 16-B row segments
   g256::barrier();  // every wave is past its last fragment read
@@ -680,9 +729,15 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int lc = j * 16 + 4 * g;
+      f32x4_t v = acc[f][j];
+      if (sk_slot >= 0) {
+        v = __builtin_amdgcn_raw_buffer_load_b128(srs, tid * 16, (f * 8 + j) * THREADS * 16, 0);
+        for (int z = 1; z < SK.sk; ++z)
+          v += __builtin_amdgcn_raw_buffer_load_b128(srs, tid * 16, z * 262144 + (f * 8 + j) * THREADS * 16, 0);
+      }
       bf16x4_t o;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(acc[f][j][r] * alpha);
+      for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r] * alpha);
       *reinterpret_cast<bf16x4_t*>(stg + lr * 256 + (((lc >> 3) ^ (lr & 15)) << 4) + (lc & 4) * 2) = o;
     }
   }
@@ -698,14 +753,15 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
 }  // namespace g4
 
 // The 4-wave NT kernel's contract: both operands K-major, whole 256 x 256 tiles (M, N % 256), K % 64, 16-B aligned
-// rows, a plain bf16 output (no bias / activation / pre-activation / accumulate, alpha allowed), no split and no
-// stream-K tail, and at least one wave of tiles. $K8S_AMD_GEMM_W4=0 keeps such products on the ring kernel (A/B;
+// rows, a plain bf16 output (no bias / activation / pre-activation / accumulate, alpha allowed), no tall-K split, and
+// at least one wave of tiles (a partial last wave takes the stream-K tail). $K8S_AMD_GEMM_W4=0 keeps such products on the ring kernel (A/B;
 // read per call, both sides tested).
 static bool w4_ok(bool a_kmajor, bool b_kmajor, bool c_f32, int M, int N, int K, long lda, long ldb, long ldc,
                   const float* bias, int act, const uint16_t* pre, bool accumulate, int splits, int sk) {
   const char* e = getenv("K8S_AMD_GEMM_W4");
   if (e && e[0] == '0') return false;
-  return a_kmajor && b_kmajor && !c_f32 && !bias && act == 0 && !pre && !accumulate && splits == 1 && sk == 1 &&
+  (void)sk;
+  return a_kmajor && b_kmajor && !c_f32 && !bias && act == 0 && !pre && !accumulate && splits == 1 &&
          M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && (lda | ldb | ldc) % 8 == 0 && (M / 256) * (N / 256) >= 256;
 }
 
@@ -789,8 +845,16 @@ void launch_gemm256(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* 
   if (splits > 1 || !sk_slabs || !sk_sync) plan.sk = 1;  // tall-K split, or no stream-K workspace given
   using namespace g256r;
   if (w4_ok(a_kmajor, b_kmajor, c_f32, M, N, K, lda, ldb, ldc, bias, act, pre, accumulate, splits, plan.sk)) {
-    hipLaunchKernelGGL(g4::gemm_w4_kernel, dim3((M / 256) * (N / 256)), dim3(g4::THREADS), 0, st, A, lda, B, ldb,
-                       reinterpret_cast<uint16_t*>(C), ldc, M, N, K, alpha);
+    const int tiles = (M / 256) * (N / 256);
+    g256r::SkArgs sk{tiles, 1, nullptr, nullptr};
+    int blocks = tiles, kps = K;
+    if (plan.sk > 1) {  // the stream-K tail (gemm256_plan), fixed up in-kernel as in the ring kernel
+      sk = g256r::SkArgs{plan.full, plan.sk, sk_slabs, sk_sync};
+      kps = plan.kps;
+      blocks = plan.full + (tiles - plan.full) * plan.sk;
+    }
+    hipLaunchKernelGGL(g4::gemm_w4_kernel, dim3(blocks), dim3(g4::THREADS), 0, st, A, lda, B, ldb,
+                       reinterpret_cast<uint16_t*>(C), ldc, M, N, K, alpha, kps, sk);
     return;
   }
   if (a_kmajor && b_kmajor)

@@ -121,8 +121,10 @@ def test_gemm256_stream_k_tail_matches_fp32(cuda, monkeypatch, M, N, K, ak, bk):
     assert _rel(c, ref) < 1e-4
     for _ in range(3):
         assert torch.equal(_C().gemm(A, ak, B, bk, None, True, None, 0, None, False, 1.0, 1), c)
-    cb = _C().gemm(A, ak, B, bk, None, False, None, 0, None, False, 1.0, 1)
+    cb = _C().gemm(A, ak, B, bk, None, False, None, 0, None, False, 1.0, 1)  # bf16: the 4-wave kernel's tail (NT)
     assert _rel(cb, ref) < 1e-2
+    for _ in range(3):
+        assert torch.equal(_C().gemm(A, ak, B, bk, None, False, None, 0, None, False, 1.0, 1), cb)
     _sk_env(monkeypatch, False)  # the whole-tile path agrees to fp32 rounding
     c0 = _C().gemm(A, ak, B, bk, None, True, None, 0, None, False, 1.0, 1)
     assert _rel(c0, c) < 1e-5
@@ -158,6 +160,8 @@ def test_gemm256_stream_k_sync_words_reset(cuda, monkeypatch):
         b = torch.randn(N, K, device=cuda).bfloat16()
         c = _C().gemm(a, True, b, True, None, True, None, 0, None, False, 1.0, 1)
         assert _rel(c, a.float() @ b.float().t()) < 1e-4, (M, N, K)
+        cb = _C().gemm(a, True, b, True, None, False, None, 0, None, False, 1.0, 1)  # 4-wave kernel's sync words
+        assert _rel(cb, a.float() @ b.float().t()) < 1e-2, (M, N, K)
 
 
 @pytest.mark.parametrize("M", [4, 12, 1000])
