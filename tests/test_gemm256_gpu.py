@@ -206,22 +206,24 @@ def test_gemm256_mode_switch_sides(cuda, monkeypatch, mode):
         assert _rel(c, ref) < 1e-4, (ak, bk)
 
 
-# 4-wave NT kernel (gemm256.hip g4): K-major x K-major, whole 256 tiles, plain bf16 output, >= 256 tiles. K = 64 / 128 /
-# 192 run the one-, two- and three-stage paths of its peeled K loop.
+# 4-wave kernel (gemm256.hip g4): A K-major, B K-major or MN-major, whole 256 tiles, plain bf16 output, >= 256 tiles.
+# K = 64 / 128 / 192 run the one-, two- and three-stage paths of its peeled K loop.
 W4_SHAPES = [(4096, 4096, 64), (4096, 4096, 128), (4096, 4096, 192), (2048, 8192, 4096), (8192, 4096, 640)]
 
 
+@pytest.mark.parametrize("bk", [True, False])  # B K-major (forward) / MN-major (data gradient)
 @pytest.mark.parametrize("M,N,K", W4_SHAPES)
-def test_gemm_w4_nt_matches_fp32(cuda, monkeypatch, M, N, K):
+def test_gemm_w4_matches_fp32(cuda, monkeypatch, M, N, K, bk):
     torch.manual_seed(6)
     a = torch.randn(M, K, device=cuda).bfloat16()
     b = torch.randn(N, K, device=cuda).bfloat16()
     ref = a.float() @ b.float().t()
+    B = b if bk else b.t().contiguous()
     monkeypatch.setenv("K8S_AMD_GEMM_W4", "1")
-    y = _C().gemm(a, True, b, True, None, False, None, 0, None, False, 1.0, 1)
+    y = _C().gemm(a, True, B, bk, None, False, None, 0, None, False, 1.0, 1)
     assert _rel(y, ref) < 1e-2
-    y2 = _C().gemm(a, True, b, True, None, False, None, 0, None, False, 0.5, 1)  # alpha
+    y2 = _C().gemm(a, True, B, bk, None, False, None, 0, None, False, 0.5, 1)  # alpha
     assert _rel(y2, 0.5 * ref) < 1e-2
     monkeypatch.setenv("K8S_AMD_GEMM_W4", "0")  # the ring kernel: the same product to bf16 rounding
-    y0 = _C().gemm(a, True, b, True, None, False, None, 0, None, False, 1.0, 1)
+    y0 = _C().gemm(a, True, B, bk, None, False, None, 0, None, False, 1.0, 1)
     assert _rel(y, y0) < 1e-2
