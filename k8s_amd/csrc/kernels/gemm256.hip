@@ -528,8 +528,9 @@ static void launch_ring(const AS& a, const BS& b, const Epi& e, int M, int N, in
 }  // namespace g256
 
 // ============================================================================ 4-wave kernel
-// The forward (both operands K-major) and data-gradient (B MN-major, read by ds_read_b64_tr_b16 from the ring
-// kernel's MNMaj image) forms of a plain bf16 product, on the schedule hipBLASLt's MT256x256x64 kernel
+// Every operand layout (K-major rows, or MN-major through the ring kernel's MNMaj sub-images and ds_read_b64_tr_b16)
+// with a plain bf16 or fp32 (stored / accumulated) output -- the forward, data-gradient and weight-gradient products
+// of the transformer linears whose grids fill the chip -- on the schedule hipBLASLt's MT256x256x64 kernel
 // uses on gfx950 (its disassembly: 4 waves, 128 MFMAs + 32 ds_read_b128 + 16 LDS-DMA per 64-deep stage, 2 stages,
 // accumulators in AGPRs): the ring kernel above reaches 0.78-0.85x hipBLASLt on this form only
 // (profiles/r04_gemm_all_vs_hipblaslt.jsonl) with 2x its L2 requests -- its 32-deep stages read half cache lines
@@ -554,11 +555,11 @@ constexpr int LDS_BYTES = 2 * STAGE;   // 128 KB
 #define K8S_G4_MFMA(acc, b, a) \
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a))
 
-template <bool BMN>
+template <bool AMN, bool BMN>
 __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __restrict__ A, long lda,
-                                                             const uint16_t* __restrict__ B, long ldb,
-                                                             uint16_t* __restrict__ C, long ldc, int M, int N, int K,
-                                                             float alpha, int kps, g256r::SkArgs SK) {
+                                                             const uint16_t* __restrict__ B, long ldb, void* Cv,
+                                                             long ldc, int M, int N, int K, float alpha, int kps,
+                                                             g256r::SkArgs SK, int out_f32, int accumulate) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -587,11 +588,12 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
   // instruction q = wid + 4 i of an operand's stage covers rows 8 q .. 8 q + 7 (1 KB of LDS); lane l loads row
   // 8 q + l / 8, logical chunk (l & 7) ^ (row & 6) = (l & 7) ^ ((l >> 3) & 6)
   const int drow = wid * 8 + (lane >> 3), lch = (lane & 7) ^ ((lane >> 3) & 6);
-  const __amdgpu_buffer_rsrc_t rsa =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)m0 * lda + koff), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(AMN ? A + koff * lda + m0 : A + (long)m0 * lda + koff), (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(BMN ? B + koff * ldb + n0 : B + (long)n0 * ldb + koff), (short)0, 0x7fffffff, 0x00020000);
-  const int va = (drow * (int)lda + lch * 8) * 2;
+  const int va = AMN ? ((drow * (int)lda) + (((lane & 7) ^ g256::mn128_swz(drow)) * 8)) * 2
+                     : (drow * (int)lda + lch * 8) * 2;
   // B MN-major ([K][N], the data gradient's weight): the stage is 8 sub-images [32 k][64 n] (k-half p >> 2, column
   // block p & 3) of 128-B rows, 16-B unit u of k-row r at u ^ h(r) (the ring kernel's MNMaj image, read by
   // ds_read_b64_tr_b16). Piece p of wave w is sub-image p's k-rows 8 w .. 8 w + 7: lane l loads k-row 8 w + l / 8,
@@ -604,7 +606,11 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
     char* d = smem + dbuf * STAGE + wid * 1024 + (p & 7) * 4096 + (p >> 3) * STAGE_A;
     auto* l = (__attribute__((address_space(3))) void*)d;
     if (p < 8) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, l, 16, va, p * sa + t * (KS * 2), 0, 0);
+      if constexpr (AMN)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, l, 16, va, ((p >> 2) * 32 * (int)lda + (p & 3) * 64) * 2 +
+                                                                     t * (KS * 2) * (int)lda, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, l, 16, va, p * sa + t * (KS * 2), 0, 0);
     } else if constexpr (BMN) {
       const int q = p - 8;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, l, 16, vb, ((q >> 2) * 32 * (int)ldb + (q & 3) * 64) * 2 +
@@ -615,16 +621,18 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
   };
   // B MN-major fragment j of k-half kk (ring kernel's MNMaj::load): two transposed reads at k-rows r0 = 8 g + q_
   // and r0 + 4 of sub-image (2 wc + j / 4), unit 2 (j & 3) + pp / 2; the per-lane parts precomputed for j & 3
-  int bmo[2][4];
+  int bmo[2][4], amo[2][4];  // (A MN-major: the same with the wave's rows, sub-image 2 wr + f / 4)
   {
     const int li_ = lane & 15, q_ = li_ >> 2, pp = li_ & 3, r0 = 8 * (lane >> 4) + q_;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int r = r0 + 4 * h;
 #pragma unroll
-      for (int j4 = 0; j4 < 4; ++j4)
-        bmo[h][j4] = STAGE_A + wc * 2 * 4096 + r * 128 + (((2 * j4 + (pp >> 1)) ^ g256::mn128_swz(r)) << 4) +
-                     (pp & 1) * 8;
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const int u = (((2 * j4 + (pp >> 1)) ^ g256::mn128_swz(r)) << 4) + (pp & 1) * 8 + r * 128;
+        bmo[h][j4] = STAGE_A + wc * 2 * 4096 + u;
+        amo[h][j4] = wr * 2 * 4096 + u;
+      }
     }
   }
   // fragment f of the wave's A piece: row wr * 128 + 16 f + (lane & 15), chunk 4 kk + (lane >> 4)
@@ -648,7 +656,14 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
   // 5-7 % faster than packed one per two MFMAs into the half's second quarter (gate_up 730 -> 677 us, same box;
   // moving the A pieces into the first halves measured slower again, 691 -> 722). rd_c / dm_c are
   // std::integral_constant<bool, ...>, so the sequence carries no branches.
-  short4_t blo[8], bhi[8];  // B MN-major: the next k-half's raw transposed reads (tied and joined after a wait)
+  short4_t blo[8], bhi[8], alo[8], ahi[8];  // MN-major operands: the next k-half's raw transposed reads (tied and
+                                           // joined after a wait)
+  auto tra = [&](int nbuf, int nkk, int f, int h) {
+    tr16_asm(h ? ahi[f] : alo[f], smem + nbuf * STAGE + nkk * 16384 + (f >> 2) * 4096 + amo[h][f & 3]);
+  };
+  auto trb = [&](int nbuf, int nkk, int j, int h) {
+    tr16_asm(h ? bhi[j] : blo[j], smem + nbuf * STAGE + nkk * 16384 + (j >> 2) * 4096 + bmo[h][j & 3]);
+  };
   auto mm = [&](int lo, int hi, const mfma_bf16x8 (&af)[8], const mfma_bf16x8 (&bf)[8], mfma_bf16x8 (&na)[8],
                 mfma_bf16x8 (&nb)[8], auto rd_c, int nbuf, int nkk, auto dm_c, int dt, int dbuf) {
     constexpr bool rd = decltype(rd_c)::value, dm = decltype(dm_c)::value;
@@ -657,13 +672,17 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
       K8S_G4_MFMA(acc[x >> 3][x & 7], bf[x & 7], af[x >> 3]);
       const int k = x >> 2;
       if constexpr (rd) {
-        if constexpr (BMN) {  // 16 transposed B reads after the odd MFMAs of the first half, 8 A reads after
-          if ((x & 1) && x < 32) {
-            const int jj = x >> 2, h = (x >> 1) & 1;
-            const char* ad = smem + nbuf * STAGE + nkk * 16384 + (jj >> 2) * 4096 + bmo[h][jj & 3];
-            tr16_asm(h ? bhi[jj] : blo[jj], ad);
+        if constexpr (AMN && BMN) {  // 32 transposed reads, one after each MFMA of the first half (A, then B)
+          if (x < 32) {
+            if (x < 16) tra(nbuf, nkk, x >> 1, x & 1);
+            else trb(nbuf, nkk, (x - 16) >> 1, x & 1);
           }
+        } else if constexpr (BMN) {  // 16 transposed B reads after the odd MFMAs of the first half, 8 A reads after
+          if ((x & 1) && x < 32) trb(nbuf, nkk, x >> 2, (x >> 1) & 1);
           if ((x & 3) == 1 && x >= 32) na[k - 8] = frag(nbuf, nkk, ra + (k - 8) * 2048);
+        } else if constexpr (AMN) {  // 16 transposed A reads after the odd MFMAs of the first half, 8 B reads after
+          if ((x & 1) && x < 32) tra(nbuf, nkk, x >> 2, (x >> 1) & 1);
+          if ((x & 3) == 1 && x >= 32) nb[k - 8] = frag(nbuf, nkk, rb + (k - 8) * 2048);
         } else if ((x & 3) == 1) {
           if (k < 8) nb[k] = frag(nbuf, nkk, rb + k * 2048);
           else na[k - 8] = frag(nbuf, nkk, ra + (k - 8) * 2048);
@@ -675,8 +694,14 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  // B MN-major: after an lgkmcnt(0) wait, make the raw transposed reads MFMA operands (tied to the wait)
-  auto bjoin = [&](mfma_bf16x8 (&nb)[8]) {
+  // MN-major operands: after an lgkmcnt(0) wait, make the raw transposed reads MFMA operands (tied to the wait)
+  auto joins = [&](mfma_bf16x8 (&na)[8], mfma_bf16x8 (&nb)[8]) {
+    if constexpr (AMN) {
+      K8S_LDS_TIE8("", alo[0], alo[1], alo[2], alo[3], alo[4], alo[5], alo[6], alo[7]);
+      K8S_LDS_TIE8("", ahi[0], ahi[1], ahi[2], ahi[3], ahi[4], ahi[5], ahi[6], ahi[7]);
+#pragma unroll
+      for (int f = 0; f < 8; ++f) na[f] = join8(alo[f], ahi[f]);
+    }
     if constexpr (BMN) {
       K8S_LDS_TIE8("", blo[0], blo[1], blo[2], blo[3], blo[4], blo[5], blo[6], blo[7]);
       K8S_LDS_TIE8("", bhi[0], bhi[1], bhi[2], bhi[3], bhi[4], bhi[5], bhi[6], bhi[7]);
@@ -701,17 +726,22 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
   mfma_bf16x8 a0[8], b0[8], a1[8], b1[8];
 #pragma unroll
   for (int f = 0; f < 8; ++f) {
-    a0[f] = frag(0, 0, ra + f * 2048);
+    if constexpr (AMN) {
+      tra(0, 0, f, 0);
+      tra(0, 0, f, 1);
+    } else {
+      a0[f] = frag(0, 0, ra + f * 2048);
+    }
     if constexpr (BMN) {
-      tr16_asm(blo[f], smem + (f >> 2) * 4096 + bmo[0][f & 3]);
-      tr16_asm(bhi[f], smem + (f >> 2) * 4096 + bmo[1][f & 3]);
+      trb(0, 0, f, 0);
+      trb(0, 0, f, 1);
     } else {
       b0[f] = frag(0, 0, rb + f * 2048);
     }
   }
-  if constexpr (BMN) {
+  if constexpr (AMN || BMN) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    bjoin(b0);
+    joins(a0, b0);
   }
   // first k-half of stage s (+ its second half's reads), the stage's hand-over -- stage s + 1 landed and visible,
   // every wave done with stage s's buffer -- with the last two MFMAs of the half around it
@@ -719,15 +749,15 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
     mm(0, 62, a0, b0, a1, b1, T_{}, s & 1, 1, F_{}, 0, 0);
     g256::vmwait<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    bjoin(b1);
+    joins(a1, b1);
     mm(62, 63, a0, b0, a1, b1, F_{}, 0, 0, F_{}, 0, 0);
     g256::barrier();
     mm(63, 64, a0, b0, a1, b1, F_{}, 0, 0, F_{}, 0, 0);
   };
-  auto second_done = [&]() {  // B MN-major: the next first half's fragments
-    if constexpr (BMN) {
+  auto second_done = [&]() {  // MN-major operands: the next first half's fragments
+    if constexpr (AMN || BMN) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      bjoin(b0);
+      joins(a0, b0);
     }
   };
   int s = 0;
@@ -744,7 +774,7 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
   }
   mm(0, 64, a0, b0, a1, b1, T_{}, s & 1, 1, F_{}, 0, 0);  // the last stage
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  bjoin(b1);
+  joins(a1, b1);
   mm(0, 64, a1, b1, a0, b0, F_{}, 0, 0, F_{}, 0, 0);
 
   // stream-K tail: every split stores its fp32 partial (fragment-native order, the slab layout of sk_fixup), takes a
@@ -784,6 +814,29 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
     }
     __syncthreads();
   }
+  if (out_f32) {  // fp32 (the weight gradients, stored or accumulated into the flat slots): straight from the
+                  // fragments, 16 B per lane (4 lanes = one 64-B row piece)
+    float* C = reinterpret_cast<float*>(Cv);
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      const long m = m0 + wr * 128 + f * 16 + li;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        f32x4_t v = acc[f][j];
+        if (sk_slot >= 0) {
+          v = __builtin_amdgcn_raw_buffer_load_b128(srs, tid * 16, (f * 8 + j) * THREADS * 16, 0);
+          for (int z = 1; z < SK.sk; ++z)
+            v += __builtin_amdgcn_raw_buffer_load_b128(srs, tid * 16, z * 262144 + (f * 8 + j) * THREADS * 16, 0);
+        }
+        v *= alpha;
+        f32x4_t* cp = reinterpret_cast<f32x4_t*>(C + m * ldc + n0 + wc * 128 + j * 16 + 4 * g);
+        if (accumulate) v += *cp;
+        *cp = v;
+      }
+    }
+    return;
+  }
+  uint16_t* C = reinterpret_cast<uint16_t*>(Cv);
   // epilogue: each wave stages its 128 x 128 bf16 piece (32 KB, wave-private; 256-B rows, 16-B chunk c of row r at
   // c ^ (r & 15)) and stores whole 16-B row segments
   g256::barrier();  // every wave is past its last fragment read
@@ -826,9 +879,10 @@ static bool w4_ok(bool a_kmajor, bool b_kmajor, bool c_f32, int M, int N, int K,
   const char* e = getenv("K8S_AMD_GEMM_W4");
   if (e && e[0] == '0') return false;
   (void)sk;
-  (void)b_kmajor;  // both B layouts: K-major (forward) and MN-major (data gradient)
-  return a_kmajor && !c_f32 && !bias && act == 0 && !pre && !accumulate && splits == 1 &&
-         M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && (lda | ldb | ldc) % 8 == 0 && (M / 256) * (N / 256) >= 256;
+  (void)a_kmajor;  // every operand layout: K-major (read as rows) or MN-major (transposed reads)
+  (void)b_kmajor;
+  return !bias && act == 0 && !pre && (!accumulate || c_f32) && splits == 1 && M % 256 == 0 && N % 256 == 0 &&
+         K % 64 == 0 && (lda | ldb | ldc) % 8 == 0 && (M / 256) * (N / 256) >= 256;
 }
 
 // Stream-K tail plan for a grid of 256 x 256 tiles on 256 CUs (one block per CU): with T = w * 256 + r tiles and
@@ -919,12 +973,14 @@ void launch_gemm256(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* 
       kps = plan.kps;
       blocks = plan.full + (tiles - plan.full) * plan.sk;
     }
-    if (b_kmajor)
-      hipLaunchKernelGGL(g4::gemm_w4_kernel<false>, dim3(blocks), dim3(g4::THREADS), 0, st, A, lda, B, ldb,
-                         reinterpret_cast<uint16_t*>(C), ldc, M, N, K, alpha, kps, sk);
-    else
-      hipLaunchKernelGGL(g4::gemm_w4_kernel<true>, dim3(blocks), dim3(g4::THREADS), 0, st, A, lda, B, ldb,
-                         reinterpret_cast<uint16_t*>(C), ldc, M, N, K, alpha, kps, sk);
+#define K8S_W4L(AM, BM)                                                                                     \
+  hipLaunchKernelGGL((g4::gemm_w4_kernel<AM, BM>), dim3(blocks), dim3(g4::THREADS), 0, st, A, lda, B, ldb, C, ldc, \
+                     M, N, K, alpha, kps, sk, c_f32 ? 1 : 0, accumulate ? 1 : 0)
+    if (a_kmajor && b_kmajor) K8S_W4L(false, false);
+    else if (a_kmajor) K8S_W4L(false, true);
+    else if (b_kmajor) K8S_W4L(true, false);
+    else K8S_W4L(true, true);
+#undef K8S_W4L
     return;
   }
   if (a_kmajor && b_kmajor)

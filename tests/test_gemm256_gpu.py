@@ -211,19 +211,27 @@ def test_gemm256_mode_switch_sides(cuda, monkeypatch, mode):
 W4_SHAPES = [(4096, 4096, 64), (4096, 4096, 128), (4096, 4096, 192), (2048, 8192, 4096), (8192, 4096, 640)]
 
 
-@pytest.mark.parametrize("bk", [True, False])  # B K-major (forward) / MN-major (data gradient)
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, False), (False, True)])  # fwd, dgrad, wgrad
 @pytest.mark.parametrize("M,N,K", W4_SHAPES)
-def test_gemm_w4_matches_fp32(cuda, monkeypatch, M, N, K, bk):
+def test_gemm_w4_matches_fp32(cuda, monkeypatch, M, N, K, ak, bk):
     torch.manual_seed(6)
     a = torch.randn(M, K, device=cuda).bfloat16()
     b = torch.randn(N, K, device=cuda).bfloat16()
     ref = a.float() @ b.float().t()
+    A = a if ak else a.t().contiguous()
     B = b if bk else b.t().contiguous()
     monkeypatch.setenv("K8S_AMD_GEMM_W4", "1")
-    y = _C().gemm(a, True, B, bk, None, False, None, 0, None, False, 1.0, 1)
+    y = _C().gemm(A, ak, B, bk, None, False, None, 0, None, False, 1.0, 1)
     assert _rel(y, ref) < 1e-2
-    y2 = _C().gemm(a, True, B, bk, None, False, None, 0, None, False, 0.5, 1)  # alpha
+    y2 = _C().gemm(A, ak, B, bk, None, False, None, 0, None, False, 0.5, 1)  # alpha
     assert _rel(y2, 0.5 * ref) < 1e-2
-    monkeypatch.setenv("K8S_AMD_GEMM_W4", "0")  # the ring kernel: the same product to bf16 rounding
-    y0 = _C().gemm(a, True, B, bk, None, False, None, 0, None, False, 1.0, 1)
+    c = _C().gemm(A, ak, B, bk, None, True, None, 0, None, False, 1.0, 1)  # fp32 output (weight gradients)
+    assert _rel(c, ref) < 1e-4
+    out = torch.full((M, N), -1.5, device=cuda)
+    _C().gemm(A, ak, B, bk, out, True, None, 0, None, True, 0.5, 1)  # accumulate into an existing fp32 buffer
+    assert _rel(out + 1.5, 0.5 * ref) < 1e-4
+    monkeypatch.setenv("K8S_AMD_GEMM_W4", "0")  # the ring kernel: the same product to bf16 / fp32 rounding
+    y0 = _C().gemm(A, ak, B, bk, None, False, None, 0, None, False, 1.0, 1)
     assert _rel(y, y0) < 1e-2
+    c0 = _C().gemm(A, ak, B, bk, None, True, None, 0, None, False, 1.0, 1)
+    assert _rel(c, c0) < 1e-5
