@@ -532,20 +532,25 @@ static void launch_ring(const AS& a, const BS& b, const Epi& e, int M, int N, in
 // with a plain bf16 or fp32 (stored / accumulated) output -- the forward, data-gradient and weight-gradient products
 // of the transformer linears whose grids fill the chip -- on the schedule hipBLASLt's MT256x256x64 kernel
 // uses on gfx950 (its disassembly: 4 waves, 128 MFMAs + 32 ds_read_b128 + 16 LDS-DMA per 64-deep stage, 2 stages,
-// accumulators in AGPRs): the ring kernel above reaches 0.78-0.85x hipBLASLt on this form only
+// accumulators in AGPRs). The ring kernel above reached 0.78-0.85x hipBLASLt on the forward form
 // (profiles/r04_gemm_all_vs_hipblaslt.jsonl) with 2x its L2 requests -- its 32-deep stages read half cache lines
-// of a K-major row per DMA piece.
+// of a K-major row per DMA piece; it keeps the products outside this kernel's contract (w4_ok).
 //  * 256 threads = 4 waves as 2 x 2, each wave a 128 x 128 piece = 8 x 8 tiles of v_mfma_f32_16x16x32_bf16: 0.25
 //    LDS reads per MFMA (the 8-wave ring: 0.375). The 64 accumulators live in AGPRs: the MFMAs are inline asm with
 //    "+a" operands (the builtin's register choice moved the 256 accumulator registers between AGPRs and VGPRs every
 //    phase in a first 4-wave version, 0.97 vs 1.25 PF/s).
-//  * 64-deep stages (A 256 x 64 + B 256 x 64 = 64 KB), 2 in LDS; a row's 64 k are one 128-B line, read by 8 lanes of
-//    one DMA instruction. Stage s + 2 is issued right after the barrier in the middle of stage s, a whole stage
-//    (128 MFMAs per wave, one wave per SIMD) ahead of its wait.
-//  * fragments double-buffered in VGPRs: the k-half read while the other half's 64 MFMAs run.
-//  * LDS images [256 rows][64 k], 128-B rows, 16-B chunk c of row r at c ^ (r & 6): conflict-free ds_read_b128 for
-//    16-row fragment groups (the conv3x3 swizzle); a lane's row & 6 is lane & 6, so every fragment address is one
-//    of two per-lane bases plus an immediate.
+//  * 64-deep stages (A 256 x 64 + B 256 x 64 = 64 KB), 2 in LDS; a K-major row's 64 k are one 128-B line, an
+//    MN-major k-row's 64 columns of a sub-image too, read by 8 lanes of one DMA instruction. Stage s + 2 is issued
+//    in the half after the barrier in the middle of stage s, a whole stage (128 MFMAs per wave, one wave per SIMD)
+//    ahead of its wait.
+//  * fragments double-buffered in VGPRs: the next k-half read while this half's 64 MFMAs run; the transposed reads
+//    of MN-major operands are inline asm (the builtin draws a vmcnt(0) drain in front of it) tied to an explicit
+//    lgkmcnt(0) at each half's end.
+//  * K-major LDS images [256 rows][64 k], 128-B rows, 16-B chunk c of row r at c ^ (r & 6): conflict-free
+//    ds_read_b128 for 16-row fragment groups (the conv3x3 swizzle); a lane's row & 6 is lane & 6, so every fragment
+//    address is one of two per-lane bases plus an immediate.
+//  * stream-K tail (gemm256_plan) with a slab-sum epilogue; bf16 output staged through LDS in 16-B row segments,
+//    fp32 output (stored or accumulated) straight from the fragments.
 namespace g4 {
 constexpr int THREADS = 256, KS = 64;
 constexpr int STAGE_A = 256 * KS * 2;  // 32 KB
