@@ -22,7 +22,11 @@
 //   8-wave / 256-query blocks (each K/V tile staged once per 256 queries) with a 3-stage ring 258 us causal / 312 us
 //   non-causal, with 2 stages 235 / 291, vs this kernel 205 / 302 (scripts/gpurun/r3_attn7.sh); the row sums of P
 //   on the matrix cores (ones^T P^T, 4 extra MFMAs per tile instead of 32 v_add_f32) measured neutral; an
-//   unconditional rescale (one basic block per tile for the scheduler) 196 / 305 vs 188-194 / 294 us.)
+//   unconditional rescale (one basic block per tile for the scheduler) 196 / 305 vs 188-194 / 294 us. Round 4: a
+//   software pipeline over the full tiles -- S(t+1) = K(t+1) Q^T computed next to tile t's softmax, K streamed one tile
+//   ahead of V in the same 64 KB -- spilled at D = 128 (a second S tile beside 233 VGPRs) and at D = 64 ran slower
+//   on every shape: BERT s128 16 vs 13 us, s512 32 vs 26.5 us, Llama-1B s2048 84 vs 74.5 us (same box, alternating
+//   processes, scripts/gpurun/r4/fapipe.sh); not kept.)
 //
 // Backward (FA2 order, dK/dV kernel: one block = 64 keys of one KV head, looping over every query tile
 // of every query head of its GQA group, so dK/dV accumulate in VGPRs without atomics):
