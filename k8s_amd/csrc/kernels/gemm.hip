@@ -1083,6 +1083,13 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
                  float alpha, int splits, float* ws, hipStream_t st, const AddEpi* add,
                  const float* xform_b, int xform_c) {
   splits = effective_splits(K, splits);
+  // the data-gradient form (K-major dy, MN-major w) of a short reduction: the streaming kernel of gemm_short.hip
+  if (a_kmajor && !b_kmajor && !c_f32 && !bias && act == 0 && !pre && (mode == 0 || mode == 1) && splits == 1 &&
+      alpha == 1.f && !xform_b && ldb == N && (!add || add->mask) && gemm_short_ok(M, N, K, lda, ldc)) {
+    launch_gemm_short(A, B, ldb, true, reinterpret_cast<uint16_t*>(C), add ? add->src : nullptr,
+                      add ? add->mask : nullptr, nullptr, nullptr, M, N, K, add ? 2 : mode, st);
+    return;
+  }
   const bool slab = splits > 1;
   Epi e = make_epi(slab ? (void*)ws : C, slab ? (long)N : ldc, c_f32, bias, act, pre, slab ? 3 : mode, alpha);
   e.slab = (long)M * N;
@@ -1133,7 +1140,13 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, 
   if (xform && C % 64 != 0) throw std::runtime_error("normalize-on-load convolution needs C % 64 == 0");
   if (R == 1 && S == 1 && stride == 1 && pad == 0 && !sg && C % 64 == 0) {
     // a plain 1x1 convolution is the GEMM y[M][K] = x[M][C] . w[K][C]^T: the K-major source needs no im2col
-    // decode (ConvA's per-row (n, ho, wo) cursors were ~1/4 of the VALU of these memory-bound kernels)
+    // decode (ConvA's per-row (n, ho, wo) cursors were ~1/4 of the VALU of these memory-bound kernels); short
+    // reductions stream through gemm_short.hip
+    if (!y_f32 && !bias && act == 0 && mode == 0 && gemm_short_ok(M, K, C, C, K)) {
+      launch_gemm_short(x, w, C, false, reinterpret_cast<uint16_t*>(y), nullptr, nullptr, xform, stats, M, K, C, 0,
+                        st);
+      return;
+    }
     KMajor a{x, (long)C, M};
     if (xform) {
       const XForm xf{xform, C, make_fastdiv(C)};

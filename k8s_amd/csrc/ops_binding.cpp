@@ -1094,5 +1094,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_bwd", &flash_bwd, py::arg("dO"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("causal"), py::arg("kv_lens"), py::arg("scale"), py::arg("dqkv") = py::none());
   m.attr("conv_stat_replicas") = k8s_amd::kConvStatReplicas;
+  m.def("gemm_short_ok", [](int64_t M, int64_t N, int64_t K) { return k8s_amd::gemm_short_ok((int)M, (int)N, (int)K, K, N); },
+        "whether C[M,N] = A[M,K] . B^T (contiguous) takes the short-K streaming kernel (gemm_short.hip)");
   m.attr("arch") = "gfx950";
 }

@@ -90,10 +90,17 @@ def main():
                 res["dgrad"] = timed(lambda: conv._dgrad_hip(C_, gy, w, pad), a.reps)
             else:
                 res["dgrad"] = timed(lambda: conv._dgrad_strided_hip(C_, gy, w, s, pad, H, H), a.reps)
+        # compulsory HBM bytes per op (bf16 activations, fp32 weight gradient) and the speed-of-light floor
+        # max(bytes / 8 TB/s, flops / 2.5 PF/s): "sol" = floor / measured.
+        xb, yb, wb = N * H * H * C * 2, M * K * 2, K * R * R * C * 2
+        nb = {"fwd": xb + yb + wb, "wgrad": xb + yb + 2 * wb, "dgrad": yb + xb + wb}
         for op in ("fwd", "wgrad", "dgrad"):
             if op in res:
+                floor = max(nb[op] / 8e9, flops / 2.5e12)
                 rows.append({"layer": name, "op": op, "count": cnt, "ms": round(res[op], 4),
-                             "step_ms": round(res[op] * cnt, 3), "tflops": round(flops / res[op] / 1e9, 1)})
+                             "step_ms": round(res[op] * cnt, 3), "tflops": round(flops / res[op] / 1e9, 1),
+                             "floor_ms": round(floor, 4), "sol": round(floor / res[op], 2),
+                             "lost_ms_per_step": round((res[op] - floor) * cnt, 3)})
                 tot[op] = tot.get(op, 0.0) + res[op] * cnt
         # BatchNorm of this conv's output y [M, K]
         y = gy
@@ -111,7 +118,8 @@ def main():
             t = timed(lambda: C_.bn_fwd_from_sums(y, resid, g, b, sums, rm, rv, 0.1, 1e-5, relu, mask_out), a.reps)
             nbytes = elems * (4 + (2 if resid is not None else 0) + (0.125 if mask_out else 0))
             rows.append({"layer": name, "op": "bn_fwd", "count": cnt, "ms": round(t, 4), "step_ms": round(t * cnt, 3),
-                         "tbps": round(nbytes / t / 1e9, 2)})
+                         "tbps": round(nbytes / t / 1e9, 2), "sol": round(nbytes / 8e9 / t, 2),
+                         "lost_ms_per_step": round((t - nbytes / 8e9) * cnt, 3)})
             tot["bn_fwd"] = tot.get("bn_fwd", 0.0) + t * cnt
         if "bnb" in only:
             out = C_.bn_fwd_from_sums(y, resid, g, b, sums, rm, rv, 0.1, 1e-5, relu, mask_out)
@@ -124,7 +132,8 @@ def main():
             # reduce: dy + x (+ mask); apply: dy + x (+ mask) -> dx (+ dres)
             nbytes = elems * (4 + 4 + 2 + (2 if bnk == "res" else 0) + (0.25 if mask_out else 0))
             rows.append({"layer": name, "op": "bn_bwd", "count": cnt, "ms": round(t, 4), "step_ms": round(t * cnt, 3),
-                         "tbps": round(nbytes / t / 1e9, 2)})
+                         "tbps": round(nbytes / t / 1e9, 2), "sol": round(nbytes / 8e9 / t, 2),
+                         "lost_ms_per_step": round((t - nbytes / 8e9) * cnt, 3)})
             tot["bn_bwd"] = tot.get("bn_bwd", 0.0) + t * cnt
         for r in rows:
             print(json.dumps(r), flush=True)

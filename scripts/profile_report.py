@@ -19,7 +19,7 @@ CATS = [
     ("BatchNorm", r"k8s_amd::bn_|relu_mask|pool_bn_bwd"),
     ("weight gradient", r"wgrad_stream|ConvWgB|MNMajorK, k8s_amd::MNMajorK|MNMaj, k8s_amd::g256r::MNMaj|gemm_w4_kernel<true, true>|splitk_reduce|"
                         r"wgrad3x3|wg3_reduce|stem_wgrad|stem_dw"),
-    ("conv / GEMM fwd + dgrad", r"gemm_bf16_kernel|gemm256|gemm_w4|conv3x3_kernel|conv_dgrad_wtrans|stem_conv_fwd|stem_w_s2d"),
+    ("conv / GEMM fwd + dgrad", r"gemm_bf16_kernel|gemm256|gemm_w4|gemm_short_kernel|conv3x3_kernel|conv_dgrad_wtrans|stem_conv_fwd|stem_w_s2d"),
     ("pooling", r"pool"),
     ("optimizer / loss", r"sgd_|adam_|xent|sumsq|clip"),
     ("attention / norms / elementwise", r"flash_|norm_|swiglu|rope|gelu|relu_bwd|colsum"),
