@@ -1,4 +1,4 @@
-// Short-K streaming GEMM: C[M][N] (bf16) = op(A)[M][K] . B^T, K in {128, 256} (64 built, not routed), N % 128 == 0:
+// Short-K streaming GEMM: C[M][N] (bf16) = op(A)[M][K] . B^T for K in {64, 128, 256} and N % 128 == 0:
 // the 1x1 convolutions of ResNet-50 as GEMMs (forward: A = the NHWC activation, B = w[Kout][C]; data gradient: A =
 // dy, B = w read transposed), reference parity: the 1x1 conv2d calls of the reference's tf_cnn_benchmarks ResNet
 // (SURVEY.md §2.6 K3 / BASELINE.json configs[1]).
@@ -61,8 +61,8 @@ template <int K, int EPI, bool XF, bool STATS>
 struct Cfg {
   static constexpr int KC = K / 32;
   static constexpr bool HEAVY = EPI != 0 || (XF && STATS);  // the variants with the most live state
-  static constexpr int OCC = K == 256 || (K == 128 && HEAVY) ? 1 : 2;
-  static constexpr int NBUF = OCC == 1 ? (K == 256 ? 2 : 3) : (K == 64 && !HEAVY ? 4 : 2);
+  static constexpr int OCC = K == 256 || (K == 128 && HEAVY) || (K == 64 && EPI == 2) ? 1 : 2;
+  static constexpr int NBUF = OCC == 1 ? (K == 256 ? 2 : 3) : (K == 64 && !HEAVY ? 3 : 2);
 };
 
 __device__ __forceinline__ mfma_bf16x8 as_frag(i32x4 v) { return __builtin_bit_cast(mfma_bf16x8, v); }
@@ -113,8 +113,10 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
   constexpr int KC = Cfg<K, EPI, XF, STATS>::KC, NBUF = Cfg<K, EPI, XF, STATS>::NBUF;
   constexpr int WBYTES = NB * KC * 1024;
   constexpr int XBYTES = XF ? KC * 4 * 64 : 0;
+  constexpr int SBYTES = TM * BN * 2;  // per-wave staging of one bf16 output tile (the row-contiguous copy-out)
+  constexpr int STG = (WBYTES + XBYTES + 1023) / 1024 * 1024;
   constexpr int RBYTES = STATS ? 4 * 2 * BN * 4 : 0;
-  constexpr int LDS = WBYTES + XBYTES > RBYTES ? WBYTES + XBYTES : RBYTES;
+  constexpr int LDS = STG + 4 * SBYTES > RBYTES ? STG + 4 * SBYTES : RBYTES;
   __shared__ __attribute__((aligned(1024))) char smem[LDS];
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bid = blockIdx.x, xcd = bid & 7, jb = bid >> 3;
@@ -158,17 +160,16 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
   const int q = lane >> 4;
   const uint32_t la = (uint32_t)(((lane & 15) * g.lda + q * 8) * 2);
   const uint32_t lda16 = (uint32_t)(16 * g.lda * 2), rowA = (uint32_t)(WG * TM * g.lda * 2);
-  // output / addend: row r0 + 16 mb + (l & 15), 8 columns from n0 + 16 (q & 1) + 8 (q >> 1) + 32 p (see epilogue)
-  const uint32_t lc = (uint32_t)(((lane & 15) * N + n0 + 16 * (q & 1) + 8 * (q >> 1)) * 2);
-  const uint32_t n16 = (uint32_t)(16 * N * 2), rowC = (uint32_t)(WG * TM * N * 2);
-  const uint32_t lm = (uint32_t)(((lane & 15) * N + n0) >> 3);  // the row's 16 mask bytes of this panel
-  const uint32_t n16m = (uint32_t)(2 * N), rowM = (uint32_t)(WG * TM * N / 8);
-
-  constexpr int NP = NB / 2, D = NBUF - 1;  // column-block pairs; tiles loaded ahead
+  // output / addend, in the copy-out layout: row r0 + 4 k + (l >> 4), 8 columns from n0 + 8 (l & 15)
+  const uint32_t lc = (uint32_t)(((lane >> 4) * N + n0 + 8 * (lane & 15)) * 2);
+  const uint32_t n4 = (uint32_t)(4 * N * 2), rowC = (uint32_t)(WG * TM * N * 2);
+  const uint32_t lm = (uint32_t)((((lane >> 4) * N + n0) >> 3) + (lane & 15));  // the lane's mask byte
+  const uint32_t n4m = (uint32_t)(N / 2), rowM = (uint32_t)(WG * TM * N / 8);
+  constexpr int NP = NB / 2, D = NBUF - 1, KO = TM / 4;  // column-block pairs; tiles loaded ahead; copy-out rows
 
   i32x4 abuf[NBUF][MB][KC];
-  i32x4 obuf[NBUF][EPI ? MB : 1][EPI ? NP : 1];
-  i32x4 mbuf[NBUF][EPI == 2 ? MB : 1];
+  i32x4 obuf[NBUF][EPI ? KO : 1];
+  uint32_t mbuf[NBUF][EPI == 2 ? KO : 1];
   auto load_a = [&](i32x4 (&dst)[MB][KC], int t) __attribute__((always_inline)) {
     const uint32_t base = (uint32_t)(gw * TM) * (uint32_t)(g.lda * 2) + (uint32_t)t * rowA + la;
 #pragma unroll
@@ -180,13 +181,11 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
     if constexpr (EPI != 0) {
       const uint32_t base = (uint32_t)(gw * TM) * (uint32_t)(N * 2) + (uint32_t)t * rowC + lc;
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-        for (int p = 0; p < NP; ++p) bload16(obuf[slot][mb][p], base + mb * n16 + p * 64, EPI == 2 ? radd : rc);
+      for (int k = 0; k < KO; ++k) bload16(obuf[slot][k], base + k * n4, EPI == 2 ? radd : rc);
       if constexpr (EPI == 2) {
         const uint32_t mrow = (uint32_t)(gw * TM) * (uint32_t)(N / 8) + (uint32_t)t * rowM + lm;
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb) bload16(mbuf[slot][mb], mrow + mb * n16m, rmask);
+        for (int k = 0; k < KO; ++k) mbuf[slot][k] = __builtin_amdgcn_raw_buffer_load_b8(rmask, mrow + k * n4m, 0, 0);
       }
     }
   };
@@ -234,41 +233,31 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
       __builtin_amdgcn_sched_barrier(0);
     }
     // ---- epilogue. Lane group q of column blocks (2p, 2p + 1) holds columns 32p + 4q and 32p + 16 + 4q (4 each);
-    // one v_permlane16_swap per dword pair gives lane group q the 8 consecutive columns
-    // 32p + 16 (q & 1) + 8 (q >> 1) .. +7 -> one 16-B store per (row block, pair)
-    const uint32_t cb = (uint32_t)(gw * TM) * (uint32_t)(N * 2) + (uint32_t)t * rowC + lc;
+    // one v_permlane16_swap per dword pair gives it the 8 consecutive columns 32p + 16 (q & 1) + 8 (q >> 1) .. +7
+    // (16-B chunk c = 4p + 2 (q & 1) + (q >> 1) of its row). The chunks go to this wave's staging rows (chunk XOR
+    // row: conflict-free), and come back row-contiguous: each store instruction then writes 4 whole 256-B rows
+    // (straight from the MFMA layout every instruction wrote 16 rows x 64 B: 1.1-1.2x slower on output-heavy
+    // shapes). The statistics are taken from the same bf16 values before the round trip.
+    char* stg = smem + STG + wid * SBYTES;
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
+      const int r = mb * 16 + (lane & 15);
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
         i32x2 pa = __builtin_bit_cast(i32x2, __builtin_convertvector(acc[mb][2 * p], bf16v4_t));
         i32x2 pb = __builtin_bit_cast(i32x2, __builtin_convertvector(acc[mb][2 * p + 1], bf16v4_t));
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
-          const auto r = __builtin_amdgcn_permlane16_swap(pa[d], pb[d], false, false);
-          pa[d] = r[0];
-          pb[d] = r[1];
+          const auto rr = __builtin_amdgcn_permlane16_swap(pa[d], pb[d], false, false);
+          pa[d] = rr[0];
+          pb[d] = rr[1];
         }
-        i32x4 o = {pa[0], pa[1], pb[0], pb[1]};
-        if constexpr (EPI != 0) {  // one more bf16 rounding on top of the stored product (<= 1 ulp)
-          const i32x4 old = obuf[u][mb][p];
-          uint32_t keep = 0xFFu;
-          if constexpr (EPI == 2)
-            keep = ((uint32_t)mbuf[u][mb][p] >> ((2 * (q & 1) + (q >> 1)) * 8)) & 0xFFu;
-          float f[8];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const uint32_t w = (uint32_t)o[j], ow = (uint32_t)old[j];
-            f[2 * j] = __uint_as_float(w << 16) + (((keep >> (2 * j)) & 1u) ? __uint_as_float(ow << 16) : 0.f);
-            f[2 * j + 1] = __uint_as_float(w & 0xFFFF0000u) +
-                           (((keep >> (2 * j + 1)) & 1u) ? __uint_as_float(ow & 0xFFFF0000u) : 0.f);
-          }
-          o = __builtin_bit_cast(i32x4, pack_bf16x8(f));
-        }
-        bstore16(o, cb + mb * n16 + p * 64, rc);
+        const i32x4 o = {pa[0], pa[1], pb[0], pb[1]};
+        const int c = 4 * p + 2 * (q & 1) + (q >> 1);
+        *reinterpret_cast<i32x4*>(stg + r * (BN * 2) + ((c ^ (r & 15)) << 4)) = o;
         if constexpr (STATS) {
           // rows past M: A read as 0, but normalised on load that is relu(shift), not 0 -- keep them out
-          const bool live = !XF || (gw + t * WG) * TM + mb * 16 + (lane & 15) < g.M;
+          const bool live = !XF || (gw + t * WG) * TM + r < g.M;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const uint32_t w = live ? (uint32_t)o[j] : 0u;
@@ -278,6 +267,26 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
           }
         }
       }
+    }
+    const uint32_t cb = (uint32_t)(gw * TM) * (uint32_t)(N * 2) + (uint32_t)t * rowC + lc;
+#pragma unroll
+    for (int k = 0; k < KO; ++k) {
+      const int r = 4 * k + (lane >> 4), c = lane & 15;
+      i32x4 o = *reinterpret_cast<const i32x4*>(stg + r * (BN * 2) + ((c ^ (r & 15)) << 4));
+      if constexpr (EPI != 0) {  // one more bf16 rounding on top of the stored product (<= 1 ulp)
+        const i32x4 old = obuf[u][k];
+        const uint32_t keep = EPI == 2 ? mbuf[u][k] : 0xFFu;
+        float f[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t w = (uint32_t)o[j], ow = (uint32_t)old[j];
+          f[2 * j] = __uint_as_float(w << 16) + (((keep >> (2 * j)) & 1u) ? __uint_as_float(ow << 16) : 0.f);
+          f[2 * j + 1] = __uint_as_float(w & 0xFFFF0000u) +
+                         (((keep >> (2 * j + 1)) & 1u) ? __uint_as_float(ow & 0xFFFF0000u) : 0.f);
+        }
+        o = __builtin_bit_cast(i32x4, pack_bf16x8(f));
+      }
+      bstore16(o, cb + k * n4, rc);
     }
   };
 
@@ -323,14 +332,14 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
 
 }  // namespace gsk
 
-// Shape contract (the caller falls back to gemm.hip otherwise): K-major A with contiguous rows of K in {128, 256},
-// N % 128 == 0, bf16 C [M][N] contiguous, every operand < 2 GiB (32-bit buffer offsets). K = 64 is built into the
-// kernel template but not routed: on ResNet-50's 64-deep layers (3.2M x 64 -> 256 forward, 64 -> 256 data
-// gradient) it measured 1.15-1.2x slower than gemm.hip's tile kernel (scripts/gpurun/r4/c1x1.py).
+// Shape contract (the caller falls back to gemm.hip otherwise): K-major A with contiguous rows of K in {64, 128,
+// 256}, N % 128 == 0, bf16 C [M][N] contiguous, every operand < 2 GiB (32-bit buffer offsets). (K = 64 lost to
+// gemm.hip's tile kernel while the epilogue stored straight from the MFMA layout; with the row-contiguous copy-out
+// it wins on ResNet-50's 64-deep layers: bench 13.88k -> 13.93k img/s routed, scripts/gpurun/r4/gsk2.sh.)
 bool gemm_short_ok(int M, int N, int K, long lda, long ldc) {
   const char* e = std::getenv("K8S_AMD_GEMM_SHORT");
   if (e && e[0] == '0') return false;
-  if (!(K == 128 || K == 256) || N % 128 != 0 || lda != K || ldc != N || M <= 0) return false;
+  if (!(K == 64 || K == 128 || K == 256) || N % 128 != 0 || lda != K || ldc != N || M <= 0) return false;
   const long lim = 1L << 31;
   return (long)M * K * 2 < lim && (long)M * N * 2 < lim && (long)K * N * 2 < lim;
 }
@@ -344,7 +353,8 @@ void launch_gemm_short(const uint16_t* A, const uint16_t* B, long ldb, bool b_mn
   if (epi != 0 && stats) throw std::runtime_error("gemm_short: statistics only with a plain store");
   gsk::Args g{A, B, C, add, mask, xf, stats, M, N, K, (int)ldb, N / gsk::BN, 0};
   // Cfg::OCC blocks per CU; the P panels of one row group share an XCD, so blocks come in multiples of 8 P
-  const int per_chip = (K == 256 || (K == 128 && (epi != 0 || (xf && stats)))) ? 256 : 512;  // Cfg::OCC
+  const bool heavy = epi != 0 || (xf && stats);
+  const int per_chip = (K == 256 || (K == 128 && heavy) || (K == 64 && epi == 2)) ? 256 : 512;  // Cfg::OCC
   const int gx = (per_chip / (8 * g.P)) > 1 ? per_chip / (8 * g.P) : 1;
   g.G = 8 * gx;
   const dim3 grid(8 * g.P * gx), block(gsk::THREADS);
@@ -352,7 +362,9 @@ void launch_gemm_short(const uint16_t* A, const uint16_t* B, long ldb, bool b_mn
   hipLaunchKernelGGL((gsk::gemm_short_kernel<KK, BM, XF, ST, EP>), grid, block, 0, st, g)
 #define K8S_GSK_K(BM, XF, ST, EP)    \
   do {                               \
-    if (K == 128)                    \
+    if (K == 64)                     \
+      K8S_GSK(64, BM, XF, ST, EP);   \
+    else if (K == 128)               \
       K8S_GSK(128, BM, XF, ST, EP);  \
     else                             \
       K8S_GSK(256, BM, XF, ST, EP);  \

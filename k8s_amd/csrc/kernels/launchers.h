@@ -75,7 +75,7 @@ struct AddEpi {
   const uint16_t* src;
   const uint8_t* mask;
 };
-// gemm_short.hip: the short-K streaming GEMM (K in {128, 256}, N % 128 == 0; see its header)
+// gemm_short.hip: the short-K streaming GEMM (K in {64, 128, 256}, N % 128 == 0; see its header)
 bool gemm_short_ok(int M, int N, int K, long lda, long ldc);
 void launch_gemm_short(const uint16_t* A, const uint16_t* B, long ldb, bool b_mn, uint16_t* C, const uint16_t* add,
                        const uint8_t* mask, const float* xf, float* stats, int M, int N, int K, int epi,

@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU job (round 4): short-K GEMM final -- tests, 1x1 shapes, bench A/B (K8S_AMD_GEMM_SHORT=1/0), kernel trace.
+set -o pipefail
+O=gpurun_out/r4_gsk3; rm -rf $O; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gemm_short_gpu.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+timeout -k 10 300 python -u -m pytest tests/test_gemm_conv_gpu.py tests/test_resnet_gpu.py -x -q --timeout 120 --timeout-method thread > $O/tests2.log 2>&1 || { tail -40 $O/tests2.log; exit 1; }
+tail -1 $O/tests2.log
+timeout -k 10 300 python -u scripts/gpurun/r4/c1x1.py > $O/on.jsonl 2> $O/err || { tail -30 $O/err; exit 1; }
+cat $O/on.jsonl
+for r in 1 2; do
+  for v in 1 0; do
+    K8S_AMD_GEMM_SHORT=$v timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/bench_${v}_$r.json 2>> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+    echo "short=$v $(python3 -c "import json;d=json.load(open('$O/bench_${v}_$r.json'));print(d['value'], d['ms_per_step'])")"
+  done
+done
+export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/prof -o rn -- python3 bench.py --steps 8 --warmup 3 > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
+python3 scripts/profile_report.py $(ls $O/prof/*kernel_trace.csv | head -1) --step-marker sgd_kernel --top 70 --title "ResNet-50 b1024, round 4 (short-K GEMM, row-contiguous copy-out)" > $O/rn.md && head -14 $O/rn.md
