@@ -1138,11 +1138,12 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, 
     e.rb = sg->b;
   }
   if (xform && C % 64 != 0) throw std::runtime_error("normalize-on-load convolution needs C % 64 == 0");
-  if (R == 1 && S == 1 && stride == 1 && pad == 0 && !sg && C % 64 == 0) {
+  if (R == 1 && S == 1 && stride == 1 && pad == 0 && (!sg || (Ho == H && Wo == W)) && C % 64 == 0) {
     // a plain 1x1 convolution is the GEMM y[M][K] = x[M][C] . w[K][C]^T: the K-major source needs no im2col
     // decode (ConvA's per-row (n, ho, wo) cursors were ~1/4 of the VALU of these memory-bound kernels); short
-    // reductions stream through gemm_short.hip
-    if (!y_f32 && !bias && act == 0 && mode == 0 && gemm_short_ok(M, K, C, C, K)) {
+    // reductions stream through gemm_short.hip. The live parity of a strided 1x1 data gradient (a sub-grid output,
+    // scattered by the epilogue) takes the same source: 2-4 % faster per layer than ConvA (scripts/gpurun/r4/sgkm.sh)
+    if (!sg && !y_f32 && !bias && act == 0 && mode == 0 && gemm_short_ok(M, K, C, C, K)) {
       launch_gemm_short(x, w, C, false, reinterpret_cast<uint16_t*>(y), nullptr, nullptr, xform, stats, M, K, C, 0,
                         st);
       return;
