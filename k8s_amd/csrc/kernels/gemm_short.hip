@@ -39,7 +39,6 @@ namespace gsk {
 
 constexpr int THREADS = 256;           // 4 waves
 constexpr int BN = 128, NB = BN / 16;  // column panel of a block, 16-wide MFMA blocks
-constexpr int TM = 32, MB = TM / 16;   // rows of one wave tile
 constexpr int REPL = kConvStatReplicas;
 
 typedef __attribute__((ext_vector_type(2))) int i32x2;
@@ -57,15 +56,17 @@ struct Args {
   int P, G;              // column panels, row groups
 };
 
-// A-fragment ring depth (tiles in flight incl. the one being computed): sized so the ring fits beside 64
-// accumulators, the statistics and (EPI > 0) the addend: K <= 128 at 2 waves per SIMD (256 registers), K = 256 and
-// the K = 128 variants with the most live state at one wave per SIMD with a deeper ring
+// A-fragment ring depth (tiles in flight incl. the one being computed), tile rows and waves per SIMD: sized so the
+// ring fits beside the accumulators, the statistics and (EPI > 0) the addend in 256 registers (2 waves per SIMD)
 template <int K, int EPI, bool XF, bool STATS>
 struct Cfg {
   static constexpr int KC = K / 32;
   static constexpr bool HEAVY = EPI != 0 || (XF && STATS);  // the variants with the most live state
-  static constexpr int OCC = K == 256 || (K == 128 && HEAVY) || (K == 64 && EPI == 2) ? 1 : 2;
-  static constexpr int NBUF = OCC == 1 ? (K == 256 ? 2 : 3) : (K == 64 && !HEAVY ? 3 : 2);
+  // rows per wave tile: the heavy variants and K = 256 take 16-row tiles so they fit 2 waves per SIMD (MFMAs and
+  // epilogues then overlap across the two waves; at one wave per SIMD with 32-row tiles they serialised)
+  static constexpr int TM = HEAVY || K == 256 ? 16 : 32;
+  static constexpr int OCC = 2;
+  static constexpr int NBUF = !HEAVY && K != 128 ? 3 : 2;
 };
 
 __device__ __forceinline__ mfma_bf16x8 as_frag(i32x4 v) { return __builtin_bit_cast(mfma_bf16x8, v); }
@@ -114,9 +115,10 @@ __device__ __forceinline__ mfma_bf16x8 xform8(i32x4 raw, const float* tab) {
 template <int K, bool BMN, bool XF, bool STATS, int EPI>
 __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_short_kernel(Args g) {
   constexpr int KC = Cfg<K, EPI, XF, STATS>::KC, NBUF = Cfg<K, EPI, XF, STATS>::NBUF;
+  constexpr int TM = Cfg<K, EPI, XF, STATS>::TM, MB = TM / 16;
   constexpr int WBYTES = NB * KC * 1024;
   constexpr int XBYTES = XF ? KC * 4 * 64 : 0;
-  constexpr int SBYTES = TM * BN * 2;  // per-wave staging of one bf16 output tile (the row-contiguous copy-out)
+  constexpr int SBYTES = TM * 128;  // per-wave staging of half a bf16 output tile (64 columns; the copy-out)
   constexpr int STG = (WBYTES + XBYTES + 1023) / 1024 * 1024;
   constexpr int RBYTES = STATS ? 4 * 2 * BN * 4 : 0;
   constexpr int LDS = STG + 4 * SBYTES > RBYTES ? STG + 4 * SBYTES : RBYTES;
@@ -163,16 +165,17 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
   const int q = lane >> 4;
   const uint32_t la = (uint32_t)(((lane & 15) * g.lda + q * 8) * 2);
   const uint32_t lda16 = (uint32_t)(16 * g.lda * 2), rowA = (uint32_t)(WG * TM * g.lda * 2);
-  // output / addend, in the copy-out layout: row r0 + 4 k + (l >> 4), 8 columns from n0 + 8 (l & 15)
-  const uint32_t lc = (uint32_t)(((lane >> 4) * N + n0 + 8 * (lane & 15)) * 2);
-  const uint32_t n4 = (uint32_t)(4 * N * 2), rowC = (uint32_t)(WG * TM * N * 2);
-  const uint32_t lm = (uint32_t)((((lane >> 4) * N + n0) >> 3) + (lane & 15));  // the lane's mask byte
-  const uint32_t n4m = (uint32_t)(N / 2), rowM = (uint32_t)(WG * TM * N / 8);
-  constexpr int NP = NB / 2, D = NBUF - 1, KO = TM / 4;  // column-block pairs; tiles loaded ahead; copy-out rows
+  // output / addend, in the copy-out layout: half h of the panel, row r0 + 8 k + (l >> 3), 8 columns from
+  // n0 + 64 h + 8 (l & 7)
+  const uint32_t lc = (uint32_t)(((lane >> 3) * N + n0 + 8 * (lane & 7)) * 2);
+  const uint32_t n8 = (uint32_t)(8 * N * 2), rowC = (uint32_t)(WG * TM * N * 2);
+  const uint32_t lm = (uint32_t)((((lane >> 3) * N + n0) >> 3) + (lane & 7));  // the lane's mask byte
+  const uint32_t n8m = (uint32_t)N, rowM = (uint32_t)(WG * TM * N / 8);
+  constexpr int NP = NB / 2, D = NBUF - 1, KO = TM / 8;  // column-block pairs; tiles ahead; copy-out rows / 8
 
   i32x4 abuf[NBUF][MB][KC];
-  i32x4 obuf[NBUF][EPI ? KO : 1];
-  uint32_t mbuf[NBUF][EPI == 2 ? KO : 1];
+  i32x4 obuf[NBUF][EPI ? 2 : 1][EPI ? KO : 1];
+  uint32_t mbuf[NBUF][EPI == 2 ? 2 : 1][EPI == 2 ? KO : 1];
   auto load_a = [&](i32x4 (&dst)[MB][KC], int t) __attribute__((always_inline)) {
     const uint32_t base = (uint32_t)(gw * TM) * (uint32_t)(g.lda * 2) + (uint32_t)t * rowA + la;
 #pragma unroll
@@ -184,11 +187,16 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
     if constexpr (EPI != 0) {
       const uint32_t base = (uint32_t)(gw * TM) * (uint32_t)(N * 2) + (uint32_t)t * rowC + lc;
 #pragma unroll
-      for (int k = 0; k < KO; ++k) bload16(obuf[slot][k], base + k * n4, EPI == 2 ? radd : rc);
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int k = 0; k < KO; ++k) bload16(obuf[slot][h][k], base + h * 128 + k * n8, EPI == 2 ? radd : rc);
       if constexpr (EPI == 2) {
         const uint32_t mrow = (uint32_t)(gw * TM) * (uint32_t)(N / 8) + (uint32_t)t * rowM + lm;
 #pragma unroll
-        for (int k = 0; k < KO; ++k) mbuf[slot][k] = __builtin_amdgcn_raw_buffer_load_b8(rmask, mrow + k * n4m, 0, 0);
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int k = 0; k < KO; ++k)
+            mbuf[slot][h][k] = __builtin_amdgcn_raw_buffer_load_b8(rmask, mrow + h * 8 + k * n8m, 0, 0);
       }
     }
   };
@@ -220,12 +228,19 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
     mfma_bf16x8 wf[NB];
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) wf[nb] = *reinterpret_cast<const mfma_bf16x8*>(smem + (nb * KC * 64 + lane) * 16);
+    // A operands: with XF the next chunk's normalisation is computed inside this chunk's region, so its VALU work
+    // issues between this chunk's MFMAs instead of in front of the next chunk's
+    mfma_bf16x8 af[MB];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) af[mb] = XF ? xform8(abuf[u][mb][0], xtab) : as_frag(abuf[u][mb][0]);
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
-      mfma_bf16x8 af[MB];
+      mfma_bf16x8 an[MB];
+      if (kc + 1 < KC) {
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb)
-        af[mb] = XF ? xform8(abuf[u][mb][kc], xtab + kc * 64) : as_frag(abuf[u][mb][kc]);
+        for (int mb = 0; mb < MB; ++mb)
+          an[mb] = XF ? xform8(abuf[u][mb][kc + 1], xtab + (kc + 1) * 64) : as_frag(abuf[u][mb][kc + 1]);
+      }
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
 #pragma unroll
@@ -234,62 +249,70 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
           wf[nb] = *reinterpret_cast<const mfma_bf16x8*>(smem + ((nb * KC + kc + 1) * 64 + lane) * 16);
       }
       __builtin_amdgcn_sched_barrier(0);
+      if (kc + 1 < KC) {
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) af[mb] = an[mb];
+      }
     }
     // ---- epilogue. Lane group q of column blocks (2p, 2p + 1) holds columns 32p + 4q and 32p + 16 + 4q (4 each);
-    // one v_permlane16_swap per dword pair gives it the 8 consecutive columns 32p + 16 (q & 1) + 8 (q >> 1) .. +7
-    // (16-B chunk c = 4p + 2 (q & 1) + (q >> 1) of its row). The chunks go to this wave's staging rows (chunk XOR
-    // row: conflict-free), and come back row-contiguous: each store instruction then writes 4 whole 256-B rows
-    // (straight from the MFMA layout every instruction wrote 16 rows x 64 B: 1.1-1.2x slower on output-heavy
-    // shapes). The statistics are taken from the same bf16 values before the round trip.
+    // one v_permlane16_swap per dword pair gives it the 8 consecutive columns 32p + 16 (q & 1) + 8 (q >> 1) .. +7.
+    // Per 64-column half, the chunks go to this wave's staging rows (128 B, chunk XOR row: conflict-free both ways)
+    // and come back row-contiguous: each 16-B store instruction then writes 8 whole 128-B row segments (straight
+    // from the MFMA layout every instruction wrote 16 rows x 64 B: 1.1-1.2x slower on output-heavy shapes). The
+    // statistics are taken from the same bf16 values before the round trip.
     char* stg = smem + STG + wid * SBYTES;
+    const uint32_t cb = (uint32_t)(gw * TM) * (uint32_t)(N * 2) + (uint32_t)t * rowC + lc;
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
-      const int r = mb * 16 + (lane & 15);
+    for (int h = 0; h < 2; ++h) {
 #pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        i32x2 pa = __builtin_bit_cast(i32x2, __builtin_convertvector(acc[mb][2 * p], bf16v4_t));
-        i32x2 pb = __builtin_bit_cast(i32x2, __builtin_convertvector(acc[mb][2 * p + 1], bf16v4_t));
+      for (int mb = 0; mb < MB; ++mb) {
+        const int r = mb * 16 + (lane & 15);
 #pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          const auto rr = __builtin_amdgcn_permlane16_swap(pa[d], pb[d], false, false);
-          pa[d] = rr[0];
-          pb[d] = rr[1];
-        }
-        const i32x4 o = {pa[0], pa[1], pb[0], pb[1]};
-        const int c = 4 * p + 2 * (q & 1) + (q >> 1);
-        *reinterpret_cast<i32x4*>(stg + r * (BN * 2) + ((c ^ (r & 15)) << 4)) = o;
-        if constexpr (STATS) {
-          // rows past M: A read as 0, but normalised on load that is relu(shift), not 0 -- keep them out
-          const bool live = !XF || (gw + t * WG) * TM + r < g.M;
+        for (int pp = 0; pp < 2; ++pp) {
+          const int p = 2 * h + pp;
+          i32x2 pa = __builtin_bit_cast(i32x2, __builtin_convertvector(acc[mb][2 * p], bf16v4_t));
+          i32x2 pb = __builtin_bit_cast(i32x2, __builtin_convertvector(acc[mb][2 * p + 1], bf16v4_t));
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const uint32_t w = live ? (uint32_t)o[j] : 0u;
-            const f32x2_t y = {__uint_as_float(w << 16), __uint_as_float(w & 0xFFFF0000u)};
-            s2[p][j] += y;
-            q2[p][j] = __builtin_elementwise_fma(y, y, q2[p][j]);
+          for (int d = 0; d < 2; ++d) {
+            const auto rr = __builtin_amdgcn_permlane16_swap(pa[d], pb[d], false, false);
+            pa[d] = rr[0];
+            pb[d] = rr[1];
+          }
+          const i32x4 o = {pa[0], pa[1], pb[0], pb[1]};
+          const int c = 4 * pp + 2 * (q & 1) + (q >> 1);
+          *reinterpret_cast<i32x4*>(stg + r * 128 + ((c ^ (r & 7)) << 4)) = o;
+          if constexpr (STATS) {
+            // rows past M: A read as 0, but normalised on load that is relu(shift), not 0 -- keep them out
+            const bool live = !XF || (gw + t * WG) * TM + r < g.M;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const uint32_t w = live ? (uint32_t)o[j] : 0u;
+              const f32x2_t y = {__uint_as_float(w << 16), __uint_as_float(w & 0xFFFF0000u)};
+              s2[p][j] += y;
+              q2[p][j] = __builtin_elementwise_fma(y, y, q2[p][j]);
+            }
           }
         }
       }
-    }
-    const uint32_t cb = (uint32_t)(gw * TM) * (uint32_t)(N * 2) + (uint32_t)t * rowC + lc;
 #pragma unroll
-    for (int k = 0; k < KO; ++k) {
-      const int r = 4 * k + (lane >> 4), c = lane & 15;
-      i32x4 o = *reinterpret_cast<const i32x4*>(stg + r * (BN * 2) + ((c ^ (r & 15)) << 4));
-      if constexpr (EPI != 0) {  // one more bf16 rounding on top of the stored product (<= 1 ulp)
-        const i32x4 old = obuf[u][k];
-        const uint32_t keep = EPI == 2 ? mbuf[u][k] : 0xFFu;
-        float f[8];
+      for (int k = 0; k < KO; ++k) {
+        const int r = 8 * k + (lane >> 3), c = lane & 7;
+        i32x4 o = *reinterpret_cast<const i32x4*>(stg + r * 128 + ((c ^ (r & 7)) << 4));
+        if constexpr (EPI != 0) {  // one more bf16 rounding on top of the stored product (<= 1 ulp)
+          const i32x4 old = obuf[u][h][k];
+          const uint32_t keep = EPI == 2 ? mbuf[u][h][k] : 0xFFu;
+          float f[8];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t w = (uint32_t)o[j], ow = (uint32_t)old[j];
-          f[2 * j] = __uint_as_float(w << 16) + (((keep >> (2 * j)) & 1u) ? __uint_as_float(ow << 16) : 0.f);
-          f[2 * j + 1] = __uint_as_float(w & 0xFFFF0000u) +
-                         (((keep >> (2 * j + 1)) & 1u) ? __uint_as_float(ow & 0xFFFF0000u) : 0.f);
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t w = (uint32_t)o[j], ow = (uint32_t)old[j];
+            f[2 * j] = __uint_as_float(w << 16) + (((keep >> (2 * j)) & 1u) ? __uint_as_float(ow << 16) : 0.f);
+            f[2 * j + 1] = __uint_as_float(w & 0xFFFF0000u) +
+                           (((keep >> (2 * j + 1)) & 1u) ? __uint_as_float(ow & 0xFFFF0000u) : 0.f);
+          }
+          o = __builtin_bit_cast(i32x4, pack_bf16x8(f));
         }
-        o = __builtin_bit_cast(i32x4, pack_bf16x8(f));
+        bstore16(o, cb + h * 128 + k * n8, rc);
       }
-      bstore16(o, cb + k * n4, rc);
     }
   };
 
@@ -356,8 +379,7 @@ void launch_gemm_short(const uint16_t* A, const uint16_t* B, long ldb, bool b_mn
   if (epi != 0 && stats) throw std::runtime_error("gemm_short: statistics only with a plain store");
   gsk::Args g{A, B, C, add, mask, xf, stats, M, N, K, (int)ldb, N / gsk::BN, 0};
   // Cfg::OCC blocks per CU; the P panels of one row group share an XCD, so blocks come in multiples of 8 P
-  const bool heavy = epi != 0 || (xf && stats);
-  const int per_chip = (K == 256 || (K == 128 && heavy) || (K == 64 && epi == 2)) ? 256 : 512;  // Cfg::OCC
+  const int per_chip = 512;  // Cfg::OCC = 2 blocks per CU
   const int gx = (per_chip / (8 * g.P)) > 1 ? per_chip / (8 * g.P) : 1;
   g.G = 8 * gx;
   const dim3 grid(8 * g.P * gx), block(gsk::THREADS);

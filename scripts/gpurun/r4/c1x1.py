@@ -34,11 +34,13 @@ for H, C, K in [(56, 256, 64), (56, 64, 256), (28, 512, 128), (28, 128, 512), (1
     x = torch.randn(N, H, H, C, device=d, dtype=torch.bfloat16)
     w = (torch.randn(K, 1, 1, C, device=d) * C ** -0.5).bfloat16()
     st = torch.zeros(C_.conv_stat_replicas, 2, K, device=d)
+    xfp = torch.cat([torch.rand(C, device=d) + 0.5, torch.randn(C, device=d) * 0.1]).contiguous()
     x2, w2 = x.view(-1, C), w.view(K, C)
     M = x2.shape[0]
     r = {"MNK": [M, K, C],
          "conv_stats": timed(lambda: C_.conv_fwd(x, w, 1, 0, 1, False, None, 0, st)),
          "conv_nostats": timed(lambda: C_.conv_fwd(x, w, 1, 0, 1, False, None, 0, None)),
+         "conv_xf_stats": timed(lambda: C_.conv_fwd(x, w, 1, 0, 1, False, None, 0, st, xform=xfp)),
          "gemm": timed(lambda: C_.gemm(x2, True, w2, True, None, False, None, 0, None, False, 1.0, 1)),
          "blas": timed(lambda: torch.matmul(x2, w2.t()))}
     # data gradient of the same layer: dx[M, C] = dy[M, K] . w[K, C] (reduction K), plain and onto a masked addend
