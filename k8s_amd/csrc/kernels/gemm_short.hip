@@ -23,7 +23,7 @@
 //  * optional: per-column sum / sum of squares of the stored bf16 values (the BatchNorm statistics, kept in
 //    registers for the whole sweep and reduced once), A normalised on load (relu(a * scale[k] + shift[k]), the
 //    BatchNorm of the previous layer), and a bf16 addend -- the old C, or a second tensor with packed ReLU bits
-//    (a residual gradient) -- prefetched one tile ahead with the A fragments, in the copy-out layout.
+//    (a residual gradient) -- prefetched as far ahead as the A fragments, in the copy-out layout.
 // Measured (profiles/r04_gemm_short_final_ab.jsonl): 1.05-1.35x the tile kernel per ResNet-50 layer; ResNet-50 b1024
 // 13.81k -> 14.15k img/s on one box.
 #include <stdexcept>
@@ -66,7 +66,7 @@ struct Cfg {
   // epilogues then overlap across the two waves; at one wave per SIMD with 32-row tiles they serialised)
   static constexpr int TM = HEAVY || K == 256 ? 16 : 32;
   static constexpr int OCC = 2;
-  static constexpr int NBUF = !HEAVY && K != 128 ? 3 : 2;
+  static constexpr int NBUF = (!HEAVY && K != 128) || (EPI != 0 && K <= 128) ? 3 : 2;
 };
 
 __device__ __forceinline__ mfma_bf16x8 as_frag(i32x4 v) { return __builtin_bit_cast(mfma_bf16x8, v); }
@@ -214,7 +214,7 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
   auto tile = [&](auto u_c, int t) __attribute__((always_inline)) {
     constexpr int u = decltype(u_c)::value;
     load_a(abuf[(u + D) % NBUF], t + D);
-    load_add((u + 1) % NBUF, t + 1);
+    load_add((u + D) % NBUF, t + D);
     // the prefetch is issued before this tile's first wait: stores may complete out of order with loads, so a
     // load is waited for by draining to the number of LOADS issued after it -- those must already be in flight
     __builtin_amdgcn_sched_barrier(0);
@@ -316,13 +316,13 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
     }
   };
 
-  // prologue: the loads of a round (A of tiles 0 .. D - 1, the addend of tile 0) in the loop's order; then whole
+  // prologue: the loads of a round (A and addend of tiles 0 .. D - 1) in the loop's order; then whole
   // rounds with no branch inside (a skipped tile leaves its loads outstanding on one path, and the compiler's
   // wait state at the loop head -- the merge of all paths -- then drained the counter once per round); then the tail
   sfor<NBUF>([&](auto u) __attribute__((always_inline)) {
     constexpr int uu = decltype(u)::value;
     load_a(abuf[(uu + D) % NBUF], uu - NBUF + D);
-    load_add((uu + 1) % NBUF, uu - NBUF + 1);
+    load_add((uu + D) % NBUF, uu - NBUF + D);
   });
   int t0 = 0;
   for (; t0 + NBUF <= nt; t0 += NBUF) sfor<NBUF>([&](auto u) __attribute__((always_inline)) { tile(u, t0 + decltype(u)::value); });
