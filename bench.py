@@ -57,6 +57,8 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=1024, help="per-GPU batch")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--grad-comm", choices=["fp32", "bf16"], default="fp32",
+                    help="gradient all-reduce transport (bf16: all-to-all + fp32 owner sum + all-gather)")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--profile-steps", type=int, default=0, help="(internal) roctx-free short run")
     return ap.parse_args(argv)
@@ -104,6 +106,30 @@ def _launch_local_ranks(a, argv) -> int:
     return bad[0] if bad else 0
 
 
+def _comm_record(n, dev):
+    """backend / RCCL version / world size as the live process group reports them (not as requested)."""
+    import torch.distributed as tdist
+
+    rec = {"backend": "none", "world_size": 1, "rccl_version": None}
+    if tdist.is_available() and tdist.is_initialized():
+        rec["backend"] = str(tdist.get_backend())
+        rec["world_size"] = int(tdist.get_world_size())
+    if dev.type == "cuda":
+        try:
+            v = torch.cuda.nccl.version()
+            rec["rccl_version"] = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+        except Exception as e:  # noqa: BLE001 -- recorded, not fatal
+            rec["rccl_version"] = "unavailable: %s" % e
+        rec["device"] = torch.cuda.get_device_name(dev)
+        try:
+            from k8s_amd.ops._ext import load as _load_ext
+
+            rec["planner_cus"] = int(_load_ext().planner_cus())
+        except Exception:  # noqa: BLE001
+            pass
+    return rec
+
+
 def main(argv=None):
     a = parse(argv)
     if a.gpus > 1 and "RANK" not in os.environ and "WORLD_SIZE" not in os.environ:
@@ -125,8 +151,20 @@ def main(argv=None):
     if n > 1:
         torch.distributed.broadcast(store.master, 0)
         store.refresh_lowp()
-    reducer = GradReducer(store, bucket_mb=a.bucket_mb)
+    reducer = GradReducer(store, bucket_mb=a.bucket_mb,
+                          comm_dtype=torch.bfloat16 if a.grad_comm == "bf16" else torch.float32)
     opt = FusedSGD(store, lr=a.lr, momentum=0.9, weight_decay=5e-5, nesterov=False)
+    # what the collectives actually ran on, read from the process group after its first collective (the broadcast
+    # above): the driver's multi-GPU record must show by itself that RCCL initialised with every rank
+    comm = _comm_record(n, dev)
+    # step-0 transport self-check (untimed): one gradient bucket through the configured transport vs a plain fp32
+    # all_reduce of the same data; a mismatch beyond the transport's rounding fails the run before any number
+    check = reducer.self_check()
+    if not check["ok"]:
+        if info.rank == 0:
+            print("error: gradient transport self-check failed: %s" % json.dumps(check), file=sys.stderr)
+        kdist.destroy()
+        return 3
 
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
     images = torch.randn(a.batch, a.image, a.image, 3, device=dev, dtype=dtype)
@@ -211,6 +249,8 @@ def main(argv=None):
             "final_loss": round(final_loss, 4),
             "replicas_identical": identical,
             "comm_exposed_ms": round(exposed_ms, 3),
+            "comm": comm,
+            "transport_check": check,
             "grad_comm_fallbacks": dict(reducer.fallbacks),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if dev.type == "cuda" else None,
         }

@@ -779,7 +779,8 @@ int flash_dkv_splits(int B, int Sq, int Sk, int Hkv, int causal) {
   const int per_block = (Sq + 63) / 64;  // query tiles of the heaviest key block (per query head)
   if (per_block < 8) return 1;
   // measured at 512 key blocks (Llama-3-8B s4096 / s2048 b2): 2 chunks 585 / 357 us, 4 chunks 601 / 367, 8 chunks 668 / 435
-  return nblk >= 1024 ? 1 : (nblk >= 384 ? 2 : 4);
+  const long cus = planner_cus();  // thresholds measured on 256 CUs: 1024 and 384 key blocks
+  return nblk >= 4 * cus ? 1 : (2 * nblk >= 3 * cus ? 2 : 4);
 }
 
 void launch_flash_fwd(const AttnFwdArgs& a, int D, hipStream_t st) {
@@ -807,7 +808,7 @@ void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, 
   // (D = 128, or D = 64 on 128-key tiles) that form needs ~320 VGPRs (one wave per SIMD) and measured slower there
   // (round 3), so those keep QS = 1.
   const bool small = D == 64 && !big_tile(D, a.Sq);
-  const bool qs2 = small && (long)((a.Sq + 127) / 128) * a.Hq * a.B >= 512;
+  const bool qs2 = small && (long)((a.Sq + 127) / 128) * a.Hq * a.B >= 2L * planner_cus();
   const dim3 gq(((a.Sq + (qs2 ? 127 : 63)) / (qs2 ? 128 : 64)) * a.Hq * a.B), blk(FA_THREADS);
   if (D == 128) {
     hipLaunchKernelGGL((flash_bwd_dkv_kernel<128, 64>), gkv, blk, 0, st, a);

@@ -59,11 +59,12 @@ static inline BnGeom bn_geom(int C, long M) {
   BnGeom g;
   g.cgroups = C / 8;
   g.tpr = g.cgroups < BN_THREADS ? g.cgroups : BN_THREADS;
+  const long cus = planner_cus();  // 4 row-blocks per CU at most, 3 per CU counted as full
   long nbx = M / 64;
-  nbx = nbx < 1 ? 1 : (nbx > 1024 ? 1024 : nbx);
+  nbx = nbx < 1 ? 1 : (nbx > 4 * cus ? 4 * cus : nbx);
   for (;;) {
     g.grid_y = (g.cgroups + g.tpr - 1) / g.tpr;
-    if (nbx * g.grid_y >= 768 || g.tpr <= 8 || (g.tpr & 1)) break;
+    if (nbx * g.grid_y >= 3 * cus || g.tpr <= 8 || (g.tpr & 1)) break;
     g.tpr /= 2;
   }
   g.rows_per_iter = BN_THREADS / g.tpr;
@@ -807,7 +808,7 @@ int stream_dir(int fixed) { return fixed; }
 static long bn_rows_per_block(long M, const BnGeom& g) {
   // ~1024 blocks in total (4 per CU: enough loads in flight to cover HBM latency), at most M / 64 row-blocks,
   // >= 4 row trips per block
-  long blocks_x = 1024 / g.grid_y;
+  long blocks_x = 4L * planner_cus() / g.grid_y;
   const long cap = M / 64;
   if (blocks_x > cap) blocks_x = cap;
   if (blocks_x < 1) blocks_x = 1;
@@ -820,7 +821,7 @@ static long bn_rows_per_block(long M, const BnGeom& g) {
 
 // grid-stride reduction blocks along the rows: ~1024 in total (4 per CU)
 static int bn_reduce_blocks(long M, const BnGeom& g) {
-  long nb = 1024 / g.grid_y;
+  long nb = 4L * planner_cus() / g.grid_y;
   const long groups = (M + g.rows_per_iter - 1) / g.rows_per_iter;
   if (nb > groups) nb = groups;
   if (stream_order_mode()) nb = nb < 8 ? 8 : nb & ~7L;  // banded order: a multiple of 8 blocks (one band each)
@@ -975,7 +976,7 @@ void launch_pool_bn_bwd(const uint16_t* dpool, const uint8_t* idx, const uint16_
   if (ncells * (C / 8) >= (1L << 31)) throw std::runtime_error("pool_bn_bwd: tensor too large");
   const int cpb = BN_THREADS / (C / 8);
   long nb = (ncells + cpb - 1) / cpb;
-  nb = nb > 4096 ? 4096 : nb;  // ~16 blocks per CU: enough loads in flight (a 1024-block grid ran at half the roof)
+  nb = std::min(nb, 16L * planner_cus());  // ~16 blocks per CU: enough loads in flight (a 1024-block grid ran at half the roof)
   hipLaunchKernelGGL(pool_bn_bwd_reduce_kernel, dim3((unsigned)nb), dim3(BN_THREADS), 0, st, dpool, idx, x, mean,
                      invstd, gamma, beta, H, W, C, Ho, Wo, Hc, Wc, (int)ncells, work, make_fastdiv(Wc),
                      make_fastdiv(Hc));

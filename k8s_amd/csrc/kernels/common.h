@@ -99,10 +99,20 @@ inline FastDiv make_fastdiv(int d) {
 
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
-// Memory-bound launch sizing: cap at 256 CUs x 8 blocks and grid-stride.
+// CUs the launch planners size their grids for (wave quantisation, persistent grids, stream-K tails, split-K
+// fill targets, grid-stride caps). Default: the current device's hipDeviceAttributeMultiprocessorCount (256 on
+// MI355X), queried once per device. An override (set_planner_cus, or $K8S_AMD_PLANNER_CUS read on first use)
+// replaces it for every device: a rank whose CUs are partly taken by concurrently running RCCL kernels can plan
+// for fewer, and the GPU tests force odd budgets to check that every planner stays correct off the 256 grid.
+// Defined in ops_binding.cpp's translation unit set (planner.cpp) so all kernels share one value.
+int planner_cus();
+void set_planner_cus(int n);  // n <= 0: back to the device's count
+
+// Memory-bound launch sizing: at most 8 blocks per CU, grid-stride beyond that.
 inline int stream_grid(long work_items, int block) {
   long g = (work_items + block - 1) / block;
-  if (g > 2048) g = 2048;
+  const long cap = 8L * planner_cus();
+  if (g > cap) g = cap;
   if (g < 1) g = 1;
   return (int)g;
 }

@@ -1027,7 +1027,7 @@ static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act,
 // Choose split-K for small-MN / tall-K products (weight gradients) with a wave-quantisation cost model:
 //   T(s) = ceil(tiles * s / slots) * ceil(ktiles / s)            -- block rounds x K tiles per block
 //        + s * M * N * 8 B / HBM BW / t_ktile                     -- fp32 slab write + reduce read per split
-// slots = resident blocks on 256 CUs (2 per CU double-buffered, 3 single-buffered). The previous rule
+// slots = resident blocks on the chip's CUs (planner_cus(); 2 per CU double-buffered, 3 single-buffered). The previous rule
 // (double s until tiles * s >= 512) landed most ResNet-50 3x3 weight gradients on 576 blocks = 1.125
 // rounds; measured on MI355X (scripts/sweep_wgrad_splits.py) the model's choice is 1.3-1.5x faster there.
 // At most 256 splits: measured with up to 1024, the single-tile 64x64 1x1 weight gradient got slower (134 ->
@@ -1036,12 +1036,13 @@ int gemm_choose_splits(int M, int N, int K) {
   const long tiles = (long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const int ktiles = (K + BK - 1) / BK;
   const double slab_cost = (double)M * N * 8.0 / 5.0e12 / 2.0e-6;  // in units of one K tile (~2 us / block)
+  const long cus = planner_cus();
   int best_s = 1;
   double best = 1e30;
   for (int s = 1; s <= 256 && s <= ktiles; ++s) {
     const int kpt = (ktiles + s - 1) / s;       // K tiles per split
     if ((ktiles + kpt - 1) / kpt != s) continue;  // same kps as a smaller s
-    const long slots = kpt * BK <= single_buf_maxk() ? 3 * 256 : 2 * 256;
+    const long slots = kpt * BK <= single_buf_maxk() ? 3 * cus : 2 * cus;
     const long rounds = (tiles * s + slots - 1) / slots;
     const double t = (double)rounds * kpt + (s > 1 ? s * slab_cost : 0.0);
     if (t < best * 0.999) {

@@ -887,11 +887,11 @@ static bool w4_ok(bool a_kmajor, bool b_kmajor, bool c_f32, int M, int N, int K,
   (void)a_kmajor;  // every operand layout: K-major (read as rows) or MN-major (transposed reads)
   (void)b_kmajor;
   return !bias && act == 0 && !pre && (!accumulate || c_f32) && splits == 1 && M % 256 == 0 && N % 256 == 0 &&
-         K % 64 == 0 && (lda | ldb | ldc) % 8 == 0 && (M / 256) * (N / 256) >= 256;
+         K % 64 == 0 && (lda | ldb | ldc) % 8 == 0 && (M / 256) * (N / 256) >= planner_cus();
 }
 
-// Stream-K tail plan for a grid of 256 x 256 tiles on 256 CUs (one block per CU): with T = w * 256 + r tiles and
-// 0 < r <= 128, the last r tiles are split sk = min(256 / r, 4) ways along K (each split a multiple of 64 deep and
+// Stream-K tail plan for a grid of 256 x 256 tiles on P = planner_cus() CUs (one block per CU; 256 on MI355X): with
+// T = w * P + r tiles and 0 < r <= P / 2, the last r tiles are split sk = min(P / r, 4) ways along K (each split a multiple of 64 deep and
 // >= 512), so the tail costs ~1/sk of a wave (+ the fix-up) instead of a whole one. Not for grids of 8+ waves (the
 // tail is then a small fraction) or when the split would be too shallow.
 Gemm256Plan gemm256_plan(int M, int N, int K) {
@@ -900,7 +900,7 @@ Gemm256Plan gemm256_plan(int M, int N, int K) {
   p.full = p.tiles;
   p.sk = 1;
   p.kps = K;
-  constexpr int P = 256;
+  const int P = planner_cus();
   const int waves = p.tiles / P, r = p.tiles % P;
   // sub-wave grids (waves == 0, e.g. BERT's M = 8192 x N = 768 products, 96 tiles) stay on the 128 x 128 kernel:
   // split 2 ways onto this kernel they measured 72-82 us per call in the BERT step against 51-62 us there
@@ -934,24 +934,27 @@ bool gemm256_eligible(int M, int N, int K, bool a_kmajor, bool b_kmajor) {
   if (N % 4 != 0) return false;
   const Gemm256Plan plan = gemm256_plan(M, N, K);
   const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
-  // waves of 256 tiles, the stream-K tail counted as 1/sk of a wave (+5 % for its fix-up)
-  const double w256 = plan.sk > 1 ? plan.full / 256 + 1.05 / plan.sk : (double)((plan.tiles + 255) / 256);
+  const long P = planner_cus();
+  // waves of P tiles, the stream-K tail counted as 1/sk of a wave (+5 % for its fix-up)
+  const double w256 = plan.sk > 1 ? plan.full / P + 1.05 / plan.sk : (double)((plan.tiles + P - 1) / P);
   const double c256 = w256 * 65536.0 / 1.25;
-  const double c128 = (double)((t128 + 511) / 512) * 32768.0;
+  const double c128 = (double)((t128 + 2 * P - 1) / (2 * P)) * 32768.0;
   return c256 <= c128;
 }
 
 // Split-K for the tall-K fp32 products (weight gradients of small output, e.g. ResNet's 1x1 layers: 256 x 1024
 // outputs over 200k pixels): the smallest split count that puts >= 192 blocks on the chip, each split a multiple of
 // 64 deep and >= 1024 (the ring's prologue / epilogue), at most 64 splits. 1 when the tiles alone fill the chip.
+// ("Fill" = 3/4 of planner_cus(): 192 blocks on MI355X's 256 CUs.)
 int gemm256_choose_splits(int M, int N, int K) {
   const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
+  const long fill = 3L * planner_cus() / 4;
   int best = 1;
   for (int s = 2; s <= 64; ++s) {
-    if (tiles * (s / 2) >= 192) break;  // the previous s already filled the chip
+    if (tiles * (s / 2) >= fill) break;  // the previous s already filled the chip
     if (K % (64 * s) != 0 || K / s < 1024) continue;
     best = s;
-    if (tiles * s >= 192) break;
+    if (tiles * s >= fill) break;
   }
   return best;
 }

@@ -379,7 +379,7 @@ void launch_gemm_short(const uint16_t* A, const uint16_t* B, long ldb, bool b_mn
   if (epi != 0 && stats) throw std::runtime_error("gemm_short: statistics only with a plain store");
   gsk::Args g{A, B, C, add, mask, xf, stats, M, N, K, (int)ldb, N / gsk::BN, 0};
   // Cfg::OCC blocks per CU; the P panels of one row group share an XCD, so blocks come in multiples of 8 P
-  const int per_chip = 512;  // Cfg::OCC = 2 blocks per CU
+  const int per_chip = 2 * planner_cus();  // Cfg::OCC = 2 blocks per CU
   const int gx = (per_chip / (8 * g.P)) > 1 ? per_chip / (8 * g.P) : 1;
   g.G = 8 * gx;
   const dim3 grid(8 * g.P * gx), block(gsk::THREADS);

@@ -7,6 +7,10 @@
 
 namespace k8s_amd {
 
+// planner.hip: the CU count every launch planner sizes its grid for (see common.h)
+int planner_cus();
+void set_planner_cus(int n);
+
 // optim.hip
 void launch_sgd(float* p, float* mom, const void* g, bool g_bf16, uint16_t* pbf, long n, const uint8_t* decay_mask, float lr,
                 float mu, float wd, float scale, const float* scale_ptr, const float* hyper, bool nesterov,

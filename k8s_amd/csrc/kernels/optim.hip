@@ -261,8 +261,8 @@ void launch_adam(float* p, float* m1, float* m2, const void* g, bool g_bf16, uin
 
 void launch_sumsq(const void* g, bool g_bf16, long n, float* out, hipStream_t st) {
   const long n4 = n / 4;
-  // 8 blocks of 256 per CU (2048): enough loads in flight to stream, few enough atomics
-  const int grid = stream_grid(n4, 256) > 2048 ? 2048 : stream_grid(n4, 256);
+  // 8 blocks of 256 per CU (stream_grid's cap): enough loads in flight to stream, few enough atomics
+  const int grid = stream_grid(n4, 256);
   if (g_bf16)
     hipLaunchKernelGGL(sumsq_kernel<uint16_t>, dim3(grid), dim3(256), 0, st, (const uint16_t*)g, n4, out);
   else

@@ -326,7 +326,7 @@ __global__ void __launch_bounds__(256, 3) stem_wgrad_kernel(const uint16_t* __re
 
 int stem_wgrad_blocks(int N, int Hs) {
   const long ntiles = (long)N * ((Hs - 3 + SWG_RT - 1) / SWG_RT);
-  return (int)std::min<long>(ntiles, 768);  // persistent: 3 blocks per CU (47 KB LDS, ~130 VGPRs)
+  return (int)std::min<long>(ntiles, 3L * planner_cus());  // persistent: 3 blocks per CU (47 KB LDS, ~130 VGPRs)
 }
 
 void launch_stem_wgrad(const uint16_t* xs, const uint16_t* dy, float* ws, float* dw4, int N, int Hs, int Ws,

@@ -205,7 +205,7 @@ static int wg3_rt(int W) { return W == 56 ? 4 : W == 28 ? 8 : W == 16 ? 2 : 16; 
 int wgrad3x3_tiled_blocks(int N, int H, int W, int C) {
   const int pieces = (C / wg3::CS) * (C / wg3::CS);
   const long tiles = (long)N * ((H + wg3_rt(W) - 1) / wg3_rt(W));
-  return (int)std::max<long>(1, std::min<long>(tiles, std::max(512 / pieces, 32)));
+  return (int)std::max<long>(1, std::min<long>(tiles, std::max(2 * planner_cus() / pieces, 32)));
 }
 
 static int wg3_groups(int nb) { return std::max(1, nb / 16); }

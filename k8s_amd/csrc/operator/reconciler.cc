@@ -208,10 +208,10 @@ bool TrainingJob::update_status() {
 }
 
 void TrainingJob::record_event(const std::string& type, const std::string& reason, const std::string& message) {
-  const std::string key = reason + "\n" + message;
+  const std::string ev_key = reason + "\n" + message;
   const std::string now = now_rfc3339();
   const std::string ns = job_.ns();
-  auto it = events_.find(key);
+  auto it = events_.find(ev_key);
   if (it != events_.end()) {  // seen before: count + 1 on the stored object (carries its resourceVersion)
     Json ev = it->second.clone();
     ev["count"] = (long long)(ev.find("count") && ev.at("count").is_number() ? ev.at("count").as_int() : 1) + 1;
@@ -219,7 +219,7 @@ void TrainingJob::record_event(const std::string& type, const std::string& reaso
     const std::string name = ev.find("metadata") ? get_str(ev.at("metadata"), "name") : "";
     ApiResult r = call("PUT", core_path(ns, "events", name), &ev);
     if (r.ok()) it->second = r.body;
-    else log_v(1, "job %s: could not update event %s: HTTP %d", key.c_str(), name.c_str(), r.code);
+    else log_v(1, "job %s: could not update event %s: HTTP %d", key().c_str(), name.c_str(), r.code);
     return;
   }
   Json ev = Json::object();
@@ -246,7 +246,7 @@ void TrainingJob::record_event(const std::string& type, const std::string& reaso
   src["component"] = "tf-operator";
   ev["source"] = src;
   ApiResult r = call("POST", core_path(ns, "events"), &ev);
-  if (r.ok()) events_[key] = r.body.is_object() ? r.body : ev;
+  if (r.ok()) events_[ev_key] = r.body.is_object() ? r.body : ev;
   else log_v(1, "job %s: could not record event %s: HTTP %d", this->key().c_str(), reason.c_str(), r.code);
 }
 

@@ -444,14 +444,15 @@ static bool use_gemm256(long M, long N, long K, bool a_kmajor, bool b_kmajor) {
   return m != 0 && k8s_amd::gemm256_eligible((int)M, (int)N, (int)K, a_kmajor, b_kmajor);
 }
 
-// Zero-initialised int words for the stream-K tickets / flags, one buffer per device, grown on demand. The kernel
-// leaves every word it used at zero again, so no per-call clear is needed. GEMMs run on one compute stream, so one
-// buffer per device is never used by two launches at once.
+// Zero-initialised int words for the stream-K tickets / flags, one buffer per (device, stream), grown on demand.
+// The kernel leaves every word it used at zero again, so no per-call clear is needed; launches on one stream are
+// ordered, so they never share the words concurrently, and two streams (a side stream, user streams) get their own.
 static int* sk_sync_words(long n, const c10::Device& dev) {
   static std::mutex mu;
-  static std::map<int, Tensor> bufs;
+  static std::map<std::pair<int, int64_t>, Tensor> bufs;
+  const int64_t sid = at::hip::getCurrentHIPStream(dev.index()).id();
   std::lock_guard<std::mutex> g(mu);
-  Tensor& t = bufs[dev.index()];
+  Tensor& t = bufs[{dev.index(), sid}];
   if (!t.defined() || t.numel() < n)
     t = torch::zeros({std::max<long>(n, 1 << 16)}, torch::TensorOptions().dtype(at::kInt).device(dev));
   return t.data_ptr<int>();
@@ -1096,5 +1097,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("conv_stat_replicas") = k8s_amd::kConvStatReplicas;
   m.def("gemm_short_ok", [](int64_t M, int64_t N, int64_t K) { return k8s_amd::gemm_short_ok((int)M, (int)N, (int)K, K, N); },
         "whether C[M,N] = A[M,K] . B^T (contiguous) takes the short-K streaming kernel (gemm_short.hip)");
+  m.def("planner_cus", &k8s_amd::planner_cus,
+        "CUs the launch planners size grids for (the device's multiprocessor count unless overridden)");
+  m.def("set_planner_cus", &k8s_amd::set_planner_cus, py::arg("n"),
+        "override the planners' CU budget for every device (n <= 0: back to the device's count)");
   m.attr("arch") = "gfx950";
 }

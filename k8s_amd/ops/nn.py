@@ -279,6 +279,8 @@ class _BnAct(torch.autograd.Function):
 # costs the staged forward +0.36 ms and the tiled weight gradient +0.71 ms (a VALU / LDS phase between the window
 # DMA and the MFMAs): 13.78-13.84k vs 13.85-13.87k img/s, so it stays opt-in.
 BN_ONLOAD = os.environ.get("K8S_AMD_BN_ONLOAD", "1x1")
+if BN_ONLOAD not in ("0", "1x1", "3x3"):  # an unknown value must not quietly mean "1x1"
+    raise ValueError("K8S_AMD_BN_ONLOAD must be 0 (BN applied by its own pass), 1x1 or 3x3, not %r" % BN_ONLOAD)
 
 
 def _bn_param_grads(store, pg, pb, device):
@@ -335,6 +337,8 @@ class _BnReluConv(torch.autograd.Function):
 def onload_ok(x, conv) -> bool:
     """Whether ``conv`` can consume relu(BN(x)) normalised on load in all three of its products: a 1x1 stride-1
     convolution (the GEMM operand paths), or a 3x3 one the staged-window kernels take (``BN_ONLOAD == "3x3"``)."""
+    if BN_ONLOAD == "0":
+        return False
     K_, R, S, C = conv.w.shape
     if R == 1 and S == 1:
         return conv.stride == 1 and conv.pad == 0

@@ -34,7 +34,8 @@ backward; ``finish()`` only joins that stream. (The ZeRO-1 sharded service,
 """
 from __future__ import annotations
 
-from typing import List, Optional
+import os
+from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -87,14 +88,39 @@ class GradReducer:
         self.next_launch = 0
         self.side = torch.cuda.Stream(store.grad.device) if (store.grad.is_cuda and self.enabled) else None
         self.side_busy = False
-        self.padded = 0  # bf16 exchanges zero-padded to a multiple of the world (counted, reported by bench.py)
+        self.padded = set()  # indices of the buckets whose bf16 exchange is zero-padded to a multiple of the world
+        # fault injection for the transport self-check's own test: a wrong reduction (MAX instead of SUM, or one
+        # rank's bf16 contribution dropped) that the check must catch
+        self.fault = os.environ.get("K8S_AMD_FAULT_TRANSPORT") == "1"
         store.hooks.append(self._on_deposit)
 
     @property
     def fallbacks(self):
         """Transport deviations from the requested ``comm_dtype`` (none: a ragged bucket is padded, not demoted to
         fp32); reported next to the GEMM fallbacks so the multi-GPU harness never changes transport silently."""
-        return {"bf16_padded_buckets": self.padded} if self.padded else {}
+        return {"bf16_padded_buckets": len(self.padded)} if self.padded else {}
+
+    def _slice_sum(self, recv, n, out_bf):
+        w = self.world - 1 if self.fault else self.world
+        slice_sum(recv[:w * n], w, None, out_bf)
+
+    def self_check(self) -> Dict[str, object]:
+        """Step-0 transport check (outside any timed region): reduce bucket 0 with the configured transport and
+        with a plain fp32 ``all_reduce`` of the same data, and compare within the transport's rounding. Collective;
+        the bucket's gradient range is restored afterwards."""
+        if not self.enabled or not self.buckets:
+            return {"ok": True, "transport": "none (world 1)"}
+        b = self.buckets[0]
+
+        def run():
+            self.works = []
+            b.launched = False
+            self._launch(b)
+            self._drain()
+            b.launched = False
+
+        return transport_check(self.store.grad, b.lo, b.hi, (b.lo, b.hi), run, self.comm_dtype, self.group,
+                               "allreduce-" + ("bf16" if self.comm_dtype == torch.bfloat16 else "fp32"))
 
     # ------------------------------------------------------------------ step protocol
     def begin_step(self):
@@ -133,7 +159,7 @@ class GradReducer:
             else:  # a world that does not divide the 64-element alignment (e.g. 7 ranks): zero-padded exchange
                 send = torch.zeros(_round_up(length, self.world), dtype=torch.bfloat16, device=t.device)
                 send[:length].copy_(cast_bf16(t))
-                self.padded += 1
+                self.padded.add(b.index)
             recv = torch.empty_like(send)
             w = dist.all_to_all_single(recv, send, group=self.group, async_op=True)
             if self.side is None:
@@ -146,15 +172,15 @@ class GradReducer:
                 # the reduced slice lands in this rank's own chunk of `send` (already on the wire), then the
                 # all-gather fills the other chunks in place and the bucket is expanded back to fp32
                 red = send[me * n:(me + 1) * n]
-                slice_sum(recv, self.world, None, red)
+                self._slice_sum(recv, n, red)
                 dist.all_gather_into_tensor(send, red, group=self.group, async_op=True).wait()
                 t.copy_(send[:length])
             send.record_stream(self.side)
             recv.record_stream(self.side)
             self.side_busy = True
         else:
-            self.works.append((b, None, None, dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group,
-                                                              async_op=True)))
+            op = dist.ReduceOp.MAX if self.fault else dist.ReduceOp.SUM
+            self.works.append((b, None, None, dist.all_reduce(t, op=op, group=self.group, async_op=True)))
 
     def finish(self):
         """Zero never-used gradients, flush remaining buckets, order the current stream after RCCL."""
@@ -167,23 +193,64 @@ class GradReducer:
                 b.pending = 0
         if self.enabled:
             self._launch_ready()
-            gathers = []
-            for b, send, recv, w in self.works:
-                w.wait()
-                if send is None:
-                    continue
-                n = send.numel() // self.world
-                red = torch.empty(n, dtype=torch.bfloat16, device=recv.device)
-                slice_sum(recv, self.world, None, red)  # fp32 accumulate in rank order, one rounding
-                gathers.append((b, send, dist.all_gather_into_tensor(send, red, group=self.group, async_op=True)))
-            for b, full, w in gathers:
-                w.wait()
-                self.store.grad[b.lo:b.hi].copy_(full[:b.hi - b.lo])
-            if self.side_busy:
-                torch.cuda.current_stream(self.store.grad.device).wait_stream(self.side)
-                self.side_busy = False
+            self._drain()
+        self.works = []
+
+    def _drain(self):
+        """Wait for every launched bucket (host-side for gloo; device-side ordering for RCCL)."""
+        gathers = []
+        for b, send, recv, w in self.works:
+            w.wait()
+            if send is None:
+                continue
+            n = send.numel() // self.world
+            red = torch.empty(n, dtype=torch.bfloat16, device=recv.device)
+            self._slice_sum(recv, n, red)  # fp32 accumulate in rank order, one rounding
+            gathers.append((b, send, dist.all_gather_into_tensor(send, red, group=self.group, async_op=True)))
+        for b, full, w in gathers:
+            w.wait()
+            self.store.grad[b.lo:b.hi].copy_(full[:b.hi - b.lo])
+        if self.side_busy:
+            torch.cuda.current_stream(self.store.grad.device).wait_stream(self.side)
+            self.side_busy = False
         self.works = []
 
     @property
     def grad_scale(self) -> float:
         return 1.0 / self.world if self.enabled else 1.0
+
+
+def transport_check(grad: torch.Tensor, lo: int, hi: int, cmp: Tuple[int, int], run: Callable[[], None],
+                    comm_dtype: torch.dtype, group=None, name: str = "") -> Dict[str, object]:
+    """Shared body of the step-0 transport self-checks (``GradReducer.self_check``,
+    ``ShardedParameterService.self_check``): fill ``grad[lo:hi]`` with rank-seeded normal values, reduce a copy
+    with a plain fp32 ``all_reduce`` (the reference), run the configured transport (``run``), and compare
+    ``grad[cmp]`` with the reference's same range.
+
+    Tolerance per element: ``2^-7 * sum_r |x_r|`` for a bf16 transport (each rank's contribution and the reduced
+    value are rounded to bf16 once: <= 2^-8 relative each) and ``1e-5 * sum_r |x_r|`` for fp32 (summation order only).
+    A transport that drops or duplicates a contribution, misorders streams, or reduces with the wrong operator is
+    off by about one rank's |x| -- tens of times the bound at any world size the pool has. The verdict is made
+    identical on every rank (MAX of the per-rank error ratio)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    g = grad[lo:hi]
+    save = g.clone()
+    gen = torch.Generator(device=g.device)
+    gen.manual_seed(0x5EED + 7919 * rank)
+    x = torch.randn(g.shape, generator=gen, device=g.device, dtype=g.dtype)
+    g.copy_(x)
+    ref = x.clone()
+    dist.all_reduce(ref, group=group)
+    mag = x.abs()
+    dist.all_reduce(mag, group=group)
+    run()
+    a, b = cmp[0] - lo, cmp[1] - lo
+    tol = (2.0 ** -7 if comm_dtype == torch.bfloat16 else 1e-5) * mag[a:b] + 1e-30
+    ratio = ((g[a:b] - ref[a:b]).abs() / tol).max() if b > a else torch.zeros((), device=g.device)
+    worst = torch.tensor([float(ratio)], dtype=torch.float64, device=g.device)
+    dist.all_reduce(worst, op=dist.ReduceOp.MAX, group=group)
+    g.copy_(save)
+    worst_v = float(worst.item())
+    return {"ok": bool(worst_v <= 1.0), "transport": name, "world": world, "elements": int(hi - lo),
+            "max_err_over_tol": round(worst_v, 4)}

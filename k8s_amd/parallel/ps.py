@@ -60,6 +60,7 @@ resumes from the newest committed snapshot (``parallel/ps_vars.py``).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -115,6 +116,7 @@ class ShardedParameterService:
         # bf16 pushes on the GPU: the owner's fp32 sum runs on this stream, device-ordered behind each exchange
         self.side = (torch.cuda.Stream(store.grad.device) if store.grad.is_cuda and self.world > 1 else None)
         self.side_busy = False
+        self.fault = os.environ.get("K8S_AMD_FAULT_TRANSPORT") == "1"  # see GradReducer.fault
         store.hooks.append(self._on_deposit)
         # pull: "lowp" = bf16 working copy + fp32 non-lowp parameters (GPU default), "fp32" = the full fp32 master
         if pull not in ("auto", "lowp", "fp32"):
@@ -139,7 +141,8 @@ class ShardedParameterService:
 
     # ---------------------------------------------------------------- step protocol
     def begin_step(self):
-        self.store.wait_pending()  # every bucket of the last pull, read by this step's forward or not
+        # (no wait for the last pull here: each bucket is waited by the first forward layer that reads it,
+        # ``Param.weight``, and the rest by ``step`` before the optimizer rewrites the working copy)
         self.store.begin_step()
         for b in self.buckets:
             b.pending = sum(p.uses for p in b.params)
@@ -169,7 +172,8 @@ class ShardedParameterService:
                 lo, hi = self.shard(b)
                 with torch.cuda.stream(self.side):
                     w.wait()  # device-side: the side stream waits for this bucket's exchange, the host does not
-                    _load_ext().slice_sum(recv, self.world, self.store.grad[lo:hi], None)
+                    nw = self.world - 1 if self.fault else self.world
+                    _load_ext().slice_sum(recv[:nw * (hi - lo)], nw, self.store.grad[lo:hi], None)
                 send.record_stream(self.side)
                 recv.record_stream(self.side)
                 self.side_busy = True
@@ -177,7 +181,8 @@ class ShardedParameterService:
                 self.a2a.append((b, send, recv, w))
         else:
             lo, hi = self.shard(b)  # in place: the output is this rank's slice of the input
-            self.works.append(dist.reduce_scatter_tensor(self.store.grad[lo:hi], g, group=self.group,
+            op = dist.ReduceOp.MAX if self.fault else dist.ReduceOp.SUM
+            self.works.append(dist.reduce_scatter_tensor(self.store.grad[lo:hi], g, op=op, group=self.group,
                                                          async_op=True))
 
     def _finish_pushes(self):
@@ -188,11 +193,30 @@ class ShardedParameterService:
             w.wait()
             lo, hi = self.shard(b)
             # fp32 accumulation of the world bf16 contributions, in rank order (deterministic)
-            slice_sum(recv, self.world, self.store.grad[lo:hi])
+            nw = self.world - 1 if self.fault else self.world
+            slice_sum(recv[:nw * (hi - lo)], nw, self.store.grad[lo:hi])
         self.a2a = []
         if self.side_busy:
             torch.cuda.current_stream(self.store.grad.device).wait_stream(self.side)
             self.side_busy = False
+
+    def self_check(self) -> Dict[str, object]:
+        """Step-0 transport check of the push (outside any timed region): push bucket 0 with the configured
+        transport and compare this rank's owned slice with a plain fp32 ``all_reduce`` of the same data
+        (``ddp.transport_check``). Collective; the bucket's gradient range is restored afterwards."""
+        from k8s_amd.parallel.ddp import transport_check
+
+        if self.world == 1 or not self.buckets:
+            return {"ok": True, "transport": "none (world 1)"}
+        b = self.buckets[0]
+
+        def run():
+            self.works, self.a2a = [], []
+            self._push(b)
+            self._finish_pushes()
+
+        name = "zero1-" + ("bf16" if self.comm_dtype == torch.bfloat16 else "fp32")
+        return transport_check(self.store.grad, b.lo, b.hi, self.shard(b), run, self.comm_dtype, self.group, name)
 
     # ---------------------------------------------------------------- bf16 pull
     def _build_f32_pack(self):
@@ -231,21 +255,28 @@ class ShardedParameterService:
         self.f32_dst_idx = torch.cat(dst).to(dev) if width else None
 
     def _pull_lowp(self):
-        """bf16 all-gather of every bucket's working copy (async; waited lazily by ``Param.weight`` or at
-        ``begin_step``), and the fp32 all-gather of the non-lowp parameters (waited here: a few hundred K values)."""
+        """The fp32 all-gather of the non-lowp parameters (a few hundred K values, waited here), then the bf16
+        all-gather of every bucket's working copy (async; waited lazily by ``Param.weight``, the rest in ``step``).
+
+        Order matters on RCCL: one communicator runs its collectives in issue order, so the small fp32 gather goes
+        FIRST (waiting on it after the bf16 buckets would wait for all of them), and the bf16 buckets go in
+        ascending offset order -- ``self.buckets`` is built from the END of the flat buffer, so that is
+        ``reversed(self.buckets)``: the first layers' weights arrive first and the next forward starts behind the
+        first bucket instead of the whole pull."""
         s = self.store
-        pending = {}
-        for b in self.buckets:  # ascending offsets: the first layers' weights are requested first
-            lo, hi = self.shard(b)
-            pending[b.index] = dist.all_gather_into_tensor(s.half[b.lo:b.hi], s.half[lo:hi], group=self.group,
-                                                           async_op=True)
-        s.set_pending(pending, self.buckets_of)
         if self.f32_width:
             send = s.master.index_select(0, self.f32_send_idx)
             recv = torch.empty(self.world * self.f32_width, dtype=send.dtype, device=send.device)
             dist.all_gather_into_tensor(recv, send, group=self.group)
             s.master.index_copy_(0, self.f32_dst_idx, recv.index_select(0, self.f32_recv_pos))
+        pending = {}
+        for b in reversed(self.buckets):  # ascending offsets: the first layers' weights are requested first
+            lo, hi = self.shard(b)
+            pending[b.index] = dist.all_gather_into_tensor(s.half[b.lo:b.hi], s.half[lo:hi], group=self.group,
+                                                           async_op=True)
+        s.set_pending(pending, self.buckets_of)
         self.master_stale = True
+        self.pull_order = [b.index for b in reversed(self.buckets)]
 
     def sync_master(self):
         """Make the whole fp32 master current on every rank (checkpoints, PS snapshots, end-of-run checks):
@@ -267,6 +298,8 @@ class ShardedParameterService:
                 b.pending = 0
         self._launch_ready()
         self._finish_pushes()
+        # buckets of the last pull that no forward layer read: the optimizer below rewrites their owned slices
+        self.store.wait_pending()
         reduce = None
         if self.world > 1:
             def reduce(stats):

@@ -345,6 +345,15 @@ def train(a) -> int:
 
         psv = PsVariables(ps_addrs)
     start_step = _restore(a, w, opt, dev, chief, world, metrics, psv, svc)
+    if world > 1:
+        # step-0 transport self-check: one gradient bucket through the configured transport
+        # (fp32 / bf16 all-reduce, ZeRO-1 push) against a plain fp32 all_reduce; the verdict is the same on every
+        # rank, so all ranks exit together, with a permanent code: a wrong transport must not train
+        check = (svc if svc is not None else red).self_check()
+        metrics.event(event="transport_check", **check)
+        if not check["ok"]:
+            metrics.event(event="error", error="gradient transport self-check failed")
+            return EXIT_PERMANENT
 
     def save(step):
         # sharded optimizer state gathered to the chief only, bucket by bucket, into host memory (collective); the

@@ -59,6 +59,37 @@ def test_bench_eight_ranks_without_a_launcher():
     assert abs(r["value"] - 16 * 2 / (r["ms_per_step"] * 2 / 1000.0)) / r["value"] < 0.02
     assert r["replicas_identical"] is True
     assert r["comm_exposed_ms"] >= 0 and r["grad_comm_fallbacks"] == {}
+    # the record shows what the process group really ran on, and the step-0 transport
+    # check passed for the full world
+    assert r["comm"]["backend"] == "gloo" and r["comm"]["world_size"] == 8
+    assert r["transport_check"]["ok"] is True and r["transport_check"]["world"] == 8
+    assert r["transport_check"]["transport"] == "allreduce-fp32"
+
+
+def _run_fail(args, nproc, **env_extra):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(REPO, "bench.py")] + args
+    return subprocess.run(cmd, env=_env(**env_extra), cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                          text=True, timeout=300)
+
+
+def test_bench_bf16_transport_self_check_passes_and_reports():
+    recs = _run("bench.py", ["--gpus", "4", "--steps", "1", "--warmup", "1", "--batch", "2", "--image", "32",
+                             "--grad-comm", "bf16"], nproc=4)
+    r = recs[0]
+    assert r["transport_check"]["ok"] is True and r["transport_check"]["transport"] == "allreduce-bf16"
+    assert r["transport_check"]["max_err_over_tol"] < 1.0 and r["comm"]["world_size"] == 4
+
+
+def test_bench_corrupted_transport_exits_nonzero():
+    """A deliberately wrong reduction (K8S_AMD_FAULT_TRANSPORT: MAX instead of SUM for fp32, one rank's bf16 slice
+    dropped) is caught by the step-0 self-check: exit 3 before any timed step, no JSON line."""
+    for comm in ("fp32", "bf16"):
+        r = _run_fail(["--gpus", "2", "--steps", "1", "--warmup", "0", "--batch", "2", "--image", "32",
+                       "--grad-comm", comm], 2, K8S_AMD_FAULT_TRANSPORT="1")
+        assert r.returncode != 0, (comm, r.stdout, r.stderr)
+        assert not [line for line in r.stdout.splitlines() if line.startswith("{")]
+        assert "transport self-check failed" in r.stderr, r.stderr[-2000:]
 
 
 def test_bench_world_mismatch_fails_closed():

@@ -111,7 +111,7 @@ def test_resnet_bottleneck_onload_matches_apply_path(cuda, monkeypatch):
     from k8s_amd.parallel.flat import ParamStore
 
     outs = {}
-    for mode in ("3x3", "1x1"):
+    for mode in ("3x3", "1x1", "0"):  # "0": every BN applied by its own pass (honoured)
         monkeypatch.setattr(K, "BN_ONLOAD", mode)
         torch.manual_seed(4)
         store = ParamStore()
@@ -124,7 +124,8 @@ def test_resnet_bottleneck_onload_matches_apply_path(cuda, monkeypatch):
         y = blk(x)
         y.float().square().mean().backward()
         outs[mode] = (y.detach().float(), x.grad.float(), store.grad.clone())
-    a, b = outs["3x3"], outs["1x1"]
-    assert _rel(a[0], b[0]) < 1e-2
-    assert _rel(a[1], b[1]) < 2e-2
-    assert _rel(a[2], b[2]) < 2e-2
+    for other in ("1x1", "0"):
+        a, b = outs["3x3"], outs[other]
+        assert _rel(a[0], b[0]) < 1e-2
+        assert _rel(a[1], b[1]) < 2e-2
+        assert _rel(a[2], b[2]) < 2e-2

@@ -247,3 +247,62 @@ def test_bf16_pull_bit_exact_against_fp32_pull(world, comm):
     assert a["stale_ok"]
     for k in ("master", "half", "exp_avg", "exp_avg_sq"):
         assert torch.equal(a[k], b[k]), k
+
+
+def _check_worker(rank, world, port, out_dir, fault):
+    from k8s_amd.ops.optim import FusedAdam
+    from k8s_amd.parallel.ddp import GradReducer
+    from k8s_amd.parallel.flat import ALIGN, ParamStore, init_normal
+    from k8s_amd.parallel.ps import ShardedParameterService
+
+    if fault:
+        os.environ["K8S_AMD_FAULT_TRANSPORT"] = "1"
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    res = {}
+    for strategy in ("allreduce", "ps"):
+        for comm in ("fp32", "bf16"):
+            store = ParamStore()
+            for i, s in enumerate(SHAPES):
+                store.new("p%d" % i, s, init_normal(0.5), lowp=(i % 3 != 2))
+            store.finalize("cpu", pad_to=world * ALIGN, seed=5)
+            dtype = torch.bfloat16 if comm == "bf16" else torch.float32
+            before = store.grad.clone()
+            if strategy == "ps":
+                svc = ShardedParameterService(store, FusedAdam(store, lr=0.01), bucket_mb=0.002, comm_dtype=dtype,
+                                              pull="lowp")
+                r = svc.self_check()
+                # the bf16 pull is issued in ascending offset order (first layers first)
+                svc.step()
+                offs = [svc.buckets[i].lo for i in svc.pull_order]
+                r["pull_ascending"] = offs == sorted(offs)
+                store.wait_pending()
+            else:
+                r = GradReducer(store, bucket_mb=0.002, comm_dtype=dtype).self_check()
+                r["restored"] = torch.equal(before, store.grad)
+            res["%s-%s" % (strategy, comm)] = r
+    if rank == 0:
+        torch.save(res, os.path.join(out_dir, "check.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fault", [False, True])
+def test_transport_self_check(fault):
+    """the step-0 self-check of every gradient transport (all-reduce fp32/bf16, ZeRO-1
+    push fp32/bf16) passes on a healthy 4-rank world, restores the gradient range it used, and fails every
+    transport when the reduction is deliberately corrupted."""
+    world = 4
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_check_worker, args=(world, free_port(), d, fault), nprocs=world)
+        res = torch.load(os.path.join(d, "check.pt"), weights_only=True)
+    assert sorted(res) == ["allreduce-bf16", "allreduce-fp32", "ps-bf16", "ps-fp32"]
+    for name, r in res.items():
+        assert r["world"] == world, name
+        assert r["ok"] is (not fault), (name, r)
+        if fault:
+            assert r["max_err_over_tol"] > 10, (name, r)
+        if name.startswith("ps"):
+            assert r["pull_ascending"], name
+        else:
+            assert r["restored"], name

@@ -27,9 +27,11 @@ def _env(tf_config=None):
     return env
 
 
-def _trainer(args, tf_config=None):
+def _trainer(args, tf_config=None, **extra_env):
+    env = _env(tf_config)
+    env.update(extra_env)
     return subprocess.Popen([sys.executable, "-m", "k8s_amd.trainer", "--device", "cpu"] + args,
-                            env=_env(tf_config), stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+                            env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
 
 
 def _events(out):
@@ -129,6 +131,8 @@ def test_two_rank_allreduce_and_sharded_ps_agree(tmp_path):
     a, _ = _run_job(tmp_path, "allreduce", with_ps=False)
     b, outs = _run_job(tmp_path, "ps", with_ps=True)
     assert "Started server /job:ps/task:0" in outs[0]
+    checks = [e for e in _events(outs[1]) if e.get("event") == "transport_check"]
+    assert checks and checks[0]["ok"] is True and checks[0]["transport"] == "zero1-fp32", outs[1][-2000:]
     for k in a:
         if k.startswith("params/") or k.startswith("optim/"):
             torch.testing.assert_close(a[k], b[k], rtol=1e-4, atol=1e-5, msg=k)
@@ -306,3 +310,20 @@ def test_default_ps_ignores_unknown_flags():
     a, unknown = srv.build_parser().parse_known_args(
         ["--cluster_spec", "ps|127.0.0.1:1", "--job_name", "ps", "--task_id", "0", "--log_dir", "/tmp/x", "--foo"])
     assert a.job_name == "ps" and unknown == ["--log_dir", "/tmp/x", "--foo"]
+
+
+def test_corrupted_gradient_transport_fails_the_job_at_step_0(tmp_path):
+    """with a deliberately wrong reduction (K8S_AMD_FAULT_TRANSPORT) both ranks fail the
+    step-0 transport self-check together and exit with a permanent code, before any training step."""
+    pm, pw = _distinct_ports(2)
+    cluster = {"master": ["127.0.0.1:%d" % pm], "worker": ["127.0.0.1:%d" % pw]}
+    common = ["--model", "resnet_tiny", "--steps", "2", "--log-every", "1", "--grad-comm", "bf16"]
+    procs = [_trainer(common, {"cluster": cluster, "task": {"type": t, "index": 0}, "environment": "cloud"},
+                      K8S_AMD_FAULT_TRANSPORT="1") for t in ("master", "worker")]
+    for p in procs:
+        out, _ = p.communicate(timeout=300)
+        assert 0 < p.returncode < 128, out
+        ev = _events(out)
+        assert not [e for e in ev if e.get("event") in ("step0", "step")], out[-2000:]
+    checks = [e for e in _events(out) if e.get("event") == "transport_check"]
+    assert checks and checks[0]["ok"] is False
