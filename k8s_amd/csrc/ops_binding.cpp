@@ -593,7 +593,7 @@ void conv_fwd_subgrid(Tensor x, Tensor w, int64_t pad, int64_t Hs, int64_t Ws, T
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && out.dim() == 4 && out.is_contiguous());
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int K = w.size(0), R = w.size(1), S = w.size(2);
-  TORCH_CHECK(w.size(3) == C && C % 64 == 0 && K % 8 == 0, "sub-grid conv needs C % 64 == 0, K % 8 == 0");
+  TORCH_CHECK(w.size(3) == C && C % 8 == 0 && K % 8 == 0, "sub-grid conv needs C % 8 == 0, K % 8 == 0");
   TORCH_CHECK(out.size(0) == N && out.size(3) == K, "out shape");
   const int OH = out.size(1), OW = out.size(2);
   TORCH_CHECK(stride >= 1 && a >= 0 && a < stride && b >= 0 && b < stride, "parity out of range");

@@ -69,9 +69,10 @@ _WARNED = set()
 
 
 def _vendor(op, x, w, stride, padding):
-    """Count (and on the GPU warn once about) a product that has to use ATen/MIOpen."""
-    STATS["aten_" + op] += 1
+    """Count and warn once about a GPU product that has to use ATen/MIOpen (CPU tensors always use ATen: the
+    plain-PyTorch oracle path, not counted)."""
     if x.is_cuda:
+        STATS["aten_" + op] += 1
         key = _key("conv_" + op, x, w, stride, padding)
         if key not in _WARNED:
             _WARNED.add(key)
@@ -146,7 +147,7 @@ def _parity_taps(R, a, pad, stride):
 
 def strided_dgrad_ok(gy, w, stride, padding):
     K, R, S, C = w.shape
-    if stride < 2 or K % 64 or C % 8:
+    if stride < 2 or K % 8 or C % 8:
         return False
     for a in range(stride):
         for b in range(stride):
@@ -201,7 +202,7 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, xform=None
                                   and p.grad.dtype == torch.float32):
         raise RuntimeError("normalize-on-load weight gradient outside the kernels' contract")
     if addend is not None and not torch.is_tensor(addend) and not (
-            hip and stride == 1 and K % 64 == 0 and C % 8 == 0):
+            hip and stride == 1 and K % 8 == 0 and C % 8 == 0):
         addend = addend.materialize()  # only the stride-1 dgrad on our kernels takes the (dy, mask) pair
     # ---- weight gradient
     dw_done = False
@@ -217,7 +218,7 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, xform=None
     # ---- data gradient
     dx = None
     if need_dx:
-        if hip and stride == 1 and K % 64 == 0 and C % 8 == 0:
+        if hip and stride == 1 and K % 8 == 0 and C % 8 == 0:
             STATS["hip_dgrad"] += 1
             dx = _dgrad_hip(C_, gy, w, padding, addend)
         elif hip and strided_dgrad_ok(gy, w, stride, padding):

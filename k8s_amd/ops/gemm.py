@@ -48,9 +48,9 @@ def mm(a, b, a_kmajor=True, b_kmajor=True, out=None, out_f32=False, bias=None, a
 def _shape_ok(M, N, K) -> bool:
     """The kernels' contract for a Linear layer's products: any M (the row tails are masked in-kernel); the K-major
     reduction dims (K forward, N in the data gradient) and the MN-major extents (N and K in the weight gradient)
-    in whole 16-B units -- K % 8 and N % 8 -- and N % 4 for the forward epilogue. A backward with N % 8 != 0 runs on
-    zero-padded copies (``linear_bwd``), so only K % 8 is required there."""
-    return K % 8 == 0 and N % 4 == 0
+    in whole 16-B units -- K % 8 and N % 8 -- and N % 4 for the forward epilogue. A ragged N runs on zero-padded
+    weight rows (forward: ``_hip_fwd``; backward: ``linear_bwd``), so only K % 8 is required."""
+    return K % 8 == 0
 
 
 def _act_fwd(y, act):
@@ -83,6 +83,10 @@ def _act_bwd(gy, pre_or_out, act):
 
 def _hip_fwd(x, w, b, act):
     M, N = x.shape[0], w.shape[0]
+    if N % 4:  # ragged N (e.g. a 10-class head): zero weight rows up to a 16-B unit, the padded columns cut off
+        n8 = (N + 7) // 8 * 8
+        y, saved = _hip_fwd(x, F.pad(w, (0, 0, 0, n8 - N)), None if b is None else F.pad(b, (0, n8 - N)), act)
+        return y[:, :N].contiguous(), (None if saved is None else saved[:, :N].contiguous())
     pre = torch.empty((M, N), device=x.device, dtype=torch.bfloat16) if act == "gelu" else None
     y = mm(x, w, True, True, bias=b, act=act, pre=pre)
     return y, (pre if act == "gelu" else (y if act == "relu" else None))

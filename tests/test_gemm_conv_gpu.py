@@ -119,7 +119,11 @@ def test_conv_wgrad(cuda, case):
     assert _rel(dw, wr.grad.permute(0, 2, 3, 1)) < 5e-3
 
 
-@pytest.mark.parametrize("case", [c for c in CONV_CASES if c[6] == 1])
+# + reductions (the dgrad's K) that are not a multiple of 64 (K % 8 is the contract)
+@pytest.mark.parametrize("case", [c for c in CONV_CASES if c[6] == 1] + [(2, 15, 13, 24, 40, 3, 1, 1),
+                                                                         (1, 9, 9, 8, 16, 1, 1, 0),
+                                                                         (2, 8, 8, 8, 8, 1, 1, 0),
+                                                                         (2, 6, 6, 32, 32, 3, 1, 1)])
 def test_conv_dgrad_stride1(cuda, case):
     from k8s_amd.ops import conv as kc
 
@@ -205,7 +209,10 @@ def test_maxpool_nhwc(cuda, shape, ksp):
 # parity-decomposed implicit GEMM with the sub-grid epilogue
 @pytest.mark.parametrize("N,H,C,K,R,st,pad", [(4, 56, 128, 128, 3, 2, 1), (4, 28, 256, 512, 1, 2, 0),
                                               (2, 15, 64, 128, 3, 2, 1), (2, 32, 8, 64, 7, 2, 3),
-                                              (3, 14, 512, 1024, 1, 2, 0)])
+                                              (3, 14, 512, 1024, 1, 2, 0),
+                                              # K (and C) % 64 != 0: the per-unit implicit-GEMM decode
+                                              (8, 8, 32, 32, 3, 2, 1), (2, 9, 24, 40, 3, 2, 1),
+                                              (3, 8, 16, 24, 1, 2, 0)])
 def test_conv_dgrad_strided(cuda, N, H, C, K, R, st, pad):
     from k8s_amd.ops import conv as kc
 
@@ -224,7 +231,7 @@ def test_conv_dgrad_strided(cuda, N, H, C, K, R, st, pad):
 # the residual-gradient add fused into the strided dgrad: every parity accumulates onto the addend in the
 # GEMM epilogue; parities no tap reaches keep the addend unchanged
 @pytest.mark.parametrize("N,H,C,K,R,st,pad", [(4, 28, 256, 512, 1, 2, 0), (2, 15, 64, 128, 3, 2, 1),
-                                              (3, 14, 512, 1024, 1, 2, 0)])
+                                              (3, 14, 512, 1024, 1, 2, 0), (8, 8, 32, 32, 3, 2, 1)])
 def test_conv_dgrad_strided_accumulate(cuda, N, H, C, K, R, st, pad):
     from k8s_amd.ops import conv as kc
 
@@ -260,6 +267,32 @@ def test_linear_head_1000_classes_no_fallback(cuda):
     assert _rel(dx, gy.float() @ w.float()) < 1e-2
     assert _rel(dw, gy.float().t() @ x.float()) < 1e-2
     assert _rel(db, gy.float().sum(0)) < 1e-2
+
+
+@pytest.mark.parametrize("N", [10, 6, 13])
+@pytest.mark.parametrize("act", [None, "relu"])
+def test_linear_ragged_n_no_fallback(cuda, N, act):
+    """A 10-class head (N % 4 != 0) runs forward and backward on our kernels over zero-padded weight rows."""
+    from k8s_amd.ops import gemm
+
+    torch.manual_seed(5)
+    M, K = 64, 256
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) * 0.05).bfloat16()
+    b = torch.randn(N, device=cuda)
+    gy = torch.randn(M, N, device=cuda).bfloat16()
+    before = dict(gemm.FALLBACKS)
+    y, saved = gemm.linear_fwd(x, w, b, act)
+    dx, dw, db = gemm.linear_bwd(gy, x, w, saved, act)
+    assert gemm.FALLBACKS == before
+    pre = x.float() @ w.float().t() + b
+    ref = torch.relu(pre) if act == "relu" else pre
+    assert y.shape == (M, N) and y.is_contiguous()
+    assert _rel(y, ref) < 1e-2
+    g = gy.float() * (pre > 0) if act == "relu" else gy.float()
+    assert _rel(dx, g @ w.float()) < 2e-2
+    assert _rel(dw, g.t() @ x.float()) < 2e-2
+    assert _rel(db, g.sum(0)) < 2e-2
 
 
 def _unpack_bits(mask, shape):

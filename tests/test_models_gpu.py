@@ -9,6 +9,20 @@ from k8s_amd.ops.optim import FusedAdam
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def no_aten_products():
+    """every conv and linear product of these models runs on our kernels (no ATen
+    fallback is counted), so the tests exercise the HIP path end to end."""
+    from k8s_amd.ops import conv, gemm
+
+    before = dict(conv.STATS)
+    gemm.FALLBACKS.clear()
+    yield
+    aten = {k: conv.STATS[k] - before[k] for k in conv.STATS if k.startswith("aten_")}
+    assert not any(aten.values()), aten
+    assert gemm.FALLBACKS == {}, gemm.FALLBACKS
+
+
 @pytest.mark.parametrize("name", ["bert_tiny", "llama_tiny"])
 def test_loss_matches_cpu_fp32(cuda, name):
     g = build(name, cuda, batch=4, seed=3)

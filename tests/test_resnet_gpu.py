@@ -12,6 +12,20 @@ from k8s_amd.parallel.flat import ParamStore
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def no_aten_products():
+    """every conv and linear product of these models runs on our kernels (no ATen
+    fallback is counted), so the tests exercise the HIP path end to end."""
+    from k8s_amd.ops import conv, gemm
+
+    before = dict(conv.STATS)
+    gemm.FALLBACKS.clear()
+    yield
+    aten = {k: conv.STATS[k] - before[k] for k in conv.STATS if k.startswith("aten_")}
+    assert not any(aten.values()), aten
+    assert gemm.FALLBACKS == {}, gemm.FALLBACKS
+
+
 def _run(dev, dtype, steps=3):
     torch.manual_seed(0)
     store = ParamStore()
