@@ -33,13 +33,43 @@ Json crd_manifest() {
 }
 
 Controller::Controller(KubeApi& api, ControllerConfig cfg, ControllerOptions opts)
-    : api_(api), cfg_(std::move(cfg)), opts_(std::move(opts)) {}
+    : api_(api), cfg_(std::move(cfg)), opts_(std::move(opts)) {
+  if (opts_.informers) {
+    // every replica Job / Pod the operator creates carries the `tensorflow.org` label (replicas.cc Labels)
+    InformerOptions io;
+    io.watch_timeout = opts_.watch_timeout;
+    io.watch_idle_grace = opts_.watch_idle_grace;
+    jobs_inf_ = std::make_unique<Informer>(api_, group_path("batch/v1", opts_.ns, "jobs"), "tensorflow.org", io);
+    pods_inf_ = std::make_unique<Informer>(api_, core_path(opts_.ns, "pods"), "tensorflow.org", io);
+    jobs_inf_->set_on_change([this](const std::string&, const Json& o) { poke_owner(o); });
+    pods_inf_->set_on_change([this](const std::string&, const Json& o) { poke_owner(o); });
+    opts_.reconcile.jobs_cache = jobs_inf_.get();
+    opts_.reconcile.pods_cache = pods_inf_.get();
+  }
+}
 
 Controller::~Controller() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& kv : jobs_) kv.second->stop();
+  }
+  // the informers' callbacks take mu_: stop them before the workers go away
+  if (jobs_inf_) jobs_inf_->stop();
+  if (pods_inf_) pods_inf_->stop();
   std::lock_guard<std::mutex> g(mu_);
-  for (auto& kv : jobs_) kv.second->stop();
   jobs_.clear();
   retiring_.clear();  // each finishes its requested delete, then joins
+}
+
+void Controller::poke_owner(const Json& obj) {
+  const Json* m = obj.find("metadata");
+  const Json* l = m ? m->find("labels") : nullptr;
+  const Json* n = l ? l->find("tf_job_name") : nullptr;
+  if (!n || !n->is_string()) return;
+  const std::string key = get_str(*m, "namespace") + "/" + n->as_string();
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = jobs_.find(key);
+  if (it != jobs_.end() && !it->second->finished()) it->second->poke();
 }
 
 static bool crd_established(const Json& crd) {
@@ -215,6 +245,14 @@ std::string Controller::run() {
     log_error("initResource failed: %s; retrying in %lld ms", err.c_str(), (long long)opts_.init_retry.count());
     for (int i = 0; i < opts_.init_retry.count() / 100 && !stop_; ++i)
       std::this_thread::sleep_for(std::chrono::milliseconds(100));
+  }
+  if (jobs_inf_) {
+    jobs_inf_->start();
+    pods_inf_->start();
+    // re-adopted jobs read their replicas from the caches from the first tick (a cache that is slow to sync is
+    // not waited for: get_status reads the API server until it is)
+    jobs_inf_->wait_synced(std::chrono::milliseconds(5000));
+    pods_inf_->wait_synced(std::chrono::milliseconds(5000));
   }
   std::string rv;
   while (!stop_) {

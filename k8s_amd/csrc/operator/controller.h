@@ -41,6 +41,10 @@ struct ControllerOptions {
   std::chrono::milliseconds watch_idle_grace{30000};
   // full relist + diff (the 410 path) this often, so an event lost anywhere is still picked up (0 = off)
   std::chrono::milliseconds resync_period{300000};
+  // shared watch caches of the replica Jobs / Pods (informer.h): reconcile ticks read them instead of per-replica
+  // GET / LIST requests, and a change to a job's Job or Pod pokes its worker at once. false: the reference's
+  // polling reads (kept for A/B and for API servers that refuse cluster-wide watches).
+  bool informers = true;
 };
 
 Json crd_manifest();  // the CustomResourceDefinition the operator installs
@@ -56,6 +60,8 @@ class Controller {
 
   // introspection for tests
   size_t num_jobs();
+  const Informer* jobs_cache() const { return jobs_inf_.get(); }
+  const Informer* pods_cache() const { return pods_inf_.get(); }
   std::map<std::string, TfJobStatus> statuses();
 
   // one-shot pieces, public for tests
@@ -73,11 +79,14 @@ class Controller {
   ControllerConfig cfg_;
   ControllerOptions opts_;
   void watchdog_loop();
+  void poke_owner(const Json& obj);  // informer change callback: reconcile the TfJob that owns obj now
 
   std::atomic<bool> stop_{false};
   // panicTimer (pkg/controller/util.go:50-76): steady-clock ns at which the current event handler started,
   // 0 when idle; a watchdog thread aborts the process while a handler is still running past event_watchdog
   std::atomic<long long> handler_started_ns_{0};
+  // declared before the workers: destroyed after them (every worker reads these caches)
+  std::unique_ptr<Informer> jobs_inf_, pods_inf_;
   std::mutex mu_;
   std::map<std::string, std::unique_ptr<JobWorker>> jobs_;  // ns/name -> worker
   std::map<std::string, std::string> job_rvs_;               // ns/name -> resourceVersion

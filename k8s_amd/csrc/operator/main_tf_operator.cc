@@ -78,6 +78,7 @@ int main(int argc, char** argv) {
   fl.def("watch-timeout", "5m", "Each TfJob watch asks the server to end it after a random timeoutSeconds in [t, 2t)");
   fl.def("watch-idle-grace", "30s", "A watch still open this long past its timeoutSeconds is half-open: re-watch");
   fl.def("resync-period", "5m", "Full relist of the TfJobs this often (0: never), so a lost watch event is recovered");
+  fl.def("informers", "true", "Shared watch caches of the replica Jobs / Pods (false: per-replica GET / LIST every tick)", true);
   std::string err = fl.parse(argc, argv);
   if (!err.empty()) {
     fprintf(stderr, "%s\nUsage of tf_operator:\n%s", err.c_str(), fl.usage().c_str());
@@ -138,6 +139,7 @@ int main(int argc, char** argv) {
   opts.watch_timeout = std::chrono::milliseconds(parse_duration_ms(fl.str("watch-timeout"), 300000));
   opts.watch_idle_grace = std::chrono::milliseconds(parse_duration_ms(fl.str("watch-idle-grace"), 30000));
   opts.resync_period = std::chrono::milliseconds(parse_duration_ms(fl.str("resync-period"), 300000));
+  opts.informers = fl.on("informers");
   if (!cfg.grpc_server_file_path.empty()) {
     try {
       opts.reconcile.ps_server_source = read_file(cfg.grpc_server_file_path);

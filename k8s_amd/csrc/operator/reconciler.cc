@@ -142,6 +142,9 @@ void TrainingJob::create_resources() {
 
 void TrainingJob::get_status(std::string& state, std::vector<TfReplicaStatus>& out) {
   const std::string ns = job_.ns();
+  // the caches count only once synced (a reconcile racing the operator's start reads the API server)
+  const Informer* jobs_cache = opts_.jobs_cache && opts_.jobs_cache->synced() ? opts_.jobs_cache : nullptr;
+  const Informer* pods_cache = opts_.pods_cache && opts_.pods_cache->synced() ? opts_.pods_cache : nullptr;
   out.clear();
   for (auto& r : replicas_) {
     TfReplicaStatus st;
@@ -150,19 +153,30 @@ void TrainingJob::get_status(std::string& state, std::vector<TfReplicaStatus>& o
     const int n = r.replicas.value_or(1);
     for (int i = 0; i < n; ++i) {
       const std::string name = replica_job_name(job_, r.type, i);
-      ApiResult jr = call("GET", group_path("batch/v1", ns, "jobs", name));
-      if (!jr.ok()) {
-        if (jr.not_found()) existing_.erase(group_path("batch/v1", ns, "jobs") + "/" + name);  // recreate next tick
-        st.replicas_states["Unknown"]++;
-        continue;
+      Json jobj;
+      if (jobs_cache && jobs_cache->get(ns, name, jobj)) {
+        ++cache_reads_;
+      } else {  // no cache, or not in it yet: ask the API server
+        ApiResult jr = call("GET", group_path("batch/v1", ns, "jobs", name));
+        if (!jr.ok()) {
+          if (jr.not_found()) existing_.erase(group_path("batch/v1", ns, "jobs") + "/" + name);  // recreate
+          st.replicas_states["Unknown"]++;
+          continue;
+        }
+        jobj = jr.body;
       }
-      const Json* js = jr.body.find("status");
+      const Json* js = jobj.find("status");
       if (js && js->find("succeeded") && js->at("succeeded").is_number() && js->at("succeeded").as_int() >= 1) {
         st.replicas_states["Succeeded"]++;
         continue;
       }
-      const std::string sel = selector_string(task_labels(job_, r.type, i));
-      ApiResult pl = call("GET", core_path(ns, "pods") + "?labelSelector=" + url_escape(sel));
+      const Labels tl = task_labels(job_, r.type, i);
+      if (pods_cache) {
+        ++cache_reads_;
+        st.replicas_states[replica_state_from_pods(pods_cache->list(ns, tl), kTensorflowContainer)]++;
+        continue;
+      }
+      ApiResult pl = call("GET", core_path(ns, "pods") + "?labelSelector=" + url_escape(selector_string(tl)));
       if (!pl.ok()) {
         st.replicas_states["Unknown"]++;  // Q6: transient API error is not a failure
         continue;

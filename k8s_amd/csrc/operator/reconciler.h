@@ -29,6 +29,7 @@
 #include <string>
 #include <thread>
 
+#include "informer.h"
 #include "kube_api.h"
 #include "replicas.h"
 #include "spec.h"
@@ -39,6 +40,11 @@ struct ReconcileOptions {
   std::chrono::milliseconds interval{8000};
   std::string ps_script_path = std::string(kPSServerMount) + "/" + kPSServerFile;
   std::string ps_server_source;  // contents of ControllerConfig.grpcServerFilePath (read once)
+  // shared watch caches of the replica batch Jobs / Pods (informer.h; owned by the Controller, outliving every
+  // worker). When synced, a tick reads replica state from them instead of a Job GET + Pod LIST per replica; a
+  // Job missing from the cache (e.g. created a moment ago) is confirmed with a direct GET.
+  const Informer* jobs_cache = nullptr;
+  const Informer* pods_cache = nullptr;
 };
 
 std::string rand_string(int n);  // [0-9a-z], DNS-1035 friendly (pkg/util/util.go:25-54)
@@ -58,6 +64,7 @@ class TrainingJob {
   const TfJobStatus& status() const { return status_; }
   std::string key() const { return job_.ns() + "/" + job_.name(); }
   int api_calls() const { return api_calls_; }
+  long long cache_reads() const { return cache_reads_; }
 
   // Build replica bookkeeping from the (defaulted) spec; returns error text.
   std::string build_replica_sets();
@@ -87,6 +94,7 @@ class TrainingJob {
   std::set<std::string> existing_;  // objects known to exist (kind/name)
   std::map<std::string, Json> events_;  // reason + "\n" + message -> the last stored Event object
   int api_calls_ = 0;
+  long long cache_reads_ = 0;
 };
 
 // Runs a TrainingJob on its own thread: reconcile immediately, then every

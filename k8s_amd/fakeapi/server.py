@@ -69,6 +69,10 @@ class _Handler(BaseHTTPRequestHandler):
                                        "user_agent": b.get("user_agent", "")})
             return self._send(200, {"stalls": len(self.server.stalls)})
         self._stall()
+        with self.server.count_lock:  # requests per client (User-Agent) and kind: the operator scale test's API load
+            ua = self.headers.get("User-Agent", "")
+            kind = "WATCH" if "watch=" in u.query else method
+            self.server.ua_counts[(ua, kind)] = self.server.ua_counts.get((ua, kind), 0) + 1
         accept = self.server.accept_token
         if accept is not None:  # bearer-token check (credential refresh tests)
             auth = self.headers.get("Authorization", "")
@@ -142,19 +146,27 @@ class _Handler(BaseHTTPRequestHandler):
         self._dispatch("DELETE")
 
 
+class _Server(ThreadingHTTPServer):
+    # listen backlog: socketserver's default of 5 resets connections when ~100 reconciler threads, the kubelet and
+    # the clients connect at once (the operator scale test)
+    request_queue_size = 1024
+
+
 class FakeApiServer:
     """Run an ApiStore behind HTTP on 127.0.0.1:<port> in a background thread."""
 
     def __init__(self, store: Optional[ApiStore] = None, port: int = 0, host: str = "127.0.0.1"):
         self.store = store or ApiStore()
         handler = type("Handler", (_Handler,), {"store": self.store})
-        self.httpd = ThreadingHTTPServer((host, port), handler)
+        self.httpd = _Server((host, port), handler)
         self.httpd.daemon_threads = True
         self.httpd.stalls = []  # fault injection rules (POST /debug/stall, or stall() below)
         self.httpd.blackhole_before = 0.0  # watches opened before this time are black holes (blackhole_watches)
         self.httpd.accept_token = None  # callable(token) -> bool: reject other bearer tokens with 401
         self.httpd.accepted, self.httpd.rejected = [], []
         self.httpd.stopping = False
+        self.httpd.count_lock = threading.Lock()
+        self.httpd.ua_counts = {}  # (User-Agent, GET/POST/PUT/DELETE/WATCH) -> requests
         self.port = self.httpd.server_address[1]
         self.url = "http://%s:%d" % (host, self.port)
         self.thread = threading.Thread(target=self.httpd.serve_forever, daemon=True)
@@ -167,6 +179,15 @@ class FakeApiServer:
         """Stop answering matching requests for ``seconds`` (requests arriving meanwhile hang until then)."""
         self.httpd.stalls.append({"until": time.time() + seconds, "path_prefix": path_prefix,
                                   "user_agent": user_agent})
+
+    def request_counts(self, ua_prefix: str = "") -> dict:
+        """{method: requests} of the clients whose User-Agent starts with ``ua_prefix`` (WATCH = watch opens)."""
+        out = {}
+        with self.httpd.count_lock:
+            for (ua, kind), n in self.httpd.ua_counts.items():
+                if ua.startswith(ua_prefix):
+                    out[kind] = out.get(kind, 0) + n
+        return out
 
     def blackhole_watches(self):
         """Every watch open right now silently stops: no more events and no end of stream (a half-open TCP
