@@ -8,7 +8,9 @@ reconciles each with its own goroutine, one Job GET + one Pod LIST per replica i
 measures, from the API server's side (requests counted by User-Agent):
 
 * steady-state operator API requests per second, total and per job, while every job is Running;
-* create -> Succeeded per job (the MASTER exits 0 after ``--hold`` seconds; reported minus the hold);
+* create -> every job Running, and release -> Succeeded per job: the MASTERs wait for a marker file, created after
+  the steady-state window; the time from it to each TfJob's Succeeded status is the operator's detection latency
+  (pod exit -> kubelet status -> operator -> TfJob status);
 * the operator's thread count;
 * cleanup: every TfJob deleted, every child Job / Pod / Service gone.
 
@@ -33,14 +35,15 @@ from k8s_amd.fakeapi.client import tfjobs_path  # noqa: E402
 OP_UA = "tf_operator-amd/"
 
 
-def _job(name, hold):
+def _job(name, marker):
     def rep(t, cmd):
         return {"replicas": 1, "tfReplicaType": t, "template": {"spec": {
             "containers": [{"name": "tensorflow", "image": "busybox", "command": ["sh", "-c", cmd]}],
             "restartPolicy": "OnFailure"}}}
     return {"apiVersion": "tensorflow.org/v1alpha1", "kind": "TfJob",
             "metadata": {"name": name, "namespace": "default"},
-            "spec": {"replicaSpecs": [rep("MASTER", "exec sleep %g" % hold), rep("WORKER", "exec sleep 600")]}}
+            "spec": {"replicaSpecs": [rep("MASTER", "while [ ! -f %s ]; do sleep 0.5; done" % marker),
+                                      rep("WORKER", "exec sleep 600")]}}
 
 
 def _threads(pid):
@@ -58,14 +61,15 @@ def _pct(xs, q):
     return xs[min(len(xs) - 1, int(round(q * (len(xs) - 1))))] if xs else None
 
 
-def run(jobs=100, informers=True, hold=20.0, window=5.0, interval="2s", timeout=240.0, log=print):
+def run(jobs=100, informers=True, window=5.0, interval="2s", timeout=240.0, log=print):
     t_begin = time.time()
     args = ["-informers=%s" % ("true" if informers else "false")]
     with LocalCluster(reconcile_interval=interval, operator_args=args) as c:
+        marker = os.path.join(c.log_dir, "release")
         names = ["scale-%03d" % i for i in range(jobs)]
         created = {}
         for n in names:
-            c.create(_job(n, hold))
+            c.create(_job(n, marker))
             created[n] = time.time()
         t_created = time.time()
         # every job Running with both pods up
@@ -98,7 +102,9 @@ def run(jobs=100, informers=True, hold=20.0, window=5.0, interval="2s", timeout=
         qps = sum(steady.values()) / (t1 - t0)
         log("steady: %d jobs, informers=%s: %.1f req/s (%s), %d operator threads"
             % (jobs, informers, qps, steady, threads))
-        # wait for every job to finish (MASTER exits 0 after `hold`)
+        # release every MASTER (exit 0) and wait for every job to finish
+        open(marker, "w").close()
+        t_release = time.time()
         while time.time() < end and len(done) < jobs:
             items = c.client.get(tfjobs_path("default"))["items"]
             now = time.time()
@@ -111,7 +117,7 @@ def run(jobs=100, informers=True, hold=20.0, window=5.0, interval="2s", timeout=
         states = {}
         for n, (_, s) in done.items():
             states[s] = states.get(s, 0) + 1
-        lat = [done[n][0] - created[n] - hold for n in done]
+        lat = [done[n][0] - t_release for n in done]
         # cleanup: delete every TfJob; the operator deletes the children, ownerReferences GC the rest
         t_del = time.time()
         for n in names:
@@ -128,15 +134,15 @@ def run(jobs=100, informers=True, hold=20.0, window=5.0, interval="2s", timeout=
         total = c.server.request_counts(OP_UA)
         op_log = c.operator_log()
     return {
-        "jobs": jobs, "informers": informers, "reconcile_interval": interval, "hold_s": hold,
+        "jobs": jobs, "informers": informers, "reconcile_interval": interval,
         "create_all_s": round(t_created - t_begin, 3),
         "all_running_s": round(running_at - t_created, 3),
         "steady_window_s": round(t1 - t0, 3), "steady_requests": steady,
         "steady_qps": round(qps, 2), "steady_qps_per_job": round(qps / jobs, 4),
         "operator_threads": threads,
         "states": states,
-        "create_to_succeeded_minus_hold_s": {"p50": round(_pct(lat, 0.5), 3), "p90": round(_pct(lat, 0.9), 3),
-                                             "max": round(max(lat), 3)} if lat else None,
+        "release_to_succeeded_s": {"p50": round(_pct(lat, 0.5), 3), "p90": round(_pct(lat, 0.9), 3),
+                                   "max": round(max(lat), 3)} if lat else None,
         "cleanup_s": round(cleanup_s, 3), "left_after_cleanup": left,
         "operator_requests_total": total,
         "operator_errors": sum(1 for line in op_log.splitlines() if " E" in line[:3] or "ERROR" in line),
@@ -148,13 +154,12 @@ def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--jobs", type=int, default=100)
     ap.add_argument("--informers", choices=["true", "false", "both"], default="both")
-    ap.add_argument("--hold", type=float, default=20.0)
     ap.add_argument("--window", type=float, default=5.0)
     ap.add_argument("--interval", default="2s", help="operator -reconcile-interval (reference: 8s)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     modes = {"true": [True], "false": [False], "both": [False, True]}[a.informers]
-    out = [run(a.jobs, m, a.hold, a.window, a.interval, log=lambda s: print(s, file=sys.stderr)) for m in modes]
+    out = [run(a.jobs, m, a.window, a.interval, log=lambda s: print(s, file=sys.stderr)) for m in modes]
     text = "\n".join(json.dumps(r) for r in out)
     print(text)
     if a.out:

@@ -34,6 +34,14 @@
 //  * epilogue: the bf16 tile goes through LDS, leaves as 16-B row segments, and the per-channel sum / sum of squares
 //    of the stored values are accumulated for the following BatchNorm (the [STAT_REPL][2][K] layout of gemm.hip).
 //  * <= 80 KB LDS: 2 blocks per CU, so one block's window staging overlaps the other's MFMAs.
+//  * the per-tap barrier is a raw s_barrier after explicit waits (__syncthreads() adds a release fence, i.e.
+//    s_waitcnt vmcnt(0), which drained the in-flight weight tap every step): 2-5 % per layer (round 5).
+//  * not kept (round 5, profiles/r05_conv3x3_c3p_ab.jsonl, r05_conv3x3_pmc.txt): a persistent form with one block
+//    per CU walking a range of tiles, both windows and a 4-slot weight ring in flight, fragments read one k-half
+//    ahead among the MFMAs (the g4 GEMM's schedule) and the epilogue stored from registers -- 0.63-0.76x this
+//    kernel at 28 x 28 / 14 x 14. With 8 waves (2 per SIMD) it read 0.64 fragments per MFMA and saturated the LDS
+//    (26-30 % MFMA busy); with 4 (one per SIMD) the loop ran ~60 % MFMA-busy cycles but the kernel still lost on
+//    wall time to this one's two blocks per CU, and its register-direct epilogue with statistics cost ~25 %.
 #include <stdexcept>
 
 #include "common.h"
@@ -48,6 +56,12 @@ constexpr int STAT_REPL = 32;  // = gemm.hip STAT_REPL = kConvStatReplicas
 __device__ __attribute__((aligned(64))) uint16_t g_c3_zero[64];  // source of the rows outside the image
 
 __device__ __forceinline__ int swz(int p) { return p & 6; }
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 template <int W, int RT, int KT, bool XF>
 struct Geo {
@@ -231,10 +245,12 @@ __global__ void __launch_bounds__(THREADS, 2) conv3x3_kernel(const uint16_t* __r
                 acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[f], acc[f][j], 0, 0, 0);
           }
         }
-        // step g + 1's weights landed (step g + NS - 1's may still be in flight)
+        // step g + 1's weights landed (step g + NS - 1's may still be in flight). A raw s_barrier: __syncthreads()
+        // adds a workgroup release fence -- s_waitcnt vmcnt(0) -- which drained the in-flight weight tap every step
         if (NS > 2 && gp < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WOPS * (NS - 2)) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        raw_barrier();
       }
     }
   }
@@ -297,280 +313,6 @@ __global__ void __launch_bounds__(THREADS, 2) conv3x3_kernel(const uint16_t* __r
   }
 }
 
-// ---------------------------------------------------------------------------------------------------------------------
-// Persistent, software-pipelined form (c3p) for the 28 x 28 and 14 x 14 layers (C, K >= 128: two or more 64-channel
-// slices per tile). The kernel above stages a slice's window and only then starts its MFMAs, so every slice of every
-// block begins with an exposed load, and the two co-resident blocks per CU overlapped those phases poorly
-// (profiles/r04_conv3x3_pmc.txt: 45-53 % MFMA busy). Here ONE block of 8 waves per CU walks a contiguous range of
-// output tiles, and the work is one stream of units u = (tile, slice) of 9 tap steps each:
-//  * two window buffers: the DMA of unit u + 1's window is issued at the start of unit u (behind its MFMAs), so a
-//    slice's window -- the next tile's first one included -- has landed before its first tap;
-//  * one 3-slot weight ring over the whole stream (step g's MFMAs run while g + 1 / g + 2 stream in);
-//  * the epilogue stores straight from the MFMA registers (bf16x4 per lane; the L2 merges a pixel's 256-B row from
-//    the four channel waves) and is DEFERRED: a tile's outputs are packed when its last MFMA retires and stored at
-//    the start of the next tile's first step, so the stores drain under that step's MFMAs instead of in front of
-//    the following load wait (gfx950 counts stores in vmcnt and lets them complete out of order with the loads:
-//    a wait for a load issued before them must also wait for them);
-//  * every wave issues the same number of window-DMA instructions per unit (a spare one into a 1-KB dump area), so
-//    the per-step waits are exact compile-time vmcnt counts.
-// Waves: 2 (pixel halves, MF x 16 pixels) x 4 (32-channel quarters, NF = 2). LDS: 2 windows + 3 weight slots +
-// dump <= 160 KB (one block per CU).
-namespace c3p {
-constexpr int THREADS = 512;
-
-template <int W, int RT, int KT>
-struct Geo {
-  static constexpr int WP = (W + 7) / 8 * 8 + (W % 8 == 0 ? 8 : 0), P = RT * W;
-  static constexpr int NPOS = (RT + 2) * WP + 8;
-  static constexpr int MF = (P + 31) / 32, NF = KT / 64;
-  static constexpr int WIN_B = NPOS * 128, WT_B = KT * 128, NS = 3;
-  static constexpr int IPR = (W * 8 + 63) / 64, NWI = (RT + 2) * IPR, NWW = (NWI + 7) / 8;
-  static constexpr int WOPS = KT * 8 / THREADS;
-  static constexpr int DUMP = 2 * WIN_B + NS * WT_B;
-  static constexpr int LDS = DUMP + 1024;
-  static_assert(LDS <= 160 * 1024, "one block per CU");
-  static_assert(NF == 2 && KT * 8 % THREADS == 0, "4 channel waves x 2 fragments");
-  static_assert(NWW + WOPS < 64, "vmcnt immediate");
-};
-
-template <int W, int RT, int KT>
-__global__ void __launch_bounds__(THREADS, 1) conv3x3p_kernel(const uint16_t* __restrict__ x,
-                                                             const uint16_t* __restrict__ wt,
-                                                             uint16_t* __restrict__ y, float* __restrict__ stats,
-                                                             int N, int H, int C, int K, int tiles_per_img,
-                                                             int ntiles) {
-  using G = Geo<W, RT, KT>;
-  constexpr int WP = G::WP, NPOS = G::NPOS, P = G::P, MF = G::MF, NF = G::NF, NS = G::NS;
-  constexpr int NWW = G::NWW, WOPS = G::WOPS, IPR = G::IPR, NWI = G::NWI;
-  __shared__ __attribute__((aligned(1024))) char smem[G::LDS];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 2, wn = wid & 3;
-  // this block's tiles: a contiguous range (consecutive row tiles of an image share their halo rows in L2)
-  const int t_begin = (int)((long)blockIdx.x * ntiles / gridDim.x);
-  const int t_end = (int)((long)(blockIdx.x + 1) * ntiles / gridDim.x);
-  const int nsl = C >> 6, per_kc = N * tiles_per_img;
-  const int nunits = (t_end - t_begin) * nsl, nsteps = nunits * 9;
-  if (nunits <= 0) return;
-
-  int pw[MF];
-#pragma unroll
-  for (int f = 0; f < MF; ++f) {
-    int m = (wm * MF + f) * 16 + (lane & 15);
-    m = m < P ? m : P - 1;  // pad lanes of the last fragment compute a duplicate pixel, never stored
-    const int r = m / W;
-    pw[f] = r * WP + 7 + (m - r * W);
-  }
-  int boff[2][NF];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-    for (int j = 0; j < NF; ++j) {
-      const int r = wn * 32 + j * 16 + (lane & 15), ch = kk * 4 + (lane >> 4);
-      boff[kk][j] = r * 128 + ((ch ^ c3::swz(r)) << 4);
-    }
-  // zero padding of both window buffers (never written by the DMA)
-#pragma unroll 1
-  for (int c = tid; c < 2 * NPOS * 8; c += THREADS) {
-    const int q = ((c % (NPOS * 8)) >> 3) - 8;
-    if (q < 0 || q - q / WP * WP >= W || q >= (RT + 2) * WP)
-      *reinterpret_cast<bf16x8_t*>(smem + c * 16) = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-  }
-  const int lch = (lane & 7) ^ ((lane >> 3) & 6);
-  // window of unit u into buffer (u & 1); u >= nunits: the same instruction count into the dump area
-  auto load_window = [&](int u) {
-    char* wb = smem + (u & 1) * G::WIN_B;
-    int n = 0, h0 = 0, c0 = 0;
-    const bool live = u < nunits;
-    if (live) {
-      const int tl = u / nsl, t = t_begin + tl, rem = t % per_kc;
-      n = rem / tiles_per_img;
-      h0 = (rem - n * tiles_per_img) * RT;
-      c0 = (u - tl * nsl) * 64;
-    }
-#pragma unroll
-    for (int q = 0; q < NWW; ++q) {
-      const int wi = wid + q * 8;
-      if (live && wi < NWI) {
-        const int wr = wi / IPR, i = wi - wr * IPR, px = i * 8 + (lane >> 3), h = h0 - 1 + wr;
-        if (px < W) {
-          const void* src = (unsigned)h < (unsigned)H
-                                ? (const void*)(x + (((long)n * H + h) * W + px) * C + c0 + lch * 8)
-                                : (const void*)c3::g_c3_zero;
-          glds16(src, wb + (wr * WP + 8 + i * 8) * 128);
-        }
-      } else {
-        glds16(c3::g_c3_zero + (lane & 7) * 8, smem + G::DUMP);
-      }
-    }
-  };
-  auto tap_of = [](int k) { return (k % 3) * 3 + k / 3; };
-  // weights of global step gp (unit gp / 9, tap gp % 9) into ring slot gp % NS
-  auto stage_w = [&](int gp) {
-    const int u = gp / 9, t9 = gp - u * 9, tl = u / nsl, cs = u - tl * nsl;
-    const int k0 = (t_begin + tl) / per_kc * KT;
-    const int tap = tap_of(t9);
-    char* d = smem + 2 * G::WIN_B + (gp % NS) * G::WT_B;
-#pragma unroll
-    for (int i = 0; i < WOPS; ++i) {
-      const int c = i * THREADS + tid, row = c >> 3, lc = (c & 7) ^ c3::swz(row);
-      glds16(wt + ((long)(k0 + row) * 9 + tap) * C + cs * 64 + lc * 8, d + (i * THREADS + wid * 64) * 16);
-    }
-  };
-
-  f32x4_t acc[MF][NF];
-  bf16x4_t outp[MF][NF];  // the previous tile's packed outputs, stored at the start of the next tile
-#pragma unroll
-  for (int f = 0; f < MF; ++f)
-#pragma unroll
-    for (int j = 0; j < NF; ++j) {
-      acc[f][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      outp[f][j] = bf16x4_t{0, 0, 0, 0};
-    }
-  int pend_tile = -1;  // tile whose outputs sit in outp
-
-  // stores + BN statistics of tile t from outp (lane: pixel lane & 15 of fragment f, channels 4 (lane >> 4) + r of
-  // fragment j)
-  auto flush = [&](int t) {
-    const int kc = t / per_kc, rem = t - kc * per_kc, n = rem / tiles_per_img;
-    const int h0 = (rem - n * tiles_per_img) * RT;
-    const int kb = kc * KT + wn * 32 + (lane >> 4) * 4;
-    f32x2_t s[NF][2], q[NF][2];
-#pragma unroll
-    for (int j = 0; j < NF; ++j)
-#pragma unroll
-      for (int r = 0; r < 2; ++r) s[j][r] = q[j][r] = f32x2_t{0.f, 0.f};
-#pragma unroll
-    for (int f = 0; f < MF; ++f) {
-      const int m = (wm * MF + f) * 16 + (lane & 15), hr = m / W, h = h0 + hr;
-      if (m < P && h < H) {
-        uint16_t* dst = y + (((long)n * H + h) * W + (m - hr * W)) * K + kb;
-#pragma unroll
-        for (int j = 0; j < NF; ++j) {
-          *reinterpret_cast<bf16x4_t*>(dst + j * 16) = outp[f][j];
-          if (stats) {
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(&outp[f][j]);
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-              const f32x2_t v = {__uint_as_float(w[r] << 16), __uint_as_float(w[r] & 0xFFFF0000u)};
-              s[j][r] += v;
-              q[j][r] = __builtin_elementwise_fma(v, v, q[j][r]);
-            }
-          }
-        }
-      }
-    }
-    if (stats) {
-      float* so = stats + (long)(t % c3::STAT_REPL) * 2 * K;
-#pragma unroll
-      for (int j = 0; j < NF; ++j)
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const float a = row16_sum(s[j][r][e]), b = row16_sum(q[j][r][e]);
-            if ((lane & 15) == 0) {
-              const int col = kb + j * 16 + 2 * r + e;
-              atomicAdd(so + col, a);
-              atomicAdd(so + K + col, b);
-            }
-          }
-    }
-  };
-
-  // prologue: unit 0's window and the first two weight taps
-  load_window(0);
-  stage_w(0);
-  if (1 < nsteps) stage_w(1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-#pragma unroll 1
-  for (int u = 0; u < nunits; ++u) {
-    const int tl = u / nsl, cs = u - tl * nsl;
-    const char* wbuf = smem + (u & 1) * G::WIN_B;
-#pragma unroll 1
-    for (int ds = 0; ds < 3; ++ds) {
-      int aoff[2][MF];
-#pragma unroll
-      for (int f = 0; f < MF; ++f) {
-        const int p = pw[f] + ds;
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) aoff[kk][f] = p * 128 + (((kk * 4 + (lane >> 4)) ^ c3::swz(p)) << 4);
-      }
-#pragma unroll
-      for (int dr = 0; dr < 3; ++dr) {
-        const int g = u * 9 + ds * 3 + dr, gp = g + NS - 1;
-        const bool first = ds == 0 && dr == 0;
-        if (first) {
-          if (pend_tile >= 0 && cs == 0) {  // the previous tile's deferred epilogue (see the header)
-            flush(pend_tile);
-            pend_tile = -1;
-          }
-          load_window(u + 1);  // into the buffer unit u - 1 read (all waves are past it: barrier)
-        }
-        if (gp < nsteps) stage_w(gp);  // slot last read in step g - 1
-        const char* ws = smem + 2 * G::WIN_B + (g % NS) * G::WT_B;
-        const char* wa = wbuf + dr * WP * 128;
-        mfma_bf16x8 af[2][MF], bfr[2][NF];
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-          for (int f = 0; f < MF; ++f)
-            af[kk][f] = __builtin_bit_cast(mfma_bf16x8, *reinterpret_cast<const bf16x8_t*>(wa + aoff[kk][f]));
-#pragma unroll
-          for (int j = 0; j < NF; ++j)
-            bfr[kk][j] = __builtin_bit_cast(mfma_bf16x8, *reinterpret_cast<const bf16x8_t*>(ws + boff[kk][j]));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          if (kk == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(MF + NF) : "memory");
-          else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int f = 0; f < MF; ++f)
-#pragma unroll
-            for (int j = 0; j < NF; ++j)
-              acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[kk][j], af[kk][f], acc[f][j], 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if (ds == 2 && dr == 2 && cs == nsl - 1) {  // the tile's last MFMA: pack, clear, store later
-#pragma unroll
-          for (int f = 0; f < MF; ++f)
-#pragma unroll
-            for (int j = 0; j < NF; ++j) {
-              outp[f][j] = __builtin_bit_cast(bf16x4_t, __builtin_convertvector(acc[f][j], bf16v4_t));
-              acc[f][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            }
-          pend_tile = t_begin + tl;
-        }
-        // step g + 1's weights (and at a unit's last step the next unit's window) have landed: everything issued
-        // before W(g + 1) is complete once at most the instructions issued after it are outstanding -- W(g + 2),
-        // plus this unit's next-window DMA at its first step (deferred stores are not counted: waited for, too)
-        if (gp < nsteps) {
-          if (first) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NWW + WOPS) : "memory");
-          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WOPS) : "memory");
-        } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-      }
-    }
-  }
-  if (pend_tile >= 0) flush(pend_tile);
-}
-
-template <int W, int RT, int KT>
-static void launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H, int C, int K,
-                   hipStream_t st) {
-  const int tpi = (H + RT - 1) / RT;
-  const int ntiles = N * tpi * (K / KT);
-  const int grid = ntiles < planner_cus() ? ntiles : planner_cus();
-  hipLaunchKernelGGL((conv3x3p_kernel<W, RT, KT>), dim3(grid), dim3(THREADS), 0, st, x, w, y, stats, N, H, C, K, tpi,
-                     ntiles);
-}
-}  // namespace c3p
 
 template <int W, int RT, int KT, bool XF>
 static void launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const float* xf, int N, int H,
@@ -600,21 +342,8 @@ bool conv3x3_eligible(int H, int W, int C, int K, int R, int S, int stride, int 
   return (W == 28 || W == 14) && K % 128 == 0;
 }
 
-// The persistent pipelined form (c3p) takes the 28 x 28 / 14 x 14 layers without normalize-on-load;
-// $K8S_AMD_C3P=0 keeps them on the per-tile kernel (A/B; read per call, both sides tested).
-static bool c3p_ok(int W, int K, const float* xform) {
-  const char* e = getenv("K8S_AMD_C3P");
-  if (e && e[0] == '0') return false;
-  return !xform && (W == 28 || W == 14) && K % 128 == 0;
-}
-
 void launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const float* xform, int N,
                     int H, int W, int C, int K, hipStream_t st) {
-  if (c3p_ok(W, K, xform)) {
-    if (W == 28) c3::c3p::launch<28, 7, 128>(x, w, y, stats, N, H, C, K, st);
-    else c3::c3p::launch<14, 14, 128>(x, w, y, stats, N, H, C, K, st);
-    return;
-  }
   if (W == 56 && K == 64) c3::launch_x<56, 4, 64>(x, w, y, stats, xform, N, H, C, K, st);
   else if (W == 28 && K % 128 == 0) c3::launch_x<28, 8, 128>(x, w, y, stats, xform, N, H, C, K, st);
   else if (W == 14 && K % 128 == 0) c3::launch_x<14, 14, 128>(x, w, y, stats, xform, N, H, C, K, st);

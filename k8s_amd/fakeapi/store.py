@@ -105,6 +105,7 @@ class ApiStore:
         self.request_log: List[Tuple[str, str]] = []
         self.hooks: List[Callable] = []  # fn(method, path, body) -> Optional[(code, body)] fault injection
         self.established_delay = established_delay
+        self.live_uids = set()  # uids of every stored object (dangling-owner garbage collection)
 
     # ------------------------------------------------------------------ routing
     def _resources(self, gv):
@@ -233,8 +234,15 @@ class ApiStore:
         if rt.plural == "customresourcedefinitions":
             self._register_crd(body)
         tbl[key] = body
+        self.live_uids.add(md["uid"])
         self._emit(rt.gv, rt.plural, ns, "ADDED", body)
-        return 201, copy.deepcopy(body)
+        out = copy.deepcopy(body)
+        refs = md.get("ownerReferences") or []
+        if refs and not any(r.get("uid") in self.live_uids for r in refs):
+            # every owner is already gone (e.g. a pod created for a Job deleted a moment earlier): the garbage
+            # collector removes such a dependent right after its creation, as Kubernetes' GC does for dangling owners
+            self._remove(rt.gv, rt.plural, ns, md["name"])
+        return 201, out
 
     def _register_crd(self, crd):
         spec = crd.get("spec", {})
@@ -289,6 +297,7 @@ class ApiStore:
         o = tbl.pop((ns, name), None)
         if o is None:
             return None
+        self.live_uids.discard(o["metadata"].get("uid"))
         o["metadata"]["resourceVersion"] = self._bump()
         self._emit(gv, plural, ns, "DELETED", o)
         self._gc(o["metadata"]["uid"])

@@ -49,9 +49,9 @@ def main():
             "fwd_bn_onload": lambda: C_.conv_fwd(x, w, 1, 1, 1, False, None, 0, stats, xform=params),
             "dgrad": lambda: C_.conv_fwd(gy, w2, 1, 1, 1, False, None, 0, None),
         }
-        # arms: the persistent pipelined kernel (c3p, 28 x 28 / 14 x 14 without on-load), the per-tile staged kernel,
-        # the implicit GEMM
-        arms = {"c3p": ("1", "1"), "staged": ("1", "0"), "implicit": ("0", "0")}
+        # arms: the staged-window kernel, the implicit GEMM (round 5 also timed a persistent pipelined form, "c3p":
+        # profiles/r05_conv3x3_c3p_ab.jsonl)
+        arms = {"staged": ("1", "0"), "implicit": ("0", "0")}
         for form, fn in forms.items():
             t = {k: [] for k in arms}
             for _ in range(a.rounds):
@@ -63,7 +63,7 @@ def main():
                 us = min(t[arm]) * 1e3
                 rec[arm + "_us"] = round(us, 1)
                 rec[arm + "_tf"] = round(flop / us / 1e6)
-            rec["c3p_vs_staged"] = round(rec["staged_us"] / rec["c3p_us"], 3)
+            rec["staged_vs_implicit"] = round(rec["implicit_us"] / rec["staged_us"], 3)
             print(json.dumps(rec), flush=True)
         del x, w, gy, w2
         torch.cuda.empty_cache()

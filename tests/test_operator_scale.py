@@ -18,7 +18,7 @@ pytestmark = pytest.mark.skipif(not os.path.exists(OPERATOR_BIN), reason="bin/tf
 def test_hundred_concurrent_tfjobs_with_and_without_informers():
     from benchmarks.operator_scale import run
 
-    res = {m: run(jobs=100, informers=m, hold=20.0, window=4.0, interval="2s", timeout=180.0, log=lambda s: None)
+    res = {m: run(jobs=100, informers=m, window=4.0, interval="2s", timeout=240.0, log=lambda s: None)
            for m in (False, True)}
     for m, r in res.items():
         assert r["states"] == {"Succeeded": 100}, (m, r)
@@ -30,3 +30,6 @@ def test_hundred_concurrent_tfjobs_with_and_without_informers():
     # polling: ~2 reads per replica per 2 s tick per job; cached: only status writes when something changes
     assert polled >= 0.5, res[False]
     assert cached * 2 <= polled, (cached, polled)
+    # the caches' change callback pokes the owning job's worker: a finished MASTER is seen at watch latency, not at the
+    # next resync tick
+    assert res[True]["release_to_succeeded_s"]["p50"] <= res[False]["release_to_succeeded_s"]["p50"] + 1.0, res
