@@ -382,14 +382,20 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
 
-  // ---- XCD-aware bijective remap, then grouped (GROUP_M = 8) tile order
+  // ---- XCD-aware bijective remap over the whole (tile, split) grid, then grouped (GROUP_M = 8) tile order. The
+  // hardware hands workgroups to the 8 XCDs round-robin in dispatch order (x fastest, then z); remapping the LINEAR
+  // id puts every tile of one K split on one XCD, so a split-K weight gradient with few output tiles (ResNet's 1x1
+  // layers: 4 tiles of 128 x 128 over 800k pixels) reads the operand the tiles share from that XCD's L2 once instead
+  // of from HBM once per tile (remapping x alone spread a split's 4 tiles over 4 XCDs)
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   const int nwg = tiles_m * tiles_n;
-  const int bid = blockIdx.x;
-  int wg;
+  int wg, zsplit;
   {
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int L = blockIdx.x + nwg * blockIdx.z, tot = nwg * gridDim.z;
+    const int xcd = L & 7, q = tot >> 3, r = tot & 7;
+    const int lam = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+    zsplit = lam / nwg;
+    wg = lam - zsplit * nwg;
   }
   const int group = 8 * tiles_n;
   const int first_m = (wg / group) * 8;
@@ -398,7 +404,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
   const int tn = (wg % group) / gm;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  const int kbeg = blockIdx.z * k_per_split;
+  const int kbeg = zsplit * k_per_split;
   const int kend = min(K, kbeg + k_per_split);
   const int nt = (kend - kbeg + BK - 1) / BK;
 
@@ -559,7 +565,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
   // ---- epilogue: lane holds C[m][n..n+3]
   // locals, not writes into the by-value kernarg struct: mutating E makes the compiler copy the whole
   // (large) Epi into scratch memory
-  void* const ec = E.mode == 3 ? (void*)(reinterpret_cast<float*>(E.c) + (long)blockIdx.z * E.slab) : E.c;
+  void* const ec = E.mode == 3 ? (void*)(reinterpret_cast<float*>(E.c) + (long)zsplit * E.slab) : E.c;
   const int emode = E.mode == 3 ? 0 : E.mode;  // mode 3 = this split's private fp32 slab, plain stores
   // LEAN (bf16 C, no bias / activation / pre-activation copy, mode store or accumulate; the convolution forward
   // and the data gradients): the tile goes through LDS and leaves as 16-B row-contiguous stores, and none of the

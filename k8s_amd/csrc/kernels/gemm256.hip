@@ -413,8 +413,15 @@ __global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, 
 
   const int tiles_m = (M + 255) >> 8, tiles_n = (N + 255) >> 8;
   const int bid = blockIdx.x;
-  int wg, split = 0, sk_slot = -1;
-  if (bid < SK.full) {
+  int wg, split = 0, sk_slot = -1, ysplit = 0;
+  if (gridDim.y > 1) {
+    // tall-K split over blockIdx.y (no stream-K): remap the LINEAR dispatch id (XCD = id % 8) so every tile of one
+    // split shares an XCD and the operand those tiles share is read once into its L2 (gemm.hip does the same)
+    const int L = bid + gridDim.x * blockIdx.y;
+    const int lam = xcd_remap(L, gridDim.x * gridDim.y);
+    ysplit = lam / gridDim.x;
+    wg = lam - ysplit * gridDim.x;
+  } else if (bid < SK.full) {
     wg = xcd_remap(bid, SK.full);
   } else {  // stream-K tail: a tile's splits are consecutive after the remap, so they share an XCD's L2
     const int j = xcd_remap(bid - SK.full, gridDim.x - SK.full);
@@ -432,8 +439,8 @@ __global__ void __launch_bounds__(g256::THREADS, 2) gemm256r_kernel(AS A, BS B, 
   // split-K: blockIdx.y (tall-K products, fp32 slabs combined by splitk_reduce) or the stream-K split; this block
   // reduces K range [koff, koff + kps)
   if (bid < SK.full && SK.sk > 1) kps = K;  // a whole tile of a stream-K launch: the full K range
-  const long koff = (long)(blockIdx.y + split) * kps;
-  if (E.slab) E.c = reinterpret_cast<float*>(E.c) + blockIdx.y * E.slab;
+  const long koff = (long)(ysplit + split) * kps;
+  if (E.slab) E.c = reinterpret_cast<float*>(E.c) + ysplit * E.slab;
   const uint16_t* ca0 = A.cursor(tid, 0, m0) + (AS::kmajor ? koff : koff * A.ld);
   const uint16_t* ca1 = A.cursor(tid, 1, m0) + (AS::kmajor ? koff : koff * A.ld);
   const uint16_t* cb0 = B.cursor(tid, 0, n0) + (BS::kmajor ? koff : koff * B.ld);

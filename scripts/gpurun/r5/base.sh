@@ -1,8 +1,8 @@
 #!/bin/bash
-# GPU job (round 5 start): whole GPU suite, smoke, default bench, ResNet-50 b1024 steady-state trace.
+# GPU job (round 5 ${1:-start}): whole GPU suite, smoke, default bench, ResNet-50 b1024 steady-state trace.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r5_base; rm -rf $O; mkdir -p $O
+O=gpurun_out/${1:-r5_base}; rm -rf $O; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/suite.log 2>&1 || { tail -40 $O/suite.log; exit 1; }
 tail -1 $O/suite.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
@@ -10,4 +10,4 @@ tail -1 $O/smoke.log
 timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 cut -c1-300 $O/bench.json
 timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/prof -o rn -- python3 bench.py --steps 8 --warmup 3 > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
-python3 scripts/profile_report.py $(ls $O/prof/*kernel_trace.csv | head -1) --step-marker sgd_kernel --top 75 --title "ResNet-50 b1024, round 5 start" > $O/rn.md && head -14 $O/rn.md
+python3 scripts/profile_report.py $(ls $O/prof/*kernel_trace.csv | head -1) --step-marker sgd_kernel --top 75 --title "ResNet-50 b1024, round 5 ${1:-start}" > $O/rn.md && head -14 $O/rn.md
