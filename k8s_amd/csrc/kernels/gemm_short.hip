@@ -365,9 +365,18 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
 bool gemm_short_ok(int M, int N, int K, long lda, long ldc) {
   const char* e = std::getenv("K8S_AMD_GEMM_SHORT");
   if (e && e[0] == '0') return false;
-  if (!(K == 64 || K == 128 || K == 256) || N % 128 != 0 || lda != K || ldc != N || M <= 0) return false;
-  const long lim = 1L << 31;
-  return (long)M * K * 2 < lim && (long)M * N * 2 < lim && (long)K * N * 2 < lim;
+  return (K == 64 || K == 128 || K == 256) && N % 128 == 0 && lda == K && ldc == N && M > 0;
+}
+
+// Rows per launch: every operand of one launch stays below 2 GiB (the kernel's 32-bit buffer offsets); larger
+// products (batch >= 2048 at 56 x 56: a 3.3 GB activation) run as consecutive row ranges, the statistics epilogue
+// accumulating across them. A multiple of 32 rows (whole tiles, whole mask bytes).
+static int gemm_short_rows_per_launch(int M, int N, int K) {
+  const long lim = (1L << 31) - (1L << 20);
+  const long per_row = 2L * (N > K ? N : K);
+  long rows = lim / per_row;
+  rows -= rows % 32;
+  return (int)(rows < M ? rows : M);
 }
 
 // epi 0: C = op(A) B^T; 1: C += ...; 2: C = op(A) B^T + (mask ? add : 0). b_mn: B stored [K][N] (ldb) else [N][K].
@@ -375,6 +384,16 @@ void launch_gemm_short(const uint16_t* A, const uint16_t* B, long ldb, bool b_mn
                        const uint8_t* mask, const float* xf, float* stats, int M, int N, int K, int epi,
                        hipStream_t st) {
   if (!gemm_short_ok(M, N, K, K, N)) throw std::runtime_error("gemm_short: shape outside the kernel's contract");
+  if ((long)K * N * 2 >= (1L << 31)) throw std::runtime_error("gemm_short: weight operand >= 2 GiB");
+  const int rows = gemm_short_rows_per_launch(M, N, K);
+  if (rows < M) {
+    for (int r0 = 0; r0 < M; r0 += rows) {
+      const int mr = M - r0 < rows ? M - r0 : rows;
+      launch_gemm_short(A + (long)r0 * K, B, ldb, b_mn, C + (long)r0 * N, add ? add + (long)r0 * N : nullptr,
+                        mask ? mask + (long)r0 * N / 8 : nullptr, xf, stats, mr, N, K, epi, st);
+    }
+    return;
+  }
   if ((epi == 2) != (add != nullptr) || (epi == 2 && !mask)) throw std::runtime_error("gemm_short: bad addend");
   if (epi != 0 && stats) throw std::runtime_error("gemm_short: statistics only with a plain store");
   gsk::Args g{A, B, C, add, mask, xf, stats, M, N, K, (int)ldb, N / gsk::BN, 0};

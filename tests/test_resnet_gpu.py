@@ -210,3 +210,37 @@ def test_downsample_bn_dual_matches_separate(cuda):
         # the first block's inputs are identical in both runs; later blocks see the other rounding of the residual
         tol = 1e-3 if n.startswith("blocks.0.") else 3e-2
         assert torch.allclose(s1[n], r, rtol=tol, atol=1e-3), (n, (s1[n] - r).abs().max().item())
+
+
+@pytest.mark.parametrize("half", [1024, 1536])
+def test_resnet50_large_batch_indexing_matches_half_batch(cuda, half):
+    """Every kernel at the 288-GB-sized batches (2048 / 3072 images: 56 x 56 activations past 2^31 bytes, and past
+    2^31 elements at 3072) against the same step at half the batch: a batch made of two copies of the half batch has
+    the same BatchNorm statistics, loss and parameter gradients (everything else is per sample), so any 32-bit
+    offset overflow in a kernel shows up as a mismatch."""
+    torch.manual_seed(0)
+    g = torch.Generator().manual_seed(11)
+    imgs = torch.randn(half, 224, 224, 3, generator=g).to(cuda).bfloat16()
+    y = torch.randint(0, 1000, (half,), generator=g).to(cuda)
+
+    def run(images, labels):
+        from k8s_amd.models.resnet import resnet50
+
+        store = ParamStore()
+        m = resnet50(store).finalize(cuda, seed=5)
+        m.train()
+        x = m.prepare_input(images).contiguous()
+        store.begin_step()
+        loss = K.cross_entropy(m(x), labels)
+        loss.backward()
+        store.zero_unwritten()
+        out = (float(loss.float().item()), store.grad.clone())
+        del m, store, x
+        torch.cuda.empty_cache()
+        return out
+
+    l1, g1 = run(imgs, y)
+    l2, g2 = run(torch.cat([imgs, imgs]), torch.cat([y, y]))
+    assert abs(l1 - l2) < 1e-3 * max(1.0, abs(l1)), (l1, l2)
+    rel = ((g1 - g2).norm() / (g1.norm() + 1e-12)).item()
+    assert rel < 2e-2, rel
