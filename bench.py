@@ -6,7 +6,7 @@ Metric and config come from BASELINE.json ("images/sec ResNet-50 TfJob at
 classes, random-init weights -- no datasets or checkpoints are reachable),
 bf16 compute with fp32 master weights/BN statistics, SGD+momentum (fused HIP
 kernel), data parallel with bucketed RCCL all-reduce overlapped with
-backward. Per-GPU batch (default 1024, sized for 288 GB HBM) is fixed as N grows (weak scaling).
+backward. Per-GPU batch (default 3072, 113 GB of the 288 GB HBM) is fixed as N grows (weak scaling).
 
     python bench.py --gpus N --steps K --warmup W
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -51,10 +51,11 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    # 1024 images per GPU (41 GB peak of 288 GB HBM, reported as peak_mem_gb): measured on MI355X 9102 img/s vs
-    # 8913 at 768, 8498 at 512 and 7535 at 256 -- the 7x7 / 14x14 layers fill the 256 CUs only at large batch
-    # (profiles/r01_batch_sweep.md)
-    ap.add_argument("--batch", type=int, default=1024, help="per-GPU batch")
+    # 3072 images per GPU (113 GB peak of 288 GB HBM, reported as peak_mem_gb): one MI355X box, round 5 tree,
+    # 14,870 img/s vs 14,712 at 2048 and 14,287 at 1024 (profiles/r05_batch_sweep.jsonl) -- the 7x7 / 14x14
+    # layers and the per-launch prologues amortise over more rows; >= 2048 exercises the chunked short-K launches
+    # (tests/test_resnet_gpu.py duplicated-half-batch check at 2048 / 3072)
+    ap.add_argument("--batch", type=int, default=3072, help="per-GPU batch")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--grad-comm", choices=["fp32", "bf16"], default="fp32",

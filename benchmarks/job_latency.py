@@ -6,9 +6,9 @@ Brings up the one-box cluster (fake API server + local kubelet + the C++
 ``amd.com/gpu: 1`` (CPU fallback: ``resnet_tiny`` without a GPU), and
 measures from just before the create POST to the trainer's ``step0`` record
 (first optimizer step finished, loss synced to host). Also reports the split:
-create -> trainer process start (operator reconcile + kubelet) and process
-start -> step 0 (imports, model build on the GPU, first step incl. conv
-autotuning), and the job's total time to ``Succeeded``.
+create -> trainer process start (operator reconcile + kubelet), the process's
+interpreter start + imports, setup (model / optimizer / synthetic data on the
+GPU) and the first step itself, and the job's total time to ``Succeeded``.
 
     python benchmarks/job_latency.py [--runs 3] [--steps 5]
 
@@ -92,6 +92,13 @@ def main(argv=None):
             results.append({"create_to_step0_s": ev["step0"]["time"] - t0, "create_to_trainer_start_s": start - t0,
                             "trainer_start_to_step0_s": ev["step0"]["time"] - start,
                             "create_to_succeeded_s": t_done - t0})
+            proc = ev["start"].get("process_start_time")
+            if proc:  # operator + kubelet, then interpreter start + imports (torch, the extension)
+                results[-1]["create_to_process_start_s"] = proc - t0
+                results[-1]["process_imports_s"] = start - proc
+            for k in ("setup_s", "first_step_s"):  # model / optimizer / data build, then step 0 itself
+                if k in ev["step0"]:
+                    results[-1]["step0_" + k] = ev["step0"][k]
             rates = [v for r in steps_ev for k, v in r.items() if k.endswith("_per_sec")]
             if len(rates) >= 2:  # the first interval includes the warm-up steps after step 0
                 results[-1]["tfjob_steady_rate"] = statistics.median(rates[1:])

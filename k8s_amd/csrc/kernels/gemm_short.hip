@@ -375,6 +375,10 @@ static int gemm_short_rows_per_launch(int M, int N, int K) {
   const long lim = (1L << 31) - (1L << 20);
   const long per_row = 2L * (N > K ? N : K);
   long rows = lim / per_row;
+  if (const char* e = std::getenv("K8S_AMD_GEMM_SHORT_ROWS")) {  // tests: force the chunked path at small sizes
+    const long r = std::atol(e);
+    if (r >= 32 && r < rows) rows = r;
+  }
   rows -= rows % 32;
   return (int)(rows < M ? rows : M);
 }

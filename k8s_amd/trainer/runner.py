@@ -101,8 +101,21 @@ def parse(argv=None):
 
 # resnet50: the headline config's per-GPU batch (bench.py --batch default), so the TfJob path and the bench run the
 # same thing
-_DEFAULT_BATCH = {"resnet50": 1024, "resnet_tiny": 8, "bert_base": 64, "bert_tiny": 4, "llama3_8b": 2,
+_DEFAULT_BATCH = {"resnet50": 3072, "resnet_tiny": 8, "bert_base": 64, "bert_tiny": 4, "llama3_8b": 2,
                   "llama_1b": 4, "llama_tiny": 2}
+
+
+def _process_start_time() -> Optional[float]:
+    """Wall-clock start of this process (age from /proc/self/stat starttime vs /proc/uptime, 10 ms resolution): the
+    interpreter and import time before train() runs is part of create -> step 0 and is reported apart from it."""
+    try:
+        with open("/proc/self/stat") as f:
+            ticks = int(f.read().rsplit(")", 1)[1].split()[19])  # field 22 of stat(5); the split starts at field 3
+        with open("/proc/uptime") as f:
+            up = float(f.read().split()[0])
+        return time.time() - (up - ticks / os.sysconf("SC_CLK_TCK"))
+    except (OSError, ValueError, IndexError):
+        return None
 
 
 class _Metrics:
@@ -277,6 +290,7 @@ def train(a) -> int:
     from k8s_amd.utils.trace import Tracer, Watchdog
 
     t_start = time.time()
+    t_proc = _process_start_time()
     tf_config = os.environ.get("TF_CONFIG")
     info = kdist.rank_from_env()
     if info is not None and info.role == "ps" and tf_config:
@@ -305,7 +319,7 @@ def train(a) -> int:
     comm = a.grad_comm if a.grad_comm != "auto" else "fp32"
     metrics = _Metrics(a.logdir, chief)
     metrics.event(event="start", rank=rank, world=world, role=info.role, model=a.model, strategy=a.strategy,
-                  device=str(dev), start_time=t_start, zero1=bool(sharded and world > 1), grad_comm=comm,
+                  device=str(dev), start_time=t_start, process_start_time=t_proc, zero1=bool(sharded and world > 1), grad_comm=comm,
                   optimizer=opt_name, batch=batch)
 
     # the sharded parameter service needs the flat buffers divisible into world equal 64-aligned shards
@@ -345,6 +359,7 @@ def train(a) -> int:
 
         psv = PsVariables(ps_addrs)
     start_step = _restore(a, w, opt, dev, chief, world, metrics, psv, svc)
+    t_ready = time.time()  # model, optimizer and data built, checkpoint restored
     if world > 1:
         # step-0 transport self-check: one gradient bucket through the configured transport
         # (fp32 / bf16 all-reduce, ZeRO-1 push) against a plain fp32 all_reduce; the verdict is the same on every
@@ -457,7 +472,8 @@ def train(a) -> int:
                 now = time.time()
                 rate = n_last * w.units_per_step * world / max(now - t_last, 1e-9)
                 if step == start_step:
-                    metrics.event(event="step0", step=step, loss=loss_v, since_start=now - t_start)
+                    metrics.event(event="step0", step=step, loss=loss_v, since_start=now - t_start,
+                                  setup_s=round(t_ready - t_start, 4), first_step_s=round(now - t_ready, 4))
                 else:
                     extra = {"phase_ms": tracer.summary_ms()} if tracer.sync else {}
                     metrics.event(event="step", step=step, loss=loss_v, lr=cur_lr,

@@ -124,4 +124,36 @@ def test_short_contract(cuda):
     assert not C_.gemm_short_ok(1024, 192, 128)   # N % 128
     assert not C_.gemm_short_ok(1024, 256, 512)   # long reduction: the tile kernels
     assert not C_.gemm_short_ok(1024, 256, 96)
-    assert not C_.gemm_short_ok(1 << 24, 256, 128)  # > 2 GiB operand: 32-bit buffer offsets
+    # > 2 GiB operands run as row-chunked launches (each under the 32-bit buffer-offset range)
+    assert C_.gemm_short_ok(1 << 24, 256, 128)
+
+
+@pytest.mark.parametrize("M,K,N", [(6272, 128, 256), (10007, 64, 256)])
+def test_short_row_chunked_launches_match_one_launch(cuda, M, K, N, monkeypatch):
+    """Products above 2 GiB run as consecutive row ranges (gemm_short_rows_per_launch); K8S_AMD_GEMM_SHORT_ROWS
+    forces that path at a small size. Outputs are bit-identical to one launch (rows are independent); the BN
+    statistics accumulate across the launches; the masked dgrad reads its mask bytes from each range's offset."""
+    C_ = _C()
+    torch.manual_seed(5)
+    x = (torch.randn(1, 1, M, K, device=cuda) + 0.2).bfloat16()
+    w = (torch.randn(N, 1, 1, K, device=cuda) * K ** -0.5).bfloat16()
+    p = _bn_params(K, cuda, 6)
+    gy = torch.randn(M, K, device=cuda).bfloat16()
+    wd = (torch.randn(K, N, device=cuda) * K ** -0.5).bfloat16()
+    dy = torch.randn(M, N, device=cuda).bfloat16()
+    mask = torch.randint(0, 256, (M * N // 8,), device=cuda, dtype=torch.uint8)
+
+    def run():
+        st = torch.zeros(C_.conv_stat_replicas, 2, N, device=cuda)
+        y = C_.conv_fwd(x, w, 1, 0, 1, False, None, 0, st, xform=p)
+        out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+        C_.gemm(gy, True, wd, False, out, False, None, 0, None, True, 1.0, 1, dy, mask)
+        torch.cuda.synchronize()
+        return y, st.sum(0), out
+
+    y1, s1, d1 = run()
+    monkeypatch.setenv("K8S_AMD_GEMM_SHORT_ROWS", "1024")  # 7-10 launches, the last one ragged
+    y2, s2, d2 = run()
+    assert torch.equal(y1, y2)
+    assert torch.equal(d1, d2)
+    torch.testing.assert_close(s2, s1, rtol=1e-5, atol=1e-2)
