@@ -4,7 +4,9 @@ Times every unique conv (fwd with the BN-statistics epilogue, weight gradient, d
 BatchNorm (forward apply, backward reduce + apply) of ResNet-50 v1.5 at the bench batch, multiplies by how
 often the shape occurs per step, and prints one JSON line per (layer, op) with the achieved TFLOP/s (convs) or
 TB/s of compulsory HBM traffic (BN), then a summary line. Shapes and dispatch are exactly the trainer's
-(``ops/conv.py``, ``ops/nn.py``).
+(``ops/conv.py``, ``ops/nn.py``): the stem is the space-to-depth 4x4 kernel pair of ``stem.hip``, the conv3 layers
+read their input normalised on load (BN2, ``nn._BnReluConv``: forward and weight gradient with ``xform``), and the
+identity blocks' conv1 data gradient adds the masked residual gradient in its epilogue (``nn.MaskedGrad``).
 
     python scripts/layer_roofline.py [--batch 1024] [--reps 5]
 """
@@ -79,15 +81,36 @@ def main():
         flops = 2.0 * N * Ho * Ho * K * C * R * R
         M = N * Ho * Ho
         res = {}
+        # the bench's operand paths (module docstring)
+        xf = None
+        if name.endswith("conv3"):
+            xf = torch.cat([torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1]).contiguous()
+        addend = None
+        if name.endswith("bx.conv1"):
+            from k8s_amd.ops import nn as K_
+
+            addend = K_.MaskedGrad(torch.randn(N, H, H, C, device=dev, dtype=torch.bfloat16),
+                                   torch.randint(0, 256, (N * H * H * C // 8,), device=dev, dtype=torch.uint8))
+        if name == "stem":
+            img = torch.randn(N, 224, 224, 8, device=dev, dtype=torch.bfloat16)
+            xs = C_.stem_s2d_input(img, 3)
+            w4 = C_.stem_w_s2d(w)
         if "fwd" in only:
             st = torch.zeros(C_.conv_stat_replicas, 2, K, device=dev)
-            res["fwd"] = timed(lambda: C_.conv_fwd(x, w, s, pad, 1, False, None, 0, st), a.reps)
+            if name == "stem":
+                res["fwd"] = timed(lambda: C_.stem_conv_fwd(xs, w4, st), a.reps)
+            else:
+                res["fwd"] = timed(lambda: C_.conv_fwd(x, w, s, pad, 1, False, None, 0, st, xform=xf), a.reps)
         if "wgrad" in only:
             dw = torch.empty(K, R, R, C, device=dev)
-            res["wgrad"] = timed(lambda: conv._wgrad_hip(C_, gy, x, dw, s, pad, False), a.reps)
+            if name == "stem":
+                dw4 = torch.empty(tuple(w4.shape), device=dev)
+                res["wgrad"] = timed(lambda: (C_.stem_wgrad(xs, gy, dw4), C_.stem_dw_s2d(dw4, dw)), a.reps)
+            else:
+                res["wgrad"] = timed(lambda: conv._wgrad_hip(C_, gy, x, dw, s, pad, False, xf), a.reps)
         if "dgrad" in only and name != "stem":
             if s == 1:
-                res["dgrad"] = timed(lambda: conv._dgrad_hip(C_, gy, w, pad), a.reps)
+                res["dgrad"] = timed(lambda: conv._dgrad_hip(C_, gy, w, pad, addend), a.reps)
             else:
                 res["dgrad"] = timed(lambda: conv._dgrad_strided_hip(C_, gy, w, s, pad, H, H), a.reps)
         # compulsory HBM bytes per op (bf16 activations, fp32 weight gradient) and the speed-of-light floor
@@ -97,7 +120,7 @@ def main():
         for op in ("fwd", "wgrad", "dgrad"):
             if op in res:
                 floor = max(nb[op] / 8e9, flops / 2.5e12)
-                rows.append({"layer": name, "op": op, "count": cnt, "ms": round(res[op], 4),
+                rows.append({"layer": name, "op": op, "count": cnt, "batch": N, "ms": round(res[op], 4),
                              "step_ms": round(res[op] * cnt, 3), "tflops": round(flops / res[op] / 1e9, 1),
                              "floor_ms": round(floor, 4), "sol": round(floor / res[op], 2),
                              "lost_ms_per_step": round((res[op] - floor) * cnt, 3)})
