@@ -100,8 +100,10 @@ def parse(argv=None):
 
 
 # resnet50: the headline config's per-GPU batch (bench.py --batch default), so the TfJob path and the bench run the
-# same thing
-_DEFAULT_BATCH = {"resnet50": 3072, "resnet_tiny": 8, "bert_base": 64, "bert_tiny": 4, "llama3_8b": 2,
+# same thing. Transformers sized for the 288 GB HBM (one MI355X, round 5, profiles/r05_transformer_batch.jsonl):
+# BERT-base s128 676k tok/s at 64 -> 930k at 256 -> 1.03M at 512 -> 1.06M at 1024 (41 GB); Llama-3-8B s4096
+# 17.9k at 1 -> 20.1-20.5k at 2 -> 21.7k at 4 (211 GB peak)
+_DEFAULT_BATCH = {"resnet50": 3072, "resnet_tiny": 8, "bert_base": 1024, "bert_tiny": 4, "llama3_8b": 4,
                   "llama_1b": 4, "llama_tiny": 2}
 
 
@@ -504,7 +506,9 @@ def train(a) -> int:
     from k8s_amd.ops import gemm as kgemm
 
     metrics.event(event="done", steps=a.steps, loss=loss_v, elapsed=time.time() - t_start, rank=rank,
-                  weights_sum=float(w.store.master.double().sum().item()), gemm_fallbacks=dict(kgemm.FALLBACKS))
+                  weights_sum=float(w.store.master.double().sum().item()), gemm_fallbacks=dict(kgemm.FALLBACKS),
+                  peak_mem_gb=(round(torch.cuda.max_memory_allocated(w.store.master.device) / 2**30, 1)
+                               if w.store.master.is_cuda else None))
     metrics.close()
     if chief:
         _shutdown_ps(tf_config)
