@@ -567,11 +567,20 @@ constexpr int LDS_BYTES = 2 * STAGE;   // 128 KB
 #define K8S_G4_MFMA(acc, b, a) \
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a))
 
-template <bool AMN, bool BMN>
+// X: the transformer linears' bf16 epilogue extras -- bias (fp32, added before the one rounding of the staged
+// value), ReLU / GELU of the staged pre-activation, its copy to `pre` (what the activation backward reads) and a bf16
+// accumulate (C = result + old C; a residual's second gradient contribution) -- in the row-contiguous copy-out. Its
+// own instantiation so the plain kernels keep their code and registers.
+// Tall-K split (gridDim.y > 1, the weight gradients of outputs with fewer tiles than CUs): split y reduces K range
+// [y kps, min(K, (y + 1) kps)) into the fp32 slab at C + y * slab (plain store), combined by splitk_reduce; the last
+// split may be shorter, so the split count is free to fill the chip (9 BERT tiles x 28 splits = 252 blocks).
+template <bool AMN, bool BMN, bool X>
 __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __restrict__ A, long lda,
                                                              const uint16_t* __restrict__ B, long ldb, void* Cv,
                                                              long ldc, int M, int N, int K, float alpha, int kps,
-                                                             g256r::SkArgs SK, int out_f32, int accumulate) {
+                                                             g256r::SkArgs SK, int out_f32, int accumulate,
+                                                             const float* __restrict__ bias, int act,
+                                                             uint16_t* __restrict__ pre, long slab) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -581,7 +590,12 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
   // whole tiles [0, SK.full), then the stream-K tail: (tile, split) pairs of K range kps (as gemm256r_kernel)
   const int bid = blockIdx.x;
   int wg, split = 0, sk_slot = -1;
-  if (bid < SK.full) {
+  if (gridDim.y > 1) {  // tall-K split: the linear (tile, split) id remapped so a split's tiles share an XCD
+    const int lam = g256r::xcd_remap(bid + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+    split = lam / gridDim.x;
+    wg = lam - split * gridDim.x;
+    Cv = reinterpret_cast<float*>(Cv) + (long)split * slab;
+  } else if (bid < SK.full) {
     wg = g256r::xcd_remap(bid, SK.full);
     kps = K;
   } else {
@@ -724,7 +738,7 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
   using T_ = std::true_type;
   using F_ = std::false_type;
 
-  const int nst = kps / KS;
+  const int nst = (int)(((long)K - koff < kps ? (long)K - koff : (long)kps) / KS);  // a tall-K split's last range
 #pragma unroll
   for (int p = 0; p < 16; ++p) dma(p, 0, 0);
   if (nst > 1) {
@@ -865,9 +879,16 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
         for (int z = 1; z < SK.sk; ++z)
           v += __builtin_amdgcn_raw_buffer_load_b128(srs, tid * 16, z * 262144 + (f * 8 + j) * THREADS * 16, 0);
       }
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (X) {
+        if (bias) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bv[r] = bias[n0 + wc * 128 + lc + r];
+        }
+      }
       bf16x4_t o;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r] * alpha);
+      for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(__builtin_fmaf(v[r], alpha, bv[r]));
       *reinterpret_cast<bf16x4_t*>(stg + lr * 256 + (((lc >> 3) ^ (lr & 15)) << 4) + (lc & 4) * 2) = o;
     }
   }
@@ -875,27 +896,55 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
 #pragma unroll 4
   for (int it = 0; it < 32; ++it) {
     const int idx = it * 64 + lane, lr = idx >> 4, ch = idx & 15;
-    const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(stg + lr * 256 + ((ch ^ (lr & 15)) << 4));
-    *reinterpret_cast<bf16x8_t*>(C + (long)(m0 + wr * 128 + lr) * ldc + n0 + wc * 128 + ch * 8) = v;
+    bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(stg + lr * 256 + ((ch ^ (lr & 15)) << 4));
+    const long off = (long)(m0 + wr * 128 + lr) * ldc + n0 + wc * 128 + ch * 8;
+    if constexpr (X) {
+      if (pre) *reinterpret_cast<bf16x8_t*>(pre + off) = v;  // the staged pre-activation (bias included)
+      if (act || accumulate) {
+        float f[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float x = bf2f((uint16_t)v[r]);
+          f[r] = act == 1 ? fmaxf(x, 0.f) : (act == 2 ? g256::gelu_tanh(x) : x);
+        }
+        if (accumulate) {  // one more bf16 rounding on top of the staged value (<= 1 ulp), as gemm.hip's lean path
+          const bf16x8_t old = *reinterpret_cast<const bf16x8_t*>(C + off);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) f[r] += bf2f((uint16_t)old[r]);
+        }
+        v = pack_bf16x8(f);
+      }
+    }
+    *reinterpret_cast<bf16x8_t*>(C + off) = v;
   }
 }
 #undef K8S_G4_MFMA
 }  // namespace g4
 
-// The 4-wave NT kernel's contract: both operands K-major, whole 256 x 256 tiles (M, N % 256), K % 64, 16-B aligned
-// rows, a plain bf16 output (no bias / activation / pre-activation / accumulate, alpha allowed), no tall-K split, and
-// at least one wave of tiles (a partial last wave takes the stream-K tail). $K8S_AMD_GEMM_W4=0 keeps such products on the ring kernel (A/B;
-// read per call, both sides tested).
+// The 4-wave kernel's contract: any operand layout, whole 256 x 256 tiles (M, N % 256), K % 64, 16-B aligned rows;
+// a bf16 output with the X extras (bias / ReLU / GELU / pre-activation copy / bf16 accumulate) or an fp32 one (stored or
+// accumulated, alpha allowed); at least one wave of tiles (a partial last wave takes the stream-K tail) -- or, as a
+// tall-K split of a plain fp32 product, one wave of (tile, split) blocks. $K8S_AMD_GEMM_W4=0 keeps such products on
+// the ring kernel (A/B; read per call, both sides tested).
+static bool w4_enabled() {
+  const char* e = getenv("K8S_AMD_GEMM_W4");
+  return !(e && e[0] == '0');
+}
 static bool w4_ok(bool a_kmajor, bool b_kmajor, bool c_f32, int M, int N, int K, long lda, long ldb, long ldc,
                   const float* bias, int act, const uint16_t* pre, bool accumulate, int splits, int sk) {
-  const char* e = getenv("K8S_AMD_GEMM_W4");
-  if (e && e[0] == '0') return false;
+  if (!w4_enabled()) return false;
   (void)sk;
   (void)a_kmajor;  // every operand layout: K-major (read as rows) or MN-major (transposed reads)
   (void)b_kmajor;
-  return !bias && act == 0 && !pre && (!accumulate || c_f32) && splits == 1 && M % 256 == 0 && N % 256 == 0 &&
-         K % 64 == 0 && (lda | ldb | ldc) % 8 == 0 && (M / 256) * (N / 256) >= planner_cus();
+  const bool extras = bias || act != 0 || pre || (accumulate && !c_f32);
+  if (c_f32 && extras) return false;             // fp32 outputs: plain store / accumulate
+  if (splits > 1 && (!c_f32 || accumulate)) return false;  // split slabs: plain fp32 stores
+  if (M % 256 != 0 || N % 256 != 0 || K % 64 != 0 || (lda | ldb | ldc) % 8 != 0) return false;
+  const long tiles = (long)(M / 256) * (N / 256);
+  return splits > 1 ? tiles * splits >= 3L * planner_cus() / 4 : tiles >= planner_cus();
 }
+// K range per split of a tall-K split on the 4-wave kernel (whole 64-deep stages; the last split takes the rest)
+static int w4_split_kps(int K, int splits) { return (K / 64 + splits - 1) / splits * 64; }
 
 // Stream-K tail plan for a grid of 256 x 256 tiles on P = planner_cus() CUs (one block per CU; 256 on MI355X): with
 // T = w * P + r tiles and 0 < r <= P / 2, the last r tiles are split sk = min(P / r, 4) ways along K (each split a multiple of 64 deep and
@@ -956,6 +1005,18 @@ bool gemm256_eligible(int M, int N, int K, bool a_kmajor, bool b_kmajor) {
 int gemm256_choose_splits(int M, int N, int K) {
   const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
   const long fill = 3L * planner_cus() / 4;
+  if (w4_enabled() && M % 256 == 0 && N % 256 == 0 && K % 64 == 0) {
+    // the 4-wave kernel takes uneven splits: as many as fit one wave of (tile, split) blocks at one block per CU,
+    // each >= 512 deep (8 stages) -- BERT-base's weight gradients at 131k tokens: 9 tiles x 28, 27 x 9, 36 x 7
+    long s = planner_cus() / tiles;
+    s = s > 64 ? 64 : s;
+    while (s > 1 && K / s < 512) --s;
+    if (s >= 2 && tiles * s >= fill) {  // (w4_ok's split condition)
+      const int kps = w4_split_kps(K, (int)s);
+      return (K + kps - 1) / kps;  // splits actually launched (every one non-empty)
+    }
+    if (tiles >= fill) return 1;
+  }
   int best = 1;
   for (int s = 2; s <= 64; ++s) {
     if (tiles * (s / 2) >= fill) break;  // the previous s already filled the chip
@@ -972,31 +1033,53 @@ void launch_gemm256(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* 
                     int* sk_sync) {
   if (K % 64 != 0) throw std::runtime_error("gemm256: K must be a multiple of 64");
   if (splits < 1) splits = 1;
-  if (splits > 1 && (!c_f32 || bias || act || pre || !ws || K % (64 * splits) != 0 || ldc != N))
-    throw std::runtime_error("gemm256 split-K: plain fp32 output, K % (64 * splits) == 0, a workspace");
+  if (splits > 1 && (!c_f32 || bias || act || pre || !ws || ldc != N))
+    throw std::runtime_error("gemm256 split-K: plain fp32 output and a workspace");
   g256::Epi e{splits > 1 ? (void*)ws : C, ldc, bias, pre, c_f32 ? 1 : 0, act, (splits == 1 && accumulate) ? 1 : 0,
               alpha, splits > 1 ? (long)M * N : 0};
   Gemm256Plan plan = gemm256_plan(M, N, K);
   if (splits > 1 || !sk_slabs || !sk_sync) plan.sk = 1;  // tall-K split, or no stream-K workspace given
   using namespace g256r;
-  if (w4_ok(a_kmajor, b_kmajor, c_f32, M, N, K, lda, ldb, ldc, bias, act, pre, accumulate, splits, plan.sk)) {
+  if (w4_ok(a_kmajor, b_kmajor, c_f32, M, N, K, lda, ldb, ldc, bias, act, pre, splits > 1 ? false : accumulate,
+            splits, plan.sk)) {
     const int tiles = (M / 256) * (N / 256);
     g256r::SkArgs sk{tiles, 1, nullptr, nullptr};
-    int blocks = tiles, kps = K;
-    if (plan.sk > 1) {  // the stream-K tail (gemm256_plan), fixed up in-kernel as in the ring kernel
+    int blocks = tiles, kps = K, ysplits = 1;
+    if (splits > 1) {  // tall-K split: slabs of ws, then splitk_reduce (which also applies `accumulate`)
+      kps = w4_split_kps(K, splits);
+      ysplits = (K + kps - 1) / kps;
+    } else if (plan.sk > 1) {  // the stream-K tail (gemm256_plan), fixed up in-kernel as in the ring kernel
       sk = g256r::SkArgs{plan.full, plan.sk, sk_slabs, sk_sync};
       kps = plan.kps;
       blocks = plan.full + (tiles - plan.full) * plan.sk;
     }
-#define K8S_W4L(AM, BM)                                                                                     \
-  hipLaunchKernelGGL((g4::gemm_w4_kernel<AM, BM>), dim3(blocks), dim3(g4::THREADS), 0, st, A, lda, B, ldb, C, ldc, \
-                     M, N, K, alpha, kps, sk, c_f32 ? 1 : 0, accumulate ? 1 : 0)
-    if (a_kmajor && b_kmajor) K8S_W4L(false, false);
-    else if (a_kmajor) K8S_W4L(false, true);
-    else if (b_kmajor) K8S_W4L(true, false);
-    else K8S_W4L(true, true);
+    const bool x = bias || act != 0 || pre || (accumulate && !c_f32);
+    void* const cv = splits > 1 ? (void*)ws : C;
+    const int acc = splits > 1 ? 0 : (accumulate ? 1 : 0);
+#define K8S_W4L(AM, BM, XX)                                                                                         \
+  hipLaunchKernelGGL((g4::gemm_w4_kernel<AM, BM, XX>), dim3(blocks, ysplits), dim3(g4::THREADS), 0, st, A, lda, B, \
+                     ldb, cv, ldc, M, N, K, alpha, kps, sk, c_f32 ? 1 : 0, acc, bias, act, pre, (long)M * N)
+#define K8S_W4X(AM, BM)       \
+  do {                        \
+    if (x)                    \
+      K8S_W4L(AM, BM, true);  \
+    else                      \
+      K8S_W4L(AM, BM, false); \
+  } while (0)
+    if (a_kmajor && b_kmajor) K8S_W4X(false, false);
+    else if (a_kmajor) K8S_W4X(false, true);
+    else if (b_kmajor) K8S_W4X(true, false);
+    else K8S_W4X(true, true);
+#undef K8S_W4X
 #undef K8S_W4L
+    if (splits > 1) splitk_reduce(ws, ysplits, (long)M * N, reinterpret_cast<float*>(C), accumulate, st);
     return;
+  }
+  while (splits > 1 && K % (64 * splits) != 0) --splits;  // the ring kernel takes even splits only (ws holds more)
+  e.slab = splits > 1 ? (long)M * N : 0;
+  if (splits == 1) {
+    e.c = C;
+    e.accumulate = accumulate ? 1 : 0;
   }
   if (a_kmajor && b_kmajor)
     g256::launch_ring(KMaj{A, lda, M}, KMaj{B, ldb, N}, e, M, N, K, splits, plan, sk_slabs, sk_sync, st);

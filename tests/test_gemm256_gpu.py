@@ -235,3 +235,60 @@ def test_gemm_w4_matches_fp32(cuda, monkeypatch, M, N, K, ak, bk):
     assert _rel(y, y0) < 1e-2
     c0 = _C().gemm(A, ak, B, bk, None, True, None, 0, None, False, 1.0, 1)
     assert _rel(c, c0) < 1e-5
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("bias", [False, True])
+def test_gemm_w4_epilogue_extras(cuda, monkeypatch, act, bias):
+    """The 4-wave kernel's X epilogue (the transformer linears at a batch that fills the chip: BERT-base at 131k
+    tokens): bias + ReLU / GELU + the pre-activation copy for the forward form, and the bf16 accumulate of the data
+    gradient, against fp32 PyTorch and against the ring kernel ($K8S_AMD_GEMM_W4=0)."""
+    torch.manual_seed(8)
+    M, N, K = 8192, 3072, 768  # 32 x 12 = 384 tiles: whole waves + a stream-K tail
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) * 0.05).bfloat16()
+    bvec = torch.randn(N, device=cuda) if bias else None
+    p_ref = a.float() @ w.float().t() + (bvec if bias else 0.0)
+    y_ref = [p_ref, torch.relu(p_ref), F.gelu(p_ref, approximate="tanh")][act]
+    out = {}
+    for side in ("1", "0"):
+        monkeypatch.setenv("K8S_AMD_GEMM_W4", side)
+        pre = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+        y = _C().gemm(a, True, w, True, None, False, bvec, act, pre, False, 1.0, 1)
+        assert _rel(pre, p_ref) < 1e-2 and _rel(y, y_ref) < 1e-2, side
+        y2 = _C().gemm(a, True, w, True, None, False, bvec, act, None, False, 1.0, 1)  # no pre-activation copy
+        assert _rel(y2, y_ref) < 1e-2, side
+        out[side] = y
+    assert _rel(out["1"], out["0"]) < 1e-2
+    # data-gradient form with a bf16 accumulate (a residual's other gradient contribution added in the epilogue)
+    g = torch.randn(M, N, device=cuda).bfloat16()
+    old = torch.randn(M, K, device=cuda).bfloat16()
+    monkeypatch.setenv("K8S_AMD_GEMM_W4", "1")
+    dx = old.clone()
+    _C().gemm(g, True, w, False, dx, False, None, 0, None, True, 1.0, 1)
+    assert _rel(dx, old.float() + g.float() @ w.float()) < 1e-2
+
+
+W4_SPLIT_SHAPES = [(768, 768, 65536), (2304, 768, 32768), (768, 3072, 16384), (256, 1024, 65536)]
+
+
+@pytest.mark.parametrize("M,N,K", W4_SPLIT_SHAPES)
+def test_gemm_w4_tall_k_split(cuda, monkeypatch, M, N, K):
+    """Weight gradients of few output tiles on the 4-wave kernel: the K range split unevenly over gridDim.y (the last
+    split shorter) into fp32 slabs, combined by splitk_reduce -- stored and accumulated into an existing slot, against
+    fp32 PyTorch and the ring kernel's even split; deterministic over repeated launches."""
+    torch.manual_seed(9)
+    g = torch.randn(K, M, device=cuda).bfloat16()  # both operands MN-major, as linear_bwd's dW = g^T x
+    x = torch.randn(K, N, device=cuda).bfloat16()
+    ref = g.float().t() @ x.float()
+    monkeypatch.setenv("K8S_AMD_GEMM_W4", "1")
+    c = _C().gemm(g, False, x, False, None, True, None, 0, None, False, 1.0, 0)
+    assert _rel(c, ref) < 1e-4
+    for _ in range(2):
+        assert torch.equal(_C().gemm(g, False, x, False, None, True, None, 0, None, False, 1.0, 0), c)
+    out = torch.full((M, N), 2.0, device=cuda)
+    _C().gemm(g, False, x, False, out, True, None, 0, None, True, 1.0, 0)
+    assert _rel(out - 2.0, ref) < 1e-4
+    monkeypatch.setenv("K8S_AMD_GEMM_W4", "0")
+    c0 = _C().gemm(g, False, x, False, None, True, None, 0, None, False, 1.0, 0)
+    assert _rel(c, c0) < 1e-5
