@@ -739,6 +739,15 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
   using F_ = std::false_type;
 
   const int nst = (int)(((long)K - koff < kps ? (long)K - koff : (long)kps) / KS);  // a tall-K split's last range
+  // X: this lane's bias columns (4 per 16-wide block j), loaded once here and held through the K loop -- loaded per
+  // fragment in the epilogue, each load's wait was exposed 64 times per tile (QKV forward 31 us per tile vs 26.5)
+  f32x4_t bj[X ? 8 : 1];
+  if constexpr (X) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      bj[j] = bias ? *reinterpret_cast<const f32x4_t*>(bias + n0 + wc * 128 + j * 16 + 4 * (lane >> 4))
+                   : f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
 #pragma unroll
   for (int p = 0; p < 16; ++p) dma(p, 0, 0);
   if (nst > 1) {
@@ -879,43 +888,63 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
         for (int z = 1; z < SK.sk; ++z)
           v += __builtin_amdgcn_raw_buffer_load_b128(srs, tid * 16, z * 262144 + (f * 8 + j) * THREADS * 16, 0);
       }
-      float bv[4] = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (X) {
-        if (bias) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) bv[r] = bias[n0 + wc * 128 + lc + r];
-        }
-      }
+      f32x4_t b4 = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (X) b4 = bj[j];
       bf16x4_t o;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(__builtin_fmaf(v[r], alpha, bv[r]));
+      for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(__builtin_fmaf(v[r], alpha, b4[r]));
       *reinterpret_cast<bf16x4_t*>(stg + lr * 256 + (((lc >> 3) ^ (lr & 15)) << 4) + (lc & 4) * 2) = o;
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private region: no barrier needed
-#pragma unroll 4
-  for (int it = 0; it < 32; ++it) {
+  auto coff = [&](int it) {
     const int idx = it * 64 + lane, lr = idx >> 4, ch = idx & 15;
-    bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(stg + lr * 256 + ((ch ^ (lr & 15)) << 4));
-    const long off = (long)(m0 + wr * 128 + lr) * ldc + n0 + wc * 128 + ch * 8;
-    if constexpr (X) {
-      if (pre) *reinterpret_cast<bf16x8_t*>(pre + off) = v;  // the staged pre-activation (bias included)
-      if (act || accumulate) {
-        float f[8];
+    return (long)(m0 + wr * 128 + lr) * ldc + n0 + wc * 128 + ch * 8;
+  };
+  auto staged = [&](int it) {
+    const int idx = it * 64 + lane, lr = idx >> 4, ch = idx & 15;
+    return *reinterpret_cast<const bf16x8_t*>(stg + lr * 256 + ((ch ^ (lr & 15)) << 4));
+  };
+  if constexpr (!X) {
+#pragma unroll 4
+    for (int it = 0; it < 32; ++it) *reinterpret_cast<bf16x8_t*>(C + coff(it)) = staged(it);
+  } else {
+    // 8 groups of 4 chunks; with `accumulate` the old C of group g + 1 is loaded before group g is processed, so
+    // each group waits for loads issued a group earlier (loaded inside the group, every wait was exposed)
+    bf16x8_t oldc[2][4];
+    if (accumulate) {
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const float x = bf2f((uint16_t)v[r]);
-          f[r] = act == 1 ? fmaxf(x, 0.f) : (act == 2 ? g256::gelu_tanh(x) : x);
-        }
-        if (accumulate) {  // one more bf16 rounding on top of the staged value (<= 1 ulp), as gemm.hip's lean path
-          const bf16x8_t old = *reinterpret_cast<const bf16x8_t*>(C + off);
+      for (int q = 0; q < 4; ++q) oldc[0][q] = *reinterpret_cast<const bf16x8_t*>(C + coff(q));
+    }
 #pragma unroll
-          for (int r = 0; r < 8; ++r) f[r] += bf2f((uint16_t)old[r]);
+    for (int grp = 0; grp < 8; ++grp) {
+      if (accumulate && grp + 1 < 8) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          oldc[(grp + 1) & 1][q] = *reinterpret_cast<const bf16x8_t*>(C + coff((grp + 1) * 4 + q));
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int it = grp * 4 + q;
+        const long off = coff(it);
+        bf16x8_t v = staged(it);
+        if (pre) *reinterpret_cast<bf16x8_t*>(pre + off) = v;  // the staged pre-activation (bias included)
+        if (act || accumulate) {
+          float f[8];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const float x = bf2f((uint16_t)v[r]);
+            f[r] = act == 1 ? fmaxf(x, 0.f) : (act == 2 ? g256::gelu_tanh(x) : x);
+          }
+          if (accumulate) {  // one more bf16 rounding on top of the staged value (<= 1 ulp), as gemm.hip's lean path
+#pragma unroll
+            for (int r = 0; r < 8; ++r) f[r] += bf2f((uint16_t)oldc[grp & 1][q][r]);
+          }
+          v = pack_bf16x8(f);
         }
-        v = pack_bf16x8(f);
+        *reinterpret_cast<bf16x8_t*>(C + off) = v;
       }
     }
-    *reinterpret_cast<bf16x8_t*>(C + off) = v;
   }
 }
 #undef K8S_G4_MFMA
@@ -938,6 +967,7 @@ static bool w4_ok(bool a_kmajor, bool b_kmajor, bool c_f32, int M, int N, int K,
   (void)b_kmajor;
   const bool extras = bias || act != 0 || pre || (accumulate && !c_f32);
   if (c_f32 && extras) return false;             // fp32 outputs: plain store / accumulate
+  if (reinterpret_cast<uintptr_t>(bias) % 16 != 0) return false;  // the epilogue reads the bias as 16-B vectors
   if (splits > 1 && (!c_f32 || accumulate)) return false;  // split slabs: plain fp32 stores
   if (M % 256 != 0 || N % 256 != 0 || K % 64 != 0 || (lda | ldb | ldc) % 8 != 0) return false;
   const long tiles = (long)(M / 256) * (N / 256);

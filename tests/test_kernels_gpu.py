@@ -233,15 +233,17 @@ def test_bn_packed_relu_mask(cuda, C, M, from_sums):
 
 # position rows summed in the tail loop only / in 8-token trips too; 150 tokens: a partial token run
 @pytest.mark.parametrize("B,S", [(4, 96), (40, 96), (3, 50)])
-def test_embedding_sum_gather_and_scatter(cuda, B, S):
+@pytest.mark.parametrize("D", [256, 776])
+def test_embedding_sum_gather_and_scatter(cuda, B, S, D):
     """BERT-style word + position + token-type lookup (embedding.hip) vs torch gathers; the backward's fp32
     scatter-adds (incl. the 2-row token-type table's register-reduced path and the position table's
-    owner-per-row path) vs index_add_."""
+    owner-per-row path) vs index_add_. D = 776: the large-table kernel's wave walks 256-column chunks, the last one
+    partial."""
     from k8s_amd.ops import nn as K
     from k8s_amd.parallel.flat import ParamStore, init_normal
 
     torch.manual_seed(3)
-    D, V = 256, 1000
+    V = 1000
     store = ParamStore()
     word = store.new("word", (V, D), init_normal(0.5))
     pos = store.new("pos", (128, D), init_normal(0.5))
