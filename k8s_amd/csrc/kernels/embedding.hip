@@ -139,32 +139,36 @@ __global__ void __launch_bounds__(256) embed_bwd_small_kernel(EmbArgs a, const u
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[r][j] = 0.f;
   const int t0 = run * EMB_RUN, t1 = min(a.T, t0 + EMB_RUN);
-  auto add = [&](int row, const float (&v)[8]) {
+  int t = t0;
+  // 8 tokens per trip with every id and 16-B gradient load issued first (one token at a time, each trip waited a
+  // full load latency: 490 us for BERT-base's 201 MB token-type gradient at batch 1024)
+  for (; t + 8 <= t1; t += 8) {
+    int rows[8];
+    bf16x8_t raw[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      rows[u] = emb_row(tb, t + u, a.S);
+      raw[u] = *reinterpret_cast<const bf16x8_t*>(g + (long)(t + u) * a.D + c);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float on = rows[u] == r ? 1.f : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[r][j] = __builtin_fmaf(on, bf2f((uint16_t)raw[u][j]), acc[r][j]);
+      }
+  }
+  for (; t < t1; ++t) {
+    const int row = emb_row(tb, t, a.S);
+    float v[8];
+    load8(g + (long)t * a.D + c, v);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       if (row == r) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[r][j] += v[j];
       }
-  };
-  int t = t0;
-  // 8 tokens per trip with every id and 16-B gradient load issued first (one token at a time, each trip waited a
-  // full load latency: 490 us for BERT-base's 201 MB token-type gradient at batch 1024)
-  for (; t + 8 <= t1; t += 8) {
-    int rows[8];
-    float v[8][8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      rows[u] = emb_row(tb, t + u, a.S);
-      load8(g + (long)(t + u) * a.D + c, v[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) add(rows[u], v[u]);
-  }
-  for (; t < t1; ++t) {
-    float v[8];
-    load8(g + (long)t * a.D + c, v);
-    add(emb_row(tb, t, a.S), v);
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
