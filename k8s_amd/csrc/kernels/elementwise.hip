@@ -276,6 +276,9 @@ void launch_act_bwd_colsum(int act, const uint16_t* dy, const uint16_t* pre, uin
     hipLaunchKernelGGL(act_bwd_colsum_partial_kernel<2>, grid, dim3(256), 0, st, dy, pre, g, R, C, rpb, work);
   hipLaunchKernelGGL(colsum_fold_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, work, (int)nb, C, out, (int)accumulate);
 }
+void launch_colsum_fold(const float* part, int P, int C, float* out, bool accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(colsum_fold_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, part, P, C, out, (int)accumulate);
+}
 void launch_colsum(const uint16_t* x, long R, int C, float* work, float* out, bool accumulate, hipStream_t st) {
   const long nb = colsum_row_blocks(R);
   const long rpb = (R + nb - 1) / nb;

@@ -124,58 +124,71 @@ __global__ void __launch_bounds__(256) embed_bwd_pos_kernel(EmbArgs a, const uin
   for (int j = 0; j < 8; ++j) dst[j] += acc[j];
 }
 
-// small tables (V <= 4): thread = (run of RUN tokens, 8 columns); per-row sums in registers, then V*8 atomics
-constexpr int EMB_RUN = 64;
-__global__ void __launch_bounds__(256) embed_bwd_small_kernel(EmbArgs a, const uint16_t* __restrict__ g, int tab,
-                                                              int nthreads) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= nthreads) return;
-  const int cv = a.D >> 3;
-  const int run = e / cv, c = (e - run * cv) * 8;
+// small tables (V <= 4, BERT's token types): block = 32 column groups (8 columns each) x 8 token lanes over a chunk
+// of EMB_CHUNK tokens; per-row sums in registers (8 tokens' ids and 16-B loads issued per trip), folded over the 8
+// token lanes in LDS, then one atomic per (row, column) per block. (A thread per 64-token run with its own atomics
+// put 2,048 adds on each of the 2 x 768 addresses at BERT's 131k tokens: 463 us, atomic-bound.)
+constexpr int EMB_CHUNK = 512;
+__global__ void __launch_bounds__(256) embed_bwd_small_kernel(EmbArgs a, const uint16_t* __restrict__ g, int tab) {
+  const int cgl = threadIdx.x & 31, tl = threadIdx.x >> 5;
+  const int cg = blockIdx.x * 32 + cgl, c = cg * 8;
+  const bool on = c < a.D;
   const EmbTab& tb = a.t[tab];
   float acc[4][8];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[r][j] = 0.f;
-  const int t0 = run * EMB_RUN, t1 = min(a.T, t0 + EMB_RUN);
-  int t = t0;
-  // 8 tokens per trip with every id and 16-B gradient load issued first (one token at a time, each trip waited a
-  // full load latency: 490 us for BERT-base's 201 MB token-type gradient at batch 1024)
-  for (; t + 8 <= t1; t += 8) {
-    int rows[8];
-    bf16x8_t raw[8];
+  const int t0 = blockIdx.y * EMB_CHUNK, t1 = min(a.T, t0 + EMB_CHUNK);
+  if (on) {
+    int t = t0 + tl;
+    for (; t + 56 < t1; t += 64) {  // 8 tokens of this lane per trip, all loads first
+      int rows[8];
+      bf16x8_t raw[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      rows[u] = emb_row(tb, t + u, a.S);
-      raw[u] = *reinterpret_cast<const bf16x8_t*>(g + (long)(t + u) * a.D + c);
+      for (int u = 0; u < 8; ++u) {
+        rows[u] = emb_row(tb, t + 8 * u, a.S);
+        raw[u] = *reinterpret_cast<const bf16x8_t*>(g + (long)(t + 8 * u) * a.D + c);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float w = rows[u] == r ? 1.f : 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[r][j] = __builtin_fmaf(w, bf2f((uint16_t)raw[u][j]), acc[r][j]);
+        }
     }
+    for (; t < t1; t += 8) {
+      const int row = emb_row(tb, t, a.S);
+      float v[8];
+      load8(g + (long)t * a.D + c, v);
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+      for (int r = 0; r < 4; ++r)
+        if (row == r) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float on = rows[u] == r ? 1.f : 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[r][j] = __builtin_fmaf(on, bf2f((uint16_t)raw[u][j]), acc[r][j]);
-      }
+          for (int j = 0; j < 8; ++j) acc[r][j] += v[j];
+        }
+    }
   }
-  for (; t < t1; ++t) {
-    const int row = emb_row(tb, t, a.S);
-    float v[8];
-    load8(g + (long)t * a.D + c, v);
+  __shared__ float sh[8][32][33];  // [token lane][column group][row * 8 + j] (+1 pad)
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (row == r) {
+  for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[r][j] += v[j];
-      }
-  }
+    for (int j = 0; j < 8; ++j) sh[tl][cgl][r * 8 + j] = acc[r][j];
+  __syncthreads();
+  // 256 threads: (column group, 4 of the 32 (row, j) slots each) sum the 8 token lanes and add once
+  const int k0 = tl * 4;
+  if (on) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    if (r >= tb.V) break;
-    float* dst = tb.g + (long)r * a.D + c;
+    for (int k = k0; k < k0 + 4; ++k) {
+      const int r = k >> 3, j = k & 7;
+      if (r >= tb.V) continue;
+      float v = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) atomicAdd(dst + j, acc[r][j]);
+      for (int q = 0; q < 8; ++q) v += sh[q][cgl][k];
+      atomicAdd(tb.g + (long)r * a.D + c + j, v);
+    }
   }
 }
 
@@ -204,8 +217,8 @@ void launch_embed_bwd(const EmbTable* tabs, int ntab, int T, int D, int S, const
   int big = 0;
   for (int i = 0; i < ntab; ++i) {
     if (tabs[i].V <= 4) {
-      const int nthreads = cdiv(T, EMB_RUN) * (D / 8);
-      hipLaunchKernelGGL(embed_bwd_small_kernel, dim3(cdiv(nthreads, 256)), dim3(256), 0, st, a, g, i, nthreads);
+      hipLaunchKernelGGL(embed_bwd_small_kernel, dim3(cdiv(D / 8, 32), cdiv(T, EMB_CHUNK)), dim3(256), 0, st, a, g,
+                         i);
     } else if (!tabs[i].ids && S > 0 && S <= tabs[i].V) {  // position table: rows 0 .. S-1, one owner each
       const int nthreads = S * (D / 8);
       hipLaunchKernelGGL(embed_bwd_pos_kernel, dim3(cdiv(nthreads, 256)), dim3(256), 0, st, a, g, i, nthreads);

@@ -592,22 +592,39 @@ __device__ __forceinline__ void gelu8(float (&f)[8]) {
 // the X copy-out (8 groups of 4 chunks of this wave's staged 128 x 128 tile): pre-activation copy, ACT (0 none, 1 ReLU,
 // 2 GELU) and ACC (C = result + old C, the old C of group g + 1 loaded before group g is processed, so each group
 // waits for loads issued a group earlier)
+// d/dx GELU(tanh) (elementwise.hip's act_bwd form: t = tanh(k0 (x + k1 x^3)) on v_exp / v_rcp)
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(2.8853900817779268f * k0 *
+                                                                                  (x + k1 * x * x * x)));
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+}
+
+// ACT < 0: the data gradient of a linear whose input is an activation's output, fused with that activation's
+// backward (-1 ReLU: `pre` holds the ReLU output; -2 GELU: the pre-activation): C = dgrad * act'(pre), and the
+// per-column sums of the stored bf16 C (the producing linear's bias gradient) -- this wave's 128 columns summed over
+// its 128 rows into one partial row of `cpart` (folded by colsum_fold_kernel). `pre` is read a group ahead, as the
+// accumulate's old C.
 template <int ACT, bool ACC, class Off, class Stg>
 __device__ __forceinline__ void copy_out_x(uint16_t* __restrict__ C, uint16_t* __restrict__ pre, const char* stg,
-                                           const Off& coff, const Stg& staged) {
+                                           const Off& coff, const Stg& staged, float* __restrict__ cpart = nullptr) {
   (void)stg;
+  static_assert(!(ACT < 0 && ACC), "activation backward without accumulate");
+  constexpr bool RD = ACC || ACT < 0;  // a bf16 operand per chunk read a group ahead (old C, or pre)
   bf16x8_t oldc[2][4];
-  if constexpr (ACC) {
+  const uint16_t* rsrc = ACT < 0 ? pre : C;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if constexpr (RD) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) oldc[0][q] = *reinterpret_cast<const bf16x8_t*>(C + coff(q));
+    for (int q = 0; q < 4; ++q) oldc[0][q] = *reinterpret_cast<const bf16x8_t*>(rsrc + coff(q));
   }
 #pragma unroll
   for (int grp = 0; grp < 8; ++grp) {
-    if constexpr (ACC) {
+    if constexpr (RD) {
       if (grp + 1 < 8) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          oldc[(grp + 1) & 1][q] = *reinterpret_cast<const bf16x8_t*>(C + coff((grp + 1) * 4 + q));
+          oldc[(grp + 1) & 1][q] = *reinterpret_cast<const bf16x8_t*>(rsrc + coff((grp + 1) * 4 + q));
       }
     }
 #pragma unroll
@@ -615,6 +632,19 @@ __device__ __forceinline__ void copy_out_x(uint16_t* __restrict__ C, uint16_t* _
       const int it = grp * 4 + q;
       const long off = coff(it);
       bf16x8_t v = staged(it);
+      if constexpr (ACT < 0) {
+        float f[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float x = bf2f((uint16_t)oldc[grp & 1][q][r]);
+          f[r] = bf2f((uint16_t)v[r]) * (ACT == -1 ? (x > 0.f ? 1.f : 0.f) : gelu_tanh_grad(x));
+        }
+        v = pack_bf16x8(f);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) cs[r] += bf2f((uint16_t)v[r]);
+        *reinterpret_cast<bf16x8_t*>(C + off) = v;
+        continue;
+      }
       if (pre) *reinterpret_cast<bf16x8_t*>(pre + off) = v;  // the staged pre-activation (bias included)
       if constexpr (ACT != 0 || ACC) {
         float f[8];
@@ -635,6 +665,19 @@ __device__ __forceinline__ void copy_out_x(uint16_t* __restrict__ C, uint16_t* _
       *reinterpret_cast<bf16x8_t*>(C + off) = v;
     }
   }
+  if constexpr (ACT < 0) {
+    // lanes l, l ^ 16, l ^ 32, l ^ 48 hold the same 8 columns (chunk l & 15) of different rows
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      cs[r] += __shfl_xor(cs[r], 16);
+      cs[r] += __shfl_xor(cs[r], 32);
+    }
+    if ((threadIdx.x & 63) < 16) {
+      float* d = cpart + (threadIdx.x & 15) * 8;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) d[r] = cs[r];
+    }
+  }
 }
 
 template <bool AMN, bool BMN, bool X>
@@ -643,7 +686,8 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
                                                              long ldc, int M, int N, int K, float alpha, int kps,
                                                              g256r::SkArgs SK, int out_f32, int accumulate,
                                                              const float* __restrict__ bias, int act,
-                                                             uint16_t* __restrict__ pre, long slab) {
+                                                             uint16_t* __restrict__ pre, long slab,
+                                                             float* __restrict__ cpart) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -975,7 +1019,13 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
     // the activation and the accumulate are compile-time in the loop body (copy_out<ACT, ACC>): with them as run-time
     // values the compiler branched per ELEMENT and serialised every GELU chain (exp -> add -> rcp -> mul, s_nop
     // between): BERT-base's FFN1 forward took 1013 us against 543 us for the bias-only QKV forward of 3/4 its FLOPs
-    if (act == 2) {
+    if (act < 0) {  // activation backward (data-gradient form only): a partial row of column sums per (tile, wave row)
+      if constexpr (!AMN && BMN) {
+        float* const cp = cpart + (long)((m0 >> 8) * 2 + wr) * N + n0 + wc * 128;
+        if (act == -2) copy_out_x<-2, false>(C, pre, stg, coff, staged, cp);
+        else copy_out_x<-1, false>(C, pre, stg, coff, staged, cp);
+      }
+    } else if (act == 2) {
       if (accumulate) copy_out_x<2, true>(C, pre, stg, coff, staged); else copy_out_x<2, false>(C, pre, stg, coff, staged);
     } else if (act == 1) {
       if (accumulate) copy_out_x<1, true>(C, pre, stg, coff, staged); else copy_out_x<1, false>(C, pre, stg, coff, staged);
@@ -1012,6 +1062,34 @@ static bool w4_ok(bool a_kmajor, bool b_kmajor, bool c_f32, int M, int N, int K,
 }
 // K range per split of a tall-K split on the 4-wave kernel (whole 64-deep stages; the last split takes the rest)
 static int w4_split_kps(int K, int splits) { return (K / 64 + splits - 1) / splits * 64; }
+
+// Data gradient fused with the backward of the activation that produced the GEMM's input (see copy_out_x, ACT < 0):
+// C[M][N] = (A . B) * act'(pre), db[N] = column sums of C (fp32, written or added), A K-major [M][K], B [K][N]
+// (the linear's weight). 4-wave kernel shapes only (w4_dact_ok); `part` holds (M / 128) x N floats.
+bool gemm_w4_dact_ok(int M, int N, int K, long lda, long ldb, long ldc) {
+  return w4_enabled() && M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && (lda | ldb | ldc) % 8 == 0 &&
+         (long)(M / 256) * (N / 256) >= planner_cus();
+}
+long gemm_w4_dact_part_floats(int M, int N) { return (long)(M / 128) * N; }
+void launch_gemm_w4_dact(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* C, long ldc, int M, int N,
+                         int K, const uint16_t* pre, int act, float* part, float* db, bool db_accumulate,
+                         float* sk_slabs, int* sk_sync, hipStream_t st) {
+  if (!gemm_w4_dact_ok(M, N, K, lda, ldb, ldc) || (act != 1 && act != 2) || ldc != N)
+    throw std::runtime_error("gemm_w4_dact: shape / activation outside the 4-wave kernel's contract");
+  Gemm256Plan plan = gemm256_plan(M, N, K);
+  if (!sk_slabs || !sk_sync) plan.sk = 1;
+  const int tiles = (M / 256) * (N / 256);
+  g256r::SkArgs sk{tiles, 1, nullptr, nullptr};
+  int blocks = tiles, kps = K;
+  if (plan.sk > 1) {
+    sk = g256r::SkArgs{plan.full, plan.sk, sk_slabs, sk_sync};
+    kps = plan.kps;
+    blocks = plan.full + (tiles - plan.full) * plan.sk;
+  }
+  hipLaunchKernelGGL((g4::gemm_w4_kernel<false, true, true>), dim3(blocks), dim3(g4::THREADS), 0, st, A, lda, B, ldb,
+                     (void*)C, ldc, M, N, K, 1.f, kps, sk, 0, 0, nullptr, -act, const_cast<uint16_t*>(pre), 0L, part);
+  launch_colsum_fold(part, M / 128, N, db, db_accumulate, st);
+}
 
 // Stream-K tail plan for a grid of 256 x 256 tiles on P = planner_cus() CUs (one block per CU; 256 on MI355X): with
 // T = w * P + r tiles and 0 < r <= P / 2, the last r tiles are split sk = min(P / r, 4) ways along K (each split a multiple of 64 deep and
@@ -1125,7 +1203,7 @@ void launch_gemm256(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* 
     const int acc = splits > 1 ? 0 : (accumulate ? 1 : 0);
 #define K8S_W4L(AM, BM, XX)                                                                                         \
   hipLaunchKernelGGL((g4::gemm_w4_kernel<AM, BM, XX>), dim3(blocks, ysplits), dim3(g4::THREADS), 0, st, A, lda, B, \
-                     ldb, cv, ldc, M, N, K, alpha, kps, sk, c_f32 ? 1 : 0, acc, bias, act, pre, (long)M * N)
+                     ldb, cv, ldc, M, N, K, alpha, kps, sk, c_f32 ? 1 : 0, acc, bias, act, pre, (long)M * N, nullptr)
 #define K8S_W4X(AM, BM)       \
   do {                        \
     if (x)                    \

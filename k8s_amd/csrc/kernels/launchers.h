@@ -100,6 +100,12 @@ void launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, float* st
 bool gemm256_eligible(int M, int N, int K, bool a_kmajor, bool b_kmajor);
 // split count for the tall-K fp32 products on the 256 x 256 kernel (1 = none)
 int gemm256_choose_splits(int M, int N, int K);
+// gemm256.hip: data gradient fused with the backward of the activation that produced the GEMM's input (4-wave kernel)
+bool gemm_w4_dact_ok(int M, int N, int K, long lda, long ldb, long ldc);
+long gemm_w4_dact_part_floats(int M, int N);
+void launch_gemm_w4_dact(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* C, long ldc, int M, int N,
+                         int K, const uint16_t* pre, int act, float* part, float* db, bool db_accumulate,
+                         float* sk_slabs, int* sk_sync, hipStream_t st);
 // stream-K tail plan (gemm256.hip): tiles [full, tiles) are split sk ways along K (sk == 1: none), kps deep each
 struct Gemm256Plan {
   int tiles, full, sk, kps;
@@ -147,6 +153,8 @@ void launch_gelu_bwd(const uint16_t* dy, const uint16_t* pre, uint16_t* dx, long
 void launch_relu_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n, hipStream_t st);
 int colsum_workspace_floats(long R, int C);
 void launch_colsum(const uint16_t* x, long R, int C, float* work, float* out, bool accumulate, hipStream_t st);
+// the fold of P partial rows of column sums (colsum_fold_kernel)
+void launch_colsum_fold(const float* part, int P, int C, float* out, bool accumulate, hipStream_t st);
 // g = dy * act'(pre) (1 ReLU, pre = its output; 2 GELU(tanh), pre = the pre-activation) and out = column sums of g
 void launch_act_bwd_colsum(int act, const uint16_t* dy, const uint16_t* pre, uint16_t* g, long R, int C, float* work,
                            float* out, bool accumulate, hipStream_t st);

@@ -555,6 +555,38 @@ Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tens
   return c;
 }
 
+// dx = (g . W) * act'(pre) and db (+)= column sums of dx: the data gradient of a linear whose input is the output of
+// an activation (1 ReLU: pre = the ReLU output, 2 GELU: the pre-activation), fused with that activation's backward and
+// the producing linear's bias gradient in the 4-wave GEMM's epilogue (gemm256.hip copy_out_x, ACT < 0).
+// g [M, N_out] bf16, w [N_out, K_in] bf16 (read MN-major), pre [M, K_in] bf16, db fp32 [K_in].
+bool gemm_dact_ok(int64_t M, int64_t N, int64_t K) { return k8s_amd::gemm_w4_dact_ok((int)M, (int)N, (int)K, K, N, N); }
+Tensor gemm_dact(Tensor g, Tensor w, Tensor pre, int64_t act, Tensor db, bool db_accumulate) {
+  check_bf16_operand(g, "g");
+  check_bf16_operand(w, "w");
+  check_bf16_operand(pre, "pre");
+  const long M = g.size(0), K = g.size(1), N = w.size(1);
+  TORCH_CHECK(w.size(0) == K, "g [M, K] . w [K, N]");
+  TORCH_CHECK(pre.is_contiguous() && pre.size(0) == M && pre.size(1) == N, "pre must be a contiguous [M, N]");
+  TORCH_CHECK(db.is_cuda() && db.scalar_type() == at::kFloat && db.is_contiguous() && db.numel() == N,
+              "db: contiguous fp32 [N]");
+  TORCH_CHECK(act == 1 || act == 2, "act: 1 ReLU, 2 GELU(tanh)");
+  TORCH_CHECK(k8s_amd::gemm_w4_dact_ok((int)M, (int)N, (int)K, g.stride(0), w.stride(0), N),
+              "gemm_dact: shape outside the 4-wave kernel's contract");
+  Tensor c = torch::empty({M, N}, g.options());
+  Tensor part = torch::empty({k8s_amd::gemm_w4_dact_part_floats((int)M, (int)N)}, db.options());
+  const k8s_amd::Gemm256Plan plan = k8s_amd::gemm256_plan((int)M, (int)N, (int)K);
+  Tensor slabs;
+  int* sync = nullptr;
+  if (plan.sk > 1) {
+    slabs = torch::empty({k8s_amd::gemm256_sk_slab_floats(plan)}, db.options());
+    sync = sk_sync_words(k8s_amd::gemm256_sk_sync_ints(plan), g.device());
+  }
+  k8s_amd::launch_gemm_w4_dact(cbf(g), g.stride(0), cbf(w), w.stride(0), bf(c), N, (int)M, (int)N, (int)K, cbf(pre),
+                               (int)act, f32(part), f32(db), db_accumulate, sync ? f32(slabs) : nullptr, sync,
+                               cur_stream());
+  return c;
+}
+
 static inline int conv_out(int in, int k, int st, int pad, int dil) { return (in + 2 * pad - dil * (k - 1) - 1) / st + 1; }
 
 Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, bool out_f32, c10::optional<Tensor> bias,
@@ -1060,6 +1092,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out") = py::none());
   m.def("relu_bwd", &relu_bwd);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none());
+  m.def("gemm_dact", &gemm_dact, "linear data gradient fused with the input activation's backward and bias gradient",
+        py::arg("g"), py::arg("w"), py::arg("pre"), py::arg("act"), py::arg("db"), py::arg("db_accumulate"));
+  m.def("gemm_dact_ok", &gemm_dact_ok, py::arg("M"), py::arg("N"), py::arg("K"));
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
         py::arg("out_f32"), py::arg("bias"), py::arg("act"), py::arg("stats"),
         py::arg("xform") = py::none());

@@ -84,8 +84,10 @@ class BertLayer(nn.Module):
         o = attention_qkv(qkv, B, S, nh, nh, d, causal=False, kv_lens=kv_lens)  # packed QKV gradient in place
         a = K.linear(o.reshape(B * S, h), self.o_w, self.o_b, bias_link=b1)
         x, _ = K.layer_norm(a, self.ln1_g, self.ln1_b, c.eps, residual=x, res_link=l1, bias_link=b1)
-        f = K.linear(x, self.f1_w, self.f1_b, act="gelu", grad_link=l2)
-        f = K.linear(f, self.f2_w, self.f2_b, bias_link=b2)
+        # FFN1's GELU backward and bias gradient inside FFN2's data-gradient epilogue (ActLink)
+        al = K.ActLink()
+        f = K.linear(x, self.f1_w, self.f1_b, act="gelu", grad_link=l2, act_link=al)
+        f = K.linear(f, self.f2_w, self.f2_b, bias_link=b2, act_in=al)
         x, _ = K.layer_norm(f, self.ln2_g, self.ln2_b, c.eps, residual=x, res_link=l2, bias_link=b2)
         return x
 

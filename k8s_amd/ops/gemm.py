@@ -108,12 +108,38 @@ def linear_fwd(x, w, b, act=None):
     return y, (pre if act == "gelu" else (y if act == "relu" else None))
 
 
-def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True, dx_addend=None, pb=None):
+def dact_ok(x, w, dx_addend=None) -> bool:
+    """Whether a linear's data gradient can take its input activation's backward in the GEMM epilogue (``linear_bwd``
+    ``dx_act``): the 4-wave kernel's whole-tile shapes, GPU bf16, no second gradient contribution to add."""
+    M, K = x.shape
+    N = w.shape[0]
+    return (dx_addend is None and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and bool(_load().gemm_dact_ok(M, K, N)))
+
+
+def _dgrad_act(g, w, dx_act):
+    """dx = (g . w) * act'(pre) with the producing linear's bias gradient (column sums of dx) deposited into its flat
+    slot -- ``dx_act`` = (pre, act, pb, store) -- in one 4-wave GEMM launch (+ the column-sum fold)."""
+    pre, act, pb, store = dx_act
+    C = _load()
+    slot = store.slot_for_write(pb)
+    if slot is not None:
+        dx = C.gemm_dact(g, w, pre.contiguous(), ACT[act], slot.view(-1), False)
+        store.mark_written(pb)
+    else:  # already written this step (tied bias): add the column sums onto it
+        dx = C.gemm_dact(g, w, pre.contiguous(), ACT[act], pb.grad.view(-1), True)
+        store._notify(pb)
+    return dx
+
+
+def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True, dx_addend=None, pb=None, dx_act=None):
     """dx and the parameter gradient. With (pw, store) on GPU the weight gradient is written
     (or accumulated) straight into the flat fp32 gradient slot; returns (dx, dw_or_None, db).
     ``dx_addend`` (bf16, x's shape): another gradient contribution of x, accumulated in the dgrad epilogue (it is
     overwritten and returned as dx). With ``pb`` the bias gradient goes straight into its flat slot on first use
-    (db is then returned as None)."""
+    (db is then returned as None). ``dx_act`` = (pre, act, producer bias param, its store): x is the output of that
+    activation and dx is returned already through its backward, the producer's bias gradient deposited
+    (``dact_ok`` must hold)."""
     M, K = x.shape
     N = w.shape[0]
     db = None
@@ -155,7 +181,10 @@ def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True, dx_adden
             return dx, dw, db
         acc = dx_addend is not None and dx_addend.is_contiguous() and dx_addend.dtype == torch.bfloat16
         # dgrad reduces over N; a ragged N (e.g. the 1000-class head) is masked by the kernel's K tail (zeros)
-        dx = mm(g, w, True, False, out=dx_addend if acc else None, accumulate=acc)
+        if dx_act is not None:
+            dx = _dgrad_act(g, w, dx_act)
+        else:
+            dx = mm(g, w, True, False, out=dx_addend if acc else None, accumulate=acc)
         if dx_addend is not None and not acc:
             dx = dx + dx_addend
         if pw is not None and store is not None and pw.grad.dtype == torch.float32:

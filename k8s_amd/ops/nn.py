@@ -69,6 +69,18 @@ class BiasLink:
         self.pb, self.done = None, False
 
 
+class ActLink:
+    """Joins a linear with an activation (the producer, ``linear(x, W1, b1, act="gelu", act_link=l)``) to the linear
+    that reads its output (the consumer, ``linear(y, W2, b2, act_in=l)``): the consumer's data gradient is formed as
+    (dy . W2) * act'(pre), with the producer's bias gradient as its column sums, in the 4-wave GEMM's epilogue
+    (gemm256.hip copy_out_x ACT < 0; ``gemm.dact_ok`` shapes) -- the producer's backward then skips its
+    activation-backward pass (read dy and pre, write g) and its bias column sums. BERT's FFN1 -> FFN2."""
+    __slots__ = ("saved", "act", "pb", "done")
+
+    def __init__(self):
+        self.saved, self.act, self.pb, self.done = None, None, None, False
+
+
 class MaskedGrad:
     """A residual gradient handed over unmaterialised: ``dy`` masked by the packed 1-bit ReLU ``mask`` of the BN
     forward (bit j of byte e = element 8e + j). The 1x1 dgrad that receives it reads the pair in its epilogue
@@ -470,7 +482,7 @@ def _gemm():
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, anchor, pw, pb, act, grad_link=None, bias_link=None):
+    def forward(ctx, x, anchor, pw, pb, act, grad_link=None, bias_link=None, act_link=None, act_in=None):
         g = _gemm()
         w = pw.weight if x.dtype == pw.weight.dtype else pw.master.to(x.dtype)
         x2 = x.reshape(-1, x.shape[-1])
@@ -481,6 +493,13 @@ class _Linear(torch.autograd.Function):
         ctx.bias_link = bias_link
         if bias_link is not None and act is None:
             bias_link.pb = pb
+        # producer end of an ActLink: what the consumer's fused data gradient needs (saved: the GELU pre-activation /
+        # the ReLU output, as this node's own backward would read)
+        ctx.act_link = act_link if (act_link is not None and act is not None and pb is not None and
+                                    pre is not None and pre.dtype == torch.bfloat16) else None
+        if ctx.act_link is not None:
+            act_link.saved, act_link.act, act_link.pb, act_link.done = pre, act, pb, False
+        ctx.act_in = act_in
         return y.reshape(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -496,22 +515,39 @@ class _Linear(torch.autograd.Function):
             addend = link.grad.reshape(x2.shape)
             link.grad = None
         db_done = ctx.bias_link is not None and ctx.bias_link.done  # the reading norm produced it
-        dx, dw, db = g.linear_bwd(gy2, x2, w, pre, ctx.act, pw=pw, store=pw.store,
-                                  need_db=pb is not None and not db_done, dx_addend=addend, pb=pb)
+        act = ctx.act
+        if ctx.act_link is not None and ctx.act_link.done:  # the consumer's data gradient applied act' and took db
+            ctx.act_link.done, ctx.act_link.saved = False, None
+            act, db_done = None, True
+        dx_act = None
+        li = ctx.act_in
+        if li is not None and li.saved is not None and g.dact_ok(x2, w, addend):
+            dx_act = (li.saved, li.act, li.pb, li.pb.store)
+        dx, dw, db = g.linear_bwd(gy2, x2, w, pre, act, pw=pw, store=pw.store,
+                                  need_db=pb is not None and not db_done, dx_addend=addend, pb=pb, dx_act=dx_act)
+        if dx_act is not None:
+            li.done, li.saved = True, None
         if dw is not None:
             pw.store.deposit(pw, dw)
         if pb is not None and db is not None:  # None: written straight into its slot
             pb.store.deposit(pb, db)
         if link is not None and addend is None:  # ran first: hand dx to the norm backward, which forms the sum
             link.grad = dx.reshape(ctx.xshape)
-            return None, None, None, None, None, None, None
-        return dx.reshape(ctx.xshape), None, None, None, None, None, None
+            return (None,) * 9
+        return (dx.reshape(ctx.xshape),) + (None,) * 8
 
 
-def linear(x, pw, pb=None, act: Optional[str] = None, grad_link=None, bias_link=None):
+# BERT's FFN1 -> FFN2 activation backward fused into FFN2's data gradient (ActLink); tests switch it off to compare
+ACT_FUSE = True
+
+
+def linear(x, pw, pb=None, act: Optional[str] = None, grad_link=None, bias_link=None, act_link=None, act_in=None):
     """y = act(x @ W^T + b); W [out, in] bf16 from the flat store. ``grad_link``: see ``layer_norm``;
-    ``bias_link``: see ``BiasLink``."""
-    return _Linear.apply(x, pw.store.anchor, pw, pb, act, grad_link, bias_link)
+    ``bias_link``: see ``BiasLink``; ``act_link`` (on the producer, with ``act``) / ``act_in`` (on the consumer):
+    see ``ActLink``."""
+    if not ACT_FUSE:
+        act_link = act_in = None
+    return _Linear.apply(x, pw.store.anchor, pw, pb, act, grad_link, bias_link, act_link, act_in)
 
 
 # =========================================================================== embedding

@@ -292,3 +292,69 @@ def test_gemm_w4_tall_k_split(cuda, monkeypatch, M, N, K):
     monkeypatch.setenv("K8S_AMD_GEMM_W4", "0")
     c0 = _C().gemm(g, False, x, False, None, True, None, 0, None, False, 1.0, 0)
     assert _rel(c, c0) < 1e-5
+
+
+def _gelu_grad(x):
+    k0, k1 = 0.7978845608028654, 0.044715
+    t = torch.tanh(k0 * (x + k1 * x ** 3))
+    return 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k0 * (1 + 3 * k1 * x * x)
+
+
+@pytest.mark.parametrize("act", [1, 2])
+def test_gemm_dact_matches_fp32(cuda, act):
+    """Data gradient fused with the input activation's backward and the producer's bias gradient (gemm256.hip
+    copy_out_x ACT < 0, `gemm_dact`): dx = (g . W) * act'(pre), db = column sums of dx, against fp32 PyTorch; db
+    written, then accumulated onto an existing value."""
+    torch.manual_seed(10)
+    M, Nout, Kin = 16384, 768, 3072  # BERT-base FFN2's data gradient: 64 x 12 = 768 tiles
+    g = torch.randn(M, Nout, device=cuda).bfloat16()
+    w = (torch.randn(Nout, Kin, device=cuda) * 0.05).bfloat16()
+    pre = torch.randn(M, Kin, device=cuda).bfloat16()
+    if act == 1:
+        pre = torch.relu(pre)  # the ReLU path reads the ReLU output
+    assert _C().gemm_dact_ok(M, Kin, Nout)
+    db = torch.empty(Kin, device=cuda)
+    dx = _C().gemm_dact(g, w, pre, act, db, False)
+    d = g.float() @ w.float()
+    deriv = (pre.float() > 0).float() if act == 1 else _gelu_grad(pre.float())
+    ref = d * deriv
+    assert _rel(dx, ref) < 1e-2
+    assert _rel(db, dx.float().sum(0)) < 1e-4  # the sums of the stored bf16 values
+    assert _rel(db, ref.sum(0)) < 1e-2
+    db2 = torch.full((Kin,), 0.5, device=cuda)
+    dx2 = _C().gemm_dact(g, w, pre, act, db2, True)
+    assert torch.equal(dx2, dx)
+    assert _rel(db2 - 0.5, db) < 1e-5
+
+
+def test_linear_act_link_matches_unfused(cuda):
+    """BERT's FFN (linear + GELU -> linear) with FFN1's GELU backward and bias gradient fused into FFN2's data
+    gradient (nn.ActLink) against the unfused path (nn.ACT_FUSE = False): x, W1, b1, W2, b2 gradients."""
+    from k8s_amd.ops import nn as K
+    from k8s_amd.parallel.flat import ParamStore, init_normal
+
+    torch.manual_seed(11)
+    T, H, F4 = 16384, 768, 3072
+    grads = {}
+    for fuse in (True, False):
+        K.ACT_FUSE = fuse
+        try:
+            store = ParamStore()
+            w1 = store.new("w1", (F4, H), init_normal(0.02))
+            b1 = store.new("b1", (F4,), init_normal(0.02), decay=False, lowp=False)
+            w2 = store.new("w2", (H, F4), init_normal(0.02))
+            b2 = store.new("b2", (H,), init_normal(0.02), decay=False, lowp=False)
+            store.finalize(cuda, seed=5)
+            g = torch.Generator(device=cuda).manual_seed(12)
+            x = torch.randn(T, H, device=cuda, generator=g).bfloat16().requires_grad_(True)
+            gy = torch.randn(T, H, device=cuda, generator=g).bfloat16()
+            store.begin_step()
+            al = K.ActLink()
+            f = K.linear(x, w1, b1, act="gelu", act_link=al)
+            y = K.linear(f, w2, b2, act_in=al)
+            y.backward(gy)
+            grads[fuse] = (x.grad.float(), w1.grad.clone(), b1.grad.clone(), w2.grad.clone(), b2.grad.clone())
+        finally:
+            K.ACT_FUSE = True
+    for a, b, name in zip(grads[True], grads[False], ("x", "w1", "b1", "w2", "b2")):
+        assert _rel(a, b) < 1e-3, name
