@@ -600,6 +600,28 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
 }
 
+// f *= GELU'(x) for 8 values, 2 at a time on the packed fp32 ALU (the gelu_tanh_grad formula)
+__device__ __forceinline__ void gelu_grad_mul8(float (&f)[8], const float (&xs)[8]) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const f32x2_t one = {1.f, 1.f}, half = {0.5f, 0.5f};
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const f32x2_t x = {xs[2 * p], xs[2 * p + 1]};
+    const f32x2_t x2 = x * x;
+    const f32x2_t u = x * __builtin_elementwise_fma(x2, f32x2_t{k1, k1}, one) *
+                      f32x2_t{2.8853900817779268f * k0, 2.8853900817779268f * k0};  // 2 log2(e) k0 (x + k1 x^3)
+    const f32x2_t d = {1.f + __builtin_amdgcn_exp2f(u[0]), 1.f + __builtin_amdgcn_exp2f(u[1])};
+    const f32x2_t r = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+    const f32x2_t t = __builtin_elementwise_fma(r, f32x2_t{-2.f, -2.f}, one);  // tanh
+    const f32x2_t a = __builtin_elementwise_fma(t, half, half);
+    const f32x2_t b = x * __builtin_elementwise_fma(-t, t, one) * __builtin_elementwise_fma(x2, f32x2_t{3.f * k1, 3.f * k1}, one) *
+                      f32x2_t{0.5f * k0, 0.5f * k0};
+    const f32x2_t y = f32x2_t{f[2 * p], f[2 * p + 1]} * (a + b);
+    f[2 * p] = y[0];
+    f[2 * p + 1] = y[1];
+  }
+}
+
 // ACT < 0: the data gradient of a linear whose input is an activation's output, fused with that activation's
 // backward (-1 ReLU: `pre` holds the ReLU output; -2 GELU: the pre-activation): C = dgrad * act'(pre), and the
 // per-column sums of the stored bf16 C (the producing linear's bias gradient) -- this wave's 128 columns summed over
@@ -633,11 +655,17 @@ __device__ __forceinline__ void copy_out_x(uint16_t* __restrict__ C, uint16_t* _
       const long off = coff(it);
       bf16x8_t v = staged(it);
       if constexpr (ACT < 0) {
-        float f[8];
+        float f[8], x[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-          const float x = bf2f((uint16_t)oldc[grp & 1][q][r]);
-          f[r] = bf2f((uint16_t)v[r]) * (ACT == -1 ? (x > 0.f ? 1.f : 0.f) : gelu_tanh_grad(x));
+          x[r] = bf2f((uint16_t)oldc[grp & 1][q][r]);
+          f[r] = bf2f((uint16_t)v[r]);
+        }
+        if constexpr (ACT == -1) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) f[r] = x[r] > 0.f ? f[r] : 0.f;
+        } else {
+          gelu_grad_mul8(f, x);
         }
         v = pack_bf16x8(f);
 #pragma unroll
