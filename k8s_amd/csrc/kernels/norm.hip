@@ -12,6 +12,8 @@
 // are reproducible.
 #include <stdexcept>
 
+#include <type_traits>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -175,7 +177,14 @@ __global__ void __launch_bounds__(256) norm_bwd_dx_kernel(const uint16_t* __rest
   }
 }
 
-constexpr int NORM_PARAM_ROWS = 64;  // rows per column-partial block
+constexpr int NORM_PARAM_ROWS = 64;  // rows per column-partial block (at least; norm_param_rows)
+// rows per column-partial block: 64, or enough that at most 512 partial rows remain for the fold, whose D / 32 blocks
+// walk them serially (BERT-base at 131k tokens: 2,048 partials took the fold 49 us per call, 1.3 ms per step)
+static int norm_param_rows(long R) {
+  long rows = (R + 511) / 512;
+  rows = (rows + 31) / 32 * 32;
+  return (int)(rows < NORM_PARAM_ROWS ? NORM_PARAM_ROWS : rows);
+}
 
 // part[blockIdx.x][0][k] = sum dy * xhat, part[blockIdx.x][1][k] = sum dy over the block's rows; block = 32 column
 // chunks (256 columns) x 8 row groups, LDS combine of the row groups
@@ -188,7 +197,7 @@ __global__ void __launch_bounds__(256) norm_bwd_param_kernel(const uint16_t* __r
                                                              const float* __restrict__ rstd,
                                                              const float* __restrict__ rowab,
                                                              const float* __restrict__ gamma,
-                                                             float* __restrict__ part, long R, int D) {
+                                                             float* __restrict__ part, long R, int D, int prows) {
   const int nch = D / 8;
   const int ch = blockIdx.y * 32 + (threadIdx.x & 31), rg = threadIdx.x >> 5;
   float pg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pb[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pd[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -198,8 +207,8 @@ __global__ void __launch_bounds__(256) norm_bwd_param_kernel(const uint16_t* __r
     for (int j = 0; j < 8; ++j) gm[j] = gamma[ch * 8 + j];
   }
   if (ch < nch) {
-    const long r0 = (long)blockIdx.x * NORM_PARAM_ROWS;
-    const long r1 = r0 + NORM_PARAM_ROWS < R ? r0 + NORM_PARAM_ROWS : R;
+    const long r0 = (long)blockIdx.x * prows;
+    const long r1 = r0 + prows < R ? r0 + prows : R;
     for (long r = r0 + rg; r < r1; r += 32) {  // 4 rows per trip, loads first (clamped, zero-weighted tail)
       float g[4][8], xv[4][8], mu[4], rs[4];
 #pragma unroll
@@ -309,6 +318,120 @@ __global__ void __launch_bounds__(256) norm_colsum_kernel(const float* __restric
   }
 }
 
+// Many short rows (BERT-base: 131k rows of 768): the dx kernel and the column partials in ONE pass. Each wave walks
+// RPW consecutive rows with the next row's dy / x (/ dres) loads issued before this row's math, keeps the per-column
+// sums of dy * xhat, dy and dx (the upstream linear's bias gradient) in registers, and the block's 4 waves combine them
+// in LDS into one partial row [3][D]. The separate column kernel re-read dy and x (91 us per BERT call) and its
+// 64-row partials made a 2,048-row fold. CPL <= 2 (D <= 1024).
+constexpr int NORM_FUSED_RPW = 32;
+template <int CPL, bool RMS>
+__global__ void __launch_bounds__(256) norm_bwd_fused_kernel(const uint16_t* __restrict__ dy,
+                                                             const uint16_t* __restrict__ x,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ rstd,
+                                                             const uint16_t* __restrict__ dres,
+                                                             uint16_t* __restrict__ dx, float* __restrict__ part,
+                                                             long R, int D, int want_dsum) {
+  static_assert(CPL <= 2, "short rows only");
+  constexpr int RPW = NORM_FUSED_RPW;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long row0 = ((long)blockIdx.x * NORM_WAVES + wave) * RPW;
+  const int nch = D / 8;
+  float gm[CPL][8], pg[CPL][8], pb[CPL][8], pd[CPL][8];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + c * 64;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      gm[c][j] = ch < nch ? gamma[ch * 8 + j] : 0.f;
+      pg[c][j] = pb[c][j] = pd[c][j] = 0.f;
+    }
+  }
+  bf16x8_t gr[2][CPL], xr[2][CPL], rr[2][CPL];
+  auto load = [&](auto slot_c, long row) {
+    constexpr int sl = decltype(slot_c)::value;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int ch = lane + c * 64;
+      const int cc = ch < nch ? ch : nch - 1;
+      gr[sl][c] = *reinterpret_cast<const bf16x8_t*>(dy + row * D + cc * 8);
+      xr[sl][c] = *reinterpret_cast<const bf16x8_t*>(x + row * D + cc * 8);
+      if (dres) rr[sl][c] = *reinterpret_cast<const bf16x8_t*>(dres + row * D + cc * 8);
+    }
+  };
+  auto step = [&](auto slot_c, long row) {
+    constexpr int sl = decltype(slot_c)::value;
+    const float mu = RMS ? 0.f : mean[row];
+    const float rs = rstd[row];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      if (lane + c * 64 < nch) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float gg = bf2f((uint16_t)gr[sl][c][j]) * gm[c][j];
+          a += gg;
+          b += gg * ((bf2f((uint16_t)xr[sl][c][j]) - mu) * rs);
+        }
+      }
+    }
+    a = wave_sum(a) / D;
+    b = wave_sum(b) / D;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nch) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float g = bf2f((uint16_t)gr[sl][c][j]);
+          const float xn = (bf2f((uint16_t)xr[sl][c][j]) - mu) * rs;
+          o[j] = rs * (g * gm[c][j] - (RMS ? 0.f : a) - xn * b);
+          pg[c][j] += g * xn;
+          pb[c][j] += g;
+          pd[c][j] += o[j];
+        }
+        if (dres) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += bf2f((uint16_t)rr[sl][c][j]);
+        }
+        store8(dx + row * D + ch * 8, o);
+      }
+    }
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  if (row0 < R) load(S0{}, row0);
+  for (int i = 0; i < RPW; i += 2) {  // two rows per trip: the register slots stay compile-time
+    const long r = row0 + i;
+    if (r >= R) break;
+    if (r + 1 < R) load(S1{}, r + 1);
+    step(S0{}, r);
+    if (r + 1 >= R) break;
+    if (i + 2 < RPW && r + 2 < R) load(S0{}, r + 2);
+    step(S1{}, r + 1);
+  }
+  // the block's 4 waves -> one partial row [3][D] (sum dy * xhat | sum dy | sum dx)
+  __shared__ float sh[NORM_WAVES][3][CPL * 512];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = (lane + c * 64) * 8 + j;
+      sh[wave][0][k] = pg[c][j];
+      sh[wave][1][k] = pb[c][j];
+      sh[wave][2][k] = pd[c][j];
+    }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 3 * D; k += 256) {
+    const int which = k / D, col = k - which * D;
+    if (which == 2 && !want_dsum) continue;
+    part[(long)blockIdx.x * 3 * D + k] =
+        (sh[0][which][col] + sh[1][which][col]) + (sh[2][which][col] + sh[3][which][col]);
+  }
+}
+
 template <bool RMS>
 static void norm_fwd_dispatch(int cpl, dim3 g, hipStream_t st, const uint16_t* x, const uint16_t* res,
                               uint16_t* xsum, const float* gamma, const float* beta, uint16_t* y, float* mean,
@@ -340,16 +463,39 @@ void launch_norm_fwd(bool rms, const uint16_t* x, const uint16_t* res, uint16_t*
     norm_fwd_dispatch<false>(cpl, g, st, x, res, xsum, gamma, beta, y, mean, rstd, R, D, eps);
 }
 
-static int norm_param_blocks(long R) { return (int)((R + NORM_PARAM_ROWS - 1) / NORM_PARAM_ROWS); }
+static int norm_param_blocks(long R) { return (int)((R + norm_param_rows(R) - 1) / norm_param_rows(R)); }
+
+// the fused one-pass backward for many short rows (norm_bwd_fused_kernel)
+static bool norm_fused_ok(long R, int D) { return norm_cpl(D) <= 2 && R >= 16384; }
+static int norm_fused_blocks(long R) { return (int)((R + NORM_WAVES * NORM_FUSED_RPW - 1) / (NORM_WAVES * NORM_FUSED_RPW)); }
 
 // [nblocks][3][D] partials + [R][2] row coefficients
-int norm_workspace_floats(long R, int D) { return (int)(norm_param_blocks(R) * 3L * D + 2 * R); }
+int norm_workspace_floats(long R, int D) {
+  const long two = norm_param_blocks(R) * 3L * D + 2 * R;
+  const long one = norm_fused_ok(R, D) ? norm_fused_blocks(R) * 3L * D : 0;
+  return (int)(two > one ? two : one);
+}
 
 void launch_norm_bwd(bool rms, const uint16_t* dy, const uint16_t* x, const float* gamma, const float* mean,
                      const float* rstd, const uint16_t* dres, uint16_t* dx, float* dgamma, float* dbeta, float* work,
                      long R, int D, hipStream_t st, float* dsum) {
   if (dsum && dres) throw std::runtime_error("norm_bwd: the dx column sums exclude a residual gradient");
   const int cpl = norm_cpl(D);
+  if (norm_fused_ok(R, D)) {
+    const int nbf = norm_fused_blocks(R);
+#define NBF(C, RM)                                                                                                    \
+  hipLaunchKernelGGL((norm_bwd_fused_kernel<C, RM>), dim3(nbf), dim3(256), 0, st, dy, x, gamma, mean, rstd, dres, dx, \
+                     work, R, D, dsum ? 1 : 0)
+    if (cpl == 1) {
+      if (rms) NBF(1, true); else NBF(1, false);
+    } else {
+      if (rms) NBF(2, true); else NBF(2, false);
+    }
+#undef NBF
+    hipLaunchKernelGGL(norm_colsum_kernel, dim3(cdiv(D, 32)), dim3(256), 0, st, work, nbf, D, dgamma,
+                       rms ? nullptr : dbeta, dsum);
+    return;
+  }
   const dim3 g(cdiv(R, NORM_WAVES));
   const int nb = norm_param_blocks(R);
   float* const rowab = dsum ? work + (long)nb * 3 * D : nullptr;
@@ -371,10 +517,10 @@ void launch_norm_bwd(bool rms, const uint16_t* dy, const uint16_t* x, const floa
   const dim3 gp(nb, cdiv(D / 8, 32));
   if (rms)
     hipLaunchKernelGGL(norm_bwd_param_kernel<true>, gp, dim3(256), 0, st, dy, x, mean, rstd, rowab, gamma, work, R,
-                       D);
+                       D, norm_param_rows(R));
   else
     hipLaunchKernelGGL(norm_bwd_param_kernel<false>, gp, dim3(256), 0, st, dy, x, mean, rstd, rowab, gamma, work, R,
-                       D);
+                       D, norm_param_rows(R));
   hipLaunchKernelGGL(norm_colsum_kernel, dim3(cdiv(D, 32)), dim3(256), 0, st, work, nb, D, dgamma,
                      rms ? nullptr : dbeta, dsum);
 }

@@ -82,7 +82,9 @@ def test_bn_from_conv_sums_and_relu_from_x(cuda, C, M):
 @pytest.mark.parametrize("D", [768, 4096, 1024, 136])
 @pytest.mark.parametrize("rms", [False, True])
 @pytest.mark.parametrize("res", [False, True])
-@pytest.mark.parametrize("R", [257, 2100])  # one partial block / many, ragged tails
+# one partial block / many, ragged tails; 16411 rows: the fused one-pass backward of short rows (D <= 1024), its last
+# block partial and an odd row count (the two-row trips' early exit)
+@pytest.mark.parametrize("R", [257, 2100, 16411])
 def test_norm_fwd_bwd(cuda, D, rms, res, R):
     torch.manual_seed(1)
     x = torch.randn(R, D, device=cuda).bfloat16()
