@@ -764,6 +764,201 @@ __global__ void __launch_bounds__(FA_THREADS, (QS == 2 && D * TILE >= 8192) ? 1 
   }
 }
 
+// ---- short sequences (Sq, Sk <= 128, D = 64, one KV head per query head): the whole backward of one (batch, head)
+// in one block. Prologue: Q, dO, K staged by global_load_lds, lse loaded and delta = rowsum(dO * O) computed into LDS.
+// Per 64-key chunk: the dK/dV kernel's body (wave w: keys 16w .. +15 of the chunk, K fragments from the LDS tile,
+// V fragments from global; S, dP, P, dS for all queries in 64-query halves; dV^T += dO^T P, dK^T += Q^T dS), dS of the
+// chunk parked in LDS as bf16 [query][key], then dQ^T += K^T dS^T over the chunk (wave w: queries 32w .. +31, K^T read
+// transposed from the K tile, dS^T rows read straight: lane = query, two 8-B reads per 32 keys in the permuted k order).
+// BERT s128: the delta / dK-dV / dQ kernels each re-read Q, dO, K, V (664 us per layer at ~3.7 TB/s); here every input
+// is read once and nothing round-trips through HBM (no delta array).
+constexpr int FS_S = 128;   // longest sequence of the one-block form
+constexpr int FS_DSR = 72;  // dS row stride in bf16: 64 keys + 8 pad (row r at bank 36 r: the dQ reads of 16 query rows
+                            // x 2 lane groups cover the 64 banks once; the dS writes of 4g-apart rows land 16 banks apart)
+__global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_short_kernel(AttnBwdArgs a, const uint16_t* o, long sob,
+                                                                       long sos, long soh) {
+  constexpr int NK = 2, ND = 4, TQ = FS_S * 64 * 2;  // Q / dO / K tile bytes (16 KB, one K-major half)
+  __shared__ __attribute__((aligned(1024))) char smem[3 * TQ + FS_S * FS_DSR * 2 + 2 * FS_S * 4];
+  char* tq = smem;
+  char* tdo = smem + TQ;
+  char* tk = smem + 2 * TQ;
+  uint16_t* dsl = reinterpret_cast<uint16_t*>(smem + 3 * TQ);
+  float* tl = reinterpret_cast<float*>(smem + 3 * TQ + FS_S * FS_DSR * 2);  // lse [128] | delta [128]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  const int b = blockIdx.x / a.Hq, h = blockIdx.x - b * a.Hq;
+  const int off = a.Sk - a.Sq;
+  int kv_end = a.Sk;
+  if (a.kv_lens) kv_end = min(kv_end, a.kv_lens[b]);
+
+  const uint16_t* qp = a.q + (long)b * a.sqb + (long)h * a.sqh;
+  const uint16_t* dop = a.dO + (long)b * a.sdb + (long)h * a.sdh;
+  const uint16_t* kp = a.k + (long)b * a.skb + (long)h * a.skh;
+  const uint16_t* vp = a.v + (long)b * a.svb + (long)h * a.svh;
+  const uint16_t* op = o + (long)b * sob + (long)h * soh;
+
+  // ---- prologue: tiles (rows past the sequence clamped to its last row; their P / dS are masked to 0)
+#pragma unroll
+  for (int rd = 0; rd < TQ / (16 * FA_THREADS); ++rd) {
+    const int s = rd * FA_THREADS + tid;
+    const size_t wb = (size_t)(rd * FA_THREADS + wid_u * 64) * 16;
+    glds16(kh_src(qp, a.sqs, FS_S, 0, a.Sq, s), tq + wb);
+    glds16(kh_src(dop, a.sds, FS_S, 0, a.Sq, s), tdo + wb);
+    glds16(kh_src(kp, a.sks, FS_S, 0, a.Sk, s), tk + wb);
+  }
+  if (tid < FS_S) tl[tid] = tid < a.Sq ? a.lse[((long)b * a.Hq + h) * a.lse_ld + tid] : 0.f;
+  {
+    const int q = tid >> 1, c0 = (tid & 1) * 32;  // two lanes per query, 32 columns each
+    float acc = 0.f;
+    if (q < a.Sq) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float x[8], y[8];
+        load8(op + (long)q * sos + c0 + 8 * j, x);
+        load8(dop + (long)q * a.sds + c0 + 8 * j, y);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc += x[e] * y[e];
+      }
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    if ((tid & 1) == 0) tl[FS_S + q] = acc;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int q_ = li >> 2, pp = li & 3;
+  const int nqh = (a.Sq + 63) / 64, nkc = (a.Sk + 63) / 64;
+  f32x4_t dqa[2][ND];
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+    for (int d = 0; d < ND; ++d) dqa[qs][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int kc = 0; kc < nkc; ++kc) {
+    const int kw = kc * 64 + wid_u * 16, key = kw + li;
+    mfma_bf16x8 kf[NK], vf[NK];
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      kf[kk] = frag_kh(tk, kw, kk, lane);
+      bf16x8_t y = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (key < a.Sk) y = *reinterpret_cast<const bf16x8_t*>(vp + (long)key * a.svs + kk * 32 + g * 8);
+      vf[kk] = __builtin_bit_cast(mfma_bf16x8, y);
+    }
+    f32x4_t dka[ND], dva[ND];
+#pragma unroll
+    for (int d = 0; d < ND; ++d) dka[d] = dva[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int qh = 0; qh < nqh; ++qh) {
+      const int q0 = qh * 64;
+      f32x4_t sv[4], dp[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sv[i] = dp[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk)
+#pragma unroll
+        for (int qs = 0; qs < 4; ++qs) {
+          sv[qs] = mfma16(frag_kh(tq, q0 + qs * 16, kk, lane), kf[kk], sv[qs]);
+          dp[qs] = mfma16(frag_kh(tdo, q0 + qs * 16, kk, lane), vf[kk], dp[qs]);
+        }
+      const bool need_mask = q0 + 64 > a.Sq || kc * 64 + 64 > kv_end || (a.causal && kc * 64 + 63 > q0 + off);
+#pragma unroll
+      for (int qs = 0; qs < 4; ++qs) {
+        f32x4_t l4 = *reinterpret_cast<const f32x4_t*>(tl + q0 + qs * 16 + g * 4);
+        f32x4_t d4 = *reinterpret_cast<const f32x4_t*>(tl + FS_S + q0 + qs * 16 + g * 4);
+        if (need_mask) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int qi = q0 + qs * 16 + g * 4 + r;
+            const bool ok = qi < a.Sq && key < kv_end && !(a.causal && key > qi + off);
+            sv[qs][r] = ok ? sv[qs][r] : -INFINITY;
+            l4[r] = ok ? l4[r] : 0.f;
+            d4[r] = ok ? d4[r] : 0.f;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = fexp2(sv[qs][r] * a.scale_log2 - l4[r]);
+          sv[qs][r] = p;
+          dp[qs][r] = p * (dp[qs][r] - d4[r]);
+          dsl[(q0 + qs * 16 + g * 4 + r) * FS_DSR + wid_u * 16 + li] = f2bf(dp[qs][r]);
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const float p0[4] = {sv[2 * s2][0], sv[2 * s2][1], sv[2 * s2][2], sv[2 * s2][3]};
+        const float p1[4] = {sv[2 * s2 + 1][0], sv[2 * s2 + 1][1], sv[2 * s2 + 1][2], sv[2 * s2 + 1][3]};
+        const float d0[4] = {dp[2 * s2][0], dp[2 * s2][1], dp[2 * s2][2], dp[2 * s2][3]};
+        const float d1[4] = {dp[2 * s2 + 1][0], dp[2 * s2 + 1][1], dp[2 * s2 + 1][2], dp[2 * s2 + 1][3]};
+        const mfma_bf16x8 pf = pack8(p0, p1), dsf = pack8(d0, d1);
+        const int r0 = q0 + 32 * s2 + 4 * g + q_, r1 = r0 + 16;
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+          const int dc = d * 16 + pp * 4;
+          const mfma_bf16x8 dot = join8(tr16(kh_addr(tdo, FS_S, r0, dc)), tr16(kh_addr(tdo, FS_S, r1, dc)));
+          const mfma_bf16x8 qtf = join8(tr16(kh_addr(tq, FS_S, r0, dc)), tr16(kh_addr(tq, FS_S, r1, dc)));
+          dva[d] = mfma16(dot, pf, dva[d]);
+          dka[d] = mfma16(qtf, dsf, dka[d]);
+        }
+      }
+    }
+    if (key < a.Sk) {
+      uint16_t* dkp = a.dk + b * a.sgkb + key * a.sgks + h * a.sgkh;
+      uint16_t* dvp = a.dv + b * a.sgvb + key * a.sgvs + h * a.sgvh;
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        bf16x4_t x, y;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          x[r] = (short)f2bf(dka[d][r] * a.scale);
+          y[r] = (short)f2bf(dva[d][r]);
+        }
+        *reinterpret_cast<bf16x4_t*>(dkp + d * 16 + g * 4) = x;
+        *reinterpret_cast<bf16x4_t*>(dvp + d * 16 + g * 4) = y;
+      }
+    }
+    __syncthreads();  // the chunk's dS complete
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      mfma_bf16x8 dsf[2];
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        const uint16_t* row = dsl + (wid_u * 32 + qs * 16 + li) * FS_DSR + 32 * s2 + 4 * g;
+        dsf[qs] = join8(*reinterpret_cast<const short4_t*>(row), *reinterpret_cast<const short4_t*>(row + 16));
+      }
+      const int r0 = kc * 64 + 32 * s2 + 4 * g + q_, r1 = r0 + 16;
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        const int dc = d * 16 + pp * 4;
+        const mfma_bf16x8 kt = join8(tr16(kh_addr(tk, FS_S, r0, dc)), tr16(kh_addr(tk, FS_S, r1, dc)));
+#pragma unroll
+        for (int qs = 0; qs < 2; ++qs) dqa[qs][d] = mfma16(kt, dsf[qs], dqa[qs][d]);
+      }
+    }
+    __syncthreads();  // dS reads done before the next chunk overwrites it
+  }
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    const int qi = wid_u * 32 + qs * 16 + li;
+    if (qi < a.Sq) {
+      uint16_t* dqp = a.dq + b * a.sgqb + qi * a.sgqs + h * a.sgqh;
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        bf16x4_t x;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = (short)f2bf(dqa[qs][d][r] * a.scale);
+        *reinterpret_cast<bf16x4_t*>(dqp + d * 16 + g * 4) = x;
+      }
+    }
+  }
+}
+
+static bool short_bwd_ok(const AttnBwdArgs& a, int D) {
+  static const bool on = [] {
+    const char* e = std::getenv("K8S_AMD_FA_SHORT_BWD");
+    return !(e && e[0] == '0');
+  }();
+  return on && D == 64 && a.Sq > 0 && a.Sk > 0 && a.Sq <= FS_S && a.Sk <= FS_S && a.Hq == a.Hkv && a.dkv_split == 1;
+}
+
 // =============================================================================== launchers
 // D = 64 with long sequences: 128-wide key / query steps (same MFMA work per barrier as D = 128)
 static bool big_tile(int D, int S) { return D == 64 && S >= 1024; }
@@ -793,6 +988,12 @@ void launch_flash_fwd(const AttnFwdArgs& a, int D, hipStream_t st) {
 
 void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, long sos, long soh,
                       hipStream_t st) {
+  if (short_bwd_ok(a, D)) {
+    if ((long)a.B * a.Hq > 0)
+      hipLaunchKernelGGL(flash_bwd_short_kernel, dim3((unsigned)(a.B * a.Hq)), dim3(FA_THREADS), 0, st, a, o, sob,
+                         sos, soh);
+    return;
+  }
   const long R = (long)a.B * a.Sq * a.Hq;
   const int lpr = D / 8;
   const dim3 dgrid((unsigned)((R * lpr + 255) / 256));

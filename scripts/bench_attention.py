@@ -27,10 +27,13 @@ def bench(fn, it=20):
 
 def main():
     C = load()
-    cases = [("bert_s128", 64, 128, 12, 12, 64, False), ("bert_s512", 16, 512, 12, 12, 64, False),
+    cases = [("bert_s128", 64, 128, 12, 12, 64, False), ("bert_s128_b1024", 1024, 128, 12, 12, 64, False), ("bert_s512", 16, 512, 12, 12, 64, False),
              ("llama_s2048", 2, 2048, 32, 8, 128, True), ("llama1b_s2048_d64", 2, 2048, 32, 8, 64, True), ("llama_s4096", 1, 4096, 32, 8, 128, True),
              ("mha_s4096_nc", 1, 4096, 32, 32, 128, False)]
+    only = os.environ.get("ATTN_CASES")
     for name, B, S, Hq, Hkv, D, causal in cases:
+        if only and name not in only.split(","):
+            continue
         q = torch.randn(B, S, Hq, D, device="cuda").bfloat16()
         k = torch.randn(B, S, Hkv, D, device="cuda").bfloat16()
         v = torch.randn(B, S, Hkv, D, device="cuda").bfloat16()

@@ -33,6 +33,12 @@ CASES = [
     # lengths (key blocks past kv_len have empty chunks), ragged last query tile
     (2, 700, 6, 2, 128, True, [700, 333]),
     (1, 600, 2, 2, 64, True, [450]),
+    # one-block backward of short sequences (S <= 128, D = 64, no GQA): one query half, ragged key chunk, key
+    # lengths incl. an empty row, causal with lengths, and a GQA short case that keeps the three-kernel form
+    (3, 77, 4, 4, 64, False, [77, 30, 0]),
+    (2, 128, 3, 3, 64, True, [128, 65]),
+    (2, 100, 4, 4, 64, True, None),
+    (2, 128, 4, 2, 64, False, None),
 ]
 
 
