@@ -105,14 +105,15 @@ __device__ __forceinline__ const uint16_t* kh_src(const uint16_t* base, long rst
 }
 
 // =============================================================================== forward
-template <int D, int TILE>
-__global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a) {
+// NB: K/V stage buffers (1: every key in one tile, Sk <= TILE -- the short-sequence form, no second buffer)
+template <int D, int TILE, int NB = 2>
+__global__ void __launch_bounds__(FA_THREADS, NB == 1 ? 3 : 2) flash_fwd_kernel(AttnFwdArgs a) {
   constexpr int FA_BN = TILE;  // keys per iteration
   constexpr int NI = FA_BN / 16;       // 16-key subtiles
   constexpr int KT = FA_BN * D * 2;    // bytes of one K (or V) tile
   constexpr int UPR = D / 8;         // 16-B units per V row
   constexpr int ND = D / 16, NK = D / 32;
-  __shared__ __attribute__((aligned(1024))) char smem[4 * KT];  // [buf][K | V]
+  __shared__ __attribute__((aligned(1024))) char smem[NB * 2 * KT];  // [buf][K | V]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
 
@@ -197,8 +198,8 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_fwd_kernel(AttnFwdArgs a)
   // tile)
   auto tile = [&](const int t, auto masked_tag) {
     constexpr bool MASKED = decltype(masked_tag)::value;
-    const int cur = t & 1, key0 = t * FA_BN;
-    if (t + 1 < ntiles) stage(cur ^ 1, key0 + FA_BN);
+    const int cur = NB > 1 ? (t & 1) : 0, key0 = t * FA_BN;
+    if (NB > 1 && t + 1 < ntiles) stage(cur ^ 1, key0 + FA_BN);
     const char* tk = smem + cur * 2 * KT;
     const char* tv = tk + KT;
     const bool skip = MASKED && a.causal && key0 > q0w + 31 + off;  // whole tile masked for this wave
@@ -828,11 +829,11 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_short_kernel(AttnBwdA
 
   const int q_ = li >> 2, pp = li & 3;
   const int nqh = (a.Sq + 63) / 64, nkc = (a.Sk + 63) / 64;
-  f32x4_t dqa[2][ND];
+  f32x4_t dqa[2][ND], dks[ND], dvs[ND];  // dks / dvs: this lane's dK / dV column sums over its chunk keys (cpart)
 #pragma unroll
-  for (int qs = 0; qs < 2; ++qs)
-#pragma unroll
-    for (int d = 0; d < ND; ++d) dqa[qs][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int d = 0; d < ND; ++d) {
+    dqa[0][d] = dqa[1][d] = dks[d] = dvs[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
 
   for (int kc = 0; kc < nkc; ++kc) {
     const int kw = kc * 64 + wid_u * 16, key = kw + li;
@@ -915,6 +916,13 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_short_kernel(AttnBwdA
         *reinterpret_cast<bf16x4_t*>(dvp + d * 16 + g * 4) = y;
       }
     }
+    if (a.cpart) {  // (keys past the sequence carry zero P / dS, so zero dK / dV)
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        dks[d] += dka[d];
+        dvs[d] += dva[d];
+      }
+    }
     __syncthreads();  // the chunk's dS complete
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -949,14 +957,40 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_short_kernel(AttnBwdA
       }
     }
   }
+  if (a.cpart) {
+    // column sums of the block's dQ / dK / dV rows: each 16-lane row sums its lanes (DPP; lane = query or key), the
+    // 4 waves combine through LDS (the Q tile, free since the last chunk's closing barrier)
+    float* red = reinterpret_cast<float*>(smem);  // [dq | dk | dv][wave][64 columns]
+    const bool v0 = wid_u * 32 + li < a.Sq, v1 = wid_u * 32 + 16 + li < a.Sq;  // dS rows past Sq may be unwritten
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float sq = row16_sum((v0 ? dqa[0][d][r] : 0.f) + (v1 ? dqa[1][d][r] : 0.f));
+        const float sk = row16_sum(dks[d][r]), sv = row16_sum(dvs[d][r]);
+        if (li == 0) {
+          const int c = d * 16 + g * 4 + r;
+          red[wid_u * 64 + c] = sq * a.scale;
+          red[(4 + wid_u) * 64 + c] = sk * a.scale;
+          red[(8 + wid_u) * 64 + c] = sv;
+        }
+      }
+    __syncthreads();
+    if (tid < 192) {
+      const int part = tid >> 6, c = tid & 63;
+      const float* rp = red + part * 256 + c;
+      const float s = (rp[0] + rp[64]) + (rp[128] + rp[192]);
+      a.cpart[(long)b * a.cpart_ld + (part * a.Hq + h) * 64 + c] = s;  // q, k, v column blocks (Hkv == Hq)
+    }
+  }
 }
 
-static bool short_bwd_ok(const AttnBwdArgs& a, int D) {
+bool flash_bwd_one_block(int D, int Sq, int Sk, int Hq, int Hkv, int dkv_split) {
   static const bool on = [] {
     const char* e = std::getenv("K8S_AMD_FA_SHORT_BWD");
     return !(e && e[0] == '0');
   }();
-  return on && D == 64 && a.Sq > 0 && a.Sk > 0 && a.Sq <= FS_S && a.Sk <= FS_S && a.Hq == a.Hkv && a.dkv_split == 1;
+  return on && D == 64 && Sq > 0 && Sk > 0 && Sq <= FS_S && Sk <= FS_S && Hq == Hkv && dkv_split == 1;
 }
 
 // =============================================================================== launchers
@@ -978,17 +1012,27 @@ int flash_dkv_splits(int B, int Sq, int Sk, int Hkv, int causal) {
   return nblk >= 4 * cus ? 1 : (2 * nblk >= 3 * cus ? 2 : 4);
 }
 
+// D = 64, Sk <= 128: every key in one 128-key tile, one stage buffer (K8S_AMD_FA_ONE_TILE=0 keeps the 64-key tiles)
+static bool fwd_one_tile() {
+  static const bool on = [] {
+    const char* e = std::getenv("K8S_AMD_FA_ONE_TILE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 void launch_flash_fwd(const AttnFwdArgs& a, int D, hipStream_t st) {
   const int nqb = (a.Sq + FA_BM - 1) / FA_BM;
   const dim3 grid(nqb * a.Hq * a.B), blk(FA_THREADS);
   if (D == 128) hipLaunchKernelGGL((flash_fwd_kernel<128, 64>), grid, blk, 0, st, a);
   else if (big_tile(D, a.Sk)) hipLaunchKernelGGL((flash_fwd_kernel<64, 128>), grid, blk, 0, st, a);
+  else if (a.Sk <= 128 && fwd_one_tile()) hipLaunchKernelGGL((flash_fwd_kernel<64, 128, 1>), grid, blk, 0, st, a);
   else hipLaunchKernelGGL((flash_fwd_kernel<64, 64>), grid, blk, 0, st, a);
 }
 
 void launch_flash_bwd(const AttnBwdArgs& a, int D, const uint16_t* o, long sob, long sos, long soh,
                       hipStream_t st) {
-  if (short_bwd_ok(a, D)) {
+  if (flash_bwd_one_block(D, a.Sq, a.Sk, a.Hq, a.Hkv, a.dkv_split)) {
     if ((long)a.B * a.Hq > 0)
       hipLaunchKernelGGL(flash_bwd_short_kernel, dim3((unsigned)(a.B * a.Hq)), dim3(FA_THREADS), 0, st, a, o, sob,
                          sos, soh);

@@ -186,8 +186,14 @@ struct AttnBwdArgs {
   // dK/dV split into dkv_split chunks per key block (flash_dkv_splits): fp32 partials [dkv_split][2][B][Hkv][Sk][D]
   int dkv_split = 1;
   float* dkv_ws = nullptr;
+  // one-block short-sequence form only (flash_bwd_one_block): per-batch column sums of the packed QKV gradient,
+  // fp32 [B][cpart_ld] (the projection's bias gradient once folded over B)
+  float* cpart = nullptr;
+  int cpart_ld = 0;
 };
 int flash_dkv_splits(int B, int Sq, int Sk, int Hkv, int causal);
+// the whole backward of one (batch, head) in one block (flash_bwd_short_kernel) applies to this shape
+bool flash_bwd_one_block(int D, int Sq, int Sk, int Hq, int Hkv, int dkv_split);
 // ResNet stem BatchNorm + ReLU + 3x3 / s2 / p1 max pool, fused (batchnorm.hip): forward from the conv's epilogue sums
 // (params = fp32 [2][C] scale | shift, idx = winner byte per pooled element); backward into dx of the conv output
 // (params = fp32 [4][C] workspace, work = pool_bn_workspace_floats(C))

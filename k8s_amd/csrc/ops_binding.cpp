@@ -848,7 +848,8 @@ std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, bool causal, c10::op
 // buffer laid out like the packed QKV projection q / k / v were sliced from (q at column 0, k at Hq*D, v at
 // (Hq + Hkv)*D): the fused projection's gradient is written in place, no concatenation afterwards.
 std::vector<Tensor> flash_bwd(Tensor dO, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal,
-                              c10::optional<Tensor> kv_lens, double scale, c10::optional<Tensor> dqkv) {
+                              c10::optional<Tensor> kv_lens, double scale, c10::optional<Tensor> dqkv,
+                              c10::optional<Tensor> dbias) {
   const long D = q.size(-1);
   TORCH_CHECK(D == 64 || D == 128, "head dim must be 64 or 128");
   check_attn_operand(q, "q", D); check_attn_operand(k, "k", D); check_attn_operand(v, "v", D);
@@ -897,7 +898,19 @@ std::vector<Tensor> flash_bwd(Tensor dO, Tensor q, Tensor k, Tensor v, Tensor o,
     dkv_ws = torch::empty({a.dkv_split, 2, B, Hkv, Sk, D}, q.options().dtype(at::kFloat));
     a.dkv_ws = f32(dkv_ws);
   }
+  Tensor cpart;
+  if (dbias) {  // the packed projection's bias gradient from the one-block kernel's column partials
+    const long W = (Hq + 2 * Hkv) * D;
+    TORCH_CHECK(dqkv && k8s_amd::flash_bwd_one_block((int)D, (int)Sq, (int)Sk, (int)Hq, (int)Hkv, a.dkv_split),
+                "dbias needs the packed gradient and a one-block shape (flash_bwd_one_block)");
+    check_cuda(*dbias, "dbias"); check_dtype(*dbias, at::kFloat, "dbias");
+    TORCH_CHECK(dbias->is_contiguous() && dbias->numel() == W, "dbias must be fp32 [(Hq+2*Hkv)*D]");
+    cpart = torch::empty({B, W}, q.options().dtype(at::kFloat));
+    a.cpart = f32(cpart);
+    a.cpart_ld = (int)W;
+  }
   k8s_amd::launch_flash_bwd(a, (int)D, cbf(o), o.stride(0), o.stride(1), o.stride(2), cur_stream());
+  if (dbias) k8s_amd::launch_colsum_fold(a.cpart, (int)B, a.cpart_ld, f32(*dbias), false, cur_stream());
   return {dq, dk, dv};
 }
 
@@ -1128,7 +1141,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("flash_bwd", &flash_bwd, py::arg("dO"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
-        py::arg("lse"), py::arg("causal"), py::arg("kv_lens"), py::arg("scale"), py::arg("dqkv") = py::none());
+        py::arg("lse"), py::arg("causal"), py::arg("kv_lens"), py::arg("scale"), py::arg("dqkv") = py::none(),
+        py::arg("dbias") = py::none());
+  m.def("flash_bwd_one_block", [](int64_t D, int64_t Sq, int64_t Sk, int64_t Hq, int64_t Hkv, bool causal, int64_t B) {
+          return k8s_amd::flash_bwd_one_block((int)D, (int)Sq, (int)Sk, (int)Hq, (int)Hkv,
+                                              k8s_amd::flash_dkv_splits((int)B, (int)Sq, (int)Sk, (int)Hkv, causal));
+        }, "whether flash_bwd runs as the one-block short-sequence kernel (which can also emit the packed bias gradient)");
   m.attr("conv_stat_replicas") = k8s_amd::kConvStatReplicas;
   m.def("gemm_short_ok", [](int64_t M, int64_t N, int64_t K) { return k8s_amd::gemm_short_ok((int)M, (int)N, (int)K, K, N); },
         "whether C[M,N] = A[M,K] . B^T (contiguous) takes the short-K streaming kernel (gemm_short.hip)");

@@ -79,9 +79,11 @@ class BertLayer(nn.Module):
         # GradLink sums the two gradient contributions in the GEMM's dgrad epilogue instead of a separate add
         l1, l2 = K.GradLink(), K.GradLink()
         # and the O / FFN2 bias gradients come from the LayerNorm backward that reads their outputs (BiasLink)
-        b1, b2 = K.BiasLink(), K.BiasLink()
-        qkv = K.linear(x, self.qkv_w, self.qkv_b, grad_link=l1)  # [T, 3h]
-        o = attention_qkv(qkv, B, S, nh, nh, d, causal=False, kv_lens=kv_lens)  # packed QKV gradient in place
+        # (and short sequences take the QKV bias gradient from the attention backward's column partials)
+        b0, b1, b2 = K.BiasLink(), K.BiasLink(), K.BiasLink()
+        qkv = K.linear(x, self.qkv_w, self.qkv_b, grad_link=l1, bias_link=b0)  # [T, 3h]
+        o = attention_qkv(qkv, B, S, nh, nh, d, causal=False, kv_lens=kv_lens,
+                          bias_link=b0)  # packed QKV gradient in place
         a = K.linear(o.reshape(B * S, h), self.o_w, self.o_b, bias_link=b1)
         x, _ = K.layer_norm(a, self.ln1_g, self.ln1_b, c.eps, residual=x, res_link=l1, bias_link=b1)
         # FFN1's GELU backward and bias gradient inside FFN2's data-gradient epilogue (ActLink)

@@ -101,7 +101,7 @@ class _FlashQKV(torch.autograd.Function):
     copies on either pass."""
 
     @staticmethod
-    def forward(ctx, qkv, B, S, H, Hkv, D, causal, kv_lens, scale, pos, table):
+    def forward(ctx, qkv, B, S, H, Hkv, D, causal, kv_lens, scale, pos, table, bias_link=None):
         C = _load()
         if kv_lens is not None:
             kv_lens = kv_lens.to(device=qkv.device, dtype=torch.int32).contiguous()
@@ -115,6 +115,7 @@ class _FlashQKV(torch.autograd.Function):
         ctx.save_for_backward(x, o, lse, kv_lens if kv_lens is not None else torch.empty(0),
                               pos if pos is not None else torch.empty(0), table if table is not None else torch.empty(0))
         ctx.meta = (B, S, H, Hkv, D, causal, scale, kv_lens is not None, pos is not None)
+        ctx.bias_link = bias_link
         return o
 
     @staticmethod
@@ -125,25 +126,39 @@ class _FlashQKV(torch.autograd.Function):
         g = x.view(B, S, H + 2 * Hkv, D)
         q, k, v = g.narrow(2, 0, H), g.narrow(2, H, Hkv), g.narrow(2, H + Hkv, Hkv)
         dqkv = torch.empty_like(x)
-        C.flash_bwd(do.contiguous(), q, k, v, o, lse, causal, lens if has_lens else None, scale, dqkv)
+        # the projection's bias gradient (column sums of dqkv) from the one-block kernel (BiasLink); not with rope,
+        # which rotates dqkv after the kernel
+        bl, dsum, ss, lpb = ctx.bias_link, None, None, None
+        if bl is not None and bl.pb is not None and not has_rope and \
+                C.flash_bwd_one_block(D, S, S, H, Hkv, causal, B):
+            lpb = bl.pb
+            ss = lpb.store.slot_for_write(lpb)
+            dsum = ss.view(lpb.shape) if ss is not None else torch.empty(lpb.shape, device=x.device,
+                                                                         dtype=torch.float32)
+        C.flash_bwd(do.contiguous(), q, k, v, o, lse, causal, lens if has_lens else None, scale, dqkv, dsum)
+        if dsum is not None:
+            lpb.store.mark_written(lpb) if ss is not None else lpb.store.deposit(lpb, dsum)
+            bl.done = True
         if has_rope:
             C.rope_(dqkv[:, : (H + Hkv) * D], pos, table, True)
-        return dqkv, None, None, None, None, None, None, None, None, None, None
+        return (dqkv,) + (None,) * 11
 
 
 def attention_qkv(qkv, B: int, S: int, heads: int, kv_heads: int, head_dim: int, causal: bool = False,
                   kv_lens: Optional[torch.Tensor] = None, rope: Optional[tuple] = None,
-                  scale: Optional[float] = None):
+                  scale: Optional[float] = None, bias_link=None):
     """Self-attention of a packed QKV projection ``qkv`` [B*S, (heads + 2*kv_heads) * head_dim] (q heads, then k,
     then v); ``rope`` = (pos [B*S] int32, table) applies rotary embeddings to q and k. Returns o [B, S, heads, D].
-    GPU bf16: one fused path (``_FlashQKV``); otherwise the split + ``attention`` reference composition."""
+    GPU bf16: one fused path (``_FlashQKV``); otherwise the split + ``attention`` reference composition.
+    ``bias_link`` (``nn.BiasLink``, also given to the projection ``linear``): short sequences emit the projection's
+    bias gradient from the attention backward, and the linear skips its column-sum pass."""
     D = head_dim
     scale = scale or 1.0 / math.sqrt(D)
     W = (heads + 2 * kv_heads) * D
     if qkv.is_cuda and qkv.dtype == torch.bfloat16 and D in (64, 128) and qkv.shape[-1] == W and \
             W % 8 == 0 and qkv.is_contiguous():
         pos, table = rope if rope is not None else (None, None)
-        return _FlashQKV.apply(qkv, B, S, heads, kv_heads, D, causal, kv_lens, scale, pos, table)
+        return _FlashQKV.apply(qkv, B, S, heads, kv_heads, D, causal, kv_lens, scale, pos, table, bias_link)
     q, k, v = qkv.split([heads * D, kv_heads * D, kv_heads * D], dim=-1)
     if rope is not None:
         from k8s_amd.ops import nn as _nn

@@ -113,3 +113,26 @@ def test_attention_qkv_packed_matches_split(cuda, B, S, H, Hkv, D, causal, rope,
     rel = lambda a, b: ((a.float() - b.float()).norm() / b.float().norm()).item()  # noqa: E731
     assert rel(o, ref) < 2e-2
     assert rel(g, gr) < 3e-2
+
+
+@pytest.mark.parametrize("B,S,H,causal,lens", [(3, 128, 4, False, [128, 60, 0]), (2, 77, 3, True, None)])
+def test_flash_bwd_packed_bias_grad(cuda, B, S, H, causal, lens):
+    """One-block backward's column partials of the packed gradient (the QKV projection's bias gradient, folded over
+    the batch) against the column sums of the dqkv it wrote."""
+    from k8s_amd.ops._ext import load
+
+    C = load()
+    D = 64
+    assert C.flash_bwd_one_block(D, S, S, H, H, causal, B)
+    torch.manual_seed(3)
+    x = torch.randn(B * S, 3 * H * D, device=cuda).bfloat16()
+    g = x.view(B, S, 3 * H, D)
+    q, k, v = g.narrow(2, 0, H), g.narrow(2, H, H), g.narrow(2, 2 * H, H)
+    lens_t = torch.tensor(lens, device=cuda, dtype=torch.int32) if lens else None
+    o, lse = C.flash_fwd(q, k, v, causal, lens_t, 0.125)
+    do = torch.randn_like(o)
+    dqkv = torch.empty_like(x)
+    db = torch.full((3 * H * D,), float("nan"), device=cuda)
+    C.flash_bwd(do, q, k, v, o, lse, causal, lens_t, 0.125, dqkv, db)
+    ref = dqkv.float().sum(0)
+    _close(db, ref, 2e-2, "db")
