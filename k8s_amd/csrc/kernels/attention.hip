@@ -824,6 +824,19 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_short_kernel(AttnBwdA
     acc += __shfl_xor(acc, 1, 64);
     if ((tid & 1) == 0) tl[FS_S + q] = acc;
   }
+  // V fragments of this wave's keys in both chunks, in flight with the tiles (loaded per chunk, each chunk's first
+  // MFMAs waited on them)
+  mfma_bf16x8 vfc[2][NK];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int key = c * 64 + wid_u * 16 + li;
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      bf16x8_t y = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (key < a.Sk) y = *reinterpret_cast<const bf16x8_t*>(vp + (long)key * a.svs + kk * 32 + g * 8);
+      vfc[c][kk] = __builtin_bit_cast(mfma_bf16x8, y);
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -841,9 +854,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_short_kernel(AttnBwdA
 #pragma unroll
     for (int kk = 0; kk < NK; ++kk) {
       kf[kk] = frag_kh(tk, kw, kk, lane);
-      bf16x8_t y = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (key < a.Sk) y = *reinterpret_cast<const bf16x8_t*>(vp + (long)key * a.svs + kk * 32 + g * 8);
-      vf[kk] = __builtin_bit_cast(mfma_bf16x8, y);
+      vf[kk] = kc ? vfc[1][kk] : vfc[0][kk];
     }
     f32x4_t dka[ND], dva[ND];
 #pragma unroll
@@ -891,13 +902,23 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_short_kernel(AttnBwdA
         const float d1[4] = {dp[2 * s2 + 1][0], dp[2 * s2 + 1][1], dp[2 * s2 + 1][2], dp[2 * s2 + 1][3]};
         const mfma_bf16x8 pf = pack8(p0, p1), dsf = pack8(d0, d1);
         const int r0 = q0 + 32 * s2 + 4 * g + q_, r1 = r0 + 16;
+        // transposed reads as asm tied to an explicit LDS wait: the builtin form made the compiler drain vmcnt
+        // (the dK / dV / dQ stores in flight) in front of every read
+        short4_t ol[ND], oh[ND], ql[ND], qh4[ND];
 #pragma unroll
         for (int d = 0; d < ND; ++d) {
           const int dc = d * 16 + pp * 4;
-          const mfma_bf16x8 dot = join8(tr16(kh_addr(tdo, FS_S, r0, dc)), tr16(kh_addr(tdo, FS_S, r1, dc)));
-          const mfma_bf16x8 qtf = join8(tr16(kh_addr(tq, FS_S, r0, dc)), tr16(kh_addr(tq, FS_S, r1, dc)));
-          dva[d] = mfma16(dot, pf, dva[d]);
-          dka[d] = mfma16(qtf, dsf, dka[d]);
+          tr16_asm(ol[d], kh_addr(tdo, FS_S, r0, dc));
+          tr16_asm(oh[d], kh_addr(tdo, FS_S, r1, dc));
+          tr16_asm(ql[d], kh_addr(tq, FS_S, r0, dc));
+          tr16_asm(qh4[d], kh_addr(tq, FS_S, r1, dc));
+        }
+        K8S_LDS_TIE8("s_waitcnt lgkmcnt(0)", ol[0], ol[1], ol[2], ol[3], oh[0], oh[1], oh[2], oh[3]);
+        K8S_LDS_TIE8("", ql[0], ql[1], ql[2], ql[3], qh4[0], qh4[1], qh4[2], qh4[3]);
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+          dva[d] = mfma16(join8(ol[d], oh[d]), pf, dva[d]);
+          dka[d] = mfma16(join8(ql[d], qh4[d]), dsf, dka[d]);
         }
       }
     }
@@ -933,10 +954,17 @@ __global__ void __launch_bounds__(FA_THREADS, 2) flash_bwd_short_kernel(AttnBwdA
         dsf[qs] = join8(*reinterpret_cast<const short4_t*>(row), *reinterpret_cast<const short4_t*>(row + 16));
       }
       const int r0 = kc * 64 + 32 * s2 + 4 * g + q_, r1 = r0 + 16;
+      short4_t kl[ND], kh4[ND];
 #pragma unroll
       for (int d = 0; d < ND; ++d) {
         const int dc = d * 16 + pp * 4;
-        const mfma_bf16x8 kt = join8(tr16(kh_addr(tk, FS_S, r0, dc)), tr16(kh_addr(tk, FS_S, r1, dc)));
+        tr16_asm(kl[d], kh_addr(tk, FS_S, r0, dc));
+        tr16_asm(kh4[d], kh_addr(tk, FS_S, r1, dc));
+      }
+      K8S_LDS_TIE8("s_waitcnt lgkmcnt(0)", kl[0], kl[1], kl[2], kl[3], kh4[0], kh4[1], kh4[2], kh4[3]);
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        const mfma_bf16x8 kt = join8(kl[d], kh4[d]);
 #pragma unroll
         for (int qs = 0; qs < 2; ++qs) dqa[qs][d] = mfma16(kt, dsf[qs], dqa[qs][d]);
       }

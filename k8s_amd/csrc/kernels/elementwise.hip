@@ -218,25 +218,35 @@ __global__ void __launch_bounds__(256) act_bwd_colsum_partial_kernel(const uint1
 
 // fold of the P partial rows: block = 64 columns x 4 partial-row groups (a wave each), LDS combine. P is up to
 // 256 rows of L2-resident partials: 4 waves x P/4 independent loads per lane instead of one lane walking all P.
-__global__ void __launch_bounds__(256) colsum_fold_kernel(const float* __restrict__ part, int P, int C,
-                                                          float* __restrict__ out, int accumulate) {
+// Rows are ldp floats apart. With gridDim.y > 1 (the first level of a two-level fold of many rows): block y sums
+// rows [y gs, min(P, (y + 1) gs)) and writes the result over row y gs (only this block reads that group).
+__global__ void __launch_bounds__(256) colsum_fold_kernel(const float* part, int P, int C, float* out, int accumulate,
+                                                          long ldp = 0,
+                                                          int gs = 0) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), pg = threadIdx.x >> 6;
+  if (ldp == 0) ldp = C;
+  if (gridDim.y > 1) {
+    part += (long)blockIdx.y * gs * ldp;
+    P = min(gs, P - (int)blockIdx.y * gs);
+    out = const_cast<float*>(part);
+    accumulate = 0;
+  }
   float s = 0.f;
   if (c < C) {
     int p = pg;
     for (; p + 12 < P; p += 16) {  // 4 loads in flight per lane
-      const float a = part[(long)p * C + c], b = part[(long)(p + 4) * C + c];
-      const float d = part[(long)(p + 8) * C + c], e = part[(long)(p + 12) * C + c];
+      const float a = part[(long)p * ldp + c], b = part[(long)(p + 4) * ldp + c];
+      const float d = part[(long)(p + 8) * ldp + c], e = part[(long)(p + 12) * ldp + c];
       s += (a + b) + (d + e);
     }
-    for (; p < P; p += 4) s += part[(long)p * C + c];
+    for (; p < P; p += 4) s += part[(long)p * ldp + c];
   }
   __shared__ float sh[4][64];
   sh[pg][threadIdx.x & 63] = s;
   __syncthreads();
   if (pg == 0 && c < C) {
     s = (sh[0][threadIdx.x] + sh[1][threadIdx.x]) + (sh[2][threadIdx.x] + sh[3][threadIdx.x]);
-    out[c] = accumulate ? out[c] + s : s;
+    out[c] = accumulate ? out[c] + s : s;  // (two-level first pass: every read of this group was before the barrier)
   }
 }
 
@@ -274,17 +284,30 @@ void launch_act_bwd_colsum(int act, const uint16_t* dy, const uint16_t* pre, uin
     hipLaunchKernelGGL(act_bwd_colsum_partial_kernel<1>, grid, dim3(256), 0, st, dy, pre, g, R, C, rpb, work);
   else
     hipLaunchKernelGGL(act_bwd_colsum_partial_kernel<2>, grid, dim3(256), 0, st, dy, pre, g, R, C, rpb, work);
-  hipLaunchKernelGGL(colsum_fold_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, work, (int)nb, C, out, (int)accumulate);
+  hipLaunchKernelGGL(colsum_fold_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, work, (int)nb, C, out, (int)accumulate,
+                     0L, 0);
 }
-void launch_colsum_fold(const float* part, int P, int C, float* out, bool accumulate, hipStream_t st) {
-  hipLaunchKernelGGL(colsum_fold_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, part, P, C, out, (int)accumulate);
+// P > 256 rows (per-128-row GEMM partials, per-sequence attention partials: 1,024 at BERT b1024) fold in two levels:
+// groups of 32 rows in place, then the group results (36-48 blocks walking 1,024 rows took 29 us a fold)
+void launch_colsum_fold(float* part, int P, int C, float* out, bool accumulate, hipStream_t st) {
+  if (P > 256) {
+    constexpr int GS = 32;
+    const int G = (P + GS - 1) / GS;
+    hipLaunchKernelGGL(colsum_fold_kernel, dim3(cdiv(C, 64), G), dim3(256), 0, st, part, P, C, part, 0, (long)C, GS);
+    hipLaunchKernelGGL(colsum_fold_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, part, G, C, out, (int)accumulate,
+                       (long)GS * C, 0);
+    return;
+  }
+  hipLaunchKernelGGL(colsum_fold_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, part, P, C, out, (int)accumulate, 0L,
+                     0);
 }
 void launch_colsum(const uint16_t* x, long R, int C, float* work, float* out, bool accumulate, hipStream_t st) {
   const long nb = colsum_row_blocks(R);
   const long rpb = (R + nb - 1) / nb;
   dim3 g((unsigned)nb, (unsigned)((C / 8 + 31) / 32));
   hipLaunchKernelGGL(colsum_partial_kernel, g, dim3(256), 0, st, x, R, C, rpb, work);
-  hipLaunchKernelGGL(colsum_fold_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, work, (int)nb, C, out, (int)accumulate);
+  hipLaunchKernelGGL(colsum_fold_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, work, (int)nb, C, out, (int)accumulate,
+                     0L, 0);
 }
 
 }  // namespace k8s_amd

@@ -326,10 +326,6 @@ struct SkArgs {
   int sk;        // K splits of each remaining tile (1: none)
   float* slabs;  // [tail tiles][sk][256 x 256] fp32 partials, fragment-native order
   int* sync;     // [tail tiles][1 + sk]: arrival ticket, then one published flag per split (self-resetting)
-  // 4-wave kernel only: nsl sleeper blocks interleaved 8 / 8 into the first 2 nsl block ids (every XCD gets nsl / 8),
-  // each sleeping nslp x 8128 clocks -- half the CUs start their first tile late, so the two halves' store-bound
-  // epilogues stop coinciding (K8S_AMD_G4_STAGGER)
-  int nsl = 0, nslp = 0;
 };
 
 // Deterministic in-kernel split-K fix-up of one stream-K tile (cdna_hip_programming.md §5 "In-launch split-K
@@ -727,18 +723,7 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
 
   const int tiles_m = M >> 8, tiles_n = N >> 8;
   // whole tiles [0, SK.full), then the stream-K tail: (tile, split) pairs of K range kps (as gemm256r_kernel)
-  int bid = blockIdx.x;
-  if (SK.nsl > 0) {
-    if (bid < 2 * SK.nsl) {
-      if (((bid >> 3) & 1) == 0) {
-        for (int i = 0; i < SK.nslp; ++i) __builtin_amdgcn_s_sleep(127);
-        return;
-      }
-      bid = (bid >> 4) * 8 + (bid & 7);
-    } else {
-      bid -= SK.nsl;
-    }
-  }
+  const int bid = blockIdx.x;
   int wg, split = 0, sk_slot = -1;
   if (gridDim.y > 1) {  // tall-K split: the linear (tile, split) id remapped so a split's tiles share an XCD
     const int lam = g256r::xcd_remap(bid + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
@@ -1104,19 +1089,6 @@ static bool w4_ok(bool a_kmajor, bool b_kmajor, bool c_f32, int M, int N, int K,
   return splits > 1 ? tiles * splits >= 3L * planner_cus() / 4 : tiles >= planner_cus();
 }
 // K range per split of a tall-K split on the 4-wave kernel (whole 64-deep stages; the last split takes the rest)
-// K8S_AMD_G4_STAGGER = sleep loops of the sleeper blocks (SkArgs::nsl); applied to single-launch grids of >= 2 rounds
-static void w4_stagger(g256r::SkArgs& sk, int& blocks) {
-  static const int loops = [] {
-    const char* e = std::getenv("K8S_AMD_G4_STAGGER");
-    return e ? std::atoi(e) : 0;
-  }();
-  const int P = planner_cus();
-  if (loops <= 0 || blocks < 2 * P) return;
-  sk.nsl = (P / 2) & ~7;
-  sk.nslp = loops;
-  blocks += sk.nsl;
-}
-
 static int w4_split_kps(int K, int splits) { return (K / 64 + splits - 1) / splits * 64; }
 
 // Data gradient fused with the backward of the activation that produced the GEMM's input (see copy_out_x, ACT < 0):
@@ -1142,7 +1114,6 @@ void launch_gemm_w4_dact(const uint16_t* A, long lda, const uint16_t* B, long ld
     kps = plan.kps;
     blocks = plan.full + (tiles - plan.full) * plan.sk;
   }
-  w4_stagger(sk, blocks);
   hipLaunchKernelGGL((g4::gemm_w4_kernel<false, true, true>), dim3(blocks), dim3(g4::THREADS), 0, st, A, lda, B, ldb,
                      (void*)C, ldc, M, N, K, 1.f, kps, sk, 0, 0, nullptr, -act, const_cast<uint16_t*>(pre), 0L, part);
   launch_colsum_fold(part, M / 128, N, db, db_accumulate, st);
@@ -1255,7 +1226,6 @@ void launch_gemm256(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* 
       kps = plan.kps;
       blocks = plan.full + (tiles - plan.full) * plan.sk;
     }
-    if (ysplits == 1) w4_stagger(sk, blocks);
     const bool x = bias || act != 0 || pre || (accumulate && !c_f32);
     void* const cv = splits > 1 ? (void*)ws : C;
     const int acc = splits > 1 ? 0 : (accumulate ? 1 : 0);

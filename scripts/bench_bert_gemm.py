@@ -33,6 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--M", type=int, default=131072)
+    ap.add_argument("--blas", action="store_true", help="also plain forwards and hipBLASLt (torch.mm) arms")
     a = ap.parse_args()
     C = load()
     dev = torch.device("cuda")
@@ -46,9 +47,14 @@ def main():
         dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
         fwd = lambda: C.gemm(x, True, w, True, y, False, b, act, pre, False, 1.0, 1)  # noqa: E731
         dgr = lambda: C.gemm(g, True, w, False, dx, False, None, 0, None, False, 1.0, 1)  # noqa: E731
-        for form, fn in (("fwd", fwd), ("dgrad", dgr)):
+        cases = [("fwd", fwd), ("dgrad", dgr)]
+        if a.blas:  # the same products without epilogue extras, ours vs hipBLASLt (torch.mm)
+            cases += [("fwd_plain", lambda: C.gemm(x, True, w, True, y, False, None, 0, None, False, 1.0, 1)),
+                      ("fwd_plain_blas", lambda: torch.mm(x, w.t(), out=y)),
+                      ("dgrad_blas", lambda: torch.mm(g, w, out=dx))]
+        for form, fn in cases:
             us = min(timeit(fn, a.reps) for _ in range(3))
-            print(json.dumps({"layer": name, "form": form, "MNK": [M, N if form == "fwd" else K, K if form == "fwd" else N],
+            print(json.dumps({"layer": name, "form": form, "MNK": [M, K, N] if form.startswith("dgrad") else [M, N, K],
                               "us": round(us, 1), "tf": round(2.0 * M * N * K / us / 1e6),
                               "stagger": os.environ.get("K8S_AMD_G4_STAGGER", "0")}), flush=True)
         del x, w, g, y, pre, dx

@@ -5,7 +5,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r5_stagger; rm -rf $O; mkdir -p $O
-K8S_AMD_G4_STAGGER=4 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gemm256_gpu.py > $O/test.log 2>&1 || { tail -40 $O/test.log; exit 1; }
+K8S_AMD_G4_STAGGER=4 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gemm256_gpu.py tests/test_attention_gpu.py > $O/test.log 2>&1 || { tail -40 $O/test.log; exit 1; }
 tail -1 $O/test.log
 for v in 0 4 2 6 0 4; do
   K8S_AMD_G4_STAGGER=$v timeout -k 10 200 python -u scripts/bench_bert_gemm.py > $O/gemm_$v.jsonl 2>&1 || { tail -20 $O/gemm_$v.jsonl; exit 1; }

@@ -115,7 +115,8 @@ def test_attention_qkv_packed_matches_split(cuda, B, S, H, Hkv, D, causal, rope,
     assert rel(g, gr) < 3e-2
 
 
-@pytest.mark.parametrize("B,S,H,causal,lens", [(3, 128, 4, False, [128, 60, 0]), (2, 77, 3, True, None)])
+@pytest.mark.parametrize("B,S,H,causal,lens", [(3, 128, 4, False, [128, 60, 0]), (2, 77, 3, True, None),
+                                                (300, 16, 2, False, None)])  # > 256 partial rows: two-level fold
 def test_flash_bwd_packed_bias_grad(cuda, B, S, H, causal, lens):
     """One-block backward's column partials of the packed gradient (the QKV projection's bias gradient, folded over
     the batch) against the column sums of the dqkv it wrote."""
