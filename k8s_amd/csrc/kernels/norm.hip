@@ -14,6 +14,8 @@
 
 #include <type_traits>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -323,8 +325,10 @@ __global__ void __launch_bounds__(256) norm_colsum_kernel(const float* __restric
 // sums of dy * xhat, dy and dx (the upstream linear's bias gradient) in registers, and the block's 4 waves combine them
 // in LDS into one partial row [3][D]. The separate column kernel re-read dy and x (91 us per BERT call) and its
 // 64-row partials made a 2,048-row fold. CPL <= 2 (D <= 1024).
+// NS: register slots of the row prefetch (2: the next row's loads in flight during this row's math; 3: two rows ahead,
+// no residual gradient operand -- its slots would push D = 768 past 256 VGPRs)
 constexpr int NORM_FUSED_RPW = 32;
-template <int CPL, bool RMS>
+template <int CPL, bool RMS, int NS = 2>
 __global__ void __launch_bounds__(256) norm_bwd_fused_kernel(const uint16_t* __restrict__ dy,
                                                              const uint16_t* __restrict__ x,
                                                              const float* __restrict__ gamma,
@@ -348,7 +352,8 @@ __global__ void __launch_bounds__(256) norm_bwd_fused_kernel(const uint16_t* __r
       pg[c][j] = pb[c][j] = pd[c][j] = 0.f;
     }
   }
-  bf16x8_t gr[2][CPL], xr[2][CPL], rr[2][CPL];
+  bf16x8_t gr[NS][CPL], xr[NS][CPL], rr[NS == 2 ? NS : 1][CPL];
+  if constexpr (NS != 2) dres = nullptr;
   auto load = [&](auto slot_c, long row) {
     constexpr int sl = decltype(slot_c)::value;
 #pragma unroll
@@ -357,7 +362,9 @@ __global__ void __launch_bounds__(256) norm_bwd_fused_kernel(const uint16_t* __r
       const int cc = ch < nch ? ch : nch - 1;
       gr[sl][c] = *reinterpret_cast<const bf16x8_t*>(dy + row * D + cc * 8);
       xr[sl][c] = *reinterpret_cast<const bf16x8_t*>(x + row * D + cc * 8);
-      if (dres) rr[sl][c] = *reinterpret_cast<const bf16x8_t*>(dres + row * D + cc * 8);
+      if constexpr (NS == 2) {
+        if (dres) rr[sl][c] = *reinterpret_cast<const bf16x8_t*>(dres + row * D + cc * 8);
+      }
     }
   };
   auto step = [&](auto slot_c, long row) {
@@ -392,9 +399,11 @@ __global__ void __launch_bounds__(256) norm_bwd_fused_kernel(const uint16_t* __r
           pb[c][j] += g;
           pd[c][j] += o[j];
         }
-        if (dres) {
+        if constexpr (NS == 2) {
+          if (dres) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += bf2f((uint16_t)rr[sl][c][j]);
+            for (int j = 0; j < 8; ++j) o[j] += bf2f((uint16_t)rr[sl][c][j]);
+          }
         }
         store8(dx + row * D + ch * 8, o);
       }
@@ -402,15 +411,32 @@ __global__ void __launch_bounds__(256) norm_bwd_fused_kernel(const uint16_t* __r
   };
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
-  if (row0 < R) load(S0{}, row0);
-  for (int i = 0; i < RPW; i += 2) {  // two rows per trip: the register slots stay compile-time
-    const long r = row0 + i;
-    if (r >= R) break;
-    if (r + 1 < R) load(S1{}, r + 1);
-    step(S0{}, r);
-    if (r + 1 >= R) break;
-    if (i + 2 < RPW && r + 2 < R) load(S0{}, r + 2);
-    step(S1{}, r + 1);
+  using S2 = std::integral_constant<int, NS == 3 ? 2 : 0>;
+  const long rend = row0 + RPW < R ? row0 + RPW : R;
+  if constexpr (NS == 2) {
+    if (row0 < R) load(S0{}, row0);
+    for (int i = 0; i < RPW; i += 2) {  // two rows per trip: the register slots stay compile-time
+      const long r = row0 + i;
+      if (r >= R) break;
+      if (r + 1 < R) load(S1{}, r + 1);
+      step(S0{}, r);
+      if (r + 1 >= R) break;
+      if (i + 2 < RPW && r + 2 < R) load(S0{}, r + 2);
+      step(S1{}, r + 1);
+    }
+  } else {
+    if (row0 < rend) load(S0{}, row0);
+    if (row0 + 1 < rend) load(S1{}, row0 + 1);
+    for (long r = row0; r < rend; r += 3) {  // three rows per trip, each slot refilled three rows ahead
+      if (r + 2 < rend) load(S2{}, r + 2);
+      step(S0{}, r);
+      if (r + 1 >= rend) break;
+      if (r + 3 < rend) load(S0{}, r + 3);
+      step(S1{}, r + 1);
+      if (r + 2 >= rend) break;
+      if (r + 4 < rend) load(S1{}, r + 4);
+      step(S2{}, r + 2);
+    }
   }
   // the block's 4 waves -> one partial row [3][D] (sum dy * xhat | sum dy | sum dx)
   __shared__ float sh[NORM_WAVES][3][CPL * 512];
@@ -483,9 +509,17 @@ void launch_norm_bwd(bool rms, const uint16_t* dy, const uint16_t* x, const floa
   const int cpl = norm_cpl(D);
   if (norm_fused_ok(R, D)) {
     const int nbf = norm_fused_blocks(R);
+    static const bool deep = [] {  // K8S_AMD_NORM_PREFETCH=2 keeps the two-slot form
+      const char* e = std::getenv("K8S_AMD_NORM_PREFETCH");
+      return !(e && e[0] == '2');
+    }();
 #define NBF(C, RM)                                                                                                    \
-  hipLaunchKernelGGL((norm_bwd_fused_kernel<C, RM>), dim3(nbf), dim3(256), 0, st, dy, x, gamma, mean, rstd, dres, dx, \
-                     work, R, D, dsum ? 1 : 0)
+  if (deep && !dres)                                                                                                  \
+    hipLaunchKernelGGL((norm_bwd_fused_kernel<C, RM, 3>), dim3(nbf), dim3(256), 0, st, dy, x, gamma, mean, rstd, dres, \
+                       dx, work, R, D, dsum ? 1 : 0);                                                                 \
+  else                                                                                                                \
+    hipLaunchKernelGGL((norm_bwd_fused_kernel<C, RM, 2>), dim3(nbf), dim3(256), 0, st, dy, x, gamma, mean, rstd, dres, \
+                       dx, work, R, D, dsum ? 1 : 0)
     if (cpl == 1) {
       if (rms) NBF(1, true); else NBF(1, false);
     } else {
