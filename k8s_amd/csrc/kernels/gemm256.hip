@@ -1040,10 +1040,10 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
     const int idx = it * 64 + lane, lr = idx >> 4, ch = idx & 15;
     return *reinterpret_cast<const bf16x8_t*>(stg + lr * 256 + ((ch ^ (lr & 15)) << 4));
   };
-  if constexpr (!X) {
+  if (!X || (act == 0 && !accumulate && !pre)) {  // (a bias alone was added while staging: the plain copy)
 #pragma unroll 4
     for (int it = 0; it < 32; ++it) *reinterpret_cast<bf16x8_t*>(C + coff(it)) = staged(it);
-  } else {
+  } else if constexpr (X) {
     // the activation and the accumulate are compile-time in the loop body (copy_out<ACT, ACC>): with them as run-time
     // values the compiler branched per ELEMENT and serialised every GELU chain (exp -> add -> rcp -> mul, s_nop
     // between): BERT-base's FFN1 forward took 1013 us against 543 us for the bias-only QKV forward of 3/4 its FLOPs
