@@ -40,9 +40,14 @@ class BertConfig:
     # on the gathered masked positions only; 0 = head on every token with dense [B, S] labels
     max_predictions: int = 20
 
+    # the word table / tied decoder padded to whole 256-column tiles: the MLM decoder's three products (logits, their
+    # data and weight gradients) then run on the 4-wave 256 x 256 GEMM instead of the ring kernel's ragged-N path
+    # (the loss masks the padded logits: cross_entropy(valid=vocab_size))
+    vocab_pad: int = 256
+
     @property
     def padded_vocab(self) -> int:
-        return (self.vocab_size + 63) // 64 * 64
+        return (self.vocab_size + self.vocab_pad - 1) // self.vocab_pad * self.vocab_pad
 
 
 BERT_BASE = BertConfig()

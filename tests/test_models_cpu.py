@@ -12,9 +12,12 @@ from k8s_amd.parallel.flat import ParamStore
 def test_bert_base_parameter_count():
     s = ParamStore()
     bert.BertForPreTraining(s, bert.BERT_BASE)
-    # bert-base-uncased pretraining = 110,106,428 (+ 6 padded vocab rows / logits, + 62 padded NSP rows)
+    # bert-base-uncased pretraining = 110,106,428 (+ the padded vocab rows / logits -- 198 at 256-column padding --
+    # + 62 padded NSP rows)
     n = s.num_parameters()
-    pad = 6 * 768 + 6 + 62 * 768 + 62
+    pv = bert.BERT_BASE.padded_vocab - bert.BERT_BASE.vocab_size
+    assert bert.BERT_BASE.padded_vocab % 256 == 0 and 0 <= pv < 256
+    pad = pv * 768 + pv + 62 * 768 + 62
     assert n - pad == 110106428
 
 
