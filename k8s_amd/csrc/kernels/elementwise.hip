@@ -301,6 +301,11 @@ void launch_colsum_fold(float* part, int P, int C, float* out, bool accumulate, 
   hipLaunchKernelGGL(colsum_fold_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, part, P, C, out, (int)accumulate, 0L,
                      0);
 }
+// first level alone: rows [g gs, (g + 1) gs) of part summed into row g gs (a strided fold of the result follows)
+void launch_colsum_group(float* part, int P, int C, int gs, hipStream_t st) {
+  hipLaunchKernelGGL(colsum_fold_kernel, dim3(cdiv(C, 64), (P + gs - 1) / gs), dim3(256), 0, st, part, P, C, part, 0,
+                     (long)C, gs);
+}
 void launch_colsum(const uint16_t* x, long R, int C, float* work, float* out, bool accumulate, hipStream_t st) {
   const long nb = colsum_row_blocks(R);
   const long rpb = (R + nb - 1) / nb;

@@ -156,6 +156,8 @@ void launch_colsum(const uint16_t* x, long R, int C, float* work, float* out, bo
 // the fold of P partial rows of column sums (colsum_fold_kernel)
 // (P > 256: two levels, overwriting part)
 void launch_colsum_fold(float* part, int P, int C, float* out, bool accumulate, hipStream_t st);
+// the first level of that fold alone: the sum of rows [g gs, (g + 1) gs) written over row g gs
+void launch_colsum_group(float* part, int P, int C, int gs, hipStream_t st);
 // g = dy * act'(pre) (1 ReLU, pre = its output; 2 GELU(tanh), pre = the pre-activation) and out = column sums of g
 void launch_act_bwd_colsum(int act, const uint16_t* dy, const uint16_t* pre, uint16_t* g, long R, int C, float* work,
                            float* out, bool accumulate, hipStream_t st);

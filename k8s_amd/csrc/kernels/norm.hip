@@ -273,9 +273,10 @@ __global__ void __launch_bounds__(256) norm_bwd_param_kernel(const uint16_t* __r
 // fold partial rows: part [P][2][D] -> dgamma[D], dbeta[D]. Block = 32 columns x 8 row slices (coalesced
 // 128-B rows, 4 independent loads in flight per thread), LDS combine of the slices. P = R / 64 partial rows; a
 // thread-per-column serial loop here was latency-bound at ~260 us per call with ~1k partials.
+// (pstep: partial row p at part + p * pstep * 3 * D -- the group sums of a first-level fold, launch_colsum_group)
 __global__ void __launch_bounds__(256) norm_colsum_kernel(const float* __restrict__ part, int P, int D,
                                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                          float* __restrict__ dsum) {
+                                                          float* __restrict__ dsum, int pstep = 1) {
   __shared__ float sh[3][8][33];
   const int col = threadIdx.x & 31, sl = threadIdx.x >> 5;
   const int k = blockIdx.x * 32 + col;
@@ -286,9 +287,9 @@ __global__ void __launch_bounds__(256) norm_colsum_kernel(const float* __restric
       float av[4], bv[4], dv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        av[u] = part[((long)(p + 8 * u) * 3) * D + k];
-        bv[u] = part[((long)(p + 8 * u) * 3 + 1) * D + k];
-        dv[u] = dsum ? part[((long)(p + 8 * u) * 3 + 2) * D + k] : 0.f;
+        av[u] = part[((long)(p + 8 * u) * pstep * 3) * D + k];
+        bv[u] = part[((long)(p + 8 * u) * pstep * 3 + 1) * D + k];
+        dv[u] = dsum ? part[((long)(p + 8 * u) * pstep * 3 + 2) * D + k] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -298,9 +299,9 @@ __global__ void __launch_bounds__(256) norm_colsum_kernel(const float* __restric
       }
     }
     for (; p < P; p += 8) {
-      a += part[((long)p * 3) * D + k];
-      b += part[((long)p * 3 + 1) * D + k];
-      if (dsum) d += part[((long)p * 3 + 2) * D + k];
+      a += part[((long)p * pstep * 3) * D + k];
+      b += part[((long)p * pstep * 3 + 1) * D + k];
+      if (dsum) d += part[((long)p * pstep * 3 + 2) * D + k];
     }
   }
   sh[0][sl][col] = a;
@@ -526,8 +527,16 @@ void launch_norm_bwd(bool rms, const uint16_t* dy, const uint16_t* x, const floa
       if (rms) NBF(2, true); else NBF(2, false);
     }
 #undef NBF
-    hipLaunchKernelGGL(norm_colsum_kernel, dim3(cdiv(D, 32)), dim3(256), 0, st, work, nbf, D, dgamma,
-                       rms ? nullptr : dbeta, dsum);
+    // 1,024 partial rows at BERT b1024: folded in groups of 32 first (24 blocks walking them took 20 us a call)
+    constexpr int GS = 32;
+    if (nbf > 4 * GS) {
+      launch_colsum_group(work, nbf, 3 * D, GS, st);
+      hipLaunchKernelGGL(norm_colsum_kernel, dim3(cdiv(D, 32)), dim3(256), 0, st, work, (nbf + GS - 1) / GS, D,
+                         dgamma, rms ? nullptr : dbeta, dsum, GS);
+    } else {
+      hipLaunchKernelGGL(norm_colsum_kernel, dim3(cdiv(D, 32)), dim3(256), 0, st, work, nbf, D, dgamma,
+                         rms ? nullptr : dbeta, dsum, 1);
+    }
     return;
   }
   const dim3 g(cdiv(R, NORM_WAVES));
