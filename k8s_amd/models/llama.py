@@ -79,7 +79,8 @@ class LlamaLayer(nn.Module):
             hn, res = K.rms_norm(x, self.attn_norm, c.eps, residual=res)
         qkv = K.linear(hn, self.qkv)
         # rotary q/k, causal GQA flash attention and the packed QKV gradient in one op (no split/cat/copies)
-        o = attention_qkv(qkv, B, S, c.heads, c.kv_heads, d, causal=True, rope=(pos, table))
+        o = attention_qkv(qkv, B, S, c.heads, c.kv_heads, d, causal=True, rope=(pos, table),
+                          rope_in_place=True)  # qkv: this linear's output, read by nothing else
         a = K.linear(o.reshape(B * S, c.heads * d), self.o)
         hn, res = K.rms_norm(a, self.mlp_norm, c.eps, residual=res)
         gu = K.linear(hn, self.gate_up)

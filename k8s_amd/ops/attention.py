@@ -101,13 +101,14 @@ class _FlashQKV(torch.autograd.Function):
     copies on either pass."""
 
     @staticmethod
-    def forward(ctx, qkv, B, S, H, Hkv, D, causal, kv_lens, scale, pos, table, bias_link=None):
+    def forward(ctx, qkv, B, S, H, Hkv, D, causal, kv_lens, scale, pos, table, bias_link=None, rope_in_place=False):
         C = _load()
         if kv_lens is not None:
             kv_lens = kv_lens.to(device=qkv.device, dtype=torch.int32).contiguous()
         x = qkv.contiguous()
         if pos is not None:
-            x = x.clone() if x.data_ptr() == qkv.data_ptr() else x
+            if not rope_in_place:  # (in place: the caller's qkv is a temporary nothing else reads)
+                x = x.clone() if x.data_ptr() == qkv.data_ptr() else x
             C.rope_(x[:, : (H + Hkv) * D], pos, table, False)
         g = x.view(B, S, H + 2 * Hkv, D)
         q, k, v = g.narrow(2, 0, H), g.narrow(2, H, Hkv), g.narrow(2, H + Hkv, Hkv)
@@ -141,24 +142,27 @@ class _FlashQKV(torch.autograd.Function):
             bl.done = True
         if has_rope:
             C.rope_(dqkv[:, : (H + Hkv) * D], pos, table, True)
-        return (dqkv,) + (None,) * 11
+        return (dqkv,) + (None,) * 12
 
 
 def attention_qkv(qkv, B: int, S: int, heads: int, kv_heads: int, head_dim: int, causal: bool = False,
                   kv_lens: Optional[torch.Tensor] = None, rope: Optional[tuple] = None,
-                  scale: Optional[float] = None, bias_link=None):
+                  scale: Optional[float] = None, bias_link=None, rope_in_place: bool = False):
     """Self-attention of a packed QKV projection ``qkv`` [B*S, (heads + 2*kv_heads) * head_dim] (q heads, then k,
     then v); ``rope`` = (pos [B*S] int32, table) applies rotary embeddings to q and k. Returns o [B, S, heads, D].
     GPU bf16: one fused path (``_FlashQKV``); otherwise the split + ``attention`` reference composition.
     ``bias_link`` (``nn.BiasLink``, also given to the projection ``linear``): short sequences emit the projection's
-    bias gradient from the attention backward, and the linear skips its column-sum pass."""
+    bias gradient from the attention backward, and the linear skips its column-sum pass. ``rope_in_place``: rotate
+    q / k inside ``qkv`` itself instead of a copy (the caller's projection output is a temporary: Llama's 201 MB
+    per-layer clone at s4096 b4)."""
     D = head_dim
     scale = scale or 1.0 / math.sqrt(D)
     W = (heads + 2 * kv_heads) * D
     if qkv.is_cuda and qkv.dtype == torch.bfloat16 and D in (64, 128) and qkv.shape[-1] == W and \
             W % 8 == 0 and qkv.is_contiguous():
         pos, table = rope if rope is not None else (None, None)
-        return _FlashQKV.apply(qkv, B, S, heads, kv_heads, D, causal, kv_lens, scale, pos, table, bias_link)
+        return _FlashQKV.apply(qkv, B, S, heads, kv_heads, D, causal, kv_lens, scale, pos, table, bias_link,
+                               rope_in_place)
     q, k, v = qkv.split([heads * D, kv_heads * D, kv_heads * D], dim=-1)
     if rope is not None:
         from k8s_amd.ops import nn as _nn

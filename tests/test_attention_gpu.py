@@ -137,3 +137,27 @@ def test_flash_bwd_packed_bias_grad(cuda, B, S, H, causal, lens):
     C.flash_bwd(do, q, k, v, o, lse, causal, lens_t, 0.125, dqkv, db)
     ref = dqkv.float().sum(0)
     _close(db, ref, 2e-2, "db")
+
+
+def test_attention_qkv_rope_in_place_matches_copy(cuda):
+    """rope_in_place=True (the q / k columns of the projection output rotated where they are) gives the same output
+    and the same gradient at the projection's input as the copying form."""
+    from k8s_amd.ops import nn as K
+    from k8s_amd.ops.attention import attention_qkv
+
+    torch.manual_seed(9)
+    B, S, H, Hkv, D = 2, 256, 8, 2, 128
+    W = (H + 2 * Hkv) * D
+    base = (torch.randn(B * S, W, device=cuda) * 0.5).bfloat16()
+    pos = torch.arange(S, device=cuda, dtype=torch.int32).repeat(B)
+    table = K.rope_table(S, D, device=cuda)
+    outs = []
+    for in_place in (False, True):
+        leaf = base.clone().requires_grad_(True)
+        qkv = leaf * 1.0  # a non-leaf temporary, as a projection output is
+        o = attention_qkv(qkv, B, S, H, Hkv, D, causal=True, rope=(pos, table), rope_in_place=in_place)
+        go = torch.ones_like(o) * 0.01
+        (g,) = torch.autograd.grad(o, leaf, go)
+        outs.append((o.float(), g.float()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
