@@ -31,35 +31,18 @@ import warnings
 
 from k8s_amd.ops._ext import load as _load
 
-import os
 
 # (Round 2 built a BatchNorm-backward statistics epilogue for the data gradients -- the BN backward's reduction
 # pass computed in the dgrad that produces its input; it measured a net loss twice, 10.61k vs 11.00k img/s in round 2
 # and 12.02k vs 12.20k with only the long-K dgrads in round 3 (scripts/gpurun/env_ab.sh), and was removed.)
 
-STATS = {"hip_fwd": 0, "aten_fwd": 0, "hip_wgrad": 0, "aten_wgrad": 0, "hip_dgrad": 0, "aten_dgrad": 0,
-         "side_wgrad": 0}
+STATS = {"hip_fwd": 0, "aten_fwd": 0, "hip_wgrad": 0, "aten_wgrad": 0, "hip_dgrad": 0, "aten_dgrad": 0}
 
-# Weight gradients on a second HIP stream (ParamStore.grad_side_stream): each conv's dW kernel is forked off the
-# compute stream and overlaps the data gradient and BatchNorm backward passes that follow it (MFMA-bound next to
-# HBM-bound work). Read per call so tests can run both sides.
-def wgrad_side_enabled() -> bool:
-    return os.environ.get("K8S_AMD_WGRAD_STREAM", "0") == "1"
-
-
-def _wgrad_maybe_side(C_, gy, x, p, stride, padding, acc, xform=None):
-    """``_wgrad_hip`` into ``p``'s slot, on the store's side stream when enabled and the slot is written by this call
-    alone (first writer); the store holds the operands until the compute stream has waited for the kernel."""
-    out = p.grad.view(p.shape)
-    if not (wgrad_side_enabled() and not acc and p.uses == 1):
-        _wgrad_hip(C_, gy, x, out, stride, padding, acc, xform)
-        return
-    store = p.store
-    side = store.grad_side_stream(gy.device)
-    with torch.cuda.stream(side):
-        _wgrad_hip(C_, gy, x, out, stride, padding, acc, xform)
-    store.grad_side_issued(side, (gy, x, xform))
-    STATS["side_wgrad"] += 1
+# (Round 5 built weight gradients on a second HIP stream -- each conv's dW kernel forked off the compute stream to
+# overlap the data gradient and BatchNorm passes after it. The streams co-ran, but the HBM-bound kernels stretched:
+# +0.7 % at b1024, noise at the b3072 default (profiles/r05_wgrad_side_ab.md); its serial-vs-side gradient test then
+# failed intermittently on the GPU (1 in ~3 runs, one fixed 2e-3 difference: an unordered operand somewhere in the
+# fork / join), so it was removed rather than shipped off by default.)
 
 
 def _nchw(x):
@@ -231,7 +214,7 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, xform=None
     if hip and C % 8 == 0 and K % 8 == 0 and p is not None and p.grad.dtype == torch.float32:
         STATS["hip_wgrad"] += 1
         acc = p.written
-        _wgrad_maybe_side(C_, gy, x, p, stride, padding, acc, xform)
+        _wgrad_hip(C_, gy, x, p.grad.view(p.shape), stride, padding, acc, xform)
         if acc:
             p.store._notify(p)
         else:

@@ -83,8 +83,7 @@ class _FlatOptimizer:
     def _clip(self, scale: float, ranges, stats_reduce: Optional[Callable] = None) -> Optional[torch.Tensor]:
         """Device-side clip factor from the gradient norm over ``ranges``; ``stats_reduce`` (e.g. an
         all-reduce) combines the [sum of squares, non-finite count] partials of a sharded update. (Also the step's
-        first read of the gradients: weight gradients still on the side stream are joined here.)"""
-        self.store.join_grad_side()
+        first read of the gradients.)"""
         if not self.max_grad_norm:
             return None
         g = self.store.grad

@@ -151,7 +151,6 @@ class GradReducer:
         if b.launched:
             return
         b.launched = True
-        self.store.order_after_grad_side()  # weight gradients still running on the side stream (ops/conv.py)
         t = self.store.grad[b.lo:b.hi]
         if self.comm_dtype == torch.bfloat16:
             length = b.hi - b.lo
@@ -185,7 +184,6 @@ class GradReducer:
 
     def finish(self):
         """Zero never-used gradients, flush remaining buckets, order the current stream after RCCL."""
-        self.store.join_grad_side()
         for b in self.buckets:
             if b.pending > 0:
                 for p in b.params:

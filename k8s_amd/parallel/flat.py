@@ -23,7 +23,6 @@ whose gradients they deposit directly.
 from __future__ import annotations
 
 import math
-import os
 from typing import Callable, Dict, List, Optional
 
 import torch
@@ -145,11 +144,6 @@ class ParamStore:
         # in-flight pull collectives (bucket index -> async work) and param index -> its buckets (parallel/ps.py)
         self.pending: Dict[int, object] = {}
         self.pending_of: Dict[int, list] = {}
-        # side stream of the weight-gradient kernels that overlap the rest of backward (ops/conv.py), per device,
-        # and the stream to join it into when this backward ends (None: nothing outstanding)
-        self._gside: Dict[int, object] = {}
-        self._gside_join = None
-        self._gside_live: list = []  # (event on the side stream, operands its kernels read), oldest first
 
     # ---- construction
     def new(self, name: str, shape, init: Callable, decay: bool = True, lowp: bool = True) -> Param:
@@ -221,7 +215,6 @@ class ParamStore:
 
     # ---- gradient plumbing
     def begin_step(self):
-        self.join_grad_side()
         for p in self.params:
             p.written = False
         arena = self.__dict__.get("zero_arena")
@@ -251,61 +244,6 @@ class ParamStore:
     def _notify(self, p: Param):
         for h in self.hooks:
             h(p)
-
-    # ---- weight gradients on a side stream
-    # A convolution's weight gradient (MFMA-bound) does not feed anything else in backward, while the BatchNorm passes
-    # and data gradients that follow it are HBM-bound chains: issued on a second HIP stream, the weight gradient's
-    # workgroups fill the CUs the streaming passes leave idle. Every consumer of ``grad`` orders itself after the side
-    # stream: the collectives launched mid-backward (``order_after_grad_side``) and everything after backward (the
-    # join queued as an autograd final callback, i.e. before ``loss.backward()`` returns).
-    # Operand lifetime: the side kernels' inputs (allocated on the compute stream) are held here, not recorded on the
-    # side stream -- record_stream makes the allocator keep a freed block until the HOST sees the side event complete,
-    # and with the host a step ahead of the GPU every freed activation stayed unusable: the next forward re-allocated
-    # ~100 GB at batch 3072 and the allocator's out-of-memory path (free cache + sync) ran every step, 15x slower
-    # (profiles/r05_wgrad_side_ab.md). Instead the compute stream waits for the side kernels GSIDE_DEPTH forks later
-    # and only then drops the references, so a reused block is ordered after its last side reader on the device.
-    GSIDE_DEPTH = 2
-
-    def grad_side_stream(self, device):
-        """The side stream for a parameter-gradient kernel about to be issued, forked from the current stream now;
-        report the issued kernels' operands with ``grad_side_issued``."""
-        device = torch.device(device)
-        s = self._gside.get(device.index)
-        if s is None:
-            s = self._gside[device.index] = torch.cuda.Stream(
-                device, priority=int(os.environ.get("K8S_AMD_WGRAD_PRIO", "0")))
-        main = torch.cuda.current_stream(device)
-        while len(self._gside_live) >= self.GSIDE_DEPTH:
-            ev, _operands = self._gside_live.pop(0)
-            main.wait_event(ev)  # the operands are released after this wait is on the compute stream
-        s.wait_stream(main)
-        if self._gside_join is None:
-            self._gside_join = (main, s)
-            try:
-                torch.autograd.Variable._execution_engine.queue_callback(self.join_grad_side)
-            except RuntimeError:  # not inside an autograd backward: the caller's next join point is ours
-                pass
-        return s
-
-    def grad_side_issued(self, s, operands):
-        """Kernels reading ``operands`` were issued on side stream ``s``: keep the tensors alive until the compute
-        stream has waited for them."""
-        ev = torch.cuda.Event()
-        ev.record(s)
-        self._gside_live.append((ev, operands))
-
-    def join_grad_side(self):
-        """Order the stream that forked the side stream after everything issued on it (end of backward)."""
-        j, self._gside_join = self._gside_join, None
-        if j is not None:
-            j[0].wait_stream(j[1])
-        self._gside_live = []  # after the wait: the operands' blocks are reused in order behind it
-
-    def order_after_grad_side(self):
-        """A collective about to read ``grad`` mid-backward: the current stream waits for the side stream's work so
-        far (device-side; the host does not block)."""
-        if self._gside_join is not None:
-            torch.cuda.current_stream(self.grad.device).wait_stream(self._gside_join[1])
 
     def zero_unwritten(self):
         for p in self.params:

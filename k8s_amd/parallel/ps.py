@@ -163,7 +163,6 @@ class ShardedParameterService:
     def _push(self, b: _Range):
         if self.world == 1:
             return
-        self.store.order_after_grad_side()  # weight gradients still running on the side stream (ops/conv.py)
         g = self.store.grad[b.lo:b.hi]
         if self.comm_dtype == torch.bfloat16:
             send = cast_bf16(g)
@@ -290,7 +289,6 @@ class ShardedParameterService:
     def step(self, lr: Optional[float] = None):
         """Finish the pushes, update the owned shards, pull the new weights."""
         s = self.store
-        s.join_grad_side()
         for b in self.buckets:  # parameters never used this step contribute zero gradient
             if b.pending > 0:
                 for p in b.params:
