@@ -627,26 +627,38 @@ __device__ __forceinline__ void gelu_grad_mul8(float (&f)[8], const float (&xs)[
 // per-column sums of the stored bf16 C (the producing linear's bias gradient) -- this wave's 128 columns summed over
 // its 128 rows into one partial row of `cpart` (folded by colsum_fold_kernel). `pre` is read a group ahead, as the
 // accumulate's old C.
+// ACT = -3: SwiGLU backward (Llama's down-projection data gradient): C / pre are the [M][2F] dgu / gu buffers
+// (ldc = 2F), the GEMM's N = F columns are the gate half; with d = this data gradient, g = gate (pre at off), u = up
+// (pre at off + fo): dgate = d u silu'(g) at off, dup = d silu(g) at off + fo -- elementwise.hip's swiglu_bwd_kernel
+// formula on the same bf16 inputs, so the fused result is bit-identical to the two-pass one.
 template <int ACT, bool ACC, class Off, class Stg>
 __device__ __forceinline__ void copy_out_x(uint16_t* __restrict__ C, uint16_t* __restrict__ pre, const char* stg,
-                                           const Off& coff, const Stg& staged, float* __restrict__ cpart = nullptr) {
+                                           const Off& coff, const Stg& staged, float* __restrict__ cpart = nullptr,
+                                           long fo = 0) {
   (void)stg;
   static_assert(!(ACT < 0 && ACC), "activation backward without accumulate");
   constexpr bool RD = ACC || ACT < 0;  // a bf16 operand per chunk read a group ahead (old C, or pre)
-  bf16x8_t oldc[2][4];
+  constexpr bool SW = ACT == -3;
+  bf16x8_t oldc[2][4], oldu[SW ? 2 : 1][SW ? 4 : 1];
   const uint16_t* rsrc = ACT < 0 ? pre : C;
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if constexpr (RD) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) oldc[0][q] = *reinterpret_cast<const bf16x8_t*>(rsrc + coff(q));
+    for (int q = 0; q < 4; ++q) {
+      oldc[0][q] = *reinterpret_cast<const bf16x8_t*>(rsrc + coff(q));
+      if constexpr (SW) oldu[0][q] = *reinterpret_cast<const bf16x8_t*>(rsrc + coff(q) + fo);
+    }
   }
 #pragma unroll
   for (int grp = 0; grp < 8; ++grp) {
     if constexpr (RD) {
       if (grp + 1 < 8) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < 4; ++q) {
           oldc[(grp + 1) & 1][q] = *reinterpret_cast<const bf16x8_t*>(rsrc + coff((grp + 1) * 4 + q));
+          if constexpr (SW)
+            oldu[(grp + 1) & 1][q] = *reinterpret_cast<const bf16x8_t*>(rsrc + coff((grp + 1) * 4 + q) + fo);
+        }
       }
     }
 #pragma unroll
@@ -654,7 +666,20 @@ __device__ __forceinline__ void copy_out_x(uint16_t* __restrict__ C, uint16_t* _
       const int it = grp * 4 + q;
       const long off = coff(it);
       bf16x8_t v = staged(it);
-      if constexpr (ACT < 0) {
+      if constexpr (SW) {
+        float dg[8], du[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float gg = bf2f((uint16_t)oldc[grp & 1][q][r]), uu = bf2f((uint16_t)oldu[grp & 1][q][r]);
+          const float d = bf2f((uint16_t)v[r]);
+          const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-gg));
+          du[r] = d * (gg * sg);
+          dg[r] = d * uu * (sg * (1.f + gg * (1.f - sg)));
+        }
+        *reinterpret_cast<bf16x8_t*>(C + off) = pack_bf16x8(dg);
+        *reinterpret_cast<bf16x8_t*>(C + off + fo) = pack_bf16x8(du);
+        continue;
+      } else if constexpr (ACT < 0) {
         float f[8], x[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
@@ -693,7 +718,7 @@ __device__ __forceinline__ void copy_out_x(uint16_t* __restrict__ C, uint16_t* _
       *reinterpret_cast<bf16x8_t*>(C + off) = v;
     }
   }
-  if constexpr (ACT < 0) {
+  if constexpr (ACT < 0 && !SW) {
     // lanes l, l ^ 16, l ^ 32, l ^ 48 hold the same 8 columns (chunk l & 15) of different rows
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
@@ -1049,9 +1074,13 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
     // between): BERT-base's FFN1 forward took 1013 us against 543 us for the bias-only QKV forward of 3/4 its FLOPs
     if (act < 0) {  // activation backward (data-gradient form only): a partial row of column sums per (tile, wave row)
       if constexpr (!AMN && BMN) {
-        float* const cp = cpart + (long)((m0 >> 8) * 2 + wr) * N + n0 + wc * 128;
-        if (act == -2) copy_out_x<-2, false>(C, pre, stg, coff, staged, cp);
-        else copy_out_x<-1, false>(C, pre, stg, coff, staged, cp);
+        if (act == -3) {  // SwiGLU backward: no column sums; the up half `slab` columns to the right
+          copy_out_x<-3, false>(C, pre, stg, coff, staged, nullptr, slab);
+        } else {
+          float* const cp = cpart + (long)((m0 >> 8) * 2 + wr) * N + n0 + wc * 128;
+          if (act == -2) copy_out_x<-2, false>(C, pre, stg, coff, staged, cp);
+          else copy_out_x<-1, false>(C, pre, stg, coff, staged, cp);
+        }
       }
     } else if (act == 2) {
       if (accumulate) copy_out_x<2, true>(C, pre, stg, coff, staged); else copy_out_x<2, false>(C, pre, stg, coff, staged);
@@ -1117,6 +1146,31 @@ void launch_gemm_w4_dact(const uint16_t* A, long lda, const uint16_t* B, long ld
   hipLaunchKernelGGL((g4::gemm_w4_kernel<false, true, true>), dim3(blocks), dim3(g4::THREADS), 0, st, A, lda, B, ldb,
                      (void*)C, ldc, M, N, K, 1.f, kps, sk, 0, 0, nullptr, -act, const_cast<uint16_t*>(pre), 0L, part);
   launch_colsum_fold(part, M / 128, N, db, db_accumulate, st);
+}
+
+// Llama's down-projection data gradient fused with the SwiGLU backward (copy_out_x ACT = -3): dgu [M][2F] from
+// g [M][K] (K-major) . w [K][F] (MN-major) and gu [M][2F]; the 4-wave kernel's whole-tile shapes (N = F).
+bool gemm_w4_swiglu_ok(int M, int F, int K, long lda, long ldb) {
+  return gemm_w4_dact_ok(M, F, K, lda, ldb, 2L * F);
+}
+void launch_gemm_w4_swiglu_bwd(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* dgu,
+                               const uint16_t* gu, int M, int F, int K, float* sk_slabs, int* sk_sync, hipStream_t st) {
+  if (!gemm_w4_swiglu_ok(M, F, K, lda, ldb))
+    throw std::runtime_error("gemm_w4_swiglu_bwd: shape outside the 4-wave kernel's contract");
+  Gemm256Plan plan = gemm256_plan(M, F, K);
+  if (!sk_slabs || !sk_sync) plan.sk = 1;
+  const int tiles = (M / 256) * (F / 256);
+  g256r::SkArgs sk{tiles, 1, nullptr, nullptr};
+  int blocks = tiles, kps = K;
+  if (plan.sk > 1) {
+    sk = g256r::SkArgs{plan.full, plan.sk, sk_slabs, sk_sync};
+    kps = plan.kps;
+    blocks = plan.full + (tiles - plan.full) * plan.sk;
+  }
+  // C = dgu (row stride 2F, gate half at column 0), pre = gu, slab = F: the up half's column offset
+  hipLaunchKernelGGL((g4::gemm_w4_kernel<false, true, true>), dim3(blocks), dim3(g4::THREADS), 0, st, A, lda, B, ldb,
+                     (void*)dgu, 2L * F, M, F, K, 1.f, kps, sk, 0, 0, nullptr, -3, const_cast<uint16_t*>(gu), (long)F,
+                     nullptr);
 }
 
 // Stream-K tail plan for a grid of 256 x 256 tiles on P = planner_cus() CUs (one block per CU; 256 on MI355X): with

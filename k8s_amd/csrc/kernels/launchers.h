@@ -106,6 +106,10 @@ long gemm_w4_dact_part_floats(int M, int N);
 void launch_gemm_w4_dact(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* C, long ldc, int M, int N,
                          int K, const uint16_t* pre, int act, float* part, float* db, bool db_accumulate,
                          float* sk_slabs, int* sk_sync, hipStream_t st);
+// the down-projection data gradient fused with the SwiGLU backward: dgu [M][2F] (gemm256.hip copy_out_x ACT = -3)
+bool gemm_w4_swiglu_ok(int M, int F, int K, long lda, long ldb);
+void launch_gemm_w4_swiglu_bwd(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* dgu,
+                               const uint16_t* gu, int M, int F, int K, float* sk_slabs, int* sk_sync, hipStream_t st);
 // stream-K tail plan (gemm256.hip): tiles [full, tiles) are split sk ways along K (sk == 1: none), kps deep each
 struct Gemm256Plan {
   int tiles, full, sk, kps;

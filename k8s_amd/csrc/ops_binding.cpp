@@ -557,6 +557,33 @@ Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tens
 
 // dx = (g . W) * act'(pre) and db (+)= column sums of dx: the data gradient of a linear whose input is the output of
 // an activation (1 ReLU: pre = the ReLU output, 2 GELU: the pre-activation), fused with that activation's backward and
+// Llama's down-projection data gradient fused with the SwiGLU backward: dgu [M, 2F] = swiglu_bwd(gu, g . w),
+// g [M, K] bf16, w [K, F] bf16 (the down weight [out, in], read MN-major), gu [M, 2F] bf16 (gate | up).
+bool gemm_swiglu_bwd_ok(int64_t M, int64_t F, int64_t K) {
+  return k8s_amd::gemm_w4_swiglu_ok((int)M, (int)F, (int)K, K, F);
+}
+Tensor gemm_swiglu_bwd(Tensor g, Tensor w, Tensor gu) {
+  check_bf16_operand(g, "g");
+  check_bf16_operand(w, "w");
+  check_bf16_operand(gu, "gu");
+  const long M = g.size(0), K = g.size(1), F = w.size(1);
+  TORCH_CHECK(w.size(0) == K, "g [M, K] . w [K, F]");
+  TORCH_CHECK(gu.is_contiguous() && gu.size(0) == M && gu.size(1) == 2 * F, "gu must be a contiguous [M, 2F]");
+  TORCH_CHECK(k8s_amd::gemm_w4_swiglu_ok((int)M, (int)F, (int)K, g.stride(0), w.stride(0)),
+              "gemm_swiglu_bwd: shape outside the 4-wave kernel's contract");
+  Tensor dgu = torch::empty({M, 2 * F}, g.options());
+  const k8s_amd::Gemm256Plan plan = k8s_amd::gemm256_plan((int)M, (int)F, (int)K);
+  Tensor slabs;
+  int* sync = nullptr;
+  if (plan.sk > 1) {
+    slabs = torch::empty({k8s_amd::gemm256_sk_slab_floats(plan)}, g.options().dtype(at::kFloat));
+    sync = sk_sync_words(k8s_amd::gemm256_sk_sync_ints(plan), g.device());
+  }
+  k8s_amd::launch_gemm_w4_swiglu_bwd(cbf(g), g.stride(0), cbf(w), w.stride(0), bf(dgu), cbf(gu), (int)M, (int)F,
+                                     (int)K, sync ? f32(slabs) : nullptr, sync, cur_stream());
+  return dgu;
+}
+
 // the producing linear's bias gradient in the 4-wave GEMM's epilogue (gemm256.hip copy_out_x, ACT < 0).
 // g [M, N_out] bf16, w [N_out, K_in] bf16 (read MN-major), pre [M, K_in] bf16, db fp32 [K_in].
 bool gemm_dact_ok(int64_t M, int64_t N, int64_t K) { return k8s_amd::gemm_w4_dact_ok((int)M, (int)N, (int)K, K, N, N); }
@@ -1108,6 +1135,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_dact", &gemm_dact, "linear data gradient fused with the input activation's backward and bias gradient",
         py::arg("g"), py::arg("w"), py::arg("pre"), py::arg("act"), py::arg("db"), py::arg("db_accumulate"));
   m.def("gemm_dact_ok", &gemm_dact_ok, py::arg("M"), py::arg("N"), py::arg("K"));
+  m.def("gemm_swiglu_bwd", &gemm_swiglu_bwd, "down-projection data gradient fused with the SwiGLU backward (dgu)",
+        py::arg("g"), py::arg("w"), py::arg("gu"));
+  m.def("gemm_swiglu_bwd_ok", &gemm_swiglu_bwd_ok, py::arg("M"), py::arg("F"), py::arg("K"));
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
         py::arg("out_f32"), py::arg("bias"), py::arg("act"), py::arg("stats"),
         py::arg("xform") = py::none());

@@ -84,7 +84,8 @@ class LlamaLayer(nn.Module):
         a = K.linear(o.reshape(B * S, c.heads * d), self.o)
         hn, res = K.rms_norm(a, self.mlp_norm, c.eps, residual=res)
         gu = K.linear(hn, self.gate_up)
-        f = K.linear(K.swiglu(gu), self.down)
+        sl = K.SwiGLULink()  # the SwiGLU backward inside the down projection's data gradient
+        f = K.linear(K.swiglu(gu, link=sl), self.down, swiglu_in=sl)
         return f, res
 
 

@@ -117,6 +117,15 @@ def dact_ok(x, w, dx_addend=None) -> bool:
             and bool(_load().gemm_dact_ok(M, K, N)))
 
 
+def swiglu_ok(x, w, dx_addend=None) -> bool:
+    """Whether a linear whose input is a SwiGLU output can return the SwiGLU's input gradient (dgu) from its data
+    gradient's epilogue (``linear_bwd`` ``dx_swiglu``): GPU bf16, the 4-wave kernel's whole-tile shapes."""
+    M, F = x.shape
+    K = w.shape[0]
+    return (dx_addend is None and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and bool(_load().gemm_swiglu_bwd_ok(M, F, K)))
+
+
 def _dgrad_act(g, w, dx_act):
     """dx = (g . w) * act'(pre) with the producing linear's bias gradient (column sums of dx) deposited into its flat
     slot -- ``dx_act`` = (pre, act, pb, store) -- in one 4-wave GEMM launch (+ the column-sum fold)."""
@@ -132,14 +141,16 @@ def _dgrad_act(g, w, dx_act):
     return dx
 
 
-def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True, dx_addend=None, pb=None, dx_act=None):
+def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True, dx_addend=None, pb=None, dx_act=None,
+               dx_swiglu=None):
     """dx and the parameter gradient. With (pw, store) on GPU the weight gradient is written
     (or accumulated) straight into the flat fp32 gradient slot; returns (dx, dw_or_None, db).
     ``dx_addend`` (bf16, x's shape): another gradient contribution of x, accumulated in the dgrad epilogue (it is
     overwritten and returned as dx). With ``pb`` the bias gradient goes straight into its flat slot on first use
     (db is then returned as None). ``dx_act`` = (pre, act, producer bias param, its store): x is the output of that
     activation and dx is returned already through its backward, the producer's bias gradient deposited
-    (``dact_ok`` must hold)."""
+    (``dact_ok`` must hold). ``dx_swiglu`` = gu: x = swiglu(gu), and the gradient of gu ([M, 2F]) is returned in
+    dx's place (``swiglu_ok`` must hold)."""
     M, K = x.shape
     N = w.shape[0]
     db = None
@@ -183,6 +194,8 @@ def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True, dx_adden
         # dgrad reduces over N; a ragged N (e.g. the 1000-class head) is masked by the kernel's K tail (zeros)
         if dx_act is not None:
             dx = _dgrad_act(g, w, dx_act)
+        elif dx_swiglu is not None:
+            dx = _load().gemm_swiglu_bwd(g, w, dx_swiglu.contiguous())
         else:
             dx = mm(g, w, True, False, out=dx_addend if acc else None, accumulate=acc)
         if dx_addend is not None and not acc:

@@ -81,6 +81,17 @@ class ActLink:
         self.saved, self.act, self.pb, self.done = None, None, None, False
 
 
+class SwiGLULink:
+    """Joins ``swiglu(gu, link=l)`` to the linear that reads its output (``linear(y, W, swiglu_in=l)``, Llama's down
+    projection): that linear's data gradient takes the SwiGLU backward in its epilogue and produces the gradient of gu
+    directly (gemm256.hip copy_out_x ACT = -3, ``gemm.swiglu_ok`` shapes), so neither the [T, F] gradient of the
+    SwiGLU output nor the separate SwiGLU-backward pass over gu exists."""
+    __slots__ = ("saved", "dgu")
+
+    def __init__(self):
+        self.saved, self.dgu = None, None
+
+
 class MaskedGrad:
     """A residual gradient handed over unmaterialised: ``dy`` masked by the packed 1-bit ReLU ``mask`` of the BN
     forward (bit j of byte e = element 8e + j). The 1x1 dgrad that receives it reads the pair in its epilogue
@@ -482,7 +493,8 @@ def _gemm():
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, anchor, pw, pb, act, grad_link=None, bias_link=None, act_link=None, act_in=None):
+    def forward(ctx, x, anchor, pw, pb, act, grad_link=None, bias_link=None, act_link=None, act_in=None,
+                swiglu_in=None):
         g = _gemm()
         w = pw.weight if x.dtype == pw.weight.dtype else pw.master.to(x.dtype)
         x2 = x.reshape(-1, x.shape[-1])
@@ -500,6 +512,7 @@ class _Linear(torch.autograd.Function):
         if ctx.act_link is not None:
             act_link.saved, act_link.act, act_link.pb, act_link.done = pre, act, pb, False
         ctx.act_in = act_in
+        ctx.swiglu_in = swiglu_in
         return y.reshape(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -523,31 +536,44 @@ class _Linear(torch.autograd.Function):
         li = ctx.act_in
         if li is not None and li.saved is not None and g.dact_ok(x2, w, addend):
             dx_act = (li.saved, li.act, li.pb, li.pb.store)
+        sl, dx_swiglu = ctx.swiglu_in, None
+        if dx_act is None and sl is not None and sl.saved is not None and g.swiglu_ok(x2, w, addend):
+            dx_swiglu = sl.saved
         dx, dw, db = g.linear_bwd(gy2, x2, w, pre, act, pw=pw, store=pw.store,
-                                  need_db=pb is not None and not db_done, dx_addend=addend, pb=pb, dx_act=dx_act)
+                                  need_db=pb is not None and not db_done, dx_addend=addend, pb=pb, dx_act=dx_act,
+                                  dx_swiglu=dx_swiglu)
         if dx_act is not None:
             li.done, li.saved = True, None
+        if dx_swiglu is not None:  # the SwiGLU's backward returns dgu; x's own gradient is never formed
+            sl.dgu, sl.saved = dx, None
+            dx = dx.new_zeros(()).expand(ctx.xshape)  # (stride 0: never materialised, ignored by the SwiGLU node)
         if dw is not None:
             pw.store.deposit(pw, dw)
         if pb is not None and db is not None:  # None: written straight into its slot
             pb.store.deposit(pb, db)
         if link is not None and addend is None:  # ran first: hand dx to the norm backward, which forms the sum
             link.grad = dx.reshape(ctx.xshape)
-            return (None,) * 9
-        return (dx.reshape(ctx.xshape),) + (None,) * 8
+            return (None,) * 10
+        return (dx.reshape(ctx.xshape),) + (None,) * 9
 
 
 # BERT's FFN1 -> FFN2 activation backward fused into FFN2's data gradient (ActLink); tests switch it off to compare
 ACT_FUSE = True
+# Llama's SwiGLU backward fused into the down projection's data gradient (SwiGLULink); likewise (and
+# K8S_AMD_SWIGLU_FUSE=0 for whole-run A/Bs)
+SWIGLU_FUSE = os.environ.get("K8S_AMD_SWIGLU_FUSE", "1") != "0"
 
 
-def linear(x, pw, pb=None, act: Optional[str] = None, grad_link=None, bias_link=None, act_link=None, act_in=None):
+def linear(x, pw, pb=None, act: Optional[str] = None, grad_link=None, bias_link=None, act_link=None, act_in=None,
+           swiglu_in=None):
     """y = act(x @ W^T + b); W [out, in] bf16 from the flat store. ``grad_link``: see ``layer_norm``;
     ``bias_link``: see ``BiasLink``; ``act_link`` (on the producer, with ``act``) / ``act_in`` (on the consumer):
     see ``ActLink``."""
     if not ACT_FUSE:
         act_link = act_in = None
-    return _Linear.apply(x, pw.store.anchor, pw, pb, act, grad_link, bias_link, act_link, act_in)
+    if not SWIGLU_FUSE:
+        swiglu_in = None
+    return _Linear.apply(x, pw.store.anchor, pw, pb, act, grad_link, bias_link, act_link, act_in, swiglu_in)
 
 
 # =========================================================================== embedding
@@ -821,7 +847,7 @@ def global_avg_pool_nhwc(x):
 # =========================================================================== transformer elementwise (K9)
 class _SwiGLU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, gu):
+    def forward(ctx, gu, link=None):
         gu = gu.contiguous()
         F2 = gu.shape[-1] // 2
         if _gpu(gu) and gu.dtype == torch.bfloat16 and F2 % 8 == 0:
@@ -830,24 +856,33 @@ class _SwiGLU(torch.autograd.Function):
             g, u = gu.float().split(F2, -1)
             y = (torch.nn.functional.silu(g) * u).to(gu.dtype)
         ctx.save_for_backward(gu)
+        ctx.link = link
+        if link is not None:
+            link.saved, link.dgu = gu.reshape(-1, 2 * F2), None
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (gu,) = ctx.saved_tensors
+        link = ctx.link
+        if link is not None and link.dgu is not None:  # formed by the consuming linear's data gradient
+            dgu, link.dgu, link.saved = link.dgu, None, None
+            return dgu.reshape(gu.shape), None
+        if link is not None:
+            link.saved = None
         F2 = gu.shape[-1] // 2
         dy = dy.contiguous()
         if _gpu(gu) and gu.dtype == torch.bfloat16 and F2 % 8 == 0:
-            return _C().swiglu_bwd(gu, dy)
+            return _C().swiglu_bwd(gu, dy), None
         g, u = gu.float().split(F2, -1)
         s = torch.sigmoid(g)
         d = dy.float()
-        return torch.cat([d * u * s * (1 + g * (1 - s)), d * g * s], -1).to(gu.dtype)
+        return torch.cat([d * u * s * (1 + g * (1 - s)), d * g * s], -1).to(gu.dtype), None
 
 
-def swiglu(gu):
-    """silu(gate) * up over a fused [.., 2F] gate|up projection."""
-    return _SwiGLU.apply(gu)
+def swiglu(gu, link=None):
+    """silu(gate) * up over a fused [.., 2F] gate|up projection. ``link``: see ``SwiGLULink``."""
+    return _SwiGLU.apply(gu, link if SWIGLU_FUSE else None)
 
 
 def rope_table(max_pos: int, dim: int, theta: float = 10000.0, device=None) -> torch.Tensor:

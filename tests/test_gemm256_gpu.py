@@ -358,3 +358,25 @@ def test_linear_act_link_matches_unfused(cuda):
             K.ACT_FUSE = True
     for a, b, name in zip(grads[True], grads[False], ("x", "w1", "b1", "w2", "b2")):
         assert _rel(a, b) < 1e-3, name
+
+
+def test_gemm_swiglu_bwd_matches_two_pass():
+    """The down projection's data gradient with the SwiGLU backward in its epilogue (dgu [M, 2F] from g . w and gu)
+    against the two-pass form on the same kernels (bit-identical: same accumulators, same bf16 rounding, the SwiGLU
+    kernel's formula) and against an fp32 reference."""
+    torch.manual_seed(4)
+    C = _C()
+    M, F, K = 4096, 4096, 512
+    assert C.gemm_swiglu_bwd_ok(M, F, K)
+    g = (torch.randn(M, K, device="cuda") * 0.5).bfloat16()
+    w = (torch.randn(K, F, device="cuda") * 0.05).bfloat16()
+    gu = torch.randn(M, 2 * F, device="cuda").bfloat16()
+    dgu = C.gemm_swiglu_bwd(g, w, gu)
+    dy = C.gemm(g, True, w, False, None, False, None, 0, None, False, 1.0, 1)
+    two = C.swiglu_bwd(gu, dy)
+    assert torch.equal(dgu, two)
+    gg, uu = gu.float().split(F, -1)
+    s = torch.sigmoid(gg)
+    d = g.float() @ w.float()
+    ref = torch.cat([d * uu * s * (1 + gg * (1 - s)), d * gg * s], -1)
+    assert _rel(dgu, ref) < 2e-2

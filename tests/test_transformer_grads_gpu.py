@@ -171,3 +171,35 @@ def test_bert_tiny_gradients_match_fp32_twin(cuda, gathered):
     _, stock = _bert_twin(m, store, ids, tt, dense, nsp, kv_lens, autocast=True)
     # padded key rows of the [CLS]-only NSP head see no gradient in either path; pad decoder columns neither
     _check(store, loss.float().item(), ref_loss, ref, stock)
+
+
+def test_llama_swiglu_fused_backward_matches_unfused(cuda):
+    """Llama with the SwiGLU backward inside the down projection's data gradient (nn.SwiGLULink) gives the same
+    loss and parameter gradients as the separate SwiGLU-backward pass (a shape the 4-wave kernel takes:
+    4,096 tokens x 4,096 intermediate)."""
+    import dataclasses
+
+    from k8s_amd.models import llama as M
+    from k8s_amd.ops import nn as K
+    from k8s_amd.parallel.flat import ParamStore
+
+    cfg = dataclasses.replace(M.LLAMA_TINY, layers=1, intermediate=4096, max_position=1024)
+    out = []
+    for fuse in (False, True):
+        K.SWIGLU_FUSE = fuse
+        try:
+            store = ParamStore()
+            model = M.LlamaForCausalLM(store, cfg).finalize(cuda, seed=2)
+            gen = torch.Generator(device=cuda)
+            gen.manual_seed(3)
+            batch = M.synthetic_batch(cfg, 4, 1024, cuda, generator=gen)
+            store.begin_step()
+            loss = model(*batch, dtype=torch.bfloat16)
+            loss.backward()
+            store.zero_unwritten()
+            out.append((loss.float().item(), store.grad.clone()))
+        finally:
+            K.SWIGLU_FUSE = True
+    (l0, g0), (l1, g1) = out
+    assert l0 == l1
+    assert torch.equal(g0, g1), (g0 - g1).abs().max().item()
