@@ -105,9 +105,12 @@ __device__ __forceinline__ const uint16_t* kh_src(const uint16_t* base, long rst
 }
 
 // =============================================================================== forward
-// NB: K/V stage buffers (1: every key in one tile, Sk <= TILE -- the short-sequence form, no second buffer)
-template <int D, int TILE, int NB = 2>
-__global__ void __launch_bounds__(FA_THREADS, NB == 1 ? 3 : 2) flash_fwd_kernel(AttnFwdArgs a) {
+// NB: K/V stage buffers (1: every key in one tile, Sk <= TILE -- the short-sequence form, no second buffer).
+// QS: 16-query sets per wave (2: 128-query blocks. 1 -- 64-query blocks, 110 VGPRs / 4 blocks per CU -- measured
+// slower on BERT s128 b1024: 200 vs 182 us, scripts/gpurun/r5/faqs.sh)
+template <int D, int TILE, int NB = 2, int QS = 2>
+__global__ void __launch_bounds__(FA_THREADS, NB == 1 ? (QS == 1 ? 4 : 3) : 2) flash_fwd_kernel(AttnFwdArgs a) {
+  constexpr int BM = 64 * QS;  // queries per block
   constexpr int FA_BN = TILE;  // keys per iteration
   constexpr int NI = FA_BN / 16;       // 16-key subtiles
   constexpr int KT = FA_BN * D * 2;    // bytes of one K (or V) tile
@@ -117,19 +120,19 @@ __global__ void __launch_bounds__(FA_THREADS, NB == 1 ? 3 : 2) flash_fwd_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
 
-  const int nqb = (a.Sq + FA_BM - 1) / FA_BM;
+  const int nqb = (a.Sq + BM - 1) / BM;
   const int nwg = nqb * a.Hq * a.B;
   const int wg = xcd_remap(blockIdx.x, nwg);
   const int qb = nqb - 1 - (wg % nqb);  // heavier (causal) query blocks first
   const int h = (wg / nqb) % a.Hq;
   const int b = wg / (nqb * a.Hq);
   const int hk = h / (a.Hq / a.Hkv);
-  const int q0 = qb * FA_BM, q0w = q0 + wid_u * 32;  // wave-uniform (SGPR): per-wave skip / mask tests branch on scc
+  const int q0 = qb * BM, q0w = q0 + wid_u * 16 * QS;  // wave-uniform (SGPR): per-wave skip / mask tests branch on scc
   const int off = a.Sk - a.Sq;
   int kv_end = a.Sk;
   if (a.kv_lens) kv_end = min(kv_end, a.kv_lens[b]);
   int kv_stop = kv_end;
-  if (a.causal) kv_stop = min(kv_stop, q0 + FA_BM + off);
+  if (a.causal) kv_stop = min(kv_stop, q0 + BM + off);
   const int ntiles = kv_stop > 0 ? (kv_stop + FA_BN - 1) / FA_BN : 0;
 
   const uint16_t* qp = a.q + (long)b * a.sqb + (long)h * a.sqh;
@@ -137,9 +140,9 @@ __global__ void __launch_bounds__(FA_THREADS, NB == 1 ? 3 : 2) flash_fwd_kernel(
   const uint16_t* vp = a.v + (long)b * a.svb + (long)hk * a.svh;
 
   // Q fragments (operand "B" of S^T = K Q^T): query q0w + 16*qs + li, d = 32*kk + 8*g
-  mfma_bf16x8 qf[2][NK];
+  mfma_bf16x8 qf[QS][NK];
 #pragma unroll
-  for (int qs = 0; qs < 2; ++qs) {
+  for (int qs = 0; qs < QS; ++qs) {
     const int qi = q0w + qs * 16 + li;
 #pragma unroll
     for (int kk = 0; kk < NK; ++kk) {
@@ -149,10 +152,15 @@ __global__ void __launch_bounds__(FA_THREADS, NB == 1 ? 3 : 2) flash_fwd_kernel(
     }
   }
 
-  f32x4_t oacc[ND][2];
+  f32x4_t oacc[ND][QS];
+  float m[QS], l[QS];
 #pragma unroll
-  for (int i = 0; i < ND; ++i) oacc[i][0] = oacc[i][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float m[2] = {-1e30f, -1e30f}, l[2] = {0.f, 0.f};
+  for (int qs = 0; qs < QS; ++qs) {
+#pragma unroll
+    for (int i = 0; i < ND; ++i) oacc[i][qs] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    m[qs] = -1e30f;
+    l[qs] = 0.f;
+  }
 
   // Staging geometry, fixed across tiles: round rd moves K unit s = rd * 256 + tid (tile row, element offset inside
   // the row) and V unit s. The element offsets row * stride + column are computed once -- for full tiles and, rows
@@ -202,25 +210,27 @@ __global__ void __launch_bounds__(FA_THREADS, NB == 1 ? 3 : 2) flash_fwd_kernel(
     if (NB > 1 && t + 1 < ntiles) stage(cur ^ 1, key0 + FA_BN);
     const char* tk = smem + cur * 2 * KT;
     const char* tv = tk + KT;
-    const bool skip = MASKED && a.causal && key0 > q0w + 31 + off;  // whole tile masked for this wave
+    const bool skip = MASKED && a.causal && key0 > q0w + 16 * QS - 1 + off;  // whole tile masked for this wave
     if (!skip) {
       // ---- S^T = K Q^T
-      f32x4_t s[NI][2];
+      f32x4_t s[NI][QS];
 #pragma unroll
-      for (int i = 0; i < NI; ++i) s[i][0] = s[i][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int qs = 0; qs < QS; ++qs) s[i][qs] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
           const mfma_bf16x8 kf = frag_kh(tk + (kk >> 1) * (FA_BN * 128), i * 16, kk & 1, lane);
-          s[i][0] = mfma16(kf, qf[0][kk], s[i][0]);
-          s[i][1] = mfma16(kf, qf[1][kk], s[i][1]);
+#pragma unroll
+          for (int qs = 0; qs < QS; ++qs) s[i][qs] = mfma16(kf, qf[qs][kk], s[i][qs]);
         }
       }
       // ---- online softmax (per query column = lane & 15)
       const bool need_mask = MASKED && ((key0 + FA_BN > kv_end) || (a.causal && key0 + FA_BN - 1 > q0w + off));
 #pragma unroll
-      for (int qs = 0; qs < 2; ++qs) {
+      for (int qs = 0; qs < QS; ++qs) {
         const int qi = q0w + qs * 16 + li;
         // max over the raw scores (scale_log2 > 0 commutes with max), the scale folded into the exponent's fma
         if (need_mask) {  // wave-uniform; one compare per score against min(kv_end - 1, causal diagonal)
@@ -261,9 +271,9 @@ __global__ void __launch_bounds__(FA_THREADS, NB == 1 ? 3 : 2) flash_fwd_kernel(
       // ---- O^T += V^T P^T (k = keys in the permuted order of the S^T accumulators)
 #pragma unroll
       for (int s2 = 0; s2 < NI / 2; ++s2) {
-        mfma_bf16x8 pf[2];
+        mfma_bf16x8 pf[QS];
 #pragma unroll
-        for (int qs = 0; qs < 2; ++qs) {
+        for (int qs = 0; qs < QS; ++qs) {
           const float lo[4] = {s[2 * s2][qs][0], s[2 * s2][qs][1], s[2 * s2][qs][2], s[2 * s2][qs][3]};
           const float hi[4] = {s[2 * s2 + 1][qs][0], s[2 * s2 + 1][qs][1], s[2 * s2 + 1][qs][2], s[2 * s2 + 1][qs][3]};
           pf[qs] = pack8(lo, hi);
@@ -276,8 +286,8 @@ __global__ void __launch_bounds__(FA_THREADS, NB == 1 ? 3 : 2) flash_fwd_kernel(
           const char* a0 = tv + r0 * (2 * D) + ((u ^ v_swz<D>(r0)) << 4) + (p & 1) * 8;
           const char* a1 = tv + r1 * (2 * D) + ((u ^ v_swz<D>(r1)) << 4) + (p & 1) * 8;
           const mfma_bf16x8 vf = join8(tr16(a0), tr16(a1));
-          oacc[d][0] = mfma16(vf, pf[0], oacc[d][0]);
-          oacc[d][1] = mfma16(vf, pf[1], oacc[d][1]);
+#pragma unroll
+          for (int qs = 0; qs < QS; ++qs) oacc[d][qs] = mfma16(vf, pf[qs], oacc[d][qs]);
         }
       }
     }
@@ -296,7 +306,7 @@ __global__ void __launch_bounds__(FA_THREADS, NB == 1 ? 3 : 2) flash_fwd_kernel(
   // ---- epilogue: O = O^T / l, lse2 = m + log2(l)
   uint16_t* op = a.o + (long)b * a.sob + (long)h * a.soh;
 #pragma unroll
-  for (int qs = 0; qs < 2; ++qs) {
+  for (int qs = 0; qs < QS; ++qs) {
     float lt = l[qs];
     lt += __shfl_xor(lt, 16, 64);
     lt += __shfl_xor(lt, 32, 64);
