@@ -55,10 +55,8 @@ def main():
         dw = torch.empty(K, R, R, C, device=dev)
         flops = 2.0 * N * Ho * Ho * K * R * R * C
         out = {"shape": [N, H, C, K, R, s, p]}
-        os.environ["K8S_AMD_WGRAD_STREAM"] = "0"
         out["generic_tf"] = round(flops / timed(lambda: C_.conv_wgrad(x, gy, dw, s, p, 1, 0, False)) / 1e9, 1)
         ref = dw.clone()
-        os.environ.pop("K8S_AMD_WGRAD_STREAM", None)
         os.environ["K8S_AMD_WGS_ANY"] = "1"  # time the streaming kernel on every shape
         for tile in TILES:
             os.environ["K8S_AMD_WGS_TILE"] = tile
