@@ -62,6 +62,8 @@ def parse(argv=None):
                     help="gradient all-reduce transport (bf16: all-to-all + fp32 owner sum + all-gather)")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--profile-steps", type=int, default=0, help="(internal) roctx-free short run")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="create the process group and run the gradient transport even at world 1 (RCCL on one GPU)")
     return ap.parse_args(argv)
 
 
@@ -135,7 +137,7 @@ def main(argv=None):
     a = parse(argv)
     if a.gpus > 1 and "RANK" not in os.environ and "WORLD_SIZE" not in os.environ:
         return _launch_local_ranks(a, argv)
-    info = kdist.init_process_group()
+    info = kdist.init_process_group(force=a.force_dist)
     n = info.world_size
     if n != a.gpus:
         # fail closed: a number measured on a different world than the one asked for must not be reported
@@ -152,7 +154,7 @@ def main(argv=None):
     if n > 1:
         torch.distributed.broadcast(store.master, 0)
         store.refresh_lowp()
-    reducer = GradReducer(store, bucket_mb=a.bucket_mb,
+    reducer = GradReducer(store, bucket_mb=a.bucket_mb, enabled=(n > 1 or a.force_dist),
                           comm_dtype=torch.bfloat16 if a.grad_comm == "bf16" else torch.float32)
     opt = FusedSGD(store, lr=a.lr, momentum=0.9, weight_decay=5e-5, nesterov=False)
     # what the collectives actually ran on, read from the process group after its first collective (the broadcast

@@ -39,6 +39,7 @@ Controller::Controller(KubeApi& api, ControllerConfig cfg, ControllerOptions opt
     InformerOptions io;
     io.watch_timeout = opts_.watch_timeout;
     io.watch_idle_grace = opts_.watch_idle_grace;
+    io.resync_period = opts_.resync_period;  // same relist period as the TfJob loop (--resync-period)
     jobs_inf_ = std::make_unique<Informer>(api_, group_path("batch/v1", opts_.ns, "jobs"), "tensorflow.org", io);
     pods_inf_ = std::make_unique<Informer>(api_, core_path(opts_.ns, "pods"), "tensorflow.org", io);
     jobs_inf_->set_on_change([this](const std::string&, const Json& o) { poke_owner(o); });

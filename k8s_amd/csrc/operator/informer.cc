@@ -22,6 +22,19 @@ void Informer::stop() {
   if (th_.joinable()) th_.join();
 }
 
+void Informer::touch() {
+  last_ok_ns_ = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                    std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+bool Informer::fresh() const {
+  if (!synced_.load()) return false;
+  if (watching_.load()) return true;
+  const long long now = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                            std::chrono::steady_clock::now().time_since_epoch()).count();
+  return now - last_ok_ns_.load() <= std::chrono::duration_cast<std::chrono::nanoseconds>(opts_.stale_after).count();
+}
+
 bool Informer::wait_synced(std::chrono::milliseconds timeout) {
   std::unique_lock<std::mutex> lk(sync_mu_);
   // system_clock deadline: see JobWorker::run (ThreadSanitizer and pthread_cond_clockwait)
@@ -150,6 +163,7 @@ bool Informer::relist(std::string& rv) {
     apply(had ? "MODIFIED" : "ADDED", kv.second);
   }
   if (const Json* m = r.body.find("metadata")) rv = get_str(*m, "resourceVersion");
+  touch();
   if (!synced_.exchange(true)) {
     std::lock_guard<std::mutex> g(sync_mu_);
     sync_cv_.notify_all();
@@ -162,36 +176,58 @@ void Informer::run() {
   using clock = std::chrono::steady_clock;
   std::string rv;
   bool need_list = true;
+  int watch_failures = 0;
+  clock::time_point listed_at = clock::now();
   auto pause = [&] {
     for (long i = 0; i < opts_.retry.count() / 50 && !stop_; ++i)
       std::this_thread::sleep_for(std::chrono::milliseconds(50));
   };
+  auto resync_due = [&] {
+    return opts_.resync_period.count() > 0 && clock::now() - listed_at >= opts_.resync_period;
+  };
   while (!stop_) {
-    if (need_list) {
+    if (need_list || resync_due()) {
       if (!relist(rv)) {
         pause();
         continue;
       }
       need_list = false;
+      watch_failures = 0;
+      listed_at = clock::now();
     }
     const long tmin = std::max<long>(1, (long)(opts_.watch_timeout.count() / 1000));
-    const long timeout_s = std::uniform_int_distribution<long>(tmin, std::max(tmin, 2 * tmin - 1))(rng);
+    long timeout_s = std::uniform_int_distribution<long>(tmin, std::max(tmin, 2 * tmin - 1))(rng);
+    if (opts_.resync_period.count() > 0) {  // end the watch by the next resync
+      const long left = (long)std::chrono::duration_cast<std::chrono::seconds>(
+                            opts_.resync_period - (clock::now() - listed_at)).count();
+      timeout_s = std::max<long>(1, std::min(timeout_s, left));
+    }
     std::string q = "?watch=true&resourceVersion=" + rv + "&timeoutSeconds=" + std::to_string(timeout_s);
     if (!selector_.empty()) q += "&labelSelector=" + url_escape(selector_);
     std::string err;
     ++watches_;
     auto w = api_.watch(path_ + q, err);
     if (!w) {
-      log_warn("informer %s: watch failed: %s", path_.c_str(), err.c_str());
+      ++watch_failures;
+      // the rv may be gone (410) or the watch forbidden (403): re-watching from it would fail forever, leaving the
+      // cache frozen at its last list. Relist at once on those, and after a run of any other failures.
+      const bool gone = err.find("HTTP 410") != std::string::npos || err.find("HTTP 403") != std::string::npos;
+      if (gone || watch_failures >= opts_.relist_after_watch_failures) need_list = true;
+      log_warn("informer %s: watch failed (%d in a row): %s%s", path_.c_str(), watch_failures, err.c_str(),
+               need_list ? ": relisting" : "");
       pause();
       continue;
     }
+    watch_failures = 0;
+    watching_ = true;
+    touch();
     const auto dead_after = clock::now() + std::chrono::seconds(timeout_s) + opts_.watch_idle_grace;
     while (!stop_) {
       if (clock::now() > dead_after) {
         log_warn("informer %s: watch past its timeoutSeconds: re-watching from rv=%s", path_.c_str(), rv.c_str());
         break;
       }
+      if (resync_due()) break;
       Json ev;
       if (!w->next(ev, 500, err)) break;  // stream ended: re-watch from rv
       if (ev.is_null()) continue;
@@ -205,11 +241,14 @@ void Informer::run() {
         need_list = true;
         break;
       }
+      touch();
       if (const Json* m = obj->find("metadata")) rv = get_str(*m, "resourceVersion");
       if (type == "ADDED" || type == "MODIFIED" || type == "DELETED") apply(type, *obj);
     }
+    watching_ = false;
     w->close();
   }
+  watching_ = false;
 }
 
 }  // namespace tfop

@@ -11,7 +11,9 @@
 // Per collection (batch/v1 jobs, v1 pods; label selector `tensorflow.org`, the label every replica object carries):
 // LIST -> store keyed by namespace/name + an index by (namespace, tf_job_name label); WATCH from the list's
 // resourceVersion with a server-side timeoutSeconds; a stream that outlives timeoutSeconds by the grace is a
-// half-open connection and is re-established; 410 Gone relists. Readers get immutable shared objects (an update
+// half-open connection and is re-established; 410 Gone relists, on the stream or on the watch open (as does a 403,
+// or a watch open that keeps failing), and a resync period relists a healthy cache too. fresh() tells readers
+// whether to trust the cache or to read the API directly (a cache frozen behind a failing watch is not trusted). Readers get immutable shared objects (an update
 // replaces the entry, it never mutates one in place).
 #pragma once
 
@@ -35,6 +37,15 @@ struct InformerOptions {
   std::chrono::milliseconds watch_timeout{300000};  // timeoutSeconds in [t, 2t) per watch (client-go reflector)
   std::chrono::milliseconds watch_idle_grace{30000};
   std::chrono::milliseconds retry{1000};            // after a failed list / watch
+  // periodic relist even while the watch is healthy (client-go resyncPeriod): bounds how long a missed event can
+  // hide a replica's state change. 0 = never.
+  std::chrono::milliseconds resync_period{300000};
+  // consecutive failed watch OPENS after which the next attempt relists instead of re-watching from the same rv
+  // (a 410 / 403 on open relists at once)
+  int relist_after_watch_failures{3};
+  // fresh(): the cache is trusted while a watch is established, or within this bound of the last successful list /
+  // watch open / event; readers fall back to direct API reads past it
+  std::chrono::milliseconds stale_after{60000};
 };
 
 class Informer {
@@ -52,6 +63,9 @@ class Informer {
   void stop();
 
   bool synced() const { return synced_.load(); }
+  // synced AND (a watch is open, or the last successful list / watch open / event is within stale_after): what a
+  // reader checks before trusting the cache over a direct GET / LIST
+  bool fresh() const;
   bool wait_synced(std::chrono::milliseconds timeout);
 
   // namespace/name lookup; false when the object is not in the cache
@@ -78,7 +92,10 @@ class Informer {
   mutable std::mutex mu_;
   std::map<std::string, Json> objs_;                  // ns/name -> object
   std::map<std::string, std::set<std::string>> idx_;  // ns/tf_job_name -> {ns/name}
-  std::atomic<bool> synced_{false}, stop_{false};
+  void touch();  // a successful list / watch open / event: the cache is current as of now
+
+  std::atomic<bool> synced_{false}, stop_{false}, watching_{false};
+  std::atomic<long long> last_ok_ns_{0};  // steady_clock of the last touch()
   std::atomic<long long> lists_{0}, watches_{0}, events_{0};
   std::mutex sync_mu_;
   std::condition_variable sync_cv_;

@@ -12,6 +12,7 @@
 #include "controller.h"
 #include "election.h"
 #include "flags.h"
+#include "informer.h"
 #include "kube_api.h"
 #include "reconciler.h"
 #include "replicas.h"
@@ -58,6 +59,25 @@ struct PyReconciler {
     o.ps_server_source = ps_src;
     ControllerConfig cfg = cfg_json.empty() ? ControllerConfig{} : controller_config_from_json(Json::parse(cfg_json));
     job = std::make_unique<TrainingJob>(*api, job_of(job_json), cfg, o);
+  }
+};
+
+// A shared watch cache over the real HTTP transport (tests of the informer's relist / resync / freshness rules
+// against the fake API server's fault injection)
+struct PyInformer {
+  std::unique_ptr<KubeApi> api;
+  std::unique_ptr<Informer> inf;
+  PyInformer(const std::string& url, const std::string& path, const std::string& selector, int watch_timeout_ms,
+             int retry_ms, int resync_ms, int relist_after, int stale_ms) {
+    api = make_http_api(parse_master_url(url));
+    InformerOptions o;
+    o.watch_timeout = std::chrono::milliseconds(watch_timeout_ms);
+    o.watch_idle_grace = std::chrono::milliseconds(2000);
+    o.retry = std::chrono::milliseconds(retry_ms);
+    o.resync_period = std::chrono::milliseconds(resync_ms);
+    o.relist_after_watch_failures = relist_after;
+    o.stale_after = std::chrono::milliseconds(stale_ms);
+    inf = std::make_unique<Informer>(*api, path, selector, o);
   }
 };
 
@@ -194,6 +214,32 @@ PYBIND11_MODULE(_operator, m) {
   }, py::arg("url"), py::arg("method") = "GET", py::arg("path") = "/", py::arg("ca_data") = "",
      py::arg("server_name") = "", py::arg("timeout_ms") = 0, py::arg("repeat") = 1, py::arg("cert_data") = "",
      py::arg("key_data") = "");
+
+  py::class_<PyInformer>(m, "Informer")
+      .def(py::init<std::string, std::string, std::string, int, int, int, int, int>(), py::arg("url"),
+           py::arg("path"), py::arg("selector") = "", py::arg("watch_timeout_ms") = 300000,
+           py::arg("retry_ms") = 1000, py::arg("resync_ms") = 300000, py::arg("relist_after") = 3,
+           py::arg("stale_ms") = 60000)
+      .def("start", [](PyInformer& i) { i.inf->start(); })
+      .def("stop", [](PyInformer& i) {
+        py::gil_scoped_release nogil;
+        i.inf->stop();
+      })
+      .def("wait_synced", [](PyInformer& i, int ms) {
+        py::gil_scoped_release nogil;
+        return i.inf->wait_synced(std::chrono::milliseconds(ms));
+      })
+      .def("synced", [](PyInformer& i) { return i.inf->synced(); })
+      .def("fresh", [](PyInformer& i) { return i.inf->fresh(); })
+      .def("size", [](PyInformer& i) { return i.inf->size(); })
+      .def("lists", [](PyInformer& i) { return i.inf->lists(); })
+      .def("watches", [](PyInformer& i) { return i.inf->watches(); })
+      .def("names", [](PyInformer& i, const std::string& ns) {
+        std::vector<std::string> out;
+        Json items = i.inf->list(ns, Labels{});
+        for (auto& o : items.as_array()) out.push_back(get_str(o.at("metadata"), "name"));
+        return out;
+      });
 
   py::class_<PyReconciler>(m, "Reconciler")
       .def(py::init<py::function, std::string, std::string, std::string>(), py::arg("api"), py::arg("job"),

@@ -143,8 +143,9 @@ void TrainingJob::create_resources() {
 void TrainingJob::get_status(std::string& state, std::vector<TfReplicaStatus>& out) {
   const std::string ns = job_.ns();
   // the caches count only once synced (a reconcile racing the operator's start reads the API server)
-  const Informer* jobs_cache = opts_.jobs_cache && opts_.jobs_cache->synced() ? opts_.jobs_cache : nullptr;
-  const Informer* pods_cache = opts_.pods_cache && opts_.pods_cache->synced() ? opts_.pods_cache : nullptr;
+  // a cache that is not fresh (its watch keeps failing and no list succeeded lately) is bypassed: direct GET / LIST
+  const Informer* jobs_cache = opts_.jobs_cache && opts_.jobs_cache->fresh() ? opts_.jobs_cache : nullptr;
+  const Informer* pods_cache = opts_.pods_cache && opts_.pods_cache->fresh() ? opts_.pods_cache : nullptr;
   out.clear();
   for (auto& r : replicas_) {
     TfReplicaStatus st;

@@ -69,6 +69,13 @@ class _Handler(BaseHTTPRequestHandler):
                                        "user_agent": b.get("user_agent", "")})
             return self._send(200, {"stalls": len(self.server.stalls)})
         self._stall()
+        for rule in list(self.server.failures):  # fault injection: answer matching requests with an error status
+            is_watch = "watch=" in u.query
+            if time.time() < rule["until"] and u.path.startswith(rule["path_prefix"]) and \
+                    (rule["watch"] is None or rule["watch"] == is_watch):
+                rule["hits"] += 1
+                return self._send(rule["code"], {"kind": "Status", "apiVersion": "v1", "status": "Failure",
+                                                 "reason": "Injected", "code": rule["code"]})
         with self.server.count_lock:  # requests per client (User-Agent) and kind: the operator scale test's API load
             ua = self.headers.get("User-Agent", "")
             kind = "WATCH" if "watch=" in u.query else method
@@ -161,6 +168,7 @@ class FakeApiServer:
         self.httpd = _Server((host, port), handler)
         self.httpd.daemon_threads = True
         self.httpd.stalls = []  # fault injection rules (POST /debug/stall, or stall() below)
+        self.httpd.failures = []  # error-status injection rules (fail() below)
         self.httpd.blackhole_before = 0.0  # watches opened before this time are black holes (blackhole_watches)
         self.httpd.accept_token = None  # callable(token) -> bool: reject other bearer tokens with 401
         self.httpd.accepted, self.httpd.rejected = [], []
@@ -179,6 +187,14 @@ class FakeApiServer:
         """Stop answering matching requests for ``seconds`` (requests arriving meanwhile hang until then)."""
         self.httpd.stalls.append({"until": time.time() + seconds, "path_prefix": path_prefix,
                                   "user_agent": user_agent})
+
+    def fail(self, code: int, seconds: float, path_prefix: str = "/", watch: Optional[bool] = None) -> dict:
+        """Answer matching requests with HTTP ``code`` (a Status body) for ``seconds``: ``watch`` True = only watch
+        opens, False = only plain requests, None = both. Returns the rule (its ``hits`` counts the failed requests)."""
+        rule = {"until": time.time() + seconds, "path_prefix": path_prefix, "code": int(code), "watch": watch,
+                "hits": 0}
+        self.httpd.failures.append(rule)
+        return rule
 
     def request_counts(self, ua_prefix: str = "") -> dict:
         """{method: requests} of the clients whose User-Agent starts with ``ua_prefix`` (WATCH = watch opens)."""

@@ -16,6 +16,7 @@ import math
 from typing import Optional
 
 import torch
+from torch.autograd.graph import increment_version
 
 from k8s_amd.ops._ext import load as _load
 
@@ -110,6 +111,11 @@ class _FlashQKV(torch.autograd.Function):
             if not rope_in_place:  # (in place: the caller's qkv is a temporary nothing else reads)
                 x = x.clone() if x.data_ptr() == qkv.data_ptr() else x
             C.rope_(x[:, : (H + Hkv) * D], pos, table, False)
+            if x.data_ptr() == qkv.data_ptr():
+                # the raw-pointer rotation does not bump autograd's version counter: bump it, so any other holder
+                # of the projection output saved for its backward (a hook, a saved ReLU y, a grad_link) fails loudly
+                # in backward instead of silently reading rotated values
+                increment_version(qkv)
         g = x.view(B, S, H + 2 * Hkv, D)
         q, k, v = g.narrow(2, 0, H), g.narrow(2, H, Hkv), g.narrow(2, H + Hkv, Hkv)
         o, lse = C.flash_fwd(q, k, v, causal, kv_lens, scale)

@@ -108,22 +108,23 @@ def linear_fwd(x, w, b, act=None):
     return y, (pre if act == "gelu" else (y if act == "relu" else None))
 
 
-def dact_ok(x, w, dx_addend=None) -> bool:
+def dact_ok(x, w, dx_addend=None, gy=None) -> bool:
     """Whether a linear's data gradient can take its input activation's backward in the GEMM epilogue (``linear_bwd``
-    ``dx_act``): the 4-wave kernel's whole-tile shapes, GPU bf16, no second gradient contribution to add."""
+    ``dx_act``): the 4-wave kernel's whole-tile shapes, GPU bf16 operands (x, w and the incoming gradient gy), no
+    second gradient contribution to add."""
     M, K = x.shape
     N = w.shape[0]
     return (dx_addend is None and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
-            and bool(_load().gemm_dact_ok(M, K, N)))
+            and (gy is None or gy.dtype == torch.bfloat16) and N % 8 == 0 and bool(_load().gemm_dact_ok(M, K, N)))
 
 
-def swiglu_ok(x, w, dx_addend=None) -> bool:
+def swiglu_ok(x, w, dx_addend=None, gy=None) -> bool:
     """Whether a linear whose input is a SwiGLU output can return the SwiGLU's input gradient (dgu) from its data
     gradient's epilogue (``linear_bwd`` ``dx_swiglu``): GPU bf16, the 4-wave kernel's whole-tile shapes."""
     M, F = x.shape
     K = w.shape[0]
     return (dx_addend is None and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
-            and bool(_load().gemm_swiglu_bwd_ok(M, F, K)))
+            and (gy is None or gy.dtype == torch.bfloat16) and K % 8 == 0 and bool(_load().gemm_swiglu_bwd_ok(M, F, K)))
 
 
 def _dgrad_act(g, w, dx_act):
@@ -150,10 +151,18 @@ def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True, dx_adden
     (db is then returned as None). ``dx_act`` = (pre, act, producer bias param, its store): x is the output of that
     activation and dx is returned already through its backward, the producer's bias gradient deposited
     (``dact_ok`` must hold). ``dx_swiglu`` = gu: x = swiglu(gu), and the gradient of gu ([M, 2F]) is returned in
-    dx's place (``swiglu_ok`` must hold)."""
+    dx's place (``swiglu_ok`` must hold).
+
+    The two fused forms exist only on the whole-tile HIP branch: a call that asks for one and would take any other
+    path (ragged N, the torch.matmul fallback) raises instead of returning a gradient WITHOUT the activation /
+    SwiGLU backward applied (the caller marks the producer's backward as done on return)."""
     M, K = x.shape
     N = w.shape[0]
     db = None
+    if (dx_act is not None or dx_swiglu is not None) and not (
+            gy.dtype == torch.bfloat16 and hip_ok(gy, x, w) and _shape_ok(M, N, K) and N % 8 == 0):
+        raise RuntimeError("linear_bwd: fused %s backward requested on a path without it (%dx%dx%d, gy %s)"
+                           % ("activation" if dx_act is not None else "SwiGLU", M, N, K, gy.dtype))
     if (need_db and act in ("relu", "gelu") and gy.is_cuda and gy.dtype == torch.bfloat16 and N % 8 == 0
             and saved is not None and saved.dtype == torch.bfloat16):
         # activation backward and the bias gradient (its column sums) in one pass

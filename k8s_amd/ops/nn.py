@@ -534,10 +534,10 @@ class _Linear(torch.autograd.Function):
             act, db_done = None, True
         dx_act = None
         li = ctx.act_in
-        if li is not None and li.saved is not None and g.dact_ok(x2, w, addend):
+        if li is not None and li.saved is not None and g.dact_ok(x2, w, addend, gy):
             dx_act = (li.saved, li.act, li.pb, li.pb.store)
         sl, dx_swiglu = ctx.swiglu_in, None
-        if dx_act is None and sl is not None and sl.saved is not None and g.swiglu_ok(x2, w, addend):
+        if dx_act is None and sl is not None and sl.saved is not None and g.swiglu_ok(x2, w, addend, gy):
             dx_swiglu = sl.saved
         dx, dw, db = g.linear_bwd(gy2, x2, w, pre, act, pw=pw, store=pw.store,
                                   need_db=pb is not None and not db_done, dx_addend=addend, pb=pb, dx_act=dx_act,

@@ -41,7 +41,7 @@ import torch
 import torch.distributed as dist
 
 from k8s_amd.parallel.flat import ALIGN, ParamStore, _round_up
-from k8s_amd.parallel.ps import cast_bf16, slice_sum
+from k8s_amd.parallel.ps import CommBufferPool, cast_bf16, slice_sum
 
 
 class _Bucket:
@@ -89,9 +89,12 @@ class GradReducer:
         self.side = torch.cuda.Stream(store.grad.device) if (store.grad.is_cuda and self.enabled) else None
         self.side_busy = False
         self.padded = set()  # indices of the buckets whose bf16 exchange is zero-padded to a multiple of the world
+        self.pool = CommBufferPool()  # persistent bf16 send / recv per bucket (no record_stream, see CommBufferPool)
         # fault injection for the transport self-check's own test: a wrong reduction (MAX instead of SUM, or one
-        # rank's bf16 contribution dropped) that the check must catch
-        self.fault = os.environ.get("K8S_AMD_FAULT_TRANSPORT") == "1"
+        # rank's bf16 contribution dropped) that the check must catch. Armed only inside ``self_check`` (the
+        # training steps never run the corrupted transport); ``fault_injection`` defaults to the env switch.
+        self.fault_injection = os.environ.get("K8S_AMD_FAULT_TRANSPORT") == "1"
+        self.fault = False
         store.hooks.append(self._on_deposit)
 
     @property
@@ -115,8 +118,12 @@ class GradReducer:
         def run():
             self.works = []
             b.launched = False
-            self._launch(b)
-            self._drain()
+            self.fault = self.fault_injection
+            try:
+                self._launch(b)
+                self._drain()
+            finally:
+                self.fault = False
             b.launched = False
 
         return transport_check(self.store.grad, b.lo, b.hi, (b.lo, b.hi), run, self.comm_dtype, self.group,
@@ -154,13 +161,13 @@ class GradReducer:
         t = self.store.grad[b.lo:b.hi]
         if self.comm_dtype == torch.bfloat16:
             length = b.hi - b.lo
-            if length % self.world == 0:
-                send = cast_bf16(t)
-            else:  # a world that does not divide the 64-element alignment (e.g. 7 ranks): zero-padded exchange
-                send = torch.zeros(_round_up(length, self.world), dtype=torch.bfloat16, device=t.device)
-                send[:length].copy_(cast_bf16(t))
+            total = _round_up(length, self.world)
+            if total != length:  # a world that does not divide the 64-element alignment (e.g. 7 ranks): zero pad
                 self.padded.add(b.index)
-            recv = torch.empty_like(send)
+            send, recv = self.pool.acquire(b.index, total, t.device)
+            if total != length:
+                send[length:].zero_()
+            cast_bf16(t, send[:length])
             w = dist.all_to_all_single(recv, send, group=self.group, async_op=True)
             if self.side is None:
                 self.works.append((b, send, recv, w))
@@ -175,8 +182,7 @@ class GradReducer:
                 self._slice_sum(recv, n, red)
                 dist.all_gather_into_tensor(send, red, group=self.group, async_op=True).wait()
                 t.copy_(send[:length])
-            send.record_stream(self.side)
-            recv.record_stream(self.side)
+            self.pool.release(b.index, self.side)  # the next step's cast waits for this on the device
             self.side_busy = True
         else:
             op = dist.ReduceOp.MAX if self.fault else dist.ReduceOp.SUM

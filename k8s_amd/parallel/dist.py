@@ -188,11 +188,18 @@ def rank_from_env() -> Optional[RankInfo]:
 
 
 def init_process_group(info: Optional[RankInfo] = None, backend: Optional[str] = None,
-                       timeout_s: float = 600.0) -> RankInfo:
+                       timeout_s: float = 600.0, force: bool = False) -> RankInfo:
     """Initialise torch.distributed (nccl == RCCL on ROCm, gloo on CPU; ``K8S_AMD_DIST_BACKEND`` overrides the
-    default). Idempotent."""
-    info = info or rank_from_env() or RankInfo(0, 1, 0, "127.0.0.1", 29500)
-    if info.world_size > 1 and not dist.is_initialized():
+    default). Idempotent. A world of one creates no group unless ``force`` (a one-rank RCCL communicator: the
+    transports then run their real collectives on one GPU -- ``bench.py --force-dist``, ``tests/test_rccl_gpu.py``);
+    a forced world-1 group without a torchrun env rendezvouses on a free local port."""
+    env_info = rank_from_env()
+    if info is None and env_info is None and force:
+        from k8s_amd.fakeapi.server import free_port
+
+        info = RankInfo(0, 1, 0, "127.0.0.1", free_port())
+    info = info or env_info or RankInfo(0, 1, 0, "127.0.0.1", 29500)
+    if (info.world_size > 1 or force) and not dist.is_initialized():
         if backend is None:
             backend = os.environ.get("K8S_AMD_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if torch.cuda.is_available():

@@ -23,11 +23,13 @@ whose gradients they deposit directly.
 from __future__ import annotations
 
 import math
+import os
 from typing import Callable, Dict, List, Optional
 
 import torch
 
 ALIGN = 64
+_DEBUG_PULL = os.environ.get("K8S_AMD_DEBUG_PULL") == "1"
 
 
 def _round_up(n: int, a: int = ALIGN) -> int:
@@ -61,6 +63,8 @@ class Param:
         """The tensor compute kernels consume: bf16 copy for MFMA weights, fp32 master otherwise. With a bf16 pull in
         flight (ZeRO-1, parallel/ps.py) the first read of a weight waits for its bucket(s) only."""
         if self.store.pending:
+            if _DEBUG_PULL and torch.cuda.current_stream() != torch.cuda.default_stream():
+                raise RuntimeError("Param.weight read on a side stream while a bf16 pull is pending (%s)" % self.name)
             self.store.wait_param(self)
         return self.half if self.half is not None else self.master
 
@@ -198,7 +202,14 @@ class ParamStore:
 
     def wait_param(self, p: Param):
         """Order the current stream after the pull of ``p``'s bucket(s) (device-side wait for RCCL; blocking for
-        gloo), once per bucket."""
+        gloo), once per bucket.
+
+        Contract (the pull is lazily waited, ``parallel/ps.py``): every reader of the working copy goes through
+        ``Param.weight``, and the first read of a bucket happens on the stream that later reads it -- the work is
+        popped after ONE device-side wait, so a direct ``store.half`` / ``p.half`` read, or a first read on a side
+        stream, would race the in-flight all-gather. ``ShardedParameterService._check_pull`` pins the wait itself;
+        ``K8S_AMD_DEBUG_PULL=1`` makes ``Param.weight`` refuse a read from a non-default stream while a pull is
+        pending."""
         for b in self.pending_of.get(p.index, ()):
             w = self.pending.pop(b.index, None)
             if w is not None:

@@ -81,11 +81,17 @@ class _Range:
 
 class ShardedParameterService:
     def __init__(self, store: ParamStore, optimizer, group=None, bucket_mb: float = 64.0,
-                 comm_dtype: torch.dtype = torch.float32, zero1: bool = True, pull: str = "auto"):
+                 comm_dtype: torch.dtype = torch.float32, zero1: bool = True, pull: str = "auto",
+                 enabled: Optional[bool] = None):
         self.store, self.opt, self.group = store, optimizer, group
         init = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(group) if init else 1
         self.rank = dist.get_rank(group) if init else 0
+        # enabled: run the push / pull collectives (default: world > 1). ``enabled=True`` at world 1 drives the whole
+        # transport through a one-rank process group -- how the GPU tests pin RCCL's stream semantics on one GPU
+        self.active = (self.world > 1) if enabled is None else bool(enabled)
+        if self.active and not init:
+            raise ValueError("enabled=True needs an initialised process group")
         if comm_dtype not in (torch.float32, torch.bfloat16):
             raise ValueError("comm_dtype must be float32 or bfloat16")
         self.comm_dtype = comm_dtype
@@ -110,13 +116,15 @@ class ShardedParameterService:
         self.works = []
         self.a2a = []  # (bucket, send, recv, work) of in-flight bf16 pushes
         self.next_launch = 0
-        self.sharded = zero1 and self.world > 1
+        self.sharded = zero1 and self.active
         if self.sharded:
             optimizer.shard(self.owned_ranges)
         # bf16 pushes on the GPU: the owner's fp32 sum runs on this stream, device-ordered behind each exchange
-        self.side = (torch.cuda.Stream(store.grad.device) if store.grad.is_cuda and self.world > 1 else None)
+        self.side = (torch.cuda.Stream(store.grad.device) if store.grad.is_cuda and self.active else None)
         self.side_busy = False
-        self.fault = os.environ.get("K8S_AMD_FAULT_TRANSPORT") == "1"  # see GradReducer.fault
+        self.fault_injection = os.environ.get("K8S_AMD_FAULT_TRANSPORT") == "1"  # see GradReducer.fault_injection
+        self.fault = False
+        self.pool = CommBufferPool()
         store.hooks.append(self._on_deposit)
         # pull: "lowp" = bf16 working copy + fp32 non-lowp parameters (GPU default), "fp32" = the full fp32 master
         if pull not in ("auto", "lowp", "fp32"):
@@ -161,12 +169,12 @@ class ShardedParameterService:
             self.next_launch += 1
 
     def _push(self, b: _Range):
-        if self.world == 1:
+        if not self.active:
             return
         g = self.store.grad[b.lo:b.hi]
         if self.comm_dtype == torch.bfloat16:
-            send = cast_bf16(g)
-            recv = torch.empty_like(send)
+            send, recv = self.pool.acquire(b.index, b.hi - b.lo, g.device)
+            cast_bf16(g, send)
             w = dist.all_to_all_single(recv, send, group=self.group, async_op=True)
             if self.side is not None:
                 lo, hi = self.shard(b)
@@ -174,8 +182,7 @@ class ShardedParameterService:
                     w.wait()  # device-side: the side stream waits for this bucket's exchange, the host does not
                     nw = self.world - 1 if self.fault else self.world
                     _load_ext().slice_sum(recv[:nw * (hi - lo)], nw, self.store.grad[lo:hi], None)
-                send.record_stream(self.side)
-                recv.record_stream(self.side)
+                self.pool.release(b.index, self.side)  # no record_stream: see CommBufferPool
                 self.side_busy = True
             else:
                 self.a2a.append((b, send, recv, w))
@@ -206,17 +213,59 @@ class ShardedParameterService:
         (``ddp.transport_check``). Collective; the bucket's gradient range is restored afterwards."""
         from k8s_amd.parallel.ddp import transport_check
 
-        if self.world == 1 or not self.buckets:
+        if not self.active or not self.buckets:
             return {"ok": True, "transport": "none (world 1)"}
         b = self.buckets[0]
 
         def run():
             self.works, self.a2a = [], []
-            self._push(b)
-            self._finish_pushes()
+            self.fault = self.fault_injection  # armed for the check only, never for a training step
+            try:
+                self._push(b)
+                self._finish_pushes()
+            finally:
+                self.fault = False
 
         name = "zero1-" + ("bf16" if self.comm_dtype == torch.bfloat16 else "fp32")
-        return transport_check(self.store.grad, b.lo, b.hi, self.shard(b), run, self.comm_dtype, self.group, name)
+        res = transport_check(self.store.grad, b.lo, b.hi, self.shard(b), run, self.comm_dtype, self.group, name)
+        if self.pull == "lowp":
+            pull = self._check_pull(b)
+            res["pull"] = pull
+            res["ok"] = bool(res["ok"] and pull["ok"])
+        return res
+
+    def _check_pull(self, b: _Range) -> Dict[str, object]:
+        """Step-0 check of the lazily-waited bf16 pull: every rank writes a rank-keyed pattern (exact in bf16) into
+        its owned slice of bucket ``b``'s working copy, the bucket is all-gathered asynchronously and registered as
+        pending exactly like ``_pull_lowp`` does, and the comparison kernel runs after the wait ``Param.weight``
+        performs (the device-side ``Work.wait`` on the current stream). A missing or host-only wait, a wrong shard
+        order or a wrong gather would leave other ranks' slices stale. The working copy is restored afterwards."""
+        s = self.store
+        half = s.half[b.lo:b.hi]
+        save = half.clone()
+        n = (b.hi - b.lo) // self.world
+        idx = torch.arange(n, device=half.device)
+        expect = torch.stack([(((idx * 7 + r * 131) % 509) - 254).float() / 64.0 for r in range(self.world)])
+        expect = expect.reshape(-1).to(half.dtype)
+        lo, hi = self.shard(b)
+        half[lo - b.lo:hi - b.lo].copy_(expect[lo - b.lo:hi - b.lo])
+        keep_pending, keep_of = s.pending, s.pending_of
+        s.pending, s.pending_of = {}, {}
+        work = dist.all_gather_into_tensor(half, half[lo - b.lo:hi - b.lo], group=self.group, async_op=True)
+        s.pending, s.pending_of = {b.index: work}, self.buckets_of
+        reader = next((p for p in b.params if p.lowp), None)
+        if reader is not None:
+            reader.weight  # noqa: B018 -- the lazy wait under test
+        else:  # a bucket of fp32-read parameters only: the step's catch-all wait
+            s.wait_pending()
+        bad = torch.zeros(1, dtype=torch.float64, device=half.device)
+        bad[0] = (half != expect).sum()
+        dist.all_reduce(bad, group=self.group)
+        s.wait_pending()
+        s.pending, s.pending_of = keep_pending, keep_of
+        half.copy_(save)
+        wrong = int(bad.item())
+        return {"ok": wrong == 0, "transport": "zero1-pull-bf16", "elements": int(b.hi - b.lo), "wrong": wrong}
 
     # ---------------------------------------------------------------- bf16 pull
     def _build_f32_pack(self):
@@ -281,7 +330,7 @@ class ShardedParameterService:
     def sync_master(self):
         """Make the whole fp32 master current on every rank (checkpoints, PS snapshots, end-of-run checks):
         the full fp32 all-gather the bf16 pull skips every step. Collective."""
-        if self.world > 1 and self.master_stale:
+        if self.active and self.master_stale:
             self.store.wait_pending()
             self._pull(self.store.master)
             self.master_stale = False
@@ -301,11 +350,11 @@ class ShardedParameterService:
         # buckets of the last pull that no forward layer read: the optimizer below rewrites their owned slices
         self.store.wait_pending()
         reduce = None
-        if self.world > 1:
+        if self.active:
             def reduce(stats):
                 dist.all_reduce(stats, group=self.group)
         self.opt.step(grad_scale=1.0 / self.world, lr=lr, ranges=self.owned_ranges, stats_reduce=reduce)
-        if self.world > 1:
+        if self.active:
             if self.pull == "lowp":
                 self._pull_lowp()
             else:
@@ -374,16 +423,59 @@ class ShardedParameterService:
 
     def sync_state(self):
         """Kept for callers of the unsharded service: gather the owners' state onto every rank."""
-        if self.world == 1 or self.sharded:
+        if not self.active or self.sharded:
             return
         for t in self.opt.state_tensors():
             self._pull(t)
 
 
-def cast_bf16(g: torch.Tensor) -> torch.Tensor:
-    """fp32 -> bf16 copy of a gradient bucket (HIP kernel on the GPU)."""
+class CommBufferPool:
+    """Per-bucket bf16 send / receive buffers of the bf16 transports, allocated once and reused every step.
+
+    The transient form (a fresh ``torch.empty`` per bucket per step, kept alive for the side stream with
+    ``Tensor.record_stream``) makes the caching allocator hold every freed block until the HOST has seen an event
+    recorded on the side stream at free time: with the host a whole step ahead of the GPU, each step's buckets are
+    allocated anew, and under memory pressure through the out-of-memory release path (15x slower in the round-5
+    side-stream weight-gradient experiment, ``profiles/r05_notes.md``). Here a bucket's buffers live as long as the
+    reducer, and reuse is ordered on the device: ``release`` records an event on the stream of the buffers' last use
+    (the side stream, after the all-gather / owner sum that read them); ``acquire`` makes the acquiring stream wait
+    for it. Memory: one bf16 copy of the gradient per buffer kind -- the transient form held the same amount at the
+    end of backward, when every bucket is in flight. ``reserved_bytes`` is what the memory test pins."""
+
+    def __init__(self):
+        self.bufs: Dict[Tuple[int, str], torch.Tensor] = {}
+        self.free_ev: Dict[int, torch.cuda.Event] = {}
+
+    def acquire(self, key: int, n: int, device, kinds=("send", "recv")) -> List[torch.Tensor]:
+        out = []
+        for k in kinds:
+            t = self.bufs.get((key, k))
+            if t is None or t.numel() != n:
+                t = torch.empty(n, dtype=torch.bfloat16, device=device)
+                self.bufs[(key, k)] = t
+            out.append(t)
+        ev = self.free_ev.pop(key, None)
+        if ev is not None:
+            torch.cuda.current_stream(device).wait_event(ev)
+        return out
+
+    def release(self, key: int, stream) -> None:
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        self.free_ev[key] = ev
+
+    @property
+    def reserved_bytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in self.bufs.values())
+
+
+def cast_bf16(g: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 -> bf16 copy of a gradient bucket (HIP kernel on the GPU), into ``out`` when given."""
     if g.is_cuda:
-        return _load_ext().cast_bf16(g.contiguous())
+        return _load_ext().cast_bf16(g.contiguous(), out)
+    if out is not None:
+        out.copy_(g)
+        return out
     return g.to(torch.bfloat16)
 
 

@@ -17,6 +17,7 @@ from k8s_amd.parallel.flat import ParamStore  # noqa: E402
 
 def main():
     mode = sys.argv[1] if len(sys.argv) > 1 else "allreduce-fp32"
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     info = kdist.init_process_group()
     gpu = torch.cuda.is_available()
     dev = torch.device("cuda", info.device_index) if gpu else torch.device("cpu")  # CPU: a dry run of this script
@@ -42,13 +43,15 @@ def main():
             red.finish()
             opt.step(grad_scale=red.grad_scale)
     g = torch.Generator(device="cpu").manual_seed(100 + info.rank)  # different data per rank
-    for _ in range(3):
+    reserved = []  # caching-allocator reservation after each step: the bf16 transports must not grow it
+    for _ in range(steps):
         x = torch.randn(8, 32, 32, 3, generator=g).to(dev, torch.bfloat16 if gpu else torch.float32)
         y = torch.randint(0, 10, (8,), generator=g).to(dev)
         begin()
         loss = K.cross_entropy(model(model.prepare_input(x).contiguous()), y)
         loss.backward()
         finish()
+        reserved.append(torch.cuda.memory_reserved(dev) if gpu else 0)
     pull = "none"
     if mode.startswith("zero"):
         pull = svc.pull
@@ -62,9 +65,10 @@ def main():
     same = torch.tensor([int(torch.equal(state, ref))])
     torch.distributed.all_reduce(same, op=torch.distributed.ReduceOp.MIN)
     if info.rank == 0:
-        print("{\"replicas_identical\": %d, \"world\": %d, \"loss\": %.5f, \"pull\": \"%s\", \"wsum\": %r}"
-              % (int(same), info.world_size, float(loss.detach()), pull, float(store.master.double().sum())),
-              flush=True)
+        print("{\"replicas_identical\": %d, \"world\": %d, \"loss\": %.5f, \"pull\": \"%s\", \"wsum\": %r, "
+              "\"reserved\": %s}"
+              % (int(same), info.world_size, float(loss.detach()), pull, float(store.master.double().sum()),
+                 reserved), flush=True)
     kdist.destroy()
 
 

@@ -52,3 +52,14 @@ def test_bench_two_ranks_on_gpu():
     (r,) = _torchrun("bench.py", ["--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "16", "--image", "64"])
     assert r["n_gpus"] == 2 and r["dtype"] == "bf16" and r["config"]["parallelism"] == "dp2"
     assert r["config"]["global_batch"] == 32 and r["value"] > 0 and r["final_loss"] == r["final_loss"]
+
+
+@pytest.mark.parametrize("mode", ["zero-bf16", "allreduce-bf16"])
+def test_bf16_transport_memory_flat_on_gpu(mode):
+    """The bf16 transports reuse one send / recv buffer pair per bucket (``parallel/ps.py`` CommBufferPool) instead
+    of per-step allocations kept alive with ``record_stream``: the caching allocator's reservation is flat from the
+    second step to the tenth on the 2-rank path."""
+    (rec,) = _torchrun("tests/dist_gpu_worker.py", [mode, "10"])
+    assert rec["replicas_identical"] == 1
+    res = rec["reserved"]
+    assert len(res) == 10 and res[-1] == res[1], res
