@@ -16,7 +16,6 @@ import math
 from typing import Optional
 
 import torch
-from torch.autograd.graph import increment_version
 
 from k8s_amd.ops._ext import load as _load
 
@@ -110,12 +109,10 @@ class _FlashQKV(torch.autograd.Function):
         if pos is not None:
             if not rope_in_place:  # (in place: the caller's qkv is a temporary nothing else reads)
                 x = x.clone() if x.data_ptr() == qkv.data_ptr() else x
+            # (in place, the raw-pointer rotation does not bump autograd's version counter -- and cannot: qkv is
+            # the view output of the projection's custom Function, where autograd forbids in-place modification
+            # outright. Contract, see ``attention_qkv``: nothing else may hold the projection output.)
             C.rope_(x[:, : (H + Hkv) * D], pos, table, False)
-            if x.data_ptr() == qkv.data_ptr():
-                # the raw-pointer rotation does not bump autograd's version counter: bump it, so any other holder
-                # of the projection output saved for its backward (a hook, a saved ReLU y, a grad_link) fails loudly
-                # in backward instead of silently reading rotated values
-                increment_version(qkv)
         g = x.view(B, S, H + 2 * Hkv, D)
         q, k, v = g.narrow(2, 0, H), g.narrow(2, H, Hkv), g.narrow(2, H + Hkv, Hkv)
         o, lse = C.flash_fwd(q, k, v, causal, kv_lens, scale)
@@ -160,7 +157,9 @@ def attention_qkv(qkv, B: int, S: int, heads: int, kv_heads: int, head_dim: int,
     ``bias_link`` (``nn.BiasLink``, also given to the projection ``linear``): short sequences emit the projection's
     bias gradient from the attention backward, and the linear skips its column-sum pass. ``rope_in_place``: rotate
     q / k inside ``qkv`` itself instead of a copy (the caller's projection output is a temporary: Llama's 201 MB
-    per-layer clone at s4096 b4)."""
+    per-layer clone at s4096 b4). Contract of ``rope_in_place``: the projection output has no other reader --
+    no hook, no saved-for-backward reference (``_Linear`` saves its input, not its output), no ``grad_link`` --
+    since those would see the rotated values; ``tests/test_attention_gpu.py`` pins in place == copy bitwise."""
     D = head_dim
     scale = scale or 1.0 / math.sqrt(D)
     W = (heads + 2 * kv_heads) * D

@@ -357,10 +357,18 @@ class _BnReluConv(torch.autograd.Function):
         return (dx if ctx.x_requires_grad else None,) + (None,) * 11
 
 
+# Largest BatchNorm channel count normalised on load (K8S_AMD_ONLOAD_MAXC). The on-load operand path feeds the MFMAs
+# through VGPRs instead of the LDS-DMA path: in the compute-bound stage-3/4 1x1 products (bn2 of 256 / 512 channels)
+# it ran the conv3 forward and weight gradient at 0.19-0.33 of their floor against 0.41-0.52 for the same layers'
+# plain data gradient (profiles/r05_resnet50_roofline.jsonl), more than the [M, C/4] apply pass it saves. Round 6,
+# same box alternating (profiles/r06_notes.md): limit 128 +1.0-1.3 %, 256 +0.4-0.8 %, none = the round-5 default.
+ONLOAD_MAXC = int(os.environ.get("K8S_AMD_ONLOAD_MAXC", "128"))
+
+
 def onload_ok(x, conv) -> bool:
     """Whether ``conv`` can consume relu(BN(x)) normalised on load in all three of its products: a 1x1 stride-1
     convolution (the GEMM operand paths), or a 3x3 one the staged-window kernels take (``BN_ONLOAD == "3x3"``)."""
-    if BN_ONLOAD == "0":
+    if BN_ONLOAD == "0" or x.shape[-1] > ONLOAD_MAXC:
         return False
     K_, R, S, C = conv.w.shape
     if R == 1 and S == 1:
