@@ -33,6 +33,9 @@
 //    CU overlap their phases poorly. The swizzle, address and weight-ring changes above moved it by < 1 %.
 //  * epilogue: the bf16 tile goes through LDS, leaves as 16-B row segments, and the per-channel sum / sum of squares
 //    of the stored values are accumulated for the following BatchNorm (the [STAT_REPL][2][K] layout of gemm.hip).
+//  * per-tile prologue (round 6): only the padding positions are zeroed (enumerated, 2 iterations at 56 x 56 instead
+//    of a divide-and-test over all 12 window chunks per thread), the window and weight DMA addresses are a lane offset
+//    fixed per tile plus a wave-uniform offset: 3-8.5 % per layer (profiles/r06_conv3x3_lean.jsonl).
 //  * <= 80 KB LDS: 2 blocks per CU, so one block's window staging overlaps the other's MFMAs.
 //  * the per-tap barrier is a raw s_barrier after explicit waits (__syncthreads() adds a release fence, i.e.
 //    s_waitcnt vmcnt(0), which drained the in-flight weight tap every step): 2-5 % per layer (round 5).
@@ -117,22 +120,29 @@ __global__ void __launch_bounds__(THREADS, 2) conv3x3_kernel(const uint16_t* __r
     for (int j = 0; j < NF; ++j) acc[f][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   // the padding positions (everything that is not image data) are zeroed once; the DMA never writes them
-#pragma unroll 1
-  for (int c = tid; c < NPOS * 8; c += THREADS) {
-    const int q = (c >> 3) - 8;
-    if (q < 0 || q - q / WP * WP >= W || q >= (RT + 2) * WP)
-      *reinterpret_cast<bf16x8_t*>(win + c * 16) = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  constexpr int PADR = WP - W, NPAD = 8 + (RT + 2) * PADR;  // 8 leading positions + PADR after every window row
+#pragma unroll
+  for (int t0 = 0; t0 < NPAD * 8; t0 += THREADS) {  // only the padding positions, enumerated
+    const int t = t0 + tid, pi = t >> 3;
+    if (t < NPAD * 8) {
+      const int r = (pi - 8) / PADR;
+      const int pos = pi < 8 ? pi : 8 + r * WP + W + (pi - 8 - r * PADR);
+      *reinterpret_cast<bf16x8_t*>(win + (pos * 8 + (t & 7)) * 16) = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
   }
   // window DMA: row wr, instruction i covers positions wr * WP + 8 + 8 i + [0, 8) (lane-linear 16-B pieces); the
   // logical chunk of a lane is fixed because every instruction's first position is a multiple of 8
   constexpr int IPR = (W * 8 + 63) / 64, NWI = (RT + 2) * IPR;
   const int lch = (lane & 7) ^ ((lane >> 3) & 6);
+  // the lane's part of the address is fixed per tile (image n, pixel lane >> 3, chunk lch); per instruction only
+  // a wave-uniform row / pixel-group offset is added
+  const uint16_t* const xlane = x + ((long)n * H * W + (lane >> 3)) * C + lch * 8;
   auto load_window = [&](int c0) {
 #pragma unroll 1
-    for (int wi = wid; wi < NWI; wi += THREADS / 64) {
-      const int wr = wi / IPR, i = wi - wr * IPR, px = i * 8 + (lane >> 3), h = h0 - 1 + wr;
-      if (px < W) {
-        const void* src = (unsigned)h < (unsigned)H ? (const void*)(x + (((long)n * H + h) * W + px) * C + c0 + lch * 8)
+    for (int wi = wid; wi < NWI; wi += THREADS / 64) {  // wave-uniform
+      const int wr = wi / IPR, i = wi - wr * IPR, h = h0 - 1 + wr;
+      if (i * 8 + (lane >> 3) < W) {
+        const void* src = (unsigned)h < (unsigned)H ? (const void*)(xlane + (h * W + i * 8) * C + c0)
                                                     : (const void*)g_c3_zero;
         glds16(src, win + (wr * WP + 8 + i * 8) * 128);
       }
@@ -160,12 +170,18 @@ __global__ void __launch_bounds__(THREADS, 2) conv3x3_kernel(const uint16_t* __r
     }
     __syncthreads();
   };
+  // per-thread weight source offsets (row k0 + row, chunk lc) computed once; a tap adds a uniform offset
+  uint32_t wlane[WOPS];  // byte offsets (32-bit: the tap's uniform base + a lane offset, the saddr load form)
+#pragma unroll
+  for (int i = 0; i < WOPS; ++i) {
+    const int c = i * THREADS + tid, row = c >> 3, lc = (c & 7) ^ swz(row);
+    wlane[i] = (uint32_t)(((k0 + row) * 9 * C + lc * 8) * 2);
+  }
   auto stage_w = [&](int tap, int c0, int slot) {
     char* d = smem + G::WIN_B + slot * G::WT_B;
 #pragma unroll
     for (int i = 0; i < WOPS; ++i) {
-      const int c = i * THREADS + tid, row = c >> 3, lc = (c & 7) ^ swz(row);
-      glds16(wt + ((long)(k0 + row) * 9 + tap) * C + c0 + lc * 8, d + (i * THREADS + wid * 64) * 16);
+      glds16(reinterpret_cast<const char*>(wt + tap * C + c0) + wlane[i], d + (i * THREADS + wid * 64) * 16);
     }
   };
   // steps g = slice * 9 + 3 ds + dr visit the taps ds-major; tap_of(k) for k = g % 9

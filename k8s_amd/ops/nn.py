@@ -363,6 +363,9 @@ class _BnReluConv(torch.autograd.Function):
 # plain data gradient (profiles/r05_resnet50_roofline.jsonl), more than the [M, C/4] apply pass it saves. Round 6,
 # same box alternating (profiles/r06_notes.md): limit 128 +1.0-1.3 %, 256 +0.4-0.8 %, none = the round-5 default.
 ONLOAD_MAXC = int(os.environ.get("K8S_AMD_ONLOAD_MAXC", "128"))
+# bn1 normalised on load by the staged-window 3x3 kernels up to this many channels (K8S_AMD_ONLOAD3_MAXC; 0 = only
+# with BN_ONLOAD == "3x3")
+ONLOAD3_MAXC = int(os.environ.get("K8S_AMD_ONLOAD3_MAXC", "0"))
 
 
 def onload_ok(x, conv) -> bool:
@@ -373,7 +376,7 @@ def onload_ok(x, conv) -> bool:
     K_, R, S, C = conv.w.shape
     if R == 1 and S == 1:
         return conv.stride == 1 and conv.pad == 0
-    return (BN_ONLOAD == "3x3" and x.dim() == 4 and
+    return ((BN_ONLOAD == "3x3" or x.shape[-1] <= ONLOAD3_MAXC) and x.dim() == 4 and
             bool(_C().conv3x3_staged_ok(x.shape[1], x.shape[2], C, K_, R, S, conv.stride, conv.pad)))
 
 

@@ -52,6 +52,8 @@ def main():
         # arms: the staged-window kernel, the implicit GEMM (round 5 also timed a persistent pipelined form, "c3p":
         # profiles/r05_conv3x3_c3p_ab.jsonl)
         arms = {"staged": ("1", "0"), "implicit": ("0", "0")}
+        # (round 6 timed the lean prologue against the round-5 kernel with these arms: profiles/r06_conv3x3_lean.jsonl,
+        # "staged" = lean, "implicit" = round 5)
         for form, fn in forms.items():
             t = {k: [] for k in arms}
             for _ in range(a.rounds):
