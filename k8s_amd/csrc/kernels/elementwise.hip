@@ -20,15 +20,19 @@ __device__ __forceinline__ float ftanh(float u) {
 // gu: [T, 2F] (gate in [:, :F], up in [:, F:]) -> y: [T, F]
 // Flat launches, one 16-B vector per thread: grid (T rows, F/8 / 256 column blocks), so no 64-bit index division
 // (the former grid-stride form divided by F/8 per vector)
+// gu column layout: blk == 0 -> [gate F | up F]; blk > 0 -> blocks of blk gate columns then blk up columns (the layout
+// the gate|up GEMM's fused SwiGLU epilogue produces, gemm256.hip copy_out_swiglu): gate j at (j / blk) 2 blk + j % blk
+__device__ __forceinline__ int swiglu_gcol(int c, int F, int blk) { return blk ? (c / blk) * 2 * blk + c % blk : c; }
+
 __global__ void __launch_bounds__(256) swiglu_fwd_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ y,
-                                                         long T, int F) {
+                                                         long T, int F, int blk) {
   const int cvec = blockIdx.y * 256 + threadIdx.x;
   if (cvec >= F / 8) return;
   const long t = blockIdx.x;
-  const int c = cvec * 8;
+  const int c = cvec * 8, gc = swiglu_gcol(c, F, blk), uo = blk ? blk : F;
   float g[8], u[8], o[8];
-  load8(gu + t * 2 * F + c, g);
-  load8(gu + t * 2 * F + F + c, u);
+  load8(gu + t * 2 * F + gc, g);
+  load8(gu + t * 2 * F + gc + uo, u);
 #pragma unroll
   for (int j = 0; j < 8; ++j) o[j] = silu(g[j]) * u[j];
   store8(y + t * F + c, o);
@@ -37,14 +41,14 @@ __global__ void __launch_bounds__(256) swiglu_fwd_kernel(const uint16_t* __restr
 // dgu[:, :F] = dy * u * silu'(g),  dgu[:, F:] = dy * silu(g)
 __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restrict__ gu,
                                                          const uint16_t* __restrict__ dy, uint16_t* __restrict__ dgu,
-                                                         long T, int F) {
+                                                         long T, int F, int blk) {
   const int cvec = blockIdx.y * 256 + threadIdx.x;
   if (cvec >= F / 8) return;
   const long t = blockIdx.x;
-  const int c = cvec * 8;
+  const int c = cvec * 8, gc = swiglu_gcol(c, F, blk), uo = blk ? blk : F;
   float g[8], u[8], d[8], dg[8], du[8];
-  load8(gu + t * 2 * F + c, g);
-  load8(gu + t * 2 * F + F + c, u);
+  load8(gu + t * 2 * F + gc, g);
+  load8(gu + t * 2 * F + gc + uo, u);
   load8(dy + t * F + c, d);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -53,8 +57,8 @@ __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restr
     du[j] = d[j] * sl;
     dg[j] = d[j] * u[j] * (s * (1.f + g[j] * (1.f - s)));
   }
-  store8(dgu + t * 2 * F + c, dg);
-  store8(dgu + t * 2 * F + F + c, du);
+  store8(dgu + t * 2 * F + gc, dg);
+  store8(dgu + t * 2 * F + gc + uo, du);
 }
 
 // x: [T, H, D] bf16 (row stride ld elements between tokens), pos: [T] int32, table: [maxpos, D/2] (cos, sin)
@@ -78,8 +82,8 @@ __global__ void __launch_bounds__(256) rope_kernel(uint16_t* __restrict__ x, lon
     for (int j = 0; j < 8; ++j) {
       const float cs = tb[j].x, sn = sign * tb[j].y;
       const float x1 = a[j], x2 = b[j];
-      a[j] = x1 * cs - x2 * sn;
-      b[j] = x2 * cs + x1 * sn;
+      a[j] = __builtin_fmaf(x1, cs, -(x2 * sn));  // explicit fmas: the rounding gemm256.hip copy_out_rope repeats
+      b[j] = __builtin_fmaf(x2, cs, x1 * sn);
     }
     store8(row + c, a);
     store8(row + half + c, b);
@@ -251,11 +255,11 @@ __global__ void __launch_bounds__(256) colsum_fold_kernel(const float* part, int
 }
 
 // ----------------------------------------------------------------------------- launchers
-void launch_swiglu_fwd(const uint16_t* gu, uint16_t* y, long T, int F, hipStream_t st) {
-  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(T, cdiv(F / 8, 256)), dim3(256), 0, st, gu, y, T, F);
+void launch_swiglu_fwd(const uint16_t* gu, uint16_t* y, long T, int F, int blk, hipStream_t st) {
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(T, cdiv(F / 8, 256)), dim3(256), 0, st, gu, y, T, F, blk);
 }
-void launch_swiglu_bwd(const uint16_t* gu, const uint16_t* dy, uint16_t* dgu, long T, int F, hipStream_t st) {
-  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(T, cdiv(F / 8, 256)), dim3(256), 0, st, gu, dy, dgu, T, F);
+void launch_swiglu_bwd(const uint16_t* gu, const uint16_t* dy, uint16_t* dgu, long T, int F, int blk, hipStream_t st) {
+  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(T, cdiv(F / 8, 256)), dim3(256), 0, st, gu, dy, dgu, T, F, blk);
 }
 void launch_rope(uint16_t* x, long ld, const int* pos, const float* table, long T, int H, int D, bool inverse,
                  hipStream_t st) {

@@ -733,6 +733,78 @@ __device__ __forceinline__ void copy_out_x(uint16_t* __restrict__ C, uint16_t* _
   }
 }
 
+// ACT = 3: the gate|up projection with its SwiGLU in the epilogue (Llama). The weight's rows are laid out in blocks of
+// 128 gate rows then the 128 matching up rows, so a 256-wide output tile holds gate block t in waves (wr, 0) and up
+// block t in waves (wr, 1), for the same rows. Every wave stores its own staged piece to C (= gu [M][2F], what the
+// backward reads); after a barrier, waves (wr, 0) / (wr, 1) take rows 0-63 / 64-127 of the pair's 128 and write
+// h = silu(g) u (elementwise.hip swiglu_fwd_kernel's formula on the same bf16 inputs: bit-identical) from both staged
+// pieces to `hout` [M][F] at column n0 / 2 -- the separate SwiGLU pass (read gu, write h) is gone.
+template <class Off, class Stg>
+__device__ __forceinline__ void copy_out_swiglu(uint16_t* __restrict__ C, uint16_t* __restrict__ hout, const char* smem,
+                                                const Off& coff, const Stg& staged, int m0, int n0, int wr, int wc,
+                                                int N) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll 4
+  for (int it = 0; it < 32; ++it) *reinterpret_cast<bf16x8_t*>(C + coff(it)) = staged(it);
+  g256::barrier();  // every wave's piece staged (each waited for its own LDS writes before the copy above)
+  const char* sg = smem + (2 * wr) * 32768;
+  const char* su = smem + (2 * wr + 1) * 32768;
+  const long F = N / 2;
+#pragma unroll 4
+  for (int it = 0; it < 16; ++it) {
+    const int idx = it * 64 + lane, lr = wc * 64 + (idx >> 4), ch = idx & 15;
+    const int o = lr * 256 + ((ch ^ (lr & 15)) << 4);
+    const bf16x8_t g = *reinterpret_cast<const bf16x8_t*>(sg + o), u = *reinterpret_cast<const bf16x8_t*>(su + o);
+    float h[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const float gg = bf2f((uint16_t)g[r]);
+      h[r] = gg * __builtin_amdgcn_rcpf(1.f + __expf(-gg)) * bf2f((uint16_t)u[r]);
+    }
+    *reinterpret_cast<bf16x8_t*>(hout + (long)(m0 + wr * 128 + lr) * F + n0 / 2 + ch * 8) = pack_bf16x8(h);
+  }
+}
+
+// ACT = 4: the QKV projection with the rotary embedding of its q / k heads in the copy-out (Llama). A wave's staged
+// 128 columns are exactly one head of D = 128; the rotate-half partner of chunk ch (8 columns) is chunk ch ^ 8 of the
+// same staged row, the angle table row is pos[row]. elementwise.hip rope_kernel's formula (explicit fmas, the same
+// rounding), so the fused output is bit-identical to the projection + the in-place rope pass it replaces. `rot`: this
+// wave's head is a q / k head (columns < rcols); the v heads are stored as staged.
+template <class Off>
+__device__ __forceinline__ void copy_out_rope(uint16_t* __restrict__ C, const char* stg, const Off& coff, int row0,
+                                              bool rot, const int* __restrict__ rpos, const float* __restrict__ rtab) {
+  const int lane = threadIdx.x & 63;
+  if (!rot) {
+#pragma unroll 4
+    for (int it = 0; it < 32; ++it) {
+      const int idx = it * 64 + lane, lr = idx >> 4, ch = idx & 15;
+      *reinterpret_cast<bf16x8_t*>(C + coff(it)) =
+          *reinterpret_cast<const bf16x8_t*>(stg + lr * 256 + ((ch ^ (lr & 15)) << 4));
+    }
+    return;
+  }
+#pragma unroll 2
+  for (int it = 0; it < 32; ++it) {
+    const int idx = it * 64 + lane, lr = idx >> 4, ch = idx & 15;
+    const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(stg + lr * 256 + ((ch ^ (lr & 15)) << 4));
+    const bf16x8_t w = *reinterpret_cast<const bf16x8_t*>(stg + lr * 256 + (((ch ^ 8) ^ (lr & 15)) << 4));
+    const f32x4_t* tb = reinterpret_cast<const f32x4_t*>(rtab + ((long)rpos[row0 + lr] * 64 + (ch & 7) * 8) * 2);
+    float o[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4_t t = tb[q];  // (cos, sin) of elements 2q, 2q + 1
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const float cs = t[2 * e], sn = t[2 * e + 1];
+        const float a = bf2f((uint16_t)v[2 * q + e]), b = bf2f((uint16_t)w[2 * q + e]);
+        // first half: x1 c - x2 s (a = x1, b = x2); second half: x2 c + x1 s (a = x2, b = x1)
+        o[2 * q + e] = ch < 8 ? __builtin_fmaf(a, cs, -(b * sn)) : __builtin_fmaf(a, cs, b * sn);
+      }
+    }
+    *reinterpret_cast<bf16x8_t*>(C + coff(it)) = pack_bf16x8(o);
+  }
+}
+
 template <bool AMN, bool BMN, bool X>
 __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __restrict__ A, long lda,
                                                              const uint16_t* __restrict__ B, long ldb, void* Cv,
@@ -740,7 +812,8 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
                                                              g256r::SkArgs SK, int out_f32, int accumulate,
                                                              const float* __restrict__ bias, int act,
                                                              uint16_t* __restrict__ pre, long slab,
-                                                             float* __restrict__ cpart) {
+                                                             float* __restrict__ cpart, const int* __restrict__ rpos,
+                                                             const float* __restrict__ rtab, int rcols) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1076,12 +1149,23 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
       if constexpr (!AMN && BMN) {
         if (act == -3) {  // SwiGLU backward: no column sums; the up half `slab` columns to the right
           copy_out_x<-3, false>(C, pre, stg, coff, staged, nullptr, slab);
+        } else if (act == -4) {  // the same on the 128-blocked gate|up layout (copy_out_swiglu): this wave's 128
+                                 // columns j0.. are gate columns 2 j0.., their up columns 128 further
+          auto coff_b = [&](int it) {
+            const int idx = it * 64 + lane, lr = idx >> 4, ch = idx & 15;
+            return (long)(m0 + wr * 128 + lr) * ldc + 2 * (n0 + wc * 128) + ch * 8;
+          };
+          copy_out_x<-3, false>(C, pre, stg, coff_b, staged, nullptr, 128);
         } else {
           float* const cp = cpart + (long)((m0 >> 8) * 2 + wr) * N + n0 + wc * 128;
           if (act == -2) copy_out_x<-2, false>(C, pre, stg, coff, staged, cp);
           else copy_out_x<-1, false>(C, pre, stg, coff, staged, cp);
         }
       }
+    } else if (act == 3) {
+      copy_out_swiglu(C, pre, smem, coff, staged, m0, n0, wr, wc, N);
+    } else if (act == 4) {
+      copy_out_rope(C, stg, coff, m0 + wr * 128, n0 + wc * 128 < rcols, rpos, rtab);
     } else if (act == 2) {
       if (accumulate) copy_out_x<2, true>(C, pre, stg, coff, staged); else copy_out_x<2, false>(C, pre, stg, coff, staged);
     } else if (act == 1) {
@@ -1144,7 +1228,8 @@ void launch_gemm_w4_dact(const uint16_t* A, long lda, const uint16_t* B, long ld
     blocks = plan.full + (tiles - plan.full) * plan.sk;
   }
   hipLaunchKernelGGL((g4::gemm_w4_kernel<false, true, true>), dim3(blocks), dim3(g4::THREADS), 0, st, A, lda, B, ldb,
-                     (void*)C, ldc, M, N, K, 1.f, kps, sk, 0, 0, nullptr, -act, const_cast<uint16_t*>(pre), 0L, part);
+                     (void*)C, ldc, M, N, K, 1.f, kps, sk, 0, 0, nullptr, -act, const_cast<uint16_t*>(pre), 0L, part,
+                     nullptr, nullptr, 0);
   launch_colsum_fold(part, M / 128, N, db, db_accumulate, st);
 }
 
@@ -1154,8 +1239,9 @@ bool gemm_w4_swiglu_ok(int M, int F, int K, long lda, long ldb) {
   return gemm_w4_dact_ok(M, F, K, lda, ldb, 2L * F);
 }
 void launch_gemm_w4_swiglu_bwd(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* dgu,
-                               const uint16_t* gu, int M, int F, int K, float* sk_slabs, int* sk_sync, hipStream_t st) {
-  if (!gemm_w4_swiglu_ok(M, F, K, lda, ldb))
+                               const uint16_t* gu, int M, int F, int K, int blk, float* sk_slabs, int* sk_sync,
+                               hipStream_t st) {
+  if (!gemm_w4_swiglu_ok(M, F, K, lda, ldb) || (blk != 0 && blk != 128))
     throw std::runtime_error("gemm_w4_swiglu_bwd: shape outside the 4-wave kernel's contract");
   Gemm256Plan plan = gemm256_plan(M, F, K);
   if (!sk_slabs || !sk_sync) plan.sk = 1;
@@ -1167,10 +1253,62 @@ void launch_gemm_w4_swiglu_bwd(const uint16_t* A, long lda, const uint16_t* B, l
     kps = plan.kps;
     blocks = plan.full + (tiles - plan.full) * plan.sk;
   }
-  // C = dgu (row stride 2F, gate half at column 0), pre = gu, slab = F: the up half's column offset
+  // C = dgu (row stride 2F, gate half at column 0), pre = gu, slab = F: the up half's column offset (blk = 128: the
+  // blocked layout, act -4)
   hipLaunchKernelGGL((g4::gemm_w4_kernel<false, true, true>), dim3(blocks), dim3(g4::THREADS), 0, st, A, lda, B, ldb,
-                     (void*)dgu, 2L * F, M, F, K, 1.f, kps, sk, 0, 0, nullptr, -3, const_cast<uint16_t*>(gu), (long)F,
-                     nullptr);
+                     (void*)dgu, 2L * F, M, F, K, 1.f, kps, sk, 0, 0, nullptr, blk ? -4 : -3,
+                     const_cast<uint16_t*>(gu), (long)F, nullptr, nullptr, nullptr, 0);
+}
+
+// Llama's gate|up projection with the SwiGLU in the epilogue (copy_out_swiglu): gu [M][2F] = A [M][K] . B [2F][K]^T
+// (both K-major; B's rows in the 128-blocked gate|up order) and h [M][F] = silu(gate) up. Whole 256 x 256 tiles.
+bool gemm_w4_swiglu_fwd_ok(int M, int F, int K, long lda, long ldb) {
+  return w4_enabled() && M % 256 == 0 && F % 128 == 0 && K % 64 == 0 && (lda | ldb) % 8 == 0 &&
+         (long)(M / 256) * (2 * F / 256) >= planner_cus();
+}
+void launch_gemm_w4_swiglu_fwd(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* gu, uint16_t* h,
+                               int M, int F, int K, float* sk_slabs, int* sk_sync, hipStream_t st) {
+  if (!gemm_w4_swiglu_fwd_ok(M, F, K, lda, ldb))
+    throw std::runtime_error("gemm_w4_swiglu_fwd: shape outside the 4-wave kernel's contract");
+  const int N = 2 * F;
+  Gemm256Plan plan = gemm256_plan(M, N, K);
+  if (!sk_slabs || !sk_sync) plan.sk = 1;
+  const int tiles = (M / 256) * (N / 256);
+  g256r::SkArgs sk{tiles, 1, nullptr, nullptr};
+  int blocks = tiles, kps = K;
+  if (plan.sk > 1) {
+    sk = g256r::SkArgs{plan.full, plan.sk, sk_slabs, sk_sync};
+    kps = plan.kps;
+    blocks = plan.full + (tiles - plan.full) * plan.sk;
+  }
+  hipLaunchKernelGGL((g4::gemm_w4_kernel<false, false, true>), dim3(blocks), dim3(g4::THREADS), 0, st, A, lda, B, ldb,
+                     (void*)gu, (long)N, M, N, K, 1.f, kps, sk, 0, 0, nullptr, 3, h, 0L, nullptr, nullptr, nullptr, 0);
+}
+
+// Llama's QKV projection with the rotary embedding of the q / k heads (columns < rot_cols, head dim 128) in the
+// copy-out (copy_out_rope): y [M][N] = A [M][K] . B [N][K]^T, both K-major; pos [M] int32, table [maxpos][64][2].
+bool gemm_w4_rope_ok(int M, int N, int K, long lda, long ldb, int rot_cols) {
+  return w4_enabled() && M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && (lda | ldb) % 8 == 0 && rot_cols % 128 == 0 &&
+         rot_cols <= N && (long)(M / 256) * (N / 256) >= planner_cus();
+}
+void launch_gemm_w4_rope(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* y, int M, int N, int K,
+                         const int* pos, const float* table, int rot_cols, float* sk_slabs, int* sk_sync,
+                         hipStream_t st) {
+  if (!gemm_w4_rope_ok(M, N, K, lda, ldb, rot_cols))
+    throw std::runtime_error("gemm_w4_rope: shape outside the 4-wave kernel's contract");
+  Gemm256Plan plan = gemm256_plan(M, N, K);
+  if (!sk_slabs || !sk_sync) plan.sk = 1;
+  const int tiles = (M / 256) * (N / 256);
+  g256r::SkArgs sk{tiles, 1, nullptr, nullptr};
+  int blocks = tiles, kps = K;
+  if (plan.sk > 1) {
+    sk = g256r::SkArgs{plan.full, plan.sk, sk_slabs, sk_sync};
+    kps = plan.kps;
+    blocks = plan.full + (tiles - plan.full) * plan.sk;
+  }
+  hipLaunchKernelGGL((g4::gemm_w4_kernel<false, false, true>), dim3(blocks), dim3(g4::THREADS), 0, st, A, lda, B, ldb,
+                     (void*)y, (long)N, M, N, K, 1.f, kps, sk, 0, 0, nullptr, 4, nullptr, 0L, nullptr, pos, table,
+                     rot_cols);
 }
 
 // Stream-K tail plan for a grid of 256 x 256 tiles on P = planner_cus() CUs (one block per CU; 256 on MI355X): with
@@ -1285,7 +1423,8 @@ void launch_gemm256(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* 
     const int acc = splits > 1 ? 0 : (accumulate ? 1 : 0);
 #define K8S_W4L(AM, BM, XX)                                                                                         \
   hipLaunchKernelGGL((g4::gemm_w4_kernel<AM, BM, XX>), dim3(blocks, ysplits), dim3(g4::THREADS), 0, st, A, lda, B, \
-                     ldb, cv, ldc, M, N, K, alpha, kps, sk, c_f32 ? 1 : 0, acc, bias, act, pre, (long)M * N, nullptr)
+                     ldb, cv, ldc, M, N, K, alpha, kps, sk, c_f32 ? 1 : 0, acc, bias, act, pre, (long)M * N, nullptr,   \
+                     nullptr, nullptr, 0)
 #define K8S_W4X(AM, BM)       \
   do {                        \
     if (x)                    \

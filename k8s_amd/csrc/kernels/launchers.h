@@ -109,7 +109,15 @@ void launch_gemm_w4_dact(const uint16_t* A, long lda, const uint16_t* B, long ld
 // the down-projection data gradient fused with the SwiGLU backward: dgu [M][2F] (gemm256.hip copy_out_x ACT = -3)
 bool gemm_w4_swiglu_ok(int M, int F, int K, long lda, long ldb);
 void launch_gemm_w4_swiglu_bwd(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* dgu,
-                               const uint16_t* gu, int M, int F, int K, float* sk_slabs, int* sk_sync, hipStream_t st);
+                               const uint16_t* gu, int M, int F, int K, int blk, float* sk_slabs, int* sk_sync,
+                               hipStream_t st);
+bool gemm_w4_rope_ok(int M, int N, int K, long lda, long ldb, int rot_cols);
+void launch_gemm_w4_rope(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* y, int M, int N, int K,
+                         const int* pos, const float* table, int rot_cols, float* sk_slabs, int* sk_sync,
+                         hipStream_t st);
+bool gemm_w4_swiglu_fwd_ok(int M, int F, int K, long lda, long ldb);
+void launch_gemm_w4_swiglu_fwd(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* gu, uint16_t* h,
+                               int M, int F, int K, float* sk_slabs, int* sk_sync, hipStream_t st);
 // stream-K tail plan (gemm256.hip): tiles [full, tiles) are split sk ways along K (sk == 1: none), kps deep each
 struct Gemm256Plan {
   int tiles, full, sk, kps;
@@ -149,8 +157,8 @@ void launch_conv_dgrad_wsub(const uint16_t* w, uint16_t* out, int K, int RS, int
                             hipStream_t st);
 
 // elementwise.hip
-void launch_swiglu_fwd(const uint16_t* gu, uint16_t* y, long T, int F, hipStream_t st);
-void launch_swiglu_bwd(const uint16_t* gu, const uint16_t* dy, uint16_t* dgu, long T, int F, hipStream_t st);
+void launch_swiglu_fwd(const uint16_t* gu, uint16_t* y, long T, int F, int blk, hipStream_t st);
+void launch_swiglu_bwd(const uint16_t* gu, const uint16_t* dy, uint16_t* dgu, long T, int F, int blk, hipStream_t st);
 void launch_rope(uint16_t* x, long ld, const int* pos, const float* table, long T, int H, int D, bool inverse,
                  hipStream_t st);
 void launch_gelu_bwd(const uint16_t* dy, const uint16_t* pre, uint16_t* dx, long n, hipStream_t st);

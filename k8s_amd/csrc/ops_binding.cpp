@@ -562,7 +562,7 @@ Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tens
 bool gemm_swiglu_bwd_ok(int64_t M, int64_t F, int64_t K) {
   return k8s_amd::gemm_w4_swiglu_ok((int)M, (int)F, (int)K, K, F);
 }
-Tensor gemm_swiglu_bwd(Tensor g, Tensor w, Tensor gu) {
+Tensor gemm_swiglu_bwd(Tensor g, Tensor w, Tensor gu, int64_t blk) {
   check_bf16_operand(g, "g");
   check_bf16_operand(w, "w");
   check_bf16_operand(gu, "gu");
@@ -579,9 +579,67 @@ Tensor gemm_swiglu_bwd(Tensor g, Tensor w, Tensor gu) {
     slabs = torch::empty({k8s_amd::gemm256_sk_slab_floats(plan)}, g.options().dtype(at::kFloat));
     sync = sk_sync_words(k8s_amd::gemm256_sk_sync_ints(plan), g.device());
   }
+  TORCH_CHECK(blk == 0 || blk == 128, "gemm_swiglu_bwd: blk is 0 (gate | up halves) or 128 (blocked layout)");
   k8s_amd::launch_gemm_w4_swiglu_bwd(cbf(g), g.stride(0), cbf(w), w.stride(0), bf(dgu), cbf(gu), (int)M, (int)F,
-                                     (int)K, sync ? f32(slabs) : nullptr, sync, cur_stream());
+                                     (int)K, (int)blk, sync ? f32(slabs) : nullptr, sync, cur_stream());
   return dgu;
+}
+
+// Llama's QKV projection with the rotary embedding of its q / k heads (the first rot_cols columns, head dim 128) in
+// the epilogue: y [M, N] = x [M, K] . w [N, K]^T, pos [M] int32, table [maxpos, 64, 2] fp32 (gemm256.hip copy_out_rope)
+bool gemm_rope_ok(int64_t M, int64_t N, int64_t K, int64_t rot_cols) {
+  return k8s_amd::gemm_w4_rope_ok((int)M, (int)N, (int)K, K, K, (int)rot_cols);
+}
+Tensor gemm_rope(Tensor x, Tensor w, Tensor pos, Tensor table, int64_t rot_cols) {
+  check_bf16_operand(x, "x");
+  check_bf16_operand(w, "w");
+  const long M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && x.stride(1) == 1 && w.stride(1) == 1, "x [M, K] . w [N, K]^T, row-major");
+  TORCH_CHECK(pos.is_cuda() && pos.scalar_type() == at::kInt && pos.is_contiguous() && pos.numel() == M, "pos: [M] int32");
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kFloat && table.is_contiguous() && table.dim() == 3 &&
+                  table.size(1) == 64 && table.size(2) == 2, "table: [maxpos, 64, 2] fp32 (head dim 128)");
+  TORCH_CHECK(k8s_amd::gemm_w4_rope_ok((int)M, (int)N, (int)K, x.stride(0), w.stride(0), (int)rot_cols),
+              "gemm_rope: shape outside the 4-wave kernel's contract");
+  Tensor y = torch::empty({M, N}, x.options());
+  const k8s_amd::Gemm256Plan plan = k8s_amd::gemm256_plan((int)M, (int)N, (int)K);
+  Tensor slabs;
+  int* sync = nullptr;
+  if (plan.sk > 1) {
+    slabs = torch::empty({k8s_amd::gemm256_sk_slab_floats(plan)}, x.options().dtype(at::kFloat));
+    sync = sk_sync_words(k8s_amd::gemm256_sk_sync_ints(plan), x.device());
+  }
+  k8s_amd::launch_gemm_w4_rope(cbf(x), x.stride(0), cbf(w), w.stride(0), bf(y), (int)M, (int)N, (int)K,
+                               pos.data_ptr<int>(), f32(table), (int)rot_cols, sync ? f32(slabs) : nullptr, sync,
+                               cur_stream());
+  return y;
+}
+
+// Llama's gate|up projection with the SwiGLU in the epilogue: returns (gu [M, 2F], h [M, F] = silu(gate) up) from
+// x [M, K] bf16 and w [2F, K] bf16 whose rows are in the 128-blocked gate|up order (gemm256.hip copy_out_swiglu).
+bool gemm_swiglu_fwd_ok(int64_t M, int64_t F, int64_t K) {
+  return k8s_amd::gemm_w4_swiglu_fwd_ok((int)M, (int)F, (int)K, K, K);
+}
+std::vector<Tensor> gemm_swiglu_fwd(Tensor x, Tensor w) {
+  check_bf16_operand(x, "x");
+  check_bf16_operand(w, "w");
+  const long M = x.size(0), K = x.size(1), F2 = w.size(0);
+  TORCH_CHECK(w.size(1) == K && F2 % 2 == 0, "x [M, K] . w [2F, K]^T");
+  TORCH_CHECK(x.stride(1) == 1 && w.stride(1) == 1, "x and w must be row-major");
+  const long F = F2 / 2;
+  TORCH_CHECK(k8s_amd::gemm_w4_swiglu_fwd_ok((int)M, (int)F, (int)K, x.stride(0), w.stride(0)),
+              "gemm_swiglu_fwd: shape outside the 4-wave kernel's contract");
+  Tensor gu = torch::empty({M, F2}, x.options());
+  Tensor h = torch::empty({M, F}, x.options());
+  const k8s_amd::Gemm256Plan plan = k8s_amd::gemm256_plan((int)M, (int)F2, (int)K);
+  Tensor slabs;
+  int* sync = nullptr;
+  if (plan.sk > 1) {
+    slabs = torch::empty({k8s_amd::gemm256_sk_slab_floats(plan)}, x.options().dtype(at::kFloat));
+    sync = sk_sync_words(k8s_amd::gemm256_sk_sync_ints(plan), x.device());
+  }
+  k8s_amd::launch_gemm_w4_swiglu_fwd(cbf(x), x.stride(0), cbf(w), w.stride(0), bf(gu), bf(h), (int)M, (int)F, (int)K,
+                                     sync ? f32(slabs) : nullptr, sync, cur_stream());
+  return {gu, h};
 }
 
 // the producing linear's bias gradient in the 4-wave GEMM's epilogue (gemm256.hip copy_out_x, ACT < 0).
@@ -729,7 +787,7 @@ Tensor conv_dgrad_wtrans(Tensor w) {
 }
 
 // ------------------------------------------------------------------ elementwise (K9)
-Tensor swiglu_fwd(Tensor gu) {
+Tensor swiglu_fwd(Tensor gu, int64_t blk) {
   check_cuda(gu, "gu"); check_dtype(gu, at::kBFloat16, "gu");
   const long F2 = gu.size(-1);
   TORCH_CHECK(F2 % 16 == 0, "2F must be a multiple of 16");
@@ -737,15 +795,17 @@ Tensor swiglu_fwd(Tensor gu) {
   auto sizes = gu.sizes().vec();
   sizes.back() = F2 / 2;
   auto y = torch::empty(sizes, gu.options());
-  k8s_amd::launch_swiglu_fwd(cbf(gu), bf(y), T, (int)(F2 / 2), cur_stream());
+  TORCH_CHECK(blk == 0 || (blk % 8 == 0 && (F2 / 2) % blk == 0), "swiglu: blk must divide F (multiple of 8)");
+  k8s_amd::launch_swiglu_fwd(cbf(gu), bf(y), T, (int)(F2 / 2), (int)blk, cur_stream());
   return y;
 }
-Tensor swiglu_bwd(Tensor gu, Tensor dy) {
+Tensor swiglu_bwd(Tensor gu, Tensor dy, int64_t blk) {
   check_cuda(gu, "gu"); check_cuda(dy, "dy");
   const long F2 = gu.size(-1);
   TORCH_CHECK(dy.numel() * 2 == gu.numel());
   auto dgu = torch::empty_like(gu);
-  k8s_amd::launch_swiglu_bwd(cbf(gu), cbf(dy), bf(dgu), gu.numel() / F2, (int)(F2 / 2), cur_stream());
+  TORCH_CHECK(blk == 0 || (blk % 8 == 0 && (F2 / 2) % blk == 0), "swiglu: blk must divide F (multiple of 8)");
+  k8s_amd::launch_swiglu_bwd(cbf(gu), cbf(dy), bf(dgu), gu.numel() / F2, (int)(F2 / 2), (int)blk, cur_stream());
   return dgu;
 }
 // in place on x [T, H*D]: contiguous, or a 2-D column slice of a wider row-major tensor (row stride = its
@@ -1124,8 +1184,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_finalize", &bn_finalize, py::arg("sums"), py::arg("gamma"), py::arg("beta"), py::arg("run_mean"),
         py::arg("run_var"), py::arg("count"), py::arg("momentum"), py::arg("eps"));
   m.def("mask_apply", &mask_apply, "out = bit ? src : 0 (packed 1-bit mask per element)");
-  m.def("swiglu_fwd", &swiglu_fwd);
-  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("swiglu_fwd", &swiglu_fwd, py::arg("gu"), py::arg("blk") = 0);
+  m.def("swiglu_bwd", &swiglu_bwd, py::arg("gu"), py::arg("dy"), py::arg("blk") = 0);
   m.def("rope_", &rope_);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("act_bwd_colsum", &act_bwd_colsum, py::arg("dy"), py::arg("pre"), py::arg("act"),
@@ -1136,7 +1196,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("g"), py::arg("w"), py::arg("pre"), py::arg("act"), py::arg("db"), py::arg("db_accumulate"));
   m.def("gemm_dact_ok", &gemm_dact_ok, py::arg("M"), py::arg("N"), py::arg("K"));
   m.def("gemm_swiglu_bwd", &gemm_swiglu_bwd, "down-projection data gradient fused with the SwiGLU backward (dgu)",
-        py::arg("g"), py::arg("w"), py::arg("gu"));
+        py::arg("g"), py::arg("w"), py::arg("gu"), py::arg("blk") = 0);
+  m.def("gemm_swiglu_fwd", &gemm_swiglu_fwd, "gate|up projection with the SwiGLU in the epilogue: (gu, h)");
+  m.def("gemm_swiglu_fwd_ok", &gemm_swiglu_fwd_ok, py::arg("M"), py::arg("F"), py::arg("K"));
+  m.def("gemm_rope", &gemm_rope, "QKV projection with the q / k rotary embedding in the epilogue");
+  m.def("gemm_rope_ok", &gemm_rope_ok, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("rot_cols"));
   m.def("gemm_swiglu_bwd_ok", &gemm_swiglu_bwd_ok, py::arg("M"), py::arg("F"), py::arg("K"));
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
         py::arg("out_f32"), py::arg("bias"), py::arg("act"), py::arg("stats"),

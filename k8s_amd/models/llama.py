@@ -10,8 +10,8 @@ grads 32 GB + Adam 64 GB fit one 288 GB GPU with room for activations, so the
 8-GPU config is pure data parallel with a ring all-reduce of the flat gradient
 buffer (``parallel/ddp.py``) -- no tensor/pipeline parallelism needed.
 
-Per layer: RMSNorm (fused residual add) -> fused QKV GEMM [T, 6144] -> RoPE on
-q/k -> causal GQA flash attention -> O GEMM -> RMSNorm (+residual) -> fused
+Per layer: RMSNorm (fused residual add) -> fused QKV GEMM [T, 6144] with RoPE on
+q/k in its epilogue -> causal GQA flash attention -> O GEMM -> RMSNorm (+residual) -> fused
 gate|up GEMM [T, 28672] -> SwiGLU -> down GEMM.
 """
 from __future__ import annotations
@@ -64,7 +64,10 @@ class LlamaLayer(nn.Module):
         self.o = store.new(name + ".self_attn.o_proj.weight", (h, c.heads * d), out_std)
         self.mlp_norm = store.new(name + ".post_attention_layernorm.weight", (h,), init_const(1), decay=False,
                                   lowp=False)
+        # rows: blocks of 128 gate rows then the matching 128 up rows (ops.nn.linear_swiglu), so the gate|up GEMM's
+        # output tiles hold matching gate / up columns and its epilogue applies the SwiGLU; halves if F % 128 != 0
         self.gate_up = store.new(name + ".mlp.gate_up_proj.weight", (2 * c.intermediate, h), std)
+        self.swiglu_blk = 128 if c.intermediate % 128 == 0 else 0
         self.down = store.new(name + ".mlp.down_proj.weight", (h, c.intermediate), out_std)
 
     def forward(self, x, res, B, S, pos, table):
@@ -77,15 +80,17 @@ class LlamaLayer(nn.Module):
             hn = K.rms_norm(x, self.attn_norm, c.eps)
         else:
             hn, res = K.rms_norm(x, self.attn_norm, c.eps, residual=res)
-        qkv = K.linear(hn, self.qkv)
-        # rotary q/k, causal GQA flash attention and the packed QKV gradient in one op (no split/cat/copies)
+        # the q / k rotary embedding in the QKV GEMM's epilogue where the kernel takes the shape (else in place below)
+        qkv, rotated = K.linear_rope(hn, self.qkv, pos, table, (c.heads + c.kv_heads) * d)
+        # causal GQA flash attention and the packed QKV gradient in one op (no split/cat/copies)
         o = attention_qkv(qkv, B, S, c.heads, c.kv_heads, d, causal=True, rope=(pos, table),
-                          rope_in_place=True)  # qkv: this linear's output, read by nothing else
+                          rope_in_place=True,  # qkv: this linear's output, read by nothing else
+                          rope_applied=rotated)
         a = K.linear(o.reshape(B * S, c.heads * d), self.o)
         hn, res = K.rms_norm(a, self.mlp_norm, c.eps, residual=res)
-        gu = K.linear(hn, self.gate_up)
-        sl = K.SwiGLULink()  # the SwiGLU backward inside the down projection's data gradient
-        f = K.linear(K.swiglu(gu, link=sl), self.down, swiglu_in=sl)
+        sl = K.SwiGLULink(self.swiglu_blk)  # the SwiGLU backward inside the down projection's data gradient
+        # gate|up projection + SwiGLU: one GEMM with the SwiGLU in its epilogue where the kernel takes the shape
+        f = K.linear(K.linear_swiglu(hn, self.gate_up, link=sl, blk=self.swiglu_blk), self.down, swiglu_in=sl)
         return f, res
 
 

@@ -101,12 +101,13 @@ class _FlashQKV(torch.autograd.Function):
     copies on either pass."""
 
     @staticmethod
-    def forward(ctx, qkv, B, S, H, Hkv, D, causal, kv_lens, scale, pos, table, bias_link=None, rope_in_place=False):
+    def forward(ctx, qkv, B, S, H, Hkv, D, causal, kv_lens, scale, pos, table, bias_link=None, rope_in_place=False,
+                rope_applied=False):
         C = _load()
         if kv_lens is not None:
             kv_lens = kv_lens.to(device=qkv.device, dtype=torch.int32).contiguous()
         x = qkv.contiguous()
-        if pos is not None:
+        if pos is not None and not rope_applied:  # (applied: the projection's epilogue rotated q / k, ops.nn.linear_rope)
             if not rope_in_place:  # (in place: the caller's qkv is a temporary nothing else reads)
                 x = x.clone() if x.data_ptr() == qkv.data_ptr() else x
             # (in place, the raw-pointer rotation does not bump autograd's version counter -- and cannot: qkv is
@@ -145,12 +146,13 @@ class _FlashQKV(torch.autograd.Function):
             bl.done = True
         if has_rope:
             C.rope_(dqkv[:, : (H + Hkv) * D], pos, table, True)
-        return (dqkv,) + (None,) * 12
+        return (dqkv,) + (None,) * 13
 
 
 def attention_qkv(qkv, B: int, S: int, heads: int, kv_heads: int, head_dim: int, causal: bool = False,
                   kv_lens: Optional[torch.Tensor] = None, rope: Optional[tuple] = None,
-                  scale: Optional[float] = None, bias_link=None, rope_in_place: bool = False):
+                  scale: Optional[float] = None, bias_link=None, rope_in_place: bool = False,
+                  rope_applied: bool = False):
     """Self-attention of a packed QKV projection ``qkv`` [B*S, (heads + 2*kv_heads) * head_dim] (q heads, then k,
     then v); ``rope`` = (pos [B*S] int32, table) applies rotary embeddings to q and k. Returns o [B, S, heads, D].
     GPU bf16: one fused path (``_FlashQKV``); otherwise the split + ``attention`` reference composition.
@@ -159,7 +161,10 @@ def attention_qkv(qkv, B: int, S: int, heads: int, kv_heads: int, head_dim: int,
     q / k inside ``qkv`` itself instead of a copy (the caller's projection output is a temporary: Llama's 201 MB
     per-layer clone at s4096 b4). Contract of ``rope_in_place``: the projection output has no other reader --
     no hook, no saved-for-backward reference (``_Linear`` saves its input, not its output), no ``grad_link`` --
-    since those would see the rotated values; ``tests/test_attention_gpu.py`` pins in place == copy bitwise."""
+    since those would see the rotated values; ``tests/test_attention_gpu.py`` pins in place == copy bitwise.
+    ``rope_applied``: q / k already rotated by the projection's epilogue (``ops.nn.linear_rope``); the backward still
+    returns the gradient of the UN-rotated projection output (dqkv rotated back), which is what that linear's backward
+    takes."""
     D = head_dim
     scale = scale or 1.0 / math.sqrt(D)
     W = (heads + 2 * kv_heads) * D
@@ -167,7 +172,9 @@ def attention_qkv(qkv, B: int, S: int, heads: int, kv_heads: int, head_dim: int,
             W % 8 == 0 and qkv.is_contiguous():
         pos, table = rope if rope is not None else (None, None)
         return _FlashQKV.apply(qkv, B, S, heads, kv_heads, D, causal, kv_lens, scale, pos, table, bias_link,
-                               rope_in_place)
+                               rope_in_place, rope_applied)
+    if rope_applied:
+        raise RuntimeError("attention_qkv: q / k rotated by the projection epilogue need the fused GPU path")
     q, k, v = qkv.split([heads * D, kv_heads * D, kv_heads * D], dim=-1)
     if rope is not None:
         from k8s_amd.ops import nn as _nn

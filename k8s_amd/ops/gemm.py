@@ -143,7 +143,7 @@ def _dgrad_act(g, w, dx_act):
 
 
 def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True, dx_addend=None, pb=None, dx_act=None,
-               dx_swiglu=None):
+               dx_swiglu=None, swiglu_blk=0):
     """dx and the parameter gradient. With (pw, store) on GPU the weight gradient is written
     (or accumulated) straight into the flat fp32 gradient slot; returns (dx, dw_or_None, db).
     ``dx_addend`` (bf16, x's shape): another gradient contribution of x, accumulated in the dgrad epilogue (it is
@@ -204,7 +204,7 @@ def linear_bwd(gy, x, w, saved, act, pw=None, store=None, need_db=True, dx_adden
         if dx_act is not None:
             dx = _dgrad_act(g, w, dx_act)
         elif dx_swiglu is not None:
-            dx = _load().gemm_swiglu_bwd(g, w, dx_swiglu.contiguous())
+            dx = _load().gemm_swiglu_bwd(g, w, dx_swiglu.contiguous(), swiglu_blk)
         else:
             dx = mm(g, w, True, False, out=dx_addend if acc else None, accumulate=acc)
         if dx_addend is not None and not acc:

@@ -85,11 +85,12 @@ class SwiGLULink:
     """Joins ``swiglu(gu, link=l)`` to the linear that reads its output (``linear(y, W, swiglu_in=l)``, Llama's down
     projection): that linear's data gradient takes the SwiGLU backward in its epilogue and produces the gradient of gu
     directly (gemm256.hip copy_out_x ACT = -3, ``gemm.swiglu_ok`` shapes), so neither the [T, F] gradient of the
-    SwiGLU output nor the separate SwiGLU-backward pass over gu exists."""
-    __slots__ = ("saved", "dgu")
+    SwiGLU output nor the separate SwiGLU-backward pass over gu exists. ``blk``: gu's column layout (0 = gate | up
+    halves, 128 = blocks of 128 gate then 128 up columns, ``linear_swiglu``)."""
+    __slots__ = ("saved", "dgu", "blk")
 
-    def __init__(self):
-        self.saved, self.dgu = None, None
+    def __init__(self, blk: int = 0):
+        self.saved, self.dgu, self.blk = None, None, blk
 
 
 class MaskedGrad:
@@ -552,7 +553,7 @@ class _Linear(torch.autograd.Function):
             dx_swiglu = sl.saved
         dx, dw, db = g.linear_bwd(gy2, x2, w, pre, act, pw=pw, store=pw.store,
                                   need_db=pb is not None and not db_done, dx_addend=addend, pb=pb, dx_act=dx_act,
-                                  dx_swiglu=dx_swiglu)
+                                  dx_swiglu=dx_swiglu, swiglu_blk=sl.blk if dx_swiglu is not None else 0)
         if dx_act is not None:
             li.done, li.saved = True, None
         if dx_swiglu is not None:  # the SwiGLU's backward returns dgu; x's own gradient is never formed
@@ -856,20 +857,48 @@ def global_avg_pool_nhwc(x):
 
 
 # =========================================================================== transformer elementwise (K9)
+def _swiglu_split(gu, blk):
+    """(gate, up) fp32 views of a [.., 2F] gate|up tensor in either column layout (``SwiGLULink.blk``)."""
+    F2 = gu.shape[-1] // 2
+    if not blk:
+        return gu.float().split(F2, -1)
+    v = gu.float().reshape(*gu.shape[:-1], F2 // blk, 2, blk)
+    return v[..., 0, :].reshape(*gu.shape[:-1], F2), v[..., 1, :].reshape(*gu.shape[:-1], F2)
+
+
+def _swiglu_join(dg, du, blk):
+    if not blk:
+        return torch.cat([dg, du], -1)
+    F2 = dg.shape[-1]
+    lead = dg.shape[:-1]
+    return torch.stack([dg.reshape(*lead, F2 // blk, blk), du.reshape(*lead, F2 // blk, blk)], -2).reshape(
+        *lead, 2 * F2)
+
+
+def _swiglu_bwd_any(gu, dy, blk):
+    F2 = gu.shape[-1] // 2
+    if _gpu(gu) and gu.dtype == torch.bfloat16 and F2 % 8 == 0:
+        return _C().swiglu_bwd(gu, dy.contiguous(), blk)
+    g, u = _swiglu_split(gu, blk)
+    s_ = torch.sigmoid(g)
+    d = dy.float()
+    return _swiglu_join(d * u * s_ * (1 + g * (1 - s_)), d * g * s_, blk).to(gu.dtype)
+
+
 class _SwiGLU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, gu, link=None):
+    def forward(ctx, gu, link=None, blk=0):
         gu = gu.contiguous()
         F2 = gu.shape[-1] // 2
         if _gpu(gu) and gu.dtype == torch.bfloat16 and F2 % 8 == 0:
-            y = _C().swiglu_fwd(gu)
+            y = _C().swiglu_fwd(gu, blk)
         else:
-            g, u = gu.float().split(F2, -1)
+            g, u = _swiglu_split(gu, blk)
             y = (torch.nn.functional.silu(g) * u).to(gu.dtype)
         ctx.save_for_backward(gu)
-        ctx.link = link
+        ctx.link, ctx.blk = link, blk
         if link is not None:
-            link.saved, link.dgu = gu.reshape(-1, 2 * F2), None
+            link.saved, link.dgu, link.blk = gu.reshape(-1, 2 * F2), None, blk
         return y
 
     @staticmethod
@@ -878,22 +907,107 @@ class _SwiGLU(torch.autograd.Function):
         link = ctx.link
         if link is not None and link.dgu is not None:  # formed by the consuming linear's data gradient
             dgu, link.dgu, link.saved = link.dgu, None, None
-            return dgu.reshape(gu.shape), None
+            return dgu.reshape(gu.shape), None, None
         if link is not None:
             link.saved = None
-        F2 = gu.shape[-1] // 2
-        dy = dy.contiguous()
-        if _gpu(gu) and gu.dtype == torch.bfloat16 and F2 % 8 == 0:
-            return _C().swiglu_bwd(gu, dy), None
-        g, u = gu.float().split(F2, -1)
-        s = torch.sigmoid(g)
-        d = dy.float()
-        return torch.cat([d * u * s * (1 + g * (1 - s)), d * g * s], -1).to(gu.dtype), None
+        return _swiglu_bwd_any(gu, dy, ctx.blk), None, None
 
 
-def swiglu(gu, link=None):
-    """silu(gate) * up over a fused [.., 2F] gate|up projection. ``link``: see ``SwiGLULink``."""
-    return _SwiGLU.apply(gu, link if SWIGLU_FUSE else None)
+def swiglu(gu, link=None, blk: int = 0):
+    """silu(gate) * up over a fused [.., 2F] gate|up projection (``blk``: its column layout, see ``SwiGLULink``).
+    ``link``: see ``SwiGLULink``."""
+    return _SwiGLU.apply(gu, link if SWIGLU_FUSE else None, blk)
+
+
+# The gate|up projection's SwiGLU in its GEMM epilogue (gemm256.hip copy_out_swiglu; K8S_AMD_SWIGLU_EPI=0 for A/Bs).
+SWIGLU_EPI = os.environ.get("K8S_AMD_SWIGLU_EPI", "1") != "0"
+
+
+class _LinearSwiGLU(torch.autograd.Function):
+    """h = silu(x Wg^T) * (x Wu^T) from ONE 4-wave GEMM whose epilogue writes both gu (what the backward reads) and h:
+    the weight's rows are in the 128-blocked gate|up order, so every 256-wide output tile holds a gate block and its
+    up block (``SwiGLULink.blk`` = 128). Backward: dgu from the down projection's fused data gradient (``link``) or
+    the SwiGLU-backward kernel, then the projection's data / weight gradients (``gemm.linear_bwd``)."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, pw, link=None):
+        x2 = x.reshape(-1, x.shape[-1])
+        gu, h = _C().gemm_swiglu_fwd(x2, pw.weight)
+        ctx.save_for_backward(x2, gu)
+        ctx.pw, ctx.link, ctx.xshape = pw, link, x.shape
+        if link is not None:
+            link.saved, link.dgu, link.blk = gu, None, 128
+        return h.reshape(*x.shape[:-1], h.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dh):
+        x2, gu = ctx.saved_tensors
+        link, pw = ctx.link, ctx.pw
+        if link is not None and link.dgu is not None:
+            dgu, link.dgu, link.saved = link.dgu, None, None
+        else:
+            if link is not None:
+                link.saved = None
+            dgu = _swiglu_bwd_any(gu, dh.reshape(gu.shape[0], -1), 128)
+        dx, dw, _ = _gemm().linear_bwd(dgu.reshape(gu.shape), x2, pw.weight, None, None, pw=pw, store=pw.store,
+                                       need_db=False)
+        if dw is not None:
+            pw.store.deposit(pw, dw)
+        return dx.reshape(ctx.xshape), None, None, None
+
+
+# The QKV projection's rotary embedding in its GEMM epilogue (gemm256.hip copy_out_rope; K8S_AMD_ROPE_EPI=0 for A/Bs).
+ROPE_EPI = os.environ.get("K8S_AMD_ROPE_EPI", "1") != "0"
+
+
+class _LinearRope(torch.autograd.Function):
+    """y = rope(x W^T) on the first ``rot_cols`` columns (the q / k heads, head dim 128) from one 4-wave GEMM with the
+    rotation in its copy-out. Backward takes the gradient of the UN-rotated output -- what ``attention_qkv(...,
+    rope_applied=True)`` returns (it rotates dqkv back, as for its own in-place rotation) -- so it is a plain linear
+    backward."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, pw, pos, table, rot_cols):
+        x2 = x.reshape(-1, x.shape[-1])
+        y = _C().gemm_rope(x2, pw.weight, pos, table, rot_cols)
+        ctx.save_for_backward(x2)
+        ctx.pw, ctx.xshape = pw, x.shape
+        return y.reshape(*x.shape[:-1], y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x2,) = ctx.saved_tensors
+        pw = ctx.pw
+        gy2 = gy.reshape(-1, gy.shape[-1]).contiguous()
+        dx, dw, _ = _gemm().linear_bwd(gy2, x2, pw.weight, None, None, pw=pw, store=pw.store, need_db=False)
+        if dw is not None:
+            pw.store.deposit(pw, dw)
+        return dx.reshape(ctx.xshape), None, None, None, None, None
+
+
+def linear_rope(x, pw, pos, table, rot_cols: int):
+    """(y, rotated): the projection ``x pw^T`` with the rotary embedding of its first ``rot_cols`` columns applied in
+    the GEMM epilogue when the kernel takes the shape (``rotated`` True: pass ``rope_applied=True`` to
+    ``attention_qkv``), else the plain projection (``rotated`` False: the attention op rotates)."""
+    x2 = x.reshape(-1, x.shape[-1])
+    if (ROPE_EPI and _gpu(x) and x.dtype == torch.bfloat16 and pw.weight.dtype == torch.bfloat16 and x2.is_contiguous()
+            and pw.grad.dtype == torch.float32 and table.dim() == 3 and table.shape[1] == 64
+            and bool(_C().gemm_rope_ok(x2.shape[0], pw.shape[0], x2.shape[1], rot_cols))):
+        return _LinearRope.apply(x, pw.store.anchor, pw, pos, table, rot_cols), True
+    return linear(x, pw), False
+
+
+def linear_swiglu(x, pw, link=None, blk: int = 128):
+    """silu(gate) * up of the fused gate|up projection ``pw`` ([2F, in], rows in ``blk``-blocked gate|up order) of x:
+    on the GPU's whole-tile shapes one GEMM with the SwiGLU in its epilogue (``_LinearSwiGLU``), else the projection
+    then ``swiglu``. ``link``: the SwiGLULink of the consuming down projection."""
+    x2 = x.reshape(-1, x.shape[-1])
+    F = pw.shape[0] // 2
+    if (SWIGLU_EPI and blk == 128 and _gpu(x) and x.dtype == torch.bfloat16 and pw.weight.dtype == torch.bfloat16
+            and x2.is_contiguous() and pw.grad.dtype == torch.float32
+            and bool(_C().gemm_swiglu_fwd_ok(x2.shape[0], F, x2.shape[1]))):
+        return _LinearSwiGLU.apply(x, pw.store.anchor, pw, link if SWIGLU_FUSE else None)
+    return swiglu(linear(x, pw), link=link, blk=blk)
 
 
 def rope_table(max_pos: int, dim: int, theta: float = 10000.0, device=None) -> torch.Tensor:

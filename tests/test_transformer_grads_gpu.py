@@ -77,7 +77,9 @@ def _llama_twin(m, store, ids, labels, autocast):
                       True)
             x = x + o.reshape(B * S, -1) @ P[n + "self_attn.o_proj.weight"].t()
             h = _rms(x, P[n + "post_attention_layernorm.weight"], c.eps)
-            g, u = (h @ P[n + "mlp.gate_up_proj.weight"].t()).chunk(2, -1)
+            gu = h @ P[n + "mlp.gate_up_proj.weight"].t()  # rows in 128-blocked gate|up order (models/llama.py)
+            gu = gu.reshape(gu.shape[0], -1, 2, 128)
+            g, u = gu[:, :, 0].reshape(gu.shape[0], -1), gu[:, :, 1].reshape(gu.shape[0], -1)
             x = x + (F.silu(g) * u) @ P[n + "mlp.down_proj.weight"].t()
         h = _rms(x, P["model.norm.weight"], c.eps)
         logits = h @ P["lm_head.weight"].t()
@@ -200,6 +202,70 @@ def test_llama_swiglu_fused_backward_matches_unfused(cuda):
             out.append((loss.float().item(), store.grad.clone()))
         finally:
             K.SWIGLU_FUSE = True
+    (l0, g0), (l1, g1) = out
+    assert l0 == l1
+    assert torch.equal(g0, g1), (g0 - g1).abs().max().item()
+
+
+def test_llama_swiglu_epilogue_matches_separate_pass(cuda):
+    """Llama with the SwiGLU in the gate|up GEMM's epilogue (ops.nn.linear_swiglu) gives the same loss and parameter
+    gradients, bitwise, as the projection followed by the separate SwiGLU kernel (a shape the 4-wave kernel takes)."""
+    import dataclasses
+
+    from k8s_amd.models import llama as M
+    from k8s_amd.ops import nn as K
+    from k8s_amd.parallel.flat import ParamStore
+
+    cfg = dataclasses.replace(M.LLAMA_TINY, layers=1, intermediate=4096, max_position=1024)
+    out = []
+    for epi in (False, True):
+        K.SWIGLU_EPI = epi
+        try:
+            store = ParamStore()
+            model = M.LlamaForCausalLM(store, cfg).finalize(cuda, seed=2)
+            gen = torch.Generator(device=cuda)
+            gen.manual_seed(3)
+            batch = M.synthetic_batch(cfg, 4, 1024, cuda, generator=gen)
+            store.begin_step()
+            loss = model(*batch, dtype=torch.bfloat16)
+            loss.backward()
+            store.zero_unwritten()
+            out.append((loss.float().item(), store.grad.clone()))
+        finally:
+            K.SWIGLU_EPI = True
+    (l0, g0), (l1, g1) = out
+    assert l0 == l1
+    assert torch.equal(g0, g1), (g0 - g1).abs().max().item()
+
+
+def test_llama_rope_epilogue_matches_in_place_rope(cuda):
+    """Llama with the q / k rotary embedding in the QKV GEMM's epilogue (ops.nn.linear_rope + attention_qkv
+    rope_applied) gives the same loss and parameter gradients, bitwise, as the in-place rope pass (a shape the 4-wave
+    kernel takes)."""
+    import dataclasses
+
+    from k8s_amd.models import llama as M
+    from k8s_amd.ops import nn as K
+    from k8s_amd.parallel.flat import ParamStore
+
+    cfg = dataclasses.replace(M.LLAMA_TINY, layers=1, hidden=1024, heads=8, kv_heads=2, intermediate=4096,
+                              max_position=1024)
+    out = []
+    for epi in (False, True):
+        K.ROPE_EPI = epi
+        try:
+            store = ParamStore()
+            model = M.LlamaForCausalLM(store, cfg).finalize(cuda, seed=2)
+            gen = torch.Generator(device=cuda)
+            gen.manual_seed(3)
+            batch = M.synthetic_batch(cfg, 4, 1024, cuda, generator=gen)
+            store.begin_step()
+            loss = model(*batch, dtype=torch.bfloat16)
+            loss.backward()
+            store.zero_unwritten()
+            out.append((loss.float().item(), store.grad.clone()))
+        finally:
+            K.ROPE_EPI = True
     (l0, g0), (l1, g1) = out
     assert l0 == l1
     assert torch.equal(g0, g1), (g0 - g1).abs().max().item()
