@@ -734,34 +734,30 @@ __device__ __forceinline__ void copy_out_x(uint16_t* __restrict__ C, uint16_t* _
 }
 
 // ACT = 3: the gate|up projection with its SwiGLU in the epilogue (Llama). The weight's rows are laid out in blocks of
-// 128 gate rows then the 128 matching up rows, so a 256-wide output tile holds gate block t in waves (wr, 0) and up
-// block t in waves (wr, 1), for the same rows. Every wave stores its own staged piece to C (= gu [M][2F], what the
-// backward reads); after a barrier, waves (wr, 0) / (wr, 1) take rows 0-63 / 64-127 of the pair's 128 and write
-// h = silu(g) u (elementwise.hip swiglu_fwd_kernel's formula on the same bf16 inputs: bit-identical) from both staged
-// pieces to `hout` [M][F] at column n0 / 2 -- the separate SwiGLU pass (read gu, write h) is gone.
+// 64 gate rows then the 64 matching up rows, so each wave's staged 128 columns hold gate block b in columns 0-63 and up
+// block b in 64-127 (the rotate-half pairing of copy_out_rope): chunk c's partner is chunk c + 8 of the same staged
+// row, no other wave's piece is read and no barrier is needed. Every wave stores its staged piece to C (= gu [M][2F],
+// what the backward reads), then h = silu(g) u (elementwise.hip swiglu_fwd_kernel's formula on the same bf16 inputs:
+// bit-identical) to `hout` [M][F] at column (n0 + wc 128) / 2 -- the separate SwiGLU pass (read gu, write h) is gone.
 template <class Off, class Stg>
-__device__ __forceinline__ void copy_out_swiglu(uint16_t* __restrict__ C, uint16_t* __restrict__ hout, const char* smem,
-                                                const Off& coff, const Stg& staged, int m0, int n0, int wr, int wc,
-                                                int N) {
+__device__ __forceinline__ void copy_out_swiglu(uint16_t* __restrict__ C, uint16_t* __restrict__ hout, const char* stg,
+                                                const Off& coff, const Stg& staged, int row0, int hcol0, int N) {
   const int lane = threadIdx.x & 63;
 #pragma unroll 4
   for (int it = 0; it < 32; ++it) *reinterpret_cast<bf16x8_t*>(C + coff(it)) = staged(it);
-  g256::barrier();  // every wave's piece staged (each waited for its own LDS writes before the copy above)
-  const char* sg = smem + (2 * wr) * 32768;
-  const char* su = smem + (2 * wr + 1) * 32768;
   const long F = N / 2;
 #pragma unroll 4
   for (int it = 0; it < 16; ++it) {
-    const int idx = it * 64 + lane, lr = wc * 64 + (idx >> 4), ch = idx & 15;
-    const int o = lr * 256 + ((ch ^ (lr & 15)) << 4);
-    const bf16x8_t g = *reinterpret_cast<const bf16x8_t*>(sg + o), u = *reinterpret_cast<const bf16x8_t*>(su + o);
+    const int idx = it * 64 + lane, lr = idx >> 3, c = idx & 7;
+    const bf16x8_t g = *reinterpret_cast<const bf16x8_t*>(stg + lr * 256 + ((c ^ (lr & 15)) << 4));
+    const bf16x8_t u = *reinterpret_cast<const bf16x8_t*>(stg + lr * 256 + (((c + 8) ^ (lr & 15)) << 4));
     float h[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const float gg = bf2f((uint16_t)g[r]);
       h[r] = gg * __builtin_amdgcn_rcpf(1.f + __expf(-gg)) * bf2f((uint16_t)u[r]);
     }
-    *reinterpret_cast<bf16x8_t*>(hout + (long)(m0 + wr * 128 + lr) * F + n0 / 2 + ch * 8) = pack_bf16x8(h);
+    *reinterpret_cast<bf16x8_t*>(hout + (long)(row0 + lr) * F + hcol0 + c * 8) = pack_bf16x8(h);
   }
 }
 
@@ -770,38 +766,41 @@ __device__ __forceinline__ void copy_out_swiglu(uint16_t* __restrict__ C, uint16
 // same staged row, the angle table row is pos[row]. elementwise.hip rope_kernel's formula (explicit fmas, the same
 // rounding), so the fused output is bit-identical to the projection + the in-place rope pass it replaces. `rot`: this
 // wave's head is a q / k head (columns < rcols); the v heads are stored as staged.
-template <class Off>
-__device__ __forceinline__ void copy_out_rope(uint16_t* __restrict__ C, const char* stg, const Off& coff, int row0,
-                                              bool rot, const int* __restrict__ rpos, const float* __restrict__ rtab) {
+__device__ __forceinline__ void copy_out_rope(uint16_t* __restrict__ C, const char* stg, long cbase, long ldc,
+                                              bool rot, const int* __restrict__ rpos, const float* __restrict__ rtab,
+                                              int row0) {
   const int lane = threadIdx.x & 63;
   if (!rot) {
 #pragma unroll 4
     for (int it = 0; it < 32; ++it) {
       const int idx = it * 64 + lane, lr = idx >> 4, ch = idx & 15;
-      *reinterpret_cast<bf16x8_t*>(C + coff(it)) =
+      *reinterpret_cast<bf16x8_t*>(C + cbase + lr * ldc + ch * 8) =
           *reinterpret_cast<const bf16x8_t*>(stg + lr * 256 + ((ch ^ (lr & 15)) << 4));
     }
     return;
   }
+  // each lane rotates one (x1 chunk c, x2 chunk c + 8) pair of a row: one table read and one LDS read per operand
 #pragma unroll 2
-  for (int it = 0; it < 32; ++it) {
-    const int idx = it * 64 + lane, lr = idx >> 4, ch = idx & 15;
-    const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(stg + lr * 256 + ((ch ^ (lr & 15)) << 4));
-    const bf16x8_t w = *reinterpret_cast<const bf16x8_t*>(stg + lr * 256 + (((ch ^ 8) ^ (lr & 15)) << 4));
-    const f32x4_t* tb = reinterpret_cast<const f32x4_t*>(rtab + ((long)rpos[row0 + lr] * 64 + (ch & 7) * 8) * 2);
-    float o[8];
+  for (int it = 0; it < 16; ++it) {
+    const int idx = it * 64 + lane, lr = idx >> 3, c = idx & 7;
+    const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(stg + lr * 256 + ((c ^ (lr & 15)) << 4));
+    const bf16x8_t w = *reinterpret_cast<const bf16x8_t*>(stg + lr * 256 + (((c + 8) ^ (lr & 15)) << 4));
+    const f32x4_t* tb = reinterpret_cast<const f32x4_t*>(rtab + ((long)rpos[row0 + lr] * 64 + c * 8) * 2);
+    float o1[8], o2[8];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const f32x4_t t = tb[q];  // (cos, sin) of elements 2q, 2q + 1
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const float cs = t[2 * e], sn = t[2 * e + 1];
-        const float a = bf2f((uint16_t)v[2 * q + e]), b = bf2f((uint16_t)w[2 * q + e]);
-        // first half: x1 c - x2 s (a = x1, b = x2); second half: x2 c + x1 s (a = x2, b = x1)
-        o[2 * q + e] = ch < 8 ? __builtin_fmaf(a, cs, -(b * sn)) : __builtin_fmaf(a, cs, b * sn);
+        const float x1 = bf2f((uint16_t)v[2 * q + e]), x2 = bf2f((uint16_t)w[2 * q + e]);
+        o1[2 * q + e] = __builtin_fmaf(x1, cs, -(x2 * sn));  // rope_kernel's formula
+        o2[2 * q + e] = __builtin_fmaf(x2, cs, x1 * sn);
       }
     }
-    *reinterpret_cast<bf16x8_t*>(C + coff(it)) = pack_bf16x8(o);
+    uint16_t* d = C + cbase + lr * ldc + c * 8;
+    *reinterpret_cast<bf16x8_t*>(d) = pack_bf16x8(o1);
+    *reinterpret_cast<bf16x8_t*>(d + 64) = pack_bf16x8(o2);
   }
 }
 
@@ -1149,13 +1148,13 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
       if constexpr (!AMN && BMN) {
         if (act == -3) {  // SwiGLU backward: no column sums; the up half `slab` columns to the right
           copy_out_x<-3, false>(C, pre, stg, coff, staged, nullptr, slab);
-        } else if (act == -4) {  // the same on the 128-blocked gate|up layout (copy_out_swiglu): this wave's 128
-                                 // columns j0.. are gate columns 2 j0.., their up columns 128 further
+        } else if (act == -4) {  // the same on the 64-blocked gate|up layout (copy_out_swiglu): h column j is gate
+                                 // column (j / 64) 128 + j % 64, its up column 64 further
           auto coff_b = [&](int it) {
             const int idx = it * 64 + lane, lr = idx >> 4, ch = idx & 15;
-            return (long)(m0 + wr * 128 + lr) * ldc + 2 * (n0 + wc * 128) + ch * 8;
+            return (long)(m0 + wr * 128 + lr) * ldc + 2 * (n0 + wc * 128) + (ch >> 3) * 128 + (ch & 7) * 8;
           };
-          copy_out_x<-3, false>(C, pre, stg, coff_b, staged, nullptr, 128);
+          copy_out_x<-3, false>(C, pre, stg, coff_b, staged, nullptr, 64);
         } else {
           float* const cp = cpart + (long)((m0 >> 8) * 2 + wr) * N + n0 + wc * 128;
           if (act == -2) copy_out_x<-2, false>(C, pre, stg, coff, staged, cp);
@@ -1163,9 +1162,10 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
         }
       }
     } else if (act == 3) {
-      copy_out_swiglu(C, pre, smem, coff, staged, m0, n0, wr, wc, N);
+      copy_out_swiglu(C, pre, stg, coff, staged, m0 + wr * 128, (n0 + wc * 128) / 2, N);
     } else if (act == 4) {
-      copy_out_rope(C, stg, coff, m0 + wr * 128, n0 + wc * 128 < rcols, rpos, rtab);
+      copy_out_rope(C, stg, (long)(m0 + wr * 128) * ldc + n0 + wc * 128, ldc, n0 + wc * 128 < rcols, rpos, rtab,
+                    m0 + wr * 128);
     } else if (act == 2) {
       if (accumulate) copy_out_x<2, true>(C, pre, stg, coff, staged); else copy_out_x<2, false>(C, pre, stg, coff, staged);
     } else if (act == 1) {
@@ -1241,7 +1241,7 @@ bool gemm_w4_swiglu_ok(int M, int F, int K, long lda, long ldb) {
 void launch_gemm_w4_swiglu_bwd(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* dgu,
                                const uint16_t* gu, int M, int F, int K, int blk, float* sk_slabs, int* sk_sync,
                                hipStream_t st) {
-  if (!gemm_w4_swiglu_ok(M, F, K, lda, ldb) || (blk != 0 && blk != 128))
+  if (!gemm_w4_swiglu_ok(M, F, K, lda, ldb) || (blk != 0 && blk != 64))
     throw std::runtime_error("gemm_w4_swiglu_bwd: shape outside the 4-wave kernel's contract");
   Gemm256Plan plan = gemm256_plan(M, F, K);
   if (!sk_slabs || !sk_sync) plan.sk = 1;
@@ -1253,7 +1253,7 @@ void launch_gemm_w4_swiglu_bwd(const uint16_t* A, long lda, const uint16_t* B, l
     kps = plan.kps;
     blocks = plan.full + (tiles - plan.full) * plan.sk;
   }
-  // C = dgu (row stride 2F, gate half at column 0), pre = gu, slab = F: the up half's column offset (blk = 128: the
+  // C = dgu (row stride 2F, gate half at column 0), pre = gu, slab = F: the up half's column offset (blk = 64: the
   // blocked layout, act -4)
   hipLaunchKernelGGL((g4::gemm_w4_kernel<false, true, true>), dim3(blocks), dim3(g4::THREADS), 0, st, A, lda, B, ldb,
                      (void*)dgu, 2L * F, M, F, K, 1.f, kps, sk, 0, 0, nullptr, blk ? -4 : -3,
@@ -1261,10 +1261,10 @@ void launch_gemm_w4_swiglu_bwd(const uint16_t* A, long lda, const uint16_t* B, l
 }
 
 // Llama's gate|up projection with the SwiGLU in the epilogue (copy_out_swiglu): gu [M][2F] = A [M][K] . B [2F][K]^T
-// (both K-major; B's rows in the 128-blocked gate|up order) and h [M][F] = silu(gate) up. Whole 256 x 256 tiles.
+// (both K-major; B's rows in the 64-blocked gate|up order) and h [M][F] = silu(gate) up. Whole 256 x 256 tiles.
 bool gemm_w4_swiglu_fwd_ok(int M, int F, int K, long lda, long ldb) {
   return w4_enabled() && M % 256 == 0 && F % 128 == 0 && K % 64 == 0 && (lda | ldb) % 8 == 0 &&
-         (long)(M / 256) * (2 * F / 256) >= planner_cus();
+         (long)(M / 256) * (2 * F / 256) >= planner_cus();  // (2F % 256: whole tiles, each 2 gate|up block pairs)
 }
 void launch_gemm_w4_swiglu_fwd(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* gu, uint16_t* h,
                                int M, int F, int K, float* sk_slabs, int* sk_sync, hipStream_t st) {

@@ -579,7 +579,7 @@ Tensor gemm_swiglu_bwd(Tensor g, Tensor w, Tensor gu, int64_t blk) {
     slabs = torch::empty({k8s_amd::gemm256_sk_slab_floats(plan)}, g.options().dtype(at::kFloat));
     sync = sk_sync_words(k8s_amd::gemm256_sk_sync_ints(plan), g.device());
   }
-  TORCH_CHECK(blk == 0 || blk == 128, "gemm_swiglu_bwd: blk is 0 (gate | up halves) or 128 (blocked layout)");
+  TORCH_CHECK(blk == 0 || blk == 64, "gemm_swiglu_bwd: blk is 0 (gate | up halves) or 64 (blocked layout)");
   k8s_amd::launch_gemm_w4_swiglu_bwd(cbf(g), g.stride(0), cbf(w), w.stride(0), bf(dgu), cbf(gu), (int)M, (int)F,
                                      (int)K, (int)blk, sync ? f32(slabs) : nullptr, sync, cur_stream());
   return dgu;
@@ -615,7 +615,7 @@ Tensor gemm_rope(Tensor x, Tensor w, Tensor pos, Tensor table, int64_t rot_cols)
 }
 
 // Llama's gate|up projection with the SwiGLU in the epilogue: returns (gu [M, 2F], h [M, F] = silu(gate) up) from
-// x [M, K] bf16 and w [2F, K] bf16 whose rows are in the 128-blocked gate|up order (gemm256.hip copy_out_swiglu).
+// x [M, K] bf16 and w [2F, K] bf16 whose rows are in the 64-blocked gate|up order (gemm256.hip copy_out_swiglu).
 bool gemm_swiglu_fwd_ok(int64_t M, int64_t F, int64_t K) {
   return k8s_amd::gemm_w4_swiglu_fwd_ok((int)M, (int)F, (int)K, K, K);
 }

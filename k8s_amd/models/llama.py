@@ -64,10 +64,10 @@ class LlamaLayer(nn.Module):
         self.o = store.new(name + ".self_attn.o_proj.weight", (h, c.heads * d), out_std)
         self.mlp_norm = store.new(name + ".post_attention_layernorm.weight", (h,), init_const(1), decay=False,
                                   lowp=False)
-        # rows: blocks of 128 gate rows then the matching 128 up rows (ops.nn.linear_swiglu), so the gate|up GEMM's
-        # output tiles hold matching gate / up columns and its epilogue applies the SwiGLU; halves if F % 128 != 0
+        # rows: blocks of 64 gate rows then the matching 64 up rows (ops.nn.linear_swiglu), so every wave tile of the
+        # gate|up GEMM holds matching gate / up columns and its epilogue applies the SwiGLU; halves if F % 64 != 0
         self.gate_up = store.new(name + ".mlp.gate_up_proj.weight", (2 * c.intermediate, h), std)
-        self.swiglu_blk = 128 if c.intermediate % 128 == 0 else 0
+        self.swiglu_blk = 64 if c.intermediate % 64 == 0 else 0
         self.down = store.new(name + ".mlp.down_proj.weight", (h, c.intermediate), out_std)
 
     def forward(self, x, res, B, S, pos, table):

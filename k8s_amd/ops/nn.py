@@ -86,7 +86,7 @@ class SwiGLULink:
     projection): that linear's data gradient takes the SwiGLU backward in its epilogue and produces the gradient of gu
     directly (gemm256.hip copy_out_x ACT = -3, ``gemm.swiglu_ok`` shapes), so neither the [T, F] gradient of the
     SwiGLU output nor the separate SwiGLU-backward pass over gu exists. ``blk``: gu's column layout (0 = gate | up
-    halves, 128 = blocks of 128 gate then 128 up columns, ``linear_swiglu``)."""
+    halves, 64 = blocks of 64 gate then 64 up columns, ``linear_swiglu``)."""
     __slots__ = ("saved", "dgu", "blk")
 
     def __init__(self, blk: int = 0):
@@ -925,8 +925,8 @@ SWIGLU_EPI = os.environ.get("K8S_AMD_SWIGLU_EPI", "1") != "0"
 
 class _LinearSwiGLU(torch.autograd.Function):
     """h = silu(x Wg^T) * (x Wu^T) from ONE 4-wave GEMM whose epilogue writes both gu (what the backward reads) and h:
-    the weight's rows are in the 128-blocked gate|up order, so every 256-wide output tile holds a gate block and its
-    up block (``SwiGLULink.blk`` = 128). Backward: dgu from the down projection's fused data gradient (``link``) or
+    the weight's rows are in the 64-blocked gate|up order, so every wave's 128 output columns hold a gate block and its
+    up block (``SwiGLULink.blk`` = 64). Backward: dgu from the down projection's fused data gradient (``link``) or
     the SwiGLU-backward kernel, then the projection's data / weight gradients (``gemm.linear_bwd``)."""
 
     @staticmethod
@@ -936,7 +936,7 @@ class _LinearSwiGLU(torch.autograd.Function):
         ctx.save_for_backward(x2, gu)
         ctx.pw, ctx.link, ctx.xshape = pw, link, x.shape
         if link is not None:
-            link.saved, link.dgu, link.blk = gu, None, 128
+            link.saved, link.dgu, link.blk = gu, None, 64
         return h.reshape(*x.shape[:-1], h.shape[-1])
 
     @staticmethod
@@ -948,7 +948,7 @@ class _LinearSwiGLU(torch.autograd.Function):
         else:
             if link is not None:
                 link.saved = None
-            dgu = _swiglu_bwd_any(gu, dh.reshape(gu.shape[0], -1), 128)
+            dgu = _swiglu_bwd_any(gu, dh.reshape(gu.shape[0], -1), 64)
         dx, dw, _ = _gemm().linear_bwd(dgu.reshape(gu.shape), x2, pw.weight, None, None, pw=pw, store=pw.store,
                                        need_db=False)
         if dw is not None:
@@ -997,13 +997,13 @@ def linear_rope(x, pw, pos, table, rot_cols: int):
     return linear(x, pw), False
 
 
-def linear_swiglu(x, pw, link=None, blk: int = 128):
+def linear_swiglu(x, pw, link=None, blk: int = 64):
     """silu(gate) * up of the fused gate|up projection ``pw`` ([2F, in], rows in ``blk``-blocked gate|up order) of x:
     on the GPU's whole-tile shapes one GEMM with the SwiGLU in its epilogue (``_LinearSwiGLU``), else the projection
     then ``swiglu``. ``link``: the SwiGLULink of the consuming down projection."""
     x2 = x.reshape(-1, x.shape[-1])
     F = pw.shape[0] // 2
-    if (SWIGLU_EPI and blk == 128 and _gpu(x) and x.dtype == torch.bfloat16 and pw.weight.dtype == torch.bfloat16
+    if (SWIGLU_EPI and blk == 64 and _gpu(x) and x.dtype == torch.bfloat16 and pw.weight.dtype == torch.bfloat16
             and x2.is_contiguous() and pw.grad.dtype == torch.float32
             and bool(_C().gemm_swiglu_fwd_ok(x2.shape[0], F, x2.shape[1]))):
         return _LinearSwiGLU.apply(x, pw.store.anchor, pw, link if SWIGLU_FUSE else None)

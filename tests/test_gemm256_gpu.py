@@ -382,7 +382,7 @@ def test_gemm_swiglu_bwd_matches_two_pass():
     assert _rel(dgu, ref) < 2e-2
 
 
-def _blocked_split(gu, blk=128):
+def _blocked_split(gu, blk=64):
     F2 = gu.shape[-1] // 2
     v = gu.float().reshape(gu.shape[0], F2 // blk, 2, blk)
     return v[:, :, 0].reshape(gu.shape[0], F2), v[:, :, 1].reshape(gu.shape[0], F2)
@@ -390,7 +390,7 @@ def _blocked_split(gu, blk=128):
 
 def test_gemm_swiglu_fwd_matches_two_pass():
     """The gate|up projection with the SwiGLU in its epilogue (gemm256.hip copy_out_swiglu: gu and h = silu(g) u
-    from one 4-wave GEMM, gate / up in 128-column blocks) against the plain GEMM + the blocked SwiGLU kernel
+    from one 4-wave GEMM, gate / up in 64-column blocks) against the plain GEMM + the blocked SwiGLU kernel
     (bit-identical: same accumulation, same bf16 rounding, the SwiGLU kernel's formula) and an fp32 reference."""
     torch.manual_seed(5)
     C = _C()
@@ -399,15 +399,15 @@ def test_gemm_swiglu_fwd_matches_two_pass():
     x = (torch.randn(M, K, device="cuda") * 0.5).bfloat16()
     w = (torch.randn(2 * F, K, device="cuda") * 0.05).bfloat16()
     gu, h = C.gemm_swiglu_fwd(x, w)
-    gu2 = C.gemm(x, False, w, True, None, False, None, 0, None, False, 1.0, 1)
+    gu2 = C.gemm(x, True, w, True, None, False, None, 0, None, False, 1.0, 1)
     assert torch.equal(gu, gu2)
-    assert torch.equal(h, C.swiglu_fwd(gu2, 128))
+    assert torch.equal(h, C.swiglu_fwd(gu2, 64))
     g, u = _blocked_split((x.float() @ w.float().t()))
     assert _rel(h, torch.nn.functional.silu(g) * u) < 2e-2
 
 
 def test_gemm_swiglu_bwd_blocked_matches_two_pass():
-    """The SwiGLU backward in the down projection's data gradient on the 128-blocked gate|up layout (act -4) against
+    """The SwiGLU backward in the down projection's data gradient on the 64-blocked gate|up layout (act -4) against
     the two-pass form (blocked SwiGLU-backward kernel), bit-identical, and an fp32 reference."""
     torch.manual_seed(6)
     C = _C()
@@ -415,14 +415,14 @@ def test_gemm_swiglu_bwd_blocked_matches_two_pass():
     g = (torch.randn(M, K, device="cuda") * 0.5).bfloat16()
     w = (torch.randn(K, F, device="cuda") * 0.05).bfloat16()
     gu = torch.randn(M, 2 * F, device="cuda").bfloat16()
-    dgu = C.gemm_swiglu_bwd(g, w, gu, 128)
+    dgu = C.gemm_swiglu_bwd(g, w, gu, 64)
     dy = C.gemm(g, True, w, False, None, False, None, 0, None, False, 1.0, 1)
-    assert torch.equal(dgu, C.swiglu_bwd(gu, dy, 128))
+    assert torch.equal(dgu, C.swiglu_bwd(gu, dy, 64))
     gg, uu = _blocked_split(gu)
     s = torch.sigmoid(gg)
     d = g.float() @ w.float()
     dg, du = d * uu * s * (1 + gg * (1 - s)), d * gg * s
-    ref = torch.stack([dg.reshape(M, -1, 128), du.reshape(M, -1, 128)], 2).reshape(M, 2 * F)
+    ref = torch.stack([dg.reshape(M, -1, 64), du.reshape(M, -1, 64)], 2).reshape(M, 2 * F)
     assert _rel(dgu, ref) < 2e-2
 
 
@@ -434,7 +434,7 @@ def test_gemm_rope_matches_two_pass():
 
     torch.manual_seed(7)
     C = _C()
-    B, S, H, Hkv, D = 2, 1024, 8, 2, 128
+    B, S, H, Hkv, D = 8, 2048, 8, 2, 128  # 64 x 6 = 384 output tiles: a full wave of the 4-wave kernel
     M, N, Kd, rot = B * S, (H + 2 * Hkv) * D, 512, (H + Hkv) * D
     assert C.gemm_rope_ok(M, N, Kd, rot)
     x = (torch.randn(M, Kd, device="cuda") * 0.5).bfloat16()
@@ -442,7 +442,7 @@ def test_gemm_rope_matches_two_pass():
     pos = torch.arange(S, device="cuda", dtype=torch.int32).repeat(B)
     table = K.rope_table(4096, D, 500000.0, "cuda")
     y = C.gemm_rope(x, w, pos, table, rot)
-    y2 = C.gemm(x, False, w, True, None, False, None, 0, None, False, 1.0, 1)
+    y2 = C.gemm(x, True, w, True, None, False, None, 0, None, False, 1.0, 1)
     C.rope_(y2[:, :rot], pos, table, False)
     assert torch.equal(y, y2)
     ref = x.float() @ w.float().t()

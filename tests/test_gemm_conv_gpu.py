@@ -167,12 +167,12 @@ def test_elementwise_kernels(cuda, F2):
     a, b = gg.split(F2 // 2, -1)
     (F.silu(a) * b).backward(dy.float())
     assert _rel(_C().swiglu_bwd(gu, dy), gg.grad) < 1e-2
-    if (F2 // 2) % 128 == 0:  # the 128-blocked gate|up layout (Llama's fused gate|up epilogue) against the CPU op
+    if (F2 // 2) % 64 == 0:  # the 64-blocked gate|up layout (Llama's fused gate|up epilogue) against the CPU op
         gcpu = gu.cpu()
-        assert _rel(_C().swiglu_fwd(gu, 128), K.swiglu(gcpu.float(), blk=128)) < 1e-2
+        assert _rel(_C().swiglu_fwd(gu, 64).cpu(), K.swiglu(gcpu.float(), blk=64)) < 1e-2
         gq = gcpu.float().requires_grad_(True)
-        K.swiglu(gq, blk=128).backward(dy.cpu().float())
-        assert _rel(_C().swiglu_bwd(gu, dy, 128), gq.grad) < 1e-2
+        K.swiglu(gq, blk=64).backward(dy.cpu().float())
+        assert _rel(_C().swiglu_bwd(gu, dy, 64).cpu(), gq.grad) < 1e-2
     # rope forward then inverse = identity; matches the reference
     H, D = 4, 128
     x = torch.randn(T, H * D, device=cuda).bfloat16()

@@ -77,8 +77,8 @@ def _llama_twin(m, store, ids, labels, autocast):
                       True)
             x = x + o.reshape(B * S, -1) @ P[n + "self_attn.o_proj.weight"].t()
             h = _rms(x, P[n + "post_attention_layernorm.weight"], c.eps)
-            gu = h @ P[n + "mlp.gate_up_proj.weight"].t()  # rows in 128-blocked gate|up order (models/llama.py)
-            gu = gu.reshape(gu.shape[0], -1, 2, 128)
+            gu = h @ P[n + "mlp.gate_up_proj.weight"].t()  # rows in 64-blocked gate|up order (models/llama.py)
+            gu = gu.reshape(gu.shape[0], -1, 2, 64)
             g, u = gu[:, :, 0].reshape(gu.shape[0], -1), gu[:, :, 1].reshape(gu.shape[0], -1)
             x = x + (F.silu(g) * u) @ P[n + "mlp.down_proj.weight"].t()
         h = _rms(x, P["model.norm.weight"], c.eps)
@@ -217,6 +217,7 @@ def test_llama_swiglu_epilogue_matches_separate_pass(cuda):
     from k8s_amd.parallel.flat import ParamStore
 
     cfg = dataclasses.replace(M.LLAMA_TINY, layers=1, intermediate=4096, max_position=1024)
+    assert K._C().gemm_swiglu_fwd_ok(4 * 1024, cfg.intermediate, cfg.hidden)  # the epilogue path is the one taken
     out = []
     for epi in (False, True):
         K.SWIGLU_EPI = epi
@@ -248,8 +249,11 @@ def test_llama_rope_epilogue_matches_in_place_rope(cuda):
     from k8s_amd.ops import nn as K
     from k8s_amd.parallel.flat import ParamStore
 
-    cfg = dataclasses.replace(M.LLAMA_TINY, layers=1, hidden=1024, heads=8, kv_heads=2, intermediate=4096,
+    cfg = dataclasses.replace(M.LLAMA_TINY, layers=1, hidden=2048, heads=16, kv_heads=4, intermediate=4096,
                               max_position=1024)
+    # 8 x 1024 tokens x 24 heads of 128: 32 x 12 tiles of the 4-wave kernel, so the epilogue path is the one taken
+    assert K._C().gemm_rope_ok(8 * 1024, (cfg.heads + 2 * cfg.kv_heads) * 128, cfg.hidden,
+                               (cfg.heads + cfg.kv_heads) * 128)
     out = []
     for epi in (False, True):
         K.ROPE_EPI = epi
@@ -258,7 +262,7 @@ def test_llama_rope_epilogue_matches_in_place_rope(cuda):
             model = M.LlamaForCausalLM(store, cfg).finalize(cuda, seed=2)
             gen = torch.Generator(device=cuda)
             gen.manual_seed(3)
-            batch = M.synthetic_batch(cfg, 4, 1024, cuda, generator=gen)
+            batch = M.synthetic_batch(cfg, 8, 1024, cuda, generator=gen)
             store.begin_step()
             loss = model(*batch, dtype=torch.bfloat16)
             loss.backward()
