@@ -1155,6 +1155,14 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, 
                         st);
       return;
     }
+    // deep reductions (C >= 512: ResNet stage-3/4 conv1 / conv3) with whole 256 x 256 tiles filling the chip: the
+    // 4-wave kernel with the statistics epilogue (gemm256.hip copy_out_stats). Stream-K tails are not taken here
+    // (no workspace): such grids stay on the tile kernel.
+    if (!sg && !xform && !y_f32 && !bias && act == 0 && mode == 0 && stats && gemm_w4_stats_ok(M, K, C) &&
+        gemm256_plan(M, K, C).sk == 1) {
+      launch_gemm_w4_stats(x, C, w, C, reinterpret_cast<uint16_t*>(y), M, K, C, stats, nullptr, nullptr, st);
+      return;
+    }
     KMajor a{x, (long)C, M};
     if (xform) {
       const XForm xf{xform, C, make_fastdiv(C)};

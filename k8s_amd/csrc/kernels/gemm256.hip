@@ -804,6 +804,54 @@ __device__ __forceinline__ void copy_out_rope(uint16_t* __restrict__ C, const ch
   }
 }
 
+// ACT = 5: the BatchNorm statistics of the stored bf16 values (per-column sum / sum of squares -- the conv epilogue
+// statistics of gemm.hip, [kConvStatReplicas][2][N]) for ResNet's deep-reduction 1x1 convolutions. Every lane keeps the
+// sums of its fixed 8 columns (chunk lane & 15) over its rows; lanes l, l ^ 16, l ^ 32, l ^ 48 are folded by shuffles,
+// each wave parks its 128 + 128 partials at the head of its own (already copied-out) staged region, and after one
+// barrier thread t adds the two wave rows' partials of column t % 128 of wave column t / 128: 2 full-wave atomic
+// instructions per wave.
+template <class Off, class Stg>
+__device__ __forceinline__ void copy_out_stats(uint16_t* __restrict__ C, float* __restrict__ stats, char* smem,
+                                               char* stg, const Off& coff, const Stg& staged, int rep, int N, int n0) {
+  const int lane = threadIdx.x & 63;
+  float sm[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, sq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int it = 0; it < 32; ++it) {
+    const bf16x8_t v = staged(it);
+    *reinterpret_cast<bf16x8_t*>(C + coff(it)) = v;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const float f = bf2f((uint16_t)v[r]);
+      sm[r] += f;
+      sq[r] = __builtin_fmaf(f, f, sq[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    sm[r] += __shfl_xor(sm[r], 16);
+    sm[r] += __shfl_xor(sm[r], 32);
+    sq[r] += __shfl_xor(sq[r], 16);
+    sq[r] += __shfl_xor(sq[r], 32);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's staged reads are done: reuse its region
+  if (lane < 16) {
+    float* part = reinterpret_cast<float*>(stg);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      part[lane * 8 + r] = sm[r];
+      part[128 + lane * 8 + r] = sq[r];
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  g256::barrier();
+  const int t = threadIdx.x, wcol = t >> 7, c = t & 127;
+  const float* p0 = reinterpret_cast<const float*>(smem + (0 * 2 + wcol) * 32768);  // wave (wr 0, wc)
+  const float* p1 = reinterpret_cast<const float*>(smem + (1 * 2 + wcol) * 32768);  // wave (wr 1, wc)
+  float* d = stats + (long)rep * 2 * N + n0 + wcol * 128 + c;
+  atomicAdd(d, p0[c] + p1[c]);
+  atomicAdd(d + N, p0[128 + c] + p1[128 + c]);
+}
+
 template <bool AMN, bool BMN, bool X>
 __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __restrict__ A, long lda,
                                                              const uint16_t* __restrict__ B, long ldb, void* Cv,
@@ -1163,6 +1211,8 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
       }
     } else if (act == 3) {
       copy_out_swiglu(C, pre, stg, coff, staged, m0 + wr * 128, (n0 + wc * 128) / 2, N);
+    } else if (act == 5) {
+      copy_out_stats(C, cpart, smem, stg, coff, staged, (m0 >> 8) % kConvStatReplicas, N, n0);
     } else if (act == 4) {
       copy_out_rope(C, stg, (long)(m0 + wr * 128) * ldc + n0 + wc * 128, ldc, n0 + wc * 128 < rcols, rpos, rtab,
                     m0 + wr * 128);
@@ -1309,6 +1359,35 @@ void launch_gemm_w4_rope(const uint16_t* A, long lda, const uint16_t* B, long ld
   hipLaunchKernelGGL((g4::gemm_w4_kernel<false, false, true>), dim3(blocks), dim3(g4::THREADS), 0, st, A, lda, B, ldb,
                      (void*)y, (long)N, M, N, K, 1.f, kps, sk, 0, 0, nullptr, 4, nullptr, 0L, nullptr, pos, table,
                      rot_cols);
+}
+
+// ResNet's deep-reduction 1x1 convolution forwards with the BatchNorm statistics epilogue (copy_out_stats):
+// y [M][N] = x [M][K] . w [N][K]^T, stats [kConvStatReplicas][2][N] (zeroed by the caller). $K8S_AMD_W4_STATS=0 keeps
+// them on the 128 x 128 tile kernel (A/B; read per call); K8S_AMD_W4_STATS_MINK (default 512) is the smallest
+// reduction taken.
+bool gemm_w4_stats_ok(int M, int N, int K) {
+  const char* e = getenv("K8S_AMD_W4_STATS");
+  if (e && e[0] == '0') return false;
+  const char* mk = getenv("K8S_AMD_W4_STATS_MINK");
+  const int mink = mk ? atoi(mk) : 512;
+  return w4_enabled() && K >= mink && M % 256 == 0 && N % 256 == 0 && K % 64 == 0 &&
+         (long)(M / 256) * (N / 256) >= planner_cus();
+}
+void launch_gemm_w4_stats(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* y, int M, int N, int K,
+                          float* stats, float* sk_slabs, int* sk_sync, hipStream_t st) {
+  Gemm256Plan plan = gemm256_plan(M, N, K);
+  if (!sk_slabs || !sk_sync) plan.sk = 1;
+  const int tiles = (M / 256) * (N / 256);
+  g256r::SkArgs sk{tiles, 1, nullptr, nullptr};
+  int blocks = tiles, kps = K;
+  if (plan.sk > 1) {
+    sk = g256r::SkArgs{plan.full, plan.sk, sk_slabs, sk_sync};
+    kps = plan.kps;
+    blocks = plan.full + (tiles - plan.full) * plan.sk;
+  }
+  hipLaunchKernelGGL((g4::gemm_w4_kernel<false, false, true>), dim3(blocks), dim3(g4::THREADS), 0, st, A, lda, B, ldb,
+                     (void*)y, (long)N, M, N, K, 1.f, kps, sk, 0, 0, nullptr, 5, nullptr, 0L, stats, nullptr, nullptr,
+                     0);
 }
 
 // Stream-K tail plan for a grid of 256 x 256 tiles on P = planner_cus() CUs (one block per CU; 256 on MI355X): with

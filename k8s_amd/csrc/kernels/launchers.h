@@ -111,6 +111,9 @@ bool gemm_w4_swiglu_ok(int M, int F, int K, long lda, long ldb);
 void launch_gemm_w4_swiglu_bwd(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* dgu,
                                const uint16_t* gu, int M, int F, int K, int blk, float* sk_slabs, int* sk_sync,
                                hipStream_t st);
+bool gemm_w4_stats_ok(int M, int N, int K);
+void launch_gemm_w4_stats(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* y, int M, int N, int K,
+                          float* stats, float* sk_slabs, int* sk_sync, hipStream_t st);
 bool gemm_w4_rope_ok(int M, int N, int K, long lda, long ldb, int rot_cols);
 void launch_gemm_w4_rope(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* y, int M, int N, int K,
                          const int* pos, const float* table, int rot_cols, float* sk_slabs, int* sk_sync,

@@ -502,3 +502,28 @@ def test_gemm256_splitk(cuda, M, N, K, ak, bk, accumulate):
     out = base.clone() if accumulate else None
     c = _C().gemm(A, ak, B, bk, out, True, None, 0, None, accumulate, 1.0, 0)
     assert _rel(c, ref + (base if accumulate else 0)) < 2e-3
+
+
+@pytest.mark.parametrize("shape", [(1024, 16, 16, 1024, 256), (256, 14, 14, 512, 2048)])
+def test_conv1x1_deep_w4_stats_epilogue(cuda, shape, monkeypatch):
+    """ResNet's deep-reduction 1x1 forwards on the 4-wave GEMM with the BatchNorm-statistics epilogue (gemm256.hip
+    copy_out_stats; whole 256 x 256 tiles filling the chip): y against an fp32 reference, the statistics against the
+    stored values, and both against the 128 x 128 tile kernel (K8S_AMD_W4_STATS=0)."""
+    N, H, W, C, K = shape
+    assert _C().gemm_rope_ok is not None  # (the extension is the in-tree one)
+    torch.manual_seed(9)
+    x = (torch.randn(N, H, W, C, device=cuda) * 0.5).bfloat16()
+    w = (torch.randn(K, 1, 1, C, device=cuda) * 0.03).bfloat16()
+    out = {}
+    for arm in ("1", "0"):
+        monkeypatch.setenv("K8S_AMD_W4_STATS", arm)
+        stats = torch.zeros(_C().conv_stat_replicas, 2, K, device=cuda)
+        y = _C().conv_fwd(x, w, 1, 0, 1, False, None, 0, stats)
+        out[arm] = (y, stats.sum(0))
+    ref = x.float().reshape(-1, C) @ w.float().reshape(K, C).t()
+    for arm, (y, tot) in out.items():
+        yf = y.float().reshape(-1, K)
+        assert _rel(yf, ref) < 1e-2, arm
+        assert _rel(tot[0], yf.sum(0)) < 1e-3, arm
+        assert _rel(tot[1], (yf * yf).sum(0)) < 1e-3, arm
+    assert _rel(out["1"][0], out["0"][0]) < 5e-3
