@@ -1428,7 +1428,16 @@ long gemm256_sk_sync_ints(const Gemm256Plan& p) { return p.sk > 1 ? (long)(p.til
 bool gemm256_eligible(int M, int N, int K, bool a_kmajor, bool b_kmajor) {
   // short reductions (ResNet's 1x1 convolutions as GEMMs, K = 64..512) leave the 5-stage ring mostly in its
   // prologue/epilogue; the 128 x 128 kernel's single-buffered 3-blocks/CU variant is built for them
-  if (K % 64 != 0 || K < 768) return false;
+  if (K % 64 != 0) return false;
+  if (K < 768) {
+    // K = 512 (8 stages): the 4-wave kernel's 2-stage pipeline, not the ring, when it takes the whole-tile grid --
+    // K8S_AMD_GEMM256_MINK (default 768: off) for the A/B
+    const char* e = getenv("K8S_AMD_GEMM256_MINK");
+    const int mink = e ? atoi(e) : 768;
+    if (K < mink || !w4_enabled() || M % 256 != 0 || N % 256 != 0 ||
+        (long)(M / 256) * (N / 256) < planner_cus())
+      return false;
+  }
   if (!a_kmajor && M % 8 != 0) return false;
   if (!b_kmajor && N % 8 != 0) return false;
   if (N % 4 != 0) return false;

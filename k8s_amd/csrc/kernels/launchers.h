@@ -268,6 +268,7 @@ void launch_stem_wgrad(const uint16_t* xs, const uint16_t* dy, float* ws, float*
 void launch_stem_dw_s2d(const float* dw4, int K, int R, int Cw, float* dw7, hipStream_t st);
 
 // ---- NHWC max pooling (pool.hip): idx = winning window position per output element (uint8)
+void launch_subsample_nhwc(const uint16_t* x, uint16_t* y, int N, int H, int W, int C, int s, hipStream_t st);
 void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
                         int k, int s, int p, hipStream_t st);
 void launch_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W, int C, int Ho,

@@ -321,4 +321,27 @@ void launch_avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, 
                      make_fastdiv(C / 8), make_fastdiv(HW), 1.f / (float)HW);
 }
 
+// Stride-s subsample of an NHWC tensor, y[n][i][j][:] = x[n][s i][s j][:] (the input of a 1x1 / stride-s / pad-0
+// convolution, which then runs as a plain stride-1 GEMM on y: ResNet's downsample convolutions). One 16-B chunk per
+// thread, grid-strided; the source rows are read as whole 16-B pieces.
+__global__ void __launch_bounds__(256) subsample_nhwc_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                             long total, int Ho, int Wo, int H, int W, int C8,
+                                                             int s) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long pix = e / C8;
+    const int c = (int)(e - pix * C8);
+    const long n = pix / ((long)Ho * Wo);
+    const int r = (int)(pix - n * Ho * Wo), i = r / Wo, j = r - i * Wo;
+    const long src = ((n * H + (long)i * s) * W + (long)j * s) * C8 + c;
+    reinterpret_cast<bf16x8_t*>(y)[e] = reinterpret_cast<const bf16x8_t*>(x)[src];
+  }
+}
+
+void launch_subsample_nhwc(const uint16_t* x, uint16_t* y, int N, int H, int W, int C, int s, hipStream_t st) {
+  const int Ho = (H + s - 1) / s, Wo = (W + s - 1) / s;
+  const long total = (long)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(subsample_nhwc_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, st, x, y, total, Ho, Wo, H,
+                     W, C / 8, s);
+}
+
 }  // namespace k8s_amd

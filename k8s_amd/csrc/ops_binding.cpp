@@ -1076,6 +1076,16 @@ void embed_bwd(Tensor g, std::vector<Tensor> grads, std::vector<c10::optional<Te
 }
 
 // ------------------------------------------------------------------ space-to-depth stem
+// y[n][i][j] = x[n][s i][s j]: the input of a 1x1 / stride-s / pad-0 convolution as a contiguous tensor
+Tensor subsample_nhwc(Tensor x, int64_t s) {
+  check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous() && x.size(3) % 8 == 0 && s >= 1, "x: contiguous NHWC, C % 8 == 0");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  auto y = torch::empty({N, (H + s - 1) / s, (W + s - 1) / s, C}, x.options());
+  k8s_amd::launch_subsample_nhwc(cbf(x), bf(y), N, H, W, C, (int)s, cur_stream());
+  return y;
+}
+
 Tensor stem_s2d_input(Tensor x, int64_t pad) {
   check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x");
   TORCH_CHECK(x.dim() == 4 && x.size(3) <= 8, "x must be NHWC with <= 8 channels");
@@ -1228,6 +1238,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_bwd", &embed_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("stem_s2d_input", &stem_s2d_input);
+  m.def("subsample_nhwc", &subsample_nhwc, py::arg("x"), py::arg("s"));
   m.def("stem_w_s2d", &stem_w_s2d);
   m.def("stem_conv_fwd", &stem_conv_fwd);
   m.def("stem_wgrad", &stem_wgrad);

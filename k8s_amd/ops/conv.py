@@ -24,10 +24,11 @@ view; on the GPU they are counted in ``STATS`` and warned about once.
 """
 from __future__ import annotations
 
+import os
+import warnings
+
 import torch
 import torch.nn.functional as F
-
-import warnings
 
 from k8s_amd.ops._ext import load as _load
 
@@ -195,13 +196,19 @@ def _dgrad_strided_hip(C_, gy, w, stride, padding, H, W, addend=None):
     return dx
 
 
-def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, xform=None):
+def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, xform=None, x_sub=None):
     """Returns dx (+ ``addend``, e.g. the residual branch's gradient of the same tensor, fused into the
     dgrad epilogue where our kernel runs) or None; deposits dw into ``p``'s flat gradient slot. ``xform``: the
     convolution's input is relu(bn(x)) normalised on load (see ``_wgrad_hip``); dx is then the gradient w.r.t.
-    that normalised input."""
+    that normalised input. ``x_sub``: a 1x1 / pad-0 convolution's input already subsampled by its stride
+    (``nn._Conv2dNHWC`` with ``subsample_ok``): the weight gradient runs as the stride-1 product on it; ``x`` then only gives dx's shape."""
     K, R, S, C = w.shape
     C_ = _load() if gy.is_cuda else None
+    if x_sub is not None:
+        _wgrad_hip(C_, gy, x_sub, p.grad.view(p.shape), 1, 0, p.written)
+        STATS["hip_wgrad"] += 1
+        p.store._notify(p) if p.written else p.store.mark_written(p)
+        p = None  # done
     hip = _hip(gy, x, w)
     if xform is not None and not (hip and C % 64 == 0 and K % 8 == 0 and p is not None
                                   and p.grad.dtype == torch.float32):
@@ -235,6 +242,19 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, xform=None
             if addend is not None:
                 dx = dx + addend
     return _finish_dw(dx, dw_done, p, gy, x, w, stride, padding)
+
+
+# 1x1 / stride-2 / pad-0 convolutions (ResNet's downsample branch) as stride-1 GEMMs on the subsampled input: one
+# subsample pass (pool.hip), then the forward (with the BN statistics, the 4-wave / short-K kernels) and the weight
+# gradient take the plain-GEMM paths instead of the strided implicit-GEMM gather; the data gradient keeps the
+# strided parity path (it accumulates onto the block input's other gradient). K8S_AMD_SUB1X1=0 for the A/B.
+SUB1X1 = os.environ.get("K8S_AMD_SUB1X1", "1") != "0"
+
+
+def subsample_ok(x, w, stride, padding) -> bool:
+    K, R, S, C = w.shape
+    return (SUB1X1 and stride > 1 and R == 1 and S == 1 and padding == 0 and _hip(x, w) and C % 64 == 0
+            and K % 8 == 0 and x.is_contiguous())
 
 
 def _finish_dw(dx, dw_done, p, gy, x, w, stride, padding):

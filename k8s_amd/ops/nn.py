@@ -127,8 +127,13 @@ class _Conv2dNHWC(torch.autograd.Function):
         if with_stats and impl.fwd_uses_hip(x, w, stride, padding):
             sums = _zero_scratch(p.store, x.device, _C().conv_stat_replicas * 2 * w.shape[0]).view(
                 _C().conv_stat_replicas, 2, w.shape[0])
-        y = impl.conv_fwd(x, w, stride, padding, sums)
-        ctx.save_for_backward(x)
+        xs = None
+        if impl.subsample_ok(x, w, stride, padding):  # 1x1 / stride 2: a stride-1 GEMM on the subsampled input
+            xs = _C().subsample_nhwc(x, stride)
+            y = impl.conv_fwd(xs, w, 1, 0, sums)
+        else:
+            y = impl.conv_fwd(x, w, stride, padding, sums)
+        ctx.save_for_backward(x, xs)
         ctx.p, ctx.stride, ctx.padding, ctx.link = p, stride, padding, link
         ctx.x_requires_grad = x.requires_grad
         if sums is not None:
@@ -140,7 +145,7 @@ class _Conv2dNHWC(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy, _gsums=None):
-        (x,) = ctx.saved_tensors
+        x, xs = ctx.saved_tensors
         p = ctx.p
         impl = _conv_impl()
         w = p.weight if x.dtype == p.weight.dtype else p.master.to(x.dtype)
@@ -149,9 +154,9 @@ class _Conv2dNHWC(torch.autograd.Function):
         if ctx.link is not None:
             addend, ctx.link.grad = ctx.link.grad, None
             if addend is None and ctx.link.shared and ctx.x_requires_grad:  # first of the two readers of x
-                ctx.link.grad = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, True, p)
+                ctx.link.grad = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, True, p, x_sub=xs)
                 return None, None, None, None, None, None, None
-        dx = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, ctx.x_requires_grad, p, addend=addend)
+        dx = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, ctx.x_requires_grad, p, addend=addend, x_sub=xs)
         return dx, None, None, None, None, None, None
 
 

@@ -5,8 +5,9 @@ BatchNorm (forward apply, backward reduce + apply) of ResNet-50 v1.5 at the benc
 often the shape occurs per step, and prints one JSON line per (layer, op) with the achieved TFLOP/s (convs) or
 TB/s of compulsory HBM traffic (BN), then a summary line. Shapes and dispatch are exactly the trainer's
 (``ops/conv.py``, ``ops/nn.py``): the stem is the space-to-depth 4x4 kernel pair of ``stem.hip``, the conv3 layers
-read their input normalised on load (BN2, ``nn._BnReluConv``: forward and weight gradient with ``xform``), and the
-identity blocks' conv1 data gradient adds the masked residual gradient in its epilogue (``nn.MaskedGrad``).
+of stages 1-2 read their input normalised on load (BN2, ``nn._BnReluConv``: forward and weight gradient with
+``xform``; ``nn.ONLOAD_MAXC``), and the identity blocks' conv1 data gradient adds the masked residual gradient in its
+epilogue (``nn.MaskedGrad``) -- counted in that row's floor bytes.
 
     python scripts/layer_roofline.py [--batch 1024] [--reps 5]
 """
@@ -83,7 +84,9 @@ def main():
         res = {}
         # the bench's operand paths (module docstring)
         xf = None
-        if name.endswith("conv3"):
+        from k8s_amd.ops import nn as K_nn
+
+        if name.endswith("conv3") and C <= K_nn.ONLOAD_MAXC:  # bn2 on load only up to ONLOAD_MAXC channels (round 6)
             xf = torch.cat([torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1]).contiguous()
         addend = None
         if name.endswith("bx.conv1"):
@@ -116,11 +119,16 @@ def main():
         # compulsory HBM bytes per op (bf16 activations, fp32 weight gradient) and the speed-of-light floor
         # max(bytes / 8 TB/s, flops / 2.5 PF/s): "sol" = floor / measured.
         xb, yb, wb = N * H * H * C * 2, M * K * 2, K * R * R * C * 2
-        nb = {"fwd": xb + yb + wb, "wgrad": xb + yb + 2 * wb, "dgrad": yb + xb + wb}
+        # fused operands each form really moves (round 6): the identity blocks' conv1 data
+        # gradient also reads the masked residual addend (bf16, dx's shape) and its packed ReLU bits (1 bit / element);
+        # the normalize-on-load forms read the same bytes as the plain ones; the statistics outputs are [R][2][K]
+        dg_extra = (xb + xb // 16) if addend is not None else 0
+        nb = {"fwd": xb + yb + wb, "wgrad": xb + yb + 2 * wb, "dgrad": yb + xb + wb + dg_extra}
         for op in ("fwd", "wgrad", "dgrad"):
             if op in res:
                 floor = max(nb[op] / 8e9, flops / 2.5e12)
                 rows.append({"layer": name, "op": op, "count": cnt, "batch": N, "ms": round(res[op], 4),
+                             "gbytes": round(nb[op] / 1e9, 3), "onload": bool(xf is not None and op != "dgrad"),
                              "step_ms": round(res[op] * cnt, 3), "tflops": round(flops / res[op] / 1e9, 1),
                              "floor_ms": round(floor, 4), "sol": round(floor / res[op], 2),
                              "lost_ms_per_step": round((res[op] - floor) * cnt, 3)})

@@ -527,3 +527,35 @@ def test_conv1x1_deep_w4_stats_epilogue(cuda, shape, monkeypatch):
         assert _rel(tot[0], yf.sum(0)) < 1e-3, arm
         assert _rel(tot[1], (yf * yf).sum(0)) < 1e-3, arm
     assert _rel(out["1"][0], out["0"][0]) < 5e-3
+
+
+@pytest.mark.parametrize("arm", ["1", "0"])
+def test_downsample_1x1_stride2_subsampled(cuda, arm, monkeypatch):
+    """The 1x1 / stride-2 downsample convolution as a stride-1 GEMM on the subsampled input (pool.hip
+    subsample_nhwc; ops.conv.SUB1X1) and on the strided implicit-GEMM path: y, BN statistics, dx and dW against
+    fp32 PyTorch."""
+    from k8s_amd.ops import conv as kc
+    from k8s_amd.ops import nn as K
+    from k8s_amd.parallel.flat import ParamStore, init_normal
+
+    monkeypatch.setattr(kc, "SUB1X1", arm == "1")
+    torch.manual_seed(10)
+    N, H, C, Ko = 8, 28, 256, 512
+    store = ParamStore()
+    p = store.new("down", (Ko, 1, 1, C), init_normal(0.05))
+    store.finalize(cuda)
+    x = torch.randn(N, H, H, C, device=cuda).bfloat16().requires_grad_(True)
+    store.begin_step()
+    y, sums = K.conv2d_nhwc(x, p, 2, 0, with_stats=True)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = p.master.detach().clone().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.conv2d(xr, wr.bfloat16().float(), None, 2, 0)
+    yr.backward(gy.float().permute(0, 3, 1, 2))
+    yrf = yr.detach().permute(0, 2, 3, 1)
+    assert _rel(y, yrf) < 1e-2
+    yf = y.float().reshape(-1, Ko)
+    assert _rel(sums.sum(0)[0], yf.sum(0)) < 1e-3
+    assert _rel(x.grad, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+    assert _rel(p.grad, wr.grad.permute(0, 2, 3, 1)) < 1e-2
