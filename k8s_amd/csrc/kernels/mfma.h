@@ -45,6 +45,16 @@ __device__ __forceinline__ short4_t tr16(const char* addr) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(addr));
 }
 
+// the same from an LDS-address-space base and a byte offset: pointer arithmetic in address space 3, so a constant part
+// of the offset can fold into the instruction's 16-bit offset field (the generic-pointer form adds it in VALU)
+typedef __attribute__((address_space(3))) char lds_char;
+__device__ __forceinline__ const lds_char* lds_ptr(const void* p) {
+  return (const lds_char*)(p);
+}
+__device__ __forceinline__ short4_t tr16l(const lds_char* base, int off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(base + off));
+}
+
 // ds_read_b64_tr_b16 as inline asm. hipcc (ROCm 7.2) cannot prove that the builtin's read does not alias an
 // in-flight global_load_lds into the same LDS array and puts `s_waitcnt vmcnt(0)` in front of it, which drains a
 // counted LDS-DMA pipeline every K step (seen in the .s of gemm256r / wgrad_stream). The asm form is invisible to

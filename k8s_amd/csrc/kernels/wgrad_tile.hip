@@ -11,6 +11,9 @@
 // lanes), and each block keeps its fp32 partial of the piece in accumulator registers (wave w: output columns
 // 144 w .. 144 w + 143) until its last tile; wg3_reduce1/2 sum the blocks' partials into dw.
 //   LDS images: [position][64 ch] bf16, 128-B rows, 16-B chunk c of row p at c ^ (p & 7) (window and dy alike).
+//   Wave w computes q tiles 4 tap + w (channel group w of every tap), so a tap's row / column offsets are compile-time;
+//   with the window pitch a multiple of 8, per k step each lane forms 3 addresses per pixel (column taps) and the row
+//   taps are immediate offsets (round 6: the per-tap swizzle arithmetic was 3.3 VALU per MFMA).
 //   tile: RT rows x W pixels, RT * W = 224 (7 k-steps of 32 pixels; a tile may run past the image: zero dy rows;
 //   the W = 16 test shape: 2 rows)
 #include <algorithm>
@@ -36,16 +39,29 @@ __global__ void __launch_bounds__(256, 2) wgrad3x3_kernel(const uint16_t* __rest
                                                          const uint16_t* __restrict__ dy, float* __restrict__ ws,
                                                          int H, int C, int K, int tiles_per_img, int ntiles,
                                                          const float* __restrict__ xf) {
-  constexpr int WP = W + 2, WIN = (RT + 2) * WP, PX = RT * W, NKS = PX / 32;
+  // window pitch a multiple of 8 positions: a position's swizzle (p & 7) is then the same for the three filter rows,
+  // so the row taps are immediate LDS offsets of one per-(k step, column tap) address
+  constexpr int WP = (W + 2 + 7) / 8 * 8, WIN = (RT + 2) * WP, PX = RT * W, NKS = PX / 32;
   static_assert(PX % 32 == 0, "whole 32-pixel k steps");
   __shared__ __attribute__((aligned(1024))) char smem[(WIN + PX) * 128];
   char* const xw = smem;
   char* const dl = smem + WIN * 128;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, G = lane >> 4, q4 = li >> 2, p4 = li & 3;
   const int cpieces = C / CS, k0 = (blockIdx.y / cpieces) * CS, c0 = (blockIdx.y % cpieces) * CS;
+  const int hb = (p4 & 1) * 8, c1 = p4 >> 1;
+  // dy^T fragment offsets in the dy image, tile- and k-step-invariant: the k step's first pixel 32 ks + 8 G is a
+  // multiple of 8, so the swizzle of pixel + q4 (+ 4) is q4 (+ 4); a k step adds 32 positions (4 KB, uniform)
+  int aoff[4][2];
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) {
+    const int ch16 = 2 * kt + c1;
+    aoff[kt][0] = (8 * G + q4) * 128 + ((ch16 ^ q4) << 4) + hb;
+    aoff[kt][1] = (8 * G + 4 + q4) * 128 + ((ch16 ^ (q4 + 4)) << 4) + hb;
+  }
+  const int cq5 = wid << 5;  // this wave's 16-channel group (q tile 4 tap + wid) as a swizzled-chunk XOR term
 
-  f32x4_t acc[4][9];  // [k tile][q tile 9 wid + j]: lane holds piece[16 kt + 4 G + r][16 (9 wid + j) + li]
+  f32x4_t acc[4][9];  // [k tile][tap j]: lane holds piece[16 kt + 4 G + r][16 (4 j + wid) + li]
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -112,29 +128,31 @@ __global__ void __launch_bounds__(256, 2) wgrad3x3_kernel(const uint16_t* __rest
       }
       __syncthreads();
     }
-#pragma unroll 1
+#pragma unroll  // (unrolled: the dy reads' k-step offsets are immediates, the window addresses tile-invariant)
     for (int ks = 0; ks < NKS; ++ks) {
-      const int pb = 32 * ks + 8 * G;  // this lane group's 8 pixels of the k step
-      mfma_bf16x8 af[4];               // dy^T: row = output channel 16 kt + li, k = 8 pixels
+      const lds_char* const dk = lds_ptr(dl) + ks * 4096;
+      mfma_bf16x8 af[4];  // dy^T: row = output channel 16 kt + li, k = 8 pixels
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        const int ch16 = 2 * kt + (p4 >> 1);
-        const short4_t lo = tr16(dl + off(pb + q4, ch16) + (p4 & 1) * 8);
-        const short4_t hi = tr16(dl + off(pb + 4 + q4, ch16) + (p4 & 1) * 8);
-        af[kt] = join8(lo, hi);
-      }
-      // window positions of this lane's two pixels (pb + q4, pb + 4 + q4) at tap (0, 0)
-      const int pa = pb + q4, pc = pb + 4 + q4;
+      for (int kt = 0; kt < 4; ++kt) af[kt] = join8(tr16l(dk, aoff[kt][0]), tr16l(dk, aoff[kt][1]));
+      // window positions of this lane's two pixels (pb + q4, pb + 4 + q4) at tap (0, 0), and per column tap s the
+      // byte address of this wave's 16-channel group there (row taps: + r WP 128, immediate)
+      const int pa = 32 * ks + 8 * G + q4, pc = pa + 4;
       const int ra = pa / W, rc = pc / W;
       const int posa = ra * WP + (pa - ra * W), posc = rc * WP + (pc - rc * W);
+      int za[3], zc[3];
 #pragma unroll
-      for (int j = 0; j < 9; ++j) {
-        const int qt = 9 * wid + j, tap = qt >> 2, cq = qt & 3, tr = tap / 3, ts = tap - tr * 3;
-        const int toff = tr * WP + ts;
-        const int ch16 = 2 * cq + (p4 >> 1);
-        const short4_t lo = tr16(xw + off(posa + toff, ch16) + (p4 & 1) * 8);
-        const short4_t hi = tr16(xw + off(posc + toff, ch16) + (p4 & 1) * 8);
-        const mfma_bf16x8 bf = join8(lo, hi);
+      for (int s_ = 0; s_ < 3; ++s_) {
+        const int qa = posa + s_, qc = posc + s_;
+        za[s_] = qa * 128 + hb + (cq5 ^ (((qa & 7) ^ c1) << 4));
+        zc[s_] = qc * 128 + hb + (cq5 ^ (((qc & 7) ^ c1) << 4));
+        // opaque: otherwise the compiler re-associates the row-tap constants into the sums and adds per read
+        asm volatile("" : "+v"(za[s_]), "+v"(zc[s_]));
+      }
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {  // tap j = 3 r + s (compile-time), channel group wid
+        const int r_ = j / 3, s_ = j - 3 * r_;
+        const lds_char* const xr = lds_ptr(xw) + r_ * WP * 128;  // (immediate)
+        const mfma_bf16x8 bf = join8(tr16l(xr, za[s_]), tr16l(xr, zc[s_]));
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) acc[kt][j] = mfma16(af[kt], bf, acc[kt][j]);
       }
@@ -147,7 +165,7 @@ __global__ void __launch_bounds__(256, 2) wgrad3x3_kernel(const uint16_t* __rest
 #pragma unroll
     for (int j = 0; j < 9; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) out[(kt * 16 + G * 4 + r) * NQ + (9 * wid + j) * 16 + li] = acc[kt][j][r];
+      for (int r = 0; r < 4; ++r) out[(kt * 16 + G * 4 + r) * NQ + (4 * j + wid) * 16 + li] = acc[kt][j][r];
 }
 
 // Two-pass deterministic sum of the nb per-block partials of every piece: pass 1 (blockIdx.y = slab group s of SG)
