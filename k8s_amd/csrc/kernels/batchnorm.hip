@@ -515,6 +515,30 @@ __global__ void __launch_bounds__(256) bn_bwd_final_kernel(const float* __restri
   }
 }
 
+// bn_bwd_final_kernel for sums accumulated by a data-gradient epilogue (gemm_short.hip EPI 3 / 4): replicas
+// [nrep][2][C], slot 0 of `sg` = sum g, slot 1 of `sd` = sum g (x - mean) (dual: the second BatchNorm's sums share g)
+__global__ void __launch_bounds__(256) bn_bwd_final_sums_kernel(const float* __restrict__ sg,
+                                                                const float* __restrict__ sd, int nrep, int C,
+                                                                float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                                float inv_m, const float* __restrict__ mean,
+                                                                const float* __restrict__ invstd,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta,
+                                                                float* __restrict__ params) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f, b = 0.f;
+#pragma unroll 16
+  for (int r = 0; r < nrep; ++r) {
+    a += sg[(long)r * 2 * C + c];
+    b += sd[(long)r * 2 * C + C + c];
+  }
+  b *= invstd[c];
+  if (dbeta) dbeta[c] = a;
+  if (dgamma) dgamma[c] = b;
+  bn_bwd_consts(c, C, a, b, inv_m, mean, invstd, gamma, beta, params);
+}
+
 // dx = sc*dy_eff + B*x + D; dres = dy_eff. dy_eff = dy masked by the packed bits (residual BN), by relu_on(x)
 // (non-residual BN + ReLU) or not at all. One vector per thread (see the header).
 __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(const uint16_t* __restrict__ dy,
@@ -925,6 +949,34 @@ void launch_bn_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, con
   hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, nb, C, dgamma, dbeta,
                      1.f / (float)M, mean, invstd, gamma, beta, params);
   launch_bn_bwd_apply(dy, x, mask, params, relu_x, dx, dres, M, C, st);
+}
+
+// launch_bn_bwd with the reduce done by dy's producer (the sums of bn_bwd_final_sums_kernel): the final and apply
+// passes only. mask: the packed ReLU bits (residual BatchNorm).
+void launch_bn_bwd_from_sums(const uint16_t* dy, const uint16_t* x, const uint8_t* mask, const float* sums, int nrep,
+                             const float* mean, const float* invstd, const float* gamma, const float* beta,
+                             uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, float* params, long M, int C,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_final_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, sums, nrep, C, dgamma,
+                     dbeta, 1.f / (float)M, mean, invstd, gamma, beta, params);
+  launch_bn_bwd_apply(dy, x, mask, params, false, dx, dres, M, C, st);
+}
+
+void launch_bn_bwd_dual_from_sums(const uint16_t* dy, const uint8_t* mask, const uint16_t* x, const float* sums,
+                                  int nrep, const float* mean, const float* invstd, const float* gamma,
+                                  const float* beta, uint16_t* dx, float* dgamma, float* dbeta, float* params,
+                                  const uint16_t* x2, const float* sums2, const float* mean2, const float* invstd2,
+                                  const float* gamma2, const float* beta2, uint16_t* dx2, float* dgamma2,
+                                  float* dbeta2, float* params2, long M, int C, hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_final_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, sums, nrep, C, dgamma,
+                     dbeta, 1.f / (float)M, mean, invstd, gamma, beta, params);
+  hipLaunchKernelGGL(bn_bwd_final_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, sums2, nrep, C, dgamma2,
+                     dbeta2, 1.f / (float)M, mean2, invstd2, gamma2, beta2, params2);
+  const long nvec = M * C / 8;
+  if (nvec >= (1L << 31)) throw std::runtime_error("BatchNorm tensor too large (>= 2^31 vectors)");
+  hipLaunchKernelGGL(bn_bwd_apply_dual_kernel, dim3(cdiv(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, dy, mask, x,
+                     params, dx, x2, params2, dx2, (int)nvec, C, make_fastdiv(C / 8),
+                     stream_order_mode() ? (stream_dir(0) ? 1 : 2) : 0);
 }
 
 // Backward of launch_bn_fwd_from_sums_dual: both BatchNorms' (dgamma, dbeta, dx) from one masked dy in one reduce

@@ -52,12 +52,22 @@ struct Args {
   const uint8_t* mask;   // EPI 2: packed bits of the addend (bit j of byte e keeps element 8 e + j)
   const float* xf;       // XF: [2][K] scale | shift
   float* stats;          // STATS: [REPL][2][N]
+  // EPI 3 / 4: BatchNorm-backward statistics of the stored output (see the kernel's epilogue)
+  const uint16_t* bx;    // the BatchNorm's input [M][N]
+  const uint16_t* bx2;   // EPI 4: the second BatchNorm's input [M][N]
+  const uint8_t* bmask;  // the BatchNorm's packed ReLU bits [M][N / 8]
+  const float* bmean;    // [N]
+  const float* bmean2;   // EPI 4: [N]
+  float* bst;            // [REPL][2][N]: sum g, sum g (x - mean)
+  float* bst2;           // EPI 4: [REPL][2][N], slot 1: sum g (x2 - mean2)
   int M, N, lda, ldb;
   int P, G;              // column panels, row groups
 };
 
 // A-fragment ring depth (tiles in flight incl. the one being computed), tile rows and waves per SIMD: sized so the
 // ring fits beside the accumulators, the statistics and (EPI > 0) the addend in 256 registers (2 waves per SIMD)
+// EPI: 0 plain store, 1 accumulate onto C, 2 + a masked addend, 3 = 2 + the BatchNorm-backward statistics of the
+// stored result (one BatchNorm), 4 = 3 for two BatchNorms fed by the same masked gradient
 template <int K, int EPI, bool XF, bool STATS>
 struct Cfg {
   static constexpr int KC = K / 32;
@@ -66,7 +76,7 @@ struct Cfg {
   // epilogues then overlap across the two waves; at one wave per SIMD with 32-row tiles they serialised)
   static constexpr int TM = HEAVY || K == 256 ? 16 : 32;
   static constexpr int OCC = 2;
-  static constexpr int NBUF = (!HEAVY && K != 128) || (EPI != 0 && K <= 128) ? 3 : 2;
+  static constexpr int NBUF = (!HEAVY && K != 128) || (EPI != 0 && EPI < 3 && K <= 128) || (EPI == 3 && K == 64) ? 3 : 2;
 };
 
 __device__ __forceinline__ mfma_bf16x8 as_frag(i32x4 v) { return __builtin_bit_cast(mfma_bf16x8, v); }
@@ -119,8 +129,11 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
   constexpr int WBYTES = NB * KC * 1024;
   constexpr int XBYTES = XF ? KC * 4 * 64 : 0;
   constexpr int SBYTES = TM * 128;  // per-wave staging of half a bf16 output tile (64 columns; the copy-out)
-  constexpr int STG = (WBYTES + XBYTES + 1023) / 1024 * 1024;
-  constexpr int RBYTES = STATS ? 4 * 2 * BN * 4 : 0;
+  constexpr bool BST = EPI >= 3;
+  constexpr int NS = EPI == 4 ? 3 : 2;  // BatchNorm-backward sums: g, g (x - mean) [, g (x2 - mean2)]
+  constexpr int MBYTES = BST ? (NS - 1) * BN * 4 : 0;
+  constexpr int STG = (WBYTES + XBYTES + MBYTES + 1023) / 1024 * 1024;
+  constexpr int RBYTES = STATS ? 4 * 2 * BN * 4 : BST ? 4 * NS * BN * 4 : 0;
   constexpr int LDS = STG + 4 * SBYTES > RBYTES ? STG + 4 * SBYTES : RBYTES;
   __shared__ __attribute__((aligned(1024))) char smem[LDS];
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -152,6 +165,13 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
       tab[c] = g.xf[(e >> 3) * K + kc * 32 + q * 8 + (e & 7)];
     }
   }
+  float* const mtab = reinterpret_cast<float*>(smem + WBYTES + XBYTES);  // BST: [NS - 1][BN] means
+  if constexpr (BST) {
+    for (int c = tid; c < BN; c += THREADS) {
+      mtab[c] = g.bmean[n0 + c];
+      if constexpr (EPI == 4) mtab[BN + c] = g.bmean2[n0 + c];
+    }
+  }
   __builtin_amdgcn_s_waitcnt(0);  // the LDS DMA drained (a wait the compiler's own counter tracking sees)
   __syncthreads();
 
@@ -160,8 +180,11 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
   const int nt = gw < MT ? (MT - gw + WG - 1) / WG : 0;
   const __amdgpu_buffer_rsrc_t ra = rsrc(g.A, (uint32_t)((long)g.M * g.lda * 2));
   const __amdgpu_buffer_rsrc_t rc = rsrc(g.C, (uint32_t)((long)g.M * N * 2));
-  const __amdgpu_buffer_rsrc_t radd = EPI == 2 ? rsrc(g.add, (uint32_t)((long)g.M * N * 2)) : rc;
-  const __amdgpu_buffer_rsrc_t rmask = EPI == 2 ? rsrc(g.mask, (uint32_t)((long)g.M * N / 8)) : rc;
+  const __amdgpu_buffer_rsrc_t radd = EPI >= 2 ? rsrc(g.add, (uint32_t)((long)g.M * N * 2)) : rc;
+  const __amdgpu_buffer_rsrc_t rmask = EPI >= 2 ? rsrc(g.mask, (uint32_t)((long)g.M * N / 8)) : rc;
+  const __amdgpu_buffer_rsrc_t rbx = BST ? rsrc(g.bx, (uint32_t)((long)g.M * N * 2)) : rc;
+  const __amdgpu_buffer_rsrc_t rbx2 = EPI == 4 ? rsrc(g.bx2, (uint32_t)((long)g.M * N * 2)) : rc;
+  const __amdgpu_buffer_rsrc_t rbm = BST ? rsrc(g.bmask, (uint32_t)((long)g.M * N / 8)) : rc;
   const int q = lane >> 4;
   const uint32_t la = (uint32_t)(((lane & 15) * g.lda + q * 8) * 2);
   const uint32_t lda16 = (uint32_t)(16 * g.lda * 2), rowA = (uint32_t)(WG * TM * g.lda * 2);
@@ -175,7 +198,12 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
 
   i32x4 abuf[NBUF][MB][KC];
   i32x4 obuf[NBUF][EPI ? 2 : 1][EPI ? KO : 1];
-  uint32_t mbuf[NBUF][EPI == 2 ? 2 : 1][EPI == 2 ? KO : 1];
+  uint32_t mbuf[NBUF][EPI >= 2 ? 2 : 1][EPI >= 2 ? KO : 1];
+  // BST: the BatchNorm input(s) and ReLU bits of the next tile, in the copy-out layout: one slot, loaded right after
+  // a tile's stores (a whole tile period ahead of their use, in registers the A / addend ring does not hold)
+  i32x4 xbuf[BST ? 2 : 1][BST ? KO : 1];
+  i32x4 x2buf[EPI == 4 ? 2 : 1][EPI == 4 ? KO : 1];
+  uint32_t bbuf[BST ? 2 : 1][BST ? KO : 1];
   auto load_a = [&](i32x4 (&dst)[MB][KC], int t) __attribute__((always_inline)) {
     const uint32_t base = (uint32_t)(gw * TM) * (uint32_t)(g.lda * 2) + (uint32_t)t * rowA + la;
 #pragma unroll
@@ -189,8 +217,8 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int k = 0; k < KO; ++k) bload16(obuf[slot][h][k], base + h * 128 + k * n8, EPI == 2 ? radd : rc);
-      if constexpr (EPI == 2) {
+        for (int k = 0; k < KO; ++k) bload16(obuf[slot][h][k], base + h * 128 + k * n8, EPI >= 2 ? radd : rc);
+      if constexpr (EPI >= 2) {
         const uint32_t mrow = (uint32_t)(gw * TM) * (uint32_t)(N / 8) + (uint32_t)t * rowM + lm;
 #pragma unroll
         for (int h = 0; h < 2; ++h)
@@ -200,6 +228,20 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
       }
     }
   };
+  auto load_bx = [&](int t) __attribute__((always_inline)) {
+    if constexpr (BST) {
+      const uint32_t base = (uint32_t)(gw * TM) * (uint32_t)(N * 2) + (uint32_t)t * rowC + lc;
+      const uint32_t mrow = (uint32_t)(gw * TM) * (uint32_t)(N / 8) + (uint32_t)t * rowM + lm;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int k = 0; k < KO; ++k) {
+          bload16(xbuf[h][k], base + h * 128 + k * n8, rbx);
+          if constexpr (EPI == 4) bload16(x2buf[h][k], base + h * 128 + k * n8, rbx2);
+          bbuf[h][k] = __builtin_amdgcn_raw_buffer_load_b8(rbm, mrow + h * 8 + k * n8m, 0, 0);
+        }
+    }
+  };
 
   f32x2_t s2[STATS ? NP : 1][4], q2[STATS ? NP : 1][4];
   if constexpr (STATS) {
@@ -207,6 +249,18 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
     for (int p = 0; p < NP; ++p)
 #pragma unroll
       for (int j = 0; j < 4; ++j) s2[p][j] = q2[p][j] = f32x2_t{0.f, 0.f};
+  }
+
+  // BST: per lane, half h, dword j: columns 64 h + 8 (l & 7) + 2 j, + 1 -- sum g, sum g (x - mean) [, x2]
+  f32x2_t bs[BST ? 2 : 1][4], bq[BST ? 2 : 1][4], bq2[EPI == 4 ? 2 : 1][4];
+  if constexpr (BST) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bs[h][j] = bq[h][j] = f32x2_t{0.f, 0.f};
+        if constexpr (EPI == 4) bq2[h][j] = f32x2_t{0.f, 0.f};
+      }
   }
 
   const float* xtab = reinterpret_cast<const float*>(smem + WBYTES) + q * 16;
@@ -300,7 +354,7 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
         i32x4 o = *reinterpret_cast<const i32x4*>(stg + r * 128 + ((c ^ (r & 7)) << 4));
         if constexpr (EPI != 0) {  // one more bf16 rounding on top of the stored product (<= 1 ulp)
           const i32x4 old = obuf[u][h][k];
-          const uint32_t keep = EPI == 2 ? mbuf[u][h][k] : 0xFFu;
+          const uint32_t keep = EPI >= 2 ? mbuf[u][h][k] : 0xFFu;
           float f[8];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -311,9 +365,31 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
           }
           o = __builtin_bit_cast(i32x4, pack_bf16x8(f));
         }
+        if constexpr (BST) {  // g = the stored value where the BatchNorm's ReLU passed; rows past M load x = bits = 0
+          const uint32_t bits = bbuf[h][k];
+          const i32x4 xv = xbuf[h][k];
+          const float* mt = mtab + 64 * h + 8 * (lane & 7);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t w = (uint32_t)o[j], xw = (uint32_t)xv[j];
+            const f32x2_t gv = {((bits >> (2 * j)) & 1u) ? __uint_as_float(w << 16) : 0.f,
+                                ((bits >> (2 * j + 1)) & 1u) ? __uint_as_float(w & 0xFFFF0000u) : 0.f};
+            const f32x2_t mu = {mt[2 * j], mt[2 * j + 1]};
+            const f32x2_t xd = f32x2_t{__uint_as_float(xw << 16), __uint_as_float(xw & 0xFFFF0000u)} - mu;
+            bs[h][j] += gv;
+            bq[h][j] = __builtin_elementwise_fma(gv, xd, bq[h][j]);
+            if constexpr (EPI == 4) {
+              const uint32_t x2w = (uint32_t)x2buf[h][k][j];
+              const f32x2_t mu2 = {mt[BN + 2 * j], mt[BN + 2 * j + 1]};
+              const f32x2_t xd2 = f32x2_t{__uint_as_float(x2w << 16), __uint_as_float(x2w & 0xFFFF0000u)} - mu2;
+              bq2[h][j] = __builtin_elementwise_fma(gv, xd2, bq2[h][j]);
+            }
+          }
+        }
         bstore16(o, cb + h * 128 + k * n8, rc);
       }
     }
+    load_bx(t + 1);
   };
 
   // prologue: the loads of a round (A and addend of tiles 0 .. D - 1) in the loop's order; then whole
@@ -324,6 +400,7 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
     load_a(abuf[(uu + D) % NBUF], uu - NBUF + D);
     load_add((uu + D) % NBUF, uu - NBUF + D);
   });
+  load_bx(0);
   int t0 = 0;
   for (; t0 + NBUF <= nt; t0 += NBUF) sfor<NBUF>([&](auto u) __attribute__((always_inline)) { tile(u, t0 + decltype(u)::value); });
   sfor<NBUF>([&](auto u) __attribute__((always_inline)) {
@@ -354,6 +431,40 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
                     red[(6 + which) * BN + col];
     atomicAdd(g.stats + (long)(bid % REPL) * 2 * N + (long)which * N + n0 + col, v);
   }
+  if constexpr (BST) {
+    // lanes with equal l & 7 hold the same 16 columns: xor-sum over the 8 row lanes, the 4 waves through LDS, then
+    // one atomic per (column, sum) per block into replica bid % REPL
+    __syncthreads();  // every wave is past its last read of the weight panel and the mean table
+    float* red = reinterpret_cast<float*>(smem);  // [wave][NS][BN]
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          float v[NS] = {bs[h][j][e], bq[h][j][e]};
+          if constexpr (EPI == 4) v[NS - 1] = bq2[h][j][e];
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            v[s] += __shfl_xor(v[s], 8);
+            v[s] += __shfl_xor(v[s], 16);
+            v[s] += __shfl_xor(v[s], 32);
+          }
+          if (lane < 8) {
+            const int col = 64 * h + 8 * lane + 2 * j + e;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) red[(wid * NS + s) * BN + col] = v[s];
+          }
+        }
+    __syncthreads();
+    for (int i = tid; i < NS * BN; i += THREADS) {
+      const int col = i & (BN - 1), which = i >> 7;
+      const float v = red[which * BN + col] + red[(NS + which) * BN + col] + red[(2 * NS + which) * BN + col] +
+                      red[(3 * NS + which) * BN + col];
+      float* dst = which < 2 ? g.bst + (long)which * N : g.bst2 + N;
+      atomicAdd(dst + (long)(bid % REPL) * 2 * N + n0 + col, v);
+    }
+  }
 }
 
 }  // namespace gsk
@@ -366,6 +477,14 @@ bool gemm_short_ok(int M, int N, int K, long lda, long ldc) {
   const char* e = std::getenv("K8S_AMD_GEMM_SHORT");
   if (e && e[0] == '0') return false;
   return (K == 64 || K == 128 || K == 256) && N % 128 == 0 && lda == K && ldc == N && M > 0;
+}
+
+// Whether a masked-addend data gradient can also take the BatchNorm-backward statistics of one (dual = two) BatchNorms
+// in its epilogue (K8S_AMD_BN_BSTATS=0 turns the fusion off for A/B runs).
+bool gemm_short_bnstats_ok(int M, int N, int K, bool dual) {
+  const char* e = std::getenv("K8S_AMD_BN_BSTATS");
+  if (e && e[0] == '0') return false;
+  return gemm_short_ok(M, N, K, K, N) && (!dual || K == 64);
 }
 
 // Rows per launch: every operand of one launch stays below 2 GiB (the kernel's 32-bit buffer offsets); larger
@@ -386,21 +505,34 @@ static int gemm_short_rows_per_launch(int M, int N, int K) {
 // epi 0: C = op(A) B^T; 1: C += ...; 2: C = op(A) B^T + (mask ? add : 0). b_mn: B stored [K][N] (ldb) else [N][K].
 void launch_gemm_short(const uint16_t* A, const uint16_t* B, long ldb, bool b_mn, uint16_t* C, const uint16_t* add,
                        const uint8_t* mask, const float* xf, float* stats, int M, int N, int K, int epi,
-                       hipStream_t st) {
+                       hipStream_t st, const GemmShortBnStats* bst) {
   if (!gemm_short_ok(M, N, K, K, N)) throw std::runtime_error("gemm_short: shape outside the kernel's contract");
   if ((long)K * N * 2 >= (1L << 31)) throw std::runtime_error("gemm_short: weight operand >= 2 GiB");
   const int rows = gemm_short_rows_per_launch(M, N, K);
   if (rows < M) {
     for (int r0 = 0; r0 < M; r0 += rows) {
       const int mr = M - r0 < rows ? M - r0 : rows;
+      GemmShortBnStats sub;
+      if (bst) {
+        sub = *bst;
+        sub.x += (long)r0 * N;
+        if (sub.x2) sub.x2 += (long)r0 * N;
+        sub.mask += (long)r0 * N / 8;
+      }
       launch_gemm_short(A + (long)r0 * K, B, ldb, b_mn, C + (long)r0 * N, add ? add + (long)r0 * N : nullptr,
-                        mask ? mask + (long)r0 * N / 8 : nullptr, xf, stats, mr, N, K, epi, st);
+                        mask ? mask + (long)r0 * N / 8 : nullptr, xf, stats, mr, N, K, epi, st, bst ? &sub : nullptr);
     }
     return;
   }
   if ((epi == 2) != (add != nullptr) || (epi == 2 && !mask)) throw std::runtime_error("gemm_short: bad addend");
   if (epi != 0 && stats) throw std::runtime_error("gemm_short: statistics only with a plain store");
-  gsk::Args g{A, B, C, add, mask, xf, stats, M, N, K, (int)ldb, N / gsk::BN, 0};
+  if (bst && (epi != 2 || !b_mn || !bst->x || !bst->mask || !bst->mean || !bst->sums ||
+              (bst->x2 && (!bst->mean2 || !bst->sums2))))
+    throw std::runtime_error("gemm_short: BatchNorm-backward statistics need the masked-addend data gradient");
+  gsk::Args g{A, B, C, add, mask, xf, stats,
+              bst ? bst->x : nullptr, bst ? bst->x2 : nullptr, bst ? bst->mask : nullptr,
+              bst ? bst->mean : nullptr, bst ? bst->mean2 : nullptr, bst ? bst->sums : nullptr,
+              bst ? bst->sums2 : nullptr, M, N, K, (int)ldb, N / gsk::BN, 0};
   // Cfg::OCC blocks per CU; the P panels of one row group share an XCD, so blocks come in multiples of 8 P
   const int per_chip = 2 * planner_cus();  // Cfg::OCC = 2 blocks per CU
   const int gx = (per_chip / (8 * g.P)) > 1 ? per_chip / (8 * g.P) : 1;
@@ -433,6 +565,12 @@ void launch_gemm_short(const uint16_t* A, const uint16_t* B, long ldb, bool b_mn
       K8S_GSK_K(true, false, false, 0);
     else if (epi == 1)
       K8S_GSK_K(true, false, false, 1);
+    else if (bst && bst->x2) {
+      // two BatchNorms' sums fit the register budget at K = 64 only (gemm_short_bnstats_ok)
+      if (K != 64) throw std::runtime_error("gemm_short: two-BatchNorm statistics need K = 64");
+      K8S_GSK(64, true, false, false, 4);
+    } else if (bst)
+      K8S_GSK_K(true, false, false, 3);
     else
       K8S_GSK_K(true, false, false, 2);
   }

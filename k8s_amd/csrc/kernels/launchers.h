@@ -40,6 +40,16 @@ void launch_bn_fwd_from_sums_dual(const uint16_t* x, const float* gamma, const f
                                   const float* sums_r, int nrep_r, float* save_mean_r, float* save_invstd_r,
                                   float* run_mean_r, float* run_var_r, float* params_r, uint16_t* y, uint8_t* mask,
                                   long M, int C, float eps, float momentum, hipStream_t st);
+void launch_bn_bwd_from_sums(const uint16_t* dy, const uint16_t* x, const uint8_t* mask, const float* sums, int nrep,
+                             const float* mean, const float* invstd, const float* gamma, const float* beta,
+                             uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, float* params, long M, int C,
+                             hipStream_t st);
+void launch_bn_bwd_dual_from_sums(const uint16_t* dy, const uint8_t* mask, const uint16_t* x, const float* sums,
+                                  int nrep, const float* mean, const float* invstd, const float* gamma,
+                                  const float* beta, uint16_t* dx, float* dgamma, float* dbeta, float* params,
+                                  const uint16_t* x2, const float* sums2, const float* mean2, const float* invstd2,
+                                  const float* gamma2, const float* beta2, uint16_t* dx2, float* dgamma2,
+                                  float* dbeta2, float* params2, long M, int C, hipStream_t st);
 void launch_bn_bwd_dual(const uint16_t* dy, const uint8_t* mask, const uint16_t* x, const float* mean,
                         const float* invstd, const float* gamma, const float* beta, uint16_t* dx, float* dgamma,
                         float* dbeta, float* work, float* params, const uint16_t* x2, const float* mean2,
@@ -81,9 +91,23 @@ struct AddEpi {
 };
 // gemm_short.hip: the short-K streaming GEMM (K in {64, 128, 256}, N % 128 == 0; see its header)
 bool gemm_short_ok(int M, int N, int K, long lda, long ldc);
+bool gemm_short_bnstats_ok(int M, int N, int K, bool dual);
+// The BatchNorm-backward statistics a masked-addend data gradient can take in its epilogue: for the stored result g'
+// of the BatchNorm y = relu(BN(x) + ...) whose packed ReLU bits are `mask`, g = mask ? g' : 0 and
+//   sums[r][0][c] += sum g,  sums[r][1][c] += sum g (x - mean)   (r = the block's replica of kConvStatReplicas)
+// and for a second BatchNorm fed by the same masked gradient (x2: sums2[r][1][c] += sum g (x2 - mean2)).
+struct GemmShortBnStats {
+  const uint16_t* x = nullptr;
+  const uint8_t* mask = nullptr;
+  const float* mean = nullptr;
+  float* sums = nullptr;
+  const uint16_t* x2 = nullptr;
+  const float* mean2 = nullptr;
+  float* sums2 = nullptr;
+};
 void launch_gemm_short(const uint16_t* A, const uint16_t* B, long ldb, bool b_mn, uint16_t* C, const uint16_t* add,
                        const uint8_t* mask, const float* xf, float* stats, int M, int N, int K, int epi,
-                       hipStream_t st);
+                       hipStream_t st, const GemmShortBnStats* bst = nullptr);
 void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                  long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
                  float alpha, int splits, float* ws, hipStream_t st, const AddEpi* add = nullptr,

@@ -468,6 +468,106 @@ Tensor mask_apply(Tensor src, Tensor mask) {
   return out;
 }
 
+// 1x1 data gradient dx[M, N] = gy[M, K] . w[K, N] + (add_mask ? add_src : 0) that also accumulates the
+// BatchNorm-backward statistics of dx for the BatchNorm(s) that produced the convolution's input (gemm_short.hip
+// EPI 3 / 4): sums[r][0][c] += sum g, sums[r][1][c] += sum g (x - mean), g = bit ? dx : 0 with the BatchNorm's packed
+// ReLU bits `mask`; with x2 (a ResNet downsample block's second BatchNorm) sums2[r][1][c] += sum g (x2 - mean2).
+// sums / sums2: zeroed fp32 [conv_stat_replicas, 2, N].
+Tensor dgrad_short_bnstats(Tensor gy, Tensor w, Tensor add_src, Tensor add_mask, Tensor x, Tensor mask, Tensor mean,
+                           Tensor sums, c10::optional<Tensor> x2, c10::optional<Tensor> mean2,
+                           c10::optional<Tensor> sums2) {
+  for (const Tensor* t : {&gy, &w, &add_src, &x}) {
+    check_cuda(*t, "gy / w / add_src / x");
+    check_dtype(*t, at::kBFloat16, "gy / w / add_src / x");
+    TORCH_CHECK(t->is_contiguous() && t->dim() == 2, "gy / w / add_src / x: contiguous 2-d");
+  }
+  const long M = gy.size(0), K = gy.size(1), N = w.size(1);
+  TORCH_CHECK(w.size(0) == K && add_src.sizes() == x.sizes() && x.size(0) == M && x.size(1) == N,
+              "shapes: gy [M, K], w [K, N], add_src / x [M, N]");
+  TORCH_CHECK(M < (1L << 31) && k8s_amd::gemm_short_bnstats_ok((int)M, (int)N, (int)K, x2.has_value()),
+              "dgrad_short_bnstats: shape outside the kernel's contract (gemm_short_bnstats_ok)");
+  for (const Tensor* t : {&add_mask, &mask})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kByte && t->is_contiguous() && t->numel() * 8 == M * N,
+                "masks: packed uint8, one bit per element");
+  const long nrep = k8s_amd::kConvStatReplicas;
+  auto chk_sums = [&](const Tensor& t) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == nrep * 2 * N,
+                "sums: zeroed fp32 [conv_stat_replicas, 2, N]");
+  };
+  chk_sums(sums);
+  TORCH_CHECK(mean.numel() == N && mean.scalar_type() == at::kFloat && mean.is_cuda(), "mean: fp32 [N]");
+  k8s_amd::GemmShortBnStats b;
+  b.x = cbf(x);
+  b.mask = mask.data_ptr<uint8_t>();
+  b.mean = f32(mean);
+  b.sums = f32(sums);
+  if (x2) {
+    TORCH_CHECK(mean2 && sums2, "x2 needs mean2 and sums2");
+    check_cuda(*x2, "x2");
+    check_dtype(*x2, at::kBFloat16, "x2");
+    TORCH_CHECK(x2->is_contiguous() && x2->sizes() == x.sizes(), "x2: the shape of x");
+    TORCH_CHECK(mean2->numel() == N && mean2->scalar_type() == at::kFloat, "mean2: fp32 [N]");
+    chk_sums(*sums2);
+    b.x2 = cbf(*x2);
+    b.mean2 = f32(*mean2);
+    b.sums2 = f32(*sums2);
+  }
+  Tensor out = torch::empty({M, N}, gy.options());
+  k8s_amd::launch_gemm_short(cbf(gy), cbf(w), N, true, bf(out), cbf(add_src), add_mask.data_ptr<uint8_t>(), nullptr,
+                             nullptr, (int)M, (int)N, (int)K, 2, cur_stream(), &b);
+  return out;
+}
+
+// BatchNorm backward (dx, dres) with the reduction already done by dy's producer (dgrad_short_bnstats sums).
+std::vector<Tensor> bn_bwd_from_sums(Tensor dy, Tensor x, Tensor mask, Tensor sums, Tensor mean, Tensor invstd,
+                                     Tensor gamma, Tensor beta, Tensor dgamma, Tensor dbeta, bool want_dres) {
+  check_cuda(dy, "dy"); check_cuda(x, "x");
+  check_dtype(dy, at::kBFloat16, "dy"); check_dtype(x, at::kBFloat16, "x");
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.is_contiguous() && x.is_contiguous(), "dy / x: same contiguous shape");
+  const int C = (int)x.size(-1);
+  const long M = x.numel() / C;
+  TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == at::kByte && mask.numel() * 8 == x.numel(), "mask: packed bits");
+  TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kFloat && sums.numel() % (2 * C) == 0, "sums: fp32 [R, 2, C]");
+  TORCH_CHECK(dgamma.numel() == C && dbeta.numel() == C && dgamma.is_contiguous() && dbeta.is_contiguous());
+  auto dx = torch::empty_like(x);
+  Tensor dres = want_dres ? torch::empty_like(x) : Tensor();
+  auto params = torch::empty({4 * C}, gamma.options());
+  k8s_amd::launch_bn_bwd_from_sums(cbf(dy), cbf(x), mask.data_ptr<uint8_t>(), f32(sums), (int)(sums.numel() / (2 * C)),
+                                   f32(mean), f32(invstd), f32(gamma), f32(beta), bf(dx),
+                                   want_dres ? bf(dres) : nullptr, f32(dgamma), f32(dbeta), f32(params), M, C,
+                                   cur_stream());
+  return {dx, dres};
+}
+
+// bn_bwd_dual with the reduction done by dy's producer: sums (sum g, sum g (x - mean)) and sums2 (slot 1:
+// sum g (x2 - mean2)).
+std::vector<Tensor> bn_bwd_dual_from_sums(Tensor dy, Tensor mask, Tensor x, Tensor mean, Tensor invstd, Tensor gamma,
+                                          Tensor beta, Tensor dgamma, Tensor dbeta, Tensor sums, Tensor x2,
+                                          Tensor mean2, Tensor invstd2, Tensor gamma2, Tensor beta2, Tensor dgamma2,
+                                          Tensor dbeta2, Tensor sums2) {
+  for (const Tensor* t : {&dy, &x, &x2}) {
+    check_cuda(*t, "dy / x / x2"); check_dtype(*t, at::kBFloat16, "dy / x / x2");
+    TORCH_CHECK(t->is_contiguous() && t->sizes() == x.sizes(), "dy / x / x2: same contiguous shape");
+  }
+  const int C = (int)x.size(-1);
+  const long M = x.numel() / C;
+  for (const Tensor* t : {&mean, &invstd, &gamma, &beta, &dgamma, &dbeta, &mean2, &invstd2, &gamma2, &beta2, &dgamma2,
+                          &dbeta2})
+    TORCH_CHECK(t->numel() == C && t->scalar_type() == at::kFloat && t->is_contiguous(), "per-channel fp32 of C");
+  TORCH_CHECK(mask.numel() == x.numel() / 8 && mask.scalar_type() == at::kByte, "packed mask: M*C/8 bytes");
+  for (const Tensor* t : {&sums, &sums2})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == sums.numel() && t->numel() % (2 * C) == 0,
+                "sums / sums2: fp32 [R, 2, C]");
+  auto dx = torch::empty_like(x), dx2 = torch::empty_like(x);
+  auto params = torch::empty({4 * C}, gamma.options()), params2 = torch::empty({4 * C}, gamma.options());
+  k8s_amd::launch_bn_bwd_dual_from_sums(cbf(dy), mask.data_ptr<uint8_t>(), cbf(x), f32(sums),
+                                        (int)(sums.numel() / (2 * C)), f32(mean), f32(invstd), f32(gamma), f32(beta),
+                                        bf(dx), f32(dgamma), f32(dbeta), f32(params), cbf(x2), f32(sums2), f32(mean2),
+                                        f32(invstd2), f32(gamma2), f32(beta2), bf(dx2), f32(dgamma2), f32(dbeta2),
+                                        f32(params2), M, C, cur_stream());
+  return {dx, dx2};
+}
+
 Tensor gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, c10::optional<Tensor> out, bool out_f32,
             c10::optional<Tensor> bias, int64_t act, c10::optional<Tensor> pre, bool accumulate, double alpha,
             int64_t splits, c10::optional<Tensor> add_src, c10::optional<Tensor> add_mask, c10::optional<Tensor> xform_b,
@@ -1193,6 +1293,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd_from_sums_dual", &bn_fwd_from_sums_dual, "relu(BN(x) + BN_r(xr)), statistics from conv sums");
   m.def("bn_finalize", &bn_finalize, py::arg("sums"), py::arg("gamma"), py::arg("beta"), py::arg("run_mean"),
         py::arg("run_var"), py::arg("count"), py::arg("momentum"), py::arg("eps"));
+  m.def("dgrad_short_bnstats", &dgrad_short_bnstats, py::arg("gy"), py::arg("w"), py::arg("add_src"),
+        py::arg("add_mask"), py::arg("x"), py::arg("mask"), py::arg("mean"), py::arg("sums"),
+        py::arg("x2") = py::none(), py::arg("mean2") = py::none(), py::arg("sums2") = py::none(),
+        "1x1 masked-addend data gradient with the BatchNorm-backward statistics of its result (gemm_short EPI 3/4)");
+  m.def("gemm_short_bnstats_ok", [](int64_t M, int64_t N, int64_t K, bool dual) {
+    return M < (1L << 31) && k8s_amd::gemm_short_bnstats_ok((int)M, (int)N, (int)K, dual);
+  });
+  m.def("bn_bwd_from_sums", &bn_bwd_from_sums, "BatchNorm backward from a producer's reduction sums (final + apply)");
+  m.def("bn_bwd_dual_from_sums", &bn_bwd_dual_from_sums, "bn_bwd_dual from a producer's reduction sums");
   m.def("mask_apply", &mask_apply, "out = bit ? src : 0 (packed 1-bit mask per element)");
   m.def("swiglu_fwd", &swiglu_fwd, py::arg("gu"), py::arg("blk") = 0);
   m.def("swiglu_bwd", &swiglu_bwd, py::arg("gu"), py::arg("dy"), py::arg("blk") = 0);

@@ -37,7 +37,8 @@ from k8s_amd.ops._ext import load as _load
 # pass computed in the dgrad that produces its input; it measured a net loss twice, 10.61k vs 11.00k img/s in round 2
 # and 12.02k vs 12.20k with only the long-K dgrads in round 3 (scripts/gpurun/env_ab.sh), and was removed.)
 
-STATS = {"hip_fwd": 0, "aten_fwd": 0, "hip_wgrad": 0, "aten_wgrad": 0, "hip_dgrad": 0, "aten_dgrad": 0}
+STATS = {"hip_fwd": 0, "aten_fwd": 0, "hip_wgrad": 0, "aten_wgrad": 0, "hip_dgrad": 0, "aten_dgrad": 0,
+         "bn_bstats": 0}
 
 # (Round 5 built weight gradients on a second HIP stream -- each conv's dW kernel forked off the compute stream to
 # overlap the data gradient and BatchNorm passes after it. The streams co-ran, but the HBM-bound kernels stretched:
@@ -118,13 +119,26 @@ def _wgrad_hip(C_, gy, x, out, stride, padding, acc, xform=None):
         C_.conv_wgrad(x, gy, out, stride, padding, 1, 0, acc, xform=xform)
 
 
-def _dgrad_hip(C_, gy, w, padding, addend=None):
+def _dgrad_hip(C_, gy, w, padding, addend=None, bn_link=None):
     """dx on our kernels; with ``addend`` (bf16, shape of dx) a 1x1 dgrad accumulates onto it in the GEMM
-    epilogue and returns it (the fused residual-gradient add)."""
+    epilogue and returns it (the fused residual-gradient add). ``bn_link`` (nn.BnStatLink, with a masked addend):
+    the epilogue also accumulates the BatchNorm-backward sums of dx for the BatchNorm(s) that produced x."""
     K, R, S, C = w.shape
     masked = addend is not None and not torch.is_tensor(addend)  # nn.MaskedGrad: (dy, packed ReLU mask)
     if R == 1 and S == 1 and padding == 0:
         N, H, W_, _ = gy.shape
+        if masked and bn_link is not None and bn_link.x is not None and bn_link.x.shape == (N, H, W_, C) and \
+                C_.gemm_short_bnstats_ok(N * H * W_, C, K, bn_link.x2 is not None):
+            R_ = C_.conv_stat_replicas
+            sums = torch.zeros(R_, 2, C, device=gy.device, dtype=torch.float32)
+            sums2 = torch.zeros(R_, 2, C, device=gy.device, dtype=torch.float32) if bn_link.x2 is not None else None
+            out = C_.dgrad_short_bnstats(
+                gy.reshape(-1, K), w.reshape(K, C), addend.dy.view(-1, C), addend.mask, bn_link.x.view(-1, C),
+                bn_link.mask, bn_link.mean, sums, None if sums2 is None else bn_link.x2.view(-1, C), bn_link.mean2,
+                sums2).view(N, H, W_, C)
+            bn_link.sums, bn_link.sums2, bn_link.dy_key = sums, sums2, (out.data_ptr(), tuple(out.shape))
+            STATS["bn_bstats"] += 1
+            return out
         if masked:  # the epilogue reads dy and the mask bits itself: no materialised residual gradient
             out = torch.empty(N, H, W_, C, device=gy.device, dtype=gy.dtype)
             C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, out.view(-1, C), False, None, 0, None, True,
@@ -196,7 +210,7 @@ def _dgrad_strided_hip(C_, gy, w, stride, padding, H, W, addend=None):
     return dx
 
 
-def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, xform=None, x_sub=None):
+def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, xform=None, x_sub=None, bn_link=None):
     """Returns dx (+ ``addend``, e.g. the residual branch's gradient of the same tensor, fused into the
     dgrad epilogue where our kernel runs) or None; deposits dw into ``p``'s flat gradient slot. ``xform``: the
     convolution's input is relu(bn(x)) normalised on load (see ``_wgrad_hip``); dx is then the gradient w.r.t.
@@ -232,7 +246,7 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, xform=None
     if need_dx:
         if hip and stride == 1 and K % 8 == 0 and C % 8 == 0:
             STATS["hip_dgrad"] += 1
-            dx = _dgrad_hip(C_, gy, w, padding, addend)
+            dx = _dgrad_hip(C_, gy, w, padding, addend, bn_link)
         elif hip and strided_dgrad_ok(gy, w, stride, padding):
             STATS["hip_dgrad"] += 1
             dx = _dgrad_strided_hip(C_, gy, w, stride, padding, x.shape[1], x.shape[2], addend)

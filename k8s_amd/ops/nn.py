@@ -107,6 +107,35 @@ class MaskedGrad:
         return _C().mask_apply(self.dy, self.mask)
 
 
+class BnStatLink:
+    """Joins a residual BatchNorm (``y = relu(BN(x) + r)``, packed ReLU mask; or the two-BatchNorm form of a ResNet
+    downsample block) to the 1x1 convolution that reads y with a masked residual addend (a ResNet identity block's
+    conv1): that convolution's data gradient -- the whole gradient of y -- also accumulates the BatchNorm-backward
+    sums (sum g, sum g (x - mean) for g = mask ? dy : 0) in its epilogue (gemm_short.hip EPI 3 / 4), so the
+    BatchNorm's backward skips its reduction sweep over dy and x. The BatchNorm's forward fills (x, mask, mean[, x2,
+    mean2]) and tags y with the link (``y._k8s_bnstat``); the convolution's backward deposits the sums and the
+    identity of the dy they were taken over; the BatchNorm's backward uses them only when it receives exactly that dy
+    (so a second consumer of y, whose gradient autograd would add, falls back to the reduction)."""
+    __slots__ = ("x", "mask", "mean", "x2", "mean2", "sums", "sums2", "dy_key")
+
+    def __init__(self):
+        self.x = self.mask = self.mean = self.x2 = self.mean2 = None
+        self.sums = self.sums2 = self.dy_key = None
+
+    def take(self, dy):
+        """(sums, sums2) if they were taken over ``dy``, else None; clears the deposit either way."""
+        sums, sums2, key = self.sums, self.sums2, self.dy_key
+        self.sums = self.sums2 = self.dy_key = None
+        self.x = self.mask = self.mean = self.x2 = self.mean2 = None  # the BatchNorm's backward is the last reader
+        if sums is None or key != (dy.data_ptr(), tuple(dy.shape)):
+            return None
+        return sums, sums2
+
+
+# BatchNorm-backward sums in the masked-addend 1x1 dgrad epilogue (BnStatLink); K8S_AMD_BN_BSTATS=0 for the A/B
+BN_BSTATS = os.environ.get("K8S_AMD_BN_BSTATS", "1") != "0"
+
+
 class MaskLink:
     """Joins a residual BN (ReLU, packed mask) to the plain BN that produced its residual input (a ResNet
     downsample branch): the residual BN's backward passes its incoming dy through unchanged as the residual's
@@ -120,7 +149,7 @@ class MaskLink:
 
 class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, anchor, p, stride, padding, with_stats, link=None):
+    def forward(ctx, x, anchor, p, stride, padding, with_stats, link=None, bn_link=None):
         impl = _conv_impl()
         w = p.weight if x.dtype == p.weight.dtype else p.master.to(x.dtype)
         sums = None
@@ -134,7 +163,7 @@ class _Conv2dNHWC(torch.autograd.Function):
         else:
             y = impl.conv_fwd(x, w, stride, padding, sums)
         ctx.save_for_backward(x, xs)
-        ctx.p, ctx.stride, ctx.padding, ctx.link = p, stride, padding, link
+        ctx.p, ctx.stride, ctx.padding, ctx.link, ctx.bn_link = p, stride, padding, link, bn_link
         ctx.x_requires_grad = x.requires_grad
         if sums is not None:
             ctx.mark_non_differentiable(sums)
@@ -155,9 +184,10 @@ class _Conv2dNHWC(torch.autograd.Function):
             addend, ctx.link.grad = ctx.link.grad, None
             if addend is None and ctx.link.shared and ctx.x_requires_grad:  # first of the two readers of x
                 ctx.link.grad = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, True, p, x_sub=xs)
-                return None, None, None, None, None, None, None
-        dx = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, ctx.x_requires_grad, p, addend=addend, x_sub=xs)
-        return dx, None, None, None, None, None, None
+                return None, None, None, None, None, None, None, None
+        dx = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, ctx.x_requires_grad, p, addend=addend, x_sub=xs,
+                           bn_link=ctx.bn_link if isinstance(addend, MaskedGrad) else None)
+        return dx, None, None, None, None, None, None, None
 
 
 def conv2d_nhwc(x: torch.Tensor, p, stride: int = 1, padding: int = 0, with_stats: bool = False,
@@ -168,7 +198,8 @@ def conv2d_nhwc(x: torch.Tensor, p, stride: int = 1, padding: int = 0, with_stat
     accumulated in the conv epilogue (None when the layer runs on the fallback path) -- the following
     ``batch_norm_act(..., sums=sums)`` then needs no statistics pass. ``grad_link``: a gradient for x
     deposited there by a later-backward node (``batch_norm_act(res_link=...)``) is added to dx in the dgrad."""
-    y, sums = _Conv2dNHWC.apply(x, p.store.anchor, p, stride, padding, with_stats, grad_link)
+    bn_link = getattr(x, "_k8s_bnstat", None) if (grad_link is not None and not grad_link.shared) else None
+    y, sums = _Conv2dNHWC.apply(x, p.store.anchor, p, stride, padding, with_stats, grad_link, bn_link)
     return (y, sums) if with_stats else y
 
 
@@ -232,7 +263,7 @@ def stem_s2d_input(images, pad: int = 3):
 class _BnAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu, sums=None,
-                res_link=None, dy_link=None):
+                res_link=None, dy_link=None, stat_link=None):
         x = x.contiguous()
         if res is not None:
             res = res.contiguous()
@@ -257,6 +288,10 @@ class _BnAct(torch.autograd.Function):
         ctx.pg, ctx.pb, ctx.has_res, ctx.res_link = pg, pb, res is not None, res_link
         ctx.relu_x = relu and not keep_y and mask is None
         ctx.dy_link = dy_link if (dy_link is not None and not relu and res is None) else None
+        ctx.stat_link = None
+        if stat_link is not None and mask is not None and training:
+            stat_link.x, stat_link.mask, stat_link.mean = x, mask, mean
+            ctx.stat_link = stat_link
         return y
 
     @staticmethod
@@ -274,8 +309,14 @@ class _BnAct(torch.autograd.Function):
             db = sb if sb is not None else torch.empty(pb.shape, device=x.device, dtype=torch.float32)
             # residual gradient for a linked consumer: (dy, mask) instead of a written dres tensor
             handoff = isinstance(ctx.res_link, GradLink) and ctx.has_res and mask is not None
-            dx, dres = _C().bn_bwd(dy, x, y, mean, invstd, pg.master, pb.master, ctx.relu_x, dg, db,
-                                   ctx.has_res and not (handoff or mask_out), mask)
+            want_dres = ctx.has_res and not (handoff or mask_out)
+            pre = ctx.stat_link.take(dy) if ctx.stat_link is not None else None
+            if pre is not None:  # the reduction came with dy from its producer's epilogue (BnStatLink)
+                dx, dres = _C().bn_bwd_from_sums(dy, x, mask, pre[0], mean, invstd, pg.master, pb.master, dg, db,
+                                                 want_dres)
+            else:
+                dx, dres = _C().bn_bwd(dy, x, y, mean, invstd, pg.master, pb.master, ctx.relu_x, dg, db, want_dres,
+                                       mask)
             if handoff:
                 dres = MaskedGrad(dy, mask)
             elif mask_out:  # the producing plain BN masks dy itself (MaskLink)
@@ -296,7 +337,7 @@ class _BnAct(torch.autograd.Function):
         if ctx.has_res and isinstance(ctx.res_link, GradLink):  # hand dres to the node that adds it in a kernel
             ctx.res_link.grad, dres = dres, None
         return (dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None, None,
-                None)
+                None, None)
 
 
 # Which BatchNorm + ReLU outputs of a ResNet bottleneck are normalised on load by the convolution that consumes them
@@ -409,8 +450,12 @@ def batch_norm_act(x, pg, pb, run_mean, run_var, residual=None, relu=True, train
     ``res_link``: the residual's gradient is handed to that GradLink (and NOT returned to autograd); the
     node consuming the link must add it (``conv2d_nhwc(..., grad_link=link)`` on the same tensor).
     ``res_link`` may also be a MaskLink whose ``dy_link`` end is the plain BN that produced ``residual``."""
-    return _BnAct.apply(x, residual, pg.store.anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu,
-                        sums, res_link, dy_link)
+    link = BnStatLink() if (BN_BSTATS and relu and residual is not None and training and _gpu(x)) else None
+    y = _BnAct.apply(x, residual, pg.store.anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu,
+                     sums, res_link, dy_link, link)
+    if link is not None and link.x is not None:
+        y._k8s_bnstat = link
+    return y
 
 
 # =========================================================================== layernorm / rmsnorm
@@ -804,13 +849,16 @@ class _BnActDual(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, sums, xr, sums_r, anchor, pg, pb, run_mean, run_var, pgr, pbr, run_mean_r, run_var_r,
-                momentum, eps):
+                momentum, eps, stat_link=None):
         x, xr = x.contiguous(), xr.contiguous()
         y, mean, invstd, mask, mean_r, invstd_r = _C().bn_fwd_from_sums_dual(
             x, sums, pg.master, pb.master, run_mean, run_var, xr, sums_r, pgr.master, pbr.master, run_mean_r,
             run_var_r, momentum, eps)
         ctx.save_for_backward(x, xr, mean, invstd, mask, mean_r, invstd_r)
         ctx.p = (pg, pb, pgr, pbr)
+        ctx.stat_link = stat_link
+        if stat_link is not None:
+            stat_link.x, stat_link.mask, stat_link.mean, stat_link.x2, stat_link.mean2 = x, mask, mean, xr, mean_r
         return y
 
     @staticmethod
@@ -821,12 +869,17 @@ class _BnActDual(torch.autograd.Function):
         C_ = _C()
         dg, db, finish = _bn_param_grads(pg.store, pg, pb, x.device)
         dgr, dbr, finish_r = _bn_param_grads(pgr.store, pgr, pbr, x.device)
-        # one reduce sweep and one apply pass for both (dy and the mask read once per pass)
-        dx, dxr = C_.bn_bwd_dual(dy, mask, x, mean, invstd, pg.master, pb.master, dg, db, xr, mean_r, invstd_r,
-                                 pgr.master, pbr.master, dgr, dbr)
+        pre = ctx.stat_link.take(dy) if ctx.stat_link is not None else None
+        if pre is not None and pre[1] is not None:  # both reductions came with dy (BnStatLink)
+            dx, dxr = C_.bn_bwd_dual_from_sums(dy, mask, x, mean, invstd, pg.master, pb.master, dg, db, pre[0], xr,
+                                               mean_r, invstd_r, pgr.master, pbr.master, dgr, dbr, pre[1])
+        else:
+            # one reduce sweep and one apply pass for both (dy and the mask read once per pass)
+            dx, dxr = C_.bn_bwd_dual(dy, mask, x, mean, invstd, pg.master, pb.master, dg, db, xr, mean_r, invstd_r,
+                                     pgr.master, pbr.master, dgr, dbr)
         finish()
         finish_r()
-        return (dx, None, dxr) + (None,) * 12
+        return (dx, None, dxr) + (None,) * 13
 
 
 def bn_act_dual(t, bn, tr, bn_r):
@@ -838,9 +891,13 @@ def bn_act_dual(t, bn, tr, bn_r):
     if (sums is None or sums_r is None or not (bn.training and bn_r.training) or not _gpu(x)
             or x.dtype != torch.bfloat16 or xr.shape != x.shape or x.shape[-1] % 8 != 0):
         return None
-    return _BnActDual.apply(x, sums, xr, sums_r, bn.gamma.store.anchor, bn.gamma, bn.beta, bn.running_mean,
-                            bn.running_var, bn_r.gamma, bn_r.beta, bn_r.running_mean, bn_r.running_var, bn.momentum,
-                            bn.eps)
+    link = BnStatLink() if BN_BSTATS else None
+    y = _BnActDual.apply(x, sums, xr, sums_r, bn.gamma.store.anchor, bn.gamma, bn.beta, bn.running_mean,
+                         bn.running_var, bn_r.gamma, bn_r.beta, bn_r.running_mean, bn_r.running_var, bn.momentum,
+                         bn.eps, link)
+    if link is not None:
+        y._k8s_bnstat = link
+    return y
 
 
 class _AvgPoolNHWC(torch.autograd.Function):

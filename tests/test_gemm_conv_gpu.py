@@ -559,3 +559,65 @@ def test_downsample_1x1_stride2_subsampled(cuda, arm, monkeypatch):
     assert _rel(sums.sum(0)[0], yf.sum(0)) < 1e-3
     assert _rel(x.grad, xr.grad.permute(0, 2, 3, 1)) < 1e-2
     assert _rel(p.grad, wr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+@pytest.mark.parametrize("M,K,N,dual,rows", [(3000, 64, 256, False, 0), (3000, 64, 256, True, 0),
+                                             (2056, 128, 512, False, 0), (1000, 256, 1024, False, 0),
+                                             # row-chunked launches (the stage-1 form at batch >= 2048)
+                                             (3000, 64, 256, True, 1024), (2056, 128, 512, False, 512)])
+def test_dgrad_short_bnstats_epilogue(cuda, M, K, N, dual, rows, monkeypatch):
+    """The identity-block 1x1 data gradient with a masked addend that also accumulates the BatchNorm-backward sums of
+    its result (gemm_short.hip EPI 3 / 4): dx bitwise equal to the plain masked-addend dgrad, the sums against fp32
+    sums over the stored dx: sum g and sum g (x - mean), g = bit ? dx : 0 with the BatchNorm's own ReLU bits."""
+    C_ = _C()
+    if rows:
+        monkeypatch.setenv("K8S_AMD_GEMM_SHORT_ROWS", str(rows))
+    assert C_.gemm_short_bnstats_ok(M, N, K, dual)
+    torch.manual_seed(11)
+    gy = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(K, N, device=cuda) * 0.1).bfloat16()
+    dy = torch.randn(M, N, device=cuda).bfloat16()
+    amask = torch.randint(0, 256, (M * N // 8,), device=cuda, dtype=torch.uint8)
+    x = (torch.randn(M, N, device=cuda) * 2 + 0.5).bfloat16()
+    bmask = torch.randint(0, 256, (M * N // 8,), device=cuda, dtype=torch.uint8)
+    mean = torch.randn(N, device=cuda) * 0.3
+    R = C_.conv_stat_replicas
+    sums = torch.zeros(R, 2, N, device=cuda)
+    x2 = mean2 = sums2 = None
+    if dual:
+        x2 = (torch.randn(M, N, device=cuda) - 0.25).bfloat16()
+        mean2 = torch.randn(N, device=cuda) * 0.2
+        sums2 = torch.zeros(R, 2, N, device=cuda)
+    out = C_.dgrad_short_bnstats(gy, w, dy, amask, x, bmask, mean, sums, x2, mean2, sums2)
+    plain = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    C_.gemm(gy, True, w, False, plain, False, None, 0, None, True, 1.0, 1, dy, amask)
+    assert torch.equal(out, plain)
+    g = torch.where(_unpack_bits(bmask, (M, N)), out.float(), torch.zeros(M, N, device=cuda))
+    tot = sums.sum(0)
+    assert _rel(tot[0], g.sum(0)) < 1e-4
+    assert _rel(tot[1], (g * (x.float() - mean)).sum(0)) < 1e-4
+    if dual:
+        assert _rel(sums2.sum(0)[1], (g * (x2.float() - mean2)).sum(0)) < 1e-4
+
+
+def test_bn_bwd_from_sums_matches_reduce(cuda):
+    """bn_bwd_from_sums (final + apply from a producer's sums) against bn_bwd (its own reduction sweep) on the same
+    masked dy: dx, dgamma, dbeta."""
+    C_ = _C()
+    torch.manual_seed(12)
+    M, C = 4096, 256
+    x = (torch.randn(M, C, device=cuda) * 1.5 + 0.3).bfloat16()
+    dy = torch.randn(M, C, device=cuda).bfloat16()
+    mask = torch.randint(0, 256, (M * C // 8,), device=cuda, dtype=torch.uint8)
+    mean = x.float().mean(0)
+    invstd = torch.rsqrt(x.float().var(0, unbiased=False) + 1e-5)
+    gamma, beta = torch.rand(C, device=cuda) + 0.5, torch.randn(C, device=cuda) * 0.1
+    g = torch.where(_unpack_bits(mask, (M, C)), dy.float(), torch.zeros(M, C, device=cuda))
+    sums = torch.zeros(C_.conv_stat_replicas, 2, C, device=cuda)
+    sums[0, 0] = g.sum(0)
+    sums[0, 1] = (g * (x.float() - mean)).sum(0)
+    dg1, db1, dg2, db2 = (torch.empty(C, device=cuda) for _ in range(4))
+    dx1, _ = C_.bn_bwd(dy, x, None, mean, invstd, gamma, beta, False, dg1, db1, False, mask)
+    dx2, _ = C_.bn_bwd_from_sums(dy, x, mask, sums, mean, invstd, gamma, beta, dg2, db2, False)
+    assert _rel(db2, db1) < 1e-5 and _rel(dg2, dg1) < 1e-4
+    assert _rel(dx2, dx1) < 5e-3

@@ -244,3 +244,50 @@ def test_resnet50_large_batch_indexing_matches_half_batch(cuda, half):
     assert abs(l1 - l2) < 1e-3 * max(1.0, abs(l1)), (l1, l2)
     rel = ((g1 - g2).norm() / (g1.norm() + 1e-12)).item()
     assert rel < 2e-2, rel
+
+
+def test_bn_backward_sums_in_dgrad_epilogue_match_reduction(cuda):
+    """BatchNorm-backward sums taken in the identity-block conv1 data-gradient epilogue (ops.nn.BnStatLink,
+    gemm_short.hip EPI 3 / 4: single residual BN at K = 64 / 128, the downsample block's two BNs at K = 64) against the
+    BatchNorms' own reduction sweeps (ops.nn.BN_BSTATS off): same loss, every gradient within fp32 summation-order
+    noise, and the fused path taken at least three times."""
+    from k8s_amd.models.resnet import ResNet
+    from k8s_amd.ops import conv as kc
+
+    def run(on):
+        old = K.BN_BSTATS
+        K.BN_BSTATS = on
+        try:
+            torch.manual_seed(0)
+            store = ParamStore()
+            m = ResNet(store, (3, 3, 1, 1), 10, width=64).finalize(cuda, seed=3)
+            with torch.no_grad():
+                gen = torch.Generator(device="cpu").manual_seed(11)
+                for p in store.params:
+                    if "bn" in p.name or "downsample.1" in p.name:
+                        p.master.copy_((torch.rand(p.shape, generator=gen) * 0.8 + 0.6 if p.name.endswith("weight")
+                                        else torch.randn(p.shape, generator=gen) * 0.1).to(cuda))
+            store.refresh_lowp()
+            m.train()
+            images = torch.randn(16, 64, 64, 3, generator=torch.Generator(device="cpu").manual_seed(1)).to(cuda)
+            x = m.prepare_input(images.bfloat16())
+            y = torch.arange(16, device=cuda) % 10
+            n0 = kc.STATS["bn_bstats"]
+            store.begin_step()
+            loss = K.cross_entropy(m(x), y)
+            loss.backward()
+            store.zero_unwritten()
+            return loss.item(), {p.name: p.grad.float().clone() for p in store.params}, kc.STATS["bn_bstats"] - n0
+        finally:
+            K.BN_BSTATS = old
+
+    l1, g1, n1 = run(True)
+    l0, g0, n0 = run(False)
+    assert n0 == 0 and n1 >= 3, (n0, n1)
+    assert l1 == l0
+    bad = []
+    for name, r in g0.items():
+        err = (g1[name] - r).norm().item() / (r.norm().item() + 1e-6)
+        if err > 2e-2:
+            bad.append((name, round(err, 4)))
+    assert not bad, bad
