@@ -23,24 +23,7 @@
 
 namespace k8s_amd {
 
-// The forward's affine pair; the backward recomputes it with the same operations, so the ReLU decision
-// relu_on(x) below is bit-identical in every pass that makes it.
-__device__ __forceinline__ void bn_affine_regs(float gamma, float beta, float mean, float invstd, float& scale,
-                                               float& shift) {
-  scale = gamma * invstd;
-  shift = __builtin_fmaf(-mean, scale, beta);
-}
-__device__ __forceinline__ void bn_affine(float gamma, float beta, float mean, float invstd, float* scale,
-                                          float* shift) {
-  float a, b;
-  bn_affine_regs(gamma, beta, mean, invstd, a, b);
-  *scale = a;
-  *shift = b;
-}
-// y > 0 for a non-residual BN + ReLU, from its input: the stored bf16 of fma(x, scale, shift) is positive
-__device__ __forceinline__ bool relu_on(float x, float scale, float shift) {
-  return bf2f(f2bf(__builtin_fmaf(x, scale, shift))) > 0.f;
-}
+// bn_affine_regs / bn_affine / relu_on: common.h (the 3x3 conv's BatchNorm-backward epilogue makes the same decision)
 
 constexpr int BN_THREADS = 256;
 
@@ -960,6 +943,15 @@ void launch_bn_bwd_from_sums(const uint16_t* dy, const uint16_t* x, const uint8_
   hipLaunchKernelGGL(bn_bwd_final_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, sums, nrep, C, dgamma,
                      dbeta, 1.f / (float)M, mean, invstd, gamma, beta, params);
   launch_bn_bwd_apply(dy, x, mask, params, false, dx, dres, M, C, st);
+}
+
+void launch_bn_bwd_relu_from_sums(const uint16_t* dy, const uint16_t* x, const float* sums, int nrep,
+                                  const float* mean, const float* invstd, const float* gamma, const float* beta,
+                                  uint16_t* dx, float* dgamma, float* dbeta, float* params, long M, int C,
+                                  hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_final_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, sums, nrep, C, dgamma,
+                     dbeta, 1.f / (float)M, mean, invstd, gamma, beta, params);
+  launch_bn_bwd_apply(dy, x, nullptr, params, true, dx, nullptr, M, C, st);
 }
 
 void launch_bn_bwd_dual_from_sums(const uint16_t* dy, const uint8_t* mask, const uint16_t* x, const float* sums,

@@ -31,6 +31,25 @@ typedef __attribute__((ext_vector_type(8))) float f32x8_t;
 // GEMM epilogues) were VALU-bound on that sequence at ~4.5 TB/s
 __device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 
+// The forward's affine pair; the backward recomputes it with the same operations, so the ReLU decision
+// relu_on(x) below is bit-identical in every pass that makes it.
+__device__ __forceinline__ void bn_affine_regs(float gamma, float beta, float mean, float invstd, float& scale,
+                                               float& shift) {
+  scale = gamma * invstd;
+  shift = __builtin_fmaf(-mean, scale, beta);
+}
+__device__ __forceinline__ void bn_affine(float gamma, float beta, float mean, float invstd, float* scale,
+                                          float* shift) {
+  float a, b;
+  bn_affine_regs(gamma, beta, mean, invstd, a, b);
+  *scale = a;
+  *shift = b;
+}
+// y > 0 for a non-residual BN + ReLU, from its input: the stored bf16 of fma(x, scale, shift) is positive
+__device__ __forceinline__ bool relu_on(float x, float scale, float shift) {
+  return bf2f(f2bf(__builtin_fmaf(x, scale, shift))) > 0.f;
+}
+
 // 8 floats -> 8 bf16 (4 v_cvt_pk_bf16_f32)
 __device__ __forceinline__ bf16x8_t pack_bf16x8(const float (&o)[8]) {
   const f32x8_t f = {o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7]};

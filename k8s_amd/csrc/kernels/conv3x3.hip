@@ -84,7 +84,7 @@ template <int W, int RT, int KT, bool XF>
 __global__ void __launch_bounds__(THREADS, 2) conv3x3_kernel(const uint16_t* __restrict__ x,
                                                             const uint16_t* __restrict__ wt, uint16_t* __restrict__ y,
                                                             float* __restrict__ stats, const float* __restrict__ xf,
-                                                            int H, int C, int K, int tiles_per_img) {
+                                                            int H, int C, int K, int tiles_per_img, BnBwdSums bb) {
   using G = Geo<W, RT, KT, XF>;
   constexpr int WP = G::WP, NPOS = G::NPOS, P = G::P, MF = G::MF, NF = G::NF, NS = G::NS;
   constexpr int WOPS = KT * 8 / THREADS;  // weight DMA instructions per thread per tap
@@ -272,8 +272,31 @@ __global__ void __launch_bounds__(THREADS, 2) conv3x3_kernel(const uint16_t* __r
   }
 
   // ---- epilogue: [32 MF][KT] bf16 tile in LDS (16-B chunk c of row r at c ^ (r % CPR)), 16-B copy-out with the BN
-  // statistics of the stored values
+  // statistics of the stored values -- or, as a data gradient (bb.sums), the BatchNorm-backward sums of the
+  // non-residual BatchNorm + ReLU that produced the convolution's input: g = relu_on(x) ? dx : 0, sum g and
+  // sum g (x - mean) per channel, x read at the output positions (prefetched here, into the registers the
+  // accumulators free, so the loads overlap the staging)
   constexpr int CPR = KT / 8;
+  constexpr int RSTEP = THREADS / CPR, NR = (P + RSTEP - 1) / RSTEP;
+  const int c = tid % CPR, row0 = tid / CPR;
+  const bool bst = bb.sums != nullptr;
+  bf16x8_t xr[NR];
+  float bsc[8], bsh[8], bmu[8];
+  if (bst) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = k0 + c * 8 + j;
+      bmu[j] = bb.mean[col];
+      bn_affine_regs(bb.gamma[col], bb.beta[col], bmu[j], bb.invstd[col], bsc[j], bsh[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int m = row0 + i * RSTEP, hr = m / W, h = h0 + hr;
+      xr[i] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      if (m < P && h < H)
+        xr[i] = *reinterpret_cast<const bf16x8_t*>(bb.x + (((long)n * H + h) * W + (m - hr * W)) * K + k0 + c * 8);
+    }
+  }
   uint16_t* const ctile = reinterpret_cast<uint16_t*>(smem);
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
@@ -286,11 +309,31 @@ __global__ void __launch_bounds__(THREADS, 2) conv3x3_kernel(const uint16_t* __r
     }
   }
   __syncthreads();
-  constexpr int RSTEP = THREADS / CPR;
-  const int c = tid % CPR, row0 = tid / CPR;
   f32x2_t s2[4], q2[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) s2[r] = q2[r] = f32x2_t{0.f, 0.f};
+  if (bst) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int m = row0 + i * RSTEP, hr = m / W, h = h0 + hr;
+      if (m < P && h < H) {
+        const bf16x8_t o = *reinterpret_cast<const bf16x8_t*>(ctile + m * KT + ((c ^ (m % CPR)) << 3));
+        *reinterpret_cast<bf16x8_t*>(y + (((long)n * H + h) * W + (m - hr * W)) * K + k0 + c * 8) = o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          f32x2_t g, d;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const float xv = bf2f((uint16_t)xr[i][2 * r + e]);
+            g[e] = relu_on(xv, bsc[2 * r + e], bsh[2 * r + e]) ? bf2f((uint16_t)o[2 * r + e]) : 0.f;
+            d[e] = xv - bmu[2 * r + e];
+          }
+          s2[r] += g;
+          q2[r] = __builtin_elementwise_fma(g, d, q2[r]);
+        }
+      }
+    }
+  } else {
 #pragma unroll 2
   for (int m = row0; m < P; m += RSTEP) {
     const int hr = m / W, h = h0 + hr;
@@ -308,7 +351,8 @@ __global__ void __launch_bounds__(THREADS, 2) conv3x3_kernel(const uint16_t* __r
       }
     }
   }
-  if (stats) {
+  }
+  if (stats || bst) {
     __syncthreads();
     float* part = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -324,7 +368,7 @@ __global__ void __launch_bounds__(THREADS, 2) conv3x3_kernel(const uint16_t* __r
       float v = 0.f;
 #pragma unroll 4
       for (int t = cc; t < THREADS; t += CPR) v += part[t * 16 + which * 8 + r];
-      atomicAdd(stats + (long)(tile % STAT_REPL) * 2 * K + (long)which * K + k0 + col, v);
+      atomicAdd((bst ? bb.sums : stats) + (long)(tile % STAT_REPL) * 2 * K + (long)which * K + k0 + col, v);
     }
   }
 }
@@ -332,17 +376,17 @@ __global__ void __launch_bounds__(THREADS, 2) conv3x3_kernel(const uint16_t* __r
 
 template <int W, int RT, int KT, bool XF>
 static void launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const float* xf, int N, int H,
-                   int C, int K, hipStream_t st) {
+                   int C, int K, hipStream_t st, const BnBwdSums& bb) {
   const int tpi = (H + RT - 1) / RT;
   hipLaunchKernelGGL((conv3x3_kernel<W, RT, KT, XF>), dim3(N * tpi, K / KT), dim3(THREADS), 0, st, x, w, y, stats, xf,
-                     H, C, K, tpi);
+                     H, C, K, tpi, bb);
 }
 
 template <int W, int RT, int KT>
 static void launch_x(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const float* xf, int N, int H,
-                     int C, int K, hipStream_t st) {
-  if (xf) launch<W, RT, KT, true>(x, w, y, stats, xf, N, H, C, K, st);
-  else launch<W, RT, KT, false>(x, w, y, stats, xf, N, H, C, K, st);
+                     int C, int K, hipStream_t st, const BnBwdSums& bb) {
+  if (xf) launch<W, RT, KT, true>(x, w, y, stats, xf, N, H, C, K, st, bb);
+  else launch<W, RT, KT, false>(x, w, y, stats, xf, N, H, C, K, st, bb);
 }
 }  // namespace c3
 
@@ -359,10 +403,13 @@ bool conv3x3_eligible(int H, int W, int C, int K, int R, int S, int stride, int 
 }
 
 void launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const float* xform, int N,
-                    int H, int W, int C, int K, hipStream_t st) {
-  if (W == 56 && K == 64) c3::launch_x<56, 4, 64>(x, w, y, stats, xform, N, H, C, K, st);
-  else if (W == 28 && K % 128 == 0) c3::launch_x<28, 8, 128>(x, w, y, stats, xform, N, H, C, K, st);
-  else if (W == 14 && K % 128 == 0) c3::launch_x<14, 14, 128>(x, w, y, stats, xform, N, H, C, K, st);
+                    int H, int W, int C, int K, hipStream_t st, const BnBwdSums* bsums) {
+  const BnBwdSums bb = bsums ? *bsums : BnBwdSums{};
+  if (bb.sums && (stats || !bb.x || !bb.gamma || !bb.beta || !bb.mean || !bb.invstd))
+    throw std::runtime_error("conv3x3: BatchNorm-backward sums need x / gamma / beta / mean / invstd, no statistics");
+  if (W == 56 && K == 64) c3::launch_x<56, 4, 64>(x, w, y, stats, xform, N, H, C, K, st, bb);
+  else if (W == 28 && K % 128 == 0) c3::launch_x<28, 8, 128>(x, w, y, stats, xform, N, H, C, K, st, bb);
+  else if (W == 14 && K % 128 == 0) c3::launch_x<14, 14, 128>(x, w, y, stats, xform, N, H, C, K, st, bb);
   else throw std::runtime_error("conv3x3: shape outside the staged-window kernel's contract");
 }
 

@@ -335,6 +335,9 @@ struct Epi {
   // 1-bit mask instead of from a materialised residual gradient.
   const uint16_t* addsrc;
   const uint8_t* addmask;
+  // BST instantiation (lean fast path, identity rows, ldc == N): the BatchNorm-backward sums of the stored output
+  // for the relu(BN(x)) that produced this data gradient's input (launchers.h BnBwdSums), into bb.sums
+  BnBwdSums bb;
 };
 constexpr int STAT_REPL = 32;
 
@@ -369,8 +372,9 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 // (MN-major: a weight gradient's im2col / activation operand) is loaded through VGPRs, transformed and written to
 // its LDS slot by ds_write instead of by LDS-DMA (same lane-linear image, same swizzle). The staging registers of
 // the next K step are filled behind this step's MFMAs and written after them, before the step's barrier.
+// BST (lean only): the BatchNorm-backward sums epilogue of a data gradient (Epi::bb) instead of the statistics.
 template <class ASrc, class BSrc, int NBUF, int WM = 2, int WN = 2, bool LEAN = false, bool XEPI = false,
-          bool F32S = false, int XF = 0>
+          bool F32S = false, int XF = 0, bool BST = false>
 __global__ void __launch_bounds__(GEMM_THREADS, (NBUF == 1 && (XF == 0 || (XF == 1 && WM == 2))) ? 3 : 2)
 gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XForm X) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
@@ -611,7 +615,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
     __syncthreads();
     // copy-out: thread t always handles 16-B chunk c = t % CPR of its rows (GEMM_THREADS % CPR == 0), so it
     // also accumulates the BN statistics (sum, sum of squares) of those 8 columns from the bf16 values it stores
-    float* const stat_out = E.stats;
+    float* const stat_out = BST ? E.bb.sums : E.stats;
     float ps[8], pq[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) ps[r] = pq[r] = 0.f;
@@ -635,6 +639,18 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
         f32x2_t s2[4], q2[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) s2[r] = q2[r] = f32x2_t{0.f, 0.f};
+        // BST: this thread's 8 columns' ReLU affine (the forward's, recomputed bit-identically) and means; x walks
+        // with the output (ldc == N)
+        float bsc[BST ? 8 : 1], bsh[BST ? 8 : 1], bmu[BST ? 8 : 1];
+        const uint16_t* xp = nullptr;
+        if constexpr (BST) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            bmu[j] = E.bb.mean[n + j];
+            bn_affine_regs(E.bb.gamma[n + j], E.bb.beta[n + j], bmu[j], E.bb.invstd[n + j], bsc[j], bsh[j]);
+          }
+          xp = E.bb.x + off0;
+        }
 #pragma unroll 4
         for (int row = row0; row < BM; row += RSTEP) {
           if (m0 + row < M) {
@@ -649,7 +665,21 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
               o = pack_bf16x8(f);
             }
             *reinterpret_cast<bf16x8_t*>(cp) = o;
-            if (stat_out) {
+            if constexpr (BST) {
+              const bf16x8_t xv = *reinterpret_cast<const bf16x8_t*>(xp);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                f32x2_t g, d;
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                  const float xf = bf2f((uint16_t)xv[2 * r + e]);
+                  g[e] = relu_on(xf, bsc[2 * r + e], bsh[2 * r + e]) ? bf2f((uint16_t)o[2 * r + e]) : 0.f;
+                  d[e] = xf - bmu[2 * r + e];
+                }
+                s2[r] += g;
+                q2[r] = __builtin_elementwise_fma(g, d, q2[r]);
+              }
+            } else if (stat_out) {
               const uint32_t* w = reinterpret_cast<const uint32_t*>(&o);
 #pragma unroll
               for (int r = 0; r < 4; ++r) {  // pair r = elements (2r, 2r+1): bf16 -> fp32 is a shift / a mask
@@ -661,6 +691,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
           }
           cp += (long)RSTEP * ldc;
           lp += RSTEP * BN;
+          if constexpr (BST) xp += (long)RSTEP * ldc;
           if (ap) ap += (long)RSTEP * ldc;
           if (mp) mp += ((long)RSTEP * ldc) >> 3;
         }
@@ -923,15 +954,16 @@ static int effective_splits(int K, int splits) {
   return (K + kps - 1) / kps;
 }
 
-template <class ASrc, class BSrc, int WM, int WN, bool LEAN, bool XEPI = false, bool F32S = false, int XF = 0>
+template <class ASrc, class BSrc, int WM, int WN, bool LEAN, bool XEPI = false, bool F32S = false, int XF = 0,
+          bool BST = false>
 static void launch_tiles2(const ASrc& a, const BSrc& b, const Epi& e, int M, int N, int K, int kps, int splits,
                           hipStream_t st, const XForm& x = XForm{nullptr, 0, FastDiv{}}) {
   const int tiles = ((M + 64 * WM - 1) / (64 * WM)) * ((N + 64 * WN - 1) / (64 * WN));
   if (kps <= single_buf_maxk())
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN, LEAN, XEPI, F32S, XF>), dim3(tiles, 1, splits),
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 1, WM, WN, LEAN, XEPI, F32S, XF, BST>), dim3(tiles, 1, splits),
                        dim3(GEMM_THREADS), 0, st, a, b, e, M, N, K, kps, x);
   else
-    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2, WM, WN, LEAN, XEPI, F32S, XF>), dim3(tiles, 1, splits),
+    hipLaunchKernelGGL((gemm_bf16_kernel<ASrc, BSrc, 2, WM, WN, LEAN, XEPI, F32S, XF, BST>), dim3(tiles, 1, splits),
                        dim3(GEMM_THREADS), 0, st, a, b, e, M, N, K, kps, x);
 }
 
@@ -967,6 +999,16 @@ static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int 
       }
     }
     throw std::runtime_error("normalize-on-load: no instantiation for this operand pair / epilogue");
+  }
+  // a data gradient (K-major dy, MN-major w) with the BatchNorm-backward sums of its output
+  if (e.bb.sums) {
+    if constexpr (std::is_same_v<ASrc, KMajor> && std::is_same_v<BSrc, MNMajorK> && WM == 2 && WN == 2) {
+      if (lean_epi(e, N, false) && e.mode == 0 && !e.stats && !e.rst && !e.addsrc && splits == 1 && e.ldc == N) {
+        launch_tiles2<ASrc, BSrc, WM, WN, true, false, false, 0, true>(a, b, e, M, N, K, kps, splits, st);
+        return;
+      }
+    }
+    throw std::runtime_error("BatchNorm-backward sums epilogue: a plain bf16 data gradient (K-major dy, MN-major w)");
   }
   // the linear forward (both operands K-major) is the one pair with a bias / activation epilogue instantiation
   constexpr bool kXepi = std::is_same_v<ASrc, KMajor> && std::is_same_v<BSrc, KMajor>;
@@ -1025,6 +1067,7 @@ static Epi make_epi(void* c, long ldc, bool out_f32, const float* bias, int act,
   e.rst = e.rHo = e.rWo = e.rH = e.rW = e.ra = e.rb = 0;
   e.addsrc = nullptr;
   e.addmask = nullptr;
+  e.bb = BnBwdSums{};
   // (Issuing the next K step's loads behind the first MFMA half sped up the isolated 56x56 / 28x28 3x3 convolutions
   // 7-12 % but cost the ResNet-50 step 1.5 % at any K threshold -- round 2, scripts/gpurun/bench_ab.sh; removed.)
   return e;
@@ -1118,6 +1161,17 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
   else
     launch(MNMajorK{A, lda, M, K}, MNMajorK{B, ldb, N, K}, e, M, N, K, splits, st);
   if (slab) splitk_reduce(ws, splits, (long)M * N, reinterpret_cast<float*>(C), mode == 1, st);
+}
+
+// dx[M, N] = dy[M, K] . w[K, N] (bf16, the 1x1 data gradient) on the tile kernel with the BatchNorm-backward sums
+// of dx for the relu(BN(x)) that produced the convolution's input (Epi::bb, BST instantiation).
+void launch_gemm_dgrad_bnstats(const uint16_t* A, const uint16_t* B, uint16_t* C, int M, int N, int K,
+                               const BnBwdSums& bb, hipStream_t st) {
+  if (!bb.sums || !bb.x || !bb.gamma || !bb.beta || !bb.mean || !bb.invstd || N % 8)
+    throw std::runtime_error("gemm dgrad BatchNorm-backward sums: x / gamma / beta / mean / invstd / sums, N % 8 == 0");
+  Epi e = make_epi(C, N, false, nullptr, 0, nullptr, 0, 1.f);
+  e.bb = bb;
+  launch(KMajor{A, (long)K, M, K}, MNMajorK{B, (long)N, N, K}, e, M, N, K, 1, st);
 }
 
 // NHWC conv forward: y[N,Ho,Wo,K] = conv(x[N,H,W,C], w[K,R,S,C]); C % 64 == 0 takes the per-tile (r, s)

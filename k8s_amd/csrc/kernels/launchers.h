@@ -44,6 +44,10 @@ void launch_bn_bwd_from_sums(const uint16_t* dy, const uint16_t* x, const uint8_
                              const float* mean, const float* invstd, const float* gamma, const float* beta,
                              uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, float* params, long M, int C,
                              hipStream_t st);
+void launch_bn_bwd_relu_from_sums(const uint16_t* dy, const uint16_t* x, const float* sums, int nrep,
+                                  const float* mean, const float* invstd, const float* gamma, const float* beta,
+                                  uint16_t* dx, float* dgamma, float* dbeta, float* params, long M, int C,
+                                  hipStream_t st);
 void launch_bn_bwd_dual_from_sums(const uint16_t* dy, const uint8_t* mask, const uint16_t* x, const float* sums,
                                   int nrep, const float* mean, const float* invstd, const float* gamma,
                                   const float* beta, uint16_t* dx, float* dgamma, float* dbeta, float* params,
@@ -96,6 +100,17 @@ bool gemm_short_bnstats_ok(int M, int N, int K, bool dual);
 // of the BatchNorm y = relu(BN(x) + ...) whose packed ReLU bits are `mask`, g = mask ? g' : 0 and
 //   sums[r][0][c] += sum g,  sums[r][1][c] += sum g (x - mean)   (r = the block's replica of kConvStatReplicas)
 // and for a second BatchNorm fed by the same masked gradient (x2: sums2[r][1][c] += sum g (x2 - mean2)).
+// The BatchNorm-backward sums a data-gradient epilogue accumulates for the non-residual BatchNorm + ReLU
+// z = relu(BN(x)) that produced the convolution's input: g = relu_on(x) ? dx : 0 (the forward's ReLU decision, from
+// gamma / beta / mean / invstd), sums[r][0][c] += sum g, sums[r][1][c] += sum g (x - mean). sums == nullptr: off.
+struct BnBwdSums {
+  const uint16_t* x = nullptr;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  const float* mean = nullptr;
+  const float* invstd = nullptr;
+  float* sums = nullptr;
+};
 struct GemmShortBnStats {
   const uint16_t* x = nullptr;
   const uint8_t* mask = nullptr;
@@ -108,6 +123,8 @@ struct GemmShortBnStats {
 void launch_gemm_short(const uint16_t* A, const uint16_t* B, long ldb, bool b_mn, uint16_t* C, const uint16_t* add,
                        const uint8_t* mask, const float* xf, float* stats, int M, int N, int K, int epi,
                        hipStream_t st, const GemmShortBnStats* bst = nullptr);
+void launch_gemm_dgrad_bnstats(const uint16_t* A, const uint16_t* B, uint16_t* C, int M, int N, int K,
+                               const BnBwdSums& bb, hipStream_t st);
 void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                  long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
                  float alpha, int splits, float* ws, hipStream_t st, const AddEpi* add = nullptr,
@@ -119,7 +136,8 @@ long gemm_splitk_workspace(int M, int N, int splits);  // fp32 elements of the s
 // fp32 [2][C] scale | shift), bf16 output, optional BN statistics [kConvStatReplicas][2][K]
 bool conv3x3_eligible(int H, int W, int C, int K, int R, int S, int stride, int pad, int dil);
 void launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const float* xform, int N,
-                    int H, int W, int C, int K, hipStream_t st);
+                    int H, int W, int C, int K, hipStream_t st,
+                    const BnBwdSums* bsums = nullptr);
 // gemm256.hip: 256 x 256-tile, 8-wave phased MFMA GEMM for the large (transformer) products
 bool gemm256_eligible(int M, int N, int K, bool a_kmajor, bool b_kmajor);
 // split count for the tall-K fp32 products on the 256 x 256 kernel (1 = none)

@@ -518,6 +518,89 @@ Tensor dgrad_short_bnstats(Tensor gy, Tensor w, Tensor add_src, Tensor add_mask,
   return out;
 }
 
+// 3x3 / stride-1 / pad-1 data gradient dx = conv(gy, wt) on the staged-window kernel (wt = conv_dgrad_wtrans(w))
+// that also accumulates the BatchNorm-backward sums of dx for the non-residual BatchNorm + ReLU relu(BN(x)) that
+// produced the convolution's input (conv3x3.hip epilogue): sums[r][0][c] += sum g, sums[r][1][c] += sum g (x - mean),
+// g = relu_on(x) ? dx : 0. sums: zeroed fp32 [conv_stat_replicas, 2, C].
+Tensor conv3x3_dgrad_bnstats(Tensor gy, Tensor wt, Tensor x, Tensor gamma, Tensor beta, Tensor mean, Tensor invstd,
+                             Tensor sums) {
+  for (const Tensor* t : {&gy, &wt, &x}) {
+    check_cuda(*t, "gy / wt / x");
+    check_dtype(*t, at::kBFloat16, "gy / wt / x");
+    TORCH_CHECK(t->is_contiguous() && t->dim() == 4, "gy / wt / x: contiguous NHWC / KRSC");
+  }
+  const int N = (int)gy.size(0), H = (int)gy.size(1), W = (int)gy.size(2), Kc = (int)gy.size(3);
+  const int C = (int)wt.size(0);
+  TORCH_CHECK(wt.size(1) == 3 && wt.size(2) == 3 && wt.size(3) == Kc, "wt: [C, 3, 3, K]");
+  TORCH_CHECK(x.size(0) == N && x.size(1) == H && x.size(2) == W && x.size(3) == C, "x: the shape of dx");
+  TORCH_CHECK(k8s_amd::conv3x3_eligible(H, W, Kc, C, 3, 3, 1, 1, 1), "conv3x3_dgrad_bnstats: outside the kernel");
+  for (const Tensor* t : {&gamma, &beta, &mean, &invstd})
+    TORCH_CHECK(t->is_cuda() && t->numel() == C && t->scalar_type() == at::kFloat && t->is_contiguous(),
+                "per-channel fp32 [C]");
+  TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kFloat && sums.is_contiguous() &&
+                  sums.numel() == (long)k8s_amd::kConvStatReplicas * 2 * C,
+              "sums: zeroed fp32 [conv_stat_replicas, 2, C]");
+  Tensor dx = torch::empty({N, H, W, C}, gy.options());
+  k8s_amd::BnBwdSums bb;
+  bb.x = cbf(x);
+  bb.gamma = f32(gamma);
+  bb.beta = f32(beta);
+  bb.mean = f32(mean);
+  bb.invstd = f32(invstd);
+  bb.sums = f32(sums);
+  k8s_amd::launch_conv3x3(cbf(gy), cbf(wt), bf(dx), nullptr, nullptr, N, H, W, Kc, C, cur_stream(), &bb);
+  return dx;
+}
+
+// 1x1 data gradient dx[M, N] = gy[M, K] . w[K, N] on the tile kernel with the BatchNorm-backward sums of dx for the
+// relu(BN(x)) that produced the convolution's input (gemm.hip BST epilogue); for shapes the 4-wave kernel does not
+// take (gemm_dgrad_bnstats_ok). sums: zeroed fp32 [conv_stat_replicas, 2, N].
+Tensor gemm_dgrad_bnstats(Tensor gy, Tensor w, Tensor x, Tensor gamma, Tensor beta, Tensor mean, Tensor invstd,
+                          Tensor sums) {
+  for (const Tensor* t : {&gy, &w, &x}) {
+    check_cuda(*t, "gy / w / x");
+    check_dtype(*t, at::kBFloat16, "gy / w / x");
+    TORCH_CHECK(t->is_contiguous() && t->dim() == 2, "gy / w / x: contiguous 2-d");
+  }
+  const long M = gy.size(0), K = gy.size(1), N = w.size(1);
+  TORCH_CHECK(w.size(0) == K && x.size(0) == M && x.size(1) == N, "shapes: gy [M, K], w [K, N], x [M, N]");
+  TORCH_CHECK(N % 8 == 0 && M < (1L << 31), "N % 8 == 0");
+  for (const Tensor* t : {&gamma, &beta, &mean, &invstd})
+    TORCH_CHECK(t->is_cuda() && t->numel() == N && t->scalar_type() == at::kFloat && t->is_contiguous(),
+                "per-channel fp32 [N]");
+  TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kFloat && sums.is_contiguous() &&
+                  sums.numel() == (long)k8s_amd::kConvStatReplicas * 2 * N,
+              "sums: zeroed fp32 [conv_stat_replicas, 2, N]");
+  Tensor out = torch::empty({M, N}, gy.options());
+  k8s_amd::BnBwdSums bb;
+  bb.x = cbf(x);
+  bb.gamma = f32(gamma);
+  bb.beta = f32(beta);
+  bb.mean = f32(mean);
+  bb.invstd = f32(invstd);
+  bb.sums = f32(sums);
+  k8s_amd::launch_gemm_dgrad_bnstats(cbf(gy), cbf(w), bf(out), (int)M, (int)N, (int)K, bb, cur_stream());
+  return out;
+}
+
+// bn_bwd (relu_x: the ReLU recomputed from x) with the reduction done by dy's producer.
+std::vector<Tensor> bn_bwd_relu_from_sums(Tensor dy, Tensor x, Tensor sums, Tensor mean, Tensor invstd, Tensor gamma,
+                                          Tensor beta, Tensor dgamma, Tensor dbeta) {
+  check_cuda(dy, "dy"); check_cuda(x, "x");
+  check_dtype(dy, at::kBFloat16, "dy"); check_dtype(x, at::kBFloat16, "x");
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.is_contiguous() && x.is_contiguous(), "dy / x: same contiguous shape");
+  const int C = (int)x.size(-1);
+  const long M = x.numel() / C;
+  TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kFloat && sums.numel() % (2 * C) == 0, "sums: fp32 [R, 2, C]");
+  TORCH_CHECK(dgamma.numel() == C && dbeta.numel() == C && dgamma.is_contiguous() && dbeta.is_contiguous());
+  auto dx = torch::empty_like(x);
+  auto params = torch::empty({4 * C}, gamma.options());
+  k8s_amd::launch_bn_bwd_relu_from_sums(cbf(dy), cbf(x), f32(sums), (int)(sums.numel() / (2 * C)), f32(mean),
+                                        f32(invstd), f32(gamma), f32(beta), bf(dx), f32(dgamma), f32(dbeta),
+                                        f32(params), M, C, cur_stream());
+  return {dx};
+}
+
 // BatchNorm backward (dx, dres) with the reduction already done by dy's producer (dgrad_short_bnstats sums).
 std::vector<Tensor> bn_bwd_from_sums(Tensor dy, Tensor x, Tensor mask, Tensor sums, Tensor mean, Tensor invstd,
                                      Tensor gamma, Tensor beta, Tensor dgamma, Tensor dbeta, bool want_dres) {
@@ -1300,6 +1383,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_short_bnstats_ok", [](int64_t M, int64_t N, int64_t K, bool dual) {
     return M < (1L << 31) && k8s_amd::gemm_short_bnstats_ok((int)M, (int)N, (int)K, dual);
   });
+  m.def("conv3x3_dgrad_bnstats", &conv3x3_dgrad_bnstats,
+        "3x3 stride-1 data gradient with the BatchNorm-backward sums of a relu(BN(x)) input (conv3x3.hip)");
+  m.def("gemm_dgrad_bnstats", &gemm_dgrad_bnstats,
+        "1x1 data gradient with the BatchNorm-backward sums of a relu(BN(x)) input (gemm.hip BST epilogue)");
+  m.def("gemm_dgrad_bnstats_ok", [](int64_t M, int64_t N, int64_t K) {
+    const char* e = std::getenv("K8S_AMD_BN_BSTATS");
+    if (e && e[0] == '0') return false;
+    return M < (1L << 31) && N % 8 == 0 && !use_gemm256(M, N, K, true, false) &&
+           !k8s_amd::gemm_short_ok((int)M, (int)N, (int)K, K, N);
+  }, "whether a 1x1 data gradient takes gemm_dgrad_bnstats (the tile kernel is its regular path)");
+  m.def("bn_bwd_relu_from_sums", &bn_bwd_relu_from_sums, "relu_x BatchNorm backward from a producer's sums");
   m.def("bn_bwd_from_sums", &bn_bwd_from_sums, "BatchNorm backward from a producer's reduction sums (final + apply)");
   m.def("bn_bwd_dual_from_sums", &bn_bwd_dual_from_sums, "bn_bwd_dual from a producer's reduction sums");
   m.def("mask_apply", &mask_apply, "out = bit ? src : 0 (packed 1-bit mask per element)");

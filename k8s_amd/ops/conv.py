@@ -125,9 +125,19 @@ def _dgrad_hip(C_, gy, w, padding, addend=None, bn_link=None):
     the epilogue also accumulates the BatchNorm-backward sums of dx for the BatchNorm(s) that produced x."""
     K, R, S, C = w.shape
     masked = addend is not None and not torch.is_tensor(addend)  # nn.MaskedGrad: (dy, packed ReLU mask)
+    if (bn_link is not None and bn_link.relu and bn_link.x is not None and addend is None and R == 3 and S == 3
+            and padding == 1 and gy.shape[1] == gy.shape[2] and bn_link.x.shape[:3] == gy.shape[:3]
+            and C_.conv3x3_staged_ok(gy.shape[1], gy.shape[2], C, K, 3, 3, 1, 1)):
+        sums = torch.zeros(C_.conv_stat_replicas, 2, C, device=gy.device, dtype=torch.float32)
+        dx = C_.conv3x3_dgrad_bnstats(gy, C_.conv_dgrad_wtrans(w), bn_link.x, bn_link.gamma, bn_link.beta,
+                                      bn_link.mean, bn_link.invstd, sums)
+        bn_link.sums, bn_link.sums2, bn_link.dy_key = sums, None, (dx.data_ptr(), tuple(dx.shape))
+        STATS["bn_bstats"] += 1
+        return dx
     if R == 1 and S == 1 and padding == 0:
         N, H, W_, _ = gy.shape
-        if masked and bn_link is not None and bn_link.x is not None and bn_link.x.shape == (N, H, W_, C) and \
+        if masked and bn_link is not None and not bn_link.relu and bn_link.x is not None and \
+                bn_link.x.shape == (N, H, W_, C) and \
                 C_.gemm_short_bnstats_ok(N * H * W_, C, K, bn_link.x2 is not None):
             R_ = C_.conv_stat_replicas
             sums = torch.zeros(R_, 2, C, device=gy.device, dtype=torch.float32)
@@ -137,6 +147,14 @@ def _dgrad_hip(C_, gy, w, padding, addend=None, bn_link=None):
                 bn_link.mask, bn_link.mean, sums, None if sums2 is None else bn_link.x2.view(-1, C), bn_link.mean2,
                 sums2).view(N, H, W_, C)
             bn_link.sums, bn_link.sums2, bn_link.dy_key = sums, sums2, (out.data_ptr(), tuple(out.shape))
+            STATS["bn_bstats"] += 1
+            return out
+        if (bn_link is not None and bn_link.relu and bn_link.x is not None and addend is None
+                and bn_link.x.shape == (N, H, W_, C) and C_.gemm_dgrad_bnstats_ok(N * H * W_, C, K)):
+            sums = torch.zeros(C_.conv_stat_replicas, 2, C, device=gy.device, dtype=torch.float32)
+            out = C_.gemm_dgrad_bnstats(gy.reshape(-1, K), w.reshape(K, C), bn_link.x.view(-1, C), bn_link.gamma,
+                                        bn_link.beta, bn_link.mean, bn_link.invstd, sums).view(N, H, W_, C)
+            bn_link.sums, bn_link.sums2, bn_link.dy_key = sums, None, (out.data_ptr(), tuple(out.shape))
             STATS["bn_bstats"] += 1
             return out
         if masked:  # the epilogue reads dy and the mask bits itself: no materialised residual gradient

@@ -112,14 +112,18 @@ class BnStatLink:
     downsample block) to the 1x1 convolution that reads y with a masked residual addend (a ResNet identity block's
     conv1): that convolution's data gradient -- the whole gradient of y -- also accumulates the BatchNorm-backward
     sums (sum g, sum g (x - mean) for g = mask ? dy : 0) in its epilogue (gemm_short.hip EPI 3 / 4), so the
-    BatchNorm's backward skips its reduction sweep over dy and x. The BatchNorm's forward fills (x, mask, mean[, x2,
+    BatchNorm's backward skips its reduction sweep over dy and x. The same for a non-residual BatchNorm + ReLU
+    (``relu``: ResNet's bn1) read by a stride-1 3x3 convolution on the staged-window kernel (conv3x3.hip epilogue,
+    g = relu_on(x) ? dy : 0 from the BatchNorm's affine). The BatchNorm's forward fills (x, mask, mean[, x2,
     mean2]) and tags y with the link (``y._k8s_bnstat``); the convolution's backward deposits the sums and the
     identity of the dy they were taken over; the BatchNorm's backward uses them only when it receives exactly that dy
     (so a second consumer of y, whose gradient autograd would add, falls back to the reduction)."""
-    __slots__ = ("x", "mask", "mean", "x2", "mean2", "sums", "sums2", "dy_key")
+    __slots__ = ("x", "mask", "mean", "x2", "mean2", "invstd", "gamma", "beta", "relu", "sums", "sums2", "dy_key")
 
     def __init__(self):
         self.x = self.mask = self.mean = self.x2 = self.mean2 = None
+        self.invstd = self.gamma = self.beta = None
+        self.relu = False  # a non-residual BatchNorm + ReLU (mask None: g = relu_on(x) ? dy : 0, from the affine)
         self.sums = self.sums2 = self.dy_key = None
 
     def take(self, dy):
@@ -127,6 +131,7 @@ class BnStatLink:
         sums, sums2, key = self.sums, self.sums2, self.dy_key
         self.sums = self.sums2 = self.dy_key = None
         self.x = self.mask = self.mean = self.x2 = self.mean2 = None  # the BatchNorm's backward is the last reader
+        self.invstd = self.gamma = self.beta = None
         if sums is None or key != (dy.data_ptr(), tuple(dy.shape)):
             return None
         return sums, sums2
@@ -186,7 +191,7 @@ class _Conv2dNHWC(torch.autograd.Function):
                 ctx.link.grad = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, True, p, x_sub=xs)
                 return None, None, None, None, None, None, None, None
         dx = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, ctx.x_requires_grad, p, addend=addend, x_sub=xs,
-                           bn_link=ctx.bn_link if isinstance(addend, MaskedGrad) else None)
+                           bn_link=ctx.bn_link)
         return dx, None, None, None, None, None, None, None
 
 
@@ -198,7 +203,7 @@ def conv2d_nhwc(x: torch.Tensor, p, stride: int = 1, padding: int = 0, with_stat
     accumulated in the conv epilogue (None when the layer runs on the fallback path) -- the following
     ``batch_norm_act(..., sums=sums)`` then needs no statistics pass. ``grad_link``: a gradient for x
     deposited there by a later-backward node (``batch_norm_act(res_link=...)``) is added to dx in the dgrad."""
-    bn_link = getattr(x, "_k8s_bnstat", None) if (grad_link is not None and not grad_link.shared) else None
+    bn_link = getattr(x, "_k8s_bnstat", None) if (grad_link is None or not grad_link.shared) else None
     y, sums = _Conv2dNHWC.apply(x, p.store.anchor, p, stride, padding, with_stats, grad_link, bn_link)
     return (y, sums) if with_stats else y
 
@@ -289,8 +294,10 @@ class _BnAct(torch.autograd.Function):
         ctx.relu_x = relu and not keep_y and mask is None
         ctx.dy_link = dy_link if (dy_link is not None and not relu and res is None) else None
         ctx.stat_link = None
-        if stat_link is not None and mask is not None and training:
+        if stat_link is not None and training and (mask is not None or ctx.relu_x):
             stat_link.x, stat_link.mask, stat_link.mean = x, mask, mean
+            if mask is None:
+                stat_link.relu, stat_link.invstd, stat_link.gamma, stat_link.beta = True, invstd, pg.master, pb.master
             ctx.stat_link = stat_link
         return y
 
@@ -311,7 +318,9 @@ class _BnAct(torch.autograd.Function):
             handoff = isinstance(ctx.res_link, GradLink) and ctx.has_res and mask is not None
             want_dres = ctx.has_res and not (handoff or mask_out)
             pre = ctx.stat_link.take(dy) if ctx.stat_link is not None else None
-            if pre is not None:  # the reduction came with dy from its producer's epilogue (BnStatLink)
+            if pre is not None and mask is None:  # relu_x: the reduction came with dy (BnStatLink)
+                dx, dres = _C().bn_bwd_relu_from_sums(dy, x, pre[0], mean, invstd, pg.master, pb.master, dg, db)[0], None
+            elif pre is not None:  # the reduction came with dy from its producer's epilogue (BnStatLink)
                 dx, dres = _C().bn_bwd_from_sums(dy, x, mask, pre[0], mean, invstd, pg.master, pb.master, dg, db,
                                                  want_dres)
             else:
@@ -397,9 +406,19 @@ class _BnReluConv(torch.autograd.Function):
         pg, pb, pw = ctx.pg, ctx.pb, ctx.pw
         impl = _conv_impl()
         gy = gy.contiguous()
-        dz = impl.conv_bwd(gy, x, pw.weight, ctx.stride, ctx.padding, True, pw, xform=params)
+        # the BatchNorm-backward sums in the data gradient's epilogue where a kernel takes them (BnStatLink)
+        link = None
+        if BN_BSTATS:
+            link = BnStatLink()
+            link.x, link.mean, link.invstd, link.gamma, link.beta, link.relu = (x, mean, invstd, pg.master, pb.master,
+                                                                                True)
+        dz = impl.conv_bwd(gy, x, pw.weight, ctx.stride, ctx.padding, True, pw, xform=params, bn_link=link)
         dg, db, finish = _bn_param_grads(pg.store, pg, pb, x.device)
-        dx, _ = _C().bn_bwd(dz, x, None, mean, invstd, pg.master, pb.master, True, dg, db, False)
+        pre = link.take(dz) if link is not None else None
+        if pre is not None:
+            dx = _C().bn_bwd_relu_from_sums(dz, x, pre[0], mean, invstd, pg.master, pb.master, dg, db)[0]
+        else:
+            dx, _ = _C().bn_bwd(dz, x, None, mean, invstd, pg.master, pb.master, True, dg, db, False)
         finish()
         return (dx if ctx.x_requires_grad else None,) + (None,) * 11
 
@@ -450,7 +469,7 @@ def batch_norm_act(x, pg, pb, run_mean, run_var, residual=None, relu=True, train
     ``res_link``: the residual's gradient is handed to that GradLink (and NOT returned to autograd); the
     node consuming the link must add it (``conv2d_nhwc(..., grad_link=link)`` on the same tensor).
     ``res_link`` may also be a MaskLink whose ``dy_link`` end is the plain BN that produced ``residual``."""
-    link = BnStatLink() if (BN_BSTATS and relu and residual is not None and training and _gpu(x)) else None
+    link = BnStatLink() if (BN_BSTATS and relu and training and _gpu(x)) else None
     y = _BnAct.apply(x, residual, pg.store.anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu,
                      sums, res_link, dy_link, link)
     if link is not None and link.x is not None:

@@ -621,3 +621,57 @@ def test_bn_bwd_from_sums_matches_reduce(cuda):
     dx2, _ = C_.bn_bwd_from_sums(dy, x, mask, sums, mean, invstd, gamma, beta, dg2, db2, False)
     assert _rel(db2, db1) < 1e-5 and _rel(dg2, dg1) < 1e-4
     assert _rel(dx2, dx1) < 5e-3
+
+
+@pytest.mark.parametrize("N,H,C,K", [(3, 56, 64, 64), (2, 28, 128, 128), (3, 14, 256, 256)])
+def test_conv3x3_dgrad_bnstats_epilogue(cuda, N, H, C, K):
+    """The stride-1 3x3 data gradient on the staged-window kernel with the BatchNorm-backward sums of the
+    relu(BN(x)) that fed the convolution (conv3x3.hip epilogue): dx bitwise equal to the plain dgrad, the sums
+    against fp32 sums over the stored dx with the forward's ReLU decision relu_on(x) recomputed from the affine."""
+    C_ = _C()
+    torch.manual_seed(13)
+    gy = torch.randn(N, H, H, K, device=cuda).bfloat16()
+    w = (torch.randn(K, 3, 3, C, device=cuda) * 0.05).bfloat16()
+    x = (torch.randn(N, H, H, C, device=cuda) * 1.5 + 0.2).bfloat16()
+    mean = x.float().reshape(-1, C).mean(0)
+    invstd = torch.rsqrt(x.float().reshape(-1, C).var(0, unbiased=False) + 1e-5)
+    gamma, beta = torch.rand(C, device=cuda) + 0.5, torch.randn(C, device=cuda) * 0.2
+    sums = torch.zeros(C_.conv_stat_replicas, 2, C, device=cuda)
+    wt = C_.conv_dgrad_wtrans(w)
+    dx = C_.conv3x3_dgrad_bnstats(gy, wt, x, gamma, beta, mean, invstd, sums)
+    plain = C_.conv_fwd(gy, wt, 1, 1, 1, False, None, 0, None)
+    assert torch.equal(dx, plain)
+    scale = gamma * invstd
+    shift = torch.addcmul(beta, -mean, scale)  # fma(-mean, scale, beta) up to rounding: compare the decision loosely
+    z = (x.float() * scale + shift).bfloat16().float()
+    g = torch.where(z > 0, dx.float(), torch.zeros_like(dx.float())).reshape(-1, C)
+    tot = sums.sum(0)
+    assert _rel(tot[0], g.sum(0)) < 1e-3
+    assert _rel(tot[1], (g * (x.float().reshape(-1, C) - mean)).sum(0)) < 1e-3
+
+
+@pytest.mark.parametrize("M,K,N", [(9000, 256, 64), (4100, 512, 128), (1000, 384, 72)])
+def test_gemm_dgrad_bnstats_epilogue(cuda, M, K, N):
+    """The 1x1 data gradient on the tile kernel with the BatchNorm-backward sums of the relu(BN(x)) that fed the
+    convolution (gemm.hip BST epilogue): dx bitwise equal to the plain dgrad, the sums against fp32 sums over the
+    stored dx with the forward's ReLU decision."""
+    C_ = _C()
+    assert C_.gemm_dgrad_bnstats_ok(M, N, K)
+    torch.manual_seed(14)
+    gy = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(K, N, device=cuda) * 0.05).bfloat16()
+    x = (torch.randn(M, N, device=cuda) * 1.5 + 0.2).bfloat16()
+    mean = x.float().mean(0)
+    invstd = torch.rsqrt(x.float().var(0, unbiased=False) + 1e-5)
+    gamma, beta = torch.rand(N, device=cuda) + 0.5, torch.randn(N, device=cuda) * 0.2
+    sums = torch.zeros(C_.conv_stat_replicas, 2, N, device=cuda)
+    dx = C_.gemm_dgrad_bnstats(gy, w, x, gamma, beta, mean, invstd, sums)
+    plain = C_.gemm(gy, True, w, False, None, False, None, 0, None, False, 1.0, 1)
+    assert torch.equal(dx, plain)
+    scale = gamma * invstd
+    shift = torch.addcmul(beta, -mean, scale)
+    z = (x.float() * scale + shift).bfloat16().float()
+    g = torch.where(z > 0, dx.float(), torch.zeros_like(dx.float()))
+    tot = sums.sum(0)
+    assert _rel(tot[0], g.sum(0)) < 1e-3
+    assert _rel(tot[1], (g * (x.float() - mean)).sum(0)) < 1e-3

@@ -249,8 +249,11 @@ def test_resnet50_large_batch_indexing_matches_half_batch(cuda, half):
 def test_bn_backward_sums_in_dgrad_epilogue_match_reduction(cuda):
     """BatchNorm-backward sums taken in the identity-block conv1 data-gradient epilogue (ops.nn.BnStatLink,
     gemm_short.hip EPI 3 / 4: single residual BN at K = 64 / 128, the downsample block's two BNs at K = 64) against the
-    BatchNorms' own reduction sweeps (ops.nn.BN_BSTATS off): same loss, every gradient within fp32 summation-order
-    noise, and the fused path taken at least three times."""
+    BatchNorms' own reduction sweeps (ops.nn.BN_BSTATS off), whole model: same loss, every gradient within fp32
+    summation-order noise, and the fused path taken. (64 x 64 images at batch 4: the forward is deterministic -- at
+    224 x 224, or batch 16, two runs of the SAME path already differ by 30-40 % in the early layers' gradients: the
+    forward's atomically accumulated BatchNorm statistics flip bf16 roundings, and this net -- every BatchNorm gamma
+    drawn in [0.6, 1.4], bn3 included -- amplifies them.)"""
     from k8s_amd.models.resnet import ResNet
     from k8s_amd.ops import conv as kc
 
@@ -269,9 +272,10 @@ def test_bn_backward_sums_in_dgrad_epilogue_match_reduction(cuda):
                                         else torch.randn(p.shape, generator=gen) * 0.1).to(cuda))
             store.refresh_lowp()
             m.train()
-            images = torch.randn(16, 64, 64, 3, generator=torch.Generator(device="cpu").manual_seed(1)).to(cuda)
+            # batch 4: every conv's statistics replica gets one tile, so the forward is bitwise repeatable
+            images = torch.randn(4, 64, 64, 3, generator=torch.Generator(device="cpu").manual_seed(1)).to(cuda)
             x = m.prepare_input(images.bfloat16())
-            y = torch.arange(16, device=cuda) % 10
+            y = torch.arange(4, device=cuda) % 10
             n0 = kc.STATS["bn_bstats"]
             store.begin_step()
             loss = K.cross_entropy(m(x), y)
@@ -283,11 +287,64 @@ def test_bn_backward_sums_in_dgrad_epilogue_match_reduction(cuda):
 
     l1, g1, n1 = run(True)
     l0, g0, n0 = run(False)
-    assert n0 == 0 and n1 >= 3, (n0, n1)
-    assert l1 == l0
+    assert n0 == 0 and n1 >= 6, (n0, n1)  # s1b0 (dual), s1b1, s2b1 + the stage-1 bn2 sums in conv3's dgrad
+    assert abs(l1 - l0) < 1e-3 * max(1.0, abs(l0)), (l1, l0)
     bad = []
     for name, r in g0.items():
         err = (g1[name] - r).norm().item() / (r.norm().item() + 1e-6)
-        if err > 2e-2:
+        if err > 1e-2:
+            bad.append((name, round(err, 4)))
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("H,cin,width", [(56, 256, 64), (28, 512, 128), (14, 1024, 256)])
+def test_bn_backward_sums_bottleneck_3x3_and_residual(cuda, H, cin, width):
+    """One identity bottleneck at a staged-window 3x3 size behind a residual BatchNorm: bn1's sums in the 3x3 conv2
+    data-gradient epilogue (conv3x3.hip) and the input BN's sums in conv1's masked-addend dgrad (gemm_short.hip,
+    where its contract holds) against the separate reductions (ops.nn.BN_BSTATS off): every gradient, the input's
+    included, within fp32 summation-order noise."""
+    from k8s_amd.models.resnet import BN, Bottleneck, Conv
+    from k8s_amd.ops import conv as kc
+
+    def run(on):
+        old = K.BN_BSTATS
+        K.BN_BSTATS = on
+        try:
+            torch.manual_seed(0)
+            store = ParamStore()
+            pre, bn = Conv(store, "pre", cin, cin, 1), BN(store, "prebn", cin)
+            blk = Bottleneck(store, "blk", cin, width, 1, False)
+            store.finalize(cuda, seed=5)
+            with torch.no_grad():
+                gen = torch.Generator(device="cpu").manual_seed(11)
+                for p in store.params:
+                    if "bn" in p.name:
+                        p.master.copy_((torch.rand(p.shape, generator=gen) * 0.8 + 0.6 if p.name.endswith("weight")
+                                        else torch.randn(p.shape, generator=gen) * 0.1).to(cuda))
+            store.refresh_lowp()
+            bn.to(cuda)
+            blk.to(cuda)
+            g = torch.Generator(device="cpu").manual_seed(2)
+            x0 = torch.randn(2, H, H, cin, generator=g).to(cuda).bfloat16().requires_grad_(True)
+            r = torch.randn(2, H, H, cin, generator=g).to(cuda).bfloat16()
+            gy = torch.randn(2, H, H, cin, generator=g).to(cuda)
+            n0 = kc.STATS["bn_bstats"]
+            store.begin_step()
+            out = blk(bn(pre(x0), residual=r, relu=True))
+            (out.float() * gy).sum().backward()
+            store.zero_unwritten()
+            grads = {p.name: p.grad.float().clone() for p in store.params}
+            grads["x0"] = x0.grad.float().clone()
+            return grads, kc.STATS["bn_bstats"] - n0
+        finally:
+            K.BN_BSTATS = old
+
+    g1, n1 = run(True)
+    g0, n0 = run(False)
+    assert n0 == 0 and n1 >= 1, (n0, n1)
+    bad = []
+    for name, r in g0.items():
+        err = (g1[name] - r).norm().item() / (r.norm().item() + 1e-6)
+        if err > 1e-2:
             bad.append((name, round(err, 4)))
     assert not bad, bad
