@@ -187,8 +187,28 @@ __global__ void __launch_bounds__(THREADS, 2) conv3x3_kernel(const uint16_t* __r
   // steps g = slice * 9 + 3 ds + dr visit the taps ds-major; tap_of(k) for k = g % 9
   auto tap_of = [](int k) { return (k % 3) * 3 + k / 3; };
 
+  // BatchNorm-backward sums (bb.sums, a data gradient): this thread's x chunks at its output positions. With a 64-wide
+  // K tile (the 56 x 56 layers: 7 chunks, 28 VGPRs beside 186) they are loaded here, behind the first window DMA, so
+  // the epilogue never waits on them (loaded at the epilogue, their latency was exposed once per tile: +0.5 ms per
+  // 56 x 56 call); the 128-wide tiles have no such room and load them when the accumulators are freed.
+  constexpr int CPR = KT / 8;
+  constexpr int RSTEP = THREADS / CPR, NR = (P + RSTEP - 1) / RSTEP;
+  constexpr bool XEARLY = KT == 64;
+  const int c = tid % CPR, row0 = tid / CPR;
+  const bool bst = bb.sums != nullptr;
+  bf16x8_t xr[NR];
+  auto load_xr = [&]() {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int m = row0 + i * RSTEP, hr = m / W, h = h0 + hr;
+      xr[i] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      if (m < P && h < H)
+        xr[i] = *reinterpret_cast<const bf16x8_t*>(bb.x + (((long)n * H + h) * W + (m - hr * W)) * K + k0 + c * 8);
+    }
+  };
   const int nsteps = (C >> 6) * 9;
   load_window(0);
+  if (XEARLY && bst) load_xr();
 #pragma unroll
   for (int g = 0; g < NS - 1; ++g)
     if (g < nsteps) stage_w(tap_of(g), 0, g);
@@ -276,11 +296,6 @@ __global__ void __launch_bounds__(THREADS, 2) conv3x3_kernel(const uint16_t* __r
   // non-residual BatchNorm + ReLU that produced the convolution's input: g = relu_on(x) ? dx : 0, sum g and
   // sum g (x - mean) per channel, x read at the output positions (prefetched here, into the registers the
   // accumulators free, so the loads overlap the staging)
-  constexpr int CPR = KT / 8;
-  constexpr int RSTEP = THREADS / CPR, NR = (P + RSTEP - 1) / RSTEP;
-  const int c = tid % CPR, row0 = tid / CPR;
-  const bool bst = bb.sums != nullptr;
-  bf16x8_t xr[NR];
   float bsc[8], bsh[8], bmu[8];
   if (bst) {
 #pragma unroll
@@ -289,13 +304,7 @@ __global__ void __launch_bounds__(THREADS, 2) conv3x3_kernel(const uint16_t* __r
       bmu[j] = bb.mean[col];
       bn_affine_regs(bb.gamma[col], bb.beta[col], bmu[j], bb.invstd[col], bsc[j], bsh[j]);
     }
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int m = row0 + i * RSTEP, hr = m / W, h = h0 + hr;
-      xr[i] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-      if (m < P && h < H)
-        xr[i] = *reinterpret_cast<const bf16x8_t*>(bb.x + (((long)n * H + h) * W + (m - hr * W)) * K + k0 + c * 8);
-    }
+    if (!XEARLY) load_xr();
   }
   uint16_t* const ctile = reinterpret_cast<uint16_t*>(smem);
 #pragma unroll

@@ -119,13 +119,20 @@ def _wgrad_hip(C_, gy, x, out, stride, padding, acc, xform=None):
         C_.conv_wgrad(x, gy, out, stride, padding, 1, 0, acc, xform=xform)
 
 
+# which data-gradient kernels take a non-residual BatchNorm + ReLU's backward sums (nn.BnStatLink, relu): the 3x3
+# staged-window kernel and the 1x1 tile kernel (K8S_AMD_BN_BSTATS_3X3 / _GEMM = 0 for the A/B)
+BSTATS_3X3 = os.environ.get("K8S_AMD_BN_BSTATS_3X3", "1") != "0"
+BSTATS_GEMM = os.environ.get("K8S_AMD_BN_BSTATS_GEMM", "1") != "0"
+
+
 def _dgrad_hip(C_, gy, w, padding, addend=None, bn_link=None):
     """dx on our kernels; with ``addend`` (bf16, shape of dx) a 1x1 dgrad accumulates onto it in the GEMM
     epilogue and returns it (the fused residual-gradient add). ``bn_link`` (nn.BnStatLink, with a masked addend):
     the epilogue also accumulates the BatchNorm-backward sums of dx for the BatchNorm(s) that produced x."""
     K, R, S, C = w.shape
     masked = addend is not None and not torch.is_tensor(addend)  # nn.MaskedGrad: (dy, packed ReLU mask)
-    if (bn_link is not None and bn_link.relu and bn_link.x is not None and addend is None and R == 3 and S == 3
+    if (BSTATS_3X3 and bn_link is not None and bn_link.relu and bn_link.x is not None and addend is None and R == 3
+            and S == 3
             and padding == 1 and gy.shape[1] == gy.shape[2] and bn_link.x.shape[:3] == gy.shape[:3]
             and C_.conv3x3_staged_ok(gy.shape[1], gy.shape[2], C, K, 3, 3, 1, 1)):
         sums = torch.zeros(C_.conv_stat_replicas, 2, C, device=gy.device, dtype=torch.float32)
@@ -149,7 +156,7 @@ def _dgrad_hip(C_, gy, w, padding, addend=None, bn_link=None):
             bn_link.sums, bn_link.sums2, bn_link.dy_key = sums, sums2, (out.data_ptr(), tuple(out.shape))
             STATS["bn_bstats"] += 1
             return out
-        if (bn_link is not None and bn_link.relu and bn_link.x is not None and addend is None
+        if (BSTATS_GEMM and bn_link is not None and bn_link.relu and bn_link.x is not None and addend is None
                 and bn_link.x.shape == (N, H, W_, C) and C_.gemm_dgrad_bnstats_ok(N * H * W_, C, K)):
             sums = torch.zeros(C_.conv_stat_replicas, 2, C, device=gy.device, dtype=torch.float32)
             out = C_.gemm_dgrad_bnstats(gy.reshape(-1, K), w.reshape(K, C), bn_link.x.view(-1, C), bn_link.gamma,
