@@ -125,6 +125,16 @@ BSTATS_3X3 = os.environ.get("K8S_AMD_BN_BSTATS_3X3", "1") != "0"
 BSTATS_GEMM = os.environ.get("K8S_AMD_BN_BSTATS_GEMM", "1") != "0"
 
 
+def _bn_sums(C_, bn_link, C, device):
+    """Zeroed fp32 [conv_stat_replicas, 2, C] for a BnStatLink's sums: the BatchNorm store's per-step scratch (one fill
+    per step) where it has one, else a fresh zeros tensor."""
+    R = C_.conv_stat_replicas
+    if bn_link.store is not None:
+        from k8s_amd.ops.nn import _zero_scratch
+        return _zero_scratch(bn_link.store, device, R * 2 * C).view(R, 2, C)
+    return torch.zeros(R, 2, C, device=device, dtype=torch.float32)
+
+
 def _dgrad_hip(C_, gy, w, padding, addend=None, bn_link=None):
     """dx on our kernels; with ``addend`` (bf16, shape of dx) a 1x1 dgrad accumulates onto it in the GEMM
     epilogue and returns it (the fused residual-gradient add). ``bn_link`` (nn.BnStatLink, with a masked addend):
@@ -135,7 +145,7 @@ def _dgrad_hip(C_, gy, w, padding, addend=None, bn_link=None):
             and S == 3
             and padding == 1 and gy.shape[1] == gy.shape[2] and bn_link.x.shape[:3] == gy.shape[:3]
             and C_.conv3x3_staged_ok(gy.shape[1], gy.shape[2], C, K, 3, 3, 1, 1)):
-        sums = torch.zeros(C_.conv_stat_replicas, 2, C, device=gy.device, dtype=torch.float32)
+        sums = _bn_sums(C_, bn_link, C, gy.device)
         dx = C_.conv3x3_dgrad_bnstats(gy, C_.conv_dgrad_wtrans(w), bn_link.x, bn_link.gamma, bn_link.beta,
                                       bn_link.mean, bn_link.invstd, sums)
         bn_link.sums, bn_link.sums2, bn_link.dy_key = sums, None, (dx.data_ptr(), tuple(dx.shape))
@@ -146,9 +156,8 @@ def _dgrad_hip(C_, gy, w, padding, addend=None, bn_link=None):
         if masked and bn_link is not None and not bn_link.relu and bn_link.x is not None and \
                 bn_link.x.shape == (N, H, W_, C) and \
                 C_.gemm_short_bnstats_ok(N * H * W_, C, K, bn_link.x2 is not None):
-            R_ = C_.conv_stat_replicas
-            sums = torch.zeros(R_, 2, C, device=gy.device, dtype=torch.float32)
-            sums2 = torch.zeros(R_, 2, C, device=gy.device, dtype=torch.float32) if bn_link.x2 is not None else None
+            sums = _bn_sums(C_, bn_link, C, gy.device)
+            sums2 = _bn_sums(C_, bn_link, C, gy.device) if bn_link.x2 is not None else None
             out = C_.dgrad_short_bnstats(
                 gy.reshape(-1, K), w.reshape(K, C), addend.dy.view(-1, C), addend.mask, bn_link.x.view(-1, C),
                 bn_link.mask, bn_link.mean, sums, None if sums2 is None else bn_link.x2.view(-1, C), bn_link.mean2,
@@ -158,7 +167,7 @@ def _dgrad_hip(C_, gy, w, padding, addend=None, bn_link=None):
             return out
         if (BSTATS_GEMM and bn_link is not None and bn_link.relu and bn_link.x is not None and addend is None
                 and bn_link.x.shape == (N, H, W_, C) and C_.gemm_dgrad_bnstats_ok(N * H * W_, C, K)):
-            sums = torch.zeros(C_.conv_stat_replicas, 2, C, device=gy.device, dtype=torch.float32)
+            sums = _bn_sums(C_, bn_link, C, gy.device)
             out = C_.gemm_dgrad_bnstats(gy.reshape(-1, K), w.reshape(K, C), bn_link.x.view(-1, C), bn_link.gamma,
                                         bn_link.beta, bn_link.mean, bn_link.invstd, sums).view(N, H, W_, C)
             bn_link.sums, bn_link.sums2, bn_link.dy_key = sums, None, (out.data_ptr(), tuple(out.shape))

@@ -118,9 +118,11 @@ class BnStatLink:
     mean2]) and tags y with the link (``y._k8s_bnstat``); the convolution's backward deposits the sums and the
     identity of the dy they were taken over; the BatchNorm's backward uses them only when it receives exactly that dy
     (so a second consumer of y, whose gradient autograd would add, falls back to the reduction)."""
-    __slots__ = ("x", "mask", "mean", "x2", "mean2", "invstd", "gamma", "beta", "relu", "sums", "sums2", "dy_key")
+    __slots__ = ("x", "mask", "mean", "x2", "mean2", "invstd", "gamma", "beta", "relu", "sums", "sums2", "dy_key",
+                 "store")
 
-    def __init__(self):
+    def __init__(self, store=None):
+        self.store = store  # the BatchNorm's ParamStore: its per-step zeroed scratch holds the sums
         self.x = self.mask = self.mean = self.x2 = self.mean2 = None
         self.invstd = self.gamma = self.beta = None
         self.relu = False  # a non-residual BatchNorm + ReLU (mask None: g = relu_on(x) ? dy : 0, from the affine)
@@ -295,7 +297,7 @@ class _BnAct(torch.autograd.Function):
         ctx.dy_link = dy_link if (dy_link is not None and not relu and res is None) else None
         ctx.stat_link = None
         if stat_link is not None and training and (mask is not None or ctx.relu_x):
-            stat_link.x, stat_link.mask, stat_link.mean = x, mask, mean
+            stat_link.x, stat_link.mask, stat_link.mean, stat_link.store = x, mask, mean, pg.store
             if mask is None:
                 stat_link.relu, stat_link.invstd, stat_link.gamma, stat_link.beta = True, invstd, pg.master, pb.master
             ctx.stat_link = stat_link
@@ -409,7 +411,7 @@ class _BnReluConv(torch.autograd.Function):
         # the BatchNorm-backward sums in the data gradient's epilogue where a kernel takes them (BnStatLink)
         link = None
         if BN_BSTATS:
-            link = BnStatLink()
+            link = BnStatLink(pg.store)
             link.x, link.mean, link.invstd, link.gamma, link.beta, link.relu = (x, mean, invstd, pg.master, pb.master,
                                                                                 True)
         dz = impl.conv_bwd(gy, x, pw.weight, ctx.stride, ctx.padding, True, pw, xform=params, bn_link=link)
@@ -878,6 +880,7 @@ class _BnActDual(torch.autograd.Function):
         ctx.stat_link = stat_link
         if stat_link is not None:
             stat_link.x, stat_link.mask, stat_link.mean, stat_link.x2, stat_link.mean2 = x, mask, mean, xr, mean_r
+            stat_link.store = pg.store
         return y
 
     @staticmethod
