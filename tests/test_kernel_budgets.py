@@ -68,7 +68,7 @@ def _waves_per_simd(k, threads=256):
 BUDGETS = [
     (r"c314conv3x3_kernel", 2, 256),
     (r"g414gemm_w4_kernel", 1, 256),
-    (r"g256r14gemm256r_kernel", 1, 512),
+    (r"gemm256r_kernel", 1, 512),
     (r"gsk17gemm_short_kernel", 2, 256),
     (r"3wg3\d*wgrad3x3_kernel|wgrad3x3_kernel", 2, 256),
     (r"stem_conv_fwd_kernel", 2, 256),
