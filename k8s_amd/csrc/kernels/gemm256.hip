@@ -852,6 +852,66 @@ __device__ __forceinline__ void copy_out_stats(uint16_t* __restrict__ C, float* 
   atomicAdd(d + N, p0[128 + c] + p1[128 + c]);
 }
 
+// ACT = 6 (a data gradient dx = dy . w): the BatchNorm-backward sums of dx for the relu(BN(x)) that produced the
+// convolution's input (launchers.h BnBwdSums): g = relu_on(x) ? dx : 0, sums[rep][0][c] += sum g, [1][c] += sum g (x -
+// mean). x is read at the output positions (same layout), in two halves of 16 rows per lane, each half's loads issued
+// before the previous half is consumed; tab = [gamma | beta | mean | invstd] fp32 [4][N].
+template <class Off, class Stg>
+__device__ __forceinline__ void copy_out_bnbwd(uint16_t* __restrict__ C, const uint16_t* __restrict__ x,
+                                               const float* __restrict__ tab, float* __restrict__ sums, char* smem,
+                                               char* stg, const Off& coff, const Stg& staged, int rep, int N,
+                                               int n0, int col0) {
+  const int lane = threadIdx.x & 63, col = col0 + (lane & 15) * 8;
+  float sc[8], sh[8], mu[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    mu[r] = tab[2 * N + col + r];
+    bn_affine_regs(tab[col + r], tab[N + col + r], mu[r], tab[3 * N + col + r], sc[r], sh[r]);
+  }
+  float sm[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, sq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  bf16x8_t xv[16];
+#pragma unroll
+  for (int it = 0; it < 16; ++it) xv[it] = *reinterpret_cast<const bf16x8_t*>(x + coff(it));
+#pragma unroll
+  for (int it = 0; it < 32; ++it) {
+    const bf16x8_t v = staged(it);
+    *reinterpret_cast<bf16x8_t*>(C + coff(it)) = v;
+    const bf16x8_t xx = xv[it & 15];
+    if (it < 16) xv[it] = *reinterpret_cast<const bf16x8_t*>(x + coff(it + 16));
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const float xf = bf2f((uint16_t)xx[r]);
+      const float g = relu_on(xf, sc[r], sh[r]) ? bf2f((uint16_t)v[r]) : 0.f;
+      sm[r] += g;
+      sq[r] = __builtin_fmaf(g, xf - mu[r], sq[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    sm[r] += __shfl_xor(sm[r], 16);
+    sm[r] += __shfl_xor(sm[r], 32);
+    sq[r] += __shfl_xor(sq[r], 16);
+    sq[r] += __shfl_xor(sq[r], 32);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's staged reads are done: reuse its region
+  if (lane < 16) {
+    float* part = reinterpret_cast<float*>(stg);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      part[lane * 8 + r] = sm[r];
+      part[128 + lane * 8 + r] = sq[r];
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  g256::barrier();
+  const int t = threadIdx.x, wcol = t >> 7, c = t & 127;
+  const float* p0 = reinterpret_cast<const float*>(smem + (0 * 2 + wcol) * 32768);  // wave (wr 0, wc)
+  const float* p1 = reinterpret_cast<const float*>(smem + (1 * 2 + wcol) * 32768);  // wave (wr 1, wc)
+  float* d = sums + (long)rep * 2 * N + n0 + wcol * 128 + c;
+  atomicAdd(d, p0[c] + p1[c]);
+  atomicAdd(d + N, p0[128 + c] + p1[128 + c]);
+}
+
 template <bool AMN, bool BMN, bool X>
 __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __restrict__ A, long lda,
                                                              const uint16_t* __restrict__ B, long ldb, void* Cv,
@@ -1213,6 +1273,9 @@ __global__ void __launch_bounds__(THREADS, 1) gemm_w4_kernel(const uint16_t* __r
       copy_out_swiglu(C, pre, stg, coff, staged, m0 + wr * 128, (n0 + wc * 128) / 2, N);
     } else if (act == 5) {
       copy_out_stats(C, cpart, smem, stg, coff, staged, (m0 >> 8) % kConvStatReplicas, N, n0);
+    } else if (act == 6) {
+      copy_out_bnbwd(C, pre, rtab, cpart, smem, stg, coff, staged, (m0 >> 8) % kConvStatReplicas, N, n0,
+                     n0 + wc * 128);
     } else if (act == 4) {
       copy_out_rope(C, stg, (long)(m0 + wr * 128) * ldc + n0 + wc * 128, ldc, n0 + wc * 128 < rcols, rpos, rtab,
                     m0 + wr * 128);
@@ -1388,6 +1451,30 @@ void launch_gemm_w4_stats(const uint16_t* A, long lda, const uint16_t* B, long l
   hipLaunchKernelGGL((g4::gemm_w4_kernel<false, false, true>), dim3(blocks), dim3(g4::THREADS), 0, st, A, lda, B, ldb,
                      (void*)y, (long)N, M, N, K, 1.f, kps, sk, 0, 0, nullptr, 5, nullptr, 0L, stats, nullptr, nullptr,
                      0);
+}
+
+// A data gradient dx [M][N] = dy [M][K] . w [K][N] (w stored MN-major, the 1x1 convolution's [Kout][Cin]) with the
+// BatchNorm-backward sums of dx in the epilogue (copy_out_bnbwd); whole 256 x 256 tiles, stream-K tail with a workspace.
+bool gemm_w4_dgrad_bnstats_ok(int M, int N, int K) {
+  return w4_enabled() && M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && (long)(M / 256) * (N / 256) >= planner_cus();
+}
+void launch_gemm_w4_dgrad_bnstats(const uint16_t* A, const uint16_t* B, uint16_t* y, int M, int N, int K,
+                                  const uint16_t* x, const float* tab, float* sums, float* sk_slabs, int* sk_sync,
+                                  hipStream_t st) {
+  if (!gemm_w4_dgrad_bnstats_ok(M, N, K)) throw std::runtime_error("w4 dgrad BatchNorm sums: outside the contract");
+  Gemm256Plan plan = gemm256_plan(M, N, K);
+  if (!sk_slabs || !sk_sync) plan.sk = 1;
+  const int tiles = (M / 256) * (N / 256);
+  g256r::SkArgs sk{tiles, 1, nullptr, nullptr};
+  int blocks = tiles, kps = K;
+  if (plan.sk > 1) {
+    sk = g256r::SkArgs{plan.full, plan.sk, sk_slabs, sk_sync};
+    kps = plan.kps;
+    blocks = plan.full + (tiles - plan.full) * plan.sk;
+  }
+  hipLaunchKernelGGL((g4::gemm_w4_kernel<false, true, true>), dim3(blocks), dim3(g4::THREADS), 0, st, A, (long)K, B,
+                     (long)N, (void*)y, (long)N, M, N, K, 1.f, kps, sk, 0, 0, nullptr, 6, const_cast<uint16_t*>(x), 0L,
+                     sums, nullptr, tab, 0);
 }
 
 // Stream-K tail plan for a grid of 256 x 256 tiles on P = planner_cus() CUs (one block per CU; 256 on MI355X): with

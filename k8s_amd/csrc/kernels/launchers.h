@@ -154,6 +154,10 @@ void launch_gemm_w4_swiglu_bwd(const uint16_t* A, long lda, const uint16_t* B, l
                                const uint16_t* gu, int M, int F, int K, int blk, float* sk_slabs, int* sk_sync,
                                hipStream_t st);
 bool gemm_w4_stats_ok(int M, int N, int K);
+bool gemm_w4_dgrad_bnstats_ok(int M, int N, int K);
+void launch_gemm_w4_dgrad_bnstats(const uint16_t* A, const uint16_t* B, uint16_t* y, int M, int N, int K,
+                                  const uint16_t* x, const float* tab, float* sums, float* sk_slabs, int* sk_sync,
+                                  hipStream_t st);
 void launch_gemm_w4_stats(const uint16_t* A, long lda, const uint16_t* B, long ldb, uint16_t* y, int M, int N, int K,
                           float* stats, float* sk_slabs, int* sk_sync, hipStream_t st);
 bool gemm_w4_rope_ok(int M, int N, int K, long lda, long ldb, int rot_cols);

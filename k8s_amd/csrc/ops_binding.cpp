@@ -572,6 +572,20 @@ Tensor gemm_dgrad_bnstats(Tensor gy, Tensor w, Tensor x, Tensor gamma, Tensor be
                   sums.numel() == (long)k8s_amd::kConvStatReplicas * 2 * N,
               "sums: zeroed fp32 [conv_stat_replicas, 2, N]");
   Tensor out = torch::empty({M, N}, gy.options());
+  if (use_gemm256(M, N, K, true, false)) {  // the product's regular path is the 256 x 256 kernel: its epilogue
+    TORCH_CHECK(k8s_amd::gemm_w4_dgrad_bnstats_ok((int)M, (int)N, (int)K), "gemm_dgrad_bnstats: 4-wave contract");
+    Tensor tab = torch::cat({gamma, beta, mean, invstd});
+    const k8s_amd::Gemm256Plan plan = k8s_amd::gemm256_plan((int)M, (int)N, (int)K);
+    Tensor slabs;
+    int* sync = nullptr;
+    if (plan.sk > 1) {
+      slabs = torch::empty({k8s_amd::gemm256_sk_slab_floats(plan)}, gy.options().dtype(at::kFloat));
+      sync = sk_sync_words(k8s_amd::gemm256_sk_sync_ints(plan), gy.device());
+    }
+    k8s_amd::launch_gemm_w4_dgrad_bnstats(cbf(gy), cbf(w), bf(out), (int)M, (int)N, (int)K, cbf(x), f32(tab),
+                                          f32(sums), sync ? f32(slabs) : nullptr, sync, cur_stream());
+    return out;
+  }
   k8s_amd::BnBwdSums bb;
   bb.x = cbf(x);
   bb.gamma = f32(gamma);
@@ -1390,9 +1404,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_dgrad_bnstats_ok", [](int64_t M, int64_t N, int64_t K) {
     const char* e = std::getenv("K8S_AMD_BN_BSTATS");
     if (e && e[0] == '0') return false;
-    return M < (1L << 31) && N % 8 == 0 && !use_gemm256(M, N, K, true, false) &&
-           !k8s_amd::gemm_short_ok((int)M, (int)N, (int)K, K, N);
-  }, "whether a 1x1 data gradient takes gemm_dgrad_bnstats (the tile kernel is its regular path)");
+    if (M >= (1L << 31) || N % 8 != 0) return false;
+    if (use_gemm256(M, N, K, true, false)) {
+      const char* g = std::getenv("K8S_AMD_BN_BSTATS_W4");
+      return !(g && g[0] == '0') && k8s_amd::gemm_w4_dgrad_bnstats_ok((int)M, (int)N, (int)K);
+    }
+    return !k8s_amd::gemm_short_ok((int)M, (int)N, (int)K, K, N);
+  }, "whether a 1x1 data gradient takes gemm_dgrad_bnstats (on its regular kernel: the 4-wave or the tile kernel)");
   m.def("bn_bwd_relu_from_sums", &bn_bwd_relu_from_sums, "relu_x BatchNorm backward from a producer's sums");
   m.def("bn_bwd_from_sums", &bn_bwd_from_sums, "BatchNorm backward from a producer's reduction sums (final + apply)");
   m.def("bn_bwd_dual_from_sums", &bn_bwd_dual_from_sums, "bn_bwd_dual from a producer's reduction sums");

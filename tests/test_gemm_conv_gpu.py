@@ -650,11 +650,13 @@ def test_conv3x3_dgrad_bnstats_epilogue(cuda, N, H, C, K):
     assert _rel(tot[1], (g * (x.float().reshape(-1, C) - mean)).sum(0)) < 1e-3
 
 
-@pytest.mark.parametrize("M,K,N", [(9000, 256, 64), (4100, 512, 128), (1000, 384, 72)])
+@pytest.mark.parametrize("M,K,N", [(9000, 256, 64), (4100, 512, 128), (1000, 384, 72),
+                                   # the 4-wave kernel's copy_out_bnbwd: whole waves, and a stream-K tail
+                                   (65536, 1024, 256), (150528, 2048, 512)])
 def test_gemm_dgrad_bnstats_epilogue(cuda, M, K, N):
-    """The 1x1 data gradient on the tile kernel with the BatchNorm-backward sums of the relu(BN(x)) that fed the
-    convolution (gemm.hip BST epilogue): dx bitwise equal to the plain dgrad, the sums against fp32 sums over the
-    stored dx with the forward's ReLU decision."""
+    """The 1x1 data gradient on its regular kernel (the tile kernel's BST epilogue, or the 4-wave kernel's ACT 6
+    copy-out) with the BatchNorm-backward sums of the relu(BN(x)) that fed the convolution: dx bitwise equal to the
+    plain dgrad, the sums against fp32 sums over the stored dx with the forward's ReLU decision."""
     C_ = _C()
     assert C_.gemm_dgrad_bnstats_ok(M, N, K)
     torch.manual_seed(14)

@@ -247,14 +247,14 @@ def test_resnet50_large_batch_indexing_matches_half_batch(cuda, half):
 
 
 def test_bn_backward_sums_in_dgrad_epilogue_match_reduction(cuda):
-    """BatchNorm-backward sums taken in the identity-block conv1 data-gradient epilogue (ops.nn.BnStatLink,
-    gemm_short.hip EPI 3 / 4: single residual BN at K = 64 / 128, the downsample block's two BNs at K = 64) against the
-    BatchNorms' own reduction sweeps (ops.nn.BN_BSTATS off), whole model: same loss, every gradient within fp32
-    summation-order noise, and the fused path taken. (64 x 64 images at batch 4: the forward is deterministic -- at
-    224 x 224, or batch 16, two runs of the SAME path already differ by 30-40 % in the early layers' gradients: the
-    forward's atomically accumulated BatchNorm statistics flip bf16 roundings, and this net -- every BatchNorm gamma
-    drawn in [0.6, 1.4], bn3 included -- amplifies them.)"""
+    """BatchNorm-backward sums taken in the data-gradient epilogues (ops.nn.BnStatLink: the residual BNs in the
+    identity-block conv1 dgrad, gemm_short.hip EPI 3 / 4; the on-load bn2 in conv3's tile-kernel dgrad, gemm.hip BST)
+    against the BatchNorms' own reduction sweeps (ops.nn.BN_BSTATS off), whole model, both against the fp32 torch twin:
+    the fused path's error may not exceed the separate path's beyond summation-order noise. (Compared through the
+    reference, not to each other: in this net -- every BatchNorm gamma in [0.6, 1.4], bn3 included -- an fp32-ulp
+    difference deep in the backward grows to ~5 % at the stem's bn1 bias by the time it gets there.)"""
     from k8s_amd.models.resnet import ResNet
+    from k8s_amd.models.resnet_ref import reference_grads
     from k8s_amd.ops import conv as kc
 
     def run(on):
@@ -275,25 +275,28 @@ def test_bn_backward_sums_in_dgrad_epilogue_match_reduction(cuda):
             # batch 4: every conv's statistics replica gets one tile, so the forward is bitwise repeatable
             images = torch.randn(4, 64, 64, 3, generator=torch.Generator(device="cpu").manual_seed(1)).to(cuda)
             x = m.prepare_input(images.bfloat16())
+            x8 = m.prepare_input(images.bfloat16(), s2d=False)
             y = torch.arange(4, device=cuda) % 10
             n0 = kc.STATS["bn_bstats"]
             store.begin_step()
             loss = K.cross_entropy(m(x), y)
             loss.backward()
             store.zero_unwritten()
-            return loss.item(), {p.name: p.grad.float().clone() for p in store.params}, kc.STATS["bn_bstats"] - n0
+            n = kc.STATS["bn_bstats"] - n0
+            _, ref = reference_grads(m, store, x8, y)
+            err = {}
+            for p in store.params:
+                r = ref[p.name].float()
+                err[p.name] = (p.grad.float() - r).norm().item() / (r.norm().item() + 1e-6)
+            return loss.item(), err, n
         finally:
             K.BN_BSTATS = old
 
-    l1, g1, n1 = run(True)
-    l0, g0, n0 = run(False)
-    assert n0 == 0 and n1 >= 6, (n0, n1)  # s1b0 (dual), s1b1, s2b1 + the stage-1 bn2 sums in conv3's dgrad
-    assert abs(l1 - l0) < 1e-3 * max(1.0, abs(l0)), (l1, l0)
-    bad = []
-    for name, r in g0.items():
-        err = (g1[name] - r).norm().item() / (r.norm().item() + 1e-6)
-        if err > 1e-2:
-            bad.append((name, round(err, 4)))
+    l1, e1, n1 = run(True)
+    l0, e0, n0 = run(False)
+    assert n0 == 0 and n1 >= 6, (n0, n1)  # s1b0 (dual), s1b1, s2b1 + the stage-1/2 bn2 sums in conv3's dgrad
+    assert l1 == l0, (l1, l0)  # the forward is untouched (and deterministic at this size)
+    bad = [(k, round(e1[k], 4), round(e0[k], 4)) for k in e0 if e1[k] > 1.5 * e0[k] + 0.02]
     assert not bad, bad
 
 
