@@ -375,7 +375,7 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 // BST (lean only): the BatchNorm-backward sums epilogue of a data gradient (Epi::bb) instead of the statistics.
 template <class ASrc, class BSrc, int NBUF, int WM = 2, int WN = 2, bool LEAN = false, bool XEPI = false,
           bool F32S = false, int XF = 0, bool BST = false>
-__global__ void __launch_bounds__(GEMM_THREADS, (NBUF == 1 && !BST && (XF == 0 || (XF == 1 && WM == 2))) ? 3 : 2)
+__global__ void __launch_bounds__(GEMM_THREADS, (NBUF == 1 && (XF == 0 || (XF == 1 && WM == 2))) ? 3 : 2)
 gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XForm X) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
   constexpr int TA = BM * BK * 2, TB = BN * BK * 2;  // operand tile bytes
@@ -419,19 +419,23 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   // BST: this thread's BatchNorm-input chunks for the epilogue's fast path (chunk column c, rows row0 + i RSTEP),
-  // loaded before the K loop so their latency hides behind it (loaded in the epilogue it was exposed once per tile:
-  // +0.35 ms per ResNet-50 stage-1 call); 32 VGPRs, so the instantiation runs 2 blocks per CU
+  // the first XE of them loaded before the K loop so their latency hides behind it, the rest at the epilogue's start.
+  // All in the epilogue: the latency was exposed once per tile (+0.35 ms per ResNet-50 stage-1 call); all before the K
+  // loop (32 VGPRs): the single-buffer kernel fell to 2 blocks per CU and gained nothing; 2 of 8 rows (8 VGPRs) keep
+  // its 3 blocks per CU: +0.4 % ResNet-50 b3072 against the separate reduction (profiles/r06_notes.md)
   constexpr int XCPR = BN / 8, XRSTEP = GEMM_THREADS / XCPR, XR = BST ? BM / XRSTEP : 1;
+  constexpr int XE = BST ? (NBUF == 1 ? XR / 4 : XR) : 0;
   bf16x8_t bxr[XR];
-  if constexpr (BST) {
+  auto load_bxr = [&](int i0, int i1) {
     const int c = tid % XCPR, row0 = tid / XCPR, n = n0 + c * 8;
 #pragma unroll
-    for (int i = 0; i < XR; ++i) {
+    for (int i = i0; i < i1; ++i) {
       const int m = m0 + row0 + i * XRSTEP;
       bxr[i] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
       if (n < N && m < M) bxr[i] = *reinterpret_cast<const bf16x8_t*>(E.bb.x + (long)m * N + n);
     }
-  }
+  };
+  if constexpr (BST) load_bxr(0, XE);
 
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);  // provably wave-uniform for the M0 (LDS base) operand
   constexpr int RA = TA / (16 * GEMM_THREADS), RB = TB / (16 * GEMM_THREADS);
@@ -597,6 +601,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
 #pragma unroll
     for (int r = 0; r < 4; ++r) st_s[j][r] = st_q[j][r] = 0.f;
   if constexpr (LEAN) {
+    if constexpr (BST && XE < XR) load_bxr(XE, XR);
     // bias (fp32, added before the one bf16 rounding of the staged value): this lane's 4 columns of each j
     float bj[4][4];
 #pragma unroll
