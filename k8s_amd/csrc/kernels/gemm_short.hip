@@ -197,8 +197,11 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
   constexpr int NP = NB / 2, D = NBUF - 1, KO = TM / 8;  // column-block pairs; tiles ahead; copy-out rows / 8
 
   i32x4 abuf[NBUF][MB][KC];
-  i32x4 obuf[NBUF][EPI ? 2 : 1][EPI ? KO : 1];
-  uint32_t mbuf[NBUF][EPI >= 2 ? 2 : 1][EPI >= 2 ? KO : 1];
+  // the addend ring (EPI 1 / 2); with the BatchNorm sums (BST) the addend and its bits instead travel with x in the
+  // one-slot, a-tile-ahead buffers of load_bx (registers for the second BatchNorm's operand at K >= 128)
+  constexpr int AR = BST ? 1 : NBUF;
+  i32x4 obuf[AR][EPI ? 2 : 1][EPI ? KO : 1];
+  uint32_t mbuf[AR][EPI >= 2 ? 2 : 1][EPI >= 2 ? KO : 1];
   // BST: the BatchNorm input(s) and ReLU bits of the next tile, in the copy-out layout: one slot, loaded right after
   // a tile's stores (a whole tile period ahead of their use, in registers the A / addend ring does not hold)
   i32x4 xbuf[BST ? 2 : 1][BST ? KO : 1];
@@ -212,7 +215,7 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
       for (int kc = 0; kc < KC; ++kc) bload16(dst[mb][kc], base + mb * lda16 + kc * 64, ra);
   };
   auto load_add = [&](int slot, int t) __attribute__((always_inline)) {
-    if constexpr (EPI != 0) {
+    if constexpr (EPI != 0 && !BST) {
       const uint32_t base = (uint32_t)(gw * TM) * (uint32_t)(N * 2) + (uint32_t)t * rowC + lc;
 #pragma unroll
       for (int h = 0; h < 2; ++h)
@@ -236,6 +239,8 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int k = 0; k < KO; ++k) {
+          bload16(obuf[0][h][k], base + h * 128 + k * n8, radd);
+          mbuf[0][h][k] = __builtin_amdgcn_raw_buffer_load_b8(rmask, mrow + h * 8 + k * n8m, 0, 0);
           bload16(xbuf[h][k], base + h * 128 + k * n8, rbx);
           if constexpr (EPI == 4) bload16(x2buf[h][k], base + h * 128 + k * n8, rbx2);
           bbuf[h][k] = __builtin_amdgcn_raw_buffer_load_b8(rbm, mrow + h * 8 + k * n8m, 0, 0);
@@ -353,8 +358,8 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
         const int r = 8 * k + (lane >> 3), c = lane & 7;
         i32x4 o = *reinterpret_cast<const i32x4*>(stg + r * 128 + ((c ^ (r & 7)) << 4));
         if constexpr (EPI != 0) {  // one more bf16 rounding on top of the stored product (<= 1 ulp)
-          const i32x4 old = obuf[u][h][k];
-          const uint32_t keep = EPI >= 2 ? mbuf[u][h][k] : 0xFFu;
+          const i32x4 old = obuf[BST ? 0 : u][h][k];
+          const uint32_t keep = EPI >= 2 ? mbuf[BST ? 0 : u][h][k] : 0xFFu;
           float f[8];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -484,7 +489,8 @@ bool gemm_short_ok(int M, int N, int K, long lda, long ldc) {
 bool gemm_short_bnstats_ok(int M, int N, int K, bool dual) {
   const char* e = std::getenv("K8S_AMD_BN_BSTATS");
   if (e && e[0] == '0') return false;
-  return gemm_short_ok(M, N, K, K, N) && (!dual || K == 64);
+  // two BatchNorms up to K = 128 (the addend travels in the one-slot buffers; at K = 256 the second one spills)
+  return gemm_short_ok(M, N, K, K, N) && (!dual || K <= 128);
 }
 
 // Rows per launch: every operand of one launch stays below 2 GiB (the kernel's 32-bit buffer offsets); larger
@@ -566,10 +572,15 @@ void launch_gemm_short(const uint16_t* A, const uint16_t* B, long ldb, bool b_mn
     else if (epi == 1)
       K8S_GSK_K(true, false, false, 1);
     else if (bst && bst->x2) {
-      // two BatchNorms' sums fit the register budget at K = 64 only (gemm_short_bnstats_ok)
-      if (K != 64) throw std::runtime_error("gemm_short: two-BatchNorm statistics need K = 64");
-      K8S_GSK(64, true, false, false, 4);
-    } else if (bst)
+      // two BatchNorms' sums fit the register budget up to K = 128 (gemm_short_bnstats_ok)
+      if (K == 64)
+        K8S_GSK(64, true, false, false, 4);
+      else if (K == 128)
+        K8S_GSK(128, true, false, false, 4);
+      else
+        throw std::runtime_error("gemm_short: two-BatchNorm statistics need K <= 128");
+    }
+    else if (bst)
       K8S_GSK_K(true, false, false, 3);
     else
       K8S_GSK_K(true, false, false, 2);

@@ -1,0 +1,11 @@
+#!/bin/bash
+# GPU job (round 6): BN-sums gemm_short epilogue with the addend in the one-slot buffers (dual BN now at K = 128 too)
+# -- tests, then a same-box bench A/B against the separate reductions of the residual BNs.
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r6_bsdual; rm -rf $O; mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gemm_conv_gpu.py -k "bnstats or masked" > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_resnet_gpu.py > $O/tests2.log 2>&1 || { tail -40 $O/tests2.log; exit 1; }
+tail -2 $O/tests2.log
+bash scripts/gpurun/r6/envab.sh r6_bsdual_ab 3 3072 "on:X=1" "off:K8S_AMD_BN_BSTATS=0"

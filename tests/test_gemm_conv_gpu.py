@@ -562,6 +562,7 @@ def test_downsample_1x1_stride2_subsampled(cuda, arm, monkeypatch):
 
 
 @pytest.mark.parametrize("M,K,N,dual,rows", [(3000, 64, 256, False, 0), (3000, 64, 256, True, 0),
+                                             (2056, 128, 512, True, 0),
                                              (2056, 128, 512, False, 0), (1000, 256, 1024, False, 0),
                                              # row-chunked launches (the stage-1 form at batch >= 2048)
                                              (3000, 64, 256, True, 1024), (2056, 128, 512, False, 512)])
