@@ -264,7 +264,8 @@ __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(const uint16_t* __
                                                               const float* __restrict__ params,
                                                               const float* __restrict__ rparams,
                                                               uint16_t* __restrict__ y, uint8_t* __restrict__ mask,
-                                                              int nvec, int C, FastDiv fcg, int relu, int rev) {
+                                                              int nvec, int C, FastDiv fcg, int relu, int rev,
+                                                              uint16_t* __restrict__ ysub, FastDiv fW, FastDiv fH) {
   const int e = bn_block_order(blockIdx.x, gridDim.x, rev) * BN_THREADS + threadIdx.x;
   if (e >= nvec) return;
   const int cgroups = C >> 3;
@@ -296,6 +297,14 @@ __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(const uint16_t* __
   const bf16x8_t ov = pack_bf16x8(v);
   *reinterpret_cast<bf16x8_t*>(y + (long)e * 8) = ov;
   if (mask) mask[e] = relu_bits(ov);
+  if (ysub) {  // the stride-2 subsample of y (the next block's downsample-convolution input) written in the same pass
+    const int pix = fcg.div(e), r = fW.div(pix), w = pix - r * (int)fW.d, n = fH.div(r), h = r - n * (int)fH.d;
+    if (((h | w) & 1) == 0) {
+      const int Ho = ((int)fH.d + 1) >> 1, Wo = ((int)fW.d + 1) >> 1;
+      const long q = (((long)n * Ho + (h >> 1)) * Wo + (w >> 1)) * cgroups + (e - pix * cgroups);
+      *reinterpret_cast<bf16x8_t*>(ysub + q * 8) = ov;
+    }
+  }
 }
 
 // Eval mode: the affine pair from the running statistics.
@@ -844,12 +853,14 @@ int bn_workspace_floats(long M, int C) {
 }
 
 static void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* params, uint16_t* y, uint8_t* mask,
-                            long M, int C, bool relu, hipStream_t st, const float* rparams = nullptr) {
+                            long M, int C, bool relu, hipStream_t st, const float* rparams = nullptr,
+                            uint16_t* ysub = nullptr, int H = 1, int W = 1) {
   const long nvec = M * C / 8;
   if (nvec >= (1L << 31)) throw std::runtime_error("BatchNorm tensor too large (>= 2^31 vectors)");
+  if (ysub && (M % ((long)H * W) != 0)) throw std::runtime_error("bn_apply subsample: M must be N * H * W");
   hipLaunchKernelGGL(bn_apply_kernel, dim3(cdiv(nvec, BN_THREADS)), dim3(BN_THREADS), 0, st, x, res, params, rparams,
                      y, mask, (int)nvec, C, make_fastdiv(C / 8), (int)relu,
-                     stream_order_mode() ? (stream_dir(1) ? 1 : 2) : 0);
+                     stream_order_mode() ? (stream_dir(1) ? 1 : 2) : 0, ysub, make_fastdiv(W), make_fastdiv(H));
 }
 
 void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta, uint16_t* y,
@@ -874,10 +885,10 @@ void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, c
 void launch_bn_fwd_from_sums(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
                              uint16_t* y, const float* sums, int nrep, float* save_mean, float* save_invstd,
                              float* run_mean, float* run_var, float* params, long M, int C, float eps, float momentum,
-                             bool relu, hipStream_t st, uint8_t* mask) {
+                             bool relu, hipStream_t st, uint8_t* mask, uint16_t* ysub, int H, int W) {
   hipLaunchKernelGGL(bn_finalize_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, nrep, C, (float)M, eps,
                      momentum, save_mean, save_invstd, run_mean, run_var, gamma, beta, params);
-  launch_bn_apply(x, res, params, y, mask, M, C, relu, st);
+  launch_bn_apply(x, res, params, y, mask, M, C, relu, st, nullptr, ysub, H, W);
 }
 
 // y = relu(BN(x) + BN_r(xr)), both BatchNorms' statistics from their convs' epilogue sums (a ResNet downsample

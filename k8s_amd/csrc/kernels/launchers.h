@@ -33,7 +33,8 @@ void launch_bn_fwd(const uint16_t* x, const uint16_t* res, const float* gamma, c
 void launch_bn_fwd_from_sums(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
                              uint16_t* y, const float* sums, int nrep, float* save_mean, float* save_invstd,
                              float* run_mean, float* run_var, float* params, long M, int C, float eps, float momentum,
-                             bool relu, hipStream_t st, uint8_t* mask = nullptr);
+                             bool relu, hipStream_t st, uint8_t* mask = nullptr, uint16_t* ysub = nullptr,
+                             int H = 1, int W = 1);
 void launch_bn_fwd_from_sums_dual(const uint16_t* x, const float* gamma, const float* beta, const float* sums,
                                   int nrep, float* save_mean, float* save_invstd, float* run_mean, float* run_var,
                                   float* params, const uint16_t* xr, const float* gamma_r, const float* beta_r,

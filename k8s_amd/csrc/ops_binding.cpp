@@ -167,7 +167,7 @@ std::vector<Tensor> bn_fwd(Tensor x, c10::optional<Tensor> res, Tensor gamma, Te
 
 std::vector<Tensor> bn_fwd_from_sums(Tensor x, c10::optional<Tensor> res, Tensor gamma, Tensor beta, Tensor sums,
                                      Tensor run_mean, Tensor run_var, double momentum, double eps, bool relu,
-                                     bool want_mask) {
+                                     bool want_mask, bool want_sub2) {
   check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x"); check_aligned(x, "x");
   const int C = (int)x.size(-1);
   TORCH_CHECK(C % 8 == 0, "channels must be a multiple of 8");
@@ -180,12 +180,24 @@ std::vector<Tensor> bn_fwd_from_sums(Tensor x, c10::optional<Tensor> res, Tensor
   auto invstd = torch::empty({C}, gamma.options());
   auto params = torch::empty({2 * C}, gamma.options());
   Tensor mask = relu_mask_for(x, want_mask);
+  // want_sub2: also y[:, ::2, ::2, :] (the next block's downsample input), written by the same pass
+  Tensor ysub;
+  int H = 1, W = 1;
+  if (want_sub2) {
+    TORCH_CHECK(x.dim() == 4 && x.is_contiguous(), "want_sub2: contiguous NHWC x");
+    H = (int)x.size(1);
+    W = (int)x.size(2);
+    ysub = torch::empty({x.size(0), (H + 1) / 2, (W + 1) / 2, C}, x.options());
+  }
   k8s_amd::launch_bn_fwd_from_sums(cbf(x), res ? cbf(*res) : nullptr, f32(gamma), f32(beta), bf(y), f32(sums),
                                    nrep, f32(mean), f32(invstd), f32(run_mean), f32(run_var), f32(params), M, C,
                                    (float)eps, (float)momentum, relu, cur_stream(),
-                                   want_mask ? mask.data_ptr<uint8_t>() : nullptr);
-  if (want_mask) return {y, mean, invstd, mask};
-  return {y, mean, invstd};
+                                   want_mask ? mask.data_ptr<uint8_t>() : nullptr, want_sub2 ? bf(ysub) : nullptr, H,
+                                   W);
+  std::vector<Tensor> out = {y, mean, invstd};
+  if (want_mask) out.push_back(mask);
+  if (want_sub2) out.push_back(ysub);
+  return out;
 }
 
 // y = relu(BN(x) + BN_r(xr)) with both BatchNorms' statistics from conv epilogue sums (ResNet downsample block:
@@ -1374,7 +1386,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mask") = py::none());
   m.def("bn_fwd_from_sums", &bn_fwd_from_sums, py::arg("x"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
         py::arg("sums"), py::arg("run_mean"), py::arg("run_var"), py::arg("momentum"), py::arg("eps"),
-        py::arg("relu"), py::arg("want_mask") = false);
+        py::arg("relu"), py::arg("want_mask") = false, py::arg("want_sub2") = false);
   m.def("norm_fwd", &norm_fwd);
   m.def("norm_bwd", &norm_bwd, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
         py::arg("dres"), py::arg("dgamma"), py::arg("dbeta"), py::arg("rms"), py::arg("dsum") = py::none());

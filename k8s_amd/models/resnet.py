@@ -31,13 +31,13 @@ class BN(nn.Module):
         self.register_buffer("running_var", torch.ones(c))
         self.momentum, self.eps = 0.1, 1e-5
 
-    def forward(self, x, residual=None, relu=True, res_link=None, dy_link=None):
+    def forward(self, x, residual=None, relu=True, res_link=None, dy_link=None, sub2=False):
         sums = None
         if isinstance(x, tuple):  # (conv output, fused statistics)
             x, sums = x
         return K.batch_norm_act(x, self.gamma, self.beta, self.running_mean, self.running_var, residual, relu,
                                 self.training, self.momentum, self.eps, sums=sums, res_link=res_link,
-                                dy_link=dy_link)
+                                dy_link=dy_link, sub2=sub2)
 
 
 class Conv(nn.Module):
@@ -68,7 +68,9 @@ class Bottleneck(nn.Module):
             self.down = Conv(store, name + ".downsample.0", cin, cout, 1, stride)
             self.down_bn = BN(store, name + ".downsample.1", cout)
 
-    def forward(self, x):
+    def forward(self, x, sub2=False):
+        """``sub2``: the next block is a stride-2 downsample block -- bn3's apply pass also writes y[:, ::2, ::2]
+        for its downsample convolution (ops.nn.SubLink)."""
         idn = x
         identity = self.down is None and x.requires_grad
         # identity block: x's two gradient contributions (residual via bn3, main path via conv1) are summed
@@ -98,7 +100,7 @@ class Bottleneck(nn.Module):
             if y is not None:
                 return y
             idn = self.down_bn(dn, relu=False, dy_link=mlink)
-        return self.bn3(t, residual=idn, relu=True, res_link=link or mlink)
+        return self.bn3(t, residual=idn, relu=True, res_link=link or mlink, sub2=sub2)
 
 
 class ResNet(nn.Module):
@@ -154,8 +156,9 @@ class ResNet(nn.Module):
             t = self.conv1(x)
         # bn1 + ReLU + 3x3/s2 max pool: one fused pass each way on the GPU (the 112x112 BN output is never stored)
         y = K.bn_relu_maxpool(t, self.bn1)
-        for b in self.blocks:
-            y = b(y)
+        for i, b in enumerate(self.blocks):
+            nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
+            y = b(y, sub2=nxt is not None and nxt.down is not None and nxt.down.stride == 2)
         y = K.global_avg_pool_nhwc(y)
         return K.linear(y, self.fc_w, self.fc_b)
 

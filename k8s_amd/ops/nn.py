@@ -165,7 +165,9 @@ class _Conv2dNHWC(torch.autograd.Function):
                 _C().conv_stat_replicas, 2, w.shape[0])
         xs = None
         if impl.subsample_ok(x, w, stride, padding):  # 1x1 / stride 2: a stride-1 GEMM on the subsampled input
-            xs = _C().subsample_nhwc(x, stride)
+            xs = getattr(x, "_k8s_sub2", None) if stride == 2 else None  # written by x's BatchNorm (SubLink)
+            if xs is None or xs.shape[:3] != ((x.shape[0], (x.shape[1] + 1) // 2, (x.shape[2] + 1) // 2)):
+                xs = _C().subsample_nhwc(x, stride)
             y = impl.conv_fwd(xs, w, 1, 0, sums)
         else:
             y = impl.conv_fwd(x, w, stride, padding, sums)
@@ -270,7 +272,7 @@ def stem_s2d_input(images, pad: int = 3):
 class _BnAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu, sums=None,
-                res_link=None, dy_link=None, stat_link=None):
+                res_link=None, dy_link=None, stat_link=None, sub2=None):
         x = x.contiguous()
         if res is not None:
             res = res.contiguous()
@@ -278,9 +280,12 @@ class _BnAct(torch.autograd.Function):
         # backward's reduce and apply passes read instead of the bf16 output (saves ~2 B/elem per pass)
         want_mask = relu and res is not None and _gpu(x)
         mask = None
+        want_sub = sub2 is not None and x.dim() == 4
         if _gpu(x) and sums is not None and training:
             out = _C().bn_fwd_from_sums(x, res, pg.master, pb.master, sums, run_mean, run_var, momentum, eps, relu,
-                                        want_mask)
+                                        want_mask, want_sub)
+            if want_sub:  # y[:, ::2, ::2] for the next block's downsample convolution (SubLink)
+                sub2.y = out[-1]
         elif _gpu(x):
             out = _C().bn_fwd(x, res, pg.master, pb.master, run_mean, run_var, training, momentum, eps, relu,
                               want_mask)
@@ -348,7 +353,7 @@ class _BnAct(torch.autograd.Function):
         if ctx.has_res and isinstance(ctx.res_link, GradLink):  # hand dres to the node that adds it in a kernel
             ctx.res_link.grad, dres = dres, None
         return (dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None, None,
-                None, None)
+                None, None, None)
 
 
 # Which BatchNorm + ReLU outputs of a ResNet bottleneck are normalised on load by the convolution that consumes them
@@ -463,8 +468,23 @@ def bn_relu_conv(t, bn, conv):
     return conv(bn(t))
 
 
+# BatchNorm apply passes write the stride-2 subsample for a following downsample block (SubLink);
+# K8S_AMD_SUB2_FUSED=0: the separate subsample pass (A/B)
+SUB2_FUSED = os.environ.get("K8S_AMD_SUB2_FUSED", "1") != "0"
+
+
+class SubLink:
+    """The stride-2 subsample of a BatchNorm output, written by the BatchNorm's own apply pass (bn_apply_kernel) when
+    the next ResNet block is a downsample block: its 1x1 / stride-2 downsample convolution (run as a stride-1 GEMM on
+    the subsampled input, ops.conv.SUB1X1) then takes it instead of a separate subsample pass over the tensor."""
+    __slots__ = ("y",)
+
+    def __init__(self):
+        self.y = None
+
+
 def batch_norm_act(x, pg, pb, run_mean, run_var, residual=None, relu=True, training=True, momentum=0.1,
-                   eps=1e-5, sums=None, res_link=None, dy_link=None):
+                   eps=1e-5, sums=None, res_link=None, dy_link=None, sub2=False):
     """y = act(BN(x) + residual) over the last (channel) dim of an NHWC tensor.
 
     ``sums`` (fp32 [2, C] from ``conv2d_nhwc(..., with_stats=True)``) skips the statistics pass.
@@ -472,10 +492,13 @@ def batch_norm_act(x, pg, pb, run_mean, run_var, residual=None, relu=True, train
     node consuming the link must add it (``conv2d_nhwc(..., grad_link=link)`` on the same tensor).
     ``res_link`` may also be a MaskLink whose ``dy_link`` end is the plain BN that produced ``residual``."""
     link = BnStatLink() if (BN_BSTATS and relu and training and _gpu(x)) else None
+    sub = SubLink() if (sub2 and SUB2_FUSED and sums is not None and _gpu(x)) else None
     y = _BnAct.apply(x, residual, pg.store.anchor, pg, pb, run_mean, run_var, training, momentum, eps, relu,
-                     sums, res_link, dy_link, link)
+                     sums, res_link, dy_link, link, sub)
     if link is not None and link.x is not None:
         y._k8s_bnstat = link
+    if sub is not None and sub.y is not None:
+        y._k8s_sub2 = sub.y
     return y
 
 

@@ -351,3 +351,35 @@ def test_bn_backward_sums_bottleneck_3x3_and_residual(cuda, H, cin, width):
         if err > 1e-2:
             bad.append((name, round(err, 4)))
     assert not bad, bad
+
+
+def test_fused_subsample_matches_separate_pass(cuda):
+    """bn3's apply pass writing y[:, ::2, ::2] for the next (downsample) block (ops.nn.SubLink) against the separate
+    subsample pass: bitwise the same loss and gradients (the same bf16 values reach the downsample convolution), and
+    the fused tensor actually used."""
+    from k8s_amd.models.resnet import ResNet
+
+    def run(fused):
+        old = K.SUB2_FUSED
+        K.SUB2_FUSED = fused
+        try:
+            torch.manual_seed(0)
+            store = ParamStore()
+            m = ResNet(store, (2, 2, 2, 1), 10, width=64).finalize(cuda, seed=3)
+            m.train()
+            images = torch.randn(4, 64, 64, 3, generator=torch.Generator(device="cpu").manual_seed(1)).to(cuda)
+            x = m.prepare_input(images.bfloat16())
+            y = torch.arange(4, device=cuda) % 10
+            store.begin_step()
+            loss = K.cross_entropy(m(x), y)
+            loss.backward()
+            store.zero_unwritten()
+            return loss.item(), {p.name: p.grad.float().clone() for p in store.params}
+        finally:
+            K.SUB2_FUSED = old
+
+    l1, g1 = run(True)
+    l0, g0 = run(False)
+    assert l1 == l0
+    for name, r in g0.items():
+        assert torch.equal(g1[name], r), name
