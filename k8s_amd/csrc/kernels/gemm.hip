@@ -435,7 +435,9 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
       if (n < N && m < M) bxr[i] = *reinterpret_cast<const bf16x8_t*>(E.bb.x + (long)m * N + n);
     }
   };
-  if constexpr (BST) load_bxr(0, XE);
+  if constexpr (BST) {
+    if (!E.bb.mask) load_bxr(0, XE);  // (the relu-kind fast path; the mask-kind sub-grid correction reads x itself)
+  }
 
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);  // provably wave-uniform for the M0 (LDS base) operand
   constexpr int RA = TA / (16 * GEMM_THREADS), RB = TB / (16 * GEMM_THREADS);
@@ -601,7 +603,9 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
 #pragma unroll
     for (int r = 0; r < 4; ++r) st_s[j][r] = st_q[j][r] = 0.f;
   if constexpr (LEAN) {
-    if constexpr (BST && XE < XR) load_bxr(XE, XR);
+    if constexpr (BST && XE < XR) {
+      if (!E.bb.mask) load_bxr(XE, XR);
+    }
     // bias (fp32, added before the one bf16 rounding of the staged value): this lane's 4 columns of each j
     float bj[4][4];
 #pragma unroll
@@ -727,7 +731,16 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
           pq[2 * r + 1] = q2[r][1];
         }
       }
-    } else
+    } else {
+    // BST on the row-remapped (sub-grid) path: the correction of a residual BatchNorm's backward sums (packed ReLU
+    // bits bb.mask) for the elements this accumulating product changes -- sum bit (new - old), sum bit (new - old)
+    // (x - mean) -- the first data gradient into the same tensor having counted the old values (ops.conv)
+    float gmu[BST ? 8 : 1];
+    if constexpr (BST) {
+      const int nt = n0 + (tid % CPR) * 8;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) gmu[r] = nt + r < N ? E.bb.mean[nt + r] : 0.f;
+    }
 #pragma unroll 2
     for (int q = tid; q < CHUNKS; q += GEMM_THREADS) {
       const int row = q / CPR, c = q % CPR;
@@ -764,9 +777,19 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
         }
 #pragma unroll
         for (int r = 0; r < 8; ++r) o[r] = (short)f2bf(bf2f((uint16_t)o[r]) + bf2f((uint16_t)old[r]));
+        if constexpr (BST) {
+          const bf16x8_t xv = *reinterpret_cast<const bf16x8_t*>(E.bb.x + aoff);
+          const uint32_t bits = E.bb.mask[aoff >> 3];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const float d = ((bits >> r) & 1u) ? bf2f((uint16_t)o[r]) - bf2f((uint16_t)old[r]) : 0.f;
+            ps[r] += d;
+            pq[r] = __builtin_fmaf(d, bf2f((uint16_t)xv[r]) - gmu[r], pq[r]);
+          }
+        }
       }
       *reinterpret_cast<bf16x8_t*>(cp) = o;
-      if (stat_out) {
+      if (!BST && stat_out) {  // (BST: stat_out is the BatchNorm sums, corrected above)
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           const float v = bf2f((uint16_t)o[r]);
@@ -774,6 +797,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
           pq[r] += v * v;
         }
       }
+    }
     }
     if (stat_out) {
       // partials [GEMM_THREADS][16] in LDS, then thread (which, col) sums the GEMM_THREADS / CPR partials of its
@@ -1032,6 +1056,12 @@ static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int 
         return;
       }
     }
+    if constexpr (std::is_same_v<ASrc, KMajor> && std::is_same_v<BSrc, KMajor> && WM == 2 && WN == 2) {
+      if (lean_epi(e, N, false) && e.mode == 1 && !e.stats && e.rst && !e.addsrc && splits == 1 && e.bb.mask) {
+        launch_tiles2<ASrc, BSrc, WM, WN, true, false, false, 0, true>(a, b, e, M, N, K, kps, splits, st);
+        return;
+      }
+    }
     throw std::runtime_error("BatchNorm-backward sums epilogue: a plain bf16 data gradient (K-major dy, MN-major w)");
   }
   // the linear forward (both operands K-major) is the one pair with a bias / activation epilogue instantiation
@@ -1203,7 +1233,10 @@ void launch_gemm_dgrad_bnstats(const uint16_t* A, const uint16_t* B, uint16_t* C
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int K,
                      int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
                      int mode, float* stats, hipStream_t st, const SubGrid* sg,
-                     const float* xform) {
+                     const float* xform, const BnBwdSums* bb) {
+  if (bb && (!sg || mode != 1 || R != 1 || S != 1 || stride != 1 || pad != 0 || y_f32 || stats || xform || !bb->mask ||
+             !bb->x || !bb->mean || !bb->sums))
+    throw std::runtime_error("conv: BatchNorm-sum corrections only on an accumulating 1x1 sub-grid data gradient");
   if (!sg && !y_f32 && !bias && act == 0 && mode == 0 && conv3x3_eligible(H, W, C, K, R, S, stride, pad, dil)) {
     launch_conv3x3(x, w, reinterpret_cast<uint16_t*>(y), stats, xform, N, H, W, C, K, st);  // staged window
     return;
@@ -1212,6 +1245,7 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, 
   KMajor b{w, (long)RSC, K, RSC};
   Epi e = make_epi(y, K, y_f32, bias, act, nullptr, mode, 1.f);
   e.stats = stats;
+  if (bb) e.bb = *bb;
   if (sg) {
     if (stats) throw std::runtime_error("sub-grid output takes no statistics epilogue");
     e.rst = sg->stride;

@@ -66,7 +66,9 @@ struct Args {
 
 // A-fragment ring depth (tiles in flight incl. the one being computed), tile rows and waves per SIMD: sized so the
 // ring fits beside the accumulators, the statistics and (EPI > 0) the addend in 256 registers (2 waves per SIMD)
-// EPI: 0 plain store, 1 accumulate onto C, 2 + a masked addend, 3 = 2 + the BatchNorm-backward statistics of the
+// EPI: 0 plain store, 1 accumulate onto C, 2 + a masked addend, 5 = 0 + the BatchNorm-backward statistics of the
+// stored result (one BatchNorm: the first of two data gradients into a ResNet stage-entry input, see ops.conv),
+// 3 = 2 + the BatchNorm-backward statistics of the
 // stored result (one BatchNorm), 4 = 3 for two BatchNorms fed by the same masked gradient
 template <int K, int EPI, bool XF, bool STATS>
 struct Cfg {
@@ -130,6 +132,7 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
   constexpr int XBYTES = XF ? KC * 4 * 64 : 0;
   constexpr int SBYTES = TM * 128;  // per-wave staging of half a bf16 output tile (64 columns; the copy-out)
   constexpr bool BST = EPI >= 3;
+  constexpr bool ADD = EPI >= 2 && EPI <= 4;  // a masked addend
   constexpr int NS = EPI == 4 ? 3 : 2;  // BatchNorm-backward sums: g, g (x - mean) [, g (x2 - mean2)]
   constexpr int MBYTES = BST ? (NS - 1) * BN * 4 : 0;
   constexpr int STG = (WBYTES + XBYTES + MBYTES + 1023) / 1024 * 1024;
@@ -180,8 +183,8 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
   const int nt = gw < MT ? (MT - gw + WG - 1) / WG : 0;
   const __amdgpu_buffer_rsrc_t ra = rsrc(g.A, (uint32_t)((long)g.M * g.lda * 2));
   const __amdgpu_buffer_rsrc_t rc = rsrc(g.C, (uint32_t)((long)g.M * N * 2));
-  const __amdgpu_buffer_rsrc_t radd = EPI >= 2 ? rsrc(g.add, (uint32_t)((long)g.M * N * 2)) : rc;
-  const __amdgpu_buffer_rsrc_t rmask = EPI >= 2 ? rsrc(g.mask, (uint32_t)((long)g.M * N / 8)) : rc;
+  const __amdgpu_buffer_rsrc_t radd = ADD ? rsrc(g.add, (uint32_t)((long)g.M * N * 2)) : rc;
+  const __amdgpu_buffer_rsrc_t rmask = ADD ? rsrc(g.mask, (uint32_t)((long)g.M * N / 8)) : rc;
   const __amdgpu_buffer_rsrc_t rbx = BST ? rsrc(g.bx, (uint32_t)((long)g.M * N * 2)) : rc;
   const __amdgpu_buffer_rsrc_t rbx2 = EPI == 4 ? rsrc(g.bx2, (uint32_t)((long)g.M * N * 2)) : rc;
   const __amdgpu_buffer_rsrc_t rbm = BST ? rsrc(g.bmask, (uint32_t)((long)g.M * N / 8)) : rc;
@@ -200,8 +203,8 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
   // the addend ring (EPI 1 / 2); with the BatchNorm sums (BST) the addend and its bits instead travel with x in the
   // one-slot, a-tile-ahead buffers of load_bx (registers for the second BatchNorm's operand at K >= 128)
   constexpr int AR = BST ? 1 : NBUF;
-  i32x4 obuf[AR][EPI ? 2 : 1][EPI ? KO : 1];
-  uint32_t mbuf[AR][EPI >= 2 ? 2 : 1][EPI >= 2 ? KO : 1];
+  i32x4 obuf[AR][EPI == 1 || ADD ? 2 : 1][EPI == 1 || ADD ? KO : 1];
+  uint32_t mbuf[AR][ADD ? 2 : 1][ADD ? KO : 1];
   // BST: the BatchNorm input(s) and ReLU bits of the next tile, in the copy-out layout: one slot, loaded right after
   // a tile's stores (a whole tile period ahead of their use, in registers the A / addend ring does not hold)
   i32x4 xbuf[BST ? 2 : 1][BST ? KO : 1];
@@ -221,7 +224,7 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int k = 0; k < KO; ++k) bload16(obuf[slot][h][k], base + h * 128 + k * n8, EPI >= 2 ? radd : rc);
-      if constexpr (EPI >= 2) {
+      if constexpr (ADD) {
         const uint32_t mrow = (uint32_t)(gw * TM) * (uint32_t)(N / 8) + (uint32_t)t * rowM + lm;
 #pragma unroll
         for (int h = 0; h < 2; ++h)
@@ -239,8 +242,10 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int k = 0; k < KO; ++k) {
-          bload16(obuf[0][h][k], base + h * 128 + k * n8, radd);
-          mbuf[0][h][k] = __builtin_amdgcn_raw_buffer_load_b8(rmask, mrow + h * 8 + k * n8m, 0, 0);
+          if constexpr (ADD) {
+            bload16(obuf[0][h][k], base + h * 128 + k * n8, radd);
+            mbuf[0][h][k] = __builtin_amdgcn_raw_buffer_load_b8(rmask, mrow + h * 8 + k * n8m, 0, 0);
+          }
           bload16(xbuf[h][k], base + h * 128 + k * n8, rbx);
           if constexpr (EPI == 4) bload16(x2buf[h][k], base + h * 128 + k * n8, rbx2);
           bbuf[h][k] = __builtin_amdgcn_raw_buffer_load_b8(rbm, mrow + h * 8 + k * n8m, 0, 0);
@@ -357,9 +362,9 @@ __global__ __launch_bounds__(THREADS, (Cfg<K, EPI, XF, STATS>::OCC)) void gemm_s
       for (int k = 0; k < KO; ++k) {
         const int r = 8 * k + (lane >> 3), c = lane & 7;
         i32x4 o = *reinterpret_cast<const i32x4*>(stg + r * 128 + ((c ^ (r & 7)) << 4));
-        if constexpr (EPI != 0) {  // one more bf16 rounding on top of the stored product (<= 1 ulp)
+        if constexpr (EPI == 1 || ADD) {  // one more bf16 rounding on top of the stored product (<= 1 ulp)
           const i32x4 old = obuf[BST ? 0 : u][h][k];
-          const uint32_t keep = EPI >= 2 ? mbuf[BST ? 0 : u][h][k] : 0xFFu;
+          const uint32_t keep = ADD ? mbuf[BST ? 0 : u][h][k] : 0xFFu;
           float f[8];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -532,9 +537,9 @@ void launch_gemm_short(const uint16_t* A, const uint16_t* B, long ldb, bool b_mn
   }
   if ((epi == 2) != (add != nullptr) || (epi == 2 && !mask)) throw std::runtime_error("gemm_short: bad addend");
   if (epi != 0 && stats) throw std::runtime_error("gemm_short: statistics only with a plain store");
-  if (bst && (epi != 2 || !b_mn || !bst->x || !bst->mask || !bst->mean || !bst->sums ||
-              (bst->x2 && (!bst->mean2 || !bst->sums2))))
-    throw std::runtime_error("gemm_short: BatchNorm-backward statistics need the masked-addend data gradient");
+  if (bst && ((epi != 2 && epi != 0) || !b_mn || !bst->x || !bst->mask || !bst->mean || !bst->sums ||
+              (bst->x2 && (epi != 2 || !bst->mean2 || !bst->sums2))))
+    throw std::runtime_error("gemm_short: BatchNorm-backward statistics need a plain or masked-addend data gradient");
   gsk::Args g{A, B, C, add, mask, xf, stats,
               bst ? bst->x : nullptr, bst ? bst->x2 : nullptr, bst ? bst->mask : nullptr,
               bst ? bst->mean : nullptr, bst ? bst->mean2 : nullptr, bst ? bst->sums : nullptr,
@@ -567,7 +572,9 @@ void launch_gemm_short(const uint16_t* A, const uint16_t* B, long ldb, bool b_mn
       K8S_GSK_K(false, false, false, 0);
   } else {  // the data gradient: plain, accumulating, or with a masked addend
     if (xf || stats) throw std::runtime_error("gemm_short: MN-major B takes no statistics / normalisation");
-    if (epi == 0)
+    if (epi == 0 && bst)
+      K8S_GSK_K(true, false, false, 5);
+    else if (epi == 0)
       K8S_GSK_K(true, false, false, 0);
     else if (epi == 1)
       K8S_GSK_K(true, false, false, 1);

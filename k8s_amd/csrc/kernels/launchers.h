@@ -111,6 +111,9 @@ struct BnBwdSums {
   const float* mean = nullptr;
   const float* invstd = nullptr;
   float* sums = nullptr;
+  // mask kind (a residual BatchNorm's packed ReLU bits instead of the affine ReLU decision): the row-remapped
+  // accumulating data gradient's correction (gemm.hip BST sub-grid path); gamma / beta / invstd unused
+  const uint8_t* mask = nullptr;
 };
 struct GemmShortBnStats {
   const uint16_t* x = nullptr;
@@ -186,7 +189,8 @@ struct SubGrid {
 };
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int K,
                      int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
-                     int mode, float* stats, hipStream_t st, const SubGrid* sg = nullptr, const float* xform = nullptr);
+                     int mode, float* stats, hipStream_t st, const SubGrid* sg = nullptr, const float* xform = nullptr,
+                     const BnBwdSums* bb = nullptr);
 // xform (here and in launch_gemm / launch_wgrad_stream): fp32 [2][C] BatchNorm (scale | shift): the activation
 // operand x is consumed as relu(x * scale + shift), normalised as it is loaded (gemm.hip XForm)
 void launch_conv_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int C, int K, int R,

@@ -485,9 +485,14 @@ Tensor mask_apply(Tensor src, Tensor mask) {
 // EPI 3 / 4): sums[r][0][c] += sum g, sums[r][1][c] += sum g (x - mean), g = bit ? dx : 0 with the BatchNorm's packed
 // ReLU bits `mask`; with x2 (a ResNet downsample block's second BatchNorm) sums2[r][1][c] += sum g (x2 - mean2).
 // sums / sums2: zeroed fp32 [conv_stat_replicas, 2, N].
-Tensor dgrad_short_bnstats(Tensor gy, Tensor w, Tensor add_src, Tensor add_mask, Tensor x, Tensor mask, Tensor mean,
-                           Tensor sums, c10::optional<Tensor> x2, c10::optional<Tensor> mean2,
-                           c10::optional<Tensor> sums2) {
+Tensor dgrad_short_bnstats(Tensor gy, Tensor w, c10::optional<Tensor> add_opt, c10::optional<Tensor> add_mask_opt,
+                           Tensor x, Tensor mask, Tensor mean, Tensor sums, c10::optional<Tensor> x2,
+                           c10::optional<Tensor> mean2, c10::optional<Tensor> sums2) {
+  // no addend (add_src None): the plain data gradient + the sums (EPI 5), one BatchNorm only
+  const bool has_add = add_opt.has_value();
+  TORCH_CHECK(has_add == add_mask_opt.has_value() && (has_add || !x2), "add_src / add_mask together; x2 needs them");
+  Tensor add_src = has_add ? *add_opt : x;
+  Tensor add_mask = has_add ? *add_mask_opt : mask;
   for (const Tensor* t : {&gy, &w, &add_src, &x}) {
     check_cuda(*t, "gy / w / add_src / x");
     check_dtype(*t, at::kBFloat16, "gy / w / add_src / x");
@@ -525,8 +530,9 @@ Tensor dgrad_short_bnstats(Tensor gy, Tensor w, Tensor add_src, Tensor add_mask,
     b.sums2 = f32(*sums2);
   }
   Tensor out = torch::empty({M, N}, gy.options());
-  k8s_amd::launch_gemm_short(cbf(gy), cbf(w), N, true, bf(out), cbf(add_src), add_mask.data_ptr<uint8_t>(), nullptr,
-                             nullptr, (int)M, (int)N, (int)K, 2, cur_stream(), &b);
+  k8s_amd::launch_gemm_short(cbf(gy), cbf(w), N, true, bf(out), has_add ? cbf(add_src) : nullptr,
+                             has_add ? add_mask.data_ptr<uint8_t>() : nullptr, nullptr, nullptr, (int)M, (int)N,
+                             (int)K, has_add ? 2 : 0, cur_stream(), &b);
   return out;
 }
 
@@ -913,7 +919,8 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, bo
 // out[n, i*stride + a, j*stride + b, :] (+)= conv(x, w)[n, i, j, :]: one output parity of a strided dgrad;
 // `accumulate` adds onto out in the epilogue (out already holds the residual branch's gradient).
 void conv_fwd_subgrid(Tensor x, Tensor w, int64_t pad, int64_t Hs, int64_t Ws, Tensor out, int64_t stride, int64_t a,
-                      int64_t b, bool accumulate) {
+                      int64_t b, bool accumulate, c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_mask,
+                      c10::optional<Tensor> bn_mean, c10::optional<Tensor> bn_sums) {
   check_cuda(x, "x"); check_cuda(w, "w"); check_cuda(out, "out");
   check_dtype(x, at::kBFloat16, "x"); check_dtype(w, at::kBFloat16, "w"); check_dtype(out, at::kBFloat16, "out");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && out.dim() == 4 && out.is_contiguous());
@@ -926,8 +933,25 @@ void conv_fwd_subgrid(Tensor x, Tensor w, int64_t pad, int64_t Hs, int64_t Ws, T
   TORCH_CHECK(Hs >= 1 && Ws >= 1 && (Hs - 1) * stride + a < OH && (Ws - 1) * stride + b < OW,
               "sub-grid exceeds the output image");
   k8s_amd::SubGrid sg{OH, OW, (int)stride, (int)a, (int)b};
+  // bn_*: the correction of a residual BatchNorm's backward sums for the elements this accumulating product changes
+  // (gemm.hip BST sub-grid path; the first data gradient into `out` took the sums over its values)
+  k8s_amd::BnBwdSums bb;
+  if (bn_sums) {
+    TORCH_CHECK(bn_x && bn_mask && bn_mean && accumulate, "bn correction: bn_x, bn_mask, bn_mean and accumulate");
+    check_dtype(*bn_x, at::kBFloat16, "bn_x");
+    TORCH_CHECK(bn_x->sizes() == out.sizes() && bn_x->is_contiguous(), "bn_x: the shape of out");
+    TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() * 8 == out.numel(), "bn_mask: packed bits");
+    TORCH_CHECK(bn_mean->numel() == K && bn_mean->scalar_type() == at::kFloat, "bn_mean: fp32 [K]");
+    TORCH_CHECK(bn_sums->numel() == (long)k8s_amd::kConvStatReplicas * 2 * K && bn_sums->scalar_type() == at::kFloat,
+                "bn_sums: fp32 [conv_stat_replicas, 2, K]");
+    bb.x = cbf(*bn_x);
+    bb.mask = bn_mask->data_ptr<uint8_t>();
+    bb.mean = f32(*bn_mean);
+    bb.sums = f32(*bn_sums);
+  }
   k8s_amd::launch_conv_fwd(cbf(x), cbf(w), out.data_ptr(), false, N, H, W, C, K, R, S, 1, (int)pad, 1, (int)Hs,
-                           (int)Ws, nullptr, 0, accumulate ? 1 : 0, nullptr, cur_stream(), &sg);
+                           (int)Ws, nullptr, 0, accumulate ? 1 : 0, nullptr, cur_stream(), &sg, nullptr,
+                           bn_sums ? &bb : nullptr);
 }
 
 // dw[K,R,S,C] fp32 (+)= dy^T . im2col(x)
@@ -1458,7 +1482,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
         py::arg("dil"), py::arg("splits"), py::arg("accumulate"), py::arg("xform") = py::none());
   m.def("conv_fwd_subgrid", &conv_fwd_subgrid, py::arg("x"), py::arg("w"), py::arg("pad"), py::arg("Hs"),
-        py::arg("Ws"), py::arg("out"), py::arg("stride"), py::arg("a"), py::arg("b"), py::arg("accumulate") = false);
+        py::arg("Ws"), py::arg("out"), py::arg("stride"), py::arg("a"), py::arg("b"), py::arg("accumulate") = false,
+        py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none(),
+        py::arg("bn_sums") = py::none());
   m.def("conv_dgrad_wtrans", &conv_dgrad_wtrans);
   m.def("conv_dgrad_wsub", &conv_dgrad_wsub);
   m.def("flash_fwd", &flash_fwd);

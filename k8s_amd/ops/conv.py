@@ -123,6 +123,8 @@ def _wgrad_hip(C_, gy, x, out, stride, padding, acc, xform=None):
 # staged-window kernel and the 1x1 tile kernel (K8S_AMD_BN_BSTATS_3X3 / _GEMM = 0 for the A/B)
 BSTATS_3X3 = os.environ.get("K8S_AMD_BN_BSTATS_3X3", "1") != "0"
 BSTATS_GEMM = os.environ.get("K8S_AMD_BN_BSTATS_GEMM", "1") != "0"
+# a stage-entry block's residual BN: sums over conv1's dgrad completed by the downsample's strided dgrad
+BSTATS_ENTRY = os.environ.get("K8S_AMD_BN_BSTATS_ENTRY", "1") != "0"
 
 
 def _bn_sums(C_, bn_link, C, device):
@@ -173,6 +175,17 @@ def _dgrad_hip(C_, gy, w, padding, addend=None, bn_link=None):
             bn_link.sums, bn_link.sums2, bn_link.dy_key = sums, None, (out.data_ptr(), tuple(out.shape))
             STATS["bn_bstats"] += 1
             return out
+        if (BSTATS_ENTRY and addend is None and bn_link is not None and not bn_link.relu and bn_link.mask is not None
+                and bn_link.x2 is None and bn_link.x is not None and bn_link.x.shape == (N, H, W_, C)
+                and C_.gemm_short_bnstats_ok(N * H * W_, C, K, False)):
+            # the first of two data gradients into a residual BN's output (a stage-entry block's conv1): the sums
+            # over its values, completed by the downsample's strided dgrad (_dgrad_strided_hip)
+            sums = _bn_sums(C_, bn_link, C, gy.device)
+            out = C_.dgrad_short_bnstats(gy.reshape(-1, K), w.reshape(K, C), None, None, bn_link.x.view(-1, C),
+                                         bn_link.mask, bn_link.mean, sums).view(N, H, W_, C)
+            bn_link.sums, bn_link.sums2, bn_link.dy_key, bn_link.pending = sums, None, None, True
+            STATS["bn_bstats"] += 1
+            return out
         if masked:  # the epilogue reads dy and the mask bits itself: no materialised residual gradient
             out = torch.empty(N, H, W_, C, device=gy.device, dtype=gy.dtype)
             C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, out.view(-1, C), False, None, 0, None, True,
@@ -213,7 +226,7 @@ def strided_dgrad_ok(gy, w, stride, padding):
     return True
 
 
-def _dgrad_strided_hip(C_, gy, w, stride, padding, H, W, addend=None):
+def _dgrad_strided_hip(C_, gy, w, stride, padding, H, W, addend=None, bn_link=None):
     """dx [N, H, W, C] of a stride-s conv on our implicit-GEMM kernel, one launch per output parity.
 
     With ``addend`` (bf16 [N, H, W, C], e.g. the gradient the block input already got from the other branch)
@@ -221,6 +234,13 @@ def _dgrad_strided_hip(C_, gy, w, stride, padding, H, W, addend=None):
     tap reaches (they keep the addend) and no separate add pass."""
     K, R, S, C = w.shape
     N = gy.shape[0]
+    # completing a residual BN's backward sums started by the first data gradient into `addend` (nn.BnStatLink
+    # pending): the live parity's epilogue adds the changes it makes (gemm.hip BST sub-grid path)
+    fix = (bn_link is not None and bn_link.pending and R == 1 and S == 1 and padding == 0 and addend is not None
+           and torch.is_tensor(addend) and addend.is_contiguous() and bn_link.x is not None
+           and bn_link.x.shape == addend.shape)
+    if bn_link is not None and bn_link.pending and not fix:
+        bn_link.sums, bn_link.pending = None, False  # cannot complete: the BN takes its own reduction
     parities = [(a, b) for a in range(stride) for b in range(stride)]
     empty = [(a, b) for a, b in parities
              if not _parity_taps(R, a, padding, stride) or not _parity_taps(S, b, padding, stride)]
@@ -240,7 +260,13 @@ def _dgrad_strided_hip(C_, gy, w, stride, padding, H, W, addend=None):
         n = C * len(tr) * len(ts) * K
         wsub = packed[offs[i]:offs[i] + n].view(C, len(tr), len(ts), K)
         Hs, Ws = (H - a + stride - 1) // stride, (W - b + stride - 1) // stride
-        C_.conv_fwd_subgrid(gy, wsub, -tr[0][0], Hs, Ws, dx, stride, a, b, addend is not None)
+        if fix:
+            C_.conv_fwd_subgrid(gy, wsub, -tr[0][0], Hs, Ws, dx, stride, a, b, True, bn_link.x, bn_link.mask,
+                                bn_link.mean, bn_link.sums)
+        else:
+            C_.conv_fwd_subgrid(gy, wsub, -tr[0][0], Hs, Ws, dx, stride, a, b, addend is not None)
+    if fix:
+        bn_link.dy_key, bn_link.pending = (dx.data_ptr(), tuple(dx.shape)), False
     return dx
 
 
@@ -283,7 +309,7 @@ def conv_bwd(gy, x, w, stride, padding, need_dx, p=None, addend=None, xform=None
             dx = _dgrad_hip(C_, gy, w, padding, addend, bn_link)
         elif hip and strided_dgrad_ok(gy, w, stride, padding):
             STATS["hip_dgrad"] += 1
-            dx = _dgrad_strided_hip(C_, gy, w, stride, padding, x.shape[1], x.shape[2], addend)
+            dx = _dgrad_strided_hip(C_, gy, w, stride, padding, x.shape[1], x.shape[2], addend, bn_link)
         else:
             _vendor("dgrad", x, w, stride, padding)
             dx, _ = _aten_bwd(gy, x, w, stride, padding, True, False)

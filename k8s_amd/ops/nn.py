@@ -119,7 +119,7 @@ class BnStatLink:
     identity of the dy they were taken over; the BatchNorm's backward uses them only when it receives exactly that dy
     (so a second consumer of y, whose gradient autograd would add, falls back to the reduction)."""
     __slots__ = ("x", "mask", "mean", "x2", "mean2", "invstd", "gamma", "beta", "relu", "sums", "sums2", "dy_key",
-                 "store")
+                 "store", "pending")
 
     def __init__(self, store=None):
         self.store = store  # the BatchNorm's ParamStore: its per-step zeroed scratch holds the sums
@@ -127,6 +127,9 @@ class BnStatLink:
         self.invstd = self.gamma = self.beta = None
         self.relu = False  # a non-residual BatchNorm + ReLU (mask None: g = relu_on(x) ? dy : 0, from the affine)
         self.sums = self.sums2 = self.dy_key = None
+        # sums over the first of two data gradients into y (a stage-entry block's conv1), awaiting the second's
+        # correction (its downsample convolution, ops.conv._dgrad_strided_hip); dy_key is set only once complete
+        self.pending = False
 
     def take(self, dy):
         """(sums, sums2) if they were taken over ``dy``, else None; clears the deposit either way."""
@@ -192,7 +195,8 @@ class _Conv2dNHWC(torch.autograd.Function):
         if ctx.link is not None:
             addend, ctx.link.grad = ctx.link.grad, None
             if addend is None and ctx.link.shared and ctx.x_requires_grad:  # first of the two readers of x
-                ctx.link.grad = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, True, p, x_sub=xs)
+                ctx.link.grad = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, True, p, x_sub=xs,
+                                              bn_link=ctx.bn_link)
                 return None, None, None, None, None, None, None, None
         dx = impl.conv_bwd(gy, x, w, ctx.stride, ctx.padding, ctx.x_requires_grad, p, addend=addend, x_sub=xs,
                            bn_link=ctx.bn_link)
@@ -207,7 +211,7 @@ def conv2d_nhwc(x: torch.Tensor, p, stride: int = 1, padding: int = 0, with_stat
     accumulated in the conv epilogue (None when the layer runs on the fallback path) -- the following
     ``batch_norm_act(..., sums=sums)`` then needs no statistics pass. ``grad_link``: a gradient for x
     deposited there by a later-backward node (``batch_norm_act(res_link=...)``) is added to dx in the dgrad."""
-    bn_link = getattr(x, "_k8s_bnstat", None) if (grad_link is None or not grad_link.shared) else None
+    bn_link = getattr(x, "_k8s_bnstat", None)
     y, sums = _Conv2dNHWC.apply(x, p.store.anchor, p, stride, padding, with_stats, grad_link, bn_link)
     return (y, sums) if with_stats else y
 

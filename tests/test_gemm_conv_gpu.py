@@ -678,3 +678,40 @@ def test_gemm_dgrad_bnstats_epilogue(cuda, M, K, N):
     tot = sums.sum(0)
     assert _rel(tot[0], g.sum(0)) < 1e-3
     assert _rel(tot[1], (g * (x.float() - mean)).sum(0)) < 1e-3
+
+
+@pytest.mark.parametrize("N,H,K1,C,K2", [(4, 16, 128, 256, 512), (2, 14, 256, 512, 1024)])
+def test_stage_entry_bn_sums_two_dgrads(cuda, N, H, K1, C, K2):
+    """A residual BN's backward sums over the sum of two data gradients into its output (a ResNet stage-entry block:
+    conv1's 1x1 dgrad, then the downsample's 1x1 / stride-2 dgrad accumulated onto it): the first takes the sums over
+    its values (gemm_short EPI 5), the second adds the changes it makes at its parity (gemm.hip BST sub-grid path).
+    Against fp32 sums over the final tensor with the BN's packed ReLU bits."""
+    from k8s_amd.ops import conv as kc
+    from k8s_amd.ops import nn as K
+
+    C_ = _C()
+    torch.manual_seed(15)
+    M = N * H * H
+    gy = torch.randn(M, K1, device=cuda).bfloat16()
+    w1 = (torch.randn(K1, C, device=cuda) * 0.05).bfloat16()
+    x = (torch.randn(N, H, H, C, device=cuda) * 1.5 + 0.2).bfloat16()
+    mask = torch.randint(0, 256, (M * C // 8,), device=cuda, dtype=torch.uint8)
+    mean = torch.randn(C, device=cuda) * 0.2
+    link = K.BnStatLink()
+    link.x, link.mask, link.mean = x, mask, mean
+    sums = torch.zeros(C_.conv_stat_replicas, 2, C, device=cuda)
+    out = C_.dgrad_short_bnstats(gy, w1, None, None, x.view(-1, C), mask, mean, sums).view(N, H, H, C)
+    plain = C_.gemm(gy, True, w1, False, None, False, None, 0, None, False, 1.0, 1)
+    assert torch.equal(out.view(-1, C), plain)
+    link.sums, link.pending = sums, True
+    dy2 = torch.randn(N, H // 2, H // 2, K2, device=cuda).bfloat16()
+    w2 = (torch.randn(K2, 1, 1, C, device=cuda) * 0.05).bfloat16()
+    dx = kc._dgrad_strided_hip(C_, dy2, w2, 2, 0, H, H, out, link)
+    assert dx.data_ptr() == out.data_ptr() and not link.pending and link.dy_key == (dx.data_ptr(), tuple(dx.shape))
+    ref_dx = plain.float().view(N, H, H, C).clone()
+    ref_dx[:, ::2, ::2, :] += (dy2.float().reshape(-1, K2) @ w2.float().reshape(K2, C)).view(N, H // 2, H // 2, C)
+    assert _rel(dx, ref_dx) < 1e-2
+    g = torch.where(_unpack_bits(mask, (M, C)), dx.float().view(-1, C), torch.zeros(M, C, device=cuda))
+    tot = sums.sum(0)
+    assert _rel(tot[0], g.sum(0)) < 1e-3
+    assert _rel(tot[1], (g * (x.float().view(-1, C) - mean)).sum(0)) < 1e-3

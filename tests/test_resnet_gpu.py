@@ -294,7 +294,8 @@ def test_bn_backward_sums_in_dgrad_epilogue_match_reduction(cuda):
 
     l1, e1, n1 = run(True)
     l0, e0, n0 = run(False)
-    assert n0 == 0 and n1 >= 6, (n0, n1)  # s1b0 (dual), s1b1, s2b1 + the stage-1/2 bn2 sums in conv3's dgrad
+    # s1b0 (dual), s1b1, s2b1, the stage-1/2 bn2 sums in conv3's dgrad, the s1b2 / s2b2 outputs' two-dgrad sums
+    assert n0 == 0 and n1 >= 8, (n0, n1)
     assert l1 == l0, (l1, l0)  # the forward is untouched (and deterministic at this size)
     bad = [(k, round(e1[k], 4), round(e0[k], 4)) for k in e0 if e1[k] > 1.5 * e0[k] + 0.02]
     assert not bad, bad
