@@ -614,7 +614,8 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_dual_kernel(
 // write z, read z; backward 2 reads of x + the dx write instead of writing dz and reading it twice with x.
 __global__ void __launch_bounds__(BN_THREADS) bn_relu_maxpool_fwd_kernel(
     const uint16_t* __restrict__ x, const float* __restrict__ params, uint16_t* __restrict__ y,
-    uint8_t* __restrict__ idx, int H, int W, int C, int Ho, int Wo, int total, FastDiv fcv, FastDiv fWo, FastDiv fHo) {
+    uint8_t* __restrict__ idx, int H, int W, int C, int Ho, int Wo, int total, FastDiv fcv, FastDiv fWo, FastDiv fHo,
+    uint16_t* __restrict__ xarg, uint8_t* __restrict__ ybits) {
   const int e = blockIdx.x * BN_THREADS + threadIdx.x;
   if (e >= total) return;
   const int cv = C >> 3;
@@ -638,6 +639,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_relu_maxpool_fwd_kernel(
     }
   float best[8];
   uint32_t arg[8];
+  bf16x8_t bx = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};  // the winner's x (xarg)
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     best[j] = -INFINITY;
@@ -654,6 +656,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_relu_maxpool_fwd_kernel(
         if (z > best[j] || (z != z && best[j] == best[j])) {
           best[j] = z;
           arg[j] = (uint32_t)(dh * 3 + dw);
+          bx[j] = v[dh * 3 + dw][j];
         }
       }
     }
@@ -662,6 +665,15 @@ __global__ void __launch_bounds__(BN_THREADS) bn_relu_maxpool_fwd_kernel(
 #pragma unroll
   for (int j = 0; j < 8; ++j) packed |= (uint64_t)arg[j] << (8 * j);
   *reinterpret_cast<uint64_t*>(idx + (long)e * 8) = packed;
+  // for the BatchNorm-backward sums in the consuming data gradients' epilogues (nn.BnStatLink): per pooled element
+  // the winner's x and whether its ReLU passed (y > 0) -- g = bit ? dpool : 0 routes to exactly that x
+  if (xarg) {
+    *reinterpret_cast<bf16x8_t*>(xarg + (long)e * 8) = bx;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bits |= (best[j] > 0.f ? 1u : 0u) << j;
+    ybits[e] = (uint8_t)bits;
+  }
 }
 
 // dz of the 4 pixels of input cell (n, kc, jc), channels c .. c+7: the max-pool gradient (bf16-rounded)
@@ -1009,7 +1021,7 @@ void launch_bn_bwd_dual(const uint16_t* dy, const uint8_t* mask, const uint16_t*
 void launch_bn_relu_maxpool_fwd(const uint16_t* x, const float* gamma, const float* beta, const float* sums, int nrep,
                                 float* save_mean, float* save_invstd, float* run_mean, float* run_var, float* params,
                                 uint16_t* y, uint8_t* idx, int N, int H, int W, int C, float eps, float momentum,
-                                hipStream_t st) {
+                                hipStream_t st, uint16_t* xarg, uint8_t* ybits) {
   const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;  // (H + 2 - 3) / 2 + 1
   const long total = (long)N * Ho * Wo * (C / 8);
   if ((long)N * H * W * C / 8 >= (1L << 31)) throw std::runtime_error("bn_relu_maxpool: tensor too large");
@@ -1017,7 +1029,8 @@ void launch_bn_relu_maxpool_fwd(const uint16_t* x, const float* gamma, const flo
                      (float)((long)N * H * W), eps, momentum, save_mean, save_invstd, run_mean, run_var, gamma, beta,
                      params);
   hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel, dim3(cdiv(total, BN_THREADS)), dim3(BN_THREADS), 0, st, x, params,
-                     y, idx, H, W, C, Ho, Wo, (int)total, make_fastdiv(C / 8), make_fastdiv(Wo), make_fastdiv(Ho));
+                     y, idx, H, W, C, Ho, Wo, (int)total, make_fastdiv(C / 8), make_fastdiv(Wo), make_fastdiv(Ho),
+                     xarg, ybits);
 }
 
 int pool_bn_workspace_floats(int C) { return 4096 * C * 2; }
@@ -1037,6 +1050,24 @@ void launch_pool_bn_bwd(const uint16_t* dpool, const uint8_t* idx, const uint16_
                      make_fastdiv(Hc));
   hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, FIN_CH)), dim3(256), 0, st, work, (int)nb, C, dgamma, dbeta,
                      1.f / (float)((long)N * H * W), mean, invstd, gamma, beta, params);
+  const long total = ncells * (C / 8);
+  hipLaunchKernelGGL(pool_bn_bwd_apply_kernel, dim3(cdiv(total, BN_THREADS)), dim3(BN_THREADS), 0, st, dpool, idx, x,
+                     params, dx, H, W, C, Ho, Wo, (int)total, make_fastdiv(C / 8), make_fastdiv(Wc),
+                     make_fastdiv(Hc));
+}
+
+// launch_pool_bn_bwd with the sums taken by the data gradients into the pooled output (the winner's x and ReLU bit
+// per pooled element, bn_relu_maxpool_fwd_kernel's xarg / ybits): the final and apply passes only
+void launch_pool_bn_bwd_from_sums(const uint16_t* dpool, const uint8_t* idx, const uint16_t* x, const float* mean,
+                                  const float* invstd, const float* gamma, const float* beta, uint16_t* dx,
+                                  float* dgamma, float* dbeta, const float* sums, int nrep, float* params, int N,
+                                  int H, int W, int C, hipStream_t st) {
+  if (C % 8 || BN_THREADS % (C / 8)) throw std::runtime_error("pool_bn_bwd: C / 8 must divide 256");
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2, Hc = (H + 1) / 2, Wc = (W + 1) / 2;
+  const long ncells = (long)N * Hc * Wc;
+  if (ncells * (C / 8) >= (1L << 31)) throw std::runtime_error("pool_bn_bwd: tensor too large");
+  hipLaunchKernelGGL(bn_bwd_final_sums_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, sums, nrep, C, dgamma,
+                     dbeta, 1.f / (float)((long)N * H * W), mean, invstd, gamma, beta, params);
   const long total = ncells * (C / 8);
   hipLaunchKernelGGL(pool_bn_bwd_apply_kernel, dim3(cdiv(total, BN_THREADS)), dim3(BN_THREADS), 0, st, dpool, idx, x,
                      params, dx, H, W, C, Ho, Wo, (int)total, make_fastdiv(C / 8), make_fastdiv(Wc),

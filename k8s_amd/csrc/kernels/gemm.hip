@@ -436,7 +436,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
     }
   };
   if constexpr (BST) {
-    if (!E.bb.mask) load_bxr(0, XE);  // (the relu-kind fast path; the mask-kind sub-grid correction reads x itself)
+    if (!E.rst) load_bxr(0, XE);  // (the identity-row fast path; the sub-grid correction reads x itself)
   }
 
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);  // provably wave-uniform for the M0 (LDS base) operand
@@ -604,7 +604,7 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
     for (int r = 0; r < 4; ++r) st_s[j][r] = st_q[j][r] = 0.f;
   if constexpr (LEAN) {
     if constexpr (BST && XE < XR) {
-      if (!E.bb.mask) load_bxr(XE, XR);
+      if (!E.rst) load_bxr(XE, XR);
     }
     // bias (fp32, added before the one bf16 rounding of the staged value): this lane's 4 columns of each j
     float bj[4][4];
@@ -664,27 +664,40 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
 #pragma unroll
         for (int r = 0; r < 4; ++r) s2[r] = q2[r] = f32x2_t{0.f, 0.f};
         // BST: this thread's 8 columns' ReLU affine (the forward's, recomputed bit-identically) and means; x walks
-        // with the output (ldc == N)
+        // with the output (ldc == N). Mask kind (bb.mask, a BatchNorm whose ReLU bits are stored: the stem pool's
+        // output): g = bit ? dx : 0, and the product may accumulate onto C (an unmasked addend: the first of two
+        // data gradients into the same tensor)
         float bsc[BST ? 8 : 1], bsh[BST ? 8 : 1], bmu[BST ? 8 : 1];
         if constexpr (BST) {
+          const bool mk = E.bb.mask != nullptr;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             bmu[j] = E.bb.mean[n + j];
-            bn_affine_regs(E.bb.gamma[n + j], E.bb.beta[n + j], bmu[j], E.bb.invstd[n + j], bsc[j], bsh[j]);
+            bsc[j] = bsh[j] = 0.f;
+            if (!mk) bn_affine_regs(E.bb.gamma[n + j], E.bb.beta[n + j], bmu[j], E.bb.invstd[n + j], bsc[j], bsh[j]);
           }
 #pragma unroll
           for (int i = 0; i < XR; ++i) {  // whole tile, unrolled: the prefetched x registers indexed statically
             const int row = row0 + i * RSTEP;
             if (m0 + row < M) {
-              const bf16x8_t o = *reinterpret_cast<const bf16x8_t*>(lp + i * RSTEP * BN + ((c ^ (row % CPR)) << 3));
+              bf16x8_t o = *reinterpret_cast<const bf16x8_t*>(lp + i * RSTEP * BN + ((c ^ (row % CPR)) << 3));
+              if (ap) {  // (the general path's rounding: the staged bf16 value + old C, one more rounding)
+                const bf16x8_t old = *reinterpret_cast<const bf16x8_t*>(ap + (long)i * RSTEP * ldc);
+                float f[8];
+#pragma unroll
+                for (int r = 0; r < 8; ++r) f[r] = bf2f((uint16_t)o[r]) + bf2f((uint16_t)old[r]);
+                o = pack_bf16x8(f);
+              }
               *reinterpret_cast<bf16x8_t*>(cp + (long)i * RSTEP * ldc) = o;
+              const uint32_t bits = mk ? (uint32_t)E.bb.mask[(off0 + (long)i * RSTEP * ldc) >> 3] : 0u;
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 f32x2_t g, d;
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                   const float xf = bf2f((uint16_t)bxr[i][2 * r + e]);
-                  g[e] = relu_on(xf, bsc[2 * r + e], bsh[2 * r + e]) ? bf2f((uint16_t)o[2 * r + e]) : 0.f;
+                  const bool on = mk ? ((bits >> (2 * r + e)) & 1u) != 0 : relu_on(xf, bsc[2 * r + e], bsh[2 * r + e]);
+                  g[e] = on ? bf2f((uint16_t)o[2 * r + e]) : 0.f;
                   d[e] = xf - bmu[2 * r + e];
                 }
                 s2[r] += g;
@@ -1051,7 +1064,8 @@ static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int 
   // a data gradient (K-major dy, MN-major w) with the BatchNorm-backward sums of its output
   if (e.bb.sums) {
     if constexpr (std::is_same_v<ASrc, KMajor> && std::is_same_v<BSrc, MNMajorK> && WM == 2 && WN == 2) {
-      if (lean_epi(e, N, false) && e.mode == 0 && !e.stats && !e.rst && !e.addsrc && splits == 1 && e.ldc == N) {
+      if (lean_epi(e, N, false) && (e.mode == 0 || (e.mode == 1 && e.bb.mask)) && !e.stats && !e.rst && !e.addsrc &&
+          !e.addmask && splits == 1 && e.ldc == N) {
         launch_tiles2<ASrc, BSrc, WM, WN, true, false, false, 0, true>(a, b, e, M, N, K, kps, splits, st);
         return;
       }
@@ -1220,10 +1234,12 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
 // dx[M, N] = dy[M, K] . w[K, N] (bf16, the 1x1 data gradient) on the tile kernel with the BatchNorm-backward sums
 // of dx for the relu(BN(x)) that produced the convolution's input (Epi::bb, BST instantiation).
 void launch_gemm_dgrad_bnstats(const uint16_t* A, const uint16_t* B, uint16_t* C, int M, int N, int K,
-                               const BnBwdSums& bb, hipStream_t st) {
-  if (!bb.sums || !bb.x || !bb.gamma || !bb.beta || !bb.mean || !bb.invstd || N % 8)
-    throw std::runtime_error("gemm dgrad BatchNorm-backward sums: x / gamma / beta / mean / invstd / sums, N % 8 == 0");
-  Epi e = make_epi(C, N, false, nullptr, 0, nullptr, 0, 1.f);
+                               const BnBwdSums& bb, hipStream_t st, bool accumulate) {
+  // relu kind: x / gamma / beta / mean / invstd; mask kind (bb.mask): x / mean, and C may be accumulated onto
+  if (!bb.sums || !bb.x || !bb.mean || N % 8 || (!bb.mask && (!bb.gamma || !bb.beta || !bb.invstd || accumulate)))
+    throw std::runtime_error("gemm dgrad BatchNorm-backward sums: x / mean / sums (+ gamma / beta / invstd without a "
+                             "mask; accumulate only with one), N % 8 == 0");
+  Epi e = make_epi(C, N, false, nullptr, 0, nullptr, accumulate ? 1 : 0, 1.f);
   e.bb = bb;
   launch(KMajor{A, (long)K, M, K}, MNMajorK{B, (long)N, N, K}, e, M, N, K, 1, st);
 }

@@ -128,7 +128,7 @@ void launch_gemm_short(const uint16_t* A, const uint16_t* B, long ldb, bool b_mn
                        const uint8_t* mask, const float* xf, float* stats, int M, int N, int K, int epi,
                        hipStream_t st, const GemmShortBnStats* bst = nullptr);
 void launch_gemm_dgrad_bnstats(const uint16_t* A, const uint16_t* B, uint16_t* C, int M, int N, int K,
-                               const BnBwdSums& bb, hipStream_t st);
+                               const BnBwdSums& bb, hipStream_t st, bool accumulate = false);
 void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                  long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
                  float alpha, int splits, float* ws, hipStream_t st, const AddEpi* add = nullptr,
@@ -269,7 +269,11 @@ bool flash_bwd_one_block(int D, int Sq, int Sk, int Hq, int Hkv, int dkv_split);
 void launch_bn_relu_maxpool_fwd(const uint16_t* x, const float* gamma, const float* beta, const float* sums, int nrep,
                                 float* save_mean, float* save_invstd, float* run_mean, float* run_var, float* params,
                                 uint16_t* y, uint8_t* idx, int N, int H, int W, int C, float eps, float momentum,
-                                hipStream_t st);
+                                hipStream_t st, uint16_t* xarg = nullptr, uint8_t* ybits = nullptr);
+void launch_pool_bn_bwd_from_sums(const uint16_t* dpool, const uint8_t* idx, const uint16_t* x, const float* mean,
+                                  const float* invstd, const float* gamma, const float* beta, uint16_t* dx,
+                                  float* dgamma, float* dbeta, const float* sums, int nrep, float* params, int N,
+                                  int H, int W, int C, hipStream_t st);
 int pool_bn_workspace_floats(int C);
 void launch_pool_bn_bwd(const uint16_t* dpool, const uint8_t* idx, const uint16_t* x, const float* mean,
                         const float* invstd, const float* gamma, const float* beta, uint16_t* dx, float* dgamma,

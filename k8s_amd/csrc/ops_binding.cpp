@@ -249,9 +249,10 @@ std::vector<Tensor> bn_finalize(Tensor sums, Tensor gamma, Tensor beta, Tensor r
 }
 
 // ResNet stem: BatchNorm (statistics from the conv epilogue sums) + ReLU + 3x3 / s2 / p1 max pool in one pass; the
-// BN output is never stored. Returns (pooled y, winner idx, mean, invstd).
+// BN output is never stored. Returns (pooled y, winner idx, mean, invstd); with `want_link` also (xarg, ybits): the
+// winner's x and packed ReLU bits per pooled element (the BatchNorm-backward sums in the consumers' dgrad epilogues).
 std::vector<Tensor> bn_relu_maxpool(Tensor x, Tensor sums, Tensor gamma, Tensor beta, Tensor run_mean, Tensor run_var,
-                                    double momentum, double eps) {
+                                    double momentum, double eps, bool want_link) {
   check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x");
   TORCH_CHECK(x.dim() == 4 && x.is_contiguous(), "x must be a contiguous NHWC tensor");
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
@@ -266,10 +267,41 @@ std::vector<Tensor> bn_relu_maxpool(Tensor x, Tensor sums, Tensor gamma, Tensor 
   auto mean = torch::empty({C}, gamma.options());
   auto invstd = torch::empty({C}, gamma.options());
   auto params = torch::empty({2 * C}, gamma.options());
+  Tensor xarg, ybits;
+  if (want_link) {
+    xarg = torch::empty({N, Ho, Wo, C}, x.options());
+    ybits = torch::empty({(long)N * Ho * Wo * C / 8}, x.options().dtype(at::kByte));
+  }
   k8s_amd::launch_bn_relu_maxpool_fwd(cbf(x), f32(gamma), f32(beta), f32(sums), (int)(sums.numel() / (2 * C)),
                                       f32(mean), f32(invstd), f32(run_mean), f32(run_var), f32(params), bf(y),
-                                      idx.data_ptr<uint8_t>(), N, H, W, C, (float)eps, (float)momentum, cur_stream());
+                                      idx.data_ptr<uint8_t>(), N, H, W, C, (float)eps, (float)momentum, cur_stream(),
+                                      want_link ? bf(xarg) : nullptr,
+                                      want_link ? ybits.data_ptr<uint8_t>() : nullptr);
+  if (want_link) return {y, idx, mean, invstd, xarg, ybits};
   return {y, idx, mean, invstd};
+}
+
+// pool_bn_bwd with the BatchNorm-backward sums already taken (fp32 [conv_stat_replicas, 2, C] over g = bit ? dpool :
+// 0 at the winners' x, by the data gradients into the pooled output): the final and apply passes only.
+Tensor pool_bn_bwd_from_sums(Tensor dpool, Tensor idx, Tensor x, Tensor mean, Tensor invstd, Tensor gamma,
+                             Tensor beta, Tensor dgamma, Tensor dbeta, Tensor sums) {
+  check_cuda(dpool, "dpool"); check_dtype(dpool, at::kBFloat16, "dpool");
+  check_cuda(x, "x"); check_dtype(x, at::kBFloat16, "x");
+  check_dtype(idx, at::kByte, "idx");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous() && dpool.is_contiguous() && idx.is_contiguous());
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(dpool.sizes() == idx.sizes() && dpool.size(0) == N && dpool.size(1) == (H + 1) / 2 &&
+                  dpool.size(2) == (W + 1) / 2 && dpool.size(3) == C, "dpool / idx shape mismatch");
+  TORCH_CHECK(dgamma.numel() == C && dbeta.numel() == C && dgamma.is_contiguous() && dbeta.is_contiguous());
+  check_dtype(dgamma, at::kFloat, "dgamma"); check_dtype(dbeta, at::kFloat, "dbeta");
+  TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kFloat && sums.is_contiguous() &&
+                  sums.numel() == (long)k8s_amd::kConvStatReplicas * 2 * C, "sums: fp32 [conv_stat_replicas, 2, C]");
+  auto dx = torch::empty_like(x);
+  auto params = torch::empty({4 * C}, gamma.options());
+  k8s_amd::launch_pool_bn_bwd_from_sums(cbf(dpool), idx.data_ptr<uint8_t>(), cbf(x), f32(mean), f32(invstd),
+                                        f32(gamma), f32(beta), bf(dx), f32(dgamma), f32(dbeta), f32(sums),
+                                        k8s_amd::kConvStatReplicas, f32(params), N, H, W, C, cur_stream());
+  return dx;
 }
 
 // Backward of bn_relu_maxpool: dx of the conv output; dgamma / dbeta written into the given fp32 tensors.
@@ -612,6 +644,33 @@ Tensor gemm_dgrad_bnstats(Tensor gy, Tensor w, Tensor x, Tensor gamma, Tensor be
   bb.invstd = f32(invstd);
   bb.sums = f32(sums);
   k8s_amd::launch_gemm_dgrad_bnstats(cbf(gy), cbf(w), bf(out), (int)M, (int)N, (int)K, bb, cur_stream());
+  return out;
+}
+
+// out[M, N] += gy[M, K] . w[K, N] on the tile kernel, also accumulating the BatchNorm-backward sums of the final out
+// for a BatchNorm whose ReLU bits are stored (mask kind: g = bit ? out : 0, sum g, sum g (x - mean)) -- the second
+// of two data gradients into that BatchNorm's output (the stem pool's, nn.BnStatLink.last_full). Returns out.
+Tensor gemm_dgrad_bnstats_mask(Tensor gy, Tensor w, Tensor out, Tensor x, Tensor mask, Tensor mean, Tensor sums) {
+  for (const Tensor* t : {&gy, &w, &out, &x}) {
+    check_cuda(*t, "gy / w / out / x");
+    check_dtype(*t, at::kBFloat16, "gy / w / out / x");
+    TORCH_CHECK(t->is_contiguous() && t->dim() == 2, "gy / w / out / x: contiguous 2-d");
+  }
+  const long M = gy.size(0), K = gy.size(1), N = w.size(1);
+  TORCH_CHECK(w.size(0) == K && x.size(0) == M && x.size(1) == N && out.sizes() == x.sizes(),
+              "shapes: gy [M, K], w [K, N], out / x [M, N]");
+  TORCH_CHECK(N % 8 == 0 && M < (1L << 31), "N % 8 == 0");
+  TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == at::kByte && mask.numel() * 8 == M * N, "mask: packed bits");
+  TORCH_CHECK(mean.is_cuda() && mean.numel() == N && mean.scalar_type() == at::kFloat, "mean: fp32 [N]");
+  TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kFloat && sums.is_contiguous() &&
+                  sums.numel() == (long)k8s_amd::kConvStatReplicas * 2 * N,
+              "sums: zeroed fp32 [conv_stat_replicas, 2, N]");
+  k8s_amd::BnBwdSums bb;
+  bb.x = cbf(x);
+  bb.mask = mask.data_ptr<uint8_t>();
+  bb.mean = f32(mean);
+  bb.sums = f32(sums);
+  k8s_amd::launch_gemm_dgrad_bnstats(cbf(gy), cbf(w), bf(out), (int)M, (int)N, (int)K, bb, cur_stream(), true);
   return out;
 }
 
@@ -1490,7 +1549,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_fwd", &flash_fwd);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("bn_relu_maxpool", &bn_relu_maxpool, py::arg("x"), py::arg("sums"), py::arg("gamma"), py::arg("beta"),
-        py::arg("run_mean"), py::arg("run_var"), py::arg("momentum"), py::arg("eps"));
+        py::arg("run_mean"), py::arg("run_var"), py::arg("momentum"), py::arg("eps"), py::arg("want_link") = false);
+  m.def("pool_bn_bwd_from_sums", &pool_bn_bwd_from_sums);
+  m.def("gemm_dgrad_bnstats_mask", &gemm_dgrad_bnstats_mask);
   m.def("pool_bn_bwd", &pool_bn_bwd, py::arg("dpool"), py::arg("idx"), py::arg("x"), py::arg("mean"),
         py::arg("invstd"), py::arg("gamma"), py::arg("beta"), py::arg("dgamma"), py::arg("dbeta"));
   m.def("embed_fwd", &embed_fwd);

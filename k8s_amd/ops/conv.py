@@ -175,7 +175,7 @@ def _dgrad_hip(C_, gy, w, padding, addend=None, bn_link=None):
             bn_link.sums, bn_link.sums2, bn_link.dy_key = sums, None, (out.data_ptr(), tuple(out.shape))
             STATS["bn_bstats"] += 1
             return out
-        if (BSTATS_ENTRY and addend is None and bn_link is not None and not bn_link.relu and bn_link.mask is not None
+        if (BSTATS_ENTRY and addend is None and bn_link is not None and not bn_link.relu and not bn_link.last_full and bn_link.mask is not None
                 and bn_link.x2 is None and bn_link.x is not None and bn_link.x.shape == (N, H, W_, C)
                 and C_.gemm_short_bnstats_ok(N * H * W_, C, K, False)):
             # the first of two data gradients into a residual BN's output (a stage-entry block's conv1): the sums
@@ -191,6 +191,17 @@ def _dgrad_hip(C_, gy, w, padding, addend=None, bn_link=None):
             C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, out.view(-1, C), False, None, 0, None, True,
                     1.0, 1, add_src=addend.dy.view(-1, C), add_mask=addend.mask)
             return out
+        if (addend is not None and bn_link is not None and bn_link.last_full and bn_link.x is not None
+                and bn_link.mask is not None and bn_link.x.shape == (N, H, W_, C) and addend.is_contiguous()
+                and C % 8 == 0 and N * H * W_ < 2 ** 31):
+            # the second of two data gradients into a BatchNorm's output (nn.BnStatLink.last_full: the stem pool's,
+            # 64 channels, the tile kernel): accumulated onto the first's, the sums taken over the final tensor
+            sums = _bn_sums(C_, bn_link, C, gy.device)
+            C_.gemm_dgrad_bnstats_mask(gy.reshape(-1, K), w.reshape(K, C), addend.view(-1, C), bn_link.x.view(-1, C),
+                                       bn_link.mask, bn_link.mean, sums)
+            bn_link.sums, bn_link.sums2, bn_link.dy_key = sums, None, (addend.data_ptr(), tuple(addend.shape))
+            STATS["bn_bstats"] += 1
+            return addend
         if addend is not None:
             C_.gemm(gy.reshape(-1, K), True, w.reshape(K, C), False, addend.view(-1, C), False, None, 0, None, True,
                     1.0, 1)

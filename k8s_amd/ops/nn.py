@@ -119,7 +119,7 @@ class BnStatLink:
     identity of the dy they were taken over; the BatchNorm's backward uses them only when it receives exactly that dy
     (so a second consumer of y, whose gradient autograd would add, falls back to the reduction)."""
     __slots__ = ("x", "mask", "mean", "x2", "mean2", "invstd", "gamma", "beta", "relu", "sums", "sums2", "dy_key",
-                 "store", "pending")
+                 "store", "pending", "last_full")
 
     def __init__(self, store=None):
         self.store = store  # the BatchNorm's ParamStore: its per-step zeroed scratch holds the sums
@@ -130,6 +130,9 @@ class BnStatLink:
         # sums over the first of two data gradients into y (a stage-entry block's conv1), awaiting the second's
         # correction (its downsample convolution, ops.conv._dgrad_strided_hip); dy_key is set only once complete
         self.pending = False
+        # two stride-1 data gradients into y (the stem pool's output, read by layer 1's conv1 and downsample): the
+        # first takes no sums, the second -- accumulating onto the first -- takes them over the final tensor
+        self.last_full = False
 
     def take(self, dy):
         """(sums, sums2) if they were taken over ``dy``, else None; clears the deposit either way."""
@@ -144,6 +147,8 @@ class BnStatLink:
 
 # BatchNorm-backward sums in the masked-addend 1x1 dgrad epilogue (BnStatLink); K8S_AMD_BN_BSTATS=0 for the A/B
 BN_BSTATS = os.environ.get("K8S_AMD_BN_BSTATS", "1") != "0"
+# ... and for the stem's BatchNorm + ReLU + max pool (its sums in layer 1's downsample dgrad)
+BSTATS_POOL = os.environ.get("K8S_AMD_BN_BSTATS_POOL", "1") != "0"
 
 
 class MaskLink:
@@ -854,9 +859,19 @@ class _BnReluMaxPool(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, sums, anchor, pg, pb, run_mean, run_var, momentum, eps):
         x = x.contiguous()
-        y, idx, mean, invstd = _C().bn_relu_maxpool(x, sums, pg.master, pb.master, run_mean, run_var, momentum, eps)
+        # BnStatLink (mask kind): the pooled output's data gradients take the BatchNorm-backward sums in their
+        # epilogue -- g = bit ? dpool : 0 lands on the window winner, so (winner's x, its ReLU bit) per pooled
+        # element is all they need -- and the backward skips pool_bn_bwd_reduce's sweep over the 112 x 112 x
+        want = BN_BSTATS and BSTATS_POOL
+        outs = _C().bn_relu_maxpool(x, sums, pg.master, pb.master, run_mean, run_var, momentum, eps, want)
+        y, idx, mean, invstd = outs[:4]
         ctx.save_for_backward(x, idx, mean, invstd)
         ctx.pg, ctx.pb = pg, pb
+        ctx.link = None
+        if want:
+            link = BnStatLink(pg.store)
+            link.x, link.mask, link.mean, link.last_full = outs[4], outs[5], mean, True
+            y._k8s_bnstat = ctx.link = link
         ctx.mark_non_differentiable(idx)
         return y
 
@@ -865,7 +880,12 @@ class _BnReluMaxPool(torch.autograd.Function):
         x, idx, mean, invstd = ctx.saved_tensors
         pg, pb = ctx.pg, ctx.pb
         dg, db, finish = _bn_param_grads(pg.store, pg, pb, x.device)
-        dx = _C().pool_bn_bwd(dy.contiguous(), idx, x, mean, invstd, pg.master, pb.master, dg, db)
+        dy = dy.contiguous()
+        pre = ctx.link.take(dy) if ctx.link is not None else None
+        if pre is not None:
+            dx = _C().pool_bn_bwd_from_sums(dy, idx, x, mean, invstd, pg.master, pb.master, dg, db, pre[0])
+        else:
+            dx = _C().pool_bn_bwd(dy, idx, x, mean, invstd, pg.master, pb.master, dg, db)
         finish()
         return (dx,) + (None,) * 8
 

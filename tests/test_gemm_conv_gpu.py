@@ -715,3 +715,37 @@ def test_stage_entry_bn_sums_two_dgrads(cuda, N, H, K1, C, K2):
     tot = sums.sum(0)
     assert _rel(tot[0], g.sum(0)) < 1e-3
     assert _rel(tot[1], (g * (x.float().view(-1, C) - mean)).sum(0)) < 1e-3
+
+
+def test_gemm_dgrad_bnstats_mask_accumulate(cuda):
+    """The second of two stride-1 data gradients into the stem pool's output (layer 1's downsample after its conv1):
+    the tile kernel accumulates onto the first's gradient and takes the BatchNorm-backward sums (mask kind) over the
+    final tensor in its epilogue (gemm.hip BST fast path; ops.conv._dgrad_hip, BnStatLink.last_full) -- against fp32
+    sums. Ragged M (not a multiple of the 128-row tile)."""
+    from k8s_amd.ops import conv as kc
+    from k8s_amd.ops import nn as K
+
+    C_ = _C()
+    torch.manual_seed(21)
+    N, H, C, K1, K2 = 4, 27, 64, 64, 256
+    M = N * H * H
+    x = (torch.randn(N, H, H, C, device=cuda) * 1.5 + 0.2).bfloat16()
+    mask = torch.randint(0, 256, (M * C // 8,), device=cuda, dtype=torch.uint8)
+    mean = torch.randn(C, device=cuda) * 0.2
+    gy1 = torch.randn(N, H, H, K1, device=cuda).bfloat16()
+    w1 = (torch.randn(K1, 1, 1, C, device=cuda) * 0.05).bfloat16()
+    gy2 = torch.randn(N, H, H, K2, device=cuda).bfloat16()
+    w2 = (torch.randn(K2, 1, 1, C, device=cuda) * 0.05).bfloat16()
+    link = K.BnStatLink()
+    link.x, link.mask, link.mean, link.last_full = x, mask, mean, True
+    dx1 = kc._dgrad_hip(C_, gy1, w1, 0, None, link)
+    assert link.sums is None and not link.pending
+    dx = kc._dgrad_hip(C_, gy2, w2, 0, dx1, link)
+    assert dx.data_ptr() == dx1.data_ptr()
+    assert link.dy_key == (dx.data_ptr(), tuple(dx.shape)) and link.sums is not None
+    ref = gy1.float().reshape(-1, K1) @ w1.float().reshape(K1, C) + gy2.float().reshape(-1, K2) @ w2.float().reshape(K2, C)
+    assert _rel(dx.view(-1, C), ref) < 1e-2
+    g = torch.where(_unpack_bits(mask, (M, C)), dx.float().view(-1, C), torch.zeros(M, C, device=cuda))
+    tot = link.sums.sum(0)
+    assert _rel(tot[0], g.sum(0)) < 1e-3
+    assert _rel(tot[1], (g * (x.float().view(-1, C) - mean)).sum(0)) < 1e-3

@@ -339,3 +339,33 @@ def test_bn_relu_maxpool_fused_vs_fp32(cuda, N, H, W, C):
     _close(dg, dgr, 1e-3)
     rel = ((dx.float().reshape(-1, C) - dxr).norm() / dxr.norm()).item()
     assert rel < 1e-2, rel
+    # the BnStatLink outputs (each pooled element's winner x and ReLU bit) and the backward from sums taken over them
+    # (what the consumers' dgrad epilogues accumulate: g = bit ? dy : 0, sum g, sum g (x_winner - mean))
+    rm2, rv2 = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    y2, idx2, mean2, invstd2, xarg, ybits = _C().bn_relu_maxpool(x, sums, g, b, rm2, rv2, 0.1, 1e-5, True)
+    assert torch.equal(y2, y) and torch.equal(idx2, idx)
+    bits = ((ybits.view(-1, 1) >> torch.arange(8, device=cuda, dtype=torch.uint8)) & 1).bool().view(y.shape)
+    assert torch.equal(bits, y > 0)
+    # winner x from the saved window position: tap (dh, dw) of window (ho, wo) is pixel (2 ho - 1 + dh, 2 wo - 1 + dw)
+    Ho, Wo = y.shape[1], y.shape[2]
+    pos = idx.long()
+    hh = (2 * torch.arange(Ho, device=cuda).view(1, Ho, 1, 1) - 1 + pos // 3).clamp(0, H - 1)
+    ww = (2 * torch.arange(Wo, device=cuda).view(1, 1, Wo, 1) - 1 + pos % 3).clamp(0, W - 1)
+    nn_ = torch.arange(N, device=cuda).view(N, 1, 1, 1).expand_as(pos)
+    cc = torch.arange(C, device=cuda).view(1, 1, 1, C).expand_as(pos)
+    xw = x[nn_, hh, ww, cc]
+    valid = y > 0
+    assert torch.equal(xarg[valid], xw[valid])
+    R = _C().conv_stat_replicas
+    gsel = torch.where(bits, dy.float(), torch.zeros_like(dy.float())).reshape(-1, C)
+    bsums = torch.zeros(R, 2, C, device=cuda)
+    bsums[0, 0] = gsel.sum(0)
+    bsums[1, 1] = (gsel * (xarg.float().reshape(-1, C) - mean2)).sum(0)
+    dg2, db2 = torch.empty(C, device=cuda), torch.empty(C, device=cuda)
+    dx2 = _C().pool_bn_bwd_from_sums(dy, idx2, x, mean2, invstd2, g, b, dg2, db2, bsums)
+    # sums over the pooled gradient itself: a pixel that wins several windows adds their dy unrounded (the reference
+    # and the reduce pass sum the bf16-rounded dz of that pixel), so ~1 bf16 ulp of such pixels apart
+    _close(db2, dbr, 5e-3)
+    _close(dg2, dgr, 5e-3)
+    rel = ((dx2.float().reshape(-1, C) - dxr).norm() / dxr.norm()).item()
+    assert rel < 1e-2, rel
