@@ -683,9 +683,11 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
               bf16x8_t o = *reinterpret_cast<const bf16x8_t*>(lp + i * RSTEP * BN + ((c ^ (row % CPR)) << 3));
               if (ap) {  // (the general path's rounding: the staged bf16 value + old C, one more rounding)
                 const bf16x8_t old = *reinterpret_cast<const bf16x8_t*>(ap + (long)i * RSTEP * ldc);
+                const uint32_t abits = mp ? (uint32_t)mp[((long)i * RSTEP * ldc) >> 3] : 0xFFu;
                 float f[8];
 #pragma unroll
-                for (int r = 0; r < 8; ++r) f[r] = bf2f((uint16_t)o[r]) + bf2f((uint16_t)old[r]);
+                for (int r = 0; r < 8; ++r)
+                  f[r] = bf2f((uint16_t)o[r]) + (((abits >> r) & 1u) ? bf2f((uint16_t)old[r]) : 0.f);
                 o = pack_bf16x8(f);
               }
               *reinterpret_cast<bf16x8_t*>(cp + (long)i * RSTEP * ldc) = o;
@@ -1064,8 +1066,8 @@ static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int 
   // a data gradient (K-major dy, MN-major w) with the BatchNorm-backward sums of its output
   if (e.bb.sums) {
     if constexpr (std::is_same_v<ASrc, KMajor> && std::is_same_v<BSrc, MNMajorK> && WM == 2 && WN == 2) {
-      if (lean_epi(e, N, false) && (e.mode == 0 || (e.mode == 1 && e.bb.mask)) && !e.stats && !e.rst && !e.addsrc &&
-          !e.addmask && splits == 1 && e.ldc == N) {
+      if (lean_epi(e, N, false) && (e.mode == 0 || (e.mode == 1 && e.bb.mask)) && !e.stats && !e.rst &&
+          (!e.addmask || e.addsrc) && splits == 1 && e.ldc == N) {
         launch_tiles2<ASrc, BSrc, WM, WN, true, false, false, 0, true>(a, b, e, M, N, K, kps, splits, st);
         return;
       }
@@ -1234,13 +1236,17 @@ void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, 
 // dx[M, N] = dy[M, K] . w[K, N] (bf16, the 1x1 data gradient) on the tile kernel with the BatchNorm-backward sums
 // of dx for the relu(BN(x)) that produced the convolution's input (Epi::bb, BST instantiation).
 void launch_gemm_dgrad_bnstats(const uint16_t* A, const uint16_t* B, uint16_t* C, int M, int N, int K,
-                               const BnBwdSums& bb, hipStream_t st, bool accumulate) {
+                               const BnBwdSums& bb, hipStream_t st, bool accumulate, const uint16_t* add_src,
+                               const uint8_t* add_mask) {
   // relu kind: x / gamma / beta / mean / invstd; mask kind (bb.mask): x / mean, and C may be accumulated onto
   if (!bb.sums || !bb.x || !bb.mean || N % 8 || (!bb.mask && (!bb.gamma || !bb.beta || !bb.invstd || accumulate)))
     throw std::runtime_error("gemm dgrad BatchNorm-backward sums: x / mean / sums (+ gamma / beta / invstd without a "
                              "mask; accumulate only with one), N % 8 == 0");
+  if ((add_src || add_mask) && !accumulate) throw std::runtime_error("gemm dgrad BatchNorm sums: an addend accumulates");
   Epi e = make_epi(C, N, false, nullptr, 0, nullptr, accumulate ? 1 : 0, 1.f);
   e.bb = bb;
+  e.addsrc = add_src;  // out = product + (add_mask bit ? add_src : 0) (a ResNet identity block's residual gradient)
+  e.addmask = add_mask;
   launch(KMajor{A, (long)K, M, K}, MNMajorK{B, (long)N, N, K}, e, M, N, K, 1, st);
 }
 

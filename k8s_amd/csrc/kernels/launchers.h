@@ -128,7 +128,8 @@ void launch_gemm_short(const uint16_t* A, const uint16_t* B, long ldb, bool b_mn
                        const uint8_t* mask, const float* xf, float* stats, int M, int N, int K, int epi,
                        hipStream_t st, const GemmShortBnStats* bst = nullptr);
 void launch_gemm_dgrad_bnstats(const uint16_t* A, const uint16_t* B, uint16_t* C, int M, int N, int K,
-                               const BnBwdSums& bb, hipStream_t st, bool accumulate = false);
+                               const BnBwdSums& bb, hipStream_t st, bool accumulate = false,
+                               const uint16_t* add_src = nullptr, const uint8_t* add_mask = nullptr);
 void launch_gemm(const uint16_t* A, long lda, bool a_kmajor, const uint16_t* B, long ldb, bool b_kmajor, void* C,
                  long ldc, bool c_f32, int M, int N, int K, const float* bias, int act, uint16_t* pre, int mode,
                  float alpha, int splits, float* ws, hipStream_t st, const AddEpi* add = nullptr,

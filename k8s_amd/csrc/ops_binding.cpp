@@ -650,7 +650,10 @@ Tensor gemm_dgrad_bnstats(Tensor gy, Tensor w, Tensor x, Tensor gamma, Tensor be
 // out[M, N] += gy[M, K] . w[K, N] on the tile kernel, also accumulating the BatchNorm-backward sums of the final out
 // for a BatchNorm whose ReLU bits are stored (mask kind: g = bit ? out : 0, sum g, sum g (x - mean)) -- the second
 // of two data gradients into that BatchNorm's output (the stem pool's, nn.BnStatLink.last_full). Returns out.
-Tensor gemm_dgrad_bnstats_mask(Tensor gy, Tensor w, Tensor out, Tensor x, Tensor mask, Tensor mean, Tensor sums) {
+// With add_src / add_mask (a ResNet identity block's residual gradient as (dy, packed ReLU bits)): out = product +
+// (bit ? add_src : 0), out's old values unread.
+Tensor gemm_dgrad_bnstats_mask(Tensor gy, Tensor w, Tensor out, Tensor x, Tensor mask, Tensor mean, Tensor sums,
+                               c10::optional<Tensor> add_src, c10::optional<Tensor> add_mask) {
   for (const Tensor* t : {&gy, &w, &out, &x}) {
     check_cuda(*t, "gy / w / out / x");
     check_dtype(*t, at::kBFloat16, "gy / w / out / x");
@@ -670,7 +673,16 @@ Tensor gemm_dgrad_bnstats_mask(Tensor gy, Tensor w, Tensor out, Tensor x, Tensor
   bb.mask = mask.data_ptr<uint8_t>();
   bb.mean = f32(mean);
   bb.sums = f32(sums);
-  k8s_amd::launch_gemm_dgrad_bnstats(cbf(gy), cbf(w), bf(out), (int)M, (int)N, (int)K, bb, cur_stream(), true);
+  TORCH_CHECK(add_src.has_value() == add_mask.has_value(), "add_src and add_mask together");
+  if (add_src) {
+    check_dtype(*add_src, at::kBFloat16, "add_src");
+    TORCH_CHECK(add_src->is_cuda() && add_src->is_contiguous() && add_src->numel() == M * N, "add_src: [M, N]");
+    TORCH_CHECK(add_mask->is_cuda() && add_mask->scalar_type() == at::kByte && add_mask->numel() * 8 == M * N,
+                "add_mask: packed bits");
+  }
+  k8s_amd::launch_gemm_dgrad_bnstats(cbf(gy), cbf(w), bf(out), (int)M, (int)N, (int)K, bb, cur_stream(), true,
+                                     add_src ? cbf(*add_src) : nullptr,
+                                     add_src ? add_mask->data_ptr<uint8_t>() : nullptr);
   return out;
 }
 
@@ -1551,7 +1563,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_relu_maxpool", &bn_relu_maxpool, py::arg("x"), py::arg("sums"), py::arg("gamma"), py::arg("beta"),
         py::arg("run_mean"), py::arg("run_var"), py::arg("momentum"), py::arg("eps"), py::arg("want_link") = false);
   m.def("pool_bn_bwd_from_sums", &pool_bn_bwd_from_sums);
-  m.def("gemm_dgrad_bnstats_mask", &gemm_dgrad_bnstats_mask);
+  m.def("gemm_dgrad_bnstats_mask", &gemm_dgrad_bnstats_mask, py::arg("gy"), py::arg("w"), py::arg("out"), py::arg("x"),
+        py::arg("mask"), py::arg("mean"), py::arg("sums"), py::arg("add_src") = py::none(),
+        py::arg("add_mask") = py::none());
   m.def("pool_bn_bwd", &pool_bn_bwd, py::arg("dpool"), py::arg("idx"), py::arg("x"), py::arg("mean"),
         py::arg("invstd"), py::arg("gamma"), py::arg("beta"), py::arg("dgamma"), py::arg("dbeta"));
   m.def("embed_fwd", &embed_fwd);

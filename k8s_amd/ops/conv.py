@@ -125,6 +125,8 @@ BSTATS_3X3 = os.environ.get("K8S_AMD_BN_BSTATS_3X3", "1") != "0"
 BSTATS_GEMM = os.environ.get("K8S_AMD_BN_BSTATS_GEMM", "1") != "0"
 # a stage-entry block's residual BN: sums over conv1's dgrad completed by the downsample's strided dgrad
 BSTATS_ENTRY = os.environ.get("K8S_AMD_BN_BSTATS_ENTRY", "1") != "0"
+# a residual BN's sums in a masked-addend 1x1 dgrad too deep for gemm_short (the tile kernel: stage 4, K = 512)
+BSTATS_TILE_MASK = os.environ.get("K8S_AMD_BN_BSTATS_TILE_MASK", "1") != "0"
 
 
 def _bn_sums(C_, bn_link, C, device):
@@ -165,6 +167,17 @@ def _dgrad_hip(C_, gy, w, padding, addend=None, bn_link=None):
                 bn_link.mask, bn_link.mean, sums, None if sums2 is None else bn_link.x2.view(-1, C), bn_link.mean2,
                 sums2).view(N, H, W_, C)
             bn_link.sums, bn_link.sums2, bn_link.dy_key = sums, sums2, (out.data_ptr(), tuple(out.shape))
+            STATS["bn_bstats"] += 1
+            return out
+        if (masked and BSTATS_TILE_MASK and bn_link is not None and not bn_link.relu and bn_link.x is not None
+                and bn_link.mask is not None and bn_link.x2 is None and bn_link.x.shape == (N, H, W_, C)
+                and N * H * W_ < 2 ** 31):
+            # the same on the tile kernel (K = 512: the stage-4 identity blocks), one BatchNorm
+            out = torch.empty(N, H, W_, C, device=gy.device, dtype=gy.dtype)
+            sums = _bn_sums(C_, bn_link, C, gy.device)
+            C_.gemm_dgrad_bnstats_mask(gy.reshape(-1, K), w.reshape(K, C), out.view(-1, C), bn_link.x.view(-1, C),
+                                       bn_link.mask, bn_link.mean, sums, addend.dy.view(-1, C), addend.mask)
+            bn_link.sums, bn_link.sums2, bn_link.dy_key = sums, None, (out.data_ptr(), tuple(out.shape))
             STATS["bn_bstats"] += 1
             return out
         if (BSTATS_GEMM and bn_link is not None and bn_link.relu and bn_link.x is not None and addend is None

@@ -749,3 +749,28 @@ def test_gemm_dgrad_bnstats_mask_accumulate(cuda):
     tot = link.sums.sum(0)
     assert _rel(tot[0], g.sum(0)) < 1e-3
     assert _rel(tot[1], (g * (x.float().view(-1, C) - mean)).sum(0)) < 1e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 256, 512), (3 * 49 * 4, 2048, 512)])
+def test_gemm_dgrad_bnstats_masked_addend(cuda, M, N, K):
+    """A stage-4 identity block's conv1 data gradient (K = 512: not a gemm_short depth) on the tile kernel: out =
+    dgrad + (addend bit ? addend : 0) with the residual BatchNorm's backward sums of out in the same epilogue
+    (gemm.hip BST fast path, masked addend), against fp32."""
+    C_ = _C()
+    torch.manual_seed(23)
+    gy = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(K, N, device=cuda) * 0.05).bfloat16()
+    add = torch.randn(M, N, device=cuda).bfloat16()
+    amask = torch.randint(0, 256, (M * N // 8,), device=cuda, dtype=torch.uint8)
+    x = (torch.randn(M, N, device=cuda) * 1.5 + 0.2).bfloat16()
+    mask = torch.randint(0, 256, (M * N // 8,), device=cuda, dtype=torch.uint8)
+    mean = torch.randn(N, device=cuda) * 0.2
+    sums = torch.zeros(C_.conv_stat_replicas, 2, N, device=cuda)
+    out = torch.full((M, N), float("nan"), device=cuda).bfloat16()
+    C_.gemm_dgrad_bnstats_mask(gy, w, out, x, mask, mean, sums, add, amask)
+    ref = gy.float() @ w.float() + torch.where(_unpack_bits(amask, (M, N)), add.float(), torch.zeros(M, N, device=cuda))
+    assert _rel(out, ref) < 1e-2
+    g = torch.where(_unpack_bits(mask, (M, N)), out.float(), torch.zeros(M, N, device=cuda))
+    tot = sums.sum(0)
+    assert _rel(tot[0], g.sum(0)) < 1e-3
+    assert _rel(tot[1], (g * (x.float() - mean)).sum(0)) < 1e-3
