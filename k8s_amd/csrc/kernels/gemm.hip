@@ -640,9 +640,13 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
     // copy-out: thread t always handles 16-B chunk c = t % CPR of its rows (GEMM_THREADS % CPR == 0), so it
     // also accumulates the BN statistics (sum, sum of squares) of those 8 columns from the bf16 values it stores
     float* const stat_out = BST ? E.bb.sums : E.stats;
-    float ps[8], pq[8];
+    float ps[8], pq[8], pq2[BST ? 8 : 1];
 #pragma unroll
     for (int r = 0; r < 8; ++r) ps[r] = pq[r] = 0.f;
+    if constexpr (BST) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) pq2[r] = 0.f;
+    }
     constexpr int CHUNKS = BM * CPR;
     // fast path (convolution forward with statistics, plain and accumulating data gradients): identity rows. A
     // thread's chunk column is fixed and its rows advance by GEMM_THREADS / CPR per trip, so the
@@ -667,13 +671,16 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
         // with the output (ldc == N). Mask kind (bb.mask, a BatchNorm whose ReLU bits are stored: the stem pool's
         // output): g = bit ? dx : 0, and the product may accumulate onto C (an unmasked addend: the first of two
         // data gradients into the same tensor)
+        // Two-BatchNorm form (bb.x2, mask kind only): bsh holds the second BN's means, q2b its sum g (x2 - mean2).
         float bsc[BST ? 8 : 1], bsh[BST ? 8 : 1], bmu[BST ? 8 : 1];
         if constexpr (BST) {
           const bool mk = E.bb.mask != nullptr;
+          const uint16_t* const x2p = E.bb.x2 ? E.bb.x2 + off0 : nullptr;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             bmu[j] = E.bb.mean[n + j];
-            bsc[j] = bsh[j] = 0.f;
+            bsc[j] = 0.f;
+            bsh[j] = x2p ? E.bb.mean2[n + j] : 0.f;
             if (!mk) bn_affine_regs(E.bb.gamma[n + j], E.bb.beta[n + j], bmu[j], E.bb.invstd[n + j], bsc[j], bsh[j]);
           }
 #pragma unroll
@@ -704,6 +711,14 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
                 }
                 s2[r] += g;
                 q2[r] = __builtin_elementwise_fma(g, d, q2[r]);
+              }
+              if (x2p) {
+                const bf16x8_t x2v = *reinterpret_cast<const bf16x8_t*>(x2p + (long)i * RSTEP * ldc);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                  const float g = ((bits >> r) & 1u) ? bf2f((uint16_t)o[r]) : 0.f;
+                  pq2[r] = __builtin_fmaf(g, bf2f((uint16_t)x2v[r]) - bsh[r], pq2[r]);
+                }
               }
             }
           }
@@ -750,11 +765,18 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
     // BST on the row-remapped (sub-grid) path: the correction of a residual BatchNorm's backward sums (packed ReLU
     // bits bb.mask) for the elements this accumulating product changes -- sum bit (new - old), sum bit (new - old)
     // (x - mean) -- the first data gradient into the same tensor having counted the old values (ops.conv)
-    float gmu[BST ? 8 : 1];
+    // Relu kind (no bb.mask, a plain store: the parities of a stride-2 3x3 data gradient, each writing its own
+    // pixels): g = relu_on(x) ? dx : 0 from the BatchNorm's affine, sum g and sum g (x - mean) of the stored values.
+    float gmu[BST ? 8 : 1], gsc[BST ? 8 : 1], gsh[BST ? 8 : 1];
     if constexpr (BST) {
       const int nt = n0 + (tid % CPR) * 8;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) gmu[r] = nt + r < N ? E.bb.mean[nt + r] : 0.f;
+      for (int r = 0; r < 8; ++r) {
+        gmu[r] = nt + r < N ? E.bb.mean[nt + r] : 0.f;
+        gsc[r] = gsh[r] = 0.f;
+        if (!E.bb.mask && nt + r < N)
+          bn_affine_regs(E.bb.gamma[nt + r], E.bb.beta[nt + r], gmu[r], E.bb.invstd[nt + r], gsc[r], gsh[r]);
+      }
     }
 #pragma unroll 2
     for (int q = tid; q < CHUNKS; q += GEMM_THREADS) {
@@ -803,6 +825,18 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
           }
         }
       }
+      if constexpr (BST) {
+        if (!E.bb.mask) {
+          const bf16x8_t xv = *reinterpret_cast<const bf16x8_t*>(E.bb.x + orow * E.ldc + n);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const float xf = bf2f((uint16_t)xv[r]);
+            const float g = relu_on(xf, gsc[r], gsh[r]) ? bf2f((uint16_t)o[r]) : 0.f;
+            ps[r] += g;
+            pq[r] = __builtin_fmaf(g, xf - gmu[r], pq[r]);
+          }
+        }
+      }
       *reinterpret_cast<bf16x8_t*>(cp) = o;
       if (!BST && stat_out) {  // (BST: stat_out is the BatchNorm sums, corrected above)
 #pragma unroll
@@ -834,6 +868,24 @@ gemm_bf16_kernel(ASrc A, BSrc B, Epi E, int M, int N, int K, int k_per_split, XF
 #pragma unroll 4
           for (int t = c; t < GEMM_THREADS; t += CPR) v += part[t * 16 + which * 8 + r];
           atomicAdd(stat_out + (long)(tm % STAT_REPL) * 2 * N + (long)which * N + n, v);
+        }
+      }
+      if constexpr (BST) {
+        if (E.bb.x2) {  // the second BatchNorm's sum g (x2 - mean2) into sums2[.][1] (its sum g is the first's)
+          __syncthreads();
+#pragma unroll
+          for (int r = 0; r < 8; ++r) part[tid * 16 + r] = pq2[r];
+          __syncthreads();
+          if (tid < BN) {
+            const int n = n0 + tid;
+            if (n < N) {
+              const int c = tid >> 3, r = tid & 7;
+              float v = 0.f;
+#pragma unroll 4
+              for (int t = c; t < GEMM_THREADS; t += CPR) v += part[t * 16 + r];
+              atomicAdd(E.bb.sums2 + (long)(tm % STAT_REPL) * 2 * N + N + n, v);
+            }
+          }
         }
       }
     }
@@ -1072,8 +1124,13 @@ static void launch_tiles(const ASrc& a, const BSrc& b, const Epi& e, int M, int 
         return;
       }
     }
-    if constexpr (std::is_same_v<ASrc, KMajor> && std::is_same_v<BSrc, KMajor> && WM == 2 && WN == 2) {
-      if (lean_epi(e, N, false) && e.mode == 1 && !e.stats && e.rst && !e.addsrc && splits == 1 && e.bb.mask) {
+    // the row-remapped (sub-grid) data gradients: a 1x1 parity accumulating a residual BatchNorm's correction (mask
+    // kind), or a parity of a stride-2 convolution's data gradient storing with a BatchNorm + ReLU's sums (relu kind;
+    // the 1x1 parity on the K-major source, the others on the implicit GEMM)
+    if constexpr ((std::is_same_v<ASrc, KMajor> || std::is_same_v<ASrc, ConvA>) && std::is_same_v<BSrc, KMajor> &&
+                  WM == 2 && WN == 2) {
+      if (lean_epi(e, N, false) && !e.stats && e.rst && !e.addsrc && !e.addmask && splits == 1 &&
+          ((e.mode == 1 && e.bb.mask && std::is_same_v<ASrc, KMajor>) || (e.mode == 0 && !e.bb.mask))) {
         launch_tiles2<ASrc, BSrc, WM, WN, true, false, false, 0, true>(a, b, e, M, N, K, kps, splits, st);
         return;
       }
@@ -1239,6 +1296,8 @@ void launch_gemm_dgrad_bnstats(const uint16_t* A, const uint16_t* B, uint16_t* C
                                const BnBwdSums& bb, hipStream_t st, bool accumulate, const uint16_t* add_src,
                                const uint8_t* add_mask) {
   // relu kind: x / gamma / beta / mean / invstd; mask kind (bb.mask): x / mean, and C may be accumulated onto
+  if (bb.x2 && (!bb.mask || !bb.mean2 || !bb.sums2))
+    throw std::runtime_error("gemm dgrad BatchNorm sums: the two-BatchNorm form is mask kind with mean2 / sums2");
   if (!bb.sums || !bb.x || !bb.mean || N % 8 || (!bb.mask && (!bb.gamma || !bb.beta || !bb.invstd || accumulate)))
     throw std::runtime_error("gemm dgrad BatchNorm-backward sums: x / mean / sums (+ gamma / beta / invstd without a "
                              "mask; accumulate only with one), N % 8 == 0");
@@ -1256,10 +1315,16 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, void* y, bool y_f32, 
                      int R, int S, int stride, int pad, int dil, int Ho, int Wo, const float* bias, int act,
                      int mode, float* stats, hipStream_t st, const SubGrid* sg,
                      const float* xform, const BnBwdSums* bb) {
-  if (bb && (!sg || mode != 1 || R != 1 || S != 1 || stride != 1 || pad != 0 || y_f32 || stats || xform || !bb->mask ||
-             !bb->x || !bb->mean || !bb->sums))
+  if (bb && bb->mask &&
+      (!sg || mode != 1 || R != 1 || S != 1 || stride != 1 || pad != 0 || y_f32 || stats || xform || !bb->x ||
+       !bb->mean || !bb->sums))
     throw std::runtime_error("conv: BatchNorm-sum corrections only on an accumulating 1x1 sub-grid data gradient");
-  if (!sg && !y_f32 && !bias && act == 0 && mode == 0 && conv3x3_eligible(H, W, C, K, R, S, stride, pad, dil)) {
+  // relu kind: a sub-grid parity's plain store (a stride-2 data gradient) on the tile kernel, C % 64 == 0, K > 64
+  if (bb && !bb->mask &&
+      (!sg || mode != 0 || y_f32 || stats || xform || bias || act || C % 64 || K <= 64 || !bb->x || !bb->mean ||
+       !bb->sums || !bb->gamma || !bb->beta || !bb->invstd))
+    throw std::runtime_error("conv: BatchNorm + ReLU sums only on a stored sub-grid data gradient (C % 64, K > 64)");
+  if (!bb && !sg && !y_f32 && !bias && act == 0 && mode == 0 && conv3x3_eligible(H, W, C, K, R, S, stride, pad, dil)) {
     launch_conv3x3(x, w, reinterpret_cast<uint16_t*>(y), stats, xform, N, H, W, C, K, st);  // staged window
     return;
   }

@@ -114,6 +114,11 @@ struct BnBwdSums {
   // mask kind (a residual BatchNorm's packed ReLU bits instead of the affine ReLU decision): the row-remapped
   // accumulating data gradient's correction (gemm.hip BST sub-grid path); gamma / beta / invstd unused
   const uint8_t* mask = nullptr;
+  // mask kind, the two-BatchNorm form (a ResNet downsample block's output: bn3 and the downsample BN share g):
+  // sums2[.][1] += sum g (x2 - mean2) (identity-row path only)
+  const uint16_t* x2 = nullptr;
+  const float* mean2 = nullptr;
+  float* sums2 = nullptr;
 };
 struct GemmShortBnStats {
   const uint16_t* x = nullptr;

@@ -652,8 +652,10 @@ Tensor gemm_dgrad_bnstats(Tensor gy, Tensor w, Tensor x, Tensor gamma, Tensor be
 // of two data gradients into that BatchNorm's output (the stem pool's, nn.BnStatLink.last_full). Returns out.
 // With add_src / add_mask (a ResNet identity block's residual gradient as (dy, packed ReLU bits)): out = product +
 // (bit ? add_src : 0), out's old values unread.
+// x2 / mean2 / sums2: the two-BatchNorm form (a ResNet downsample block's output), sums2[.][1] += sum g (x2 - mean2).
 Tensor gemm_dgrad_bnstats_mask(Tensor gy, Tensor w, Tensor out, Tensor x, Tensor mask, Tensor mean, Tensor sums,
-                               c10::optional<Tensor> add_src, c10::optional<Tensor> add_mask) {
+                               c10::optional<Tensor> add_src, c10::optional<Tensor> add_mask,
+                               c10::optional<Tensor> x2, c10::optional<Tensor> mean2, c10::optional<Tensor> sums2) {
   for (const Tensor* t : {&gy, &w, &out, &x}) {
     check_cuda(*t, "gy / w / out / x");
     check_dtype(*t, at::kBFloat16, "gy / w / out / x");
@@ -673,6 +675,17 @@ Tensor gemm_dgrad_bnstats_mask(Tensor gy, Tensor w, Tensor out, Tensor x, Tensor
   bb.mask = mask.data_ptr<uint8_t>();
   bb.mean = f32(mean);
   bb.sums = f32(sums);
+  TORCH_CHECK(x2.has_value() == mean2.has_value() && x2.has_value() == sums2.has_value(), "x2 / mean2 / sums2 together");
+  if (x2) {
+    check_dtype(*x2, at::kBFloat16, "x2");
+    TORCH_CHECK(x2->is_cuda() && x2->is_contiguous() && x2->sizes() == x.sizes(), "x2: the shape of x");
+    TORCH_CHECK(mean2->is_cuda() && mean2->numel() == N && mean2->scalar_type() == at::kFloat, "mean2: fp32 [N]");
+    TORCH_CHECK(sums2->is_cuda() && sums2->scalar_type() == at::kFloat && sums2->is_contiguous() &&
+                    sums2->numel() == (long)k8s_amd::kConvStatReplicas * 2 * N, "sums2: fp32 [conv_stat_replicas, 2, N]");
+    bb.x2 = cbf(*x2);
+    bb.mean2 = f32(*mean2);
+    bb.sums2 = f32(*sums2);
+  }
   TORCH_CHECK(add_src.has_value() == add_mask.has_value(), "add_src and add_mask together");
   if (add_src) {
     check_dtype(*add_src, at::kBFloat16, "add_src");
@@ -991,7 +1004,8 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, bo
 // `accumulate` adds onto out in the epilogue (out already holds the residual branch's gradient).
 void conv_fwd_subgrid(Tensor x, Tensor w, int64_t pad, int64_t Hs, int64_t Ws, Tensor out, int64_t stride, int64_t a,
                       int64_t b, bool accumulate, c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_mask,
-                      c10::optional<Tensor> bn_mean, c10::optional<Tensor> bn_sums) {
+                      c10::optional<Tensor> bn_mean, c10::optional<Tensor> bn_sums, c10::optional<Tensor> bn_gamma,
+                      c10::optional<Tensor> bn_beta, c10::optional<Tensor> bn_invstd) {
   check_cuda(x, "x"); check_cuda(w, "w"); check_cuda(out, "out");
   check_dtype(x, at::kBFloat16, "x"); check_dtype(w, at::kBFloat16, "w"); check_dtype(out, at::kBFloat16, "out");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && out.dim() == 4 && out.is_contiguous());
@@ -1007,18 +1021,33 @@ void conv_fwd_subgrid(Tensor x, Tensor w, int64_t pad, int64_t Hs, int64_t Ws, T
   // bn_*: the correction of a residual BatchNorm's backward sums for the elements this accumulating product changes
   // (gemm.hip BST sub-grid path; the first data gradient into `out` took the sums over its values)
   k8s_amd::BnBwdSums bb;
+  // relu kind (bn_gamma / bn_beta / bn_invstd, no bn_mask, a plain store): the sums of a BatchNorm + ReLU over this
+  // parity's stored pixels (a stride-2 data gradient; the parities partition the output)
   if (bn_sums) {
-    TORCH_CHECK(bn_x && bn_mask && bn_mean && accumulate, "bn correction: bn_x, bn_mask, bn_mean and accumulate");
+    const bool relu_kind = !bn_mask;
+    TORCH_CHECK(bn_x && bn_mean, "bn sums: bn_x and bn_mean");
+    TORCH_CHECK(relu_kind ? (bn_gamma && bn_beta && bn_invstd && !accumulate) : accumulate,
+                "bn sums: bn_mask + accumulate (a correction) or bn_gamma / bn_beta / bn_invstd + a plain store");
     check_dtype(*bn_x, at::kBFloat16, "bn_x");
     TORCH_CHECK(bn_x->sizes() == out.sizes() && bn_x->is_contiguous(), "bn_x: the shape of out");
-    TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() * 8 == out.numel(), "bn_mask: packed bits");
+    TORCH_CHECK(relu_kind || (bn_mask->scalar_type() == at::kByte && bn_mask->numel() * 8 == out.numel()),
+                "bn_mask: packed bits");
     TORCH_CHECK(bn_mean->numel() == K && bn_mean->scalar_type() == at::kFloat, "bn_mean: fp32 [K]");
     TORCH_CHECK(bn_sums->numel() == (long)k8s_amd::kConvStatReplicas * 2 * K && bn_sums->scalar_type() == at::kFloat,
                 "bn_sums: fp32 [conv_stat_replicas, 2, K]");
     bb.x = cbf(*bn_x);
-    bb.mask = bn_mask->data_ptr<uint8_t>();
     bb.mean = f32(*bn_mean);
     bb.sums = f32(*bn_sums);
+    if (relu_kind) {
+      for (const c10::optional<Tensor>* t : {&bn_gamma, &bn_beta, &bn_invstd})
+        TORCH_CHECK((*t)->numel() == K && (*t)->scalar_type() == at::kFloat && (*t)->is_contiguous(),
+                    "bn_gamma / bn_beta / bn_invstd: fp32 [K]");
+      bb.gamma = f32(*bn_gamma);
+      bb.beta = f32(*bn_beta);
+      bb.invstd = f32(*bn_invstd);
+    } else {
+      bb.mask = bn_mask->data_ptr<uint8_t>();
+    }
   }
   k8s_amd::launch_conv_fwd(cbf(x), cbf(w), out.data_ptr(), false, N, H, W, C, K, R, S, 1, (int)pad, 1, (int)Hs,
                            (int)Ws, nullptr, 0, accumulate ? 1 : 0, nullptr, cur_stream(), &sg, nullptr,
@@ -1555,7 +1584,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd_subgrid", &conv_fwd_subgrid, py::arg("x"), py::arg("w"), py::arg("pad"), py::arg("Hs"),
         py::arg("Ws"), py::arg("out"), py::arg("stride"), py::arg("a"), py::arg("b"), py::arg("accumulate") = false,
         py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none(),
-        py::arg("bn_sums") = py::none());
+        py::arg("bn_sums") = py::none(), py::arg("bn_gamma") = py::none(), py::arg("bn_beta") = py::none(),
+        py::arg("bn_invstd") = py::none());
   m.def("conv_dgrad_wtrans", &conv_dgrad_wtrans);
   m.def("conv_dgrad_wsub", &conv_dgrad_wsub);
   m.def("flash_fwd", &flash_fwd);
@@ -1565,7 +1595,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pool_bn_bwd_from_sums", &pool_bn_bwd_from_sums);
   m.def("gemm_dgrad_bnstats_mask", &gemm_dgrad_bnstats_mask, py::arg("gy"), py::arg("w"), py::arg("out"), py::arg("x"),
         py::arg("mask"), py::arg("mean"), py::arg("sums"), py::arg("add_src") = py::none(),
-        py::arg("add_mask") = py::none());
+        py::arg("add_mask") = py::none(), py::arg("x2") = py::none(), py::arg("mean2") = py::none(),
+        py::arg("sums2") = py::none());
   m.def("pool_bn_bwd", &pool_bn_bwd, py::arg("dpool"), py::arg("idx"), py::arg("x"), py::arg("mean"),
         py::arg("invstd"), py::arg("gamma"), py::arg("beta"), py::arg("dgamma"), py::arg("dbeta"));
   m.def("embed_fwd", &embed_fwd);

@@ -127,6 +127,11 @@ BSTATS_GEMM = os.environ.get("K8S_AMD_BN_BSTATS_GEMM", "1") != "0"
 BSTATS_ENTRY = os.environ.get("K8S_AMD_BN_BSTATS_ENTRY", "1") != "0"
 # a residual BN's sums in a masked-addend 1x1 dgrad too deep for gemm_short (the tile kernel: stage 4, K = 512)
 BSTATS_TILE_MASK = os.environ.get("K8S_AMD_BN_BSTATS_TILE_MASK", "1") != "0"
+# a BatchNorm + ReLU's sums in the parities of a stride-2 data gradient (ResNet's stage-entry bn1)
+BSTATS_STRIDED = os.environ.get("K8S_AMD_BN_BSTATS_STRIDED", "1") != "0"
+# ... including the two-BatchNorm form at a gemm_short depth (K = 256: that epilogue spills; the plain product would
+# run on gemm_short)
+BSTATS_TILE_SHORT = os.environ.get("K8S_AMD_BN_BSTATS_TILE_SHORT", "1") != "0"
 
 
 def _bn_sums(C_, bn_link, C, device):
@@ -170,14 +175,19 @@ def _dgrad_hip(C_, gy, w, padding, addend=None, bn_link=None):
             STATS["bn_bstats"] += 1
             return out
         if (masked and BSTATS_TILE_MASK and bn_link is not None and not bn_link.relu and bn_link.x is not None
-                and bn_link.mask is not None and bn_link.x2 is None and bn_link.x.shape == (N, H, W_, C)
-                and N * H * W_ < 2 ** 31):
-            # the same on the tile kernel (K = 512: the stage-4 identity blocks), one BatchNorm
+                and bn_link.mask is not None and bn_link.x.shape == (N, H, W_, C) and N * H * W_ < 2 ** 31
+                and (BSTATS_TILE_SHORT or bn_link.x2 is None or not C_.gemm_short_bnstats_ok(N * H * W_, C, K, False))):
+            # the same on the tile kernel: K = 512 (the stage-4 identity blocks) and the two-BatchNorm form past
+            # gemm_short's K = 128 (a downsample block's output read by the next block's conv1 at stages 3-4)
             out = torch.empty(N, H, W_, C, device=gy.device, dtype=gy.dtype)
             sums = _bn_sums(C_, bn_link, C, gy.device)
+            dual = bn_link.x2 is not None
+            sums2 = _bn_sums(C_, bn_link, C, gy.device) if dual else None
             C_.gemm_dgrad_bnstats_mask(gy.reshape(-1, K), w.reshape(K, C), out.view(-1, C), bn_link.x.view(-1, C),
-                                       bn_link.mask, bn_link.mean, sums, addend.dy.view(-1, C), addend.mask)
-            bn_link.sums, bn_link.sums2, bn_link.dy_key = sums, None, (out.data_ptr(), tuple(out.shape))
+                                       bn_link.mask, bn_link.mean, sums, addend.dy.view(-1, C), addend.mask,
+                                       bn_link.x2.view(-1, C) if dual else None, bn_link.mean2 if dual else None,
+                                       sums2)
+            bn_link.sums, bn_link.sums2, bn_link.dy_key = sums, sums2, (out.data_ptr(), tuple(out.shape))
             STATS["bn_bstats"] += 1
             return out
         if (BSTATS_GEMM and bn_link is not None and bn_link.relu and bn_link.x is not None and addend is None
@@ -265,6 +275,11 @@ def _dgrad_strided_hip(C_, gy, w, stride, padding, H, W, addend=None, bn_link=No
            and bn_link.x.shape == addend.shape)
     if bn_link is not None and bn_link.pending and not fix:
         bn_link.sums, bn_link.pending = None, False  # cannot complete: the BN takes its own reduction
+    # a BatchNorm + ReLU's sums (nn.BnStatLink relu kind: ResNet's bn1 before a stride-2 3x3 conv2): every parity
+    # stores its own pixels and adds the sums over them (gemm.hip BST sub-grid path, relu kind)
+    relu_sums = (BSTATS_STRIDED and bn_link is not None and bn_link.relu and bn_link.x is not None and addend is None
+                 and not bn_link.pending and bn_link.x.shape == (N, H, W, C) and C > 64 and K % 64 == 0)
+    rsums = _bn_sums(C_, bn_link, C, gy.device) if relu_sums else None
     parities = [(a, b) for a in range(stride) for b in range(stride)]
     empty = [(a, b) for a, b in parities
              if not _parity_taps(R, a, padding, stride) or not _parity_taps(S, b, padding, stride)]
@@ -287,10 +302,16 @@ def _dgrad_strided_hip(C_, gy, w, stride, padding, H, W, addend=None, bn_link=No
         if fix:
             C_.conv_fwd_subgrid(gy, wsub, -tr[0][0], Hs, Ws, dx, stride, a, b, True, bn_link.x, bn_link.mask,
                                 bn_link.mean, bn_link.sums)
+        elif relu_sums:
+            C_.conv_fwd_subgrid(gy, wsub, -tr[0][0], Hs, Ws, dx, stride, a, b, False, bn_link.x, None, bn_link.mean,
+                                rsums, bn_link.gamma, bn_link.beta, bn_link.invstd)
         else:
             C_.conv_fwd_subgrid(gy, wsub, -tr[0][0], Hs, Ws, dx, stride, a, b, addend is not None)
     if fix:
         bn_link.dy_key, bn_link.pending = (dx.data_ptr(), tuple(dx.shape)), False
+    if relu_sums:
+        bn_link.sums, bn_link.sums2, bn_link.dy_key = rsums, None, (dx.data_ptr(), tuple(dx.shape))
+        STATS["bn_bstats"] += 1
     return dx
 
 

@@ -751,8 +751,9 @@ def test_gemm_dgrad_bnstats_mask_accumulate(cuda):
     assert _rel(tot[1], (g * (x.float().view(-1, C) - mean)).sum(0)) < 1e-3
 
 
-@pytest.mark.parametrize("M,N,K", [(1000, 256, 512), (3 * 49 * 4, 2048, 512)])
-def test_gemm_dgrad_bnstats_masked_addend(cuda, M, N, K):
+@pytest.mark.parametrize("M,N,K,dual", [(1000, 256, 512, False), (3 * 49 * 4, 2048, 512, False),
+                                        (1000, 256, 256, True), (3 * 49 * 4, 2048, 512, True)])
+def test_gemm_dgrad_bnstats_masked_addend(cuda, M, N, K, dual):
     """A stage-4 identity block's conv1 data gradient (K = 512: not a gemm_short depth) on the tile kernel: out =
     dgrad + (addend bit ? addend : 0) with the residual BatchNorm's backward sums of out in the same epilogue
     (gemm.hip BST fast path, masked addend), against fp32."""
@@ -767,10 +768,51 @@ def test_gemm_dgrad_bnstats_masked_addend(cuda, M, N, K):
     mean = torch.randn(N, device=cuda) * 0.2
     sums = torch.zeros(C_.conv_stat_replicas, 2, N, device=cuda)
     out = torch.full((M, N), float("nan"), device=cuda).bfloat16()
-    C_.gemm_dgrad_bnstats_mask(gy, w, out, x, mask, mean, sums, add, amask)
+    x2 = (torch.randn(M, N, device=cuda) - 0.3).bfloat16() if dual else None
+    mean2 = torch.randn(N, device=cuda) * 0.1 if dual else None
+    sums2 = torch.zeros(C_.conv_stat_replicas, 2, N, device=cuda) if dual else None
+    C_.gemm_dgrad_bnstats_mask(gy, w, out, x, mask, mean, sums, add, amask, x2, mean2, sums2)
     ref = gy.float() @ w.float() + torch.where(_unpack_bits(amask, (M, N)), add.float(), torch.zeros(M, N, device=cuda))
     assert _rel(out, ref) < 1e-2
     g = torch.where(_unpack_bits(mask, (M, N)), out.float(), torch.zeros(M, N, device=cuda))
     tot = sums.sum(0)
     assert _rel(tot[0], g.sum(0)) < 1e-3
     assert _rel(tot[1], (g * (x.float() - mean)).sum(0)) < 1e-3
+    if dual:
+        assert _rel(sums2.sum(0)[1], (g * (x2.float() - mean2)).sum(0)) < 1e-3
+
+
+@pytest.mark.parametrize("N,H,C,K", [(4, 28, 128, 128), (2, 14, 256, 256), (3, 13, 128, 192)])
+def test_strided_dgrad_bn_relu_sums(cuda, N, H, C, K):
+    """A stride-2 3x3 data gradient (ResNet's stage-entry conv2) as its four parities, each storing its own pixels and
+    adding the BatchNorm + ReLU backward sums of the bn1 that fed the convolution (gemm.hip BST sub-grid path, relu
+    kind; the 1x1 parity on the K-major source, the others on the implicit GEMM): dx equal to the parity path without
+    the sums, the sums against fp32 sums over the stored dx with the forward's ReLU decision. Odd H: ragged parities."""
+    from k8s_amd.ops import conv as kc
+    from k8s_amd.ops import nn as K_
+
+    C_ = _C()
+    torch.manual_seed(16)
+    Ho = (H + 1) // 2
+    gy = torch.randn(N, Ho, Ho, K, device=cuda).bfloat16()
+    w = (torch.randn(K, 3, 3, C, device=cuda) * 0.05).bfloat16()
+    x = (torch.randn(N, H, H, C, device=cuda) * 1.5 + 0.2).bfloat16()
+    mean = x.float().reshape(-1, C).mean(0)
+    invstd = torch.rsqrt(x.float().reshape(-1, C).var(0, unbiased=False) + 1e-5)
+    gamma, beta = torch.rand(C, device=cuda) + 0.5, torch.randn(C, device=cuda) * 0.2
+    link = K_.BnStatLink()
+    link.x, link.mean, link.invstd, link.gamma, link.beta, link.relu = x, mean, invstd, gamma, beta, True
+    dx = kc._dgrad_strided_hip(C_, gy, w, 2, 1, H, H, None, link)
+    assert link.sums is not None and link.dy_key == (dx.data_ptr(), tuple(dx.shape))
+    plain = kc._dgrad_strided_hip(C_, gy, w, 2, 1, H, H, None, None)
+    assert torch.equal(dx, plain)
+    ref = torch.nn.grad.conv2d_input((N, C, H, H), w.float().permute(0, 3, 1, 2), gy.float().permute(0, 3, 1, 2),
+                                     stride=2, padding=1).permute(0, 2, 3, 1)
+    assert _rel(dx, ref) < 1e-2
+    scale = gamma * invstd
+    shift = torch.addcmul(beta, -mean, scale)
+    z = (x.float() * scale + shift).bfloat16().float()
+    g = torch.where(z > 0, dx.float(), torch.zeros_like(dx.float())).reshape(-1, C)
+    tot = link.sums.sum(0)
+    assert _rel(tot[0], g.sum(0)) < 1e-3
+    assert _rel(tot[1], (g * (x.float().reshape(-1, C) - mean)).sum(0)) < 1e-3
