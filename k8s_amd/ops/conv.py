@@ -127,11 +127,14 @@ BSTATS_GEMM = os.environ.get("K8S_AMD_BN_BSTATS_GEMM", "1") != "0"
 BSTATS_ENTRY = os.environ.get("K8S_AMD_BN_BSTATS_ENTRY", "1") != "0"
 # a residual BN's sums in a masked-addend 1x1 dgrad too deep for gemm_short (the tile kernel: stage 4, K = 512)
 BSTATS_TILE_MASK = os.environ.get("K8S_AMD_BN_BSTATS_TILE_MASK", "1") != "0"
-# a BatchNorm + ReLU's sums in the parities of a stride-2 data gradient (ResNet's stage-entry bn1)
-BSTATS_STRIDED = os.environ.get("K8S_AMD_BN_BSTATS_STRIDED", "1") != "0"
-# ... including the two-BatchNorm form at a gemm_short depth (K = 256: that epilogue spills; the plain product would
-# run on gemm_short)
-BSTATS_TILE_SHORT = os.environ.get("K8S_AMD_BN_BSTATS_TILE_SHORT", "1") != "0"
+# a BatchNorm + ReLU's sums in the parities of a stride-2 data gradient (ResNet's stage-entry bn1). Off by default:
+# the parities' epilogue x reads cost what the reduction saves (b3072: +1.7 ms in the parity kernels for the 1.55 ms of
+# the three reductions; same-box A/B within noise, profiles/r06_notes.md)
+BSTATS_STRIDED = os.environ.get("K8S_AMD_BN_BSTATS_STRIDED", "0") != "0"
+# ... including the two-BatchNorm form at a gemm_short depth (K = 256: that epilogue spills). Off by default: the
+# plain product runs on gemm_short at 659 us, the tile kernel with the sums at 1,537 us, for a ~510 us reduction
+# (scripts/microbench/bst_shapes.py, profiles/r06_bst_shapes.jsonl)
+BSTATS_TILE_SHORT = os.environ.get("K8S_AMD_BN_BSTATS_TILE_SHORT", "0") != "0"
 
 
 def _bn_sums(C_, bn_link, C, device):

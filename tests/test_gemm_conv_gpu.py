@@ -783,7 +783,7 @@ def test_gemm_dgrad_bnstats_masked_addend(cuda, M, N, K, dual):
 
 
 @pytest.mark.parametrize("N,H,C,K", [(4, 28, 128, 128), (2, 14, 256, 256), (3, 13, 128, 192)])
-def test_strided_dgrad_bn_relu_sums(cuda, N, H, C, K):
+def test_strided_dgrad_bn_relu_sums(cuda, monkeypatch, N, H, C, K):
     """A stride-2 3x3 data gradient (ResNet's stage-entry conv2) as its four parities, each storing its own pixels and
     adding the BatchNorm + ReLU backward sums of the bn1 that fed the convolution (gemm.hip BST sub-grid path, relu
     kind; the 1x1 parity on the K-major source, the others on the implicit GEMM): dx equal to the parity path without
@@ -802,6 +802,7 @@ def test_strided_dgrad_bn_relu_sums(cuda, N, H, C, K):
     gamma, beta = torch.rand(C, device=cuda) + 0.5, torch.randn(C, device=cuda) * 0.2
     link = K_.BnStatLink()
     link.x, link.mean, link.invstd, link.gamma, link.beta, link.relu = x, mean, invstd, gamma, beta, True
+    monkeypatch.setattr(kc, "BSTATS_STRIDED", True)  # (off by default: neutral at the step level)
     dx = kc._dgrad_strided_hip(C_, gy, w, 2, 1, H, H, None, link)
     assert link.sums is not None and link.dy_key == (dx.data_ptr(), tuple(dx.shape))
     plain = kc._dgrad_strided_hip(C_, gy, w, 2, 1, H, H, None, None)
